@@ -1,0 +1,107 @@
+/*
+ * tb_state_machine.h -- the reference's StateMachine contract for the commit path, as a C ABI.
+ *
+ * Mirrors `StateMachineType(Storage)` (src/state_machine.zig:222-2958) as consumed by
+ * `ReplicaType(StateMachine, ...)` (src/vsr/replica.zig:144-152) for the operations of this path:
+ * pulse, create_accounts, create_transfers, lookup_accounts, lookup_transfers. Bodies are
+ * multi-batch encoded exactly as src/vsr/multi_batch.zig; replies are multi-batch encoded the
+ * same way. The executor underneath is pluggable (tb_executor): the product binds the HIP
+ * executor (tbg.h) with tb_sm_open_gpu; tests may bind another executor with the same semantics.
+ *
+ *   tb_sm_input_valid     <- StateMachine.input_valid   :980-1032 (+ batch_valid :1036-1067)
+ *   tb_sm_prepare         <- StateMachine.prepare       :1070-1101
+ *   tb_sm_pulse_needed    <- StateMachine.pulse_needed  :1138-1144
+ *   tb_sm_prefetch        <- StateMachine.prefetch      :1146-1226 (completes immediately:
+ *                            the tables are HBM-resident; the callback runs before return)
+ *   tb_sm_commit          <- StateMachine.commit        :2564-2669 / execute_multi_batch :2702
+ *   tb_sm_{get,set}_*_timestamp <- fields prepare_timestamp / commit_timestamp /
+ *                            prefetch_timestamp (:229-231), written by the replica.
+ */
+#ifndef TB_STATE_MACHINE_H
+#define TB_STATE_MACHINE_H
+
+#include "tb_types.h"
+#include "tbg.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Operation numbers (src/tigerbeetle.zig:685-716, vsr_operations_reserved = 128). */
+enum {
+    TB_OPERATION_PULSE = 128,
+    TB_OPERATION_LOOKUP_ACCOUNTS = 140,
+    TB_OPERATION_LOOKUP_TRANSFERS = 141,
+    TB_OPERATION_CREATE_ACCOUNTS = 146,
+    TB_OPERATION_CREATE_TRANSFERS = 147,
+};
+
+/* An executor of the path: create_* take all batches of one commit. */
+typedef struct tb_executor {
+    void* self;
+    int (*create_accounts)(void* self, const tb_account_t* events, uint32_t n,
+                           const uint32_t* batch_lens, const uint64_t* batch_timestamps,
+                           uint32_t n_batches, tb_create_result_t* results);
+    int (*create_transfers)(void* self, const tb_transfer_t* events, uint32_t n,
+                            const uint32_t* batch_lens, const uint64_t* batch_timestamps,
+                            uint32_t n_batches, tb_create_result_t* results);
+    int64_t (*pulse)(void* self, uint64_t timestamp);
+    uint64_t (*pulse_next_timestamp)(void* self);
+    int64_t (*lookup_accounts)(void* self, const tb_uint128_t* ids, uint32_t n, tb_account_t* out);
+    int64_t (*lookup_transfers)(void* self, const tb_uint128_t* ids, uint32_t n,
+                                tb_transfer_t* out);
+} tb_executor;
+
+typedef struct tb_sm tb_sm;
+
+typedef struct tb_sm_options {
+    uint32_t batch_size_limit;      /* Options.batch_size_limit (<= message_body_size_max) */
+    uint32_t message_body_size_max; /* constants.message_body_size_max (1 MiB - 256 in prod) */
+    uint32_t pulse_batch_max;       /* batch_max.create_transfers (prepare delta of a pulse) */
+} tb_sm_options;
+
+/* Binds an executor (copied). */
+tb_sm* tb_sm_open(const tb_sm_options* options, const tb_executor* executor);
+/* Opens the HIP executor (tbg_open) and binds it; the tb_sm owns it. */
+tb_sm* tb_sm_open_gpu(const tb_sm_options* options, const tbg_options* executor_options);
+void tb_sm_close(tb_sm* sm);
+/* The bound HIP executor of a tb_sm_open_gpu state machine (NULL otherwise). */
+tbg_ctx* tb_sm_executor_gpu(tb_sm* sm);
+
+int tb_sm_input_valid(const tb_sm* sm, uint8_t operation, const void* body, uint32_t size);
+void tb_sm_prepare(tb_sm* sm, uint8_t operation, const void* body, uint32_t size);
+int tb_sm_pulse_needed(const tb_sm* sm, uint64_t timestamp);
+
+typedef void (*tb_sm_prefetch_callback)(void* context);
+void tb_sm_prefetch(tb_sm* sm, tb_sm_prefetch_callback callback, void* context, uint64_t op,
+                    uint64_t snapshot, uint8_t operation, const void* body, uint32_t size);
+
+/* Returns the reply size in bytes written to `output` (>= message_body_size_max bytes), or a
+ * negative value on executor failure. `client` is u128 {lo, hi}; client == 0 only for pulse. */
+int64_t tb_sm_commit(tb_sm* sm, uint64_t client_lo, uint64_t client_hi, uint64_t op,
+                     uint64_t timestamp, uint8_t operation, const void* body, uint32_t size,
+                     void* output);
+
+uint64_t tb_sm_get_prepare_timestamp(const tb_sm* sm);
+uint64_t tb_sm_get_commit_timestamp(const tb_sm* sm);
+uint64_t tb_sm_get_prefetch_timestamp(const tb_sm* sm);
+void tb_sm_set_prepare_timestamp(tb_sm* sm, uint64_t v);
+void tb_sm_set_commit_timestamp(tb_sm* sm, uint64_t v);
+void tb_sm_set_prefetch_timestamp(tb_sm* sm, uint64_t v);
+
+/* Multi-batch codec (src/vsr/multi_batch.zig), exported for clients/tests.
+ * encode: writes the payload of `n_batches` batches (element counts `counts`) laid out
+ * contiguously in `buffer` followed by the trailer; returns the total body size.
+ * decode: returns the batch count (>0) and fills counts[] (capacity `counts_max`) and
+ * *payload_size; returns -1 if the body is not a valid multi-batch encoding. */
+int64_t tb_multi_batch_encode_trailer(void* buffer, uint32_t payload_size, uint32_t element_size,
+                                      const uint16_t* counts, uint32_t n_batches);
+int64_t tb_multi_batch_decode(const void* body, uint32_t size, uint32_t element_size,
+                              uint16_t* counts, uint32_t counts_max, uint32_t* payload_size);
+uint32_t tb_multi_batch_trailer_total_size(uint32_t element_size, uint32_t batch_count);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TB_STATE_MACHINE_H */

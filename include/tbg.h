@@ -1,0 +1,115 @@
+/*
+ * tbg.h -- C ABI of the MI355X batch executor for TigerBeetle's commit path.
+ *
+ * The executor holds the state the reference keeps in its Forest grooves for this path, resident
+ * in HBM: the account table (groove `accounts`), the transfer table with orphaned ids (groove
+ * `transfers`), TransferPending statuses (groove `transfers_pending`), the `expires_at` index and
+ * `pulse_next_timestamp`. It executes create_accounts / create_transfers / pulse with results
+ * bit-identical to the reference's serial execution.
+ *
+ * Entry points and the reference interface each one replaces (all in src/state_machine.zig):
+ *   tbg_create_accounts   <- execute_create(.create_accounts)   :3002-3213, create_account :3613
+ *   tbg_create_transfers  <- execute_create(.create_transfers)  :3002-3213, create_transfer :3719
+ *   tbg_pulse             <- prefetch_expire_pending_transfers  :2436-2562 +
+ *                            execute_expire_pending_transfers   :4511-4628
+ *   tbg_pulse_next_timestamp <- ExpirePendingTransfers.pulse_next_timestamp :4906-4909
+ *   tbg_lookup_accounts   <- execute_lookup_accounts            :3255-3272
+ *   tbg_lookup_transfers  <- execute_lookup_transfers           :3274-3292
+ * prefetch (:1146-1420) has no counterpart: every table is HBM-resident, nothing is staged.
+ *
+ * Batches: one call executes `n_batches` consecutive batches (a multi-batch body, or any sequence
+ * of commits). Batch b holds batch_lens[b] events and `batch_timestamps[b]` is the `timestamp`
+ * argument execute_create receives for it (its highest event timestamp); event i of batch b is
+ * stamped batch_timestamps[b] - batch_lens[b] + i + 1. Batches are executed in order; linked
+ * chains and the imported flag are scoped to a batch exactly as in the reference.
+ *
+ * Conventions: the caller owns every buffer. Calls are synchronous (results are on the host when
+ * the call returns) except the *_device variants, which are stream-ordered and take device
+ * pointers. A ctx is single-thread-affine (the reference state machine is single-threaded).
+ * Return values: 0 (or a count) on success, a negative errno-style value on API misuse or a HIP
+ * failure. Domain failures are per-event statuses in the results, never return codes.
+ */
+#ifndef TBG_H
+#define TBG_H
+
+#include "tb_types.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct tbg_ctx tbg_ctx;
+
+typedef struct tbg_options {
+    uint64_t account_capacity;  /* max accounts ever submitted (rows + 2x hash slots) */
+    uint64_t transfer_capacity; /* max transfer events ever submitted (rows + 2x hash slots) */
+    uint32_t batch_events_max;  /* max events per call */
+    uint32_t batch_count_max;   /* max batches per call */
+    uint32_t pulse_batch_max;   /* batch_max.create_transfers: 8190 in production */
+    uint32_t device;            /* HIP device ordinal */
+    uint64_t pulse_next_timestamp_init; /* TB_TIMESTAMP_MIN in production */
+} tbg_options;
+
+/* Errors (negative). */
+#define TBG_EINVAL (-22)
+#define TBG_ENOMEM (-12)
+#define TBG_ENOSPC (-28)
+#define TBG_EHIP (-5)
+
+tbg_ctx* tbg_open(const tbg_options* options);
+void tbg_close(tbg_ctx* ctx);
+/* Last HIP / API error message of this ctx (never NULL). */
+const char* tbg_last_error(const tbg_ctx* ctx);
+
+int tbg_create_accounts(tbg_ctx* ctx, const tb_account_t* events, uint32_t n,
+                        const uint32_t* batch_lens, const uint64_t* batch_timestamps,
+                        uint32_t n_batches, tb_create_result_t* results);
+int tbg_create_transfers(tbg_ctx* ctx, const tb_transfer_t* events, uint32_t n,
+                         const uint32_t* batch_lens, const uint64_t* batch_timestamps,
+                         uint32_t n_batches, tb_create_result_t* results);
+
+/* Device-resident variants: every pointer is device memory; batch_ends[b] = exclusive end index
+ * of batch b (prefix sum of batch_lens). Enqueued on `stream` (a hipStream_t, NULL = the ctx's
+ * stream); results are complete when the stream reaches this point. */
+int tbg_create_accounts_device(tbg_ctx* ctx, const tb_account_t* d_events, uint32_t n,
+                               const uint32_t* d_batch_ends, const uint64_t* d_batch_timestamps,
+                               uint32_t n_batches, tb_create_result_t* d_results, void* stream);
+int tbg_create_transfers_device(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t n,
+                                const uint32_t* d_batch_ends, const uint64_t* d_batch_timestamps,
+                                uint32_t n_batches, tb_create_result_t* d_results, void* stream);
+
+/* Returns the number of pending transfers expired (<= pulse_batch_max). */
+int64_t tbg_pulse(tbg_ctx* ctx, uint64_t timestamp);
+uint64_t tbg_pulse_next_timestamp(tbg_ctx* ctx);
+
+/* Found objects only, in request order; returns the count written. */
+int64_t tbg_lookup_accounts(tbg_ctx* ctx, const tb_uint128_t* ids, uint32_t n, tb_account_t* out);
+int64_t tbg_lookup_transfers(tbg_ctx* ctx, const tb_uint128_t* ids, uint32_t n,
+                             tb_transfer_t* out);
+
+/* Parity dumps: live objects in creation order; `out` may be NULL to query the count. */
+int64_t tbg_dump_accounts(tbg_ctx* ctx, tb_account_t* out);
+int64_t tbg_dump_transfers(tbg_ctx* ctx, tb_transfer_t* out, uint8_t* pending_status);
+
+/* Test-harness `setup` action (src/state_machine_tests.zig:657-676). */
+int tbg_debug_set_account_balances(tbg_ctx* ctx, tb_uint128_t id, tb_uint128_t debits_pending,
+                                   tb_uint128_t debits_posted, tb_uint128_t credits_pending,
+                                   tb_uint128_t credits_posted);
+
+/* Per-call execution statistics of the last create_* call (diagnostics / bench). */
+typedef struct tbg_stats {
+    uint64_t events;       /* events in the call */
+    uint64_t fast;         /* applied by the parallel path */
+    uint64_t replayed;     /* executed by the ordered replay */
+    uint64_t static_fail;  /* failed on checks that depend on no in-call state */
+} tbg_stats;
+int tbg_last_stats(tbg_ctx* ctx, tbg_stats* out);
+
+/* Forces every event through the ordered replay (self-check of the fast path). */
+int tbg_debug_force_replay(tbg_ctx* ctx, int enable);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TBG_H */

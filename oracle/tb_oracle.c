@@ -1,0 +1,983 @@
+/*
+ * tb_oracle.c -- TEST INFRASTRUCTURE: serial CPU restatement of TigerBeetle's commit path.
+ *
+ * This file is the parity checker for the HIP executor (tigerbeetle_amd/csrc) and the CPU
+ * baseline of bench.py. It is never linked into the product library. It restates, event by
+ * event and in the reference's exact check order:
+ *
+ *   execute_create             src/state_machine.zig:3002-3213
+ *   transient_error            src/state_machine.zig:3215-3252
+ *   create_account(_exists)    src/state_machine.zig:3613-3703
+ *   create_transfer(_exists)   src/state_machine.zig:3719-4051
+ *   post_or_void_pending_...   src/state_machine.zig:4053-4382
+ *   execute_expire_pending_... src/state_machine.zig:4511-4628 with the scan/finish rules of
+ *                              ExpirePendingTransfersType, src/state_machine.zig:4875-5029 and
+ *                              src/lsm/scan_lookup.zig:150-175 (buffer_finished before next()).
+ *   sum_overflows              src/state_machine.zig:5144-5149
+ *
+ * Groove semantics (src/lsm/groove.zig:885-951, :1770-1949; src/lsm/cache_map.zig:331-385;
+ * src/lsm/tree.zig:178-226) are modelled with hash maps plus a scope undo log:
+ *   - inserts/updates are visible to later events of the same batch;
+ *   - scope_close(discard) reverts objects, statuses and the objects trees' key_range;
+ *   - orphaned transfer ids (transient failures) are inserted outside any scope and never revert;
+ *   - pulse_next_timestamp is state-machine state, not groove state: it is never reverted.
+ *
+ * Parity pin: tests/test_oracle_tables.py replays the reference's table tests
+ * (src/state_machine_tests.zig) against this file.
+ */
+#include "tb_oracle.h"
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+typedef unsigned __int128 u128;
+
+static inline u128 U(tb_uint128_t x) { return ((u128)x.hi << 64) | x.lo; }
+static inline tb_uint128_t W(u128 x) {
+    tb_uint128_t r;
+    r.lo = (uint64_t)x;
+    r.hi = (uint64_t)(x >> 64);
+    return r;
+}
+static const u128 U128_MAX = ~(u128)0;
+
+static void* xrealloc(void* p, size_t n) {
+    void* q = realloc(p, n);
+    if (!q && n) {
+        fprintf(stderr, "tb_oracle: out of memory\n");
+        abort();
+    }
+    return q;
+}
+
+/* ---- u128 -> u64 hash map: linear probing, backward-shift deletion --------------------------*/
+
+typedef struct {
+    u128* keys;
+    uint64_t* vals;
+    uint8_t* used;
+    uint64_t cap; /* power of two */
+    uint64_t count;
+} map_t;
+
+static inline uint64_t mix64(uint64_t h) {
+    h ^= h >> 33;
+    h *= 0xff51afd7ed558ccdull;
+    h ^= h >> 33;
+    h *= 0xc4ceb9fe1a85ec53ull;
+    h ^= h >> 33;
+    return h;
+}
+static inline uint64_t hash128(u128 k) {
+    return mix64((uint64_t)k ^ mix64((uint64_t)(k >> 64) + 0x9E3779B97F4A7C15ull));
+}
+
+static void map_init(map_t* m, uint64_t cap) {
+    m->cap = cap;
+    m->count = 0;
+    m->keys = (u128*)xrealloc(NULL, cap * sizeof(u128));
+    m->vals = (uint64_t*)xrealloc(NULL, cap * sizeof(uint64_t));
+    m->used = (uint8_t*)calloc(cap, 1);
+}
+static void map_free(map_t* m) {
+    free(m->keys);
+    free(m->vals);
+    free(m->used);
+}
+static int map_get(const map_t* m, u128 key, uint64_t* val) {
+    uint64_t mask = m->cap - 1, i = hash128(key) & mask;
+    while (m->used[i]) {
+        if (m->keys[i] == key) {
+            if (val) *val = m->vals[i];
+            return 1;
+        }
+        i = (i + 1) & mask;
+    }
+    return 0;
+}
+static void map_put(map_t* m, u128 key, uint64_t val);
+static void map_grow(map_t* m) {
+    map_t n;
+    map_init(&n, m->cap * 2);
+    for (uint64_t i = 0; i < m->cap; i++)
+        if (m->used[i]) map_put(&n, m->keys[i], m->vals[i]);
+    map_free(m);
+    *m = n;
+}
+static void map_put(map_t* m, u128 key, uint64_t val) {
+    if ((m->count + 1) * 2 > m->cap) map_grow(m);
+    uint64_t mask = m->cap - 1, i = hash128(key) & mask;
+    while (m->used[i]) {
+        if (m->keys[i] == key) {
+            m->vals[i] = val;
+            return;
+        }
+        i = (i + 1) & mask;
+    }
+    m->used[i] = 1;
+    m->keys[i] = key;
+    m->vals[i] = val;
+    m->count++;
+}
+static void map_del(map_t* m, u128 key) {
+    uint64_t mask = m->cap - 1, i = hash128(key) & mask;
+    while (m->used[i] && m->keys[i] != key) i = (i + 1) & mask;
+    if (!m->used[i]) return;
+    m->used[i] = 0;
+    m->count--;
+    /* Backward-shift: re-seat the rest of the cluster. */
+    uint64_t j = (i + 1) & mask;
+    while (m->used[j]) {
+        u128 k = m->keys[j];
+        uint64_t v = m->vals[j];
+        m->used[j] = 0;
+        m->count--;
+        map_put(m, k, v);
+        j = (j + 1) & mask;
+    }
+}
+
+/* ---- state ----------------------------------------------------------------------------------*/
+
+#define ORPHAN UINT64_MAX
+
+enum { UNDO_ACCOUNT = 1, UNDO_STATUS = 2 };
+typedef struct {
+    uint32_t kind;
+    uint64_t index;
+    tb_account_t account; /* UNDO_ACCOUNT: the row before the update */
+    uint8_t status;       /* UNDO_STATUS: the TransferPending status before the update */
+} undo_t;
+
+typedef struct {
+    int has;
+    uint64_t key_max; /* tree.key_range.key_max of the objects tree (timestamps) */
+} key_range_t;
+
+struct tbo_ctx {
+    tb_account_t* accounts;
+    uint64_t n_accounts, cap_accounts;
+    tb_transfer_t* transfers;
+    uint8_t* pending_status; /* TransferPending.status, keyed by the transfer (= its timestamp) */
+    uint64_t n_transfers, cap_transfers;
+
+    map_t account_by_id, account_by_ts;
+    map_t transfer_by_id, transfer_by_ts; /* transfer_by_id value ORPHAN = orphaned id */
+    key_range_t accounts_range, transfers_range;
+
+    uint64_t* expiry; /* transfers with flags.pending and timeout > 0 (expires_at index) */
+    uint64_t n_expiry, cap_expiry;
+
+    uint64_t pulse_next_timestamp;
+    uint32_t pulse_batch_max;
+    uint64_t commit_timestamp;
+
+    /* One active scope at a time (tree.zig:178-197). */
+    int scope_active;
+    uint64_t scope_n_accounts, scope_n_transfers, scope_n_expiry;
+    key_range_t scope_accounts_range, scope_transfers_range;
+    undo_t* undo;
+    uint64_t n_undo, cap_undo;
+};
+
+tbo_ctx* tbo_open(uint32_t pulse_batch_max, uint64_t pulse_next_timestamp_init) {
+    tbo_ctx* c = (tbo_ctx*)calloc(1, sizeof(tbo_ctx));
+    map_init(&c->account_by_id, 1024);
+    map_init(&c->account_by_ts, 1024);
+    map_init(&c->transfer_by_id, 1024);
+    map_init(&c->transfer_by_ts, 1024);
+    c->pulse_batch_max = pulse_batch_max;
+    c->pulse_next_timestamp = pulse_next_timestamp_init;
+    return c;
+}
+
+void tbo_close(tbo_ctx* c) {
+    if (!c) return;
+    free(c->accounts);
+    free(c->transfers);
+    free(c->pending_status);
+    free(c->expiry);
+    free(c->undo);
+    map_free(&c->account_by_id);
+    map_free(&c->account_by_ts);
+    map_free(&c->transfer_by_id);
+    map_free(&c->transfer_by_ts);
+    free(c);
+}
+
+static void undo_push(tbo_ctx* c, undo_t* u) {
+    if (!c->scope_active) return;
+    if (c->n_undo == c->cap_undo) {
+        c->cap_undo = c->cap_undo ? c->cap_undo * 2 : 256;
+        c->undo = (undo_t*)xrealloc(c->undo, c->cap_undo * sizeof(undo_t));
+    }
+    c->undo[c->n_undo++] = *u;
+}
+
+static void scope_open(tbo_ctx* c) {
+    c->scope_active = 1;
+    c->scope_n_accounts = c->n_accounts;
+    c->scope_n_transfers = c->n_transfers;
+    c->scope_n_expiry = c->n_expiry;
+    c->scope_accounts_range = c->accounts_range;
+    c->scope_transfers_range = c->transfers_range;
+    c->n_undo = 0;
+}
+
+static void scope_close(tbo_ctx* c, int discard) {
+    if (discard) {
+        /* Reverse order, like cache_map.zig:361-385. */
+        for (uint64_t k = c->n_undo; k-- > 0;) {
+            undo_t* u = &c->undo[k];
+            if (u->kind == UNDO_ACCOUNT) {
+                c->accounts[u->index] = u->account;
+            } else {
+                c->pending_status[u->index] = u->status;
+            }
+        }
+        for (uint64_t i = c->scope_n_accounts; i < c->n_accounts; i++) {
+            map_del(&c->account_by_id, U(c->accounts[i].id));
+            map_del(&c->account_by_ts, c->accounts[i].timestamp);
+        }
+        for (uint64_t i = c->scope_n_transfers; i < c->n_transfers; i++) {
+            map_del(&c->transfer_by_id, U(c->transfers[i].id));
+            map_del(&c->transfer_by_ts, c->transfers[i].timestamp);
+        }
+        c->n_accounts = c->scope_n_accounts;
+        c->n_transfers = c->scope_n_transfers;
+        c->n_expiry = c->scope_n_expiry;
+        c->accounts_range = c->scope_accounts_range;
+        c->transfers_range = c->scope_transfers_range;
+    }
+    c->scope_active = 0;
+    c->n_undo = 0;
+}
+
+static tb_account_t* get_account(tbo_ctx* c, u128 id) {
+    uint64_t v;
+    if (!map_get(&c->account_by_id, id, &v)) return NULL;
+    return &c->accounts[v];
+}
+
+/* groove.get for transfers: 0 = not_found, 1 = found_object, 2 = found_orphaned */
+static int get_transfer(tbo_ctx* c, u128 id, uint64_t* index) {
+    uint64_t v;
+    if (!map_get(&c->transfer_by_id, id, &v)) return 0;
+    if (v == ORPHAN) return 2;
+    *index = v;
+    return 1;
+}
+
+static void key_range_update(key_range_t* r, uint64_t key) {
+    if (!r->has || key > r->key_max) r->key_max = key;
+    r->has = 1;
+}
+
+static void insert_account(tbo_ctx* c, const tb_account_t* a) {
+    if (c->n_accounts == c->cap_accounts) {
+        c->cap_accounts = c->cap_accounts ? c->cap_accounts * 2 : 1024;
+        c->accounts = (tb_account_t*)xrealloc(c->accounts, c->cap_accounts * sizeof(tb_account_t));
+    }
+    uint64_t i = c->n_accounts++;
+    c->accounts[i] = *a;
+    map_put(&c->account_by_id, U(a->id), i);
+    map_put(&c->account_by_ts, a->timestamp, i);
+    key_range_update(&c->accounts_range, a->timestamp);
+}
+
+static void update_account(tbo_ctx* c, tb_account_t* row, const tb_account_t* next) {
+    uint64_t index = (uint64_t)(row - c->accounts);
+    if (c->scope_active && index < c->scope_n_accounts) {
+        undo_t u;
+        memset(&u, 0, sizeof(u));
+        u.kind = UNDO_ACCOUNT;
+        u.index = index;
+        u.account = *row;
+        undo_push(c, &u);
+    }
+    *row = *next;
+}
+
+static uint64_t insert_transfer(tbo_ctx* c, const tb_transfer_t* t, uint8_t status) {
+    if (c->n_transfers == c->cap_transfers) {
+        c->cap_transfers = c->cap_transfers ? c->cap_transfers * 2 : 1024;
+        c->transfers =
+            (tb_transfer_t*)xrealloc(c->transfers, c->cap_transfers * sizeof(tb_transfer_t));
+        c->pending_status = (uint8_t*)xrealloc(c->pending_status, c->cap_transfers);
+    }
+    uint64_t i = c->n_transfers++;
+    c->transfers[i] = *t;
+    c->pending_status[i] = status;
+    map_put(&c->transfer_by_id, U(t->id), i);
+    map_put(&c->transfer_by_ts, t->timestamp, i);
+    key_range_update(&c->transfers_range, t->timestamp);
+    if ((t->flags & TB_TRANSFER_PENDING) && t->timeout > 0) {
+        if (c->n_expiry == c->cap_expiry) {
+            c->cap_expiry = c->cap_expiry ? c->cap_expiry * 2 : 1024;
+            c->expiry = (uint64_t*)xrealloc(c->expiry, c->cap_expiry * sizeof(uint64_t));
+        }
+        c->expiry[c->n_expiry++] = i;
+    }
+    return i;
+}
+
+static void update_pending_status(tbo_ctx* c, uint64_t index, uint8_t status) {
+    if (c->scope_active && index < c->scope_n_transfers) {
+        undo_t u;
+        memset(&u, 0, sizeof(u));
+        u.kind = UNDO_STATUS;
+        u.index = index;
+        u.status = c->pending_status[index];
+        undo_push(c, &u);
+    }
+    c->pending_status[index] = status;
+}
+
+static inline int sum_overflows_u128(u128 a, u128 b) { return a + b < a; }
+
+/* ---- create_account (state_machine.zig:3613-3703) ------------------------------------------*/
+
+static uint32_t create_account_exists(const tb_account_t* a, const tb_account_t* e,
+                                      uint64_t* ts) {
+    if (a->flags != e->flags) return TB_CA_EXISTS_WITH_DIFFERENT_FLAGS;
+    if (U(a->user_data_128) != U(e->user_data_128))
+        return TB_CA_EXISTS_WITH_DIFFERENT_USER_DATA_128;
+    if (a->user_data_64 != e->user_data_64) return TB_CA_EXISTS_WITH_DIFFERENT_USER_DATA_64;
+    if (a->user_data_32 != e->user_data_32) return TB_CA_EXISTS_WITH_DIFFERENT_USER_DATA_32;
+    if (a->ledger != e->ledger) return TB_CA_EXISTS_WITH_DIFFERENT_LEDGER;
+    if (a->code != e->code) return TB_CA_EXISTS_WITH_DIFFERENT_CODE;
+    *ts = e->timestamp;
+    return TB_CA_EXISTS;
+}
+
+static uint32_t create_account(tbo_ctx* c, uint64_t timestamp_event, const tb_account_t* a,
+                               uint64_t* ts) {
+    if (a->reserved != 0) return TB_CA_RESERVED_FIELD;
+    if (a->flags & TB_ACCOUNT_PADDING_MASK) return TB_CA_RESERVED_FLAG;
+    u128 id = U(a->id);
+    if (id == 0) return TB_CA_ID_MUST_NOT_BE_ZERO;
+    if (id == U128_MAX) return TB_CA_ID_MUST_NOT_BE_INT_MAX;
+
+    tb_account_t* e = get_account(c, id);
+    if (e) return create_account_exists(a, e, ts);
+
+    if ((a->flags & TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS) &&
+        (a->flags & TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS))
+        return TB_CA_FLAGS_ARE_MUTUALLY_EXCLUSIVE;
+    if (U(a->debits_pending) != 0) return TB_CA_DEBITS_PENDING_MUST_BE_ZERO;
+    if (U(a->debits_posted) != 0) return TB_CA_DEBITS_POSTED_MUST_BE_ZERO;
+    if (U(a->credits_pending) != 0) return TB_CA_CREDITS_PENDING_MUST_BE_ZERO;
+    if (U(a->credits_posted) != 0) return TB_CA_CREDITS_POSTED_MUST_BE_ZERO;
+    if (a->ledger == 0) return TB_CA_LEDGER_MUST_NOT_BE_ZERO;
+    if (a->code == 0) return TB_CA_CODE_MUST_NOT_BE_ZERO;
+
+    uint64_t timestamp_actual = timestamp_event;
+    if (a->flags & TB_ACCOUNT_IMPORTED) {
+        if (c->accounts_range.has && a->timestamp <= c->accounts_range.key_max)
+            return TB_CA_IMPORTED_EVENT_TIMESTAMP_MUST_NOT_REGRESS;
+        if (map_get(&c->transfer_by_ts, a->timestamp, NULL))
+            return TB_CA_IMPORTED_EVENT_TIMESTAMP_MUST_NOT_REGRESS;
+        timestamp_actual = a->timestamp;
+    }
+
+    tb_account_t row;
+    memset(&row, 0, sizeof(row));
+    row.id = a->id;
+    row.user_data_128 = a->user_data_128;
+    row.user_data_64 = a->user_data_64;
+    row.user_data_32 = a->user_data_32;
+    row.ledger = a->ledger;
+    row.code = a->code;
+    row.flags = a->flags;
+    row.timestamp = timestamp_actual;
+    insert_account(c, &row);
+    c->commit_timestamp = timestamp_actual;
+    *ts = timestamp_actual;
+    return TB_STATUS_CREATED;
+}
+
+/* ---- create_transfer (state_machine.zig:3719-4051) -----------------------------------------*/
+
+static uint32_t post_or_void_pending_transfer_exists(const tb_transfer_t* t,
+                                                     const tb_transfer_t* e,
+                                                     const tb_transfer_t* p, uint64_t* ts) {
+    if (U(t->debit_account_id) != 0 && U(t->debit_account_id) != U(e->debit_account_id))
+        return TB_CT_EXISTS_WITH_DIFFERENT_DEBIT_ACCOUNT_ID;
+    if (U(t->credit_account_id) != 0 && U(t->credit_account_id) != U(e->credit_account_id))
+        return TB_CT_EXISTS_WITH_DIFFERENT_CREDIT_ACCOUNT_ID;
+    if (t->flags & TB_TRANSFER_VOID_PENDING) {
+        if (U(t->amount) == 0) {
+            if (U(e->amount) != U(p->amount)) return TB_CT_EXISTS_WITH_DIFFERENT_AMOUNT;
+        } else {
+            if (U(t->amount) != U(e->amount)) return TB_CT_EXISTS_WITH_DIFFERENT_AMOUNT;
+        }
+    }
+    if (t->flags & TB_TRANSFER_POST_PENDING) {
+        if (U(t->amount) == U128_MAX) {
+            if (U(e->amount) != U(p->amount)) return TB_CT_EXISTS_WITH_DIFFERENT_AMOUNT;
+        } else {
+            if (U(t->amount) != U(e->amount)) return TB_CT_EXISTS_WITH_DIFFERENT_AMOUNT;
+        }
+    }
+    if (U(t->user_data_128) == 0) {
+        if (U(e->user_data_128) != U(p->user_data_128))
+            return TB_CT_EXISTS_WITH_DIFFERENT_USER_DATA_128;
+    } else if (U(t->user_data_128) != U(e->user_data_128)) {
+        return TB_CT_EXISTS_WITH_DIFFERENT_USER_DATA_128;
+    }
+    if (t->user_data_64 == 0) {
+        if (e->user_data_64 != p->user_data_64) return TB_CT_EXISTS_WITH_DIFFERENT_USER_DATA_64;
+    } else if (t->user_data_64 != e->user_data_64) {
+        return TB_CT_EXISTS_WITH_DIFFERENT_USER_DATA_64;
+    }
+    if (t->user_data_32 == 0) {
+        if (e->user_data_32 != p->user_data_32) return TB_CT_EXISTS_WITH_DIFFERENT_USER_DATA_32;
+    } else if (t->user_data_32 != e->user_data_32) {
+        return TB_CT_EXISTS_WITH_DIFFERENT_USER_DATA_32;
+    }
+    if (t->ledger != 0 && t->ledger != e->ledger) return TB_CT_EXISTS_WITH_DIFFERENT_LEDGER;
+    if (t->code != 0 && t->code != e->code) return TB_CT_EXISTS_WITH_DIFFERENT_CODE;
+    *ts = e->timestamp;
+    return TB_CT_EXISTS;
+}
+
+static uint32_t create_transfer_exists(tbo_ctx* c, const tb_transfer_t* t,
+                                       const tb_transfer_t* e, uint64_t* ts) {
+    if (t->flags != e->flags) return TB_CT_EXISTS_WITH_DIFFERENT_FLAGS;
+    if (U(t->pending_id) != U(e->pending_id)) return TB_CT_EXISTS_WITH_DIFFERENT_PENDING_ID;
+    if (t->timeout != e->timeout) return TB_CT_EXISTS_WITH_DIFFERENT_TIMEOUT;
+
+    if (t->flags & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) {
+        uint64_t pi = 0;
+        int found = get_transfer(c, U(t->pending_id), &pi);
+        if (found != 1) abort(); /* the reference asserts the pending transfer exists */
+        return post_or_void_pending_transfer_exists(t, e, &c->transfers[pi], ts);
+    }
+    if (U(t->debit_account_id) != U(e->debit_account_id))
+        return TB_CT_EXISTS_WITH_DIFFERENT_DEBIT_ACCOUNT_ID;
+    if (U(t->credit_account_id) != U(e->credit_account_id))
+        return TB_CT_EXISTS_WITH_DIFFERENT_CREDIT_ACCOUNT_ID;
+    if (t->flags & (TB_TRANSFER_BALANCING_DEBIT | TB_TRANSFER_BALANCING_CREDIT)) {
+        if (U(t->amount) < U(e->amount)) return TB_CT_EXISTS_WITH_DIFFERENT_AMOUNT;
+    } else {
+        if (U(t->amount) != U(e->amount)) return TB_CT_EXISTS_WITH_DIFFERENT_AMOUNT;
+    }
+    if (U(t->user_data_128) != U(e->user_data_128))
+        return TB_CT_EXISTS_WITH_DIFFERENT_USER_DATA_128;
+    if (t->user_data_64 != e->user_data_64) return TB_CT_EXISTS_WITH_DIFFERENT_USER_DATA_64;
+    if (t->user_data_32 != e->user_data_32) return TB_CT_EXISTS_WITH_DIFFERENT_USER_DATA_32;
+    if (t->ledger != e->ledger) return TB_CT_EXISTS_WITH_DIFFERENT_LEDGER;
+    if (t->code != e->code) return TB_CT_EXISTS_WITH_DIFFERENT_CODE;
+    *ts = e->timestamp;
+    return TB_CT_EXISTS;
+}
+
+static uint32_t post_or_void_pending_transfer(tbo_ctx* c, uint64_t timestamp_event,
+                                              const tb_transfer_t* t, uint64_t* ts) {
+    const uint16_t f = t->flags;
+    if ((f & TB_TRANSFER_POST_PENDING) && (f & TB_TRANSFER_VOID_PENDING))
+        return TB_CT_FLAGS_ARE_MUTUALLY_EXCLUSIVE;
+    if (f & (TB_TRANSFER_PENDING | TB_TRANSFER_BALANCING_DEBIT | TB_TRANSFER_BALANCING_CREDIT |
+             TB_TRANSFER_CLOSING_DEBIT | TB_TRANSFER_CLOSING_CREDIT))
+        return TB_CT_FLAGS_ARE_MUTUALLY_EXCLUSIVE;
+
+    u128 pending_id = U(t->pending_id);
+    if (pending_id == 0) return TB_CT_PENDING_ID_MUST_NOT_BE_ZERO;
+    if (pending_id == U128_MAX) return TB_CT_PENDING_ID_MUST_NOT_BE_INT_MAX;
+    if (pending_id == U(t->id)) return TB_CT_PENDING_ID_MUST_BE_DIFFERENT;
+    if (t->timeout != 0) return TB_CT_TIMEOUT_RESERVED_FOR_PENDING_TRANSFER;
+
+    uint64_t pi = 0;
+    if (get_transfer(c, pending_id, &pi) != 1) return TB_CT_PENDING_TRANSFER_NOT_FOUND;
+    const tb_transfer_t p = c->transfers[pi]; /* copy: inserts below may realloc */
+    if (!(p.flags & TB_TRANSFER_PENDING)) return TB_CT_PENDING_TRANSFER_NOT_PENDING;
+
+    tb_account_t* dr = get_account(c, U(p.debit_account_id));
+    tb_account_t* cr = get_account(c, U(p.credit_account_id));
+    if (!dr || !cr) abort(); /* asserted by the reference */
+
+    if (U(t->debit_account_id) > 0 && U(t->debit_account_id) != U(p.debit_account_id))
+        return TB_CT_PENDING_TRANSFER_HAS_DIFFERENT_DEBIT_ACCOUNT_ID;
+    if (U(t->credit_account_id) > 0 && U(t->credit_account_id) != U(p.credit_account_id))
+        return TB_CT_PENDING_TRANSFER_HAS_DIFFERENT_CREDIT_ACCOUNT_ID;
+    if (t->ledger > 0 && t->ledger != p.ledger) return TB_CT_PENDING_TRANSFER_HAS_DIFFERENT_LEDGER;
+    if (t->code > 0 && t->code != p.code) return TB_CT_PENDING_TRANSFER_HAS_DIFFERENT_CODE;
+
+    u128 amount_actual;
+    if (f & TB_TRANSFER_VOID_PENDING) {
+        amount_actual = U(t->amount) == 0 ? U(p.amount) : U(t->amount);
+    } else {
+        amount_actual = U(t->amount) == U128_MAX ? U(p.amount) : U(t->amount);
+    }
+    if (amount_actual > U(p.amount)) return TB_CT_EXCEEDS_PENDING_TRANSFER_AMOUNT;
+    if ((f & TB_TRANSFER_VOID_PENDING) && amount_actual < U(p.amount))
+        return TB_CT_PENDING_TRANSFER_HAS_DIFFERENT_AMOUNT;
+
+    switch (c->pending_status[pi]) {
+        case TB_PENDING_PENDING: break;
+        case TB_PENDING_POSTED: return TB_CT_PENDING_TRANSFER_ALREADY_POSTED;
+        case TB_PENDING_VOIDED: return TB_CT_PENDING_TRANSFER_ALREADY_VOIDED;
+        case TB_PENDING_EXPIRED: return TB_CT_PENDING_TRANSFER_EXPIRED;
+        default: abort();
+    }
+
+    int has_expiry = p.timeout != 0;
+    uint64_t expires_at = 0;
+    if (has_expiry) {
+        expires_at = p.timestamp + (uint64_t)p.timeout * TB_NS_PER_S;
+        if (expires_at <= timestamp_event) return TB_CT_PENDING_TRANSFER_EXPIRED;
+    }
+
+    uint64_t timestamp_actual = timestamp_event;
+    if (f & TB_TRANSFER_IMPORTED) {
+        if (c->transfers_range.has && t->timestamp <= c->transfers_range.key_max)
+            return TB_CT_IMPORTED_EVENT_TIMESTAMP_MUST_NOT_REGRESS;
+        if (map_get(&c->account_by_ts, t->timestamp, NULL))
+            return TB_CT_IMPORTED_EVENT_TIMESTAMP_MUST_NOT_REGRESS;
+        timestamp_actual = t->timestamp;
+    }
+
+    if ((dr->flags & TB_ACCOUNT_CLOSED) && !(f & TB_TRANSFER_VOID_PENDING))
+        return TB_CT_DEBIT_ACCOUNT_ALREADY_CLOSED;
+    if ((cr->flags & TB_ACCOUNT_CLOSED) && !(f & TB_TRANSFER_VOID_PENDING))
+        return TB_CT_CREDIT_ACCOUNT_ALREADY_CLOSED;
+
+    tb_transfer_t row;
+    memset(&row, 0, sizeof(row));
+    row.id = t->id;
+    row.debit_account_id = p.debit_account_id;
+    row.credit_account_id = p.credit_account_id;
+    row.user_data_128 = U(t->user_data_128) > 0 ? t->user_data_128 : p.user_data_128;
+    row.user_data_64 = t->user_data_64 > 0 ? t->user_data_64 : p.user_data_64;
+    row.user_data_32 = t->user_data_32 > 0 ? t->user_data_32 : p.user_data_32;
+    row.ledger = p.ledger;
+    row.code = p.code;
+    row.pending_id = t->pending_id;
+    row.timeout = 0;
+    row.timestamp = timestamp_actual;
+    row.flags = t->flags;
+    row.amount = W(amount_actual);
+    /* dr/cr pointers stay valid: insert_transfer does not touch the accounts array. */
+    insert_transfer(c, &row, TB_PENDING_NONE);
+
+    if (has_expiry) {
+        /* The expires_at index entry is removed (status below); reset the pulse flag. */
+        if (c->pulse_next_timestamp == expires_at) c->pulse_next_timestamp = TB_TIMESTAMP_MIN;
+    }
+    update_pending_status(c, pi, (f & TB_TRANSFER_POST_PENDING) ? TB_PENDING_POSTED
+                                                                 : TB_PENDING_VOIDED);
+
+    tb_account_t dr_new = *dr, cr_new = *cr;
+    dr_new.debits_pending = W(U(dr_new.debits_pending) - U(p.amount));
+    cr_new.credits_pending = W(U(cr_new.credits_pending) - U(p.amount));
+    if (f & TB_TRANSFER_POST_PENDING) {
+        dr_new.debits_posted = W(U(dr_new.debits_posted) + amount_actual);
+        cr_new.credits_posted = W(U(cr_new.credits_posted) + amount_actual);
+    }
+    if (f & TB_TRANSFER_VOID_PENDING) {
+        if (p.flags & TB_TRANSFER_CLOSING_DEBIT) dr_new.flags &= (uint16_t)~TB_ACCOUNT_CLOSED;
+        if (p.flags & TB_TRANSFER_CLOSING_CREDIT) cr_new.flags &= (uint16_t)~TB_ACCOUNT_CLOSED;
+    }
+    if (amount_actual > 0 || U(p.amount) > 0 || dr_new.flags != dr->flags)
+        update_account(c, dr, &dr_new);
+    if (amount_actual > 0 || U(p.amount) > 0 || cr_new.flags != cr->flags)
+        update_account(c, cr, &cr_new);
+
+    c->commit_timestamp = timestamp_actual;
+    *ts = timestamp_actual;
+    return TB_STATUS_CREATED;
+}
+
+static uint32_t create_transfer(tbo_ctx* c, uint64_t timestamp_event, const tb_transfer_t* t,
+                                uint64_t* ts) {
+    const uint16_t f = t->flags;
+    if (f & TB_TRANSFER_PADDING_MASK) return TB_CT_RESERVED_FLAG;
+    u128 id = U(t->id);
+    if (id == 0) return TB_CT_ID_MUST_NOT_BE_ZERO;
+    if (id == U128_MAX) return TB_CT_ID_MUST_NOT_BE_INT_MAX;
+
+    uint64_t ei = 0;
+    switch (get_transfer(c, id, &ei)) {
+        case 1: {
+            const tb_transfer_t e = c->transfers[ei];
+            return create_transfer_exists(c, t, &e, ts);
+        }
+        case 2: return TB_CT_ID_ALREADY_FAILED;
+        default: break;
+    }
+
+    if (f & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING))
+        return post_or_void_pending_transfer(c, timestamp_event, t, ts);
+
+    u128 dr_id = U(t->debit_account_id), cr_id = U(t->credit_account_id);
+    if (dr_id == 0) return TB_CT_DEBIT_ACCOUNT_ID_MUST_NOT_BE_ZERO;
+    if (dr_id == U128_MAX) return TB_CT_DEBIT_ACCOUNT_ID_MUST_NOT_BE_INT_MAX;
+    if (cr_id == 0) return TB_CT_CREDIT_ACCOUNT_ID_MUST_NOT_BE_ZERO;
+    if (cr_id == U128_MAX) return TB_CT_CREDIT_ACCOUNT_ID_MUST_NOT_BE_INT_MAX;
+    if (cr_id == dr_id) return TB_CT_ACCOUNTS_MUST_BE_DIFFERENT;
+
+    if (U(t->pending_id) != 0) return TB_CT_PENDING_ID_MUST_BE_ZERO;
+    if (!(f & TB_TRANSFER_PENDING)) {
+        if (t->timeout != 0) return TB_CT_TIMEOUT_RESERVED_FOR_PENDING_TRANSFER;
+        if (f & (TB_TRANSFER_CLOSING_DEBIT | TB_TRANSFER_CLOSING_CREDIT))
+            return TB_CT_CLOSING_TRANSFER_MUST_BE_PENDING;
+    }
+    if (t->ledger == 0) return TB_CT_LEDGER_MUST_NOT_BE_ZERO;
+    if (t->code == 0) return TB_CT_CODE_MUST_NOT_BE_ZERO;
+
+    tb_account_t* dr = get_account(c, dr_id);
+    if (!dr) return TB_CT_DEBIT_ACCOUNT_NOT_FOUND;
+    tb_account_t* cr = get_account(c, cr_id);
+    if (!cr) return TB_CT_CREDIT_ACCOUNT_NOT_FOUND;
+
+    if (dr->ledger != cr->ledger) return TB_CT_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;
+    if (t->ledger != dr->ledger) return TB_CT_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
+
+    uint64_t timestamp_actual = timestamp_event;
+    if (f & TB_TRANSFER_IMPORTED) {
+        if (c->transfers_range.has && t->timestamp <= c->transfers_range.key_max)
+            return TB_CT_IMPORTED_EVENT_TIMESTAMP_MUST_NOT_REGRESS;
+        if (map_get(&c->account_by_ts, t->timestamp, NULL))
+            return TB_CT_IMPORTED_EVENT_TIMESTAMP_MUST_NOT_REGRESS;
+        if (t->timestamp <= dr->timestamp)
+            return TB_CT_IMPORTED_EVENT_TIMESTAMP_MUST_POSTDATE_DEBIT_ACCOUNT;
+        if (t->timestamp <= cr->timestamp)
+            return TB_CT_IMPORTED_EVENT_TIMESTAMP_MUST_POSTDATE_CREDIT_ACCOUNT;
+        if (t->timeout != 0) return TB_CT_IMPORTED_EVENT_TIMEOUT_MUST_BE_ZERO;
+        timestamp_actual = t->timestamp;
+    }
+
+    if (dr->flags & TB_ACCOUNT_CLOSED) return TB_CT_DEBIT_ACCOUNT_ALREADY_CLOSED;
+    if (cr->flags & TB_ACCOUNT_CLOSED) return TB_CT_CREDIT_ACCOUNT_ALREADY_CLOSED;
+
+    u128 amount = U(t->amount);
+    if (f & TB_TRANSFER_BALANCING_DEBIT) {
+        u128 dr_balance = U(dr->debits_posted) + U(dr->debits_pending);
+        u128 cp = U(dr->credits_posted);
+        u128 room = cp > dr_balance ? cp - dr_balance : 0; /* -| */
+        if (room < amount) amount = room;
+    }
+    if (f & TB_TRANSFER_BALANCING_CREDIT) {
+        u128 cr_balance = U(cr->credits_posted) + U(cr->credits_pending);
+        u128 dp = U(cr->debits_posted);
+        u128 room = dp > cr_balance ? dp - cr_balance : 0;
+        if (room < amount) amount = room;
+    }
+
+    if (f & TB_TRANSFER_PENDING) {
+        if (sum_overflows_u128(amount, U(dr->debits_pending))) return TB_CT_OVERFLOWS_DEBITS_PENDING;
+        if (sum_overflows_u128(amount, U(cr->credits_pending)))
+            return TB_CT_OVERFLOWS_CREDITS_PENDING;
+    }
+    if (sum_overflows_u128(amount, U(dr->debits_posted))) return TB_CT_OVERFLOWS_DEBITS_POSTED;
+    if (sum_overflows_u128(amount, U(cr->credits_posted))) return TB_CT_OVERFLOWS_CREDITS_POSTED;
+    if (sum_overflows_u128(amount, U(dr->debits_pending) + U(dr->debits_posted)))
+        return TB_CT_OVERFLOWS_DEBITS;
+    if (sum_overflows_u128(amount, U(cr->credits_pending) + U(cr->credits_posted)))
+        return TB_CT_OVERFLOWS_CREDITS;
+    /* u63 overflow of timestamp + timeout * 1e9 (the product always fits u63). */
+    if (timestamp_actual + (uint64_t)t->timeout * TB_NS_PER_S > TB_TIMESTAMP_MAX)
+        return TB_CT_OVERFLOWS_TIMEOUT;
+
+    if ((dr->flags & TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS) &&
+        U(dr->debits_pending) + U(dr->debits_posted) + amount > U(dr->credits_posted))
+        return TB_CT_EXCEEDS_CREDITS;
+    if ((cr->flags & TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS) &&
+        U(cr->credits_pending) + U(cr->credits_posted) + amount > U(cr->debits_posted))
+        return TB_CT_EXCEEDS_DEBITS;
+
+    tb_transfer_t row = *t;
+    row.amount = W(amount);
+    row.timestamp = timestamp_actual;
+    insert_transfer(c, &row, (f & TB_TRANSFER_PENDING) ? TB_PENDING_PENDING : TB_PENDING_NONE);
+
+    tb_account_t dr_new = *dr, cr_new = *cr;
+    if (f & TB_TRANSFER_PENDING) {
+        dr_new.debits_pending = W(U(dr_new.debits_pending) + amount);
+        cr_new.credits_pending = W(U(cr_new.credits_pending) + amount);
+    } else {
+        dr_new.debits_posted = W(U(dr_new.debits_posted) + amount);
+        cr_new.credits_posted = W(U(cr_new.credits_posted) + amount);
+    }
+    if (f & TB_TRANSFER_CLOSING_DEBIT) dr_new.flags |= TB_ACCOUNT_CLOSED;
+    if (f & TB_TRANSFER_CLOSING_CREDIT) cr_new.flags |= TB_ACCOUNT_CLOSED;
+    if (amount > 0 || (dr_new.flags & TB_ACCOUNT_CLOSED)) update_account(c, dr, &dr_new);
+    if (amount > 0 || (cr_new.flags & TB_ACCOUNT_CLOSED)) update_account(c, cr, &cr_new);
+
+    if (t->timeout > 0) {
+        uint64_t expires_at = timestamp_actual + (uint64_t)t->timeout * TB_NS_PER_S;
+        if (expires_at < c->pulse_next_timestamp) c->pulse_next_timestamp = expires_at;
+    }
+    c->commit_timestamp = timestamp_actual;
+    *ts = timestamp_actual;
+    return TB_STATUS_CREATED;
+}
+
+/* ---- execute_create (state_machine.zig:3002-3213) ------------------------------------------*/
+
+static void execute_create(tbo_ctx* c, int is_transfers, const void* events_, uint32_t n,
+                           uint64_t timestamp, tb_create_result_t* results) {
+    const tb_account_t* accounts = (const tb_account_t*)events_;
+    const tb_transfer_t* transfers = (const tb_transfer_t*)events_;
+    int64_t chain = -1;
+    int chain_broken = 0;
+    uint16_t imported_flag = is_transfers ? TB_TRANSFER_IMPORTED : TB_ACCOUNT_IMPORTED;
+    uint16_t linked_flag = is_transfers ? TB_TRANSFER_LINKED : TB_ACCOUNT_LINKED;
+    int batch_imported = n > 0 && ((is_transfers ? transfers[0].flags : accounts[0].flags) &
+                                   imported_flag) != 0;
+
+    for (uint32_t index = 0; index < n; index++) {
+        uint16_t flags = is_transfers ? transfers[index].flags : accounts[index].flags;
+        uint64_t ev_ts = is_transfers ? transfers[index].timestamp : accounts[index].timestamp;
+        const uint64_t timestamp_event = timestamp - n + index + 1;
+        uint32_t status;
+        uint64_t timestamp_actual = timestamp_event;
+
+        do {
+            if (flags & linked_flag) {
+                if (chain < 0) {
+                    chain = index;
+                    scope_open(c);
+                }
+                if (index == n - 1) {
+                    status = TB_CT_LINKED_EVENT_CHAIN_OPEN; /* same value for accounts */
+                    break;
+                }
+            }
+            if (chain_broken) {
+                status = TB_CT_LINKED_EVENT_FAILED;
+                break;
+            }
+            int imported = (flags & imported_flag) != 0;
+            if (batch_imported != imported) {
+                if (is_transfers)
+                    status = imported ? TB_CT_IMPORTED_EVENT_NOT_EXPECTED
+                                      : TB_CT_IMPORTED_EVENT_EXPECTED;
+                else
+                    status = imported ? TB_CA_IMPORTED_EVENT_NOT_EXPECTED
+                                      : TB_CA_IMPORTED_EVENT_EXPECTED;
+                break;
+            }
+            if (imported) {
+                if (ev_ts < TB_TIMESTAMP_MIN || ev_ts > TB_TIMESTAMP_MAX) {
+                    status = is_transfers ? TB_CT_IMPORTED_EVENT_TIMESTAMP_OUT_OF_RANGE
+                                          : TB_CA_IMPORTED_EVENT_TIMESTAMP_OUT_OF_RANGE;
+                    break;
+                }
+                if (ev_ts >= timestamp) {
+                    status = is_transfers ? TB_CT_IMPORTED_EVENT_TIMESTAMP_MUST_NOT_ADVANCE
+                                          : TB_CA_IMPORTED_EVENT_TIMESTAMP_MUST_NOT_ADVANCE;
+                    break;
+                }
+            } else if (ev_ts != 0) {
+                status = TB_CT_TIMESTAMP_MUST_BE_ZERO; /* same value for accounts */
+                break;
+            }
+            uint64_t ts = timestamp_event;
+            status = is_transfers ? create_transfer(c, timestamp_event, &transfers[index], &ts)
+                                  : create_account(c, timestamp_event, &accounts[index], &ts);
+            /* .created and .exists carry the object's timestamp (state_machine.zig:3098-3104). */
+            int exists = is_transfers ? status == TB_CT_EXISTS : status == TB_CA_EXISTS;
+            if (status == TB_STATUS_CREATED || exists) timestamp_actual = ts;
+        } while (0);
+
+        if (status != TB_STATUS_CREATED) {
+            if (chain >= 0) {
+                if (!chain_broken) {
+                    chain_broken = 1;
+                    scope_close(c, 1);
+                    for (int64_t ci = chain; ci < index; ci++)
+                        results[ci].status = TB_CT_LINKED_EVENT_FAILED;
+                }
+            }
+            /* transient_error: orphan the id (outside any scope). */
+            if (is_transfers && tb_transfer_status_transient(status)) {
+                map_put(&c->transfer_by_id, U(transfers[index].id), ORPHAN);
+            }
+        }
+        results[index].timestamp = timestamp_actual;
+        results[index].status = status;
+        results[index].reserved = 0;
+
+        if (chain >= 0 && (!(flags & linked_flag) || status == TB_CT_LINKED_EVENT_CHAIN_OPEN)) {
+            if (!chain_broken) scope_close(c, 0);
+            chain = -1;
+            chain_broken = 0;
+        }
+    }
+}
+
+void tbo_create_accounts(tbo_ctx* c, const tb_account_t* events, uint32_t n, uint64_t timestamp,
+                         tb_create_result_t* results) {
+    execute_create(c, 0, events, n, timestamp, results);
+}
+
+void tbo_create_transfers(tbo_ctx* c, const tb_transfer_t* events, uint32_t n,
+                          uint64_t timestamp, tb_create_result_t* results) {
+    execute_create(c, 1, events, n, timestamp, results);
+}
+
+/* ---- pulse ----------------------------------------------------------------------------------*/
+
+typedef struct {
+    uint64_t expires_at, timestamp, index;
+} expiry_key_t;
+
+static int expiry_cmp(const void* a_, const void* b_) {
+    const expiry_key_t* a = (const expiry_key_t*)a_;
+    const expiry_key_t* b = (const expiry_key_t*)b_;
+    if (a->expires_at != b->expires_at) return a->expires_at < b->expires_at ? -1 : 1;
+    if (a->timestamp != b->timestamp) return a->timestamp < b->timestamp ? -1 : 1;
+    return 0;
+}
+
+uint32_t tbo_pulse(tbo_ctx* c, uint64_t timestamp) {
+    /* Scan the expires_at index (entries: pending-status transfers with timeout > 0). */
+    expiry_key_t* keys = (expiry_key_t*)xrealloc(NULL, (c->n_expiry + 1) * sizeof(expiry_key_t));
+    uint64_t n_keys = 0, w = 0;
+    for (uint64_t k = 0; k < c->n_expiry; k++) {
+        uint64_t i = c->expiry[k];
+        if (c->pending_status[i] != TB_PENDING_PENDING) continue; /* removed from the index */
+        c->expiry[w++] = i;                                        /* compact the list */
+        const tb_transfer_t* p = &c->transfers[i];
+        keys[n_keys].expires_at = p->timestamp + (uint64_t)p->timeout * TB_NS_PER_S;
+        keys[n_keys].timestamp = p->timestamp;
+        keys[n_keys].index = i;
+        n_keys++;
+    }
+    c->n_expiry = w;
+    qsort(keys, n_keys, sizeof(expiry_key_t), expiry_cmp);
+
+    uint64_t expired = 0;
+    while (expired < n_keys && expired < c->pulse_batch_max &&
+           keys[expired].expires_at <= timestamp)
+        expired++;
+
+    /* ExpirePendingTransfers.finish: buffer_finished iff the buffer filled up. */
+    if (expired == c->pulse_batch_max) {
+        c->pulse_next_timestamp = keys[expired - 1].expires_at;
+    } else if (expired < n_keys) {
+        c->pulse_next_timestamp = keys[expired].expires_at; /* first unexpired */
+    } else {
+        c->pulse_next_timestamp = TB_TIMESTAMP_MAX;
+    }
+
+    for (uint64_t k = 0; k < expired; k++) {
+        const tb_transfer_t* p = &c->transfers[keys[k].index];
+        tb_account_t* dr = get_account(c, U(p->debit_account_id));
+        tb_account_t* cr = get_account(c, U(p->credit_account_id));
+        if (!dr || !cr) abort();
+        tb_account_t dr_new = *dr, cr_new = *cr;
+        dr_new.debits_pending = W(U(dr_new.debits_pending) - U(p->amount));
+        cr_new.credits_pending = W(U(cr_new.credits_pending) - U(p->amount));
+        if (p->flags & TB_TRANSFER_CLOSING_DEBIT) dr_new.flags &= (uint16_t)~TB_ACCOUNT_CLOSED;
+        if (p->flags & TB_TRANSFER_CLOSING_CREDIT) cr_new.flags &= (uint16_t)~TB_ACCOUNT_CLOSED;
+        *dr = dr_new;
+        *cr = cr_new;
+        c->pending_status[keys[k].index] = TB_PENDING_EXPIRED;
+        c->commit_timestamp = timestamp - expired + k + 1;
+    }
+    free(keys);
+    return (uint32_t)expired;
+}
+
+int tbo_pulse_needed(const tbo_ctx* c, uint64_t timestamp) {
+    return c->pulse_next_timestamp <= timestamp;
+}
+
+uint64_t tbo_pulse_next_timestamp(const tbo_ctx* c) { return c->pulse_next_timestamp; }
+
+/* ---- lookups / dumps ------------------------------------------------------------------------*/
+
+uint32_t tbo_lookup_accounts(const tbo_ctx* c, const tb_uint128_t* ids, uint32_t n,
+                             tb_account_t* out) {
+    uint32_t count = 0;
+    for (uint32_t k = 0; k < n; k++) {
+        uint64_t v;
+        if (map_get(&c->account_by_id, U(ids[k]), &v)) out[count++] = c->accounts[v];
+    }
+    return count;
+}
+
+uint32_t tbo_lookup_transfers(const tbo_ctx* c, const tb_uint128_t* ids, uint32_t n,
+                              tb_transfer_t* out) {
+    uint32_t count = 0;
+    for (uint32_t k = 0; k < n; k++) {
+        uint64_t v;
+        if (map_get(&c->transfer_by_id, U(ids[k]), &v) && v != ORPHAN)
+            out[count++] = c->transfers[v];
+    }
+    return count;
+}
+
+int tbo_set_account_balances(tbo_ctx* c, tb_uint128_t id, tb_uint128_t debits_pending,
+                             tb_uint128_t debits_posted, tb_uint128_t credits_pending,
+                             tb_uint128_t credits_posted) {
+    tb_account_t* a = get_account(c, U(id));
+    if (!a) return -1;
+    a->debits_pending = debits_pending;
+    a->debits_posted = debits_posted;
+    a->credits_pending = credits_pending;
+    a->credits_posted = credits_posted;
+    return 0;
+}
+
+uint64_t tbo_account_count(const tbo_ctx* c) { return c->n_accounts; }
+uint64_t tbo_transfer_count(const tbo_ctx* c) { return c->n_transfers; }
+
+uint64_t tbo_dump_accounts(const tbo_ctx* c, tb_account_t* out) {
+    if (out) memcpy(out, c->accounts, c->n_accounts * sizeof(tb_account_t));
+    return c->n_accounts;
+}
+uint64_t tbo_dump_transfers(const tbo_ctx* c, tb_transfer_t* out) {
+    if (out) memcpy(out, c->transfers, c->n_transfers * sizeof(tb_transfer_t));
+    return c->n_transfers;
+}
+uint64_t tbo_dump_pending_status(const tbo_ctx* c, uint8_t* out) {
+    if (out) memcpy(out, c->pending_status, c->n_transfers);
+    return c->n_transfers;
+}
+
+/* ---- executor binding (tb_state_machine.h) --------------------------------------------------*/
+
+static int ex_create_accounts(void* self, const tb_account_t* events, uint32_t n,
+                              const uint32_t* lens, const uint64_t* ts, uint32_t nb,
+                              tb_create_result_t* results) {
+    uint32_t offset = 0;
+    for (uint32_t b = 0; b < nb; b++) {
+        tbo_create_accounts((tbo_ctx*)self, events + offset, lens[b], ts[b], results + offset);
+        offset += lens[b];
+    }
+    return offset == n ? 0 : -22;
+}
+static int ex_create_transfers(void* self, const tb_transfer_t* events, uint32_t n,
+                               const uint32_t* lens, const uint64_t* ts, uint32_t nb,
+                               tb_create_result_t* results) {
+    uint32_t offset = 0;
+    for (uint32_t b = 0; b < nb; b++) {
+        tbo_create_transfers((tbo_ctx*)self, events + offset, lens[b], ts[b], results + offset);
+        offset += lens[b];
+    }
+    return offset == n ? 0 : -22;
+}
+static int64_t ex_pulse(void* self, uint64_t ts) { return tbo_pulse((tbo_ctx*)self, ts); }
+static uint64_t ex_pulse_next(void* self) { return tbo_pulse_next_timestamp((tbo_ctx*)self); }
+static int64_t ex_lookup_accounts(void* self, const tb_uint128_t* ids, uint32_t n,
+                                  tb_account_t* out) {
+    return tbo_lookup_accounts((tbo_ctx*)self, ids, n, out);
+}
+static int64_t ex_lookup_transfers(void* self, const tb_uint128_t* ids, uint32_t n,
+                                   tb_transfer_t* out) {
+    return tbo_lookup_transfers((tbo_ctx*)self, ids, n, out);
+}
+
+void tbo_executor_fill(tbo_ctx* c, tb_executor* ex) {
+    ex->self = c;
+    ex->create_accounts = ex_create_accounts;
+    ex->create_transfers = ex_create_transfers;
+    ex->pulse = ex_pulse;
+    ex->pulse_next_timestamp = ex_pulse_next;
+    ex->lookup_accounts = ex_lookup_accounts;
+    ex->lookup_transfers = ex_lookup_transfers;
+}

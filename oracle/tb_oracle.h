@@ -1,0 +1,70 @@
+/*
+ * tb_oracle.h -- CPU oracle for the create_accounts / create_transfers commit path.
+ *
+ * TEST INFRASTRUCTURE ONLY. This is a serial, single-threaded C restatement of the reference's
+ * state machine (src/state_machine.zig) used as the parity checker for the HIP executor and as
+ * the CPU baseline leg of bench.py. Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline may load it; the product path (tigerbeetle_amd/, libtbg.so) never does.
+ *
+ * Parity is pinned by the reference's own table-driven tests (src/state_machine_tests.zig,
+ * transcribed as data under tests/golden/tables/ by tests/golden/extract_tables.py).
+ */
+#ifndef TB_ORACLE_H
+#define TB_ORACLE_H
+
+#include "../include/tb_types.h"
+#include "../include/tb_state_machine.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct tbo_ctx tbo_ctx;
+
+/* pulse_batch_max: transfers expired per pulse (batch_max.create_transfers; 8190 in production,
+ * 30 under the reference's test config). pulse_next_timestamp_init: TB_TIMESTAMP_MIN in
+ * production (state_machine.zig:4908), TB_TIMESTAMP_MAX in the unit-test harness
+ * (state_machine_tests.zig:148-157). */
+tbo_ctx* tbo_open(uint32_t pulse_batch_max, uint64_t pulse_next_timestamp_init);
+void tbo_close(tbo_ctx* ctx);
+
+/* execute_create (state_machine.zig:3002-3213) for one batch whose highest timestamp is
+ * `timestamp`; event i gets timestamp - n + i + 1. Writes n dense results. */
+void tbo_create_accounts(tbo_ctx* ctx, const tb_account_t* events, uint32_t n, uint64_t timestamp,
+                         tb_create_result_t* results);
+void tbo_create_transfers(tbo_ctx* ctx, const tb_transfer_t* events, uint32_t n,
+                          uint64_t timestamp, tb_create_result_t* results);
+
+/* pulse: prefetch_expire_pending_transfers + execute_expire_pending_transfers
+ * (state_machine.zig:2436-2562, :4511-4628, :4875-5029). Returns the number expired. */
+uint32_t tbo_pulse(tbo_ctx* ctx, uint64_t timestamp);
+int tbo_pulse_needed(const tbo_ctx* ctx, uint64_t timestamp);
+uint64_t tbo_pulse_next_timestamp(const tbo_ctx* ctx);
+
+/* execute_lookup_accounts / execute_lookup_transfers (state_machine.zig:3255-3292):
+ * found objects only, in request order. Returns the count written. */
+uint32_t tbo_lookup_accounts(const tbo_ctx* ctx, const tb_uint128_t* ids, uint32_t n,
+                             tb_account_t* out);
+uint32_t tbo_lookup_transfers(const tbo_ctx* ctx, const tb_uint128_t* ids, uint32_t n,
+                              tb_transfer_t* out);
+
+/* Test-harness `setup` action (state_machine_tests.zig:657-676): overwrite balances. */
+int tbo_set_account_balances(tbo_ctx* ctx, tb_uint128_t id, tb_uint128_t debits_pending,
+                             tb_uint128_t debits_posted, tb_uint128_t credits_pending,
+                             tb_uint128_t credits_posted);
+
+/* Dumps for parity checks. Returns counts; `out` may be NULL to query the count. */
+uint64_t tbo_account_count(const tbo_ctx* ctx);
+uint64_t tbo_transfer_count(const tbo_ctx* ctx);
+uint64_t tbo_dump_accounts(const tbo_ctx* ctx, tb_account_t* out);   /* creation order */
+uint64_t tbo_dump_transfers(const tbo_ctx* ctx, tb_transfer_t* out); /* creation order */
+uint64_t tbo_dump_pending_status(const tbo_ctx* ctx, uint8_t* out);  /* per transfer */
+
+/* Binds this oracle as a tb_executor (tb_state_machine.h) for the StateMachine mirror. */
+void tbo_executor_fill(tbo_ctx* ctx, tb_executor* ex);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TB_ORACLE_H */

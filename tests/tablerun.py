@@ -1,0 +1,513 @@
+"""Table-test runner: the reference's state-machine table DSL and TestContext, restated in Python.
+
+Follows src/testing/table.zig (row DSL) and src/state_machine_tests.zig:37-1086 (TestContext,
+TestAction, check_version for the dense `create_*` operation encoding). Each table row is an input
+event with its expected result; `commit <op>` submits the accumulated batch through a StateMachine
+(tb_sm_*, include/tb_state_machine.h) and compares the reply byte-for-byte with the expected reply
+derived by the harness rules (:704-735, :757-811).
+
+The StateMachine under test is bound to an executor: the CPU oracle (oracle/liboracle.so) or the
+HIP executor (libtbg.so). Query operations outside this path (get_account_transfers,
+get_account_balances, query_*, get_change_events) are skipped: they do not change state.
+"""
+import ctypes
+import os
+import struct
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from tigerbeetle_amd import native  # noqa: E402
+from tigerbeetle_amd.types import (  # noqa: E402
+    ACCOUNT_DTYPE, RESULT_DTYPE, TRANSFER_DTYPE, CreateAccountStatus, CreateTransferStatus,
+    Operation, TIMESTAMP_MAX, U128_MAX, NS_PER_S)
+
+TABLE_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "tables")
+
+# The reference's unit-test configuration (config.zig test_min + state_machine_tests.zig:123):
+# message_size_max = 4096 -> message_body_size_max = 3840; batch_size_limit = 30 * 128.
+TEST_MESSAGE_BODY_SIZE_MAX = 4096 - 256
+TEST_BATCH_SIZE_LIMIT = 30 * 128
+# batch_max.create_transfers = max(event_max) over the create_transfers encodings
+# = message_body_size_max / 128 (the unbatched encoding) = 30.
+TEST_PULSE_BATCH_MAX = TEST_MESSAGE_BODY_SIZE_MAX // 128
+
+SKIPPED_OPS = {"get_account_transfers", "get_account_balances", "query_accounts",
+               "query_transfers", "get_change_events"}
+
+
+# ---- row DSL (src/testing/table.zig) --------------------------------------------------------
+
+class Tokens:
+    def __init__(self, toks):
+        self.toks = toks
+        self.i = 0
+
+    def next(self):
+        t = self.toks[self.i]
+        self.i += 1
+        return t
+
+    def peek(self):
+        return self.toks[self.i] if self.i < len(self.toks) else None
+
+    def eat(self, t):
+        if self.peek() == t:
+            self.i += 1
+            return True
+        return False
+
+
+def parse_uint(tok: str, bits: int) -> int:
+    off = 1 if tok[0].isalpha() else 0
+    body = tok[off:]
+    mx = (1 << bits) - 1
+    if body.startswith("-"):
+        return mx - int(body[1:])
+    v = int(body)
+    assert 0 <= v <= mx, tok
+    return v
+
+
+def parse_int(tok: str) -> int:
+    off = 1 if tok[0].isalpha() else 0
+    return int(tok[off:])
+
+
+# Field specs: (name, kind, default). kind: ("u", bits) | ("flag", NAME) | ("status",)
+ACCOUNT_FIELDS = [
+    ("id", ("u", 128), None), ("debits_pending", ("u", 128), 0), ("debits_posted", ("u", 128), 0),
+    ("credits_pending", ("u", 128), 0), ("credits_posted", ("u", 128), 0),
+    ("user_data_128", ("u", 128), 0), ("user_data_64", ("u", 64), 0),
+    ("user_data_32", ("u", 32), 0), ("reserved", ("u", 1), 0), ("ledger", ("u", 32), None),
+    ("code", ("u", 16), None), ("LNK", ("flag", "LNK"), 0), ("D<C", ("flag", "D<C"), 0),
+    ("C<D", ("flag", "C<D"), 0), ("HIST", ("flag", "HIST"), 0), ("IMP", ("flag", "IMP"), 0),
+    ("CLSD", ("flag", "CLSD"), 0), ("padding", ("u", 10), 0), ("timestamp", ("u", 64), 0),
+]
+ACCOUNT_FLAG_BITS = {"LNK": 0, "D<C": 1, "C<D": 2, "HIST": 3, "IMP": 4, "CLSD": 5}
+
+TRANSFER_FIELDS = [
+    ("id", ("u", 128), None), ("debit_account_id", ("u", 128), None),
+    ("credit_account_id", ("u", 128), None), ("amount", ("u", 128), 0),
+    ("pending_id", ("u", 128), 0), ("user_data_128", ("u", 128), 0),
+    ("user_data_64", ("u", 64), 0), ("user_data_32", ("u", 32), 0), ("timeout", ("u", 32), 0),
+    ("ledger", ("u", 32), None), ("code", ("u", 16), None), ("LNK", ("flag", "LNK"), 0),
+    ("PEN", ("flag", "PEN"), 0), ("POS", ("flag", "POS"), 0), ("VOI", ("flag", "VOI"), 0),
+    ("BDR", ("flag", "BDR"), 0), ("BCR", ("flag", "BCR"), 0), ("IMP", ("flag", "IMP"), 0),
+    ("CDR", ("flag", "CDR"), 0), ("CCR", ("flag", "CCR"), 0), ("padding", ("u", 5), 0),
+    ("timestamp", ("u", 64), 0),
+]
+TRANSFER_FLAG_BITS = {"LNK": 0, "PEN": 1, "POS": 2, "VOI": 3, "BDR": 4, "BCR": 5, "CDR": 6,
+                      "CCR": 7, "IMP": 8}
+
+
+def parse_fields(tokens: Tokens, spec):
+    out = {}
+    for name, kind, default in spec:
+        if default is not None and tokens.eat("_"):
+            out[name] = default
+            continue
+        tok = tokens.next()
+        if kind[0] == "u":
+            out[name] = parse_uint(tok, kind[1])
+        elif kind[0] == "flag":
+            assert tok == kind[1], (tok, kind)
+            out[name] = 1
+    return out
+
+
+def parse_row(line: str):
+    toks = line.split()
+    if not toks:
+        return None
+    t = Tokens(toks)
+    kind = t.next()
+    row = {"kind": kind}
+    if kind == "account":
+        row.update(parse_fields(t, ACCOUNT_FIELDS))
+        row["status"] = CreateAccountStatus[t.next()]
+    elif kind == "transfer":
+        row.update(parse_fields(t, TRANSFER_FIELDS))
+        row["status"] = CreateTransferStatus[t.next()]
+    elif kind == "setup":
+        row["account"] = parse_uint(t.next(), 128)
+        for f in ("debits_pending", "debits_posted", "credits_pending", "credits_posted"):
+            row[f] = parse_uint(t.next(), 128)
+    elif kind == "tick":
+        row["value"] = parse_int(t.next())
+        row["unit"] = t.next()
+        assert row["unit"] in ("nanoseconds", "seconds")
+    elif kind == "commit":
+        row["operation"] = t.next()
+    elif kind == "lookup_account":
+        row["id"] = parse_uint(t.next(), 128)
+        if t.eat("_"):
+            row["data"] = None
+        else:
+            d = {}
+            for f in ("debits_pending", "debits_posted", "credits_pending", "credits_posted"):
+                d[f] = parse_uint(t.next(), 128)
+            if t.eat("_"):
+                d["closed"] = False
+            else:
+                assert t.next() == "CLSD"
+                d["closed"] = True
+            row["data"] = d
+    elif kind == "lookup_transfer":
+        row["id"] = parse_uint(t.next(), 128)
+        variant = t.next()
+        tok = t.next()
+        if variant == "exists":
+            row["data"] = ("exists", tok in ("1", "true", "T"))
+        elif variant == "amount":
+            row["data"] = ("amount", parse_uint(tok, 128))
+        elif variant == "timestamp":
+            row["data"] = ("timestamp", parse_uint(tok, 64))
+        else:
+            raise ValueError(line)
+    elif kind.split("_result")[0] in SKIPPED_OPS or kind in SKIPPED_OPS:
+        row["kind"] = "skip"
+        row["op"] = kind
+        return row
+    else:
+        raise ValueError(f"unknown row: {line}")
+    rest = t.peek()
+    assert rest is None or rest == "//", line
+    return row
+
+
+def load_table(path: str):
+    rows = []
+    for line in open(path):
+        line = line.rstrip("\n")
+        if line.startswith("#"):
+            continue
+        r = parse_row(line)
+        if r is not None:
+            rows.append(r)
+    return rows
+
+
+def table_files():
+    return sorted(f for f in os.listdir(TABLE_DIR) if f.endswith(".txt"))
+
+
+# ---- event images -----------------------------------------------------------------------------
+
+def _set_u128(rec, name, v):
+    rec[name][0] = v & 0xFFFFFFFFFFFFFFFF
+    rec[name][1] = v >> 64
+
+
+def account_event(r) -> np.ndarray:
+    a = np.zeros(1, dtype=ACCOUNT_DTYPE)[0]
+    for f in ("id", "debits_pending", "debits_posted", "credits_pending", "credits_posted",
+              "user_data_128"):
+        _set_u128(a, f, r[f])
+    a["user_data_64"] = r["user_data_64"]
+    a["user_data_32"] = r["user_data_32"]
+    a["reserved"] = r["reserved"]
+    a["ledger"] = r["ledger"]
+    a["code"] = r["code"]
+    flags = r["padding"] << 6
+    for name, bit in ACCOUNT_FLAG_BITS.items():
+        if r[name]:
+            flags |= 1 << bit
+    a["flags"] = flags
+    a["timestamp"] = r["timestamp"]
+    return a
+
+
+def transfer_event(r) -> np.ndarray:
+    t = np.zeros(1, dtype=TRANSFER_DTYPE)[0]
+    for f in ("id", "debit_account_id", "credit_account_id", "amount", "pending_id",
+              "user_data_128"):
+        _set_u128(t, f, r[f])
+    t["user_data_64"] = r["user_data_64"]
+    t["user_data_32"] = r["user_data_32"]
+    t["timeout"] = r["timeout"]
+    t["ledger"] = r["ledger"]
+    t["code"] = r["code"]
+    flags = r["padding"] << 9
+    for name, bit in TRANSFER_FLAG_BITS.items():
+        if r[name]:
+            flags |= 1 << bit
+    t["flags"] = flags
+    t["timestamp"] = r["timestamp"]
+    return t
+
+
+def u128_of(rec, name) -> int:
+    return int(rec[name][0]) | (int(rec[name][1]) << 64)
+
+
+# ---- StateMachine harness (TestContext, state_machine_tests.zig:37-285) ------------------------
+
+class StateMachineHandle:
+    """A tb_sm bound to an executor, plus the executor's `setup` hook."""
+
+    def __init__(self, lib, sm, set_balances, close):
+        self.lib = lib
+        self.sm = sm
+        self.set_balances = set_balances
+        self._close = close
+        self.output = ctypes.create_string_buffer(TEST_MESSAGE_BODY_SIZE_MAX + 256)
+
+    def close(self):
+        self._close()
+
+
+def encode_multi_batch(lib, payload: bytes, element_size: int) -> bytes:
+    n = len(payload) // element_size
+    trailer = lib.tb_multi_batch_trailer_total_size(element_size, 1)
+    buf = ctypes.create_string_buffer(len(payload) + trailer + 2)
+    ctypes.memmove(buf, payload, len(payload))
+    counts = (ctypes.c_uint16 * 1)(n)
+    size = lib.tb_multi_batch_encode_trailer(buf, len(payload), element_size, counts, 1)
+    assert size > 0
+    return buf.raw[:size]
+
+
+def decode_multi_batch_single(lib, body: bytes, element_size: int) -> bytes:
+    counts = (ctypes.c_uint16 * 8)()
+    payload = ctypes.c_uint32(0)
+    nb = lib.tb_multi_batch_decode(body, len(body), element_size, counts, 8,
+                                   ctypes.byref(payload))
+    assert nb == 1, nb
+    return body[:payload.value]
+
+
+class TableContext:
+    def __init__(self, handle: StateMachineHandle):
+        self.h = handle
+        self.lib = handle.lib
+        self.sm = handle.sm
+        self.op = 1
+        self._cb = native.PREFETCH_CALLBACK(lambda ctx: None)
+
+    # TestContext.prepare (:230-241)
+    def prepare(self, operation: int, body: bytes):
+        lib, sm = self.lib, self.sm
+        lib.tb_sm_set_commit_timestamp(sm, lib.tb_sm_get_prepare_timestamp(sm))
+        lib.tb_sm_set_prepare_timestamp(sm, lib.tb_sm_get_prepare_timestamp(sm) + 1)
+        lib.tb_sm_prepare(sm, operation, body, len(body))
+
+    # TestContext.execute (:258-285)
+    def execute(self, operation: int, body: bytes) -> bytes:
+        lib, sm = self.lib, self.sm
+        timestamp = lib.tb_sm_get_prepare_timestamp(sm)
+        lib.tb_sm_set_prefetch_timestamp(sm, timestamp)
+        lib.tb_sm_prefetch(sm, self._cb, None, self.op, self.op, operation, body, len(body))
+        size = lib.tb_sm_commit(sm, 1, 0, self.op, timestamp, operation, body, len(body),
+                                self.h.output)
+        assert size >= 0, f"commit failed: {size}"
+        return self.h.output.raw[:size]
+
+    # TestContext.pulse (:243-256)
+    def pulse(self):
+        lib, sm = self.lib, self.sm
+        if lib.tb_sm_pulse_needed(sm, lib.tb_sm_get_prepare_timestamp(sm)):
+            self.prepare(Operation.pulse, b"")
+            size = self.execute(Operation.pulse, b"")
+            assert len(size) == 0
+            self.op += 1
+
+    # TestContext.submit (:178-228)
+    def submit(self, operation: int, payload: bytes, element_size: int, result_size: int) -> bytes:
+        body = encode_multi_batch(self.lib, payload, element_size)
+        assert self.lib.tb_sm_input_valid(self.sm, operation, body, len(body)) == 1
+        self.prepare(operation, body)
+        pulse_needed = self.lib.tb_sm_pulse_needed(self.sm,
+                                                   self.lib.tb_sm_get_prepare_timestamp(self.sm))
+        reply = self.execute(operation, body)
+        if pulse_needed:
+            self.pulse()
+        return decode_multi_batch_single(self.lib, reply, result_size)
+
+
+class TableMismatch(AssertionError):
+    pass
+
+
+def run_table(handle: StateMachineHandle, rows, label=""):
+    """check_version (state_machine_tests.zig:620-1079) for the dense create_* encoding."""
+    ctx = TableContext(handle)
+    lib, sm = ctx.lib, ctx.sm
+    accounts = {}
+    transfers = {}
+    linked_events_failed = {}
+    request = []
+    reply = []
+    operation = None
+    commits = 0
+
+    for row in rows:
+        kind = row["kind"]
+        if kind == "skip":
+            operation = "skip"
+            continue
+        if kind == "setup":
+            assert operation is None
+            rc = handle.set_balances(row["account"], row["debits_pending"], row["debits_posted"],
+                                     row["credits_pending"], row["credits_posted"])
+            assert rc == 0, f"setup of unknown account {row['account']}"
+        elif kind == "tick":
+            interval = abs(row["value"]) * (1 if row["unit"] == "nanoseconds" else NS_PER_S)
+            pts = lib.tb_sm_get_prepare_timestamp(sm)
+            pts += interval if row["value"] > 0 else TIMESTAMP_MAX - interval
+            lib.tb_sm_set_prepare_timestamp(sm, pts & 0xFFFFFFFFFFFFFFFF)
+            ctx.pulse()
+        elif kind == "account":
+            assert operation in (None, "create_accounts")
+            operation = "create_accounts"
+            event = account_event(row)
+            request.append(event.tobytes())
+            timestamp_commit = lib.tb_sm_get_prepare_timestamp(sm) + 1 + len(request)
+            if event["timestamp"] == 0:
+                event["timestamp"] = timestamp_commit
+            status = row["status"]
+            if status == CreateAccountStatus.created:
+                accounts[row["id"]] = event.copy()
+            if status in (CreateAccountStatus.created, CreateAccountStatus.linked_event_failed):
+                ts = int(event["timestamp"])
+            elif status == CreateAccountStatus.exists:
+                ts = int(accounts[row["id"]]["timestamp"]) if row["id"] in accounts \
+                    else linked_events_failed[row["id"]]
+            else:
+                ts = timestamp_commit
+            reply.append(struct.pack("<QII", ts, int(status), 0))
+            if row["LNK"]:
+                if status == CreateAccountStatus.linked_event_failed:
+                    assert row["id"] not in linked_events_failed
+                    linked_events_failed[row["id"]] = int(event["timestamp"])
+            else:
+                linked_events_failed.clear()
+        elif kind == "transfer":
+            assert operation in (None, "create_transfers")
+            operation = "create_transfers"
+            event = transfer_event(row)
+            request.append(event.tobytes())
+            timestamp_commit = lib.tb_sm_get_prepare_timestamp(sm) + 1 + len(request)
+            if row["timestamp"] == 0:
+                event["timestamp"] = timestamp_commit
+            status = row["status"]
+            if status == CreateTransferStatus.created:
+                if row["pending_id"] != 0:
+                    p = transfers[row["pending_id"]]
+                    for f in ("debit_account_id", "credit_account_id", "user_data_128"):
+                        if u128_of(event, f) == 0:
+                            event[f] = p[f]
+                    for f in ("ledger", "code", "user_data_64", "user_data_32"):
+                        if int(event[f]) == 0:
+                            event[f] = p[f]
+                    if int(event["flags"]) & (1 << 3) and u128_of(event, "amount") == 0:
+                        event["amount"] = p["amount"]
+                transfers[row["id"]] = event.copy()
+            if status in (CreateTransferStatus.created, CreateTransferStatus.linked_event_failed):
+                ts = int(event["timestamp"])
+            elif status == CreateTransferStatus.exists:
+                ts = int(transfers[row["id"]]["timestamp"]) if row["id"] in transfers \
+                    else linked_events_failed[row["id"]]
+            else:
+                ts = timestamp_commit
+            reply.append(struct.pack("<QII", ts, int(status), 0))
+            if row["LNK"]:
+                if status == CreateTransferStatus.linked_event_failed:
+                    assert row["id"] not in linked_events_failed
+                    linked_events_failed[row["id"]] = int(event["timestamp"])
+            else:
+                linked_events_failed.clear()
+        elif kind == "lookup_account":
+            assert operation in (None, "lookup_accounts")
+            operation = "lookup_accounts"
+            request.append(struct.pack("<QQ", row["id"] & 0xFFFFFFFFFFFFFFFF, row["id"] >> 64))
+            d = row["data"]
+            if d is not None:
+                a = accounts[row["id"]].copy()
+                for f in ("debits_pending", "debits_posted", "credits_pending", "credits_posted"):
+                    _set_u128(a, f, d[f])
+                flags = int(a["flags"]) & ~(1 << 5)
+                if d["closed"]:
+                    flags |= 1 << 5
+                a["flags"] = flags
+                reply.append(a.tobytes())
+        elif kind == "lookup_transfer":
+            assert operation in (None, "lookup_transfers")
+            operation = "lookup_transfers"
+            request.append(struct.pack("<QQ", row["id"] & 0xFFFFFFFFFFFFFFFF, row["id"] >> 64))
+            variant, value = row["data"]
+            if variant == "exists":
+                if value:
+                    reply.append(transfers[row["id"]].tobytes())
+            else:
+                t = transfers[row["id"]].copy()
+                if variant == "amount":
+                    _set_u128(t, "amount", value)
+                else:
+                    t["timestamp"] = value
+                reply.append(t.tobytes())
+        elif kind == "commit":
+            op_name = row["operation"]
+            if operation == "skip" or op_name in SKIPPED_OPS:
+                request.clear()
+                reply.clear()
+                operation = None
+                continue
+            assert operation in (None, op_name), (operation, op_name)
+            commits += 1
+            payload = b"".join(request)
+            if op_name == "create_accounts":
+                actual = ctx.submit(Operation.create_accounts, payload, 128, 16)
+            elif op_name == "create_transfers":
+                actual = ctx.submit(Operation.create_transfers, payload, 128, 16)
+            elif op_name == "lookup_accounts":
+                actual = ctx.submit(Operation.lookup_accounts, payload, 16, 128)
+            elif op_name == "lookup_transfers":
+                actual = ctx.submit(Operation.lookup_transfers, payload, 16, 128)
+            else:
+                raise ValueError(op_name)
+            expected = b"".join(reply)
+            if actual != expected:
+                raise TableMismatch(describe_mismatch(label, commits, op_name, expected, actual))
+            request.clear()
+            reply.clear()
+            operation = None
+        else:
+            raise ValueError(kind)
+    assert operation is None and not request and not reply
+    return commits
+
+
+def describe_mismatch(label, commit_index, op_name, expected: bytes, actual: bytes) -> str:
+    lines = [f"{label}: commit #{commit_index} ({op_name}) reply mismatch "
+             f"(expected {len(expected)} B, actual {len(actual)} B)"]
+    if op_name.startswith("create"):
+        e = np.frombuffer(expected, dtype=RESULT_DTYPE)
+        a = np.frombuffer(actual, dtype=RESULT_DTYPE)
+        enum_t = CreateAccountStatus if op_name == "create_accounts" else CreateTransferStatus
+        for i in range(max(len(e), len(a))):
+            es = (int(e[i]["timestamp"]), enum_t(int(e[i]["status"])).name) if i < len(e) else None
+            as_ = (int(a[i]["timestamp"]), enum_t(int(a[i]["status"])).name) if i < len(a) else None
+            mark = "   " if es == as_ else ">>>"
+            lines.append(f"{mark} [{i}] expected={es} actual={as_}")
+    else:
+        dt = ACCOUNT_DTYPE if op_name == "lookup_accounts" else TRANSFER_DTYPE
+        e = np.frombuffer(expected, dtype=dt)
+        a = np.frombuffer(actual, dtype=dt)
+        for i in range(max(len(e), len(a))):
+            ei = e[i] if i < len(e) else None
+            ai = a[i] if i < len(a) else None
+            mark = "   " if (ei is not None and ai is not None and ei.tobytes() == ai.tobytes()) \
+                else ">>>"
+            lines.append(f"{mark} [{i}] expected={ei}\n        actual={ai}")
+    return "\n".join(lines)
+
+
+def sm_options():
+    o = native.SmOptions()
+    o.batch_size_limit = TEST_BATCH_SIZE_LIMIT
+    o.message_body_size_max = TEST_MESSAGE_BODY_SIZE_MAX
+    o.pulse_batch_max = TEST_PULSE_BATCH_MAX
+    return o

@@ -1,0 +1,349 @@
+// StateMachine mirror for the commit path (include/tb_state_machine.h).
+//
+// Restates the host-side control of src/state_machine.zig for the operations of this path:
+// input_valid / batch_valid (:980-1067), prepare / prepare_delta_nanoseconds (:1070-1136),
+// pulse_needed (:1138-1144), prefetch (:1146-1226; a no-op here), commit (:2564-2669) and
+// execute_multi_batch (:2702-2762), plus the multi-batch codec (src/vsr/multi_batch.zig). The
+// per-event work is delegated to a tb_executor: the HIP executor (tbg.h) in production.
+
+#include "../../include/tb_state_machine.h"
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <vector>
+
+namespace {
+
+constexpr uint16_t kBatchCountMax = 0xFFFF - 1;  // Postamble.batch_count_max
+constexpr uint16_t kTrailerPadding = 0xFFFF;      // TrailerItem.padding
+
+uint32_t div_ceil(uint32_t a, uint32_t b) { return (a + b - 1) / b; }
+
+struct OperationInfo {
+    uint32_t event_size;
+    uint32_t result_size;
+    bool multi_batch;
+};
+
+bool operation_info(uint8_t operation, OperationInfo* info) {
+    switch (operation) {
+        case TB_OPERATION_PULSE: *info = {0, 1, false}; return true;
+        case TB_OPERATION_CREATE_ACCOUNTS: *info = {128, 16, true}; return true;
+        case TB_OPERATION_CREATE_TRANSFERS: *info = {128, 16, true}; return true;
+        case TB_OPERATION_LOOKUP_ACCOUNTS: *info = {16, 128, true}; return true;
+        case TB_OPERATION_LOOKUP_TRANSFERS: *info = {16, 128, true}; return true;
+        default: return false;
+    }
+}
+
+}  // namespace
+
+extern "C" uint32_t tb_multi_batch_trailer_total_size(uint32_t element_size,
+                                                      uint32_t batch_count) {
+    // multi_batch.zig:101-118
+    uint32_t unpadded = batch_count * 2 + 2;
+    if (element_size == 0) return unpadded;
+    return div_ceil(unpadded, element_size) * element_size;
+}
+
+extern "C" int64_t tb_multi_batch_decode(const void* body_, uint32_t size, uint32_t element_size,
+                                         uint16_t* counts, uint32_t counts_max,
+                                         uint32_t* payload_size) {
+    // MultiBatchDecoder.init, multi_batch.zig:135-230. Parses suffixes from the end.
+    const uint8_t* body = static_cast<const uint8_t*>(body_);
+    if (size < 2 || (reinterpret_cast<uintptr_t>(body + size - 2) & 1u)) return -1;
+    uint16_t batch_count;
+    std::memcpy(&batch_count, body + size - 2, 2);
+    if (batch_count == 0 || batch_count > kBatchCountMax) return -1;
+    uint32_t trailer_size = tb_multi_batch_trailer_total_size(element_size, batch_count);
+    uint32_t items_size = uint32_t(batch_count) * 2;
+    if (size < 2 + items_size) return -1;
+    if (trailer_size > size) return -1;
+    // Padding between the used items and the start of the trailer must be all 0xFF.
+    uint32_t padding_size = trailer_size - 2 - items_size;
+    const uint8_t* trailer = body + size - trailer_size;
+    for (uint32_t i = 0; i < padding_size; i++)
+        if (trailer[i] != 0xFF) return -1;
+    const uint8_t* items = body + size - 2 - items_size;
+    uint64_t total = 0;
+    if (counts_max < batch_count) return -1;
+    for (uint32_t b = 0; b < batch_count; b++) {
+        // The last item corresponds to the first batch.
+        uint16_t c;
+        std::memcpy(&c, items + (uint32_t(batch_count) - 1 - b) * 2, 2);
+        if (c == kTrailerPadding) return -1;
+        counts[b] = c;
+        total += c;
+    }
+    if (element_size == 0 && total != 0) return -1;
+    uint64_t payload = total * element_size;
+    if (payload > 0xFFFFFFFFull) return -1;
+    uint32_t trailer_pad = uint32_t(payload % 2);  // only for 1-byte elements
+    if (trailer_pad) {
+        if (size < trailer_size + trailer_pad) return -1;
+        if (body[size - trailer_size - 1] != 0xFF) return -1;
+    }
+    if (payload != uint64_t(size) - trailer_size - trailer_pad) return -1;
+    *payload_size = uint32_t(payload);
+    return batch_count;
+}
+
+extern "C" int64_t tb_multi_batch_encode_trailer(void* buffer_, uint32_t payload_size,
+                                                 uint32_t element_size, const uint16_t* counts,
+                                                 uint32_t n_batches) {
+    // MultiBatchEncoder.finish, multi_batch.zig:428-490.
+    if (n_batches == 0 || n_batches > kBatchCountMax) return -1;
+    uint8_t* buffer = static_cast<uint8_t*>(buffer_);
+    uint32_t padding = payload_size % 2;
+    if (padding) buffer[payload_size] = 0xFF;
+    uint32_t trailer_size = tb_multi_batch_trailer_total_size(element_size, n_batches);
+    uint8_t* trailer = buffer + payload_size + padding;
+    uint32_t items = (trailer_size - 2) / 2;
+    for (uint32_t i = 0; i < items - n_batches; i++)
+        std::memcpy(trailer + i * 2, &kTrailerPadding, 2);
+    for (uint32_t b = 0; b < n_batches; b++) {
+        uint16_t c = counts[b];
+        std::memcpy(trailer + (items - 1 - b) * 2, &c, 2);
+    }
+    uint16_t bc = uint16_t(n_batches);
+    std::memcpy(trailer + trailer_size - 2, &bc, 2);
+    return int64_t(payload_size) + padding + trailer_size;
+}
+
+struct tb_sm {
+    tb_sm_options options;
+    tb_executor executor;
+    tbg_ctx* gpu = nullptr;  // owned when opened with tb_sm_open_gpu
+
+    uint64_t prepare_timestamp = 0;
+    uint64_t commit_timestamp = 0;
+    uint64_t prefetch_timestamp = 0;
+
+    std::vector<uint16_t> counts;
+    std::vector<uint32_t> lens;
+    std::vector<uint64_t> batch_ts;
+    std::vector<tb_create_result_t> results;
+
+    // Operation.event_max (src/tigerbeetle.zig:853-901).
+    uint32_t event_max(const OperationInfo& info, uint32_t batch_size_limit) const {
+        if (!info.multi_batch) {
+            return info.event_size == 0 ? options.message_body_size_max / info.result_size
+                                        : std::min(batch_size_limit / info.event_size,
+                                                   options.message_body_size_max / info.result_size);
+        }
+        uint32_t reply_trailer_min = tb_multi_batch_trailer_total_size(info.result_size, 1);
+        uint32_t request_trailer_min = tb_multi_batch_trailer_total_size(info.event_size, 1);
+        return std::min((batch_size_limit - request_trailer_min) / info.event_size,
+                        (options.message_body_size_max - reply_trailer_min) / info.result_size);
+    }
+
+    bool batch_valid(uint8_t operation, const OperationInfo& info, uint32_t batch_size) const {
+        if (operation == TB_OPERATION_PULSE) return batch_size == 0;
+        if (batch_size % info.event_size != 0) return false;
+        return batch_size / info.event_size <= event_max(info, options.batch_size_limit);
+    }
+};
+
+namespace {
+
+int gpu_create_accounts(void* self, const tb_account_t* e, uint32_t n, const uint32_t* lens,
+                        const uint64_t* ts, uint32_t nb, tb_create_result_t* r) {
+    return tbg_create_accounts(static_cast<tbg_ctx*>(self), e, n, lens, ts, nb, r);
+}
+int gpu_create_transfers(void* self, const tb_transfer_t* e, uint32_t n, const uint32_t* lens,
+                         const uint64_t* ts, uint32_t nb, tb_create_result_t* r) {
+    return tbg_create_transfers(static_cast<tbg_ctx*>(self), e, n, lens, ts, nb, r);
+}
+int64_t gpu_pulse(void* self, uint64_t ts) { return tbg_pulse(static_cast<tbg_ctx*>(self), ts); }
+uint64_t gpu_pulse_next(void* self) {
+    return tbg_pulse_next_timestamp(static_cast<tbg_ctx*>(self));
+}
+int64_t gpu_lookup_accounts(void* self, const tb_uint128_t* ids, uint32_t n, tb_account_t* out) {
+    return tbg_lookup_accounts(static_cast<tbg_ctx*>(self), ids, n, out);
+}
+int64_t gpu_lookup_transfers(void* self, const tb_uint128_t* ids, uint32_t n,
+                             tb_transfer_t* out) {
+    return tbg_lookup_transfers(static_cast<tbg_ctx*>(self), ids, n, out);
+}
+
+}  // namespace
+
+extern "C" tb_sm* tb_sm_open(const tb_sm_options* options, const tb_executor* executor) {
+    if (!options || !executor) return nullptr;
+    if (options->batch_size_limit == 0 || options->batch_size_limit > options->message_body_size_max)
+        return nullptr;
+    tb_sm* sm = new (std::nothrow) tb_sm();
+    if (!sm) return nullptr;
+    sm->options = *options;
+    sm->executor = *executor;
+    return sm;
+}
+
+extern "C" tb_sm* tb_sm_open_gpu(const tb_sm_options* options, const tbg_options* executor_options) {
+    tbg_ctx* ctx = tbg_open(executor_options);
+    if (!ctx) return nullptr;
+    tb_executor ex;
+    ex.self = ctx;
+    ex.create_accounts = gpu_create_accounts;
+    ex.create_transfers = gpu_create_transfers;
+    ex.pulse = gpu_pulse;
+    ex.pulse_next_timestamp = gpu_pulse_next;
+    ex.lookup_accounts = gpu_lookup_accounts;
+    ex.lookup_transfers = gpu_lookup_transfers;
+    tb_sm* sm = tb_sm_open(options, &ex);
+    if (!sm) {
+        tbg_close(ctx);
+        return nullptr;
+    }
+    sm->gpu = ctx;
+    return sm;
+}
+
+extern "C" void tb_sm_close(tb_sm* sm) {
+    if (!sm) return;
+    if (sm->gpu) tbg_close(sm->gpu);
+    delete sm;
+}
+
+extern "C" tbg_ctx* tb_sm_executor_gpu(tb_sm* sm) { return sm ? sm->gpu : nullptr; }
+
+extern "C" int tb_sm_input_valid(const tb_sm* sm, uint8_t operation, const void* body,
+                                 uint32_t size) {
+    OperationInfo info;
+    if (!operation_info(operation, &info)) return 0;
+    if (size > sm->options.batch_size_limit) return 0;
+    if (!info.multi_batch) return sm->batch_valid(operation, info, size) ? 1 : 0;
+
+    std::vector<uint16_t> counts(kBatchCountMax);
+    uint32_t payload = 0;
+    int64_t nb = tb_multi_batch_decode(body, size, info.event_size, counts.data(),
+                                       uint32_t(counts.size()), &payload);
+    if (nb <= 0) return 0;
+    uint64_t result_count_expected = 0;
+    uint32_t result_max = sm->event_max(info, sm->options.message_body_size_max);
+    for (int64_t b = 0; b < nb; b++) {
+        if (!sm->batch_valid(operation, info, uint32_t(counts[b]) * info.event_size)) return 0;
+        result_count_expected += std::min<uint32_t>(counts[b], result_max);
+    }
+    uint64_t reply_trailer = tb_multi_batch_trailer_total_size(info.result_size, uint32_t(nb));
+    if (sm->options.message_body_size_max < result_count_expected * info.result_size + reply_trailer)
+        return 0;
+    return 1;
+}
+
+extern "C" void tb_sm_prepare(tb_sm* sm, uint8_t operation, const void* body, uint32_t size) {
+    OperationInfo info;
+    if (!operation_info(operation, &info)) return;
+    uint64_t delta = 0;
+    if (operation == TB_OPERATION_PULSE) {
+        delta = sm->options.pulse_batch_max;
+    } else if (operation == TB_OPERATION_CREATE_ACCOUNTS ||
+               operation == TB_OPERATION_CREATE_TRANSFERS) {
+        uint32_t payload = 0;
+        sm->counts.resize(kBatchCountMax);
+        int64_t nb = tb_multi_batch_decode(body, size, info.event_size, sm->counts.data(),
+                                           uint32_t(sm->counts.size()), &payload);
+        if (nb > 0) delta = payload / info.event_size;
+    }
+    sm->prepare_timestamp += delta;
+}
+
+extern "C" int tb_sm_pulse_needed(const tb_sm* sm, uint64_t timestamp) {
+    return sm->executor.pulse_next_timestamp(sm->executor.self) <= timestamp;
+}
+
+extern "C" void tb_sm_prefetch(tb_sm* sm, tb_sm_prefetch_callback callback, void* context,
+                               uint64_t op, uint64_t snapshot, uint8_t operation,
+                               const void* body, uint32_t size) {
+    (void)sm;
+    (void)op;
+    (void)snapshot;
+    (void)operation;
+    (void)body;
+    (void)size;
+    // Every table is resident in HBM: there is nothing to stage.
+    if (callback) callback(context);
+}
+
+extern "C" int64_t tb_sm_commit(tb_sm* sm, uint64_t client_lo, uint64_t client_hi, uint64_t op,
+                                uint64_t timestamp, uint8_t operation, const void* body,
+                                uint32_t size, void* output) {
+    (void)client_lo;
+    (void)client_hi;
+    (void)op;
+    OperationInfo info;
+    if (!operation_info(operation, &info)) return TBG_EINVAL;
+    if (operation == TB_OPERATION_PULSE) {
+        // execute_expire_pending_transfers (:4511-4628): scans with expires_at_max =
+        // prefetch_timestamp (:2463); no output.
+        int64_t expired = sm->executor.pulse(sm->executor.self, timestamp);
+        if (expired < 0) return expired;
+        if (expired > 0) sm->commit_timestamp = timestamp;
+        return 0;
+    }
+
+    uint32_t payload = 0;
+    sm->counts.resize(kBatchCountMax);
+    int64_t nb = tb_multi_batch_decode(body, size, info.event_size, sm->counts.data(),
+                                       uint32_t(sm->counts.size()), &payload);
+    if (nb <= 0) return TBG_EINVAL;
+    const uint32_t n = payload / info.event_size;
+    uint8_t* out = static_cast<uint8_t*>(output);
+
+    if (operation == TB_OPERATION_CREATE_ACCOUNTS || operation == TB_OPERATION_CREATE_TRANSFERS) {
+        // execute_multi_batch: execute_timestamp starts at timestamp - delta(payload) and each
+        // batch advances it by its own delta before executing (:2717-2737).
+        sm->lens.resize(size_t(nb));
+        sm->batch_ts.resize(size_t(nb));
+        uint64_t execute_timestamp = timestamp - n;
+        for (int64_t b = 0; b < nb; b++) {
+            sm->lens[b] = sm->counts[b];
+            execute_timestamp += sm->counts[b];
+            sm->batch_ts[b] = execute_timestamp;
+        }
+        tb_create_result_t* results = reinterpret_cast<tb_create_result_t*>(out);
+        int rc = operation == TB_OPERATION_CREATE_ACCOUNTS
+                     ? sm->executor.create_accounts(sm->executor.self,
+                                                    static_cast<const tb_account_t*>(body), n,
+                                                    sm->lens.data(), sm->batch_ts.data(),
+                                                    uint32_t(nb), results)
+                     : sm->executor.create_transfers(sm->executor.self,
+                                                     static_cast<const tb_transfer_t*>(body), n,
+                                                     sm->lens.data(), sm->batch_ts.data(),
+                                                     uint32_t(nb), results);
+        if (rc < 0) return rc;
+        return tb_multi_batch_encode_trailer(out, n * 16u, 16, sm->counts.data(), uint32_t(nb));
+    }
+
+    // lookup_accounts / lookup_transfers: per batch, found objects only (:3255-3292).
+    const tb_uint128_t* ids = static_cast<const tb_uint128_t*>(body);
+    uint32_t written = 0, offset = 0;
+    std::vector<uint16_t> reply_counts(static_cast<size_t>(nb));
+    for (int64_t b = 0; b < nb; b++) {
+        int64_t found = operation == TB_OPERATION_LOOKUP_ACCOUNTS
+                            ? sm->executor.lookup_accounts(
+                                  sm->executor.self, ids + offset, sm->counts[b],
+                                  reinterpret_cast<tb_account_t*>(out + written))
+                            : sm->executor.lookup_transfers(
+                                  sm->executor.self, ids + offset, sm->counts[b],
+                                  reinterpret_cast<tb_transfer_t*>(out + written));
+        if (found < 0) return found;
+        reply_counts[b] = uint16_t(found);
+        written += uint32_t(found) * 128u;
+        offset += sm->counts[b];
+    }
+    return tb_multi_batch_encode_trailer(out, written, 128, reply_counts.data(), uint32_t(nb));
+}
+
+extern "C" uint64_t tb_sm_get_prepare_timestamp(const tb_sm* sm) { return sm->prepare_timestamp; }
+extern "C" uint64_t tb_sm_get_commit_timestamp(const tb_sm* sm) { return sm->commit_timestamp; }
+extern "C" uint64_t tb_sm_get_prefetch_timestamp(const tb_sm* sm) {
+    return sm->prefetch_timestamp;
+}
+extern "C" void tb_sm_set_prepare_timestamp(tb_sm* sm, uint64_t v) { sm->prepare_timestamp = v; }
+extern "C" void tb_sm_set_commit_timestamp(tb_sm* sm, uint64_t v) { sm->commit_timestamp = v; }
+extern "C" void tb_sm_set_prefetch_timestamp(tb_sm* sm, uint64_t v) {
+    sm->prefetch_timestamp = v;
+}

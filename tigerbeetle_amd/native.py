@@ -1,0 +1,137 @@
+"""ctypes bindings of the product library libtbg.so (include/tbg.h, include/tb_state_machine.h).
+
+The library is built in-tree by ``__graft_entry__.build()`` (or ``make -C tigerbeetle_amd/csrc``)
+into ``tigerbeetle_amd/lib/libtbg.so``. There is no fallback: if the library is missing, importing
+the product path raises.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libtbg.so")
+
+c_u8p = ctypes.POINTER(ctypes.c_uint8)
+c_u16p = ctypes.POINTER(ctypes.c_uint16)
+c_u32p = ctypes.POINTER(ctypes.c_uint32)
+c_u64p = ctypes.POINTER(ctypes.c_uint64)
+vp = ctypes.c_void_p
+
+
+class U128(ctypes.Structure):
+    _fields_ = [("lo", ctypes.c_uint64), ("hi", ctypes.c_uint64)]
+
+    @classmethod
+    def of(cls, x: int):
+        return cls(x & 0xFFFFFFFFFFFFFFFF, (x >> 64) & 0xFFFFFFFFFFFFFFFF)
+
+
+class TbgOptions(ctypes.Structure):
+    _fields_ = [
+        ("account_capacity", ctypes.c_uint64),
+        ("transfer_capacity", ctypes.c_uint64),
+        ("batch_events_max", ctypes.c_uint32),
+        ("batch_count_max", ctypes.c_uint32),
+        ("pulse_batch_max", ctypes.c_uint32),
+        ("device", ctypes.c_uint32),
+        ("pulse_next_timestamp_init", ctypes.c_uint64),
+    ]
+
+
+class TbgStats(ctypes.Structure):
+    _fields_ = [
+        ("events", ctypes.c_uint64),
+        ("fast", ctypes.c_uint64),
+        ("replayed", ctypes.c_uint64),
+        ("static_fail", ctypes.c_uint64),
+    ]
+
+
+class SmOptions(ctypes.Structure):
+    _fields_ = [
+        ("batch_size_limit", ctypes.c_uint32),
+        ("message_body_size_max", ctypes.c_uint32),
+        ("pulse_batch_max", ctypes.c_uint32),
+    ]
+
+
+# tb_executor (tb_state_machine.h): a vtable of C function pointers.
+class Executor(ctypes.Structure):
+    _fields_ = [
+        ("self", vp),
+        ("create_accounts", vp),
+        ("create_transfers", vp),
+        ("pulse", vp),
+        ("pulse_next_timestamp", vp),
+        ("lookup_accounts", vp),
+        ("lookup_transfers", vp),
+    ]
+
+
+PREFETCH_CALLBACK = ctypes.CFUNCTYPE(None, vp)
+
+# Exported symbols: (name, restype, argtypes). tests/test_abi.py checks each one against the
+# declarations in include/*.h.
+SIGNATURES = [
+    ("tbg_open", vp, [ctypes.POINTER(TbgOptions)]),
+    ("tbg_close", None, [vp]),
+    ("tbg_last_error", ctypes.c_char_p, [vp]),
+    ("tbg_create_accounts", ctypes.c_int, [vp, vp, ctypes.c_uint32, c_u32p, c_u64p,
+                                          ctypes.c_uint32, vp]),
+    ("tbg_create_transfers", ctypes.c_int, [vp, vp, ctypes.c_uint32, c_u32p, c_u64p,
+                                           ctypes.c_uint32, vp]),
+    ("tbg_create_accounts_device", ctypes.c_int, [vp, vp, ctypes.c_uint32, vp, vp,
+                                                 ctypes.c_uint32, vp, vp]),
+    ("tbg_create_transfers_device", ctypes.c_int, [vp, vp, ctypes.c_uint32, vp, vp,
+                                                  ctypes.c_uint32, vp, vp]),
+    ("tbg_pulse", ctypes.c_int64, [vp, ctypes.c_uint64]),
+    ("tbg_pulse_next_timestamp", ctypes.c_uint64, [vp]),
+    ("tbg_lookup_accounts", ctypes.c_int64, [vp, vp, ctypes.c_uint32, vp]),
+    ("tbg_lookup_transfers", ctypes.c_int64, [vp, vp, ctypes.c_uint32, vp]),
+    ("tbg_dump_accounts", ctypes.c_int64, [vp, vp]),
+    ("tbg_dump_transfers", ctypes.c_int64, [vp, vp, vp]),
+    ("tbg_debug_set_account_balances", ctypes.c_int, [vp, U128, U128, U128, U128, U128]),
+    ("tbg_last_stats", ctypes.c_int, [vp, ctypes.POINTER(TbgStats)]),
+    ("tbg_debug_force_replay", ctypes.c_int, [vp, ctypes.c_int]),
+    ("tb_sm_open", vp, [ctypes.POINTER(SmOptions), ctypes.POINTER(Executor)]),
+    ("tb_sm_open_gpu", vp, [ctypes.POINTER(SmOptions), ctypes.POINTER(TbgOptions)]),
+    ("tb_sm_close", None, [vp]),
+    ("tb_sm_executor_gpu", vp, [vp]),
+    ("tb_sm_input_valid", ctypes.c_int, [vp, ctypes.c_uint8, vp, ctypes.c_uint32]),
+    ("tb_sm_prepare", None, [vp, ctypes.c_uint8, vp, ctypes.c_uint32]),
+    ("tb_sm_pulse_needed", ctypes.c_int, [vp, ctypes.c_uint64]),
+    ("tb_sm_prefetch", None, [vp, PREFETCH_CALLBACK, vp, ctypes.c_uint64, ctypes.c_uint64,
+                              ctypes.c_uint8, vp, ctypes.c_uint32]),
+    ("tb_sm_commit", ctypes.c_int64, [vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                      ctypes.c_uint64, ctypes.c_uint8, vp, ctypes.c_uint32, vp]),
+    ("tb_sm_get_prepare_timestamp", ctypes.c_uint64, [vp]),
+    ("tb_sm_get_commit_timestamp", ctypes.c_uint64, [vp]),
+    ("tb_sm_get_prefetch_timestamp", ctypes.c_uint64, [vp]),
+    ("tb_sm_set_prepare_timestamp", None, [vp, ctypes.c_uint64]),
+    ("tb_sm_set_commit_timestamp", None, [vp, ctypes.c_uint64]),
+    ("tb_sm_set_prefetch_timestamp", None, [vp, ctypes.c_uint64]),
+    ("tb_multi_batch_encode_trailer", ctypes.c_int64, [vp, ctypes.c_uint32, ctypes.c_uint32,
+                                                      c_u16p, ctypes.c_uint32]),
+    ("tb_multi_batch_decode", ctypes.c_int64, [vp, ctypes.c_uint32, ctypes.c_uint32, c_u16p,
+                                              ctypes.c_uint32, c_u32p]),
+    ("tb_multi_batch_trailer_total_size", ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint32]),
+]
+
+_lib = None
+
+
+def load(path: str = None):
+    """Load libtbg.so (once). Raises OSError if it is missing: there is no fallback path."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise OSError(f"libtbg.so not built: {p} (run __graft_entry__.build())")
+    lib = ctypes.CDLL(p)
+    for name, res, args in SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib
