@@ -1,0 +1,333 @@
+#!/usr/bin/env python3
+"""bench.py -- validated create_transfers/s on MI355X (BASELINE.json metric), config 2 workload.
+
+Workload (BASELINE.json configs[1]): 10,000 accounts (ledger 2, code 1, history)
+and 10,000,000 uniform create_transfers in 8189-event batches (1,221 x 8189 + 1,231), sequential
+ids, `amount = Exp(10_000) +| 1`, seed 42. A *step* is one pass of the hot path over that whole
+synthetic input: one tbg_create_transfers_device call carrying all 1,222 batches (each batch with
+its own commit timestamp, TestContext rule prepare_ts += 1 + n). Inputs are resident in HBM when
+the timed region starts; every step uses fresh transfer ids, so every step does the full work.
+
+Multi-GPU (weak scaling): one process per GPU; each rank owns its own ledger shard
+(own accounts and transfers, ledger 2 + rank) with no data-path collective. The timed region is
+bracketed by a barrier + device synchronise on every rank; the reported time is the max over ranks.
+
+Validation (after the timed region): every result must be `created`, and every account's final
+balances must equal the exact per-account sums of the steps' amounts (the workload is
+order-independent, so this is the serial reference outcome).
+
+Output: one JSON line on rank 0 with `roofline` (dominant kernel, HIP-event timed) and
+`cpu_baseline` (the serial C oracle on one host core, bounded sample of the same workload).
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from tigerbeetle_amd import native, workload  # noqa: E402
+from tigerbeetle_amd.types import ACCOUNT_DTYPE, RESULT_DTYPE, TRANSFER_DTYPE  # noqa: E402
+
+METRIC = "validated create_transfers/sec (1/2/4/8 GPU) + % of HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+BATCH = 8189           # Operation.create_transfers.event_max (src/tigerbeetle.zig:853-901)
+
+# Algorithmic bytes per event of each kernel of the create_transfers path: the
+# fields the kernel must read or write for its function, counted once.
+KERNEL_BYTES_PER_EVENT = {
+    "tr_prepare": 50 + 16 + 28,      # id/dr/cr/flags, id-slot claim, per-event scratch
+    "tr_mark": 2 + 16 + 8,
+    "tr_classify": 128 + 8 + 28 + 2,
+    "tr_fast": 128 + 20 + 128 + 1 + 16,
+    "tr_finalize": 8 + 8 + 16 + 1,
+}
+
+
+def parse_args():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--transfers", type=int, default=10_000_000)
+    ap.add_argument("--accounts", type=int, default=10_000)
+    ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="bounded CPU-oracle sample (rank 0, N=1)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-validate", action="store_true")
+    return ap.parse_args()
+
+
+def dist_init(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as td
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        td.init_process_group(backend=backend)
+        dist = td
+    return world, rank, local, dist
+
+
+def barrier(dist):
+    if dist is not None:
+        dist.barrier()
+
+
+def max_over_ranks(dist, x: float) -> float:
+    if dist is None:
+        return x
+    import torch
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+class Device:
+    """Device buffers via the HIP runtime (the product library already links it)."""
+
+    def __init__(self):
+        self.hip = ctypes.CDLL("libamdhip64.so")
+        self.hip.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
+        self.hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                       ctypes.c_int]
+        self.hip.hipFree.argtypes = [ctypes.c_void_p]
+        self.hip.hipDeviceSynchronize.argtypes = []
+        self.hip.hipSetDevice.argtypes = [ctypes.c_int]
+        self.ptrs = []
+
+    def set_device(self, d):
+        assert self.hip.hipSetDevice(d) == 0
+
+    def upload(self, a: np.ndarray) -> ctypes.c_void_p:
+        p = ctypes.c_void_p()
+        assert self.hip.hipMalloc(ctypes.byref(p), max(a.nbytes, 16)) == 0, "hipMalloc"
+        assert self.hip.hipMemcpy(p, a.ctypes.data_as(ctypes.c_void_p), a.nbytes, 1) == 0
+        self.ptrs.append(p)
+        return p
+
+    def alloc(self, nbytes) -> ctypes.c_void_p:
+        p = ctypes.c_void_p()
+        assert self.hip.hipMalloc(ctypes.byref(p), max(nbytes, 16)) == 0, "hipMalloc"
+        self.ptrs.append(p)
+        return p
+
+    def download(self, p, a: np.ndarray):
+        assert self.hip.hipMemcpy(a.ctypes.data_as(ctypes.c_void_p), p, a.nbytes, 2) == 0
+
+    def sync(self):
+        assert self.hip.hipDeviceSynchronize() == 0
+
+    def free_all(self):
+        for p in self.ptrs:
+            self.hip.hipFree(p)
+        self.ptrs = []
+
+
+def batch_plan(n):
+    lens = [BATCH] * (n // BATCH) + ([n % BATCH] if n % BATCH else [])
+    return np.asarray(lens, dtype=np.int64)
+
+
+def step_timestamps(prepare_ts, lens):
+    """TestContext rule per commit: prepare_ts += 1 + n; the batch's timestamp is prepare_ts."""
+    ts = prepare_ts + np.cumsum(lens + 1)
+    return ts.astype(np.uint64), int(ts[-1])
+
+
+def cpu_baseline(args, acc, base, lens):
+    """The serial C oracle (oracle/liboracle.so) on one core, bounded sample of the workload."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_binding
+    olib = oracle_binding.load()
+    o = olib.tbo_open(8190, 1)
+    res = np.zeros(len(acc), dtype=RESULT_DTYPE)
+    olib.tbo_create_accounts(o, acc.ctypes.data_as(ctypes.c_void_p), len(acc), 1 + len(acc),
+                             res.ctypes.data_as(ctypes.c_void_p))
+    ts = 2 + len(acc)
+    out = np.zeros(BATCH, dtype=RESULT_DTYPE)
+    done, off, b = 0, 0, 0
+    t0 = time.perf_counter()
+    while b < len(lens):
+        n = int(lens[b])
+        ts += 1 + n
+        olib.tbo_create_transfers(o, base[off:off + n].ctypes.data_as(ctypes.c_void_p), n, ts,
+                                  out.ctypes.data_as(ctypes.c_void_p))
+        assert (out["status"][:n] == 0xFFFFFFFF).all()
+        done += n
+        off += n
+        b += 1
+        if time.perf_counter() - t0 >= args.cpu_seconds:
+            break
+    elapsed = time.perf_counter() - t0
+    olib.tbo_close(o)
+    return {"value": done / elapsed, "unit": "transfers/s", "cores": 1, "kind": "port",
+            "sample": f"{done} of the {len(base)} config-2 transfers ({b} batches of <= {BATCH}) "
+                      f"through oracle/tb_oracle.c, single-threaded, {elapsed:.1f} s"}
+
+
+def main():
+    args = parse_args()
+    world, rank, local, dist = dist_init(args)
+    N, A, K, W = args.transfers, args.accounts, args.steps, args.warmup
+    lib = native.load()
+    dev = Device()
+    dev.set_device(local)
+
+    ledger = 2 + rank
+    acc = workload.accounts(A, seed=args.seed, ledger=ledger)
+    base = workload.transfers_uniform(N, A, seed=args.seed, ledger=ledger)
+    lens = batch_plan(N)
+    ends = np.cumsum(lens).astype(np.uint32)
+
+    opt = native.TbgOptions()
+    opt.account_capacity = A
+    opt.transfer_capacity = N * (K + W)
+    opt.batch_events_max = N
+    opt.batch_count_max = len(lens)
+    opt.pulse_batch_max = 8190
+    opt.device = local
+    opt.pulse_next_timestamp_init = 1
+    g = lib.tbg_open(ctypes.byref(opt))
+    assert g, "tbg_open failed"
+
+    res_acc = np.zeros(A, dtype=RESULT_DTYPE)
+    a_lens = np.asarray([A], dtype=np.uint32)
+    a_ts = np.asarray([1 + A], dtype=np.uint64)
+    rc = lib.tbg_create_accounts(g, acc.ctypes.data_as(ctypes.c_void_p), A,
+                                 a_lens.ctypes.data_as(native.c_u32p),
+                                 a_ts.ctypes.data_as(native.c_u64p), 1,
+                                 res_acc.ctypes.data_as(ctypes.c_void_p))
+    assert rc == 0 and (res_acc["status"] == 0xFFFFFFFF).all()
+    prepare_ts = 1 + A
+
+    # Per-step inputs, resident in HBM before timing: fresh ids per step.
+    d_ends = dev.upload(ends)
+    steps = []
+    for s in range(W + K):
+        ev = base.copy()
+        ev["id"][:, 0] += np.uint64(s * N)
+        ts, prepare_ts = step_timestamps(prepare_ts, lens)
+        steps.append((dev.upload(ev), dev.upload(ts), dev.alloc(N * 16)))
+        del ev
+    dev.sync()
+
+    def run_step(s):
+        d_ev, d_ts, d_res = steps[s]
+        rc = lib.tbg_create_transfers_device(g, d_ev, N, d_ends, d_ts, len(lens), d_res, None)
+        if rc != 0:
+            raise RuntimeError(f"tbg_create_transfers_device: {rc} {lib.tbg_last_error(g)}")
+
+    for s in range(W):
+        run_step(s)
+    lib.tbg_profile(g, 1)
+    dev.sync()
+    barrier(dist)
+    dev.sync()
+    t0 = time.perf_counter()
+    for s in range(W, W + K):
+        run_step(s)
+    dev.sync()
+    barrier(dist)
+    t_local = time.perf_counter() - t0
+    t_max = max_over_ranks(dist, t_local)
+
+    # Kernel times (HIP events on the executor's stream over the timed steps).
+    kernels = {}
+    i = 0
+    name = ctypes.create_string_buffer(64)
+    ms, cnt = ctypes.c_double(), ctypes.c_uint64()
+    while lib.tbg_profile_read(g, i, name, 64, ctypes.byref(ms), ctypes.byref(cnt)):
+        kernels[name.value.decode()] = (ms.value, cnt.value)
+        i += 1
+    lib.tbg_profile(g, 0)
+
+    stats = native.TbgStats()
+    lib.tbg_last_stats(g, ctypes.byref(stats))
+
+    validated = None
+    if not args.no_validate:
+        ok = True
+        r = np.zeros(N, dtype=RESULT_DTYPE)
+        for s in range(W + K):
+            dev.download(steps[s][2], r)
+            ok &= bool((r["status"] == 0xFFFFFFFF).all())
+        dump = np.zeros(A, dtype=ACCOUNT_DTYPE)
+        assert lib.tbg_dump_accounts(g, dump.ctypes.data_as(ctypes.c_void_p)) == A
+        dr = base["debit_account_id"][:, 0].astype(np.int64) - 1
+        cr = base["credit_account_id"][:, 0].astype(np.int64) - 1
+        amt = base["amount"][:, 0].astype(np.int64)
+        exp_d = np.bincount(dr, weights=amt, minlength=A).astype(np.int64) * (W + K)
+        exp_c = np.bincount(cr, weights=amt, minlength=A).astype(np.int64) * (W + K)
+        ok &= bool((dump["debits_posted"][:, 0].astype(np.int64) == exp_d).all())
+        ok &= bool((dump["credits_posted"][:, 0].astype(np.int64) == exp_c).all())
+        ok &= bool((dump["debits_posted"][:, 1] == 0).all() and (dump["credits_pending"] == 0).all())
+        validated = ok
+        if not ok:
+            print(json.dumps({"error": "validation failed"}), file=sys.stderr)
+
+    # Algorithmic bytes of the path: 288 B per event + 256 B per distinct account.
+    distinct = len(np.union1d(base["debit_account_id"][:, 0], base["credit_account_id"][:, 0]))
+    path_bytes = 288 * N + 256 * distinct
+    dev_ms_total = sum(v[0] for k, v in kernels.items() if k not in ("begin", "host_sync"))
+    dom = max(((k, v) for k, v in kernels.items() if k in KERNEL_BYTES_PER_EVENT),
+              key=lambda kv: kv[1][0], default=None)
+    roofline = None
+    if dom is not None:
+        kname, (kms, kcount) = dom
+        avg_s = kms / kcount / 1e3
+        kbytes = KERNEL_BYTES_PER_EVENT[kname] * N
+        achieved = kbytes / avg_s / 1e9
+        roofline = {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1),
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                    "traffic": None, "alg_bytes_per_launch": kbytes,
+                    "avg_launch_ms": round(kms / kcount, 4),
+                    "path": {"alg_bytes_per_step": path_bytes,
+                             "device_ms_per_step": round(dev_ms_total / K, 4),
+                             "achieved": round(path_bytes / (dev_ms_total / K / 1e3) / 1e9, 1),
+                             "frac": round(path_bytes / (dev_ms_total / K / 1e3) / 1e9 /
+                                           HBM_PEAK_GBS, 4)},
+                    "kernels_ms_per_step": {k: round(v[0] / K, 4) for k, v in kernels.items()}}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, acc, base, lens)
+
+    value = N * K * world / t_max
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "transfers/s",
+            "n_gpus": world, "steps": K, "warmup": W,
+            "ms_per_step": round(t_max / K * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u128",
+            "data": "synthetic (seeded; benchmark_load.zig distributions, sequential ids)",
+            "config": {"workload": "config2: 10k accounts, 10M uniform create_transfers in "
+                                   "8189-event batches, 1 ledger shard per GPU",
+                       "transfers_per_step_per_gpu": N, "accounts_per_gpu": A,
+                       "batches_per_step": int(len(lens)), "parallelism": f"ledger-shard x{world}"},
+            "validated": validated,
+            "replayed_events_last_step": int(stats.replayed),
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line))
+    lib.tbg_close(g)
+    dev.free_all()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -210,8 +210,14 @@ enum {
 #define TB_TIMESTAMP_MAX 0x7FFFFFFFFFFFFFFFull
 #define TB_NS_PER_S 1000000000ull
 
+#if defined(__HIPCC__)
+#define TB_INLINE __host__ __device__ static inline
+#else
+#define TB_INLINE static inline
+#endif
+
 /* CreateTransferStatus.transient(), src/tigerbeetle.zig:322-399. */
-static inline int tb_transfer_status_transient(uint32_t s) {
+TB_INLINE int tb_transfer_status_transient(uint32_t s) {
     return s == TB_CT_DEBIT_ACCOUNT_NOT_FOUND || s == TB_CT_CREDIT_ACCOUNT_NOT_FOUND ||
            s == TB_CT_PENDING_TRANSFER_NOT_FOUND || s == TB_CT_EXCEEDS_CREDITS ||
            s == TB_CT_EXCEEDS_DEBITS || s == TB_CT_DEBIT_ACCOUNT_ALREADY_CLOSED ||

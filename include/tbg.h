@@ -108,6 +108,13 @@ int tbg_last_stats(tbg_ctx* ctx, tbg_stats* out);
 /* Forces every event through the ordered replay (self-check of the fast path). */
 int tbg_debug_force_replay(tbg_ctx* ctx, int enable);
 
+/* Per-kernel timing with HIP events on the call's stream (off by default; resets the totals).
+ * tbg_profile_read returns 1 and fills name / accumulated milliseconds / launches for entry
+ * `index`, or 0 past the last entry. */
+int tbg_profile(tbg_ctx* ctx, int enable);
+int tbg_profile_read(tbg_ctx* ctx, uint32_t index, char* name, uint32_t name_len,
+                     double* total_ms, uint64_t* launches);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,196 @@
+"""Executor-level parity harness: the HIP executor (libtbg.so) against the CPU oracle.
+
+Both sides receive the same calls -- create_accounts / create_transfers over multi-batch commits,
+pulses when `pulse_needed` -- with timestamps advanced by the TestContext rule
+(state_machine_tests.zig:230-241: prepare_ts += 1 + events). Results must be byte-identical and,
+at the end, so must every live Account row, every live Transfer row and every TransferPending
+status (in creation order).
+"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from tigerbeetle_amd import native  # noqa: E402
+from tigerbeetle_amd.types import (  # noqa: E402
+    ACCOUNT_DTYPE, RESULT_DTYPE, TRANSFER_DTYPE, TIMESTAMP_MAX, CreateAccountStatus,
+    CreateTransferStatus)
+
+import oracle_binding  # noqa: E402
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class ParityError(AssertionError):
+    pass
+
+
+class Pair:
+    def __init__(self, account_capacity=1 << 16, transfer_capacity=1 << 20,
+                 batch_events_max=1 << 16, batch_count_max=4096, pulse_batch_max=8190,
+                 pulse_next_timestamp_init=TIMESTAMP_MAX, force_replay=False, device=0):
+        self.lib = native.load()
+        self.olib = oracle_binding.load()
+        o = native.TbgOptions()
+        o.account_capacity = account_capacity
+        o.transfer_capacity = transfer_capacity
+        o.batch_events_max = batch_events_max
+        o.batch_count_max = batch_count_max
+        o.pulse_batch_max = pulse_batch_max
+        o.device = device
+        o.pulse_next_timestamp_init = pulse_next_timestamp_init
+        self.g = self.lib.tbg_open(ctypes.byref(o))
+        if not self.g:
+            raise RuntimeError("tbg_open failed")
+        if force_replay:
+            self.lib.tbg_debug_force_replay(self.g, 1)
+        self.o = self.olib.tbo_open(pulse_batch_max, pulse_next_timestamp_init)
+        self.prepare_timestamp = 0
+        self._pulse_delta = pulse_batch_max
+        self.calls = 0
+        self.stats = {"events": 0, "fast": 0, "replayed": 0, "static_fail": 0}
+
+    def close(self):
+        if self.g:
+            self.lib.tbg_close(self.g)
+            self.g = None
+        if self.o:
+            self.olib.tbo_close(self.o)
+            self.o = None
+
+    def _batches(self, lens):
+        """One commit holding len(lens) batches (a multi-batch body)."""
+        n = int(sum(lens))
+        self.prepare_timestamp += 1 + n
+        ts = self.prepare_timestamp
+        ends = np.cumsum(np.asarray(lens, dtype=np.int64))
+        batch_ts = (ts - n + ends).astype(np.uint64)
+        return n, np.asarray(lens, dtype=np.uint32), batch_ts
+
+    def _check(self, kind, events, r_gpu, r_orc):
+        if r_gpu.tobytes() != r_orc.tobytes():
+            bad = np.nonzero((r_gpu["status"] != r_orc["status"]) |
+                             (r_gpu["timestamp"] != r_orc["timestamp"]))[0]
+            enum_t = CreateAccountStatus if kind == "accounts" else CreateTransferStatus
+            lines = [f"create_{kind} call #{self.calls}: {len(bad)} results differ"]
+            for i in bad[:12]:
+                def name(s):
+                    try:
+                        return enum_t(int(s)).name
+                    except ValueError:
+                        return str(int(s))
+                lines.append(f"  [{i}] gpu=({int(r_gpu[i]['timestamp'])}, "
+                             f"{name(r_gpu[i]['status'])}) oracle=({int(r_orc[i]['timestamp'])}, "
+                             f"{name(r_orc[i]['status'])}) flags={int(events[i]['flags']):#x}")
+            raise ParityError("\n".join(lines))
+
+    def _stats(self):
+        s = native.TbgStats()
+        self.lib.tbg_last_stats(self.g, ctypes.byref(s))
+        for k in self.stats:
+            self.stats[k] += getattr(s, k)
+
+    def create_accounts(self, events: np.ndarray, lens=None):
+        events = np.ascontiguousarray(events, dtype=ACCOUNT_DTYPE)
+        lens = [len(events)] if lens is None else lens
+        n, lens_a, batch_ts = self._batches(lens)
+        r_gpu = np.zeros(n, dtype=RESULT_DTYPE)
+        r_orc = np.zeros(n, dtype=RESULT_DTYPE)
+        rc = self.lib.tbg_create_accounts(
+            self.g, _ptr(events), n, lens_a.ctypes.data_as(native.c_u32p),
+            batch_ts.ctypes.data_as(native.c_u64p), len(lens), _ptr(r_gpu))
+        if rc != 0:
+            raise RuntimeError(f"tbg_create_accounts: {rc} {self.lib.tbg_last_error(self.g)}")
+        off = 0
+        for b, ln in enumerate(lens):
+            self.olib.tbo_create_accounts(self.o, _ptr(events[off:off + ln]), ln,
+                                          int(batch_ts[b]), _ptr(r_orc[off:off + ln]))
+            off += ln
+        self.calls += 1
+        self._stats()
+        self._check("accounts", events, r_gpu, r_orc)
+        self._maybe_pulse()
+        return r_orc
+
+    def create_transfers(self, events: np.ndarray, lens=None):
+        events = np.ascontiguousarray(events, dtype=TRANSFER_DTYPE)
+        lens = [len(events)] if lens is None else lens
+        n, lens_a, batch_ts = self._batches(lens)
+        r_gpu = np.zeros(n, dtype=RESULT_DTYPE)
+        r_orc = np.zeros(n, dtype=RESULT_DTYPE)
+        rc = self.lib.tbg_create_transfers(
+            self.g, _ptr(events), n, lens_a.ctypes.data_as(native.c_u32p),
+            batch_ts.ctypes.data_as(native.c_u64p), len(lens), _ptr(r_gpu))
+        if rc != 0:
+            raise RuntimeError(f"tbg_create_transfers: {rc} {self.lib.tbg_last_error(self.g)}")
+        off = 0
+        for b, ln in enumerate(lens):
+            self.olib.tbo_create_transfers(self.o, _ptr(events[off:off + ln]), ln,
+                                           int(batch_ts[b]), _ptr(r_orc[off:off + ln]))
+            off += ln
+        self.calls += 1
+        self._stats()
+        self._check("transfers", events, r_gpu, r_orc)
+        self._maybe_pulse()
+        return r_orc
+
+    def pulse_next(self):
+        a = self.lib.tbg_pulse_next_timestamp(self.g)
+        b = self.olib.tbo_pulse_next_timestamp(self.o)
+        if a != b:
+            raise ParityError(f"pulse_next_timestamp: gpu={a} oracle={b} (call #{self.calls})")
+        return a
+
+    def _maybe_pulse(self):
+        # Best-effort pulse after the commit (state_machine_tests.zig:201-207, :243-256).
+        if self.pulse_next() <= self.prepare_timestamp:
+            # prepare(pulse): prepare_ts += 1 + batch_max.create_transfers (:1113).
+            self.prepare_timestamp += 1 + self._pulse_delta
+            ts = self.prepare_timestamp
+            eg = self.lib.tbg_pulse(self.g, ts)
+            eo = self.olib.tbo_pulse(self.o, ts)
+            if eg != eo:
+                raise ParityError(f"pulse at {ts}: gpu expired {eg}, oracle {eo}")
+            self.pulse_next()
+
+    def tick(self, ns: int):
+        self.prepare_timestamp += ns
+        self._maybe_pulse()
+
+    def compare_state(self):
+        na = self.lib.tbg_dump_accounts(self.g, None)
+        a_gpu = np.zeros(max(na, 0), dtype=ACCOUNT_DTYPE)
+        self.lib.tbg_dump_accounts(self.g, _ptr(a_gpu))
+        a_orc = np.zeros(self.olib.tbo_account_count(self.o), dtype=ACCOUNT_DTYPE)
+        self.olib.tbo_dump_accounts(self.o, _ptr(a_orc))
+        if a_gpu.tobytes() != a_orc.tobytes():
+            raise ParityError(f"accounts differ: gpu {len(a_gpu)} rows, oracle {len(a_orc)} rows; "
+                              f"first diff at {_first_diff(a_gpu, a_orc)}")
+        nt = self.lib.tbg_dump_transfers(self.g, None, None)
+        t_gpu = np.zeros(max(nt, 0), dtype=TRANSFER_DTYPE)
+        s_gpu = np.zeros(max(nt, 0), dtype=np.uint8)
+        self.lib.tbg_dump_transfers(self.g, _ptr(t_gpu), _ptr(s_gpu))
+        ntr = self.olib.tbo_transfer_count(self.o)
+        t_orc = np.zeros(ntr, dtype=TRANSFER_DTYPE)
+        s_orc = np.zeros(ntr, dtype=np.uint8)
+        self.olib.tbo_dump_transfers(self.o, _ptr(t_orc))
+        self.olib.tbo_dump_pending_status(self.o, _ptr(s_orc))
+        if t_gpu.tobytes() != t_orc.tobytes():
+            raise ParityError(f"transfers differ: gpu {len(t_gpu)} rows, oracle {len(t_orc)}; "
+                              f"first diff at {_first_diff(t_gpu, t_orc)}")
+        if s_gpu.tobytes() != s_orc.tobytes():
+            raise ParityError("TransferPending statuses differ")
+        return len(a_orc), len(t_orc)
+
+
+def _first_diff(a, b):
+    n = min(len(a), len(b))
+    for i in range(n):
+        if a[i].tobytes() != b[i].tobytes():
+            return f"row {i}: gpu={a[i]} oracle={b[i]}"
+    return f"length {len(a)} vs {len(b)}"

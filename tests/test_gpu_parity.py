@@ -1,0 +1,105 @@
+"""HIP executor vs CPU oracle on seeded synthetic workloads (bit-exact results and state)."""
+import numpy as np
+import pytest
+
+from parity import Pair
+from tigerbeetle_amd import workload
+from tigerbeetle_amd.types import TIMESTAMP_MAX, NS_PER_S
+
+pytestmark = pytest.mark.gpu
+
+
+def _split(n, rng, max_batch):
+    lens = []
+    while n > 0:
+        b = int(min(n, rng.integers(1, max_batch + 1)))
+        lens.append(b)
+        n -= b
+    return lens
+
+
+@pytest.mark.parametrize("force_replay", [False, True], ids=["parallel", "replay"])
+@pytest.mark.parametrize("seed", range(6))
+def test_fuzz(seed, force_replay):
+    rng = np.random.default_rng(1000 + seed)
+    p = Pair(account_capacity=1 << 12, transfer_capacity=1 << 15, batch_events_max=4096,
+             pulse_batch_max=16, pulse_next_timestamp_init=TIMESTAMP_MAX,
+             force_replay=force_replay)
+    try:
+        n_acc = 24
+        a = workload.fuzz_accounts(rng, 40, n_acc)
+        p.create_accounts(a, _split(len(a), rng, 12))
+        # A clean set of accounts so that most transfers reach the deep checks.
+        clean = workload.accounts(n_acc, seed=seed, id_offset=0, ledger=1)
+        clean["flags"] = rng.choice([0, 0, 2, 4, 8], size=n_acc).astype(np.uint16)
+        p.create_accounts(clean, _split(n_acc, rng, 8))
+        ids_seen = []
+        for step in range(8):
+            pend = np.array(ids_seen[-200:], dtype=np.uint64) if ids_seen else None
+            t = workload.fuzz_transfers(rng, 300, 400, n_acc + 1, pending_ids=pend)
+            ids_seen.extend(int(x) for x in t["id"][:, 0])
+            p.create_transfers(t, _split(len(t), rng, 64))
+            if step % 3 == 2:
+                p.tick(int(rng.integers(1, 3)) * NS_PER_S)
+        p.compare_state()
+    finally:
+        p.close()
+
+
+def test_uniform_config2_small():
+    """Config 2 shape at small scale: 10k accounts, 8189-event batches; all `created`."""
+    p = Pair(account_capacity=1 << 14, transfer_capacity=1 << 17, batch_events_max=1 << 17)
+    try:
+        acc = workload.accounts(10_000, seed=42)
+        r = p.create_accounts(acc, [8189, 10_000 - 8189])
+        assert (r["status"] == 0xFFFFFFFF).all()
+        t = workload.transfers_uniform(100_000, 10_000, seed=42)
+        lens = [8189] * (100_000 // 8189) + [100_000 % 8189]
+        r = p.create_transfers(t, lens)
+        assert (r["status"] == 0xFFFFFFFF).all()
+        assert p.stats["replayed"] == 0
+        p.compare_state()
+    finally:
+        p.close()
+
+
+def test_hot_limits_config3_small():
+    """Config 3 shape at small scale: Zipfian hot accounts with debits_must_not_exceed_credits."""
+    p = Pair(account_capacity=1 << 14, transfer_capacity=1 << 16, batch_events_max=1 << 15)
+    try:
+        acc = workload.accounts(2_000, seed=3)
+        acc["flags"][1:101] |= 2
+        p.create_accounts(acc)
+        p.create_transfers(workload.funding_transfers(100, 200_000, id_offset=10_000_000))
+        t = workload.transfers_hot_limits(20_000, n_accounts=2_000, n_hot=100, seed=3)
+        r = p.create_transfers(t, [8189, 8189, 20_000 - 2 * 8189])
+        failed = (r["status"] == 54).sum()
+        assert failed > 0, "the workload should exercise exceeds_credits"
+        p.compare_state()
+    finally:
+        p.close()
+
+
+def test_two_phase_config4_small():
+    """Config 4 shape: pending with timeouts, post/void, linked chains with failures, resubmits,
+    pulses."""
+    rng = np.random.default_rng(4)
+    p = Pair(account_capacity=1 << 12, transfer_capacity=1 << 17, batch_events_max=1 << 15,
+             pulse_batch_max=8190)
+    try:
+        p.create_accounts(workload.accounts(1_000, seed=4))
+        pending, seen = np.zeros(0, dtype=np.uint64), np.zeros(0, dtype=np.uint64)
+        offset = 0
+        for step in range(6):
+            t = workload.transfers_two_phase(8_000, 1_000, seed=40 + step, id_offset=offset,
+                                             prior_pending_ids=pending, prior_ids=seen)
+            offset += 8_000
+            r = p.create_transfers(t, [4_000, 4_000])
+            created = r["status"] == 0xFFFFFFFF
+            is_pending = (t["flags"] & 2) != 0
+            pending = np.concatenate([pending, t["id"][created & is_pending, 0]])[-5_000:]
+            seen = np.concatenate([seen, t["id"][:, 0]])[-20_000:]
+            p.tick(int(rng.integers(1, 3)) * NS_PER_S)
+        p.compare_state()
+    finally:
+        p.close()

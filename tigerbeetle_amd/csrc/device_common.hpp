@@ -1,0 +1,143 @@
+// Device-side building blocks of the executor: u128 helpers, the HBM id tables, slot encoding.
+//
+// Tables (one per groove of the reference's Forest, src/state_machine.zig:278-283):
+//   * rows: an append-only array of 128-byte objects (tb_account_t / tb_transfer_t). Row r of
+//     the transfer store is the r-th create_transfers event ever submitted (likewise accounts), so
+//     an in-flight event and its row share one index; `live[r]` says whether row r is an object.
+//   * slots: an open-addressing (linear probing) hash index id -> row, one u64 word per slot:
+//       0                 empty
+//       kTomb             deleted (a claim whose event did not create an object); probes skip it
+//       (row + 1)         the object at `row`          (bit 62 set: an orphaned id, transfers only)
+//     During a call, a slot may hold an in-flight claim: (row + 1) with row >= row_base of the
+//     call; the id of such a row is read from the call's input events. Claims race with
+//     atomicCAS(0 -> ref) and duplicates resolve with atomicMin, so the earliest event of the call
+//     owns the slot -- the serial order's first occurrence.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/tb_types.h"
+
+namespace tbg {
+
+typedef unsigned __int128 u128;
+
+constexpr uint64_t kEmpty = 0;
+constexpr uint64_t kTomb = ~0ull;
+constexpr uint64_t kOrphanBit = 1ull << 62;
+constexpr uint64_t kRefMask = (1ull << 62) - 1;
+constexpr uint64_t kNone = ~0ull;  // "no row" in per-event scratch
+constexpr u128 kU128Max = ~(u128)0;
+
+__host__ __device__ inline u128 U(const tb_uint128_t& x) { return ((u128)x.hi << 64) | x.lo; }
+__host__ __device__ inline tb_uint128_t W(u128 x) {
+    tb_uint128_t r;
+    r.lo = (uint64_t)x;
+    r.hi = (uint64_t)(x >> 64);
+    return r;
+}
+__host__ __device__ inline bool u128_eq(const tb_uint128_t& a, const tb_uint128_t& b) {
+    return a.lo == b.lo && a.hi == b.hi;
+}
+__host__ __device__ inline bool u128_is_zero(const tb_uint128_t& a) { return (a.lo | a.hi) == 0; }
+__host__ __device__ inline bool u128_is_max(const tb_uint128_t& a) {
+    return (a.lo & a.hi) == ~0ull;
+}
+
+__host__ __device__ inline uint64_t mix64(uint64_t h) {
+    h ^= h >> 33;
+    h *= 0xff51afd7ed558ccdull;
+    h ^= h >> 33;
+    h *= 0xc4ceb9fe1a85ec53ull;
+    h ^= h >> 33;
+    return h;
+}
+__host__ __device__ inline uint64_t hash_id(const tb_uint128_t& id) {
+    return mix64(id.lo ^ mix64(id.hi + 0x9E3779B97F4A7C15ull));
+}
+
+// Non-temporal / plain 16-byte vector copies of 128-byte rows.
+struct alignas(16) Row128 {
+    uint4 q[8];
+};
+
+__device__ inline void copy_row(void* dst, const void* src) {
+    const uint4* s = reinterpret_cast<const uint4*>(src);
+    uint4* d = reinterpret_cast<uint4*>(dst);
+#pragma unroll
+    for (int i = 0; i < 8; i++) d[i] = s[i];
+}
+
+// u128 atomic add/sub on a {lo, hi} pair: the carry/borrow of each u64 add is propagated with a
+// second atomic. Concurrent adds commute, so the final value is the exact sum.
+__device__ inline void atomic_add_u128(tb_uint128_t* p, u128 v) {
+    uint64_t lo = (uint64_t)v, hi = (uint64_t)(v >> 64);
+    if (lo) {
+        uint64_t old = atomicAdd((unsigned long long*)&p->lo, (unsigned long long)lo);
+        if (old + lo < old) hi += 1;
+    }
+    if (hi) atomicAdd((unsigned long long*)&p->hi, (unsigned long long)hi);
+}
+__device__ inline void atomic_sub_u128(tb_uint128_t* p, u128 v) {
+    uint64_t lo = (uint64_t)v, hi = (uint64_t)(v >> 64);
+    if (lo) {
+        uint64_t old = atomicAdd((unsigned long long*)&p->lo, (unsigned long long)(0 - lo));
+        if (old < lo) hi += 1;  // borrow
+    }
+    if (hi) atomicAdd((unsigned long long*)&p->hi, (unsigned long long)(0 - hi));
+}
+
+// The 32-bit word holding {code, flags} of an Account (offset 116): flags are its high half.
+__device__ inline uint32_t* account_code_flags_word(tb_account_t* a) {
+    return reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(a) + 116);
+}
+
+// A table view passed by value to kernels.
+struct IdTable {
+    unsigned long long* slots;
+    uint64_t mask;  // slot count - 1
+};
+
+// Read-only probe: returns the slot index holding `id`, or kNone. `row_id(r)` gives the id of row
+// r (committed rows from the store, in-flight rows from the call's input).
+template <typename RowId>
+__device__ inline uint64_t probe_find(const IdTable& t, const tb_uint128_t& id, RowId row_id) {
+    uint64_t s = hash_id(id) & t.mask;
+    for (uint64_t n = 0; n <= t.mask; n++) {
+        uint64_t w = t.slots[s];
+        if (w == kEmpty) return kNone;
+        if (w != kTomb) {
+            uint64_t r = (w & kRefMask) - 1;
+            if (u128_eq(row_id(r), id)) return s;
+        }
+        s = (s + 1) & t.mask;
+    }
+    return kNone;
+}
+
+// Claim-or-find: inserts an in-flight claim `ref` for `id` unless `id` is already present.
+// Returns the slot of `id`. Duplicates within the call keep the smallest ref (earliest event).
+template <typename RowId>
+__device__ inline uint64_t probe_claim(const IdTable& t, const tb_uint128_t& id, uint64_t ref,
+                                       uint64_t row_base, RowId row_id) {
+    uint64_t s = hash_id(id) & t.mask;
+    for (uint64_t n = 0; n <= t.mask; n++) {
+        uint64_t w = t.slots[s];
+        if (w == kEmpty) {
+            w = atomicCAS(&t.slots[s], (unsigned long long)kEmpty, (unsigned long long)ref);
+            if (w == kEmpty) return s;
+        }
+        if (w != kTomb) {
+            uint64_t r = (w & kRefMask) - 1;
+            if (u128_eq(row_id(r), id)) {
+                if (r >= row_base && ref < w) atomicMin(&t.slots[s], (unsigned long long)ref);
+                return s;
+            }
+        }
+        s = (s + 1) & t.mask;
+    }
+    return kNone;  // table full: the host sizes tables so this cannot happen
+}
+
+}  // namespace tbg

@@ -1,0 +1,651 @@
+// The ordered replay: execute_create restated for one device thread, over the HBM tables.
+//
+// The replay executes, in the serial order of the call, every event whose outcome can depend on
+// in-call state: linked chains, duplicate ids, post/void, balancing, limits, closing, imported
+// batches, overflow-risk amounts, and every event touching an account such events touch. It is a
+// statement-for-statement restatement of src/state_machine.zig (execute_create :3002-3213,
+// create_account :3613-3703, create_transfer :3719-4051, post_or_void_pending_transfer
+// :4053-4382) with the groove operations mapped onto the HBM tables of device_common.hpp.
+//
+// In-call id visibility (the groove's get() during a batch): the slot of an id holds the ref of
+// the earliest in-call event with that id (or a committed row). For a lookup made by event k, an
+// in-call holder j is interpreted through results[j], which is final for every j < k (the parallel
+// path and static checks ran before the replay; the replay runs in order):
+//   j >= k                  -> not found (the holder has not executed yet)
+//   results[j] == created   -> found (row row_base + j)
+//   results[j] transient    -> orphaned id
+//   otherwise               -> not found
+// When an event that found its id "not found" creates it (or orphans it), it becomes the holder.
+// A chain rollback rewrites results[] of the chain to linked_event_failed, which makes the ids the
+// chain created read as "not found" again -- exactly the groove's scope discard.
+#pragma once
+
+#include "device_common.hpp"
+
+namespace tbg {
+
+struct DevScalars {
+    unsigned long long pulse_next_timestamp;
+    unsigned long long accounts_key_max;   // objects tree key_range.key_max (0 = no key_range)
+    unsigned long long transfers_key_max;
+    unsigned long long expiry_count;       // entries in the expires_at list
+    unsigned int flags;                    // per call: kFlag*
+    unsigned int slow_count;               // per call: events in the replay list
+    unsigned long long stats[4];           // per call: events, fast, replayed, static
+};
+
+enum : unsigned int {
+    kFlagImported = 1u << 0,   // some event of the call has the imported flag
+    kFlagPostVoid = 1u << 1,   // some event of the call posts or voids
+    kFlagUndoOverflow = 1u << 2,
+    kFlagTableFull = 1u << 3,
+};
+
+enum : uint8_t { kClassDone = 0, kClassFast = 1, kClassSlow = 2 };
+
+struct UndoEntry {
+    uint64_t kind_index;  // kind in the top byte
+    tb_account_t row;     // kUndoAccount: the whole row before the update
+};
+constexpr uint64_t kUndoAccount = 1ull << 56;
+constexpr uint64_t kUndoStatus = 2ull << 56;
+constexpr uint64_t kUndoIndexMask = (1ull << 56) - 1;
+
+// Everything a kernel needs, passed by value.
+struct Tables {
+    IdTable acc;
+    tb_account_t* acc_rows;
+    uint8_t* acc_live;
+    uint32_t* acc_hot;       // epoch of the last call that routed an event of this account to replay
+    uint32_t* acc_closable;  // epoch of the last call whose events may change `closed` here
+    uint64_t acc_rows_used;
+
+    IdTable tr;
+    tb_transfer_t* tr_rows;
+    uint8_t* tr_live;
+    uint8_t* tr_status;  // TransferPending.status per row (src/tigerbeetle.zig:118-130)
+    uint64_t tr_rows_used;
+
+    uint64_t* expiry;  // rows of pending transfers with timeout > 0 (the expires_at index)
+    uint64_t expiry_capacity;
+
+    const uint64_t* acc_ts_index;  // sorted timestamps of live accounts (imported checks)
+    uint64_t acc_ts_count;
+    const uint64_t* tr_ts_index;   // sorted timestamps of live transfers
+    uint64_t tr_ts_count;
+
+    DevScalars* scalars;
+    UndoEntry* undo;
+    uint64_t undo_capacity;
+};
+
+template <typename Event>
+struct Call {
+    const Event* events;
+    uint32_t n;
+    const uint32_t* batch_ends;
+    const uint64_t* batch_ts;
+    uint32_t n_batches;
+    tb_create_result_t* results;
+    uint64_t row_base;
+    uint32_t epoch;
+    uint32_t force_replay;
+    // per-event scratch
+    uint32_t* ev_batch;
+    uint64_t* ev_slot;
+    uint64_t* ev_dr;
+    uint64_t* ev_cr;
+    uint64_t* ev_p_slot;
+    uint8_t* ev_class;
+    const uint32_t* slow_list;
+};
+
+__device__ inline uint32_t batch_of(const uint32_t* ends, uint32_t n_batches, uint32_t k) {
+    uint32_t lo = 0, hi = n_batches;  // first b with ends[b] > k
+    while (lo < hi) {
+        uint32_t mid = (lo + hi) >> 1;
+        if (ends[mid] > k) hi = mid;
+        else lo = mid + 1;
+    }
+    return lo;
+}
+
+__device__ inline bool ts_index_contains(const uint64_t* idx, uint64_t n, uint64_t ts) {
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) {
+        uint64_t mid = (lo + hi) >> 1;
+        if (idx[mid] < ts) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo < n && idx[lo] == ts;
+}
+
+// ---- account lookup (accounts do not change during a create_transfers call) ----------------
+
+__device__ inline uint64_t account_find(const Tables& T, const tb_uint128_t& id) {
+    const tb_account_t* rows = T.acc_rows;
+    uint64_t s = probe_find(T.acc, id, [&](uint64_t r) { return rows[r].id; });
+    if (s == kNone) return kNone;
+    return (T.acc.slots[s] & kRefMask) - 1;
+}
+
+// ---- the replay state -------------------------------------------------------------------------
+
+struct Scope {
+    bool open = false;
+    uint64_t undo_len = 0;
+    unsigned long long accounts_key_max = 0, transfers_key_max = 0, expiry_count = 0;
+};
+
+struct Replay {
+    const Tables& T;
+    Scope scope;
+    uint64_t undo_len = 0;
+    bool overflow = false;
+
+    __device__ explicit Replay(const Tables& t) : T(t) {}
+
+    __device__ void scope_open() {
+        scope.open = true;
+        scope.undo_len = undo_len;
+        scope.accounts_key_max = T.scalars->accounts_key_max;
+        scope.transfers_key_max = T.scalars->transfers_key_max;
+        scope.expiry_count = T.scalars->expiry_count;
+    }
+    __device__ void scope_close(bool discard) {
+        if (discard) {
+            for (uint64_t i = undo_len; i-- > scope.undo_len;) {
+                const UndoEntry& u = T.undo[i];
+                uint64_t idx = u.kind_index & kUndoIndexMask;
+                if ((u.kind_index & ~kUndoIndexMask) == kUndoAccount) {
+                    copy_row(&T.acc_rows[idx], &u.row);
+                } else {
+                    T.tr_status[idx] = (uint8_t)u.row.timestamp;
+                }
+            }
+            T.scalars->accounts_key_max = scope.accounts_key_max;
+            T.scalars->transfers_key_max = scope.transfers_key_max;
+            T.scalars->expiry_count = scope.expiry_count;
+        }
+        undo_len = scope.undo_len;
+        scope.open = false;
+    }
+    __device__ void log_account(uint64_t row) {
+        if (!scope.open) return;
+        if (undo_len >= T.undo_capacity) {
+            overflow = true;
+            return;
+        }
+        T.undo[undo_len].kind_index = kUndoAccount | row;
+        copy_row(&T.undo[undo_len].row, &T.acc_rows[row]);
+        undo_len++;
+    }
+    __device__ void log_status(uint64_t row) {
+        if (!scope.open) return;
+        if (undo_len >= T.undo_capacity) {
+            overflow = true;
+            return;
+        }
+        T.undo[undo_len].kind_index = kUndoStatus | row;
+        T.undo[undo_len].row.timestamp = T.tr_status[row];
+        undo_len++;
+    }
+    __device__ void update_account(uint64_t row, const tb_account_t& next) {
+        log_account(row);
+        T.acc_rows[row] = next;
+    }
+    __device__ void update_status(uint64_t row, uint8_t status) {
+        log_status(row);
+        T.tr_status[row] = status;
+    }
+};
+
+// ---- transfers --------------------------------------------------------------------------------
+
+// groove.get for transfers as seen by in-call event k: 0 not found, 1 object (row), 2 orphaned.
+template <typename C>
+__device__ inline int replay_get_transfer_at_slot(const Tables& T, const C& c, uint64_t s,
+                                                  uint32_t k, uint64_t* row) {
+    if (s == kNone) return 0;
+    uint64_t w = T.tr.slots[s];
+    if (w == kEmpty || w == kTomb) return 0;
+    uint64_t r = (w & kRefMask) - 1;
+    if (r < c.row_base) {
+        if (w & kOrphanBit) return 2;
+        *row = r;
+        return 1;
+    }
+    uint64_t j = r - c.row_base;
+    if (j >= k) return 0;
+    uint32_t st = c.results[j].status;
+    if (st == TB_STATUS_CREATED) {
+        *row = r;
+        return 1;
+    }
+    if (tb_transfer_status_transient(st)) return 2;
+    return 0;
+}
+
+template <typename C>
+__device__ inline uint64_t transfer_slot_find(const Tables& T, const C& c,
+                                              const tb_uint128_t& id) {
+    const tb_transfer_t* rows = T.tr_rows;
+    const tb_transfer_t* events = c.events;
+    uint64_t base = c.row_base;
+    return probe_find(T.tr, id, [&](uint64_t r) {
+        return r >= base ? events[r - base].id : rows[r].id;
+    });
+}
+
+__device__ inline uint32_t post_or_void_pending_transfer_exists(const tb_transfer_t& t,
+                                                               const tb_transfer_t& e,
+                                                               const tb_transfer_t& p,
+                                                               uint64_t* ts) {
+    if (U(t.debit_account_id) != 0 && U(t.debit_account_id) != U(e.debit_account_id))
+        return TB_CT_EXISTS_WITH_DIFFERENT_DEBIT_ACCOUNT_ID;
+    if (U(t.credit_account_id) != 0 && U(t.credit_account_id) != U(e.credit_account_id))
+        return TB_CT_EXISTS_WITH_DIFFERENT_CREDIT_ACCOUNT_ID;
+    if (t.flags & TB_TRANSFER_VOID_PENDING) {
+        if (U(t.amount) == 0) {
+            if (U(e.amount) != U(p.amount)) return TB_CT_EXISTS_WITH_DIFFERENT_AMOUNT;
+        } else if (U(t.amount) != U(e.amount)) {
+            return TB_CT_EXISTS_WITH_DIFFERENT_AMOUNT;
+        }
+    }
+    if (t.flags & TB_TRANSFER_POST_PENDING) {
+        if (U(t.amount) == kU128Max) {
+            if (U(e.amount) != U(p.amount)) return TB_CT_EXISTS_WITH_DIFFERENT_AMOUNT;
+        } else if (U(t.amount) != U(e.amount)) {
+            return TB_CT_EXISTS_WITH_DIFFERENT_AMOUNT;
+        }
+    }
+    if (U(t.user_data_128) == 0) {
+        if (U(e.user_data_128) != U(p.user_data_128))
+            return TB_CT_EXISTS_WITH_DIFFERENT_USER_DATA_128;
+    } else if (U(t.user_data_128) != U(e.user_data_128)) {
+        return TB_CT_EXISTS_WITH_DIFFERENT_USER_DATA_128;
+    }
+    if (t.user_data_64 == 0) {
+        if (e.user_data_64 != p.user_data_64) return TB_CT_EXISTS_WITH_DIFFERENT_USER_DATA_64;
+    } else if (t.user_data_64 != e.user_data_64) {
+        return TB_CT_EXISTS_WITH_DIFFERENT_USER_DATA_64;
+    }
+    if (t.user_data_32 == 0) {
+        if (e.user_data_32 != p.user_data_32) return TB_CT_EXISTS_WITH_DIFFERENT_USER_DATA_32;
+    } else if (t.user_data_32 != e.user_data_32) {
+        return TB_CT_EXISTS_WITH_DIFFERENT_USER_DATA_32;
+    }
+    if (t.ledger != 0 && t.ledger != e.ledger) return TB_CT_EXISTS_WITH_DIFFERENT_LEDGER;
+    if (t.code != 0 && t.code != e.code) return TB_CT_EXISTS_WITH_DIFFERENT_CODE;
+    *ts = e.timestamp;
+    return TB_CT_EXISTS;
+}
+
+// create_transfer_exists (:3988-4051) given the pending transfer p (post/void only).
+__device__ inline uint32_t create_transfer_exists(const tb_transfer_t& t, const tb_transfer_t& e,
+                                                  const tb_transfer_t* p, uint64_t* ts) {
+    if (t.flags != e.flags) return TB_CT_EXISTS_WITH_DIFFERENT_FLAGS;
+    if (U(t.pending_id) != U(e.pending_id)) return TB_CT_EXISTS_WITH_DIFFERENT_PENDING_ID;
+    if (t.timeout != e.timeout) return TB_CT_EXISTS_WITH_DIFFERENT_TIMEOUT;
+    if (t.flags & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING))
+        return post_or_void_pending_transfer_exists(t, e, *p, ts);
+    if (U(t.debit_account_id) != U(e.debit_account_id))
+        return TB_CT_EXISTS_WITH_DIFFERENT_DEBIT_ACCOUNT_ID;
+    if (U(t.credit_account_id) != U(e.credit_account_id))
+        return TB_CT_EXISTS_WITH_DIFFERENT_CREDIT_ACCOUNT_ID;
+    if (t.flags & (TB_TRANSFER_BALANCING_DEBIT | TB_TRANSFER_BALANCING_CREDIT)) {
+        if (U(t.amount) < U(e.amount)) return TB_CT_EXISTS_WITH_DIFFERENT_AMOUNT;
+    } else if (U(t.amount) != U(e.amount)) {
+        return TB_CT_EXISTS_WITH_DIFFERENT_AMOUNT;
+    }
+    if (U(t.user_data_128) != U(e.user_data_128)) return TB_CT_EXISTS_WITH_DIFFERENT_USER_DATA_128;
+    if (t.user_data_64 != e.user_data_64) return TB_CT_EXISTS_WITH_DIFFERENT_USER_DATA_64;
+    if (t.user_data_32 != e.user_data_32) return TB_CT_EXISTS_WITH_DIFFERENT_USER_DATA_32;
+    if (t.ledger != e.ledger) return TB_CT_EXISTS_WITH_DIFFERENT_LEDGER;
+    if (t.code != e.code) return TB_CT_EXISTS_WITH_DIFFERENT_CODE;
+    *ts = e.timestamp;
+    return TB_CT_EXISTS;
+}
+
+__device__ inline void expiry_append(const Tables& T, uint64_t row, bool serial) {
+    unsigned long long i = serial ? T.scalars->expiry_count++
+                                  : atomicAdd(&T.scalars->expiry_count, 1ull);
+    if (i < T.expiry_capacity) T.expiry[i] = row;
+    else atomicOr(&T.scalars->flags, kFlagTableFull);
+}
+
+template <typename C>
+__device__ uint32_t replay_post_or_void(Replay& R, const C& c, uint32_t k, uint64_t ts_event,
+                                        const tb_transfer_t& t, uint64_t* ts_out) {
+    const Tables& T = R.T;
+    const uint16_t f = t.flags;
+    if ((f & TB_TRANSFER_POST_PENDING) && (f & TB_TRANSFER_VOID_PENDING))
+        return TB_CT_FLAGS_ARE_MUTUALLY_EXCLUSIVE;
+    if (f & (TB_TRANSFER_PENDING | TB_TRANSFER_BALANCING_DEBIT | TB_TRANSFER_BALANCING_CREDIT |
+             TB_TRANSFER_CLOSING_DEBIT | TB_TRANSFER_CLOSING_CREDIT))
+        return TB_CT_FLAGS_ARE_MUTUALLY_EXCLUSIVE;
+    if (u128_is_zero(t.pending_id)) return TB_CT_PENDING_ID_MUST_NOT_BE_ZERO;
+    if (u128_is_max(t.pending_id)) return TB_CT_PENDING_ID_MUST_NOT_BE_INT_MAX;
+    if (u128_eq(t.pending_id, t.id)) return TB_CT_PENDING_ID_MUST_BE_DIFFERENT;
+    if (t.timeout != 0) return TB_CT_TIMEOUT_RESERVED_FOR_PENDING_TRANSFER;
+
+    uint64_t p_row = 0;
+    if (replay_get_transfer_at_slot(T, c, transfer_slot_find(T, c, t.pending_id), k, &p_row) != 1)
+        return TB_CT_PENDING_TRANSFER_NOT_FOUND;
+    const tb_transfer_t p = T.tr_rows[p_row];
+    if (!(p.flags & TB_TRANSFER_PENDING)) return TB_CT_PENDING_TRANSFER_NOT_PENDING;
+
+    uint64_t dr_row = account_find(T, p.debit_account_id);
+    uint64_t cr_row = account_find(T, p.credit_account_id);
+    if (dr_row == kNone || cr_row == kNone) return TB_CT_PENDING_TRANSFER_NOT_FOUND;  // unreachable
+    const tb_account_t dr = T.acc_rows[dr_row];
+    const tb_account_t cr = T.acc_rows[cr_row];
+
+    if (!u128_is_zero(t.debit_account_id) && !u128_eq(t.debit_account_id, p.debit_account_id))
+        return TB_CT_PENDING_TRANSFER_HAS_DIFFERENT_DEBIT_ACCOUNT_ID;
+    if (!u128_is_zero(t.credit_account_id) && !u128_eq(t.credit_account_id, p.credit_account_id))
+        return TB_CT_PENDING_TRANSFER_HAS_DIFFERENT_CREDIT_ACCOUNT_ID;
+    if (t.ledger > 0 && t.ledger != p.ledger) return TB_CT_PENDING_TRANSFER_HAS_DIFFERENT_LEDGER;
+    if (t.code > 0 && t.code != p.code) return TB_CT_PENDING_TRANSFER_HAS_DIFFERENT_CODE;
+
+    u128 p_amount = U(p.amount);
+    u128 amount = (f & TB_TRANSFER_VOID_PENDING)
+                      ? (U(t.amount) == 0 ? p_amount : U(t.amount))
+                      : (U(t.amount) == kU128Max ? p_amount : U(t.amount));
+    if (amount > p_amount) return TB_CT_EXCEEDS_PENDING_TRANSFER_AMOUNT;
+    if ((f & TB_TRANSFER_VOID_PENDING) && amount < p_amount)
+        return TB_CT_PENDING_TRANSFER_HAS_DIFFERENT_AMOUNT;
+
+    switch (T.tr_status[p_row]) {
+        case TB_PENDING_PENDING: break;
+        case TB_PENDING_POSTED: return TB_CT_PENDING_TRANSFER_ALREADY_POSTED;
+        case TB_PENDING_VOIDED: return TB_CT_PENDING_TRANSFER_ALREADY_VOIDED;
+        default: return TB_CT_PENDING_TRANSFER_EXPIRED;
+    }
+    const bool has_expiry = p.timeout != 0;
+    uint64_t expires_at = 0;
+    if (has_expiry) {
+        expires_at = p.timestamp + (uint64_t)p.timeout * TB_NS_PER_S;
+        if (expires_at <= ts_event) return TB_CT_PENDING_TRANSFER_EXPIRED;
+    }
+    uint64_t ts_actual = ts_event;
+    if (f & TB_TRANSFER_IMPORTED) {
+        if (t.timestamp <= T.scalars->transfers_key_max)
+            return TB_CT_IMPORTED_EVENT_TIMESTAMP_MUST_NOT_REGRESS;
+        if (ts_index_contains(T.acc_ts_index, T.acc_ts_count, t.timestamp))
+            return TB_CT_IMPORTED_EVENT_TIMESTAMP_MUST_NOT_REGRESS;
+        ts_actual = t.timestamp;
+    }
+    if ((dr.flags & TB_ACCOUNT_CLOSED) && !(f & TB_TRANSFER_VOID_PENDING))
+        return TB_CT_DEBIT_ACCOUNT_ALREADY_CLOSED;
+    if ((cr.flags & TB_ACCOUNT_CLOSED) && !(f & TB_TRANSFER_VOID_PENDING))
+        return TB_CT_CREDIT_ACCOUNT_ALREADY_CLOSED;
+
+    // Insert the posting/voiding transfer at this event's row.
+    const uint64_t row = c.row_base + k;
+    tb_transfer_t o;
+    o.id = t.id;
+    o.debit_account_id = p.debit_account_id;
+    o.credit_account_id = p.credit_account_id;
+    o.amount = W(amount);
+    o.pending_id = t.pending_id;
+    o.user_data_128 = U(t.user_data_128) > 0 ? t.user_data_128 : p.user_data_128;
+    o.user_data_64 = t.user_data_64 > 0 ? t.user_data_64 : p.user_data_64;
+    o.user_data_32 = t.user_data_32 > 0 ? t.user_data_32 : p.user_data_32;
+    o.timeout = 0;
+    o.ledger = p.ledger;
+    o.code = p.code;
+    o.flags = t.flags;
+    o.timestamp = ts_actual;
+    T.tr_rows[row] = o;
+    T.tr_status[row] = TB_PENDING_NONE;
+    if (ts_actual > T.scalars->transfers_key_max) T.scalars->transfers_key_max = ts_actual;
+
+    if (has_expiry && T.scalars->pulse_next_timestamp == expires_at)
+        T.scalars->pulse_next_timestamp = TB_TIMESTAMP_MIN;
+    R.update_status(p_row, (f & TB_TRANSFER_POST_PENDING) ? TB_PENDING_POSTED : TB_PENDING_VOIDED);
+
+    tb_account_t dr_new = dr, cr_new = cr;
+    dr_new.debits_pending = W(U(dr.debits_pending) - p_amount);
+    cr_new.credits_pending = W(U(cr.credits_pending) - p_amount);
+    if (f & TB_TRANSFER_POST_PENDING) {
+        dr_new.debits_posted = W(U(dr.debits_posted) + amount);
+        cr_new.credits_posted = W(U(cr.credits_posted) + amount);
+    }
+    if (f & TB_TRANSFER_VOID_PENDING) {
+        if (p.flags & TB_TRANSFER_CLOSING_DEBIT) dr_new.flags &= (uint16_t)~TB_ACCOUNT_CLOSED;
+        if (p.flags & TB_TRANSFER_CLOSING_CREDIT) cr_new.flags &= (uint16_t)~TB_ACCOUNT_CLOSED;
+    }
+    if (amount > 0 || p_amount > 0 || dr_new.flags != dr.flags) R.update_account(dr_row, dr_new);
+    if (amount > 0 || p_amount > 0 || cr_new.flags != cr.flags) R.update_account(cr_row, cr_new);
+    *ts_out = ts_actual;
+    return TB_STATUS_CREATED;
+}
+
+template <typename C>
+__device__ uint32_t replay_create_transfer(Replay& R, const C& c, uint32_t k, uint64_t ts_event,
+                                           const tb_transfer_t& t, uint64_t* ts_out) {
+    const Tables& T = R.T;
+    const uint16_t f = t.flags;
+    if (f & TB_TRANSFER_PADDING_MASK) return TB_CT_RESERVED_FLAG;
+    if (u128_is_zero(t.id)) return TB_CT_ID_MUST_NOT_BE_ZERO;
+    if (u128_is_max(t.id)) return TB_CT_ID_MUST_NOT_BE_INT_MAX;
+
+    uint64_t e_row = 0;
+    switch (replay_get_transfer_at_slot(T, c, c.ev_slot[k], k, &e_row)) {
+        case 1: {
+            const tb_transfer_t e = T.tr_rows[e_row];
+            if ((t.flags == e.flags) && U(t.pending_id) == U(e.pending_id) &&
+                t.timeout == e.timeout &&
+                (t.flags & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING))) {
+                uint64_t p_row = 0;
+                replay_get_transfer_at_slot(T, c, transfer_slot_find(T, c, t.pending_id), k,
+                                            &p_row);
+                const tb_transfer_t p = T.tr_rows[p_row];
+                return create_transfer_exists(t, e, &p, ts_out);
+            }
+            return create_transfer_exists(t, e, nullptr, ts_out);
+        }
+        case 2: return TB_CT_ID_ALREADY_FAILED;
+        default: break;
+    }
+
+    if (f & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING))
+        return replay_post_or_void(R, c, k, ts_event, t, ts_out);
+
+    if (u128_is_zero(t.debit_account_id)) return TB_CT_DEBIT_ACCOUNT_ID_MUST_NOT_BE_ZERO;
+    if (u128_is_max(t.debit_account_id)) return TB_CT_DEBIT_ACCOUNT_ID_MUST_NOT_BE_INT_MAX;
+    if (u128_is_zero(t.credit_account_id)) return TB_CT_CREDIT_ACCOUNT_ID_MUST_NOT_BE_ZERO;
+    if (u128_is_max(t.credit_account_id)) return TB_CT_CREDIT_ACCOUNT_ID_MUST_NOT_BE_INT_MAX;
+    if (u128_eq(t.credit_account_id, t.debit_account_id)) return TB_CT_ACCOUNTS_MUST_BE_DIFFERENT;
+    if (!u128_is_zero(t.pending_id)) return TB_CT_PENDING_ID_MUST_BE_ZERO;
+    if (!(f & TB_TRANSFER_PENDING)) {
+        if (t.timeout != 0) return TB_CT_TIMEOUT_RESERVED_FOR_PENDING_TRANSFER;
+        if (f & (TB_TRANSFER_CLOSING_DEBIT | TB_TRANSFER_CLOSING_CREDIT))
+            return TB_CT_CLOSING_TRANSFER_MUST_BE_PENDING;
+    }
+    if (t.ledger == 0) return TB_CT_LEDGER_MUST_NOT_BE_ZERO;
+    if (t.code == 0) return TB_CT_CODE_MUST_NOT_BE_ZERO;
+
+    const uint64_t dr_row = c.ev_dr[k];
+    if (dr_row == kNone) return TB_CT_DEBIT_ACCOUNT_NOT_FOUND;
+    const uint64_t cr_row = c.ev_cr[k];
+    if (cr_row == kNone) return TB_CT_CREDIT_ACCOUNT_NOT_FOUND;
+    const tb_account_t dr = T.acc_rows[dr_row];
+    const tb_account_t cr = T.acc_rows[cr_row];
+    if (dr.ledger != cr.ledger) return TB_CT_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;
+    if (t.ledger != dr.ledger) return TB_CT_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
+
+    uint64_t ts_actual = ts_event;
+    if (f & TB_TRANSFER_IMPORTED) {
+        if (t.timestamp <= T.scalars->transfers_key_max)
+            return TB_CT_IMPORTED_EVENT_TIMESTAMP_MUST_NOT_REGRESS;
+        if (ts_index_contains(T.acc_ts_index, T.acc_ts_count, t.timestamp))
+            return TB_CT_IMPORTED_EVENT_TIMESTAMP_MUST_NOT_REGRESS;
+        if (t.timestamp <= dr.timestamp)
+            return TB_CT_IMPORTED_EVENT_TIMESTAMP_MUST_POSTDATE_DEBIT_ACCOUNT;
+        if (t.timestamp <= cr.timestamp)
+            return TB_CT_IMPORTED_EVENT_TIMESTAMP_MUST_POSTDATE_CREDIT_ACCOUNT;
+        if (t.timeout != 0) return TB_CT_IMPORTED_EVENT_TIMEOUT_MUST_BE_ZERO;
+        ts_actual = t.timestamp;
+    }
+    if (dr.flags & TB_ACCOUNT_CLOSED) return TB_CT_DEBIT_ACCOUNT_ALREADY_CLOSED;
+    if (cr.flags & TB_ACCOUNT_CLOSED) return TB_CT_CREDIT_ACCOUNT_ALREADY_CLOSED;
+
+    u128 amount = U(t.amount);
+    if (f & TB_TRANSFER_BALANCING_DEBIT) {
+        u128 bal = U(dr.debits_posted) + U(dr.debits_pending);
+        u128 cp = U(dr.credits_posted);
+        u128 room = cp > bal ? cp - bal : 0;
+        if (room < amount) amount = room;
+    }
+    if (f & TB_TRANSFER_BALANCING_CREDIT) {
+        u128 bal = U(cr.credits_posted) + U(cr.credits_pending);
+        u128 dp = U(cr.debits_posted);
+        u128 room = dp > bal ? dp - bal : 0;
+        if (room < amount) amount = room;
+    }
+    const u128 dpe = U(dr.debits_pending), dpo = U(dr.debits_posted);
+    const u128 cpe = U(cr.credits_pending), cpo = U(cr.credits_posted);
+    if (f & TB_TRANSFER_PENDING) {
+        if (amount + dpe < amount) return TB_CT_OVERFLOWS_DEBITS_PENDING;
+        if (amount + cpe < amount) return TB_CT_OVERFLOWS_CREDITS_PENDING;
+    }
+    if (amount + dpo < amount) return TB_CT_OVERFLOWS_DEBITS_POSTED;
+    if (amount + cpo < amount) return TB_CT_OVERFLOWS_CREDITS_POSTED;
+    if (amount + (dpe + dpo) < amount) return TB_CT_OVERFLOWS_DEBITS;
+    if (amount + (cpe + cpo) < amount) return TB_CT_OVERFLOWS_CREDITS;
+    if (ts_actual + (uint64_t)t.timeout * TB_NS_PER_S > TB_TIMESTAMP_MAX)
+        return TB_CT_OVERFLOWS_TIMEOUT;
+    if ((dr.flags & TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS) && dpe + dpo + amount > U(dr.credits_posted))
+        return TB_CT_EXCEEDS_CREDITS;
+    if ((cr.flags & TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS) && cpe + cpo + amount > U(cr.debits_posted))
+        return TB_CT_EXCEEDS_DEBITS;
+
+    const uint64_t row = c.row_base + k;
+    tb_transfer_t o = t;
+    o.amount = W(amount);
+    o.timestamp = ts_actual;
+    T.tr_rows[row] = o;
+    T.tr_status[row] = (f & TB_TRANSFER_PENDING) ? TB_PENDING_PENDING : TB_PENDING_NONE;
+    if (ts_actual > T.scalars->transfers_key_max) T.scalars->transfers_key_max = ts_actual;
+    if ((f & TB_TRANSFER_PENDING) && t.timeout > 0) expiry_append(T, row, true);
+
+    tb_account_t dr_new = dr, cr_new = cr;
+    if (f & TB_TRANSFER_PENDING) {
+        dr_new.debits_pending = W(dpe + amount);
+        cr_new.credits_pending = W(cpe + amount);
+    } else {
+        dr_new.debits_posted = W(dpo + amount);
+        cr_new.credits_posted = W(cpo + amount);
+    }
+    if (f & TB_TRANSFER_CLOSING_DEBIT) dr_new.flags |= TB_ACCOUNT_CLOSED;
+    if (f & TB_TRANSFER_CLOSING_CREDIT) cr_new.flags |= TB_ACCOUNT_CLOSED;
+    if (amount > 0 || (dr_new.flags & TB_ACCOUNT_CLOSED)) R.update_account(dr_row, dr_new);
+    if (amount > 0 || (cr_new.flags & TB_ACCOUNT_CLOSED)) R.update_account(cr_row, cr_new);
+
+    if (t.timeout > 0) {
+        uint64_t expires_at = ts_actual + (uint64_t)t.timeout * TB_NS_PER_S;
+        if (expires_at < T.scalars->pulse_next_timestamp)
+            T.scalars->pulse_next_timestamp = expires_at;
+    }
+    *ts_out = ts_actual;
+    return TB_STATUS_CREATED;
+}
+
+// ---- accounts ---------------------------------------------------------------------------------
+
+template <typename C>
+__device__ inline int replay_get_account_at_slot(const Tables& T, const C& c, uint64_t s,
+                                                 uint32_t k, uint64_t* row) {
+    if (s == kNone) return 0;
+    uint64_t w = T.acc.slots[s];
+    if (w == kEmpty || w == kTomb) return 0;
+    uint64_t r = (w & kRefMask) - 1;
+    if (r < c.row_base) {
+        *row = r;
+        return 1;
+    }
+    uint64_t j = r - c.row_base;
+    if (j >= k) return 0;
+    if (c.results[j].status == TB_STATUS_CREATED) {
+        *row = r;
+        return 1;
+    }
+    return 0;
+}
+
+__device__ inline uint32_t create_account_exists(const tb_account_t& a, const tb_account_t& e,
+                                                 uint64_t* ts) {
+    if (a.flags != e.flags) return TB_CA_EXISTS_WITH_DIFFERENT_FLAGS;
+    if (U(a.user_data_128) != U(e.user_data_128)) return TB_CA_EXISTS_WITH_DIFFERENT_USER_DATA_128;
+    if (a.user_data_64 != e.user_data_64) return TB_CA_EXISTS_WITH_DIFFERENT_USER_DATA_64;
+    if (a.user_data_32 != e.user_data_32) return TB_CA_EXISTS_WITH_DIFFERENT_USER_DATA_32;
+    if (a.ledger != e.ledger) return TB_CA_EXISTS_WITH_DIFFERENT_LEDGER;
+    if (a.code != e.code) return TB_CA_EXISTS_WITH_DIFFERENT_CODE;
+    *ts = e.timestamp;
+    return TB_CA_EXISTS;
+}
+
+// The checks of create_account after the id lookup (:3636-3650), shared by the parallel path.
+__device__ inline uint32_t create_account_checks(const tb_account_t& a) {
+    if ((a.flags & TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS) &&
+        (a.flags & TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS))
+        return TB_CA_FLAGS_ARE_MUTUALLY_EXCLUSIVE;
+    if (!u128_is_zero(a.debits_pending)) return TB_CA_DEBITS_PENDING_MUST_BE_ZERO;
+    if (!u128_is_zero(a.debits_posted)) return TB_CA_DEBITS_POSTED_MUST_BE_ZERO;
+    if (!u128_is_zero(a.credits_pending)) return TB_CA_CREDITS_PENDING_MUST_BE_ZERO;
+    if (!u128_is_zero(a.credits_posted)) return TB_CA_CREDITS_POSTED_MUST_BE_ZERO;
+    if (a.ledger == 0) return TB_CA_LEDGER_MUST_NOT_BE_ZERO;
+    if (a.code == 0) return TB_CA_CODE_MUST_NOT_BE_ZERO;
+    return TB_STATUS_CREATED;
+}
+
+__device__ inline tb_account_t account_row_of(const tb_account_t& a, uint64_t ts) {
+    tb_account_t o;
+    o.id = a.id;
+    o.debits_pending = W(0);
+    o.debits_posted = W(0);
+    o.credits_pending = W(0);
+    o.credits_posted = W(0);
+    o.user_data_128 = a.user_data_128;
+    o.user_data_64 = a.user_data_64;
+    o.user_data_32 = a.user_data_32;
+    o.reserved = 0;
+    o.ledger = a.ledger;
+    o.code = a.code;
+    o.flags = a.flags;
+    o.timestamp = ts;
+    return o;
+}
+
+template <typename C>
+__device__ uint32_t replay_create_account(Replay& R, const C& c, uint32_t k, uint64_t ts_event,
+                                          const tb_account_t& a, uint64_t* ts_out) {
+    const Tables& T = R.T;
+    if (a.reserved != 0) return TB_CA_RESERVED_FIELD;
+    if (a.flags & TB_ACCOUNT_PADDING_MASK) return TB_CA_RESERVED_FLAG;
+    if (u128_is_zero(a.id)) return TB_CA_ID_MUST_NOT_BE_ZERO;
+    if (u128_is_max(a.id)) return TB_CA_ID_MUST_NOT_BE_INT_MAX;
+    uint64_t e_row = 0;
+    if (replay_get_account_at_slot(T, c, c.ev_slot[k], k, &e_row) == 1) {
+        const tb_account_t e = T.acc_rows[e_row];
+        return create_account_exists(a, e, ts_out);
+    }
+    uint32_t s = create_account_checks(a);
+    if (s != TB_STATUS_CREATED) return s;
+    uint64_t ts_actual = ts_event;
+    if (a.flags & TB_ACCOUNT_IMPORTED) {
+        if (a.timestamp <= T.scalars->accounts_key_max)
+            return TB_CA_IMPORTED_EVENT_TIMESTAMP_MUST_NOT_REGRESS;
+        if (ts_index_contains(T.tr_ts_index, T.tr_ts_count, a.timestamp))
+            return TB_CA_IMPORTED_EVENT_TIMESTAMP_MUST_NOT_REGRESS;
+        ts_actual = a.timestamp;
+    }
+    T.acc_rows[c.row_base + k] = account_row_of(a, ts_actual);
+    if (ts_actual > T.scalars->accounts_key_max) T.scalars->accounts_key_max = ts_actual;
+    *ts_out = ts_actual;
+    return TB_STATUS_CREATED;
+}
+
+}  // namespace tbg

@@ -1,0 +1,225 @@
+"""Seeded synthetic workloads for the commit path (BASELINE.json configs).
+
+All generators are numpy-vectorised and return records in the reference's extern layouts
+(ACCOUNT_DTYPE / TRANSFER_DTYPE). Ids are sequential (``--id-order=sequential``,
+src/testing/id.zig:29-31). Distributions follow src/tigerbeetle/benchmark_load.zig:941-1020:
+uniform account choice with the credit index bumped on collision, ``code = rand(u16) +| 1``,
+``amount = Exp(mean 10_000) +| 1``.
+"""
+import numpy as np
+
+from .types import ACCOUNT_DTYPE, TRANSFER_DTYPE, AccountFlags, TransferFlags
+
+U64 = np.uint64
+
+
+def _u128_col(a, name, lo, hi=None):
+    a[name][:, 0] = lo
+    a[name][:, 1] = 0 if hi is None else hi
+
+
+def accounts(n: int, seed: int = 42, id_offset: int = 0, ledger=2, code: int = 1,
+             flags=None) -> np.ndarray:
+    """`n` accounts with ids id_offset+1 .. id_offset+n (benchmark_load.zig:941-963)."""
+    rng = np.random.default_rng(seed)
+    a = np.zeros(n, dtype=ACCOUNT_DTYPE)
+    _u128_col(a, "id", np.arange(id_offset + 1, id_offset + n + 1, dtype=U64))
+    a["user_data_128"] = rng.integers(0, 2**63, size=(n, 2), dtype=np.int64).astype(U64)
+    a["user_data_64"] = rng.integers(0, 2**63, size=n, dtype=np.int64).astype(U64)
+    a["user_data_32"] = rng.integers(0, 2**32, size=n, dtype=np.int64).astype(np.uint32)
+    a["ledger"] = ledger
+    a["code"] = code
+    a["flags"] = int(AccountFlags.history) if flags is None else flags
+    return a
+
+
+def _codes(rng, n):
+    r = rng.integers(0, 2**16, size=n, dtype=np.int64)
+    return np.minimum(r + 1, 0xFFFF).astype(np.uint16)  # rand(u16) +| 1
+
+
+def _amounts(rng, n, mean=10_000):
+    e = np.floor(rng.exponential(mean, size=n)).astype(np.int64)
+    return (e + 1).astype(U64)  # Exp(mean) +| 1
+
+
+def transfers_uniform(n: int, n_accounts: int, seed: int = 42, id_offset: int = 0,
+                      account_id_offset: int = 0, ledger: int = 2) -> np.ndarray:
+    """Config 1/2: uniform debit/credit over the accounts, no pending (benchmark_load.zig:965)."""
+    rng = np.random.default_rng(seed)
+    t = np.zeros(n, dtype=TRANSFER_DTYPE)
+    _u128_col(t, "id", np.arange(id_offset + 1, id_offset + n + 1, dtype=U64))
+    dr = rng.integers(0, n_accounts, size=n, dtype=np.int64)
+    cr = rng.integers(0, n_accounts, size=n, dtype=np.int64)
+    cr = np.where(cr == dr, (cr + 1) % n_accounts, cr)
+    _u128_col(t, "debit_account_id", (dr + 1 + account_id_offset).astype(U64))
+    _u128_col(t, "credit_account_id", (cr + 1 + account_id_offset).astype(U64))
+    t["user_data_128"] = rng.integers(0, 2**63, size=(n, 2), dtype=np.int64).astype(U64)
+    t["user_data_64"] = rng.integers(0, 2**63, size=n, dtype=np.int64).astype(U64)
+    t["user_data_32"] = rng.integers(0, 2**32, size=n, dtype=np.int64).astype(np.uint32)
+    t["ledger"] = ledger
+    t["code"] = _codes(rng, n)
+    _u128_col(t, "amount", _amounts(rng, n))
+    return t
+
+
+def zipf_indices(rng, n_items: int, theta: float, size: int) -> np.ndarray:
+    """Zipfian ranks in [0, n_items) with P(i) ~ 1/(i+1)^theta."""
+    w = 1.0 / np.power(np.arange(1, n_items + 1, dtype=np.float64), theta)
+    cdf = np.cumsum(w)
+    cdf /= cdf[-1]
+    return np.searchsorted(cdf, rng.random(size), side="right").clip(0, n_items - 1)
+
+
+def hot_limits_setup(n_accounts: int = 10_000, n_hot: int = 100, seed: int = 42,
+                     funding: int = 2_000_000):
+    """Config 3 accounts + funding transfers.
+
+    Account 1 is an unlimited source; accounts 2..n_hot+1 are `hot` with
+    debits_must_not_exceed_credits; the rest are cold. The funding transfers credit every hot
+    account `funding` units from the source so that a fraction of hot debits later exceeds
+    credits.
+    """
+    a = accounts(n_accounts, seed=seed)
+    a["flags"][1:n_hot + 1] |= int(AccountFlags.debits_must_not_exceed_credits)
+    f = np.zeros(n_hot, dtype=TRANSFER_DTYPE)
+    return a, f, funding
+
+
+def transfers_hot_limits(n: int, n_accounts: int = 10_000, n_hot: int = 100, seed: int = 42,
+                         id_offset: int = 0, theta: float = 0.99, hot_debit_ratio: float = 0.9,
+                         hot_credit_ratio: float = 0.1, amount_mean: int = 10_000) -> np.ndarray:
+    """Config 3: 90% of debits from Zipf-chosen hot (limited) accounts, ~10% of credits to hot."""
+    rng = np.random.default_rng(seed)
+    t = transfers_uniform(n, n_accounts, seed=seed + 1, id_offset=id_offset)
+    cold_lo, cold_n = n_hot + 1, n_accounts - n_hot - 1  # cold indices [n_hot+1, n_accounts)
+    hot = rng.random(n) < hot_debit_ratio
+    dr = np.where(hot, 1 + zipf_indices(rng, n_hot, theta, n),
+                  cold_lo + rng.integers(0, cold_n, size=n))
+    to_hot = rng.random(n) < hot_credit_ratio
+    cr = np.where(to_hot, 1 + rng.integers(0, n_hot, size=n),
+                  cold_lo + rng.integers(0, cold_n, size=n))
+    cr = np.where(cr == dr, np.where(cr + 1 < n_accounts, cr + 1, cold_lo), cr)
+    _u128_col(t, "debit_account_id", (dr + 1).astype(U64))
+    _u128_col(t, "credit_account_id", (cr + 1).astype(U64))
+    _u128_col(t, "amount", _amounts(rng, n, amount_mean))
+    return t
+
+
+def funding_transfers(n_hot: int, amount: int, id_offset: int, source_index: int = 0):
+    """One transfer per hot account from the unlimited source (account index 0 -> id 1)."""
+    t = np.zeros(n_hot, dtype=TRANSFER_DTYPE)
+    _u128_col(t, "id", np.arange(id_offset + 1, id_offset + n_hot + 1, dtype=U64))
+    _u128_col(t, "debit_account_id", np.full(n_hot, source_index + 1, dtype=U64))
+    _u128_col(t, "credit_account_id", np.arange(2, n_hot + 2, dtype=U64))
+    _u128_col(t, "amount", np.full(n_hot, amount, dtype=U64))
+    t["ledger"] = 2
+    t["code"] = 1
+    return t
+
+
+def transfers_two_phase(n: int, n_accounts: int, seed: int, id_offset: int,
+                        prior_pending_ids: np.ndarray, pending_ratio=0.3, chain_ratio=0.3,
+                        chain_len=8, fail_ratio=0.1, resubmit_ratio=0.01,
+                        prior_ids: np.ndarray = None) -> np.ndarray:
+    """Config 4: pending with timeouts, post/void of earlier pending transfers, linked chains
+    with injected failures, and resubmitted ids."""
+    rng = np.random.default_rng(seed)
+    t = transfers_uniform(n, n_accounts, seed=seed, id_offset=id_offset)
+    kind = rng.random(n)
+    pend = kind < pending_ratio
+    t["flags"][pend] |= int(TransferFlags.pending)
+    t["timeout"][pend] = rng.integers(1, 6, size=int(pend.sum()), dtype=np.int64)
+    if prior_pending_ids is not None and len(prior_pending_ids):
+        resolve = (~pend) & (kind < pending_ratio + 0.3)
+        idx = np.nonzero(resolve)[0]
+        pick = prior_pending_ids[rng.integers(0, len(prior_pending_ids), size=len(idx))]
+        post = rng.random(len(idx)) < 0.67
+        t["flags"][idx] = np.where(post, int(TransferFlags.post_pending_transfer),
+                                   int(TransferFlags.void_pending_transfer)).astype(np.uint16)
+        t["pending_id"][idx, 0] = pick
+        t["pending_id"][idx, 1] = 0
+        # Post: amount maxInt half the time (post the full pending amount), else <= pending.
+        full = rng.random(len(idx)) < 0.5
+        amt = t["amount"][idx, 0]
+        t["amount"][idx, 0] = np.where(post & full, np.uint64(2**64 - 1),
+                                       np.where(post, amt // 4, 0))
+        t["amount"][idx, 1] = np.where(post & full, np.uint64(2**64 - 1), 0)
+        t["debit_account_id"][idx] = 0
+        t["credit_account_id"][idx] = 0
+        t["ledger"][idx] = 0
+        t["code"][idx] = 0
+        t["timeout"][idx] = 0
+    # Linked chains of `chain_len` events.
+    n_chains = int(n * chain_ratio / chain_len)
+    starts = rng.choice(max(n - chain_len, 1), size=n_chains, replace=False) if n > chain_len else []
+    for s in sorted(starts):
+        t["flags"][s:s + chain_len - 1] |= int(TransferFlags.linked)
+        t["flags"][s + chain_len - 1] &= ~np.uint16(int(TransferFlags.linked))
+        if rng.random() < fail_ratio:
+            j = s + int(rng.integers(0, chain_len))
+            t["debit_account_id"][j, 0] = n_accounts + 1000  # missing account
+    # Resubmitted ids.
+    if prior_ids is not None and len(prior_ids):
+        m = int(n * resubmit_ratio)
+        idx = rng.choice(n, size=m, replace=False)
+        t["id"][idx, 0] = prior_ids[rng.integers(0, len(prior_ids), size=m)]
+    return t
+
+
+def fuzz_accounts(rng, n: int, id_space: int) -> np.ndarray:
+    """Edge-biased create_accounts events (valid and invalid mixed)."""
+    a = accounts(n, seed=int(rng.integers(0, 2**31)))
+    a["id"][:, 0] = rng.integers(1, id_space + 1, size=n).astype(U64)
+    a["ledger"] = rng.choice([1, 1, 1, 2, 0], size=n)
+    a["code"] = rng.choice([1, 1, 1, 2, 0], size=n)
+    fl = np.zeros(n, dtype=np.int64)
+    for bit, p in ((0, 0.15), (1, 0.25), (2, 0.15), (3, 0.3), (5, 0.05)):
+        fl |= (rng.random(n) < p).astype(np.int64) << bit
+    a["flags"] = fl.astype(np.uint16)
+    a["reserved"] = (rng.random(n) < 0.02).astype(np.uint32)
+    a["timestamp"] = (rng.random(n) < 0.02).astype(U64)
+    a["debits_posted"][:, 0] = (rng.random(n) < 0.02).astype(U64)
+    a["id"][rng.random(n) < 0.01] = 0
+    return a
+
+
+def fuzz_transfers(rng, n: int, id_space: int, n_accounts: int, pending_ids=None) -> np.ndarray:
+    """Edge-biased create_transfers events covering every status path."""
+    t = transfers_uniform(n, n_accounts, seed=int(rng.integers(0, 2**31)))
+    t["ledger"] = rng.choice([1, 1, 1, 1, 2, 0], size=n)
+    t["id"][:, 0] = rng.integers(1, id_space + 1, size=n).astype(U64)
+    dr = rng.integers(1, n_accounts + 3, size=n)
+    cr = rng.integers(1, n_accounts + 3, size=n)
+    t["debit_account_id"][:, 0] = dr.astype(U64)
+    t["credit_account_id"][:, 0] = cr.astype(U64)
+    small = rng.random(n) < 0.5
+    t["amount"][:, 0] = np.where(small, rng.integers(0, 50, size=n), t["amount"][:, 0]).astype(U64)
+    big = rng.random(n) < 0.03
+    t["amount"][big, 0] = np.uint64(2**64 - 1)
+    t["amount"][big, 1] = np.uint64(2**64 - 1)
+    fl = np.zeros(n, dtype=np.int64)
+    for bit, p in ((0, 0.2), (1, 0.3), (2, 0.12), (3, 0.08), (4, 0.08), (5, 0.08), (6, 0.03),
+                   (7, 0.03)):
+        fl |= (rng.random(n) < p).astype(np.int64) << bit
+    fl |= (rng.random(n) < 0.01).astype(np.int64) << 10  # padding
+    t["flags"] = fl.astype(np.uint16)
+    pend = (fl & int(TransferFlags.pending)) != 0
+    t["timeout"] = np.where(pend & (rng.random(n) < 0.5), rng.integers(1, 4, size=n), 0)
+    t["timeout"][rng.random(n) < 0.02] = 7
+    pv = (fl & (int(TransferFlags.post_pending_transfer) |
+                int(TransferFlags.void_pending_transfer))) != 0
+    if pending_ids is not None and len(pending_ids):
+        pick = pending_ids[rng.integers(0, len(pending_ids), size=n)]
+        t["pending_id"][:, 0] = np.where(pv, pick, 0).astype(U64)
+    else:
+        t["pending_id"][:, 0] = np.where(pv, rng.integers(1, id_space + 1, size=n), 0).astype(U64)
+    zero_acc = pv & (rng.random(n) < 0.7)
+    t["debit_account_id"][zero_acc] = 0
+    t["credit_account_id"][zero_acc] = 0
+    t["ledger"][zero_acc & (rng.random(n) < 0.7)] = 0
+    t["code"][pv & (rng.random(n) < 0.5)] = 0
+    t["code"][rng.random(n) < 0.01] = 0
+    t["timestamp"] = (rng.random(n) < 0.01).astype(U64)
+    t["id"][rng.random(n) < 0.005] = 0
+    return t
