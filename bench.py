@@ -41,11 +41,15 @@ BATCH = 8189           # Operation.create_transfers.event_max (src/tigerbeetle.z
 # Algorithmic bytes per event of each kernel of the create_transfers path: the
 # fields the kernel must read or write for its function, counted once.
 KERNEL_BYTES_PER_EVENT = {
-    "tr_prepare": 50 + 16 + 28,      # id/dr/cr/flags, id-slot claim, per-event scratch
-    "tr_mark": 2 + 16 + 8,
-    "tr_classify": 128 + 8 + 28 + 2,
-    "tr_fast": 128 + 20 + 128 + 1 + 16,
-    "tr_finalize": 8 + 8 + 16 + 1,
+    # event 128 R, id-key claim 16, transfer row 128 W, result 16 W, per-event record 21 W
+    "tr_ingest": 128 + 16 + 128 + 16 + 21,
+    # record 21 R + result timestamp 8 R, liveness 1 W, 2 balance items 24 W (the id-slot
+    # re-check reads only when ingest saw a duplicate id)
+    "tr_commit": 21 + 8 + 1 + 24,
+    # 2 items x (4 B key + 8 B amount), read and written once
+    "bal_sort": 2 * 12 * 2,
+    # sorted items read once (account rows are per distinct account)
+    "bal_reduce": 2 * 12,
 }
 
 

@@ -53,8 +53,14 @@ __host__ __device__ inline uint64_t mix64(uint64_t h) {
     h ^= h >> 33;
     return h;
 }
+// Home slot of an id. Ids that differ only in their 3 low bits share one 8-slot (64-byte) group:
+// sequential ids (the reference's --id-order=sequential, and TigerBeetle's recommended
+// time-based ids within a millisecond) land in consecutive slots, so a wave's claims hit 8 cache
+// lines instead of 64. Everything above the low 3 bits is fully mixed, so random ids still spread
+// uniformly over the table.
 __host__ __device__ inline uint64_t hash_id(const tb_uint128_t& id) {
-    return mix64(id.lo ^ mix64(id.hi + 0x9E3779B97F4A7C15ull));
+    const uint64_t group = mix64((id.lo >> 3) ^ mix64(id.hi + 0x9E3779B97F4A7C15ull));
+    return (group << 3) | (id.lo & 7);
 }
 
 // Non-temporal / plain 16-byte vector copies of 128-byte rows.
@@ -118,9 +124,11 @@ __device__ inline uint64_t probe_find(const IdTable& t, const tb_uint128_t& id, 
 
 // Claim-or-find: inserts an in-flight claim `ref` for `id` unless `id` is already present.
 // Returns the slot of `id`. Duplicates within the call keep the smallest ref (earliest event).
+// `*dup` is set when another in-flight claim of the same id is found: of two same-id events, the
+// one probing second always sees the other's claim, so a call with no `dup` has unique ids.
 template <typename RowId>
 __device__ inline uint64_t probe_claim(const IdTable& t, const tb_uint128_t& id, uint64_t ref,
-                                       uint64_t row_base, RowId row_id) {
+                                       uint64_t row_base, RowId row_id, bool* dup) {
     uint64_t s = hash_id(id) & t.mask;
     for (uint64_t n = 0; n <= t.mask; n++) {
         uint64_t w = t.slots[s];
@@ -131,7 +139,10 @@ __device__ inline uint64_t probe_claim(const IdTable& t, const tb_uint128_t& id,
         if (w != kTomb) {
             uint64_t r = (w & kRefMask) - 1;
             if (u128_eq(row_id(r), id)) {
-                if (r >= row_base && ref < w) atomicMin(&t.slots[s], (unsigned long long)ref);
+                if (r >= row_base) {
+                    *dup = true;
+                    if (ref < w) atomicMin(&t.slots[s], (unsigned long long)ref);
+                }
                 return s;
             }
         }

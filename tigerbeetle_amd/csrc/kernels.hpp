@@ -1,0 +1,902 @@
+// Device kernels of the executor (host orchestration in executor.hip).
+//
+// create_transfers, per call of N events:
+//
+//   tr_ingest    one lane per event, one read of the 128-byte event: the reference's checks in
+//                their order (state_machine.zig:3029-3104, :3719-3873) up to the first check that
+//                depends on in-call state; claim of the event's id in the transfer id table
+//                (earliest duplicate wins); debit/credit account rows; `closable` marks (closing
+//                transfers, voids). Outcome per event: DONE (result fixed), FAST (commits in
+//                parallel: the transfer row and result are written here), SLOW (ordered replay,
+//                marks its accounts `hot`).
+//   tr_commit    one lane per event: re-validates what ingest could only know provisionally
+//                (still the earliest holder of its id, no hot/closable account, no post/void in
+//                the call for pending-with-timeout) and commits FAST events (status, liveness,
+//                expires_at entry, pulse_next_timestamp, balance deltas) or demotes them to SLOW;
+//                finalises the id slots of DONE events (orphan / tombstone).
+//   balances     FAST balance deltas as (account field, amount) items, radix-sorted by field
+//                (hipcub) and reduced per run into u128 sums (bal_reduce_tiles); small calls use
+//                u128 atomics in tr_commit instead.
+//   replay       the SLOW events in serial order on one lane (replay.hpp), then their id slots.
+//
+// Exactness argument: DESIGN.md §4.
+#pragma once
+
+#include "device_common.hpp"
+#include "replay.hpp"
+
+namespace tbg {
+
+constexpr int kBlock = 256;
+
+__device__ inline void count_stat(DevScalars* s, int which, bool pred) {
+    unsigned long long mask = __ballot(pred);
+    if ((threadIdx.x & 63) == 0 && mask)
+        atomicAdd(&s->stats[which], (unsigned long long)__popcll(mask));
+}
+
+__device__ inline void set_flag_any(DevScalars* s, bool pred, unsigned int flag) {
+    if (__any(pred) && (threadIdx.x & 63) == 0) atomicOr(&s->flags, flag);
+}
+
+// Block-wide reduction (kBlock threads, every thread participates); the result is returned to
+// every thread. Keeps call-wide counters at one atomic per block: same-address atomics from every
+// wave serialise at the memory side and cost milliseconds at 10^7 events.
+struct OpAdd {
+    template <typename V>
+    __device__ V operator()(V a, V b) const { return a + b; }
+};
+struct OpMax {
+    template <typename V>
+    __device__ V operator()(V a, V b) const { return a > b ? a : b; }
+};
+struct OpOr {
+    template <typename V>
+    __device__ V operator()(V a, V b) const { return a | b; }
+};
+
+template <typename V, typename Op>
+__device__ inline V block_reduce(V v, Op op) {
+    __shared__ V lds[kBlock / 64];
+    for (int off = 32; off > 0; off >>= 1) v = op(v, __shfl_xor(v, off));
+    if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = v;
+    __syncthreads();
+    V r = lds[0];
+#pragma unroll
+    for (int i = 1; i < kBlock / 64; i++) r = op(r, lds[i]);
+    __syncthreads();
+    return r;
+}
+
+// Grid-stride kernels run at most this many blocks (16 per CU on 256 CUs).
+constexpr uint32_t kMaxGrid = 4096;
+
+template <typename Event>
+__device__ inline uint64_t ts_event_of(const Call<Event>& c, uint32_t b, uint32_t k) {
+    return c.batch_ts[b] - c.batch_ends[b] + k + 1;
+}
+
+template <typename Event>
+__device__ inline uint32_t batch_start_of(const Call<Event>& c, uint32_t b) {
+    return b == 0 ? 0 : c.batch_ends[b - 1];
+}
+
+__device__ inline uint32_t row32(uint64_t r) { return r == kNone ? kNone32 : uint32_t(r); }
+
+// ================================ create_transfers ==========================================
+
+// The checks after the id lookup (create_transfer, :3727-3873), on the ingest snapshot.
+__device__ inline uint8_t classify_after_lookup(const Tables& T, const Call<tb_transfer_t>& c,
+                                                uint32_t k, uint64_t ts_event,
+                                                const tb_transfer_t& t, uint64_t slot,
+                                                uint32_t dr_row, uint32_t cr_row,
+                                                uint32_t* status, uint64_t* ts_out,
+                                                uint8_t* info) {
+    const uint16_t f = t.flags;
+    const uint64_t w = T.tr.slots[slot];
+    const uint64_t r = (w & kRefMask) - 1;
+    if (r < c.row_base) {  // a committed id: the result is final for every event of the call
+        if (w & kOrphanBit) {
+            *status = TB_CT_ID_ALREADY_FAILED;
+            return kClassDone;
+        }
+        const tb_transfer_t& e = T.tr_rows[r];  // committed rows are immutable
+        const tb_transfer_t* p = nullptr;
+        if (t.flags == e.flags && U(t.pending_id) == U(e.pending_id) && t.timeout == e.timeout &&
+            (t.flags & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING))) {
+            const uint64_t ps = transfer_slot_find(T, c, t.pending_id);
+            if (ps == kNone) return kClassSlow;
+            const uint64_t pw = T.tr.slots[ps];
+            const uint64_t pr = (pw & kRefMask) - 1;
+            if (pr >= c.row_base || (pw & kOrphanBit)) return kClassSlow;
+            p = &T.tr_rows[pr];
+        }
+        *status = create_transfer_exists(t, e, p, ts_out);
+        return kClassDone;
+    }
+    if (w != c.row_base + k + 1) return kClassSlow;  // a later duplicate of an in-call id
+    // Provisionally the first occurrence: every DONE below is valid only if that holds.
+    *info |= kInfoPostLookup;
+    if (f & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) return kClassSlow;
+    uint32_t st = 0;
+    if (u128_is_zero(t.debit_account_id)) st = TB_CT_DEBIT_ACCOUNT_ID_MUST_NOT_BE_ZERO;
+    else if (u128_is_max(t.debit_account_id)) st = TB_CT_DEBIT_ACCOUNT_ID_MUST_NOT_BE_INT_MAX;
+    else if (u128_is_zero(t.credit_account_id)) st = TB_CT_CREDIT_ACCOUNT_ID_MUST_NOT_BE_ZERO;
+    else if (u128_is_max(t.credit_account_id)) st = TB_CT_CREDIT_ACCOUNT_ID_MUST_NOT_BE_INT_MAX;
+    else if (u128_eq(t.credit_account_id, t.debit_account_id)) st = TB_CT_ACCOUNTS_MUST_BE_DIFFERENT;
+    else if (!u128_is_zero(t.pending_id)) st = TB_CT_PENDING_ID_MUST_BE_ZERO;
+    else if (!(f & TB_TRANSFER_PENDING) && t.timeout != 0)
+        st = TB_CT_TIMEOUT_RESERVED_FOR_PENDING_TRANSFER;
+    else if (!(f & TB_TRANSFER_PENDING) &&
+             (f & (TB_TRANSFER_CLOSING_DEBIT | TB_TRANSFER_CLOSING_CREDIT)))
+        st = TB_CT_CLOSING_TRANSFER_MUST_BE_PENDING;
+    else if (t.ledger == 0) st = TB_CT_LEDGER_MUST_NOT_BE_ZERO;
+    else if (t.code == 0) st = TB_CT_CODE_MUST_NOT_BE_ZERO;
+    else if (dr_row == kNone32) st = TB_CT_DEBIT_ACCOUNT_NOT_FOUND;
+    else if (cr_row == kNone32) st = TB_CT_CREDIT_ACCOUNT_NOT_FOUND;
+    if (st) {
+        *status = st;
+        return kClassDone;
+    }
+    const tb_account_t* dr = &T.acc_rows[dr_row];
+    const tb_account_t* cr = &T.acc_rows[cr_row];
+    const uint32_t dr_ledger = dr->ledger, cr_ledger = cr->ledger;
+    if (dr_ledger != cr_ledger) {
+        *status = TB_CT_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;
+        return kClassDone;
+    }
+    if (t.ledger != dr_ledger) {
+        *status = TB_CT_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
+        return kClassDone;
+    }
+    if (T.acc_closable[dr_row] == c.epoch || T.acc_closable[cr_row] == c.epoch) return kClassSlow;
+    const uint16_t dr_flags = dr->flags, cr_flags = cr->flags;
+    if (dr_flags & TB_ACCOUNT_CLOSED) {
+        *status = TB_CT_DEBIT_ACCOUNT_ALREADY_CLOSED;
+        *info |= kInfoClosedDep;
+        return kClassDone;
+    }
+    if (cr_flags & TB_ACCOUNT_CLOSED) {
+        *status = TB_CT_CREDIT_ACCOUNT_ALREADY_CLOSED;
+        *info |= kInfoClosedDep;
+        return kClassDone;
+    }
+    if (f & (TB_TRANSFER_BALANCING_DEBIT | TB_TRANSFER_BALANCING_CREDIT |
+             TB_TRANSFER_CLOSING_DEBIT | TB_TRANSFER_CLOSING_CREDIT))
+        return kClassSlow;
+    // Overflow is impossible when every balance is < 2^126 and every amount < 2^64.
+    constexpr uint64_t kHiLimit = 1ull << 62;
+    if (t.amount.hi != 0 || dr->debits_pending.hi >= kHiLimit ||
+        dr->debits_posted.hi >= kHiLimit || cr->credits_pending.hi >= kHiLimit ||
+        cr->credits_posted.hi >= kHiLimit)
+        return kClassSlow;
+    if (ts_event + (uint64_t)t.timeout * TB_NS_PER_S > TB_TIMESTAMP_MAX) {
+        *status = TB_CT_OVERFLOWS_TIMEOUT;
+        return kClassDone;
+    }
+    if (dr_flags & TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS) return kClassSlow;
+    if (cr_flags & TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS) return kClassSlow;
+    if (f & TB_TRANSFER_PENDING) *info |= kInfoPending;
+    if (t.timeout > 0) *info |= kInfoTimeout;
+    return kClassFast;
+}
+
+// One event of tr_ingest; returns the call flags it raises (kFlagImported / kFlagPostVoid).
+__device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_transfer_t>& c,
+                                            uint32_t k) {
+    bool imported = false, post_void = false, dup = false, closable = false, hot = false;
+    {
+        // One 128-byte vector load of the event; every field below comes from registers.
+        tb_transfer_t t;
+        {
+            const uint4* src = reinterpret_cast<const uint4*>(&c.events[k]);
+            uint4* dst = reinterpret_cast<uint4*>(&t);
+#pragma unroll
+            for (int i = 0; i < 8; i++) dst[i] = src[i];
+        }
+        const uint16_t f = t.flags;
+        imported = (f & TB_TRANSFER_IMPORTED) != 0;
+        post_void = (f & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) != 0;
+        const uint32_t b = batch_of_guess(c.batch_ends, c.n_batches, c.n, k);
+        const uint32_t bstart = batch_start_of(c, b);
+        const uint64_t ts_event = ts_event_of(c, b, k);
+        // The row store takes the event as it is, stamped (rows of events that do not create
+        // an object stay dead); streaming the copy first keeps the event out of registers.
+        {
+            tb_transfer_t o = t;
+            o.timestamp = ts_event;
+            const uint4* src = reinterpret_cast<const uint4*>(&o);
+            uint4* dst = reinterpret_cast<uint4*>(&T.tr_rows[c.row_base + k]);
+#pragma unroll
+            for (int i = 0; i < 8; i++) dst[i] = src[i];
+        }
+        const bool chain = (f & TB_TRANSFER_LINKED) ||
+                           (k > bstart && (c.events[k - 1].flags & TB_TRANSFER_LINKED));
+        const bool valid_id = !u128_is_zero(t.id) && !u128_is_max(t.id);
+
+        uint32_t status = 0;
+        uint64_t ts_out = ts_event;
+        uint8_t info = 0, cls = kClassSlow;
+        bool pre_done = false;
+        if (!chain && !c.force_replay) {
+            // execute_create's per-event checks before create_transfer (:3052-3081) and the
+            // checks before the id lookup (:3729-3733): independent of every table.
+            const bool batch_imported = (c.events[bstart].flags & TB_TRANSFER_IMPORTED) != 0;
+            if (batch_imported != imported) {
+                status = imported ? TB_CT_IMPORTED_EVENT_NOT_EXPECTED : TB_CT_IMPORTED_EVENT_EXPECTED;
+                pre_done = true;
+            } else if (!imported && t.timestamp != 0) {
+                status = TB_CT_TIMESTAMP_MUST_BE_ZERO;
+                pre_done = true;
+            } else if (!imported && (f & TB_TRANSFER_PADDING_MASK)) {
+                status = TB_CT_RESERVED_FLAG;
+                pre_done = true;
+            } else if (!imported && !valid_id) {
+                status = u128_is_zero(t.id) ? TB_CT_ID_MUST_NOT_BE_ZERO : TB_CT_ID_MUST_NOT_BE_INT_MAX;
+                pre_done = true;
+            }
+        }
+        uint64_t slot = kNone;
+        uint32_t dr_row = kNone32, cr_row = kNone32;
+        if (pre_done) {
+            cls = kClassDone;
+        } else {
+            const tb_transfer_t* ev = c.events;
+            const tb_transfer_t* rows = T.tr_rows;
+            const uint64_t base = c.row_base;
+            if (valid_id) {
+                slot = probe_claim(T.tr, t.id, base + k + 1, base, [=](uint64_t r) {
+                    return r >= base ? ev[r - base].id : rows[r].id;
+                }, &dup);
+                if (slot == kNone) atomicOr(&T.scalars->flags, kFlagTableFull);
+                else info |= kInfoClaimed;
+            }
+            if (!u128_is_zero(t.debit_account_id) && !u128_is_max(t.debit_account_id))
+                dr_row = row32(account_find(T, t.debit_account_id));
+            if (!u128_is_zero(t.credit_account_id) && !u128_is_max(t.credit_account_id))
+                cr_row = row32(account_find(T, t.credit_account_id));
+            // Accounts whose `closed` flag an event of this call may change.
+            if ((f & TB_TRANSFER_CLOSING_DEBIT) && dr_row != kNone32) {
+                T.acc_closable[dr_row] = c.epoch;
+                closable = true;
+            }
+            if ((f & TB_TRANSFER_CLOSING_CREDIT) && cr_row != kNone32) {
+                T.acc_closable[cr_row] = c.epoch;
+                closable = true;
+            }
+            if ((f & TB_TRANSFER_VOID_PENDING) && !u128_is_zero(t.pending_id) &&
+                !u128_is_max(t.pending_id)) {
+                const uint64_t ps = transfer_slot_find(T, c, t.pending_id);
+                if (ps != kNone) {
+                    const uint64_t pr = (T.tr.slots[ps] & kRefMask) - 1;
+                    const tb_transfer_t& p = pr >= base ? ev[pr - base] : rows[pr];
+                    const uint64_t pd = account_find(T, p.debit_account_id);
+                    const uint64_t pc = account_find(T, p.credit_account_id);
+                    if (pd != kNone) T.acc_closable[pd] = c.epoch;
+                    if (pc != kNone) T.acc_closable[pc] = c.epoch;
+                    closable = true;
+                }
+            }
+            if (!chain && !c.force_replay && !imported && slot != kNone) {
+                cls = classify_after_lookup(T, c, k, ts_event, t, slot, dr_row, cr_row, &status,
+                                            &ts_out, &info);
+            }
+        }
+        info |= cls;
+        c.ev_info[k] = info;
+        c.ev_slot[k] = slot == kNone ? kNone32 : uint32_t(slot);
+        c.ev_dr[k] = dr_row;
+        c.ev_cr[k] = cr_row;
+        if (cls == kClassDone) {
+            tb_create_result_t res;
+            res.timestamp = status == TB_CT_EXISTS ? ts_out : ts_event;
+            res.status = status;
+            res.reserved = 0;
+            c.results[k] = res;
+        } else if (cls == kClassFast) {
+            // Speculative commit of the result (the row is already written); tr_commit confirms
+            // or demotes.
+            const uint64_t row = c.row_base + k;
+            T.tr_status[row] = (f & TB_TRANSFER_PENDING) ? TB_PENDING_PENDING : TB_PENDING_NONE;
+            c.ev_amount[k] = t.amount.lo;
+            tb_create_result_t res;
+            res.timestamp = ts_event;
+            res.status = TB_STATUS_CREATED;
+            res.reserved = 0;
+            c.results[k] = res;
+        } else {
+            // Accounts whose balances or flags an event executes on in order.
+            if (dr_row != kNone32) T.acc_hot[dr_row] = c.epoch;
+            if (cr_row != kNone32) T.acc_hot[cr_row] = c.epoch;
+            hot = dr_row != kNone32 || cr_row != kNone32;
+        }
+    }
+    return (imported ? kFlagImported : 0u) | (post_void ? kFlagPostVoid : 0u) |
+           (dup ? kFlagDuplicate : 0u) | (closable ? kFlagClosable : 0u) | (hot ? kFlagHot : 0u);
+}
+
+__global__ void tr_ingest(Tables T, Call<tb_transfer_t> c) {
+    unsigned int flags = 0;
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < c.n; k += gridDim.x * blockDim.x)
+        flags |= ingest_event(T, c, k);
+    flags = block_reduce(flags, OpOr());
+    if (threadIdx.x == 0 && flags) atomicOr(&T.scalars->flags, flags);
+}
+
+// Balance-delta item: key = account_row * 4 + field (0 dp, 1 dpo, 2 cp, 3 cpo).
+__device__ inline tb_uint128_t* account_field(tb_account_t* rows, uint32_t key) {
+    tb_account_t* a = &rows[key >> 2];
+    return reinterpret_cast<tb_uint128_t*>(reinterpret_cast<uint8_t*>(a) + 16 + 16 * (key & 3));
+}
+
+// One event of tr_commit: applied (committed FAST), done (final DONE), ts_applied (its timestamp).
+__device__ inline void commit_event(const Tables& T, const Call<tb_transfer_t>& c, uint32_t k,
+                                    unsigned int call_flags, uint32_t* keys, uint64_t* vals,
+                                    int use_sort, uint32_t sentinel, bool& applied, bool& done,
+                                    bool& slow_out, uint64_t& ts_applied) {
+    applied = false;
+    done = false;
+    slow_out = false;
+    ts_applied = 0;
+    {
+        const uint8_t info = c.ev_info[k];
+        const uint8_t cls = info & kInfoClassMask;
+        const uint64_t row = c.row_base + k;
+        const uint64_t ref = row + 1;
+        bool slow = cls == kClassSlow || (call_flags & kFlagImported);
+        if (!slow && cls == kClassFast) {
+            const uint32_t s = c.ev_slot[k];
+            const uint32_t dr = c.ev_dr[k], cr = c.ev_cr[k];
+            // Each re-check reads only when ingest raised the flag that can make it fail.
+            if (((call_flags & kFlagDuplicate) && T.tr.slots[s] != ref) ||
+                ((call_flags & kFlagClosable) &&
+                 (T.acc_closable[dr] == c.epoch || T.acc_closable[cr] == c.epoch)) ||
+                ((call_flags & kFlagHot) && (T.acc_hot[dr] == c.epoch || T.acc_hot[cr] == c.epoch)) ||
+                ((info & kInfoPending) && (info & kInfoTimeout) && (call_flags & kFlagPostVoid))) {
+                slow = true;
+            } else {
+                applied = true;
+                ts_applied = c.results[k].timestamp;
+                T.tr_live[row] = 1;
+                const bool pending = (info & kInfoPending) != 0;
+                const uint64_t amount = c.ev_amount[k];
+                if (use_sort) {
+                    keys[2 * uint64_t(k)] = dr * 4 + (pending ? 0 : 1);
+                    keys[2 * uint64_t(k) + 1] = cr * 4 + (pending ? 2 : 3);
+                    vals[2 * uint64_t(k)] = amount;
+                    vals[2 * uint64_t(k) + 1] = amount;
+                } else if (amount) {
+                    atomic_add_u128(account_field(T.acc_rows, dr * 4 + (pending ? 0 : 1)), amount);
+                    atomic_add_u128(account_field(T.acc_rows, cr * 4 + (pending ? 2 : 3)), amount);
+                }
+                if (pending && (info & kInfoTimeout)) {
+                    expiry_append(T, row, false);
+                    const uint64_t timeout = T.tr_rows[row].timeout;
+                    atomicMin(&T.scalars->pulse_next_timestamp,
+                              (unsigned long long)(ts_applied + timeout * TB_NS_PER_S));
+                }
+            }
+        } else if (!slow && cls == kClassDone) {
+            done = true;
+            if (info & kInfoPostLookup) {
+                const uint32_t s = c.ev_slot[k];
+                const uint32_t dr = c.ev_dr[k], cr = c.ev_cr[k];
+                if ((call_flags & kFlagDuplicate) && T.tr.slots[s] != ref) {
+                    slow = true;  // a later duplicate: its outcome follows the earlier event's
+                } else if ((info & kInfoClosedDep) && (call_flags & kFlagClosable) &&
+                           (T.acc_closable[dr] == c.epoch || T.acc_closable[cr] == c.epoch)) {
+                    slow = true;
+                } else {
+                    // transient_error (:3215-3252): the id stays taken (orphan); else released.
+                    if (tb_transfer_status_transient(c.results[k].status)) {
+                        T.tr_rows[row].id = c.events[k].id;
+                        T.tr.slots[s] = ref | kOrphanBit;
+                    } else {
+                        T.tr.slots[s] = kTomb;
+                    }
+                }
+            }
+            if (slow) done = false;
+            else T.tr_live[row] = 0;
+        }
+        if (!applied && use_sort) {
+            keys[2 * uint64_t(k)] = sentinel;
+            keys[2 * uint64_t(k) + 1] = sentinel;
+        }
+        c.ev_slow[k] = slow;
+        slow_out = slow;
+    }
+}
+
+__global__ void tr_commit(Tables T, Call<tb_transfer_t> c, uint32_t* keys, uint64_t* vals,
+                          int use_sort, uint32_t sentinel) {
+    const unsigned int call_flags = T.scalars->flags;
+    uint64_t n_applied = 0, n_done = 0, n_slow = 0, ts_max = 0;
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < c.n;
+         k += gridDim.x * blockDim.x) {
+        bool applied, done, slow;
+        uint64_t ts;
+        commit_event(T, c, k, call_flags, keys, vals, use_sort, sentinel, applied, done, slow, ts);
+        n_applied += applied;
+        n_done += done;
+        n_slow += slow;
+        ts_max = ts > ts_max ? ts : ts_max;
+    }
+    // transfers objects tree key_range (groove.zig:1780): the largest committed timestamp.
+    n_applied = block_reduce(n_applied, OpAdd());
+    n_done = block_reduce(n_done, OpAdd());
+    n_slow = block_reduce(n_slow, OpAdd());
+    ts_max = block_reduce(ts_max, OpMax());
+    if (threadIdx.x == 0) {
+        if (ts_max) atomicMax(&T.scalars->transfers_key_max, (unsigned long long)ts_max);
+        if (n_applied) atomicAdd(&T.scalars->stats[1], (unsigned long long)n_applied);
+        if (n_done) atomicAdd(&T.scalars->stats[3], (unsigned long long)n_done);
+        if (n_slow) atomicAdd(&T.scalars->stats[0], (unsigned long long)n_slow);
+    }
+}
+
+// Sorted balance items -> u128 sums added to the account fields, one tile of kReduceTile items
+// per block. Each lane reduces 16 consecutive items (vector loads); lane-edge runs are merged in
+// order through LDS by lane 0. A run that touches neither tile edge is owned by this block: plain
+// read-modify-write. The tile's first and last runs may continue in a neighbour tile: u128 atomics
+// (at most two per tile).
+constexpr uint32_t kReducePerLane = 16;
+constexpr uint32_t kReduceTile = kBlock * kReducePerLane;
+
+__device__ inline void add_field(tb_account_t* rows, uint32_t key, u128 sum, bool shared) {
+    if (sum == 0) return;
+    tb_uint128_t* field = account_field(rows, key);
+    if (shared) atomic_add_u128(field, sum);
+    else *field = W(U(*field) + sum);
+}
+
+__global__ void bal_reduce_tiles(tb_account_t* rows, const uint32_t* keys, const uint64_t* vals,
+                                 uint64_t n, uint32_t sentinel) {
+    __shared__ uint32_t first_key[kBlock], last_key[kBlock];
+    __shared__ uint64_t first_lo[kBlock], first_hi[kBlock], last_lo[kBlock], last_hi[kBlock];
+    __shared__ uint8_t single[kBlock];
+    const uint64_t tile = uint64_t(blockIdx.x) * kReduceTile;
+    const uint64_t begin = tile + uint64_t(threadIdx.x) * kReducePerLane;
+    const uint64_t tile_end = tile + kReduceTile < n ? tile + kReduceTile : n;
+    uint32_t fk = sentinel, lk = sentinel;
+    u128 fs = 0, ls = 0;
+    bool one = true;
+    if (begin < tile_end) {
+        const uint64_t end = begin + kReducePerLane < tile_end ? begin + kReducePerLane : tile_end;
+        uint32_t k_items[kReducePerLane];
+        uint64_t v_items[kReducePerLane];
+        if (end - begin == kReducePerLane) {
+            const uint4* kp = reinterpret_cast<const uint4*>(keys + begin);
+            const uint4* vp = reinterpret_cast<const uint4*>(vals + begin);
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                uint4 q = kp[i];
+                k_items[4 * i] = q.x; k_items[4 * i + 1] = q.y;
+                k_items[4 * i + 2] = q.z; k_items[4 * i + 3] = q.w;
+            }
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                uint4 q = vp[i];
+                v_items[2 * i] = (uint64_t(q.y) << 32) | q.x;
+                v_items[2 * i + 1] = (uint64_t(q.w) << 32) | q.z;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < (int)kReducePerLane; i++) {
+                k_items[i] = begin + i < end ? keys[begin + i] : sentinel;
+                v_items[i] = begin + i < end ? vals[begin + i] : 0;
+            }
+        }
+        uint32_t cur = k_items[0];
+        u128 sum = 0;
+        bool first_run = true;
+#pragma unroll
+        for (int i = 0; i < (int)kReducePerLane; i++) {
+            if (k_items[i] != cur) {
+                if (first_run) {
+                    fk = cur;
+                    fs = sum;
+                    first_run = false;
+                    one = false;
+                } else if (cur < sentinel) {
+                    add_field(rows, cur, sum, false);  // interior run of this lane: owned
+                }
+                cur = k_items[i];
+                sum = 0;
+            }
+            sum += v_items[i];
+        }
+        if (first_run) {
+            fk = cur;
+            fs = sum;
+        }
+        lk = cur;
+        ls = sum;
+    }
+    first_key[threadIdx.x] = fk;
+    last_key[threadIdx.x] = lk;
+    first_lo[threadIdx.x] = uint64_t(fs);
+    first_hi[threadIdx.x] = uint64_t(fs >> 64);
+    last_lo[threadIdx.x] = uint64_t(ls);
+    last_hi[threadIdx.x] = uint64_t(ls >> 64);
+    single[threadIdx.x] = one;
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    // Merge lane-edge runs in order. `open` is the run being accumulated; `shared` marks a run
+    // that touches the tile's first item (it may continue from the previous tile).
+    uint32_t open = first_key[0];
+    u128 acc = 0;
+    bool open_shared = true;
+    for (uint32_t t = 0; t < kBlock; t++) {
+        const uint32_t f = first_key[t];
+        const u128 fsum = ((u128)first_hi[t] << 64) | first_lo[t];
+        if (f != open) {
+            if (open < sentinel) add_field(rows, open, acc, open_shared);
+            open = f;
+            acc = 0;
+            open_shared = false;
+        }
+        acc += fsum;
+        if (!single[t]) {
+            // The lane's first run ends inside the lane; its last run opens.
+            if (open < sentinel) add_field(rows, open, acc, open_shared);
+            open = last_key[t];
+            acc = ((u128)last_hi[t] << 64) | last_lo[t];
+            open_shared = false;
+        }
+    }
+    // The tile's last run may continue into the next tile.
+    if (open < sentinel) add_field(rows, open, acc, true);
+}
+
+// ================================ the ordered replay ========================================
+
+template <typename Event>
+__device__ inline void replay_chain_step(Replay& R, const Call<Event>& c, uint32_t k,
+                                         bool is_transfers, bool& chain_open,
+                                         uint32_t& chain_start, bool& chain_broken) {
+    const Tables& T = R.T;
+    const Event ev = c.events[k];
+    const uint32_t b = batch_of(c.batch_ends, c.n_batches, k);
+    const uint32_t bstart = batch_start_of(c, b);
+    const uint32_t bend = c.batch_ends[b];
+    const uint64_t ts_event = ts_event_of(c, b, k);
+    const uint16_t linked_flag = is_transfers ? TB_TRANSFER_LINKED : TB_ACCOUNT_LINKED;
+    const uint16_t imported_flag = is_transfers ? TB_TRANSFER_IMPORTED : TB_ACCOUNT_IMPORTED;
+    const uint16_t f = ev.flags;
+    uint32_t status = 0;
+    uint64_t ts_actual = ts_event;
+
+    do {  // execute_create's loop body (:3030-3105)
+        if (f & linked_flag) {
+            if (!chain_open) {
+                chain_open = true;
+                chain_start = k;
+                chain_broken = false;
+                R.scope_open();
+            }
+            if (k == bend - 1) {
+                status = TB_CT_LINKED_EVENT_CHAIN_OPEN;
+                break;
+            }
+        }
+        if (chain_broken) {
+            status = TB_CT_LINKED_EVENT_FAILED;
+            break;
+        }
+        const bool batch_imported = (c.events[bstart].flags & imported_flag) != 0;
+        const bool imported = (f & imported_flag) != 0;
+        if (batch_imported != imported) {
+            if (is_transfers)
+                status = imported ? TB_CT_IMPORTED_EVENT_NOT_EXPECTED : TB_CT_IMPORTED_EVENT_EXPECTED;
+            else
+                status = imported ? TB_CA_IMPORTED_EVENT_NOT_EXPECTED : TB_CA_IMPORTED_EVENT_EXPECTED;
+            break;
+        }
+        if (imported) {
+            if (ev.timestamp < TB_TIMESTAMP_MIN || ev.timestamp > TB_TIMESTAMP_MAX) {
+                status = is_transfers ? TB_CT_IMPORTED_EVENT_TIMESTAMP_OUT_OF_RANGE
+                                      : TB_CA_IMPORTED_EVENT_TIMESTAMP_OUT_OF_RANGE;
+                break;
+            }
+            if (ev.timestamp >= c.batch_ts[b]) {
+                status = is_transfers ? TB_CT_IMPORTED_EVENT_TIMESTAMP_MUST_NOT_ADVANCE
+                                      : TB_CA_IMPORTED_EVENT_TIMESTAMP_MUST_NOT_ADVANCE;
+                break;
+            }
+        } else if (ev.timestamp != 0) {
+            status = TB_CT_TIMESTAMP_MUST_BE_ZERO;
+            break;
+        }
+        uint64_t ts = ts_event;
+        if constexpr (__is_same(Event, tb_transfer_t)) {
+            status = replay_create_transfer(R, c, k, ts_event, ev, &ts);
+            if (status == TB_STATUS_CREATED || status == TB_CT_EXISTS) ts_actual = ts;
+        } else {
+            status = replay_create_account(R, c, k, ts_event, ev, &ts);
+            if (status == TB_STATUS_CREATED || status == TB_CA_EXISTS) ts_actual = ts;
+        }
+    } while (0);
+
+    // The event becomes the holder of its id's slot when it created or orphaned the id.
+    const bool transient = is_transfers && status != TB_STATUS_CREATED &&
+                           tb_transfer_status_transient(status);
+    if ((status == TB_STATUS_CREATED || transient) && c.ev_slot[k] != kNone32) {
+        unsigned long long* slots = is_transfers ? T.tr.slots : T.acc.slots;
+        slots[c.ev_slot[k]] = c.row_base + k + 1;
+    }
+    if (status != TB_STATUS_CREATED && chain_open && !chain_broken) {
+        chain_broken = true;
+        R.scope_close(true);
+        for (uint32_t ci = chain_start; ci < k; ci++)
+            c.results[ci].status = TB_CT_LINKED_EVENT_FAILED;
+    }
+    tb_create_result_t res;
+    res.timestamp = ts_actual;
+    res.status = status;
+    res.reserved = 0;
+    c.results[k] = res;
+    if (chain_open && (!(f & linked_flag) || status == TB_CT_LINKED_EVENT_CHAIN_OPEN)) {
+        if (!chain_broken) R.scope_close(false);
+        chain_open = false;
+        chain_broken = false;
+    }
+}
+
+template <typename Event>
+__global__ void replay_kernel(Tables T, Call<Event> c, int is_transfers) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    Replay R(T);
+    bool chain_open = false, chain_broken = false;
+    uint32_t chain_start = 0;
+    const uint32_t n = T.scalars->slow_count;
+    for (uint32_t i = 0; i < n; i++) {
+        replay_chain_step<Event>(R, c, c.slow_list[i], is_transfers != 0, chain_open, chain_start,
+                                 chain_broken);
+        if (R.overflow) {
+            atomicOr(&T.scalars->flags, kFlagUndoOverflow);
+            break;
+        }
+    }
+    T.scalars->stats[2] = n;
+}
+
+// Id slots and liveness of events: created -> object, transient -> orphan, else tombstone.
+template <typename Event>
+__device__ inline void finalize_event(const Tables& T, const Call<Event>& c, uint32_t k,
+                                      bool is_transfers) {
+    const uint64_t row = c.row_base + k;
+    const uint32_t status = c.results[k].status;
+    const bool created = status == TB_STATUS_CREATED;
+    const uint32_t s = c.ev_slot[k];
+    unsigned long long* slots = is_transfers ? T.tr.slots : T.acc.slots;
+    if (s != kNone32 && slots[s] == row + 1) {
+        if (created) {
+            // the slot names a committed object
+        } else if (is_transfers && tb_transfer_status_transient(status)) {
+            T.tr_rows[row].id = c.events[k].id;  // orphaned ids keep their key for probes
+            slots[s] = (row + 1) | kOrphanBit;
+        } else {
+            slots[s] = kTomb;
+        }
+    }
+    if (is_transfers) T.tr_live[row] = created;
+    else T.acc_live[row] = created;
+}
+
+template <typename Event>
+__global__ void finalize_slow(Tables T, Call<Event> c, int is_transfers) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= T.scalars->slow_count) return;
+    finalize_event(T, c, c.slow_list[i], is_transfers != 0);
+}
+
+template <typename Event>
+__global__ void finalize_all(Tables T, Call<Event> c, int is_transfers) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= c.n) return;
+    finalize_event(T, c, k, is_transfers != 0);
+}
+
+// ================================ create_accounts ===========================================
+
+__global__ void acc_prepare(Tables T, Call<tb_account_t> c) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    bool imported = false;
+    if (k < c.n) {
+        const tb_account_t* ev = c.events;
+        const tb_account_t& a = ev[k];
+        imported = (a.flags & TB_ACCOUNT_IMPORTED) != 0;
+        uint64_t slot = kNone;
+        if (!u128_is_zero(a.id) && !u128_is_max(a.id)) {
+            const tb_account_t* rows = T.acc_rows;
+            const uint64_t base = c.row_base;
+            bool dup = false;
+            slot = probe_claim(T.acc, a.id, base + k + 1, base, [&](uint64_t r) {
+                return r >= base ? ev[r - base].id : rows[r].id;
+            }, &dup);
+            if (slot == kNone) atomicOr(&T.scalars->flags, kFlagTableFull);
+        }
+        c.ev_slot[k] = slot == kNone ? kNone32 : uint32_t(slot);
+    }
+    set_flag_any(T.scalars, imported, kFlagImported);
+}
+
+__global__ void acc_classify(Tables T, Call<tb_account_t> c) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    uint8_t cls = kClassDone;
+    bool created = false;
+    uint64_t ts_created = 0;
+    if (k < c.n) {
+        const uint32_t b = batch_of(c.batch_ends, c.n_batches, k);
+        const uint64_t ts_event = ts_event_of(c, b, k);
+        const tb_account_t a = c.events[k];
+        const uint32_t bstart = batch_start_of(c, b);
+        uint32_t status = 0;
+        uint64_t ts = ts_event;
+        const uint16_t f = a.flags;
+        if (c.force_replay || (T.scalars->flags & kFlagImported) || (f & TB_ACCOUNT_LINKED) ||
+            (k > bstart && (c.events[k - 1].flags & TB_ACCOUNT_LINKED))) {
+            cls = kClassSlow;
+        } else if (a.timestamp != 0) {
+            status = TB_CA_TIMESTAMP_MUST_BE_ZERO;
+        } else if (a.reserved != 0) {
+            status = TB_CA_RESERVED_FIELD;
+        } else if (f & TB_ACCOUNT_PADDING_MASK) {
+            status = TB_CA_RESERVED_FLAG;
+        } else if (u128_is_zero(a.id)) {
+            status = TB_CA_ID_MUST_NOT_BE_ZERO;
+        } else if (u128_is_max(a.id)) {
+            status = TB_CA_ID_MUST_NOT_BE_INT_MAX;
+        } else {
+            const uint32_t s = c.ev_slot[k];
+            if (s == kNone32) {
+                cls = kClassSlow;
+            } else {
+                const uint64_t w = T.acc.slots[s];
+                const uint64_t r = (w & kRefMask) - 1;
+                if (r < c.row_base) {
+                    const tb_account_t e = T.acc_rows[r];
+                    status = create_account_exists(a, e, &ts);
+                } else if (r != c.row_base + k) {
+                    cls = kClassSlow;  // a later duplicate of an in-call id
+                } else {
+                    status = create_account_checks(a);
+                    if (status == TB_STATUS_CREATED) {
+                        T.acc_rows[c.row_base + k] = account_row_of(a, ts_event);
+                        created = true;
+                        ts_created = ts_event;
+                    }
+                }
+            }
+        }
+        if (cls == kClassDone) {
+            tb_create_result_t res;
+            res.timestamp = (status == TB_CA_EXISTS || created) ? ts : ts_event;
+            res.status = status;
+            res.reserved = 0;
+            c.results[k] = res;
+        }
+        c.ev_slow[k] = cls == kClassSlow;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        uint64_t o = __shfl_xor(ts_created, off);
+        ts_created = o > ts_created ? o : ts_created;
+    }
+    if ((threadIdx.x & 63) == 0 && ts_created)
+        atomicMax(&T.scalars->accounts_key_max, (unsigned long long)ts_created);
+    count_stat(T.scalars, 1, created);
+    count_stat(T.scalars, 3, k < c.n && cls == kClassDone && !created);
+}
+
+// ================================ pulse ======================================================
+
+// One lane per expires_at entry: drop entries that left the index (posted / voided / expired /
+// rolled back), collect the expired ones, and find the earliest unexpired expiry.
+__global__ void pulse_collect(Tables T, uint64_t timestamp, uint64_t count, uint64_t* keep,
+                              unsigned long long* keep_count, uint64_t* cand_expires,
+                              uint64_t* cand_ts, uint64_t* cand_row,
+                              unsigned long long* cand_count, unsigned long long* next_unexpired) {
+    const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    const uint64_t row = T.expiry[i];
+    if (!T.tr_live[row] || T.tr_status[row] != TB_PENDING_PENDING) return;
+    const tb_transfer_t& p = T.tr_rows[row];
+    const uint64_t expires_at = p.timestamp + (uint64_t)p.timeout * TB_NS_PER_S;
+    keep[atomicAdd(keep_count, 1ull)] = row;
+    if (expires_at <= timestamp) {
+        const unsigned long long j = atomicAdd(cand_count, 1ull);
+        cand_expires[j] = expires_at;
+        cand_ts[j] = p.timestamp;
+        cand_row[j] = row;
+    } else {
+        atomicMin(next_unexpired, (unsigned long long)expires_at);
+    }
+}
+
+// execute_expire_pending_transfers (:4540-4626) for the selected rows.
+__global__ void pulse_apply(Tables T, const uint64_t* rows, uint64_t n) {
+    const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t row = rows[i];
+    const tb_transfer_t& p = T.tr_rows[row];
+    const uint64_t dr_row = account_find(T, p.debit_account_id);
+    const uint64_t cr_row = account_find(T, p.credit_account_id);
+    if (dr_row == kNone || cr_row == kNone) return;
+    tb_account_t* dr = &T.acc_rows[dr_row];
+    tb_account_t* cr = &T.acc_rows[cr_row];
+    const u128 amount = U(p.amount);
+    if (amount) {
+        atomic_sub_u128(&dr->debits_pending, amount);
+        atomic_sub_u128(&cr->credits_pending, amount);
+    }
+    if (p.flags & TB_TRANSFER_CLOSING_DEBIT)
+        atomicAnd(account_code_flags_word(dr), ~(uint32_t(TB_ACCOUNT_CLOSED) << 16));
+    if (p.flags & TB_TRANSFER_CLOSING_CREDIT)
+        atomicAnd(account_code_flags_word(cr), ~(uint32_t(TB_ACCOUNT_CLOSED) << 16));
+    T.tr_status[row] = TB_PENDING_EXPIRED;
+}
+
+// ================================ lookups, dumps, indexes ===================================
+
+__global__ void lookup_accounts_kernel(Tables T, const tb_uint128_t* ids, uint32_t n,
+                                       uint64_t* rows, uint8_t* found) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t r = account_find(T, ids[i]);
+    found[i] = r != kNone;
+    rows[i] = r;
+}
+
+__global__ void lookup_transfers_kernel(Tables T, const tb_uint128_t* ids, uint32_t n,
+                                        uint64_t* rows, uint8_t* found) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const tb_transfer_t* trs = T.tr_rows;
+    const uint64_t s = probe_find(T.tr, ids[i], [&](uint64_t r) { return trs[r].id; });
+    uint64_t r = kNone;
+    if (s != kNone) {
+        const uint64_t w = T.tr.slots[s];
+        if (!(w & kOrphanBit)) r = (w & kRefMask) - 1;
+    }
+    found[i] = r != kNone;
+    rows[i] = r;
+}
+
+template <typename Row>
+__global__ void gather_rows(const Row* src, const uint64_t* rows, const uint32_t* sel, uint32_t n,
+                            Row* dst) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    dst[i] = src[rows ? rows[sel[i]] : sel[i]];
+}
+
+template <typename Row>
+__global__ void gather_timestamps(const Row* src, const uint32_t* sel, uint64_t n, uint64_t* dst) {
+    const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    dst[i] = src[sel[i]].timestamp;
+}
+
+__global__ void gather_status(const uint8_t* src, const uint32_t* sel, uint64_t n, uint8_t* dst) {
+    const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    dst[i] = src[sel[i]];
+}
+
+__global__ void set_balances_kernel(Tables T, tb_uint128_t id, tb_uint128_t dp, tb_uint128_t dpo,
+                                    tb_uint128_t cp, tb_uint128_t cpo, int* rc) {
+    const uint64_t r = account_find(T, id);
+    if (r == kNone) {
+        *rc = -1;
+        return;
+    }
+    tb_account_t* a = &T.acc_rows[r];
+    a->debits_pending = dp;
+    a->debits_posted = dpo;
+    a->credits_pending = cp;
+    a->credits_posted = cpo;
+    *rc = 0;
+}
+
+}  // namespace tbg

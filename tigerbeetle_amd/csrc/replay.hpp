@@ -39,6 +39,9 @@ enum : unsigned int {
     kFlagPostVoid = 1u << 1,   // some event of the call posts or voids
     kFlagUndoOverflow = 1u << 2,
     kFlagTableFull = 1u << 3,
+    kFlagDuplicate = 1u << 4,  // two events of the call carry the same id
+    kFlagHot = 1u << 5,        // some account is marked hot (a SLOW event touches it)
+    kFlagClosable = 1u << 6,   // some account is marked closable
 };
 
 enum : uint8_t { kClassDone = 0, kClassFast = 1, kClassSlow = 2 };
@@ -90,15 +93,33 @@ struct Call {
     uint64_t row_base;
     uint32_t epoch;
     uint32_t force_replay;
-    // per-event scratch
-    uint32_t* ev_batch;
-    uint64_t* ev_slot;
-    uint64_t* ev_dr;
-    uint64_t* ev_cr;
-    uint64_t* ev_p_slot;
-    uint8_t* ev_class;
+    // per-event scratch (structure of arrays; kNone32 = absent)
+    uint32_t* ev_slot;     // slot of the event's id in the id table
+    uint32_t* ev_dr;       // account rows (create_transfers)
+    uint32_t* ev_cr;
+    uint64_t* ev_amount;   // amount low word of parallel-path candidates
+    uint8_t* ev_info;      // kInfo* bits
+    uint8_t* ev_slow;      // 1 = executes in the ordered replay
     const uint32_t* slow_list;
 };
+
+constexpr uint32_t kNone32 = 0xFFFFFFFFu;
+
+// ev_info bits written by the ingest pass and consumed by the commit pass.
+enum : uint8_t {
+    kInfoClassMask = 3,        // kClassDone / kClassFast / kClassSlow
+    kInfoPostLookup = 1 << 2,  // status decided after the id lookup: valid only for the holder
+    kInfoClosedDep = 1 << 3,   // status depends on `closed` of an account
+    kInfoPending = 1 << 4,     // flags.pending
+    kInfoTimeout = 1 << 5,     // timeout > 0
+    kInfoClaimed = 1 << 6,     // the event claimed / found its id slot
+};
+
+template <typename C>
+__device__ inline uint64_t slot_of(const C& c, uint32_t k) {
+    const uint32_t s = c.ev_slot[k];
+    return s == kNone32 ? kNone : uint64_t(s);
+}
 
 __device__ inline uint32_t batch_of(const uint32_t* ends, uint32_t n_batches, uint32_t k) {
     uint32_t lo = 0, hi = n_batches;  // first b with ends[b] > k
@@ -108,6 +129,23 @@ __device__ inline uint32_t batch_of(const uint32_t* ends, uint32_t n_batches, ui
         else lo = mid + 1;
     }
     return lo;
+}
+
+// batch_of with a guess: batches of (near-)uniform length resolve in one or two loads instead of
+// a dependent binary search; otherwise fall back to the search.
+__device__ inline uint32_t batch_of_guess(const uint32_t* ends, uint32_t n_batches, uint32_t n,
+                                          uint32_t k) {
+    const uint32_t avg = n_batches ? (n / n_batches > 0 ? n / n_batches : 1) : 1;
+    uint32_t b = k / avg;
+    if (b >= n_batches) b = n_batches - 1;
+    for (int step = 0; step < 4; step++) {
+        const bool above = ends[b] <= k;                 // k lies in a later batch
+        const bool below = b > 0 && ends[b - 1] > k;     // k lies in an earlier batch
+        if (!above && !below) return b;
+        b = above ? b + 1 : b - 1;
+        if (b >= n_batches) break;
+    }
+    return batch_of(ends, n_batches, k);
 }
 
 __device__ inline bool ts_index_contains(const uint64_t* idx, uint64_t n, uint64_t ts) {
@@ -124,7 +162,7 @@ __device__ inline bool ts_index_contains(const uint64_t* idx, uint64_t n, uint64
 
 __device__ inline uint64_t account_find(const Tables& T, const tb_uint128_t& id) {
     const tb_account_t* rows = T.acc_rows;
-    uint64_t s = probe_find(T.acc, id, [&](uint64_t r) { return rows[r].id; });
+    uint64_t s = probe_find(T.acc, id, [=](uint64_t r) { return rows[r].id; });
     if (s == kNone) return kNone;
     return (T.acc.slots[s] & kRefMask) - 1;
 }
@@ -232,7 +270,7 @@ __device__ inline uint64_t transfer_slot_find(const Tables& T, const C& c,
     const tb_transfer_t* rows = T.tr_rows;
     const tb_transfer_t* events = c.events;
     uint64_t base = c.row_base;
-    return probe_find(T.tr, id, [&](uint64_t r) {
+    return probe_find(T.tr, id, [=](uint64_t r) {
         return r >= base ? events[r - base].id : rows[r].id;
     });
 }
@@ -432,7 +470,7 @@ __device__ uint32_t replay_create_transfer(Replay& R, const C& c, uint32_t k, ui
     if (u128_is_max(t.id)) return TB_CT_ID_MUST_NOT_BE_INT_MAX;
 
     uint64_t e_row = 0;
-    switch (replay_get_transfer_at_slot(T, c, c.ev_slot[k], k, &e_row)) {
+    switch (replay_get_transfer_at_slot(T, c, slot_of(c, k), k, &e_row)) {
         case 1: {
             const tb_transfer_t e = T.tr_rows[e_row];
             if ((t.flags == e.flags) && U(t.pending_id) == U(e.pending_id) &&
@@ -467,10 +505,10 @@ __device__ uint32_t replay_create_transfer(Replay& R, const C& c, uint32_t k, ui
     if (t.ledger == 0) return TB_CT_LEDGER_MUST_NOT_BE_ZERO;
     if (t.code == 0) return TB_CT_CODE_MUST_NOT_BE_ZERO;
 
-    const uint64_t dr_row = c.ev_dr[k];
-    if (dr_row == kNone) return TB_CT_DEBIT_ACCOUNT_NOT_FOUND;
-    const uint64_t cr_row = c.ev_cr[k];
-    if (cr_row == kNone) return TB_CT_CREDIT_ACCOUNT_NOT_FOUND;
+    const uint32_t dr_row = c.ev_dr[k];
+    if (dr_row == kNone32) return TB_CT_DEBIT_ACCOUNT_NOT_FOUND;
+    const uint32_t cr_row = c.ev_cr[k];
+    if (cr_row == kNone32) return TB_CT_CREDIT_ACCOUNT_NOT_FOUND;
     const tb_account_t dr = T.acc_rows[dr_row];
     const tb_account_t cr = T.acc_rows[cr_row];
     if (dr.ledger != cr.ledger) return TB_CT_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;
@@ -628,7 +666,7 @@ __device__ uint32_t replay_create_account(Replay& R, const C& c, uint32_t k, uin
     if (u128_is_zero(a.id)) return TB_CA_ID_MUST_NOT_BE_ZERO;
     if (u128_is_max(a.id)) return TB_CA_ID_MUST_NOT_BE_INT_MAX;
     uint64_t e_row = 0;
-    if (replay_get_account_at_slot(T, c, c.ev_slot[k], k, &e_row) == 1) {
+    if (replay_get_account_at_slot(T, c, slot_of(c, k), k, &e_row) == 1) {
         const tb_account_t e = T.acc_rows[e_row];
         return create_account_exists(a, e, ts_out);
     }
