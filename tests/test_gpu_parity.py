@@ -4,7 +4,7 @@ import pytest
 
 from parity import Pair
 from tigerbeetle_amd import workload
-from tigerbeetle_amd.types import TIMESTAMP_MAX, NS_PER_S
+from tigerbeetle_amd.types import NS_PER_S, TIMESTAMP_MAX, TRANSFER_DTYPE
 
 pytestmark = pytest.mark.gpu
 
@@ -100,6 +100,45 @@ def test_two_phase_config4_small():
             pending = np.concatenate([pending, t["id"][created & is_pending, 0]])[-5_000:]
             seen = np.concatenate([seen, t["id"][:, 0]])[-20_000:]
             p.tick(int(rng.integers(1, 3)) * NS_PER_S)
+        p.compare_state()
+    finally:
+        p.close()
+
+
+def _transfers(rows):
+    t = np.zeros(len(rows), dtype=TRANSFER_DTYPE)
+    for i, r in enumerate(rows):
+        for k, v in r.items():
+            if k in ("id", "debit_account_id", "credit_account_id", "pending_id", "amount"):
+                t[k][i, 0] = v
+            else:
+                t[k][i] = v
+    return t
+
+
+@pytest.mark.parametrize("force_replay", [False, True], ids=["parallel", "replay"])
+def test_reopened_account_with_limit(force_replay):
+    """A transfer that fails `closed` against an account a void in the same call reopens must
+    replay with the serial balances of its limited debit account: a later parallel credit to that
+    account may not leak into its exceeds_credits check."""
+    p = Pair(account_capacity=64, transfer_capacity=1024, batch_events_max=256,
+             force_replay=force_replay)
+    try:
+        acc = workload.accounts(4, seed=1, ledger=1)
+        acc["flags"] = [2, 0, 0, 0]  # A: debits_must_not_exceed_credits; B, S, C plain
+        p.create_accounts(acc)
+        # S -> A 100 (A's credits); a pending closing_credit transfer C -> B closes B.
+        p.create_transfers(_transfers([
+            dict(id=10, debit_account_id=3, credit_account_id=1, amount=100, ledger=1, code=1),
+            dict(id=11, debit_account_id=4, credit_account_id=2, amount=5, ledger=1, code=1,
+                 flags=2 | 128),
+        ]))
+        r = p.create_transfers(_transfers([
+            dict(id=20, pending_id=11, flags=8),                                       # void: reopens B
+            dict(id=21, debit_account_id=1, credit_account_id=2, amount=150, ledger=1, code=1),
+            dict(id=22, debit_account_id=3, credit_account_id=1, amount=100, ledger=1, code=1),
+        ]))
+        assert list(r["status"]) == [0xFFFFFFFF, 54, 0xFFFFFFFF]  # 54: exceeds_credits
         p.compare_state()
     finally:
         p.close()

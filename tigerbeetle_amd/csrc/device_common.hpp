@@ -7,9 +7,11 @@
 //   * slots: an open-addressing (linear probing) hash index id -> row, one u64 word per slot:
 //       0                 empty
 //       kTomb             deleted (a claim whose event did not create an object); probes skip it
-//       (row + 1)         the object at `row`          (bit 62 set: an orphaned id, transfers only)
-//     During a call, a slot may hold an in-flight claim: (row + 1) with row >= row_base of the
-//     call; the id of such a row is read from the call's input events. Claims race with
+//       tag | (row + 1)   the object at `row`: bits 0-31 row + 1, bits 32-61 a 30-bit tag of the
+//                         id (a probe passes a slot whose tag differs without reading its row),
+//                         bit 62 set: an orphaned id (transfers only)
+//     During a call, a slot may hold an in-flight claim: tag | (row + 1) with row >= row_base of
+//     the call; the id of such a row is read from the call's input events. Claims race with
 //     atomicCAS(0 -> ref) and duplicates resolve with atomicMin, so the earliest event of the call
 //     owns the slot -- the serial order's first occurrence.
 #pragma once
@@ -26,7 +28,8 @@ typedef unsigned __int128 u128;
 constexpr uint64_t kEmpty = 0;
 constexpr uint64_t kTomb = ~0ull;
 constexpr uint64_t kOrphanBit = 1ull << 62;
-constexpr uint64_t kRefMask = (1ull << 62) - 1;
+constexpr uint64_t kRefMask = 0xFFFFFFFFull;            // row + 1
+constexpr uint64_t kTagMask = ((1ull << 30) - 1) << 32;
 constexpr uint64_t kNone = ~0ull;  // "no row" in per-event scratch
 constexpr u128 kU128Max = ~(u128)0;
 
@@ -61,6 +64,15 @@ __host__ __device__ inline uint64_t mix64(uint64_t h) {
 __host__ __device__ inline uint64_t hash_id(const tb_uint128_t& id) {
     const uint64_t group = mix64((id.lo >> 3) ^ mix64(id.hi + 0x9E3779B97F4A7C15ull));
     return (group << 3) | (id.lo & 7);
+}
+
+// The id's tag in slot-word position (independent of the home slot's bits).
+__host__ __device__ inline uint64_t id_tag(const tb_uint128_t& id) {
+    return (mix64(id.hi ^ mix64(id.lo ^ 0x2545F4914F6CDD1Dull)) >> 34) << 32;
+}
+// A live slot word (not empty, not a tombstone) whose tag is `tag`.
+__host__ __device__ inline bool slot_tag_is(uint64_t w, uint64_t tag) {
+    return w != kEmpty && w != kTomb && (w & kTagMask) == tag;
 }
 
 // Non-temporal / plain 16-byte vector copies of 128-byte rows.
@@ -108,12 +120,13 @@ struct IdTable {
 // Read-only probe: returns the slot index holding `id`, or kNone. `row_id(r)` gives the id of row
 // r (committed rows from the store, in-flight rows from the call's input).
 template <typename RowId>
-__device__ inline uint64_t probe_find(const IdTable& t, const tb_uint128_t& id, RowId row_id) {
-    uint64_t s = hash_id(id) & t.mask;
+__device__ inline uint64_t probe_find_from(const IdTable& t, const tb_uint128_t& id, uint64_t s,
+                                           RowId row_id) {
+    const uint64_t tag = id_tag(id);
     for (uint64_t n = 0; n <= t.mask; n++) {
         uint64_t w = t.slots[s];
         if (w == kEmpty) return kNone;
-        if (w != kTomb) {
+        if (slot_tag_is(w, tag)) {
             uint64_t r = (w & kRefMask) - 1;
             if (u128_eq(row_id(r), id)) return s;
         }
@@ -121,34 +134,47 @@ __device__ inline uint64_t probe_find(const IdTable& t, const tb_uint128_t& id, 
     }
     return kNone;
 }
+template <typename RowId>
+__device__ inline uint64_t probe_find(const IdTable& t, const tb_uint128_t& id, RowId row_id) {
+    return probe_find_from(t, id, hash_id(id) & t.mask, row_id);
+}
 
 // Claim-or-find: inserts an in-flight claim `ref` for `id` unless `id` is already present.
 // Returns the slot of `id`. Duplicates within the call keep the smallest ref (earliest event).
 // `*dup` is set when another in-flight claim of the same id is found: of two same-id events, the
 // one probing second always sees the other's claim, so a call with no `dup` has unique ids.
+// `s` is the slot to start at and `w` its word as already read (the home slot, normally).
 template <typename RowId>
-__device__ inline uint64_t probe_claim(const IdTable& t, const tb_uint128_t& id, uint64_t ref,
-                                       uint64_t row_base, RowId row_id, bool* dup) {
-    uint64_t s = hash_id(id) & t.mask;
+__device__ inline uint64_t probe_claim_from(const IdTable& t, const tb_uint128_t& id, uint64_t ref,
+                                            uint64_t row_base, RowId row_id, bool* dup,
+                                            uint64_t s, uint64_t w) {
+    const uint64_t tag = id_tag(id);
+    const uint64_t tref = ref | tag;
     for (uint64_t n = 0; n <= t.mask; n++) {
-        uint64_t w = t.slots[s];
         if (w == kEmpty) {
-            w = atomicCAS(&t.slots[s], (unsigned long long)kEmpty, (unsigned long long)ref);
+            w = atomicCAS(&t.slots[s], (unsigned long long)kEmpty, (unsigned long long)tref);
             if (w == kEmpty) return s;
         }
-        if (w != kTomb) {
+        if (slot_tag_is(w, tag)) {
             uint64_t r = (w & kRefMask) - 1;
             if (u128_eq(row_id(r), id)) {
                 if (r >= row_base) {
                     *dup = true;
-                    if (ref < w) atomicMin(&t.slots[s], (unsigned long long)ref);
+                    if (tref < w) atomicMin(&t.slots[s], (unsigned long long)tref);
                 }
                 return s;
             }
         }
         s = (s + 1) & t.mask;
+        w = t.slots[s];
     }
     return kNone;  // table full: the host sizes tables so this cannot happen
+}
+template <typename RowId>
+__device__ inline uint64_t probe_claim(const IdTable& t, const tb_uint128_t& id, uint64_t ref,
+                                       uint64_t row_base, RowId row_id, bool* dup) {
+    const uint64_t s = hash_id(id) & t.mask;
+    return probe_claim_from(t, id, ref, row_base, row_id, dup, s, t.slots[s]);
 }
 
 }  // namespace tbg

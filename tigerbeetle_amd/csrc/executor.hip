@@ -225,6 +225,7 @@ Call<Event> make_call(tbg_ctx* ctx, const Event* d_events, uint32_t n, const uin
     c.row_base = row_base;
     c.epoch = ++ctx->epoch;
     c.force_replay = ctx->force_replay ? 1 : 0;
+    { const char* e = getenv("TBG_ABLATE"); c.ablate = e ? uint32_t(atoi(e)) : 0; }
     c.ev_slot = ctx->ev_slot;
     c.ev_dr = ctx->ev_dr;
     c.ev_cr = ctx->ev_cr;
@@ -510,10 +511,12 @@ int tbg_create_transfers_device(tbg_ctx* ctx, const tb_transfer_t* d_events, uin
     Call<tb_transfer_t> c = make_call(ctx, d_events, n, d_batch_ends, d_batch_ts, n_batches,
                                       d_results, ctx->T.tr_rows_used);
     const dim3 grid(std::min(grid_for(n), kMaxGrid)), block(kBlock);  // grid-stride kernels
+    uint32_t ig = grid.x;
+    { const char* e = getenv("TBG_INGEST_GRID"); if (e) ig = std::min(grid_for(n), uint32_t(atoi(e))); }
     const bool use_sort = n >= kSortThreshold && ctx->bal_keys;
     const uint32_t sentinel = uint32_t(4 * ctx->T.acc_rows_used);
     if (!rc) {
-        hipLaunchKernelGGL(tr_ingest, grid, block, 0, ctx->stream, ctx->T, c);
+        hipLaunchKernelGGL(tr_ingest, dim3(ig), block, 0, ctx->stream, ctx->T, c);
         tmark(ctx, "tr_ingest");
         hipLaunchKernelGGL(tr_commit, grid, block, 0, ctx->stream, ctx->T, c, ctx->bal_keys,
                            ctx->bal_vals, use_sort ? 1 : 0, sentinel);

@@ -85,15 +85,38 @@ __device__ inline uint32_t row32(uint64_t r) { return r == kNone ? kNone32 : uin
 
 // ================================ create_transfers ==========================================
 
-// The checks after the id lookup (create_transfer, :3727-3873), on the ingest snapshot.
+// What the checks after the id lookup read of an account: a snapshot taken by ingest. Account
+// existence, ledger and limit flags are static within a create_transfers call; `closed` and the
+// balances are not, and every decision that reads them is re-validated by tr_commit.
+struct AccSnap {
+    uint32_t row;         // kNone32: not found
+    uint32_t ledger;
+    uint16_t flags;
+    uint64_t hi_pending;  // .hi of the pending / posted balance the event adds to
+    uint64_t hi_posted;   // (debit side: debits_*, credit side: credits_*)
+};
+
+__device__ inline AccSnap acc_snap_load(const tb_account_t* a, uint32_t row, bool debit) {
+    AccSnap s;
+    s.row = row;
+    // ledger (112), code (116), flags (118): one 8-byte word.
+    const uint64_t lcf = *reinterpret_cast<const uint64_t*>(reinterpret_cast<const uint8_t*>(a) + 112);
+    s.ledger = uint32_t(lcf);
+    s.flags = uint16_t(lcf >> 48);
+    s.hi_pending = debit ? a->debits_pending.hi : a->credits_pending.hi;
+    s.hi_posted = debit ? a->debits_posted.hi : a->credits_posted.hi;
+    return s;
+}
+
+// The checks after the id lookup (create_transfer, :3727-3873), on the ingest snapshot. `w` is
+// the word of the id's slot as this event observed it.
 __device__ inline uint8_t classify_after_lookup(const Tables& T, const Call<tb_transfer_t>& c,
                                                 uint32_t k, uint64_t ts_event,
-                                                const tb_transfer_t& t, uint64_t slot,
-                                                uint32_t dr_row, uint32_t cr_row,
+                                                const tb_transfer_t& t, uint64_t w,
+                                                const AccSnap& dr, const AccSnap& cr,
                                                 uint32_t* status, uint64_t* ts_out,
                                                 uint8_t* info) {
     const uint16_t f = t.flags;
-    const uint64_t w = T.tr.slots[slot];
     const uint64_t r = (w & kRefMask) - 1;
     if (r < c.row_base) {  // a committed id: the result is final for every event of the call
         if (w & kOrphanBit) {
@@ -114,7 +137,7 @@ __device__ inline uint8_t classify_after_lookup(const Tables& T, const Call<tb_t
         *status = create_transfer_exists(t, e, p, ts_out);
         return kClassDone;
     }
-    if (w != c.row_base + k + 1) return kClassSlow;  // a later duplicate of an in-call id
+    if (r != c.row_base + k) return kClassSlow;  // a later duplicate of an in-call id
     // Provisionally the first occurrence: every DONE below is valid only if that holds.
     *info |= kInfoPostLookup;
     if (f & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) return kClassSlow;
@@ -132,56 +155,76 @@ __device__ inline uint8_t classify_after_lookup(const Tables& T, const Call<tb_t
         st = TB_CT_CLOSING_TRANSFER_MUST_BE_PENDING;
     else if (t.ledger == 0) st = TB_CT_LEDGER_MUST_NOT_BE_ZERO;
     else if (t.code == 0) st = TB_CT_CODE_MUST_NOT_BE_ZERO;
-    else if (dr_row == kNone32) st = TB_CT_DEBIT_ACCOUNT_NOT_FOUND;
-    else if (cr_row == kNone32) st = TB_CT_CREDIT_ACCOUNT_NOT_FOUND;
+    else if (dr.row == kNone32) st = TB_CT_DEBIT_ACCOUNT_NOT_FOUND;
+    else if (cr.row == kNone32) st = TB_CT_CREDIT_ACCOUNT_NOT_FOUND;
+    else if (dr.ledger != cr.ledger) st = TB_CT_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;
+    else if (t.ledger != dr.ledger) st = TB_CT_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
     if (st) {
         *status = st;
         return kClassDone;
     }
-    const tb_account_t* dr = &T.acc_rows[dr_row];
-    const tb_account_t* cr = &T.acc_rows[cr_row];
-    const uint32_t dr_ledger = dr->ledger, cr_ledger = cr->ledger;
-    if (dr_ledger != cr_ledger) {
-        *status = TB_CT_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;
-        return kClassDone;
-    }
-    if (t.ledger != dr_ledger) {
-        *status = TB_CT_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
-        return kClassDone;
-    }
-    if (T.acc_closable[dr_row] == c.epoch || T.acc_closable[cr_row] == c.epoch) return kClassSlow;
-    const uint16_t dr_flags = dr->flags, cr_flags = cr->flags;
-    if (dr_flags & TB_ACCOUNT_CLOSED) {
-        *status = TB_CT_DEBIT_ACCOUNT_ALREADY_CLOSED;
-        *info |= kInfoClosedDep;
-        return kClassDone;
-    }
-    if (cr_flags & TB_ACCOUNT_CLOSED) {
-        *status = TB_CT_CREDIT_ACCOUNT_ALREADY_CLOSED;
-        *info |= kInfoClosedDep;
-        return kClassDone;
-    }
-    if (f & (TB_TRANSFER_BALANCING_DEBIT | TB_TRANSFER_BALANCING_CREDIT |
-             TB_TRANSFER_CLOSING_DEBIT | TB_TRANSFER_CLOSING_CREDIT))
-        return kClassSlow;
+    // From here on every outcome follows the `closed` check: a DONE is confirmed by tr_commit
+    // against the call's closable marks, a FAST against closable and hot marks.
+    *info |= kInfoClosedDep;
+    const bool balancing_or_closing =
+        (f & (TB_TRANSFER_BALANCING_DEBIT | TB_TRANSFER_BALANCING_CREDIT |
+              TB_TRANSFER_CLOSING_DEBIT | TB_TRANSFER_CLOSING_CREDIT)) != 0;
     // Overflow is impossible when every balance is < 2^126 and every amount < 2^64.
     constexpr uint64_t kHiLimit = 1ull << 62;
-    if (t.amount.hi != 0 || dr->debits_pending.hi >= kHiLimit ||
-        dr->debits_posted.hi >= kHiLimit || cr->credits_pending.hi >= kHiLimit ||
-        cr->credits_posted.hi >= kHiLimit)
-        return kClassSlow;
+    const bool overflow_possible = t.amount.hi != 0 || dr.hi_pending >= kHiLimit ||
+                                   dr.hi_posted >= kHiLimit || cr.hi_pending >= kHiLimit ||
+                                   cr.hi_posted >= kHiLimit;
+    const bool limited = (dr.flags & TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS) ||
+                         (cr.flags & TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS);
+    if ((dr.flags | cr.flags) & TB_ACCOUNT_CLOSED) {
+        // A `closed` DONE that tr_commit demotes (an event of the call may reopen the account)
+        // replays without hot marks on its accounts, so it may only be one whose later checks
+        // read no order-dependent balance.
+        if (balancing_or_closing || overflow_possible || limited) return kClassSlow;
+        *status = (dr.flags & TB_ACCOUNT_CLOSED) ? TB_CT_DEBIT_ACCOUNT_ALREADY_CLOSED
+                                                 : TB_CT_CREDIT_ACCOUNT_ALREADY_CLOSED;
+        return kClassDone;
+    }
+    if (balancing_or_closing || overflow_possible) return kClassSlow;
     if (ts_event + (uint64_t)t.timeout * TB_NS_PER_S > TB_TIMESTAMP_MAX) {
         *status = TB_CT_OVERFLOWS_TIMEOUT;
         return kClassDone;
     }
-    if (dr_flags & TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS) return kClassSlow;
-    if (cr_flags & TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS) return kClassSlow;
+    if (limited) return kClassSlow;
     if (f & TB_TRANSFER_PENDING) *info |= kInfoPending;
     if (t.timeout > 0) *info |= kInfoTimeout;
     return kClassFast;
 }
 
-// One event of tr_ingest; returns the call flags it raises (kFlagImported / kFlagPostVoid).
+// An account probe resolved from its home-slot word `w` and the row that word names, both
+// already loaded (`home_id` / `home` are that row's id and snapshot). Falls back to the full
+// linear probe when the home slot holds another id.
+__device__ inline AccSnap acc_resolve(const Tables& T, const tb_uint128_t& id, bool valid,
+                                      uint64_t s, uint64_t w, const tb_uint128_t& home_id,
+                                      const AccSnap& home, bool debit) {
+    AccSnap a = home;
+    if (!valid || w == kEmpty) {
+        a.row = kNone32;
+        return a;
+    }
+    if (slot_tag_is(w, id_tag(id)) && u128_eq(home_id, id)) return a;
+    const tb_account_t* rows = T.acc_rows;
+    const uint64_t fs = probe_find_from(T.acc, id, (s + 1) & T.acc.mask,
+                                        [=](uint64_t r) { return rows[r].id; });
+    if (fs == kNone) {
+        a.row = kNone32;
+        return a;
+    }
+    const uint32_t r = uint32_t((T.acc.slots[fs] & kRefMask) - 1);
+    return acc_snap_load(&rows[r], r, debit);
+}
+
+// One event of tr_ingest; returns the call flags it raises (kFlag*).
+//
+// Memory-level parallelism: after the event's own 128-byte load, the three table lookups (id,
+// debit account, credit account) run side by side in two rounds -- the home-slot words, then the
+// id claim (one CAS) together with the account rows those words name -- instead of three
+// dependent probe loops.
 __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_transfer_t>& c,
                                             uint32_t k) {
     bool imported = false, post_void = false, dup = false, closable = false, hot = false;
@@ -197,11 +240,23 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
         const uint16_t f = t.flags;
         imported = (f & TB_TRANSFER_IMPORTED) != 0;
         post_void = (f & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) != 0;
+        const bool valid_id = !u128_is_zero(t.id) && !u128_is_max(t.id);
+        const bool dr_ok = !u128_is_zero(t.debit_account_id) && !u128_is_max(t.debit_account_id);
+        const bool cr_ok = !u128_is_zero(t.credit_account_id) && !u128_is_max(t.credit_account_id);
+
+        // Round 1: the home-slot words of the three ids (independent of the batch lookup).
+        const uint64_t s_id = hash_id(t.id) & T.tr.mask;
+        const uint64_t s_dr = hash_id(t.debit_account_id) & T.acc.mask;
+        const uint64_t s_cr = hash_id(t.credit_account_id) & T.acc.mask;
+        const uint64_t w_id = T.tr.slots[s_id];
+        const uint64_t w_dr = T.acc.slots[s_dr];
+        const uint64_t w_cr = T.acc.slots[s_cr];
+
         const uint32_t b = batch_of_guess(c.batch_ends, c.n_batches, c.n, k);
         const uint32_t bstart = batch_start_of(c, b);
         const uint64_t ts_event = ts_event_of(c, b, k);
-        // The row store takes the event as it is, stamped (rows of events that do not create
-        // an object stay dead); streaming the copy first keeps the event out of registers.
+        // The row store takes every event as it is, stamped (rows of events that do not create
+        // an object stay dead; an orphaned id keeps its key there).
         {
             tb_transfer_t o = t;
             o.timestamp = ts_event;
@@ -212,7 +267,6 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
         }
         const bool chain = (f & TB_TRANSFER_LINKED) ||
                            (k > bstart && (c.events[k - 1].flags & TB_TRANSFER_LINKED));
-        const bool valid_id = !u128_is_zero(t.id) && !u128_is_max(t.id);
 
         uint32_t status = 0;
         uint64_t ts_out = ts_event;
@@ -237,31 +291,52 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
             }
         }
         uint64_t slot = kNone;
-        uint32_t dr_row = kNone32, cr_row = kNone32;
+        AccSnap dr, cr;
+        dr.row = cr.row = kNone32;
         if (pre_done) {
             cls = kClassDone;
         } else {
             const tb_transfer_t* ev = c.events;
             const tb_transfer_t* rows = T.tr_rows;
             const uint64_t base = c.row_base;
+            const uint64_t tref = (base + k + 1) | id_tag(t.id);
+            // Round 2: claim an empty home slot, and read the account rows the home slots name.
+            uint64_t w_seen = w_id;
+            if (valid_id && w_id == kEmpty)
+                w_seen = atomicCAS(&T.tr.slots[s_id], (unsigned long long)kEmpty,
+                                   (unsigned long long)tref);
+            const uint32_t dr_home = w_dr == kEmpty || w_dr == kTomb
+                                         ? 0u : uint32_t((w_dr & kRefMask) - 1);
+            const uint32_t cr_home = w_cr == kEmpty || w_cr == kTomb
+                                         ? 0u : uint32_t((w_cr & kRefMask) - 1);
+            const tb_account_t* pd = &T.acc_rows[dr_home];
+            const tb_account_t* pc = &T.acc_rows[cr_home];
+            const tb_uint128_t d_id = pd->id, c_id = pc->id;
+            const AccSnap d_home = acc_snap_load(pd, dr_home, true);
+            const AccSnap c_home = acc_snap_load(pc, cr_home, false);
+
+            uint64_t w_slot = tref;
             if (valid_id) {
-                slot = probe_claim(T.tr, t.id, base + k + 1, base, [=](uint64_t r) {
-                    return r >= base ? ev[r - base].id : rows[r].id;
-                }, &dup);
+                if (w_id == kEmpty && w_seen == kEmpty) {
+                    slot = s_id;  // claimed
+                } else {
+                    slot = probe_claim_from(T.tr, t.id, base + k + 1, base, [=](uint64_t r) {
+                        return r >= base ? ev[r - base].id : rows[r].id;
+                    }, &dup, s_id, w_seen);
+                    if (slot != kNone) w_slot = T.tr.slots[slot];
+                }
                 if (slot == kNone) atomicOr(&T.scalars->flags, kFlagTableFull);
                 else info |= kInfoClaimed;
             }
-            if (!u128_is_zero(t.debit_account_id) && !u128_is_max(t.debit_account_id))
-                dr_row = row32(account_find(T, t.debit_account_id));
-            if (!u128_is_zero(t.credit_account_id) && !u128_is_max(t.credit_account_id))
-                cr_row = row32(account_find(T, t.credit_account_id));
+            dr = acc_resolve(T, t.debit_account_id, dr_ok, s_dr, w_dr, d_id, d_home, true);
+            cr = acc_resolve(T, t.credit_account_id, cr_ok, s_cr, w_cr, c_id, c_home, false);
             // Accounts whose `closed` flag an event of this call may change.
-            if ((f & TB_TRANSFER_CLOSING_DEBIT) && dr_row != kNone32) {
-                T.acc_closable[dr_row] = c.epoch;
+            if ((f & TB_TRANSFER_CLOSING_DEBIT) && dr.row != kNone32) {
+                T.acc_closable[dr.row] = c.epoch;
                 closable = true;
             }
-            if ((f & TB_TRANSFER_CLOSING_CREDIT) && cr_row != kNone32) {
-                T.acc_closable[cr_row] = c.epoch;
+            if ((f & TB_TRANSFER_CLOSING_CREDIT) && cr.row != kNone32) {
+                T.acc_closable[cr.row] = c.epoch;
                 closable = true;
             }
             if ((f & TB_TRANSFER_VOID_PENDING) && !u128_is_zero(t.pending_id) &&
@@ -270,23 +345,23 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
                 if (ps != kNone) {
                     const uint64_t pr = (T.tr.slots[ps] & kRefMask) - 1;
                     const tb_transfer_t& p = pr >= base ? ev[pr - base] : rows[pr];
-                    const uint64_t pd = account_find(T, p.debit_account_id);
-                    const uint64_t pc = account_find(T, p.credit_account_id);
-                    if (pd != kNone) T.acc_closable[pd] = c.epoch;
-                    if (pc != kNone) T.acc_closable[pc] = c.epoch;
+                    const uint64_t pd_row = account_find(T, p.debit_account_id);
+                    const uint64_t pc_row = account_find(T, p.credit_account_id);
+                    if (pd_row != kNone) T.acc_closable[pd_row] = c.epoch;
+                    if (pc_row != kNone) T.acc_closable[pc_row] = c.epoch;
                     closable = true;
                 }
             }
             if (!chain && !c.force_replay && !imported && slot != kNone) {
-                cls = classify_after_lookup(T, c, k, ts_event, t, slot, dr_row, cr_row, &status,
+                cls = classify_after_lookup(T, c, k, ts_event, t, w_slot, dr, cr, &status,
                                             &ts_out, &info);
             }
         }
         info |= cls;
         c.ev_info[k] = info;
         c.ev_slot[k] = slot == kNone ? kNone32 : uint32_t(slot);
-        c.ev_dr[k] = dr_row;
-        c.ev_cr[k] = cr_row;
+        c.ev_dr[k] = dr.row;
+        c.ev_cr[k] = cr.row;
         if (cls == kClassDone) {
             tb_create_result_t res;
             res.timestamp = status == TB_CT_EXISTS ? ts_out : ts_event;
@@ -306,9 +381,9 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
             c.results[k] = res;
         } else {
             // Accounts whose balances or flags an event executes on in order.
-            if (dr_row != kNone32) T.acc_hot[dr_row] = c.epoch;
-            if (cr_row != kNone32) T.acc_hot[cr_row] = c.epoch;
-            hot = dr_row != kNone32 || cr_row != kNone32;
+            if (dr.row != kNone32) T.acc_hot[dr.row] = c.epoch;
+            if (cr.row != kNone32) T.acc_hot[cr.row] = c.epoch;
+            hot = dr.row != kNone32 || cr.row != kNone32;
         }
     }
     return (imported ? kFlagImported : 0u) | (post_void ? kFlagPostVoid : 0u) |
@@ -348,7 +423,7 @@ __device__ inline void commit_event(const Tables& T, const Call<tb_transfer_t>& 
             const uint32_t s = c.ev_slot[k];
             const uint32_t dr = c.ev_dr[k], cr = c.ev_cr[k];
             // Each re-check reads only when ingest raised the flag that can make it fail.
-            if (((call_flags & kFlagDuplicate) && T.tr.slots[s] != ref) ||
+            if (((call_flags & kFlagDuplicate) && (T.tr.slots[s] & kRefMask) != ref) ||
                 ((call_flags & kFlagClosable) &&
                  (T.acc_closable[dr] == c.epoch || T.acc_closable[cr] == c.epoch)) ||
                 ((call_flags & kFlagHot) && (T.acc_hot[dr] == c.epoch || T.acc_hot[cr] == c.epoch)) ||
@@ -381,7 +456,7 @@ __device__ inline void commit_event(const Tables& T, const Call<tb_transfer_t>& 
             if (info & kInfoPostLookup) {
                 const uint32_t s = c.ev_slot[k];
                 const uint32_t dr = c.ev_dr[k], cr = c.ev_cr[k];
-                if ((call_flags & kFlagDuplicate) && T.tr.slots[s] != ref) {
+                if ((call_flags & kFlagDuplicate) && (T.tr.slots[s] & kRefMask) != ref) {
                     slow = true;  // a later duplicate: its outcome follows the earlier event's
                 } else if ((info & kInfoClosedDep) && (call_flags & kFlagClosable) &&
                            (T.acc_closable[dr] == c.epoch || T.acc_closable[cr] == c.epoch)) {
@@ -390,7 +465,7 @@ __device__ inline void commit_event(const Tables& T, const Call<tb_transfer_t>& 
                     // transient_error (:3215-3252): the id stays taken (orphan); else released.
                     if (tb_transfer_status_transient(c.results[k].status)) {
                         T.tr_rows[row].id = c.events[k].id;
-                        T.tr.slots[s] = ref | kOrphanBit;
+                        T.tr.slots[s] |= kOrphanBit;
                     } else {
                         T.tr.slots[s] = kTomb;
                     }
@@ -623,7 +698,7 @@ __device__ inline void replay_chain_step(Replay& R, const Call<Event>& c, uint32
                            tb_transfer_status_transient(status);
     if ((status == TB_STATUS_CREATED || transient) && c.ev_slot[k] != kNone32) {
         unsigned long long* slots = is_transfers ? T.tr.slots : T.acc.slots;
-        slots[c.ev_slot[k]] = c.row_base + k + 1;
+        slots[c.ev_slot[k]] = (c.row_base + k + 1) | id_tag(ev.id);
     }
     if (status != TB_STATUS_CREATED && chain_open && !chain_broken) {
         chain_broken = true;
@@ -670,12 +745,12 @@ __device__ inline void finalize_event(const Tables& T, const Call<Event>& c, uin
     const bool created = status == TB_STATUS_CREATED;
     const uint32_t s = c.ev_slot[k];
     unsigned long long* slots = is_transfers ? T.tr.slots : T.acc.slots;
-    if (s != kNone32 && slots[s] == row + 1) {
+    if (s != kNone32 && (slots[s] & kRefMask) == row + 1) {
         if (created) {
             // the slot names a committed object
         } else if (is_transfers && tb_transfer_status_transient(status)) {
             T.tr_rows[row].id = c.events[k].id;  // orphaned ids keep their key for probes
-            slots[s] = (row + 1) | kOrphanBit;
+            slots[s] |= kOrphanBit;
         } else {
             slots[s] = kTomb;
         }

@@ -93,6 +93,7 @@ struct Call {
     uint64_t row_base;
     uint32_t epoch;
     uint32_t force_replay;
+    uint32_t ablate;  // perf experiments only (TBG_ABLATE): bits skip parts of tr_ingest
     // per-event scratch (structure of arrays; kNone32 = absent)
     uint32_t* ev_slot;     // slot of the event's id in the id table
     uint32_t* ev_dr;       // account rows (create_transfers)
