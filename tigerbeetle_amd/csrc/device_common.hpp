@@ -56,15 +56,24 @@ __host__ __device__ inline uint64_t mix64(uint64_t h) {
     h ^= h >> 33;
     return h;
 }
-// Home slot of an id. Ids that differ only in their 3 low bits share one 8-slot (64-byte) group:
-// sequential ids (the reference's --id-order=sequential, and TigerBeetle's recommended
-// time-based ids within a millisecond) land in consecutive slots, so a wave's claims hit 8 cache
-// lines instead of 64. Everything above the low 3 bits is fully mixed, so random ids still spread
-// uniformly over the table.
+// Home slot of an id, and the probe sequence. Ids that differ only in their 4 low bits share one
+// 16-slot group (one 128-byte line): sequential ids (the reference's --id-order=sequential, and
+// TigerBeetle's recommended time-based ids within a millisecond) land in one line per 16 ids, so a
+// wave's claims touch 4-5 lines instead of 64. The offset inside the group is the id's low bits
+// XOR bits of the group hash, so ids that share their low bits (strided ids) still spread over
+// every offset. A probe steps a whole group at a time (s + 16): an id whose home group is taken
+// by another run of sequential ids reaches a free group in one step instead of walking the run.
+constexpr uint64_t kProbeStride = 16;
+
 __host__ __device__ inline uint64_t hash_id(const tb_uint128_t& id) {
-    const uint64_t group = mix64((id.lo >> 3) ^ mix64(id.hi + 0x9E3779B97F4A7C15ull));
-    return (group << 3) | (id.lo & 7);
+    const uint64_t group = mix64((id.lo >> 4) ^ mix64(id.hi + 0x9E3779B97F4A7C15ull));
+    return (group << 4) | ((id.lo ^ (group >> 59)) & 15);
 }
+__host__ __device__ inline uint64_t probe_next(uint64_t s, uint64_t mask) {
+    return (s + kProbeStride) & mask;
+}
+// Slots a probe may visit before it has seen every slot of its offset class once.
+__host__ __device__ inline uint64_t probe_limit(uint64_t mask) { return (mask >> 4) + 1; }
 
 // The id's tag in slot-word position (independent of the home slot's bits).
 __host__ __device__ inline uint64_t id_tag(const tb_uint128_t& id) {
@@ -89,13 +98,16 @@ __device__ inline void copy_row(void* dst, const void* src) {
 
 // u128 atomic add/sub on a {lo, hi} pair: the carry/borrow of each u64 add is propagated with a
 // second atomic. Concurrent adds commute, so the final value is the exact sum.
-__device__ inline void atomic_add_u128(tb_uint128_t* p, u128 v) {
+// atomic_add_u128 returns the hi word it produced when it changed the hi word (else 0): the
+// adder that moves the hi word last observes its final value.
+__device__ inline uint64_t atomic_add_u128(tb_uint128_t* p, u128 v) {
     uint64_t lo = (uint64_t)v, hi = (uint64_t)(v >> 64);
     if (lo) {
         uint64_t old = atomicAdd((unsigned long long*)&p->lo, (unsigned long long)lo);
         if (old + lo < old) hi += 1;
     }
-    if (hi) atomicAdd((unsigned long long*)&p->hi, (unsigned long long)hi);
+    if (hi) return atomicAdd((unsigned long long*)&p->hi, (unsigned long long)hi) + hi;
+    return 0;
 }
 __device__ inline void atomic_sub_u128(tb_uint128_t* p, u128 v) {
     uint64_t lo = (uint64_t)v, hi = (uint64_t)(v >> 64);
@@ -123,14 +135,14 @@ template <typename RowId>
 __device__ inline uint64_t probe_find_from(const IdTable& t, const tb_uint128_t& id, uint64_t s,
                                            RowId row_id) {
     const uint64_t tag = id_tag(id);
-    for (uint64_t n = 0; n <= t.mask; n++) {
+    for (uint64_t n = 0; n < probe_limit(t.mask); n++) {
         uint64_t w = t.slots[s];
         if (w == kEmpty) return kNone;
         if (slot_tag_is(w, tag)) {
             uint64_t r = (w & kRefMask) - 1;
             if (u128_eq(row_id(r), id)) return s;
         }
-        s = (s + 1) & t.mask;
+        s = probe_next(s, t.mask);
     }
     return kNone;
 }
@@ -150,7 +162,7 @@ __device__ inline uint64_t probe_claim_from(const IdTable& t, const tb_uint128_t
                                             uint64_t s, uint64_t w) {
     const uint64_t tag = id_tag(id);
     const uint64_t tref = ref | tag;
-    for (uint64_t n = 0; n <= t.mask; n++) {
+    for (uint64_t n = 0; n < probe_limit(t.mask); n++) {
         if (w == kEmpty) {
             w = atomicCAS(&t.slots[s], (unsigned long long)kEmpty, (unsigned long long)tref);
             if (w == kEmpty) return s;
@@ -165,7 +177,7 @@ __device__ inline uint64_t probe_claim_from(const IdTable& t, const tb_uint128_t
                 return s;
             }
         }
-        s = (s + 1) & t.mask;
+        s = probe_next(s, t.mask);
         w = t.slots[s];
     }
     return kNone;  // table full: the host sizes tables so this cannot happen
@@ -175,6 +187,100 @@ __device__ inline uint64_t probe_claim(const IdTable& t, const tb_uint128_t& id,
                                        uint64_t row_base, RowId row_id, bool* dup) {
     const uint64_t s = hash_id(id) & t.mask;
     return probe_claim_from(t, id, ref, row_base, row_id, dup, s, t.slots[s]);
+}
+
+// The account index: a read-mostly cache of the id -> row mapping together with what the
+// create_transfers checks read of an account, one 32-byte entry per account (4 per 128-byte line),
+// linear probing on a fully mixed hash. A lookup is one 32-byte load: the id compare, the row, the
+// ledger and the flags arrive together, so the common path never touches the 128-byte row.
+//
+// Entries are inserted when create_accounts calls finish (accounts never leave the index after
+// that) and are immutable except `hazard`, a conservative summary of the account's dynamic state
+// that is only ever set: bit kHazardClosed when the account may be closed, kHazardHigh when one of
+// its balances may have reached 2^126 (hi word >= 2^62). While hazard is zero the account is open
+// and no u128 balance can overflow within a call of < 2^32 events with amounts < 2^64; otherwise
+// the reader takes the row itself. Writers: create_accounts (closed accounts), the ordered replay
+// (update_account), balance application (bal_reduce, u128 atomics), debug balance setters.
+struct alignas(16) AccEntry {
+    tb_uint128_t id;   // 0: empty (an account id is never 0)
+    uint32_t ref;      // row + 1 (0: empty)
+    uint32_t ledger;
+    uint16_t flags;    // Account.flags at creation (`closed` is tracked by hazard)
+    uint16_t hazard;
+    uint32_t reserved;
+};
+static_assert(sizeof(AccEntry) == 32, "AccEntry is 32 bytes");
+
+enum : uint16_t { kHazardClosed = 1, kHazardHigh = 2 };
+constexpr uint64_t kHazardHiLimit = 1ull << 62;
+
+__host__ __device__ inline uint64_t acc_entry_home(const tb_uint128_t& id) {
+    return mix64(id.lo ^ mix64(id.hi ^ 0xD6E8FEB86659FD93ull));
+}
+
+struct AccIndex {
+    AccEntry* entries;
+    uint64_t mask;
+};
+
+// One 32-byte load per probe step; returns the entry index or kNone.
+__device__ inline uint64_t acc_index_find(const AccIndex& x, const tb_uint128_t& id, AccEntry* out) {
+    if (u128_is_zero(id)) return kNone;
+    uint64_t s = acc_entry_home(id) & x.mask;
+    for (uint64_t n = 0; n <= x.mask; n++) {
+        const uint4* p = reinterpret_cast<const uint4*>(&x.entries[s]);
+        const uint4 a = p[0], b = p[1];
+        const uint64_t lo = (uint64_t(a.y) << 32) | a.x, hi = (uint64_t(a.w) << 32) | a.z;
+        if (b.x == 0) return kNone;  // empty
+        if (lo == id.lo && hi == id.hi) {
+            out->id.lo = lo;
+            out->id.hi = hi;
+            out->ref = b.x;
+            out->ledger = b.y;
+            out->flags = uint16_t(b.z);
+            out->hazard = uint16_t(b.z >> 16);
+            out->reserved = b.w;
+            return s;
+        }
+        s = (s + 1) & x.mask;
+    }
+    return kNone;
+}
+
+// Inserts a new id (the caller guarantees it is absent); returns the entry index or kNone.
+__device__ inline uint64_t acc_index_insert(const AccIndex& x, const tb_uint128_t& id, uint32_t row,
+                                            uint32_t ledger, uint16_t flags, uint16_t hazard) {
+    uint64_t s = acc_entry_home(id) & x.mask;
+    for (uint64_t n = 0; n <= x.mask; n++) {
+        AccEntry* e = &x.entries[s];
+        if (atomicCAS(&e->ref, 0u, row + 1) == 0u) {
+            e->id = id;
+            e->ledger = ledger;
+            e->flags = flags;
+            e->hazard = hazard;
+            return s;
+        }
+        s = (s + 1) & x.mask;
+    }
+    return kNone;
+}
+
+__device__ inline void acc_hazard_set(const AccIndex& x, const uint32_t* entry_of, uint64_t row,
+                                      uint16_t bits) {
+    const uint32_t s = entry_of[row];
+    if (s == 0xFFFFFFFFu) return;  // not indexed yet (an account of the running create_accounts)
+    // hazard is the high half of the 32-bit word at offset 24 (flags | hazard << 16).
+    unsigned int* w = reinterpret_cast<unsigned int*>(reinterpret_cast<uint8_t*>(&x.entries[s]) + 24);
+    if (!((*w >> 16) & bits)) atomicOr(w, (unsigned int)bits << 16);
+}
+
+// The hazard bits an account row warrants.
+__device__ inline uint16_t acc_hazard_of(const tb_account_t& a) {
+    uint16_t h = (a.flags & TB_ACCOUNT_CLOSED) ? kHazardClosed : 0;
+    if (a.debits_pending.hi >= kHazardHiLimit || a.debits_posted.hi >= kHazardHiLimit ||
+        a.credits_pending.hi >= kHazardHiLimit || a.credits_posted.hi >= kHazardHiLimit)
+        h |= kHazardHigh;
+    return h;
 }
 
 }  // namespace tbg

@@ -418,8 +418,14 @@ tbg_ctx* tbg_open(const tbg_options* options) {
                      "hipStreamCreate");
     const uint64_t acc_cap = options->account_capacity, tr_cap = options->transfer_capacity;
     const uint64_t ev_max = options->batch_events_max;
-    const uint64_t acc_slots = next_pow2(acc_cap * 2), tr_slots = next_pow2(tr_cap * 2);
+    // Slot tables hold at least 4 probe groups (hash_id / probe_next step 16 slots at a time).
+    const uint64_t acc_slots = std::max<uint64_t>(next_pow2(acc_cap * 2), 64);
+    const uint64_t tr_slots = std::max<uint64_t>(next_pow2(tr_cap * 2), 64);
+    const uint64_t acc_entries = std::max<uint64_t>(next_pow2(acc_cap * 2), 64);
     Tables& T = ctx->T;
+    ok = ok && dev_alloc(ctx, &T.acc_index.entries, acc_entries, true) &&
+         dev_alloc(ctx, &T.acc_entry_of, acc_cap, false) &&
+         hip_ok(ctx, hipMemsetAsync(T.acc_entry_of, 0xFF, acc_cap * sizeof(uint32_t), ctx->stream), "memset");
     ok = ok && dev_alloc(ctx, &T.acc.slots, acc_slots, true) &&
          dev_alloc(ctx, &T.acc_rows, acc_cap, true) && dev_alloc(ctx, &T.acc_live, acc_cap, true) &&
          dev_alloc(ctx, &T.acc_hot, acc_cap, true) &&
@@ -455,6 +461,7 @@ tbg_ctx* tbg_open(const tbg_options* options) {
         return nullptr;
     }
     T.acc.mask = acc_slots - 1;
+    T.acc_index.mask = acc_entries - 1;
     T.tr.mask = tr_slots - 1;
     T.expiry_capacity = tr_cap;
     T.undo_capacity = undo_cap;
@@ -475,7 +482,7 @@ tbg_ctx* tbg_open(const tbg_options* options) {
 void tbg_close(tbg_ctx* ctx) {
     if (!ctx) return;
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    void* ptrs[] = {ctx->T.acc.slots, ctx->T.acc_rows, ctx->T.acc_live, ctx->T.acc_hot,
+    void* ptrs[] = {ctx->T.acc_index.entries, ctx->T.acc_entry_of, ctx->T.acc.slots, ctx->T.acc_rows, ctx->T.acc_live, ctx->T.acc_hot,
                     ctx->T.acc_closable, ctx->T.tr.slots, ctx->T.tr_rows, ctx->T.tr_live,
                     ctx->T.tr_status, ctx->T.expiry, ctx->d_scalars, ctx->T.undo, ctx->d_events,
                     ctx->d_results, ctx->d_batch_ends, ctx->d_batch_ts, ctx->ev_slot, ctx->ev_dr,
@@ -542,8 +549,9 @@ int tbg_create_transfers_device(tbg_ctx* ctx, const tb_transfer_t* d_events, uin
         tmark(ctx, "bal_sort");
         if (!rc) {
             const uint64_t tiles = (uint64_t(items) + kReduceTile - 1) / kReduceTile;
+            const BalTarget target{ctx->T.acc_rows, ctx->T.acc_index, ctx->T.acc_entry_of};
             hipLaunchKernelGGL(bal_reduce_tiles, dim3(uint32_t(tiles)), block, 0, ctx->stream,
-                               ctx->T.acc_rows, ctx->bal_keys_sorted, ctx->bal_vals_sorted,
+                               target, ctx->bal_keys_sorted, ctx->bal_vals_sorted,
                                uint64_t(items), sentinel);
             tmark(ctx, "bal_reduce");
             rc = hip_ok(ctx, hipGetLastError(), "launch") ? 0 : TBG_EHIP;
@@ -593,6 +601,12 @@ int tbg_create_accounts_device(tbg_ctx* ctx, const tb_account_t* d_events, uint3
         rc = hip_ok(ctx, hipGetLastError(), "launch") ? 0 : TBG_EHIP;
     }
     if (!rc) rc = run_replay(ctx, c, false, true);
+    if (!rc) {
+        hipLaunchKernelGGL(acc_index_build, grid, block, 0, ctx->stream, ctx->T,
+                           ctx->T.acc_rows_used, n);
+        tmark(ctx, "acc_index_build");
+        rc = hip_ok(ctx, hipGetLastError(), "launch") ? 0 : TBG_EHIP;
+    }
     if (!rc) rc = end_call(ctx, n);
     ctx->stream = saved;
     ctx->T.acc_rows_used += n;

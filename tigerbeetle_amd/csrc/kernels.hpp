@@ -108,6 +108,28 @@ __device__ inline AccSnap acc_snap_load(const tb_account_t* a, uint32_t row, boo
     return s;
 }
 
+// An account as the checks see it, from its index entry (one 32-byte load). An entry with no
+// hazard bit names an open account whose balances are all < 2^126: the snapshot is complete
+// without the row (balance hi words read as 0, which classify_after_lookup only compares with
+// 2^62). Otherwise the row is read.
+__device__ inline AccSnap acc_lookup_snap(const Tables& T, const tb_uint128_t& id, bool valid,
+                                          bool debit) {
+    AccSnap a;
+    a.row = kNone32;
+    a.ledger = 0;
+    a.flags = 0;
+    a.hi_pending = a.hi_posted = 0;
+    if (!valid) return a;
+    AccEntry e;
+    if (acc_index_find(T.acc_index, id, &e) == kNone) return a;
+    const uint32_t row = e.ref - 1;
+    if (e.hazard) return acc_snap_load(&T.acc_rows[row], row, debit);
+    a.row = row;
+    a.ledger = e.ledger;
+    a.flags = e.flags;
+    return a;
+}
+
 // The checks after the id lookup (create_transfer, :3727-3873), on the ingest snapshot. `w` is
 // the word of the id's slot as this event observed it.
 __device__ inline uint8_t classify_after_lookup(const Tables& T, const Call<tb_transfer_t>& c,
@@ -196,204 +218,218 @@ __device__ inline uint8_t classify_after_lookup(const Tables& T, const Call<tb_t
     return kClassFast;
 }
 
-// An account probe resolved from its home-slot word `w` and the row that word names, both
-// already loaded (`home_id` / `home` are that row's id and snapshot). Falls back to the full
-// linear probe when the home slot holds another id.
-__device__ inline AccSnap acc_resolve(const Tables& T, const tb_uint128_t& id, bool valid,
-                                      uint64_t s, uint64_t w, const tb_uint128_t& home_id,
-                                      const AccSnap& home, bool debit) {
-    AccSnap a = home;
-    if (!valid || w == kEmpty) {
-        a.row = kNone32;
-        return a;
-    }
-    if (slot_tag_is(w, id_tag(id)) && u128_eq(home_id, id)) return a;
-    const tb_account_t* rows = T.acc_rows;
-    const uint64_t fs = probe_find_from(T.acc, id, (s + 1) & T.acc.mask,
-                                        [=](uint64_t r) { return rows[r].id; });
-    if (fs == kNone) {
-        a.row = kNone32;
-        return a;
-    }
-    const uint32_t r = uint32_t((T.acc.slots[fs] & kRefMask) - 1);
-    return acc_snap_load(&rows[r], r, debit);
-}
-
-// One event of tr_ingest; returns the call flags it raises (kFlag*).
+// One event of tr_ingest, `t` being the event as staged in LDS; returns the call flags it raises
+// (kFlag*). The row store is done by the caller (the whole wave's rows at once, coalesced).
 //
-// Memory-level parallelism: after the event's own 128-byte load, the three table lookups (id,
-// debit account, credit account) run side by side in two rounds -- the home-slot words, then the
-// id claim (one CAS) together with the account rows those words name -- instead of three
-// dependent probe loops.
+// Memory-level parallelism: the id claim (one CAS at the home slot, no preceding load) and the two
+// account-index loads are independent and issue together; the common event pays one round trip.
 __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_transfer_t>& c,
-                                            uint32_t k) {
+                                            uint32_t k, const tb_transfer_t& t, uint32_t b,
+                                            uint64_t ts_event, bool prev_linked) {
     bool imported = false, post_void = false, dup = false, closable = false, hot = false;
-    {
-        // One 128-byte vector load of the event; every field below comes from registers.
-        tb_transfer_t t;
-        {
-            const uint4* src = reinterpret_cast<const uint4*>(&c.events[k]);
-            uint4* dst = reinterpret_cast<uint4*>(&t);
-#pragma unroll
-            for (int i = 0; i < 8; i++) dst[i] = src[i];
+    const uint16_t f = t.flags;
+    imported = (f & TB_TRANSFER_IMPORTED) != 0;
+    post_void = (f & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) != 0;
+    const tb_uint128_t id = t.id;
+    const bool valid_id = !u128_is_zero(id) && !u128_is_max(id);
+    const uint32_t bstart = batch_start_of(c, b);
+    const bool chain = (f & TB_TRANSFER_LINKED) || (k > bstart && prev_linked);
+
+    uint32_t status = 0;
+    uint64_t ts_out = ts_event;
+    uint8_t info = 0, cls = kClassSlow;
+    bool pre_done = false;
+    if (!chain && !c.force_replay) {
+        // execute_create's per-event checks before create_transfer (:3052-3081) and the
+        // checks before the id lookup (:3729-3733): independent of every table.
+        const bool batch_imported = (c.events[bstart].flags & TB_TRANSFER_IMPORTED) != 0;
+        if (batch_imported != imported) {
+            status = imported ? TB_CT_IMPORTED_EVENT_NOT_EXPECTED : TB_CT_IMPORTED_EVENT_EXPECTED;
+            pre_done = true;
+        } else if (!imported && t.timestamp != 0) {
+            status = TB_CT_TIMESTAMP_MUST_BE_ZERO;
+            pre_done = true;
+        } else if (!imported && (f & TB_TRANSFER_PADDING_MASK)) {
+            status = TB_CT_RESERVED_FLAG;
+            pre_done = true;
+        } else if (!imported && !valid_id) {
+            status = u128_is_zero(id) ? TB_CT_ID_MUST_NOT_BE_ZERO : TB_CT_ID_MUST_NOT_BE_INT_MAX;
+            pre_done = true;
         }
-        const uint16_t f = t.flags;
-        imported = (f & TB_TRANSFER_IMPORTED) != 0;
-        post_void = (f & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) != 0;
-        const bool valid_id = !u128_is_zero(t.id) && !u128_is_max(t.id);
-        const bool dr_ok = !u128_is_zero(t.debit_account_id) && !u128_is_max(t.debit_account_id);
-        const bool cr_ok = !u128_is_zero(t.credit_account_id) && !u128_is_max(t.credit_account_id);
-
-        // Round 1: the home-slot words of the three ids (independent of the batch lookup).
-        const uint64_t s_id = hash_id(t.id) & T.tr.mask;
-        const uint64_t s_dr = hash_id(t.debit_account_id) & T.acc.mask;
-        const uint64_t s_cr = hash_id(t.credit_account_id) & T.acc.mask;
-        const uint64_t w_id = T.tr.slots[s_id];
-        const uint64_t w_dr = T.acc.slots[s_dr];
-        const uint64_t w_cr = T.acc.slots[s_cr];
-
-        const uint32_t b = batch_of_guess(c.batch_ends, c.n_batches, c.n, k);
-        const uint32_t bstart = batch_start_of(c, b);
-        const uint64_t ts_event = ts_event_of(c, b, k);
-        // The row store takes every event as it is, stamped (rows of events that do not create
-        // an object stay dead; an orphaned id keeps its key there).
-        {
-            tb_transfer_t o = t;
-            o.timestamp = ts_event;
-            const uint4* src = reinterpret_cast<const uint4*>(&o);
-            uint4* dst = reinterpret_cast<uint4*>(&T.tr_rows[c.row_base + k]);
-#pragma unroll
-            for (int i = 0; i < 8; i++) dst[i] = src[i];
-        }
-        const bool chain = (f & TB_TRANSFER_LINKED) ||
-                           (k > bstart && (c.events[k - 1].flags & TB_TRANSFER_LINKED));
-
-        uint32_t status = 0;
-        uint64_t ts_out = ts_event;
-        uint8_t info = 0, cls = kClassSlow;
-        bool pre_done = false;
-        if (!chain && !c.force_replay) {
-            // execute_create's per-event checks before create_transfer (:3052-3081) and the
-            // checks before the id lookup (:3729-3733): independent of every table.
-            const bool batch_imported = (c.events[bstart].flags & TB_TRANSFER_IMPORTED) != 0;
-            if (batch_imported != imported) {
-                status = imported ? TB_CT_IMPORTED_EVENT_NOT_EXPECTED : TB_CT_IMPORTED_EVENT_EXPECTED;
-                pre_done = true;
-            } else if (!imported && t.timestamp != 0) {
-                status = TB_CT_TIMESTAMP_MUST_BE_ZERO;
-                pre_done = true;
-            } else if (!imported && (f & TB_TRANSFER_PADDING_MASK)) {
-                status = TB_CT_RESERVED_FLAG;
-                pre_done = true;
-            } else if (!imported && !valid_id) {
-                status = u128_is_zero(t.id) ? TB_CT_ID_MUST_NOT_BE_ZERO : TB_CT_ID_MUST_NOT_BE_INT_MAX;
-                pre_done = true;
+    }
+    uint64_t slot = kNone;
+    AccSnap dr, cr;
+    dr.row = cr.row = kNone32;
+    if (pre_done) {
+        cls = kClassDone;
+    } else {
+        const tb_transfer_t* ev = c.events;
+        const tb_transfer_t* rows = T.tr_rows;
+        const uint64_t base = c.row_base;
+        const uint64_t tref = (base + k + 1) | id_tag(id);
+        const uint64_t s_id = hash_id(id) & T.tr.mask;
+        // The claim: a CAS at the home slot; only a taken home slot continues the probe.
+        uint64_t w_slot = tref;
+        if (valid_id) {
+            const uint64_t w_seen = atomicCAS(&T.tr.slots[s_id], (unsigned long long)kEmpty,
+                                              (unsigned long long)tref);
+            const tb_uint128_t dr_id = t.debit_account_id, cr_id = t.credit_account_id;
+            dr = acc_lookup_snap(T, dr_id, !u128_is_zero(dr_id) && !u128_is_max(dr_id), true);
+            cr = acc_lookup_snap(T, cr_id, !u128_is_zero(cr_id) && !u128_is_max(cr_id), false);
+            if (w_seen == kEmpty) {
+                slot = s_id;  // claimed
+            } else {
+                slot = probe_claim_from(T.tr, id, base + k + 1, base, [=](uint64_t r) {
+                    return r >= base ? ev[r - base].id : rows[r].id;
+                }, &dup, s_id, w_seen);
+                if (slot != kNone) w_slot = T.tr.slots[slot];
             }
-        }
-        uint64_t slot = kNone;
-        AccSnap dr, cr;
-        dr.row = cr.row = kNone32;
-        if (pre_done) {
-            cls = kClassDone;
+            if (slot == kNone) atomicOr(&T.scalars->flags, kFlagTableFull);
+            else info |= kInfoClaimed;
         } else {
-            const tb_transfer_t* ev = c.events;
-            const tb_transfer_t* rows = T.tr_rows;
-            const uint64_t base = c.row_base;
-            const uint64_t tref = (base + k + 1) | id_tag(t.id);
-            // Round 2: claim an empty home slot, and read the account rows the home slots name.
-            uint64_t w_seen = w_id;
-            if (valid_id && w_id == kEmpty)
-                w_seen = atomicCAS(&T.tr.slots[s_id], (unsigned long long)kEmpty,
-                                   (unsigned long long)tref);
-            const uint32_t dr_home = w_dr == kEmpty || w_dr == kTomb
-                                         ? 0u : uint32_t((w_dr & kRefMask) - 1);
-            const uint32_t cr_home = w_cr == kEmpty || w_cr == kTomb
-                                         ? 0u : uint32_t((w_cr & kRefMask) - 1);
-            const tb_account_t* pd = &T.acc_rows[dr_home];
-            const tb_account_t* pc = &T.acc_rows[cr_home];
-            const tb_uint128_t d_id = pd->id, c_id = pc->id;
-            const AccSnap d_home = acc_snap_load(pd, dr_home, true);
-            const AccSnap c_home = acc_snap_load(pc, cr_home, false);
-
-            uint64_t w_slot = tref;
-            if (valid_id) {
-                if (w_id == kEmpty && w_seen == kEmpty) {
-                    slot = s_id;  // claimed
-                } else {
-                    slot = probe_claim_from(T.tr, t.id, base + k + 1, base, [=](uint64_t r) {
-                        return r >= base ? ev[r - base].id : rows[r].id;
-                    }, &dup, s_id, w_seen);
-                    if (slot != kNone) w_slot = T.tr.slots[slot];
-                }
-                if (slot == kNone) atomicOr(&T.scalars->flags, kFlagTableFull);
-                else info |= kInfoClaimed;
-            }
-            dr = acc_resolve(T, t.debit_account_id, dr_ok, s_dr, w_dr, d_id, d_home, true);
-            cr = acc_resolve(T, t.credit_account_id, cr_ok, s_cr, w_cr, c_id, c_home, false);
-            // Accounts whose `closed` flag an event of this call may change.
-            if ((f & TB_TRANSFER_CLOSING_DEBIT) && dr.row != kNone32) {
-                T.acc_closable[dr.row] = c.epoch;
+            const tb_uint128_t dr_id = t.debit_account_id, cr_id = t.credit_account_id;
+            dr = acc_lookup_snap(T, dr_id, !u128_is_zero(dr_id) && !u128_is_max(dr_id), true);
+            cr = acc_lookup_snap(T, cr_id, !u128_is_zero(cr_id) && !u128_is_max(cr_id), false);
+        }
+        // Accounts whose `closed` flag an event of this call may change.
+        if ((f & TB_TRANSFER_CLOSING_DEBIT) && dr.row != kNone32) {
+            T.acc_closable[dr.row] = c.epoch;
+            closable = true;
+        }
+        if ((f & TB_TRANSFER_CLOSING_CREDIT) && cr.row != kNone32) {
+            T.acc_closable[cr.row] = c.epoch;
+            closable = true;
+        }
+        if ((f & TB_TRANSFER_VOID_PENDING) && !u128_is_zero(t.pending_id) &&
+            !u128_is_max(t.pending_id)) {
+            const uint64_t ps = transfer_slot_find(T, c, t.pending_id);
+            if (ps != kNone) {
+                const uint64_t pr = (T.tr.slots[ps] & kRefMask) - 1;
+                const tb_transfer_t& p = pr >= base ? ev[pr - base] : rows[pr];
+                const uint64_t pd_row = account_find(T, p.debit_account_id);
+                const uint64_t pc_row = account_find(T, p.credit_account_id);
+                if (pd_row != kNone) T.acc_closable[pd_row] = c.epoch;
+                if (pc_row != kNone) T.acc_closable[pc_row] = c.epoch;
                 closable = true;
             }
-            if ((f & TB_TRANSFER_CLOSING_CREDIT) && cr.row != kNone32) {
-                T.acc_closable[cr.row] = c.epoch;
-                closable = true;
-            }
-            if ((f & TB_TRANSFER_VOID_PENDING) && !u128_is_zero(t.pending_id) &&
-                !u128_is_max(t.pending_id)) {
-                const uint64_t ps = transfer_slot_find(T, c, t.pending_id);
-                if (ps != kNone) {
-                    const uint64_t pr = (T.tr.slots[ps] & kRefMask) - 1;
-                    const tb_transfer_t& p = pr >= base ? ev[pr - base] : rows[pr];
-                    const uint64_t pd_row = account_find(T, p.debit_account_id);
-                    const uint64_t pc_row = account_find(T, p.credit_account_id);
-                    if (pd_row != kNone) T.acc_closable[pd_row] = c.epoch;
-                    if (pc_row != kNone) T.acc_closable[pc_row] = c.epoch;
-                    closable = true;
-                }
-            }
-            if (!chain && !c.force_replay && !imported && slot != kNone) {
-                cls = classify_after_lookup(T, c, k, ts_event, t, w_slot, dr, cr, &status,
-                                            &ts_out, &info);
-            }
         }
-        info |= cls;
-        c.ev_info[k] = info;
-        c.ev_slot[k] = slot == kNone ? kNone32 : uint32_t(slot);
-        c.ev_dr[k] = dr.row;
-        c.ev_cr[k] = cr.row;
-        if (cls == kClassDone) {
-            tb_create_result_t res;
-            res.timestamp = status == TB_CT_EXISTS ? ts_out : ts_event;
-            res.status = status;
-            res.reserved = 0;
-            c.results[k] = res;
-        } else if (cls == kClassFast) {
-            // Speculative commit of the result (the row is already written); tr_commit confirms
-            // or demotes.
-            const uint64_t row = c.row_base + k;
-            T.tr_status[row] = (f & TB_TRANSFER_PENDING) ? TB_PENDING_PENDING : TB_PENDING_NONE;
-            c.ev_amount[k] = t.amount.lo;
-            tb_create_result_t res;
-            res.timestamp = ts_event;
-            res.status = TB_STATUS_CREATED;
-            res.reserved = 0;
-            c.results[k] = res;
-        } else {
-            // Accounts whose balances or flags an event executes on in order.
-            if (dr.row != kNone32) T.acc_hot[dr.row] = c.epoch;
-            if (cr.row != kNone32) T.acc_hot[cr.row] = c.epoch;
-            hot = dr.row != kNone32 || cr.row != kNone32;
+        if (!chain && !c.force_replay && !imported && slot != kNone) {
+            cls = classify_after_lookup(T, c, k, ts_event, t, w_slot, dr, cr, &status, &ts_out,
+                                        &info);
         }
+    }
+    info |= cls;
+    c.ev_info[k] = info;
+    c.ev_slot[k] = slot == kNone ? kNone32 : uint32_t(slot);
+    c.ev_dr[k] = dr.row;
+    c.ev_cr[k] = cr.row;
+    if (cls == kClassDone) {
+        tb_create_result_t res;
+        res.timestamp = status == TB_CT_EXISTS ? ts_out : ts_event;
+        res.status = status;
+        res.reserved = 0;
+        c.results[k] = res;
+    } else if (cls == kClassFast) {
+        // Speculative commit of the result (the row is already written); tr_commit confirms
+        // or demotes.
+        const uint64_t row = c.row_base + k;
+        T.tr_status[row] = (f & TB_TRANSFER_PENDING) ? TB_PENDING_PENDING : TB_PENDING_NONE;
+        c.ev_amount[k] = t.amount.lo;
+        tb_create_result_t res;
+        res.timestamp = ts_event;
+        res.status = TB_STATUS_CREATED;
+        res.reserved = 0;
+        c.results[k] = res;
+    } else {
+        // Accounts whose balances or flags an event executes on in order.
+        if (dr.row != kNone32) T.acc_hot[dr.row] = c.epoch;
+        if (cr.row != kNone32) T.acc_hot[cr.row] = c.epoch;
+        hot = dr.row != kNone32 || cr.row != kNone32;
     }
     return (imported ? kFlagImported : 0u) | (post_void ? kFlagPostVoid : 0u) |
            (dup ? kFlagDuplicate : 0u) | (closable ? kFlagClosable : 0u) | (hot ? kFlagHot : 0u);
 }
 
-__global__ void tr_ingest(Tables T, Call<tb_transfer_t> c) {
+// LDS image of a wave's 64 events: 144 bytes per event (128 + 16 of padding), so the lanes'
+// 16-byte field reads (one event per lane) fall on distinct banks.
+constexpr uint32_t kLdsEventStride = 144;
+constexpr uint32_t kIngestWaves = kBlock / 64;
+
+__device__ inline void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// tr_ingest: each wave takes 64 consecutive events at a time. The 8 KB of events arrive as 8
+// fully coalesced 16-byte loads per lane, are transposed through LDS so each lane reads its own
+// event's fields, and go back out as the transfer rows (timestamp patched) with 8 coalesced
+// stores. The next chunk's loads are issued before the current chunk's table work, so the event
+// stream overlaps the claim / index round trip.
+__global__ void __launch_bounds__(kBlock, 4) tr_ingest(Tables T, Call<tb_transfer_t> c) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds_ev[kIngestWaves][64 * kLdsEventStride];
+    __shared__ uint64_t lds_ts[kIngestWaves][64];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint8_t* my = lds_ev[wv];
+    const uint32_t nw = gridDim.x * kIngestWaves;
     unsigned int flags = 0;
-    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < c.n; k += gridDim.x * blockDim.x)
-        flags |= ingest_event(T, c, k);
+    uint4 q[8];
+    auto load_chunk = [&](uint32_t base) {
+        const uint4* src = reinterpret_cast<const uint4*>(c.events + base);
+        const uint32_t parts = (c.n - base < 64 ? c.n - base : 64) * 8;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const uint32_t idx = i * 64 + lane;
+            q[i] = idx < parts ? src[idx] : make_uint4(0, 0, 0, 0);
+        }
+    };
+    uint32_t base = (blockIdx.x * kIngestWaves + wv) * 64;
+    if (base < c.n) load_chunk(base);
+    for (; base < c.n; base += nw * 64) {
+        const uint32_t cnt = c.n - base < 64 ? c.n - base : 64;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const uint32_t e = i * 8 + (lane >> 3), part = lane & 7;
+            *reinterpret_cast<uint4*>(my + e * kLdsEventStride + part * 16) = q[i];
+        }
+        const uint32_t k = base + lane;
+        const bool active = lane < cnt;
+        uint32_t b = 0;
+        uint64_t ts_event = 0;
+        if (active) {
+            b = batch_of_guess(c.batch_ends, c.n_batches, c.n, k);
+            ts_event = ts_event_of(c, b, k);
+        }
+        lds_ts[wv][lane] = ts_event;
+        wave_lds_sync();
+        // The rows: the events as submitted, stamped with their commit timestamps (rows of
+        // events that do not create an object stay dead; an orphaned id keeps its key there).
+        uint4* dst = reinterpret_cast<uint4*>(T.tr_rows + c.row_base + base);
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const uint32_t idx = i * 64 + lane;
+            if (idx < cnt * 8) {
+                uint4 v = q[i];
+                if ((lane & 7) == 7) {
+                    const uint64_t ts = lds_ts[wv][i * 8 + (lane >> 3)];
+                    v.z = uint32_t(ts);
+                    v.w = uint32_t(ts >> 32);
+                }
+                dst[idx] = v;
+            }
+        }
+        if (active) {
+            const tb_transfer_t& t = *reinterpret_cast<const tb_transfer_t*>(my + lane * kLdsEventStride);
+            const bool prev_linked =
+                lane > 0 ? (reinterpret_cast<const tb_transfer_t*>(my + (lane - 1) * kLdsEventStride)
+                                ->flags & TB_TRANSFER_LINKED) != 0
+                         : (k > 0 && (c.events[k - 1].flags & TB_TRANSFER_LINKED) != 0);
+            flags |= ingest_event(T, c, k, t, b, ts_event, prev_linked);
+        }
+        const uint32_t next = base + nw * 64;
+        if (next < c.n) load_chunk(next);
+        wave_lds_sync();  // the LDS image is rewritten by the next chunk
+    }
     flags = block_reduce(flags, OpOr());
     if (threadIdx.x == 0 && flags) atomicOr(&T.scalars->flags, flags);
 }
@@ -441,8 +477,12 @@ __device__ inline void commit_event(const Tables& T, const Call<tb_transfer_t>& 
                     vals[2 * uint64_t(k)] = amount;
                     vals[2 * uint64_t(k) + 1] = amount;
                 } else if (amount) {
-                    atomic_add_u128(account_field(T.acc_rows, dr * 4 + (pending ? 0 : 1)), amount);
-                    atomic_add_u128(account_field(T.acc_rows, cr * 4 + (pending ? 2 : 3)), amount);
+                    if (atomic_add_u128(account_field(T.acc_rows, dr * 4 + (pending ? 0 : 1)),
+                                        amount) >= kHazardHiLimit)
+                        acc_hazard_set(T.acc_index, T.acc_entry_of, dr, kHazardHigh);
+                    if (atomic_add_u128(account_field(T.acc_rows, cr * 4 + (pending ? 2 : 3)),
+                                        amount) >= kHazardHiLimit)
+                        acc_hazard_set(T.acc_index, T.acc_entry_of, cr, kHazardHigh);
                 }
                 if (pending && (info & kInfoTimeout)) {
                     expiry_append(T, row, false);
@@ -518,14 +558,27 @@ __global__ void tr_commit(Tables T, Call<tb_transfer_t> c, uint32_t* keys, uint6
 constexpr uint32_t kReducePerLane = 16;
 constexpr uint32_t kReduceTile = kBlock * kReducePerLane;
 
-__device__ inline void add_field(tb_account_t* rows, uint32_t key, u128 sum, bool shared) {
+struct BalTarget {
+    tb_account_t* rows;
+    AccIndex index;
+    const uint32_t* entry_of;
+};
+
+__device__ inline void add_field(const BalTarget& B, uint32_t key, u128 sum, bool shared) {
     if (sum == 0) return;
-    tb_uint128_t* field = account_field(rows, key);
-    if (shared) atomic_add_u128(field, sum);
-    else *field = W(U(*field) + sum);
+    tb_uint128_t* field = account_field(B.rows, key);
+    uint64_t hi;
+    if (shared) {
+        hi = atomic_add_u128(field, sum);
+    } else {
+        const tb_uint128_t v = W(U(*field) + sum);
+        *field = v;
+        hi = v.hi;
+    }
+    if (hi >= kHazardHiLimit) acc_hazard_set(B.index, B.entry_of, key >> 2, kHazardHigh);
 }
 
-__global__ void bal_reduce_tiles(tb_account_t* rows, const uint32_t* keys, const uint64_t* vals,
+__global__ void bal_reduce_tiles(BalTarget rows, const uint32_t* keys, const uint64_t* vals,
                                  uint64_t n, uint32_t sentinel) {
     __shared__ uint32_t first_key[kBlock], last_key[kBlock];
     __shared__ uint64_t first_lo[kBlock], first_hi[kBlock], last_lo[kBlock], last_hi[kBlock];
@@ -864,6 +917,22 @@ __global__ void acc_classify(Tables T, Call<tb_account_t> c) {
     count_stat(T.scalars, 3, k < c.n && cls == kClassDone && !created);
 }
 
+// The account index entries of the accounts a create_accounts call created (after its replay).
+__global__ void acc_index_build(Tables T, uint64_t row_base, uint32_t n) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const uint64_t row = row_base + k;
+    if (!T.acc_live[row]) return;
+    const tb_account_t& a = T.acc_rows[row];
+    const uint64_t s = acc_index_insert(T.acc_index, a.id, uint32_t(row), a.ledger,
+                                        uint16_t(a.flags & ~TB_ACCOUNT_CLOSED), acc_hazard_of(a));
+    if (s == kNone) {
+        atomicOr(&T.scalars->flags, kFlagTableFull);
+        return;
+    }
+    T.acc_entry_of[row] = uint32_t(s);
+}
+
 // ================================ pulse ======================================================
 
 // One lane per expires_at entry: drop entries that left the index (posted / voided / expired /
@@ -971,6 +1040,8 @@ __global__ void set_balances_kernel(Tables T, tb_uint128_t id, tb_uint128_t dp, 
     a->debits_posted = dpo;
     a->credits_pending = cp;
     a->credits_posted = cpo;
+    const uint16_t h = acc_hazard_of(*a);
+    if (h) acc_hazard_set(T.acc_index, T.acc_entry_of, r, h);
     *rc = 0;
 }
 

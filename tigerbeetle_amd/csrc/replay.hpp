@@ -56,7 +56,9 @@ constexpr uint64_t kUndoIndexMask = (1ull << 56) - 1;
 
 // Everything a kernel needs, passed by value.
 struct Tables {
-    IdTable acc;
+    IdTable acc;             // id -> row claims of create_accounts (in-call visibility)
+    AccIndex acc_index;      // id -> {row, ledger, flags, hazard} of committed accounts
+    uint32_t* acc_entry_of;  // row -> its acc_index entry (0xFFFFFFFF until indexed)
     tb_account_t* acc_rows;
     uint8_t* acc_live;
     uint32_t* acc_hot;       // epoch of the last call that routed an event of this account to replay
@@ -162,10 +164,9 @@ __device__ inline bool ts_index_contains(const uint64_t* idx, uint64_t n, uint64
 // ---- account lookup (accounts do not change during a create_transfers call) ----------------
 
 __device__ inline uint64_t account_find(const Tables& T, const tb_uint128_t& id) {
-    const tb_account_t* rows = T.acc_rows;
-    uint64_t s = probe_find(T.acc, id, [=](uint64_t r) { return rows[r].id; });
-    if (s == kNone) return kNone;
-    return (T.acc.slots[s] & kRefMask) - 1;
+    AccEntry e;
+    if (acc_index_find(T.acc_index, id, &e) == kNone) return kNone;
+    return e.ref - 1;
 }
 
 // ---- the replay state -------------------------------------------------------------------------
@@ -232,6 +233,9 @@ struct Replay {
     __device__ void update_account(uint64_t row, const tb_account_t& next) {
         log_account(row);
         T.acc_rows[row] = next;
+        // A rollback restores the row but keeps the hazard bits: they only over-approximate.
+        const uint16_t h = acc_hazard_of(next);
+        if (h) acc_hazard_set(T.acc_index, T.acc_entry_of, row, h);
     }
     __device__ void update_status(uint64_t row, uint8_t status) {
         log_status(row);

@@ -1,0 +1,17 @@
+#!/bin/bash
+# One GPU call: parity tests, a bench line and a kernel-trace profile of the bench.
+# Usage (from the repo root, via gpurun): bash tools/gpu_check.sh <tag> [bench args...]
+set -o pipefail
+tag=${1:-run}; shift
+out=gpurun_out/$tag
+mkdir -p $out
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+    > $out/gpu_tests.log 2>&1 || { tail -30 $out/gpu_tests.log; exit 1; }
+tail -3 $out/gpu_tests.log
+timeout -k 10 300 python -u bench.py "$@" > $out/bench.json 2> $out/bench.err || { cat $out/bench.err; exit 1; }
+cat $out/bench.json
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$out/prof -o run -- \
+    python3 $GRAFT_REPO_ROOT/bench.py --no-cpu-baseline "$@" > $GRAFT_REPO_ROOT/$out/prof_bench.json 2>&1 || exit 1
+cd $GRAFT_REPO_ROOT && find $out/prof -name "*kernel_stats.csv" -exec cp {} $out/kernel_stats.csv \;
+cut -d, -f1-4 $out/kernel_stats.csv | cut -c1-160 | head -12

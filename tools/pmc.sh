@@ -1,0 +1,21 @@
+#!/bin/bash
+# PMC passes over a short bench run, one counter group per rocprofv3 run (MI355X_MICROARCH.md
+# "rocprofv3 PMC slots": FETCH_SIZE and WRITE_SIZE cannot share a pass).
+# Usage (repo root, via gpurun): bash tools/pmc.sh <tag> [bench args...]
+set -o pipefail
+tag=${1:-pmc}; shift
+R=$GRAFT_REPO_ROOT
+out=$R/gpurun_out/$tag
+mkdir -p $out
+export TMPDIR=/tmp
+cd /tmp
+args="--no-cpu-baseline --no-validate --steps 2 --warmup 1 $*"
+i=0
+for ctrs in "FETCH_SIZE" "WRITE_SIZE" \
+            "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" \
+            "TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE GRBM_COUNT"; do
+    i=$((i+1))
+    timeout -s KILL 120 rocprofv3 --pmc $ctrs --output-format csv -d $out/p$i -o run -- \
+        python3 $R/bench.py $args > $out/p$i.log 2>&1 || { echo "pass $i ($ctrs) failed"; tail -5 $out/p$i.log; exit 1; }
+done
+cd $R && python3 tools/pmc_summary.py $out > $out/summary.txt && cat $out/summary.txt
