@@ -42,14 +42,15 @@ BATCH = 8189           # Operation.create_transfers.event_max (src/tigerbeetle.z
 # fields the kernel must read or write for its function, counted once.
 KERNEL_BYTES_PER_EVENT = {
     # event 128 R, id-key claim 16, transfer row 128 W, result 16 W, per-event record 21 W
-    "tr_ingest": 128 + 16 + 128 + 16 + 21,
-    # record 21 R + result timestamp 8 R, liveness 1 W, 2 balance items 24 W (the id-slot
-    # re-check reads only when ingest saw a duplicate id)
-    "tr_commit": 21 + 8 + 1 + 24,
-    # 2 items x (4 B key + 8 B amount), read and written once
-    "bal_sort": 2 * 12 * 2,
+    # (slot, rows, amount, info), 2 packed balance items 16 W, liveness + pending status 2 W
+    "tr_ingest": 128 + 16 + 128 + 16 + 21 + 16 + 2,
+    # re-validation pass (skipped when ingest raised no commit flag): record 21 R, result
+    # timestamp 8 R, liveness 1 W
+    "tr_commit": 21 + 8 + 1,
+    # 2 packed u64 items, read and written once
+    "bal_sort": 2 * 8 * 2,
     # sorted items read once (account rows are per distinct account)
-    "bal_reduce": 2 * 12,
+    "bal_reduce": 2 * 8,
 }
 
 

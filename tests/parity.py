@@ -139,6 +139,15 @@ class Pair:
         self._maybe_pulse()
         return r_orc
 
+    def set_balances(self, account_id, dp=0, dpo=0, cp=0, cpo=0):
+        """Debug balance setter on both sides (the reference's table harness `setup`)."""
+        U = native.U128.of
+        a = self.lib.tbg_debug_set_account_balances(self.g, U(account_id), U(dp), U(dpo), U(cp),
+                                                    U(cpo))
+        b = self.olib.tbo_set_account_balances(self.o, U(account_id), U(dp), U(dpo), U(cp),
+                                               U(cpo))
+        assert a == 0 and b == 0, (a, b)
+
     def pulse_next(self):
         a = self.lib.tbg_pulse_next_timestamp(self.g)
         b = self.olib.tbo_pulse_next_timestamp(self.o)

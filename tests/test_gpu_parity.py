@@ -110,7 +110,8 @@ def _transfers(rows):
     for i, r in enumerate(rows):
         for k, v in r.items():
             if k in ("id", "debit_account_id", "credit_account_id", "pending_id", "amount"):
-                t[k][i, 0] = v
+                t[k][i, 0] = v & ((1 << 64) - 1)
+                t[k][i, 1] = v >> 64
             else:
                 t[k][i] = v
     return t
@@ -139,6 +140,47 @@ def test_reopened_account_with_limit(force_replay):
             dict(id=22, debit_account_id=3, credit_account_id=1, amount=100, ledger=1, code=1),
         ]))
         assert list(r["status"]) == [0xFFFFFFFF, 54, 0xFFFFFFFF]  # 54: exceeds_credits
+        p.compare_state()
+    finally:
+        p.close()
+
+
+@pytest.mark.parametrize("force_replay", [False, True], ids=["parallel", "replay"])
+def test_account_index_hazards(force_replay):
+    """The account index answers the create_transfers checks without the row while an account's
+    hazard bits are clear; every way an account becomes closed or gets a balance near 2^128 must
+    set them: created closed, closed by a replayed closing transfer (seen by the next call),
+    balances set to 2^127 (overflow checks)."""
+    p = Pair(account_capacity=64, transfer_capacity=1024, batch_events_max=256,
+             force_replay=force_replay)
+    try:
+        acc = workload.accounts(6, seed=2, ledger=1)
+        acc["flags"] = [32, 0, 0, 0, 0, 0]  # A created closed; B, C, D, E, F plain
+        p.create_accounts(acc)
+        r = p.create_transfers(_transfers([
+            dict(id=100, debit_account_id=2, credit_account_id=1, amount=5, ledger=1, code=1),
+            dict(id=101, debit_account_id=3, credit_account_id=4, amount=7, ledger=1, code=1,
+                 flags=2 | 64),                                                 # closes C (debit)
+            dict(id=102, debit_account_id=2, credit_account_id=4, amount=9, ledger=1, code=1),
+        ]))
+        assert list(r["status"]) == [66, 0xFFFFFFFF, 0xFFFFFFFF]
+        r = p.create_transfers(_transfers([
+            dict(id=110, debit_account_id=3, credit_account_id=2, amount=1, ledger=1, code=1),
+            dict(id=111, debit_account_id=2, credit_account_id=3, amount=1, ledger=1, code=1),
+            dict(id=112, debit_account_id=2, credit_account_id=4, amount=1, ledger=1, code=1),
+        ]))
+        assert list(r["status"]) == [65, 66, 0xFFFFFFFF]
+        p.set_balances(5, dpo=1 << 127)
+        p.set_balances(6, cp=(1 << 128) - 10)
+        r = p.create_transfers(_transfers([
+            dict(id=120, debit_account_id=5, credit_account_id=2, amount=1 << 127 | 1,
+                 ledger=1, code=1),
+            dict(id=121, debit_account_id=2, credit_account_id=6, amount=20, ledger=1, code=1,
+                 flags=2),
+            dict(id=122, debit_account_id=5, credit_account_id=2, amount=3, ledger=1, code=1),
+            dict(id=123, debit_account_id=4, credit_account_id=6, amount=3, ledger=1, code=1),
+        ]))
+        assert r["status"][0] != 0xFFFFFFFF and r["status"][1] != 0xFFFFFFFF
         p.compare_state()
     finally:
         p.close()

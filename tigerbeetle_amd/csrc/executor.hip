@@ -63,11 +63,9 @@ struct tbg_ctx {
     uint8_t* ev_info = nullptr;
     uint8_t* ev_slow = nullptr;
     uint32_t* slow_list = nullptr;
-    // balance items (2 per event) and their sorted copies
-    uint32_t* bal_keys = nullptr;
-    uint64_t* bal_vals = nullptr;
-    uint32_t* bal_keys_sorted = nullptr;
-    uint64_t* bal_vals_sorted = nullptr;
+    // balance items (2 per event, packed u64) and their sorted copy
+    uint64_t* bal_items = nullptr;
+    uint64_t* bal_items_sorted = nullptr;
     void* cub_temp = nullptr;
     size_t cub_temp_bytes = 0;
 
@@ -225,7 +223,8 @@ Call<Event> make_call(tbg_ctx* ctx, const Event* d_events, uint32_t n, const uin
     c.row_base = row_base;
     c.epoch = ++ctx->epoch;
     c.force_replay = ctx->force_replay ? 1 : 0;
-    { const char* e = getenv("TBG_ABLATE"); c.ablate = e ? uint32_t(atoi(e)) : 0; }
+    c.bal_items = nullptr;
+    c.key_bits = 0;
     c.ev_slot = ctx->ev_slot;
     c.ev_dr = ctx->ev_dr;
     c.ev_cr = ctx->ev_cr;
@@ -364,11 +363,11 @@ int64_t lookup_impl(tbg_ctx* ctx, const tb_uint128_t* ids, uint32_t n, void* out
     if (!ctx) return TBG_EINVAL;
     if (n == 0) return 0;
     if (n > ctx->opt.batch_events_max) return TBG_EINVAL;
-    // Scratch: ids and output rows in d_events; rows in bal_vals; found flags in ev_slow.
+    // Scratch: ids and output rows in d_events; rows in bal_items; found flags in ev_slow.
     HIP_TRY(ctx, hipMemcpyAsync(ctx->d_events, ids, size_t(n) * 16, hipMemcpyHostToDevice,
                                 ctx->stream));
     const tb_uint128_t* d_ids = reinterpret_cast<const tb_uint128_t*>(ctx->d_events);
-    uint64_t* d_rows = ctx->bal_vals;
+    uint64_t* d_rows = ctx->bal_items;
     if (accounts)
         hipLaunchKernelGGL(lookup_accounts_kernel, dim3(grid_for(n)), dim3(kBlock), 0, ctx->stream,
                            ctx->T, d_ids, n, d_rows, ctx->ev_slow);
@@ -443,13 +442,9 @@ tbg_ctx* tbg_open(const tbg_options* options) {
          dev_alloc(ctx, &ctx->ev_cr, ev_max, false) && dev_alloc(ctx, &ctx->ev_amount, ev_max, false) &&
          dev_alloc(ctx, &ctx->ev_info, ev_max, false) && dev_alloc(ctx, &ctx->ev_slow, ev_max, false) &&
          dev_alloc(ctx, &ctx->slow_list, ev_max, false);
-    if (ev_max >= kSortThreshold)
-        ok = ok && dev_alloc(ctx, &ctx->bal_keys, 2 * ev_max, false) &&
-             dev_alloc(ctx, &ctx->bal_vals, 2 * ev_max, false) &&
-             dev_alloc(ctx, &ctx->bal_keys_sorted, 2 * ev_max, false) &&
-             dev_alloc(ctx, &ctx->bal_vals_sorted, 2 * ev_max, false);
-    else
-        ok = ok && dev_alloc(ctx, &ctx->bal_vals, ev_max, false);  // lookup scratch
+    // (2 * ev_max items, at least ev_max u64 of lookup scratch)
+    ok = ok && dev_alloc(ctx, &ctx->bal_items, 2 * ev_max, false);
+    if (ev_max >= kSortThreshold) ok = ok && dev_alloc(ctx, &ctx->bal_items_sorted, 2 * ev_max, false);
     ok = ok && dev_alloc(ctx, &ctx->acc_ts_index, acc_cap, false) &&
          dev_alloc(ctx, &ctx->tr_ts_index, tr_cap, false) &&
          dev_alloc(ctx, &ctx->sel_buf, std::max(acc_cap, tr_cap), false);
@@ -487,7 +482,7 @@ void tbg_close(tbg_ctx* ctx) {
                     ctx->T.tr_status, ctx->T.expiry, ctx->d_scalars, ctx->T.undo, ctx->d_events,
                     ctx->d_results, ctx->d_batch_ends, ctx->d_batch_ts, ctx->ev_slot, ctx->ev_dr,
                     ctx->ev_cr, ctx->ev_amount, ctx->ev_info, ctx->ev_slow, ctx->slow_list,
-                    ctx->bal_keys, ctx->bal_vals, ctx->bal_keys_sorted, ctx->bal_vals_sorted,
+                    ctx->bal_items, ctx->bal_items_sorted,
                     ctx->cub_temp, ctx->acc_ts_index, ctx->tr_ts_index, ctx->sel_buf,
                     ctx->pulse.keep, ctx->pulse.exp, ctx->pulse.ts, ctx->pulse.rows,
                     ctx->pulse.exp_b, ctx->pulse.rows_b, ctx->pulse.counters};
@@ -520,39 +515,46 @@ int tbg_create_transfers_device(tbg_ctx* ctx, const tb_transfer_t* d_events, uin
     const dim3 grid(std::min(grid_for(n), kMaxGrid)), block(kBlock);  // grid-stride kernels
     uint32_t ig = grid.x;
     { const char* e = getenv("TBG_INGEST_GRID"); if (e) ig = std::min(grid_for(n), uint32_t(atoi(e))); }
-    const bool use_sort = n >= kSortThreshold && ctx->bal_keys;
-    const uint32_t sentinel = uint32_t(4 * ctx->T.acc_rows_used);
+    const bool use_sort = n >= kSortThreshold && ctx->bal_items_sorted;
+    // Balance items pack (amount << key_bits) | field key into a u64; the all-ones key is the
+    // "no item" sentinel, so key_bits covers 4 * accounts + 1 values. The key sits in the low
+    // bits: rocPRIM (ROCm 7.2) radix-sorts u64 keys wrongly for begin_bit > 0 with end_bit = 64
+    // on its small-input path (tools/sorttest.hip: 200k items, bits [48, 64)).
+    const uint32_t key_end = uint32_t(4 * ctx->T.acc_rows_used);
+    uint32_t key_bits = 1;
+    while ((1ull << key_bits) <= key_end) key_bits++;
+    if (use_sort) {
+        c.bal_items = ctx->bal_items;
+        c.key_bits = key_bits;
+    }
     if (!rc) {
         hipLaunchKernelGGL(tr_ingest, dim3(ig), block, 0, ctx->stream, ctx->T, c);
         tmark(ctx, "tr_ingest");
-        hipLaunchKernelGGL(tr_commit, grid, block, 0, ctx->stream, ctx->T, c, ctx->bal_keys,
-                           ctx->bal_vals, use_sort ? 1 : 0, sentinel);
+        hipLaunchKernelGGL(tr_commit, grid, block, 0, ctx->stream, ctx->T, c);
         tmark(ctx, "tr_commit");
         rc = hip_ok(ctx, hipGetLastError(), "launch") ? 0 : TBG_EHIP;
     }
     if (!rc && use_sort) {
-        // Balance deltas: sort (account field, amount) items by field, reduce runs in u128.
-        int end_bit = 1;
-        while ((1ull << end_bit) <= sentinel) end_bit++;
+        // Balance deltas: sort the packed items by field key, reduce runs in u128.
         const int items = int(2 * uint64_t(n));
         size_t bytes = 0;
-        rc = hip_ok(ctx, hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, ctx->bal_keys,
-                                                            ctx->bal_keys_sorted, ctx->bal_vals,
-                                                            ctx->bal_vals_sorted, items, 0, end_bit,
-                                                            ctx->stream), "sort size") ? 0 : TBG_EHIP;
+        rc = hip_ok(ctx, hipcub::DeviceRadixSort::SortKeys(nullptr, bytes, ctx->bal_items,
+                                                           ctx->bal_items_sorted, items, 0,
+                                                           int(key_bits), ctx->stream), "sort size")
+                 ? 0 : TBG_EHIP;
         if (!rc) rc = ensure_cub_temp(ctx, bytes);
         if (!rc)
-            rc = hip_ok(ctx, hipcub::DeviceRadixSort::SortPairs(
-                                 ctx->cub_temp, bytes, ctx->bal_keys, ctx->bal_keys_sorted,
-                                 ctx->bal_vals, ctx->bal_vals_sorted, items, 0, end_bit,
-                                 ctx->stream), "sort") ? 0 : TBG_EHIP;
+            rc = hip_ok(ctx, hipcub::DeviceRadixSort::SortKeys(ctx->cub_temp, bytes, ctx->bal_items,
+                                                               ctx->bal_items_sorted, items,
+                                                               0, int(key_bits), ctx->stream), "sort")
+                     ? 0 : TBG_EHIP;
         tmark(ctx, "bal_sort");
         if (!rc) {
             const uint64_t tiles = (uint64_t(items) + kReduceTile - 1) / kReduceTile;
             const BalTarget target{ctx->T.acc_rows, ctx->T.acc_index, ctx->T.acc_entry_of};
             hipLaunchKernelGGL(bal_reduce_tiles, dim3(uint32_t(tiles)), block, 0, ctx->stream,
-                               target, ctx->bal_keys_sorted, ctx->bal_vals_sorted,
-                               uint64_t(items), sentinel);
+                               target, ctx->bal_items_sorted, uint64_t(items), key_bits,
+                               key_end);
             tmark(ctx, "bal_reduce");
             rc = hip_ok(ctx, hipGetLastError(), "launch") ? 0 : TBG_EHIP;
         }

@@ -225,8 +225,10 @@ __device__ inline uint8_t classify_after_lookup(const Tables& T, const Call<tb_t
 // account-index loads are independent and issue together; the common event pays one round trip.
 __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_transfer_t>& c,
                                             uint32_t k, const tb_transfer_t& t, uint32_t b,
-                                            uint64_t ts_event, bool prev_linked) {
+                                            uint64_t ts_event, bool prev_linked,
+                                            uint64_t* fast_ts) {
     bool imported = false, post_void = false, dup = false, closable = false, hot = false;
+    bool need_commit = false;
     const uint16_t f = t.flags;
     imported = (f & TB_TRANSFER_IMPORTED) != 0;
     post_void = (f & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) != 0;
@@ -330,24 +332,51 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
         res.reserved = 0;
         c.results[k] = res;
     } else if (cls == kClassFast) {
-        // Speculative commit of the result (the row is already written); tr_commit confirms
-        // or demotes.
+        // Speculative commit (the row is already written): status, liveness, result and the
+        // balance items. tr_commit confirms or demotes when the call raised a commit flag.
         const uint64_t row = c.row_base + k;
-        T.tr_status[row] = (f & TB_TRANSFER_PENDING) ? TB_PENDING_PENDING : TB_PENDING_NONE;
-        c.ev_amount[k] = t.amount.lo;
+        const bool pending = (f & TB_TRANSFER_PENDING) != 0;
+        T.tr_status[row] = pending ? TB_PENDING_PENDING : TB_PENDING_NONE;
+        T.tr_live[row] = 1;
+        const uint64_t amount = t.amount.lo;
+        c.ev_amount[k] = amount;
         tb_create_result_t res;
         res.timestamp = ts_event;
         res.status = TB_STATUS_CREATED;
         res.reserved = 0;
         c.results[k] = res;
+        if (pending && t.timeout > 0) need_commit = true;  // expires_at index
+        if (c.bal_items) {
+            uint64_t* it = c.bal_items + 2 * uint64_t(k);
+            if ((amount >> (64 - c.key_bits)) == 0) {
+                it[0] = (amount << c.key_bits) | (dr.row * 4 + (pending ? 0 : 1));
+                it[1] = (amount << c.key_bits) | (cr.row * 4 + (pending ? 2 : 3));
+            } else {
+                it[0] = ~0ull;  // too wide to pack: u128 atomics in tr_commit
+                it[1] = ~0ull;
+                need_commit = true;
+            }
+        } else {
+            need_commit = true;  // unsorted calls: u128 atomics in tr_commit
+        }
+        *fast_ts = ts_event;
     } else {
         // Accounts whose balances or flags an event executes on in order.
         if (dr.row != kNone32) T.acc_hot[dr.row] = c.epoch;
         if (cr.row != kNone32) T.acc_hot[cr.row] = c.epoch;
         hot = dr.row != kNone32 || cr.row != kNone32;
     }
+    if (cls != kClassFast) {
+        need_commit = true;
+        if (c.bal_items) {
+            uint64_t* it = c.bal_items + 2 * uint64_t(k);
+            it[0] = ~0ull;
+            it[1] = ~0ull;
+        }
+    }
     return (imported ? kFlagImported : 0u) | (post_void ? kFlagPostVoid : 0u) |
-           (dup ? kFlagDuplicate : 0u) | (closable ? kFlagClosable : 0u) | (hot ? kFlagHot : 0u);
+           (dup ? kFlagDuplicate : 0u) | (closable ? kFlagClosable : 0u) | (hot ? kFlagHot : 0u) |
+           (need_commit ? kFlagNeedCommit : 0u);
 }
 
 // LDS image of a wave's 64 events: 144 bytes per event (128 + 16 of padding), so the lanes'
@@ -373,6 +402,7 @@ __global__ void __launch_bounds__(kBlock, 4) tr_ingest(Tables T, Call<tb_transfe
     uint8_t* my = lds_ev[wv];
     const uint32_t nw = gridDim.x * kIngestWaves;
     unsigned int flags = 0;
+    uint64_t n_fast = 0, ts_max = 0;
     uint4 q[8];
     auto load_chunk = [&](uint32_t base) {
         const uint4* src = reinterpret_cast<const uint4*>(c.events + base);
@@ -424,14 +454,23 @@ __global__ void __launch_bounds__(kBlock, 4) tr_ingest(Tables T, Call<tb_transfe
                 lane > 0 ? (reinterpret_cast<const tb_transfer_t*>(my + (lane - 1) * kLdsEventStride)
                                 ->flags & TB_TRANSFER_LINKED) != 0
                          : (k > 0 && (c.events[k - 1].flags & TB_TRANSFER_LINKED) != 0);
-            flags |= ingest_event(T, c, k, t, b, ts_event, prev_linked);
+            uint64_t fts = 0;
+            flags |= ingest_event(T, c, k, t, b, ts_event, prev_linked, &fts);
+            n_fast += fts != 0;
+            ts_max = fts > ts_max ? fts : ts_max;
         }
         const uint32_t next = base + nw * 64;
         if (next < c.n) load_chunk(next);
         wave_lds_sync();  // the LDS image is rewritten by the next chunk
     }
     flags = block_reduce(flags, OpOr());
-    if (threadIdx.x == 0 && flags) atomicOr(&T.scalars->flags, flags);
+    n_fast = block_reduce(n_fast, OpAdd());
+    ts_max = block_reduce(ts_max, OpMax());
+    if (threadIdx.x == 0) {
+        if (flags) atomicOr(&T.scalars->flags, flags);
+        if (n_fast) atomicAdd(&T.scalars->spec_fast, (unsigned long long)n_fast);
+        if (ts_max) atomicMax(&T.scalars->spec_ts_max, (unsigned long long)ts_max);
+    }
 }
 
 // Balance-delta item: key = account_row * 4 + field (0 dp, 1 dpo, 2 cp, 3 cpo).
@@ -442,96 +481,101 @@ __device__ inline tb_uint128_t* account_field(tb_account_t* rows, uint32_t key) 
 
 // One event of tr_commit: applied (committed FAST), done (final DONE), ts_applied (its timestamp).
 __device__ inline void commit_event(const Tables& T, const Call<tb_transfer_t>& c, uint32_t k,
-                                    unsigned int call_flags, uint32_t* keys, uint64_t* vals,
-                                    int use_sort, uint32_t sentinel, bool& applied, bool& done,
+                                    unsigned int call_flags, bool& applied, bool& done,
                                     bool& slow_out, uint64_t& ts_applied) {
     applied = false;
     done = false;
     slow_out = false;
     ts_applied = 0;
-    {
-        const uint8_t info = c.ev_info[k];
-        const uint8_t cls = info & kInfoClassMask;
-        const uint64_t row = c.row_base + k;
-        const uint64_t ref = row + 1;
-        bool slow = cls == kClassSlow || (call_flags & kFlagImported);
-        if (!slow && cls == kClassFast) {
+    const uint8_t info = c.ev_info[k];
+    const uint8_t cls = info & kInfoClassMask;
+    const uint64_t row = c.row_base + k;
+    const uint64_t ref = row + 1;
+    bool slow = cls == kClassSlow || (call_flags & kFlagImported);
+    if (cls == kClassFast) {
+        const uint32_t s = c.ev_slot[k];
+        const uint32_t dr = c.ev_dr[k], cr = c.ev_cr[k];
+        // Each re-check reads only when ingest raised the flag that can make it fail.
+        if (slow ||
+            ((call_flags & kFlagDuplicate) && (T.tr.slots[s] & kRefMask) != ref) ||
+            ((call_flags & kFlagClosable) &&
+             (T.acc_closable[dr] == c.epoch || T.acc_closable[cr] == c.epoch)) ||
+            ((call_flags & kFlagHot) && (T.acc_hot[dr] == c.epoch || T.acc_hot[cr] == c.epoch)) ||
+            ((info & kInfoPending) && (info & kInfoTimeout) && (call_flags & kFlagPostVoid))) {
+            // Demoted: undo the speculative liveness and balance items; the replay decides.
+            slow = true;
+            T.tr_live[row] = 0;
+            if (c.bal_items) {
+                uint64_t* it = c.bal_items + 2 * uint64_t(k);
+                it[0] = ~0ull;
+                it[1] = ~0ull;
+            }
+        } else {
+            applied = true;
+            ts_applied = c.results[k].timestamp;
+            const bool pending = (info & kInfoPending) != 0;
+            const uint64_t amount = c.ev_amount[k];
+            if (amount && (!c.bal_items || (amount >> (64 - c.key_bits)) != 0)) {
+                if (atomic_add_u128(account_field(T.acc_rows, dr * 4 + (pending ? 0 : 1)),
+                                    amount) >= kHazardHiLimit)
+                    acc_hazard_set(T.acc_index, T.acc_entry_of, dr, kHazardHigh);
+                if (atomic_add_u128(account_field(T.acc_rows, cr * 4 + (pending ? 2 : 3)),
+                                    amount) >= kHazardHiLimit)
+                    acc_hazard_set(T.acc_index, T.acc_entry_of, cr, kHazardHigh);
+            }
+            if (pending && (info & kInfoTimeout)) {
+                expiry_append(T, row, false);
+                const uint64_t timeout = T.tr_rows[row].timeout;
+                atomicMin(&T.scalars->pulse_next_timestamp,
+                          (unsigned long long)(ts_applied + timeout * TB_NS_PER_S));
+            }
+        }
+    } else if (!slow && cls == kClassDone) {
+        done = true;
+        if (info & kInfoPostLookup) {
             const uint32_t s = c.ev_slot[k];
             const uint32_t dr = c.ev_dr[k], cr = c.ev_cr[k];
-            // Each re-check reads only when ingest raised the flag that can make it fail.
-            if (((call_flags & kFlagDuplicate) && (T.tr.slots[s] & kRefMask) != ref) ||
-                ((call_flags & kFlagClosable) &&
-                 (T.acc_closable[dr] == c.epoch || T.acc_closable[cr] == c.epoch)) ||
-                ((call_flags & kFlagHot) && (T.acc_hot[dr] == c.epoch || T.acc_hot[cr] == c.epoch)) ||
-                ((info & kInfoPending) && (info & kInfoTimeout) && (call_flags & kFlagPostVoid))) {
+            if ((call_flags & kFlagDuplicate) && (T.tr.slots[s] & kRefMask) != ref) {
+                slow = true;  // a later duplicate: its outcome follows the earlier event's
+            } else if ((info & kInfoClosedDep) && (call_flags & kFlagClosable) &&
+                       (T.acc_closable[dr] == c.epoch || T.acc_closable[cr] == c.epoch)) {
                 slow = true;
             } else {
-                applied = true;
-                ts_applied = c.results[k].timestamp;
-                T.tr_live[row] = 1;
-                const bool pending = (info & kInfoPending) != 0;
-                const uint64_t amount = c.ev_amount[k];
-                if (use_sort) {
-                    keys[2 * uint64_t(k)] = dr * 4 + (pending ? 0 : 1);
-                    keys[2 * uint64_t(k) + 1] = cr * 4 + (pending ? 2 : 3);
-                    vals[2 * uint64_t(k)] = amount;
-                    vals[2 * uint64_t(k) + 1] = amount;
-                } else if (amount) {
-                    if (atomic_add_u128(account_field(T.acc_rows, dr * 4 + (pending ? 0 : 1)),
-                                        amount) >= kHazardHiLimit)
-                        acc_hazard_set(T.acc_index, T.acc_entry_of, dr, kHazardHigh);
-                    if (atomic_add_u128(account_field(T.acc_rows, cr * 4 + (pending ? 2 : 3)),
-                                        amount) >= kHazardHiLimit)
-                        acc_hazard_set(T.acc_index, T.acc_entry_of, cr, kHazardHigh);
-                }
-                if (pending && (info & kInfoTimeout)) {
-                    expiry_append(T, row, false);
-                    const uint64_t timeout = T.tr_rows[row].timeout;
-                    atomicMin(&T.scalars->pulse_next_timestamp,
-                              (unsigned long long)(ts_applied + timeout * TB_NS_PER_S));
-                }
-            }
-        } else if (!slow && cls == kClassDone) {
-            done = true;
-            if (info & kInfoPostLookup) {
-                const uint32_t s = c.ev_slot[k];
-                const uint32_t dr = c.ev_dr[k], cr = c.ev_cr[k];
-                if ((call_flags & kFlagDuplicate) && (T.tr.slots[s] & kRefMask) != ref) {
-                    slow = true;  // a later duplicate: its outcome follows the earlier event's
-                } else if ((info & kInfoClosedDep) && (call_flags & kFlagClosable) &&
-                           (T.acc_closable[dr] == c.epoch || T.acc_closable[cr] == c.epoch)) {
-                    slow = true;
+                // transient_error (:3215-3252): the id stays taken (orphan); else released.
+                if (tb_transfer_status_transient(c.results[k].status)) {
+                    T.tr_rows[row].id = c.events[k].id;
+                    T.tr.slots[s] |= kOrphanBit;
                 } else {
-                    // transient_error (:3215-3252): the id stays taken (orphan); else released.
-                    if (tb_transfer_status_transient(c.results[k].status)) {
-                        T.tr_rows[row].id = c.events[k].id;
-                        T.tr.slots[s] |= kOrphanBit;
-                    } else {
-                        T.tr.slots[s] = kTomb;
-                    }
+                    T.tr.slots[s] = kTomb;
                 }
             }
-            if (slow) done = false;
-            else T.tr_live[row] = 0;
         }
-        if (!applied && use_sort) {
-            keys[2 * uint64_t(k)] = sentinel;
-            keys[2 * uint64_t(k) + 1] = sentinel;
-        }
-        c.ev_slow[k] = slow;
-        slow_out = slow;
+        if (slow) done = false;
+        else T.tr_live[row] = 0;
     }
+    c.ev_slow[k] = slow;
+    slow_out = slow;
 }
 
-__global__ void tr_commit(Tables T, Call<tb_transfer_t> c, uint32_t* keys, uint64_t* vals,
-                          int use_sort, uint32_t sentinel) {
+// tr_commit: when ingest raised no commit flag, every event is a confirmed FAST event whose
+// effects ingest already wrote; only the call's counters remain (from ingest's speculative
+// ones). Otherwise every event is re-validated.
+__global__ void tr_commit(Tables T, Call<tb_transfer_t> c) {
     const unsigned int call_flags = T.scalars->flags;
+    if (!(call_flags & kCommitFlags)) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            const unsigned long long ts = T.scalars->spec_ts_max;
+            if (ts > T.scalars->transfers_key_max) T.scalars->transfers_key_max = ts;
+            T.scalars->stats[1] += T.scalars->spec_fast;
+        }
+        return;
+    }
     uint64_t n_applied = 0, n_done = 0, n_slow = 0, ts_max = 0;
     for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < c.n;
          k += gridDim.x * blockDim.x) {
         bool applied, done, slow;
         uint64_t ts;
-        commit_event(T, c, k, call_flags, keys, vals, use_sort, sentinel, applied, done, slow, ts);
+        commit_event(T, c, k, call_flags, applied, done, slow, ts);
         n_applied += applied;
         n_done += done;
         n_slow += slow;
@@ -551,7 +595,8 @@ __global__ void tr_commit(Tables T, Call<tb_transfer_t> c, uint32_t* keys, uint6
 }
 
 // Sorted balance items -> u128 sums added to the account fields, one tile of kReduceTile items
-// per block. Each lane reduces 16 consecutive items (vector loads); lane-edge runs are merged in
+// per block. An item is (amount << key_bits) | field key; keys >= key_end are the "no item"
+// sentinel. Each lane reduces 16 consecutive items (vector loads); lane-edge runs are merged in
 // order through LDS by lane 0. A run that touches neither tile edge is owned by this block: plain
 // read-modify-write. The tile's first and last runs may continue in a neighbour tile: u128 atomics
 // (at most two per tile).
@@ -578,61 +623,56 @@ __device__ inline void add_field(const BalTarget& B, uint32_t key, u128 sum, boo
     if (hi >= kHazardHiLimit) acc_hazard_set(B.index, B.entry_of, key >> 2, kHazardHigh);
 }
 
-__global__ void bal_reduce_tiles(BalTarget rows, const uint32_t* keys, const uint64_t* vals,
-                                 uint64_t n, uint32_t sentinel) {
+__global__ void bal_reduce_tiles(BalTarget rows, const uint64_t* items, uint64_t n,
+                                 uint32_t key_bits, uint32_t key_end) {
     __shared__ uint32_t first_key[kBlock], last_key[kBlock];
     __shared__ uint64_t first_lo[kBlock], first_hi[kBlock], last_lo[kBlock], last_hi[kBlock];
     __shared__ uint8_t single[kBlock];
+    const uint64_t kmask = (1ull << key_bits) - 1;
     const uint64_t tile = uint64_t(blockIdx.x) * kReduceTile;
     const uint64_t begin = tile + uint64_t(threadIdx.x) * kReducePerLane;
     const uint64_t tile_end = tile + kReduceTile < n ? tile + kReduceTile : n;
-    uint32_t fk = sentinel, lk = sentinel;
+    uint32_t fk = key_end, lk = key_end;
     u128 fs = 0, ls = 0;
     bool one = true;
     if (begin < tile_end) {
         const uint64_t end = begin + kReducePerLane < tile_end ? begin + kReducePerLane : tile_end;
-        uint32_t k_items[kReducePerLane];
-        uint64_t v_items[kReducePerLane];
+        uint64_t it[kReducePerLane];
         if (end - begin == kReducePerLane) {
-            const uint4* kp = reinterpret_cast<const uint4*>(keys + begin);
-            const uint4* vp = reinterpret_cast<const uint4*>(vals + begin);
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                uint4 q = kp[i];
-                k_items[4 * i] = q.x; k_items[4 * i + 1] = q.y;
-                k_items[4 * i + 2] = q.z; k_items[4 * i + 3] = q.w;
-            }
+            const uint4* p = reinterpret_cast<const uint4*>(items + begin);
 #pragma unroll
             for (int i = 0; i < 8; i++) {
-                uint4 q = vp[i];
-                v_items[2 * i] = (uint64_t(q.y) << 32) | q.x;
-                v_items[2 * i + 1] = (uint64_t(q.w) << 32) | q.z;
+                uint4 q = p[i];
+                it[2 * i] = (uint64_t(q.y) << 32) | q.x;
+                it[2 * i + 1] = (uint64_t(q.w) << 32) | q.z;
             }
         } else {
 #pragma unroll
-            for (int i = 0; i < (int)kReducePerLane; i++) {
-                k_items[i] = begin + i < end ? keys[begin + i] : sentinel;
-                v_items[i] = begin + i < end ? vals[begin + i] : 0;
-            }
+            for (int i = 0; i < (int)kReducePerLane; i++) it[i] = begin + i < end ? items[begin + i] : ~0ull;
         }
-        uint32_t cur = k_items[0];
+        auto key_of = [&](uint64_t x) {
+            const uint64_t kk = x & kmask;
+            return kk < key_end ? uint32_t(kk) : key_end;
+        };
+        uint32_t cur = key_of(it[0]);
         u128 sum = 0;
         bool first_run = true;
 #pragma unroll
         for (int i = 0; i < (int)kReducePerLane; i++) {
-            if (k_items[i] != cur) {
+            const uint32_t kk = key_of(it[i]);
+            if (kk != cur) {
                 if (first_run) {
                     fk = cur;
                     fs = sum;
                     first_run = false;
                     one = false;
-                } else if (cur < sentinel) {
+                } else if (cur < key_end) {
                     add_field(rows, cur, sum, false);  // interior run of this lane: owned
                 }
-                cur = k_items[i];
+                cur = kk;
                 sum = 0;
             }
-            sum += v_items[i];
+            sum += it[i] >> key_bits;
         }
         if (first_run) {
             fk = cur;
@@ -659,7 +699,7 @@ __global__ void bal_reduce_tiles(BalTarget rows, const uint32_t* keys, const uin
         const uint32_t f = first_key[t];
         const u128 fsum = ((u128)first_hi[t] << 64) | first_lo[t];
         if (f != open) {
-            if (open < sentinel) add_field(rows, open, acc, open_shared);
+            if (open < key_end) add_field(rows, open, acc, open_shared);
             open = f;
             acc = 0;
             open_shared = false;
@@ -667,14 +707,14 @@ __global__ void bal_reduce_tiles(BalTarget rows, const uint32_t* keys, const uin
         acc += fsum;
         if (!single[t]) {
             // The lane's first run ends inside the lane; its last run opens.
-            if (open < sentinel) add_field(rows, open, acc, open_shared);
+            if (open < key_end) add_field(rows, open, acc, open_shared);
             open = last_key[t];
             acc = ((u128)last_hi[t] << 64) | last_lo[t];
             open_shared = false;
         }
     }
     // The tile's last run may continue into the next tile.
-    if (open < sentinel) add_field(rows, open, acc, true);
+    if (open < key_end) add_field(rows, open, acc, true);
 }
 
 // ================================ the ordered replay ========================================

@@ -31,7 +31,9 @@ struct DevScalars {
     unsigned long long expiry_count;       // entries in the expires_at list
     unsigned int flags;                    // per call: kFlag*
     unsigned int slow_count;               // per call: events in the replay list
-    unsigned long long stats[4];           // per call: events, fast, replayed, static
+    unsigned long long stats[4];           // per call: slow, fast, replayed, static
+    unsigned long long spec_fast;          // per call: FAST events as ingest classified them
+    unsigned long long spec_ts_max;        // per call: their largest timestamp
 };
 
 enum : unsigned int {
@@ -42,7 +44,11 @@ enum : unsigned int {
     kFlagDuplicate = 1u << 4,  // two events of the call carry the same id
     kFlagHot = 1u << 5,        // some account is marked hot (a SLOW event touches it)
     kFlagClosable = 1u << 6,   // some account is marked closable
+    kFlagNeedCommit = 1u << 7, // some event is not a plain FAST event (tr_commit must run)
 };
+// Call flags under which tr_commit re-validates (and may demote) ingest's FAST events.
+constexpr unsigned int kCommitFlags = kFlagImported | kFlagPostVoid | kFlagDuplicate | kFlagHot |
+                                      kFlagClosable | kFlagNeedCommit;
 
 enum : uint8_t { kClassDone = 0, kClassFast = 1, kClassSlow = 2 };
 
@@ -95,7 +101,6 @@ struct Call {
     uint64_t row_base;
     uint32_t epoch;
     uint32_t force_replay;
-    uint32_t ablate;  // perf experiments only (TBG_ABLATE): bits skip parts of tr_ingest
     // per-event scratch (structure of arrays; kNone32 = absent)
     uint32_t* ev_slot;     // slot of the event's id in the id table
     uint32_t* ev_dr;       // account rows (create_transfers)
@@ -104,6 +109,10 @@ struct Call {
     uint8_t* ev_info;      // kInfo* bits
     uint8_t* ev_slow;      // 1 = executes in the ordered replay
     const uint32_t* slow_list;
+    // Balance items of FAST events (create_transfers, sorted calls): item 2k / 2k+1 = the debit /
+    // credit delta of event k, packed as (amount << key_bits) | account field key; ~0 = none.
+    uint64_t* bal_items;
+    uint32_t key_bits;
 };
 
 constexpr uint32_t kNone32 = 0xFFFFFFFFu;
