@@ -47,10 +47,14 @@ KERNEL_BYTES_PER_EVENT = {
     # re-validation pass (skipped when ingest raised no commit flag): record 21 R, result
     # timestamp 8 R, liveness 1 W
     "tr_commit": 21 + 8 + 1,
-    # 2 packed u64 items, read and written once
+    # 2 packed u64 items, read and written once (large key spaces)
     "bal_sort": 2 * 8 * 2,
     # sorted items read once (account rows are per distinct account)
     "bal_reduce": 2 * 8,
+    # bucketed path (small key spaces): items read + written into their buckets
+    "bal_scatter": 2 * 8 * 2,
+    # bucketed items read once (slice partials are per bucket key, not per event)
+    "bal_accumulate": 2 * 8,
 }
 
 

@@ -63,6 +63,42 @@ def test_uniform_config2_small():
         p.close()
 
 
+def test_sort_path_large_key_space():
+    """More than 262,144 accounts: balance items take the radix sort + run reduction."""
+    p = Pair(account_capacity=1 << 19, transfer_capacity=1 << 18, batch_events_max=1 << 17)
+    try:
+        n_acc = 300_000
+        acc = workload.accounts(n_acc, seed=5)
+        for i in range(0, n_acc, 100_000):
+            p.create_accounts(acc[i:i + 100_000], [8189] * 12 + [100_000 - 12 * 8189])
+        t = workload.transfers_uniform(70_000, n_acc, seed=5)
+        r = p.create_transfers(t, [8189] * 8 + [70_000 - 8 * 8189])
+        assert (r["status"] == 0xFFFFFFFF).all()
+        t = workload.transfers_uniform(70_000, 1_000, seed=6, id_offset=70_000)
+        p.create_transfers(t, [35_000, 35_000])
+        p.compare_state()
+    finally:
+        p.close()
+
+
+def test_bucket_path_hot_skew():
+    """One call of >= 65,536 events over hot limited accounts: bucketed balances with 90% of
+    the items in one bucket, next to replayed limit checks."""
+    p = Pair(account_capacity=1 << 14, transfer_capacity=1 << 18, batch_events_max=1 << 17)
+    try:
+        acc = workload.accounts(6_000, seed=7)
+        acc["flags"][1:101] |= 2
+        p.create_accounts(acc)
+        p.create_transfers(workload.funding_transfers(100, 200_000, id_offset=10_000_000))
+        t = workload.transfers_hot_limits(80_000, n_accounts=6_000, n_hot=100, seed=7)
+        p.create_transfers(t, [8189] * 9 + [80_000 - 9 * 8189])
+        t = workload.transfers_uniform(70_000, 6_000, seed=8, id_offset=20_000_000)
+        p.create_transfers(t, [70_000])
+        p.compare_state()
+    finally:
+        p.close()
+
+
 def test_hot_limits_config3_small():
     """Config 3 shape at small scale: Zipfian hot accounts with debits_must_not_exceed_credits."""
     p = Pair(account_capacity=1 << 14, transfer_capacity=1 << 16, batch_events_max=1 << 15)

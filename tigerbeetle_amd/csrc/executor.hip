@@ -65,7 +65,10 @@ struct tbg_ctx {
     uint32_t* slow_list = nullptr;
     // balance items (2 per event, packed u64) and their sorted copy
     uint64_t* bal_items = nullptr;
-    uint64_t* bal_items_sorted = nullptr;
+    uint64_t* bal_items_sorted = nullptr;  // sorted (large key spaces) or bucketed items
+    unsigned int* bucket_words = nullptr;  // counts, cursors, offsets, slice bases
+    uint64_t* bucket_partials = nullptr;   // per slice: kBucketKeys partial sums
+    uint64_t bucket_slices_max = 0;
     void* cub_temp = nullptr;
     size_t cub_temp_bytes = 0;
 
@@ -225,6 +228,8 @@ Call<Event> make_call(tbg_ctx* ctx, const Event* d_events, uint32_t n, const uin
     c.force_replay = ctx->force_replay ? 1 : 0;
     c.bal_items = nullptr;
     c.key_bits = 0;
+    c.bucket_counts = nullptr;
+    c.n_buckets = 0;
     c.ev_slot = ctx->ev_slot;
     c.ev_dr = ctx->ev_dr;
     c.ev_cr = ctx->ev_cr;
@@ -444,7 +449,12 @@ tbg_ctx* tbg_open(const tbg_options* options) {
          dev_alloc(ctx, &ctx->slow_list, ev_max, false);
     // (2 * ev_max items, at least ev_max u64 of lookup scratch)
     ok = ok && dev_alloc(ctx, &ctx->bal_items, 2 * ev_max, false);
-    if (ev_max >= kSortThreshold) ok = ok && dev_alloc(ctx, &ctx->bal_items_sorted, 2 * ev_max, false);
+    if (ev_max >= kSortThreshold) {
+        ctx->bucket_slices_max = (2 * ev_max + kSliceItems - 1) / kSliceItems + kBucketsMax;
+        ok = ok && dev_alloc(ctx, &ctx->bal_items_sorted, 2 * ev_max, false) &&
+             dev_alloc(ctx, &ctx->bucket_words, 4 * (kBucketsMax + 1), true) &&
+             dev_alloc(ctx, &ctx->bucket_partials, ctx->bucket_slices_max * kBucketKeys, false);
+    }
     ok = ok && dev_alloc(ctx, &ctx->acc_ts_index, acc_cap, false) &&
          dev_alloc(ctx, &ctx->tr_ts_index, tr_cap, false) &&
          dev_alloc(ctx, &ctx->sel_buf, std::max(acc_cap, tr_cap), false);
@@ -482,7 +492,7 @@ void tbg_close(tbg_ctx* ctx) {
                     ctx->T.tr_status, ctx->T.expiry, ctx->d_scalars, ctx->T.undo, ctx->d_events,
                     ctx->d_results, ctx->d_batch_ends, ctx->d_batch_ts, ctx->ev_slot, ctx->ev_dr,
                     ctx->ev_cr, ctx->ev_amount, ctx->ev_info, ctx->ev_slow, ctx->slow_list,
-                    ctx->bal_items, ctx->bal_items_sorted,
+                    ctx->bal_items, ctx->bal_items_sorted, ctx->bucket_words, ctx->bucket_partials,
                     ctx->cub_temp, ctx->acc_ts_index, ctx->tr_ts_index, ctx->sel_buf,
                     ctx->pulse.keep, ctx->pulse.exp, ctx->pulse.ts, ctx->pulse.rows,
                     ctx->pulse.exp_b, ctx->pulse.rows_b, ctx->pulse.counters};
@@ -523,9 +533,25 @@ int tbg_create_transfers_device(tbg_ctx* ctx, const tb_transfer_t* d_events, uin
     const uint32_t key_end = uint32_t(4 * ctx->T.acc_rows_used);
     uint32_t key_bits = 1;
     while ((1ull << key_bits) <= key_end) key_bits++;
+    // Small key spaces (<= 262,144 accounts) take the bucketed path, whose LDS sums need
+    // amounts < 2^48 (key_bits >= 16); larger ones the radix sort + run reduction.
+    const bool use_buckets = use_sort && key_end <= kBucketsMax * kBucketKeys;
+    if (use_buckets && key_bits < 16) key_bits = 16;
+    BucketPlan plan{};
     if (use_sort) {
         c.bal_items = ctx->bal_items;
         c.key_bits = key_bits;
+    }
+    if (use_buckets && !rc) {
+        plan.counts = ctx->bucket_words;
+        plan.cursor = plan.counts + kBucketsMax;
+        plan.offset = plan.cursor + kBucketsMax;
+        plan.slice_base = plan.offset + kBucketsMax + 1;
+        plan.n_buckets = std::max<uint32_t>(1, (key_end + kBucketKeys - 1) / kBucketKeys);
+        c.bucket_counts = plan.counts;
+        c.n_buckets = plan.n_buckets;
+        rc = hip_ok(ctx, hipMemsetAsync(plan.counts, 0, kBucketsMax * sizeof(unsigned int),
+                                        ctx->stream), "memset") ? 0 : TBG_EHIP;
     }
     if (!rc) {
         hipLaunchKernelGGL(tr_ingest, dim3(ig), block, 0, ctx->stream, ctx->T, c);
@@ -534,9 +560,26 @@ int tbg_create_transfers_device(tbg_ctx* ctx, const tb_transfer_t* d_events, uin
         tmark(ctx, "tr_commit");
         rc = hip_ok(ctx, hipGetLastError(), "launch") ? 0 : TBG_EHIP;
     }
-    if (!rc && use_sort) {
+    const int items = int(2 * uint64_t(n));
+    const BalTarget target{ctx->T.acc_rows, ctx->T.acc_index, ctx->T.acc_entry_of};
+    if (!rc && use_buckets) {
+        // Balance deltas: bucket the packed items by key range, sum each slice in LDS, apply.
+        hipLaunchKernelGGL(bal_bucket_plan, dim3(1), dim3(64), 0, ctx->stream, plan);
+        hipLaunchKernelGGL(bal_bucket_scatter, dim3(uint32_t((items + kScatterTile - 1) / kScatterTile)),
+                           block, 0, ctx->stream, plan, ctx->bal_items, uint64_t(items), key_bits,
+                           key_end, ctx->bal_items_sorted);
+        tmark(ctx, "bal_scatter");
+        const uint32_t slices = uint32_t((uint64_t(items) + kSliceItems - 1) / kSliceItems) +
+                                plan.n_buckets;
+        hipLaunchKernelGGL(bal_bucket_accumulate, dim3(slices), block, 0, ctx->stream, plan,
+                           ctx->bal_items_sorted, key_bits, ctx->bucket_partials);
+        tmark(ctx, "bal_accumulate");
+        hipLaunchKernelGGL(bal_bucket_apply, dim3(grid_for(key_end)), block, 0, ctx->stream,
+                           target, plan, ctx->bucket_partials, key_end);
+        tmark(ctx, "bal_apply");
+        rc = hip_ok(ctx, hipGetLastError(), "launch") ? 0 : TBG_EHIP;
+    } else if (!rc && use_sort) {
         // Balance deltas: sort the packed items by field key, reduce runs in u128.
-        const int items = int(2 * uint64_t(n));
         size_t bytes = 0;
         rc = hip_ok(ctx, hipcub::DeviceRadixSort::SortKeys(nullptr, bytes, ctx->bal_items,
                                                            ctx->bal_items_sorted, items, 0,
@@ -551,10 +594,8 @@ int tbg_create_transfers_device(tbg_ctx* ctx, const tb_transfer_t* d_events, uin
         tmark(ctx, "bal_sort");
         if (!rc) {
             const uint64_t tiles = (uint64_t(items) + kReduceTile - 1) / kReduceTile;
-            const BalTarget target{ctx->T.acc_rows, ctx->T.acc_index, ctx->T.acc_entry_of};
             hipLaunchKernelGGL(bal_reduce_tiles, dim3(uint32_t(tiles)), block, 0, ctx->stream,
-                               target, ctx->bal_items_sorted, uint64_t(items), key_bits,
-                               key_end);
+                               target, ctx->bal_items_sorted, uint64_t(items), key_bits, key_end);
             tmark(ctx, "bal_reduce");
             rc = hip_ok(ctx, hipGetLastError(), "launch") ? 0 : TBG_EHIP;
         }

@@ -29,6 +29,15 @@ namespace tbg {
 
 constexpr int kBlock = 256;
 
+// Bucketed balance path: keys (account row * 4 + field) fall into buckets of 8192 consecutive
+// keys (2048 accounts); a call uses it when 4 * accounts <= kBucketsMax * 8192.
+constexpr uint32_t kBucketShift = 13;
+constexpr uint32_t kBucketKeys = 1u << kBucketShift;
+constexpr uint32_t kBucketsMax = 128;
+// Items per accumulate block: with key_bits >= 16 every packed amount is < 2^48, so a slice's
+// u64 LDS sums stay below 2^63.
+constexpr uint32_t kSliceItems = 32768;
+
 __device__ inline void count_stat(DevScalars* s, int which, bool pred) {
     unsigned long long mask = __ballot(pred);
     if ((threadIdx.x & 63) == 0 && mask)
@@ -226,7 +235,7 @@ __device__ inline uint8_t classify_after_lookup(const Tables& T, const Call<tb_t
 __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_transfer_t>& c,
                                             uint32_t k, const tb_transfer_t& t, uint32_t b,
                                             uint64_t ts_event, bool prev_linked,
-                                            uint64_t* fast_ts) {
+                                            uint64_t* fast_ts, unsigned int* bucket_hist) {
     bool imported = false, post_void = false, dup = false, closable = false, hot = false;
     bool need_commit = false;
     const uint16_t f = t.flags;
@@ -349,8 +358,14 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
         if (c.bal_items) {
             uint64_t* it = c.bal_items + 2 * uint64_t(k);
             if ((amount >> (64 - c.key_bits)) == 0) {
-                it[0] = (amount << c.key_bits) | (dr.row * 4 + (pending ? 0 : 1));
-                it[1] = (amount << c.key_bits) | (cr.row * 4 + (pending ? 2 : 3));
+                const uint32_t kd = dr.row * 4 + (pending ? 0 : 1);
+                const uint32_t kc = cr.row * 4 + (pending ? 2 : 3);
+                it[0] = (amount << c.key_bits) | kd;
+                it[1] = (amount << c.key_bits) | kc;
+                if (bucket_hist) {
+                    atomicAdd(&bucket_hist[kd >> kBucketShift], 1u);
+                    atomicAdd(&bucket_hist[kc >> kBucketShift], 1u);
+                }
             } else {
                 it[0] = ~0ull;  // too wide to pack: u128 atomics in tr_commit
                 it[1] = ~0ull;
@@ -398,7 +413,12 @@ __device__ inline void wave_lds_sync() {
 __global__ void __launch_bounds__(kBlock, 4) tr_ingest(Tables T, Call<tb_transfer_t> c) {
     __shared__ __attribute__((aligned(16))) uint8_t lds_ev[kIngestWaves][64 * kLdsEventStride];
     __shared__ uint64_t lds_ts[kIngestWaves][64];
+    __shared__ unsigned int bucket_hist[kBucketsMax];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (c.bucket_counts) {
+        for (uint32_t i = threadIdx.x; i < c.n_buckets; i += kBlock) bucket_hist[i] = 0;
+        __syncthreads();
+    }
     uint8_t* my = lds_ev[wv];
     const uint32_t nw = gridDim.x * kIngestWaves;
     unsigned int flags = 0;
@@ -455,7 +475,8 @@ __global__ void __launch_bounds__(kBlock, 4) tr_ingest(Tables T, Call<tb_transfe
                                 ->flags & TB_TRANSFER_LINKED) != 0
                          : (k > 0 && (c.events[k - 1].flags & TB_TRANSFER_LINKED) != 0);
             uint64_t fts = 0;
-            flags |= ingest_event(T, c, k, t, b, ts_event, prev_linked, &fts);
+            flags |= ingest_event(T, c, k, t, b, ts_event, prev_linked, &fts,
+                                  c.bucket_counts ? bucket_hist : nullptr);
             n_fast += fts != 0;
             ts_max = fts > ts_max ? fts : ts_max;
         }
@@ -463,9 +484,12 @@ __global__ void __launch_bounds__(kBlock, 4) tr_ingest(Tables T, Call<tb_transfe
         if (next < c.n) load_chunk(next);
         wave_lds_sync();  // the LDS image is rewritten by the next chunk
     }
-    flags = block_reduce(flags, OpOr());
+    flags = block_reduce(flags, OpOr());  // (its barriers also order the histogram adds)
     n_fast = block_reduce(n_fast, OpAdd());
     ts_max = block_reduce(ts_max, OpMax());
+    if (c.bucket_counts)
+        for (uint32_t i = threadIdx.x; i < c.n_buckets; i += kBlock)
+            if (bucket_hist[i]) atomicAdd(&c.bucket_counts[i], bucket_hist[i]);
     if (threadIdx.x == 0) {
         if (flags) atomicOr(&T.scalars->flags, flags);
         if (n_fast) atomicAdd(&T.scalars->spec_fast, (unsigned long long)n_fast);
@@ -715,6 +739,110 @@ __global__ void bal_reduce_tiles(BalTarget rows, const uint64_t* items, uint64_t
     }
     // The tile's last run may continue into the next tile.
     if (open < key_end) add_field(rows, open, acc, true);
+}
+
+// ---- the bucketed balance path ------------------------------------------------
+//
+// ingest counts the items per bucket (block histograms); bal_bucket_plan lays the buckets out
+// (offsets, cursors, slices of <= kSliceItems); bal_bucket_scatter moves the items into their
+// buckets (one cursor reservation per block and bucket); bal_bucket_accumulate sums one slice per
+// block in LDS (64-bit LDS atomics on 8192 keys) and writes the slice's partial sums;
+// bal_bucket_apply adds, per key, its bucket's partials in u128 to the account field.
+// Counts come from ingest and may exceed the items that survive tr_commit (demotions), so the
+// buckets' real ends are the cursors after the scatter.
+
+struct BucketPlan {
+    unsigned int* counts;   // [kBucketsMax] from ingest
+    unsigned int* cursor;   // [kBucketsMax] bucket fill positions
+    unsigned int* offset;   // [kBucketsMax + 1]
+    unsigned int* slice_base;  // [kBucketsMax + 1]
+    uint32_t n_buckets;
+};
+
+__global__ void bal_bucket_plan(BucketPlan P) {
+    if (threadIdx.x != 0) return;
+    unsigned int off = 0, sl = 0;
+    for (uint32_t b = 0; b < P.n_buckets; b++) {
+        P.offset[b] = off;
+        P.cursor[b] = off;
+        P.slice_base[b] = sl;
+        off += P.counts[b];
+        sl += (P.counts[b] + kSliceItems - 1) / kSliceItems;
+    }
+    P.offset[P.n_buckets] = off;
+    P.slice_base[P.n_buckets] = sl;
+}
+
+constexpr uint32_t kScatterPerLane = 16;
+constexpr uint32_t kScatterTile = kBlock * kScatterPerLane;
+
+__global__ void __launch_bounds__(kBlock) bal_bucket_scatter(BucketPlan P, const uint64_t* items,
+                                                             uint64_t n, uint32_t key_bits,
+                                                             uint32_t key_end, uint64_t* out) {
+    __shared__ unsigned int cnt[kBucketsMax], base[kBucketsMax];
+    for (uint32_t i = threadIdx.x; i < P.n_buckets; i += kBlock) cnt[i] = 0;
+    __syncthreads();
+    const uint64_t kmask = (1ull << key_bits) - 1;
+    const uint64_t begin = uint64_t(blockIdx.x) * kScatterTile + uint64_t(threadIdx.x) * kScatterPerLane;
+    uint64_t it[kScatterPerLane];
+    unsigned int pos[kScatterPerLane];
+    if (begin + kScatterPerLane <= n) {
+        const uint4* p = reinterpret_cast<const uint4*>(items + begin);
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const uint4 q = p[i];
+            it[2 * i] = (uint64_t(q.y) << 32) | q.x;
+            it[2 * i + 1] = (uint64_t(q.w) << 32) | q.z;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < (int)kScatterPerLane; i++) it[i] = begin + i < n ? items[begin + i] : ~0ull;
+    }
+#pragma unroll
+    for (int i = 0; i < (int)kScatterPerLane; i++) {
+        const uint64_t key = it[i] & kmask;
+        pos[i] = key < key_end ? atomicAdd(&cnt[key >> kBucketShift], 1u) : ~0u;
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < P.n_buckets; i += kBlock)
+        base[i] = cnt[i] ? atomicAdd(&P.cursor[i], cnt[i]) : 0;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < (int)kScatterPerLane; i++)
+        if (pos[i] != ~0u) out[base[(it[i] & kmask) >> kBucketShift] + pos[i]] = it[i];
+}
+
+__global__ void __launch_bounds__(kBlock) bal_bucket_accumulate(BucketPlan P, const uint64_t* bucketed,
+                                                                uint32_t key_bits, uint64_t* partials) {
+    __shared__ unsigned long long acc[kBucketKeys];
+    const uint32_t s = blockIdx.x;
+    if (s >= P.slice_base[P.n_buckets]) return;
+    uint32_t b = 0;
+    while (P.slice_base[b + 1] <= s) b++;
+    for (uint32_t i = threadIdx.x; i < kBucketKeys; i += kBlock) acc[i] = 0;
+    __syncthreads();
+    const uint64_t begin = uint64_t(P.offset[b]) + uint64_t(s - P.slice_base[b]) * kSliceItems;
+    const uint64_t filled = P.cursor[b];
+    const uint64_t end = begin + kSliceItems < filled ? begin + kSliceItems : filled;
+    const uint64_t kmask = (1ull << key_bits) - 1;
+    for (uint64_t j = begin + threadIdx.x; j < end; j += kBlock) {
+        const uint64_t x = bucketed[j];
+        atomicAdd(&acc[(x & kmask) & (kBucketKeys - 1)], (unsigned long long)(x >> key_bits));
+    }
+    __syncthreads();
+    uint64_t* out = partials + uint64_t(s) * kBucketKeys;
+    for (uint32_t i = threadIdx.x; i < kBucketKeys; i += kBlock) out[i] = acc[i];
+}
+
+__global__ void bal_bucket_apply(BalTarget B, BucketPlan P, const uint64_t* partials,
+                                 uint32_t key_end) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= key_end) return;
+    const uint32_t b = k >> kBucketShift, local = k & (kBucketKeys - 1);
+    u128 sum = 0;
+    for (uint32_t s = P.slice_base[b]; s < P.slice_base[b + 1]; s++)
+        sum += partials[uint64_t(s) * kBucketKeys + local];
+    add_field(B, k, sum, false);  // one thread per key: plain read-modify-write
 }
 
 // ================================ the ordered replay ========================================

@@ -113,6 +113,9 @@ struct Call {
     // credit delta of event k, packed as (amount << key_bits) | account field key; ~0 = none.
     uint64_t* bal_items;
     uint32_t key_bits;
+    // Bucketed balance path (small key spaces): per-bucket item counts, bucket = key >> 13.
+    unsigned int* bucket_counts;
+    uint32_t n_buckets;
 };
 
 constexpr uint32_t kNone32 = 0xFFFFFFFFu;
