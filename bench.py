@@ -41,9 +41,9 @@ BATCH = 8189           # Operation.create_transfers.event_max (src/tigerbeetle.z
 # Algorithmic bytes per event of each kernel of the create_transfers path: the
 # fields the kernel must read or write for its function, counted once.
 KERNEL_BYTES_PER_EVENT = {
-    # event 128 R, id-key claim 16, transfer row 128 W, result 16 W, per-event record 21 W
-    # (slot, rows, amount, info), 2 packed balance items 16 W, liveness + pending status 2 W
-    "tr_ingest": 128 + 16 + 128 + 16 + 21 + 16 + 2,
+    # event 128 R, id-key claim 16 (8-B slot read + write), transfer row 128 W, result 16 W,
+    # 2 packed balance items 16 W, info + liveness 2 W (FAST events write no other record)
+    "tr_ingest": 128 + 16 + 128 + 16 + 16 + 2,
     # re-validation pass (skipped when ingest raised no commit flag): record 21 R, result
     # timestamp 8 R, liveness 1 W
     "tr_commit": 21 + 8 + 1,

@@ -330,10 +330,16 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
         }
     }
     info |= cls;
-    c.ev_info[k] = info;
-    c.ev_slot[k] = slot == kNone ? kNone32 : uint32_t(slot);
-    c.ev_dr[k] = dr.row;
-    c.ev_cr[k] = cr.row;
+    // A FAST event whose balance items are packed needs no per-event record: tr_commit decodes
+    // the rows and amount from the items and re-probes the slot if it has to.
+    const bool lean = cls == kClassFast && c.bal_items &&
+                      (t.amount.lo >> (64 - c.key_bits)) == 0;
+    c.ev_info[k] = info | (lean ? kInfoLean : 0);
+    if (!lean) {
+        c.ev_slot[k] = slot == kNone ? kNone32 : uint32_t(slot);
+        c.ev_dr[k] = dr.row;
+        c.ev_cr[k] = cr.row;
+    }
     if (cls == kClassDone) {
         tb_create_result_t res;
         res.timestamp = status == TB_CT_EXISTS ? ts_out : ts_event;
@@ -345,10 +351,10 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
         // balance items. tr_commit confirms or demotes when the call raised a commit flag.
         const uint64_t row = c.row_base + k;
         const bool pending = (f & TB_TRANSFER_PENDING) != 0;
-        T.tr_status[row] = pending ? TB_PENDING_PENDING : TB_PENDING_NONE;
+        if (pending) T.tr_status[row] = TB_PENDING_PENDING;  // fresh rows read TB_PENDING_NONE
         T.tr_live[row] = 1;
         const uint64_t amount = t.amount.lo;
-        c.ev_amount[k] = amount;
+        if (!lean) c.ev_amount[k] = amount;
         tb_create_result_t res;
         res.timestamp = ts_event;
         res.status = TB_STATUS_CREATED;
@@ -517,11 +523,32 @@ __device__ inline void commit_event(const Tables& T, const Call<tb_transfer_t>& 
     const uint64_t ref = row + 1;
     bool slow = cls == kClassSlow || (call_flags & kFlagImported);
     if (cls == kClassFast) {
-        const uint32_t s = c.ev_slot[k];
-        const uint32_t dr = c.ev_dr[k], cr = c.ev_cr[k];
+        uint32_t s = kNone32, dr, cr;
+        uint64_t amount;
+        const bool lean = (info & kInfoLean) != 0;
+        if (lean) {
+            const uint64_t kmask = (1ull << c.key_bits) - 1;
+            const uint64_t* it = c.bal_items + 2 * uint64_t(k);
+            const uint64_t i0 = it[0], i1 = it[1];
+            dr = uint32_t((i0 & kmask) >> 2);
+            cr = uint32_t((i1 & kmask) >> 2);
+            amount = i0 >> c.key_bits;
+        } else {
+            s = c.ev_slot[k];
+            dr = c.ev_dr[k];
+            cr = c.ev_cr[k];
+            amount = c.ev_amount[k];
+        }
+        if (lean && (slow || (call_flags & kFlagDuplicate) || (call_flags & kFlagClosable) ||
+                     (call_flags & kFlagHot) || (call_flags & kFlagPostVoid))) {
+            // The slot this event's id occupies (its own claim, or an earlier in-call holder's).
+            const uint64_t fs = transfer_slot_find(T, c, c.events[k].id);
+            s = fs == kNone ? kNone32 : uint32_t(fs);
+        }
         // Each re-check reads only when ingest raised the flag that can make it fail.
         if (slow ||
-            ((call_flags & kFlagDuplicate) && (T.tr.slots[s] & kRefMask) != ref) ||
+            ((call_flags & kFlagDuplicate) &&
+             (s == kNone32 || (T.tr.slots[s] & kRefMask) != ref)) ||
             ((call_flags & kFlagClosable) &&
              (T.acc_closable[dr] == c.epoch || T.acc_closable[cr] == c.epoch)) ||
             ((call_flags & kFlagHot) && (T.acc_hot[dr] == c.epoch || T.acc_hot[cr] == c.epoch)) ||
@@ -534,11 +561,15 @@ __device__ inline void commit_event(const Tables& T, const Call<tb_transfer_t>& 
                 it[0] = ~0ull;
                 it[1] = ~0ull;
             }
+            if (lean) {  // the replay reads the record
+                c.ev_slot[k] = s;
+                c.ev_dr[k] = dr;
+                c.ev_cr[k] = cr;
+            }
         } else {
             applied = true;
             ts_applied = c.results[k].timestamp;
             const bool pending = (info & kInfoPending) != 0;
-            const uint64_t amount = c.ev_amount[k];
             if (amount && (!c.bal_items || (amount >> (64 - c.key_bits)) != 0)) {
                 if (atomic_add_u128(account_field(T.acc_rows, dr * 4 + (pending ? 0 : 1)),
                                     amount) >= kHazardHiLimit)
@@ -825,7 +856,17 @@ __global__ void __launch_bounds__(kBlock) bal_bucket_accumulate(BucketPlan P, co
     const uint64_t filled = P.cursor[b];
     const uint64_t end = begin + kSliceItems < filled ? begin + kSliceItems : filled;
     const uint64_t kmask = (1ull << key_bits) - 1;
-    for (uint64_t j = begin + threadIdx.x; j < end; j += kBlock) {
+    // 8 independent loads in flight per lane, then their LDS adds.
+    uint64_t j = begin + threadIdx.x;
+    for (; j + 7 * kBlock < end; j += 8 * kBlock) {
+        uint64_t x[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) x[i] = bucketed[j + i * kBlock];
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+            atomicAdd(&acc[(x[i] & kmask) & (kBucketKeys - 1)], (unsigned long long)(x[i] >> key_bits));
+    }
+    for (; j < end; j += kBlock) {
         const uint64_t x = bucketed[j];
         atomicAdd(&acc[(x & kmask) & (kBucketKeys - 1)], (unsigned long long)(x >> key_bits));
     }
@@ -840,8 +881,16 @@ __global__ void bal_bucket_apply(BalTarget B, BucketPlan P, const uint64_t* part
     if (k >= key_end) return;
     const uint32_t b = k >> kBucketShift, local = k & (kBucketKeys - 1);
     u128 sum = 0;
-    for (uint32_t s = P.slice_base[b]; s < P.slice_base[b + 1]; s++)
-        sum += partials[uint64_t(s) * kBucketKeys + local];
+    uint32_t s = P.slice_base[b];
+    const uint32_t s_end = P.slice_base[b + 1];
+    for (; s + 8 <= s_end; s += 8) {
+        uint64_t x[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) x[i] = partials[uint64_t(s + i) * kBucketKeys + local];
+#pragma unroll
+        for (int i = 0; i < 8; i++) sum += x[i];
+    }
+    for (; s < s_end; s++) sum += partials[uint64_t(s) * kBucketKeys + local];
     add_field(B, k, sum, false);  // one thread per key: plain read-modify-write
 }
 

@@ -128,6 +128,8 @@ enum : uint8_t {
     kInfoPending = 1 << 4,     // flags.pending
     kInfoTimeout = 1 << 5,     // timeout > 0
     kInfoClaimed = 1 << 6,     // the event claimed / found its id slot
+    kInfoLean = 1 << 7,        // FAST with packed balance items: ev_slot / ev_dr / ev_cr /
+                               // ev_amount were not written (the items hold rows and amount)
 };
 
 template <typename C>
