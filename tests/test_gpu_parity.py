@@ -220,3 +220,37 @@ def test_account_index_hazards(force_replay):
         p.compare_state()
     finally:
         p.close()
+
+
+@pytest.mark.parametrize("force_replay", [False, True], ids=["parallel", "replay"])
+def test_account_index_wide_entries(force_replay):
+    """Index entries hold an id's low word and a ledger's low 16 bits: accounts whose id high
+    word is nonzero or whose ledger is >= 2^16 are matched and checked through the row. Ids that
+    share a low word, and ledgers that share their low 16 bits, must stay distinct."""
+    p = Pair(account_capacity=64, transfer_capacity=1024, batch_events_max=256,
+             force_replay=force_replay)
+    try:
+        acc = workload.accounts(6, seed=3, ledger=1)
+        acc["id"][:, 0] = [7, 7, 7, 8, 9, 10]
+        acc["id"][:, 1] = [0, 1, 2, 0, 0, 0]
+        acc["ledger"] = [1, 1, 1, 65537, 65537, 1]
+        acc["flags"] = 0
+        p.create_accounts(acc)
+        hi = 1 << 64
+        r = p.create_transfers(_transfers([
+            dict(id=1, debit_account_id=7, credit_account_id=7 + hi, amount=5, ledger=1, code=1),
+            dict(id=2, debit_account_id=7 + 2 * hi, credit_account_id=7 + hi, amount=3, ledger=1,
+                 code=1),
+            dict(id=3, debit_account_id=7 + 3 * hi, credit_account_id=7, amount=1, ledger=1,
+                 code=1),                                                  # debit not found
+            dict(id=4, debit_account_id=8, credit_account_id=9, amount=2, ledger=65537, code=1),
+            dict(id=5, debit_account_id=8, credit_account_id=10, amount=2, ledger=65537,
+                 code=1),                                                  # different ledgers
+            dict(id=6, debit_account_id=8, credit_account_id=9, amount=2, ledger=1, code=1),
+            dict(id=7, debit_account_id=10, credit_account_id=7, amount=2, ledger=1, code=1),
+        ]))
+        created = r["status"] == 0xFFFFFFFF
+        assert created.tolist() == [True, True, False, True, False, False, True]
+        p.compare_state()
+    finally:
+        p.close()

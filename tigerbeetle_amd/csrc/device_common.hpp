@@ -190,29 +190,41 @@ __device__ inline uint64_t probe_claim(const IdTable& t, const tb_uint128_t& id,
 }
 
 // The account index: a read-mostly cache of the id -> row mapping together with what the
-// create_transfers checks read of an account, one 32-byte entry per account (4 per 128-byte line),
-// linear probing on a fully mixed hash. A lookup is one 32-byte load: the id compare, the row, the
-// ledger and the flags arrive together, so the common path never touches the 128-byte row.
+// create_transfers checks read of an account, in 16-byte entries, linear probing on a full mix of
+// the id, 4 entries per account of capacity (load <= 0.25). A probe step is one 16-byte load --
+// one L2 request and one texture-address slot per lane, the resources tr_ingest saturates
+// (SQ_INSTS_VMEM_RD, TA_BUSY in profiles/) -- carrying the id's low word, the row, the static
+// flags, the hazard bits and the ledger's low 16 bits: the common lookup never touches the
+// 128-byte row.
+//
+// An entry stands for its account's full id and ledger only while kHazardWide is clear (the id's
+// high word is 0 and the ledger < 2^16; static, set at insertion). A wide entry matches only after
+// comparing the row's id high word, and its readers take the ledger from the row.
 //
 // Entries are inserted when create_accounts calls finish (accounts never leave the index after
-// that) and are immutable except `hazard`, a conservative summary of the account's dynamic state
-// that is only ever set: bit kHazardClosed when the account may be closed, kHazardHigh when one of
-// its balances may have reached 2^126 (hi word >= 2^62). While hazard is zero the account is open
-// and no u128 balance can overflow within a call of < 2^32 events with amounts < 2^64; otherwise
-// the reader takes the row itself. Writers: create_accounts (closed accounts), the ordered replay
-// (update_account), balance application (bal_reduce, u128 atomics), debug balance setters.
+// that) and are immutable except the hazard bits, a conservative summary of the account's dynamic
+// state that is only ever set: kHazardClosed when the account may be closed, kHazardHigh when one
+// of its balances may have reached 2^126 (hi word >= 2^62). While no hazard bit is set the account
+// is open, its ledger fits the entry, and no u128 balance can overflow within a call of < 2^32
+// events with amounts < 2^64; otherwise the reader takes the row itself. Writers: create_accounts
+// (closed and wide accounts), the ordered replay (update_account), balance application
+// (bal_reduce_tiles, bal_bucket_apply, u128 atomics), debug balance setters.
 struct alignas(16) AccEntry {
-    tb_uint128_t id;   // 0: empty (an account id is never 0)
-    uint32_t ref;      // row + 1 (0: empty)
-    uint32_t ledger;
-    uint16_t flags;    // Account.flags at creation (`closed` is tracked by hazard)
-    uint16_t hazard;
-    uint32_t reserved;
+    uint64_t id_lo;
+    uint32_t ref;   // row + 1 (0: empty)
+    uint32_t meta;  // flags (bits 0-7; `closed` is tracked by hazard) | hazard (8-15) | ledger (16-31)
 };
-static_assert(sizeof(AccEntry) == 32, "AccEntry is 32 bytes");
+static_assert(sizeof(AccEntry) == 16, "AccEntry is 16 bytes");
 
-enum : uint16_t { kHazardClosed = 1, kHazardHigh = 2 };
+enum : uint16_t { kHazardClosed = 1, kHazardHigh = 2, kHazardWide = 4 };
 constexpr uint64_t kHazardHiLimit = 1ull << 62;
+
+__host__ __device__ inline uint32_t acc_meta(uint16_t flags, uint16_t hazard, uint32_t ledger) {
+    return (flags & 0xFFu) | (uint32_t(hazard & 0xFFu) << 8) | (ledger << 16);
+}
+__host__ __device__ inline uint16_t meta_flags(uint32_t m) { return uint16_t(m & 0xFFu); }
+__host__ __device__ inline uint16_t meta_hazard(uint32_t m) { return uint16_t((m >> 8) & 0xFFu); }
+__host__ __device__ inline uint32_t meta_ledger(uint32_t m) { return m >> 16; }
 
 __host__ __device__ inline uint64_t acc_entry_home(const tb_uint128_t& id) {
     return mix64(id.lo ^ mix64(id.hi ^ 0xD6E8FEB86659FD93ull));
@@ -223,23 +235,20 @@ struct AccIndex {
     uint64_t mask;
 };
 
-// One 32-byte load per probe step; returns the entry index or kNone.
-__device__ inline uint64_t acc_index_find(const AccIndex& x, const tb_uint128_t& id, AccEntry* out) {
+// One 16-byte load per probe step; returns the entry index (its contents in *out) or kNone.
+// `rows` resolves the high word of wide entries.
+__device__ inline uint64_t acc_index_find(const AccIndex& x, const tb_account_t* rows,
+                                          const tb_uint128_t& id, AccEntry* out) {
     if (u128_is_zero(id)) return kNone;
     uint64_t s = acc_entry_home(id) & x.mask;
     for (uint64_t n = 0; n <= x.mask; n++) {
-        const uint4* p = reinterpret_cast<const uint4*>(&x.entries[s]);
-        const uint4 a = p[0], b = p[1];
-        const uint64_t lo = (uint64_t(a.y) << 32) | a.x, hi = (uint64_t(a.w) << 32) | a.z;
-        if (b.x == 0) return kNone;  // empty
-        if (lo == id.lo && hi == id.hi) {
-            out->id.lo = lo;
-            out->id.hi = hi;
-            out->ref = b.x;
-            out->ledger = b.y;
-            out->flags = uint16_t(b.z);
-            out->hazard = uint16_t(b.z >> 16);
-            out->reserved = b.w;
+        const uint4 v = *reinterpret_cast<const uint4*>(&x.entries[s]);
+        if (v.z == 0) return kNone;  // empty
+        if (((uint64_t(v.y) << 32) | v.x) == id.lo &&
+            ((meta_hazard(v.w) & kHazardWide) ? rows[v.z - 1].id.hi == id.hi : id.hi == 0)) {
+            out->id_lo = id.lo;
+            out->ref = v.z;
+            out->meta = v.w;
             return s;
         }
         s = (s + 1) & x.mask;
@@ -249,15 +258,13 @@ __device__ inline uint64_t acc_index_find(const AccIndex& x, const tb_uint128_t&
 
 // Inserts a new id (the caller guarantees it is absent); returns the entry index or kNone.
 __device__ inline uint64_t acc_index_insert(const AccIndex& x, const tb_uint128_t& id, uint32_t row,
-                                            uint32_t ledger, uint16_t flags, uint16_t hazard) {
+                                            uint32_t meta) {
     uint64_t s = acc_entry_home(id) & x.mask;
     for (uint64_t n = 0; n <= x.mask; n++) {
         AccEntry* e = &x.entries[s];
         if (atomicCAS(&e->ref, 0u, row + 1) == 0u) {
-            e->id = id;
-            e->ledger = ledger;
-            e->flags = flags;
-            e->hazard = hazard;
+            e->id_lo = id.lo;
+            e->meta = meta;
             return s;
         }
         s = (s + 1) & x.mask;
@@ -269,9 +276,8 @@ __device__ inline void acc_hazard_set(const AccIndex& x, const uint32_t* entry_o
                                       uint16_t bits) {
     const uint32_t s = entry_of[row];
     if (s == 0xFFFFFFFFu) return;  // not indexed yet (an account of the running create_accounts)
-    // hazard is the high half of the 32-bit word at offset 24 (flags | hazard << 16).
-    unsigned int* w = reinterpret_cast<unsigned int*>(reinterpret_cast<uint8_t*>(&x.entries[s]) + 24);
-    if (!((*w >> 16) & bits)) atomicOr(w, (unsigned int)bits << 16);
+    unsigned int* w = &x.entries[s].meta;
+    if (((*w >> 8) & bits) != bits) atomicOr(w, (unsigned int)bits << 8);
 }
 
 // The hazard bits an account row warrants.
@@ -280,6 +286,7 @@ __device__ inline uint16_t acc_hazard_of(const tb_account_t& a) {
     if (a.debits_pending.hi >= kHazardHiLimit || a.debits_posted.hi >= kHazardHiLimit ||
         a.credits_pending.hi >= kHazardHiLimit || a.credits_posted.hi >= kHazardHiLimit)
         h |= kHazardHigh;
+    if (a.id.hi != 0 || a.ledger >= (1u << 16)) h |= kHazardWide;
     return h;
 }
 

@@ -425,7 +425,9 @@ tbg_ctx* tbg_open(const tbg_options* options) {
     // Slot tables hold at least 4 probe groups (hash_id / probe_next step 16 slots at a time).
     const uint64_t acc_slots = std::max<uint64_t>(next_pow2(acc_cap * 2), 64);
     const uint64_t tr_slots = std::max<uint64_t>(next_pow2(tr_cap * 2), 64);
-    const uint64_t acc_entries = std::max<uint64_t>(next_pow2(acc_cap * 2), 64);
+    // 4 index entries per account (entry indexes are u32: at most 2^31 entries).
+    const uint64_t acc_entries =
+        std::min<uint64_t>(std::max<uint64_t>(next_pow2(acc_cap * 4), 64), 1ull << 31);
     Tables& T = ctx->T;
     ok = ok && dev_alloc(ctx, &T.acc_index.entries, acc_entries, true) &&
          dev_alloc(ctx, &T.acc_entry_of, acc_cap, false) &&

@@ -117,10 +117,10 @@ __device__ inline AccSnap acc_snap_load(const tb_account_t* a, uint32_t row, boo
     return s;
 }
 
-// An account as the checks see it, from its index entry (one 32-byte load). An entry with no
-// hazard bit names an open account whose balances are all < 2^126: the snapshot is complete
-// without the row (balance hi words read as 0, which classify_after_lookup only compares with
-// 2^62). Otherwise the row is read.
+// An account as the checks see it, from its index entry (one 16-byte load per probe step). An
+// entry with no hazard bit names an open account whose balances are all < 2^126 and whose ledger
+// fits the entry: the snapshot is complete without the row (balance hi words read as 0, which
+// classify_after_lookup only compares with 2^62). Otherwise the row is read.
 __device__ inline AccSnap acc_lookup_snap(const Tables& T, const tb_uint128_t& id, bool valid,
                                           bool debit) {
     AccSnap a;
@@ -130,12 +130,12 @@ __device__ inline AccSnap acc_lookup_snap(const Tables& T, const tb_uint128_t& i
     a.hi_pending = a.hi_posted = 0;
     if (!valid) return a;
     AccEntry e;
-    if (acc_index_find(T.acc_index, id, &e) == kNone) return a;
+    if (acc_index_find(T.acc_index, T.acc_rows, id, &e) == kNone) return a;
     const uint32_t row = e.ref - 1;
-    if (e.hazard) return acc_snap_load(&T.acc_rows[row], row, debit);
+    if (meta_hazard(e.meta)) return acc_snap_load(&T.acc_rows[row], row, debit);
     a.row = row;
-    a.ledger = e.ledger;
-    a.flags = e.flags;
+    a.ledger = meta_ledger(e.meta);
+    a.flags = meta_flags(e.meta);
     return a;
 }
 
@@ -233,9 +233,10 @@ __device__ inline uint8_t classify_after_lookup(const Tables& T, const Call<tb_t
 // Memory-level parallelism: the id claim (one CAS at the home slot, no preceding load) and the two
 // account-index loads are independent and issue together; the common event pays one round trip.
 __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_transfer_t>& c,
-                                            uint32_t k, const tb_transfer_t& t, uint32_t b,
-                                            uint64_t ts_event, bool prev_linked,
-                                            uint64_t* fast_ts, unsigned int* bucket_hist) {
+                                            uint32_t k, const tb_transfer_t& t, uint32_t bstart,
+                                            bool batch_imported, uint64_t ts_event,
+                                            bool prev_linked, uint64_t* fast_ts,
+                                            unsigned int* bucket_hist) {
     bool imported = false, post_void = false, dup = false, closable = false, hot = false;
     bool need_commit = false;
     const uint16_t f = t.flags;
@@ -243,7 +244,6 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
     post_void = (f & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) != 0;
     const tb_uint128_t id = t.id;
     const bool valid_id = !u128_is_zero(id) && !u128_is_max(id);
-    const uint32_t bstart = batch_start_of(c, b);
     const bool chain = (f & TB_TRANSFER_LINKED) || (k > bstart && prev_linked);
 
     uint32_t status = 0;
@@ -253,7 +253,6 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
     if (!chain && !c.force_replay) {
         // execute_create's per-event checks before create_transfer (:3052-3081) and the
         // checks before the id lookup (:3729-3733): independent of every table.
-        const bool batch_imported = (c.events[bstart].flags & TB_TRANSFER_IMPORTED) != 0;
         if (batch_imported != imported) {
             status = imported ? TB_CT_IMPORTED_EVENT_NOT_EXPECTED : TB_CT_IMPORTED_EVENT_EXPECTED;
             pre_done = true;
@@ -362,19 +361,18 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
         c.results[k] = res;
         if (pending && t.timeout > 0) need_commit = true;  // expires_at index
         if (c.bal_items) {
-            uint64_t* it = c.bal_items + 2 * uint64_t(k);
+            uint4* it = reinterpret_cast<uint4*>(c.bal_items + 2 * uint64_t(k));
             if ((amount >> (64 - c.key_bits)) == 0) {
                 const uint32_t kd = dr.row * 4 + (pending ? 0 : 1);
                 const uint32_t kc = cr.row * 4 + (pending ? 2 : 3);
-                it[0] = (amount << c.key_bits) | kd;
-                it[1] = (amount << c.key_bits) | kc;
+                const uint64_t i0 = (amount << c.key_bits) | kd, i1 = (amount << c.key_bits) | kc;
+                *it = make_uint4(uint32_t(i0), uint32_t(i0 >> 32), uint32_t(i1), uint32_t(i1 >> 32));
                 if (bucket_hist) {
                     atomicAdd(&bucket_hist[kd >> kBucketShift], 1u);
                     atomicAdd(&bucket_hist[kc >> kBucketShift], 1u);
                 }
             } else {
-                it[0] = ~0ull;  // too wide to pack: u128 atomics in tr_commit
-                it[1] = ~0ull;
+                *it = make_uint4(~0u, ~0u, ~0u, ~0u);  // too wide to pack: atomics in tr_commit
                 need_commit = true;
             }
         } else {
@@ -382,18 +380,29 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
         }
         *fast_ts = ts_event;
     } else {
-        // Accounts whose balances or flags an event executes on in order.
-        if (dr.row != kNone32) T.acc_hot[dr.row] = c.epoch;
-        if (cr.row != kNone32) T.acc_hot[cr.row] = c.epoch;
-        hot = dr.row != kNone32 || cr.row != kNone32;
+        // Accounts whose balance this event may read when it replays -- the limit flag of the
+        // side it checks, balancing, a possible overflow (create_transfer :3842-3905) -- may take
+        // no FAST delta of this call: tr_commit demotes FAST events touching them. An account it
+        // only writes needs no mark: every FAST delta is applied before the replay and the
+        // replay's own deltas commute with them. (post/void read no balance, :4053-4300; `closed`
+        // is ordered by the closable marks.)
+        const bool ovf = t.amount.hi != 0 || dr.hi_pending >= kHazardHiLimit ||
+                         dr.hi_posted >= kHazardHiLimit || cr.hi_pending >= kHazardHiLimit ||
+                         cr.hi_posted >= kHazardHiLimit;
+        const bool read_dr = dr.row != kNone32 &&
+                             (ovf || (f & TB_TRANSFER_BALANCING_DEBIT) ||
+                              (dr.flags & TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS));
+        const bool read_cr = cr.row != kNone32 &&
+                             (ovf || (f & TB_TRANSFER_BALANCING_CREDIT) ||
+                              (cr.flags & TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS));
+        if (read_dr) T.acc_hot[dr.row] = c.epoch;
+        if (read_cr) T.acc_hot[cr.row] = c.epoch;
+        hot = read_dr || read_cr;
     }
     if (cls != kClassFast) {
         need_commit = true;
-        if (c.bal_items) {
-            uint64_t* it = c.bal_items + 2 * uint64_t(k);
-            it[0] = ~0ull;
-            it[1] = ~0ull;
-        }
+        if (c.bal_items)
+            *reinterpret_cast<uint4*>(c.bal_items + 2 * uint64_t(k)) = make_uint4(~0u, ~0u, ~0u, ~0u);
     }
     return (imported ? kFlagImported : 0u) | (post_void ? kFlagPostVoid : 0u) |
            (dup ? kFlagDuplicate : 0u) | (closable ? kFlagClosable : 0u) | (hot ? kFlagHot : 0u) |
@@ -450,12 +459,22 @@ __global__ void __launch_bounds__(kBlock, 4) tr_ingest(Tables T, Call<tb_transfe
         }
         const uint32_t k = base + lane;
         const bool active = lane < cnt;
-        uint32_t b = 0;
-        uint64_t ts_event = 0;
-        if (active) {
-            b = batch_of_guess(c.batch_ends, c.n_batches, c.n, k);
+        // The chunk's batch, once per wave (scalar loads); only a chunk that straddles a batch
+        // end sends its later lanes on to the following batches.
+        const uint32_t b0 = __builtin_amdgcn_readfirstlane(
+            batch_of_guess(c.batch_ends, c.n_batches, c.n, __builtin_amdgcn_readfirstlane(base)));
+        const uint32_t end0 = c.batch_ends[b0];
+        uint32_t bstart = b0 == 0 ? 0 : c.batch_ends[b0 - 1];
+        uint64_t ts_event = c.batch_ts[b0] - end0 + k + 1;
+        bool batch_imported = (c.events[bstart].flags & TB_TRANSFER_IMPORTED) != 0;
+        if (active && k >= end0) {
+            uint32_t b = b0 + 1;
+            while (c.batch_ends[b] <= k) b++;
+            bstart = c.batch_ends[b - 1];
             ts_event = ts_event_of(c, b, k);
+            batch_imported = (c.events[bstart].flags & TB_TRANSFER_IMPORTED) != 0;
         }
+        if (!active) ts_event = 0;
         lds_ts[wv][lane] = ts_event;
         wave_lds_sync();
         // The rows: the events as submitted, stamped with their commit timestamps (rows of
@@ -481,7 +500,7 @@ __global__ void __launch_bounds__(kBlock, 4) tr_ingest(Tables T, Call<tb_transfe
                                 ->flags & TB_TRANSFER_LINKED) != 0
                          : (k > 0 && (c.events[k - 1].flags & TB_TRANSFER_LINKED) != 0);
             uint64_t fts = 0;
-            flags |= ingest_event(T, c, k, t, b, ts_event, prev_linked, &fts,
+            flags |= ingest_event(T, c, k, t, bstart, batch_imported, ts_event, prev_linked, &fts,
                                   c.bucket_counts ? bucket_hist : nullptr);
             n_fast += fts != 0;
             ts_max = fts > ts_max ? fts : ts_max;
@@ -1141,8 +1160,9 @@ __global__ void acc_index_build(Tables T, uint64_t row_base, uint32_t n) {
     const uint64_t row = row_base + k;
     if (!T.acc_live[row]) return;
     const tb_account_t& a = T.acc_rows[row];
-    const uint64_t s = acc_index_insert(T.acc_index, a.id, uint32_t(row), a.ledger,
-                                        uint16_t(a.flags & ~TB_ACCOUNT_CLOSED), acc_hazard_of(a));
+    const uint64_t s = acc_index_insert(
+        T.acc_index, a.id, uint32_t(row),
+        acc_meta(uint16_t(a.flags & ~TB_ACCOUNT_CLOSED), acc_hazard_of(a), a.ledger));
     if (s == kNone) {
         atomicOr(&T.scalars->flags, kFlagTableFull);
         return;

@@ -179,7 +179,7 @@ __device__ inline bool ts_index_contains(const uint64_t* idx, uint64_t n, uint64
 
 __device__ inline uint64_t account_find(const Tables& T, const tb_uint128_t& id) {
     AccEntry e;
-    if (acc_index_find(T.acc_index, id, &e) == kNone) return kNone;
+    if (acc_index_find(T.acc_index, T.acc_rows, id, &e) == kNone) return kNone;
     return e.ref - 1;
 }
 

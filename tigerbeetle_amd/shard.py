@@ -1,0 +1,502 @@
+"""Ledger sharding of the commit path across GPUs.
+
+Debit and credit accounts of a transfer must share the transfer's ledger
+(`accounts_must_have_the_same_ledger`, `transfer_must_have_the_same_ledger_as_accounts`,
+src/state_machine.zig:3795-3798), so ledgers are independent shards: one executor per GPU owns a
+contiguous range of ledgers -- their accounts, transfer ids, transfer rows and TransferPending
+statuses. A client call (a multi-batch commit) is split by a router on the owner of the call,
+each shard's slice travels to its GPU (point-to-point sends: RCCL over xGMI with the `nccl`
+backend, gloo on CPU), every shard executes its slice, and the 16-byte results come back.
+
+Exactness. A shard executes its slice as the reference would execute the whole call only if no
+event of the slice can observe state held by another shard. `LedgerRouter` routes by
+directories of where each account id and each transfer id (created, or orphaned by a transient
+failure) lives, and raises `RouteError` -- before any shard executes -- for every call it cannot
+place exactly:
+
+* a transfer whose debit and credit accounts live on different shards (the reference answers
+  `accounts_must_have_the_same_ledger`; a shard would answer `*_account_not_found`);
+* a linked chain whose events belong to different shards (a chain is atomic, :3002-3213);
+* an id repeated within the call where the repeat could execute on a shard other than the
+  first occurrence's (a duplicate's outcome depends on the first occurrence's result);
+* imported events (their checks read the global `key_range` maxima, :3656-3665, :3808-3817);
+* a post/void of a pending transfer that has a timeout: it resets `pulse_next_timestamp` when
+  that equals the pending transfer's expiry (:4227-4229), a comparison against the *global*
+  value at that point of the call, which no shard holds.
+
+Events whose outcome is decided before any shard-local lookup can fail (`id_must_not_be_zero`,
+accounts not found anywhere, pending transfer not found anywhere) go to the shard of their ledger.
+An event whose id already exists goes to the shard holding it: `create_transfer_exists` and
+`create_account_exists` run before any account lookup (:3636, :3733), and a post/void that exists
+finds its pending transfer on the same shard (it was created there by posting it).
+
+Timestamps are global: event k of batch b is stamped `batch_ts[b] - len[b] + k + 1`
+(`execute_multi_batch`, :2702-2762). A shard receives each batch's events as maximal runs of
+consecutive positions, each run a sub-batch whose timestamp is that of its last event, so every
+event keeps its global timestamp. Runs never cut a chain (a chain crossing a run edge crosses a
+shard edge, which the router refused), and no batch-level check besides chain ends and the
+imported flag depends on the batch extent.
+
+pulse: with the resets above excluded, `pulse_next_timestamp` only moves by `min` between pulses
+(:3979-3980), so the sharded value is the minimum over shards (an all-reduce). Each shard expires
+its own transfers at the common pulse timestamp; this is the reference's pulse while fewer than
+`pulse_batch_max` transfers expire in total (the scan stops at that many and sets
+`pulse_next_timestamp` from the last one, :4969-4999). Past it the drivers raise `RouteError`:
+the cut across shards needs an all-gather of the shards' expiry keys.
+"""
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Set
+
+import numpy as np
+
+from .types import (ACCOUNT_DTYPE, RESULT_DTYPE, STATUS_CREATED, TRANSFER_DTYPE,
+                    TRANSIENT_TRANSFER_STATUSES, AccountFlags, TransferFlags)
+
+_U128_MAX = (1 << 128) - 1
+
+
+class RouteError(RuntimeError):
+    """The call holds an event that no single shard can execute exactly (see the module doc)."""
+
+
+def _ids(col: np.ndarray) -> List[int]:
+    lo = col[:, 0].tolist()
+    hi = col[:, 1].tolist()
+    return [a | (b << 64) for a, b in zip(lo, hi)]
+
+
+@dataclass
+class ShardSlice:
+    """One shard's part of a call: global positions, sub-batch lengths and timestamps."""
+    index: np.ndarray                       # int64 global positions, ascending
+    lens: List[int] = field(default_factory=list)
+    batch_ts: List[int] = field(default_factory=list)
+
+
+@dataclass
+class Plan:
+    kind: str                               # "accounts" | "transfers"
+    shard_of: np.ndarray                    # int32 per event
+    slices: List[ShardSlice]
+
+
+def chain_starts(flags: np.ndarray, lens) -> np.ndarray:
+    """True where an event starts a chain (a batch start, or the previous event is not linked)."""
+    n = len(flags)
+    start = np.ones(n, dtype=bool)
+    if n > 1:
+        start[1:] = (flags[:-1] & 1) == 0
+    ends = np.cumsum(np.asarray(lens, dtype=np.int64))
+    inner = ends[:-1]
+    start[inner[inner < n]] = True
+    return start
+
+
+def split_runs(shard_of: np.ndarray, lens, batch_ts, shards: int) -> List[ShardSlice]:
+    """Per shard, the maximal runs of consecutive positions of each batch, as sub-batches that
+    keep every event's global timestamp."""
+    slices = [ShardSlice(index=np.zeros(0, dtype=np.int64)) for _ in range(shards)]
+    parts: List[List[np.ndarray]] = [[] for _ in range(shards)]
+    s = 0
+    for b, ln in enumerate(lens):
+        ln = int(ln)
+        if ln == 0:
+            continue
+        seg = shard_of[s:s + ln]
+        cut = np.nonzero(np.diff(seg))[0] + 1
+        starts = np.concatenate([[0], cut]).tolist()
+        stops = np.concatenate([cut, [ln]]).tolist()
+        ts_b = int(batch_ts[b])
+        for a, z in zip(starts, stops):
+            sh = int(seg[a])
+            parts[sh].append(np.arange(s + a, s + z, dtype=np.int64))
+            slices[sh].lens.append(z - a)
+            # the run's last event (batch position z - 1) is stamped ts_b - ln + z
+            slices[sh].batch_ts.append(ts_b - ln + z)
+        s += ln
+    for sh in range(shards):
+        if parts[sh]:
+            slices[sh].index = np.concatenate(parts[sh])
+    return slices
+
+
+class LedgerRouter:
+    """Routes create_accounts / create_transfers calls to ledger shards (module doc).
+
+    Ledgers 1..`ledgers` map to shards by contiguous ranges (64 ledgers / G);
+    other ledgers by `ledger % shards`. Placement of a new account follows its ledger; routing
+    of later events follows the directories, so a placement never has to be recomputed.
+    """
+
+    def __init__(self, shards: int, ledgers: int = 64):
+        if shards < 1:
+            raise ValueError("shards must be >= 1")
+        self.shards = shards
+        self.ledgers = ledgers
+        self.account_shard: Dict[int, int] = {}
+        self.transfer_shard: Dict[int, int] = {}
+        self.timed_pending: Set[int] = set()  # pending transfers created with a timeout
+
+    def shard_of_ledger(self, ledger: int) -> int:
+        if 1 <= ledger <= self.ledgers:
+            return (ledger - 1) * self.shards // self.ledgers
+        return ledger % self.shards
+
+    # -- planning ---------------------------------------------------------------------------
+
+    @staticmethod
+    def _place_chains(n, starts, pins_of, default_of, record):
+        shard_of = np.zeros(n, dtype=np.int32)
+        bounds = np.concatenate([np.nonzero(starts)[0], [n]]).astype(np.int64).tolist()
+        for a, z in zip(bounds[:-1], bounds[1:]):
+            pins = set()
+            for k in range(a, z):
+                pins |= pins_of(k)
+            if len(pins) > 1:
+                what = "linked chain" if z - a > 1 else "event"
+                raise RouteError(f"{what} at {a}..{z - 1} spans shards {sorted(pins)}")
+            sh = pins.pop() if pins else default_of(a)
+            shard_of[a:z] = sh
+            for k in range(a, z):
+                record(k, sh)
+        return shard_of
+
+    def plan_accounts(self, events: np.ndarray, lens, batch_ts) -> Plan:
+        n = len(events)
+        flags = events["flags"]
+        if n and (flags & int(AccountFlags.imported)).any():
+            raise RouteError("imported accounts: key_range checks span shards")
+        ids = _ids(events["id"])
+        ledgers = events["ledger"].tolist()
+        in_call: Dict[int, int] = {}
+
+        def pins_of(k):
+            i = ids[k]
+            if i in self.account_shard:
+                return {self.account_shard[i]}
+            if i in in_call:
+                return {in_call[i]}
+            return set()
+
+        def record(k, sh):
+            i = ids[k]
+            if i not in self.account_shard and i != 0 and i != _U128_MAX:
+                in_call.setdefault(i, sh)
+
+        shard_of = self._place_chains(n, chain_starts(flags, lens), pins_of,
+                                      lambda a: self.shard_of_ledger(ledgers[a]), record)
+        return Plan("accounts", shard_of, split_runs(shard_of, lens, batch_ts, self.shards))
+
+    def plan_transfers(self, events: np.ndarray, lens, batch_ts) -> Plan:
+        n = len(events)
+        flags = events["flags"]
+        if n and (flags & int(TransferFlags.imported)).any():
+            raise RouteError("imported transfers: key_range checks span shards")
+        ids = _ids(events["id"])
+        drs = _ids(events["debit_account_id"])
+        crs = _ids(events["credit_account_id"])
+        pids = _ids(events["pending_id"])
+        ledgers = events["ledger"].tolist()
+        timeouts = events["timeout"].tolist()
+        fl = flags.tolist()
+        in_call: Dict[int, int] = {}
+        in_call_timed: Set[int] = set()
+        post_void = int(TransferFlags.post_pending_transfer | TransferFlags.void_pending_transfer)
+        pending = int(TransferFlags.pending)
+
+        def pins_of(k):
+            i = ids[k]
+            if i in self.transfer_shard:  # exists / id_already_failed: decided on the holder
+                return {self.transfer_shard[i]}
+            pins = set()
+            if i in in_call:  # the repeat executes in full if the first occurrence fails
+                pins.add(in_call[i])
+            if fl[k] & post_void:
+                p = pids[k]
+                if p in self.timed_pending or p in in_call_timed:
+                    raise RouteError(f"event {k} posts/voids a pending transfer with a timeout")
+                if p in self.transfer_shard:
+                    pins.add(self.transfer_shard[p])
+                elif p in in_call:
+                    pins.add(in_call[p])
+            else:
+                for a in (drs[k], crs[k]):
+                    if a in self.account_shard:
+                        pins.add(self.account_shard[a])
+            return pins
+
+        def record(k, sh):
+            i = ids[k]
+            if i not in self.transfer_shard and i != 0 and i != _U128_MAX:
+                in_call.setdefault(i, sh)
+                if (fl[k] & pending) and timeouts[k] > 0:
+                    in_call_timed.add(i)
+
+        shard_of = self._place_chains(n, chain_starts(flags, lens), pins_of,
+                                      lambda a: self.shard_of_ledger(ledgers[a]), record)
+        return Plan("transfers", shard_of, split_runs(shard_of, lens, batch_ts, self.shards))
+
+    # -- directories --------------------------------------------------------------------------
+
+    def commit(self, plan: Plan, events: np.ndarray, results: np.ndarray):
+        """Record where the call's new objects (and orphaned transfer ids) now live."""
+        status = results["status"]
+        ids = events["id"]
+
+        def key(k):
+            return int(ids[k, 0]) | (int(ids[k, 1]) << 64)
+
+        if plan.kind == "accounts":
+            for k in np.nonzero(status == STATUS_CREATED)[0].tolist():
+                self.account_shard[key(k)] = int(plan.shard_of[k])
+            return
+        keep = status == STATUS_CREATED
+        for st in TRANSIENT_TRANSFER_STATUSES:
+            keep |= status == int(st)
+        for k in np.nonzero(keep)[0].tolist():
+            self.transfer_shard.setdefault(key(k), int(plan.shard_of[k]))
+        timed = ((status == STATUS_CREATED) &
+                 ((events["flags"] & int(TransferFlags.pending)) != 0) & (events["timeout"] > 0))
+        for k in np.nonzero(timed)[0].tolist():
+            self.timed_pending.add(key(k))
+
+
+def gather_results(plan: Plan, shard_results: List[Optional[np.ndarray]], n: int) -> np.ndarray:
+    out = np.zeros(n, dtype=RESULT_DTYPE)
+    for sl, r in zip(plan.slices, shard_results):
+        if len(sl.index):
+            out[sl.index] = r
+    return out
+
+
+def _check_pulse(expired: int, pulse_batch_max: int):
+    if expired >= pulse_batch_max:
+        raise RouteError(f"pulse expired {expired} >= pulse_batch_max across shards")
+
+
+class LocalShards:
+    """All shards in one process (one executor each: several HBM table sets on one GPU, or CPU
+    executors in tests). `executors[s]` provides create_accounts / create_transfers
+    (events, lens, batch_ts) -> results, pulse(timestamp) -> expired, pulse_next_timestamp()."""
+
+    def __init__(self, router: LedgerRouter, executors, pulse_batch_max: int = 8190):
+        if len(executors) != router.shards:
+            raise ValueError("one executor per shard")
+        self.router = router
+        self.executors = executors
+        self.pulse_batch_max = pulse_batch_max
+
+    def _run(self, kind, events, lens, batch_ts):
+        dtype = ACCOUNT_DTYPE if kind == "accounts" else TRANSFER_DTYPE
+        events = np.ascontiguousarray(events, dtype=dtype)
+        plan = (self.router.plan_accounts if kind == "accounts"
+                else self.router.plan_transfers)(events, lens, batch_ts)
+        outs = []
+        for sl, ex in zip(plan.slices, self.executors):
+            if not len(sl.index):
+                outs.append(None)
+                continue
+            fn = ex.create_accounts if kind == "accounts" else ex.create_transfers
+            outs.append(fn(np.ascontiguousarray(events[sl.index]), sl.lens,
+                           np.asarray(sl.batch_ts, dtype=np.uint64)))
+        results = gather_results(plan, outs, len(events))
+        self.router.commit(plan, events, results)
+        return results
+
+    def create_accounts(self, events, lens, batch_ts):
+        return self._run("accounts", events, lens, batch_ts)
+
+    def create_transfers(self, events, lens, batch_ts):
+        return self._run("transfers", events, lens, batch_ts)
+
+    def pulse_next_timestamp(self) -> int:
+        return min(int(ex.pulse_next_timestamp()) for ex in self.executors)
+
+    def pulse(self, timestamp: int) -> int:
+        expired = sum(int(ex.pulse(timestamp)) for ex in self.executors)
+        _check_pulse(expired, self.pulse_batch_max)
+        return expired
+
+
+class ShardGroup:
+    """One shard per rank of a torch.distributed group (one process per GPU). Rank 0 owns the
+    router and the client call; each call is a status broadcast, one point-to-point send of
+    each shard's slice (event bytes, sub-batch lengths, timestamps) and one gather of the
+    16-byte results. With the `nccl` backend (RCCL over xGMI) the slices travel device to
+    device; with gloo they stay on the host. `executor` is this rank's shard.
+    """
+
+    def __init__(self, executor, router: Optional[LedgerRouter] = None, group=None,
+                 device: str = "cpu", pulse_batch_max: int = 8190):
+        import torch.distributed as dist
+        self.dist = dist
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        if self.rank == 0 and (router is None or router.shards != self.world):
+            raise ValueError("rank 0 needs a router with one shard per rank")
+        self.router = router
+        self.executor = executor
+        self.device = device
+        self.pulse_batch_max = pulse_batch_max
+
+    def _peer(self, r: int) -> int:
+        return r if self.group is None else self.dist.get_global_rank(self.group, r)
+
+    def _send(self, a: np.ndarray, dst: int):
+        import torch
+        a = np.ascontiguousarray(a)
+        hdr = torch.tensor([a.nbytes], dtype=torch.int64, device=self.device)
+        self.dist.send(hdr, self._peer(dst), group=self.group)
+        if a.nbytes:
+            buf = torch.from_numpy(a.view(np.uint8).reshape(-1).copy()).to(self.device)
+            self.dist.send(buf, self._peer(dst), group=self.group)
+
+    def _recv(self, src: int, dtype) -> np.ndarray:
+        import torch
+        hdr = torch.zeros(1, dtype=torch.int64, device=self.device)
+        self.dist.recv(hdr, self._peer(src), group=self.group)
+        nb = int(hdr.item())
+        if nb == 0:
+            return np.zeros(0, dtype=dtype)
+        buf = torch.empty(nb, dtype=torch.uint8, device=self.device)
+        self.dist.recv(buf, self._peer(src), group=self.group)
+        return buf.cpu().numpy().view(dtype)
+
+    def _bcast(self, value: int) -> int:
+        import torch
+        t = torch.tensor([value], dtype=torch.int64, device=self.device)
+        self.dist.broadcast(t, self._peer(0), group=self.group)
+        return int(t.item())
+
+    def _run(self, kind, events=None, lens=None, batch_ts=None):
+        dtype = ACCOUNT_DTYPE if kind == "accounts" else TRANSFER_DTYPE
+        plan, err = None, None
+        if self.rank == 0:
+            events = np.ascontiguousarray(events, dtype=dtype)
+            try:
+                plan = (self.router.plan_accounts if kind == "accounts"
+                        else self.router.plan_transfers)(events, lens, batch_ts)
+            except RouteError as e:
+                err = e
+        if self._bcast(0 if err is None else 1):  # every rank fails a refused call
+            raise err if err is not None else RouteError("refused by the router on rank 0")
+        if self.rank == 0:
+            for s in range(1, self.world):
+                sl = plan.slices[s]
+                self._send(events[sl.index], s)
+                self._send(np.asarray(sl.lens, dtype=np.uint32), s)
+                self._send(np.asarray(sl.batch_ts, dtype=np.uint64), s)
+            sl = plan.slices[0]
+            mine = (events[sl.index], sl.lens, np.asarray(sl.batch_ts, dtype=np.uint64))
+        else:
+            ev = self._recv(0, dtype)
+            ln = self._recv(0, np.uint32)
+            ts = self._recv(0, np.uint64)
+            mine = (ev, ln.tolist(), ts)
+        res = np.zeros(0, dtype=RESULT_DTYPE)
+        if len(mine[0]):
+            fn = (self.executor.create_accounts if kind == "accounts"
+                  else self.executor.create_transfers)
+            res = fn(np.ascontiguousarray(mine[0]), mine[1], mine[2])
+        if self.rank != 0:
+            self._send(res, 0)
+            return None
+        outs = [res] + [self._recv(s, RESULT_DTYPE) for s in range(1, self.world)]
+        results = gather_results(plan, outs, len(events))
+        self.router.commit(plan, events, results)
+        return results
+
+    def create_accounts(self, events=None, lens=None, batch_ts=None):
+        """Collective: rank 0 passes the call, the other ranks call with no arguments."""
+        return self._run("accounts", events, lens, batch_ts)
+
+    def create_transfers(self, events=None, lens=None, batch_ts=None):
+        return self._run("transfers", events, lens, batch_ts)
+
+    def pulse_next_timestamp(self) -> int:
+        """Collective all-reduce(min) of the shards' pulse_next_timestamp."""
+        import torch
+        t = torch.tensor([int(self.executor.pulse_next_timestamp())], dtype=torch.int64,
+                         device=self.device)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN, group=self.group)
+        return int(t.item())
+
+    def pulse(self, timestamp: int) -> int:
+        """Collective: every shard expires at the common pulse timestamp."""
+        import torch
+        t = torch.tensor([int(self.executor.pulse(timestamp))], dtype=torch.int64,
+                         device=self.device)
+        self.dist.all_reduce(t, group=self.group)
+        expired = int(t.item())
+        _check_pulse(expired, self.pulse_batch_max)
+        return expired
+
+
+class GpuShard:
+    """A shard backed by libtbg.so (its HBM tables on `device`): the executor interface above."""
+
+    def __init__(self, account_capacity, transfer_capacity, batch_events_max=1 << 16,
+                 batch_count_max=4096, pulse_batch_max=8190, device=0,
+                 pulse_next_timestamp_init=(1 << 63) - 1):
+        import ctypes
+        from . import native
+        self._c = ctypes
+        self._native = native
+        self.lib = native.load()
+        o = native.TbgOptions()
+        o.account_capacity = account_capacity
+        o.transfer_capacity = transfer_capacity
+        o.batch_events_max = batch_events_max
+        o.batch_count_max = batch_count_max
+        o.pulse_batch_max = pulse_batch_max
+        o.device = device
+        o.pulse_next_timestamp_init = pulse_next_timestamp_init
+        self.g = self.lib.tbg_open(ctypes.byref(o))
+        if not self.g:
+            raise RuntimeError("tbg_open failed")
+
+    def close(self):
+        if self.g:
+            self.lib.tbg_close(self.g)
+            self.g = None
+
+    def _call(self, fn, events, lens, batch_ts):
+        c = self._c
+        n = len(events)
+        lens_a = np.asarray(lens, dtype=np.uint32)
+        ts_a = np.asarray(batch_ts, dtype=np.uint64)
+        out = np.zeros(n, dtype=RESULT_DTYPE)
+        rc = fn(self.g, events.ctypes.data_as(c.c_void_p), n,
+                lens_a.ctypes.data_as(self._native.c_u32p),
+                ts_a.ctypes.data_as(self._native.c_u64p), len(lens_a),
+                out.ctypes.data_as(c.c_void_p))
+        if rc != 0:
+            raise RuntimeError(f"libtbg: {rc} {self.lib.tbg_last_error(self.g)}")
+        return out
+
+    def create_accounts(self, events, lens, batch_ts):
+        return self._call(self.lib.tbg_create_accounts,
+                          np.ascontiguousarray(events, dtype=ACCOUNT_DTYPE), lens, batch_ts)
+
+    def create_transfers(self, events, lens, batch_ts):
+        return self._call(self.lib.tbg_create_transfers,
+                          np.ascontiguousarray(events, dtype=TRANSFER_DTYPE), lens, batch_ts)
+
+    def pulse(self, timestamp):
+        return int(self.lib.tbg_pulse(self.g, timestamp))
+
+    def pulse_next_timestamp(self):
+        return int(self.lib.tbg_pulse_next_timestamp(self.g))
+
+    def dump(self):
+        c = self._c
+        na = self.lib.tbg_dump_accounts(self.g, None)
+        a = np.zeros(max(na, 0), dtype=ACCOUNT_DTYPE)
+        self.lib.tbg_dump_accounts(self.g, a.ctypes.data_as(c.c_void_p))
+        nt = self.lib.tbg_dump_transfers(self.g, None, None)
+        t = np.zeros(max(nt, 0), dtype=TRANSFER_DTYPE)
+        s = np.zeros(max(nt, 0), dtype=np.uint8)
+        self.lib.tbg_dump_transfers(self.g, t.ctypes.data_as(c.c_void_p),
+                                    s.ctypes.data_as(c.c_void_p))
+        return a, t, s
