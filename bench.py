@@ -36,6 +36,9 @@ from tigerbeetle_amd.types import ACCOUNT_DTYPE, RESULT_DTYPE, TRANSFER_DTYPE  #
 
 METRIC = "validated create_transfers/sec (1/2/4/8 GPU) + % of HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+# Measured HBM bytes per launch of each kernel (tools/pmc.sh: separate rocprofv3 --pmc passes of
+# this bench's default workload; FETCH_SIZE doubled per the gfx950 note + WRITE_SIZE).
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")
 BATCH = 8189           # Operation.create_transfers.event_max (src/tigerbeetle.zig:853-901)
 
 # Algorithmic bytes per event of each kernel of the create_transfers path: the
@@ -154,6 +157,16 @@ def step_timestamps(prepare_ts, lens):
     """TestContext rule per commit: prepare_ts += 1 + n; the batch's timestamp is prepare_ts."""
     ts = prepare_ts + np.cumsum(lens + 1)
     return ts.astype(np.uint64), int(ts[-1])
+
+
+def measured_traffic(kernel):
+    """(HBM bytes per launch, source) of `kernel` from TRAFFIC_FILE, or (None, None)."""
+    try:
+        with open(TRAFFIC_FILE) as fh:
+            d = json.load(fh)
+        return float(d["kernels"][kernel]["hbm_bytes_per_launch"]), d.get("source")
+    except (OSError, ValueError, KeyError, TypeError):
+        return None, None
 
 
 def cpu_baseline(args, acc, base, lens):
@@ -299,9 +312,12 @@ def main():
         avg_s = kms / kcount / 1e3
         kbytes = KERNEL_BYTES_PER_EVENT[kname] * N
         achieved = kbytes / avg_s / 1e9
+        default_workload = (N, A) == (10_000_000, 10_000)
+        traffic, traffic_src = measured_traffic(kname) if default_workload else (None, None)
         roofline = {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                    "traffic": None, "alg_bytes_per_launch": kbytes,
+                    "traffic": traffic, "traffic_source": traffic_src,
+                    "alg_bytes_per_launch": kbytes,
                     "avg_launch_ms": round(kms / kcount, 4),
                     "path": {"alg_bytes_per_step": path_bytes,
                              "device_ms_per_step": round(dev_ms_total / K, 4),

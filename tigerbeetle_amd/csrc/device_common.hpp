@@ -190,12 +190,14 @@ __device__ inline uint64_t probe_claim(const IdTable& t, const tb_uint128_t& id,
 }
 
 // The account index: a read-mostly cache of the id -> row mapping together with what the
-// create_transfers checks read of an account, in 16-byte entries, linear probing on a full mix of
-// the id, 4 entries per account of capacity (load <= 0.25). A probe step is one 16-byte load --
-// one L2 request and one texture-address slot per lane, the resources tr_ingest saturates
-// (SQ_INSTS_VMEM_RD, TA_BUSY in profiles/) -- carrying the id's low word, the row, the static
-// flags, the hazard bits and the ledger's low 16 bits: the common lookup never touches the
-// 128-byte row.
+// create_transfers checks read of an account, in 16-byte entries carrying the id's low word, the
+// row, the static flags, the hazard bits and the ledger's low 16 bits: the common lookup never
+// touches the 128-byte row. Placement is two-choice cuckoo over 4 entries per account of
+// capacity (load <= 0.25, below the 0.5 threshold): a lookup issues exactly two 16-byte loads,
+// both candidates at once, and never loops. tr_ingest is bound by its texture-address unit
+// (TA_BUSY ~70 % in profiles/), which spends a whole wave-instruction on every probe step any
+// lane of the wave still needs: linear probing made the 128 lookups of a wave run to the
+// longest probe among them (~9 steps each, measured as 29 vector-memory reads per 64 events).
 //
 // An entry stands for its account's full id and ledger only while kHazardWide is clear (the id's
 // high word is 0 and the ledger < 2^16; static, set at insertion). A wide entry matches only after
@@ -226,8 +228,11 @@ __host__ __device__ inline uint16_t meta_flags(uint32_t m) { return uint16_t(m &
 __host__ __device__ inline uint16_t meta_hazard(uint32_t m) { return uint16_t((m >> 8) & 0xFFu); }
 __host__ __device__ inline uint32_t meta_ledger(uint32_t m) { return m >> 16; }
 
-__host__ __device__ inline uint64_t acc_entry_home(const tb_uint128_t& id) {
+__host__ __device__ inline uint64_t acc_entry_h1(const tb_uint128_t& id) {
     return mix64(id.lo ^ mix64(id.hi ^ 0xD6E8FEB86659FD93ull));
+}
+__host__ __device__ inline uint64_t acc_entry_h2(const tb_uint128_t& id) {
+    return mix64(id.hi ^ mix64(id.lo ^ 0x9FB21C651E98DF25ull) ^ 0xA24BAED4963EE407ull);
 }
 
 struct AccIndex {
@@ -235,41 +240,61 @@ struct AccIndex {
     uint64_t mask;
 };
 
-// One 16-byte load per probe step; returns the entry index (its contents in *out) or kNone.
-// `rows` resolves the high word of wide entries.
+// Does entry image `v` hold `id`? `rows` resolves the high word of wide entries.
+__device__ inline bool acc_entry_match(const uint4& v, const tb_account_t* rows,
+                                       const tb_uint128_t& id) {
+    return v.z != 0 && ((uint64_t(v.y) << 32) | v.x) == id.lo &&
+           ((meta_hazard(v.w) & kHazardWide) ? rows[v.z - 1].id.hi == id.hi : id.hi == 0);
+}
+
+// Two 16-byte loads, issued together; returns the entry index (its contents in *out) or kNone.
 __device__ inline uint64_t acc_index_find(const AccIndex& x, const tb_account_t* rows,
                                           const tb_uint128_t& id, AccEntry* out) {
     if (u128_is_zero(id)) return kNone;
-    uint64_t s = acc_entry_home(id) & x.mask;
-    for (uint64_t n = 0; n <= x.mask; n++) {
-        const uint4 v = *reinterpret_cast<const uint4*>(&x.entries[s]);
-        if (v.z == 0) return kNone;  // empty
-        if (((uint64_t(v.y) << 32) | v.x) == id.lo &&
-            ((meta_hazard(v.w) & kHazardWide) ? rows[v.z - 1].id.hi == id.hi : id.hi == 0)) {
-            out->id_lo = id.lo;
-            out->ref = v.z;
-            out->meta = v.w;
-            return s;
-        }
-        s = (s + 1) & x.mask;
+    const uint64_t s1 = acc_entry_h1(id) & x.mask, s2 = acc_entry_h2(id) & x.mask;
+    const uint4 v1 = *reinterpret_cast<const uint4*>(&x.entries[s1]);
+    const uint4 v2 = *reinterpret_cast<const uint4*>(&x.entries[s2]);
+    uint64_t s = kNone;
+    uint4 v = v1;
+    if (acc_entry_match(v1, rows, id)) {
+        s = s1;
+    } else if (acc_entry_match(v2, rows, id)) {
+        s = s2;
+        v = v2;
     }
-    return kNone;
+    if (s != kNone) {
+        out->id_lo = id.lo;
+        out->ref = v.z;
+        out->meta = v.w;
+    }
+    return s;
 }
 
-// Inserts a new id (the caller guarantees it is absent); returns the entry index or kNone.
-__device__ inline uint64_t acc_index_insert(const AccIndex& x, const tb_uint128_t& id, uint32_t row,
-                                            uint32_t meta) {
-    uint64_t s = acc_entry_home(id) & x.mask;
-    for (uint64_t n = 0; n <= x.mask; n++) {
-        AccEntry* e = &x.entries[s];
-        if (atomicCAS(&e->ref, 0u, row + 1) == 0u) {
-            e->id_lo = id.lo;
-            e->meta = meta;
-            return s;
-        }
-        s = (s + 1) & x.mask;
+// Cuckoo insertion of row `row` (its id absent from the index). Only the `ref` words move, by
+// atomic exchange, so concurrent insertions never lose an account (each holds exactly one in
+// hand); a displaced account continues at its other candidate. Every entry written is appended
+// to `dirty` (capacity `dirty_cap`; *overflow is set past it) and the caller rewrites the rest of
+// each dirty entry from the row it names (acc_index_repair). Returns false after
+// kCuckooMaxKicks displacements (the table is too full).
+constexpr int kCuckooMaxKicks = 512;
+
+__device__ inline bool acc_index_insert(const AccIndex& x, const tb_account_t* rows, uint32_t row,
+                                        uint32_t* dirty, unsigned int* dirty_count,
+                                        uint32_t dirty_cap, unsigned int* overflow) {
+    uint32_t r = row;
+    uint64_t pos = acc_entry_h1(rows[r].id) & x.mask;
+    for (int kick = 0; kick < kCuckooMaxKicks; kick++) {
+        const uint32_t old = atomicExch(&x.entries[pos].ref, r + 1);
+        const unsigned int d = atomicAdd(dirty_count, 1u);
+        if (d < dirty_cap) dirty[d] = uint32_t(pos);
+        else atomicOr(overflow, 1u);
+        if (old == 0) return true;
+        r = old - 1;
+        const tb_uint128_t id = rows[r].id;
+        const uint64_t h1 = acc_entry_h1(id) & x.mask, h2 = acc_entry_h2(id) & x.mask;
+        pos = pos == h1 ? h2 : h1;
     }
-    return kNone;
+    return false;
 }
 
 __device__ inline void acc_hazard_set(const AccIndex& x, const uint32_t* entry_of, uint64_t row,

@@ -69,6 +69,10 @@ struct tbg_ctx {
     unsigned int* bucket_words = nullptr;  // counts, cursors, offsets, slice bases
     uint64_t* bucket_partials = nullptr;   // per slice: kBucketKeys partial sums
     uint64_t bucket_slices_max = 0;
+    // account index build (cuckoo insertion + repair)
+    uint32_t* idx_dirty = nullptr;
+    unsigned int* idx_counters = nullptr;
+    uint32_t idx_dirty_cap = 0;
     void* cub_temp = nullptr;
     size_t cub_temp_bytes = 0;
 
@@ -424,11 +428,16 @@ tbg_ctx* tbg_open(const tbg_options* options) {
     const uint64_t ev_max = options->batch_events_max;
     // Slot tables hold at least 4 probe groups (hash_id / probe_next step 16 slots at a time).
     const uint64_t acc_slots = std::max<uint64_t>(next_pow2(acc_cap * 2), 64);
-    const uint64_t tr_slots = std::max<uint64_t>(next_pow2(tr_cap * 2), 64);
+    // 4 id slots per transfer of capacity: ids claim in blocks of 16 (group-16 homes), and a
+    // block whose home group is taken probes on; at group load <= 1/4 most blocks claim at home.
+    const uint64_t tr_slots = std::max<uint64_t>(next_pow2(tr_cap * 4), 64);
     // 4 index entries per account (entry indexes are u32: at most 2^31 entries).
     const uint64_t acc_entries =
         std::min<uint64_t>(std::max<uint64_t>(next_pow2(acc_cap * 4), 64), 1ull << 31);
     Tables& T = ctx->T;
+    ctx->idx_dirty_cap = uint32_t(std::min<uint64_t>(2 * ev_max + 4096, 1u << 30));
+    ok = ok && dev_alloc(ctx, &ctx->idx_dirty, ctx->idx_dirty_cap, false) &&
+         dev_alloc(ctx, &ctx->idx_counters, 2, true);
     ok = ok && dev_alloc(ctx, &T.acc_index.entries, acc_entries, true) &&
          dev_alloc(ctx, &T.acc_entry_of, acc_cap, false) &&
          hip_ok(ctx, hipMemsetAsync(T.acc_entry_of, 0xFF, acc_cap * sizeof(uint32_t), ctx->stream), "memset");
@@ -489,7 +498,7 @@ tbg_ctx* tbg_open(const tbg_options* options) {
 void tbg_close(tbg_ctx* ctx) {
     if (!ctx) return;
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    void* ptrs[] = {ctx->T.acc_index.entries, ctx->T.acc_entry_of, ctx->T.acc.slots, ctx->T.acc_rows, ctx->T.acc_live, ctx->T.acc_hot,
+    void* ptrs[] = {ctx->idx_dirty, ctx->idx_counters, ctx->T.acc_index.entries, ctx->T.acc_entry_of, ctx->T.acc.slots, ctx->T.acc_rows, ctx->T.acc_live, ctx->T.acc_hot,
                     ctx->T.acc_closable, ctx->T.tr.slots, ctx->T.tr_rows, ctx->T.tr_live,
                     ctx->T.tr_status, ctx->T.expiry, ctx->d_scalars, ctx->T.undo, ctx->d_events,
                     ctx->d_results, ctx->d_batch_ends, ctx->d_batch_ts, ctx->ev_slot, ctx->ev_dr,
@@ -647,10 +656,16 @@ int tbg_create_accounts_device(tbg_ctx* ctx, const tb_account_t* d_events, uint3
     }
     if (!rc) rc = run_replay(ctx, c, false, true);
     if (!rc) {
-        hipLaunchKernelGGL(acc_index_build, grid, block, 0, ctx->stream, ctx->T,
-                           ctx->T.acc_rows_used, n);
-        tmark(ctx, "acc_index_build");
-        rc = hip_ok(ctx, hipGetLastError(), "launch") ? 0 : TBG_EHIP;
+        const IndexBuild ib{ctx->idx_dirty, ctx->idx_counters, ctx->idx_dirty_cap};
+        rc = hip_ok(ctx, hipMemsetAsync(ctx->idx_counters, 0, 2 * sizeof(unsigned int),
+                                        ctx->stream), "memset") ? 0 : TBG_EHIP;
+        if (!rc) {
+            hipLaunchKernelGGL(acc_index_insert_rows, grid, block, 0, ctx->stream, ctx->T,
+                               ctx->T.acc_rows_used, n, ib);
+            hipLaunchKernelGGL(acc_index_repair, dim3(1024), block, 0, ctx->stream, ctx->T, ib);
+            tmark(ctx, "acc_index_build");
+            rc = hip_ok(ctx, hipGetLastError(), "launch") ? 0 : TBG_EHIP;
+        }
     }
     if (!rc) rc = end_call(ctx, n);
     ctx->stream = saved;

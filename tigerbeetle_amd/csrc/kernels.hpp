@@ -493,12 +493,14 @@ __global__ void __launch_bounds__(kBlock, 4) tr_ingest(Tables T, Call<tb_transfe
                 dst[idx] = v;
             }
         }
+        const uint32_t ubase = __builtin_amdgcn_readfirstlane(base);
+        const bool prev0 = ubase > 0 && (c.events[ubase - 1].flags & TB_TRANSFER_LINKED) != 0;
         if (active) {
             const tb_transfer_t& t = *reinterpret_cast<const tb_transfer_t*>(my + lane * kLdsEventStride);
             const bool prev_linked =
                 lane > 0 ? (reinterpret_cast<const tb_transfer_t*>(my + (lane - 1) * kLdsEventStride)
                                 ->flags & TB_TRANSFER_LINKED) != 0
-                         : (k > 0 && (c.events[k - 1].flags & TB_TRANSFER_LINKED) != 0);
+                         : prev0;
             uint64_t fts = 0;
             flags |= ingest_event(T, c, k, t, bstart, batch_imported, ts_event, prev_linked, &fts,
                                   c.bucket_counts ? bucket_hist : nullptr);
@@ -1153,21 +1155,44 @@ __global__ void acc_classify(Tables T, Call<tb_account_t> c) {
     count_stat(T.scalars, 3, k < c.n && cls == kClassDone && !created);
 }
 
-// The account index entries of the accounts a create_accounts call created (after its replay).
-__global__ void acc_index_build(Tables T, uint64_t row_base, uint32_t n) {
+// The account index after a create_accounts call: cuckoo insertion of the accounts it created
+// (only `ref` words move), then every entry the insertion wrote gets the rest of its image -- id
+// low word, flags, hazard, ledger -- from the row it now names, and that row its entry index.
+struct IndexBuild {
+    uint32_t* dirty;         // entries written by the insertion
+    unsigned int* counters;  // [0] dirty entries appended, [1] the dirty list overflowed
+    uint32_t dirty_cap;
+};
+
+__global__ void acc_index_insert_rows(Tables T, uint64_t row_base, uint32_t n, IndexBuild B) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
     const uint64_t row = row_base + k;
     if (!T.acc_live[row]) return;
-    const tb_account_t& a = T.acc_rows[row];
-    const uint64_t s = acc_index_insert(
-        T.acc_index, a.id, uint32_t(row),
-        acc_meta(uint16_t(a.flags & ~TB_ACCOUNT_CLOSED), acc_hazard_of(a), a.ledger));
-    if (s == kNone) {
+    if (!acc_index_insert(T.acc_index, T.acc_rows, uint32_t(row), B.dirty, &B.counters[0],
+                          B.dirty_cap, &B.counters[1]))
         atomicOr(&T.scalars->flags, kFlagTableFull);
+}
+
+__device__ inline void acc_index_repair_entry(const Tables& T, uint64_t pos) {
+    AccEntry* e = &T.acc_index.entries[pos];
+    const uint32_t ref = e->ref;
+    if (ref == 0) return;
+    const tb_account_t& a = T.acc_rows[ref - 1];
+    e->id_lo = a.id.lo;
+    e->meta = acc_meta(uint16_t(a.flags & ~TB_ACCOUNT_CLOSED), acc_hazard_of(a), a.ledger);
+    T.acc_entry_of[ref - 1] = uint32_t(pos);
+}
+
+__global__ void acc_index_repair(Tables T, IndexBuild B) {
+    const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+    const uint64_t i0 = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (B.counters[1]) {  // the dirty list overflowed: every entry
+        for (uint64_t p = i0; p <= T.acc_index.mask; p += stride) acc_index_repair_entry(T, p);
         return;
     }
-    T.acc_entry_of[row] = uint32_t(s);
+    const uint64_t n = B.counters[0] < B.dirty_cap ? B.counters[0] : B.dirty_cap;
+    for (uint64_t i = i0; i < n; i += stride) acc_index_repair_entry(T, B.dirty[i]);
 }
 
 // ================================ pulse ======================================================

@@ -20,4 +20,4 @@ for ctrs in "FETCH_SIZE" "WRITE_SIZE" \
     timeout -s KILL 120 rocprofv3 --pmc $ctrs --output-format csv -d $out/p$i -o run -- \
         python3 $R/bench.py $args > $out/p$i.log 2>&1 || { echo "pass $i ($ctrs) failed"; tail -5 $out/p$i.log; exit 1; }
 done
-cd $R && python3 tools/pmc_summary.py $out > $out/summary.txt && cat $out/summary.txt
+cd $R && python3 tools/pmc_summary.py $out $out/traffic.json > $out/summary.txt && cat $out/traffic.json

@@ -22,7 +22,18 @@ def short(name):
     return n[-60:]
 
 
-def main(out):
+def traffic(summary, source):
+    """Per-launch HBM bytes of each kernel (the `roofline.traffic` bench.py reports)."""
+    ks = {}
+    for k, d in summary.items():
+        if "hbm_bytes" in d:
+            ks[k] = {"hbm_bytes_per_launch": d["hbm_bytes"], "read_bytes": d["hbm_read_bytes"],
+                     "write_bytes": d["hbm_write_bytes"], "launches": d.get("FETCH_SIZE_launches")}
+    return {"source": source, "method": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950) + WRITE_SIZE, "
+                                        "separate passes, average per launch", "kernels": ks}
+
+
+def main(out, traffic_path=None):
     acc = defaultdict(lambda: defaultdict(list))
     for f in sorted(glob.glob(os.path.join(out, "p*", "**", "*counter_collection.csv"),
                               recursive=True)):
@@ -48,7 +59,11 @@ def main(out):
         summary[k] = d
     json.dump(summary, sys.stdout, indent=1, sort_keys=True)
     print()
+    if traffic_path:
+        with open(traffic_path, "w") as fh:
+            json.dump(traffic(summary, os.path.basename(os.path.normpath(out))), fh, indent=1,
+                      sort_keys=True)
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None)
