@@ -65,6 +65,7 @@ struct tbg_ctx {
     uint32_t* slow_list = nullptr;
     // balance items (2 per event, packed u64) and their sorted copy
     uint64_t* bal_items = nullptr;
+    uint4* chunk_info = nullptr;     // per 64-event chunk of a create_transfers call
     uint64_t* bal_items_sorted = nullptr;  // sorted (large key spaces) or bucketed items
     unsigned int* bucket_words = nullptr;  // counts, cursors, offsets, slice bases
     uint64_t* bucket_partials = nullptr;   // per slice: kBucketKeys partial sums
@@ -234,6 +235,7 @@ Call<Event> make_call(tbg_ctx* ctx, const Event* d_events, uint32_t n, const uin
     c.key_bits = 0;
     c.bucket_counts = nullptr;
     c.n_buckets = 0;
+    c.chunk_info = nullptr;
     c.ev_slot = ctx->ev_slot;
     c.ev_dr = ctx->ev_dr;
     c.ev_cr = ctx->ev_cr;
@@ -459,7 +461,8 @@ tbg_ctx* tbg_open(const tbg_options* options) {
          dev_alloc(ctx, &ctx->ev_info, ev_max, false) && dev_alloc(ctx, &ctx->ev_slow, ev_max, false) &&
          dev_alloc(ctx, &ctx->slow_list, ev_max, false);
     // (2 * ev_max items, at least ev_max u64 of lookup scratch)
-    ok = ok && dev_alloc(ctx, &ctx->bal_items, 2 * ev_max, false);
+    ok = ok && dev_alloc(ctx, &ctx->bal_items, 2 * ev_max, false) &&
+         dev_alloc(ctx, &ctx->chunk_info, (ev_max + 63) / 64 + 1, false);
     if (ev_max >= kSortThreshold) {
         ctx->bucket_slices_max = (2 * ev_max + kSliceItems - 1) / kSliceItems + kBucketsMax;
         ok = ok && dev_alloc(ctx, &ctx->bal_items_sorted, 2 * ev_max, false) &&
@@ -503,7 +506,7 @@ void tbg_close(tbg_ctx* ctx) {
                     ctx->T.tr_status, ctx->T.expiry, ctx->d_scalars, ctx->T.undo, ctx->d_events,
                     ctx->d_results, ctx->d_batch_ends, ctx->d_batch_ts, ctx->ev_slot, ctx->ev_dr,
                     ctx->ev_cr, ctx->ev_amount, ctx->ev_info, ctx->ev_slow, ctx->slow_list,
-                    ctx->bal_items, ctx->bal_items_sorted, ctx->bucket_words, ctx->bucket_partials,
+                    ctx->bal_items, ctx->chunk_info, ctx->bal_items_sorted, ctx->bucket_words, ctx->bucket_partials,
                     ctx->cub_temp, ctx->acc_ts_index, ctx->tr_ts_index, ctx->sel_buf,
                     ctx->pulse.keep, ctx->pulse.exp, ctx->pulse.ts, ctx->pulse.rows,
                     ctx->pulse.exp_b, ctx->pulse.rows_b, ctx->pulse.counters};
@@ -564,7 +567,11 @@ int tbg_create_transfers_device(tbg_ctx* ctx, const tb_transfer_t* d_events, uin
         rc = hip_ok(ctx, hipMemsetAsync(plan.counts, 0, kBucketsMax * sizeof(unsigned int),
                                         ctx->stream), "memset") ? 0 : TBG_EHIP;
     }
+    if (!rc && n_batches > kChunkBatchMask) rc = TBG_EINVAL;
     if (!rc) {
+        c.chunk_info = ctx->chunk_info;
+        hipLaunchKernelGGL(tr_chunk_info, dim3(grid_for((n + 63) / 64)), block, 0, ctx->stream, c,
+                           ctx->chunk_info);
         hipLaunchKernelGGL(tr_ingest, dim3(ig), block, 0, ctx->stream, ctx->T, c);
         tmark(ctx, "tr_ingest");
         hipLaunchKernelGGL(tr_commit, grid, block, 0, ctx->stream, ctx->T, c);

@@ -233,7 +233,7 @@ __device__ inline uint8_t classify_after_lookup(const Tables& T, const Call<tb_t
 // Memory-level parallelism: the id claim (one CAS at the home slot, no preceding load) and the two
 // account-index loads are independent and issue together; the common event pays one round trip.
 __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_transfer_t>& c,
-                                            uint32_t k, const tb_transfer_t& t, uint32_t bstart,
+                                            uint32_t k, const tb_transfer_t& t,
                                             bool batch_imported, uint64_t ts_event,
                                             bool prev_linked, uint64_t* fast_ts,
                                             unsigned int* bucket_hist) {
@@ -244,7 +244,8 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
     post_void = (f & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) != 0;
     const tb_uint128_t id = t.id;
     const bool valid_id = !u128_is_zero(id) && !u128_is_max(id);
-    const bool chain = (f & TB_TRANSFER_LINKED) || (k > bstart && prev_linked);
+    // prev_linked: the previous event of the same batch is linked.
+    const bool chain = (f & TB_TRANSFER_LINKED) || prev_linked;
 
     uint32_t status = 0;
     uint64_t ts_out = ts_event;
@@ -409,6 +410,30 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
            (need_commit ? kFlagNeedCommit : 0u);
 }
 
+// Per 64-event chunk of a create_transfers call (one lane each): the batch b0 of its first event,
+// that batch's end, ts_base = batch_ts[b0] - end + 1 (event k < end is stamped ts_base + k),
+// whether b0 is an imported batch, and whether the chunk's first event continues a chain of its
+// batch. tr_ingest reads it with one uniform load per chunk: the batch search costs ~10
+// vector-memory instructions per wave when each chunk repeats it (the compiler cannot use scalar
+// loads for memory the kernel may write), and tr_ingest is bound by vector-memory issue.
+constexpr uint32_t kChunkBatchMask = (1u << 30) - 1;
+constexpr uint32_t kChunkImported = 1u << 30;
+constexpr uint32_t kChunkPrevLinked = 1u << 31;
+
+__global__ void tr_chunk_info(Call<tb_transfer_t> c, uint4* out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t base = i * 64;
+    if (base >= c.n) return;
+    const uint32_t b0 = batch_of_guess(c.batch_ends, c.n_batches, c.n, base);
+    const uint32_t end0 = c.batch_ends[b0];
+    const uint32_t bstart0 = batch_start_of(c, b0);
+    const uint64_t ts_base = c.batch_ts[b0] - end0 + 1;
+    uint32_t w = b0;
+    if (c.events[bstart0].flags & TB_TRANSFER_IMPORTED) w |= kChunkImported;
+    if (base > bstart0 && (c.events[base - 1].flags & TB_TRANSFER_LINKED)) w |= kChunkPrevLinked;
+    out[i] = make_uint4(w, end0, uint32_t(ts_base), uint32_t(ts_base >> 32));
+}
+
 // LDS image of a wave's 64 events: 144 bytes per event (128 + 16 of padding), so the lanes'
 // 16-byte field reads (one event per lane) fall on distinct banks.
 constexpr uint32_t kLdsEventStride = 144;
@@ -451,58 +476,67 @@ __global__ void __launch_bounds__(kBlock, 4) tr_ingest(Tables T, Call<tb_transfe
     uint32_t base = (blockIdx.x * kIngestWaves + wv) * 64;
     if (base < c.n) load_chunk(base);
     for (; base < c.n; base += nw * 64) {
-        const uint32_t cnt = c.n - base < 64 ? c.n - base : 64;
+        const uint32_t ubase = __builtin_amdgcn_readfirstlane(base);
+        const uint4 ci = c.chunk_info[ubase >> 6];
+        const uint32_t cnt = c.n - ubase < 64 ? c.n - ubase : 64;
 #pragma unroll
         for (int i = 0; i < 8; i++) {
             const uint32_t e = i * 8 + (lane >> 3), part = lane & 7;
             *reinterpret_cast<uint4*>(my + e * kLdsEventStride + part * 16) = q[i];
         }
+        wave_lds_sync();
         const uint32_t k = base + lane;
         const bool active = lane < cnt;
-        // The chunk's batch, once per wave (scalar loads); only a chunk that straddles a batch
-        // end sends its later lanes on to the following batches.
-        const uint32_t b0 = __builtin_amdgcn_readfirstlane(
-            batch_of_guess(c.batch_ends, c.n_batches, c.n, __builtin_amdgcn_readfirstlane(base)));
-        const uint32_t end0 = c.batch_ends[b0];
-        uint32_t bstart = b0 == 0 ? 0 : c.batch_ends[b0 - 1];
-        uint64_t ts_event = c.batch_ts[b0] - end0 + k + 1;
-        bool batch_imported = (c.events[bstart].flags & TB_TRANSFER_IMPORTED) != 0;
+        // The chunk's batch bounds (tr_chunk_info); lanes past the batch end (a chunk that
+        // straddles one) find their own batch.
+        const uint32_t w0 = __builtin_amdgcn_readfirstlane(ci.x);
+        const uint32_t end0 = __builtin_amdgcn_readfirstlane(ci.y);
+        // (readfirstlane returns int: widen through uint32_t, not by sign extension)
+        const uint64_t ts_base =
+            (uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(ci.w))) << 32) |
+            uint32_t(__builtin_amdgcn_readfirstlane(ci.z));
+        const bool straddle = ubase + cnt > end0;
+        uint64_t ts_event = ts_base + k;
+        bool batch_imported = (w0 & kChunkImported) != 0;
+        bool first_of_batch = false;
         if (active && k >= end0) {
-            uint32_t b = b0 + 1;
+            uint32_t b = (w0 & kChunkBatchMask) + 1;
             while (c.batch_ends[b] <= k) b++;
-            bstart = c.batch_ends[b - 1];
+            const uint32_t bstart = c.batch_ends[b - 1];
             ts_event = ts_event_of(c, b, k);
             batch_imported = (c.events[bstart].flags & TB_TRANSFER_IMPORTED) != 0;
+            first_of_batch = k == bstart;
         }
-        if (!active) ts_event = 0;
-        lds_ts[wv][lane] = ts_event;
-        wave_lds_sync();
+        if (straddle) {
+            lds_ts[wv][lane] = active ? ts_event : 0;
+            wave_lds_sync();
+        }
         // The rows: the events as submitted, stamped with their commit timestamps (rows of
         // events that do not create an object stay dead; an orphaned id keeps its key there).
+        // Stored straight from q (timestamps patched in place): a store whose data sits in a
+        // temporary that the next store reuses makes the compiler wait for the first store's
+        // completion (vmcnt(0)) before the second, serialising the 8 stores.
         uint4* dst = reinterpret_cast<uint4*>(T.tr_rows + c.row_base + base);
+        const bool full = cnt == 64;
+        const uint64_t ts_lane = ts_base + ubase + (lane >> 3);  // + 8 i: event i * 8 + lane / 8
 #pragma unroll
         for (int i = 0; i < 8; i++) {
-            const uint32_t idx = i * 64 + lane;
-            if (idx < cnt * 8) {
-                uint4 v = q[i];
-                if ((lane & 7) == 7) {
-                    const uint64_t ts = lds_ts[wv][i * 8 + (lane >> 3)];
-                    v.z = uint32_t(ts);
-                    v.w = uint32_t(ts >> 32);
-                }
-                dst[idx] = v;
+            if ((lane & 7) == 7) {
+                const uint64_t ts = straddle ? lds_ts[wv][i * 8 + (lane >> 3)] : ts_lane + i * 8;
+                q[i].z = uint32_t(ts);
+                q[i].w = uint32_t(ts >> 32);
             }
+            if (full || i * 64 + lane < cnt * 8) dst[i * 64 + lane] = q[i];
         }
-        const uint32_t ubase = __builtin_amdgcn_readfirstlane(base);
-        const bool prev0 = ubase > 0 && (c.events[ubase - 1].flags & TB_TRANSFER_LINKED) != 0;
         if (active) {
             const tb_transfer_t& t = *reinterpret_cast<const tb_transfer_t*>(my + lane * kLdsEventStride);
             const bool prev_linked =
-                lane > 0 ? (reinterpret_cast<const tb_transfer_t*>(my + (lane - 1) * kLdsEventStride)
-                                ->flags & TB_TRANSFER_LINKED) != 0
-                         : prev0;
+                lane > 0 ? !first_of_batch &&
+                               (reinterpret_cast<const tb_transfer_t*>(my + (lane - 1) * kLdsEventStride)
+                                    ->flags & TB_TRANSFER_LINKED) != 0
+                         : (w0 & kChunkPrevLinked) != 0;
             uint64_t fts = 0;
-            flags |= ingest_event(T, c, k, t, bstart, batch_imported, ts_event, prev_linked, &fts,
+            flags |= ingest_event(T, c, k, t, batch_imported, ts_event, prev_linked, &fts,
                                   c.bucket_counts ? bucket_hist : nullptr);
             n_fast += fts != 0;
             ts_max = fts > ts_max ? fts : ts_max;

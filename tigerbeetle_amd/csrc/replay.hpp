@@ -116,6 +116,8 @@ struct Call {
     // Bucketed balance path (small key spaces): per-bucket item counts, bucket = key >> 13.
     unsigned int* bucket_counts;
     uint32_t n_buckets;
+    // create_transfers: per 64-event chunk, its batch bounds (tr_chunk_info).
+    const uint4* chunk_info;
 };
 
 constexpr uint32_t kNone32 = 0xFFFFFFFFu;
