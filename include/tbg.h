@@ -108,6 +108,11 @@ int tbg_last_stats(tbg_ctx* ctx, tbg_stats* out);
 /* Forces every event through the ordered replay (self-check of the fast path). */
 int tbg_debug_force_replay(tbg_ctx* ctx, int enable);
 
+/* Runs every ordered replay of create_transfers on one lane in call order (replay_kernel) instead
+ * of the flow replay (many lanes, units ordered by the keys they share): a self-check of the
+ * flow replay's exactness. */
+int tbg_debug_serial_replay(tbg_ctx* ctx, int enable);
+
 /* Per-kernel timing with HIP events on the call's stream (off by default; resets the totals).
  * tbg_profile_read returns 1 and fills name / accumulated milliseconds / launches for entry
  * `index`, or 0 past the last entry. */

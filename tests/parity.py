@@ -9,6 +9,7 @@ status (in creation order).
 import ctypes
 import os
 import sys
+import time
 
 import numpy as np
 
@@ -47,13 +48,16 @@ class Pair:
         self.g = self.lib.tbg_open(ctypes.byref(o))
         if not self.g:
             raise RuntimeError("tbg_open failed")
-        if force_replay:
+        if force_replay:  # True: every event through the flow replay; "serial": on one lane
             self.lib.tbg_debug_force_replay(self.g, 1)
+        if force_replay == "serial":
+            self.lib.tbg_debug_serial_replay(self.g, 1)
         self.o = self.olib.tbo_open(pulse_batch_max, pulse_next_timestamp_init)
         self.prepare_timestamp = 0
         self._pulse_delta = pulse_batch_max
         self.calls = 0
         self.stats = {"events": 0, "fast": 0, "replayed": 0, "static_fail": 0}
+        self.seconds = {"gpu": 0.0, "oracle": 0.0}  # wall time of each side's create_* calls
 
     def close(self):
         if self.g:
@@ -123,9 +127,11 @@ class Pair:
         n, lens_a, batch_ts = self._batches(lens)
         r_gpu = np.zeros(n, dtype=RESULT_DTYPE)
         r_orc = np.zeros(n, dtype=RESULT_DTYPE)
+        t0 = time.perf_counter()
         rc = self.lib.tbg_create_transfers(
             self.g, _ptr(events), n, lens_a.ctypes.data_as(native.c_u32p),
             batch_ts.ctypes.data_as(native.c_u64p), len(lens), _ptr(r_gpu))
+        t1 = time.perf_counter()
         if rc != 0:
             raise RuntimeError(f"tbg_create_transfers: {rc} {self.lib.tbg_last_error(self.g)}")
         off = 0
@@ -133,6 +139,8 @@ class Pair:
             self.olib.tbo_create_transfers(self.o, _ptr(events[off:off + ln]), ln,
                                            int(batch_ts[b]), _ptr(r_orc[off:off + ln]))
             off += ln
+        self.seconds["gpu"] += t1 - t0
+        self.seconds["oracle"] += time.perf_counter() - t1
         self.calls += 1
         self._stats()
         self._check("transfers", events, r_gpu, r_orc)

@@ -18,7 +18,7 @@ def _split(n, rng, max_batch):
     return lens
 
 
-@pytest.mark.parametrize("force_replay", [False, True], ids=["parallel", "replay"])
+@pytest.mark.parametrize("force_replay", [False, True, "serial"], ids=["parallel", "flow", "serial"])
 @pytest.mark.parametrize("seed", range(6))
 def test_fuzz(seed, force_replay):
     rng = np.random.default_rng(1000 + seed)
@@ -153,7 +153,7 @@ def _transfers(rows):
     return t
 
 
-@pytest.mark.parametrize("force_replay", [False, True], ids=["parallel", "replay"])
+@pytest.mark.parametrize("force_replay", [False, True, "serial"], ids=["parallel", "flow", "serial"])
 def test_reopened_account_with_limit(force_replay):
     """A transfer that fails `closed` against an account a void in the same call reopens must
     replay with the serial balances of its limited debit account: a later parallel credit to that
@@ -181,7 +181,7 @@ def test_reopened_account_with_limit(force_replay):
         p.close()
 
 
-@pytest.mark.parametrize("force_replay", [False, True], ids=["parallel", "replay"])
+@pytest.mark.parametrize("force_replay", [False, True, "serial"], ids=["parallel", "flow", "serial"])
 def test_account_index_hazards(force_replay):
     """The account index answers the create_transfers checks without the row while an account's
     hazard bits are clear; every way an account becomes closed or gets a balance near 2^128 must
@@ -222,7 +222,7 @@ def test_account_index_hazards(force_replay):
         p.close()
 
 
-@pytest.mark.parametrize("force_replay", [False, True], ids=["parallel", "replay"])
+@pytest.mark.parametrize("force_replay", [False, True, "serial"], ids=["parallel", "flow", "serial"])
 def test_account_index_wide_entries(force_replay):
     """Index entries hold an id's low word and a ledger's low 16 bits: accounts whose id high
     word is nonzero or whose ledger is >= 2^16 are matched and checked through the row. Ids that
@@ -251,6 +251,31 @@ def test_account_index_wide_entries(force_replay):
         ]))
         created = r["status"] == 0xFFFFFFFF
         assert created.tolist() == [True, True, False, True, False, False, True]
+        p.compare_state()
+    finally:
+        p.close()
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_flow_replay_stress(seed):
+    """Every event through the flow replay, with enough events per call for many units to run at
+    once: chains, duplicates, post/void of pending transfers created earlier in the same call,
+    limits and closing, over a small account set (long key chains) -- against the oracle."""
+    rng = np.random.default_rng(5000 + seed)
+    p = Pair(account_capacity=1 << 12, transfer_capacity=1 << 17, batch_events_max=1 << 14,
+             pulse_batch_max=64, pulse_next_timestamp_init=TIMESTAMP_MAX, force_replay=True)
+    try:
+        n_acc = 160
+        clean = workload.accounts(n_acc, seed=seed, id_offset=0, ledger=1)
+        clean["flags"] = rng.choice([0, 0, 0, 2, 4, 8], size=n_acc).astype(np.uint16)
+        p.create_accounts(clean, _split(n_acc, rng, 64))
+        ids_seen = []
+        for step in range(5):
+            pend = np.array(ids_seen[-3000:], dtype=np.uint64) if ids_seen else None
+            t = workload.fuzz_transfers(rng, 6000, 9000, n_acc + 1, pending_ids=pend)
+            ids_seen.extend(int(x) for x in t["id"][:, 0])
+            p.create_transfers(t, _split(len(t), rng, 2048))
+            p.tick(int(rng.integers(1, 3)) * NS_PER_S)
         p.compare_state()
     finally:
         p.close()

@@ -30,6 +30,8 @@ def gpu_handle(force_replay: bool):
     g = lib.tb_sm_executor_gpu(sm)
     if force_replay:
         lib.tbg_debug_force_replay(g, 1)
+    if force_replay == "serial":
+        lib.tbg_debug_serial_replay(g, 1)
 
     def set_balances(i, dp, dpo, cp, cpo):
         U = native.U128.of
@@ -38,7 +40,7 @@ def gpu_handle(force_replay: bool):
     return tablerun.StateMachineHandle(lib, sm, set_balances, lambda: lib.tb_sm_close(sm))
 
 
-@pytest.mark.parametrize("force_replay", [False, True], ids=["parallel", "replay"])
+@pytest.mark.parametrize("force_replay", [False, True, "serial"], ids=["parallel", "flow", "serial"])
 @pytest.mark.parametrize("table", tablerun.table_files())
 def test_gpu_table(table, force_replay):
     rows = tablerun.load_table(f"{tablerun.TABLE_DIR}/{table}")

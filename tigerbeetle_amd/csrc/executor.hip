@@ -14,7 +14,7 @@
 #include <vector>
 
 #include "../../include/tbg.h"
-#include "kernels.hpp"
+#include "flow.hpp"
 
 using namespace tbg;
 
@@ -38,6 +38,19 @@ struct PulseScratch {
     unsigned long long* counters = nullptr;
 };
 
+// Flow replay scratch (flow.hpp), grown on demand to the largest replay list seen.
+struct FlowScratch {
+    uint64_t cap = 0;          // positions
+    uint8_t *head8 = nullptr, *barrier8 = nullptr;
+    uint32_t *heads = nullptr, *unit_of = nullptr, *barriers = nullptr, *vals = nullptr,
+             *vals_sorted = nullptr, *pred = nullptr, *done = nullptr;
+    uint64_t *keys = nullptr, *keys_sorted = nullptr, *pnt_ops = nullptr, *pnt_scan = nullptr;
+    uint32_t* dup_mark = nullptr;  // per event (batch_events_max)
+    unsigned int* counts = nullptr;
+    unsigned long long* pnt_fired = nullptr;
+    UndoEntry* lane_undo = nullptr;
+};
+
 }  // namespace
 
 struct tbg_ctx {
@@ -49,6 +62,7 @@ struct tbg_ctx {
     DevScalars* h_scalars = nullptr;  // pinned
     uint32_t epoch = 0;
     bool force_replay = false;
+    bool serial_replay = false;  // debug: every replay on one lane (replay_kernel)
     tbg_stats stats{};
 
     // per-call scratch (capacity batch_events_max)
@@ -84,6 +98,8 @@ struct tbg_ctx {
     uint32_t* sel_buf = nullptr;  // selection output for dumps / indexes (max rows)
 
     PulseScratch pulse;
+    FlowScratch flow;
+    unsigned long long* flow_debug = nullptr;
     std::vector<uint32_t> h_ends;
 
     // Per-kernel timing (tbg_profile): HIP events recorded on the call's stream between launches.
@@ -277,12 +293,161 @@ int end_call(tbg_ctx* ctx, uint32_t n, bool already_synced = false) {
     return 0;
 }
 
+void free_flow(FlowScratch& F) {
+    void* ptrs[] = {F.head8, F.barrier8, F.heads, F.unit_of, F.barriers, F.vals, F.vals_sorted,
+                    F.pred, F.done, F.keys, F.keys_sorted, F.pnt_ops, F.pnt_scan};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    F.head8 = F.barrier8 = nullptr;
+    F.heads = F.unit_of = F.barriers = F.vals = F.vals_sorted = F.pred = F.done = nullptr;
+    F.keys = F.keys_sorted = F.pnt_ops = F.pnt_scan = nullptr;
+    F.cap = 0;
+}
+
+int ensure_flow(tbg_ctx* ctx, uint64_t m) {
+    FlowScratch& F = ctx->flow;
+    bool ok = true;
+    if (!F.dup_mark) {
+        ok = dev_alloc(ctx, &F.dup_mark, ctx->opt.batch_events_max, true) &&
+             dev_alloc(ctx, &F.counts, 4, true) && dev_alloc(ctx, &F.pnt_fired, 1, true) &&
+             dev_alloc(ctx, &F.lane_undo, uint64_t(kFlowThreads) * kFlowUndoPerLane, false);
+        if (!ok) return TBG_EHIP;
+    }
+    if (m <= F.cap) return 0;
+    free_flow(F);
+    const uint64_t cap = std::max<uint64_t>(next_pow2(m), 1u << 14);
+    const uint64_t kc = kFlowKeys * cap;
+    ok = dev_alloc(ctx, &F.head8, cap, false) && dev_alloc(ctx, &F.barrier8, cap, false) &&
+         dev_alloc(ctx, &F.heads, cap, false) && dev_alloc(ctx, &F.unit_of, cap, false) &&
+         dev_alloc(ctx, &F.barriers, cap, false) && dev_alloc(ctx, &F.done, cap, true) &&
+         dev_alloc(ctx, &F.pnt_ops, cap, false) && dev_alloc(ctx, &F.pnt_scan, cap, false) &&
+         dev_alloc(ctx, &F.vals, kc, false) && dev_alloc(ctx, &F.vals_sorted, kc, false) &&
+         dev_alloc(ctx, &F.pred, kc, false) && dev_alloc(ctx, &F.keys, kc, false) &&
+         dev_alloc(ctx, &F.keys_sorted, kc, false);
+    if (!ok) {
+        free_flow(F);
+        return TBG_EHIP;
+    }
+    F.cap = cap;
+    return 0;
+}
+
+// The flow replay of a create_transfers call (flow.hpp): plan the units and their keys, then
+// execute them on one workgroup; pulse_next_timestamp is resolved afterwards in post/void calls.
+int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned int call_flags) {
+    int rc = ensure_flow(ctx, m);
+    if (rc) return rc;
+    FlowScratch& F = ctx->flow;
+    FlowPlan P{};
+    P.m = m;
+    P.epoch = c.epoch;
+    P.slow_list = c.slow_list;
+    P.head8 = F.head8;
+    P.heads = F.heads;
+    P.counts = F.counts;
+    P.unit_of = F.unit_of;
+    P.barrier8 = F.barrier8;
+    P.barriers = F.barriers;
+    P.dup_mark = F.dup_mark;
+    P.keys = F.keys;
+    P.vals = F.vals;
+    P.keys_sorted = F.keys_sorted;
+    P.vals_sorted = F.vals_sorted;
+    P.pred = F.pred;
+    P.done = F.done;
+    const bool post_void = (call_flags & kFlagPostVoid) != 0;
+    P.pnt_ops = post_void ? F.pnt_ops : nullptr;
+    P.pnt_scan = F.pnt_scan;
+    P.pnt_fired = F.pnt_fired;
+    P.lane_undo = F.lane_undo;
+    const dim3 block(kBlock);
+    hipLaunchKernelGGL(flow_heads, dim3(grid_for(m)), block, 0, ctx->stream, ctx->T, c, P);
+    rc = select_flagged(ctx, F.head8, m, F.heads, &F.counts[0]);
+    if (rc) return rc;
+    hipLaunchKernelGGL(flow_units, dim3(grid_for(m)), block, 0, ctx->stream, P);
+    hipLaunchKernelGGL(flow_keys, dim3(grid_for(m)), block, 0, ctx->stream, ctx->T, c, P,
+                       call_flags);
+    const int pairs = int(kFlowKeys * uint64_t(m));
+    size_t bytes = 0;
+    HIP_TRY(ctx, hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, F.keys, F.keys_sorted, F.vals,
+                                                    F.vals_sorted, pairs, 0, 64, ctx->stream));
+    rc = ensure_cub_temp(ctx, bytes);
+    if (rc) return rc;
+    HIP_TRY(ctx, hipcub::DeviceRadixSort::SortPairs(ctx->cub_temp, bytes, F.keys, F.keys_sorted,
+                                                    F.vals, F.vals_sorted, pairs, 0, 64,
+                                                    ctx->stream));
+    hipLaunchKernelGGL(flow_preds, dim3(grid_for(uint64_t(pairs))), block, 0, ctx->stream, P);
+    rc = select_flagged(ctx, F.barrier8, m, F.barriers, &F.counts[1]);
+    if (rc) return rc;
+    if (post_void) {
+        HIP_TRY(ctx, hipMemsetAsync(F.pnt_ops, 0, uint64_t(m) * 8, ctx->stream));
+        HIP_TRY(ctx, hipMemsetAsync(F.pnt_fired, 0, 8, ctx->stream));
+    }
+    tmark(ctx, "flow_plan");
+    const bool debug = getenv("TBG_FLOW_DEBUG") != nullptr;
+    if (debug) {
+        if (!ctx->flow_debug) HIP_TRY(ctx, hipMalloc(&ctx->flow_debug, 128));
+        HIP_TRY(ctx, hipMemsetAsync(ctx->flow_debug, 0, 128, ctx->stream));
+        P.debug = ctx->flow_debug;
+    }
+    uint32_t lanes = kFlowThreads;
+    { const char* e = getenv("TBG_FLOW_LANES"); if (e) lanes = std::max(64, std::min(int(kFlowThreads), atoi(e))); }
+    hipLaunchKernelGGL(flow_replay, dim3(1), dim3(lanes), 0, ctx->stream, ctx->T, c, P);
+    tmark(ctx, "tr_flow");
+    if (debug) {
+        unsigned int cnt[2] = {0, 0};
+        unsigned long long d[9] = {};
+        (void)hipMemcpyAsync(cnt, F.counts, 8, hipMemcpyDeviceToHost, ctx->stream);
+        (void)hipMemcpyAsync(d, ctx->flow_debug, 72, hipMemcpyDeviceToHost, ctx->stream);
+        (void)hipStreamSynchronize(ctx->stream);
+        // wall_clock64 runs at 100 MHz on MI300-class parts
+        fprintf(stderr, "flow: m=%u units=%u barriers=%u flags=%#x lanes=%u iterations=%llu "
+                "events=%llu exec_us=%.1f engine_us=%.1f\n", m, cnt[0], cnt[1], call_flags, lanes,
+                d[0], d[1], d[2] / 100.0, d[3] / 100.0);
+        const unsigned long long nb = d[4] + d[5] + d[6] + d[7];
+        fprintf(stderr, "flow: blocked on id %llu pid %llu dr %llu cr %llu, mean distance %.1f\n",
+                d[4], d[5], d[6], d[7], nb ? double(d[8]) / nb : 0.0);
+    }
+    if (post_void) {
+        hipLaunchKernelGGL(flow_pnt_prep, dim3(grid_for(m)), block, 0, ctx->stream, P);
+        // prefix minima into keys_sorted (free after the plan)
+        size_t sb = 0;
+        HIP_TRY(ctx, hipcub::DeviceScan::InclusiveScan(nullptr, sb, F.pnt_scan, F.keys_sorted,
+                                                       hipcub::Min(), int(m), ctx->stream));
+        rc = ensure_cub_temp(ctx, sb);
+        if (rc) return rc;
+        HIP_TRY(ctx, hipcub::DeviceScan::InclusiveScan(ctx->cub_temp, sb, F.pnt_scan,
+                                                       F.keys_sorted, hipcub::Min(), int(m),
+                                                       ctx->stream));
+        hipLaunchKernelGGL(flow_pnt_check, dim3(grid_for(m)), block, 0, ctx->stream, ctx->T, P,
+                           F.keys_sorted);
+        hipLaunchKernelGGL(flow_pnt_final, dim3(1), dim3(64), 0, ctx->stream, ctx->T, P,
+                           F.keys_sorted);
+    }
+    HIP_TRY(ctx, hipGetLastError());
+    return 0;
+}
+
 // The replay list (order-preserving), the replay, and the id slots of the replayed events.
 template <typename Event>
 int run_replay(tbg_ctx* ctx, Call<Event>& c, bool is_transfers, bool finalize_everything) {
     int rc = select_flagged(ctx, ctx->ev_slow, c.n, ctx->slow_list, &ctx->d_scalars->slow_count);
     if (rc) return rc;
     tmark(ctx, "select_replay_list");
+    const unsigned int call_flags = ctx->h_scalars->flags;
+    const uint64_t m = ctx->h_scalars->stats[0];
+    if constexpr (__is_same(Event, tb_transfer_t)) {
+        if (!ctx->serial_replay && !(call_flags & kFlagImported) && m > 1 &&
+            m < (1ull << kFlowUnitBits)) {
+            rc = run_flow_replay(ctx, c, uint32_t(m), call_flags);
+            if (rc) return rc;
+            hipLaunchKernelGGL(finalize_slow<Event>, dim3(grid_for(c.n)), dim3(kBlock), 0,
+                               ctx->stream, ctx->T, c, 1);
+            tmark(ctx, "tr_finalize");
+            HIP_TRY(ctx, hipGetLastError());
+            return 0;
+        }
+    }
     hipLaunchKernelGGL(replay_kernel<Event>, dim3(1), dim3(64), 0, ctx->stream, ctx->T, c,
                        is_transfers ? 1 : 0);
     tmark(ctx, is_transfers ? "tr_replay" : "acc_replay");
@@ -509,7 +674,10 @@ void tbg_close(tbg_ctx* ctx) {
                     ctx->bal_items, ctx->chunk_info, ctx->bal_items_sorted, ctx->bucket_words, ctx->bucket_partials,
                     ctx->cub_temp, ctx->acc_ts_index, ctx->tr_ts_index, ctx->sel_buf,
                     ctx->pulse.keep, ctx->pulse.exp, ctx->pulse.ts, ctx->pulse.rows,
-                    ctx->pulse.exp_b, ctx->pulse.rows_b, ctx->pulse.counters};
+                    ctx->pulse.exp_b, ctx->pulse.rows_b, ctx->pulse.counters,
+                    ctx->flow.dup_mark, ctx->flow.counts, ctx->flow.pnt_fired,
+                    ctx->flow.lane_undo};
+    free_flow(ctx->flow);
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     for (hipEvent_t e : ctx->marks)
@@ -830,6 +998,12 @@ int tbg_last_stats(tbg_ctx* ctx, tbg_stats* out) {
 int tbg_debug_force_replay(tbg_ctx* ctx, int enable) {
     if (!ctx) return TBG_EINVAL;
     ctx->force_replay = enable != 0;
+    return 0;
+}
+
+int tbg_debug_serial_replay(tbg_ctx* ctx, int enable) {
+    if (!ctx) return TBG_EINVAL;
+    ctx->serial_replay = enable != 0;
     return 0;
 }
 

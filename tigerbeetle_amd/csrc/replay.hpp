@@ -193,17 +193,39 @@ struct Scope {
     unsigned long long accounts_key_max = 0, transfers_key_max = 0, expiry_count = 0;
 };
 
+// The replay state of one executing lane. Serial mode (replay_kernel: one lane, every replayed
+// event of the call in order) keeps the reference's scope semantics on the shared scalars. Flow
+// mode (flow_replay: many lanes, each executing whole units -- one event or one linked chain --
+// that own every key they touch, see flow.hpp) touches no shared scalar a concurrent unit could
+// also write: the undo log is the lane's own, the transfers key_max is folded in with atomicMax
+// when the unit's effects persist, pulse_next_timestamp updates are recorded per replay position
+// (resolved in order after the replay) or, in calls without post/void where only `min` updates
+// exist, applied with atomicMin, and expires_at entries are appended atomically (entries of a
+// discarded chain stay in the list and are dropped at the next pulse: their rows are not live).
+constexpr uint64_t kPntReset = 1ull << 63;  // pnt_ops: a reset-if-equal (post/void of an expiry)
+
 struct Replay {
     const Tables& T;
     Scope scope;
     uint64_t undo_len = 0;
     bool overflow = false;
+    UndoEntry* undo;
+    uint64_t undo_cap;
+    // flow mode
+    bool concurrent = false;
+    uint64_t* pnt_ops = nullptr;  // per replay position: 0, expires_at (min) or | kPntReset
+    uint32_t pos = 0;             // replay position of the executing event
+    uint64_t key_max = 0, key_max_scope = 0;
 
-    __device__ explicit Replay(const Tables& t) : T(t) {}
+    __device__ explicit Replay(const Tables& t) : T(t), undo(t.undo), undo_cap(t.undo_capacity) {}
 
     __device__ void scope_open() {
         scope.open = true;
         scope.undo_len = undo_len;
+        if (concurrent) {
+            key_max_scope = 0;
+            return;
+        }
         scope.accounts_key_max = T.scalars->accounts_key_max;
         scope.transfers_key_max = T.scalars->transfers_key_max;
         scope.expiry_count = T.scalars->expiry_count;
@@ -211,7 +233,7 @@ struct Replay {
     __device__ void scope_close(bool discard) {
         if (discard) {
             for (uint64_t i = undo_len; i-- > scope.undo_len;) {
-                const UndoEntry& u = T.undo[i];
+                const UndoEntry& u = undo[i];
                 uint64_t idx = u.kind_index & kUndoIndexMask;
                 if ((u.kind_index & ~kUndoIndexMask) == kUndoAccount) {
                     copy_row(&T.acc_rows[idx], &u.row);
@@ -219,31 +241,36 @@ struct Replay {
                     T.tr_status[idx] = (uint8_t)u.row.timestamp;
                 }
             }
-            T.scalars->accounts_key_max = scope.accounts_key_max;
-            T.scalars->transfers_key_max = scope.transfers_key_max;
-            T.scalars->expiry_count = scope.expiry_count;
+            if (!concurrent) {
+                T.scalars->accounts_key_max = scope.accounts_key_max;
+                T.scalars->transfers_key_max = scope.transfers_key_max;
+                T.scalars->expiry_count = scope.expiry_count;
+            }
+        } else if (concurrent && key_max_scope > key_max) {
+            key_max = key_max_scope;
         }
+        key_max_scope = 0;
         undo_len = scope.undo_len;
         scope.open = false;
     }
     __device__ void log_account(uint64_t row) {
         if (!scope.open) return;
-        if (undo_len >= T.undo_capacity) {
+        if (undo_len >= undo_cap) {
             overflow = true;
             return;
         }
-        T.undo[undo_len].kind_index = kUndoAccount | row;
-        copy_row(&T.undo[undo_len].row, &T.acc_rows[row]);
+        undo[undo_len].kind_index = kUndoAccount | row;
+        copy_row(&undo[undo_len].row, &T.acc_rows[row]);
         undo_len++;
     }
     __device__ void log_status(uint64_t row) {
         if (!scope.open) return;
-        if (undo_len >= T.undo_capacity) {
+        if (undo_len >= undo_cap) {
             overflow = true;
             return;
         }
-        T.undo[undo_len].kind_index = kUndoStatus | row;
-        T.undo[undo_len].row.timestamp = T.tr_status[row];
+        undo[undo_len].kind_index = kUndoStatus | row;
+        undo[undo_len].row.timestamp = T.tr_status[row];
         undo_len++;
     }
     __device__ void update_account(uint64_t row, const tb_account_t& next) {
@@ -256,6 +283,36 @@ struct Replay {
     __device__ void update_status(uint64_t row, uint8_t status) {
         log_status(row);
         T.tr_status[row] = status;
+    }
+    // The transfers objects tree key_range.key_max (groove.zig:1780) after an insert at `ts`.
+    __device__ void note_transfer_ts(uint64_t ts) {
+        if (!concurrent) {
+            if (ts > T.scalars->transfers_key_max) T.scalars->transfers_key_max = ts;
+        } else if (scope.open) {
+            if (ts > key_max_scope) key_max_scope = ts;
+        } else if (ts > key_max) {
+            key_max = ts;
+        }
+    }
+    // create_transfer :3975-3982: pulse_next_timestamp = min(pulse_next_timestamp, expires_at).
+    __device__ void pulse_min(uint64_t expires_at) {
+        if (!concurrent) {
+            if (expires_at < T.scalars->pulse_next_timestamp)
+                T.scalars->pulse_next_timestamp = expires_at;
+        } else if (pnt_ops) {
+            pnt_ops[pos] = expires_at;
+        } else {
+            atomicMin(&T.scalars->pulse_next_timestamp, (unsigned long long)expires_at);
+        }
+    }
+    // post_or_void_pending_transfer :4227-4229: reset to timestamp_min if it names this expiry.
+    __device__ void pulse_reset(uint64_t expires_at) {
+        if (!concurrent) {
+            if (T.scalars->pulse_next_timestamp == expires_at)
+                T.scalars->pulse_next_timestamp = TB_TIMESTAMP_MIN;
+        } else {
+            pnt_ops[pos] = expires_at | kPntReset;
+        }
     }
 };
 
@@ -458,10 +515,9 @@ __device__ uint32_t replay_post_or_void(Replay& R, const C& c, uint32_t k, uint6
     o.timestamp = ts_actual;
     T.tr_rows[row] = o;
     T.tr_status[row] = TB_PENDING_NONE;
-    if (ts_actual > T.scalars->transfers_key_max) T.scalars->transfers_key_max = ts_actual;
+    R.note_transfer_ts(ts_actual);
 
-    if (has_expiry && T.scalars->pulse_next_timestamp == expires_at)
-        T.scalars->pulse_next_timestamp = TB_TIMESTAMP_MIN;
+    if (has_expiry) R.pulse_reset(expires_at);
     R.update_status(p_row, (f & TB_TRANSFER_POST_PENDING) ? TB_PENDING_POSTED : TB_PENDING_VOIDED);
 
     tb_account_t dr_new = dr, cr_new = cr;
@@ -587,8 +643,8 @@ __device__ uint32_t replay_create_transfer(Replay& R, const C& c, uint32_t k, ui
     o.timestamp = ts_actual;
     T.tr_rows[row] = o;
     T.tr_status[row] = (f & TB_TRANSFER_PENDING) ? TB_PENDING_PENDING : TB_PENDING_NONE;
-    if (ts_actual > T.scalars->transfers_key_max) T.scalars->transfers_key_max = ts_actual;
-    if ((f & TB_TRANSFER_PENDING) && t.timeout > 0) expiry_append(T, row, true);
+    R.note_transfer_ts(ts_actual);
+    if ((f & TB_TRANSFER_PENDING) && t.timeout > 0) expiry_append(T, row, !R.concurrent);
 
     tb_account_t dr_new = dr, cr_new = cr;
     if (f & TB_TRANSFER_PENDING) {
@@ -603,11 +659,7 @@ __device__ uint32_t replay_create_transfer(Replay& R, const C& c, uint32_t k, ui
     if (amount > 0 || (dr_new.flags & TB_ACCOUNT_CLOSED)) R.update_account(dr_row, dr_new);
     if (amount > 0 || (cr_new.flags & TB_ACCOUNT_CLOSED)) R.update_account(cr_row, cr_new);
 
-    if (t.timeout > 0) {
-        uint64_t expires_at = ts_actual + (uint64_t)t.timeout * TB_NS_PER_S;
-        if (expires_at < T.scalars->pulse_next_timestamp)
-            T.scalars->pulse_next_timestamp = expires_at;
-    }
+    if (t.timeout > 0) R.pulse_min(ts_actual + (uint64_t)t.timeout * TB_NS_PER_S);
     *ts_out = ts_actual;
     return TB_STATUS_CREATED;
 }

@@ -92,6 +92,7 @@ SIGNATURES = [
     ("tbg_debug_set_account_balances", ctypes.c_int, [vp, U128, U128, U128, U128, U128]),
     ("tbg_last_stats", ctypes.c_int, [vp, ctypes.POINTER(TbgStats)]),
     ("tbg_debug_force_replay", ctypes.c_int, [vp, ctypes.c_int]),
+    ("tbg_debug_serial_replay", ctypes.c_int, [vp, ctypes.c_int]),
     ("tbg_profile", ctypes.c_int, [vp, ctypes.c_int]),
     ("tbg_profile_read", ctypes.c_int, [vp, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32,
                                        ctypes.POINTER(ctypes.c_double), c_u64p]),

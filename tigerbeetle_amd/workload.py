@@ -106,16 +106,30 @@ def transfers_hot_limits(n: int, n_accounts: int = 10_000, n_hot: int = 100, see
     return t
 
 
-def funding_transfers(n_hot: int, amount: int, id_offset: int, source_index: int = 0):
-    """One transfer per hot account from the unlimited source (account index 0 -> id 1)."""
+def funding_transfers(n_hot: int, amount, id_offset: int, source_index: int = 0):
+    """One transfer per hot account from the unlimited source (account index 0 -> id 1);
+    `amount` is one value for all or one per hot account."""
     t = np.zeros(n_hot, dtype=TRANSFER_DTYPE)
     _u128_col(t, "id", np.arange(id_offset + 1, id_offset + n_hot + 1, dtype=U64))
     _u128_col(t, "debit_account_id", np.full(n_hot, source_index + 1, dtype=U64))
     _u128_col(t, "credit_account_id", np.arange(2, n_hot + 2, dtype=U64))
-    _u128_col(t, "amount", np.full(n_hot, amount, dtype=U64))
+    _u128_col(t, "amount", np.broadcast_to(np.asarray(amount, dtype=U64), (n_hot,)).copy())
     t["ledger"] = 2
     t["code"] = 1
     return t
+
+
+def hot_funding_amounts(t: np.ndarray, n_hot: int = 100, fraction: float = 0.8) -> np.ndarray:
+    """Config 3 funding per hot account: `fraction` of what the stream `t` debits from it, less
+    what the stream credits to it -- so that roughly the last (1 - fraction) of each hot
+    account's debits find its credits exhausted (exceeds_credits)."""
+    dr = t["debit_account_id"][:, 0].astype(np.int64) - 2   # hot accounts are ids 2..n_hot+1
+    cr = t["credit_account_id"][:, 0].astype(np.int64) - 2
+    amt = t["amount"][:, 0].astype(np.float64)
+    hot_d, hot_c = (dr >= 0) & (dr < n_hot), (cr >= 0) & (cr < n_hot)
+    debits = np.bincount(dr[hot_d], weights=amt[hot_d], minlength=n_hot)
+    credits = np.bincount(cr[hot_c], weights=amt[hot_c], minlength=n_hot)
+    return np.maximum(fraction * debits - credits, 0).astype(U64)
 
 
 def transfers_two_phase(n: int, n_accounts: int, seed: int, id_offset: int,
