@@ -45,6 +45,7 @@ struct FlowScratch {
     uint32_t *heads = nullptr, *unit_of = nullptr, *barriers = nullptr, *vals = nullptr,
              *vals_sorted = nullptr, *pred = nullptr, *done = nullptr;
     uint64_t *keys = nullptr, *keys_sorted = nullptr, *pnt_ops = nullptr, *pnt_scan = nullptr;
+    Step* steps = nullptr;
     uint32_t* dup_mark = nullptr;  // per event (batch_events_max)
     unsigned int* counts = nullptr;
     unsigned long long* pnt_fired = nullptr;
@@ -295,12 +296,13 @@ int end_call(tbg_ctx* ctx, uint32_t n, bool already_synced = false) {
 
 void free_flow(FlowScratch& F) {
     void* ptrs[] = {F.head8, F.barrier8, F.heads, F.unit_of, F.barriers, F.vals, F.vals_sorted,
-                    F.pred, F.done, F.keys, F.keys_sorted, F.pnt_ops, F.pnt_scan};
+                    F.pred, F.done, F.keys, F.keys_sorted, F.pnt_ops, F.pnt_scan, F.steps};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     F.head8 = F.barrier8 = nullptr;
     F.heads = F.unit_of = F.barriers = F.vals = F.vals_sorted = F.pred = F.done = nullptr;
     F.keys = F.keys_sorted = F.pnt_ops = F.pnt_scan = nullptr;
+    F.steps = nullptr;
     F.cap = 0;
 }
 
@@ -323,7 +325,7 @@ int ensure_flow(tbg_ctx* ctx, uint64_t m) {
          dev_alloc(ctx, &F.pnt_ops, cap, false) && dev_alloc(ctx, &F.pnt_scan, cap, false) &&
          dev_alloc(ctx, &F.vals, kc, false) && dev_alloc(ctx, &F.vals_sorted, kc, false) &&
          dev_alloc(ctx, &F.pred, kc, false) && dev_alloc(ctx, &F.keys, kc, false) &&
-         dev_alloc(ctx, &F.keys_sorted, kc, false);
+         dev_alloc(ctx, &F.keys_sorted, kc, false) && dev_alloc(ctx, &F.steps, cap, false);
     if (!ok) {
         free_flow(F);
         return TBG_EHIP;
@@ -360,6 +362,7 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
     P.pnt_scan = F.pnt_scan;
     P.pnt_fired = F.pnt_fired;
     P.lane_undo = F.lane_undo;
+    P.steps = F.steps;
     const dim3 block(kBlock);
     hipLaunchKernelGGL(flow_heads, dim3(grid_for(m)), block, 0, ctx->stream, ctx->T, c, P);
     rc = select_flagged(ctx, F.head8, m, F.heads, &F.counts[0]);

@@ -64,8 +64,17 @@ struct FlowPlan {
     uint64_t* pnt_scan;
     unsigned long long* pnt_fired;
     UndoEntry* lane_undo;        // kFlowUndoPerLane per lane
+    struct Step* steps;          // per position: what the engine prefetches before it waits
     unsigned long long* debug;   // optional: [0] loop iterations, [1] events, [2] cycles executing,
                                  // [3] cycles of the engine (lane 0)
+};
+
+// Per position, everything the replay reads that no other unit writes, so the engine loads it
+// while the position's keys are still held by earlier units.
+struct Step {
+    uint64_t ts_event;
+    uint32_t batch, flags;  // StepInfo
+    uint32_t k, slot, dr, cr;  // the event and its EvRefs
 };
 
 __device__ inline uint64_t flow_key(uint32_t type, uint32_t index, uint32_t unit) {
@@ -156,6 +165,17 @@ __global__ void flow_keys(Tables T, Call<tb_transfer_t> c, FlowPlan P, unsigned 
         if (dr != kNone32) key[2] = flow_key(1, dr, u);
         if (cr != kNone32) key[3] = flow_key(1, cr, u);
     }
+    const StepInfo si = step_info(c, k, uint16_t(TB_TRANSFER_IMPORTED));
+    const EvRefs x = ev_refs(c, k);
+    Step st;
+    st.ts_event = si.ts_event;
+    st.batch = si.batch;
+    st.flags = si.flags;
+    st.k = k;
+    st.slot = x.slot;
+    st.dr = x.dr;
+    st.cr = x.cr;
+    P.steps[s] = st;
 #pragma unroll
     for (uint32_t j = 0; j < kFlowKeys; j++) {
         P.keys[kFlowKeys * uint64_t(s) + j] = key[j];
@@ -208,18 +228,29 @@ __global__ void __launch_bounds__(kFlowThreads) flow_replay(Tables T, Call<tb_tr
     const uint64_t t_start = wall_clock64();
     uint64_t it_count = 0, ev_count = 0, exec_cycles = 0, blocked[kFlowKeys] = {}, blocked_dist = 0;
     uint32_t u = atomicAdd(&next_unit, 1u);
-    uint32_t s = 0, end = 0, j = 0;
+    uint32_t s = 0, end = 0, need = 0;
     bool barrier = false;
+    Step st;
+    tb_transfer_t ev;
+    uint4 pr;
+    // The position's prefetch: its step record, event and predecessors.
+    auto load_position = [&]() {
+        st = P.steps[s];
+        ev = c.events[st.k];
+        pr = *reinterpret_cast<const uint4*>(P.pred + kFlowKeys * uint64_t(s));
+        need = (pr.x != kNone32 ? 1u : 0u) | (pr.y != kNone32 ? 2u : 0u) |
+               (pr.z != kNone32 ? 4u : 0u) | (pr.w != kNone32 ? 8u : 0u);
+    };
     auto begin_unit = [&]() {
         if (u >= units) return;
         s = P.heads[u];
         end = u + 1 < units ? P.heads[u + 1] : P.m;
-        j = 0;
         barrier = P.barrier8[u] != 0;
         R.undo = barrier ? T.undo : my_undo;
         R.undo_cap = barrier ? T.undo_capacity : kFlowUndoPerLane;
         R.undo_len = 0;
         R.key_max = 0;
+        load_position();
     };
     begin_unit();
     while (u < units) {
@@ -232,26 +263,36 @@ __global__ void __launch_bounds__(kFlowThreads) flow_replay(Tables T, Call<tb_tr
         else if (u == gate)
             ready = __hip_atomic_load(&done_count, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == u;
         else ready = true;
-        for (; ready && j < kFlowKeys; j++) {
-            const uint32_t p = P.pred[kFlowKeys * uint64_t(s) + j];
-            if (p != kNone32 && flow_load(&P.done[p]) != P.epoch) ready = false;
-            if (!ready) {
+        if (ready && need) {
+            // The predecessors still outstanding, loaded together.
+            const uint32_t d0 = (need & 1) ? flow_load(&P.done[pr.x]) : P.epoch;
+            const uint32_t d1 = (need & 2) ? flow_load(&P.done[pr.y]) : P.epoch;
+            const uint32_t d2 = (need & 4) ? flow_load(&P.done[pr.z]) : P.epoch;
+            const uint32_t d3 = (need & 8) ? flow_load(&P.done[pr.w]) : P.epoch;
+            need &= (d0 != P.epoch ? 1u : 0u) | (d1 != P.epoch ? 2u : 0u) |
+                    (d2 != P.epoch ? 4u : 0u) | (d3 != P.epoch ? 8u : 0u);
+            if (need) {
+                ready = false;
                 if (P.debug) {
-                    blocked[j]++;
-                    blocked_dist += u - p;
+                    const uint32_t q = __builtin_ctz(need);
+                    blocked[q]++;
+                    blocked_dist += u - (q == 0 ? pr.x : q == 1 ? pr.y : q == 2 ? pr.z : pr.w);
                 }
-                break;
             }
         }
         it_count++;
         if (!ready) {
-            __builtin_amdgcn_s_sleep(2);
+            __builtin_amdgcn_s_sleep(1);
             continue;
         }
         R.pos = s;
         const uint64_t t0 = P.debug ? wall_clock64() : 0;
-        replay_chain_step<tb_transfer_t>(R, c, P.slow_list[s], true, chain_open, chain_start,
-                                         chain_broken);
+        StepInfo si;
+        si.ts_event = st.ts_event;
+        si.batch = st.batch;
+        si.flags = st.flags;
+        replay_chain_step_at<tb_transfer_t>(R, c, st.k, ev, si, EvRefs{st.slot, st.dr, st.cr},
+                                            true, chain_open, chain_start, chain_broken);
         if (P.debug) {
             exec_cycles += wall_clock64() - t0;
             ev_count++;
@@ -261,8 +302,10 @@ __global__ void __launch_bounds__(kFlowThreads) flow_replay(Tables T, Call<tb_tr
             R.overflow = false;
         }
         s++;
-        j = 0;
-        if (s < end) continue;
+        if (s < end) {
+            load_position();
+            continue;
+        }
         // The unit is finished: publish its effects, then its completion.
         if (R.key_max) atomicMax(&T.scalars->transfers_key_max, (unsigned long long)R.key_max);
         __hip_atomic_store(&P.done[u], P.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);

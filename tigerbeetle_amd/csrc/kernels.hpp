@@ -952,15 +952,13 @@ __global__ void bal_bucket_apply(BalTarget B, BucketPlan P, const uint64_t* part
 // ================================ the ordered replay ========================================
 
 template <typename Event>
-__device__ inline void replay_chain_step(Replay& R, const Call<Event>& c, uint32_t k,
-                                         bool is_transfers, bool& chain_open,
-                                         uint32_t& chain_start, bool& chain_broken) {
+__device__ inline void replay_chain_step_at(Replay& R, const Call<Event>& c, uint32_t k,
+                                            const Event& ev, const StepInfo& si, const EvRefs& x,
+                                            bool is_transfers, bool& chain_open,
+                                            uint32_t& chain_start, bool& chain_broken) {
     const Tables& T = R.T;
-    const Event ev = c.events[k];
-    const uint32_t b = batch_of(c.batch_ends, c.n_batches, k);
-    const uint32_t bstart = batch_start_of(c, b);
-    const uint32_t bend = c.batch_ends[b];
-    const uint64_t ts_event = ts_event_of(c, b, k);
+    const uint32_t b = si.batch;
+    const uint64_t ts_event = si.ts_event;
     const uint16_t linked_flag = is_transfers ? TB_TRANSFER_LINKED : TB_ACCOUNT_LINKED;
     const uint16_t imported_flag = is_transfers ? TB_TRANSFER_IMPORTED : TB_ACCOUNT_IMPORTED;
     const uint16_t f = ev.flags;
@@ -975,7 +973,7 @@ __device__ inline void replay_chain_step(Replay& R, const Call<Event>& c, uint32
                 chain_broken = false;
                 R.scope_open();
             }
-            if (k == bend - 1) {
+            if (si.flags & StepInfo::kLastOfBatch) {
                 status = TB_CT_LINKED_EVENT_CHAIN_OPEN;
                 break;
             }
@@ -984,7 +982,7 @@ __device__ inline void replay_chain_step(Replay& R, const Call<Event>& c, uint32
             status = TB_CT_LINKED_EVENT_FAILED;
             break;
         }
-        const bool batch_imported = (c.events[bstart].flags & imported_flag) != 0;
+        const bool batch_imported = (si.flags & StepInfo::kBatchImported) != 0;
         const bool imported = (f & imported_flag) != 0;
         if (batch_imported != imported) {
             if (is_transfers)
@@ -1010,10 +1008,10 @@ __device__ inline void replay_chain_step(Replay& R, const Call<Event>& c, uint32
         }
         uint64_t ts = ts_event;
         if constexpr (__is_same(Event, tb_transfer_t)) {
-            status = replay_create_transfer(R, c, k, ts_event, ev, &ts);
+            status = replay_create_transfer(R, c, k, ts_event, ev, x, &ts);
             if (status == TB_STATUS_CREATED || status == TB_CT_EXISTS) ts_actual = ts;
         } else {
-            status = replay_create_account(R, c, k, ts_event, ev, &ts);
+            status = replay_create_account(R, c, k, ts_event, ev, x, &ts);
             if (status == TB_STATUS_CREATED || status == TB_CA_EXISTS) ts_actual = ts;
         }
     } while (0);
@@ -1021,9 +1019,9 @@ __device__ inline void replay_chain_step(Replay& R, const Call<Event>& c, uint32
     // The event becomes the holder of its id's slot when it created or orphaned the id.
     const bool transient = is_transfers && status != TB_STATUS_CREATED &&
                            tb_transfer_status_transient(status);
-    if ((status == TB_STATUS_CREATED || transient) && c.ev_slot[k] != kNone32) {
+    if ((status == TB_STATUS_CREATED || transient) && x.slot != kNone32) {
         unsigned long long* slots = is_transfers ? T.tr.slots : T.acc.slots;
-        slots[c.ev_slot[k]] = (c.row_base + k + 1) | id_tag(ev.id);
+        slots[x.slot] = (c.row_base + k + 1) | id_tag(ev.id);
     }
     if (status != TB_STATUS_CREATED && chain_open && !chain_broken) {
         chain_broken = true;
@@ -1041,6 +1039,30 @@ __device__ inline void replay_chain_step(Replay& R, const Call<Event>& c, uint32
         chain_open = false;
         chain_broken = false;
     }
+}
+
+// The event's batch facts, from the batch bounds (serial replay) or precomputed (flow plan).
+template <typename Event>
+__device__ inline StepInfo step_info(const Call<Event>& c, uint32_t k, uint16_t imported_flag) {
+    const uint32_t b = batch_of(c.batch_ends, c.n_batches, k);
+    StepInfo si;
+    si.ts_event = ts_event_of(c, b, k);
+    si.batch = b;
+    si.flags = (k == c.batch_ends[b] - 1 ? StepInfo::kLastOfBatch : 0u) |
+               ((c.events[batch_start_of(c, b)].flags & imported_flag) ? StepInfo::kBatchImported
+                                                                        : 0u);
+    return si;
+}
+
+template <typename Event>
+__device__ inline void replay_chain_step(Replay& R, const Call<Event>& c, uint32_t k,
+                                         bool is_transfers, bool& chain_open,
+                                         uint32_t& chain_start, bool& chain_broken) {
+    const Event ev = c.events[k];
+    const StepInfo si =
+        step_info(c, k, is_transfers ? uint16_t(TB_TRANSFER_IMPORTED) : uint16_t(TB_ACCOUNT_IMPORTED));
+    replay_chain_step_at<Event>(R, c, k, ev, si, ev_refs(c, k), is_transfers, chain_open,
+                                chain_start, chain_broken);
 }
 
 template <typename Event>

@@ -140,6 +140,26 @@ __device__ inline uint64_t slot_of(const C& c, uint32_t k) {
     return s == kNone32 ? kNone : uint64_t(s);
 }
 
+// An event's per-call records the replay reads: its id slot and account rows (kNone32 = none).
+struct EvRefs {
+    uint32_t slot, dr, cr;
+};
+template <typename C>
+__device__ inline EvRefs ev_refs(const C& c, uint32_t k) {
+    return EvRefs{c.ev_slot[k], c.ev_dr ? c.ev_dr[k] : kNone32, c.ev_cr ? c.ev_cr[k] : kNone32};
+}
+// Batch facts of a replayed event (execute_multi_batch / execute_create): its timestamp, its batch,
+// whether it is the batch's last event (a linked flag there is linked_event_chain_open) and
+// whether its batch is imported.
+struct StepInfo {
+    uint64_t ts_event;
+    uint32_t batch;
+    uint32_t flags;
+    static constexpr uint32_t kLastOfBatch = 1, kBatchImported = 2;
+};
+
+__device__ inline uint64_t slot_or_none(uint32_t s) { return s == kNone32 ? kNone : uint64_t(s); }
+
 __device__ inline uint32_t batch_of(const uint32_t* ends, uint32_t n_batches, uint32_t k) {
     uint32_t lo = 0, hi = n_batches;  // first b with ends[b] > k
     while (lo < hi) {
@@ -539,7 +559,8 @@ __device__ uint32_t replay_post_or_void(Replay& R, const C& c, uint32_t k, uint6
 
 template <typename C>
 __device__ uint32_t replay_create_transfer(Replay& R, const C& c, uint32_t k, uint64_t ts_event,
-                                           const tb_transfer_t& t, uint64_t* ts_out) {
+                                           const tb_transfer_t& t, const EvRefs& x,
+                                           uint64_t* ts_out) {
     const Tables& T = R.T;
     const uint16_t f = t.flags;
     if (f & TB_TRANSFER_PADDING_MASK) return TB_CT_RESERVED_FLAG;
@@ -547,7 +568,7 @@ __device__ uint32_t replay_create_transfer(Replay& R, const C& c, uint32_t k, ui
     if (u128_is_max(t.id)) return TB_CT_ID_MUST_NOT_BE_INT_MAX;
 
     uint64_t e_row = 0;
-    switch (replay_get_transfer_at_slot(T, c, slot_of(c, k), k, &e_row)) {
+    switch (replay_get_transfer_at_slot(T, c, slot_or_none(x.slot), k, &e_row)) {
         case 1: {
             const tb_transfer_t e = T.tr_rows[e_row];
             if ((t.flags == e.flags) && U(t.pending_id) == U(e.pending_id) &&
@@ -582,9 +603,9 @@ __device__ uint32_t replay_create_transfer(Replay& R, const C& c, uint32_t k, ui
     if (t.ledger == 0) return TB_CT_LEDGER_MUST_NOT_BE_ZERO;
     if (t.code == 0) return TB_CT_CODE_MUST_NOT_BE_ZERO;
 
-    const uint32_t dr_row = c.ev_dr[k];
+    const uint32_t dr_row = x.dr;
     if (dr_row == kNone32) return TB_CT_DEBIT_ACCOUNT_NOT_FOUND;
-    const uint32_t cr_row = c.ev_cr[k];
+    const uint32_t cr_row = x.cr;
     if (cr_row == kNone32) return TB_CT_CREDIT_ACCOUNT_NOT_FOUND;
     const tb_account_t dr = T.acc_rows[dr_row];
     const tb_account_t cr = T.acc_rows[cr_row];
@@ -732,14 +753,15 @@ __device__ inline tb_account_t account_row_of(const tb_account_t& a, uint64_t ts
 
 template <typename C>
 __device__ uint32_t replay_create_account(Replay& R, const C& c, uint32_t k, uint64_t ts_event,
-                                          const tb_account_t& a, uint64_t* ts_out) {
+                                          const tb_account_t& a, const EvRefs& x,
+                                          uint64_t* ts_out) {
     const Tables& T = R.T;
     if (a.reserved != 0) return TB_CA_RESERVED_FIELD;
     if (a.flags & TB_ACCOUNT_PADDING_MASK) return TB_CA_RESERVED_FLAG;
     if (u128_is_zero(a.id)) return TB_CA_ID_MUST_NOT_BE_ZERO;
     if (u128_is_max(a.id)) return TB_CA_ID_MUST_NOT_BE_INT_MAX;
     uint64_t e_row = 0;
-    if (replay_get_account_at_slot(T, c, slot_of(c, k), k, &e_row) == 1) {
+    if (replay_get_account_at_slot(T, c, slot_or_none(x.slot), k, &e_row) == 1) {
         const tb_account_t e = T.acc_rows[e_row];
         return create_account_exists(a, e, ts_out);
     }
