@@ -66,8 +66,13 @@ def parse_args():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--transfers", type=int, default=10_000_000)
-    ap.add_argument("--accounts", type=int, default=10_000)
+    ap.add_argument("--workload", choices=["config2", "config5"], default="config2",
+                    help="config2 (default, the metric's workload) or config5 (many accounts over "
+                         "64 ledgers sharded by ledger)")
+    ap.add_argument("--transfers", type=int, default=None,
+                    help="events per step (config2: 10M, config5: 1M super-batch)")
+    ap.add_argument("--accounts", type=int, default=None,
+                    help="accounts per GPU (config2: 10k, config5: 125M = 1B / 8)")
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="bounded CPU-oracle sample (rank 0, N=1)")
@@ -169,7 +174,7 @@ def measured_traffic(kernel):
         return None, None
 
 
-def cpu_baseline(args, acc, base, lens):
+def cpu_baseline(args, acc, base, lens, label):
     """The serial C oracle (oracle/liboracle.so) on one core, bounded sample of the workload."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_binding
@@ -196,28 +201,127 @@ def cpu_baseline(args, acc, base, lens):
     elapsed = time.perf_counter() - t0
     olib.tbo_close(o)
     return {"value": done / elapsed, "unit": "transfers/s", "cores": 1, "kind": "port",
-            "sample": f"{done} of the {len(base)} config-2 transfers ({b} batches of <= {BATCH}) "
+            "sample": f"{done} of the {len(base)} {label} transfers ({b} batches of <= {BATCH}) "
                       f"through oracle/tb_oracle.c, single-threaded, {elapsed:.1f} s"}
+
+
+class Config2:
+    """BASELINE.json configs[1]: 10k accounts (ledger 2 + rank), 10M uniform transfers per step."""
+    name = "config2"
+
+    def __init__(self, args, rank, world):
+        self.N = args.transfers or 10_000_000
+        self.A = args.accounts or 10_000
+        self.ledger = 2 + rank
+        self.acc = workload.accounts(self.A, seed=args.seed, ledger=self.ledger)
+        self.base = workload.transfers_uniform(self.N, self.A, seed=args.seed, ledger=self.ledger)
+        self.dr = self.base["debit_account_id"][:, 0].astype(np.int64) - 1
+        self.cr = self.base["credit_account_id"][:, 0].astype(np.int64) - 1
+        self.chunk = self.A
+        self.default = (self.N, self.A) == (10_000_000, 10_000)
+        self.config = {"workload": "config2: 10k accounts, 10M uniform create_transfers in "
+                                   "8189-event batches, 1 ledger shard per GPU",
+                       "transfers_per_step_per_gpu": self.N, "accounts_per_gpu": self.A}
+
+    def account_chunks(self):
+        yield self.acc
+
+    def validate(self, lib, g, reps):
+        """Every account's final balances equal the exact per-account sums (the workload is
+        order-independent, so this is the serial reference outcome)."""
+        dump = np.zeros(self.A, dtype=ACCOUNT_DTYPE)
+        assert lib.tbg_dump_accounts(g, dump.ctypes.data_as(ctypes.c_void_p)) == self.A
+        amt = self.base["amount"][:, 0].astype(np.int64)
+        exp_d = np.bincount(self.dr, weights=amt, minlength=self.A).astype(np.int64) * reps
+        exp_c = np.bincount(self.cr, weights=amt, minlength=self.A).astype(np.int64) * reps
+        ok = bool((dump["debits_posted"][:, 0].astype(np.int64) == exp_d).all())
+        ok &= bool((dump["credits_posted"][:, 0].astype(np.int64) == exp_c).all())
+        ok &= bool((dump["debits_posted"][:, 1] == 0).all() and (dump["credits_pending"] == 0).all())
+        return ok
+
+    def cpu_sample(self):
+        return self.acc, self.base, "config-2"
+
+
+class Config5:
+    """BASELINE.json configs[4], per GPU: `accounts` accounts (default 1B / 8 = 125M, what each
+    GPU holds at 8 GPUs) of the shard's 64 / G ledgers (account k on ledger 1 + k mod 64), one
+    1M-event super-batch per step, ledger uniform then debit / credit uniform within it."""
+    name = "config5"
+
+    def __init__(self, args, rank, world):
+        self.N = args.transfers or 1_000_000
+        self.A = args.accounts or 125_000_000
+        self.rank, self.world = rank, world
+        self.base, self.dr, self.cr = workload.transfers_config5(self.N, self.A, rank, world,
+                                                                 seed=args.seed)
+        self.chunk = min(self.A, 4_000_000)
+        self.default = False
+        first, per = workload.config5_ledgers(rank, world)
+        self.config = {"workload": f"config5: {self.A} accounts per GPU on {per} of 64 ledgers "
+                                   f"(1B accounts over 8 GPUs), 1M-event super-batches of "
+                                   f"8189-event batches, sharded by ledger",
+                       "transfers_per_step_per_gpu": self.N, "accounts_per_gpu": self.A,
+                       "ledgers_per_gpu": per}
+
+    def account_chunks(self):
+        for j0 in range(0, self.A, self.chunk):
+            j = np.arange(j0, min(self.A, j0 + self.chunk), dtype=np.int64)
+            yield workload.accounts_config5(j, self.rank, self.world)
+            if j0 and (j0 // self.chunk) % 8 == 0:
+                print(f"config5: {j0 + len(j)} accounts created", file=sys.stderr, flush=True)
+
+    def validate(self, lib, g, reps):
+        """Sampled (SURVEY.md §8d at 1B scale): 65,536 touched accounts and 4,096 others looked up
+        by id; their balances must equal the exact sums of the steps' amounts."""
+        rng = np.random.default_rng(5)
+        touched = np.unique(np.concatenate([self.dr, self.cr]))
+        sample = np.concatenate([rng.choice(touched, size=min(65_536, len(touched)), replace=False),
+                                 rng.integers(0, self.A, size=4_096)])
+        sample = np.unique(sample)
+        amt = self.base["amount"][:, 0].astype(np.int64)
+        pos = np.full(self.A, -1, dtype=np.int64)
+        pos[sample] = np.arange(len(sample))
+        exp_d = np.zeros(len(sample), dtype=np.int64)
+        exp_c = np.zeros(len(sample), dtype=np.int64)
+        md, mc = pos[self.dr] >= 0, pos[self.cr] >= 0
+        np.add.at(exp_d, pos[self.dr[md]], amt[md])
+        np.add.at(exp_c, pos[self.cr[mc]], amt[mc])
+        ids = np.zeros((len(sample), 2), dtype=np.uint64)
+        ids[:, 0] = (workload.config5_global_index(sample, self.rank, self.world) + 1)
+        out = np.zeros(len(sample), dtype=ACCOUNT_DTYPE)
+        found = lib.tbg_lookup_accounts(g, ids.ctypes.data_as(ctypes.c_void_p), len(sample),
+                                        out.ctypes.data_as(ctypes.c_void_p))
+        ok = found == len(sample) and bool((out["id"][:, 0] == ids[:, 0]).all())
+        ok &= bool((out["debits_posted"][:, 0].astype(np.int64) == exp_d * reps).all())
+        ok &= bool((out["credits_posted"][:, 0].astype(np.int64) == exp_c * reps).all())
+        return ok
+
+    def cpu_sample(self):
+        """The oracle holds only the accounts the sampled transfers touch (its hash maps do not
+        depend on the account count): the first 1M transfers of the stream."""
+        n = min(self.N, 1_000_000)
+        j = np.unique(np.concatenate([self.dr[:n], self.cr[:n]]))
+        return workload.accounts_config5(j, self.rank, self.world), self.base[:n], "config-5"
 
 
 def main():
     args = parse_args()
     world, rank, local, dist = dist_init(args)
-    N, A, K, W = args.transfers, args.accounts, args.steps, args.warmup
+    wl = (Config5 if args.workload == "config5" else Config2)(args, rank, world)
+    N, A, K, W = wl.N, wl.A, args.steps, args.warmup
     lib = native.load()
     dev = Device()
     dev.set_device(local)
 
-    ledger = 2 + rank
-    acc = workload.accounts(A, seed=args.seed, ledger=ledger)
-    base = workload.transfers_uniform(N, A, seed=args.seed, ledger=ledger)
+    base = wl.base
     lens = batch_plan(N)
     ends = np.cumsum(lens).astype(np.uint32)
 
     opt = native.TbgOptions()
     opt.account_capacity = A
     opt.transfer_capacity = N * (K + W)
-    opt.batch_events_max = N
+    opt.batch_events_max = max(N, wl.chunk)
     opt.batch_count_max = len(lens)
     opt.pulse_batch_max = 8190
     opt.device = local
@@ -225,15 +329,19 @@ def main():
     g = lib.tbg_open(ctypes.byref(opt))
     assert g, "tbg_open failed"
 
-    res_acc = np.zeros(A, dtype=RESULT_DTYPE)
-    a_lens = np.asarray([A], dtype=np.uint32)
-    a_ts = np.asarray([1 + A], dtype=np.uint64)
-    rc = lib.tbg_create_accounts(g, acc.ctypes.data_as(ctypes.c_void_p), A,
-                                 a_lens.ctypes.data_as(native.c_u32p),
-                                 a_ts.ctypes.data_as(native.c_u64p), 1,
-                                 res_acc.ctypes.data_as(ctypes.c_void_p))
-    assert rc == 0 and (res_acc["status"] == 0xFFFFFFFF).all()
-    prepare_ts = 1 + A
+    prepare_ts = 0
+    for acc in wl.account_chunks():
+        res_acc = np.zeros(len(acc), dtype=RESULT_DTYPE)
+        a_lens = np.asarray([len(acc)], dtype=np.uint32)
+        prepare_ts += 1 + len(acc)
+        a_ts = np.asarray([prepare_ts], dtype=np.uint64)
+        rc = lib.tbg_create_accounts(g, acc.ctypes.data_as(ctypes.c_void_p), len(acc),
+                                     a_lens.ctypes.data_as(native.c_u32p),
+                                     a_ts.ctypes.data_as(native.c_u64p), 1,
+                                     res_acc.ctypes.data_as(ctypes.c_void_p))
+        assert rc == 0 and (res_acc["status"] == 0xFFFFFFFF).all(), \
+            f"create_accounts: {rc} {lib.tbg_last_error(g)}"
+        del acc, res_acc
 
     # Per-step inputs, resident in HBM before timing: fresh ids per step.
     d_ends = dev.upload(ends)
@@ -286,22 +394,13 @@ def main():
         for s in range(W + K):
             dev.download(steps[s][2], r)
             ok &= bool((r["status"] == 0xFFFFFFFF).all())
-        dump = np.zeros(A, dtype=ACCOUNT_DTYPE)
-        assert lib.tbg_dump_accounts(g, dump.ctypes.data_as(ctypes.c_void_p)) == A
-        dr = base["debit_account_id"][:, 0].astype(np.int64) - 1
-        cr = base["credit_account_id"][:, 0].astype(np.int64) - 1
-        amt = base["amount"][:, 0].astype(np.int64)
-        exp_d = np.bincount(dr, weights=amt, minlength=A).astype(np.int64) * (W + K)
-        exp_c = np.bincount(cr, weights=amt, minlength=A).astype(np.int64) * (W + K)
-        ok &= bool((dump["debits_posted"][:, 0].astype(np.int64) == exp_d).all())
-        ok &= bool((dump["credits_posted"][:, 0].astype(np.int64) == exp_c).all())
-        ok &= bool((dump["debits_posted"][:, 1] == 0).all() and (dump["credits_pending"] == 0).all())
+        ok &= wl.validate(lib, g, W + K)
         validated = ok
         if not ok:
             print(json.dumps({"error": "validation failed"}), file=sys.stderr)
 
     # Algorithmic bytes of the path: 288 B per event + 256 B per distinct account.
-    distinct = len(np.union1d(base["debit_account_id"][:, 0], base["credit_account_id"][:, 0]))
+    distinct = len(np.union1d(wl.dr, wl.cr))
     path_bytes = 288 * N + 256 * distinct
     dev_ms_total = sum(v[0] for k, v in kernels.items() if k not in ("begin", "host_sync"))
     dom = max(((k, v) for k, v in kernels.items() if k in KERNEL_BYTES_PER_EVENT),
@@ -312,8 +411,7 @@ def main():
         avg_s = kms / kcount / 1e3
         kbytes = KERNEL_BYTES_PER_EVENT[kname] * N
         achieved = kbytes / avg_s / 1e9
-        default_workload = (N, A) == (10_000_000, 10_000)
-        traffic, traffic_src = measured_traffic(kname) if default_workload else (None, None)
+        traffic, traffic_src = measured_traffic(kname) if wl.default else (None, None)
         roofline = {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                     "traffic": traffic, "traffic_source": traffic_src,
@@ -328,7 +426,8 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args, acc, base, lens)
+        acc_s, base_s, label = wl.cpu_sample()
+        cpu = cpu_baseline(args, acc_s, base_s, batch_plan(len(base_s)), label)
 
     value = N * K * world / t_max
     if rank == 0:
@@ -338,10 +437,8 @@ def main():
             "ms_per_step": round(t_max / K * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u128",
             "data": "synthetic (seeded; benchmark_load.zig distributions, sequential ids)",
-            "config": {"workload": "config2: 10k accounts, 10M uniform create_transfers in "
-                                   "8189-event batches, 1 ledger shard per GPU",
-                       "transfers_per_step_per_gpu": N, "accounts_per_gpu": A,
-                       "batches_per_step": int(len(lens)), "parallelism": f"ledger-shard x{world}"},
+            "config": dict(wl.config, batches_per_step=int(len(lens)),
+                           parallelism=f"ledger-shard x{world}"),
             "validated": validated,
             "replayed_events_last_step": int(stats.replayed),
             "roofline": roofline,

@@ -64,17 +64,38 @@ def test_uniform_config2_small():
 
 
 def test_sort_path_large_key_space():
-    """More than 262,144 accounts: balance items take the radix sort + run reduction."""
-    p = Pair(account_capacity=1 << 19, transfer_capacity=1 << 18, batch_events_max=1 << 17)
+    """More than 262,144 accounts with at most 8 account fields per balance item: balance items
+    take the radix sort + run reduction -- short runs (uniform over 300k accounts) and runs that
+    span lanes and tiles (2,000 accounts)."""
+    p = Pair(account_capacity=1 << 19, transfer_capacity=1 << 19, batch_events_max=1 << 17)
     try:
         n_acc = 300_000
         acc = workload.accounts(n_acc, seed=5)
         for i in range(0, n_acc, 100_000):
             p.create_accounts(acc[i:i + 100_000], [8189] * 12 + [100_000 - 12 * 8189])
-        t = workload.transfers_uniform(70_000, n_acc, seed=5)
+        t = workload.transfers_uniform(130_000, n_acc, seed=5)
+        r = p.create_transfers(t, [8189] * 15 + [130_000 - 15 * 8189])
+        assert (r["status"] == 0xFFFFFFFF).all()
+        t = workload.transfers_uniform(130_000, 2_000, seed=6, id_offset=130_000)
+        p.create_transfers(t, [65_000, 65_000])
+        p.compare_state()
+    finally:
+        p.close()
+
+
+def test_atomic_path_sparse_keys():
+    """More than 8 account fields per balance item (config 5's shape): balance items are applied
+    with u128 atomics; then a call whose items collide on few accounts."""
+    p = Pair(account_capacity=1 << 19, transfer_capacity=1 << 18, batch_events_max=1 << 17)
+    try:
+        n_acc = 300_000
+        acc = workload.accounts(n_acc, seed=7)
+        for i in range(0, n_acc, 100_000):
+            p.create_accounts(acc[i:i + 100_000], [8189] * 12 + [100_000 - 12 * 8189])
+        t = workload.transfers_uniform(70_000, n_acc, seed=7)
         r = p.create_transfers(t, [8189] * 8 + [70_000 - 8 * 8189])
         assert (r["status"] == 0xFFFFFFFF).all()
-        t = workload.transfers_uniform(70_000, 1_000, seed=6, id_offset=70_000)
+        t = workload.transfers_uniform(70_000, 1_000, seed=8, id_offset=70_000)
         p.create_transfers(t, [35_000, 35_000])
         p.compare_state()
     finally:

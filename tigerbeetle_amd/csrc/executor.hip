@@ -30,6 +30,9 @@ uint64_t next_pow2(uint64_t x) {
 
 // Calls at least this large accumulate balances by sort + reduce instead of atomics.
 constexpr uint32_t kSortThreshold = 1u << 16;
+// Balance items use u128 atomics instead of the sort when the key space has more than this many
+// account fields per item.
+constexpr uint64_t kAtomicKeysPerItem = 8;
 
 struct PulseScratch {
     uint64_t capacity = 0;
@@ -721,6 +724,9 @@ int tbg_create_transfers_device(tbg_ctx* ctx, const tb_transfer_t* d_events, uin
     // Small key spaces (<= 262,144 accounts) take the bucketed path, whose LDS sums need
     // amounts < 2^48 (key_bits >= 16); larger ones the radix sort + run reduction.
     const bool use_buckets = use_sort && key_end <= kBucketsMax * kBucketKeys;
+    // Sparse key spaces (many more account fields than balance items, e.g. 125M accounts under
+    // 1M-event calls): u128 atomics per item instead of the sort; collisions are rare.
+    const bool use_atomic = use_sort && !use_buckets && uint64_t(key_end) > kAtomicKeysPerItem * 2 * uint64_t(n);
     if (use_buckets && key_bits < 16) key_bits = 16;
     BucketPlan plan{};
     if (use_sort) {
@@ -766,6 +772,11 @@ int tbg_create_transfers_device(tbg_ctx* ctx, const tb_transfer_t* d_events, uin
         hipLaunchKernelGGL(bal_bucket_apply, dim3(grid_for(key_end)), block, 0, ctx->stream,
                            target, plan, ctx->bucket_partials, key_end);
         tmark(ctx, "bal_apply");
+        rc = hip_ok(ctx, hipGetLastError(), "launch") ? 0 : TBG_EHIP;
+    } else if (!rc && use_atomic) {
+        hipLaunchKernelGGL(bal_atomic_apply, dim3(grid_for(uint64_t(items) / 2)), block, 0,
+                           ctx->stream, target, ctx->bal_items, uint64_t(items), key_bits, key_end);
+        tmark(ctx, "bal_atomic");
         rc = hip_ok(ctx, hipGetLastError(), "launch") ? 0 : TBG_EHIP;
     } else if (!rc && use_sort) {
         // Balance deltas: sort the packed items by field key, reduce runs in u128.

@@ -799,32 +799,40 @@ __global__ void bal_reduce_tiles(BalTarget rows, const uint64_t* items, uint64_t
     last_hi[threadIdx.x] = uint64_t(ls >> 64);
     single[threadIdx.x] = one;
     __syncthreads();
-    if (threadIdx.x != 0) return;
-    // Merge lane-edge runs in order. `open` is the run being accumulated; `shared` marks a run
-    // that touches the tile's first item (it may continue from the previous tile).
-    uint32_t open = first_key[0];
-    u128 acc = 0;
-    bool open_shared = true;
-    for (uint32_t t = 0; t < kBlock; t++) {
-        const uint32_t f = first_key[t];
-        const u128 fsum = ((u128)first_hi[t] << 64) | first_lo[t];
-        if (f != open) {
-            if (open < key_end) add_field(rows, open, acc, open_shared);
-            open = f;
-            acc = 0;
-            open_shared = false;
+    // Lane-edge runs: the lane where a run starts adds it, walking forward over the lanes that
+    // continue it. A run that touches the tile's first item (it may continue from the previous
+    // tile) or its last (it may continue into the next) is shared: u128 atomics.
+    const uint32_t t = threadIdx.x;
+    auto finish = [&](uint32_t key, u128 sum, bool shared) {
+        uint32_t q = t + 1;
+        for (; q < kBlock && first_key[q] == key; q++) {
+            sum += ((u128)first_hi[q] << 64) | first_lo[q];
+            if (!single[q]) break;  // the run ends inside lane q
         }
-        acc += fsum;
-        if (!single[t]) {
-            // The lane's first run ends inside the lane; its last run opens.
-            if (open < key_end) add_field(rows, open, acc, open_shared);
-            open = last_key[t];
-            acc = ((u128)last_hi[t] << 64) | last_lo[t];
-            open_shared = false;
-        }
+        if (q == kBlock) shared = true;
+        if (key < key_end) add_field(rows, key, sum, shared);
+    };
+    if (t == 0 || last_key[t - 1] != fk) {
+        if (one) finish(fk, fs, t == 0);
+        else if (fk < key_end) add_field(rows, fk, fs, t == 0);
     }
-    // The tile's last run may continue into the next tile.
-    if (open < key_end) add_field(rows, open, acc, true);
+    if (!one) finish(lk, ls, false);
+}
+
+// Sparse key spaces (far more account fields than items): the FAST events' packed balance items
+// applied with u128 atomics, two items per lane -- collisions are rare, no sort is needed.
+__global__ void bal_atomic_apply(BalTarget rows, const uint64_t* items, uint64_t n,
+                                 uint32_t key_bits, uint32_t key_end) {
+    const uint64_t i = 2 * (uint64_t(blockIdx.x) * blockDim.x + threadIdx.x);
+    if (i >= n) return;
+    const uint64_t kmask = (1ull << key_bits) - 1;
+    const uint4 q = *reinterpret_cast<const uint4*>(items + i);  // n is even (2 per event)
+    const uint64_t it[2] = {(uint64_t(q.y) << 32) | q.x, (uint64_t(q.w) << 32) | q.z};
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        const uint64_t key = it[j] & kmask;
+        if (key < key_end) add_field(rows, uint32_t(key), it[j] >> key_bits, true);
+    }
 }
 
 // ---- the bucketed balance path ------------------------------------------------

@@ -237,3 +237,69 @@ def fuzz_transfers(rng, n: int, id_space: int, n_accounts: int, pending_ids=None
     t["timestamp"] = (rng.random(n) < 0.01).astype(U64)
     t["id"][rng.random(n) < 0.005] = 0
     return t
+
+
+# ---- config 5: many accounts over 64 ledgers, sharded by ledger ----------
+
+LEDGERS_CONFIG5 = 64
+
+
+def config5_ledgers(rank: int, world: int):
+    """The rank's contiguous ledger range: (first ledger offset, ledgers per shard)."""
+    if LEDGERS_CONFIG5 % world:
+        raise ValueError(f"{LEDGERS_CONFIG5} ledgers do not split over {world} shards")
+    per = LEDGERS_CONFIG5 // world
+    return rank * per, per
+
+
+def config5_global_index(j: np.ndarray, rank: int, world: int) -> np.ndarray:
+    """Global account index k of the rank's local account j: account k lives on ledger
+    1 + (k mod 64); the rank holds the accounts of its ledgers, interleaved by ledger."""
+    first, per = config5_ledgers(rank, world)
+    j = np.asarray(j, dtype=np.int64)
+    return (j // per) * LEDGERS_CONFIG5 + first + (j % per)
+
+
+def accounts_config5(j: np.ndarray, rank: int, world: int) -> np.ndarray:
+    """The rank's local accounts `j` (id = global index + 1, ledger 1 + (k mod 64), code 1,
+    history; user data a fixed function of the id, so any subset is reproducible)."""
+    k = config5_global_index(j, rank, world)
+    n = len(k)
+    a = np.zeros(n, dtype=ACCOUNT_DTYPE)
+    ids = (k + 1).astype(U64)
+    _u128_col(a, "id", ids)
+    with np.errstate(over="ignore"):
+        a["user_data_128"][:, 0] = ids * U64(0x9E3779B97F4A7C15)
+        a["user_data_128"][:, 1] = ids * U64(0xC2B2AE3D27D4EB4F)
+        a["user_data_64"] = ids * U64(0x165667B19E3779F9)
+    a["user_data_32"] = (ids & U64(0xFFFFFFFF)).astype(np.uint32)
+    a["ledger"] = (1 + (k % LEDGERS_CONFIG5)).astype(np.uint32)
+    a["code"] = 1
+    a["flags"] = int(AccountFlags.history)
+    return a
+
+
+def transfers_config5(n: int, accounts_per_shard: int, rank: int, world: int, seed: int = 42,
+                      id_offset: int = 0):
+    """`n` transfers of the rank's shard: a ledger uniform over the shard's ledgers, then debit and
+    credit uniform within it (credit bumped on collision). Returns (transfers, dr_local,
+    cr_local), the local account indices for validation."""
+    first, per = config5_ledgers(rank, world)
+    groups = accounts_per_shard // per
+    if groups < 2:
+        raise ValueError("config 5 needs at least two accounts per ledger")
+    rng = np.random.default_rng(seed + 7919 * rank)
+    lo = rng.integers(0, per, size=n, dtype=np.int64)
+    gd = rng.integers(0, groups, size=n, dtype=np.int64)
+    gc = rng.integers(0, groups, size=n, dtype=np.int64)
+    gc = np.where(gc == gd, (gc + 1) % groups, gc)
+    dr_local, cr_local = gd * per + lo, gc * per + lo
+    t = np.zeros(n, dtype=TRANSFER_DTYPE)
+    _u128_col(t, "id", np.arange(id_offset + 1, id_offset + n + 1, dtype=U64))
+    _u128_col(t, "debit_account_id", (config5_global_index(dr_local, rank, world) + 1).astype(U64))
+    _u128_col(t, "credit_account_id", (config5_global_index(cr_local, rank, world) + 1).astype(U64))
+    t["user_data_64"] = rng.integers(0, 2**63, size=n, dtype=np.int64).astype(U64)
+    t["ledger"] = (1 + first + lo).astype(np.uint32)
+    t["code"] = _codes(rng, n)
+    _u128_col(t, "amount", _amounts(rng, n))
+    return t, dr_local, cr_local
