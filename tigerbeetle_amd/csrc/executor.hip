@@ -49,6 +49,8 @@ struct FlowScratch {
              *vals_sorted = nullptr, *pred = nullptr, *done = nullptr;
     uint64_t *keys = nullptr, *keys_sorted = nullptr, *pnt_ops = nullptr, *pnt_scan = nullptr;
     Step* steps = nullptr;
+    uint32_t* queue = nullptr;
+    uint8_t* ready8 = nullptr;
     uint32_t* dup_mark = nullptr;  // per event (batch_events_max)
     unsigned int* counts = nullptr;
     unsigned long long* pnt_fired = nullptr;
@@ -290,6 +292,10 @@ int end_call(tbg_ctx* ctx, uint32_t n, bool already_synced = false) {
         ctx->error = "table capacity exceeded";
         return TBG_ENOSPC;
     }
+    if (s.flags & kFlagFlowStalled) {
+        ctx->error = "flow replay stalled (watchdog)";
+        return TBG_EHIP;
+    }
     if (s.flags & kFlagUndoOverflow) {
         ctx->error = "linked chain longer than the undo log";
         return TBG_ENOSPC;
@@ -299,13 +305,16 @@ int end_call(tbg_ctx* ctx, uint32_t n, bool already_synced = false) {
 
 void free_flow(FlowScratch& F) {
     void* ptrs[] = {F.head8, F.barrier8, F.heads, F.unit_of, F.barriers, F.vals, F.vals_sorted,
-                    F.pred, F.done, F.keys, F.keys_sorted, F.pnt_ops, F.pnt_scan, F.steps};
+                    F.pred, F.done, F.keys, F.keys_sorted, F.pnt_ops, F.pnt_scan, F.steps,
+                    F.queue, F.ready8};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     F.head8 = F.barrier8 = nullptr;
     F.heads = F.unit_of = F.barriers = F.vals = F.vals_sorted = F.pred = F.done = nullptr;
     F.keys = F.keys_sorted = F.pnt_ops = F.pnt_scan = nullptr;
     F.steps = nullptr;
+    F.queue = nullptr;
+    F.ready8 = nullptr;
     F.cap = 0;
 }
 
@@ -328,7 +337,8 @@ int ensure_flow(tbg_ctx* ctx, uint64_t m) {
          dev_alloc(ctx, &F.pnt_ops, cap, false) && dev_alloc(ctx, &F.pnt_scan, cap, false) &&
          dev_alloc(ctx, &F.vals, kc, false) && dev_alloc(ctx, &F.vals_sorted, kc, false) &&
          dev_alloc(ctx, &F.pred, kc, false) && dev_alloc(ctx, &F.keys, kc, false) &&
-         dev_alloc(ctx, &F.keys_sorted, kc, false) && dev_alloc(ctx, &F.steps, cap, false);
+         dev_alloc(ctx, &F.keys_sorted, kc, false) && dev_alloc(ctx, &F.steps, cap, false) &&
+         dev_alloc(ctx, &F.queue, cap, false) && dev_alloc(ctx, &F.ready8, cap, false);
     if (!ok) {
         free_flow(F);
         return TBG_EHIP;
@@ -358,8 +368,10 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
     P.vals = F.vals;
     P.keys_sorted = F.keys_sorted;
     P.vals_sorted = F.vals_sorted;
-    P.pred = F.pred;
-    P.done = F.done;
+    P.succ = F.pred;
+    P.indeg = F.done;
+    P.queue = F.queue;
+    P.ready8 = F.ready8;
     const bool post_void = (call_flags & kFlagPostVoid) != 0;
     P.pnt_ops = post_void ? F.pnt_ops : nullptr;
     P.pnt_scan = F.pnt_scan;
@@ -382,9 +394,13 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
     HIP_TRY(ctx, hipcub::DeviceRadixSort::SortPairs(ctx->cub_temp, bytes, F.keys, F.keys_sorted,
                                                     F.vals, F.vals_sorted, pairs, 0, 64,
                                                     ctx->stream));
-    hipLaunchKernelGGL(flow_preds, dim3(grid_for(uint64_t(pairs))), block, 0, ctx->stream, P);
+    HIP_TRY(ctx, hipMemsetAsync(F.done, 0, uint64_t(m) * 4, ctx->stream));  // indeg
+    hipLaunchKernelGGL(flow_edges, dim3(grid_for(uint64_t(pairs))), block, 0, ctx->stream, P);
+    hipLaunchKernelGGL(flow_ready, dim3(grid_for(m)), block, 0, ctx->stream, P);
     rc = select_flagged(ctx, F.barrier8, m, F.barriers, &F.counts[1]);
+    if (!rc) rc = select_flagged(ctx, F.ready8, m, F.queue, &F.counts[2]);
     if (rc) return rc;
+    hipLaunchKernelGGL(flow_queue_init, dim3(grid_for(m)), block, 0, ctx->stream, P);
     if (post_void) {
         HIP_TRY(ctx, hipMemsetAsync(F.pnt_ops, 0, uint64_t(m) * 8, ctx->stream));
         HIP_TRY(ctx, hipMemsetAsync(F.pnt_fired, 0, 8, ctx->stream));
@@ -402,17 +418,20 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
     tmark(ctx, "tr_flow");
     if (debug) {
         unsigned int cnt[2] = {0, 0};
-        unsigned long long d[9] = {};
-        (void)hipMemcpyAsync(cnt, F.counts, 8, hipMemcpyDeviceToHost, ctx->stream);
-        (void)hipMemcpyAsync(d, ctx->flow_debug, 72, hipMemcpyDeviceToHost, ctx->stream);
+        unsigned long long d[12] = {};
+        unsigned int cnt3[3] = {};
+        (void)hipMemcpyAsync(cnt3, F.counts, 12, hipMemcpyDeviceToHost, ctx->stream);
+        (void)hipMemcpyAsync(d, ctx->flow_debug, 96, hipMemcpyDeviceToHost, ctx->stream);
+        cnt[0] = cnt3[0];
+        cnt[1] = cnt3[1];
+        fprintf(stderr, "flow: initially ready %u\n", cnt3[2]);
         (void)hipStreamSynchronize(ctx->stream);
         // wall_clock64 runs at 100 MHz on MI300-class parts
         fprintf(stderr, "flow: m=%u units=%u barriers=%u flags=%#x lanes=%u iterations=%llu "
                 "events=%llu exec_us=%.1f engine_us=%.1f\n", m, cnt[0], cnt[1], call_flags, lanes,
                 d[0], d[1], d[2] / 100.0, d[3] / 100.0);
-        const unsigned long long nb = d[4] + d[5] + d[6] + d[7];
-        fprintf(stderr, "flow: blocked on id %llu pid %llu dr %llu cr %llu, mean distance %.1f\n",
-                d[4], d[5], d[6], d[7], nb ? double(d[8]) / nb : 0.0);
+        fprintf(stderr, "flow: continuations %llu stall: head %llu tail %llu done %llu pos %llu\n",
+                d[4], d[8], d[9], d[10], d[11]);
     }
     if (post_void) {
         hipLaunchKernelGGL(flow_pnt_prep, dim3(grid_for(m)), block, 0, ctx->stream, P);

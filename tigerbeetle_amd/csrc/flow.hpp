@@ -42,6 +42,7 @@ constexpr uint32_t kFlowUndoPerLane = 3 * kFlowChainMax;  // 2 accounts + 1 stat
 constexpr uint32_t kFlowKeys = 4;           // keys per event
 constexpr uint64_t kFlowNoKey = ~0ull;
 constexpr uint32_t kFlowUnitBits = 31;
+constexpr uint64_t kFlowSpinLimit = 1ull << 21;  // idle polls while no unit finishes anywhere
 
 struct FlowPlan {
     uint32_t m;                  // replayed events (the replay list's length)
@@ -58,8 +59,10 @@ struct FlowPlan {
     uint32_t* vals;              // kFlowKeys * position + j
     uint64_t* keys_sorted;
     uint32_t* vals_sorted;
-    uint32_t* pred;              // kFlowKeys per position: predecessor unit or kNone32
-    uint32_t* done;              // per unit: epoch once finished
+    uint32_t* succ;              // kFlowKeys per position: successor unit or kNone32
+    uint32_t* indeg;             // per unit: predecessors not yet finished
+    uint32_t* queue;             // ready units (unit + 1; 0 = not yet pushed)
+    uint8_t* ready8;             // per unit: no predecessor
     uint64_t* pnt_ops;           // per position (post/void calls), else null
     uint64_t* pnt_scan;
     unsigned long long* pnt_fired;
@@ -183,145 +186,201 @@ __global__ void flow_keys(Tables T, Call<tb_transfer_t> c, FlowPlan P, unsigned 
     }
 }
 
-// Predecessor of each (key, unit) pair: the unit of the previous pair with the same key, unless
-// it is the same unit (a key repeated within a chain) -- then the first occurrence carries it.
-__global__ void flow_preds(FlowPlan P) {
+// The edges of the unit graph, from the (key, unit) pairs in key order: a pair whose previous
+// pair has the same key and another unit gets an edge from that unit (its predecessor on the key);
+// the last pair of a (key, unit) group records the next unit on the key (its successor). A key
+// repeated within a chain yields one edge. indeg counts each unit's edges.
+__global__ void flow_edges(FlowPlan P) {
     const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     const uint64_t n = kFlowKeys * uint64_t(P.m);
     if (i >= n) return;
     const uint64_t key = P.keys_sorted[i];
-    uint32_t pred = kNone32;
-    if (key != kFlowNoKey && i > 0) {
-        const uint64_t prev = P.keys_sorted[i - 1];
-        const uint32_t unit = uint32_t(key & ((1u << kFlowUnitBits) - 1));
-        const uint32_t prev_unit = uint32_t(prev & ((1u << kFlowUnitBits) - 1));
-        if ((prev >> kFlowUnitBits) == (key >> kFlowUnitBits) && prev_unit != unit) pred = prev_unit;
+    constexpr uint64_t kUnitMask = (1u << kFlowUnitBits) - 1;
+    uint32_t succ = kNone32;
+    if (key != kFlowNoKey) {
+        const uint32_t unit = uint32_t(key & kUnitMask);
+        if (i > 0) {
+            const uint64_t prev = P.keys_sorted[i - 1];
+            if ((prev >> kFlowUnitBits) == (key >> kFlowUnitBits) && uint32_t(prev & kUnitMask) != unit)
+                atomicAdd(&P.indeg[unit], 1u);
+        }
+        if (i + 1 < n) {
+            const uint64_t next = P.keys_sorted[i + 1];
+            if ((next >> kFlowUnitBits) == (key >> kFlowUnitBits) && uint32_t(next & kUnitMask) != unit)
+                succ = uint32_t(next & kUnitMask);
+        }
     }
-    P.pred[P.vals_sorted[i]] = pred;
+    P.succ[P.vals_sorted[i]] = succ;
 }
 
-__device__ inline uint32_t flow_load(const uint32_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+__global__ void flow_ready(FlowPlan P) {
+    const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= P.m) return;
+    P.ready8[u] = u < P.counts[0] && P.indeg[u] == 0;
 }
 
-// The engine: one workgroup of kFlowThreads lanes (see the header).
+// Initially ready units (selected in order into the queue, raw) -> queue entries unit + 1; the
+// rest of the queue empty.
+__global__ void flow_queue_init(FlowPlan P) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.counts[0]) return;
+    P.queue[i] = i < P.counts[2] ? P.queue[i] + 1 : 0;
+}
+
+// The engine: one workgroup of kFlowThreads lanes (see the header). A unit is ready once every
+// predecessor has finished (indeg 0). Ready units wait in a queue; a lane pops one, runs it, and
+// releases its successors -- the first that becomes ready it runs itself next (so a chain of units
+// on one hot key stays on one lane, its rows warm in that CU's L1), the others it pushes. Each
+// unit's last predecessor makes it ready exactly once, so every unit runs exactly once; the
+// earliest unfinished unit's predecessors have all finished, so it is ready or running: the
+// replay progresses, and lanes leave when the queue is drained and every unit has finished.
+// With a barrier unit in the call, lane 0 replays every unit in order (serial semantics).
 __global__ void __launch_bounds__(kFlowThreads) flow_replay(Tables T, Call<tb_transfer_t> c,
                                                            FlowPlan P) {
-    __shared__ unsigned int next_unit, done_count, gate_index;
+    __shared__ unsigned int q_head, q_tail, units_done;
     const uint32_t tid = threadIdx.x;
+    const uint32_t units = P.counts[0];
     if (tid == 0) {
-        next_unit = 0;
-        done_count = 0;
-        gate_index = 0;
+        q_head = 0;
+        q_tail = P.counts[2];
+        units_done = 0;
     }
     __syncthreads();
-    const uint32_t units = P.counts[0];
-    const uint32_t n_barriers = P.counts[1];
-    UndoEntry* const my_undo = P.lane_undo + uint64_t(tid) * kFlowUndoPerLane;
+    const uint64_t t_start = wall_clock64();
+    uint64_t it_count = 0, ev_count = 0, exec_cycles = 0, conts = 0;
+    bool chain_open = false, chain_broken = false;
+    uint32_t chain_start = 0;
+
+    if (P.counts[1] != 0) {  // barrier units: the serial replay, on one lane
+        if (tid == 0) {
+            Replay R(T);
+            for (uint32_t s = 0; s < P.m; s++) {
+                replay_chain_step<tb_transfer_t>(R, c, P.slow_list[s], true, chain_open,
+                                                 chain_start, chain_broken);
+                if (R.overflow) {
+                    atomicOr(&T.scalars->flags, kFlagUndoOverflow);
+                    break;
+                }
+            }
+            T.scalars->stats[2] = P.m;
+        }
+        return;
+    }
 
     Replay R(T);
     R.concurrent = true;
     R.pnt_ops = P.pnt_ops;
-    bool chain_open = false, chain_broken = false;
-    uint32_t chain_start = 0;
+    R.undo = P.lane_undo + uint64_t(tid) * kFlowUndoPerLane;
+    R.undo_cap = kFlowUndoPerLane;
 
-    const uint64_t t_start = wall_clock64();
-    uint64_t it_count = 0, ev_count = 0, exec_cycles = 0, blocked[kFlowKeys] = {}, blocked_dist = 0;
-    uint32_t u = atomicAdd(&next_unit, 1u);
-    uint32_t s = 0, end = 0, need = 0;
-    bool barrier = false;
-    Step st;
-    tb_transfer_t ev;
-    uint4 pr;
-    // The position's prefetch: its step record, event and predecessors.
-    auto load_position = [&]() {
-        st = P.steps[s];
-        ev = c.events[st.k];
-        pr = *reinterpret_cast<const uint4*>(P.pred + kFlowKeys * uint64_t(s));
-        need = (pr.x != kNone32 ? 1u : 0u) | (pr.y != kNone32 ? 2u : 0u) |
-               (pr.z != kNone32 ? 4u : 0u) | (pr.w != kNone32 ? 8u : 0u);
-    };
-    auto begin_unit = [&]() {
-        if (u >= units) return;
-        s = P.heads[u];
-        end = u + 1 < units ? P.heads[u + 1] : P.m;
-        barrier = P.barrier8[u] != 0;
-        R.undo = barrier ? T.undo : my_undo;
-        R.undo_cap = barrier ? T.undo_capacity : kFlowUndoPerLane;
+    // Runs unit u; releases its successors; returns the one this lane runs next (or kNone32).
+    auto run_unit = [&](uint32_t u) -> uint32_t {
+        const uint32_t begin = P.heads[u];
+        const uint32_t end = u + 1 < units ? P.heads[u + 1] : P.m;
         R.undo_len = 0;
         R.key_max = 0;
-        load_position();
-    };
-    begin_unit();
-    while (u < units) {
-        // The barrier gate: the earliest unfinished barrier unit, or none.
-        const uint32_t gi = __hip_atomic_load(&gate_index, __ATOMIC_ACQUIRE,
-                                              __HIP_MEMORY_SCOPE_WORKGROUP);
-        const uint32_t gate = gi < n_barriers ? P.barriers[gi] : 0xFFFFFFFFu;
-        bool ready;
-        if (u > gate) ready = false;
-        else if (u == gate)
-            ready = __hip_atomic_load(&done_count, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == u;
-        else ready = true;
-        if (ready && need) {
-            // The predecessors still outstanding, loaded together.
-            const uint32_t d0 = (need & 1) ? flow_load(&P.done[pr.x]) : P.epoch;
-            const uint32_t d1 = (need & 2) ? flow_load(&P.done[pr.y]) : P.epoch;
-            const uint32_t d2 = (need & 4) ? flow_load(&P.done[pr.z]) : P.epoch;
-            const uint32_t d3 = (need & 8) ? flow_load(&P.done[pr.w]) : P.epoch;
-            need &= (d0 != P.epoch ? 1u : 0u) | (d1 != P.epoch ? 2u : 0u) |
-                    (d2 != P.epoch ? 4u : 0u) | (d3 != P.epoch ? 8u : 0u);
-            if (need) {
-                ready = false;
-                if (P.debug) {
-                    const uint32_t q = __builtin_ctz(need);
-                    blocked[q]++;
-                    blocked_dist += u - (q == 0 ? pr.x : q == 1 ? pr.y : q == 2 ? pr.z : pr.w);
+        const uint64_t t0 = P.debug ? wall_clock64() : 0;
+        for (uint32_t s = begin; s < end; s++) {
+            const Step st = P.steps[s];
+            const tb_transfer_t ev = c.events[st.k];
+            StepInfo si;
+            si.ts_event = st.ts_event;
+            si.batch = st.batch;
+            si.flags = st.flags;
+            R.pos = s;
+            replay_chain_step_at<tb_transfer_t>(R, c, st.k, ev, si, EvRefs{st.slot, st.dr, st.cr},
+                                                true, chain_open, chain_start, chain_broken);
+            if (R.overflow) {
+                atomicOr(&T.scalars->flags, kFlagUndoOverflow);
+                R.overflow = false;
+            }
+        }
+        if (P.debug) {
+            exec_cycles += wall_clock64() - t0;
+            ev_count += end - begin;
+        }
+        if (R.key_max) atomicMax(&T.scalars->transfers_key_max, (unsigned long long)R.key_max);
+        // Release the successors (acq_rel: a successor's runner sees every predecessor's writes).
+        uint32_t next = kNone32;
+        for (uint32_t s = begin; s < end; s++) {
+            const uint4 sc = *reinterpret_cast<const uint4*>(P.succ + kFlowKeys * uint64_t(s));
+            const uint32_t vs[kFlowKeys] = {sc.x, sc.y, sc.z, sc.w};
+#pragma unroll
+            for (uint32_t q = 0; q < kFlowKeys; q++) {
+                const uint32_t v = vs[q];
+                if (v == kNone32) continue;
+                const uint32_t old = __hip_atomic_fetch_add(&P.indeg[v], 0xFFFFFFFFu,
+                                                            __ATOMIC_ACQ_REL,
+                                                            __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (old != 1) continue;
+                if (next == kNone32) {
+                    next = v;
+                } else {
+                    const uint32_t slot = atomicAdd(&q_tail, 1u);
+                    __hip_atomic_store(&P.queue[slot], v + 1, __ATOMIC_RELEASE,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
             }
         }
-        it_count++;
-        if (!ready) {
-            __builtin_amdgcn_s_sleep(1);
-            continue;
+        __hip_atomic_fetch_add(&units_done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        conts += next != kNone32;
+        return next;
+    };
+    uint32_t u = kNone32;
+    uint64_t spins = 0;
+    uint32_t last_seen = 0;
+    uint32_t pos = atomicAdd(&q_head, 1u);
+    // The loop's exit is wave-uniform (a vote): inside it every lane only takes if/else paths, so
+    // a waiting lane and a running lane of the same wave share every iteration. (With per-lane
+    // exits the compiler may form an inner loop of the waiting lanes that the running lanes of the
+    // wave only re-enter once every waiter has left it -- a waiter that needs a unit of its own
+    // wave would never leave.)
+    bool alive = true;
+    while (__any(alive)) {
+        if (alive && u == kNone32) {
+            // Pop: the queue entry at `pos`, or leave once every unit has finished.
+            if (pos >= units) {
+                alive = false;
+            } else {
+                const uint32_t w = __hip_atomic_load(&P.queue[pos], __ATOMIC_ACQUIRE,
+                                                     __HIP_MEMORY_SCOPE_WORKGROUP);
+                it_count++;
+                if (w != 0) {
+                    u = w - 1;
+                    pos = atomicAdd(&q_head, 1u);
+                    spins = 0;
+                } else {
+                    const uint32_t seen = __hip_atomic_load(&units_done, __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (seen != last_seen) {
+                        last_seen = seen;
+                        spins = 0;
+                    }
+                    if (seen == units) {
+                        alive = false;
+                    } else if (++spins > kFlowSpinLimit) {
+                        // Watchdog: a replay that stops progressing is a bug; leave with a flag
+                        // (the call fails) instead of holding the GPU.
+                        atomicOr(&T.scalars->flags, kFlagFlowStalled);
+                        if (P.debug) {
+                            P.debug[8] = q_head;
+                            P.debug[9] = q_tail;
+                            P.debug[10] = seen;
+                            P.debug[11] = pos;
+                        }
+                        alive = false;
+                    }
+                }
+            }
         }
-        R.pos = s;
-        const uint64_t t0 = P.debug ? wall_clock64() : 0;
-        StepInfo si;
-        si.ts_event = st.ts_event;
-        si.batch = st.batch;
-        si.flags = st.flags;
-        replay_chain_step_at<tb_transfer_t>(R, c, st.k, ev, si, EvRefs{st.slot, st.dr, st.cr},
-                                            true, chain_open, chain_start, chain_broken);
-        if (P.debug) {
-            exec_cycles += wall_clock64() - t0;
-            ev_count++;
-        }
-        if (R.overflow) {
-            atomicOr(&T.scalars->flags, kFlagUndoOverflow);
-            R.overflow = false;
-        }
-        s++;
-        if (s < end) {
-            load_position();
-            continue;
-        }
-        // The unit is finished: publish its effects, then its completion.
-        if (R.key_max) atomicMax(&T.scalars->transfers_key_max, (unsigned long long)R.key_max);
-        __hip_atomic_store(&P.done[u], P.epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        __hip_atomic_fetch_add(&done_count, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (barrier)
-            __hip_atomic_fetch_add(&gate_index, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        u = atomicAdd(&next_unit, 1u);
-        begin_unit();
+        if (alive && u != kNone32) u = run_unit(u);
+        else if (alive) __builtin_amdgcn_s_sleep(1);
     }
     if (P.debug) {
         atomicAdd(&P.debug[0], (unsigned long long)it_count);
         atomicAdd(&P.debug[1], (unsigned long long)ev_count);
         atomicAdd(&P.debug[2], (unsigned long long)exec_cycles);
-        for (uint32_t q = 0; q < kFlowKeys; q++)
-            atomicAdd(&P.debug[4 + q], (unsigned long long)blocked[q]);
-        atomicAdd(&P.debug[8], (unsigned long long)blocked_dist);
+        atomicAdd(&P.debug[4], (unsigned long long)conts);
     }
     __syncthreads();
     if (tid == 0) {

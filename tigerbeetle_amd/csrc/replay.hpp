@@ -45,6 +45,7 @@ enum : unsigned int {
     kFlagHot = 1u << 5,        // some account is marked hot (a SLOW event touches it)
     kFlagClosable = 1u << 6,   // some account is marked closable
     kFlagNeedCommit = 1u << 7, // some event is not a plain FAST event (tr_commit must run)
+    kFlagFlowStalled = 1u << 8, // the flow replay's watchdog fired (a bug: the call fails)
 };
 // Call flags under which tr_commit re-validates (and may demote) ingest's FAST events.
 constexpr unsigned int kCommitFlags = kFlagImported | kFlagPostVoid | kFlagDuplicate | kFlagHot |
