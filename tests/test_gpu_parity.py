@@ -300,3 +300,36 @@ def test_flow_replay_stress(seed):
         p.compare_state()
     finally:
         p.close()
+
+
+@pytest.mark.parametrize("n_acc", [200, 700], ids=["lanes", "over-lanes"])
+def test_account_lanes_limits(n_acc):
+    """Calls whose replayed events are all limit events run on the account lanes (one lane per
+    limited account): debits_must_not_exceed_credits and credits_must_not_exceed_debits on both
+    sides, transfers between two limited accounts (both verdicts needed), between a limited and an
+    unlimited account, and funding; 700 limited accounts exceed the lanes (the flow replay runs)."""
+    rng = np.random.default_rng(n_acc)
+    p = Pair(account_capacity=1 << 12, transfer_capacity=1 << 17, batch_events_max=1 << 15)
+    try:
+        acc = workload.accounts(n_acc, seed=11, ledger=2)
+        acc["flags"] = rng.choice([0, 2, 4], size=n_acc, p=[0.2, 0.4, 0.4]).astype(np.uint16)
+        acc["flags"][0] = 0  # an unlimited source
+        p.create_accounts(acc, _split(n_acc, rng, 512))
+        fund = workload.funding_transfers(n_acc - 1, 50_000, id_offset=1 << 30)
+        fund["credit_account_id"][:, 0] = np.arange(2, n_acc + 1, dtype=np.uint64)
+        p.create_transfers(fund, _split(len(fund), rng, 512))
+        back = fund.copy()  # and the other way, so credits_must_not_exceed_debits has room
+        back["id"][:, 0] += np.uint64(1 << 20)
+        back["debit_account_id"], back["credit_account_id"] = fund["credit_account_id"], fund["debit_account_id"]
+        p.create_transfers(back, _split(len(back), rng, 512))
+        off = 0
+        for step in range(4):
+            t = workload.transfers_uniform(12_000, n_acc, seed=100 + step, id_offset=off)
+            off += 12_000
+            t["amount"][:, 0] = rng.integers(1, 30_000, size=len(t)).astype(np.uint64)
+            r = p.create_transfers(t, _split(len(t), rng, 8189))
+            if step == 0:
+                assert ((r["status"] == 54) | (r["status"] == 55)).any()
+        p.compare_state()
+    finally:
+        p.close()

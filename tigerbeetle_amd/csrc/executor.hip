@@ -14,7 +14,7 @@
 #include <vector>
 
 #include "../../include/tbg.h"
-#include "flow.hpp"
+#include "lanes.hpp"
 
 using namespace tbg;
 
@@ -51,6 +51,11 @@ struct FlowScratch {
     Step* steps = nullptr;
     uint32_t* queue = nullptr;
     uint8_t* ready8 = nullptr;
+    // account lanes (lanes.hpp)
+    LaneRec* recs = nullptr;
+    uint32_t *mailbox = nullptr, *owner_starts = nullptr, *mb_index = nullptr;
+    uint8_t* owner_head8 = nullptr;
+    unsigned int* lane_counts = nullptr;
     uint32_t* dup_mark = nullptr;  // per event (batch_events_max)
     unsigned int* counts = nullptr;
     unsigned long long* pnt_fired = nullptr;
@@ -306,7 +311,7 @@ int end_call(tbg_ctx* ctx, uint32_t n, bool already_synced = false) {
 void free_flow(FlowScratch& F) {
     void* ptrs[] = {F.head8, F.barrier8, F.heads, F.unit_of, F.barriers, F.vals, F.vals_sorted,
                     F.pred, F.done, F.keys, F.keys_sorted, F.pnt_ops, F.pnt_scan, F.steps,
-                    F.queue, F.ready8};
+                    F.queue, F.ready8, F.recs, F.mailbox, F.owner_starts, F.owner_head8, F.mb_index};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     F.head8 = F.barrier8 = nullptr;
@@ -315,6 +320,9 @@ void free_flow(FlowScratch& F) {
     F.steps = nullptr;
     F.queue = nullptr;
     F.ready8 = nullptr;
+    F.recs = nullptr;
+    F.mailbox = F.owner_starts = F.mb_index = nullptr;
+    F.owner_head8 = nullptr;
     F.cap = 0;
 }
 
@@ -324,6 +332,7 @@ int ensure_flow(tbg_ctx* ctx, uint64_t m) {
     if (!F.dup_mark) {
         ok = dev_alloc(ctx, &F.dup_mark, ctx->opt.batch_events_max, true) &&
              dev_alloc(ctx, &F.counts, 4, true) && dev_alloc(ctx, &F.pnt_fired, 1, true) &&
+             dev_alloc(ctx, &F.lane_counts, 4, true) &&
              dev_alloc(ctx, &F.lane_undo, uint64_t(kFlowThreads) * kFlowUndoPerLane, false);
         if (!ok) return TBG_EHIP;
     }
@@ -338,7 +347,10 @@ int ensure_flow(tbg_ctx* ctx, uint64_t m) {
          dev_alloc(ctx, &F.vals, kc, false) && dev_alloc(ctx, &F.vals_sorted, kc, false) &&
          dev_alloc(ctx, &F.pred, kc, false) && dev_alloc(ctx, &F.keys, kc, false) &&
          dev_alloc(ctx, &F.keys_sorted, kc, false) && dev_alloc(ctx, &F.steps, cap, false) &&
-         dev_alloc(ctx, &F.queue, cap, false) && dev_alloc(ctx, &F.ready8, cap, false);
+         dev_alloc(ctx, &F.queue, cap, false) && dev_alloc(ctx, &F.ready8, cap + kFlowThreads, false) &&
+         dev_alloc(ctx, &F.recs, cap, false) && dev_alloc(ctx, &F.mailbox, cap, false) &&
+         dev_alloc(ctx, &F.mb_index, cap, false) &&
+         dev_alloc(ctx, &F.owner_starts, kc, false) && dev_alloc(ctx, &F.owner_head8, kc, false);
     if (!ok) {
         free_flow(F);
         return TBG_EHIP;
@@ -404,6 +416,43 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
     if (post_void) {
         HIP_TRY(ctx, hipMemsetAsync(F.pnt_ops, 0, uint64_t(m) * 8, ctx->stream));
         HIP_TRY(ctx, hipMemsetAsync(F.pnt_fired, 0, 8, ctx->stream));
+    }
+    // Calls of limit events only: the account lanes (lanes.hpp); the flow replay then skips.
+    P.skip = nullptr;
+    if (!(call_flags & (kFlagDuplicate | kFlagPostVoid | kFlagClosable | kFlagImported)) &&
+        !c.force_replay && !getenv("TBG_NO_LANES")) {
+        LanePlan L{};
+        L.m = m;
+        L.keys_sorted = F.keys_sorted;
+        L.n_pairs = uint64_t(pairs);
+        L.steps = F.steps;
+        L.slow_list = c.slow_list;
+        L.recs = F.recs;
+        L.mailbox = F.mailbox;
+        L.mb_index = F.mb_index;
+        L.outcome = F.ready8;  // (free once the flow plan's queue is built)
+        L.owner_head8 = F.owner_head8;
+        L.owner_starts = F.owner_starts;
+        L.counts = F.lane_counts;
+        HIP_TRY(ctx, hipMemsetAsync(F.lane_counts, 0, 16, ctx->stream));
+        hipLaunchKernelGGL(lanes_check, dim3(grid_for(m)), block, 0, ctx->stream, ctx->T, c, P, L);
+        size_t sb = 0;
+        HIP_TRY(ctx, hipcub::DeviceScan::ExclusiveSum(nullptr, sb, F.mailbox, F.mb_index, int(m),
+                                                      ctx->stream));
+        rc = ensure_cub_temp(ctx, sb);
+        if (rc) return rc;
+        HIP_TRY(ctx, hipcub::DeviceScan::ExclusiveSum(ctx->cub_temp, sb, F.mailbox, F.mb_index,
+                                                      int(m), ctx->stream));
+        hipLaunchKernelGGL(lanes_mailboxes, dim3(grid_for(m)), block, 0, ctx->stream, L);
+        hipLaunchKernelGGL(lanes_segments, dim3(grid_for(uint64_t(pairs))), block, 0, ctx->stream,
+                           ctx->T, L);
+        rc = select_flagged(ctx, F.owner_head8, uint64_t(pairs), F.owner_starts, &F.lane_counts[0]);
+        if (rc) return rc;
+        tmark(ctx, "flow_plan");
+        hipLaunchKernelGGL(lanes_replay, dim3(1), dim3(kLanesMax), 0, ctx->stream, ctx->T, c, L);
+        hipLaunchKernelGGL(lanes_finish, dim3(grid_for(m)), block, 0, ctx->stream, ctx->T, c, L);
+        tmark(ctx, "tr_lanes");
+        P.skip = &F.lane_counts[2];
     }
     tmark(ctx, "flow_plan");
     const bool debug = getenv("TBG_FLOW_DEBUG") != nullptr;
@@ -700,7 +749,7 @@ void tbg_close(tbg_ctx* ctx) {
                     ctx->cub_temp, ctx->acc_ts_index, ctx->tr_ts_index, ctx->sel_buf,
                     ctx->pulse.keep, ctx->pulse.exp, ctx->pulse.ts, ctx->pulse.rows,
                     ctx->pulse.exp_b, ctx->pulse.rows_b, ctx->pulse.counters,
-                    ctx->flow.dup_mark, ctx->flow.counts, ctx->flow.pnt_fired,
+                    ctx->flow.dup_mark, ctx->flow.counts, ctx->flow.pnt_fired, ctx->flow.lane_counts,
                     ctx->flow.lane_undo};
     free_flow(ctx->flow);
     for (void* p : ptrs)

@@ -68,6 +68,7 @@ struct FlowPlan {
     unsigned long long* pnt_fired;
     UndoEntry* lane_undo;        // kFlowUndoPerLane per lane
     struct Step* steps;          // per position: what the engine prefetches before it waits
+    const unsigned int* skip;    // nonzero: the account lanes replayed the call (lanes.hpp)
     unsigned long long* debug;   // optional: [0] loop iterations, [1] events, [2] cycles executing,
                                  // [3] cycles of the engine (lane 0)
 };
@@ -238,6 +239,7 @@ __global__ void flow_queue_init(FlowPlan P) {
 __global__ void __launch_bounds__(kFlowThreads) flow_replay(Tables T, Call<tb_transfer_t> c,
                                                            FlowPlan P) {
     __shared__ unsigned int q_head, q_tail, units_done;
+    if (P.skip && *P.skip) return;
     const uint32_t tid = threadIdx.x;
     const uint32_t units = P.counts[0];
     if (tid == 0) {
@@ -342,8 +344,9 @@ __global__ void __launch_bounds__(kFlowThreads) flow_replay(Tables T, Call<tb_tr
             if (pos >= units) {
                 alive = false;
             } else {
-                const uint32_t w = __hip_atomic_load(&P.queue[pos], __ATOMIC_ACQUIRE,
-                                                     __HIP_MEMORY_SCOPE_WORKGROUP);
+                // (An atomic read: it is served by L2, never by a line this CU's L1 kept.)
+                const uint32_t w = __hip_atomic_fetch_or(&P.queue[pos], 0u, __ATOMIC_ACQUIRE,
+                                                         __HIP_MEMORY_SCOPE_WORKGROUP);
                 it_count++;
                 if (w != 0) {
                     u = w - 1;

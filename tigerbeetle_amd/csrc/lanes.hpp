@@ -1,0 +1,307 @@
+// Account lanes: the ordered replay of calls whose only order dependence is balance limits
+// (BASELINE.json config 3: hot accounts with debits_must_not_exceed_credits), one lane per limited
+// account, its balances in registers.
+//
+// A replayed event is a *limit event* when its outcome can only be created / exceeds_credits /
+// exceeds_debits: a single (unlinked) transfer, not post/void, pending, balancing, closing or
+// imported, timeout 0, the holder of a fresh id, both accounts found and open, amount < 2^64 and
+// every balance of both accounts < 2^126 (no overflow for any interleaving of the call) -- and the
+// call has no duplicate ids, post/void, closable accounts or imported events. Such an event passed
+// every check of create_transfer (state_machine.zig:3719-3905) up to the limits; what remains is
+//   exceeds_credits  dr has debits_must_not_exceed_credits and dpe + dpo + amount > cpo
+//   exceeds_debits   cr has credits_must_not_exceed_debits and cpe + cpo + amount > dpo
+// (:3907-3913, in that order), else created with dpo(dr) += amount, cpo(cr) += amount.
+//
+// The accounts with a limit flag ("owners") each get a lane that walks the account's events in
+// call order (the flow plan's (key, unit) sort already lists them) with the account's balances in
+// registers. An owner *decides* an event when its own limit is the one checked (debit side with
+// debits_must_not_exceed_credits, credit side with credits_must_not_exceed_debits); it publishes
+// its verdict in the event's mailbox. An event's outcome is known once every deciding owner has
+// published; every owner of the event then applies it, and the writer (the debit owner, else the
+// credit owner) writes the result and adds the amount to a non-owner side with an atomic (such an
+// account's balance is never read in the call; lanes_finish). The earliest undecided event's owners have decided
+// all their earlier events, so they can all publish: the lanes always progress.
+//
+// When a call is not all limit events, or has more owners than lanes, the flow replay runs.
+#pragma once
+
+#include <utility>
+
+#include "flow.hpp"
+
+namespace tbg {
+
+constexpr uint32_t kLanesMax = kFlowThreads;
+
+// What an owner lane reads per step (16 bytes; the rest of the event is the post pass's).
+struct LaneRec {
+    uint64_t amount;
+    uint32_t dr, bits;
+};
+enum : uint32_t {
+    kLaneDrOwner = 1, kLaneCrOwner = 2,  // the account has a limit flag
+    kLaneDrDecides = 4,                  // dr has debits_must_not_exceed_credits
+    kLaneCrDecides = 8,                  // cr has credits_must_not_exceed_debits
+};
+// mailbox bits per event
+enum : uint32_t { kMbDrSet = 1, kMbDrOk = 2, kMbCrSet = 4, kMbCrOk = 8 };
+enum : uint8_t { kOutCreated = 0, kOutExceedsCredits = 1, kOutExceedsDebits = 2 };
+// LaneRec.bits above kLaneMbShift: the event's LDS mailbox index (events with two owners)
+constexpr uint32_t kLaneMbShift = 8;
+constexpr uint32_t kLaneMbWords = 16384;              // 64 KB of LDS, 8 events per word
+constexpr uint32_t kLaneMbMax = kLaneMbWords * 8;
+
+struct LanePlan {
+    uint32_t m;
+    const uint64_t* keys_sorted;  // the flow plan's (key, unit) pairs
+    uint64_t n_pairs;
+    const Step* steps;
+    const uint32_t* slow_list;
+    LaneRec* recs;            // per position
+    uint32_t* mailbox;        // per position: 1 when both sides are owned (then its LDS index)
+    uint32_t* mb_index;       // exclusive prefix sum of `mailbox`
+    uint8_t* outcome;         // per position: the writer lane's verdict (kOut*)
+    uint8_t* owner_head8;     // per sorted pair: first pair of an owner's segment
+    uint32_t* owner_starts;   // selected
+    unsigned int* counts;     // [0] owners, [1] ineligible events, [2] handled (set by the engine)
+};
+
+__device__ inline bool lanes_owner(uint16_t flags) {
+    return (flags & (TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS |
+                     TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS)) != 0;
+}
+
+__device__ inline bool lanes_low(const tb_account_t& a) {
+    constexpr uint64_t kLim = 1ull << 62;
+    return a.debits_pending.hi < kLim && a.debits_posted.hi < kLim && a.credits_pending.hi < kLim &&
+           a.credits_posted.hi < kLim;
+}
+
+// Per replayed event: is it a limit event (else count it), and its record.
+__global__ void lanes_check(Tables T, Call<tb_transfer_t> c, FlowPlan F, LanePlan L) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= L.m) return;
+    const Step st = L.steps[s];
+    const uint32_t k = st.k;
+    const tb_transfer_t& t = c.events[k];
+    bool ok = st.dr != kNone32 && st.cr != kNone32 && st.slot != kNone32 && st.dr != st.cr;
+    // a unit of its own (no chain)
+    const uint32_t u = F.unit_of[s];
+    ok = ok && F.heads[u] == s && (u + 1 == F.counts[0] ? s + 1 == L.m : F.heads[u + 1] == s + 1);
+    ok = ok && (t.flags & ~uint16_t(0)) == 0 && t.timeout == 0 && u128_is_zero(t.pending_id) &&
+         t.amount.hi == 0 && t.timestamp == 0 && !(st.flags & StepInfo::kBatchImported);
+    uint32_t bits = 0;
+    if (ok) {
+        const uint64_t w = T.tr.slots[st.slot];
+        ok = w != kEmpty && w != kTomb && (w & kRefMask) == c.row_base + k + 1;
+        const tb_account_t& dr = T.acc_rows[st.dr];
+        const tb_account_t& cr = T.acc_rows[st.cr];
+        ok = ok && !((dr.flags | cr.flags) & TB_ACCOUNT_CLOSED) && lanes_low(dr) && lanes_low(cr) &&
+             dr.ledger == cr.ledger && t.ledger == dr.ledger && t.code != 0 && t.ledger != 0 &&
+             !u128_is_zero(t.id) && !u128_is_max(t.id);
+        if (lanes_owner(dr.flags)) bits |= kLaneDrOwner;
+        if (lanes_owner(cr.flags)) bits |= kLaneCrOwner;
+        if (dr.flags & TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS) bits |= kLaneDrDecides;
+        if (cr.flags & TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS) bits |= kLaneCrDecides;
+        ok = ok && (bits & (kLaneDrOwner | kLaneCrOwner)) != 0;
+    }
+    L.mailbox[s] = ok && (bits & (kLaneDrOwner | kLaneCrOwner)) == (kLaneDrOwner | kLaneCrOwner);
+    if (!ok) {
+        atomicAdd(&L.counts[1], 1u);
+        return;
+    }
+    LaneRec r;
+    r.amount = t.amount.lo;
+    r.dr = st.dr;
+    r.bits = bits;
+    L.recs[s] = r;
+}
+
+// The LDS mailbox index of each event with two owners (too many: the flow replay runs).
+__global__ void lanes_mailboxes(LanePlan L) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= L.m || !L.mailbox[s]) return;
+    const uint32_t i = L.mb_index[s];
+    if (i >= kLaneMbMax) atomicAdd(&L.counts[1], 1u);
+    else L.recs[s].bits |= i << kLaneMbShift;
+}
+
+// The first pair of each owner account's segment in the sorted (key, unit) pairs.
+__global__ void lanes_segments(Tables T, LanePlan L) {
+    const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= L.n_pairs) return;
+    const uint64_t key = L.keys_sorted[i];
+    bool head = false;
+    if (key != kFlowNoKey && (key >> 63) == 1 &&
+        (i == 0 || (L.keys_sorted[i - 1] >> kFlowUnitBits) != (key >> kFlowUnitBits))) {
+        const uint32_t row = uint32_t((key >> kFlowUnitBits) & 0xFFFFFFFFu);
+        head = lanes_owner(T.acc_rows[row].flags);
+    }
+    L.owner_head8[i] = head;
+}
+
+__global__ void __launch_bounds__(kLanesMax) lanes_replay(Tables T, Call<tb_transfer_t> c,
+                                                          LanePlan L) {
+    __shared__ uint32_t mbox[kLaneMbWords];
+    const uint32_t owners = L.counts[0];
+    if (L.counts[1] != 0 || owners == 0 || owners > kLanesMax) return;  // the flow replay runs
+    const uint32_t o = threadIdx.x;
+    if (o == 0) L.counts[2] = 1;
+    for (uint32_t i = o; i < kLaneMbWords; i += blockDim.x) mbox[i] = 0;
+    __syncthreads();
+    bool alive = o < owners;
+    uint64_t idx = alive ? L.owner_starts[o] : 0;
+    const uint64_t my_key = alive ? (L.keys_sorted[idx] >> kFlowUnitBits) : 0;
+    const uint32_t row = uint32_t(my_key & 0xFFFFFFFFu);
+    u128 dpe = 0, dpo = 0, cpe = 0, cpo = 0;
+    uint16_t flags = 0;
+    if (alive) {
+        const tb_account_t& a = T.acc_rows[row];
+        dpe = U(a.debits_pending);
+        dpo = U(a.debits_posted);
+        cpe = U(a.credits_pending);
+        cpo = U(a.credits_posted);
+        flags = a.flags;
+    }
+    bool published = false;
+    // The account's records in call order: record loads kAhead steps ahead, and the pair loads
+    // that name them kAhead further (a step is register arithmetic; neither load chain may be its
+    // latency).
+    constexpr uint32_t kAhead = 8;
+    LaneRec ring[kAhead];
+    bool ring_ok[kAhead];
+    uint32_t ring_s[kAhead];
+    uint64_t pre_key[kAhead];  // the (key, unit) pairs of the following kAhead steps, raw
+    uint64_t fetch_idx = idx;
+    // Every load and store of the steady-state step is unconditional (a clamped index, a dummy
+    // slot) and no loaded value is used before kAhead steps later: the wait counters then keep
+    // the rings in flight instead of draining them every step.
+    auto fetch_pair = [&](uint32_t slot) {
+        const uint64_t at = fetch_idx < L.n_pairs ? fetch_idx : L.n_pairs - 1;
+        pre_key[slot] = fetch_idx < L.n_pairs ? L.keys_sorted[at] : kFlowNoKey;
+        fetch_idx++;
+    };
+    auto take_pair = [&](uint32_t slot) {  // pre_key[slot] -> ring[slot]'s record load
+        const uint64_t key = pre_key[slot];
+        const uint32_t ps = uint32_t(key & ((1u << kFlowUnitBits) - 1));
+        return std::pair<bool, uint32_t>((key >> kFlowUnitBits) == my_key, ps < L.m ? ps : 0u);
+    };
+#pragma unroll
+    for (uint32_t q = 0; q < kAhead; q++) fetch_pair(q);
+#pragma unroll
+    for (uint32_t q = 0; q < kAhead; q++) {
+        const auto t = take_pair(q);
+        ring_ok[q] = t.first;
+        ring_s[q] = t.second;
+        ring[q] = L.recs[ring_s[q]];
+        fetch_pair(q);
+    }
+    alive = alive && ring_ok[0];
+    uint64_t spins = 0;
+    while (__any(alive)) {
+        if (alive && ++spins > kFlowSpinLimit) {  // watchdog (a bug): fail the call
+            atomicOr(&T.scalars->flags, kFlagFlowStalled);
+            alive = false;
+        }
+        if (alive) {
+            const LaneRec rec = ring[0];
+            const uint32_t s = ring_s[0];
+            const bool debit = rec.dr == row;
+            const bool decides_dr = (rec.bits & kLaneDrDecides) != 0;
+            const bool decides_cr = (rec.bits & kLaneCrDecides) != 0;
+            const bool mine = debit ? decides_dr : decides_cr;     // this lane's limit is checked
+            const bool other = debit ? decides_cr : decides_dr;    // the other owner's is
+            const bool other_owner = (rec.bits & (debit ? kLaneCrOwner : kLaneDrOwner)) != 0;
+            const u128 amount = rec.amount;
+            bool my_ok = true;
+            if (mine) my_ok = debit ? !(dpe + dpo + amount > cpo) : !(cpe + cpo + amount > dpo);
+            // Verdicts between two owners go through LDS (4 bits per event whose two sides are
+            // owned): a memory round trip here would drain the record rings every step.
+            const uint32_t mbi = rec.bits >> kLaneMbShift;
+            const uint32_t mb_shift = (mbi & 7) * 4;
+            if (mine && other_owner && !published) {
+                // The other owner applies this event too: it needs the verdict.
+                atomicOr(&mbox[mbi >> 3], (debit ? (kMbDrSet | (my_ok ? kMbDrOk : 0u))
+                                                 : (kMbCrSet | (my_ok ? kMbCrOk : 0u)))
+                                              << mb_shift);
+            }
+            published = true;
+            const uint32_t mb = other ? (__hip_atomic_load(&mbox[mbi >> 3], __ATOMIC_ACQUIRE,
+                                                           __HIP_MEMORY_SCOPE_WORKGROUP) >>
+                                         mb_shift) & 15u
+                                      : 0u;
+            const bool known = !other || (mb & (debit ? kMbCrSet : kMbDrSet));
+            if (known) {
+                const bool other_ok = !other || (mb & (debit ? kMbCrOk : kMbDrOk));
+                const bool dr_fail = debit ? !my_ok : !other_ok;
+                const bool cr_fail = debit ? !other_ok : !my_ok;
+                const bool created = !dr_fail && !cr_fail;
+                if (created) {
+                    if (debit) dpo += amount;
+                    else cpo += amount;
+                }
+                const bool writer = debit || !(rec.bits & kLaneDrOwner);
+                // (non-writers store to their own dummy byte past the positions)
+                L.outcome[writer ? s : L.m + o] =
+                    created ? kOutCreated : (dr_fail ? kOutExceedsCredits : kOutExceedsDebits);
+                published = false;
+                spins = 0;
+                // Rotate (constant indices keep the rings in registers): the oldest prefetched pair
+                // becomes the newest record load, and one more pair load is issued.
+#pragma unroll
+                for (uint32_t q = 0; q + 1 < kAhead; q++) {
+                    ring[q] = ring[q + 1];
+                    ring_s[q] = ring_s[q + 1];
+                    ring_ok[q] = ring_ok[q + 1];
+                }
+                const auto t = take_pair(0);
+                ring_ok[kAhead - 1] = t.first;
+                ring_s[kAhead - 1] = t.second;
+                ring[kAhead - 1] = L.recs[ring_s[kAhead - 1]];
+#pragma unroll
+                for (uint32_t q = 0; q + 1 < kAhead; q++) pre_key[q] = pre_key[q + 1];
+                fetch_pair(kAhead - 1);
+                alive = ring_ok[0];
+            }
+        }
+    }
+    if (o < owners) {
+        tb_account_t& a = T.acc_rows[row];
+        a.debits_posted = W(dpo);
+        a.credits_posted = W(cpo);
+        const uint16_t h = acc_hazard_of(a);
+        if (h) acc_hazard_set(T.acc_index, T.acc_entry_of, row, h);
+    }
+    if (o == 0) T.scalars->stats[2] = L.m;
+}
+
+// After the lanes, one lane per event: the result (timestamp, verdict), the sides of created
+// events that no lane owns (u128 atomics: their balances are never read in the call), and the
+// transfers key_max.
+__global__ void lanes_finish(Tables T, Call<tb_transfer_t> c, LanePlan L) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t ts_max = 0;
+    if (s < L.m && L.counts[2]) {
+        const Step st = L.steps[s];
+        const LaneRec rec = L.recs[s];
+        const uint8_t out = L.outcome[s];
+        tb_create_result_t res;
+        res.timestamp = st.ts_event;
+        res.status = out == kOutCreated ? TB_STATUS_CREATED
+                                        : (out == kOutExceedsCredits ? TB_CT_EXCEEDS_CREDITS
+                                                                     : TB_CT_EXCEEDS_DEBITS);
+        res.reserved = 0;
+        c.results[st.k] = res;
+        if (out == kOutCreated) {
+            ts_max = st.ts_event;
+            const BalTarget B{T.acc_rows, T.acc_index, T.acc_entry_of};
+            if (!(rec.bits & kLaneDrOwner)) add_field(B, st.dr * 4 + 1, rec.amount, true);
+            if (!(rec.bits & kLaneCrOwner)) add_field(B, st.cr * 4 + 3, rec.amount, true);
+        }
+    }
+    ts_max = block_reduce(ts_max, OpMax());
+    if (threadIdx.x == 0 && ts_max)
+        atomicMax(&T.scalars->transfers_key_max, (unsigned long long)ts_max);
+}
+
+}  // namespace tbg
