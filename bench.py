@@ -320,7 +320,7 @@ def main():
 
     opt = native.TbgOptions()
     opt.account_capacity = A
-    opt.transfer_capacity = N * (K + W)
+    opt.transfer_capacity = N * (K + W + 1)  # + one host-buffer step (pcie_inclusive)
     opt.batch_events_max = max(N, wl.chunk)
     opt.batch_count_max = len(lens)
     opt.pulse_batch_max = 8190
@@ -399,6 +399,27 @@ def main():
         if not ok:
             print(json.dumps({"error": "validation failed"}), file=sys.stderr)
 
+    # The same step through the host-buffer ABI (tbg_create_transfers: events copied in, results
+    # copied out over PCIe) -- the rate a caller holding host buffers sees; never `value`.
+    pcie = None
+    if not args.no_validate:
+        ev = base.copy()
+        ev["id"][:, 0] += np.uint64((W + K) * N)
+        ts, prepare_ts = step_timestamps(prepare_ts, lens)
+        h_lens = lens.astype(np.uint32)
+        h_res = np.zeros(N, dtype=RESULT_DTYPE)
+        t0 = time.perf_counter()
+        rc = lib.tbg_create_transfers(g, ev.ctypes.data_as(ctypes.c_void_p), N,
+                                      h_lens.ctypes.data_as(native.c_u32p),
+                                      ts.ctypes.data_as(native.c_u64p), len(lens),
+                                      h_res.ctypes.data_as(ctypes.c_void_p))
+        t_host = time.perf_counter() - t0
+        ok = rc == 0 and bool((h_res["status"] == 0xFFFFFFFF).all())
+        validated = bool(validated) and ok
+        pcie = {"value": round(N / t_host, 1), "unit": "transfers/s", "ms": round(t_host * 1e3, 3),
+                "note": "one step through tbg_create_transfers with host buffers (events in, "
+                        "results out over PCIe)"}
+
     # Algorithmic bytes of the path: 288 B per event + 256 B per distinct account.
     distinct = len(np.union1d(wl.dr, wl.cr))
     path_bytes = 288 * N + 256 * distinct
@@ -443,6 +464,7 @@ def main():
             "replayed_events_last_step": int(stats.replayed),
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "pcie_inclusive": pcie,
         }
         print(json.dumps(line))
     lib.tbg_close(g)
