@@ -82,6 +82,18 @@ int tbg_create_transfers_device(tbg_ctx* ctx, const tb_transfer_t* d_events, uin
 int64_t tbg_pulse(tbg_ctx* ctx, uint64_t timestamp);
 uint64_t tbg_pulse_next_timestamp(tbg_ctx* ctx);
 
+/* Sharded pulses (one executor per ledger shard; the reference's single expires_at scan,
+ * ExpirePendingTransfersType :4875-5029, spans all shards): the count of this shard's
+ * expired-eligible pending transfers at `timestamp` and the first `max` of their index keys
+ * (expires_at, timestamp) in order; then the pulse that expires exactly this shard's entries up to
+ * and including a cut key -- the pulse_batch_max-th key across all shards -- and sets
+ * pulse_next_timestamp (the cut's expires_at: the scan's buffer filled). Both return a count or a
+ * negative error. */
+int64_t tbg_pulse_candidates(tbg_ctx* ctx, uint64_t timestamp, uint64_t* expires_at,
+                             uint64_t* timestamps, uint32_t max);
+int64_t tbg_pulse_cut(tbg_ctx* ctx, uint64_t timestamp, uint64_t cut_expires_at,
+                      uint64_t cut_timestamp, uint64_t pulse_next_timestamp);
+
 /* Found objects only, in request order; returns the count written. */
 int64_t tbg_lookup_accounts(tbg_ctx* ctx, const tb_uint128_t* ids, uint32_t n, tb_account_t* out);
 int64_t tbg_lookup_transfers(tbg_ctx* ctx, const tb_uint128_t* ids, uint32_t n,

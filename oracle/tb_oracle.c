@@ -832,8 +832,9 @@ static int expiry_cmp(const void* a_, const void* b_) {
     return 0;
 }
 
-uint32_t tbo_pulse(tbo_ctx* c, uint64_t timestamp) {
-    /* Scan the expires_at index (entries: pending-status transfers with timeout > 0). */
+/* The expires_at index in (expires_at, timestamp) order: pending-status transfers with
+ * timeout > 0 (state_machine.zig:443-450); compacts the list. The caller frees *out. */
+static uint64_t expiry_sorted(tbo_ctx* c, expiry_key_t** out) {
     expiry_key_t* keys = (expiry_key_t*)xrealloc(NULL, (c->n_expiry + 1) * sizeof(expiry_key_t));
     uint64_t n_keys = 0, w = 0;
     for (uint64_t k = 0; k < c->n_expiry; k++) {
@@ -848,21 +849,12 @@ uint32_t tbo_pulse(tbo_ctx* c, uint64_t timestamp) {
     }
     c->n_expiry = w;
     qsort(keys, n_keys, sizeof(expiry_key_t), expiry_cmp);
+    *out = keys;
+    return n_keys;
+}
 
-    uint64_t expired = 0;
-    while (expired < n_keys && expired < c->pulse_batch_max &&
-           keys[expired].expires_at <= timestamp)
-        expired++;
-
-    /* ExpirePendingTransfers.finish: buffer_finished iff the buffer filled up. */
-    if (expired == c->pulse_batch_max) {
-        c->pulse_next_timestamp = keys[expired - 1].expires_at;
-    } else if (expired < n_keys) {
-        c->pulse_next_timestamp = keys[expired].expires_at; /* first unexpired */
-    } else {
-        c->pulse_next_timestamp = TB_TIMESTAMP_MAX;
-    }
-
+/* execute_expire_pending_transfers (:4540-4626) for the first `expired` keys. */
+static void expire_keys(tbo_ctx* c, const expiry_key_t* keys, uint64_t expired, uint64_t timestamp) {
     for (uint64_t k = 0; k < expired; k++) {
         const tb_transfer_t* p = &c->transfers[keys[k].index];
         tb_account_t* dr = get_account(c, U(p->debit_account_id));
@@ -878,6 +870,56 @@ uint32_t tbo_pulse(tbo_ctx* c, uint64_t timestamp) {
         c->pending_status[keys[k].index] = TB_PENDING_EXPIRED;
         c->commit_timestamp = timestamp - expired + k + 1;
     }
+}
+
+uint32_t tbo_pulse(tbo_ctx* c, uint64_t timestamp) {
+    expiry_key_t* keys;
+    const uint64_t n_keys = expiry_sorted(c, &keys);
+    uint64_t expired = 0;
+    while (expired < n_keys && expired < c->pulse_batch_max &&
+           keys[expired].expires_at <= timestamp)
+        expired++;
+
+    /* ExpirePendingTransfers.finish: buffer_finished iff the buffer filled up. */
+    if (expired == c->pulse_batch_max) {
+        c->pulse_next_timestamp = keys[expired - 1].expires_at;
+    } else if (expired < n_keys) {
+        c->pulse_next_timestamp = keys[expired].expires_at; /* first unexpired */
+    } else {
+        c->pulse_next_timestamp = TB_TIMESTAMP_MAX;
+    }
+    expire_keys(c, keys, expired, timestamp);
+    free(keys);
+    return (uint32_t)expired;
+}
+
+uint64_t tbo_pulse_candidates(tbo_ctx* c, uint64_t timestamp, uint64_t* expires_at,
+                              uint64_t* timestamps, uint32_t max) {
+    expiry_key_t* keys;
+    const uint64_t n_keys = expiry_sorted(c, &keys);
+    uint64_t n = 0;
+    while (n < n_keys && keys[n].expires_at <= timestamp) {
+        if (n < max) {
+            expires_at[n] = keys[n].expires_at;
+            timestamps[n] = keys[n].timestamp;
+        }
+        n++;
+    }
+    free(keys);
+    return n;
+}
+
+uint32_t tbo_pulse_cut(tbo_ctx* c, uint64_t timestamp, uint64_t cut_expires_at,
+                       uint64_t cut_timestamp, uint64_t pulse_next_timestamp) {
+    expiry_key_t* keys;
+    const uint64_t n_keys = expiry_sorted(c, &keys);
+    uint64_t expired = 0;
+    while (expired < n_keys && keys[expired].expires_at <= timestamp &&
+           (keys[expired].expires_at < cut_expires_at ||
+            (keys[expired].expires_at == cut_expires_at && keys[expired].timestamp <= cut_timestamp)))
+        expired++;
+    c->pulse_next_timestamp = pulse_next_timestamp;
+    expire_keys(c, keys, expired, timestamp);
     free(keys);
     return (uint32_t)expired;
 }

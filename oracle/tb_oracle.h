@@ -38,6 +38,15 @@ void tbo_create_transfers(tbo_ctx* ctx, const tb_transfer_t* events, uint32_t n,
 /* pulse: prefetch_expire_pending_transfers + execute_expire_pending_transfers
  * (state_machine.zig:2436-2562, :4511-4628, :4875-5029). Returns the number expired. */
 uint32_t tbo_pulse(tbo_ctx* ctx, uint64_t timestamp);
+/* Sharded pulses: the expired-eligible entries of this shard's expires_at index,
+ * in (expires_at, timestamp) order -- their count, and the first `max` keys; then the pulse that
+ * expires exactly the entries up to a cut key (the global pulse_batch_max-th across shards) and
+ * sets pulse_next_timestamp (the cut's expires_at, as ExpirePendingTransfers.finish does when its
+ * buffer fills). */
+uint64_t tbo_pulse_candidates(tbo_ctx* ctx, uint64_t timestamp, uint64_t* expires_at,
+                              uint64_t* timestamps, uint32_t max);
+uint32_t tbo_pulse_cut(tbo_ctx* ctx, uint64_t timestamp, uint64_t cut_expires_at,
+                       uint64_t cut_timestamp, uint64_t pulse_next_timestamp);
 int tbo_pulse_needed(const tbo_ctx* ctx, uint64_t timestamp);
 uint64_t tbo_pulse_next_timestamp(const tbo_ctx* ctx);
 

@@ -38,9 +38,9 @@ def _ptr(a):
 class OracleShard:
     """The CPU oracle behind the shard executor interface (test infrastructure only)."""
 
-    def __init__(self):
+    def __init__(self, pbm=PBM):
         self.lib = oracle_binding.load()
-        self.o = self.lib.tbo_open(PBM, TIMESTAMP_MAX)
+        self.o = self.lib.tbo_open(pbm, TIMESTAMP_MAX)
 
     def close(self):
         if self.o:
@@ -66,6 +66,17 @@ class OracleShard:
 
     def pulse(self, timestamp):
         return int(self.lib.tbo_pulse(self.o, timestamp))
+
+    def pulse_candidates(self, timestamp, max_keys):
+        e = np.zeros(max(max_keys, 1), dtype=np.uint64)
+        t = np.zeros(max(max_keys, 1), dtype=np.uint64)
+        n = int(self.lib.tbo_pulse_candidates(self.o, timestamp, _ptr(e), _ptr(t), max_keys))
+        k = min(n, max_keys)
+        return n, list(zip(e[:k].tolist(), t[:k].tolist()))
+
+    def pulse_cut(self, timestamp, cut_expires_at, cut_timestamp, pulse_next_timestamp):
+        return int(self.lib.tbo_pulse_cut(self.o, timestamp, cut_expires_at, cut_timestamp,
+                                          pulse_next_timestamp))
 
     def pulse_next_timestamp(self):
         return int(self.lib.tbo_pulse_next_timestamp(self.o))
@@ -156,9 +167,10 @@ def scenario(seed, calls=8, n_acc=48):
     return ops
 
 
-def drive(cluster, ref, ops, rank0=True):
+def drive(cluster, ref, ops, rank0=True, pbm=PBM, cuts=None):
     """Runs `ops` through `cluster` (and `ref`, compared call by call); returns the pulses run.
-    Timestamps follow the TestContext rule (prepare_ts += 1 + events, pulses when due)."""
+    Timestamps follow the TestContext rule (prepare_ts += 1 + events, pulses when due). `cuts`
+    (a list) collects the pulses that expired exactly pbm transfers (a cut across shards)."""
     ts, pulses = 0, 0
     for op in ops:
         if op[0] == "tick":
@@ -181,10 +193,12 @@ def drive(cluster, ref, ops, rank0=True):
         if ref is not None:
             assert nxt == ref.pulse_next_timestamp()
         if nxt <= ts:
-            ts += 1 + PBM
+            ts += 1 + pbm
             expired = cluster.pulse(ts)
             if ref is not None:
                 assert expired == ref.pulse(ts)
+            if cuts is not None and expired == pbm:
+                cuts.append(ts)
             pulses += 1
     return pulses
 
@@ -314,17 +328,40 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _gloo_rank(rank, world, port, seed, q):
+@pytest.mark.parametrize("seed", [3, 4])
+def test_local_shards_pulse_cut(seed):
+    """pulse_batch_max 6: pulses whose expired transfers span shards and exceed the batch take
+    the global cut (the 6th key across shards) -- the same transfers, counts and
+    pulse_next_timestamp as the unsharded reference."""
+    pbm = 6
+    shards = [OracleShard(pbm) for _ in range(3)]
+    ref = OracleShard(pbm)
+    try:
+        cluster = shard.LocalShards(shard.LedgerRouter(3, ledgers=LEDGERS), shards, pbm)
+        cuts = []
+        assert drive(cluster, ref, scenario(seed, calls=10), pbm=pbm, cuts=cuts) > 0
+        assert cuts, "the scenario should expire more than pulse_batch_max at once"
+        assert_same_state([s.dump() for s in shards], ref)
+    finally:
+        for s in shards + [ref]:
+            s.close()
+
+
+def _gloo_rank(rank, world, port, seed, q, pbm=PBM):
     try:
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(port)
         import torch.distributed as dist
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        ex = OracleShard()
+        ex = OracleShard(pbm)
         router = shard.LedgerRouter(world, ledgers=LEDGERS) if rank == 0 else None
-        group = shard.ShardGroup(ex, router, device="cpu", pulse_batch_max=PBM)
-        ref = OracleShard() if rank == 0 else None
-        pulses = drive(group, ref, scenario(seed), rank0=rank == 0)
+        group = shard.ShardGroup(ex, router, device="cpu", pulse_batch_max=pbm)
+        ref = OracleShard(pbm) if rank == 0 else None
+        cuts = []
+        pulses = drive(group, ref, scenario(seed, calls=10 if pbm < PBM else 8),
+                       rank0=rank == 0, pbm=pbm, cuts=cuts)
+        if rank == 0 and pbm < PBM:
+            assert cuts, "the scenario should expire more than pulse_batch_max at once"
         dumps = [None] * world
         dist.all_gather_object(dumps, ex.dump())
         if rank == 0:
@@ -352,11 +389,12 @@ def _gloo_rank(rank, world, port, seed, q):
         q.put((rank, traceback.format_exc(), 0))
 
 
-def test_shard_group_gloo_world2():
+@pytest.mark.parametrize("pbm", [PBM, 6], ids=["pbm8190", "pbm6-cuts"])
+def test_shard_group_gloo_world2(pbm):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_gloo_rank, args=(r, 2, port, 5, q)) for r in range(2)]
+    procs = [ctx.Process(target=_gloo_rank, args=(r, 2, port, 5, q, pbm)) for r in range(2)]
     for p in procs:
         p.start()
     out = {}
@@ -382,6 +420,26 @@ def test_local_shards_gpu():
     try:
         cluster = shard.LocalShards(shard.LedgerRouter(2, ledgers=LEDGERS), shards, PBM)
         assert drive(cluster, ref, scenario(11)) > 0
+        assert_same_state([s.dump() for s in shards], ref)
+    finally:
+        for s in shards:
+            s.close()
+        ref.close()
+
+
+@pytest.mark.gpu
+def test_local_shards_gpu_pulse_cut():
+    """Two HBM executors with pulse_batch_max 6: the global pulse cut through tbg_pulse_candidates
+    / tbg_pulse_cut, against the unsharded oracle."""
+    pbm = 6
+    shards = [shard.GpuShard(1 << 10, 1 << 14, batch_events_max=4096, pulse_batch_max=pbm)
+              for _ in range(2)]
+    ref = OracleShard(pbm)
+    try:
+        cluster = shard.LocalShards(shard.LedgerRouter(2, ledgers=LEDGERS), shards, pbm)
+        cuts = []
+        assert drive(cluster, ref, scenario(12, calls=10), pbm=pbm, cuts=cuts) > 0
+        assert cuts
         assert_same_state([s.dump() for s in shards], ref)
     finally:
         for s in shards:

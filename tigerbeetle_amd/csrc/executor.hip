@@ -968,8 +968,18 @@ int tbg_create_accounts(tbg_ctx* ctx, const tb_account_t* events, uint32_t n,
     return 0;
 }
 
-int64_t tbg_pulse(tbg_ctx* ctx, uint64_t timestamp) {
-    if (!ctx) return TBG_EINVAL;
+}  // extern "C"
+
+namespace {
+
+// The expired-eligible entries of the expires_at index: candidates (rows, expires_at) at
+// S.rows / S.exp, sorted into (expires_at, timestamp) order when `sort`; the entries still pending
+// at S.keep. Row order is timestamp order, so a stable sort by row followed by a stable sort by
+// expires_at yields the index order (scan_lookup.zig:150-175).
+struct PulseGather {
+    uint64_t cands = 0, kept = 0, next_unexpired = ~0ull;
+};
+int pulse_gather(tbg_ctx* ctx, uint64_t timestamp, bool sort, PulseGather* out) {
     int rc = sync_scalars(ctx);
     if (rc) return rc;
     const uint64_t count = std::min<uint64_t>(ctx->h_scalars->expiry_count, ctx->T.expiry_capacity);
@@ -987,15 +997,11 @@ int64_t tbg_pulse(tbg_ctx* ctx, uint64_t timestamp) {
     HIP_TRY(ctx, hipMemcpyAsync(h_counters, S.counters, sizeof(h_counters), hipMemcpyDeviceToHost,
                                 ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    const uint64_t kept = h_counters[0], cands = h_counters[1];
-    const uint64_t batch_max = ctx->opt.pulse_batch_max;
-    const uint64_t expired = std::min<uint64_t>(cands, batch_max);
-    uint64_t pulse_next = h_counters[2] == ~0ull ? TB_TIMESTAMP_MAX : h_counters[2];
-    if (cands >= batch_max) {
-        // The expires_at index is ordered by (expires_at, timestamp) and the scan stops with
-        // buffer_finished after batch_max values (scan_lookup.zig:150-175): expire the first
-        // batch_max in that order. Row order is timestamp order, so a stable sort by row followed
-        // by a stable sort by expires_at yields the index order.
+    out->kept = h_counters[0];
+    out->cands = h_counters[1];
+    out->next_unexpired = h_counters[2];
+    const uint64_t cands = out->cands;
+    if (sort && cands > 1) {
         size_t bytes = 0, bytes2 = 0;
         HIP_TRY(ctx, hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, S.rows, S.rows_b, S.exp,
                                                         S.exp_b, int(cands), 0, 64, ctx->stream));
@@ -1009,12 +1015,14 @@ int64_t tbg_pulse(tbg_ctx* ctx, uint64_t timestamp) {
         HIP_TRY(ctx, hipcub::DeviceRadixSort::SortPairs(ctx->cub_temp, bytes2, S.exp_b, S.exp,
                                                         S.rows_b, S.rows, int(cands), 0, 64,
                                                         ctx->stream));
-        uint64_t last = 0;
-        HIP_TRY(ctx, hipMemcpyAsync(&last, S.exp + (batch_max - 1), 8, hipMemcpyDeviceToHost,
-                                    ctx->stream));
-        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-        pulse_next = last;
     }
+    return 0;
+}
+
+// Expire the first `expired` candidates (S.rows, in order), keep the still-pending entries, set
+// pulse_next_timestamp.
+int pulse_finish(tbg_ctx* ctx, uint64_t expired, uint64_t kept, uint64_t pulse_next) {
+    PulseScratch& S = ctx->pulse;
     if (expired)
         hipLaunchKernelGGL(pulse_apply, dim3(grid_for(expired)), dim3(kBlock), 0, ctx->stream,
                            ctx->T, S.rows, expired);
@@ -1029,7 +1037,82 @@ int64_t tbg_pulse(tbg_ctx* ctx, uint64_t timestamp) {
     HIP_TRY(ctx, hipMemcpyAsync(&ctx->d_scalars->pulse_next_timestamp, &next_ull, 8,
                                 hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    return int64_t(expired);
+    return 0;
+}
+
+// The first n sorted candidates' keys to the host.
+int pulse_keys(tbg_ctx* ctx, uint64_t n, std::vector<uint64_t>* exp, std::vector<uint64_t>* ts) {
+    PulseScratch& S = ctx->pulse;
+    exp->resize(n);
+    ts->resize(n);
+    if (!n) return 0;
+    hipLaunchKernelGGL(pulse_key_timestamps, dim3(grid_for(n)), dim3(kBlock), 0, ctx->stream,
+                       ctx->T, S.rows, n, S.ts);
+    HIP_TRY(ctx, hipMemcpyAsync(exp->data(), S.exp, n * 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(ts->data(), S.ts, n * 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t tbg_pulse(tbg_ctx* ctx, uint64_t timestamp) {
+    if (!ctx) return TBG_EINVAL;
+    PulseGather G;
+    const uint64_t batch_max = ctx->opt.pulse_batch_max;
+    int rc = pulse_gather(ctx, timestamp, false, &G);
+    if (rc) return rc;
+    uint64_t expired = std::min<uint64_t>(G.cands, batch_max);
+    uint64_t pulse_next = G.next_unexpired == ~0ull ? TB_TIMESTAMP_MAX : G.next_unexpired;
+    if (G.cands >= batch_max) {
+        // The scan stops with buffer_finished after batch_max values: expire the first batch_max
+        // in index order; pulse_next_timestamp is the last one's expires_at (:4969-4999).
+        rc = pulse_gather(ctx, timestamp, true, &G);
+        if (rc) return rc;
+        uint64_t last = 0;
+        HIP_TRY(ctx, hipMemcpyAsync(&last, ctx->pulse.exp + (batch_max - 1), 8,
+                                    hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        pulse_next = last;
+    }
+    rc = pulse_finish(ctx, expired, G.kept, pulse_next);
+    return rc ? rc : int64_t(expired);
+}
+
+int64_t tbg_pulse_candidates(tbg_ctx* ctx, uint64_t timestamp, uint64_t* expires_at,
+                             uint64_t* timestamps, uint32_t max) {
+    if (!ctx) return TBG_EINVAL;
+    PulseGather G;
+    int rc = pulse_gather(ctx, timestamp, true, &G);
+    if (rc) return rc;
+    std::vector<uint64_t> e, t;
+    rc = pulse_keys(ctx, std::min<uint64_t>(G.cands, max), &e, &t);
+    if (rc) return rc;
+    for (size_t i = 0; i < e.size(); i++) {
+        if (expires_at) expires_at[i] = e[i];
+        if (timestamps) timestamps[i] = t[i];
+    }
+    return int64_t(G.cands);
+}
+
+int64_t tbg_pulse_cut(tbg_ctx* ctx, uint64_t timestamp, uint64_t cut_expires_at,
+                      uint64_t cut_timestamp, uint64_t pulse_next_timestamp) {
+    if (!ctx) return TBG_EINVAL;
+    PulseGather G;
+    int rc = pulse_gather(ctx, timestamp, true, &G);
+    if (rc) return rc;
+    // The cut is at most the global batch_max-th key: this shard expires at most that many.
+    std::vector<uint64_t> e, t;
+    rc = pulse_keys(ctx, std::min<uint64_t>(G.cands, ctx->opt.pulse_batch_max), &e, &t);
+    if (rc) return rc;
+    uint64_t expired = 0;
+    while (expired < e.size() && (e[expired] < cut_expires_at ||
+                                  (e[expired] == cut_expires_at && t[expired] <= cut_timestamp)))
+        expired++;
+    rc = pulse_finish(ctx, expired, G.kept, pulse_next_timestamp);
+    return rc ? rc : int64_t(expired);
 }
 
 uint64_t tbg_pulse_next_timestamp(tbg_ctx* ctx) {

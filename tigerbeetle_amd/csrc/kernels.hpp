@@ -1284,6 +1284,12 @@ __global__ void pulse_collect(Tables T, uint64_t timestamp, uint64_t count, uint
     }
 }
 
+// The timestamps of the first n sorted candidates (their index keys' second half).
+__global__ void pulse_key_timestamps(Tables T, const uint64_t* rows, uint64_t n, uint64_t* ts) {
+    const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i < n) ts[i] = T.tr_rows[rows[i]].timestamp;
+}
+
 // execute_expire_pending_transfers (:4540-4626) for the selected rows.
 __global__ void pulse_apply(Tables T, const uint64_t* rows, uint64_t n) {
     const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;

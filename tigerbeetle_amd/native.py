@@ -84,6 +84,9 @@ SIGNATURES = [
     ("tbg_create_transfers_device", ctypes.c_int, [vp, vp, ctypes.c_uint32, vp, vp,
                                                   ctypes.c_uint32, vp, vp]),
     ("tbg_pulse", ctypes.c_int64, [vp, ctypes.c_uint64]),
+    ("tbg_pulse_candidates", ctypes.c_int64, [vp, ctypes.c_uint64, vp, vp, ctypes.c_uint32]),
+    ("tbg_pulse_cut", ctypes.c_int64, [vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                       ctypes.c_uint64]),
     ("tbg_pulse_next_timestamp", ctypes.c_uint64, [vp]),
     ("tbg_lookup_accounts", ctypes.c_int64, [vp, vp, ctypes.c_uint32, vp]),
     ("tbg_lookup_transfers", ctypes.c_int64, [vp, vp, ctypes.c_uint32, vp]),

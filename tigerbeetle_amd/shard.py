@@ -38,11 +38,15 @@ shard edge, which the router refused), and no batch-level check besides chain en
 imported flag depends on the batch extent.
 
 pulse: with the resets above excluded, `pulse_next_timestamp` only moves by `min` between pulses
-(:3979-3980), so the sharded value is the minimum over shards (an all-reduce). Each shard expires
-its own transfers at the common pulse timestamp; this is the reference's pulse while fewer than
-`pulse_batch_max` transfers expire in total (the scan stops at that many and sets
-`pulse_next_timestamp` from the last one, :4969-4999). Past it the drivers raise `RouteError`:
-the cut across shards needs an all-gather of the shards' expiry keys.
+(:3979-3980), so the sharded value is the minimum over shards (an all-reduce). The reference's
+pulse scans the expires_at index in (expires_at, timestamp) order and stops after
+`pulse_batch_max` entries, setting `pulse_next_timestamp` from the last one (:4969-4999,
+scan_lookup.zig:150-175). Sharded: every shard reports how many of its entries have expired and
+the first `pulse_batch_max` of their keys (an all-gather); below `pulse_batch_max` in total every
+shard expires all of its own (and keeps its earliest unexpired expiry, whose minimum over shards
+is the reference's); otherwise the `pulse_batch_max`-th key across shards is the cut: each shard
+expires its entries up to it and sets `pulse_next_timestamp` to the cut's expiry. Timestamps are
+unique, so the cut expires exactly `pulse_batch_max` transfers -- the reference's.
 """
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Set
@@ -269,9 +273,14 @@ def gather_results(plan: Plan, shard_results: List[Optional[np.ndarray]], n: int
     return out
 
 
-def _check_pulse(expired: int, pulse_batch_max: int):
-    if expired >= pulse_batch_max:
-        raise RouteError(f"pulse expired {expired} >= pulse_batch_max across shards")
+def pulse_cut(counts, key_lists, pulse_batch_max: int):
+    """The global pulse cut (module doc): None when fewer than pulse_batch_max entries expired
+    across shards, else the pulse_batch_max-th key (expires_at, timestamp) in index order. Each
+    shard reports its first pulse_batch_max keys, which hold every key up to the global cut."""
+    if sum(int(c) for c in counts) < pulse_batch_max:
+        return None
+    keys = sorted((int(e), int(t)) for ks in key_lists for e, t in ks)
+    return keys[pulse_batch_max - 1]
 
 
 class LocalShards:
@@ -313,9 +322,11 @@ class LocalShards:
         return min(int(ex.pulse_next_timestamp()) for ex in self.executors)
 
     def pulse(self, timestamp: int) -> int:
-        expired = sum(int(ex.pulse(timestamp)) for ex in self.executors)
-        _check_pulse(expired, self.pulse_batch_max)
-        return expired
+        cands = [ex.pulse_candidates(timestamp, self.pulse_batch_max) for ex in self.executors]
+        cut = pulse_cut([c for c, _ in cands], [k for _, k in cands], self.pulse_batch_max)
+        if cut is None:
+            return sum(int(ex.pulse(timestamp)) for ex in self.executors)
+        return sum(int(ex.pulse_cut(timestamp, cut[0], cut[1], cut[0])) for ex in self.executors)
 
 
 class ShardGroup:
@@ -423,14 +434,30 @@ class ShardGroup:
         return int(t.item())
 
     def pulse(self, timestamp: int) -> int:
-        """Collective: every shard expires at the common pulse timestamp."""
+        """Collective: every shard expires at the common pulse timestamp, up to the global cut
+        (an all-gather of each shard's first pulse_batch_max expiry keys)."""
         import torch
-        t = torch.tensor([int(self.executor.pulse(timestamp))], dtype=torch.int64,
-                         device=self.device)
+        B = self.pulse_batch_max
+        count, keys = self.executor.pulse_candidates(timestamp, B)
+        mine = torch.full((B + 1, 2), (1 << 63) - 1, dtype=torch.int64)
+        mine[0, 0] = int(count)
+        if keys:
+            mine[1:1 + len(keys)] = torch.tensor(keys, dtype=torch.int64)
+        mine = mine.to(self.device)
+        parts = [torch.empty_like(mine) for _ in range(self.world)]
+        self.dist.all_gather(parts, mine, group=self.group)
+        parts = [p.cpu() for p in parts]
+        counts = [int(p[0, 0]) for p in parts]
+        key_lists = [[(int(e), int(t)) for e, t in p[1:1 + min(c, B)].tolist()]
+                     for p, c in zip(parts, counts)]
+        cut = pulse_cut(counts, key_lists, B)
+        if cut is None:
+            local = int(self.executor.pulse(timestamp))
+        else:
+            local = int(self.executor.pulse_cut(timestamp, cut[0], cut[1], cut[0]))
+        t = torch.tensor([local], dtype=torch.int64, device=self.device)
         self.dist.all_reduce(t, group=self.group)
-        expired = int(t.item())
-        _check_pulse(expired, self.pulse_batch_max)
-        return expired
+        return int(t.item())
 
 
 class GpuShard:
@@ -485,6 +512,24 @@ class GpuShard:
 
     def pulse(self, timestamp):
         return int(self.lib.tbg_pulse(self.g, timestamp))
+
+    def pulse_candidates(self, timestamp, max_keys):
+        c = self._c
+        e = np.zeros(max(max_keys, 1), dtype=np.uint64)
+        t = np.zeros(max(max_keys, 1), dtype=np.uint64)
+        n = int(self.lib.tbg_pulse_candidates(self.g, timestamp, e.ctypes.data_as(c.c_void_p),
+                                              t.ctypes.data_as(c.c_void_p), max_keys))
+        if n < 0:
+            raise RuntimeError(f"libtbg: {n} {self.lib.tbg_last_error(self.g)}")
+        k = min(n, max_keys)
+        return n, list(zip(e[:k].tolist(), t[:k].tolist()))
+
+    def pulse_cut(self, timestamp, cut_expires_at, cut_timestamp, pulse_next_timestamp):
+        n = int(self.lib.tbg_pulse_cut(self.g, timestamp, cut_expires_at, cut_timestamp,
+                                       pulse_next_timestamp))
+        if n < 0:
+            raise RuntimeError(f"libtbg: {n} {self.lib.tbg_last_error(self.g)}")
+        return n
 
     def pulse_next_timestamp(self):
         return int(self.lib.tbg_pulse_next_timestamp(self.g))
