@@ -60,6 +60,8 @@ struct FlowScratch {
     unsigned int* counts = nullptr;
     unsigned long long* pnt_fired = nullptr;
     UndoEntry* lane_undo = nullptr;
+    unsigned int* engine = nullptr;  // flow engine queue counters
+    uint32_t *exp_flag = nullptr, *exp_index = nullptr;
 };
 
 }  // namespace
@@ -311,7 +313,8 @@ int end_call(tbg_ctx* ctx, uint32_t n, bool already_synced = false) {
 void free_flow(FlowScratch& F) {
     void* ptrs[] = {F.head8, F.barrier8, F.heads, F.unit_of, F.barriers, F.vals, F.vals_sorted,
                     F.pred, F.done, F.keys, F.keys_sorted, F.pnt_ops, F.pnt_scan, F.steps,
-                    F.queue, F.ready8, F.recs, F.mailbox, F.owner_starts, F.owner_head8, F.mb_index};
+                    F.queue, F.ready8, F.recs, F.mailbox, F.owner_starts, F.owner_head8, F.mb_index,
+                    F.exp_flag, F.exp_index};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     F.head8 = F.barrier8 = nullptr;
@@ -321,6 +324,7 @@ void free_flow(FlowScratch& F) {
     F.queue = nullptr;
     F.ready8 = nullptr;
     F.recs = nullptr;
+    F.exp_flag = F.exp_index = nullptr;
     F.mailbox = F.owner_starts = F.mb_index = nullptr;
     F.owner_head8 = nullptr;
     F.cap = 0;
@@ -333,7 +337,8 @@ int ensure_flow(tbg_ctx* ctx, uint64_t m) {
         ok = dev_alloc(ctx, &F.dup_mark, ctx->opt.batch_events_max, true) &&
              dev_alloc(ctx, &F.counts, 4, true) && dev_alloc(ctx, &F.pnt_fired, 1, true) &&
              dev_alloc(ctx, &F.lane_counts, 4, true) &&
-             dev_alloc(ctx, &F.lane_undo, uint64_t(kFlowThreads) * kFlowUndoPerLane, false);
+             dev_alloc(ctx, &F.lane_undo, uint64_t(kFlowLanesMax) * kFlowUndoPerLane, false) &&
+             dev_alloc(ctx, &F.engine, kFlowEngineWords, true);
         if (!ok) return TBG_EHIP;
     }
     if (m <= F.cap) return 0;
@@ -350,6 +355,7 @@ int ensure_flow(tbg_ctx* ctx, uint64_t m) {
          dev_alloc(ctx, &F.queue, cap, false) && dev_alloc(ctx, &F.ready8, cap + kFlowThreads, false) &&
          dev_alloc(ctx, &F.recs, cap, false) && dev_alloc(ctx, &F.mailbox, cap, false) &&
          dev_alloc(ctx, &F.mb_index, cap, false) &&
+         dev_alloc(ctx, &F.exp_flag, cap, false) && dev_alloc(ctx, &F.exp_index, cap, false) &&
          dev_alloc(ctx, &F.owner_starts, kc, false) && dev_alloc(ctx, &F.owner_head8, kc, false);
     if (!ok) {
         free_flow(F);
@@ -390,6 +396,14 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
     P.pnt_fired = F.pnt_fired;
     P.lane_undo = F.lane_undo;
     P.steps = F.steps;
+    P.engine = F.engine;
+    P.exp_flag = F.exp_flag;
+    P.exp_index = F.exp_index;
+    // Additive accounts get no key (Replay::additive); TBG_NO_ADDITIVE keys every account.
+    const bool lanes_possible =
+        !(call_flags & (kFlagDuplicate | kFlagPostVoid | kFlagClosable | kFlagImported)) &&
+        !c.force_replay && !getenv("TBG_NO_LANES");
+    P.add_epoch = getenv("TBG_NO_ADDITIVE") ? 0 : c.epoch;
     const dim3 block(kBlock);
     hipLaunchKernelGGL(flow_heads, dim3(grid_for(m)), block, 0, ctx->stream, ctx->T, c, P);
     rc = select_flagged(ctx, F.head8, m, F.heads, &F.counts[0]);
@@ -397,6 +411,17 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
     hipLaunchKernelGGL(flow_units, dim3(grid_for(m)), block, 0, ctx->stream, P);
     hipLaunchKernelGGL(flow_keys, dim3(grid_for(m)), block, 0, ctx->stream, ctx->T, c, P,
                        call_flags);
+    {  // the planned expires_at entries
+        size_t sb = 0;
+        HIP_TRY(ctx, hipcub::DeviceScan::ExclusiveSum(nullptr, sb, F.exp_flag, F.exp_index, int(m),
+                                                      ctx->stream));
+        rc = ensure_cub_temp(ctx, sb);
+        if (rc) return rc;
+        HIP_TRY(ctx, hipcub::DeviceScan::ExclusiveSum(ctx->cub_temp, sb, F.exp_flag, F.exp_index,
+                                                      int(m), ctx->stream));
+        hipLaunchKernelGGL(flow_expiry, dim3(grid_for(m)), block, 0, ctx->stream, ctx->T, c, P);
+        hipLaunchKernelGGL(flow_expiry_count, dim3(1), dim3(64), 0, ctx->stream, ctx->T, P);
+    }
     const int pairs = int(kFlowKeys * uint64_t(m));
     size_t bytes = 0;
     HIP_TRY(ctx, hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, F.keys, F.keys_sorted, F.vals,
@@ -412,15 +437,14 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
     rc = select_flagged(ctx, F.barrier8, m, F.barriers, &F.counts[1]);
     if (!rc) rc = select_flagged(ctx, F.ready8, m, F.queue, &F.counts[2]);
     if (rc) return rc;
-    hipLaunchKernelGGL(flow_queue_init, dim3(grid_for(m)), block, 0, ctx->stream, P);
+    hipLaunchKernelGGL(flow_queue_init, dim3(grid_for(std::max<uint64_t>(m, kFlowEngineWords))), block, 0, ctx->stream, P);
     if (post_void) {
         HIP_TRY(ctx, hipMemsetAsync(F.pnt_ops, 0, uint64_t(m) * 8, ctx->stream));
         HIP_TRY(ctx, hipMemsetAsync(F.pnt_fired, 0, 8, ctx->stream));
     }
     // Calls of limit events only: the account lanes (lanes.hpp); the flow replay then skips.
     P.skip = nullptr;
-    if (!(call_flags & (kFlagDuplicate | kFlagPostVoid | kFlagClosable | kFlagImported)) &&
-        !c.force_replay && !getenv("TBG_NO_LANES")) {
+    if (lanes_possible) {
         LanePlan L{};
         L.m = m;
         L.keys_sorted = F.keys_sorted;
@@ -461,9 +485,22 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
         HIP_TRY(ctx, hipMemsetAsync(ctx->flow_debug, 0, 128, ctx->stream));
         P.debug = ctx->flow_debug;
     }
-    uint32_t lanes = kFlowThreads;
-    { const char* e = getenv("TBG_FLOW_LANES"); if (e) lanes = std::max(64, std::min(int(kFlowThreads), atoi(e))); }
-    hipLaunchKernelGGL(flow_replay, dim3(1), dim3(lanes), 0, ctx->stream, ctx->T, c, P);
+    // Engine shape (flow.hpp): lanes per wave x waves per workgroup x workgroups; TBG_FLOW_XCD=8
+    // packs the running workgroups onto one XCD. Default (config 4 sweep, profiles/r01_fsweep):
+    // one lane per wave, 4 waves x 128 workgroups over the whole chip.
+    auto env_u = [](const char* name, uint32_t def, uint32_t lo, uint32_t hi) {
+        const char* e = getenv(name);
+        const uint32_t v = e ? uint32_t(atoi(e)) : def;
+        return std::max(lo, std::min(hi, v));
+    };
+    P.lanes_per_wave = env_u("TBG_FLOW_LPW", kFlowLanesPerWave, 1, 64);
+    const uint32_t waves = env_u("TBG_FLOW_WAVES", kFlowWaves, 1, kFlowThreads / 64);
+    const uint32_t blocks = env_u("TBG_FLOW_BLOCKS", kFlowBlocks, 1,
+                                  kFlowLanesMax / (waves * P.lanes_per_wave));
+    P.xcd_stride = env_u("TBG_FLOW_XCD", 1, 1, 8);
+    const uint32_t lanes = blocks * waves * P.lanes_per_wave;
+    hipLaunchKernelGGL(flow_replay, dim3(blocks * P.xcd_stride), dim3(waves * 64), 0, ctx->stream,
+                       ctx->T, c, P);
     tmark(ctx, "tr_flow");
     if (debug) {
         unsigned int cnt[2] = {0, 0};
@@ -750,7 +787,7 @@ void tbg_close(tbg_ctx* ctx) {
                     ctx->pulse.keep, ctx->pulse.exp, ctx->pulse.ts, ctx->pulse.rows,
                     ctx->pulse.exp_b, ctx->pulse.rows_b, ctx->pulse.counters,
                     ctx->flow.dup_mark, ctx->flow.counts, ctx->flow.pnt_fired, ctx->flow.lane_counts,
-                    ctx->flow.lane_undo};
+                    ctx->flow.lane_undo, ctx->flow.engine};
     free_flow(ctx->flow);
     for (void* p : ptrs)
         if (p) (void)hipFree(p);

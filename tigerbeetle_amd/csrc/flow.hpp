@@ -17,6 +17,8 @@
 //     pending row's, or the in-call creator's event's. When that creator is not certain (the
 //     pending id has several in-call claimants, or is not found at planning in a call with
 //     duplicate ids) the unit becomes a barrier.
+//     Additive accounts (no replayed event reads their balances or changes their `closed` flag,
+//     Replay::additive) get no key: their deltas are u128 atomics, which commute.
 // Account existence, ledgers and every FAST delta are fixed before the replay, so
 // these keys are the whole in-call state a replayed event depends on, apart from three scalars
 // handled in Replay (replay.hpp: key_range, pulse_next_timestamp, the expires_at list).
@@ -28,21 +30,27 @@
 // run: the replay always progresses and every lane reaches the exit. A barrier unit runs alone:
 // every earlier unit has finished and no later unit starts until it has.
 //
-// The engine is one workgroup: all its lanes share one CU's L1, so workgroup-scope release/acquire
-// orders a unit's writes before its successors' reads without cache maintenance.
+// The engine's lanes may sit on many CUs: a unit's writes are released (agent scope) before its
+// successors learn that it finished, and acquired by the lane that runs a successor.
 #pragma once
 
 #include "kernels.hpp"
 
 namespace tbg {
 
-constexpr uint32_t kFlowThreads = 512;      // lanes of the engine workgroup
+constexpr uint32_t kFlowThreads = 512;      // threads of an engine workgroup
+constexpr uint32_t kFlowLanesMax = 2048;    // lanes running units, over all engine workgroups
+constexpr uint32_t kFlowLanesPerWave = 1;   // default engine shape (TBG_FLOW_LPW / _WAVES / _BLOCKS)
+constexpr uint32_t kFlowWaves = 4;
+constexpr uint32_t kFlowBlocks = 128;
+constexpr uint32_t kFlowDoneShards = 16;    // units_done counter shards (one line each)
+constexpr uint32_t kFlowEngineWords = 64 + 32 * kFlowDoneShards;
 constexpr uint32_t kFlowChainMax = 256;     // longer chains run as barriers (global undo log)
 constexpr uint32_t kFlowUndoPerLane = 3 * kFlowChainMax;  // 2 accounts + 1 status per event
 constexpr uint32_t kFlowKeys = 4;           // keys per event
 constexpr uint64_t kFlowNoKey = ~0ull;
 constexpr uint32_t kFlowUnitBits = 31;
-constexpr uint64_t kFlowSpinLimit = 1ull << 21;  // idle polls while no unit finishes anywhere
+constexpr uint64_t kFlowSpinLimit = 1ull << 18;  // idle polls / 8 while no unit finishes anywhere
 
 struct FlowPlan {
     uint32_t m;                  // replayed events (the replay list's length)
@@ -69,6 +77,13 @@ struct FlowPlan {
     UndoEntry* lane_undo;        // kFlowUndoPerLane per lane
     struct Step* steps;          // per position: what the engine prefetches before it waits
     const unsigned int* skip;    // nonzero: the account lanes replayed the call (lanes.hpp)
+    uint32_t* exp_flag;          // per position: may append to the expires_at index
+    uint32_t* exp_index;         // exclusive prefix sum of exp_flag
+    uint32_t add_epoch;          // nonzero: additive accounts get no key (Replay::additive)
+    unsigned int* engine;        // [0] q_head, [32] q_tail, [64 + 32 j] units_done shard j
+                                 // (kFlowDoneShards; one 128-byte line each)
+    uint32_t lanes_per_wave;     // lanes of each engine wave that run units
+    uint32_t xcd_stride;         // only workgroups blockIdx % xcd_stride == 0 run
     unsigned long long* debug;   // optional: [0] loop iterations, [1] events, [2] cycles executing,
                                  // [3] cycles of the engine (lane 0)
 };
@@ -133,6 +148,8 @@ __global__ void flow_keys(Tables T, Call<tb_transfer_t> c, FlowPlan P, unsigned 
     const uint32_t u = P.unit_of[s];
     const tb_transfer_t& t = c.events[k];
     uint64_t key[kFlowKeys] = {kFlowNoKey, kFlowNoKey, kFlowNoKey, kFlowNoKey};
+    // Additive accounts need no ordering (Replay::additive, replay.hpp).
+    auto keyless = [&](uint64_t row) { return acc_additive(T, row, P.add_epoch); };
     if (!u128_is_zero(t.id) && !u128_is_max(t.id)) key[0] = flow_key(0, flow_id_key(t.id), u);
     if (t.flags & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) {
         if (!u128_is_zero(t.pending_id) && !u128_is_max(t.pending_id)) {
@@ -160,15 +177,20 @@ __global__ void flow_keys(Tables T, Call<tb_transfer_t> c, FlowPlan P, unsigned 
             } else if (p) {
                 const uint64_t dr = account_find(T, p->debit_account_id);
                 const uint64_t cr = account_find(T, p->credit_account_id);
-                if (dr != kNone) key[2] = flow_key(1, uint32_t(dr), u);
-                if (cr != kNone) key[3] = flow_key(1, uint32_t(cr), u);
+                if (dr != kNone && !keyless(dr)) key[2] = flow_key(1, uint32_t(dr), u);
+                if (cr != kNone && !keyless(cr)) key[3] = flow_key(1, uint32_t(cr), u);
             }
         }
     } else {
         const uint32_t dr = c.ev_dr[k], cr = c.ev_cr[k];
-        if (dr != kNone32) key[2] = flow_key(1, dr, u);
-        if (cr != kNone32) key[3] = flow_key(1, cr, u);
+        if (dr != kNone32 && !keyless(dr)) key[2] = flow_key(1, dr, u);
+        if (cr != kNone32 && !keyless(cr)) key[3] = flow_key(1, cr, u);
     }
+    // The expires_at entry a created pending transfer with a timeout appends (planned here: one
+    // slot per candidate position; a candidate that fails or whose chain is discarded leaves an
+    // entry of a row that is not live, dropped at the next pulse).
+    P.exp_flag[s] = (t.flags & TB_TRANSFER_PENDING) && t.timeout > 0 &&
+                    !(t.flags & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING));
     const StepInfo si = step_info(c, k, uint16_t(TB_TRANSFER_IMPORTED));
     const EvRefs x = ev_refs(c, k);
     Step st;
@@ -185,6 +207,20 @@ __global__ void flow_keys(Tables T, Call<tb_transfer_t> c, FlowPlan P, unsigned 
         P.keys[kFlowKeys * uint64_t(s) + j] = key[j];
         P.vals[kFlowKeys * uint64_t(s) + j] = kFlowKeys * s + j;
     }
+}
+
+// The planned expires_at entries (flow_keys): candidate s takes slot expiry_count + exp_index[s].
+__global__ void flow_expiry(Tables T, Call<tb_transfer_t> c, FlowPlan P) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= P.m || !P.exp_flag[s]) return;
+    const uint64_t i = T.scalars->expiry_count + P.exp_index[s];
+    if (i < T.expiry_capacity) T.expiry[i] = c.row_base + P.slow_list[s];
+    else atomicOr(&T.scalars->flags, kFlagTableFull);
+}
+__global__ void flow_expiry_count(Tables T, FlowPlan P) {
+    if (threadIdx.x != 0 || blockIdx.x != 0 || P.m == 0) return;
+    const uint64_t n = T.scalars->expiry_count + P.exp_index[P.m - 1] + P.exp_flag[P.m - 1];
+    T.scalars->expiry_count = n < T.expiry_capacity ? n : T.expiry_capacity;
 }
 
 // The edges of the unit graph, from the (key, unit) pairs in key order: a pair whose previous
@@ -224,11 +260,12 @@ __global__ void flow_ready(FlowPlan P) {
 // rest of the queue empty.
 __global__ void flow_queue_init(FlowPlan P) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < kFlowEngineWords) P.engine[i] = i == 32 ? P.counts[2] : 0;  // q_head, q_tail, done
     if (i >= P.counts[0]) return;
     P.queue[i] = i < P.counts[2] ? P.queue[i] + 1 : 0;
 }
 
-// The engine: one workgroup of kFlowThreads lanes (see the header). A unit is ready once every
+// The engine: lanes spread over `blocks` workgroups (see the header). A unit is ready once every
 // predecessor has finished (indeg 0). Ready units wait in a queue; a lane pops one, runs it, and
 // releases its successors -- the first that becomes ready it runs itself next (so a chain of units
 // on one hot key stays on one lane, its rows warm in that CU's L1), the others it pushes. Each
@@ -236,26 +273,39 @@ __global__ void flow_queue_init(FlowPlan P) {
 // earliest unfinished unit's predecessors have all finished, so it is ready or running: the
 // replay progresses, and lanes leave when the queue is drained and every unit has finished.
 // With a barrier unit in the call, lane 0 replays every unit in order (serial semantics).
+//
+// Lanes. Only `lanes_per_wave` lanes of each wave run units: the replay of one event is a long
+// branchy walk of dependent memory round trips, and lanes of one wave in different branches take
+// turns, so a unit's latency grows with the busy lanes of its wave. With `xcd_stride` 8 only every
+// 8th workgroup runs (workgroups are dealt round-robin over the 8 XCDs): the engine shares one L2.
+// Measured on config 4: one lane per wave over the whole chip halves the replay's time against one
+// workgroup of 512 busy lanes (116 -> 56 ms per 300k events); packing onto one XCD loses.
+//
+// Hand-offs between lanes on different CUs follow the agent-scope model (MI355X_MICROARCH.md,
+// inter-workgroup visibility): a finishing unit runs one release fence (L2 write-back) before its
+// relaxed decrements of its successors' indeg; a lane that takes a unit -- from its own decrement
+// or from a relaxed poll of the queue -- runs one acquire fence (L1 invalidate) before it reads
+// anything another unit wrote. The queue counters live in global memory (P.engine).
 __global__ void __launch_bounds__(kFlowThreads) flow_replay(Tables T, Call<tb_transfer_t> c,
                                                            FlowPlan P) {
-    __shared__ unsigned int q_head, q_tail, units_done;
     if (P.skip && *P.skip) return;
+    if (blockIdx.x % P.xcd_stride) return;
+    const uint32_t block = blockIdx.x / P.xcd_stride;
     const uint32_t tid = threadIdx.x;
+    const uint32_t wave_lane = tid & 63;
+    const uint32_t lane = (block * (blockDim.x >> 6) + (tid >> 6)) * P.lanes_per_wave + wave_lane;
     const uint32_t units = P.counts[0];
-    if (tid == 0) {
-        q_head = 0;
-        q_tail = P.counts[2];
-        units_done = 0;
-    }
-    __syncthreads();
+    unsigned int* q_head = P.engine;
+    unsigned int* q_tail = P.engine + 32;
     const uint64_t t_start = wall_clock64();
     uint64_t it_count = 0, ev_count = 0, exec_cycles = 0, conts = 0;
     bool chain_open = false, chain_broken = false;
     uint32_t chain_start = 0;
 
     if (P.counts[1] != 0) {  // barrier units: the serial replay, on one lane
-        if (tid == 0) {
+        if (block == 0 && tid == 0) {
             Replay R(T);
+            R.expiry_planned = true;
             for (uint32_t s = 0; s < P.m; s++) {
                 replay_chain_step<tb_transfer_t>(R, c, P.slow_list[s], true, chain_open,
                                                  chain_start, chain_broken);
@@ -272,8 +322,12 @@ __global__ void __launch_bounds__(kFlowThreads) flow_replay(Tables T, Call<tb_tr
     Replay R(T);
     R.concurrent = true;
     R.pnt_ops = P.pnt_ops;
-    R.undo = P.lane_undo + uint64_t(tid) * kFlowUndoPerLane;
+    R.undo = P.lane_undo + uint64_t(lane) * kFlowUndoPerLane;
     R.undo_cap = kFlowUndoPerLane;
+    R.add_epoch = P.add_epoch;
+    R.expiry_planned = true;
+    uint64_t lane_key_max = 0;
+    unsigned int* done_shard = P.engine + 64 + 32 * (lane % kFlowDoneShards);
 
     // Runs unit u; releases its successors; returns the one this lane runs next (or kNone32).
     auto run_unit = [&](uint32_t u) -> uint32_t {
@@ -301,9 +355,14 @@ __global__ void __launch_bounds__(kFlowThreads) flow_replay(Tables T, Call<tb_tr
             exec_cycles += wall_clock64() - t0;
             ev_count += end - begin;
         }
-        if (R.key_max) atomicMax(&T.scalars->transfers_key_max, (unsigned long long)R.key_max);
-        // Release the successors (acq_rel: a successor's runner sees every predecessor's writes).
+        // (transfers key_max: read only by imported events, which never take the flow replay;
+        // each lane folds its maximum in at the exit.)
+        if (R.key_max > lane_key_max) lane_key_max = R.key_max;
+        // Release: this unit's writes reach the point of coherence before any decrement.
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         uint32_t next = kNone32;
+        bool pushed = false;
         for (uint32_t s = begin; s < end; s++) {
             const uint4 sc = *reinterpret_cast<const uint4*>(P.succ + kFlowKeys * uint64_t(s));
             const uint32_t vs[kFlowKeys] = {sc.x, sc.y, sc.z, sc.w};
@@ -312,49 +371,61 @@ __global__ void __launch_bounds__(kFlowThreads) flow_replay(Tables T, Call<tb_tr
                 const uint32_t v = vs[q];
                 if (v == kNone32) continue;
                 const uint32_t old = __hip_atomic_fetch_add(&P.indeg[v], 0xFFFFFFFFu,
-                                                            __ATOMIC_ACQ_REL,
-                                                            __HIP_MEMORY_SCOPE_WORKGROUP);
+                                                            __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_AGENT);
                 if (old != 1) continue;
                 if (next == kNone32) {
+                    // Acquire what every other predecessor of v released.
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     next = v;
                 } else {
-                    const uint32_t slot = atomicAdd(&q_tail, 1u);
-                    __hip_atomic_store(&P.queue[slot], v + 1, __ATOMIC_RELEASE,
-                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (!pushed) {
+                        // Pass the acquired writes on to the lanes that pop the pushed units.
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        pushed = true;
+                    }
+                    const uint32_t slot = atomicAdd(q_tail, 1u);
+                    __hip_atomic_store(&P.queue[slot], v + 1, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
         }
-        __hip_atomic_fetch_add(&units_done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add(done_shard, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         conts += next != kNone32;
         return next;
     };
     uint32_t u = kNone32;
     uint64_t spins = 0;
-    uint32_t last_seen = 0;
-    uint32_t pos = atomicAdd(&q_head, 1u);
+    uint32_t last_seen = 0, polls = 0;
+    bool alive = wave_lane < P.lanes_per_wave;
+    uint32_t pos = alive ? atomicAdd(q_head, 1u) : 0;
     // The loop's exit is wave-uniform (a vote): inside it every lane only takes if/else paths, so
     // a waiting lane and a running lane of the same wave share every iteration. (With per-lane
     // exits the compiler may form an inner loop of the waiting lanes that the running lanes of the
     // wave only re-enter once every waiter has left it -- a waiter that needs a unit of its own
     // wave would never leave.)
-    bool alive = true;
     while (__any(alive)) {
         if (alive && u == kNone32) {
             // Pop: the queue entry at `pos`, or leave once every unit has finished.
             if (pos >= units) {
                 alive = false;
             } else {
-                // (An atomic read: it is served by L2, never by a line this CU's L1 kept.)
-                const uint32_t w = __hip_atomic_fetch_or(&P.queue[pos], 0u, __ATOMIC_ACQUIRE,
-                                                         __HIP_MEMORY_SCOPE_WORKGROUP);
+                const uint32_t w = __hip_atomic_load(&P.queue[pos], __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
                 it_count++;
                 if (w != 0) {
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     u = w - 1;
-                    pos = atomicAdd(&q_head, 1u);
+                    pos = atomicAdd(q_head, 1u);
                     spins = 0;
-                } else {
-                    const uint32_t seen = __hip_atomic_load(&units_done, __ATOMIC_RELAXED,
-                                                            __HIP_MEMORY_SCOPE_WORKGROUP);
+                } else if ((++polls & 7) == 0) {  // the shards' sum, every 8th idle poll
+                    uint32_t seen = 0;
+                    for (uint32_t j = 0; j < kFlowDoneShards; j++)
+                        seen += __hip_atomic_load(P.engine + 64 + 32 * j, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
                     if (seen != last_seen) {
                         last_seen = seen;
                         spins = 0;
@@ -366,8 +437,8 @@ __global__ void __launch_bounds__(kFlowThreads) flow_replay(Tables T, Call<tb_tr
                         // (the call fails) instead of holding the GPU.
                         atomicOr(&T.scalars->flags, kFlagFlowStalled);
                         if (P.debug) {
-                            P.debug[8] = q_head;
-                            P.debug[9] = q_tail;
+                            P.debug[8] = *q_head;
+                            P.debug[9] = *q_tail;
                             P.debug[10] = seen;
                             P.debug[11] = pos;
                         }
@@ -379,6 +450,8 @@ __global__ void __launch_bounds__(kFlowThreads) flow_replay(Tables T, Call<tb_tr
         if (alive && u != kNone32) u = run_unit(u);
         else if (alive) __builtin_amdgcn_s_sleep(1);
     }
+    if (lane_key_max)
+        atomicMax(&T.scalars->transfers_key_max, (unsigned long long)lane_key_max);
     if (P.debug) {
         atomicAdd(&P.debug[0], (unsigned long long)it_count);
         atomicAdd(&P.debug[1], (unsigned long long)ev_count);
@@ -386,7 +459,7 @@ __global__ void __launch_bounds__(kFlowThreads) flow_replay(Tables T, Call<tb_tr
         atomicAdd(&P.debug[4], (unsigned long long)conts);
     }
     __syncthreads();
-    if (tid == 0) {
+    if (block == 0 && tid == 0) {
         T.scalars->stats[2] = P.m;
         if (P.debug) P.debug[3] = wall_clock64() - t_start;
     }

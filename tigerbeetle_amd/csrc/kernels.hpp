@@ -317,11 +317,20 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
             if (ps != kNone) {
                 const uint64_t pr = (T.tr.slots[ps] & kRefMask) - 1;
                 const tb_transfer_t& p = pr >= base ? ev[pr - base] : rows[pr];
-                const uint64_t pd_row = account_find(T, p.debit_account_id);
-                const uint64_t pc_row = account_find(T, p.credit_account_id);
-                if (pd_row != kNone) T.acc_closable[pd_row] = c.epoch;
-                if (pc_row != kNone) T.acc_closable[pc_row] = c.epoch;
-                closable = true;
+                // A void un-closes only the accounts of a closing pending transfer (:4253-4262).
+                // (With duplicate ids the holder found here may not be the final one; an in-call
+                // closing creator marks its own accounts above.)
+                const uint16_t pf = p.flags;
+                if (pf & TB_TRANSFER_CLOSING_DEBIT) {
+                    const uint64_t pd_row = account_find(T, p.debit_account_id);
+                    if (pd_row != kNone) T.acc_closable[pd_row] = c.epoch;
+                    closable = true;
+                }
+                if (pf & TB_TRANSFER_CLOSING_CREDIT) {
+                    const uint64_t pc_row = account_find(T, p.credit_account_id);
+                    if (pc_row != kNone) T.acc_closable[pc_row] = c.epoch;
+                    closable = true;
+                }
             }
         }
         if (!chain && !c.force_replay && !imported && slot != kNone) {

@@ -59,6 +59,7 @@ struct UndoEntry {
 };
 constexpr uint64_t kUndoAccount = 1ull << 56;
 constexpr uint64_t kUndoStatus = 2ull << 56;
+constexpr uint64_t kUndoDelta = 3ull << 56;   // balance deltas added atomically (row's 4 fields)
 constexpr uint64_t kUndoIndexMask = (1ull << 56) - 1;
 
 // Everything a kernel needs, passed by value.
@@ -206,6 +207,14 @@ __device__ inline uint64_t account_find(const Tables& T, const tb_uint128_t& id)
     return e.ref - 1;
 }
 
+// An additive account of the call with this epoch (0: none; Replay::additive). Accounts with a
+// limit flag are never additive: the account lanes' plan (lanes.hpp) lists their events by key.
+__device__ inline bool acc_additive(const Tables& T, uint64_t row, uint32_t epoch) {
+    return epoch != 0 && T.acc_hot[row] != epoch && T.acc_closable[row] != epoch &&
+           !(T.acc_rows[row].flags & (TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS |
+                                      TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS));
+}
+
 // ---- the replay state -------------------------------------------------------------------------
 
 struct Scope {
@@ -237,6 +246,8 @@ struct Replay {
     uint64_t* pnt_ops = nullptr;  // per replay position: 0, expires_at (min) or | kPntReset
     uint32_t pos = 0;             // replay position of the executing event
     uint64_t key_max = 0, key_max_scope = 0;
+    uint32_t add_epoch = 0;       // nonzero: additive accounts of this call (additive())
+    bool expiry_planned = false;  // the flow plan wrote this call's expires_at entries
 
     __device__ explicit Replay(const Tables& t) : T(t), undo(t.undo), undo_cap(t.undo_capacity) {}
 
@@ -256,8 +267,19 @@ struct Replay {
             for (uint64_t i = undo_len; i-- > scope.undo_len;) {
                 const UndoEntry& u = undo[i];
                 uint64_t idx = u.kind_index & kUndoIndexMask;
-                if ((u.kind_index & ~kUndoIndexMask) == kUndoAccount) {
+                const uint64_t kind = u.kind_index & ~kUndoIndexMask;
+                if (kind == kUndoAccount) {
                     copy_row(&T.acc_rows[idx], &u.row);
+                } else if (kind == kUndoDelta) {
+                    tb_account_t& a = T.acc_rows[idx];
+                    if (!u128_is_zero(u.row.debits_pending))
+                        atomic_add_u128(&a.debits_pending, u128(0) - U(u.row.debits_pending));
+                    if (!u128_is_zero(u.row.debits_posted))
+                        atomic_add_u128(&a.debits_posted, u128(0) - U(u.row.debits_posted));
+                    if (!u128_is_zero(u.row.credits_pending))
+                        atomic_add_u128(&a.credits_pending, u128(0) - U(u.row.credits_pending));
+                    if (!u128_is_zero(u.row.credits_posted))
+                        atomic_add_u128(&a.credits_posted, u128(0) - U(u.row.credits_posted));
                 } else {
                     T.tr_status[idx] = (uint8_t)u.row.timestamp;
                 }
@@ -300,6 +322,36 @@ struct Replay {
         // A rollback restores the row but keeps the hazard bits: they only over-approximate.
         const uint16_t h = acc_hazard_of(next);
         if (h) acc_hazard_set(T.acc_index, T.acc_entry_of, row, h);
+    }
+    // Additive accounts (flow mode, add_epoch != 0): accounts no replayed event of the call reads
+    // a balance of (no acc_hot mark: no limit flag on a checked side, no balancing, no possible
+    // overflow; and no limit flag at all) and whose `closed` flag no event of the call changes (no
+    // acc_closable mark). A
+    // replayed event's outcome does not depend on their balances, and its effect on them is a sum,
+    // so the flow plan gives them no account key (flow_keys) and the replay adds its deltas with
+    // u128 atomics, logged as deltas for a chain's rollback.
+    __device__ bool additive(uint64_t row) const { return acc_additive(T, row, add_epoch); }
+    // Adds the four (modular) deltas to the row's debits_pending, debits_posted, credits_pending,
+    // credits_posted.
+    __device__ void add_balances(uint64_t row, u128 d_dpe, u128 d_dpo, u128 d_cpe, u128 d_cpo) {
+        tb_account_t& a = T.acc_rows[row];
+        uint64_t hi = 0;
+        if (d_dpe) hi |= atomic_add_u128(&a.debits_pending, d_dpe);
+        if (d_dpo) hi |= atomic_add_u128(&a.debits_posted, d_dpo);
+        if (d_cpe) hi |= atomic_add_u128(&a.credits_pending, d_cpe);
+        if (d_cpo) hi |= atomic_add_u128(&a.credits_posted, d_cpo);
+        if (hi >= kHazardHiLimit) acc_hazard_set(T.acc_index, T.acc_entry_of, row, kHazardHigh);
+        if (!scope.open) return;
+        if (undo_len >= undo_cap) {
+            overflow = true;
+            return;
+        }
+        UndoEntry& u = undo[undo_len++];
+        u.kind_index = kUndoDelta | row;
+        u.row.debits_pending = W(d_dpe);
+        u.row.debits_posted = W(d_dpo);
+        u.row.credits_pending = W(d_cpe);
+        u.row.credits_posted = W(d_cpo);
     }
     __device__ void update_status(uint64_t row, uint8_t status) {
         log_status(row);
@@ -552,8 +604,17 @@ __device__ uint32_t replay_post_or_void(Replay& R, const C& c, uint32_t k, uint6
         if (p.flags & TB_TRANSFER_CLOSING_DEBIT) dr_new.flags &= (uint16_t)~TB_ACCOUNT_CLOSED;
         if (p.flags & TB_TRANSFER_CLOSING_CREDIT) cr_new.flags &= (uint16_t)~TB_ACCOUNT_CLOSED;
     }
-    if (amount > 0 || p_amount > 0 || dr_new.flags != dr.flags) R.update_account(dr_row, dr_new);
-    if (amount > 0 || p_amount > 0 || cr_new.flags != cr.flags) R.update_account(cr_row, cr_new);
+    const u128 posted = (f & TB_TRANSFER_POST_PENDING) ? amount : u128(0);
+    if (R.additive(dr_row)) {  // (flags unchanged: a void of a closing transfer marks closable)
+        R.add_balances(dr_row, u128(0) - p_amount, posted, 0, 0);
+    } else if (amount > 0 || p_amount > 0 || dr_new.flags != dr.flags) {
+        R.update_account(dr_row, dr_new);
+    }
+    if (R.additive(cr_row)) {
+        R.add_balances(cr_row, 0, 0, u128(0) - p_amount, posted);
+    } else if (amount > 0 || p_amount > 0 || cr_new.flags != cr.flags) {
+        R.update_account(cr_row, cr_new);
+    }
     *ts_out = ts_actual;
     return TB_STATUS_CREATED;
 }
@@ -666,7 +727,8 @@ __device__ uint32_t replay_create_transfer(Replay& R, const C& c, uint32_t k, ui
     T.tr_rows[row] = o;
     T.tr_status[row] = (f & TB_TRANSFER_PENDING) ? TB_PENDING_PENDING : TB_PENDING_NONE;
     R.note_transfer_ts(ts_actual);
-    if ((f & TB_TRANSFER_PENDING) && t.timeout > 0) expiry_append(T, row, !R.concurrent);
+    if ((f & TB_TRANSFER_PENDING) && t.timeout > 0 && !R.expiry_planned)
+        expiry_append(T, row, !R.concurrent);
 
     tb_account_t dr_new = dr, cr_new = cr;
     if (f & TB_TRANSFER_PENDING) {
@@ -678,8 +740,17 @@ __device__ uint32_t replay_create_transfer(Replay& R, const C& c, uint32_t k, ui
     }
     if (f & TB_TRANSFER_CLOSING_DEBIT) dr_new.flags |= TB_ACCOUNT_CLOSED;
     if (f & TB_TRANSFER_CLOSING_CREDIT) cr_new.flags |= TB_ACCOUNT_CLOSED;
-    if (amount > 0 || (dr_new.flags & TB_ACCOUNT_CLOSED)) R.update_account(dr_row, dr_new);
-    if (amount > 0 || (cr_new.flags & TB_ACCOUNT_CLOSED)) R.update_account(cr_row, cr_new);
+    const bool pend = (f & TB_TRANSFER_PENDING) != 0;
+    if (R.additive(dr_row)) {  // (not closing: a closing transfer marks closable)
+        R.add_balances(dr_row, pend ? amount : 0, pend ? 0 : amount, 0, 0);
+    } else if (amount > 0 || (dr_new.flags & TB_ACCOUNT_CLOSED)) {
+        R.update_account(dr_row, dr_new);
+    }
+    if (R.additive(cr_row)) {
+        R.add_balances(cr_row, 0, 0, pend ? amount : 0, pend ? 0 : amount);
+    } else if (amount > 0 || (cr_new.flags & TB_ACCOUNT_CLOSED)) {
+        R.update_account(cr_row, cr_new);
+    }
 
     if (t.timeout > 0) R.pulse_min(ts_actual + (uint64_t)t.timeout * TB_NS_PER_S);
     *ts_out = ts_actual;
