@@ -66,6 +66,27 @@ struct LanePlan {
     unsigned int* counts;     // [0] owners, [1] ineligible events, [2] handled (set by the engine)
 };
 
+// The rings' loads are inline asm, so the compiler inserts no wait for them: its wait analysis
+// cannot see that a lane consumes slot q only after the other kAhead - 1 slots (the dispatch on
+// `phase`), and would wait for (nearly) every outstanding load at each step. The step waits
+// instead with vmcnt(kWaitNewer): when slot q is consumed, at least kWaitNewer vector-memory ops
+// were issued after its record load and after the pair load that follows it -- steady state 3 per
+// other step (outcome store, record load, pair load) = 21 and 22; the first round at least 14
+// (the initial fill issues a record and a pair load per slot after one vmcnt(0)). vmcnt counts
+// loads and stores in issue order on CDNA. The asm outputs are consumed only after that wait.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr int kWaitNewer = 14;
+__device__ inline u32x4 lane_load16(const void* p) {
+    u32x4 r;
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(p) : "memory");
+    return r;
+}
+__device__ inline uint64_t lane_load8(const void* p) {
+    uint64_t r;
+    asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(r) : "v"(p) : "memory");
+    return r;
+}
+
 __device__ inline bool lanes_owner(uint16_t flags) {
     return (flags & (TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS |
                      TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS)) != 0;
@@ -168,7 +189,8 @@ __global__ void __launch_bounds__(kLanesMax) lanes_replay(Tables T, Call<tb_tran
     // that name them kAhead further (a step is register arithmetic; neither load chain may be its
     // latency).
     constexpr uint32_t kAhead = 8;
-    LaneRec ring[kAhead];
+    static_assert(kWaitNewer == 2 * (kAhead - 1), "the rings' wait count (lane_load16)");
+    u32x4 ring[kAhead];  // raw LaneRecs (lane_load16)
     bool ring_ok[kAhead];
     uint32_t ring_s[kAhead];
     uint64_t pre_key[kAhead];  // the (key, unit) pairs of the following kAhead steps, raw
@@ -176,95 +198,111 @@ __global__ void __launch_bounds__(kLanesMax) lanes_replay(Tables T, Call<tb_tran
     // Every load and store of the steady-state step is unconditional (a clamped index, a dummy
     // slot) and no loaded value is used before kAhead steps later: the wait counters then keep
     // the rings in flight instead of draining them every step.
-    auto fetch_pair = [&](uint32_t slot) {
+    bool pre_valid[kAhead];
+    auto fetch_pair = [&](uint32_t slot) {  // (an unconditional load: no select waits for it)
         const uint64_t at = fetch_idx < L.n_pairs ? fetch_idx : L.n_pairs - 1;
-        pre_key[slot] = fetch_idx < L.n_pairs ? L.keys_sorted[at] : kFlowNoKey;
+        pre_valid[slot] = fetch_idx < L.n_pairs;
+        pre_key[slot] = lane_load8(&L.keys_sorted[at]);
         fetch_idx++;
     };
     auto take_pair = [&](uint32_t slot) {  // pre_key[slot] -> ring[slot]'s record load
         const uint64_t key = pre_key[slot];
         const uint32_t ps = uint32_t(key & ((1u << kFlowUnitBits) - 1));
-        return std::pair<bool, uint32_t>((key >> kFlowUnitBits) == my_key, ps < L.m ? ps : 0u);
+        return std::pair<bool, uint32_t>(pre_valid[slot] && (key >> kFlowUnitBits) == my_key,
+                                         ps < L.m ? ps : 0u);
     };
 #pragma unroll
     for (uint32_t q = 0; q < kAhead; q++) fetch_pair(q);
+#pragma unroll
+    for (uint32_t q = 0; q < kAhead; q++) asm volatile("s_waitcnt vmcnt(0)" : "+v"(pre_key[q]) :: "memory");
 #pragma unroll
     for (uint32_t q = 0; q < kAhead; q++) {
         const auto t = take_pair(q);
         ring_ok[q] = t.first;
         ring_s[q] = t.second;
-        ring[q] = L.recs[ring_s[q]];
+        ring[q] = lane_load16(&L.recs[ring_s[q]]);
         fetch_pair(q);
     }
     alive = alive && ring_ok[0];
     uint64_t spins = 0;
+    // The ring is consumed in place: slot q holds the record of every step t with t % kAhead == q,
+    // and the loop body is unrolled over the slots (constant indices keep the rings in registers).
+    // Moving ring entries instead would wait for every outstanding load at each step.
+    uint32_t phase = 0;  // the slot of this lane's current step
     while (__any(alive)) {
         if (alive && ++spins > kFlowSpinLimit) {  // watchdog (a bug): fail the call
             atomicOr(&T.scalars->flags, kFlagFlowStalled);
             alive = false;
         }
-        if (alive) {
-            const LaneRec rec = ring[0];
-            const uint32_t s = ring_s[0];
-            const bool debit = rec.dr == row;
-            const bool decides_dr = (rec.bits & kLaneDrDecides) != 0;
-            const bool decides_cr = (rec.bits & kLaneCrDecides) != 0;
-            const bool mine = debit ? decides_dr : decides_cr;     // this lane's limit is checked
-            const bool other = debit ? decides_cr : decides_dr;    // the other owner's is
-            const bool other_owner = (rec.bits & (debit ? kLaneCrOwner : kLaneDrOwner)) != 0;
-            const u128 amount = rec.amount;
-            bool my_ok = true;
-            if (mine) my_ok = debit ? !(dpe + dpo + amount > cpo) : !(cpe + cpo + amount > dpo);
-            // Verdicts between two owners go through LDS (4 bits per event whose two sides are
-            // owned): a memory round trip here would drain the record rings every step.
-            const uint32_t mbi = rec.bits >> kLaneMbShift;
-            const uint32_t mb_shift = (mbi & 7) * 4;
-            if (mine && other_owner && !published) {
-                // The other owner applies this event too: it needs the verdict.
-                atomicOr(&mbox[mbi >> 3], (debit ? (kMbDrSet | (my_ok ? kMbDrOk : 0u))
-                                                 : (kMbCrSet | (my_ok ? kMbCrOk : 0u)))
-                                              << mb_shift);
-            }
-            published = true;
-            const uint32_t mb = other ? (__hip_atomic_load(&mbox[mbi >> 3], __ATOMIC_ACQUIRE,
-                                                           __HIP_MEMORY_SCOPE_WORKGROUP) >>
-                                         mb_shift) & 15u
-                                      : 0u;
-            const bool known = !other || (mb & (debit ? kMbCrSet : kMbDrSet));
-            if (known) {
-                const bool other_ok = !other || (mb & (debit ? kMbCrOk : kMbDrOk));
-                const bool dr_fail = debit ? !my_ok : !other_ok;
-                const bool cr_fail = debit ? !other_ok : !my_ok;
-                const bool created = !dr_fail && !cr_fail;
-                if (created) {
-                    if (debit) dpo += amount;
-                    else cpo += amount;
-                }
-                const bool writer = debit || !(rec.bits & kLaneDrOwner);
-                // (non-writers store to their own dummy byte past the positions)
-                L.outcome[writer ? s : L.m + o] =
-                    created ? kOutCreated : (dr_fail ? kOutExceedsCredits : kOutExceedsDebits);
-                published = false;
-                spins = 0;
-                // Rotate (constant indices keep the rings in registers): the oldest prefetched pair
-                // becomes the newest record load, and one more pair load is issued.
 #pragma unroll
-                for (uint32_t q = 0; q + 1 < kAhead; q++) {
-                    ring[q] = ring[q + 1];
-                    ring_s[q] = ring_s[q + 1];
-                    ring_ok[q] = ring_ok[q + 1];
+        for (uint32_t q = 0; q < kAhead; q++) {
+            if (alive && phase == q) {
+                // Slot q's record and the pair after it are the oldest of at least kWaitNewer
+                // newer vector-memory ops (see lane_load16).
+                // (The registers are operands: no use of them is scheduled above the wait.)
+                asm volatile("s_waitcnt vmcnt(%2)"
+                             : "+v"(ring[q]), "+v"(pre_key[q])
+                             : "n"(kWaitNewer)
+                             : "memory");
+                LaneRec rec;
+                rec.amount = uint64_t(ring[q].x) | (uint64_t(ring[q].y) << 32);
+                rec.dr = ring[q].z;
+                rec.bits = ring[q].w;
+                const uint32_t s = ring_s[q];
+                const bool debit = rec.dr == row;
+                const bool decides_dr = (rec.bits & kLaneDrDecides) != 0;
+                const bool decides_cr = (rec.bits & kLaneCrDecides) != 0;
+                const bool mine = debit ? decides_dr : decides_cr;   // this lane's limit is checked
+                const bool other = debit ? decides_cr : decides_dr;  // the other owner's is
+                const bool other_owner = (rec.bits & (debit ? kLaneCrOwner : kLaneDrOwner)) != 0;
+                const u128 amount = rec.amount;
+                bool my_ok = true;
+                if (mine) my_ok = debit ? !(dpe + dpo + amount > cpo) : !(cpe + cpo + amount > dpo);
+                // Verdicts between two owners go through LDS (4 bits per event whose two sides are
+                // owned): a memory round trip here would stall the lane on every such event.
+                const uint32_t mbi = rec.bits >> kLaneMbShift;
+                const uint32_t mb_shift = (mbi & 7) * 4;
+                if (mine && other_owner && !published) {
+                    // The other owner applies this event too: it needs the verdict.
+                    atomicOr(&mbox[mbi >> 3], (debit ? (kMbDrSet | (my_ok ? kMbDrOk : 0u))
+                                                     : (kMbCrSet | (my_ok ? kMbCrOk : 0u)))
+                                                  << mb_shift);
                 }
-                const auto t = take_pair(0);
-                ring_ok[kAhead - 1] = t.first;
-                ring_s[kAhead - 1] = t.second;
-                ring[kAhead - 1] = L.recs[ring_s[kAhead - 1]];
-#pragma unroll
-                for (uint32_t q = 0; q + 1 < kAhead; q++) pre_key[q] = pre_key[q + 1];
-                fetch_pair(kAhead - 1);
-                alive = ring_ok[0];
+                published = true;
+                const uint32_t mb = other ? (__hip_atomic_load(&mbox[mbi >> 3], __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_WORKGROUP) >>
+                                             mb_shift) & 15u
+                                          : 0u;
+                const bool known = !other || (mb & (debit ? kMbCrSet : kMbDrSet));
+                if (known) {
+                    const bool other_ok = !other || (mb & (debit ? kMbCrOk : kMbDrOk));
+                    const bool dr_fail = debit ? !my_ok : !other_ok;
+                    const bool cr_fail = debit ? !other_ok : !my_ok;
+                    const bool created = !dr_fail && !cr_fail;
+                    if (created) {
+                        if (debit) dpo += amount;
+                        else cpo += amount;
+                    }
+                    const bool writer = debit || !(rec.bits & kLaneDrOwner);
+                    // (non-writers store to their own dummy byte past the positions)
+                    L.outcome[writer ? s : L.m + o] =
+                        created ? kOutCreated : (dr_fail ? kOutExceedsCredits : kOutExceedsDebits);
+                    published = false;
+                    spins = 0;
+                    // Refill the slot with the step kAhead later (its pair was loaded kAhead steps
+                    // ago) and load the pair of the step 2 * kAhead later.
+                    const auto t = take_pair(q);
+                    ring_ok[q] = t.first;
+                    ring_s[q] = t.second;
+                    ring[q] = lane_load16(&L.recs[ring_s[q]]);
+                    fetch_pair(q);
+                    phase = (q + 1) % kAhead;
+                    alive = ring_ok[(q + 1) % kAhead];
+                }
             }
         }
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the rings' last loads)
     if (o < owners) {
         tb_account_t& a = T.acc_rows[row];
         a.debits_posted = W(dpo);
