@@ -333,3 +333,64 @@ def test_account_lanes_limits(n_acc):
         p.compare_state()
     finally:
         p.close()
+
+@pytest.mark.parametrize("additive", [True, False], ids=["additive", "keyed"])
+def test_flow_additive_accounts(additive, monkeypatch):
+    """Plain accounts that no replayed event reads (Replay::additive, replay.hpp) take the flow
+    replay's deltas as u128 atomics without ordering keys: many concurrent units on the same few
+    accounts with amounts that carry into the high word, linked chains whose deltas are undone by
+    a later failure, posts (partial) and voids of non-closing pending transfers, a void of a
+    closing one (its accounts keyed), and a limited account in the mix -- against the oracle, with
+    and without the additive path (TBG_NO_ADDITIVE)."""
+    if not additive:
+        monkeypatch.setenv("TBG_NO_ADDITIVE", "1")
+    rng = np.random.default_rng(77)
+    p = Pair(account_capacity=64, transfer_capacity=1 << 14, batch_events_max=1 << 12,
+             force_replay=True)
+    try:
+        acc = workload.accounts(10, seed=7, ledger=1)
+        acc["flags"] = [0, 0, 0, 0, 0, 0, 0, 0, 2, 0]  # 9: debits_must_not_exceed_credits
+        p.create_accounts(acc)
+        big = (1 << 64) - 1
+        n = 300
+        first = []
+        for i in range(n):
+            dr, cr = rng.choice(8, size=2, replace=False) + 1
+            first.append(dict(id=1000 + i, debit_account_id=int(dr), credit_account_id=int(cr),
+                              amount=big - i, ledger=1, code=1, flags=2))  # pending
+        first.append(dict(id=5000, debit_account_id=10, credit_account_id=1, amount=9, ledger=1,
+                          code=1, flags=2 | 64))                           # pending closing_debit
+        first.append(dict(id=5001, debit_account_id=1, credit_account_id=9, amount=big, ledger=1,
+                          code=1))                                         # funds account 9
+        p.create_transfers(_transfers(first))
+        second = []
+        for i in range(n):
+            dr, cr = rng.choice(8, size=2, replace=False) + 1
+            kind = i % 5
+            if kind == 0:    # a chain whose last event fails: the first two deltas are undone
+                second += [dict(id=2000 + 10 * i, debit_account_id=int(dr), credit_account_id=int(cr),
+                                amount=big - 7, ledger=1, code=1, flags=1),
+                           dict(id=2001 + 10 * i, debit_account_id=int(cr), credit_account_id=int(dr),
+                                amount=big - 3, ledger=1, code=1, flags=1),
+                           dict(id=2002 + 10 * i, debit_account_id=int(dr), credit_account_id=99,
+                                amount=1, ledger=1, code=1)]
+            elif kind == 1:  # void (the pending transfer is not closing)
+                second.append(dict(id=2000 + 10 * i, pending_id=1000 + i, flags=8))
+            elif kind == 2:  # partial post
+                second.append(dict(id=2000 + 10 * i, pending_id=1000 + i, amount=big // 3, flags=4))
+            elif kind == 3:  # a chain that persists
+                second += [dict(id=2000 + 10 * i, debit_account_id=int(dr), credit_account_id=int(cr),
+                                amount=big, ledger=1, code=1, flags=1),
+                           dict(id=2001 + 10 * i, debit_account_id=int(cr), credit_account_id=int(dr),
+                                amount=5, ledger=1, code=1)]
+            else:            # the limited account debits
+                second.append(dict(id=2000 + 10 * i, debit_account_id=9, credit_account_id=int(cr),
+                                   amount=big // 50, ledger=1, code=1))
+        second.append(dict(id=6000, pending_id=5000, flags=8))  # void of a closing transfer
+        second.append(dict(id=6001, debit_account_id=10, credit_account_id=2, amount=1, ledger=1,
+                           code=1))                              # 10 reopened by the void
+        r = p.create_transfers(_transfers(second), [len(second)])
+        assert (r["status"] == 0xFFFFFFFF).sum() > n // 2
+        p.compare_state()
+    finally:
+        p.close()
