@@ -62,6 +62,8 @@ struct FlowScratch {
     UndoEntry* lane_undo = nullptr;
     unsigned int* engine = nullptr;  // flow engine queue counters
     uint32_t *exp_flag = nullptr, *exp_index = nullptr;
+    uint32_t* acc_free = nullptr;  // per account (lanes.hpp free owners)
+    u128 *contrib = nullptr, *prefix = nullptr;
 };
 
 }  // namespace
@@ -314,7 +316,7 @@ void free_flow(FlowScratch& F) {
     void* ptrs[] = {F.head8, F.barrier8, F.heads, F.unit_of, F.barriers, F.vals, F.vals_sorted,
                     F.pred, F.done, F.keys, F.keys_sorted, F.pnt_ops, F.pnt_scan, F.steps,
                     F.queue, F.ready8, F.recs, F.mailbox, F.owner_starts, F.owner_head8, F.mb_index,
-                    F.exp_flag, F.exp_index};
+                    F.exp_flag, F.exp_index, F.contrib, F.prefix};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     F.head8 = F.barrier8 = nullptr;
@@ -325,6 +327,7 @@ void free_flow(FlowScratch& F) {
     F.ready8 = nullptr;
     F.recs = nullptr;
     F.exp_flag = F.exp_index = nullptr;
+    F.contrib = F.prefix = nullptr;
     F.mailbox = F.owner_starts = F.mb_index = nullptr;
     F.owner_head8 = nullptr;
     F.cap = 0;
@@ -338,7 +341,8 @@ int ensure_flow(tbg_ctx* ctx, uint64_t m) {
              dev_alloc(ctx, &F.counts, 4, true) && dev_alloc(ctx, &F.pnt_fired, 1, true) &&
              dev_alloc(ctx, &F.lane_counts, 4, true) &&
              dev_alloc(ctx, &F.lane_undo, uint64_t(kFlowLanesMax) * kFlowUndoPerLane, false) &&
-             dev_alloc(ctx, &F.engine, kFlowEngineWords, true);
+             dev_alloc(ctx, &F.engine, kFlowEngineWords, true) &&
+             dev_alloc(ctx, &F.acc_free, ctx->opt.account_capacity, true);
         if (!ok) return TBG_EHIP;
     }
     if (m <= F.cap) return 0;
@@ -356,6 +360,7 @@ int ensure_flow(tbg_ctx* ctx, uint64_t m) {
          dev_alloc(ctx, &F.recs, cap, false) && dev_alloc(ctx, &F.mailbox, cap, false) &&
          dev_alloc(ctx, &F.mb_index, cap, false) &&
          dev_alloc(ctx, &F.exp_flag, cap, false) && dev_alloc(ctx, &F.exp_index, cap, false) &&
+         dev_alloc(ctx, &F.contrib, kc, false) && dev_alloc(ctx, &F.prefix, kc, false) &&
          dev_alloc(ctx, &F.owner_starts, kc, false) && dev_alloc(ctx, &F.owner_head8, kc, false);
     if (!ok) {
         free_flow(F);
@@ -473,6 +478,25 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
         rc = select_flagged(ctx, F.owner_head8, uint64_t(pairs), F.owner_starts, &F.lane_counts[0]);
         if (rc) return rc;
         tmark(ctx, "flow_plan");
+        // Free owners (lanes.hpp): contributions, their u128 prefix sums, the owners' verdicts,
+        // their events' owner bits.
+        L.epoch = c.epoch;
+        L.acc_free = F.acc_free;
+        L.contrib = F.contrib;
+        L.prefix = F.prefix;
+        if (!getenv("TBG_NO_FREE_OWNERS")) {
+            hipLaunchKernelGGL(lanes_contrib, dim3(grid_for(uint64_t(pairs))), block, 0, ctx->stream,
+                               ctx->T, L);
+            size_t pb = 0;
+            HIP_TRY(ctx, hipcub::DeviceScan::InclusiveSum(nullptr, pb, F.contrib, F.prefix, pairs,
+                                                          ctx->stream));
+            rc = ensure_cub_temp(ctx, pb);
+            if (rc) return rc;
+            HIP_TRY(ctx, hipcub::DeviceScan::InclusiveSum(ctx->cub_temp, pb, F.contrib, F.prefix,
+                                                          pairs, ctx->stream));
+            hipLaunchKernelGGL(lanes_owner_free, dim3(grid_for(m)), block, 0, ctx->stream, ctx->T, L);
+            hipLaunchKernelGGL(lanes_free, dim3(grid_for(m)), block, 0, ctx->stream, ctx->T, L);
+        }
         hipLaunchKernelGGL(lanes_replay, dim3(1), dim3(kLanesMax), 0, ctx->stream, ctx->T, c, L);
         hipLaunchKernelGGL(lanes_finish, dim3(grid_for(m)), block, 0, ctx->stream, ctx->T, c, L);
         tmark(ctx, "tr_lanes");
@@ -787,7 +811,7 @@ void tbg_close(tbg_ctx* ctx) {
                     ctx->pulse.keep, ctx->pulse.exp, ctx->pulse.ts, ctx->pulse.rows,
                     ctx->pulse.exp_b, ctx->pulse.rows_b, ctx->pulse.counters,
                     ctx->flow.dup_mark, ctx->flow.counts, ctx->flow.pnt_fired, ctx->flow.lane_counts,
-                    ctx->flow.lane_undo, ctx->flow.engine};
+                    ctx->flow.lane_undo, ctx->flow.engine, ctx->flow.acc_free};
     free_flow(ctx->flow);
     for (void* p : ptrs)
         if (p) (void)hipFree(p);

@@ -64,6 +64,11 @@ struct LanePlan {
     uint8_t* owner_head8;     // per sorted pair: first pair of an owner's segment
     uint32_t* owner_starts;   // selected
     unsigned int* counts;     // [0] owners, [1] ineligible events, [2] handled (set by the engine)
+    // free owners (lanes_contrib .. lanes_free)
+    uint32_t epoch;
+    uint32_t* acc_free;       // per account row: epoch of the call in which it is a free owner
+    u128* contrib;            // per sorted pair: the amount its owner's limit checks, else 0
+    u128* prefix;             // inclusive prefix sums of contrib
 };
 
 // The rings' loads are inline asm, so the compiler inserts no wait for them: its wait analysis
@@ -161,6 +166,67 @@ __global__ void lanes_segments(Tables T, LanePlan L) {
     L.owner_head8[i] = head;
 }
 
+// Free owners. An owner whose limit passes even if every event it checks in the call is created
+// and nothing replenishes it -- debits_must_not_exceed_credits: dpe + dpo + (sum of its checked
+// debit amounts) <= cpo; credits_must_not_exceed_debits: cpe + cpo + (sum of its checked credit
+// amounts) <= dpo, all at the call's start -- passes every check in any order (in a limit-events
+// call balances only grow by created amounts, and the checked side's sum bounds them). Its side of
+// each event is then as good as unowned: no lane walks it (lanes_free clears its owner bits; the
+// post pass adds its amounts with atomics), and an event left without owners is created. Config 3
+// (hot accounts funded for most of the stream) needs no lane at all until an account nears its
+// limit. The sums: one contribution per sorted (key, unit) pair, an inclusive u128 scan, and the
+// difference across each owner's pairs (from its start to the next owner's: the pairs between are
+// other keys, which contribute 0).
+__global__ void lanes_contrib(Tables T, LanePlan L) {
+    const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= L.n_pairs) return;
+    const uint64_t key = L.keys_sorted[i];
+    u128 v = 0;
+    if (key != kFlowNoKey && (key >> 63) == 1) {
+        const uint32_t row = uint32_t((key >> kFlowUnitBits) & 0xFFFFFFFFu);
+        const uint32_t s = uint32_t(key & ((1u << kFlowUnitBits) - 1));
+        if (s < L.m) {
+            const LaneRec r = L.recs[s];
+            const bool debit = r.dr == row;
+            if (debit ? (r.bits & kLaneDrDecides) : (r.bits & kLaneCrDecides)) v = r.amount;
+        }
+    }
+    L.contrib[i] = v;
+}
+
+__global__ void lanes_owner_free(Tables T, LanePlan L) {
+    const uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t owners = L.counts[0];
+    if (o >= owners || L.counts[1] != 0) return;
+    const uint64_t start = L.owner_starts[o];
+    const uint64_t end = o + 1 < owners ? L.owner_starts[o + 1] : L.n_pairs;
+    const u128 sum = L.prefix[end - 1] - (start ? L.prefix[start - 1] : u128(0));
+    const uint32_t row = uint32_t((L.keys_sorted[start] >> kFlowUnitBits) & 0xFFFFFFFFu);
+    const tb_account_t& a = T.acc_rows[row];
+    const u128 dpe = U(a.debits_pending), dpo = U(a.debits_posted);
+    const u128 cpe = U(a.credits_pending), cpo = U(a.credits_posted);
+    // (every balance < 2^126 and the sum < 2^96 for an eligible call: no wrap below)
+    bool free = true;
+    if (a.flags & TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS) free = free && dpe + dpo + sum <= cpo;
+    if (a.flags & TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS) free = free && cpe + cpo + sum <= dpo;
+    if (free) L.acc_free[row] = L.epoch;
+}
+
+__global__ void lanes_free(Tables T, LanePlan L) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= L.m || L.counts[1] != 0) return;
+    LaneRec r = L.recs[s];
+    const uint32_t cr = L.steps[s].cr;
+    uint32_t bits = r.bits;
+    if ((bits & kLaneDrOwner) && L.acc_free[r.dr] == L.epoch)
+        bits &= ~uint32_t(kLaneDrOwner | kLaneDrDecides);
+    if ((bits & kLaneCrOwner) && L.acc_free[cr] == L.epoch)
+        bits &= ~uint32_t(kLaneCrOwner | kLaneCrDecides);
+    if (bits == r.bits) return;
+    L.recs[s].bits = bits;
+    if (!(bits & (kLaneDrOwner | kLaneCrOwner))) L.outcome[s] = kOutCreated;
+}
+
 __global__ void __launch_bounds__(kLanesMax) lanes_replay(Tables T, Call<tb_transfer_t> c,
                                                           LanePlan L) {
     __shared__ uint32_t mbox[kLaneMbWords];
@@ -174,6 +240,8 @@ __global__ void __launch_bounds__(kLanesMax) lanes_replay(Tables T, Call<tb_tran
     uint64_t idx = alive ? L.owner_starts[o] : 0;
     const uint64_t my_key = alive ? (L.keys_sorted[idx] >> kFlowUnitBits) : 0;
     const uint32_t row = uint32_t(my_key & 0xFFFFFFFFu);
+    const bool walks = alive && L.acc_free[row] != L.epoch;  // (free owners: lanes_free)
+    alive = walks;
     u128 dpe = 0, dpo = 0, cpe = 0, cpo = 0;
     uint16_t flags = 0;
     if (alive) {
@@ -303,7 +371,7 @@ __global__ void __launch_bounds__(kLanesMax) lanes_replay(Tables T, Call<tb_tran
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the rings' last loads)
-    if (o < owners) {
+    if (walks) {
         tb_account_t& a = T.acc_rows[row];
         a.debits_posted = W(dpo);
         a.credits_posted = W(cpo);
