@@ -394,3 +394,45 @@ def test_flow_additive_accounts(additive, monkeypatch):
         p.compare_state()
     finally:
         p.close()
+
+
+@pytest.mark.parametrize("free_owners", [True, False], ids=["free", "walked"])
+def test_account_lanes_free_owners(free_owners, monkeypatch):
+    """Account lanes with free owners (lanes.hpp): limited accounts funded beyond every amount
+    they check in the call need no lane (their sides become atomics, events left without owners
+    are created), next to limited accounts that run out mid-call and still walk -- with events
+    between a free and a walked owner, between two free owners, and with credits_must_not_exceed
+    debits on the credit side; against the oracle, with and without free owners."""
+    if not free_owners:
+        monkeypatch.setenv("TBG_NO_FREE_OWNERS", "1")
+    rng = np.random.default_rng(91)
+    p = Pair(account_capacity=64, transfer_capacity=1 << 14, batch_events_max=1 << 12)
+    try:
+        acc = workload.accounts(12, seed=9, ledger=1)
+        # 1-4: debits_must_not_exceed_credits (1, 2 rich; 3, 4 poor); 5, 6:
+        # credits_must_not_exceed_debits (5 rich, 6 poor); 7-12 plain (7 funds everyone).
+        acc["flags"] = [2, 2, 2, 2, 4, 4, 0, 0, 0, 0, 0, 0]
+        p.create_accounts(acc)
+        fund = [dict(id=1 + i, debit_account_id=7, credit_account_id=a, amount=amt, ledger=1,
+                     code=1)
+                for i, (a, amt) in enumerate([(1, 10**9), (2, 10**9), (3, 3000), (4, 5000)])]
+        fund += [dict(id=10, debit_account_id=5, credit_account_id=8, amount=10**9, ledger=1,
+                      code=1),
+                 dict(id=11, debit_account_id=6, credit_account_id=8, amount=4000, ledger=1,
+                      code=1)]
+        p.create_transfers(_transfers(fund))
+        for call in range(3):
+            rows = []
+            for i in range(1500):
+                dr = int(rng.choice([1, 2, 3, 4, 9, 10]))
+                cr = int(rng.choice([5, 6, 1, 3, 11, 12]))
+                if cr == dr:
+                    cr = 12
+                rows.append(dict(id=100_000 * (call + 1) + i, debit_account_id=dr,
+                                 credit_account_id=cr, amount=int(rng.integers(1, 60)), ledger=1,
+                                 code=1))
+            r = p.create_transfers(_transfers(rows), [len(rows)])
+            assert (r["status"] == 0xFFFFFFFF).sum() > 0
+        p.compare_state()
+    finally:
+        p.close()
