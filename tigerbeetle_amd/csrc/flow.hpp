@@ -39,8 +39,8 @@
 namespace tbg {
 
 constexpr uint32_t kFlowThreads = 512;      // threads of an engine workgroup
-constexpr uint32_t kFlowLanesMax = 2048;    // lanes running units, over all engine workgroups
-constexpr uint32_t kFlowLanesPerWave = 1;   // default engine shape (TBG_FLOW_LPW / _WAVES / _BLOCKS)
+constexpr uint32_t kFlowLanesMax = 4096;    // lanes running units, over all engine workgroups
+constexpr uint32_t kFlowLanesPerWave = 8;   // default engine shape (TBG_FLOW_LPW / _WAVES / _BLOCKS)
 constexpr uint32_t kFlowWaves = 4;
 constexpr uint32_t kFlowBlocks = 128;
 constexpr uint32_t kFlowDoneShards = 16;    // units_done counter shards (one line each)
@@ -278,8 +278,10 @@ __global__ void flow_queue_init(FlowPlan P) {
 // branchy walk of dependent memory round trips, and lanes of one wave in different branches take
 // turns, so a unit's latency grows with the busy lanes of its wave. With `xcd_stride` 8 only every
 // 8th workgroup runs (workgroups are dealt round-robin over the 8 XCDs): the engine shares one L2.
-// Measured on config 4: one lane per wave over the whole chip halves the replay's time against one
-// workgroup of 512 busy lanes (116 -> 56 ms per 300k events); packing onto one XCD loses.
+// Measured on config 4: one lane per wave over the whole chip halved the replay's time against one
+// workgroup of 512 busy lanes (116 -> 56 ms per 300k events, every account keyed); packing onto one
+// XCD lost. With additive accounts unkeyed the replay has far more independent units, and more
+// lanes win: 4096 lanes (8 per wave) run 1M events in 7.8 ms against 19.9 ms on 512.
 //
 // Hand-offs between lanes on different CUs follow the agent-scope model (MI355X_MICROARCH.md,
 // inter-workgroup visibility): a finishing unit runs one release fence (L2 write-back) before its
