@@ -447,6 +447,7 @@ __global__ void tr_chunk_info(Call<tb_transfer_t> c, uint4* out) {
 // 16-byte field reads (one event per lane) fall on distinct banks.
 constexpr uint32_t kLdsEventStride = 144;
 constexpr uint32_t kIngestWaves = kBlock / 64;
+constexpr uint32_t kIngestGrid = 12288;  // tr_ingest workgroups (grid-stride beyond)
 
 __device__ inline void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
