@@ -511,7 +511,7 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
     }
     // Engine shape (flow.hpp): lanes per wave x waves per workgroup x workgroups; TBG_FLOW_XCD=8
     // packs the running workgroups onto one XCD. Default (config 4 sweeps, profiles/r01_flow2):
-    // 8 lanes per wave, 4 waves x 128 workgroups (4096 lanes) over the whole chip.
+    // 8 lanes per wave, 4 waves x 256 workgroups (8192 lanes) over the whole chip.
     auto env_u = [](const char* name, uint32_t def, uint32_t lo, uint32_t hi) {
         const char* e = getenv(name);
         const uint32_t v = e ? uint32_t(atoi(e)) : def;

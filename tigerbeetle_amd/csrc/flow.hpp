@@ -39,10 +39,10 @@
 namespace tbg {
 
 constexpr uint32_t kFlowThreads = 512;      // threads of an engine workgroup
-constexpr uint32_t kFlowLanesMax = 4096;    // lanes running units, over all engine workgroups
+constexpr uint32_t kFlowLanesMax = 8192;    // lanes running units, over all engine workgroups
 constexpr uint32_t kFlowLanesPerWave = 8;   // default engine shape (TBG_FLOW_LPW / _WAVES / _BLOCKS)
 constexpr uint32_t kFlowWaves = 4;
-constexpr uint32_t kFlowBlocks = 128;
+constexpr uint32_t kFlowBlocks = 256;
 constexpr uint32_t kFlowDoneShards = 16;    // units_done counter shards (one line each)
 constexpr uint32_t kFlowEngineWords = 64 + 32 * kFlowDoneShards;
 constexpr uint32_t kFlowChainMax = 256;     // longer chains run as barriers (global undo log)
@@ -281,7 +281,8 @@ __global__ void flow_queue_init(FlowPlan P) {
 // Measured on config 4: one lane per wave over the whole chip halved the replay's time against one
 // workgroup of 512 busy lanes (116 -> 56 ms per 300k events, every account keyed); packing onto one
 // XCD lost. With additive accounts unkeyed the replay has far more independent units, and more
-// lanes win: 4096 lanes (8 per wave) run 1M events in 7.8 ms against 19.9 ms on 512.
+// lanes win: 8192 lanes (8 per wave, 256 workgroups) run 1M events in 7.0 ms, 4096 in 8.2 ms,
+// 512 in 19.9 ms.
 //
 // Hand-offs between lanes on different CUs follow the agent-scope model (MI355X_MICROARCH.md,
 // inter-workgroup visibility): a finishing unit runs one release fence (L2 write-back) before its
