@@ -361,12 +361,21 @@ __global__ void __launch_bounds__(kFlowThreads) flow_replay(Tables T, Call<tb_tr
         // (transfers key_max: read only by imported events, which never take the flow replay;
         // each lane folds its maximum in at the exit.)
         if (R.key_max > lane_key_max) lane_key_max = R.key_max;
-        // Release: this unit's writes reach the point of coherence before any decrement.
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // Release: this unit's writes reach the point of coherence before any decrement. A unit
+        // without successors skips it (the L2 write-back is the costliest step of a short unit,
+        // and nothing in this kernel reads what it wrote; the kernel's end releases it).
+        bool any_succ = false;
+        for (uint32_t s = begin; s < end; s++) {
+            const uint4 sc = *reinterpret_cast<const uint4*>(P.succ + kFlowKeys * uint64_t(s));
+            any_succ |= (sc.x & sc.y & sc.z & sc.w) != kNone32;
+        }
         uint32_t next = kNone32;
         bool pushed = false;
-        for (uint32_t s = begin; s < end; s++) {
+        if (any_succ) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        for (uint32_t s = begin; any_succ && s < end; s++) {
             const uint4 sc = *reinterpret_cast<const uint4*>(P.succ + kFlowKeys * uint64_t(s));
             const uint32_t vs[kFlowKeys] = {sc.x, sc.y, sc.z, sc.w};
 #pragma unroll
