@@ -11,18 +11,29 @@ the timed region starts; every step uses fresh transfer ids, so every step does 
 Multi-GPU (weak scaling): one process per GPU; each rank owns its own ledger shard
 (own accounts and transfers, ledger 2 + rank) with no data-path collective. The timed region is
 bracketed by a barrier + device synchronise on every rank; the reported time is the max over ranks.
+(`tools/bench_sharded.py` times the routed path: one client stream over many ledgers, scattered
+to the shards and gathered inside the timed region.)
 
-Validation (after the timed region): every result must be `created`, and every account's final
-balances must equal the exact per-account sums of the steps' amounts (the workload is
-order-independent, so this is the serial reference outcome).
+Validation (after the timed region; the workload is order-independent, so the serial reference
+outcome is known in closed form): every result of every step is `created` with its exact event
+timestamp; every transfer row (config 2: all of them, looked up by id; config 5: a sample) equals
+the event with its commit timestamp; every account row equals the created account with the exact
+per-account sums as posted balances and zero pending balances (config 5: a sample).
 
-Output: one JSON line on rank 0 with `roofline` (dominant kernel, HIP-event timed) and
-`cpu_baseline` (the serial C oracle on one host core, bounded sample of the same workload).
+`per_commit`: the rate the drop-in sees per replica commit (state_machine.zig:2564-2669): one
+8189-event body per commit (tigerbeetle.zig:853-901) -- through tbg_create_transfers_device with the
+body resident in HBM, and through the full StateMachine boundary (tb_sm_prepare / prefetch /
+commit on host buffers, tb_state_machine.h).
+
+Output: one JSON line on rank 0 with `roofline` (dominant kernel, HIP-event timed, SURVEY.md §8d
+algorithmic bytes) and `cpu_baseline` (the serial C oracle pinned to one host core, bounded sample
+of the same workload).
 """
 import argparse
 import ctypes
 import json
 import os
+import platform
 import sys
 import time
 
@@ -40,25 +51,15 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # this bench's default workload; FETCH_SIZE doubled per the gfx950 note + WRITE_SIZE).
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")
 BATCH = 8189           # Operation.create_transfers.event_max (src/tigerbeetle.zig:853-901)
+CREATED = 0xFFFFFFFF
+MESSAGE_BODY_SIZE_MAX = (1 << 20) - 256  # constants.message_body_size_max (constants.zig:234)
+OP_CREATE_ACCOUNTS, OP_CREATE_TRANSFERS = 146, 147  # tb_state_machine.h
 
-# Algorithmic bytes per event of each kernel of the create_transfers path: the
-# fields the kernel must read or write for its function, counted once.
-KERNEL_BYTES_PER_EVENT = {
-    # event 128 R, id-key claim 16 (8-B slot read + write), transfer row 128 W, result 16 W,
-    # 2 packed balance items 16 W, info + liveness 2 W (FAST events write no other record)
-    "tr_ingest": 128 + 16 + 128 + 16 + 16 + 2,
-    # re-validation pass (skipped when ingest raised no commit flag): record 21 R, result
-    # timestamp 8 R, liveness 1 W
-    "tr_commit": 21 + 8 + 1,
-    # 2 packed u64 items, read and written once (large key spaces)
-    "bal_sort": 2 * 8 * 2,
-    # sorted items read once (account rows are per distinct account)
-    "bal_reduce": 2 * 8,
-    # bucketed path (small key spaces): items read + written into their buckets
-    "bal_scatter": 2 * 8 * 2,
-    # bucketed items read once (slice partials are per bucket key, not per event)
-    "bal_accumulate": 2 * 8,
-}
+# Algorithmic bytes per event of each kernel of the create_transfers path. tr_ingest does all of
+# SURVEY.md §8d's per-event work -- event read 128, result write 16, transfer-row write 128, id-key
+# probe 16 = 288 B; the per-account 256 B (row read + write) belong to the balance kernels, which
+# are priced per distinct account (`path` below), not per event.
+KERNEL_BYTES_PER_EVENT = {"tr_ingest": 128 + 16 + 128 + 16}
 
 
 def parse_args():
@@ -76,6 +77,8 @@ def parse_args():
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="bounded CPU-oracle sample (rank 0, N=1)")
+    ap.add_argument("--commit-reps", type=int, default=200,
+                    help="8189-event commits timed for `per_commit` (0: skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-validate", action="store_true")
     return ap.parse_args()
@@ -164,6 +167,16 @@ def step_timestamps(prepare_ts, lens):
     return ts.astype(np.uint64), int(ts[-1])
 
 
+def event_timestamps(lens, batch_ts):
+    """Event i of batch b is stamped batch_ts[b] - len[b] + i + 1 (execute_multi_batch)."""
+    lens = np.asarray(lens, dtype=np.int64)
+    starts = np.cumsum(lens) - lens
+    n = int(lens.sum())
+    within = np.arange(n, dtype=np.int64) - np.repeat(starts, lens)
+    return (np.repeat(batch_ts.astype(np.uint64) - lens.astype(np.uint64), lens)
+            + within.astype(np.uint64) + np.uint64(1))
+
+
 def measured_traffic(kernel):
     """(HBM bytes per launch, source) of `kernel` from TRAFFIC_FILE, or (None, None)."""
     try:
@@ -174,35 +187,70 @@ def measured_traffic(kernel):
         return None, None
 
 
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
 def cpu_baseline(args, acc, base, lens, label):
-    """The serial C oracle (oracle/liboracle.so) on one core, bounded sample of the workload."""
+    """The serial C oracle (oracle/liboracle.so) pinned to one host core (the equivalent of
+    `taskset -c <core>`: sched_setaffinity of this process), bounded sample of the workload."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_binding
     olib = oracle_binding.load()
-    o = olib.tbo_open(8190, 1)
-    res = np.zeros(len(acc), dtype=RESULT_DTYPE)
-    olib.tbo_create_accounts(o, acc.ctypes.data_as(ctypes.c_void_p), len(acc), 1 + len(acc),
-                             res.ctypes.data_as(ctypes.c_void_p))
-    ts = 2 + len(acc)
-    out = np.zeros(BATCH, dtype=RESULT_DTYPE)
-    done, off, b = 0, 0, 0
-    t0 = time.perf_counter()
-    while b < len(lens):
-        n = int(lens[b])
-        ts += 1 + n
-        olib.tbo_create_transfers(o, base[off:off + n].ctypes.data_as(ctypes.c_void_p), n, ts,
-                                  out.ctypes.data_as(ctypes.c_void_p))
-        assert (out["status"][:n] == 0xFFFFFFFF).all()
-        done += n
-        off += n
-        b += 1
-        if time.perf_counter() - t0 >= args.cpu_seconds:
-            break
-    elapsed = time.perf_counter() - t0
-    olib.tbo_close(o)
-    return {"value": done / elapsed, "unit": "transfers/s", "cores": 1, "kind": "port",
+    allowed = sorted(os.sched_getaffinity(0))
+    core = allowed[0]
+    os.sched_setaffinity(0, {core})
+    try:
+        o = olib.tbo_open(8190, 1)
+        res = np.zeros(len(acc), dtype=RESULT_DTYPE)
+        olib.tbo_create_accounts(o, acc.ctypes.data_as(ctypes.c_void_p), len(acc), 1 + len(acc),
+                                 res.ctypes.data_as(ctypes.c_void_p))
+        ts = 2 + len(acc)
+        out = np.zeros(BATCH, dtype=RESULT_DTYPE)
+        done, off, b = 0, 0, 0
+        t0 = time.perf_counter()
+        while b < len(lens):
+            n = int(lens[b])
+            ts += 1 + n
+            olib.tbo_create_transfers(o, base[off:off + n].ctypes.data_as(ctypes.c_void_p), n, ts,
+                                      out.ctypes.data_as(ctypes.c_void_p))
+            assert (out["status"][:n] == CREATED).all()
+            done += n
+            off += n
+            b += 1
+            if time.perf_counter() - t0 >= args.cpu_seconds:
+                break
+        elapsed = time.perf_counter() - t0
+        olib.tbo_close(o)
+    finally:
+        os.sched_setaffinity(0, set(allowed))
+    return {"value": round(done / elapsed, 1), "unit": "transfers/s", "cores": 1, "kind": "port",
+            "cpu_model": cpu_model(), "nproc": os.cpu_count(), "cpus_allowed": len(allowed),
+            "pinned_cpu": core,
             "sample": f"{done} of the {len(base)} {label} transfers ({b} batches of <= {BATCH}) "
-                      f"through oracle/tb_oracle.c, single-threaded, {elapsed:.1f} s"}
+                      f"through oracle/tb_oracle.c, single-threaded, pinned to cpu {core} "
+                      f"(sched_setaffinity = taskset -c {core}), {elapsed:.1f} s"}
+
+
+def lookup_transfer_rows(lib, g, ids_lo, chunk):
+    """Rows of the transfers with ids (lo words, hi 0), in request order, via tbg_lookup."""
+    out = np.zeros(len(ids_lo), dtype=TRANSFER_DTYPE)
+    ids = np.zeros((chunk, 2), dtype=np.uint64)
+    for a in range(0, len(ids_lo), chunk):
+        z = min(len(ids_lo), a + chunk)
+        ids[:z - a, 0] = ids_lo[a:z]
+        got = lib.tbg_lookup_transfers(g, ids.ctypes.data_as(ctypes.c_void_p), z - a,
+                                       out[a:z].ctypes.data_as(ctypes.c_void_p))
+        if got != z - a:
+            return None
+    return out
 
 
 class Config2:
@@ -219,6 +267,7 @@ class Config2:
         self.cr = self.base["credit_account_id"][:, 0].astype(np.int64) - 1
         self.chunk = self.A
         self.default = (self.N, self.A) == (10_000_000, 10_000)
+        self.account_ts = None
         self.config = {"workload": "config2: 10k accounts, 10M uniform create_transfers in "
                                    "8189-event batches, 1 ledger shard per GPU",
                        "transfers_per_step_per_gpu": self.N, "accounts_per_gpu": self.A}
@@ -226,18 +275,25 @@ class Config2:
     def account_chunks(self):
         yield self.acc
 
-    def validate(self, lib, g, reps):
-        """Every account's final balances equal the exact per-account sums (the workload is
-        order-independent, so this is the serial reference outcome)."""
+    def validate_accounts(self, lib, g, reps):
+        """Every account row byte for byte: the created account with its creation timestamp and
+        the exact per-account sums as posted balances (pending balances zero)."""
         dump = np.zeros(self.A, dtype=ACCOUNT_DTYPE)
-        assert lib.tbg_dump_accounts(g, dump.ctypes.data_as(ctypes.c_void_p)) == self.A
-        amt = self.base["amount"][:, 0].astype(np.int64)
-        exp_d = np.bincount(self.dr, weights=amt, minlength=self.A).astype(np.int64) * reps
-        exp_c = np.bincount(self.cr, weights=amt, minlength=self.A).astype(np.int64) * reps
-        ok = bool((dump["debits_posted"][:, 0].astype(np.int64) == exp_d).all())
-        ok &= bool((dump["credits_posted"][:, 0].astype(np.int64) == exp_c).all())
-        ok &= bool((dump["debits_posted"][:, 1] == 0).all() and (dump["credits_pending"] == 0).all())
-        return ok
+        if lib.tbg_dump_accounts(g, dump.ctypes.data_as(ctypes.c_void_p)) != self.A:
+            return False, "account count"
+        amt = self.base["amount"][:, 0].astype(np.uint64)
+        want = self.acc.copy()
+        want["timestamp"] = self.account_ts
+        # (exact integer sums: bincount's float64 weights would round past 2^53)
+        for col, idx in (("debits_posted", self.dr), ("credits_posted", self.cr)):
+            s = np.zeros(self.A, dtype=np.uint64)
+            np.add.at(s, idx, amt)
+            want[col][:, 0] = s * np.uint64(reps)
+        ok = dump.tobytes() == want.tobytes()
+        return ok, "" if ok else "account rows differ"
+
+    def rows_to_check(self):
+        return np.arange(self.N)  # every transfer row
 
     def cpu_sample(self):
         return self.acc, self.base, "config-2"
@@ -257,6 +313,7 @@ class Config5:
                                                                  seed=args.seed)
         self.chunk = min(self.A, 4_000_000)
         self.default = False
+        self.account_ts = None
         first, per = workload.config5_ledgers(rank, world)
         self.config = {"workload": f"config5: {self.A} accounts per GPU on {per} of 64 ledgers "
                                    f"(1B accounts over 8 GPUs), 1M-event super-batches of "
@@ -271,7 +328,7 @@ class Config5:
             if j0 and (j0 // self.chunk) % 8 == 0:
                 print(f"config5: {j0 + len(j)} accounts created", file=sys.stderr, flush=True)
 
-    def validate(self, lib, g, reps):
+    def validate_accounts(self, lib, g, reps):
         """Sampled (SURVEY.md §8d at 1B scale): 65,536 touched accounts and 4,096 others looked up
         by id; their balances must equal the exact sums of the steps' amounts."""
         rng = np.random.default_rng(5)
@@ -279,11 +336,11 @@ class Config5:
         sample = np.concatenate([rng.choice(touched, size=min(65_536, len(touched)), replace=False),
                                  rng.integers(0, self.A, size=4_096)])
         sample = np.unique(sample)
-        amt = self.base["amount"][:, 0].astype(np.int64)
+        amt = self.base["amount"][:, 0].astype(np.uint64)
         pos = np.full(self.A, -1, dtype=np.int64)
         pos[sample] = np.arange(len(sample))
-        exp_d = np.zeros(len(sample), dtype=np.int64)
-        exp_c = np.zeros(len(sample), dtype=np.int64)
+        exp_d = np.zeros(len(sample), dtype=np.uint64)
+        exp_c = np.zeros(len(sample), dtype=np.uint64)
         md, mc = pos[self.dr] >= 0, pos[self.cr] >= 0
         np.add.at(exp_d, pos[self.dr[md]], amt[md])
         np.add.at(exp_c, pos[self.cr[mc]], amt[mc])
@@ -292,10 +349,20 @@ class Config5:
         out = np.zeros(len(sample), dtype=ACCOUNT_DTYPE)
         found = lib.tbg_lookup_accounts(g, ids.ctypes.data_as(ctypes.c_void_p), len(sample),
                                         out.ctypes.data_as(ctypes.c_void_p))
-        ok = found == len(sample) and bool((out["id"][:, 0] == ids[:, 0]).all())
-        ok &= bool((out["debits_posted"][:, 0].astype(np.int64) == exp_d * reps).all())
-        ok &= bool((out["credits_posted"][:, 0].astype(np.int64) == exp_c * reps).all())
-        return ok
+        want = workload.accounts_config5(sample, self.rank, self.world)
+        ok = found == len(sample)
+        for col in ("id", "user_data_128", "user_data_64", "user_data_32", "ledger", "code",
+                    "flags", "debits_pending", "credits_pending"):
+            ok = ok and bool((out[col] == want[col]).all())
+        ok = ok and bool((out["debits_posted"][:, 0] == exp_d * np.uint64(reps)).all())
+        ok = ok and bool((out["credits_posted"][:, 0] == exp_c * np.uint64(reps)).all())
+        ok = ok and bool((out["debits_posted"][:, 1] == 0).all())
+        ok = ok and bool((out["credits_posted"][:, 1] == 0).all())
+        return ok, "" if ok else "sampled account rows differ"
+
+    def rows_to_check(self):
+        return np.sort(np.random.default_rng(6).choice(self.N, size=min(self.N, 65_536),
+                                                       replace=False))
 
     def cpu_sample(self):
         """The oracle holds only the accounts the sampled transfers touch (its hash maps do not
@@ -305,11 +372,128 @@ class Config5:
         return workload.accounts_config5(j, self.rank, self.world), self.base[:n], "config-5"
 
 
+def per_commit(args, lib, dev, g, wl, prepare_ts, id_base):
+    """One 8189-event body per replica commit: (a) tbg_create_transfers_device with the body in
+    HBM, (b) the full StateMachine boundary on host buffers (tb_sm_prepare / prefetch / commit).
+    Returns (report, prepare_ts)."""
+    R, n = args.commit_reps, min(BATCH, wl.N)
+    body_events = wl.base[:n]
+    lens1 = np.asarray([n], dtype=np.int64)
+    d_end = dev.upload(np.asarray([n], dtype=np.uint32))
+    bufs = []
+    for r in range(R):
+        ev = body_events.copy()
+        ev["id"][:, 0] += np.uint64(id_base + r * n)
+        ts, prepare_ts = step_timestamps(prepare_ts, lens1)
+        bufs.append((dev.upload(ev), dev.upload(ts), dev.alloc(n * 16), ts))
+    dev.sync()
+    lat = np.zeros(R)
+    t_all = time.perf_counter()
+    for r in range(R):
+        d_ev, d_ts, d_res, _ = bufs[r]
+        t0 = time.perf_counter()
+        rc = lib.tbg_create_transfers_device(g, d_ev, n, d_end, d_ts, 1, d_res, None)
+        lat[r] = time.perf_counter() - t0
+        if rc != 0:
+            raise RuntimeError(f"per-commit: {rc} {lib.tbg_last_error(g)}")
+    dev.sync()
+    t_all = time.perf_counter() - t_all
+    ok = True
+    res = np.zeros(n, dtype=RESULT_DTYPE)
+    for d_ev, d_ts, d_res, ts in bufs:
+        dev.download(d_res, res)
+        ok &= bool((res["status"] == CREATED).all() and
+                   (res["timestamp"] == event_timestamps(lens1, ts)).all())
+    device = {"events_per_commit": n, "commits": R, "transfers_per_s": round(n * R / t_all, 1),
+              "us_per_commit_mean": round(t_all / R * 1e6, 1),
+              "us_per_commit_p50": round(float(np.median(lat)) * 1e6, 1),
+              "validated": ok,
+              "note": "tbg_create_transfers_device, the body resident in HBM, one synchronous "
+                      "call per commit"}
+
+    # (b) the StateMachine boundary: a second executor behind tb_sm (its own tables).
+    sm_opt = native.SmOptions()
+    sm_opt.batch_size_limit = MESSAGE_BODY_SIZE_MAX
+    sm_opt.message_body_size_max = MESSAGE_BODY_SIZE_MAX
+    sm_opt.pulse_batch_max = 8190
+    topt = native.TbgOptions()
+    topt.account_capacity = wl.A if wl.name == "config2" else 1 << 21
+    topt.transfer_capacity = (R + 2) * n
+    topt.batch_events_max = BATCH
+    topt.batch_count_max = 64
+    topt.pulse_batch_max = 8190
+    topt.device = 0
+    topt.pulse_next_timestamp_init = 1
+    sm = lib.tb_sm_open_gpu(ctypes.byref(sm_opt), ctypes.byref(topt))
+    if not sm:
+        return {"device": device, "state_machine": None}, prepare_ts
+    out = ctypes.create_string_buffer(MESSAGE_BODY_SIZE_MAX + 256)
+    cb = native.PREFETCH_CALLBACK(lambda ctx: None)
+    op_counter = [0]
+
+    def encode(records):
+        payload = records.tobytes()
+        trailer = lib.tb_multi_batch_trailer_total_size(128, 1)
+        buf = ctypes.create_string_buffer(len(payload) + trailer + 2)
+        ctypes.memmove(buf, payload, len(payload))
+        size = lib.tb_multi_batch_encode_trailer(buf, len(payload), 128,
+                                                 (ctypes.c_uint16 * 1)(len(records)), 1)
+        return buf.raw[:size]
+
+    def commit(operation, body):
+        # TestContext.prepare / execute (state_machine_tests.zig:230-285)
+        lib.tb_sm_set_commit_timestamp(sm, lib.tb_sm_get_prepare_timestamp(sm))
+        lib.tb_sm_set_prepare_timestamp(sm, lib.tb_sm_get_prepare_timestamp(sm) + 1)
+        lib.tb_sm_prepare(sm, operation, body, len(body))
+        ts = lib.tb_sm_get_prepare_timestamp(sm)
+        lib.tb_sm_set_prefetch_timestamp(sm, ts)
+        op_counter[0] += 1
+        lib.tb_sm_prefetch(sm, cb, None, op_counter[0], op_counter[0], operation, body, len(body))
+        size = lib.tb_sm_commit(sm, 1, 0, op_counter[0], ts, operation, body, len(body), out)
+        if size < 0:
+            raise RuntimeError(f"tb_sm_commit: {size}")
+        return out.raw[:size]
+
+    if wl.name == "config2":
+        accs = wl.acc
+    else:
+        j = np.unique(np.concatenate([wl.dr[:n], wl.cr[:n]]))
+        accs = workload.accounts_config5(j, wl.rank, wl.world)
+    sm_ok = True
+    for a in range(0, len(accs), BATCH):
+        reply = commit(OP_CREATE_ACCOUNTS, encode(accs[a:a + BATCH]))
+        r = np.frombuffer(reply[:16 * len(accs[a:a + BATCH])], dtype=RESULT_DTYPE)
+        sm_ok &= bool((r["status"] == CREATED).all())
+    bodies = []
+    for r in range(R):
+        ev = body_events.copy()
+        ev["id"][:, 0] += np.uint64(r * n + 1)
+        bodies.append(encode(ev))
+    lat_sm = np.zeros(R)
+    t_all = time.perf_counter()
+    for r in range(R):
+        t0 = time.perf_counter()
+        reply = commit(OP_CREATE_TRANSFERS, bodies[r])
+        lat_sm[r] = time.perf_counter() - t0
+        res = np.frombuffer(reply[:16 * n], dtype=RESULT_DTYPE)
+        sm_ok &= bool((res["status"] == CREATED).all())
+    t_all = time.perf_counter() - t_all
+    lib.tb_sm_close(sm)
+    smr = {"events_per_commit": n, "commits": R, "transfers_per_s": round(n * R / t_all, 1),
+           "us_per_commit_mean": round(t_all / R * 1e6, 1),
+           "us_per_commit_p50": round(float(np.median(lat_sm)) * 1e6, 1),
+           "body_bytes": len(bodies[0]), "validated": sm_ok,
+           "note": "tb_sm_prepare + tb_sm_prefetch + tb_sm_commit per 8189-event multi-batch "
+                   "body on host buffers (body in and reply out over PCIe)"}
+    return {"device": device, "state_machine": smr}, prepare_ts
+
+
 def main():
     args = parse_args()
     world, rank, local, dist = dist_init(args)
     wl = (Config5 if args.workload == "config5" else Config2)(args, rank, world)
     N, A, K, W = wl.N, wl.A, args.steps, args.warmup
+    R = args.commit_reps if rank == 0 and world == 1 and not args.no_validate else 0
     lib = native.load()
     dev = Device()
     dev.set_device(local)
@@ -320,7 +504,8 @@ def main():
 
     opt = native.TbgOptions()
     opt.account_capacity = A
-    opt.transfer_capacity = N * (K + W + 1)  # + one host-buffer step (pcie_inclusive)
+    # + one host-buffer step (pcie_inclusive) + the per-commit bodies
+    opt.transfer_capacity = N * (K + W + 1) + R * BATCH
     opt.batch_events_max = max(N, wl.chunk)
     opt.batch_count_max = len(lens)
     opt.pulse_batch_max = 8190
@@ -330,6 +515,7 @@ def main():
     assert g, "tbg_open failed"
 
     prepare_ts = 0
+    acc_ts = []
     for acc in wl.account_chunks():
         res_acc = np.zeros(len(acc), dtype=RESULT_DTYPE)
         a_lens = np.asarray([len(acc)], dtype=np.uint32)
@@ -339,9 +525,13 @@ def main():
                                      a_lens.ctypes.data_as(native.c_u32p),
                                      a_ts.ctypes.data_as(native.c_u64p), 1,
                                      res_acc.ctypes.data_as(ctypes.c_void_p))
-        assert rc == 0 and (res_acc["status"] == 0xFFFFFFFF).all(), \
+        assert rc == 0 and (res_acc["status"] == CREATED).all(), \
             f"create_accounts: {rc} {lib.tbg_last_error(g)}"
+        if wl.name == "config2":
+            acc_ts.append(event_timestamps(np.asarray([len(acc)]), a_ts))
         del acc, res_acc
+    if acc_ts:
+        wl.account_ts = np.concatenate(acc_ts)
 
     # Per-step inputs, resident in HBM before timing: fresh ids per step.
     d_ends = dev.upload(ends)
@@ -350,12 +540,12 @@ def main():
         ev = base.copy()
         ev["id"][:, 0] += np.uint64(s * N)
         ts, prepare_ts = step_timestamps(prepare_ts, lens)
-        steps.append((dev.upload(ev), dev.upload(ts), dev.alloc(N * 16)))
+        steps.append((dev.upload(ev), dev.upload(ts), dev.alloc(N * 16), ts))
         del ev
     dev.sync()
 
     def run_step(s):
-        d_ev, d_ts, d_res = steps[s]
+        d_ev, d_ts, d_res, _ = steps[s]
         rc = lib.tbg_create_transfers_device(g, d_ev, N, d_ends, d_ts, len(lens), d_res, None)
         if rc != 0:
             raise RuntimeError(f"tbg_create_transfers_device: {rc} {lib.tbg_last_error(g)}")
@@ -387,17 +577,40 @@ def main():
     stats = native.TbgStats()
     lib.tbg_last_stats(g, ctypes.byref(stats))
 
-    validated = None
+    validated, validation = None, {}
     if not args.no_validate:
+        t_val = time.perf_counter()
         ok = True
         r = np.zeros(N, dtype=RESULT_DTYPE)
+        rows = wl.rows_to_check()
         for s in range(W + K):
-            dev.download(steps[s][2], r)
-            ok &= bool((r["status"] == 0xFFFFFFFF).all())
-        ok &= wl.validate(lib, g, W + K)
-        validated = ok
+            d_ev, d_ts, d_res, ts = steps[s]
+            dev.download(d_res, r)
+            want_ts = event_timestamps(lens, ts)
+            ok &= bool((r["status"] == CREATED).all())
+            ok &= bool((r["timestamp"] == want_ts).all() and (r["reserved"] == 0).all())
+            # transfer rows: the event as submitted, stamped with its commit timestamp
+            got = lookup_transfer_rows(lib, g, base["id"][rows, 0] + np.uint64(s * N),
+                                       min(opt.batch_events_max, 1 << 21))
+            if got is None:
+                ok = False
+                continue
+            for a in range(0, len(rows), 1 << 21):
+                sel = rows[a:a + (1 << 21)]
+                want = base[sel].copy()
+                want["id"][:, 0] += np.uint64(s * N)
+                want["timestamp"] = want_ts[sel]
+                ok &= got[a:a + len(sel)].tobytes() == want.tobytes()
+        acc_ok, why = wl.validate_accounts(lib, g, W + K)
+        ok &= acc_ok
+        validated = bool(ok)
+        validation = {"results": f"{W + K} steps x {N}: status and event timestamp",
+                      "transfer_rows": f"{len(rows)} per step, byte for byte",
+                      "accounts": "all rows byte for byte" if wl.name == "config2"
+                                  else "sampled rows (balances exact)",
+                      "seconds": round(time.perf_counter() - t_val, 1)}
         if not ok:
-            print(json.dumps({"error": "validation failed"}), file=sys.stderr)
+            print(json.dumps({"error": "validation failed", "why": why}), file=sys.stderr)
 
     # The same step through the host-buffer ABI (tbg_create_transfers: events copied in, results
     # copied out over PCIe) -- the rate a caller holding host buffers sees; never `value`.
@@ -414,11 +627,15 @@ def main():
                                       ts.ctypes.data_as(native.c_u64p), len(lens),
                                       h_res.ctypes.data_as(ctypes.c_void_p))
         t_host = time.perf_counter() - t0
-        ok = rc == 0 and bool((h_res["status"] == 0xFFFFFFFF).all())
+        ok = rc == 0 and bool((h_res["status"] == CREATED).all())
         validated = bool(validated) and ok
         pcie = {"value": round(N / t_host, 1), "unit": "transfers/s", "ms": round(t_host * 1e3, 3),
                 "note": "one step through tbg_create_transfers with host buffers (events in, "
                         "results out over PCIe)"}
+
+    commits = None
+    if R > 0:
+        commits, prepare_ts = per_commit(args, lib, dev, g, wl, prepare_ts, (W + K + 1) * N)
 
     # Algorithmic bytes of the path: 288 B per event + 256 B per distinct account.
     distinct = len(np.union1d(wl.dr, wl.cr))
@@ -437,12 +654,17 @@ def main():
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                     "traffic": traffic, "traffic_source": traffic_src,
                     "alg_bytes_per_launch": kbytes,
+                    "alg_bytes_basis": "SURVEY.md §8d: 288 B per event (event 128 R, result 16 W, "
+                                       "transfer row 128 W, id-key probe 16)",
                     "avg_launch_ms": round(kms / kcount, 4),
                     "path": {"alg_bytes_per_step": path_bytes,
+                             "alg_bytes_basis": "SURVEY.md §8d: 288 N + 256 D "
+                                                f"(N = {N}, D = {distinct} distinct accounts)",
                              "device_ms_per_step": round(dev_ms_total / K, 4),
                              "achieved": round(path_bytes / (dev_ms_total / K / 1e3) / 1e9, 1),
                              "frac": round(path_bytes / (dev_ms_total / K / 1e3) / 1e9 /
-                                           HBM_PEAK_GBS, 4)},
+                                           HBM_PEAK_GBS, 4),
+                             "frac_wall": round(path_bytes / (t_max / K) / 1e9 / HBM_PEAK_GBS, 4)},
                     "kernels_ms_per_step": {k: round(v[0] / K, 4) for k, v in kernels.items()}}
 
     cpu = None
@@ -461,10 +683,12 @@ def main():
             "config": dict(wl.config, batches_per_step=int(len(lens)),
                            parallelism=f"ledger-shard x{world}"),
             "validated": validated,
+            "validation": validation,
             "replayed_events_last_step": int(stats.replayed),
             "roofline": roofline,
             "cpu_baseline": cpu,
             "pcie_inclusive": pcie,
+            "per_commit": commits,
         }
         print(json.dumps(line))
     lib.tbg_close(g)

@@ -102,9 +102,13 @@ def test_atomic_path_sparse_keys():
         p.close()
 
 
-def test_bucket_path_hot_skew():
-    """One call of >= 65,536 events over hot limited accounts: bucketed balances with 90% of
-    the items in one bucket, next to replayed limit checks."""
+@pytest.mark.parametrize("window", [True, False], ids=["window", "buckets"])
+def test_bucket_path_hot_skew(window, monkeypatch):
+    """One call of >= 65,536 events over hot limited accounts: window (pair items, LDS counters)
+    or bucketed balances (TBG_NO_WINDOW) with 90% of the items on few accounts, next to replayed
+    limit checks."""
+    if not window:
+        monkeypatch.setenv("TBG_NO_WINDOW", "1")
     p = Pair(account_capacity=1 << 14, transfer_capacity=1 << 18, batch_events_max=1 << 17)
     try:
         acc = workload.accounts(6_000, seed=7)
@@ -115,6 +119,45 @@ def test_bucket_path_hot_skew():
         p.create_transfers(t, [8189] * 9 + [80_000 - 9 * 8189])
         t = workload.transfers_uniform(70_000, 6_000, seed=8, id_offset=20_000_000)
         p.create_transfers(t, [70_000])
+        p.compare_state()
+    finally:
+        p.close()
+
+
+@pytest.mark.parametrize("n_acc", [5_000, 9_000], ids=["4-fields", "posted-only"])
+def test_balance_window_edges(n_acc):
+    """The balance window (kernels.hpp): calls of >= 65,536 events over <= 2^14 accounts. With
+    5,000 accounts all four balance fields sit in the LDS window; with 9,000 only the posted ones
+    (pending deltas take u128 atomics on the row). Amounts from 1 to 2^32 - 1 (u32 LDS sums that
+    wrap: the carry words), 2^32 .. 2^35 (the high part through the carry words), >= 2^35 (too
+    wide for a pair item: tr_commit's atomics), pending transfers, and limited accounts whose
+    SLOW events demote FAST events (their items withdrawn); a second call checks that the carry
+    words were consumed."""
+    rng = np.random.default_rng(n_acc)
+    p = Pair(account_capacity=1 << 14, transfer_capacity=1 << 19, batch_events_max=1 << 17)
+    try:
+        acc = workload.accounts(n_acc, seed=9, ledger=2)
+        acc["flags"][1:41] |= 2  # debits_must_not_exceed_credits
+        p.create_accounts(acc, _split(n_acc, rng, 8189))
+        p.create_transfers(workload.funding_transfers(40, 10**12, id_offset=50_000_000))
+        off = 0
+        for call in range(2):
+            n = 90_000
+            t = workload.transfers_uniform(n, n_acc, seed=call + 17, id_offset=off)
+            off += n
+            kind = rng.random(n)
+            amt = t["amount"][:, 0]
+            amt[kind < 0.3] = rng.integers(2**31, 2**32, size=int((kind < 0.3).sum()),
+                                           dtype=np.uint64)
+            big = (kind >= 0.3) & (kind < 0.35)
+            amt[big] = rng.integers(2**32, 2**35, size=int(big.sum()), dtype=np.uint64)
+            wide = (kind >= 0.35) & (kind < 0.37)
+            amt[wide] = rng.integers(2**35, 2**40, size=int(wide.sum()), dtype=np.uint64)
+            t["amount"][:, 0] = amt
+            pend = (kind >= 0.37) & (kind < 0.5)
+            t["flags"][pend] |= 2
+            r = p.create_transfers(t, _split(n, rng, 8189))
+            assert (r["status"] == 0xFFFFFFFF).mean() > 0.9
         p.compare_state()
     finally:
         p.close()
@@ -144,19 +187,32 @@ def test_two_phase_config4_small():
     p = Pair(account_capacity=1 << 12, transfer_capacity=1 << 17, batch_events_max=1 << 15,
              pulse_batch_max=8190)
     try:
-        p.create_accounts(workload.accounts(1_000, seed=4))
+        acc = workload.accounts(1_000, seed=4)
+        acc["flags"][:8] |= 2  # the injected exceeds_credits failures debit these
+        p.create_accounts(acc)
         pending, seen = np.zeros(0, dtype=np.uint64), np.zeros(0, dtype=np.uint64)
+        resolved = np.zeros(0, dtype=np.uint64)
         offset = 0
+        seen_status = set()
         for step in range(6):
             t = workload.transfers_two_phase(8_000, 1_000, seed=40 + step, id_offset=offset,
-                                             prior_pending_ids=pending, prior_ids=seen)
+                                             prior_pending_ids=pending, prior_ids=seen,
+                                             prior_resolved_ids=resolved, n_limited=8)
             offset += 8_000
             r = p.create_transfers(t, [4_000, 4_000])
+            seen_status |= set(int(x) for x in r["status"])
             created = r["status"] == 0xFFFFFFFF
             is_pending = (t["flags"] & 2) != 0
+            pv = (t["flags"] & 12) != 0
             pending = np.concatenate([pending, t["id"][created & is_pending, 0]])[-5_000:]
+            resolved = np.concatenate([resolved, t["pending_id"][created & pv, 0]])[-5_000:]
             seen = np.concatenate([seen, t["id"][:, 0]])[-20_000:]
             p.tick(int(rng.integers(1, 3)) * NS_PER_S)
+        # injected failures: exceeds_credits, pending_transfer_already_posted / _voided,
+        # transfer_must_have_the_same_ledger_as_accounts, pending_transfer_has_different_amount
+        for st in (54, 24, 32):
+            assert st in seen_status, st
+        assert 33 in seen_status or 34 in seen_status
         p.compare_state()
     finally:
         p.close()
@@ -433,6 +489,57 @@ def test_account_lanes_free_owners(free_owners, monkeypatch):
                                  code=1))
             r = p.create_transfers(_transfers(rows), [len(rows)])
             assert (r["status"] == 0xFFFFFFFF).sum() > 0
+        p.compare_state()
+    finally:
+        p.close()
+
+
+@pytest.mark.parametrize("force_replay", [False, True, "serial"], ids=["parallel", "flow", "serial"])
+@pytest.mark.parametrize("length", [257, 8189])
+def test_long_linked_chains(length, force_replay):
+    """Linked chains longer than the flow replay's per-lane undo log (256 events: such a chain
+    runs as a barrier on the global undo log), up to a whole 8189-event batch
+    (state_machine.zig:3033-3207): a chain that persists, one whose last event fails (every
+    earlier event's balance deltas, statuses and ids undone, the failing id orphaned when the
+    failure is transient), one that fails in the middle on a repeated id (`exists` against the
+    chain's own earlier event), and one left open by the batch end (linked_event_chain_open)."""
+    p = Pair(account_capacity=64, transfer_capacity=1 << 17, batch_events_max=1 << 15,
+             force_replay=force_replay)
+    try:
+        acc = workload.accounts(16, seed=5, ledger=1)
+        acc["flags"] = 0
+        acc["flags"][0] = 2  # account 1: debits_must_not_exceed_credits
+        p.create_accounts(acc)
+        p.create_transfers(_transfers([dict(id=1, debit_account_id=2, credit_account_id=1,
+                                            amount=1000, ledger=1, code=1)]))
+        rng = np.random.default_rng(length)
+
+        def chain(first_id, n):
+            rows = []
+            for i in range(n):
+                dr, cr = (int(x) for x in rng.choice(np.arange(2, 17), size=2, replace=False))
+                rows.append(dict(id=first_id + i, debit_account_id=dr, credit_account_id=cr,
+                                 amount=int(rng.integers(1, 1000)), ledger=1, code=1,
+                                 flags=(1 if i < n - 1 else 0) | (2 if i % 7 == 3 else 0)))
+            return rows
+
+        a = chain(10_000, length)                        # persists
+        b = chain(20_000, length)                        # last event: exceeds_credits
+        b[-1].update(debit_account_id=1, amount=10**9)
+        c = chain(30_000, length)                        # middle event repeats an earlier id
+        c[length // 2] = dict(c[length // 3])
+        d = chain(40_000, length)                        # the batch ends inside the chain
+        d[-1]["flags"] |= 1
+        r = p.create_transfers(_transfers(a + b + c + d), [length] * 4)
+        st = r["status"]
+        assert (st[:length] == 0xFFFFFFFF).all()
+        assert st[2 * length - 1] == 54 and (st[length:2 * length - 1] == 1).all()
+        assert st[2 * length + length // 2] == 46  # exists (its own chain's earlier event)
+        assert st[4 * length - 1] == 2             # linked_event_chain_open
+        # The failed chains' ids are free again (the orphaned exceeds_credits id is not).
+        again = _transfers([dict(b[0], flags=0), dict(c[0], flags=0), dict(b[-1], flags=0)])
+        r = p.create_transfers(again)
+        assert list(r["status"]) == [0xFFFFFFFF, 0xFFFFFFFF, 68]  # 68: id_already_failed
         p.compare_state()
     finally:
         p.close()

@@ -99,6 +99,8 @@ struct tbg_ctx {
     unsigned int* bucket_words = nullptr;  // counts, cursors, offsets, slice bases
     uint64_t* bucket_partials = nullptr;   // per slice: kBucketKeys partial sums
     uint64_t bucket_slices_max = 0;
+    uint32_t* window_partials = nullptr;   // balance window: per workgroup, kWindowKeys u32 sums
+    unsigned long long* window_carry = nullptr;  // per window key (zero between calls)
     // account index build (cuckoo insertion + repair)
     uint32_t* idx_dirty = nullptr;
     unsigned int* idx_counters = nullptr;
@@ -264,6 +266,7 @@ Call<Event> make_call(tbg_ctx* ctx, const Event* d_events, uint32_t n, const uin
     c.force_replay = ctx->force_replay ? 1 : 0;
     c.bal_items = nullptr;
     c.key_bits = 0;
+    c.pair_shift = 0;
     c.bucket_counts = nullptr;
     c.n_buckets = 0;
     c.chunk_info = nullptr;
@@ -494,7 +497,7 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
             if (rc) return rc;
             HIP_TRY(ctx, hipcub::DeviceScan::InclusiveSum(ctx->cub_temp, pb, F.contrib, F.prefix,
                                                           pairs, ctx->stream));
-            hipLaunchKernelGGL(lanes_owner_free, dim3(grid_for(m)), block, 0, ctx->stream, ctx->T, L);
+            hipLaunchKernelGGL(lanes_owner_free, dim3(grid_for(2 * uint64_t(m))), block, 0, ctx->stream, ctx->T, L);
             hipLaunchKernelGGL(lanes_free, dim3(grid_for(m)), block, 0, ctx->stream, ctx->T, L);
         }
         hipLaunchKernelGGL(lanes_replay, dim3(1), dim3(kLanesMax), 0, ctx->stream, ctx->T, c, L);
@@ -694,7 +697,7 @@ int64_t lookup_impl(tbg_ctx* ctx, const tb_uint128_t* ids, uint32_t n, void* out
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     const uint32_t found = ctx->h_scalars->slow_count;
     if (found == 0) return 0;
-    void* d_out = ctx->d_events + size_t(n) * 16;  // after the ids (128 B per event available)
+    void* d_out = ctx->d_events + size_t(n) * 16;  // after the ids (144 B per event allocated)
     if (accounts)
         hipLaunchKernelGGL(gather_rows<tb_account_t>, dim3(grid_for(found)), dim3(kBlock), 0,
                            ctx->stream, ctx->T.acc_rows, d_rows, ctx->slow_list, found,
@@ -752,7 +755,8 @@ tbg_ctx* tbg_open(const tbg_options* options) {
          dev_alloc(ctx, &T.expiry, tr_cap, false) && dev_alloc(ctx, &ctx->d_scalars, 1, true);
     const uint64_t undo_cap = 3 * std::min<uint64_t>(ev_max, 65536);
     ok = ok && dev_alloc(ctx, &T.undo, undo_cap, false);
-    ok = ok && dev_alloc(ctx, &ctx->d_events, ev_max * 128, false) &&
+    // (144 B per event: tbg_lookup_* place n ids and up to n 128-B rows side by side)
+    ok = ok && dev_alloc(ctx, &ctx->d_events, ev_max * 144, false) &&
          dev_alloc(ctx, &ctx->d_results, ev_max, false) &&
          dev_alloc(ctx, &ctx->d_batch_ends, options->batch_count_max, false) &&
          dev_alloc(ctx, &ctx->d_batch_ts, options->batch_count_max, false) &&
@@ -767,7 +771,9 @@ tbg_ctx* tbg_open(const tbg_options* options) {
         ctx->bucket_slices_max = (2 * ev_max + kSliceItems - 1) / kSliceItems + kBucketsMax;
         ok = ok && dev_alloc(ctx, &ctx->bal_items_sorted, 2 * ev_max, false) &&
              dev_alloc(ctx, &ctx->bucket_words, 4 * (kBucketsMax + 1), true) &&
-             dev_alloc(ctx, &ctx->bucket_partials, ctx->bucket_slices_max * kBucketKeys, false);
+             dev_alloc(ctx, &ctx->bucket_partials, ctx->bucket_slices_max * kBucketKeys, false) &&
+             dev_alloc(ctx, &ctx->window_partials, uint64_t(kWindowGridMax) * kWindowKeys, false) &&
+             dev_alloc(ctx, &ctx->window_carry, kWindowKeys, true);
     }
     ok = ok && dev_alloc(ctx, &ctx->acc_ts_index, acc_cap, false) &&
          dev_alloc(ctx, &ctx->tr_ts_index, tr_cap, false) &&
@@ -807,6 +813,7 @@ void tbg_close(tbg_ctx* ctx) {
                     ctx->d_results, ctx->d_batch_ends, ctx->d_batch_ts, ctx->ev_slot, ctx->ev_dr,
                     ctx->ev_cr, ctx->ev_amount, ctx->ev_info, ctx->ev_slow, ctx->slow_list,
                     ctx->bal_items, ctx->chunk_info, ctx->bal_items_sorted, ctx->bucket_words, ctx->bucket_partials,
+                    ctx->window_partials, ctx->window_carry,
                     ctx->cub_temp, ctx->acc_ts_index, ctx->tr_ts_index, ctx->sel_buf,
                     ctx->pulse.keep, ctx->pulse.exp, ctx->pulse.ts, ctx->pulse.rows,
                     ctx->pulse.exp_b, ctx->pulse.rows_b, ctx->pulse.counters,
@@ -852,17 +859,24 @@ int tbg_create_transfers_device(tbg_ctx* ctx, const tb_transfer_t* d_events, uin
     const uint32_t key_end = uint32_t(4 * ctx->T.acc_rows_used);
     uint32_t key_bits = 1;
     while ((1ull << key_bits) <= key_end) key_bits++;
-    // Small key spaces (<= 262,144 accounts) take the bucketed path, whose LDS sums need
-    // amounts < 2^48 (key_bits >= 16); larger ones the radix sort + run reduction.
-    const bool use_buckets = use_sort && key_end <= kBucketsMax * kBucketKeys;
+    // Key spaces of <= 2^14 accounts take the balance window (pair items, LDS counters; config
+    // 2); up to 65,536 accounts the bucketed path, whose LDS sums need amounts < 2^48 (key_bits
+    // >= 16); larger ones the radix sort + run reduction.
+    uint32_t pair_shift = 1;
+    while ((1ull << pair_shift) < ctx->T.acc_rows_used) pair_shift++;
+    const bool use_window = use_sort && ctx->window_partials && pair_shift <= kWindowShiftMax &&
+                            !getenv("TBG_NO_WINDOW");
+    const bool use_buckets = use_sort && !use_window && key_end <= kBucketsMax * kBucketKeys;
     // Sparse key spaces (many more account fields than balance items, e.g. 125M accounts under
     // 1M-event calls): u128 atomics per item instead of the sort; collisions are rare.
-    const bool use_atomic = use_sort && !use_buckets && uint64_t(key_end) > kAtomicKeysPerItem * 2 * uint64_t(n);
+    const bool use_atomic = use_sort && !use_window && !use_buckets &&
+                            uint64_t(key_end) > kAtomicKeysPerItem * 2 * uint64_t(n);
     if (use_buckets && key_bits < 16) key_bits = 16;
     BucketPlan plan{};
     if (use_sort) {
         c.bal_items = ctx->bal_items;
         c.key_bits = key_bits;
+        if (use_window) c.pair_shift = pair_shift;
     }
     if (use_buckets && !rc) {
         plan.counts = ctx->bucket_words;
@@ -888,7 +902,20 @@ int tbg_create_transfers_device(tbg_ctx* ctx, const tb_transfer_t* d_events, uin
     }
     const int items = int(2 * uint64_t(n));
     const BalTarget target{ctx->T.acc_rows, ctx->T.acc_index, ctx->T.acc_entry_of};
-    if (!rc && use_buckets) {
+    if (!rc && use_window) {
+        // Balance deltas: pair items summed per workgroup in LDS counters, partials applied.
+        const uint32_t nwg = std::max<uint32_t>(1, std::min<uint32_t>(kWindowGridMax, n / 8192));
+        const uint32_t wkeys = std::min<uint32_t>(kWindowKeys, 4u << pair_shift);
+        hipLaunchKernelGGL(bal_window_accumulate, dim3(nwg), dim3(kWindowThreads), 0, ctx->stream,
+                           target, ctx->bal_items, n, pair_shift, wkeys, ctx->window_partials,
+                           ctx->window_carry);
+        tmark(ctx, "bal_window");
+        hipLaunchKernelGGL(bal_window_apply, dim3(grid_for(wkeys)), block, 0, ctx->stream, target,
+                           ctx->window_partials, nwg, pair_shift, wkeys, ctx->T.acc_rows_used,
+                           ctx->window_carry);
+        tmark(ctx, "bal_apply");
+        rc = hip_ok(ctx, hipGetLastError(), "launch") ? 0 : TBG_EHIP;
+    } else if (!rc && use_buckets) {
         // Balance deltas: bucket the packed items by key range, sum each slice in LDS, apply.
         hipLaunchKernelGGL(bal_bucket_plan, dim3(1), dim3(64), 0, ctx->stream, plan);
         hipLaunchKernelGGL(bal_bucket_scatter, dim3(uint32_t((items + kScatterTile - 1) / kScatterTile)),

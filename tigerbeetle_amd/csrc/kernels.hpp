@@ -227,6 +227,13 @@ __device__ inline uint8_t classify_after_lookup(const Tables& T, const Call<tb_t
     return kClassFast;
 }
 
+// Does a FAST event's amount fit its call's balance item(s)? (Else tr_commit adds it with u128
+// atomics.)
+__device__ inline bool item_packable(const Call<tb_transfer_t>& c, uint64_t amount) {
+    return c.pair_shift ? (amount >> (63 - 2 * c.pair_shift)) == 0
+                        : (amount >> (64 - c.key_bits)) == 0;
+}
+
 // One event of tr_ingest, `t` being the event as staged in LDS; returns the call flags it raises
 // (kFlag*). The row store is done by the caller (the whole wave's rows at once, coalesced).
 //
@@ -341,8 +348,7 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
     info |= cls;
     // A FAST event whose balance items are packed needs no per-event record: tr_commit decodes
     // the rows and amount from the items and re-probes the slot if it has to.
-    const bool lean = cls == kClassFast && c.bal_items &&
-                      (t.amount.lo >> (64 - c.key_bits)) == 0;
+    const bool lean = cls == kClassFast && c.bal_items && item_packable(c, t.amount.lo);
     c.ev_info[k] = info | (lean ? kInfoLean : 0);
     if (!lean) {
         c.ev_slot[k] = slot == kNone ? kNone32 : uint32_t(slot);
@@ -370,7 +376,16 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
         res.reserved = 0;
         c.results[k] = res;
         if (pending && t.timeout > 0) need_commit = true;  // expires_at index
-        if (c.bal_items) {
+        if (c.bal_items && c.pair_shift) {
+            const uint32_t ps = c.pair_shift;
+            if (item_packable(c, amount)) {
+                c.bal_items[k] = (amount << (2 * ps + 1)) | (uint64_t(pending) << (2 * ps)) |
+                                 (uint64_t(cr.row) << ps) | dr.row;
+            } else {
+                c.bal_items[k] = ~0ull;  // too wide to pack: atomics in tr_commit
+                need_commit = true;
+            }
+        } else if (c.bal_items) {
             uint4* it = reinterpret_cast<uint4*>(c.bal_items + 2 * uint64_t(k));
             if ((amount >> (64 - c.key_bits)) == 0) {
                 const uint32_t kd = dr.row * 4 + (pending ? 0 : 1);
@@ -411,7 +426,9 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
     }
     if (cls != kClassFast) {
         need_commit = true;
-        if (c.bal_items)
+        if (c.bal_items && c.pair_shift)
+            c.bal_items[k] = ~0ull;
+        else if (c.bal_items)
             *reinterpret_cast<uint4*>(c.bal_items + 2 * uint64_t(k)) = make_uint4(~0u, ~0u, ~0u, ~0u);
     }
     return (imported ? kFlagImported : 0u) | (post_void ? kFlagPostVoid : 0u) |
@@ -591,7 +608,13 @@ __device__ inline void commit_event(const Tables& T, const Call<tb_transfer_t>& 
         uint32_t s = kNone32, dr, cr;
         uint64_t amount;
         const bool lean = (info & kInfoLean) != 0;
-        if (lean) {
+        if (lean && c.pair_shift) {
+            const uint32_t ps = c.pair_shift;
+            const uint64_t x = c.bal_items[k];
+            dr = uint32_t(x & ((1ull << ps) - 1));
+            cr = uint32_t((x >> ps) & ((1ull << ps) - 1));
+            amount = x >> (2 * ps + 1);
+        } else if (lean) {
             const uint64_t kmask = (1ull << c.key_bits) - 1;
             const uint64_t* it = c.bal_items + 2 * uint64_t(k);
             const uint64_t i0 = it[0], i1 = it[1];
@@ -621,7 +644,9 @@ __device__ inline void commit_event(const Tables& T, const Call<tb_transfer_t>& 
             // Demoted: undo the speculative liveness and balance items; the replay decides.
             slow = true;
             T.tr_live[row] = 0;
-            if (c.bal_items) {
+            if (c.bal_items && c.pair_shift) {
+                c.bal_items[k] = ~0ull;
+            } else if (c.bal_items) {
                 uint64_t* it = c.bal_items + 2 * uint64_t(k);
                 it[0] = ~0ull;
                 it[1] = ~0ull;
@@ -635,7 +660,7 @@ __device__ inline void commit_event(const Tables& T, const Call<tb_transfer_t>& 
             applied = true;
             ts_applied = c.results[k].timestamp;
             const bool pending = (info & kInfoPending) != 0;
-            if (amount && (!c.bal_items || (amount >> (64 - c.key_bits)) != 0)) {
+            if (amount && (!c.bal_items || !item_packable(c, amount))) {
                 if (atomic_add_u128(account_field(T.acc_rows, dr * 4 + (pending ? 0 : 1)),
                                     amount) >= kHazardHiLimit)
                     acc_hazard_set(T.acc_index, T.acc_entry_of, dr, kHazardHigh);
@@ -843,6 +868,122 @@ __global__ void bal_atomic_apply(BalTarget rows, const uint64_t* items, uint64_t
         const uint64_t key = it[j] & kmask;
         if (key < key_end) add_field(rows, uint32_t(key), it[j] >> key_bits, true);
     }
+}
+
+// ---- the balance window path (key spaces of <= 2^14 accounts, e.g. config 2) -----
+//
+// Pair items (Call::pair_shift = s): one u64 per FAST event carries both accounts, the pending bit
+// and the amount. Fields are keyed field-major, key = f << s | row with f = 0 debits_posted,
+// 1 credits_posted, 2 debits_pending, 3 credits_pending: the posted fields of up to 2^14 accounts
+// fall in the first kWindowKeys keys. bal_window_accumulate: one workgroup per CU sums a
+// contiguous slice of the items into u32 LDS counters (the window; the u32 carries of a returning
+// LDS add, and amount bits above 32, go to a per-key u64 `carry` word with a global atomic --
+// never for config 2), fields outside the window with u128 atomics on the row; then writes its
+// counters as u32 partials. bal_window_apply: one lane per window key sums the partials and the
+// carry in u128 and adds them to the row field (plain read-modify-write: one lane per field).
+// Item traffic: 8 B written by ingest and read once, plus 4 B per window key per workgroup.
+
+constexpr uint32_t kWindowKeys = 32768;  // u32 counters: 128 KB of LDS
+constexpr uint32_t kWindowThreads = 1024;
+constexpr uint32_t kWindowGridMax = 256;  // one workgroup per CU
+constexpr uint32_t kWindowShiftMax = 14;
+
+// Byte offset in the Account row of window field f (see above).
+__device__ inline uint32_t window_field_offset(uint32_t f) {
+    return f == 0 ? 32 : f == 1 ? 64 : f == 2 ? 16 : 48;
+}
+
+__device__ inline void window_field_add(const BalTarget& B, uint32_t row, uint32_t f, u128 sum,
+                                        bool shared) {
+    if (sum == 0) return;
+    tb_uint128_t* field = reinterpret_cast<tb_uint128_t*>(
+        reinterpret_cast<uint8_t*>(&B.rows[row]) + window_field_offset(f));
+    uint64_t hi;
+    if (shared) {
+        hi = atomic_add_u128(field, sum);
+    } else {
+        const tb_uint128_t v = W(U(*field) + sum);
+        *field = v;
+        hi = v.hi;
+    }
+    if (hi >= kHazardHiLimit) acc_hazard_set(B.index, B.entry_of, row, kHazardHigh);
+}
+
+__global__ void __launch_bounds__(kWindowThreads) bal_window_accumulate(
+    BalTarget B, const uint64_t* items, uint32_t n, uint32_t ps, uint32_t wkeys,
+    uint32_t* partials, unsigned long long* carry) {
+    __shared__ uint32_t acc[kWindowKeys];
+    for (uint32_t i = threadIdx.x; i < wkeys; i += kWindowThreads) acc[i] = 0;
+    __syncthreads();
+    const uint32_t per = ((n + gridDim.x - 1) / gridDim.x + 1) & ~1u;  // even: uint4 loads
+    const uint32_t b0 = blockIdx.x * per;
+    const uint32_t b1 = b0 + per < n ? b0 + per : n;
+    const uint64_t rmask = (1ull << ps) - 1;
+    auto add = [&](uint32_t f, uint32_t row, uint64_t amount) {
+        const uint32_t key = (f << ps) | row;
+        if (key < wkeys) {
+            const uint32_t lo = uint32_t(amount);
+            const uint32_t old = atomicAdd(&acc[key], lo);
+            const uint64_t hi = (amount >> 32) + (uint32_t(old + lo) < old ? 1 : 0);
+            if (hi) atomicAdd(&carry[key], (unsigned long long)hi);
+        } else {
+            window_field_add(B, row, f, amount, true);
+        }
+    };
+    auto item = [&](uint64_t x) {
+        if (x == ~0ull) return;
+        const uint32_t dr = uint32_t(x & rmask), cr = uint32_t((x >> ps) & rmask);
+        const uint32_t pend = uint32_t(x >> (2 * ps)) & 1u;
+        const uint64_t amount = x >> (2 * ps + 1);
+        add(pend ? 2 : 0, dr, amount);
+        add(pend ? 3 : 1, cr, amount);
+    };
+    // Two items per lane per load, four loads in flight.
+    uint32_t i = b0 + 2 * threadIdx.x;
+    constexpr uint32_t kStep = 2 * kWindowThreads;
+    for (; i + 3 * kStep + 1 < b1; i += 4 * kStep) {
+        uint4 q[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) q[j] = *reinterpret_cast<const uint4*>(items + i + j * kStep);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            item((uint64_t(q[j].y) << 32) | q[j].x);
+            item((uint64_t(q[j].w) << 32) | q[j].z);
+        }
+    }
+    for (; i < b1; i += kStep) {
+        item(items[i]);
+        if (i + 1 < b1) item(items[i + 1]);
+    }
+    __syncthreads();
+    uint32_t* out = partials + uint64_t(blockIdx.x) * wkeys;
+    for (uint32_t k = threadIdx.x; k < wkeys; k += kWindowThreads) out[k] = acc[k];
+}
+
+__global__ void bal_window_apply(BalTarget B, const uint32_t* partials, uint32_t nwg,
+                                 uint32_t ps, uint32_t wkeys, uint64_t rows_used,
+                                 unsigned long long* carry) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= wkeys) return;
+    const uint32_t row = k & ((1u << ps) - 1), f = k >> ps;
+    if (row >= rows_used) return;
+    uint64_t s = 0;
+    uint32_t w = 0;
+    for (; w + 8 <= nwg; w += 8) {
+        uint32_t x[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) x[j] = partials[uint64_t(w + j) * wkeys + k];
+#pragma unroll
+        for (int j = 0; j < 8; j++) s += x[j];
+    }
+    for (; w < nwg; w++) s += partials[uint64_t(w) * wkeys + k];
+    u128 sum = s;
+    const unsigned long long c = carry[k];
+    if (c) {
+        sum += u128(c) << 32;
+        carry[k] = 0;
+    }
+    window_field_add(B, row, f, sum, false);
 }
 
 // ---- the bucketed balance path ------------------------------------------------

@@ -230,10 +230,17 @@ __global__ void lanes_free(Tables T, LanePlan L) {
 __global__ void __launch_bounds__(kLanesMax) lanes_replay(Tables T, Call<tb_transfer_t> c,
                                                           LanePlan L) {
     __shared__ uint32_t mbox[kLaneMbWords];
+    // Steps finished by any lane of the workgroup: the watchdog counts a lane's idle polls only
+    // while no lane progresses (a lane waiting on a verdict that sits late in a hot owner's walk
+    // may poll for as long as that walk takes).
+    __shared__ unsigned int progress;
     const uint32_t owners = L.counts[0];
     if (L.counts[1] != 0 || owners == 0 || owners > kLanesMax) return;  // the flow replay runs
     const uint32_t o = threadIdx.x;
-    if (o == 0) L.counts[2] = 1;
+    if (o == 0) {
+        L.counts[2] = 1;
+        progress = 0;
+    }
     for (uint32_t i = o; i < kLaneMbWords; i += blockDim.x) mbox[i] = 0;
     __syncthreads();
     bool alive = o < owners;
@@ -293,14 +300,22 @@ __global__ void __launch_bounds__(kLanesMax) lanes_replay(Tables T, Call<tb_tran
     }
     alive = alive && ring_ok[0];
     uint64_t spins = 0;
+    unsigned int seen_progress = 0;
     // The ring is consumed in place: slot q holds the record of every step t with t % kAhead == q,
     // and the loop body is unrolled over the slots (constant indices keep the rings in registers).
     // Moving ring entries instead would wait for every outstanding load at each step.
     uint32_t phase = 0;  // the slot of this lane's current step
     while (__any(alive)) {
-        if (alive && ++spins > kFlowSpinLimit) {  // watchdog (a bug): fail the call
-            atomicOr(&T.scalars->flags, kFlagFlowStalled);
-            alive = false;
+        if (alive && ++spins > kFlowSpinLimit) {
+            const unsigned int p = __hip_atomic_load(&progress, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (p != seen_progress) {
+                seen_progress = p;
+                spins = 0;
+            } else {  // watchdog (a bug): no lane progressed for kFlowSpinLimit polls
+                atomicOr(&T.scalars->flags, kFlagFlowStalled);
+                alive = false;
+            }
         }
 #pragma unroll
         for (uint32_t q = 0; q < kAhead; q++) {
@@ -357,6 +372,7 @@ __global__ void __launch_bounds__(kLanesMax) lanes_replay(Tables T, Call<tb_tran
                         created ? kOutCreated : (dr_fail ? kOutExceedsCredits : kOutExceedsDebits);
                     published = false;
                     spins = 0;
+                    atomicAdd(&progress, 1u);
                     // Refill the slot with the step kAhead later (its pair was loaded kAhead steps
                     // ago) and load the pair of the step 2 * kAhead later.
                     const auto t = take_pair(q);
@@ -413,7 +429,8 @@ __global__ void lanes_finish(Tables T, Call<tb_transfer_t> c, LanePlan L) {
     uint64_t ts_max = 0;
     uint32_t dr_key = kNone32, cr_key = kNone32;
     uint64_t amount = 0;
-    if (s < L.m && L.counts[2]) {
+    // (a stalled walk fails the call: its outcomes are incomplete)
+    if (s < L.m && L.counts[2] && !(T.scalars->flags & kFlagFlowStalled)) {
         const Step st = L.steps[s];
         const LaneRec rec = L.recs[s];
         const uint8_t out = L.outcome[s];

@@ -115,6 +115,9 @@ struct Call {
     // credit delta of event k, packed as (amount << key_bits) | account field key; ~0 = none.
     uint64_t* bal_items;
     uint32_t key_bits;
+    // Pair items (the balance window path, key spaces of <= 2^14 accounts): pair_shift = s > 0,
+    // one item per event, (amount << 2s + 1) | (pending << 2s) | (cr << s) | dr; ~0 = none.
+    uint32_t pair_shift;
     // Bucketed balance path (small key spaces): per-bucket item counts, bucket = key >> 13.
     unsigned int* bucket_counts;
     uint32_t n_buckets;

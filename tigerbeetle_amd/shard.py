@@ -406,14 +406,34 @@ class ShardGroup:
             ts = self._recv(0, np.uint64)
             mine = (ev, ln.tolist(), ts)
         res = np.zeros(0, dtype=RESULT_DTYPE)
+        failure = None
         if len(mine[0]):
             fn = (self.executor.create_accounts if kind == "accounts"
                   else self.executor.create_transfers)
-            res = fn(np.ascontiguousarray(mine[0]), mine[1], mine[2])
+            try:
+                res = fn(np.ascontiguousarray(mine[0]), mine[1], mine[2])
+            except Exception as e:  # noqa: BLE001 -- every rank must learn of it (below)
+                failure = e
+                res = np.zeros(0, dtype=RESULT_DTYPE)
+        # Every rank reports a status word with its results, and every rank learns whether any
+        # shard failed: a rank whose executor raised (capacity, watchdog) still answers, so no
+        # rank blocks in a receive. After such a failure the shards' state is undefined.
         if self.rank != 0:
+            self._send(np.asarray([0 if failure is None else 1], dtype=np.int64), 0)
             self._send(res, 0)
+        else:
+            statuses = [0 if failure is None else 1]
+            outs = [res]
+            for s in range(1, self.world):
+                statuses.append(int(self._recv(s, np.int64)[0]))
+                outs.append(self._recv(s, RESULT_DTYPE))
+        failed = self._bcast(max(statuses) if self.rank == 0 else 0)
+        if failed:
+            if failure is not None:
+                raise failure
+            raise RuntimeError("a shard's executor failed; the shards' state is undefined")
+        if self.rank != 0:
             return None
-        outs = [res] + [self._recv(s, RESULT_DTYPE) for s in range(1, self.world)]
         results = gather_results(plan, outs, len(events))
         self.router.commit(plan, events, results)
         return results

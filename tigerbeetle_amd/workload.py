@@ -135,11 +135,28 @@ def hot_funding_amounts(t: np.ndarray, n_hot: int = 100, fraction: float = 0.8) 
 def transfers_two_phase(n: int, n_accounts: int, seed: int, id_offset: int,
                         prior_pending_ids: np.ndarray, pending_ratio=0.3, chain_ratio=0.3,
                         chain_len=8, fail_ratio=0.1, resubmit_ratio=0.01,
-                        prior_ids: np.ndarray = None) -> np.ndarray:
-    """Config 4: pending with timeouts, post/void of earlier pending transfers, linked chains
-    with injected failures, and resubmitted ids."""
+                        prior_ids: np.ndarray = None, prior_resolved_ids: np.ndarray = None,
+                        n_limited: int = 0) -> np.ndarray:
+    """Config 4: pending transfers with 1-5 s timeouts; posts (67%: half of them
+    the full amount via maxInt, half a quarter of it) and voids (33%: 70% amount 0, 30% a nonzero
+    amount, which fails with pending_transfer_has_different_amount when below the pending amount)
+    of earlier pending transfers; 8-event linked chains on `chain_ratio` of the events, a
+    `fail_ratio` of them with one injected failure at a random position -- a missing account, a
+    ledger mismatch, `exceeds_credits` (a debit of one of the `n_limited` accounts 1..n_limited,
+    which the caller creates with debits_must_not_exceed_credits, far beyond its credits; needs
+    n_limited > 0) or a post of a pending transfer already posted or voided (`prior_resolved_ids`)
+    -- and `resubmit_ratio` of ids resubmitted (exists / id_already_failed)."""
     rng = np.random.default_rng(seed)
     t = transfers_uniform(n, n_accounts, seed=seed, id_offset=id_offset)
+    if n_limited:  # plain transfers never touch the limited accounts (their failures are injected)
+        for col in ("debit_account_id", "credit_account_id"):
+            low = t[col][:, 0] <= U64(n_limited)
+            t[col][low, 0] = rng.integers(n_limited + 1, n_accounts + 1, size=int(low.sum()),
+                                          dtype=np.int64).astype(U64)
+        same = t["debit_account_id"][:, 0] == t["credit_account_id"][:, 0]
+        t["credit_account_id"][same, 0] = np.where(
+            t["credit_account_id"][same, 0] < U64(n_accounts), t["credit_account_id"][same, 0] + U64(1),
+            U64(n_limited + 1))
     kind = rng.random(n)
     pend = kind < pending_ratio
     t["flags"][pend] |= int(TransferFlags.pending)
@@ -154,25 +171,56 @@ def transfers_two_phase(n: int, n_accounts: int, seed: int, id_offset: int,
         t["pending_id"][idx, 0] = pick
         t["pending_id"][idx, 1] = 0
         # Post: amount maxInt half the time (post the full pending amount), else <= pending.
+        # Void: amount 0 (the pending amount) 70% of the time, else a nonzero amount.
         full = rng.random(len(idx)) < 0.5
+        void_amount = rng.random(len(idx)) < 0.3
         amt = t["amount"][idx, 0]
         t["amount"][idx, 0] = np.where(post & full, np.uint64(2**64 - 1),
-                                       np.where(post, amt // 4, 0))
+                                       np.where(post | void_amount, amt // 4, 0))
         t["amount"][idx, 1] = np.where(post & full, np.uint64(2**64 - 1), 0)
         t["debit_account_id"][idx] = 0
         t["credit_account_id"][idx] = 0
         t["ledger"][idx] = 0
         t["code"][idx] = 0
         t["timeout"][idx] = 0
-    # Linked chains of `chain_len` events.
+    # Linked chains of `chain_len` events, some with an injected failure.
     n_chains = int(n * chain_ratio / chain_len)
     starts = rng.choice(max(n - chain_len, 1), size=n_chains, replace=False) if n > chain_len else []
+    kinds = ["missing", "ledger"] + (["exceeds_credits"] if n_limited else []) + \
+            (["resolved"] if prior_resolved_ids is not None and len(prior_resolved_ids) else [])
     for s in sorted(starts):
         t["flags"][s:s + chain_len - 1] |= int(TransferFlags.linked)
         t["flags"][s + chain_len - 1] &= ~np.uint16(int(TransferFlags.linked))
         if rng.random() < fail_ratio:
             j = s + int(rng.integers(0, chain_len))
-            t["debit_account_id"][j, 0] = n_accounts + 1000  # missing account
+            what = kinds[int(rng.integers(0, len(kinds)))]
+            if what == "missing":
+                t["debit_account_id"][j] = [n_accounts + 1000, 0]
+            elif what == "ledger":
+                t["ledger"][j] = t["ledger"][j] + 1
+                if (t["flags"][j] & (int(TransferFlags.post_pending_transfer) |
+                                     int(TransferFlags.void_pending_transfer))):
+                    t["ledger"][j] = 7  # pending_transfer_has_different_ledger
+            elif what == "exceeds_credits":
+                f = int(t["flags"][j]) & int(TransferFlags.linked)
+                t["flags"][j] = f
+                t["pending_id"][j] = 0
+                t["timeout"][j] = 0
+                t["code"][j] = 1
+                t["ledger"][j] = 2
+                t["debit_account_id"][j] = [1 + int(rng.integers(0, n_limited)), 0]
+                t["credit_account_id"][j] = [n_limited + 1 + int(rng.integers(0, n_accounts - n_limited)), 0]
+                t["amount"][j] = [2**40, 0]
+            else:  # post of a pending transfer that was already posted or voided
+                f = int(t["flags"][j]) & int(TransferFlags.linked)
+                t["flags"][j] = f | int(TransferFlags.post_pending_transfer)
+                t["pending_id"][j] = [int(prior_resolved_ids[rng.integers(0, len(prior_resolved_ids))]), 0]
+                t["amount"][j] = [2**64 - 1, 2**64 - 1]
+                t["debit_account_id"][j] = 0
+                t["credit_account_id"][j] = 0
+                t["ledger"][j] = 0
+                t["code"][j] = 0
+                t["timeout"][j] = 0
     # Resubmitted ids.
     if prior_ids is not None and len(prior_ids):
         m = int(n * resubmit_ratio)
@@ -265,18 +313,19 @@ def accounts_config5(j: np.ndarray, rank: int, world: int) -> np.ndarray:
     history; user data a fixed function of the id, so any subset is reproducible)."""
     k = config5_global_index(j, rank, world)
     n = len(k)
-    a = np.zeros(n, dtype=ACCOUNT_DTYPE)
+    # Written through a (n, 16) u64 view of the records (word w = bytes 8w..8w+7).
+    w = np.zeros((n, 16), dtype=U64)
     ids = (k + 1).astype(U64)
-    _u128_col(a, "id", ids)
+    w[:, 0] = ids                                              # id (lo)
     with np.errstate(over="ignore"):
-        a["user_data_128"][:, 0] = ids * U64(0x9E3779B97F4A7C15)
-        a["user_data_128"][:, 1] = ids * U64(0xC2B2AE3D27D4EB4F)
-        a["user_data_64"] = ids * U64(0x165667B19E3779F9)
-    a["user_data_32"] = (ids & U64(0xFFFFFFFF)).astype(np.uint32)
-    a["ledger"] = (1 + (k % LEDGERS_CONFIG5)).astype(np.uint32)
-    a["code"] = 1
-    a["flags"] = int(AccountFlags.history)
-    return a
+        w[:, 10] = ids * U64(0x9E3779B97F4A7C15)               # user_data_128
+        w[:, 11] = ids * U64(0xC2B2AE3D27D4EB4F)
+        w[:, 12] = ids * U64(0x165667B19E3779F9)               # user_data_64
+    w[:, 13] = ids & U64(0xFFFFFFFF)                           # user_data_32, reserved 0
+    # ledger (u32) | code (u16) << 32 | flags (u16) << 48
+    w[:, 14] = ((1 + (k % LEDGERS_CONFIG5)).astype(U64) | (U64(1) << U64(32)) |
+                (U64(int(AccountFlags.history)) << U64(48)))
+    return w.view(ACCOUNT_DTYPE).reshape(n)
 
 
 def transfers_config5(n: int, accounts_per_shard: int, rank: int, world: int, seed: int = 42,

@@ -9,10 +9,11 @@ line per config with the GPU and oracle rates over the create_transfers calls.
   config3: 10k accounts, 100 hot accounts with debits_must_not_exceed_credits (Zipf 0.99 over the
            hot set takes 90% of debits, ~10% of credits go to hot accounts), funded from an
            unlimited source; 8189-event batches, `--batches` per commit.
-  config4: 10k accounts; 30% pending with 1-5 s timeouts, later post (67%) / void (33%) of earlier
-           pending transfers, 8-event linked chains on 30% of events with a missing account
-           injected into 10% of chains, 1% resubmitted ids; 1-2 s ticks with pulses between
-           commits.
+  config4: 10k accounts; 30% pending with 1-5 s timeouts, later post (67%, full or partial) /
+           void (33%, amount 0 or nonzero) of earlier pending transfers, 8-event linked chains on
+           30% of events with one injected failure in 10% of chains (missing account, ledger
+           mismatch, exceeds_credits, post of an already posted / voided transfer), 1%
+           resubmitted ids; 1-2 s ticks with pulses between commits.
 Usage: python tools/bench_configs.py [--transfers N] [--configs 3,4]
 """
 import argparse
@@ -96,21 +97,27 @@ def config4(n, commits_batches):
     p = Pair(account_capacity=1 << 14, transfer_capacity=n + (1 << 12),
              batch_events_max=BATCH * commits_batches, batch_count_max=commits_batches)
     try:
-        p.create_accounts(workload.accounts(A, seed=4))
+        acc = workload.accounts(A, seed=4)
+        acc["flags"][:16] |= 2  # debited only by injected exceeds_credits failures
+        p.create_accounts(acc)
         p.seconds = {"gpu": 0.0, "oracle": 0.0}
         p.lib.tbg_profile(p.g, 1)
         pending, seen = np.zeros(0, dtype=np.uint64), np.zeros(0, dtype=np.uint64)
+        resolved = np.zeros(0, dtype=np.uint64)
         per_commit = BATCH * commits_batches
         off, step = 0, 0
         while off < n:
             m = min(per_commit, n - off)
             t = workload.transfers_two_phase(m, A, seed=40 + step, id_offset=off,
-                                             prior_pending_ids=pending, prior_ids=seen)
+                                             prior_pending_ids=pending, prior_ids=seen,
+                                             prior_resolved_ids=resolved, n_limited=16)
             lens = [BATCH] * (m // BATCH) + ([m % BATCH] if m % BATCH else [])
             r = p.create_transfers(t, lens)
             created = r["status"] == 0xFFFFFFFF
             is_pending = (t["flags"] & 2) != 0
             pending = np.concatenate([pending, t["id"][created & is_pending, 0]])[-50_000:]
+            pv = (t["flags"] & 12) != 0
+            resolved = np.concatenate([resolved, t["pending_id"][created & pv, 0]])[-50_000:]
             seen = np.concatenate([seen, t["id"][:, 0]])[-200_000:]
             p.tick(int(rng.integers(1, 3)) * NS_PER_S)
             off += m
