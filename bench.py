@@ -79,6 +79,10 @@ def parse_args():
                     help="bounded CPU-oracle sample (rank 0, N=1)")
     ap.add_argument("--commit-reps", type=int, default=200,
                     help="8189-event commits timed for `per_commit` (0: skip)")
+    ap.add_argument("--account-events", action="store_true",
+                    help="record AccountEvents (the account_events groove, 256 B per created "
+                         "transfer) inside the timed steps; SURVEY.md §8d excludes them from the "
+                         "headline's algorithmic bytes")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-validate", action="store_true")
     return ap.parse_args()
@@ -424,6 +428,7 @@ def per_commit(args, lib, dev, g, wl, prepare_ts, id_base):
     topt.pulse_batch_max = 8190
     topt.device = 0
     topt.pulse_next_timestamp_init = 1
+    topt.account_events_capacity = (R + 2) * n  # the drop-in records AccountEvents (CDC)
     sm = lib.tb_sm_open_gpu(ctypes.byref(sm_opt), ctypes.byref(topt))
     if not sm:
         return {"device": device, "state_machine": None}, prepare_ts
@@ -484,7 +489,8 @@ def per_commit(args, lib, dev, g, wl, prepare_ts, id_base):
            "us_per_commit_p50": round(float(np.median(lat_sm)) * 1e6, 1),
            "body_bytes": len(bodies[0]), "validated": sm_ok,
            "note": "tb_sm_prepare + tb_sm_prefetch + tb_sm_commit per 8189-event multi-batch "
-                   "body on host buffers (body in and reply out over PCIe)"}
+                   "body on host buffers (body in and reply out over PCIe), AccountEvents "
+                   "recorded"}
     return {"device": device, "state_machine": smr}, prepare_ts
 
 
@@ -511,6 +517,7 @@ def main():
     opt.pulse_batch_max = 8190
     opt.device = local
     opt.pulse_next_timestamp_init = 1
+    opt.account_events_capacity = N * (K + W + 1) + R * BATCH if args.account_events else 0
     g = lib.tbg_open(ctypes.byref(opt))
     assert g, "tbg_open failed"
 
@@ -681,7 +688,8 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": "u128",
             "data": "synthetic (seeded; benchmark_load.zig distributions, sequential ids)",
             "config": dict(wl.config, batches_per_step=int(len(lens)),
-                           parallelism=f"ledger-shard x{world}"),
+                           parallelism=f"ledger-shard x{world}",
+                           account_events=bool(args.account_events)),
             "validated": validated,
             "validation": validation,
             "replayed_events_last_step": int(stats.replayed),

@@ -3,7 +3,8 @@
  *
  * Mirrors `StateMachineType(Storage)` (src/state_machine.zig:222-2958) as consumed by
  * `ReplicaType(StateMachine, ...)` (src/vsr/replica.zig:144-152) for the operations of this path:
- * pulse, create_accounts, create_transfers, lookup_accounts, lookup_transfers. Bodies are
+ * pulse, create_accounts, create_transfers, lookup_accounts, lookup_transfers and
+ * get_change_events (the account_events groove's reader, CDC). Bodies are
  * multi-batch encoded exactly as src/vsr/multi_batch.zig; replies are multi-batch encoded the
  * same way. The executor underneath is pluggable (tb_executor): the product binds the HIP
  * executor (tbg.h) with tb_sm_open_gpu; tests may bind another executor with the same semantics.
@@ -30,6 +31,7 @@ extern "C" {
 /* Operation numbers (src/tigerbeetle.zig:685-716, vsr_operations_reserved = 128). */
 enum {
     TB_OPERATION_PULSE = 128,
+    TB_OPERATION_GET_CHANGE_EVENTS = 137,
     TB_OPERATION_LOOKUP_ACCOUNTS = 140,
     TB_OPERATION_LOOKUP_TRANSFERS = 141,
     TB_OPERATION_CREATE_ACCOUNTS = 146,
@@ -50,6 +52,9 @@ typedef struct tb_executor {
     int64_t (*lookup_accounts)(void* self, const tb_uint128_t* ids, uint32_t n, tb_account_t* out);
     int64_t (*lookup_transfers)(void* self, const tb_uint128_t* ids, uint32_t n,
                                 tb_transfer_t* out);
+    /* ChangeEvents of the filter, at most min(filter->limit, limit_max); 0 if invalid. */
+    int64_t (*get_change_events)(void* self, const tb_change_events_filter_t* filter,
+                                 uint32_t limit_max, tb_change_event_t* out);
 } tb_executor;
 
 typedef struct tb_sm tb_sm;

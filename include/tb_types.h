@@ -67,6 +67,93 @@ typedef struct tb_create_result {
     uint32_t reserved;
 } tb_create_result_t;
 
+/* AccountEvent, src/state_machine.zig:104-220 -- 256 bytes, align 16, no padding: one per
+ * created transfer, post/void and expiry, with both accounts' balances and flags as they stand
+ * after the event (account_event, :4384-4465). The groove `account_events` stores it; CDC reads it
+ * back through get_change_events. */
+typedef struct tb_account_event {
+    tb_uint128_t dr_account_id;
+    tb_uint128_t dr_debits_pending;
+    tb_uint128_t dr_debits_posted;
+    tb_uint128_t dr_credits_pending;
+    tb_uint128_t dr_credits_posted;
+    tb_uint128_t cr_account_id;
+    tb_uint128_t cr_debits_pending;
+    tb_uint128_t cr_debits_posted;
+    tb_uint128_t cr_credits_pending;
+    tb_uint128_t cr_credits_posted;
+    uint64_t timestamp;
+    uint64_t dr_account_timestamp;
+    uint64_t cr_account_timestamp;
+    uint16_t dr_account_flags;
+    uint16_t cr_account_flags;
+    uint16_t transfer_flags;
+    uint16_t transfer_pending_flags;
+    tb_uint128_t transfer_pending_id;
+    tb_uint128_t amount_requested;
+    tb_uint128_t amount;
+    uint32_t ledger;
+    uint8_t transfer_pending_status; /* TB_PENDING_* of the event (expired: an expiry) */
+    uint8_t reserved[11];
+} tb_account_event_t;
+
+/* ChangeEventType, src/tigerbeetle.zig:614-620. */
+enum {
+    TB_CHANGE_SINGLE_PHASE = 0,
+    TB_CHANGE_TWO_PHASE_PENDING = 1,
+    TB_CHANGE_TWO_PHASE_POSTED = 2,
+    TB_CHANGE_TWO_PHASE_VOIDED = 3,
+    TB_CHANGE_TWO_PHASE_EXPIRED = 4,
+};
+
+/* ChangeEvent, src/tigerbeetle.zig:622-670 -- 384 bytes (a transfer + 2 accounts), align 16. */
+typedef struct tb_change_event {
+    tb_uint128_t transfer_id;
+    tb_uint128_t transfer_amount;
+    tb_uint128_t transfer_pending_id;
+    tb_uint128_t transfer_user_data_128;
+    uint64_t transfer_user_data_64;
+    uint32_t transfer_user_data_32;
+    uint32_t transfer_timeout;
+    uint16_t transfer_code;
+    uint16_t transfer_flags;
+    uint32_t ledger;
+    uint8_t type;
+    uint8_t reserved[39];
+    tb_uint128_t debit_account_id;
+    tb_uint128_t debit_account_debits_pending;
+    tb_uint128_t debit_account_debits_posted;
+    tb_uint128_t debit_account_credits_pending;
+    tb_uint128_t debit_account_credits_posted;
+    tb_uint128_t debit_account_user_data_128;
+    uint64_t debit_account_user_data_64;
+    uint32_t debit_account_user_data_32;
+    uint16_t debit_account_code;
+    uint16_t debit_account_flags;
+    tb_uint128_t credit_account_id;
+    tb_uint128_t credit_account_debits_pending;
+    tb_uint128_t credit_account_debits_posted;
+    tb_uint128_t credit_account_credits_pending;
+    tb_uint128_t credit_account_credits_posted;
+    tb_uint128_t credit_account_user_data_128;
+    uint64_t credit_account_user_data_64;
+    uint32_t credit_account_user_data_32;
+    uint16_t credit_account_code;
+    uint16_t credit_account_flags;
+    uint64_t timestamp;
+    uint64_t transfer_timestamp;
+    uint64_t debit_account_timestamp;
+    uint64_t credit_account_timestamp;
+} tb_change_event_t;
+
+/* ChangeEventsFilter, src/tigerbeetle.zig:672-682 -- 64 bytes. */
+typedef struct tb_change_events_filter {
+    uint64_t timestamp_min; /* 0: timestamp_min */
+    uint64_t timestamp_max; /* 0: timestamp_max */
+    uint32_t limit;
+    uint8_t reserved[44];
+} tb_change_events_filter_t;
+
 /* AccountFlags, src/tigerbeetle.zig:45-68 (packed struct(u16), LSB first). */
 enum {
     TB_ACCOUNT_LINKED = 1u << 0,
@@ -240,7 +327,23 @@ static_assert(offsetof(tb_transfer_t, ledger) == 112, "Transfer layout");
 static_assert(offsetof(tb_transfer_t, code) == 116, "Transfer layout");
 static_assert(offsetof(tb_transfer_t, flags) == 118, "Transfer layout");
 static_assert(offsetof(tb_transfer_t, timestamp) == 120, "Transfer layout");
+static_assert(sizeof(tb_account_event_t) == 256, "AccountEvent must be 256 bytes");
+static_assert(offsetof(tb_account_event_t, timestamp) == 160, "AccountEvent layout");
+static_assert(offsetof(tb_account_event_t, dr_account_flags) == 184, "AccountEvent layout");
+static_assert(offsetof(tb_account_event_t, transfer_pending_id) == 192, "AccountEvent layout");
+static_assert(offsetof(tb_account_event_t, ledger) == 240, "AccountEvent layout");
+static_assert(offsetof(tb_account_event_t, transfer_pending_status) == 244, "AccountEvent layout");
+static_assert(sizeof(tb_change_event_t) == 384, "ChangeEvent must be 384 bytes");
+static_assert(offsetof(tb_change_event_t, ledger) == 84, "ChangeEvent layout");
+static_assert(offsetof(tb_change_event_t, type) == 88, "ChangeEvent layout");
+static_assert(offsetof(tb_change_event_t, debit_account_id) == 128, "ChangeEvent layout");
+static_assert(offsetof(tb_change_event_t, credit_account_id) == 240, "ChangeEvent layout");
+static_assert(offsetof(tb_change_event_t, timestamp) == 352, "ChangeEvent layout");
+static_assert(sizeof(tb_change_events_filter_t) == 64, "ChangeEventsFilter must be 64 bytes");
 #else
+_Static_assert(sizeof(tb_account_event_t) == 256, "AccountEvent must be 256 bytes");
+_Static_assert(sizeof(tb_change_event_t) == 384, "ChangeEvent must be 384 bytes");
+_Static_assert(sizeof(tb_change_events_filter_t) == 64, "ChangeEventsFilter must be 64 bytes");
 _Static_assert(sizeof(tb_account_t) == 128, "Account must be 128 bytes");
 _Static_assert(sizeof(tb_transfer_t) == 128, "Transfer must be 128 bytes");
 _Static_assert(sizeof(tb_create_result_t) == 16, "Create*Result must be 16 bytes");

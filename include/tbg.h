@@ -15,6 +15,8 @@
  *   tbg_pulse_next_timestamp <- ExpirePendingTransfers.pulse_next_timestamp :4906-4909
  *   tbg_lookup_accounts   <- execute_lookup_accounts            :3255-3272
  *   tbg_lookup_transfers  <- execute_lookup_transfers           :3274-3292
+ *   tbg_get_change_events <- execute_get_change_events          :3395-3527 (the account_events
+ *                            groove written by account_event    :4384-4465)
  * prefetch (:1146-1420) has no counterpart: every table is HBM-resident, nothing is staged.
  *
  * Batches: one call executes `n_batches` consecutive batches (a multi-batch body, or any sequence
@@ -48,6 +50,9 @@ typedef struct tbg_options {
     uint32_t pulse_batch_max;   /* batch_max.create_transfers: 8190 in production */
     uint32_t device;            /* HIP device ordinal */
     uint64_t pulse_next_timestamp_init; /* TB_TIMESTAMP_MIN in production */
+    /* AccountEvents kept (the account_events groove, state_machine.zig:104-220: one per created
+     * transfer, post/void and expiry); 0 = none are recorded (get_change_events returns none). */
+    uint64_t account_events_capacity;
 } tbg_options;
 
 /* Errors (negative). */
@@ -102,6 +107,16 @@ int64_t tbg_lookup_transfers(tbg_ctx* ctx, const tb_uint128_t* ids, uint32_t n,
 /* Parity dumps: live objects in creation order; `out` may be NULL to query the count. */
 int64_t tbg_dump_accounts(tbg_ctx* ctx, tb_account_t* out);
 int64_t tbg_dump_transfers(tbg_ctx* ctx, tb_transfer_t* out, uint8_t* pending_status);
+
+/* The account_events groove (AccountEvent, state_machine.zig:104-220; written by account_event
+ * :4384-4465 for every created transfer, post/void and expiry), in timestamp order; `out` may be
+ * NULL to query the count. */
+int64_t tbg_dump_account_events(tbg_ctx* ctx, tb_account_event_t* out);
+/* get_change_events (state_machine.zig:2396-2434, :3395-3527): the ChangeEvents whose timestamps
+ * lie in the filter's range, ascending, at most min(filter->limit, limit_max); 0 for an invalid
+ * filter. Returns the count written. */
+int64_t tbg_get_change_events(tbg_ctx* ctx, const tb_change_events_filter_t* filter,
+                              uint32_t limit_max, tb_change_event_t* out);
 
 /* Test-harness `setup` action (src/state_machine_tests.zig:657-676). */
 int tbg_debug_set_account_balances(tbg_ctx* ctx, tb_uint128_t id, tb_uint128_t debits_pending,

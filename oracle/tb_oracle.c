@@ -173,9 +173,13 @@ struct tbo_ctx {
     uint32_t pulse_batch_max;
     uint64_t commit_timestamp;
 
+    /* The account_events groove (state_machine.zig:104-220), in insertion order. */
+    tb_account_event_t* events;
+    uint64_t n_events, cap_events;
+
     /* One active scope at a time (tree.zig:178-197). */
     int scope_active;
-    uint64_t scope_n_accounts, scope_n_transfers, scope_n_expiry;
+    uint64_t scope_n_accounts, scope_n_transfers, scope_n_expiry, scope_n_events;
     key_range_t scope_accounts_range, scope_transfers_range;
     undo_t* undo;
     uint64_t n_undo, cap_undo;
@@ -199,6 +203,7 @@ void tbo_close(tbo_ctx* c) {
     free(c->pending_status);
     free(c->expiry);
     free(c->undo);
+    free(c->events);
     map_free(&c->account_by_id);
     map_free(&c->account_by_ts);
     map_free(&c->transfer_by_id);
@@ -220,6 +225,7 @@ static void scope_open(tbo_ctx* c) {
     c->scope_n_accounts = c->n_accounts;
     c->scope_n_transfers = c->n_transfers;
     c->scope_n_expiry = c->n_expiry;
+    c->scope_n_events = c->n_events;
     c->scope_accounts_range = c->accounts_range;
     c->scope_transfers_range = c->transfers_range;
     c->n_undo = 0;
@@ -247,6 +253,7 @@ static void scope_close(tbo_ctx* c, int discard) {
         c->n_accounts = c->scope_n_accounts;
         c->n_transfers = c->scope_n_transfers;
         c->n_expiry = c->scope_n_expiry;
+        c->n_events = c->scope_n_events; /* account_events inserted in the scope */
         c->accounts_range = c->scope_accounts_range;
         c->transfers_range = c->scope_transfers_range;
     }
@@ -335,6 +342,46 @@ static void update_pending_status(tbo_ctx* c, uint64_t index, uint8_t status) {
 }
 
 static inline int sum_overflows_u128(u128 a, u128 b) { return a + b < a; }
+
+/* account_event (state_machine.zig:4384-4465): the accounts as they stand after the event.
+ * `p` is the pending transfer of a post / void / expiry (else NULL); an expiry has no transfer
+ * flags and no requested amount. Inserted regardless of Account.flags.history (CDC). */
+static void account_event(tbo_ctx* c, uint64_t timestamp_event, const tb_account_t* dr,
+                          const tb_account_t* cr, uint16_t transfer_flags, uint8_t pending_status,
+                          const tb_transfer_t* p, u128 amount_requested, u128 amount) {
+    if (c->n_events == c->cap_events) {
+        c->cap_events = c->cap_events ? c->cap_events * 2 : 1024;
+        c->events = (tb_account_event_t*)xrealloc(c->events,
+                                                  c->cap_events * sizeof(tb_account_event_t));
+    }
+    tb_account_event_t* e = &c->events[c->n_events++];
+    memset(e, 0, sizeof(*e));
+    e->timestamp = timestamp_event;
+    e->dr_account_id = dr->id;
+    e->dr_account_timestamp = dr->timestamp;
+    e->dr_debits_pending = dr->debits_pending;
+    e->dr_debits_posted = dr->debits_posted;
+    e->dr_credits_pending = dr->credits_pending;
+    e->dr_credits_posted = dr->credits_posted;
+    e->dr_account_flags = dr->flags;
+    e->cr_account_id = cr->id;
+    e->cr_account_timestamp = cr->timestamp;
+    e->cr_debits_pending = cr->debits_pending;
+    e->cr_debits_posted = cr->debits_posted;
+    e->cr_credits_pending = cr->credits_pending;
+    e->cr_credits_posted = cr->credits_posted;
+    e->cr_account_flags = cr->flags;
+    e->amount_requested = W(amount_requested);
+    e->amount = W(amount);
+    if (dr->ledger != cr->ledger) abort(); /* asserted by the reference */
+    e->ledger = dr->ledger;
+    e->transfer_flags = transfer_flags;
+    e->transfer_pending_status = pending_status;
+    if (p) {
+        e->transfer_pending_id = p->id;
+        e->transfer_pending_flags = p->flags;
+    }
+}
 
 /* ---- create_account (state_machine.zig:3613-3703) ------------------------------------------*/
 
@@ -583,6 +630,9 @@ static uint32_t post_or_void_pending_transfer(tbo_ctx* c, uint64_t timestamp_eve
         update_account(c, dr, &dr_new);
     if (amount_actual > 0 || U(p.amount) > 0 || cr_new.flags != cr->flags)
         update_account(c, cr, &cr_new);
+    account_event(c, timestamp_actual, &dr_new, &cr_new, t->flags,
+                  (f & TB_TRANSFER_POST_PENDING) ? TB_PENDING_POSTED : TB_PENDING_VOIDED, &p,
+                  U(t->amount), amount_actual);
 
     c->commit_timestamp = timestamp_actual;
     *ts = timestamp_actual;
@@ -704,6 +754,9 @@ static uint32_t create_transfer(tbo_ctx* c, uint64_t timestamp_event, const tb_t
     if (f & TB_TRANSFER_CLOSING_CREDIT) cr_new.flags |= TB_ACCOUNT_CLOSED;
     if (amount > 0 || (dr_new.flags & TB_ACCOUNT_CLOSED)) update_account(c, dr, &dr_new);
     if (amount > 0 || (cr_new.flags & TB_ACCOUNT_CLOSED)) update_account(c, cr, &cr_new);
+    account_event(c, timestamp_actual, &dr_new, &cr_new, t->flags,
+                  (f & TB_TRANSFER_PENDING) ? TB_PENDING_PENDING : TB_PENDING_NONE, NULL,
+                  U(t->amount), amount);
 
     if (t->timeout > 0) {
         uint64_t expires_at = timestamp_actual + (uint64_t)t->timeout * TB_NS_PER_S;
@@ -869,6 +922,8 @@ static void expire_keys(tbo_ctx* c, const expiry_key_t* keys, uint64_t expired, 
         *cr = cr_new;
         c->pending_status[keys[k].index] = TB_PENDING_EXPIRED;
         c->commit_timestamp = timestamp - expired + k + 1;
+        account_event(c, c->commit_timestamp, &dr_new, &cr_new, 0, TB_PENDING_EXPIRED, p, 0,
+                      U(p->amount));
     }
 }
 
@@ -981,6 +1036,102 @@ uint64_t tbo_dump_pending_status(const tbo_ctx* c, uint8_t* out) {
     return c->n_transfers;
 }
 
+uint64_t tbo_dump_account_events(const tbo_ctx* c, tb_account_event_t* out) {
+    if (out) memcpy(out, c->events, c->n_events * sizeof(tb_account_event_t));
+    return c->n_events;
+}
+
+/* ---- get_change_events (state_machine.zig:2396-2434 filter, :3395-3527 execution) -----------*/
+
+static const tbo_ctx* g_sort_ctx;
+static int event_index_cmp(const void* a_, const void* b_) {
+    const uint64_t a = *(const uint64_t*)a_, b = *(const uint64_t*)b_;
+    const uint64_t ta = g_sort_ctx->events[a].timestamp, tb = g_sort_ctx->events[b].timestamp;
+    if (ta != tb) return ta < tb ? -1 : 1;
+    return a < b ? -1 : (a > b);
+}
+
+int64_t tbo_get_change_events(const tbo_ctx* c, const tb_change_events_filter_t* filter,
+                              uint32_t limit_max, tb_change_event_t* out) {
+    /* get_scan_from_change_events_filter: an invalid filter yields no results. */
+    int reserved_zero = 1;
+    for (int i = 0; i < 44; i++) reserved_zero &= filter->reserved[i] == 0;
+    const uint64_t tmin = filter->timestamp_min, tmax = filter->timestamp_max;
+    int valid = (tmin == 0 || (tmin >= TB_TIMESTAMP_MIN && tmin <= TB_TIMESTAMP_MAX)) &&
+                (tmax == 0 || (tmax >= TB_TIMESTAMP_MIN && tmax <= TB_TIMESTAMP_MAX)) &&
+                (tmax == 0 || tmin <= tmax) && filter->limit != 0 && reserved_zero;
+    if (!valid) return 0;
+    const uint64_t lo = tmin == 0 ? TB_TIMESTAMP_MIN : tmin;
+    const uint64_t hi = tmax == 0 ? TB_TIMESTAMP_MAX : tmax;
+    const uint32_t limit = filter->limit < limit_max ? filter->limit : limit_max;
+    /* The groove is keyed by timestamp: ascending order. */
+    uint64_t* order = (uint64_t*)xrealloc(NULL, (c->n_events + 1) * sizeof(uint64_t));
+    for (uint64_t i = 0; i < c->n_events; i++) order[i] = i;
+    g_sort_ctx = c;
+    qsort(order, c->n_events, sizeof(uint64_t), event_index_cmp);
+    uint32_t count = 0;
+    for (uint64_t j = 0; j < c->n_events && count < limit; j++) {
+        const tb_account_event_t* e = &c->events[order[j]];
+        if (e->timestamp < lo || e->timestamp > hi) continue;
+        uint64_t ti = 0;
+        /* get_change_event: the transfer by timestamp, the pending transfer for an expiry. */
+        if (e->transfer_pending_status == TB_PENDING_EXPIRED) {
+            if (get_transfer((tbo_ctx*)c, U(e->transfer_pending_id), &ti) != 1) abort();
+        } else if (!map_get(&c->transfer_by_ts, e->timestamp, &ti)) {
+            abort();
+        }
+        const tb_transfer_t* t = &c->transfers[ti];
+        const tb_account_t* dr = get_account((tbo_ctx*)c, U(e->dr_account_id));
+        const tb_account_t* cr = get_account((tbo_ctx*)c, U(e->cr_account_id));
+        if (!dr || !cr) abort();
+        tb_change_event_t* o = &out[count++];
+        memset(o, 0, sizeof(*o));
+        o->transfer_id = t->id;
+        o->transfer_amount = e->amount;
+        o->transfer_pending_id = t->pending_id;
+        o->transfer_user_data_128 = t->user_data_128;
+        o->transfer_user_data_64 = t->user_data_64;
+        o->transfer_user_data_32 = t->user_data_32;
+        o->transfer_timeout = t->timeout;
+        o->ledger = e->ledger;
+        o->transfer_code = t->code;
+        o->transfer_flags = t->flags;
+        switch (e->transfer_pending_status) {
+            case TB_PENDING_NONE: o->type = TB_CHANGE_SINGLE_PHASE; break;
+            case TB_PENDING_PENDING: o->type = TB_CHANGE_TWO_PHASE_PENDING; break;
+            case TB_PENDING_POSTED: o->type = TB_CHANGE_TWO_PHASE_POSTED; break;
+            case TB_PENDING_VOIDED: o->type = TB_CHANGE_TWO_PHASE_VOIDED; break;
+            default: o->type = TB_CHANGE_TWO_PHASE_EXPIRED; break;
+        }
+        o->debit_account_id = dr->id;
+        o->debit_account_debits_pending = e->dr_debits_pending;
+        o->debit_account_debits_posted = e->dr_debits_posted;
+        o->debit_account_credits_pending = e->dr_credits_pending;
+        o->debit_account_credits_posted = e->dr_credits_posted;
+        o->debit_account_user_data_128 = dr->user_data_128;
+        o->debit_account_user_data_64 = dr->user_data_64;
+        o->debit_account_user_data_32 = dr->user_data_32;
+        o->debit_account_code = dr->code;
+        o->debit_account_flags = e->dr_account_flags;
+        o->credit_account_id = cr->id;
+        o->credit_account_debits_pending = e->cr_debits_pending;
+        o->credit_account_debits_posted = e->cr_debits_posted;
+        o->credit_account_credits_pending = e->cr_credits_pending;
+        o->credit_account_credits_posted = e->cr_credits_posted;
+        o->credit_account_user_data_128 = cr->user_data_128;
+        o->credit_account_user_data_64 = cr->user_data_64;
+        o->credit_account_user_data_32 = cr->user_data_32;
+        o->credit_account_code = cr->code;
+        o->credit_account_flags = e->cr_account_flags;
+        o->timestamp = e->timestamp;
+        o->transfer_timestamp = t->timestamp;
+        o->debit_account_timestamp = dr->timestamp;
+        o->credit_account_timestamp = cr->timestamp;
+    }
+    free(order);
+    return count;
+}
+
 /* ---- executor binding (tb_state_machine.h) --------------------------------------------------*/
 
 static int ex_create_accounts(void* self, const tb_account_t* events, uint32_t n,
@@ -1013,6 +1164,10 @@ static int64_t ex_lookup_transfers(void* self, const tb_uint128_t* ids, uint32_t
                                    tb_transfer_t* out) {
     return tbo_lookup_transfers((tbo_ctx*)self, ids, n, out);
 }
+static int64_t ex_get_change_events(void* self, const tb_change_events_filter_t* filter,
+                                    uint32_t limit_max, tb_change_event_t* out) {
+    return tbo_get_change_events((tbo_ctx*)self, filter, limit_max, out);
+}
 
 void tbo_executor_fill(tbo_ctx* c, tb_executor* ex) {
     ex->self = c;
@@ -1022,4 +1177,5 @@ void tbo_executor_fill(tbo_ctx* c, tb_executor* ex) {
     ex->pulse_next_timestamp = ex_pulse_next;
     ex->lookup_accounts = ex_lookup_accounts;
     ex->lookup_transfers = ex_lookup_transfers;
+    ex->get_change_events = ex_get_change_events;
 }

@@ -69,6 +69,13 @@ uint64_t tbo_dump_accounts(const tbo_ctx* ctx, tb_account_t* out);   /* creation
 uint64_t tbo_dump_transfers(const tbo_ctx* ctx, tb_transfer_t* out); /* creation order */
 uint64_t tbo_dump_pending_status(const tbo_ctx* ctx, uint8_t* out);  /* per transfer */
 
+/* The account_events groove in insertion order (AccountEvent, state_machine.zig:104-220). */
+uint64_t tbo_dump_account_events(const tbo_ctx* ctx, tb_account_event_t* out);
+/* get_change_events (state_machine.zig:2396-2434, :3395-3527): ChangeEvents with timestamps in the
+ * filter's range, ascending, at most min(filter->limit, limit_max); 0 for an invalid filter. */
+int64_t tbo_get_change_events(const tbo_ctx* ctx, const tb_change_events_filter_t* filter,
+                              uint32_t limit_max, tb_change_event_t* out);
+
 /* Binds this oracle as a tb_executor (tb_state_machine.h) for the StateMachine mirror. */
 void tbo_executor_fill(tbo_ctx* ctx, tb_executor* ex);
 

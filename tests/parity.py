@@ -17,8 +17,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from tigerbeetle_amd import native  # noqa: E402
 from tigerbeetle_amd.types import (  # noqa: E402
-    ACCOUNT_DTYPE, RESULT_DTYPE, TRANSFER_DTYPE, TIMESTAMP_MAX, CreateAccountStatus,
-    CreateTransferStatus)
+    ACCOUNT_DTYPE, ACCOUNT_EVENT_DTYPE, CHANGE_EVENT_DTYPE, CHANGE_EVENTS_FILTER_DTYPE,
+    RESULT_DTYPE, TRANSFER_DTYPE, TIMESTAMP_MAX, CreateAccountStatus, CreateTransferStatus)
 
 import oracle_binding  # noqa: E402
 
@@ -34,7 +34,8 @@ class ParityError(AssertionError):
 class Pair:
     def __init__(self, account_capacity=1 << 16, transfer_capacity=1 << 20,
                  batch_events_max=1 << 16, batch_count_max=4096, pulse_batch_max=8190,
-                 pulse_next_timestamp_init=TIMESTAMP_MAX, force_replay=False, device=0):
+                 pulse_next_timestamp_init=TIMESTAMP_MAX, force_replay=False, device=0,
+                 account_events=True):
         self.lib = native.load()
         self.olib = oracle_binding.load()
         o = native.TbgOptions()
@@ -45,6 +46,9 @@ class Pair:
         o.pulse_batch_max = pulse_batch_max
         o.device = device
         o.pulse_next_timestamp_init = pulse_next_timestamp_init
+        # AccountEvents (one per created transfer and per expiry), compared in compare_state.
+        o.account_events_capacity = 2 * transfer_capacity if account_events else 0
+        self.account_events = account_events
         self.g = self.lib.tbg_open(ctypes.byref(o))
         if not self.g:
             raise RuntimeError("tbg_open failed")
@@ -202,7 +206,33 @@ class Pair:
                               f"first diff at {_first_diff(t_gpu, t_orc)}")
         if s_gpu.tobytes() != s_orc.tobytes():
             raise ParityError("TransferPending statuses differ")
+        if self.account_events:
+            ne = self.lib.tbg_dump_account_events(self.g, None)
+            e_gpu = np.zeros(max(ne, 0), dtype=ACCOUNT_EVENT_DTYPE)
+            self.lib.tbg_dump_account_events(self.g, _ptr(e_gpu))
+            e_orc = np.zeros(self.olib.tbo_dump_account_events(self.o, None),
+                             dtype=ACCOUNT_EVENT_DTYPE)
+            self.olib.tbo_dump_account_events(self.o, _ptr(e_orc))
+            # (the groove is keyed by timestamp: the oracle's insertion order sorted, stable)
+            e_orc = e_orc[np.argsort(e_orc["timestamp"], kind="stable")]
+            if e_gpu.tobytes() != e_orc.tobytes():
+                raise ParityError(f"account events differ: gpu {len(e_gpu)}, oracle {len(e_orc)}; "
+                                  f"first diff at {_first_diff(e_gpu, e_orc)}")
         return len(a_orc), len(t_orc)
+
+    def change_events(self, timestamp_min=0, timestamp_max=0, limit=1 << 31, limit_max=8190):
+        """get_change_events on both sides; they must agree byte for byte."""
+        f = np.zeros(1, dtype=CHANGE_EVENTS_FILTER_DTYPE)
+        f["timestamp_min"], f["timestamp_max"], f["limit"] = timestamp_min, timestamp_max, limit
+        cap = min(limit, limit_max)
+        g = np.zeros(cap, dtype=CHANGE_EVENT_DTYPE)
+        o = np.zeros(cap, dtype=CHANGE_EVENT_DTYPE)
+        ng = self.lib.tbg_get_change_events(self.g, _ptr(f), limit_max, _ptr(g))
+        no = self.olib.tbo_get_change_events(self.o, _ptr(f), limit_max, _ptr(o))
+        if ng != no or g[:ng].tobytes() != o[:no].tobytes():
+            raise ParityError(f"get_change_events differ: gpu {ng}, oracle {no}; first diff at "
+                              f"{_first_diff(g[:ng], o[:no])}")
+        return g[:ng]
 
 
 def _first_diff(a, b):

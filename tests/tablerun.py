@@ -7,8 +7,10 @@ event with its expected result; `commit <op>` submits the accumulated batch thro
 derived by the harness rules (:704-735, :757-811).
 
 The StateMachine under test is bound to an executor: the CPU oracle (oracle/liboracle.so) or the
-HIP executor (libtbg.so). Query operations outside this path (get_account_transfers,
-get_account_balances, query_*, get_change_events) are skipped: they do not change state.
+HIP executor (libtbg.so). get_change_events (the account_events groove read back as
+ChangeEvents, :2396-2434, :3395-3527) is checked with the reference's own `match` rules
+(TestGetChangeEventsResult, :502-599). The other queries (get_account_transfers,
+get_account_balances, query_*) are outside this path and skipped: they do not change state.
 """
 import ctypes
 import os
@@ -21,8 +23,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from tigerbeetle_amd import native  # noqa: E402
 from tigerbeetle_amd.types import (  # noqa: E402
-    ACCOUNT_DTYPE, RESULT_DTYPE, TRANSFER_DTYPE, CreateAccountStatus, CreateTransferStatus,
-    Operation, TIMESTAMP_MAX, U128_MAX, NS_PER_S)
+    ACCOUNT_DTYPE, CHANGE_EVENT_DTYPE, CHANGE_EVENTS_FILTER_DTYPE, RESULT_DTYPE, TRANSFER_DTYPE,
+    CreateAccountStatus, CreateTransferStatus, Operation, TIMESTAMP_MAX, U128_MAX, NS_PER_S)
 
 TABLE_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "tables")
 
@@ -35,7 +37,7 @@ TEST_BATCH_SIZE_LIMIT = 30 * 128
 TEST_PULSE_BATCH_MAX = TEST_MESSAGE_BODY_SIZE_MAX // 128
 
 SKIPPED_OPS = {"get_account_transfers", "get_account_balances", "query_accounts",
-               "query_transfers", "get_change_events"}
+               "query_transfers"}
 
 
 # ---- row DSL (src/testing/table.zig) --------------------------------------------------------
@@ -167,6 +169,23 @@ def parse_row(line: str):
             row["data"] = ("timestamp", parse_uint(tok, 64))
         else:
             raise ValueError(line)
+    elif kind == "get_change_events":
+        # TestGetChangeEventsFilter (:496-500): optional transfer ids for the timestamp bounds
+        row["min"] = None if t.eat("_") else parse_uint(t.next(), 128)
+        row["max"] = None if t.eat("_") else parse_uint(t.next(), 128)
+        row["limit"] = parse_uint(t.next(), 32)
+    elif kind == "get_change_events_result":
+        # TestGetChangeEventsResult (:502-517)
+        row["event_type"] = None if t.eat("_") else t.next()
+        row["timestamp_transfer"] = None if t.eat("_") else parse_uint(t.next(), 128)
+        row["amount"] = parse_uint(t.next(), 128)
+        row["pending_id"] = None if t.eat("_") else parse_uint(t.next(), 128)
+        for side in ("dr", "cr"):
+            b = {"account_id": parse_uint(t.next(), 128)}
+            for f in ("debits_pending", "debits_posted", "credits_pending", "credits_posted"):
+                b[f] = parse_uint(t.next(), 128)
+            b["closed"] = False if t.eat("_") else (t.next() == "CLSD")
+            row[side] = b
     elif kind.split("_result")[0] in SKIPPED_OPS or kind in SKIPPED_OPS:
         row["kind"] = "skip"
         row["op"] = kind
@@ -314,6 +333,17 @@ class TableContext:
             assert len(size) == 0
             self.op += 1
 
+    def submit_query(self, operation: int, body: bytes) -> bytes:
+        """A non-multi-batch operation (get_change_events): the body is the filter itself."""
+        assert self.lib.tb_sm_input_valid(self.sm, operation, body, len(body)) == 1
+        self.prepare(operation, body)
+        pulse_needed = self.lib.tb_sm_pulse_needed(self.sm,
+                                                   self.lib.tb_sm_get_prepare_timestamp(self.sm))
+        reply = self.execute(operation, body)
+        if pulse_needed:
+            self.pulse()
+        return reply
+
     # TestContext.submit (:178-228)
     def submit(self, operation: int, payload: bytes, element_size: int, result_size: int) -> bytes:
         body = encode_multi_batch(self.lib, payload, element_size)
@@ -448,8 +478,36 @@ def run_table(handle: StateMachineHandle, rows, label=""):
                 else:
                     t["timestamp"] = value
                 reply.append(t.tobytes())
+        elif kind == "get_change_events":
+            assert operation is None
+            operation = "get_change_events"
+            f = np.zeros(1, dtype=CHANGE_EVENTS_FILTER_DTYPE)
+            f["timestamp_min"] = 0 if row["min"] is None else int(transfers[row["min"]]["timestamp"])
+            f["timestamp_max"] = 0 if row["max"] is None else int(transfers[row["max"]]["timestamp"])
+            f["limit"] = row["limit"]
+            request.append(f.tobytes())
+        elif kind == "get_change_events_result":
+            assert operation == "get_change_events"
+            reply.append(row)
         elif kind == "commit":
             op_name = row["operation"]
+            if op_name == "get_change_events":
+                assert operation == "get_change_events" and len(request) == 1
+                commits += 1
+                actual = ctx.submit_query(Operation.get_change_events, request[0])
+                events = np.frombuffer(actual, dtype=CHANGE_EVENT_DTYPE)
+                if len(events) != len(reply):
+                    raise TableMismatch(f"{label}: commit #{commits} (get_change_events): "
+                                        f"{len(events)} events, expected {len(reply)}")
+                for i, (ev, want) in enumerate(zip(events, reply)):
+                    why = change_event_mismatch(want, ev, accounts, transfers)
+                    if why:
+                        raise TableMismatch(f"{label}: commit #{commits} (get_change_events) "
+                                            f"event {i}: {why}\n  actual={ev}")
+                request.clear()
+                reply.clear()
+                operation = None
+                continue
             if operation == "skip" or op_name in SKIPPED_OPS:
                 request.clear()
                 reply.clear()
@@ -478,6 +536,76 @@ def run_table(handle: StateMachineHandle, rows, label=""):
             raise ValueError(kind)
     assert operation is None and not request and not reply
     return commits
+
+
+_CHANGE_TYPES = {None: 0, "PEN": 1, "POS": 2, "VOI": 3, "EXP": 4}
+
+
+def _match_transfer(ev, t):
+    """TestGetChangeEventsResult.match_transfer (state_machine_tests.zig:582-598)."""
+    if int(ev["transfer_timestamp"]) != int(t["timestamp"]):
+        return "transfer_timestamp"
+    if u128_of(ev, "transfer_id") != u128_of(t, "id"):
+        return "transfer_id"
+    if u128_of(ev, "transfer_amount") != u128_of(t, "amount") and u128_of(t, "amount") != U128_MAX:
+        return "transfer_amount"
+    if u128_of(ev, "transfer_pending_id") != u128_of(t, "pending_id"):
+        return "transfer_pending_id"
+    if u128_of(ev, "transfer_user_data_128") != u128_of(t, "user_data_128"):
+        return "transfer_user_data_128"
+    for a, b in (("transfer_user_data_64", "user_data_64"), ("transfer_user_data_32", "user_data_32"),
+                 ("transfer_code", "code"), ("ledger", "ledger"), ("transfer_flags", "flags")):
+        if int(ev[a]) != int(t[b]):
+            return a
+    return None
+
+
+def change_event_mismatch(want, ev, accounts, transfers):
+    """TestGetChangeEventsResult.match (state_machine_tests.zig:519-580); None when it matches."""
+    if want["timestamp_transfer"] is not None:
+        t = transfers[want["timestamp_transfer"]]
+        if int(ev["type"]) == 4:
+            return "expired event for a transfer timestamp"
+        if int(ev["timestamp"]) != int(t["timestamp"]):
+            return "timestamp"
+        why = _match_transfer(ev, t)
+        if why:
+            return why
+    if int(ev["type"]) != _CHANGE_TYPES[want["event_type"]]:
+        return "type"
+    if u128_of(ev, "transfer_amount") != want["amount"]:
+        return "amount"
+    if want["pending_id"] is not None:
+        typ = int(ev["type"])
+        if typ in (0, 1):
+            return "pending id on a single-phase / pending event"
+        if typ in (2, 3):
+            if u128_of(ev, "transfer_pending_id") != want["pending_id"]:
+                return "transfer_pending_id"
+        else:
+            t = transfers[want["pending_id"]]
+            if int(t["timeout"]) == 0:
+                return "expired transfer without timeout"
+            if int(ev["timestamp"]) < int(t["timestamp"]) + int(t["timeout"]) * NS_PER_S:
+                return "expired before its expiry"
+            why = _match_transfer(ev, t)
+            if why:
+                return why
+    for side, prefix in (("dr", "debit_account_"), ("cr", "credit_account_")):
+        b = want[side]
+        a = accounts[b["account_id"]]
+        if int(a["ledger"]) != int(ev["ledger"]):
+            return f"{side} ledger"
+        if u128_of(ev, prefix + "id") != b["account_id"]:
+            return f"{side} account id"
+        if int(a["timestamp"]) != int(ev[prefix + "timestamp"]):
+            return f"{side} account timestamp"
+        for f in ("debits_pending", "debits_posted", "credits_pending", "credits_posted"):
+            if u128_of(ev, prefix + f) != b[f]:
+                return f"{side} {f}"
+        if bool(int(ev[prefix + "flags"]) & (1 << 5)) != b["closed"]:
+            return f"{side} closed"
+    return None
 
 
 def describe_mismatch(label, commit_index, op_name, expected: bytes, actual: bytes) -> str:

@@ -34,4 +34,9 @@ def test_struct_sizes():
     from tigerbeetle_amd.types import ACCOUNT_DTYPE, RESULT_DTYPE, TRANSFER_DTYPE
     assert ACCOUNT_DTYPE.itemsize == 128 and TRANSFER_DTYPE.itemsize == 128
     assert RESULT_DTYPE.itemsize == 16
-    assert ctypes.sizeof(native.TbgOptions) == 40
+    assert ctypes.sizeof(native.TbgOptions) == 48
+    assert ctypes.sizeof(native.Executor) == 8 * 8
+    from tigerbeetle_amd.types import (ACCOUNT_EVENT_DTYPE, CHANGE_EVENT_DTYPE,
+                                       CHANGE_EVENTS_FILTER_DTYPE)
+    assert ACCOUNT_EVENT_DTYPE.itemsize == 256 and CHANGE_EVENT_DTYPE.itemsize == 384
+    assert CHANGE_EVENTS_FILTER_DTYPE.itemsize == 64

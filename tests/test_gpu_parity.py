@@ -543,3 +543,65 @@ def test_long_linked_chains(length, force_replay):
         p.compare_state()
     finally:
         p.close()
+
+
+@pytest.mark.parametrize("force_replay", [False, True, "serial"], ids=["parallel", "flow", "serial"])
+def test_change_events(force_replay):
+    """AccountEvents (state_machine.zig:4384-4465) and get_change_events (:3395-3527) against the
+    oracle: single-phase, pending, posted (partial), voided (also of closing transfers) and
+    expired events, balancing amounts, rolled-back chains; then filters by timestamp range and
+    limit, and an invalid filter."""
+    rng = np.random.default_rng(31)
+    p = Pair(account_capacity=1 << 10, transfer_capacity=1 << 15, batch_events_max=4096,
+             pulse_batch_max=16, pulse_next_timestamp_init=TIMESTAMP_MAX,
+             force_replay=force_replay)
+    try:
+        acc = workload.accounts(30, seed=3, ledger=1)
+        acc["flags"] = rng.choice([0, 0, 2, 4, 8], size=30).astype(np.uint16)
+        p.create_accounts(acc)
+        ids = []
+        for step in range(6):
+            pend = np.array(ids[-300:], dtype=np.uint64) if ids else None
+            t = workload.fuzz_transfers(rng, 400, 2000, 31, pending_ids=pend)
+            ids.extend(int(x) for x in t["id"][:, 0])
+            p.create_transfers(t, _split(len(t), rng, 64))
+            p.tick(int(rng.integers(1, 3)) * NS_PER_S)
+        p.compare_state()
+        all_events = p.change_events()
+        assert len(all_events) > 100 and {0, 1, 2, 3, 4} <= set(all_events["type"].tolist())
+        ts = all_events["timestamp"]
+        p.change_events(timestamp_min=int(ts[10]), timestamp_max=int(ts[60]))
+        p.change_events(timestamp_min=int(ts[5]), limit=7)
+        p.change_events(timestamp_max=int(ts[-20]), limit=1000, limit_max=33)
+        p.change_events(timestamp_min=int(ts[-1]) + 1)
+        assert len(p.change_events(timestamp_min=int(ts[50]), timestamp_max=int(ts[40]))) == 0
+        assert len(p.change_events(limit=0)) == 0
+    finally:
+        p.close()
+
+
+def test_change_events_imported_before_expiries():
+    """An imported batch whose timestamps precede a pulse's expiry events (the imported checks
+    compare with the transfers' key range, not the events'): the account_events groove is keyed
+    by timestamp, so the executor's log must come back in timestamp order."""
+    p = Pair(account_capacity=64, transfer_capacity=4096, batch_events_max=256,
+             pulse_next_timestamp_init=TIMESTAMP_MAX)
+    try:
+        acc = workload.accounts(4, seed=1, ledger=1)
+        acc["flags"] = 0
+        p.create_accounts(acc)
+        p.create_transfers(_transfers([dict(id=1, debit_account_id=1, credit_account_id=2,
+                                            amount=5, ledger=1, code=1, flags=2, timeout=1)]))
+        key_max = p.prepare_timestamp
+        p.tick(2 * NS_PER_S)  # the pending transfer expires (events at the pulse's timestamps)
+        assert p.pulse_next() == TIMESTAMP_MAX
+        imp = _transfers([dict(id=10 + i, debit_account_id=3, credit_account_id=4, amount=7,
+                               ledger=1, code=1, flags=256, timestamp=key_max + 10 + i)
+                          for i in range(3)])
+        r = p.create_transfers(imp)
+        assert (r["status"] == 0xFFFFFFFF).all()
+        p.compare_state()
+        ev = p.change_events()
+        assert list(ev["type"]) == [1, 0, 0, 0, 4]
+    finally:
+        p.close()

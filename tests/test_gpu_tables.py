@@ -25,6 +25,7 @@ def gpu_handle(force_replay: bool):
     o.pulse_batch_max = tablerun.TEST_PULSE_BATCH_MAX
     o.device = 0
     o.pulse_next_timestamp_init = TIMESTAMP_MAX
+    o.account_events_capacity = 8192  # get_change_events reads the account_events groove
     sm = lib.tb_sm_open_gpu(ctypes.byref(tablerun.sm_options()), ctypes.byref(o))
     assert sm, "tb_sm_open_gpu failed"
     g = lib.tb_sm_executor_gpu(sm)

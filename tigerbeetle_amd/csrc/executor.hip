@@ -15,6 +15,7 @@
 
 #include "../../include/tbg.h"
 #include "lanes.hpp"
+#include "events.hpp"
 
 using namespace tbg;
 
@@ -116,6 +117,17 @@ struct tbg_ctx {
 
     PulseScratch pulse;
     FlowScratch flow;
+
+    // The account_events groove (events.hpp): AccountEvents in timestamp order + their references.
+    tb_account_event_t* ae_log = nullptr;
+    AeRef* ae_ref = nullptr;
+    uint64_t ae_cap = 0, ae_used = 0, ae_last_ts = 0;
+    bool ae_sorted = true;
+    AeScratch ae{};
+    uint64_t ae_touch_cap = 0;
+    uint8_t* ae_flags = nullptr;
+    uint32_t* ae_list = nullptr;
+    unsigned long long* ae_words = nullptr;  // bounds / counts
     unsigned long long* flow_debug = nullptr;
     std::vector<uint32_t> h_ends;
 
@@ -656,6 +668,152 @@ int64_t dump_impl(tbg_ctx* ctx, const Row* rows, const uint8_t* live, uint64_t u
     return result;
 }
 
+// ---- AccountEvents (events.hpp) ---------------------------------------------------------------
+
+int ensure_ae_scratch(tbg_ctx* ctx, uint64_t touches) {
+    if (touches <= ctx->ae_touch_cap) return 0;
+    AeScratch& S = ctx->ae;
+    void* ptrs[] = {S.keys, S.vals, S.keys_sorted, S.vals_sorted, S.deltas, S.seg, S.values,
+                    S.scanned};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    S = AeScratch{};
+    ctx->ae_touch_cap = 0;
+    const uint64_t cap = std::max<uint64_t>(next_pow2(touches), 1u << 14);
+    if (!(dev_alloc(ctx, &S.keys, cap, false) && dev_alloc(ctx, &S.vals, cap, false) &&
+          dev_alloc(ctx, &S.keys_sorted, cap, false) && dev_alloc(ctx, &S.vals_sorted, cap, false) &&
+          dev_alloc(ctx, &S.deltas, cap, false) && dev_alloc(ctx, &S.seg, cap, false) &&
+          dev_alloc(ctx, &S.values, cap, false) && dev_alloc(ctx, &S.scanned, cap, false)))
+        return TBG_ENOMEM;
+    ctx->ae_touch_cap = cap;
+    return 0;
+}
+
+// Appends m AccountEvents: `collect` writes their event-level fields and both touches of each;
+// the account halves follow from the final rows and the later events' sums per account.
+template <typename Collect>
+int ae_append(tbg_ctx* ctx, uint32_t m, Collect collect) {
+    if (m == 0) return 0;
+    if (ctx->ae_used + m > ctx->ae_cap) {
+        ctx->error = "account_events capacity exceeded";
+        return TBG_ENOSPC;
+    }
+    const uint64_t touches = 2 * uint64_t(m);
+    int rc = ensure_ae_scratch(ctx, touches);
+    if (rc) return rc;
+    AeScratch& S = ctx->ae;
+    tb_account_event_t* log = ctx->ae_log + ctx->ae_used;
+    collect(S, log, ctx->ae_ref + ctx->ae_used);
+    uint32_t row_bits = 1;
+    while ((1ull << row_bits) < ctx->T.acc_rows_used) row_bits++;
+    size_t bytes = 0;
+    HIP_TRY(ctx, hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, S.keys, S.keys_sorted, S.vals,
+                                                    S.vals_sorted, int(touches), 0,
+                                                    int(32 + row_bits), ctx->stream));
+    rc = ensure_cub_temp(ctx, bytes);
+    if (rc) return rc;
+    HIP_TRY(ctx, hipcub::DeviceRadixSort::SortPairs(ctx->cub_temp, bytes, S.keys, S.keys_sorted,
+                                                    S.vals, S.vals_sorted, int(touches), 0,
+                                                    int(32 + row_bits), ctx->stream));
+    hipLaunchKernelGGL(ae_values, dim3(grid_for(touches)), dim3(kBlock), 0, ctx->stream, S,
+                       uint32_t(touches));
+    Bal5 zero{};
+    bytes = 0;
+    HIP_TRY(ctx, hipcub::DeviceScan::ExclusiveScanByKey(nullptr, bytes, S.seg, S.values, S.scanned,
+                                                        Bal5Add(), zero, int(touches),
+                                                        hipcub::Equality(), ctx->stream));
+    rc = ensure_cub_temp(ctx, bytes);
+    if (rc) return rc;
+    HIP_TRY(ctx, hipcub::DeviceScan::ExclusiveScanByKey(ctx->cub_temp, bytes, S.seg, S.values,
+                                                        S.scanned, Bal5Add(), zero, int(touches),
+                                                        hipcub::Equality(), ctx->stream));
+    hipLaunchKernelGGL(ae_emit, dim3(grid_for(touches)), dim3(kBlock), 0, ctx->stream, ctx->T, S,
+                       uint32_t(touches), log);
+    tmark(ctx, "account_events");
+    HIP_TRY(ctx, hipGetLastError());
+    // The log stays in timestamp order unless this block starts before the last one ended (an
+    // imported batch after a pulse's expiries); then get_change_events sorts it first.
+    uint64_t first = 0, last = 0;
+    HIP_TRY(ctx, hipMemcpyAsync(&first, &log[0].timestamp, 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(&last, &log[m - 1].timestamp, 8, hipMemcpyDeviceToHost,
+                                ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (ctx->ae_used && first <= ctx->ae_last_ts) ctx->ae_sorted = false;
+    ctx->ae_last_ts = std::max(ctx->ae_last_ts, last);
+    ctx->ae_used += m;
+    return 0;
+}
+
+// AccountEvents of a create_transfers call: its created events in call order.
+int ae_transfers(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
+    hipLaunchKernelGGL(ae_created_flags, dim3(grid_for(c.n)), dim3(kBlock), 0, ctx->stream, c,
+                       ctx->ae_flags);
+    unsigned int* d_count = reinterpret_cast<unsigned int*>(ctx->ae_words);
+    int rc = select_flagged(ctx, ctx->ae_flags, c.n, ctx->ae_list, d_count);
+    if (rc) return rc;
+    unsigned int m = 0;
+    HIP_TRY(ctx, hipMemcpyAsync(&m, d_count, 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    const uint32_t* list = ctx->ae_list;
+    return ae_append(ctx, m, [&](const AeScratch& S, tb_account_event_t* log, AeRef* refs) {
+        hipLaunchKernelGGL(ae_collect_transfers, dim3(grid_for(m)), dim3(kBlock), 0, ctx->stream,
+                           ctx->T, c, list, m, S, log, refs);
+    });
+}
+
+// AccountEvents of a pulse: the expired rows in expiry order.
+int ae_expiry(tbg_ctx* ctx, const uint64_t* rows, uint64_t m, uint64_t timestamp) {
+    return ae_append(ctx, uint32_t(m), [&](const AeScratch& S, tb_account_event_t* log,
+                                           AeRef* refs) {
+        hipLaunchKernelGGL(ae_collect_expiry, dim3(grid_for(m)), dim3(kBlock), 0, ctx->stream,
+                           ctx->T, rows, uint32_t(m), timestamp, S, log, refs);
+    });
+}
+
+// Restores timestamp order of the log (stable) when an append broke it.
+int ae_sort_log(tbg_ctx* ctx) {
+    if (ctx->ae_sorted || ctx->ae_used < 2) {
+        ctx->ae_sorted = true;
+        return 0;
+    }
+    const uint64_t n = ctx->ae_used;
+    uint64_t *keys = nullptr, *keys2 = nullptr;
+    uint32_t *idx = nullptr, *idx2 = nullptr;
+    tb_account_event_t* log2 = nullptr;
+    AeRef* ref2 = nullptr;
+    int rc = 0;
+    if (!(dev_alloc(ctx, &keys, n, false) && dev_alloc(ctx, &keys2, n, false) &&
+          dev_alloc(ctx, &idx, n, false) && dev_alloc(ctx, &idx2, n, false) &&
+          dev_alloc(ctx, &log2, n, false) && dev_alloc(ctx, &ref2, n, false)))
+        rc = TBG_ENOMEM;
+    if (!rc) {
+        hipLaunchKernelGGL(ae_sort_keys, dim3(grid_for(n)), dim3(kBlock), 0, ctx->stream,
+                           ctx->ae_log, n, keys, idx);
+        size_t bytes = 0;
+        if (hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, keys, keys2, idx, idx2, int(n), 0,
+                                               64, ctx->stream) != hipSuccess)
+            rc = TBG_EHIP;
+        if (!rc) rc = ensure_cub_temp(ctx, bytes);
+        if (!rc && hipcub::DeviceRadixSort::SortPairs(ctx->cub_temp, bytes, keys, keys2, idx, idx2,
+                                                      int(n), 0, 64, ctx->stream) != hipSuccess)
+            rc = TBG_EHIP;
+        if (!rc) {
+            hipLaunchKernelGGL(ae_permute, dim3(grid_for(n)), dim3(kBlock), 0, ctx->stream,
+                               ctx->ae_log, ctx->ae_ref, idx2, n, log2, ref2);
+            if (hipMemcpyAsync(ctx->ae_log, log2, n * sizeof(tb_account_event_t),
+                               hipMemcpyDeviceToDevice, ctx->stream) != hipSuccess ||
+                hipMemcpyAsync(ctx->ae_ref, ref2, n * sizeof(AeRef), hipMemcpyDeviceToDevice,
+                               ctx->stream) != hipSuccess ||
+                hipStreamSynchronize(ctx->stream) != hipSuccess)
+                rc = TBG_EHIP;
+        }
+    }
+    for (void* p : {(void*)keys, (void*)keys2, (void*)idx, (void*)idx2, (void*)log2, (void*)ref2})
+        if (p) (void)hipFree(p);
+    if (!rc) ctx->ae_sorted = true;
+    return rc;
+}
+
 int upload_batches(tbg_ctx* ctx, uint32_t n, const uint32_t* batch_lens, const uint64_t* batch_ts,
                    uint32_t nb) {
     if (nb == 0 || nb > ctx->opt.batch_count_max) return TBG_EINVAL;
@@ -778,6 +936,14 @@ tbg_ctx* tbg_open(const tbg_options* options) {
     ok = ok && dev_alloc(ctx, &ctx->acc_ts_index, acc_cap, false) &&
          dev_alloc(ctx, &ctx->tr_ts_index, tr_cap, false) &&
          dev_alloc(ctx, &ctx->sel_buf, std::max(acc_cap, tr_cap), false);
+    if (options->account_events_capacity) {
+        ctx->ae_cap = options->account_events_capacity;
+        ok = ok && dev_alloc(ctx, &ctx->ae_log, ctx->ae_cap, false) &&
+             dev_alloc(ctx, &ctx->ae_ref, ctx->ae_cap, false) &&
+             dev_alloc(ctx, &ctx->ae_flags, std::max<uint64_t>(ev_max, options->pulse_batch_max), false) &&
+             dev_alloc(ctx, &ctx->ae_list, std::max<uint64_t>(ev_max, options->pulse_batch_max), false) &&
+             dev_alloc(ctx, &ctx->ae_words, 4, true);
+    }
     ok = ok && hip_ok(ctx, hipHostMalloc(reinterpret_cast<void**>(&ctx->h_scalars),
                                          sizeof(DevScalars)), "hipHostMalloc");
     if (!ok) {
@@ -818,7 +984,10 @@ void tbg_close(tbg_ctx* ctx) {
                     ctx->pulse.keep, ctx->pulse.exp, ctx->pulse.ts, ctx->pulse.rows,
                     ctx->pulse.exp_b, ctx->pulse.rows_b, ctx->pulse.counters,
                     ctx->flow.dup_mark, ctx->flow.counts, ctx->flow.pnt_fired, ctx->flow.lane_counts,
-                    ctx->flow.lane_undo, ctx->flow.engine, ctx->flow.acc_free};
+                    ctx->flow.lane_undo, ctx->flow.engine, ctx->flow.acc_free,
+                    ctx->ae_log, ctx->ae_ref, ctx->ae_flags, ctx->ae_list, ctx->ae_words,
+                    ctx->ae.keys, ctx->ae.vals, ctx->ae.keys_sorted, ctx->ae.vals_sorted,
+                    ctx->ae.deltas, ctx->ae.seg, ctx->ae.values, ctx->ae.scanned};
     free_flow(ctx->flow);
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -910,7 +1079,8 @@ int tbg_create_transfers_device(tbg_ctx* ctx, const tb_transfer_t* d_events, uin
                            target, ctx->bal_items, n, pair_shift, wkeys, ctx->window_partials,
                            ctx->window_carry);
         tmark(ctx, "bal_window");
-        hipLaunchKernelGGL(bal_window_apply, dim3(grid_for(wkeys)), block, 0, ctx->stream, target,
+        hipLaunchKernelGGL(bal_window_apply, dim3((wkeys + 63) / 64), dim3(kApplyThreads), 0,
+                           ctx->stream, target,
                            ctx->window_partials, nwg, pair_shift, wkeys, ctx->T.acc_rows_used,
                            ctx->window_carry);
         tmark(ctx, "bal_apply");
@@ -968,6 +1138,7 @@ int tbg_create_transfers_device(tbg_ctx* ctx, const tb_transfer_t* d_events, uin
     if (replay && (ctx->h_scalars->flags & kFlagImported)) rc = check_imported_indexes(ctx, true);
     if (replay && !rc) rc = run_replay(ctx, c, true, false);
     if (!rc) rc = end_call(ctx, n, !replay);
+    if (!rc && ctx->ae_log) rc = ae_transfers(ctx, c);
     ctx->stream = saved;
     ctx->T.tr_rows_used += n;  // rows are consumed whether or not the events created objects
     ctx->tr_ts_stale = true;
@@ -1152,7 +1323,8 @@ int64_t tbg_pulse(tbg_ctx* ctx, uint64_t timestamp) {
     if (!ctx) return TBG_EINVAL;
     PulseGather G;
     const uint64_t batch_max = ctx->opt.pulse_batch_max;
-    int rc = pulse_gather(ctx, timestamp, false, &G);
+    // AccountEvents are stamped in expiry order: the candidates must be in index order.
+    int rc = pulse_gather(ctx, timestamp, ctx->ae_log != nullptr, &G);
     if (rc) return rc;
     uint64_t expired = std::min<uint64_t>(G.cands, batch_max);
     uint64_t pulse_next = G.next_unexpired == ~0ull ? TB_TIMESTAMP_MAX : G.next_unexpired;
@@ -1168,6 +1340,7 @@ int64_t tbg_pulse(tbg_ctx* ctx, uint64_t timestamp) {
         pulse_next = last;
     }
     rc = pulse_finish(ctx, expired, G.kept, pulse_next);
+    if (!rc && ctx->ae_log) rc = ae_expiry(ctx, ctx->pulse.rows, expired, timestamp);
     return rc ? rc : int64_t(expired);
 }
 
@@ -1202,6 +1375,7 @@ int64_t tbg_pulse_cut(tbg_ctx* ctx, uint64_t timestamp, uint64_t cut_expires_at,
                                   (e[expired] == cut_expires_at && t[expired] <= cut_timestamp)))
         expired++;
     rc = pulse_finish(ctx, expired, G.kept, pulse_next_timestamp);
+    if (!rc && ctx->ae_log) rc = ae_expiry(ctx, ctx->pulse.rows, expired, timestamp);
     return rc ? rc : int64_t(expired);
 }
 
@@ -1242,6 +1416,53 @@ int tbg_debug_set_account_balances(tbg_ctx* ctx, tb_uint128_t id, tb_uint128_t d
     HIP_TRY(ctx, hipMemcpyAsync(&rc, d_rc, 4, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     return rc;
+}
+
+int64_t tbg_dump_account_events(tbg_ctx* ctx, tb_account_event_t* out) {
+    if (!ctx) return TBG_EINVAL;
+    if (!out || ctx->ae_used == 0) return int64_t(ctx->ae_used);
+    int rc = ae_sort_log(ctx);
+    if (rc) return rc;
+    HIP_TRY(ctx, hipMemcpyAsync(out, ctx->ae_log, ctx->ae_used * sizeof(tb_account_event_t),
+                                hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return int64_t(ctx->ae_used);
+}
+
+int64_t tbg_get_change_events(tbg_ctx* ctx, const tb_change_events_filter_t* filter,
+                              uint32_t limit_max, tb_change_event_t* out) {
+    if (!ctx || !filter) return TBG_EINVAL;
+    // get_scan_from_change_events_filter (:2396-2434): an invalid filter yields no results.
+    bool reserved_zero = true;
+    for (int i = 0; i < 44; i++) reserved_zero &= filter->reserved[i] == 0;
+    const uint64_t tmin = filter->timestamp_min, tmax = filter->timestamp_max;
+    const bool valid = (tmin == 0 || (tmin >= TB_TIMESTAMP_MIN && tmin <= TB_TIMESTAMP_MAX)) &&
+                       (tmax == 0 || (tmax >= TB_TIMESTAMP_MIN && tmax <= TB_TIMESTAMP_MAX)) &&
+                       (tmax == 0 || tmin <= tmax) && filter->limit != 0 && reserved_zero;
+    if (!valid || ctx->ae_used == 0) return 0;
+    int rc = ae_sort_log(ctx);
+    if (rc) return rc;
+    const uint64_t lo = tmin == 0 ? TB_TIMESTAMP_MIN : tmin;
+    const uint64_t hi = tmax == 0 ? TB_TIMESTAMP_MAX : tmax;
+    hipLaunchKernelGGL(ae_bounds, dim3(1), dim3(64), 0, ctx->stream, ctx->ae_log, ctx->ae_used, lo,
+                       hi, ctx->ae_words);
+    unsigned long long b[2] = {0, 0};
+    HIP_TRY(ctx, hipMemcpyAsync(b, ctx->ae_words, 16, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    const uint64_t limit = std::min<uint64_t>(filter->limit, limit_max);
+    const uint32_t count = uint32_t(std::min<uint64_t>(limit, b[1] - b[0]));
+    if (count == 0 || !out) return count;
+    tb_change_event_t* d_out = nullptr;
+    if (!dev_alloc(ctx, &d_out, count, false)) return TBG_ENOMEM;
+    hipLaunchKernelGGL(ae_change_events, dim3(grid_for(count)), dim3(kBlock), 0, ctx->stream,
+                       ctx->T, ctx->ae_log, ctx->ae_ref, b[0], count, d_out);
+    int64_t result = count;
+    if (!hip_ok(ctx, hipMemcpyAsync(out, d_out, size_t(count) * sizeof(tb_change_event_t),
+                                    hipMemcpyDeviceToHost, ctx->stream), "change events copy") ||
+        !hip_ok(ctx, hipStreamSynchronize(ctx->stream), "sync"))
+        result = TBG_EHIP;
+    (void)hipFree(d_out);
+    return result;
 }
 
 int tbg_last_stats(tbg_ctx* ctx, tbg_stats* out) {

@@ -960,23 +960,35 @@ __global__ void __launch_bounds__(kWindowThreads) bal_window_accumulate(
     for (uint32_t k = threadIdx.x; k < wkeys; k += kWindowThreads) out[k] = acc[k];
 }
 
-__global__ void bal_window_apply(BalTarget B, const uint32_t* partials, uint32_t nwg,
-                                 uint32_t ps, uint32_t wkeys, uint64_t rows_used,
-                                 unsigned long long* carry) {
-    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= wkeys) return;
+// One workgroup per 64 window keys: its 16 waves each sum every 16th workgroup's partials for
+// those keys (coalesced 256-B rows), then LDS combines them -- 5,000 waves over the chip instead
+// of one lane walking all partials of a key.
+constexpr uint32_t kApplyThreads = 1024;
+__global__ void __launch_bounds__(kApplyThreads) bal_window_apply(
+    BalTarget B, const uint32_t* partials, uint32_t nwg, uint32_t ps, uint32_t wkeys,
+    uint64_t rows_used, unsigned long long* carry) {
+    __shared__ uint64_t part[kApplyThreads / 64][64];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t k = blockIdx.x * 64 + lane;
+    uint64_t s = 0;
+    if (k < wkeys) {
+        uint32_t w = wv;
+        for (; w + 3 * (kApplyThreads / 64) < nwg; w += 4 * (kApplyThreads / 64)) {
+            uint32_t x[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                x[j] = partials[uint64_t(w + j * (kApplyThreads / 64)) * wkeys + k];
+#pragma unroll
+            for (int j = 0; j < 4; j++) s += x[j];
+        }
+        for (; w < nwg; w += kApplyThreads / 64) s += partials[uint64_t(w) * wkeys + k];
+    }
+    part[wv][lane] = s;
+    __syncthreads();
+    if (wv != 0 || k >= wkeys) return;
+    for (uint32_t j = 1; j < kApplyThreads / 64; j++) s += part[j][lane];
     const uint32_t row = k & ((1u << ps) - 1), f = k >> ps;
     if (row >= rows_used) return;
-    uint64_t s = 0;
-    uint32_t w = 0;
-    for (; w + 8 <= nwg; w += 8) {
-        uint32_t x[8];
-#pragma unroll
-        for (int j = 0; j < 8; j++) x[j] = partials[uint64_t(w + j) * wkeys + k];
-#pragma unroll
-        for (int j = 0; j < 8; j++) s += x[j];
-    }
-    for (; w < nwg; w++) s += partials[uint64_t(w) * wkeys + k];
     u128 sum = s;
     const unsigned long long c = carry[k];
     if (c) {

@@ -34,6 +34,7 @@ bool operation_info(uint8_t operation, OperationInfo* info) {
         case TB_OPERATION_CREATE_TRANSFERS: *info = {128, 16, true}; return true;
         case TB_OPERATION_LOOKUP_ACCOUNTS: *info = {16, 128, true}; return true;
         case TB_OPERATION_LOOKUP_TRANSFERS: *info = {16, 128, true}; return true;
+        case TB_OPERATION_GET_CHANGE_EVENTS: *info = {64, 384, false}; return true;
         default: return false;
     }
 }
@@ -141,6 +142,8 @@ struct tb_sm {
 
     bool batch_valid(uint8_t operation, const OperationInfo& info, uint32_t batch_size) const {
         if (operation == TB_OPERATION_PULSE) return batch_size == 0;
+        // Not batchable (queries): exactly one filter.
+        if (operation == TB_OPERATION_GET_CHANGE_EVENTS) return batch_size == info.event_size;
         if (batch_size % info.event_size != 0) return false;
         return batch_size / info.event_size <= event_max(info, options.batch_size_limit);
     }
@@ -167,6 +170,10 @@ int64_t gpu_lookup_transfers(void* self, const tb_uint128_t* ids, uint32_t n,
                              tb_transfer_t* out) {
     return tbg_lookup_transfers(static_cast<tbg_ctx*>(self), ids, n, out);
 }
+int64_t gpu_get_change_events(void* self, const tb_change_events_filter_t* filter,
+                              uint32_t limit_max, tb_change_event_t* out) {
+    return tbg_get_change_events(static_cast<tbg_ctx*>(self), filter, limit_max, out);
+}
 
 }  // namespace
 
@@ -192,6 +199,7 @@ extern "C" tb_sm* tb_sm_open_gpu(const tb_sm_options* options, const tbg_options
     ex.pulse_next_timestamp = gpu_pulse_next;
     ex.lookup_accounts = gpu_lookup_accounts;
     ex.lookup_transfers = gpu_lookup_transfers;
+    ex.get_change_events = gpu_get_change_events;
     tb_sm* sm = tb_sm_open(options, &ex);
     if (!sm) {
         tbg_close(ctx);
@@ -282,6 +290,24 @@ extern "C" int64_t tb_sm_commit(tb_sm* sm, uint64_t client_lo, uint64_t client_h
         if (expired < 0) return expired;
         if (expired > 0) sm->commit_timestamp = timestamp;
         return 0;
+    }
+
+    if (operation == TB_OPERATION_GET_CHANGE_EVENTS) {
+        // execute_query(.get_change_events) (:2770-2800, :3395-3422): not multi-batch; the scan
+        // limit is capped by the reply size and the prefetches available per scanned result
+        // (prefetch_get_change_events_scan, :2232-2265): transfers, and 2 accounts per event.
+        if (size != sizeof(tb_change_events_filter_t) || !sm->executor.get_change_events)
+            return TBG_EINVAL;
+        tb_change_events_filter_t filter;
+        std::memcpy(&filter, body, sizeof(filter));
+        const OperationInfo lookup{16, 128, false};  // deprecated_lookup_*_unbatched
+        const uint32_t prefetch = sm->event_max(lookup, sm->options.batch_size_limit);
+        const uint32_t limit_max = std::min({sm->options.message_body_size_max / 384u, prefetch,
+                                             prefetch / 2});
+        if (limit_max == 0) return 0;
+        int64_t count = sm->executor.get_change_events(sm->executor.self, &filter, limit_max,
+                                                       static_cast<tb_change_event_t*>(output));
+        return count < 0 ? count : count * int64_t(sizeof(tb_change_event_t));
     }
 
     uint32_t payload = 0;

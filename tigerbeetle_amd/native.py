@@ -34,6 +34,7 @@ class TbgOptions(ctypes.Structure):
         ("pulse_batch_max", ctypes.c_uint32),
         ("device", ctypes.c_uint32),
         ("pulse_next_timestamp_init", ctypes.c_uint64),
+        ("account_events_capacity", ctypes.c_uint64),
     ]
 
 
@@ -64,6 +65,7 @@ class Executor(ctypes.Structure):
         ("pulse_next_timestamp", vp),
         ("lookup_accounts", vp),
         ("lookup_transfers", vp),
+        ("get_change_events", vp),
     ]
 
 
@@ -92,6 +94,8 @@ SIGNATURES = [
     ("tbg_lookup_transfers", ctypes.c_int64, [vp, vp, ctypes.c_uint32, vp]),
     ("tbg_dump_accounts", ctypes.c_int64, [vp, vp]),
     ("tbg_dump_transfers", ctypes.c_int64, [vp, vp, vp]),
+    ("tbg_dump_account_events", ctypes.c_int64, [vp, vp]),
+    ("tbg_get_change_events", ctypes.c_int64, [vp, vp, ctypes.c_uint32, vp]),
     ("tbg_debug_set_account_balances", ctypes.c_int, [vp, U128, U128, U128, U128, U128]),
     ("tbg_last_stats", ctypes.c_int, [vp, ctypes.POINTER(TbgStats)]),
     ("tbg_debug_force_replay", ctypes.c_int, [vp, ctypes.c_int]),

@@ -50,12 +50,54 @@ TRANSFER_DTYPE = np.dtype([
     ("timestamp", "<u8"),
 ])
 
+# src/state_machine.zig:104-220 (AccountEvent)
+ACCOUNT_EVENT_DTYPE = np.dtype([
+    ("dr_account_id",) + _u128, ("dr_debits_pending",) + _u128, ("dr_debits_posted",) + _u128,
+    ("dr_credits_pending",) + _u128, ("dr_credits_posted",) + _u128,
+    ("cr_account_id",) + _u128, ("cr_debits_pending",) + _u128, ("cr_debits_posted",) + _u128,
+    ("cr_credits_pending",) + _u128, ("cr_credits_posted",) + _u128,
+    ("timestamp", "<u8"), ("dr_account_timestamp", "<u8"), ("cr_account_timestamp", "<u8"),
+    ("dr_account_flags", "<u2"), ("cr_account_flags", "<u2"), ("transfer_flags", "<u2"),
+    ("transfer_pending_flags", "<u2"), ("transfer_pending_id",) + _u128,
+    ("amount_requested",) + _u128, ("amount",) + _u128, ("ledger", "<u4"),
+    ("transfer_pending_status", "u1"), ("reserved", "u1", (11,)),
+])
+
+# src/tigerbeetle.zig:622-670 (ChangeEvent)
+CHANGE_EVENT_DTYPE = np.dtype([
+    ("transfer_id",) + _u128, ("transfer_amount",) + _u128, ("transfer_pending_id",) + _u128,
+    ("transfer_user_data_128",) + _u128, ("transfer_user_data_64", "<u8"),
+    ("transfer_user_data_32", "<u4"), ("transfer_timeout", "<u4"), ("transfer_code", "<u2"),
+    ("transfer_flags", "<u2"), ("ledger", "<u4"), ("type", "u1"), ("reserved", "u1", (39,)),
+    ("debit_account_id",) + _u128, ("debit_account_debits_pending",) + _u128,
+    ("debit_account_debits_posted",) + _u128, ("debit_account_credits_pending",) + _u128,
+    ("debit_account_credits_posted",) + _u128, ("debit_account_user_data_128",) + _u128,
+    ("debit_account_user_data_64", "<u8"), ("debit_account_user_data_32", "<u4"),
+    ("debit_account_code", "<u2"), ("debit_account_flags", "<u2"),
+    ("credit_account_id",) + _u128, ("credit_account_debits_pending",) + _u128,
+    ("credit_account_debits_posted",) + _u128, ("credit_account_credits_pending",) + _u128,
+    ("credit_account_credits_posted",) + _u128, ("credit_account_user_data_128",) + _u128,
+    ("credit_account_user_data_64", "<u8"), ("credit_account_user_data_32", "<u4"),
+    ("credit_account_code", "<u2"), ("credit_account_flags", "<u2"),
+    ("timestamp", "<u8"), ("transfer_timestamp", "<u8"), ("debit_account_timestamp", "<u8"),
+    ("credit_account_timestamp", "<u8"),
+])
+
+# src/tigerbeetle.zig:672-682 (ChangeEventsFilter)
+CHANGE_EVENTS_FILTER_DTYPE = np.dtype([("timestamp_min", "<u8"), ("timestamp_max", "<u8"),
+                                       ("limit", "<u4"), ("reserved", "u1", (44,))])
+
 # src/tigerbeetle.zig:471-493
 RESULT_DTYPE = np.dtype([("timestamp", "<u8"), ("status", "<u4"), ("reserved", "<u4")])
 
 assert ACCOUNT_DTYPE.itemsize == 128
 assert TRANSFER_DTYPE.itemsize == 128
 assert RESULT_DTYPE.itemsize == 16
+assert ACCOUNT_EVENT_DTYPE.itemsize == 256
+assert CHANGE_EVENT_DTYPE.itemsize == 384
+assert CHANGE_EVENT_DTYPE.fields["debit_account_id"][1] == 128
+assert CHANGE_EVENT_DTYPE.fields["timestamp"][1] == 352
+assert CHANGE_EVENTS_FILTER_DTYPE.itemsize == 64
 
 
 class AccountFlags(enum.IntFlag):
@@ -199,6 +241,7 @@ TRANSIENT_TRANSFER_STATUSES = frozenset({
 class Operation(enum.IntEnum):
     """The operations of this path (src/tigerbeetle.zig:685-1004; vsr_operations_reserved = 128)."""
     pulse = 128
+    get_change_events = 137
     create_accounts = 146
     create_transfers = 147
     lookup_accounts = 140

@@ -6,9 +6,9 @@ tag=${1:-run}; shift
 out=gpurun_out/$tag
 mkdir -p $out
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
-    > $out/gpu_tests.log 2>&1 || { tail -30 $out/gpu_tests.log; exit 1; }
-tail -3 $out/gpu_tests.log
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+    --durations=12 > $out/gpu_tests.log 2>&1 || { tail -40 $out/gpu_tests.log; exit 1; }
+tail -16 $out/gpu_tests.log
 timeout -k 10 300 python -u bench.py "$@" > $out/bench.json 2> $out/bench.err || { cat $out/bench.err; exit 1; }
 cat $out/bench.json
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$out/prof -o run -- \
