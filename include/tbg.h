@@ -99,6 +99,10 @@ int64_t tbg_pulse_candidates(tbg_ctx* ctx, uint64_t timestamp, uint64_t* expires
 int64_t tbg_pulse_cut(tbg_ctx* ctx, uint64_t timestamp, uint64_t cut_expires_at,
                       uint64_t cut_timestamp, uint64_t pulse_next_timestamp);
 
+/* Sharded imported batches: raises the accounts / transfers objects trees' key_range.key_max
+ * (read only by imported events' must_not_regress checks) to the maxima over every shard. */
+int tbg_raise_key_max(tbg_ctx* ctx, uint64_t accounts_key_max, uint64_t transfers_key_max);
+
 /* Found objects only, in request order; returns the count written. */
 int64_t tbg_lookup_accounts(tbg_ctx* ctx, const tb_uint128_t* ids, uint32_t n, tb_account_t* out);
 int64_t tbg_lookup_transfers(tbg_ctx* ctx, const tb_uint128_t* ids, uint32_t n,

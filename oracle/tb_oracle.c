@@ -1036,6 +1036,11 @@ uint64_t tbo_dump_pending_status(const tbo_ctx* c, uint8_t* out) {
     return c->n_transfers;
 }
 
+void tbo_raise_key_max(tbo_ctx* c, uint64_t accounts_key_max, uint64_t transfers_key_max) {
+    if (accounts_key_max) key_range_update(&c->accounts_range, accounts_key_max);
+    if (transfers_key_max) key_range_update(&c->transfers_range, transfers_key_max);
+}
+
 uint64_t tbo_dump_account_events(const tbo_ctx* c, tb_account_event_t* out) {
     if (out) memcpy(out, c->events, c->n_events * sizeof(tb_account_event_t));
     return c->n_events;

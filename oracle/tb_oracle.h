@@ -69,6 +69,10 @@ uint64_t tbo_dump_accounts(const tbo_ctx* ctx, tb_account_t* out);   /* creation
 uint64_t tbo_dump_transfers(const tbo_ctx* ctx, tb_transfer_t* out); /* creation order */
 uint64_t tbo_dump_pending_status(const tbo_ctx* ctx, uint8_t* out);  /* per transfer */
 
+/* Sharded imported batches: raises the objects trees' key_range.key_max to the
+ * maxima over every shard (0 = leave), so that imported `must_not_regress` checks see them. */
+void tbo_raise_key_max(tbo_ctx* ctx, uint64_t accounts_key_max, uint64_t transfers_key_max);
+
 /* The account_events groove in insertion order (AccountEvent, state_machine.zig:104-220). */
 uint64_t tbo_dump_account_events(const tbo_ctx* ctx, tb_account_event_t* out);
 /* get_change_events (state_machine.zig:2396-2434, :3395-3527): ChangeEvents with timestamps in the

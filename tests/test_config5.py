@@ -9,8 +9,6 @@ uniform over a ledger and then over that ledger's accounts (workload.transfers_c
 * The full per-GPU size of 8 GPUs (125M accounts = 1B / 8) with size-independent properties: every
   result `created` at its exact event timestamp (execute_multi_batch :2702-2762), sampled account
   rows with exactly the sums of their transfers as balances, sampled transfer rows byte for byte.
-  The accounts are generated on the device (torch as plumbing) and created with
-  tbg_create_accounts_device.
 """
 import ctypes
 
@@ -63,30 +61,9 @@ def test_config5_parity_vs_oracle():
         p.close()
 
 
-def _device_accounts(torch, j0, j1):
-    """Config-5 account records for local indices [j0, j1) of a single shard (world 1: account k =
-    j), generated on the device as (n, 16) u64 words (same words as workload.accounts_config5;
-    int64 products wrap like u64 ones)."""
-    def s64(c):
-        return c - (1 << 64) if c >= 1 << 63 else c
-    k = torch.arange(j0, j1, dtype=torch.int64, device="cuda")
-    ids = k + 1
-    w = torch.zeros((j1 - j0, 16), dtype=torch.int64, device="cuda")
-    w[:, 0] = ids
-    w[:, 10] = ids * s64(0x9E3779B97F4A7C15)
-    w[:, 11] = ids * s64(0xC2B2AE3D27D4EB4F)
-    w[:, 12] = ids * s64(0x165667B19E3779F9)
-    w[:, 13] = ids & 0xFFFFFFFF
-    w[:, 14] = (1 + k % 64) | (1 << 32) | (8 << 48)
-    return w
-
-
 def test_config5_full_size_properties():
     """125M accounts (what each GPU holds of 1B at 8 GPUs) on 64 ledgers, two 1M-event
     super-batches: all created at exact timestamps; sampled account and transfer rows exact."""
-    torch = pytest.importorskip("torch")
-    if not torch.cuda.is_available():
-        pytest.skip("no HIP device visible to torch")
     lib = native.load()
     A, N, chunk = 125_000_000, 1_000_000, 1 << 22
     o = native.TbgOptions()
@@ -104,18 +81,17 @@ def test_config5_full_size_properties():
         for j0 in range(0, A, chunk):
             j1 = min(A, j0 + chunk)
             n = j1 - j0
-            w = _device_accounts(torch, j0, j1)
+            acc = workload.accounts_config5(np.arange(j0, j1), 0, 1)
             prepare_ts += 1 + n
-            ends = torch.tensor([n], dtype=torch.int32, device="cuda")
-            ts = torch.tensor([prepare_ts], dtype=torch.int64, device="cuda")
-            res = torch.empty((n, 2), dtype=torch.int64, device="cuda")
-            torch.cuda.synchronize()
-            rc = lib.tbg_create_accounts_device(g, w.data_ptr(), n, ends.data_ptr(),
-                                                ts.data_ptr(), 1, res.data_ptr(), None)
+            r = np.zeros(n, dtype=RESULT_DTYPE)
+            rc = lib.tbg_create_accounts(g, acc.ctypes.data_as(ctypes.c_void_p), n,
+                                         np.asarray([n], dtype=np.uint32).ctypes.data_as(
+                                             native.c_u32p),
+                                         np.asarray([prepare_ts], dtype=np.uint64).ctypes.data_as(
+                                             native.c_u64p), 1, r.ctypes.data_as(ctypes.c_void_p))
             assert rc == 0, lib.tbg_last_error(g)
-            r = res.cpu().numpy().view(RESULT_DTYPE).reshape(n)
             assert (r["status"] == CREATED).all()
-            del w, res
+            del acc
         calls = []
         for call in range(2):
             t, dr, cr = workload.transfers_config5(N, A, 0, 1, seed=7 + call, id_offset=call * N)

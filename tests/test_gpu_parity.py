@@ -566,6 +566,16 @@ def test_change_events(force_replay):
             ids.extend(int(x) for x in t["id"][:, 0])
             p.create_transfers(t, _split(len(t), rng, 64))
             p.tick(int(rng.integers(1, 3)) * NS_PER_S)
+        # Pending transfers on plain accounts (some closing), then posts (partial) and voids.
+        plain = [i + 1 for i in range(30) if int(acc["flags"][i]) in (0, 8)]
+        pend_rows = [dict(id=90_000 + i, debit_account_id=plain[i % len(plain)],
+                          credit_account_id=plain[(i + 1) % len(plain)], amount=100 + i,
+                          ledger=1, code=1, flags=2 | (64 if i % 9 == 4 else 0))
+                     for i in range(20)]
+        p.create_transfers(_transfers(pend_rows))
+        p.create_transfers(_transfers(
+            [dict(id=91_000 + i, pending_id=90_000 + i, amount=50, flags=4) for i in range(0, 20, 3)] +
+            [dict(id=92_000 + i, pending_id=90_000 + i, flags=8) for i in range(1, 20, 3)]))
         p.compare_state()
         all_events = p.change_events()
         assert len(all_events) > 100 and {0, 1, 2, 3, 4} <= set(all_events["type"].tolist())

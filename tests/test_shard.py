@@ -81,6 +81,9 @@ class OracleShard:
     def pulse_next_timestamp(self):
         return int(self.lib.tbo_pulse_next_timestamp(self.o))
 
+    def raise_key_max(self, accounts_key_max, transfers_key_max):
+        self.lib.tbo_raise_key_max(self.o, accounts_key_max, transfers_key_max)
+
     def dump(self):
         a = np.zeros(self.lib.tbo_account_count(self.o), dtype=ACCOUNT_DTYPE)
         self.lib.tbo_dump_accounts(self.o, _ptr(a))
@@ -146,6 +149,8 @@ def scenario(seed, calls=8, n_acc=48):
                     dr, cr = rng.choice(pools[ledger], size=2, replace=False)
                     if rng.random() < 0.03:
                         dr = n_acc + 100  # debit_account_not_found
+                    elif rng.random() < 0.04:  # accounts of two ledgers (often two shards)
+                        cr = int(rng.choice(pools[1 + ledger % LEDGERS]))
                     t["debit_account_id"][e, 0] = dr
                     t["credit_account_id"][e, 0] = cr
                     t["amount"][e, 0] = int(rng.integers(1, 500)) if rng.random() < 0.9 else 10**6
@@ -164,6 +169,23 @@ def scenario(seed, calls=8, n_acc=48):
         ops.append(("transfers", t, _split(rng, n, 64)))
         if c % 2 == 1:
             ops.append(("tick", int(rng.integers(1, 3)) * NS_PER_S))
+        if c == calls // 2:  # an imported batch (drive stamps it), some transfers cross-ledger
+            m = 40
+            imp = np.zeros(m, dtype=TRANSFER_DTYPE)
+            for e in range(m):
+                ledger = int(rng.integers(1, LEDGERS + 1))
+                dr, cr = rng.choice(pools[ledger], size=2, replace=False)
+                if rng.random() < 0.1:
+                    cr = int(rng.choice(pools[1 + ledger % LEDGERS]))
+                next_id += 1
+                imp["id"][e, 0] = next_id
+                imp["debit_account_id"][e, 0] = dr
+                imp["credit_account_id"][e, 0] = cr
+                imp["amount"][e, 0] = int(rng.integers(1, 50))
+                imp["ledger"][e] = ledger
+                imp["code"][e] = 1
+                imp["flags"][e] = 256  # imported
+            ops.append(("imported", imp, [m]))
     return ops
 
 
@@ -177,6 +199,10 @@ def drive(cluster, ref, ops, rank0=True, pbm=PBM, cuts=None):
             ts += op[1]
         else:
             kind, ev, lens = op
+            if kind == "imported":  # timestamps after every object so far, before the batch's
+                ev = ev.copy()
+                ev["timestamp"] = ts + 1 + np.arange(len(ev), dtype=np.uint64)
+                kind = "transfers"
             n = len(ev)
             ts += 1 + n
             batch_ts = (ts - n + np.cumsum(lens)).astype(np.uint64)
@@ -280,9 +306,18 @@ def test_router_routes_and_refuses():
     again = _transfers([dict(id=11, debit_account_id=1, credit_account_id=2, amount=1, ledger=1,
                              code=1)])
     assert r.plan_transfers(again, [1], [30]).shard_of.tolist() == [1]
-    with pytest.raises(shard.RouteError, match="spans shards"):  # accounts on two shards
-        r.plan_transfers(_transfers([dict(id=13, debit_account_id=1, credit_account_id=3,
-                                          amount=1, ledger=1, code=1)]), [1], [40])
+    # accounts on two shards: a surrogate on the debit account's shard, the reference's status
+    cross = _transfers([dict(id=13, debit_account_id=1, credit_account_id=3, amount=1, ledger=1,
+                             code=1),
+                        dict(id=14, debit_account_id=1, credit_account_id=3, amount=1, ledger=0,
+                             code=1)])
+    p = r.plan_transfers(cross, [2], [40])
+    assert p.cross == {0: 23, 1: 19}  # accounts_must_have_the_same_ledger, ledger_must_not_be_zero
+    sur = p.shard_events(cross)
+    assert (sur["credit_account_id"] == sur["debit_account_id"]).all()
+    got = _created(2, 40)
+    got["status"] = 12  # the surrogates fail with accounts_must_be_different
+    assert p.patch(got)["status"].tolist() == [23, 19]
     chain = _transfers([
         dict(id=14, debit_account_id=1, credit_account_id=2, amount=1, ledger=1, code=1, flags=1),
         dict(id=15, debit_account_id=3, credit_account_id=4, amount=1, ledger=3, code=1)])
@@ -290,10 +325,18 @@ def test_router_routes_and_refuses():
         r.plan_transfers(chain, [2], [50])
     # the same events with a batch end between them are two chains (the first one left open)
     assert r.plan_transfers(chain, [1, 1], [49, 50]).shard_of.tolist() == [0, 1]
-    with pytest.raises(shard.RouteError, match="imported"):
+    with pytest.raises(shard.RouteError, match="imported"):  # may collide with an account
         r.plan_transfers(_transfers([dict(id=16, debit_account_id=1, credit_account_id=2,
                                           amount=1, ledger=1, code=1, flags=256,
                                           timestamp=5)]), [1], [60])
+    imp = _transfers([dict(id=16, debit_account_id=1, credit_account_id=2, amount=1, ledger=1,
+                           code=1, flags=256, timestamp=55),
+                      dict(id=17, debit_account_id=3, credit_account_id=4, amount=1, ledger=3,
+                           code=1, flags=256, timestamp=56)])
+    assert r.plan_transfers(imp, [2], [60]).imported
+    imp["timestamp"] = [56, 55]  # the second may regress past the first, on another shard
+    with pytest.raises(shard.RouteError, match="regress"):
+        r.plan_transfers(imp, [2], [60])
     timed = _transfers([dict(id=17, debit_account_id=1, credit_account_id=2, amount=5, ledger=1,
                              code=1, flags=2, timeout=1)])
     r.commit(r.plan_transfers(timed, [1], [70]), timed, _created(1, 70))

@@ -1379,6 +1379,22 @@ int64_t tbg_pulse_cut(tbg_ctx* ctx, uint64_t timestamp, uint64_t cut_expires_at,
     return rc ? rc : int64_t(expired);
 }
 
+int tbg_raise_key_max(tbg_ctx* ctx, uint64_t accounts_key_max, uint64_t transfers_key_max) {
+    if (!ctx) return TBG_EINVAL;
+    int rc = sync_scalars(ctx);
+    if (rc) return rc;
+    unsigned long long a = std::max<unsigned long long>(ctx->h_scalars->accounts_key_max,
+                                                        accounts_key_max);
+    unsigned long long t = std::max<unsigned long long>(ctx->h_scalars->transfers_key_max,
+                                                        transfers_key_max);
+    HIP_TRY(ctx, hipMemcpyAsync(&ctx->d_scalars->accounts_key_max, &a, 8, hipMemcpyHostToDevice,
+                                ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(&ctx->d_scalars->transfers_key_max, &t, 8, hipMemcpyHostToDevice,
+                                ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return 0;
+}
+
 uint64_t tbg_pulse_next_timestamp(tbg_ctx* ctx) {
     if (!ctx || sync_scalars(ctx)) return 0;
     return ctx->h_scalars->pulse_next_timestamp;

@@ -90,6 +90,7 @@ SIGNATURES = [
     ("tbg_pulse_cut", ctypes.c_int64, [vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                        ctypes.c_uint64]),
     ("tbg_pulse_next_timestamp", ctypes.c_uint64, [vp]),
+    ("tbg_raise_key_max", ctypes.c_int, [vp, ctypes.c_uint64, ctypes.c_uint64]),
     ("tbg_lookup_accounts", ctypes.c_int64, [vp, vp, ctypes.c_uint32, vp]),
     ("tbg_lookup_transfers", ctypes.c_int64, [vp, vp, ctypes.c_uint32, vp]),
     ("tbg_dump_accounts", ctypes.c_int64, [vp, vp]),

@@ -11,15 +11,30 @@ backend, gloo on CPU), every shard executes its slice, and the 16-byte results c
 Exactness. A shard executes its slice as the reference would execute the whole call only if no
 event of the slice can observe state held by another shard. `LedgerRouter` routes by
 directories of where each account id and each transfer id (created, or orphaned by a transient
-failure) lives, and raises `RouteError` -- before any shard executes -- for every call it cannot
-place exactly:
+failure) lives. Hazards it executes exactly:
 
-* a transfer whose debit and credit accounts live on different shards (the reference answers
-  `accounts_must_have_the_same_ledger`; a shard would answer `*_account_not_found`);
-* a linked chain whose events belong to different shards (a chain is atomic, :3002-3213);
+* a transfer whose debit and credit accounts live on different shards: the reference answers
+  `accounts_must_have_the_same_ledger` (:3795-3798) unless an earlier static check fails first
+  (:3774-3794), and never reads a balance. The router computes that status and sends the shard
+  executing the event's chain a *surrogate* -- the event with its credit account set to its debit
+  account -- which fails at the same position with `accounts_must_be_different`, non-transient
+  like the true status, so a chain around it is rolled back exactly as the reference rolls it back;
+  the router then writes the true status into the result;
+* imported batches: their `must_not_regress` checks read the objects trees' global key ranges
+  (:3656-3665, :3808-3817), so every shard's key maxima are raised to the global ones before the
+  call (`raise_key_max`).
+
+Refused (`RouteError`, before any shard executes) -- the remaining cases no shard can execute
+alone:
+
+* a linked chain whose (non-surrogate) events belong to different shards: a chain is atomic
+  (:3002-3213) and its rollback would span shards;
 * an id repeated within the call where the repeat could execute on a shard other than the
-  first occurrence's (a duplicate's outcome depends on the first occurrence's result);
-* imported events (their checks read the global `key_range` maxima, :3656-3665, :3808-3817);
+  first occurrence's (a duplicate's outcome depends on the first occurrence's result), or a
+  cross-shard transfer whose id repeats an id of the call;
+* imported events whose outcome depends on another shard: a timestamp at or below an imported
+  timestamp of an earlier event of the call on another shard, or at or below the other groove's
+  key maximum (a possible timestamp collision, :3660, :3812);
 * a post/void of a pending transfer that has a timeout: it resets `pulse_next_timestamp` when
   that equals the pending transfer's expiry (:4227-4229), a comparison against the *global*
   value at that point of the call, which no shard holds.
@@ -57,6 +72,14 @@ from .types import (ACCOUNT_DTYPE, RESULT_DTYPE, STATUS_CREATED, TRANSFER_DTYPE,
                     TRANSIENT_TRANSFER_STATUSES, AccountFlags, TransferFlags)
 
 _U128_MAX = (1 << 128) - 1
+# CreateTransferStatus values (src/tigerbeetle.zig:220-469) of the cross-shard checks.
+_ACCOUNTS_MUST_BE_DIFFERENT = 12
+_PENDING_ID_MUST_BE_ZERO = 13
+_TIMEOUT_RESERVED_FOR_PENDING_TRANSFER = 17
+_LEDGER_MUST_NOT_BE_ZERO = 19
+_CODE_MUST_NOT_BE_ZERO = 20
+_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER = 23
+_CLOSING_TRANSFER_MUST_BE_PENDING = 64
 
 
 class RouteError(RuntimeError):
@@ -82,6 +105,25 @@ class Plan:
     kind: str                               # "accounts" | "transfers"
     shard_of: np.ndarray                    # int32 per event
     slices: List[ShardSlice]
+    # cross-shard transfers: event index -> the reference's status (the shard runs a surrogate)
+    cross: Dict[int, int] = field(default_factory=dict)
+    imported: bool = False                  # the call holds imported events (key ranges synced)
+
+    def shard_events(self, events: np.ndarray) -> np.ndarray:
+        """The events as the shards execute them: cross-shard transfers as their surrogates."""
+        if not self.cross:
+            return events
+        ev = events.copy()
+        idx = np.fromiter(self.cross.keys(), dtype=np.int64)
+        ev["credit_account_id"][idx] = ev["debit_account_id"][idx]
+        return ev
+
+    def patch(self, results: np.ndarray) -> np.ndarray:
+        """The true statuses of cross-shard transfers whose surrogate failed as planned."""
+        for k, st in self.cross.items():
+            if int(results[k]["status"]) == _ACCOUNTS_MUST_BE_DIFFERENT:
+                results[k]["status"] = st
+        return results
 
 
 def chain_starts(flags: np.ndarray, lens) -> np.ndarray:
@@ -140,6 +182,9 @@ class LedgerRouter:
         self.account_shard: Dict[int, int] = {}
         self.transfer_shard: Dict[int, int] = {}
         self.timed_pending: Set[int] = set()  # pending transfers created with a timeout
+        # objects trees' key_range.key_max over all shards (largest created timestamp)
+        self.accounts_key_max = 0
+        self.transfers_key_max = 0
 
     def shard_of_ledger(self, ledger: int) -> int:
         if 1 <= ledger <= self.ledgers:
@@ -165,11 +210,34 @@ class LedgerRouter:
                 record(k, sh)
         return shard_of
 
+    def _check_imported(self, imported: np.ndarray, own_ts: np.ndarray, lens, batch_ts,
+                        shard_of: np.ndarray, other_key_max: int, what: str):
+        """Imported events whose checks another shard's state could decide (module doc): every
+        earlier event of the call on another shard may have raised the global key range to its
+        timestamp (an imported event's own, else its commit timestamp)."""
+        lens_a = np.asarray(lens, dtype=np.int64)
+        starts = np.cumsum(lens_a) - lens_a
+        within = np.arange(int(lens_a.sum()), dtype=np.int64) - np.repeat(starts, lens_a)
+        ts = np.repeat(np.asarray(batch_ts, dtype=np.int64) - lens_a, lens_a) + within + 1
+        ts = np.where(imported, own_ts.astype(np.int64), ts).tolist()
+        imp = imported.tolist()
+        sh_of = shard_of.tolist()
+        latest: Dict[int, int] = {}  # shard -> largest timestamp of its events so far
+        for k, (t, sh) in enumerate(zip(ts, sh_of)):
+            if imp[k]:
+                if t <= other_key_max:
+                    raise RouteError(f"imported {what} {k}: timestamp {t} may collide with an "
+                                     f"object of the other groove on another shard")
+                for osh, ot in latest.items():
+                    if osh != sh and t <= ot:
+                        raise RouteError(f"imported {what} {k}: timestamp {t} may regress past "
+                                         f"an event of shard {osh}")
+            latest[sh] = max(latest.get(sh, 0), t)
+
     def plan_accounts(self, events: np.ndarray, lens, batch_ts) -> Plan:
         n = len(events)
         flags = events["flags"]
-        if n and (flags & int(AccountFlags.imported)).any():
-            raise RouteError("imported accounts: key_range checks span shards")
+        imported = (flags & int(AccountFlags.imported)) != 0
         ids = _ids(events["id"])
         ledgers = events["ledger"].tolist()
         in_call: Dict[int, int] = {}
@@ -189,24 +257,46 @@ class LedgerRouter:
 
         shard_of = self._place_chains(n, chain_starts(flags, lens), pins_of,
                                       lambda a: self.shard_of_ledger(ledgers[a]), record)
-        return Plan("accounts", shard_of, split_runs(shard_of, lens, batch_ts, self.shards))
+        if n and imported.any():
+            self._check_imported(imported, events["timestamp"], lens, batch_ts, shard_of,
+                                 self.transfers_key_max, "account")
+        return Plan("accounts", shard_of, split_runs(shard_of, lens, batch_ts, self.shards),
+                    imported=bool(n and imported.any()))
 
     def plan_transfers(self, events: np.ndarray, lens, batch_ts) -> Plan:
         n = len(events)
         flags = events["flags"]
-        if n and (flags & int(TransferFlags.imported)).any():
-            raise RouteError("imported transfers: key_range checks span shards")
+        imported = (flags & int(TransferFlags.imported)) != 0
         ids = _ids(events["id"])
         drs = _ids(events["debit_account_id"])
         crs = _ids(events["credit_account_id"])
         pids = _ids(events["pending_id"])
         ledgers = events["ledger"].tolist()
+        codes = events["code"].tolist()
         timeouts = events["timeout"].tolist()
         fl = flags.tolist()
         in_call: Dict[int, int] = {}
         in_call_timed: Set[int] = set()
+        cross: Dict[int, int] = {}
         post_void = int(TransferFlags.post_pending_transfer | TransferFlags.void_pending_transfer)
         pending = int(TransferFlags.pending)
+        closing = int(TransferFlags.closing_debit | TransferFlags.closing_credit)
+
+        def cross_status(k):
+            # create_transfer :3774-3798 after the account ids: both accounts exist, on shards of
+            # different ledgers.
+            if pids[k] != 0:
+                return _PENDING_ID_MUST_BE_ZERO
+            if not fl[k] & pending:
+                if timeouts[k] != 0:
+                    return _TIMEOUT_RESERVED_FOR_PENDING_TRANSFER
+                if fl[k] & closing:
+                    return _CLOSING_TRANSFER_MUST_BE_PENDING
+            if ledgers[k] == 0:
+                return _LEDGER_MUST_NOT_BE_ZERO
+            if codes[k] == 0:
+                return _CODE_MUST_NOT_BE_ZERO
+            return _ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER
 
         def pins_of(k):
             i = ids[k]
@@ -224,9 +314,13 @@ class LedgerRouter:
                 elif p in in_call:
                     pins.add(in_call[p])
             else:
-                for a in (drs[k], crs[k]):
-                    if a in self.account_shard:
-                        pins.add(self.account_shard[a])
+                a_dr, a_cr = self.account_shard.get(drs[k]), self.account_shard.get(crs[k])
+                if a_dr is not None and a_cr is not None and a_dr != a_cr:
+                    if i in in_call:
+                        raise RouteError(f"cross-shard transfer {k} repeats an id of the call")
+                    cross[k] = cross_status(k)  # a surrogate, on whichever shard runs its chain
+                else:
+                    pins |= {a for a in (a_dr, a_cr) if a is not None}
             return pins
 
         def record(k, sh):
@@ -238,7 +332,11 @@ class LedgerRouter:
 
         shard_of = self._place_chains(n, chain_starts(flags, lens), pins_of,
                                       lambda a: self.shard_of_ledger(ledgers[a]), record)
-        return Plan("transfers", shard_of, split_runs(shard_of, lens, batch_ts, self.shards))
+        if n and imported.any():
+            self._check_imported(imported, events["timestamp"], lens, batch_ts, shard_of,
+                                 self.accounts_key_max, "transfer")
+        return Plan("transfers", shard_of, split_runs(shard_of, lens, batch_ts, self.shards),
+                    cross=cross, imported=bool(n and imported.any()))
 
     # -- directories --------------------------------------------------------------------------
 
@@ -250,8 +348,15 @@ class LedgerRouter:
         def key(k):
             return int(ids[k, 0]) | (int(ids[k, 1]) << 64)
 
+        created = status == STATUS_CREATED
+        if created.any():
+            ts_max = int(results["timestamp"][created].max())
+            if plan.kind == "accounts":
+                self.accounts_key_max = max(self.accounts_key_max, ts_max)
+            else:
+                self.transfers_key_max = max(self.transfers_key_max, ts_max)
         if plan.kind == "accounts":
-            for k in np.nonzero(status == STATUS_CREATED)[0].tolist():
+            for k in np.nonzero(created)[0].tolist():
                 self.account_shard[key(k)] = int(plan.shard_of[k])
             return
         keep = status == STATUS_CREATED
@@ -300,15 +405,19 @@ class LocalShards:
         events = np.ascontiguousarray(events, dtype=dtype)
         plan = (self.router.plan_accounts if kind == "accounts"
                 else self.router.plan_transfers)(events, lens, batch_ts)
+        if plan.imported:
+            for ex in self.executors:
+                ex.raise_key_max(self.router.accounts_key_max, self.router.transfers_key_max)
+        exec_events = plan.shard_events(events)
         outs = []
         for sl, ex in zip(plan.slices, self.executors):
             if not len(sl.index):
                 outs.append(None)
                 continue
             fn = ex.create_accounts if kind == "accounts" else ex.create_transfers
-            outs.append(fn(np.ascontiguousarray(events[sl.index]), sl.lens,
+            outs.append(fn(np.ascontiguousarray(exec_events[sl.index]), sl.lens,
                            np.asarray(sl.batch_ts, dtype=np.uint64)))
-        results = gather_results(plan, outs, len(events))
+        results = plan.patch(gather_results(plan, outs, len(events)))
         self.router.commit(plan, events, results)
         return results
 
@@ -390,16 +499,24 @@ class ShardGroup:
                         else self.router.plan_transfers)(events, lens, batch_ts)
             except RouteError as e:
                 err = e
-        if self._bcast(0 if err is None else 1):  # every rank fails a refused call
+        # Status word: refused, or the global key maxima an imported call needs on every shard.
+        word = self._bcast_words([0 if err is None else 1,
+                                  int(plan is not None and plan.imported),
+                                  self.router.accounts_key_max if self.rank == 0 else 0,
+                                  self.router.transfers_key_max if self.rank == 0 else 0])
+        if word[0]:  # every rank fails a refused call
             raise err if err is not None else RouteError("refused by the router on rank 0")
+        if word[1]:
+            self.executor.raise_key_max(word[2], word[3])
         if self.rank == 0:
+            exec_events = plan.shard_events(events)
             for s in range(1, self.world):
                 sl = plan.slices[s]
-                self._send(events[sl.index], s)
+                self._send(exec_events[sl.index], s)
                 self._send(np.asarray(sl.lens, dtype=np.uint32), s)
                 self._send(np.asarray(sl.batch_ts, dtype=np.uint64), s)
             sl = plan.slices[0]
-            mine = (events[sl.index], sl.lens, np.asarray(sl.batch_ts, dtype=np.uint64))
+            mine = (exec_events[sl.index], sl.lens, np.asarray(sl.batch_ts, dtype=np.uint64))
         else:
             ev = self._recv(0, dtype)
             ln = self._recv(0, np.uint32)
@@ -434,9 +551,15 @@ class ShardGroup:
             raise RuntimeError("a shard's executor failed; the shards' state is undefined")
         if self.rank != 0:
             return None
-        results = gather_results(plan, outs, len(events))
+        results = plan.patch(gather_results(plan, outs, len(events)))
         self.router.commit(plan, events, results)
         return results
+
+    def _bcast_words(self, words):
+        import torch
+        t = torch.tensor(words, dtype=torch.int64, device=self.device)
+        self.dist.broadcast(t, self._peer(0), group=self.group)
+        return [int(x) for x in t.tolist()]
 
     def create_accounts(self, events=None, lens=None, batch_ts=None):
         """Collective: rank 0 passes the call, the other ranks call with no arguments."""
@@ -553,6 +676,11 @@ class GpuShard:
 
     def pulse_next_timestamp(self):
         return int(self.lib.tbg_pulse_next_timestamp(self.g))
+
+    def raise_key_max(self, accounts_key_max, transfers_key_max):
+        rc = self.lib.tbg_raise_key_max(self.g, accounts_key_max, transfers_key_max)
+        if rc != 0:
+            raise RuntimeError(f"libtbg: {rc} {self.lib.tbg_last_error(self.g)}")
 
     def dump(self):
         c = self._c
