@@ -83,6 +83,13 @@ int tbg_create_transfers_device(tbg_ctx* ctx, const tb_transfer_t* d_events, uin
                                 const uint32_t* d_batch_ends, const uint64_t* d_batch_timestamps,
                                 uint32_t n_batches, tb_create_result_t* d_results, void* stream);
 
+/* A ledger shard's slice of a routed call (tigerbeetle_amd/shard.py): the events keep their
+ * global commit timestamps, given per event (increasing, not necessarily contiguous); the slice is
+ * one batch for linked-chain and imported semantics. Device pointers, stream-ordered. */
+int tbg_create_transfers_stamped_device(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t n,
+                                        const uint64_t* d_event_timestamps,
+                                        tb_create_result_t* d_results, void* stream);
+
 /* Returns the number of pending transfers expired (<= pulse_batch_max). */
 int64_t tbg_pulse(tbg_ctx* ctx, uint64_t timestamp);
 uint64_t tbg_pulse_next_timestamp(tbg_ctx* ctx);

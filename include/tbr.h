@@ -1,0 +1,64 @@
+/*
+ * tbr.h -- C ABI of the device-side ledger router (multi-GPU).
+ *
+ * A client call (create_transfers over any number of batches) enters at one GPU; the router
+ * assigns every event to the ledger shard (GPU) that holds its accounts, and scatters the call
+ * into per-shard slices that keep every event's global commit timestamp (executed there with
+ * tbg_create_transfers_stamped_device). Its directories -- account id -> shard, transfer id ->
+ * shard (created and orphaned ids, `timed` when a pending transfer has a timeout) -- are HBM
+ * open-addressing tables probed like the executor's id tables.
+ *
+ * The device fast path (tbr_route_device) takes calls in which no event can observe another
+ * shard's state: single (unlinked), non-imported, not post/void events whose two accounts are
+ * known and on one shard and whose id is new to every shard and unique in the call. Any other
+ * event is a *hazard*: the call is left to the exact router (tigerbeetle_amd/shard.py,
+ * LedgerRouter), which reads the same directories through tbr_account_shards /
+ * tbr_transfer_shards and records its outcome with tbr_record_*.
+ *
+ * Reference: the shard boundary follows `accounts_must_have_the_same_ledger` /
+ * `transfer_must_have_the_same_ledger_as_accounts` (src/state_machine.zig:3795-3798); transfer
+ * ids are global (create_transfer's id lookup, :3733-3760).
+ */
+#ifndef TBR_H
+#define TBR_H
+
+#include "tb_types.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct tbr_ctx tbr_ctx;
+
+#define TBR_TIMED 0x80u /* transfer directory: a pending transfer with a timeout */
+
+tbr_ctx* tbr_open(uint32_t shards, uint64_t account_capacity, uint64_t transfer_capacity,
+                  uint32_t events_max, uint32_t device);
+void tbr_close(tbr_ctx* ctx);
+
+/* Directory access (host buffers). Lookups write the shard (| TBR_TIMED for transfers) or -1. */
+int tbr_record_accounts(tbr_ctx* ctx, const tb_uint128_t* ids, const uint8_t* shards, uint32_t n);
+int tbr_record_transfers(tbr_ctx* ctx, const tb_uint128_t* ids, const uint8_t* shards, uint32_t n);
+int64_t tbr_account_shards(tbr_ctx* ctx, const tb_uint128_t* ids, uint32_t n, int32_t* out);
+int64_t tbr_transfer_shards(tbr_ctx* ctx, const tb_uint128_t* ids, uint32_t n, int32_t* out);
+
+/* The fast path (device pointers, synchronous). Returns 0 when the call was routed: slices in
+ * shard order at d_out_events / d_out_timestamps (event i of shard s at offset
+ * sum(shard_counts[< s]) + i), d_out_positions = each slice event's position in the call,
+ * shard_counts[shards] on the host; the call's ids are held for it until tbr_settle_device.
+ * Returns 1 when the call holds a hazard (nothing routed, nothing held); < 0 on error. */
+int64_t tbr_route_device(tbr_ctx* ctx, const tb_transfer_t* d_events, uint32_t n,
+                         const uint32_t* d_batch_ends, const uint64_t* d_batch_timestamps,
+                         uint32_t n_batches, tb_transfer_t* d_out_events,
+                         uint64_t* d_out_timestamps, uint32_t* d_out_positions,
+                         uint32_t* shard_counts);
+/* The routed call's results (in shard order) back to call order; records the ids that now exist
+ * on their shard (created, or orphaned by a transient failure) and releases the others. */
+int tbr_settle_device(tbr_ctx* ctx, const tb_create_result_t* d_shard_results,
+                      const uint32_t* d_positions, uint32_t n, tb_create_result_t* d_results);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TBR_H */

@@ -12,21 +12,23 @@ def declared_functions(header):
     text = open(os.path.join(ROOT, "include", header)).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     names = set()
-    for m in re.finditer(r"^[A-Za-z_][\w\s\*]*?\b((?:tbg|tb_sm|tb_multi_batch)_\w+)\s*\(", text,
+    for m in re.finditer(r"^[A-Za-z_][\w\s\*]*?\b((?:tbg|tbr|tb_sm|tb_multi_batch)_\w+)\s*\(", text,
                          flags=re.M):
         names.add(m.group(1))
     return names
 
 
 def test_headers_declare_the_bound_symbols():
-    declared = declared_functions("tbg.h") | declared_functions("tb_state_machine.h")
+    declared = (declared_functions("tbg.h") | declared_functions("tb_state_machine.h") |
+                declared_functions("tbr.h"))
     bound = {name for name, _, _ in native.SIGNATURES}
     assert declared == bound, (declared - bound, bound - declared)
 
 
 def test_library_exports_every_declared_symbol():
     lib = native.load()
-    for name in declared_functions("tbg.h") | declared_functions("tb_state_machine.h"):
+    for name in (declared_functions("tbg.h") | declared_functions("tb_state_machine.h") |
+                 declared_functions("tbr.h")):
         assert hasattr(lib, name), name
 
 

@@ -293,7 +293,7 @@ def test_router_routes_and_refuses():
     acc = _accounts([1, 2, 3, 4], [1, 1, 3, 3])
     plan = r.plan_accounts(acc, [4], [10])
     r.commit(plan, acc, _created(4, 10))
-    assert r.account_shard == {1: 0, 2: 0, 3: 1, 4: 1}
+    assert r.dir.accounts == {1: 0, 2: 0, 3: 1, 4: 1}
     ok = _transfers([dict(id=10, debit_account_id=1, credit_account_id=2, amount=1, ledger=1, code=1),
                      dict(id=11, debit_account_id=3, credit_account_id=4, amount=1, ledger=3, code=1),
                      dict(id=12, debit_account_id=99, credit_account_id=4, amount=1, ledger=3,

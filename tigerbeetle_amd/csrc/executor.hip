@@ -282,6 +282,7 @@ Call<Event> make_call(tbg_ctx* ctx, const Event* d_events, uint32_t n, const uin
     c.bucket_counts = nullptr;
     c.n_buckets = 0;
     c.chunk_info = nullptr;
+    c.event_ts = nullptr;
     c.ev_slot = ctx->ev_slot;
     c.ev_dr = ctx->ev_dr;
     c.ev_cr = ctx->ev_cr;
@@ -1000,9 +1001,14 @@ void tbg_close(tbg_ctx* ctx) {
 
 const char* tbg_last_error(const tbg_ctx* ctx) { return ctx ? ctx->error.c_str() : "null ctx"; }
 
-int tbg_create_transfers_device(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t n,
-                                const uint32_t* d_batch_ends, const uint64_t* d_batch_ts,
-                                uint32_t n_batches, tb_create_result_t* d_results, void* stream) {
+}  // extern "C"
+
+namespace {
+
+int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t n,
+                          const uint32_t* d_batch_ends, const uint64_t* d_batch_ts,
+                          uint32_t n_batches, tb_create_result_t* d_results, void* stream,
+                          const uint64_t* d_event_ts) {
     if (!ctx || n > ctx->opt.batch_events_max || n_batches > ctx->opt.batch_count_max)
         return TBG_EINVAL;
     if (ctx->T.tr_rows_used + n > ctx->opt.transfer_capacity) {
@@ -1015,6 +1021,7 @@ int tbg_create_transfers_device(tbg_ctx* ctx, const tb_transfer_t* d_events, uin
     int rc = begin_call(ctx);
     Call<tb_transfer_t> c = make_call(ctx, d_events, n, d_batch_ends, d_batch_ts, n_batches,
                                       d_results, ctx->T.tr_rows_used);
+    c.event_ts = d_event_ts;
     const dim3 grid(std::min(grid_for(n), kMaxGrid)), block(kBlock);  // grid-stride kernels
     // tr_ingest: 12,288 workgroups (48 per CU) beat the grid-stride default of 4,096 by 3 % on
     // config 2 (0.707 vs 0.728 ms per 10M events); 32,768 and more lose 40 %.
@@ -1143,6 +1150,34 @@ int tbg_create_transfers_device(tbg_ctx* ctx, const tb_transfer_t* d_events, uin
     ctx->T.tr_rows_used += n;  // rows are consumed whether or not the events created objects
     ctx->tr_ts_stale = true;
     return rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+int tbg_create_transfers_device(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t n,
+                                const uint32_t* d_batch_ends, const uint64_t* d_batch_ts,
+                                uint32_t n_batches, tb_create_result_t* d_results, void* stream) {
+    return create_transfers_impl(ctx, d_events, n, d_batch_ends, d_batch_ts, n_batches, d_results,
+                                 stream, nullptr);
+}
+
+int tbg_create_transfers_stamped_device(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t n,
+                                        const uint64_t* d_event_timestamps,
+                                        tb_create_result_t* d_results, void* stream) {
+    if (!ctx || n > ctx->opt.batch_events_max || !d_event_timestamps) return TBG_EINVAL;
+    if (n == 0) return 0;
+    // One batch: its end, and its timestamp = the last event's (imported events' must_not_advance
+    // bound; the router sends no imported event on this path).
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    const uint32_t end = n;
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->d_batch_ends, &end, 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->d_batch_ts, d_event_timestamps + (n - 1), 8,
+                                hipMemcpyDeviceToDevice, st));
+    HIP_TRY(ctx, hipStreamSynchronize(st));  // (`end` is a stack value)
+    return create_transfers_impl(ctx, d_events, n, ctx->d_batch_ends, ctx->d_batch_ts, 1,
+                                 d_results, stream, d_event_timestamps);
 }
 
 int tbg_create_accounts_device(tbg_ctx* ctx, const tb_account_t* d_events, uint32_t n,

@@ -82,6 +82,7 @@ constexpr uint32_t kMaxGrid = 4096;
 
 template <typename Event>
 __device__ inline uint64_t ts_event_of(const Call<Event>& c, uint32_t b, uint32_t k) {
+    if (c.event_ts) return c.event_ts[k];
     return c.batch_ts[b] - c.batch_ends[b] + k + 1;
 }
 
@@ -522,8 +523,10 @@ __global__ void __launch_bounds__(kBlock, 4) tr_ingest(Tables T, Call<tb_transfe
         const uint64_t ts_base =
             (uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(ci.w))) << 32) |
             uint32_t(__builtin_amdgcn_readfirstlane(ci.z));
-        const bool straddle = ubase + cnt > end0;
+        // (per-event timestamps take the straddling chunk's path: rows stamped from LDS)
+        const bool straddle = ubase + cnt > end0 || c.event_ts != nullptr;
         uint64_t ts_event = ts_base + k;
+        if (c.event_ts && active) ts_event = c.event_ts[k];
         bool batch_imported = (w0 & kChunkImported) != 0;
         bool first_of_batch = false;
         if (active && k >= end0) {

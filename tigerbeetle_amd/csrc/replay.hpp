@@ -123,6 +123,9 @@ struct Call {
     uint32_t n_buckets;
     // create_transfers: per 64-event chunk, its batch bounds (tr_chunk_info).
     const uint4* chunk_info;
+    // Per-event timestamps (a ledger shard's slice of a routed call: its events keep their global
+    // timestamps, which are not contiguous); nullptr: batch_ts[b] - batch_ends[b] + k + 1.
+    const uint64_t* event_ts;
 };
 
 constexpr uint32_t kNone32 = 0xFFFFFFFFu;

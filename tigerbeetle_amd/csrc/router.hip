@@ -1,0 +1,409 @@
+// The device-side ledger router (include/tbr.h): directories and the fast path of a routed call.
+//
+// Directories are the executor's id tables (device_common.hpp: tagged slots, group-16 homes) over
+// append-only stores: accounts (id, shard) in insertion order; transfers (id, shard | TBR_TIMED)
+// per routed event position -- every event of a routed call takes a store row, like the executor's
+// transfer rows, and its slot claim is released at settle unless the id now exists on its shard.
+//
+// Fast path, per call of n events (one workgroup per 256 consecutive events, so the scatter is
+// stable): tbr_pass1 -- the hazard checks, both account lookups, the id claim, per-block counts
+// per shard; the host turns the counts into per-block offsets (shard-major exclusive sums);
+// tbr_pass2 -- each event copied to its slice with its global commit timestamp and its position.
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#include "../../include/tbr.h"
+#include "replay.hpp"
+
+using namespace tbg;
+
+namespace {
+
+constexpr uint32_t kRouteBlock = 256;
+constexpr uint32_t kShardsMax = 64;
+
+struct Dir {
+    IdTable slots;
+    tb_uint128_t* ids;
+    uint8_t* shard;
+};
+
+struct RouteArgs {
+    Dir acc, tr;
+    const tb_transfer_t* events;
+    uint32_t n;
+    const uint32_t* batch_ends;
+    const uint64_t* batch_ts;
+    uint32_t n_batches;
+    uint64_t base;          // the call's first transfer-store row
+    uint32_t shards;
+    uint32_t nblocks;
+    uint8_t* ev_shard;      // per event: its shard, 0xFF for a hazard
+    uint32_t* ev_slot;      // per event: its claimed slot (kNone32: none)
+    uint32_t* block_counts; // [shard][block]
+    unsigned int* flags;    // [0] hazard, [1] table full
+};
+
+__device__ inline uint64_t dir_find(const Dir& d, const tb_uint128_t& id) {
+    const tb_uint128_t* ids = d.ids;
+    const uint64_t s = probe_find(d.slots, id, [=](uint64_t r) { return ids[r]; });
+    if (s == kNone) return kNone;
+    return (d.slots.slots[s] & kRefMask) - 1;
+}
+
+__global__ void tbr_insert(Dir d, uint64_t base, uint32_t n, unsigned int* flags) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const tb_uint128_t* ids = d.ids;
+    bool dup = false;
+    const uint64_t s = probe_claim(d.slots, ids[base + i], base + i + 1, base,
+                                   [=](uint64_t r) { return ids[r]; }, &dup);
+    if (s == kNone) atomicOr(&flags[1], 1u);
+}
+
+__global__ void tbr_lookup(Dir d, const tb_uint128_t* q, uint32_t n, int32_t* out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t r = dir_find(d, q[i]);
+    out[i] = r == kNone ? -1 : int32_t(d.shard[r]);
+}
+
+__global__ void __launch_bounds__(kRouteBlock) tbr_pass1(RouteArgs a) {
+    __shared__ unsigned int cnt[kShardsMax];
+    for (uint32_t s = threadIdx.x; s < a.shards; s += kRouteBlock) cnt[s] = 0;
+    __syncthreads();
+    const uint32_t k = blockIdx.x * kRouteBlock + threadIdx.x;
+    bool hazard = false;
+    if (k < a.n) {
+        const tb_transfer_t& t = a.events[k];
+        const uint16_t f = t.flags;
+        uint8_t shard = 0xFF;
+        uint32_t slot = kNone32;
+        hazard = (f & (TB_TRANSFER_LINKED | TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING |
+                       TB_TRANSFER_IMPORTED | TB_TRANSFER_PADDING_MASK)) != 0 ||
+                 t.timestamp != 0 || u128_is_zero(t.id) || u128_is_max(t.id);
+        uint64_t sd = kNone;
+        if (!hazard) {
+            const uint64_t rd = dir_find(a.acc, t.debit_account_id);
+            const uint64_t rc = dir_find(a.acc, t.credit_account_id);
+            hazard = rd == kNone || rc == kNone || a.acc.shard[rd] != a.acc.shard[rc];
+            if (!hazard) sd = a.acc.shard[rd];
+        }
+        if (!hazard) {
+            // The id: new to every shard and unique in the call (the serial order's first
+            // occurrence keeps the slot; any repeat is a hazard).
+            const tb_transfer_t* ev = a.events;
+            const tb_uint128_t* ids = a.tr.ids;
+            const uint64_t base = a.base;
+            bool dup = false;
+            const uint64_t s = probe_claim(a.tr.slots, t.id, base + k + 1, base, [=](uint64_t r) {
+                return r >= base ? ev[r - base].id : ids[r];
+            }, &dup);
+            if (s == kNone) {
+                atomicOr(&a.flags[1], 1u);
+                hazard = true;
+            } else {
+                slot = uint32_t(s);
+                const uint64_t owner = (a.tr.slots.slots[s] & kRefMask) - 1;
+                hazard = dup || owner != base + k;
+                shard = uint8_t(sd);
+            }
+        }
+        a.ev_shard[k] = hazard ? 0xFF : shard;
+        a.ev_slot[k] = slot;
+        a.tr.ids[a.base + k] = t.id;
+        const bool timed = (f & TB_TRANSFER_PENDING) && t.timeout > 0;
+        a.tr.shard[a.base + k] = uint8_t(sd == kNone ? 0 : sd) | (timed ? TBR_TIMED : 0);
+        if (!hazard) atomicAdd(&cnt[shard], 1u);
+    }
+    if (__any(hazard) && (threadIdx.x & 63) == 0) atomicOr(&a.flags[0], 1u);
+    __syncthreads();
+    for (uint32_t s = threadIdx.x; s < a.shards; s += kRouteBlock)
+        a.block_counts[uint64_t(s) * a.nblocks + blockIdx.x] = cnt[s];
+}
+
+// A call with a hazard takes nothing: its claims are released.
+__global__ void tbr_release(RouteArgs a) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= a.n) return;
+    const uint32_t s = a.ev_slot[k];
+    if (s == kNone32) return;
+    unsigned long long* w = &a.tr.slots.slots[s];
+    if ((*w & kRefMask) == a.base + k + 1) *w = kTomb;
+}
+
+__global__ void __launch_bounds__(kRouteBlock) tbr_pass2(RouteArgs a, const uint32_t* offsets,
+                                                         tb_transfer_t* out_events,
+                                                         uint64_t* out_ts, uint32_t* out_pos) {
+    __shared__ unsigned int wave_cnt[kRouteBlock / 64][kShardsMax];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t k = blockIdx.x * kRouteBlock + threadIdx.x;
+    const bool active = k < a.n;
+    const uint32_t s = active ? a.ev_shard[k] : 0xFFu;
+    const uint64_t lt = (1ull << lane) - 1;
+    uint32_t my_rank = 0;
+    for (uint32_t sv = 0; sv < a.shards; sv++) {
+        const uint64_t m = __ballot(active && s == sv);
+        if (lane == 0) wave_cnt[wv][sv] = __popcll(m);
+        if (s == sv) my_rank = __popcll(m & lt);
+    }
+    __syncthreads();
+    if (!active) return;
+    uint32_t rank = my_rank;
+    for (uint32_t w = 0; w < wv; w++) rank += wave_cnt[w][s];
+    const uint32_t pos = offsets[uint64_t(s) * a.nblocks + blockIdx.x] + rank;
+    const uint4* src = reinterpret_cast<const uint4*>(&a.events[k]);
+    uint4* dst = reinterpret_cast<uint4*>(&out_events[pos]);
+#pragma unroll
+    for (int i = 0; i < 8; i++) dst[i] = src[i];
+    const uint32_t b = batch_of_guess(a.batch_ends, a.n_batches, a.n, k);
+    out_ts[pos] = a.batch_ts[b] - a.batch_ends[b] + k + 1;
+    out_pos[pos] = k;
+}
+
+// Results back to call order; ids that exist now (created, or orphaned by a transient failure)
+// stay in the directory, the others are released.
+__global__ void tbr_settle(RouteArgs a, const tb_create_result_t* shard_res, const uint32_t* pos,
+                           tb_create_result_t* results) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= a.n) return;
+    const uint32_t k = pos[j];
+    const tb_create_result_t r = shard_res[j];
+    results[k] = r;
+    const uint64_t row = a.base + k;
+    if (r.status == TB_STATUS_CREATED) return;
+    if (tb_transfer_status_transient(r.status)) {
+        a.tr.shard[row] &= uint8_t(~TBR_TIMED);  // an orphan is no pending transfer
+        return;
+    }
+    const uint32_t s = a.ev_slot[k];
+    unsigned long long* w = &a.tr.slots.slots[s];
+    if ((*w & kRefMask) == row + 1) *w = kTomb;
+}
+
+uint64_t next_pow2(uint64_t x) {
+    uint64_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+}  // namespace
+
+struct tbr_ctx {
+    uint32_t shards = 0, events_max = 0;
+    hipStream_t stream = nullptr;
+    Dir acc{}, tr{};
+    uint64_t acc_used = 0, acc_cap = 0, tr_used = 0, tr_cap = 0;
+    uint8_t* ev_shard = nullptr;
+    uint32_t* ev_slot = nullptr;
+    uint32_t* block_counts = nullptr;
+    uint32_t* offsets = nullptr;
+    unsigned int* flags = nullptr;
+    tb_uint128_t* q_ids = nullptr;  // lookup / record staging (events_max)
+    int32_t* q_out = nullptr;
+    // the routed call awaiting tbr_settle_device
+    bool pending = false;
+    uint64_t call_base = 0;
+    uint32_t call_n = 0;
+};
+
+namespace {
+
+template <typename T>
+bool alloc(T** p, uint64_t count, bool zero, hipStream_t s) {
+    if (hipMalloc(reinterpret_cast<void**>(p), std::max<size_t>(count * sizeof(T), 16)) !=
+        hipSuccess)
+        return false;
+    return !zero || hipMemsetAsync(*p, 0, std::max<size_t>(count * sizeof(T), 16), s) == hipSuccess;
+}
+
+RouteArgs route_args(tbr_ctx* r, const tb_transfer_t* ev, uint32_t n, const uint32_t* ends,
+                     const uint64_t* bts, uint32_t nb) {
+    RouteArgs a{};
+    a.acc = r->acc;
+    a.tr = r->tr;
+    a.events = ev;
+    a.n = n;
+    a.batch_ends = ends;
+    a.batch_ts = bts;
+    a.n_batches = nb;
+    a.base = r->tr_used;
+    a.shards = r->shards;
+    a.nblocks = (n + kRouteBlock - 1) / kRouteBlock;
+    a.ev_shard = r->ev_shard;
+    a.ev_slot = r->ev_slot;
+    a.block_counts = r->block_counts;
+    a.flags = r->flags;
+    return a;
+}
+
+int record(tbr_ctx* r, Dir& d, uint64_t& used, uint64_t cap, const tb_uint128_t* ids,
+           const uint8_t* shards, uint32_t n) {
+    if (n == 0) return 0;
+    if (used + n > cap) return -28;
+    if (hipMemcpyAsync(d.ids + used, ids, size_t(n) * 16, hipMemcpyHostToDevice, r->stream) ||
+        hipMemcpyAsync(d.shard + used, shards, n, hipMemcpyHostToDevice, r->stream) ||
+        hipMemsetAsync(r->flags, 0, 8, r->stream))
+        return -5;
+    hipLaunchKernelGGL(tbr_insert, dim3((n + 255) / 256), dim3(256), 0, r->stream, d, used, n,
+                       r->flags);
+    unsigned int f[2] = {0, 0};
+    if (hipMemcpyAsync(f, r->flags, 8, hipMemcpyDeviceToHost, r->stream) ||
+        hipStreamSynchronize(r->stream))
+        return -5;
+    used += n;
+    return f[1] ? -28 : 0;
+}
+
+int64_t lookup(tbr_ctx* r, const Dir& d, const tb_uint128_t* ids, uint32_t n, int32_t* out) {
+    for (uint32_t a = 0; a < n; a += r->events_max) {
+        const uint32_t m = std::min(n - a, r->events_max);
+        if (hipMemcpyAsync(r->q_ids, ids + a, size_t(m) * 16, hipMemcpyHostToDevice, r->stream))
+            return -5;
+        hipLaunchKernelGGL(tbr_lookup, dim3((m + 255) / 256), dim3(256), 0, r->stream, d, r->q_ids,
+                           m, r->q_out);
+        if (hipMemcpyAsync(out + a, r->q_out, size_t(m) * 4, hipMemcpyDeviceToHost, r->stream) ||
+            hipStreamSynchronize(r->stream))
+            return -5;
+    }
+    return n;
+}
+
+}  // namespace
+
+extern "C" {
+
+tbr_ctx* tbr_open(uint32_t shards, uint64_t account_capacity, uint64_t transfer_capacity,
+                  uint32_t events_max, uint32_t device) {
+    if (shards == 0 || shards > kShardsMax || events_max == 0 ||
+        account_capacity >= (1ull << 31) || transfer_capacity >= (1ull << 31))
+        return nullptr;
+    if (hipSetDevice(int(device)) != hipSuccess) return nullptr;
+    tbr_ctx* r = new tbr_ctx();
+    r->shards = shards;
+    r->events_max = events_max;
+    r->acc_cap = account_capacity;
+    r->tr_cap = transfer_capacity;
+    const uint64_t acc_slots = std::max<uint64_t>(next_pow2(account_capacity * 4), 64);
+    const uint64_t tr_slots = std::max<uint64_t>(next_pow2(transfer_capacity * 4), 64);
+    const uint32_t nblocks = (events_max + kRouteBlock - 1) / kRouteBlock;
+    bool ok = hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) == hipSuccess;
+    ok = ok && alloc(&r->acc.slots.slots, acc_slots, true, r->stream) &&
+         alloc(&r->acc.ids, account_capacity, false, r->stream) &&
+         alloc(&r->acc.shard, account_capacity, false, r->stream) &&
+         alloc(&r->tr.slots.slots, tr_slots, true, r->stream) &&
+         alloc(&r->tr.ids, transfer_capacity, false, r->stream) &&
+         alloc(&r->tr.shard, transfer_capacity, false, r->stream) &&
+         alloc(&r->ev_shard, events_max, false, r->stream) &&
+         alloc(&r->ev_slot, events_max, false, r->stream) &&
+         alloc(&r->block_counts, uint64_t(shards) * nblocks, false, r->stream) &&
+         alloc(&r->offsets, uint64_t(shards) * nblocks, false, r->stream) &&
+         alloc(&r->flags, 2, true, r->stream) && alloc(&r->q_ids, events_max, false, r->stream) &&
+         alloc(&r->q_out, events_max, false, r->stream);
+    ok = ok && hipStreamSynchronize(r->stream) == hipSuccess;
+    if (!ok) {
+        fprintf(stderr, "tbr_open: allocation failed\n");
+        tbr_close(r);
+        return nullptr;
+    }
+    r->acc.slots.mask = acc_slots - 1;
+    r->tr.slots.mask = tr_slots - 1;
+    return r;
+}
+
+void tbr_close(tbr_ctx* r) {
+    if (!r) return;
+    if (r->stream) (void)hipStreamSynchronize(r->stream);
+    void* ptrs[] = {r->acc.slots.slots, r->acc.ids, r->acc.shard, r->tr.slots.slots, r->tr.ids,
+                    r->tr.shard, r->ev_shard, r->ev_slot, r->block_counts, r->offsets, r->flags,
+                    r->q_ids, r->q_out};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    if (r->stream) (void)hipStreamDestroy(r->stream);
+    delete r;
+}
+
+int tbr_record_accounts(tbr_ctx* r, const tb_uint128_t* ids, const uint8_t* shards, uint32_t n) {
+    if (!r || r->pending) return -22;
+    return record(r, r->acc, r->acc_used, r->acc_cap, ids, shards, n);
+}
+
+int tbr_record_transfers(tbr_ctx* r, const tb_uint128_t* ids, const uint8_t* shards, uint32_t n) {
+    if (!r || r->pending) return -22;
+    return record(r, r->tr, r->tr_used, r->tr_cap, ids, shards, n);
+}
+
+int64_t tbr_account_shards(tbr_ctx* r, const tb_uint128_t* ids, uint32_t n, int32_t* out) {
+    if (!r) return -22;
+    return lookup(r, r->acc, ids, n, out);
+}
+
+int64_t tbr_transfer_shards(tbr_ctx* r, const tb_uint128_t* ids, uint32_t n, int32_t* out) {
+    if (!r) return -22;
+    return lookup(r, r->tr, ids, n, out);
+}
+
+int64_t tbr_route_device(tbr_ctx* r, const tb_transfer_t* d_events, uint32_t n,
+                         const uint32_t* d_batch_ends, const uint64_t* d_batch_ts,
+                         uint32_t n_batches, tb_transfer_t* d_out_events, uint64_t* d_out_ts,
+                         uint32_t* d_out_pos, uint32_t* shard_counts) {
+    if (!r || r->pending || n > r->events_max || n_batches == 0) return -22;
+    if (r->tr_used + n > r->tr_cap) return -28;
+    RouteArgs a = route_args(r, d_events, n, d_batch_ends, d_batch_ts, n_batches);
+    const dim3 grid(a.nblocks), block(kRouteBlock);
+    if (hipMemsetAsync(r->flags, 0, 8, r->stream)) return -5;
+    hipLaunchKernelGGL(tbr_pass1, grid, block, 0, r->stream, a);
+    std::vector<uint32_t> counts(uint64_t(r->shards) * a.nblocks);
+    unsigned int f[2] = {0, 0};
+    if (hipMemcpyAsync(f, r->flags, 8, hipMemcpyDeviceToHost, r->stream) ||
+        hipMemcpyAsync(counts.data(), r->block_counts, counts.size() * 4, hipMemcpyDeviceToHost,
+                       r->stream) ||
+        hipStreamSynchronize(r->stream))
+        return -5;
+    if (f[0] || f[1]) {
+        hipLaunchKernelGGL(tbr_release, grid, block, 0, r->stream, a);
+        if (hipStreamSynchronize(r->stream)) return -5;
+        return f[1] ? -28 : 1;
+    }
+    // per-block offsets: shard-major exclusive sums
+    uint32_t run = 0;
+    for (uint32_t s = 0; s < r->shards; s++) {
+        const uint32_t start = run;
+        for (uint32_t b = 0; b < a.nblocks; b++) {
+            const uint32_t c = counts[uint64_t(s) * a.nblocks + b];
+            counts[uint64_t(s) * a.nblocks + b] = run;
+            run += c;
+        }
+        shard_counts[s] = run - start;
+    }
+    if (hipMemcpyAsync(r->offsets, counts.data(), counts.size() * 4, hipMemcpyHostToDevice,
+                       r->stream))
+        return -5;
+    hipLaunchKernelGGL(tbr_pass2, grid, block, 0, r->stream, a, r->offsets, d_out_events,
+                       d_out_ts, d_out_pos);
+    if (hipGetLastError() || hipStreamSynchronize(r->stream)) return -5;
+    r->pending = true;
+    r->call_base = a.base;
+    r->call_n = n;
+    return 0;
+}
+
+int tbr_settle_device(tbr_ctx* r, const tb_create_result_t* d_shard_results,
+                      const uint32_t* d_positions, uint32_t n, tb_create_result_t* d_results) {
+    if (!r || !r->pending || n != r->call_n) return -22;
+    RouteArgs a = route_args(r, nullptr, n, nullptr, nullptr, 1);
+    a.base = r->call_base;
+    hipLaunchKernelGGL(tbr_settle, dim3((n + 255) / 256), dim3(256), 0, r->stream, a,
+                       d_shard_results, d_positions, d_results);
+    if (hipGetLastError() || hipStreamSynchronize(r->stream)) return -5;
+    r->tr_used = r->call_base + n;
+    r->pending = false;
+    return 0;
+}
+
+}  // extern "C"

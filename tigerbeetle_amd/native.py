@@ -85,6 +85,7 @@ SIGNATURES = [
                                                  ctypes.c_uint32, vp, vp]),
     ("tbg_create_transfers_device", ctypes.c_int, [vp, vp, ctypes.c_uint32, vp, vp,
                                                   ctypes.c_uint32, vp, vp]),
+    ("tbg_create_transfers_stamped_device", ctypes.c_int, [vp, vp, ctypes.c_uint32, vp, vp, vp]),
     ("tbg_pulse", ctypes.c_int64, [vp, ctypes.c_uint64]),
     ("tbg_pulse_candidates", ctypes.c_int64, [vp, ctypes.c_uint64, vp, vp, ctypes.c_uint32]),
     ("tbg_pulse_cut", ctypes.c_int64, [vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
@@ -104,6 +105,16 @@ SIGNATURES = [
     ("tbg_profile", ctypes.c_int, [vp, ctypes.c_int]),
     ("tbg_profile_read", ctypes.c_int, [vp, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32,
                                        ctypes.POINTER(ctypes.c_double), c_u64p]),
+    ("tbr_open", vp, [ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
+                      ctypes.c_uint32]),
+    ("tbr_close", None, [vp]),
+    ("tbr_record_accounts", ctypes.c_int, [vp, vp, vp, ctypes.c_uint32]),
+    ("tbr_record_transfers", ctypes.c_int, [vp, vp, vp, ctypes.c_uint32]),
+    ("tbr_account_shards", ctypes.c_int64, [vp, vp, ctypes.c_uint32, vp]),
+    ("tbr_transfer_shards", ctypes.c_int64, [vp, vp, ctypes.c_uint32, vp]),
+    ("tbr_route_device", ctypes.c_int64, [vp, vp, ctypes.c_uint32, vp, vp, ctypes.c_uint32, vp, vp,
+                                          vp, vp]),
+    ("tbr_settle_device", ctypes.c_int, [vp, vp, vp, ctypes.c_uint32, vp]),
     ("tb_sm_open", vp, [ctypes.POINTER(SmOptions), ctypes.POINTER(Executor)]),
     ("tb_sm_open_gpu", vp, [ctypes.POINTER(SmOptions), ctypes.POINTER(TbgOptions)]),
     ("tb_sm_close", None, [vp]),

@@ -166,6 +166,85 @@ def split_runs(shard_of: np.ndarray, lens, batch_ts, shards: int) -> List[ShardS
     return slices
 
 
+class DictDirectory:
+    """Host-side directories: account id -> shard; transfer id (created or orphaned) -> (shard,
+    timed: a pending transfer with a timeout). The device router keeps the same directories in
+    HBM (DeviceDirectory, include/tbr.h)."""
+
+    def __init__(self):
+        self.accounts: Dict[int, int] = {}
+        self.transfers: Dict[int, tuple] = {}
+
+    def account_shards(self, ids: List[int]) -> List[Optional[int]]:
+        return [self.accounts.get(i) for i in ids]
+
+    def transfer_info(self, ids: List[int]) -> List[Optional[tuple]]:
+        return [self.transfers.get(i) for i in ids]
+
+    def record_accounts(self, ids: List[int], shards: List[int]):
+        for i, sh in zip(ids, shards):
+            self.accounts[i] = sh
+
+    def record_transfers(self, ids: List[int], shards: List[int], timed: List[bool]):
+        for i, sh, t in zip(ids, shards, timed):
+            self.transfers.setdefault(i, (sh, t))
+
+
+def _u128_array(ids: List[int]) -> np.ndarray:
+    a = np.zeros((len(ids), 2), dtype=np.uint64)
+    if ids:
+        a[:, 0] = [i & 0xFFFFFFFFFFFFFFFF for i in ids]
+        a[:, 1] = [i >> 64 for i in ids]
+    return a
+
+
+class DeviceDirectory:
+    """The directories of the device router (tbr_ctx, include/tbr.h), read and written in bulk:
+    one source of truth for the device fast path and the exact host path."""
+    TIMED = 0x80
+
+    def __init__(self, lib, tbr):
+        self.lib = lib
+        self.tbr = tbr
+
+    def _lookup(self, fn, ids):
+        import ctypes
+        if not ids:
+            return []
+        a = _u128_array(ids)
+        out = np.zeros(len(ids), dtype=np.int32)
+        rc = fn(self.tbr, a.ctypes.data_as(ctypes.c_void_p), len(ids),
+                out.ctypes.data_as(ctypes.c_void_p))
+        if rc < 0:
+            raise RuntimeError(f"tbr lookup: {rc}")
+        return out.tolist()
+
+    def account_shards(self, ids):
+        return [None if x < 0 else x for x in self._lookup(self.lib.tbr_account_shards, ids)]
+
+    def transfer_info(self, ids):
+        return [None if x < 0 else (x & 0x7F, bool(x & self.TIMED))
+                for x in self._lookup(self.lib.tbr_transfer_shards, ids)]
+
+    def _record(self, fn, ids, shards):
+        import ctypes
+        if not ids:
+            return
+        a = _u128_array(ids)
+        sh = np.asarray(shards, dtype=np.uint8)
+        rc = fn(self.tbr, a.ctypes.data_as(ctypes.c_void_p), sh.ctypes.data_as(ctypes.c_void_p),
+                len(ids))
+        if rc != 0:
+            raise RuntimeError(f"tbr record: {rc}")
+
+    def record_accounts(self, ids, shards):
+        self._record(self.lib.tbr_record_accounts, ids, shards)
+
+    def record_transfers(self, ids, shards, timed):
+        self._record(self.lib.tbr_record_transfers, ids,
+                     [s | (self.TIMED if t else 0) for s, t in zip(shards, timed)])
+
+
 class LedgerRouter:
     """Routes create_accounts / create_transfers calls to ledger shards (module doc).
 
@@ -174,14 +253,12 @@ class LedgerRouter:
     of later events follows the directories, so a placement never has to be recomputed.
     """
 
-    def __init__(self, shards: int, ledgers: int = 64):
+    def __init__(self, shards: int, ledgers: int = 64, directory=None):
         if shards < 1:
             raise ValueError("shards must be >= 1")
         self.shards = shards
         self.ledgers = ledgers
-        self.account_shard: Dict[int, int] = {}
-        self.transfer_shard: Dict[int, int] = {}
-        self.timed_pending: Set[int] = set()  # pending transfers created with a timeout
+        self.dir = directory if directory is not None else DictDirectory()
         # objects trees' key_range.key_max over all shards (largest created timestamp)
         self.accounts_key_max = 0
         self.transfers_key_max = 0
@@ -241,18 +318,20 @@ class LedgerRouter:
         ids = _ids(events["id"])
         ledgers = events["ledger"].tolist()
         in_call: Dict[int, int] = {}
+        uniq = list(set(ids))
+        known = {i: sh for i, sh in zip(uniq, self.dir.account_shards(uniq)) if sh is not None}
 
         def pins_of(k):
             i = ids[k]
-            if i in self.account_shard:
-                return {self.account_shard[i]}
+            if i in known:
+                return {known[i]}
             if i in in_call:
                 return {in_call[i]}
             return set()
 
         def record(k, sh):
             i = ids[k]
-            if i not in self.account_shard and i != 0 and i != _U128_MAX:
+            if i not in known and i != 0 and i != _U128_MAX:
                 in_call.setdefault(i, sh)
 
         shard_of = self._place_chains(n, chain_starts(flags, lens), pins_of,
@@ -281,6 +360,12 @@ class LedgerRouter:
         post_void = int(TransferFlags.post_pending_transfer | TransferFlags.void_pending_transfer)
         pending = int(TransferFlags.pending)
         closing = int(TransferFlags.closing_debit | TransferFlags.closing_credit)
+        # the directories' answers for every id of the call, in bulk
+        uniq_t = list(set(ids) | set(pids))
+        tr_known = {i: v for i, v in zip(uniq_t, self.dir.transfer_info(uniq_t)) if v is not None}
+        uniq_a = list(set(drs) | set(crs))
+        acc_known = {i: v for i, v in zip(uniq_a, self.dir.account_shards(uniq_a))
+                     if v is not None}
 
         def cross_status(k):
             # create_transfer :3774-3798 after the account ids: both accounts exist, on shards of
@@ -300,21 +385,21 @@ class LedgerRouter:
 
         def pins_of(k):
             i = ids[k]
-            if i in self.transfer_shard:  # exists / id_already_failed: decided on the holder
-                return {self.transfer_shard[i]}
+            if i in tr_known:  # exists / id_already_failed: decided on the holder
+                return {tr_known[i][0]}
             pins = set()
             if i in in_call:  # the repeat executes in full if the first occurrence fails
                 pins.add(in_call[i])
             if fl[k] & post_void:
                 p = pids[k]
-                if p in self.timed_pending or p in in_call_timed:
+                if (p in tr_known and tr_known[p][1]) or p in in_call_timed:
                     raise RouteError(f"event {k} posts/voids a pending transfer with a timeout")
-                if p in self.transfer_shard:
-                    pins.add(self.transfer_shard[p])
+                if p in tr_known:
+                    pins.add(tr_known[p][0])
                 elif p in in_call:
                     pins.add(in_call[p])
             else:
-                a_dr, a_cr = self.account_shard.get(drs[k]), self.account_shard.get(crs[k])
+                a_dr, a_cr = acc_known.get(drs[k]), acc_known.get(crs[k])
                 if a_dr is not None and a_cr is not None and a_dr != a_cr:
                     if i in in_call:
                         raise RouteError(f"cross-shard transfer {k} repeats an id of the call")
@@ -325,7 +410,7 @@ class LedgerRouter:
 
         def record(k, sh):
             i = ids[k]
-            if i not in self.transfer_shard and i != 0 and i != _U128_MAX:
+            if i not in tr_known and i != 0 and i != _U128_MAX:
                 in_call.setdefault(i, sh)
                 if (fl[k] & pending) and timeouts[k] > 0:
                     in_call_timed.add(i)
@@ -356,18 +441,21 @@ class LedgerRouter:
             else:
                 self.transfers_key_max = max(self.transfers_key_max, ts_max)
         if plan.kind == "accounts":
-            for k in np.nonzero(created)[0].tolist():
-                self.account_shard[key(k)] = int(plan.shard_of[k])
+            ks = np.nonzero(created)[0].tolist()
+            self.dir.record_accounts([key(k) for k in ks], [int(plan.shard_of[k]) for k in ks])
             return
         keep = status == STATUS_CREATED
         for st in TRANSIENT_TRANSFER_STATUSES:
             keep |= status == int(st)
-        for k in np.nonzero(keep)[0].tolist():
-            self.transfer_shard.setdefault(key(k), int(plan.shard_of[k]))
         timed = ((status == STATUS_CREATED) &
                  ((events["flags"] & int(TransferFlags.pending)) != 0) & (events["timeout"] > 0))
-        for k in np.nonzero(timed)[0].tolist():
-            self.timed_pending.add(key(k))
+        ks, seen = [], set()
+        for k in np.nonzero(keep)[0].tolist():  # (the first holder of a repeated id)
+            if key(k) not in seen:
+                seen.add(key(k))
+                ks.append(k)
+        self.dir.record_transfers([key(k) for k in ks], [int(plan.shard_of[k]) for k in ks],
+                                  [bool(timed[k]) for k in ks])
 
 
 def gather_results(plan: Plan, shard_results: List[Optional[np.ndarray]], n: int) -> np.ndarray:
@@ -626,10 +714,19 @@ class GpuShard:
         if not self.g:
             raise RuntimeError("tbg_open failed")
 
+    @classmethod
+    def wrap(cls, lib, g):
+        """A shard over an executor the caller owns (closing it is the caller's)."""
+        import ctypes
+        from . import native
+        self = cls.__new__(cls)
+        self._c, self._native, self.lib, self.g, self._owned = ctypes, native, lib, g, False
+        return self
+
     def close(self):
-        if self.g:
+        if self.g and getattr(self, "_owned", True):
             self.lib.tbg_close(self.g)
-            self.g = None
+        self.g = None
 
     def _call(self, fn, events, lens, batch_ts):
         c = self._c
