@@ -8,11 +8,13 @@ synthetic input: one tbg_create_transfers_device call carrying all 1,222 batches
 its own commit timestamp, TestContext rule prepare_ts += 1 + n). Inputs are resident in HBM when
 the timed region starts; every step uses fresh transfer ids, so every step does the full work.
 
-Multi-GPU (weak scaling): one process per GPU; each rank owns its own ledger shard
-(own accounts and transfers, ledger 2 + rank) with no data-path collective. The timed region is
-bracketed by a barrier + device synchronise on every rank; the reported time is the max over ranks.
-(`tools/bench_sharded.py` times the routed path: one client stream over many ledgers, scattered
-to the shards and gathered inside the timed region.)
+Multi-GPU (weak scaling): one process per GPU, each owning one ledger shard (10k
+accounts on ledger 2 + rank). One client stream of 10M transfers per GPU per step, over all the
+shards' ledgers, enters at rank 0 in HBM; each step is routed there by the device router,
+scattered to the shards over RCCL (xGMI), executed, and its results gathered back in call order
+-- all inside the timed region (`main_routed`, tigerbeetle_amd/routed.py). `--independent` runs
+N unrelated single-shard streams instead (no data-path collective). The timed region is bracketed
+by a barrier + device synchronise on every rank; the reported time is the max over ranks.
 
 Validation (after the timed region; the workload is order-independent, so the serial reference
 outcome is known in closed form): every result of every step is `created` with its exact event
@@ -83,6 +85,9 @@ def parse_args():
                     help="record AccountEvents (the account_events groove, 256 B per created "
                          "transfer) inside the timed steps; SURVEY.md §8d excludes them from the "
                          "headline's algorithmic bytes")
+    ap.add_argument("--independent", action="store_true",
+                    help="N > 1: every rank runs its own client stream on its own ledger (no "
+                         "router); default: one stream routed from rank 0 over RCCL")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-validate", action="store_true")
     return ap.parse_args()
@@ -96,8 +101,11 @@ def dist_init(args):
     if world > 1:
         import torch
         import torch.distributed as td
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
-        if backend == "nccl":
+        # TBG_BENCH_BACKEND=gloo rehearses N ranks on fewer GPUs (host staging, no RCCL).
+        backend = os.environ.get("TBG_BENCH_BACKEND") or (
+            "nccl" if torch.cuda.is_available() else "gloo")
+        if torch.cuda.is_available():
+            local = local % torch.cuda.device_count()
             torch.cuda.set_device(local)
         td.init_process_group(backend=backend)
         dist = td
@@ -494,9 +502,150 @@ def per_commit(args, lib, dev, g, wl, prepare_ts, id_base):
     return {"device": device, "state_machine": smr}, prepare_ts
 
 
+def routed_call(n_per_shard, world, accounts, seed, step):
+    """The routed workload's client call for one step: world x n_per_shard transfers over `world`
+    ledgers (2 .. world + 1, `accounts` accounts each, ids (ledger - 2) * accounts + 1 ..), the
+    ledger uniform per event and debit / credit uniform within it (benchmark_load.zig
+    distributions), fresh ids per step."""
+    n = n_per_shard * world
+    t = workload.transfers_uniform(n, accounts, seed=seed, id_offset=step * n)
+    lg = np.random.default_rng(seed + 1).integers(0, world, size=n).astype(np.uint64)
+    t["debit_account_id"][:, 0] += lg * np.uint64(accounts)
+    t["credit_account_id"][:, 0] += lg * np.uint64(accounts)
+    t["ledger"] = (2 + lg).astype(np.uint32)
+    return t, lg
+
+
+def main_routed(args, world, rank, local, dist):
+    """N > 1: one client stream over N ledgers enters at rank 0, in HBM; every step is routed by
+    the device router (tbr), scattered to the ledger shards over RCCL, executed there and the
+    results gathered back to call order -- all inside the timed region (tigerbeetle_amd/routed.py,
+    SURVEY.md §8e). Weak scaling: 10M transfers per GPU per step."""
+    import torch
+    from tigerbeetle_amd.routed import RoutedShards
+    N1 = args.transfers or 10_000_000
+    A = args.accounts or 10_000
+    K, W = args.steps, args.warmup
+    N = N1 * world
+    lib = native.load()
+    cap = int(N1 * (K + W) * 1.1) + 4096
+    opt = native.TbgOptions()
+    opt.account_capacity = A
+    opt.transfer_capacity = cap
+    opt.batch_events_max = int(N1 * 1.1) + 4096
+    opt.batch_count_max = 1
+    opt.pulse_batch_max = 8190
+    opt.device = local
+    opt.pulse_next_timestamp_init = 1
+    rs = RoutedShards(opt, events_max=N, router_transfer_capacity=N * (K + W) + 4096,
+                      router_account_capacity=A * world + 4096, ledgers=world + 1,
+                      device_index=local)
+    # Each shard creates its own ledger's accounts; rank 0's directory records all of them.
+    acc = workload.accounts(A, seed=args.seed + rank, id_offset=rank * A, ledger=2 + rank)
+    res = np.zeros(A, dtype=RESULT_DTYPE)
+    rc = lib.tbg_create_accounts(rs.g, acc.ctypes.data_as(ctypes.c_void_p), A,
+                                 np.asarray([A], dtype=np.uint32).ctypes.data_as(native.c_u32p),
+                                 np.asarray([A + 1], dtype=np.uint64).ctypes.data_as(native.c_u64p),
+                                 1, res.ctypes.data_as(ctypes.c_void_p))
+    assert rc == 0 and (res["status"] == CREATED).all(), "create_accounts"
+    if rank == 0:
+        ids = np.zeros((A * world, 2), dtype=np.uint64)
+        ids[:, 0] = np.arange(1, A * world + 1, dtype=np.uint64)
+        rs.record_accounts(ids, np.arange(A * world) // A)
+    dev = torch.device("cuda", local)
+    lens = batch_plan(N)
+    prepare_ts = A + 1
+    steps, host_steps = [], []
+    if rank == 0:
+        d_ends = torch.from_numpy(np.cumsum(lens).astype(np.int32)).to(dev)
+        for s in range(W + K):
+            t, lg = routed_call(N1, world, A, args.seed, s)
+            ts, prepare_ts = step_timestamps(prepare_ts, lens)
+            steps.append((torch.from_numpy(t.view(np.uint8).reshape(-1)).to(dev),
+                          torch.from_numpy(ts.view(np.int64).copy()).to(dev),
+                          torch.zeros(N * 16, dtype=torch.uint8, device=dev)))
+            host_steps.append((ts, lg))
+            del t
+    torch.cuda.synchronize(dev)
+
+    def run_step(s):
+        if rank == 0:
+            d_ev, d_ts, d_res = steps[s]
+            mode = rs.create_transfers(d_ev.data_ptr(), N, d_ends.data_ptr(), d_ts.data_ptr(),
+                                       len(lens), d_res.data_ptr())
+            assert mode == 0, "the routed workload takes the device path"
+        else:
+            rs.create_transfers()
+
+    for s in range(W):
+        run_step(s)
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for s in range(W, W + K):
+        run_step(s)
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    t_max = max_over_ranks(dist, time.perf_counter() - t0)
+
+    # Validation: every result created at its exact timestamp (rank 0); every shard's accounts
+    # hold exactly the sums of its ledger's amounts over all steps.
+    ok = True
+    sums = torch.zeros(2 * A * world, dtype=torch.int64)
+    if rank == 0:
+        exp_d = np.zeros(A * world, dtype=np.uint64)
+        exp_c = np.zeros(A * world, dtype=np.uint64)
+        for s in range(W + K):
+            r = steps[s][2].cpu().numpy().view(RESULT_DTYPE)
+            ts, _ = host_steps[s]
+            ok &= bool((r["status"] == CREATED).all() and
+                       (r["timestamp"] == event_timestamps(lens, ts)).all())
+            t, _ = routed_call(N1, world, A, args.seed, s)
+            amt = t["amount"][:, 0]
+            np.add.at(exp_d, t["debit_account_id"][:, 0].astype(np.int64) - 1, amt)
+            np.add.at(exp_c, t["credit_account_id"][:, 0].astype(np.int64) - 1, amt)
+        sums = torch.from_numpy(np.concatenate([exp_d, exp_c]).view(np.int64).copy())
+    dist.broadcast(sums, 0) if not rs.nccl else None
+    if rs.nccl:
+        sd = sums.to(dev)
+        dist.broadcast(sd, 0)
+        sums = sd.cpu()
+    sums = sums.numpy().view(np.uint64)
+    dump = np.zeros(A, dtype=ACCOUNT_DTYPE)
+    lib.tbg_dump_accounts(rs.g, dump.ctypes.data_as(ctypes.c_void_p))
+    mine = slice(rank * A, (rank + 1) * A)
+    ok &= bool((dump["debits_posted"][:, 0] == sums[:A * world][mine]).all() and
+               (dump["credits_posted"][:, 0] == sums[A * world:][mine]).all())
+    flag = torch.tensor([0 if ok else 1], dtype=torch.int64, device=dev if rs.nccl else "cpu")
+    dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+    validated = int(flag.item()) == 0
+    value = N * K / t_max
+    if rank == 0:
+        print(json.dumps({
+            "metric": METRIC, "value": round(value, 1), "unit": "transfers/s", "n_gpus": world,
+            "steps": K, "warmup": W, "ms_per_step": round(t_max / K * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u128",
+            "data": "synthetic (seeded; benchmark_load.zig distributions, sequential ids)",
+            "config": {"workload": f"config2 routed: one client stream of {N1} transfers per GPU "
+                                   f"over {world} ledgers (10k accounts each) entering at rank 0 "
+                                   f"in HBM; device router + RCCL scatter/gather in the timed "
+                                   f"region", "transfers_per_step": N,
+                       "accounts_per_gpu": A, "batches_per_step": int(len(lens)),
+                       "parallelism": f"ledger-shard x{world}, routed from rank 0"},
+            "validated": validated,
+            "routed": {"device_calls": rs.fast_calls, "host_router_calls": rs.host_calls},
+            "roofline": None, "cpu_baseline": None,
+        }))
+    rs.close()
+    dist.destroy_process_group()
+
+
 def main():
     args = parse_args()
     world, rank, local, dist = dist_init(args)
+    if world > 1 and args.workload == "config2" and not args.independent:
+        return main_routed(args, world, rank, local, dist)
     wl = (Config5 if args.workload == "config5" else Config2)(args, rank, world)
     N, A, K, W = wl.N, wl.A, args.steps, args.warmup
     R = args.commit_reps if rank == 0 and world == 1 and not args.no_validate else 0
