@@ -8,13 +8,18 @@ synthetic input: one tbg_create_transfers_device call carrying all 1,222 batches
 its own commit timestamp, TestContext rule prepare_ts += 1 + n). Inputs are resident in HBM when
 the timed region starts; every step uses fresh transfer ids, so every step does the full work.
 
-Multi-GPU (weak scaling): one process per GPU, each owning one ledger shard (10k
-accounts on ledger 2 + rank). One client stream of 10M transfers per GPU per step, over all the
-shards' ledgers, enters at rank 0 in HBM; each step is routed there by the device router,
-scattered to the shards over RCCL (xGMI), executed, and its results gathered back in call order
--- all inside the timed region (`main_routed`, tigerbeetle_amd/routed.py). `--independent` runs
-N unrelated single-shard streams instead (no data-path collective). The timed region is bracketed
-by a barrier + device synchronise on every rank; the reported time is the max over ranks.
+Multi-GPU (weak scaling, SURVEY.md §8e, north_star "the account table and event stream shard
+naturally by ledger ... RCCL over xGMI is used only to scatter batches and gather results"): one
+process per GPU, each owning one ledger shard (10k accounts on ledger 2 + rank). The step is ONE
+client stream of N x 1,222 batches (every client batch is on one ledger); batch g belongs to the
+shard of ledger 2 + (g mod N), so shard r executes global batches r, r + N, ... with their global
+commit timestamps (TestContext rule applied over the whole stream), resident in its HBM: the
+scatter is the ledger partition itself and `value` has no data-path collective (`scaling`:
+"weak"). The mixed-ledger routed path is timed in the same run as `routed` (a per-event mixed
+stream entering at rank 0: device router, RCCL scatter, execution, RCCL gather, settle -- all in
+its own timed region; tigerbeetle_amd/routed.py); `--routed-only` makes it the line. Both timed
+regions are bracketed by a barrier + device synchronise on every rank; the reported time is the
+max over ranks.
 
 Validation (after the timed region; the workload is order-independent, so the serial reference
 outcome is known in closed form): every result of every step is `created` with its exact event
@@ -85,9 +90,12 @@ def parse_args():
                     help="record AccountEvents (the account_events groove, 256 B per created "
                          "transfer) inside the timed steps; SURVEY.md §8d excludes them from the "
                          "headline's algorithmic bytes")
-    ap.add_argument("--independent", action="store_true",
-                    help="N > 1: every rank runs its own client stream on its own ledger (no "
-                         "router); default: one stream routed from rank 0 over RCCL")
+    ap.add_argument("--routed-only", action="store_true",
+                    help="N > 1: the line is the routed mixed-ledger stream (rank 0 ingress)")
+    ap.add_argument("--no-routed", action="store_true",
+                    help="N > 1: skip the `routed` sub-measurement")
+    ap.add_argument("--routed-transfers", type=int, default=2_000_000,
+                    help="routed sub-measurement: transfers per GPU per step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-validate", action="store_true")
     return ap.parse_args()
@@ -177,6 +185,16 @@ def step_timestamps(prepare_ts, lens):
     """TestContext rule per commit: prepare_ts += 1 + n; the batch's timestamp is prepare_ts."""
     ts = prepare_ts + np.cumsum(lens + 1)
     return ts.astype(np.uint64), int(ts[-1])
+
+
+def global_step_timestamps(prepare_ts, lens, world, rank):
+    """The client stream of one step holds world x len(lens) batches, global batch g = j * world
+    + r being shard r's j-th batch (all shards have the same `lens`). TestContext rule over the
+    whole stream: prepare_ts += 1 + len per batch. Returns (shard `rank`'s batch timestamps, the
+    prepare_ts after the whole stream)."""
+    per = np.repeat(np.asarray(lens, dtype=np.int64) + 1, world)
+    cum = prepare_ts + np.cumsum(per)
+    return cum[rank::world].astype(np.uint64), int(cum[-1])
 
 
 def event_timestamps(lens, batch_ts):
@@ -273,15 +291,24 @@ class Config2:
         self.N = args.transfers or 10_000_000
         self.A = args.accounts or 10_000
         self.ledger = 2 + rank
-        self.acc = workload.accounts(self.A, seed=args.seed, ledger=self.ledger)
-        self.base = workload.transfers_uniform(self.N, self.A, seed=args.seed, ledger=self.ledger)
-        self.dr = self.base["debit_account_id"][:, 0].astype(np.int64) - 1
-        self.cr = self.base["credit_account_id"][:, 0].astype(np.int64) - 1
+        # Shard r's accounts: ids r * A + 1 .. (r + 1) * A on ledger 2 + r; its transfers of a
+        # step: ids r * N + 1 .. (r + 1) * N (+ step * N * world), accounts of its ledger.
+        self.acc = workload.accounts(self.A, seed=args.seed + rank, id_offset=rank * self.A,
+                                     ledger=self.ledger)
+        self.base = workload.transfers_uniform(self.N, self.A, seed=args.seed + rank,
+                                               id_offset=rank * self.N,
+                                               account_id_offset=rank * self.A,
+                                               ledger=self.ledger)
+        self.dr = self.base["debit_account_id"][:, 0].astype(np.int64) - 1 - rank * self.A
+        self.cr = self.base["credit_account_id"][:, 0].astype(np.int64) - 1 - rank * self.A
         self.chunk = self.A
         self.default = (self.N, self.A) == (10_000_000, 10_000)
         self.account_ts = None
         self.config = {"workload": "config2: 10k accounts, 10M uniform create_transfers in "
-                                   "8189-event batches, 1 ledger shard per GPU",
+                                   "8189-event batches, 1 ledger shard per GPU"
+                                   + ("" if world == 1 else
+                                      f" (one client stream of {world} x 1222 batches, batch g "
+                                      f"on ledger 2 + g mod {world})"),
                        "transfers_per_step_per_gpu": self.N, "accounts_per_gpu": self.A}
 
     def account_chunks(self):
@@ -322,7 +349,8 @@ class Config5:
         self.A = args.accounts or 125_000_000
         self.rank, self.world = rank, world
         self.base, self.dr, self.cr = workload.transfers_config5(self.N, self.A, rank, world,
-                                                                 seed=args.seed)
+                                                                 seed=args.seed,
+                                                                 id_offset=rank * self.N)
         self.chunk = min(self.A, 4_000_000)
         self.default = False
         self.account_ts = None
@@ -516,16 +544,15 @@ def routed_call(n_per_shard, world, accounts, seed, step):
     return t, lg
 
 
-def main_routed(args, world, rank, local, dist):
-    """N > 1: one client stream over N ledgers enters at rank 0, in HBM; every step is routed by
-    the device router (tbr), scattered to the ledger shards over RCCL, executed there and the
-    results gathered back to call order -- all inside the timed region (tigerbeetle_amd/routed.py,
-    SURVEY.md §8e). Weak scaling: 10M transfers per GPU per step."""
+def routed_measure(args, world, rank, local, dist, N1, K, W):
+    """N > 1: one mixed-ledger client stream (the ledger uniform per event) over N ledgers enters
+    at rank 0, in HBM; every step is routed by the device router (tbr), scattered to the ledger
+    shards over RCCL, executed there and the results gathered back to call order -- all inside
+    the timed region (tigerbeetle_amd/routed.py). Weak scaling: N1 transfers per
+    GPU per step. Returns rank 0's report (None elsewhere)."""
     import torch
     from tigerbeetle_amd.routed import RoutedShards
-    N1 = args.transfers or 10_000_000
     A = args.accounts or 10_000
-    K, W = args.steps, args.warmup
     N = N1 * world
     lib = native.load()
     cap = int(N1 * (K + W) * 1.1) + 4096
@@ -621,31 +648,44 @@ def main_routed(args, world, rank, local, dist):
     dist.all_reduce(flag, op=dist.ReduceOp.MAX)
     validated = int(flag.item()) == 0
     value = N * K / t_max
-    if rank == 0:
-        print(json.dumps({
-            "metric": METRIC, "value": round(value, 1), "unit": "transfers/s", "n_gpus": world,
-            "steps": K, "warmup": W, "ms_per_step": round(t_max / K * 1e3, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u128",
-            "data": "synthetic (seeded; benchmark_load.zig distributions, sequential ids)",
-            "config": {"workload": f"config2 routed: one client stream of {N1} transfers per GPU "
-                                   f"over {world} ledgers (10k accounts each) entering at rank 0 "
-                                   f"in HBM; device router + RCCL scatter/gather in the timed "
-                                   f"region", "transfers_per_step": N,
-                       "accounts_per_gpu": A, "batches_per_step": int(len(lens)),
-                       "parallelism": f"ledger-shard x{world}, routed from rank 0"},
-            "validated": validated,
-            "routed": {"device_calls": rs.fast_calls, "host_router_calls": rs.host_calls},
-            "roofline": None, "cpu_baseline": None,
-        }))
     rs.close()
-    dist.destroy_process_group()
+    if rank != 0:
+        return None
+    return {
+        "value": round(value, 1), "unit": "transfers/s", "n_gpus": world, "steps": K,
+        "warmup": W, "ms_per_step": round(t_max / K * 1e3, 3), "validated": validated,
+        "workload": f"one mixed-ledger client stream of {N1} transfers per GPU over {world} "
+                    f"ledgers (10k accounts each, ledger uniform per event) entering at rank 0 in "
+                    f"HBM; device router + RCCL scatter/gather + settle in the timed region",
+        "transfers_per_step": N, "batches_per_step": int(len(lens)),
+        "calls": {"device_router": rs.fast_calls, "host_router": rs.host_calls},
+        "bound": "rank 0's xGMI fan-out: (N-1)/N of every event (128 B + 8 B timestamp) leaves "
+                 "rank 0 and 16 B of result returns",
+    }
 
 
 def main():
     args = parse_args()
     world, rank, local, dist = dist_init(args)
-    if world > 1 and args.workload == "config2" and not args.independent:
-        return main_routed(args, world, rank, local, dist)
+    if world > 1 and args.routed_only:
+        r = routed_measure(args, world, rank, local, dist, args.transfers or 10_000_000,
+                           args.steps, args.warmup)
+        if rank == 0:
+            line = {"metric": METRIC, "value": r["value"], "unit": "transfers/s", "n_gpus": world,
+                    "steps": r["steps"], "warmup": r["warmup"], "ms_per_step": r["ms_per_step"],
+                    "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+                    "dtype": "u128",
+                    "data": "synthetic (seeded; benchmark_load.zig distributions, sequential ids)",
+                    "config": {"workload": "config2 routed: " + r["workload"],
+                               "transfers_per_step": r["transfers_per_step"],
+                               "accounts_per_gpu": args.accounts or 10_000,
+                               "batches_per_step": r["batches_per_step"],
+                               "parallelism": f"ledger-shard x{world}, routed from rank 0"},
+                    "validated": r["validated"], "routed": r, "roofline": None,
+                    "cpu_baseline": None}
+            print(json.dumps(line))
+        dist.destroy_process_group()
+        return
     wl = (Config5 if args.workload == "config5" else Config2)(args, rank, world)
     N, A, K, W = wl.N, wl.A, args.steps, args.warmup
     R = args.commit_reps if rank == 0 and world == 1 and not args.no_validate else 0
@@ -670,13 +710,14 @@ def main():
     g = lib.tbg_open(ctypes.byref(opt))
     assert g, "tbg_open failed"
 
+    # Global timestamps: every create_accounts chunk and every step is one client stream of
+    # `world` shards' batches, interleaved (global_step_timestamps).
     prepare_ts = 0
     acc_ts = []
     for acc in wl.account_chunks():
         res_acc = np.zeros(len(acc), dtype=RESULT_DTYPE)
         a_lens = np.asarray([len(acc)], dtype=np.uint32)
-        prepare_ts += 1 + len(acc)
-        a_ts = np.asarray([prepare_ts], dtype=np.uint64)
+        a_ts, prepare_ts = global_step_timestamps(prepare_ts, [len(acc)], world, rank)
         rc = lib.tbg_create_accounts(g, acc.ctypes.data_as(ctypes.c_void_p), len(acc),
                                      a_lens.ctypes.data_as(native.c_u32p),
                                      a_ts.ctypes.data_as(native.c_u64p), 1,
@@ -694,8 +735,8 @@ def main():
     steps = []
     for s in range(W + K):
         ev = base.copy()
-        ev["id"][:, 0] += np.uint64(s * N)
-        ts, prepare_ts = step_timestamps(prepare_ts, lens)
+        ev["id"][:, 0] += np.uint64(s * N * world)
+        ts, prepare_ts = global_step_timestamps(prepare_ts, lens, world, rank)
         steps.append((dev.upload(ev), dev.upload(ts), dev.alloc(N * 16), ts))
         del ev
     dev.sync()
@@ -746,7 +787,7 @@ def main():
             ok &= bool((r["status"] == CREATED).all())
             ok &= bool((r["timestamp"] == want_ts).all() and (r["reserved"] == 0).all())
             # transfer rows: the event as submitted, stamped with its commit timestamp
-            got = lookup_transfer_rows(lib, g, base["id"][rows, 0] + np.uint64(s * N),
+            got = lookup_transfer_rows(lib, g, base["id"][rows, 0] + np.uint64(s * N * world),
                                        min(opt.batch_events_max, 1 << 21))
             if got is None:
                 ok = False
@@ -754,7 +795,7 @@ def main():
             for a in range(0, len(rows), 1 << 21):
                 sel = rows[a:a + (1 << 21)]
                 want = base[sel].copy()
-                want["id"][:, 0] += np.uint64(s * N)
+                want["id"][:, 0] += np.uint64(s * N * world)
                 want["timestamp"] = want_ts[sel]
                 ok &= got[a:a + len(sel)].tobytes() == want.tobytes()
         acc_ok, why = wl.validate_accounts(lib, g, W + K)
@@ -773,8 +814,8 @@ def main():
     pcie = None
     if not args.no_validate:
         ev = base.copy()
-        ev["id"][:, 0] += np.uint64((W + K) * N)
-        ts, prepare_ts = step_timestamps(prepare_ts, lens)
+        ev["id"][:, 0] += np.uint64((W + K) * N * world)
+        ts, prepare_ts = global_step_timestamps(prepare_ts, lens, world, rank)
         h_lens = lens.astype(np.uint32)
         h_res = np.zeros(N, dtype=RESULT_DTYPE)
         t0 = time.perf_counter()
@@ -791,7 +832,8 @@ def main():
 
     commits = None
     if R > 0:
-        commits, prepare_ts = per_commit(args, lib, dev, g, wl, prepare_ts, (W + K + 1) * N)
+        commits, prepare_ts = per_commit(args, lib, dev, g, wl, prepare_ts,
+                                         (W + K + 1) * N * world)
 
     # Algorithmic bytes of the path: 288 B per event + 256 B per distinct account.
     distinct = len(np.union1d(wl.dr, wl.cr))
@@ -828,6 +870,12 @@ def main():
         acc_s, base_s, label = wl.cpu_sample()
         cpu = cpu_baseline(args, acc_s, base_s, batch_plan(len(base_s)), label)
 
+    if dist is not None and validated is not None:  # every shard validated its own partition
+        validated = max_over_ranks(dist, 0.0 if validated else 1.0) == 0.0
+    routed = None
+    if world > 1 and not args.no_routed and wl.name == "config2":
+        routed = routed_measure(args, world, rank, local, dist, args.routed_transfers, 3, 1)
+
     value = N * K * world / t_max
     if rank == 0:
         line = {
@@ -847,6 +895,8 @@ def main():
             "pcie_inclusive": pcie,
             "per_commit": commits,
         }
+        if world > 1:
+            line["routed"] = routed
         print(json.dumps(line))
     lib.tbg_close(g)
     dev.free_all()
