@@ -15,6 +15,10 @@
  *   tb_sm_prefetch        <- StateMachine.prefetch      :1146-1226 (completes immediately:
  *                            the tables are HBM-resident; the callback runs before return)
  *   tb_sm_commit          <- StateMachine.commit        :2564-2669 / execute_multi_batch :2702
+ *   tb_sm_compact         <- StateMachine.compact       :2912-2935 (the HIP executor's tables
+ *                            are compacted at the last op of each bar, TB_SM_COMPACTION_OPS)
+ *   tb_sm_checkpoint      <- StateMachine.checkpoint    :2937-2958 (an image of the tables)
+ *   tb_sm_open_gpu_checkpoint <- StateMachine.open      :964-978 (tables loaded from an image)
  *   tb_sm_{get,set}_*_timestamp <- fields prepare_timestamp / commit_timestamp /
  *                            prefetch_timestamp (:229-231), written by the replica.
  */
@@ -69,6 +73,9 @@ typedef struct tb_sm_options {
 tb_sm* tb_sm_open(const tb_sm_options* options, const tb_executor* executor);
 /* Opens the HIP executor (tbg_open) and binds it; the tb_sm owns it. */
 tb_sm* tb_sm_open_gpu(const tb_sm_options* options, const tbg_options* executor_options);
+/* Opens the HIP executor from a checkpoint image (tbg_open_checkpoint) and binds it. */
+tb_sm* tb_sm_open_gpu_checkpoint(const tb_sm_options* options,
+                                 const tbg_options* executor_options, const char* path);
 void tb_sm_close(tb_sm* sm);
 /* The bound HIP executor of a tb_sm_open_gpu state machine (NULL otherwise). */
 tbg_ctx* tb_sm_executor_gpu(tb_sm* sm);
@@ -86,6 +93,14 @@ void tb_sm_prefetch(tb_sm* sm, tb_sm_prefetch_callback callback, void* context, 
 int64_t tb_sm_commit(tb_sm* sm, uint64_t client_lo, uint64_t client_hi, uint64_t op,
                      uint64_t timestamp, uint8_t operation, const void* body, uint32_t size,
                      void* output);
+
+/* Ops per bar (constants.lsm_compaction_ops, src/constants.zig:647; 32 in the production
+ * config): the LSM spreads a bar's compaction over its ops, the executor compacts its transfer
+ * store (tbg_compact) at the bar's last op. Returns 0 or a negative executor error. */
+#define TB_SM_COMPACTION_OPS 32
+int tb_sm_compact(tb_sm* sm, uint64_t op);
+/* Writes the executor's checkpoint image to `path` (tbg_checkpoint); -22 for a non-HIP executor. */
+int tb_sm_checkpoint(tb_sm* sm, const char* path);
 
 uint64_t tb_sm_get_prepare_timestamp(const tb_sm* sm);
 uint64_t tb_sm_get_commit_timestamp(const tb_sm* sm);

@@ -129,6 +129,24 @@ int64_t tbg_dump_account_events(tbg_ctx* ctx, tb_account_event_t* out);
 int64_t tbg_get_change_events(tbg_ctx* ctx, const tb_change_events_filter_t* filter,
                               uint32_t limit_max, tb_change_event_t* out);
 
+/* Durability (the reference persists these tables through its Forest).
+ *   tbg_compact          <- StateMachine.compact (state_machine.zig:2912-2935): drops the rows of
+ *                           transfer events that created no object and orphaned no id (rows are
+ *                           consumed by every event), rebuilds the transfer id index without the
+ *                           tombstones of failed claims, keeps row order (= timestamp order).
+ *                           Returns the rows freed (>= 0) or an error. Results of later calls are
+ *                           unchanged by it.
+ *   tbg_checkpoint       <- StateMachine.checkpoint (:2937-2958): writes an image of every
+ *                           persistent table (accounts, transfers, TransferPending, expires_at,
+ *                           AccountEvents, pulse_next_timestamp, key ranges) to `path`, replacing
+ *                           it atomically (written to `path`.tmp, then renamed).
+ *   tbg_open_checkpoint  <- StateMachine.open (:964-978): opens a ctx with `options` (the same
+ *                           capacities as the ctx that wrote the image) and loads the image; NULL
+ *                           if the image is unreadable or does not fit. */
+int64_t tbg_compact(tbg_ctx* ctx);
+int tbg_checkpoint(tbg_ctx* ctx, const char* path);
+tbg_ctx* tbg_open_checkpoint(const tbg_options* options, const char* path);
+
 /* Test-harness `setup` action (src/state_machine_tests.zig:657-676). */
 int tbg_debug_set_account_balances(tbg_ctx* ctx, tb_uint128_t id, tb_uint128_t debits_pending,
                                    tb_uint128_t debits_posted, tb_uint128_t credits_pending,

@@ -49,19 +49,43 @@ class Pair:
         # AccountEvents (one per created transfer and per expiry), compared in compare_state.
         o.account_events_capacity = 2 * transfer_capacity if account_events else 0
         self.account_events = account_events
+        self.opt = o
         self.g = self.lib.tbg_open(ctypes.byref(o))
         if not self.g:
             raise RuntimeError("tbg_open failed")
-        if force_replay:  # True: every event through the flow replay; "serial": on one lane
-            self.lib.tbg_debug_force_replay(self.g, 1)
-        if force_replay == "serial":
-            self.lib.tbg_debug_serial_replay(self.g, 1)
+        self._force_replay = force_replay
+        self._apply_debug_modes()
         self.o = self.olib.tbo_open(pulse_batch_max, pulse_next_timestamp_init)
         self.prepare_timestamp = 0
         self._pulse_delta = pulse_batch_max
         self.calls = 0
         self.stats = {"events": 0, "fast": 0, "replayed": 0, "static_fail": 0}
         self.seconds = {"gpu": 0.0, "oracle": 0.0}  # wall time of each side's create_* calls
+
+    def _apply_debug_modes(self):
+        force_replay = self._force_replay
+        if force_replay:  # True: every event through the flow replay; "serial": on one lane
+            self.lib.tbg_debug_force_replay(self.g, 1)
+        if force_replay == "serial":
+            self.lib.tbg_debug_serial_replay(self.g, 1)
+
+    def compact(self):
+        """tbg_compact on the executor (the oracle has nothing to compact); rows freed."""
+        n = self.lib.tbg_compact(self.g)
+        if n < 0:
+            raise RuntimeError(f"tbg_compact: {n} {self.lib.tbg_last_error(self.g)}")
+        return n
+
+    def checkpoint_reopen(self, path):
+        """Checkpoint the executor, close it, and continue on a ctx opened from the image."""
+        rc = self.lib.tbg_checkpoint(self.g, str(path).encode())
+        if rc != 0:
+            raise RuntimeError(f"tbg_checkpoint: {rc} {self.lib.tbg_last_error(self.g)}")
+        self.lib.tbg_close(self.g)
+        self.g = self.lib.tbg_open_checkpoint(ctypes.byref(self.opt), str(path).encode())
+        if not self.g:
+            raise RuntimeError("tbg_open_checkpoint failed")
+        self._apply_debug_modes()
 
     def close(self):
         if self.g:

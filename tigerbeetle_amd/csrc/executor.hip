@@ -10,12 +10,14 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <vector>
 
 #include "../../include/tbg.h"
 #include "lanes.hpp"
 #include "events.hpp"
+#include "durability.hpp"
 
 using namespace tbg;
 
@@ -1550,6 +1552,316 @@ int tbg_profile_read(tbg_ctx* ctx, uint32_t index, char* name, uint32_t name_len
     if (total_ms) *total_ms = ctx->prof_ms[index];
     if (launches) *launches = ctx->prof_count[index];
     return 1;
+}
+
+}  // extern "C"
+
+// ---- Durability (durability.hpp) ----------------------------------------------------------------
+
+namespace {
+
+// Checkpoint image: a header, then the persistent tables in a fixed order (tbg_checkpoint).
+struct CkptHeader {
+    char magic[8];
+    uint32_t version, epoch;
+    tbg_options opt;
+    uint64_t acc_rows_used, tr_rows_used, ae_used, ae_last_ts;
+    uint64_t acc_slots, tr_slots, acc_entries;
+    uint32_t ae_sorted, pad;
+    DevScalars scalars;
+};
+constexpr char kCkptMagic[8] = {'T', 'B', 'G', 'C', 'K', 'P', 'T', '1'};
+constexpr uint32_t kCkptVersion = 1;
+constexpr size_t kStageBytes = size_t(64) << 20;
+
+// Device <-> file through one pinned staging buffer.
+struct Stager {
+    tbg_ctx* ctx;
+    FILE* f;
+    uint8_t* host = nullptr;
+    bool ok = true;
+    Stager(tbg_ctx* c, FILE* file) : ctx(c), f(file) {
+        ok = hip_ok(ctx, hipHostMalloc(reinterpret_cast<void**>(&host), kStageBytes), "stage");
+    }
+    ~Stager() {
+        if (host) (void)hipHostFree(host);
+    }
+    bool write(const void* dev, uint64_t bytes) {
+        const uint8_t* d = static_cast<const uint8_t*>(dev);
+        for (uint64_t off = 0; ok && off < bytes; off += kStageBytes) {
+            const size_t n = size_t(std::min<uint64_t>(kStageBytes, bytes - off));
+            ok = hip_ok(ctx, hipMemcpyAsync(host, d + off, n, hipMemcpyDeviceToHost, ctx->stream),
+                        "checkpoint copy") &&
+                 hip_ok(ctx, hipStreamSynchronize(ctx->stream), "checkpoint sync") &&
+                 fwrite(host, 1, n, f) == n;
+            if (!ok && ctx->error.empty()) ctx->error = "checkpoint write";
+        }
+        return ok;
+    }
+    bool read(void* dev, uint64_t bytes) {
+        uint8_t* d = static_cast<uint8_t*>(dev);
+        for (uint64_t off = 0; ok && off < bytes; off += kStageBytes) {
+            const size_t n = size_t(std::min<uint64_t>(kStageBytes, bytes - off));
+            ok = fread(host, 1, n, f) == n &&
+                 hip_ok(ctx, hipMemcpyAsync(d + off, host, n, hipMemcpyHostToDevice, ctx->stream),
+                        "restore copy") &&
+                 hip_ok(ctx, hipStreamSynchronize(ctx->stream), "restore sync");
+            if (!ok && ctx->error.empty()) ctx->error = "checkpoint image truncated";
+        }
+        return ok;
+    }
+};
+
+uint64_t acc_slot_count(const tbg_ctx* ctx) { return ctx->T.acc.mask + 1; }
+uint64_t tr_slot_count(const tbg_ctx* ctx) { return ctx->T.tr.mask + 1; }
+uint64_t acc_entry_count(const tbg_ctx* ctx) { return ctx->T.acc_index.mask + 1; }
+
+// The persistent tables, in image order: (device pointer, bytes).
+std::vector<std::pair<void*, uint64_t>> ckpt_sections(tbg_ctx* ctx, uint64_t acc_used,
+                                                      uint64_t tr_used, uint64_t expiry_count,
+                                                      uint64_t ae_used) {
+    Tables& T = ctx->T;
+    return {
+        {T.acc.slots, acc_slot_count(ctx) * 8},
+        {T.acc_index.entries, acc_entry_count(ctx) * sizeof(AccEntry)},
+        {T.acc_entry_of, acc_used * 4},
+        {T.acc_rows, acc_used * sizeof(tb_account_t)},
+        {T.acc_live, acc_used},
+        {T.tr.slots, tr_slot_count(ctx) * 8},
+        {T.tr_rows, tr_used * sizeof(tb_transfer_t)},
+        {T.tr_live, tr_used},
+        {T.tr_status, tr_used},
+        {T.expiry, expiry_count * 8},
+        {ctx->ae_log, ae_used * sizeof(tb_account_event_t)},
+        {ctx->ae_ref, ae_used * sizeof(AeRef)},
+    };
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t tbg_compact(tbg_ctx* ctx) {
+    if (!ctx) return TBG_EINVAL;
+    Tables& T = ctx->T;
+    const uint64_t used = T.tr_rows_used;
+    if (used == 0) return 0;
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->h_scalars, ctx->d_scalars, sizeof(DevScalars),
+                                hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    const uint64_t expiry_count = ctx->h_scalars->expiry_count;
+    const uint64_t chunk = std::min<uint64_t>(used, uint64_t(1) << 22);
+    uint32_t *keep32 = nullptr, *new_row = nullptr, *sel = nullptr;
+    tb_transfer_t* c_rows = nullptr;
+    uint8_t *c_live = nullptr, *c_status = nullptr, *x_flags = nullptr;
+    uint64_t* x_out = nullptr;
+    unsigned int* d_words = nullptr;
+    int64_t rc = 0;
+    const uint64_t xn = std::max<uint64_t>(expiry_count, 1);
+    if (!(dev_alloc(ctx, &keep32, used + 1, true) && dev_alloc(ctx, &new_row, used + 1, false) &&
+          dev_alloc(ctx, &c_rows, chunk, false) && dev_alloc(ctx, &c_live, chunk, false) &&
+          dev_alloc(ctx, &c_status, chunk, false) && dev_alloc(ctx, &x_flags, xn, false) &&
+          dev_alloc(ctx, &sel, xn, false) && dev_alloc(ctx, &x_out, xn, false) &&
+          dev_alloc(ctx, &d_words, 2, true)))
+        rc = TBG_ENOMEM;
+    uint32_t kept = 0;
+    if (!rc) {
+        hipLaunchKernelGGL(cmp_mark, dim3(grid_for(tr_slot_count(ctx))), dim3(kBlock), 0,
+                           ctx->stream, T.tr, used, keep32);
+        size_t bytes = 0;
+        // (keep32[used] = 0: new_row[used] is the kept count)
+        if (hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, keep32, new_row, int(used + 1),
+                                             ctx->stream) != hipSuccess)
+            rc = TBG_EHIP;
+        if (!rc) rc = ensure_cub_temp(ctx, bytes);
+        if (!rc && hipcub::DeviceScan::ExclusiveSum(ctx->cub_temp, bytes, keep32, new_row,
+                                                    int(used + 1), ctx->stream) != hipSuccess)
+            rc = TBG_EHIP;
+        if (!rc && !(hip_ok(ctx, hipMemcpyAsync(&kept, new_row + used, 4, hipMemcpyDeviceToHost,
+                                                ctx->stream), "kept") &&
+                     hip_ok(ctx, hipStreamSynchronize(ctx->stream), "sync")))
+            rc = TBG_EHIP;
+    }
+    // Rows move down in place, one chunk at a time: chunk [a, b)'s kept rows go to
+    // [new_row[a], new_row[b]), which ends at or before b and starts after every earlier chunk's.
+    for (uint64_t a = 0; !rc && a < used; a += chunk) {
+        const uint64_t b = std::min(used, a + chunk);
+        uint32_t bounds[2] = {0, 0};
+        if (!(hip_ok(ctx, hipMemcpyAsync(&bounds[0], new_row + a, 4, hipMemcpyDeviceToHost,
+                                         ctx->stream), "bounds") &&
+              hip_ok(ctx, hipMemcpyAsync(&bounds[1], new_row + b, 4, hipMemcpyDeviceToHost,
+                                         ctx->stream), "bounds") &&
+              hip_ok(ctx, hipStreamSynchronize(ctx->stream), "sync"))) {
+            rc = TBG_EHIP;
+            break;
+        }
+        const uint64_t cnt = bounds[1] - bounds[0];
+        if (cnt == 0 || (cnt == b - a && bounds[0] == a)) continue;  // nothing kept / nothing moves
+        hipLaunchKernelGGL(cmp_gather, dim3(grid_for(b - a)), dim3(kBlock), 0, ctx->stream,
+                           T.tr_rows, T.tr_live, T.tr_status, keep32, new_row, a, b, bounds[0],
+                           c_rows, c_live, c_status);
+        if (!(hip_ok(ctx, hipMemcpyAsync(T.tr_rows + bounds[0], c_rows, cnt * sizeof(tb_transfer_t),
+                                         hipMemcpyDeviceToDevice, ctx->stream), "move rows") &&
+              hip_ok(ctx, hipMemcpyAsync(T.tr_live + bounds[0], c_live, cnt,
+                                         hipMemcpyDeviceToDevice, ctx->stream), "move live") &&
+              hip_ok(ctx, hipMemcpyAsync(T.tr_status + bounds[0], c_status, cnt,
+                                         hipMemcpyDeviceToDevice, ctx->stream), "move status")))
+            rc = TBG_EHIP;
+    }
+    if (!rc) {
+        // Fresh rows read as dead with TransferPending none.
+        if (!(hip_ok(ctx, hipMemsetAsync(T.tr_live + kept, 0, used - kept, ctx->stream), "clear") &&
+              hip_ok(ctx, hipMemsetAsync(T.tr_status + kept, 0, used - kept, ctx->stream), "clear") &&
+              hip_ok(ctx, hipMemsetAsync(T.tr.slots, 0, tr_slot_count(ctx) * 8, ctx->stream),
+                     "clear slots")))
+            rc = TBG_EHIP;
+    }
+    if (!rc && kept) {
+        hipLaunchKernelGGL(cmp_insert, dim3(grid_for(kept)), dim3(kBlock), 0, ctx->stream, T.tr,
+                           T.tr_rows, T.tr_live, uint64_t(kept), d_words);
+    }
+    uint64_t x_kept = 0;
+    if (!rc && expiry_count) {
+        hipLaunchKernelGGL(cmp_expiry_flags, dim3(grid_for(expiry_count)), dim3(kBlock), 0,
+                           ctx->stream, T.expiry, expiry_count, used, keep32, x_flags);
+        rc = select_flagged(ctx, x_flags, expiry_count, sel, d_words + 1);
+        unsigned int xk = 0;
+        if (!rc && !(hip_ok(ctx, hipMemcpyAsync(&xk, d_words + 1, 4, hipMemcpyDeviceToHost,
+                                                ctx->stream), "expiry count") &&
+                     hip_ok(ctx, hipStreamSynchronize(ctx->stream), "sync")))
+            rc = TBG_EHIP;
+        x_kept = xk;
+        if (!rc && x_kept) {
+            hipLaunchKernelGGL(cmp_expiry_gather, dim3(grid_for(x_kept)), dim3(kBlock), 0,
+                               ctx->stream, T.expiry, sel, x_kept, new_row, x_out);
+            if (!hip_ok(ctx, hipMemcpyAsync(T.expiry, x_out, x_kept * 8, hipMemcpyDeviceToDevice,
+                                            ctx->stream), "expiry"))
+                rc = TBG_EHIP;
+        }
+    }
+    if (!rc && ctx->ae_used)
+        hipLaunchKernelGGL(cmp_ae_refs, dim3(grid_for(ctx->ae_used)), dim3(kBlock), 0, ctx->stream,
+                           ctx->ae_ref, ctx->ae_used, new_row);
+    unsigned int failed = 0;
+    if (!rc) {
+        const unsigned long long xc = x_kept;
+        if (!(hip_ok(ctx, hipGetLastError(), "compact launch") &&
+              hip_ok(ctx, hipMemcpyAsync(&ctx->d_scalars->expiry_count, &xc, 8,
+                                         hipMemcpyHostToDevice, ctx->stream), "expiry count") &&
+              hip_ok(ctx, hipMemcpyAsync(&failed, d_words, 4, hipMemcpyDeviceToHost, ctx->stream),
+                     "insert") &&
+              hip_ok(ctx, hipStreamSynchronize(ctx->stream), "compact sync")))
+            rc = TBG_EHIP;
+    }
+    if (!rc && failed) {
+        ctx->error = "id index full during compaction";
+        rc = TBG_ENOSPC;
+    }
+    if (!rc) {
+        T.tr_rows_used = kept;
+        ctx->tr_ts_stale = true;
+        rc = int64_t(used - kept);
+    }
+    for (void* p : {(void*)keep32, (void*)new_row, (void*)sel, (void*)c_rows, (void*)c_live,
+                    (void*)c_status, (void*)x_flags, (void*)x_out, (void*)d_words})
+        if (p) (void)hipFree(p);
+    return rc;
+}
+
+int tbg_checkpoint(tbg_ctx* ctx, const char* path) {
+    if (!ctx || !path) return TBG_EINVAL;
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->h_scalars, ctx->d_scalars, sizeof(DevScalars),
+                                hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    int rc = ae_sort_log(ctx);
+    if (rc) return rc;
+    CkptHeader h{};
+    memcpy(h.magic, kCkptMagic, 8);
+    h.version = kCkptVersion;
+    h.epoch = ctx->epoch;
+    h.opt = ctx->opt;
+    h.acc_rows_used = ctx->T.acc_rows_used;
+    h.tr_rows_used = ctx->T.tr_rows_used;
+    h.ae_used = ctx->ae_used;
+    h.ae_last_ts = ctx->ae_last_ts;
+    h.acc_slots = acc_slot_count(ctx);
+    h.tr_slots = tr_slot_count(ctx);
+    h.acc_entries = acc_entry_count(ctx);
+    h.ae_sorted = 1;
+    h.scalars = *ctx->h_scalars;
+    // (per-call words are not state)
+    memset(&h.scalars.flags, 0, sizeof(DevScalars) - offsetof(DevScalars, flags));
+    const std::string tmp = std::string(path) + ".tmp";
+    FILE* f = fopen(tmp.c_str(), "wb");
+    if (!f) {
+        ctx->error = "checkpoint: cannot create " + tmp;
+        return TBG_EINVAL;
+    }
+    bool ok = fwrite(&h, sizeof(h), 1, f) == 1;
+    {
+        Stager st(ctx, f);
+        ok = ok && st.ok;
+        for (auto& sec : ckpt_sections(ctx, h.acc_rows_used, h.tr_rows_used,
+                                       h.scalars.expiry_count, h.ae_used))
+            ok = ok && st.write(sec.first, sec.second);
+    }
+    ok = fflush(f) == 0 && ok;
+    ok = fclose(f) == 0 && ok;
+    // The image replaces the previous one only once complete (the superblock's atomic switch).
+    if (ok) ok = rename(tmp.c_str(), path) == 0;
+    if (!ok) {
+        if (ctx->error.empty()) ctx->error = "checkpoint: write failed";
+        remove(tmp.c_str());
+        return TBG_EHIP;
+    }
+    return 0;
+}
+
+tbg_ctx* tbg_open_checkpoint(const tbg_options* options, const char* path) {
+    if (!options || !path) return nullptr;
+    FILE* f = fopen(path, "rb");
+    if (!f) return nullptr;
+    CkptHeader h{};
+    if (fread(&h, sizeof(h), 1, f) != 1 || memcmp(h.magic, kCkptMagic, 8) != 0 ||
+        h.version != kCkptVersion) {
+        fclose(f);
+        return nullptr;
+    }
+    tbg_ctx* ctx = tbg_open(options);
+    if (!ctx) {
+        fclose(f);
+        return nullptr;
+    }
+    // The id tables are restored slot for slot: the table geometry must match the image's.
+    bool ok = acc_slot_count(ctx) == h.acc_slots && tr_slot_count(ctx) == h.tr_slots &&
+              acc_entry_count(ctx) == h.acc_entries &&
+              h.acc_rows_used <= options->account_capacity &&
+              h.tr_rows_used <= options->transfer_capacity &&
+              h.scalars.expiry_count <= ctx->T.expiry_capacity && h.ae_used <= ctx->ae_cap;
+    if (ok) {
+        Stager st(ctx, f);
+        ok = st.ok;
+        for (auto& sec : ckpt_sections(ctx, h.acc_rows_used, h.tr_rows_used,
+                                       h.scalars.expiry_count, h.ae_used))
+            ok = ok && st.read(sec.first, sec.second);
+    }
+    fclose(f);
+    if (ok)
+        ok = hip_ok(ctx, hipMemcpyAsync(ctx->d_scalars, &h.scalars, sizeof(DevScalars),
+                                        hipMemcpyHostToDevice, ctx->stream), "scalars") &&
+             hip_ok(ctx, hipStreamSynchronize(ctx->stream), "sync");
+    if (!ok) {
+        tbg_close(ctx);
+        return nullptr;
+    }
+    ctx->T.acc_rows_used = h.acc_rows_used;
+    ctx->T.tr_rows_used = h.tr_rows_used;
+    ctx->epoch = h.epoch;  // (the epoch marks start zeroed: no stale mark matches a later call)
+    ctx->ae_used = h.ae_used;
+    ctx->ae_last_ts = h.ae_last_ts;
+    ctx->ae_sorted = h.ae_sorted != 0;
+    ctx->acc_ts_stale = ctx->tr_ts_stale = true;
+    return ctx;
 }
 
 }  // extern "C"

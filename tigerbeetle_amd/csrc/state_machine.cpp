@@ -188,8 +188,8 @@ extern "C" tb_sm* tb_sm_open(const tb_sm_options* options, const tb_executor* ex
     return sm;
 }
 
-extern "C" tb_sm* tb_sm_open_gpu(const tb_sm_options* options, const tbg_options* executor_options) {
-    tbg_ctx* ctx = tbg_open(executor_options);
+namespace {
+tb_sm* bind_gpu(const tb_sm_options* options, tbg_ctx* ctx) {
     if (!ctx) return nullptr;
     tb_executor ex;
     ex.self = ctx;
@@ -207,6 +207,28 @@ extern "C" tb_sm* tb_sm_open_gpu(const tb_sm_options* options, const tbg_options
     }
     sm->gpu = ctx;
     return sm;
+}
+}  // namespace
+
+extern "C" tb_sm* tb_sm_open_gpu(const tb_sm_options* options, const tbg_options* executor_options) {
+    return bind_gpu(options, tbg_open(executor_options));
+}
+
+extern "C" tb_sm* tb_sm_open_gpu_checkpoint(const tb_sm_options* options,
+                                            const tbg_options* executor_options, const char* path) {
+    return bind_gpu(options, tbg_open_checkpoint(executor_options, path));
+}
+
+extern "C" int tb_sm_compact(tb_sm* sm, uint64_t op) {
+    if (!sm) return TBG_EINVAL;
+    if (!sm->gpu || (op + 1) % TB_SM_COMPACTION_OPS != 0) return 0;
+    const int64_t rc = tbg_compact(sm->gpu);
+    return rc < 0 ? int(rc) : 0;
+}
+
+extern "C" int tb_sm_checkpoint(tb_sm* sm, const char* path) {
+    if (!sm || !sm->gpu) return TBG_EINVAL;
+    return tbg_checkpoint(sm->gpu, path);
 }
 
 extern "C" void tb_sm_close(tb_sm* sm) {

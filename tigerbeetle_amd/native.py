@@ -98,6 +98,9 @@ SIGNATURES = [
     ("tbg_dump_transfers", ctypes.c_int64, [vp, vp, vp]),
     ("tbg_dump_account_events", ctypes.c_int64, [vp, vp]),
     ("tbg_get_change_events", ctypes.c_int64, [vp, vp, ctypes.c_uint32, vp]),
+    ("tbg_compact", ctypes.c_int64, [vp]),
+    ("tbg_checkpoint", ctypes.c_int, [vp, ctypes.c_char_p]),
+    ("tbg_open_checkpoint", vp, [ctypes.POINTER(TbgOptions), ctypes.c_char_p]),
     ("tbg_debug_set_account_balances", ctypes.c_int, [vp, U128, U128, U128, U128, U128]),
     ("tbg_last_stats", ctypes.c_int, [vp, ctypes.POINTER(TbgStats)]),
     ("tbg_debug_force_replay", ctypes.c_int, [vp, ctypes.c_int]),
@@ -117,7 +120,11 @@ SIGNATURES = [
     ("tbr_settle_device", ctypes.c_int, [vp, vp, vp, ctypes.c_uint32, vp]),
     ("tb_sm_open", vp, [ctypes.POINTER(SmOptions), ctypes.POINTER(Executor)]),
     ("tb_sm_open_gpu", vp, [ctypes.POINTER(SmOptions), ctypes.POINTER(TbgOptions)]),
+    ("tb_sm_open_gpu_checkpoint", vp, [ctypes.POINTER(SmOptions), ctypes.POINTER(TbgOptions),
+                                       ctypes.c_char_p]),
     ("tb_sm_close", None, [vp]),
+    ("tb_sm_compact", ctypes.c_int, [vp, ctypes.c_uint64]),
+    ("tb_sm_checkpoint", ctypes.c_int, [vp, ctypes.c_char_p]),
     ("tb_sm_executor_gpu", vp, [vp]),
     ("tb_sm_input_valid", ctypes.c_int, [vp, ctypes.c_uint8, vp, ctypes.c_uint32]),
     ("tb_sm_prepare", None, [vp, ctypes.c_uint8, vp, ctypes.c_uint32]),
