@@ -358,12 +358,16 @@ def test_flow_replay_stress(seed):
         p.close()
 
 
+@pytest.mark.parametrize("walk", ["wave", "one-lane"])
 @pytest.mark.parametrize("n_acc", [200, 700], ids=["lanes", "over-lanes"])
-def test_account_lanes_limits(n_acc):
+def test_account_lanes_limits(n_acc, walk, monkeypatch):
     """Calls whose replayed events are all limit events run on the account lanes (one lane per
     limited account): debits_must_not_exceed_credits and credits_must_not_exceed_debits on both
     sides, transfers between two limited accounts (both verdicts needed), between a limited and an
-    unlimited account, and funding; 700 limited accounts exceed the lanes (the flow replay runs)."""
+    unlimited account, and funding; 700 limited accounts exceed the lanes (the flow replay runs).
+    `walk`: one wave per walked owner (lanes_walk) or one lane (lanes_replay)."""
+    if walk == "one-lane":
+        monkeypatch.setenv("TBG_LANES_ONE_LANE", "1")
     rng = np.random.default_rng(n_acc)
     p = Pair(account_capacity=1 << 12, transfer_capacity=1 << 17, batch_events_max=1 << 15)
     try:
@@ -452,8 +456,9 @@ def test_flow_additive_accounts(additive, monkeypatch):
         p.close()
 
 
+@pytest.mark.parametrize("walk", ["wave", "one-lane"])
 @pytest.mark.parametrize("free_owners", [True, False], ids=["free", "walked"])
-def test_account_lanes_free_owners(free_owners, monkeypatch):
+def test_account_lanes_free_owners(free_owners, walk, monkeypatch):
     """Account lanes with free owners (lanes.hpp): limited accounts funded beyond every amount
     they check in the call need no lane (their sides become atomics, events left without owners
     are created), next to limited accounts that run out mid-call and still walk -- with events
@@ -461,6 +466,8 @@ def test_account_lanes_free_owners(free_owners, monkeypatch):
     debits on the credit side; against the oracle, with and without free owners."""
     if not free_owners:
         monkeypatch.setenv("TBG_NO_FREE_OWNERS", "1")
+    if walk == "one-lane":
+        monkeypatch.setenv("TBG_LANES_ONE_LANE", "1")
     rng = np.random.default_rng(91)
     p = Pair(account_capacity=64, transfer_capacity=1 << 14, batch_events_max=1 << 12)
     try:
@@ -489,6 +496,44 @@ def test_account_lanes_free_owners(free_owners, monkeypatch):
                                  code=1))
             r = p.create_transfers(_transfers(rows), [len(rows)])
             assert (r["status"] == 0xFFFFFFFF).sum() > 0
+        p.compare_state()
+    finally:
+        p.close()
+
+
+@pytest.mark.parametrize("walk", ["wave", "one-lane"])
+def test_account_walk_long_owner(walk, monkeypatch):
+    """One walked owner with ~100k events in a single call (its funding runs out a third of the
+    way), a second walked owner in another wave with a few hundred events, transfers between them
+    both ways (each needs the other's verdict) and the call's LAST event shared by both: the waiting
+    owner polls for as long as the long walk takes (the watchdog must count every wave's progress,
+    ADVICE r1)."""
+    if walk == "one-lane":
+        monkeypatch.setenv("TBG_LANES_ONE_LANE", "1")
+    rng = np.random.default_rng(4242)
+    p = Pair(account_capacity=64, transfer_capacity=1 << 18, batch_events_max=1 << 17)
+    try:
+        acc = workload.accounts(8, seed=3, ledger=1)
+        acc["flags"] = [0, 2, 2, 0, 0, 0, 0, 0]  # 2, 3: debits_must_not_exceed_credits
+        p.create_accounts(acc)
+        n = 100_000
+        p.create_transfers(_transfers([
+            dict(id=1, debit_account_id=1, credit_account_id=2, amount=n * 50 // 3, ledger=1,
+                 code=1),
+            dict(id=2, debit_account_id=1, credit_account_id=3, amount=4000, ledger=1, code=1)]))
+        t = workload.transfers_uniform(n, 8, seed=5, id_offset=100)
+        t["ledger"] = 1
+        t["debit_account_id"][:, 0] = 2
+        t["credit_account_id"][:, 0] = rng.choice([4, 5, 6, 7, 8], size=n).astype(np.uint64)
+        t["amount"][:, 0] = rng.integers(1, 100, size=n).astype(np.uint64)
+        few = rng.choice(n - 1, size=600, replace=False)
+        t["debit_account_id"][few[:300], 0] = 3          # 3 -> 2: 2 waits for 3's verdict
+        t["credit_account_id"][few[:300], 0] = 2
+        t["credit_account_id"][few[300:], 0] = 3         # 2 -> 3: 3 waits for 2's verdict
+        t["amount"][few, 0] = rng.integers(1, 40, size=600).astype(np.uint64)
+        t["credit_account_id"][n - 1, 0] = 3             # the last event: 2 -> 3
+        r = p.create_transfers(t, [8189] * (n // 8189) + [n % 8189])
+        assert (r["status"] == 54).sum() > n // 2
         p.compare_state()
     finally:
         p.close()

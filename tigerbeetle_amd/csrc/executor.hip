@@ -483,14 +483,21 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
         L.counts = F.lane_counts;
         HIP_TRY(ctx, hipMemsetAsync(F.lane_counts, 0, 16, ctx->stream));
         hipLaunchKernelGGL(lanes_check, dim3(grid_for(m)), block, 0, ctx->stream, ctx->T, c, P, L);
-        size_t sb = 0;
-        HIP_TRY(ctx, hipcub::DeviceScan::ExclusiveSum(nullptr, sb, F.mailbox, F.mb_index, int(m),
-                                                      ctx->stream));
-        rc = ensure_cub_temp(ctx, sb);
-        if (rc) return rc;
-        HIP_TRY(ctx, hipcub::DeviceScan::ExclusiveSum(ctx->cub_temp, sb, F.mailbox, F.mb_index,
-                                                      int(m), ctx->stream));
-        hipLaunchKernelGGL(lanes_mailboxes, dim3(grid_for(m)), block, 0, ctx->stream, L);
+        // One-lane walk (lanes_replay): LDS mailbox indexes. Wave walk (lanes_walk, the
+        // default): a zeroed word per position in global memory.
+        const bool one_lane = getenv("TBG_LANES_ONE_LANE") != nullptr;
+        if (one_lane) {
+            size_t sb = 0;
+            HIP_TRY(ctx, hipcub::DeviceScan::ExclusiveSum(nullptr, sb, F.mailbox, F.mb_index,
+                                                          int(m), ctx->stream));
+            rc = ensure_cub_temp(ctx, sb);
+            if (rc) return rc;
+            HIP_TRY(ctx, hipcub::DeviceScan::ExclusiveSum(ctx->cub_temp, sb, F.mailbox,
+                                                          F.mb_index, int(m), ctx->stream));
+            hipLaunchKernelGGL(lanes_mailboxes, dim3(grid_for(m)), block, 0, ctx->stream, L);
+        } else {
+            HIP_TRY(ctx, hipMemsetAsync(F.mb_index, 0, uint64_t(m) * 4, ctx->stream));
+        }
         hipLaunchKernelGGL(lanes_segments, dim3(grid_for(uint64_t(pairs))), block, 0, ctx->stream,
                            ctx->T, L);
         rc = select_flagged(ctx, F.owner_head8, uint64_t(pairs), F.owner_starts, &F.lane_counts[0]);
@@ -515,7 +522,26 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
             hipLaunchKernelGGL(lanes_owner_free, dim3(grid_for(2 * uint64_t(m))), block, 0, ctx->stream, ctx->T, L);
             hipLaunchKernelGGL(lanes_free, dim3(grid_for(m)), block, 0, ctx->stream, ctx->T, L);
         }
-        hipLaunchKernelGGL(lanes_replay, dim3(1), dim3(kLanesMax), 0, ctx->stream, ctx->T, c, L);
+        if (one_lane)
+            hipLaunchKernelGGL(lanes_replay, dim3(1), dim3(kLanesMax), 0, ctx->stream, ctx->T, c, L);
+        else {
+            const bool dbg = getenv("TBG_FLOW_DEBUG") != nullptr;
+            if (dbg) {
+                if (!ctx->flow_debug) HIP_TRY(ctx, hipMalloc(&ctx->flow_debug, 128));
+                HIP_TRY(ctx, hipMemsetAsync(ctx->flow_debug, 0, 128, ctx->stream));
+            }
+            hipLaunchKernelGGL(lanes_walk, dim3(kLanesMax / kWalkWaves), dim3(kWalkWaves * 64), 0,
+                               ctx->stream, ctx->T, c, L, F.mb_index,
+                               dbg ? ctx->flow_debug : nullptr);
+            if (dbg) {
+                unsigned long long d[8] = {};
+                (void)hipMemcpyAsync(d, ctx->flow_debug, 64, hipMemcpyDeviceToHost, ctx->stream);
+                (void)hipStreamSynchronize(ctx->stream);
+                fprintf(stderr, "walk: m=%u walks=%llu windows=%llu events=%llu polls=%llu "
+                        "poll_us=%.1f snapshot_hits=%llu longest_walk_us=%.1f\n", m, d[6], d[0],
+                        d[1], d[2], d[3] / 100.0, d[5], d[4] / 100.0);
+            }
+        }
         hipLaunchKernelGGL(lanes_finish, dim3(grid_for(m)), block, 0, ctx->stream, ctx->T, c, L);
         tmark(ctx, "tr_lanes");
         P.skip = &F.lane_counts[2];

@@ -397,6 +397,237 @@ __global__ void __launch_bounds__(kLanesMax) lanes_replay(Tables T, Call<tb_tran
     if (o == 0) T.scalars->stats[2] = L.m;
 }
 
+// The account walk on one wave per walked owner (the default; lanes_replay above is the one-lane
+// form, TBG_LANES_ONE_LANE). A wave loads 64 of its owner's (key, unit) pairs and their records
+// at a time, coalesced and one window ahead, and resolves the window's events in call order in a
+// wave-uniform loop: the owner's balances live in scalar registers, each event is a handful of
+// scalar instructions on values read out of the window's lanes. Verdicts between two owners go
+// through a u32 word per position in global memory (`mbox`, zeroed by the host): the deciding
+// owner publishes with an agent-scope atomic OR, the other owner reads it with an agent-scope
+// (sc1) load -- from a snapshot taken when the window's records were fetched, or, when the
+// verdict was not there yet, by polling (MI355X_MICROARCH.md: agent atomics on the producer side,
+// sc1 loads on the consumer side, no payload besides the word itself). Every owner waits only on
+// verdicts of earlier events, whose deciding owners have applied all their own earlier events:
+// the walks always progress. `progress` counts finished windows chip-wide; a poll that sees no
+// window finish anywhere for kFlowSpinLimit polls raises kFlagFlowStalled (a bug: the call fails).
+constexpr uint32_t kWalkWaves = 4;  // waves per workgroup (one owner each)
+
+struct WalkWindow {
+    uint32_t s;        // position (unit) of this lane's event
+    uint32_t amt_lo, amt_hi;
+    uint32_t bits;     // kWalk* flags relative to the walking owner
+    uint32_t mb;       // mailbox snapshot
+    bool valid;
+};
+enum : uint32_t {
+    kWalkDebit = 1,        // the owner is the event's debit account
+    kWalkMine = 2,         // the owner's limit is the one checked on its side
+    kWalkOther = 4,        // the other side's limit is checked: wait for its verdict
+    kWalkOtherOwner = 8,   // the owner decides and the other side is walked: publish the verdict
+    kWalkWriter = 16,      // this owner writes the outcome
+};
+
+__device__ inline uint64_t walk_u64(uint32_t lo, uint32_t hi) { return (uint64_t(hi) << 32) | lo; }
+__device__ inline uint32_t walk_uniform(uint32_t v) {
+    return uint32_t(__builtin_amdgcn_readfirstlane(int(v)));
+}
+__device__ inline uint64_t walk_uniform64(uint64_t v) {
+    return walk_u64(walk_uniform(uint32_t(v)), walk_uniform(uint32_t(v >> 32)));
+}
+__device__ inline u128 walk_uniform128(const tb_uint128_t& x) {
+    return (u128(walk_uniform64(x.hi)) << 64) | walk_uniform64(x.lo);
+}
+
+__global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_transfer_t> c,
+                                                               LanePlan L, uint32_t* mbox,
+                                                               unsigned long long* dbg) {
+    // dbg (TBG_FLOW_DEBUG): [0] windows, [1] events, [2] live polls, [3] poll cycles,
+    // [4] max walk cycles, [5] verdicts found in snapshots, [6] walks (100 MHz wall clock)
+    const uint64_t t_walk0 = wall_clock64();
+    uint64_t n_win = 0, n_ev = 0, n_poll = 0, t_poll = 0, n_snap = 0;
+    const uint32_t owners = L.counts[0];
+    const bool run = L.counts[1] == 0 && owners != 0 && owners <= kLanesMax;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && run) {
+        L.counts[2] = 1;
+        T.scalars->stats[2] = L.m;
+    }
+    if (!run) return;
+    const uint32_t lane = threadIdx.x & 63;
+    // Everything about the owner is wave-uniform: scalar registers and scalar branches.
+    const uint32_t o = walk_uniform(blockIdx.x * kWalkWaves + (threadIdx.x >> 6));
+    if (o >= owners) return;
+    const uint64_t start = walk_uniform64(L.owner_starts[o]);
+    const uint64_t my_key = walk_uniform64(L.keys_sorted[start]) >> kFlowUnitBits;
+    const uint32_t row = uint32_t(my_key & 0xFFFFFFFFu);
+    if (walk_uniform(L.acc_free[row]) == L.epoch) return;  // a free owner (lanes_free)
+    unsigned int* progress = &L.counts[3];
+
+    const tb_account_t& acc0 = T.acc_rows[row];
+    const u128 dpe = walk_uniform128(acc0.debits_pending);
+    const u128 cpe = walk_uniform128(acc0.credits_pending);
+    u128 dpo = walk_uniform128(acc0.debits_posted);
+    u128 cpo = walk_uniform128(acc0.credits_posted);
+
+    auto fetch_pairs = [&](uint64_t base, uint64_t* key) {
+        const uint64_t p = base + lane;
+        *key = p < L.n_pairs ? L.keys_sorted[p] : ~0ull;
+    };
+    auto fetch_recs = [&](uint64_t key, WalkWindow* w) {
+        w->valid = key != ~0ull && (key >> kFlowUnitBits) == my_key;
+        const uint32_t s = uint32_t(key & ((1u << kFlowUnitBits) - 1));
+        w->s = w->valid && s < L.m ? s : 0u;
+        const LaneRec r = L.recs[w->s];
+        const bool debit = r.dr == row;
+        const bool dec_dr = (r.bits & kLaneDrDecides) != 0, dec_cr = (r.bits & kLaneCrDecides) != 0;
+        const bool mine = debit ? dec_dr : dec_cr;
+        const bool other = debit ? dec_cr : dec_dr;
+        const bool other_owner = (r.bits & (debit ? kLaneCrOwner : kLaneDrOwner)) != 0;
+        const bool writer = debit || !(r.bits & kLaneDrOwner);
+        w->bits = (debit ? kWalkDebit : 0u) | (mine ? kWalkMine : 0u) | (other ? kWalkOther : 0u) |
+                  (other_owner && mine ? kWalkOtherOwner : 0u) | (writer ? kWalkWriter : 0u);
+        w->amt_lo = uint32_t(r.amount);
+        w->amt_hi = uint32_t(r.amount >> 32);
+        w->mb = other && w->valid
+                    ? __hip_atomic_load(&mbox[w->s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                    : 0u;
+    };
+
+    uint64_t base = start;
+    uint64_t key_cur, key_next;
+    fetch_pairs(base, &key_cur);
+    WalkWindow cur;
+    fetch_recs(key_cur, &cur);
+    fetch_pairs(base + 64, &key_next);
+    uint64_t spins = 0;
+    unsigned int seen = 0;
+    bool stalled = false;
+    while (true) {
+        // The window as scalar masks (one bit per event, in call order).
+        const uint64_t vmask = __ballot(cur.valid);
+        if (vmask == 0) break;
+        const uint64_t debit_m = __ballot(cur.valid && (cur.bits & kWalkDebit));
+        const uint64_t mine_m = __ballot(cur.valid && (cur.bits & kWalkMine));
+        const uint64_t other_m = __ballot(cur.valid && (cur.bits & kWalkOther));
+        const uint64_t pub_m = __ballot(cur.valid && (cur.bits & kWalkOtherOwner));
+        const bool my_debit = (cur.bits & kWalkDebit) != 0;
+        const uint64_t snap_set =
+            __ballot((cur.mb & (my_debit ? kMbCrSet : kMbDrSet)) != 0);
+        const uint64_t snap_ok = __ballot((cur.mb & (my_debit ? kMbCrOk : kMbDrOk)) != 0);
+        const bool more = (vmask >> 63) & 1;  // the segment continues past this window
+        // Prefetch: the next window's records and snapshot, the pairs after it.
+        WalkWindow nxt;
+        nxt.valid = false;
+        uint64_t key_after = ~0ull;
+        if (more) {
+            fetch_recs(key_next, &nxt);
+            fetch_pairs(base + 128, &key_after);
+        }
+        const uint32_t cnt = uint32_t(__popcll(vmask));
+        uint64_t created_m = 0, drfail_m = 0, myok_m = 0, published = 0;
+        // Verdicts this owner owes are published with one vector atomic per flush: before any
+        // poll (an owner it waits on may wait on them) and at the window's end.
+        uint64_t decided = 0;  // events this owner has decided (mine) so far in the window
+        auto publish = [&]() {
+            const uint64_t due = pub_m & decided & ~published;
+            if (due == 0) return;
+            if ((due >> lane) & 1) {
+                const bool ok = (myok_m >> lane) & 1;
+                const uint32_t v = my_debit ? (kMbDrSet | (ok ? kMbDrOk : 0u))
+                                            : (kMbCrSet | (ok ? kMbCrOk : 0u));
+                atomicOr(&mbox[cur.s], v);
+            }
+            published |= due;
+        };
+        for (uint32_t j = 0; j < cnt; j++) {
+            const uint64_t bit = 1ull << j;
+            const u128 amt = walk_u64(__builtin_amdgcn_readlane(cur.amt_lo, j),
+                                      __builtin_amdgcn_readlane(cur.amt_hi, j));
+            const bool debit = (debit_m & bit) != 0;
+            bool my_ok = true;
+            if (mine_m & bit) {
+                my_ok = debit ? !(dpe + dpo + amt > cpo) : !(cpe + cpo + amt > dpo);
+                decided |= bit;
+                if (my_ok) myok_m |= bit;
+            }
+            bool other_ok = true;
+            if (other_m & bit) {
+                uint32_t mb = 0;
+                if (snap_set & bit) {
+                    other_ok = (snap_ok & bit) != 0;
+                    n_snap++;
+                } else {
+                    const uint64_t tp0 = dbg ? wall_clock64() : 0;
+                    n_poll++;
+                    publish();  // (an owner this one waits on may wait on these)
+                    const uint32_t sj = __builtin_amdgcn_readlane(cur.s, j);
+                    const uint32_t need = debit ? kMbCrSet : kMbDrSet;
+                    while (!stalled) {
+                        mb = walk_uniform(__hip_atomic_load(&mbox[sj], __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_AGENT));
+                        if (mb & need) break;
+                        __builtin_amdgcn_s_sleep(1);
+                        if ((++spins & 255) == 0) {
+                            const unsigned int p = walk_uniform(__hip_atomic_load(
+                                progress, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                            if (p != seen) {
+                                seen = p;
+                                spins = 0;
+                            } else if (spins > kFlowSpinLimit) {
+                                stalled = true;
+                            }
+                        }
+                    }
+                    other_ok = (mb & (debit ? kMbCrOk : kMbDrOk)) != 0;
+                    if (dbg) t_poll += wall_clock64() - tp0;
+                }
+            }
+            const bool dr_fail = debit ? !my_ok : !other_ok;
+            const bool cr_fail = debit ? !other_ok : !my_ok;
+            if (!dr_fail && !cr_fail) {
+                created_m |= bit;
+                if (debit) dpo += amt;
+                else cpo += amt;
+            } else if (dr_fail) {
+                drfail_m |= bit;
+            }
+        }
+        publish();
+        if (stalled) {
+            if (lane == 0) atomicOr(&T.scalars->flags, kFlagFlowStalled);
+            return;
+        }
+        if (cur.valid && (cur.bits & kWalkWriter)) {
+            const uint8_t out = ((created_m >> lane) & 1) ? kOutCreated
+                                : ((drfail_m >> lane) & 1) ? kOutExceedsCredits
+                                                           : kOutExceedsDebits;
+            L.outcome[cur.s] = out;
+        }
+        if (lane == 0) atomicAdd(progress, 1u);
+        n_win++;
+        n_ev += cnt;
+        if (!more) break;
+        base += 64;
+        cur = nxt;
+        key_next = key_after;
+    }
+    if (lane == 0) {
+        tb_account_t& acc = T.acc_rows[row];
+        acc.debits_posted = W(dpo);
+        acc.credits_posted = W(cpo);
+        const uint16_t h = acc_hazard_of(acc);
+        if (h) acc_hazard_set(T.acc_index, T.acc_entry_of, row, h);
+        if (dbg) {
+            atomicAdd(&dbg[0], n_win);
+            atomicAdd(&dbg[1], n_ev);
+            atomicAdd(&dbg[2], n_poll);
+            atomicAdd(&dbg[3], t_poll);
+            atomicMax(&dbg[4], wall_clock64() - t_walk0);
+            atomicAdd(&dbg[5], n_snap);
+            atomicAdd(&dbg[6], 1ull);
+        }
+    }
+}
+
 // After the lanes, one lane per event: the result (timestamp, verdict), the sides of created
 // events that no lane owns (u128 atomics: their balances are never read in the call), and the
 // transfers key_max.
