@@ -538,58 +538,84 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
             }
             published |= due;
         };
-        for (uint32_t j = 0; j < cnt; j++) {
-            const uint64_t bit = 1ull << j;
-            const u128 amt = walk_u64(__builtin_amdgcn_readlane(cur.amt_lo, j),
-                                      __builtin_amdgcn_readlane(cur.amt_hi, j));
-            const bool debit = (debit_m & bit) != 0;
-            bool my_ok = true;
-            if (mine_m & bit) {
-                my_ok = debit ? !(dpe + dpo + amt > cpo) : !(cpe + cpo + amt > dpo);
-                decided |= bit;
-                if (my_ok) myok_m |= bit;
-            }
-            bool other_ok = true;
-            if (other_m & bit) {
-                uint32_t mb = 0;
-                if (snap_set & bit) {
-                    other_ok = (snap_ok & bit) != 0;
-                    n_snap++;
-                } else {
-                    const uint64_t tp0 = dbg ? wall_clock64() : 0;
-                    n_poll++;
-                    publish();  // (an owner this one waits on may wait on these)
-                    const uint32_t sj = __builtin_amdgcn_readlane(cur.s, j);
-                    const uint32_t need = debit ? kMbCrSet : kMbDrSet;
-                    while (!stalled) {
-                        mb = walk_uniform(__hip_atomic_load(&mbox[sj], __ATOMIC_RELAXED,
-                                                            __HIP_MEMORY_SCOPE_AGENT));
-                        if (mb & need) break;
-                        __builtin_amdgcn_s_sleep(1);
-                        if ((++spins & 255) == 0) {
-                            const unsigned int p = walk_uniform(__hip_atomic_load(
-                                progress, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-                            if (p != seen) {
-                                seen = p;
-                                spins = 0;
-                            } else if (spins > kFlowSpinLimit) {
-                                stalled = true;
+        // The events in call order. When the owner's balances are < 2^62 and the window's amounts
+        // < 2^56 (no sum below can wrap 64 bits), the checks run on u64 (Balances64), else on u128;
+        // amounts are read with one readlane when the window's fit in 32 bits.
+        const bool amt32 = __ballot(cur.valid && cur.amt_hi != 0) == 0;
+        const bool narrow = __ballot(cur.valid && cur.amt_hi >= (1u << 24)) == 0 &&
+                            (dpe >> 62) == 0 && (dpo >> 62) == 0 && (cpe >> 62) == 0 &&
+                            (cpo >> 62) == 0;
+        auto walk_events = [&](auto dpe_v, auto& dpo_v, auto cpe_v, auto& cpo_v) {
+            using V = decltype(dpe_v);
+            for (uint32_t j = 0; j < cnt; j++) {
+                const uint64_t bit = 1ull << j;
+                const uint32_t lo = __builtin_amdgcn_readlane(cur.amt_lo, j);
+                const V amt = amt32 ? V(lo) : V(walk_u64(lo, __builtin_amdgcn_readlane(cur.amt_hi, j)));
+                const bool debit = (debit_m & bit) != 0;
+                bool my_ok = true;
+                if (mine_m & bit) {
+                    my_ok = debit ? !(dpe_v + dpo_v + amt > cpo_v) : !(cpe_v + cpo_v + amt > dpo_v);
+                    decided |= bit;
+                    if (my_ok) myok_m |= bit;
+                    if (pub_m & bit) {  // an owner may be waiting on this verdict: publish now
+                        if (lane == j) {
+                            const uint32_t v = debit ? (kMbDrSet | (my_ok ? kMbDrOk : 0u))
+                                                     : (kMbCrSet | (my_ok ? kMbCrOk : 0u));
+                            atomicOr(&mbox[cur.s], v);
+                        }
+                        published |= bit;
+                    }
+                }
+                bool other_ok = true;
+                if (other_m & bit) {
+                    uint32_t mb = 0;
+                    if (snap_set & bit) {
+                        other_ok = (snap_ok & bit) != 0;
+                        n_snap++;
+                    } else {
+                        const uint64_t tp0 = dbg ? wall_clock64() : 0;
+                        n_poll++;
+                        publish();  // (an owner this one waits on may wait on these)
+                        const uint32_t sj = __builtin_amdgcn_readlane(cur.s, j);
+                        const uint32_t need = debit ? kMbCrSet : kMbDrSet;
+                        while (!stalled) {
+                            mb = walk_uniform(__hip_atomic_load(&mbox[sj], __ATOMIC_RELAXED,
+                                                                __HIP_MEMORY_SCOPE_AGENT));
+                            if (mb & need) break;
+                            __builtin_amdgcn_s_sleep(1);
+                            if ((++spins & 255) == 0) {
+                                const unsigned int p = walk_uniform(__hip_atomic_load(
+                                    progress, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                                if (p != seen) {
+                                    seen = p;
+                                    spins = 0;
+                                } else if (spins > kFlowSpinLimit) {
+                                    stalled = true;
+                                }
                             }
                         }
+                        other_ok = (mb & (debit ? kMbCrOk : kMbDrOk)) != 0;
+                        if (dbg) t_poll += wall_clock64() - tp0;
                     }
-                    other_ok = (mb & (debit ? kMbCrOk : kMbDrOk)) != 0;
-                    if (dbg) t_poll += wall_clock64() - tp0;
+                }
+                const bool dr_fail = debit ? !my_ok : !other_ok;
+                const bool cr_fail = debit ? !other_ok : !my_ok;
+                if (!dr_fail && !cr_fail) {
+                    created_m |= bit;
+                    if (debit) dpo_v += amt;
+                    else cpo_v += amt;
+                } else if (dr_fail) {
+                    drfail_m |= bit;
                 }
             }
-            const bool dr_fail = debit ? !my_ok : !other_ok;
-            const bool cr_fail = debit ? !other_ok : !my_ok;
-            if (!dr_fail && !cr_fail) {
-                created_m |= bit;
-                if (debit) dpo += amt;
-                else cpo += amt;
-            } else if (dr_fail) {
-                drfail_m |= bit;
-            }
+        };
+        if (narrow) {
+            uint64_t dpo64 = uint64_t(dpo), cpo64 = uint64_t(cpo);
+            walk_events(uint64_t(dpe), dpo64, uint64_t(cpe), cpo64);
+            dpo = dpo64;
+            cpo = cpo64;
+        } else {
+            walk_events(dpe, dpo, cpe, cpo);
         }
         publish();
         if (stalled) {
