@@ -25,6 +25,26 @@
 #include "device_common.hpp"
 #include "replay.hpp"
 
+// tr_ingest build knobs (same-box A/B builds: csrc/Makefile `variant`).
+#ifndef TBG_INGEST_EARLY_PREFETCH
+#define TBG_INGEST_EARLY_PREFETCH 0
+#endif
+#ifndef TBG_INGEST_NT
+#define TBG_INGEST_NT 1       // rows: non-temporal stores (written once, never re-read here)
+#endif
+#ifndef TBG_INGEST_NT_RESULTS
+#define TBG_INGEST_NT_RESULTS 1  // results: non-temporal (the host reads them after the call)
+#endif
+#ifndef TBG_INGEST_NT_LOADS
+#define TBG_INGEST_NT_LOADS 1    // events: non-temporal loads (read once)
+#endif
+#ifndef TBG_INGEST_WG_PER_CU
+#define TBG_INGEST_WG_PER_CU 4
+#endif
+#ifndef TBG_INGEST_JOINT_PROBE
+#define TBG_INGEST_JOINT_PROBE 1
+#endif
+
 namespace tbg {
 
 constexpr int kBlock = 256;
@@ -140,6 +160,40 @@ __device__ inline AccSnap acc_lookup_snap(const Tables& T, const tb_uint128_t& i
     return a;
 }
 
+// The same lookup split in two: issue both candidate entries' loads (unconditionally, entry 0 for
+// an id that is not looked up), then match. Ingest issues the id claim's CAS and both accounts'
+// four loads back to back, so the common event pays one memory round trip, not three.
+struct AccProbe {
+    uint4 v1, v2;
+};
+__device__ inline AccProbe acc_probe_issue(const AccIndex& x, const tb_uint128_t& id, bool valid) {
+    const uint64_t s1 = valid ? acc_entry_h1(id) & x.mask : 0;
+    const uint64_t s2 = valid ? acc_entry_h2(id) & x.mask : 0;
+    AccProbe p;
+    p.v1 = *reinterpret_cast<const uint4*>(&x.entries[s1]);
+    p.v2 = *reinterpret_cast<const uint4*>(&x.entries[s2]);
+    return p;
+}
+__device__ inline AccSnap acc_probe_snap(const Tables& T, const AccProbe& p, const tb_uint128_t& id,
+                                         bool valid, bool debit) {
+    AccSnap a;
+    a.row = kNone32;
+    a.ledger = 0;
+    a.flags = 0;
+    a.hi_pending = a.hi_posted = 0;
+    if (!valid) return a;
+    uint4 v;
+    if (acc_entry_match(p.v1, T.acc_rows, id)) v = p.v1;
+    else if (acc_entry_match(p.v2, T.acc_rows, id)) v = p.v2;
+    else return a;
+    const uint32_t row = v.z - 1;
+    if (meta_hazard(v.w)) return acc_snap_load(&T.acc_rows[row], row, debit);
+    a.row = row;
+    a.ledger = meta_ledger(v.w);
+    a.flags = meta_flags(v.w);
+    return a;
+}
+
 // The checks after the id lookup (create_transfer, :3727-3873), on the ingest snapshot. `w` is
 // the word of the id's slot as this event observed it.
 __device__ inline uint8_t classify_after_lookup(const Tables& T, const Call<tb_transfer_t>& c,
@@ -235,6 +289,16 @@ __device__ inline bool item_packable(const Call<tb_transfer_t>& c, uint64_t amou
                         : (amount >> (64 - c.key_bits)) == 0;
 }
 
+__device__ inline void ingest_store_result(tb_create_result_t* p, const tb_create_result_t& r) {
+#if TBG_INGEST_NT_RESULTS
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    const v4u v = {uint32_t(r.timestamp), uint32_t(r.timestamp >> 32), r.status, r.reserved};
+    __builtin_nontemporal_store(v, reinterpret_cast<v4u*>(p));
+#else
+    *p = r;
+#endif
+}
+
 // One event of tr_ingest, `t` being the event as staged in LDS; returns the call flags it raises
 // (kFlag*). The row store is done by the caller (the whole wave's rows at once, coalesced).
 //
@@ -289,12 +353,23 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
         const uint64_t s_id = hash_id(id) & T.tr.mask;
         // The claim: a CAS at the home slot; only a taken home slot continues the probe.
         uint64_t w_slot = tref;
+        const tb_uint128_t dr_id = t.debit_account_id, cr_id = t.credit_account_id;
+        const bool vd = !u128_is_zero(dr_id) && !u128_is_max(dr_id);
+        const bool vc = !u128_is_zero(cr_id) && !u128_is_max(cr_id);
+        uint64_t w_seen = kEmpty;
+        if (valid_id)
+            w_seen = atomicCAS(&T.tr.slots[s_id], (unsigned long long)kEmpty,
+                               (unsigned long long)tref);
+#if TBG_INGEST_JOINT_PROBE
+        const AccProbe pd = acc_probe_issue(T.acc_index, dr_id, vd);
+        const AccProbe pc = acc_probe_issue(T.acc_index, cr_id, vc);
+        dr = acc_probe_snap(T, pd, dr_id, vd, true);
+        cr = acc_probe_snap(T, pc, cr_id, vc, false);
+#else
+        dr = acc_lookup_snap(T, dr_id, vd, true);
+        cr = acc_lookup_snap(T, cr_id, vc, false);
+#endif
         if (valid_id) {
-            const uint64_t w_seen = atomicCAS(&T.tr.slots[s_id], (unsigned long long)kEmpty,
-                                              (unsigned long long)tref);
-            const tb_uint128_t dr_id = t.debit_account_id, cr_id = t.credit_account_id;
-            dr = acc_lookup_snap(T, dr_id, !u128_is_zero(dr_id) && !u128_is_max(dr_id), true);
-            cr = acc_lookup_snap(T, cr_id, !u128_is_zero(cr_id) && !u128_is_max(cr_id), false);
             if (w_seen == kEmpty) {
                 slot = s_id;  // claimed
             } else {
@@ -305,10 +380,6 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
             }
             if (slot == kNone) atomicOr(&T.scalars->flags, kFlagTableFull);
             else info |= kInfoClaimed;
-        } else {
-            const tb_uint128_t dr_id = t.debit_account_id, cr_id = t.credit_account_id;
-            dr = acc_lookup_snap(T, dr_id, !u128_is_zero(dr_id) && !u128_is_max(dr_id), true);
-            cr = acc_lookup_snap(T, cr_id, !u128_is_zero(cr_id) && !u128_is_max(cr_id), false);
         }
         // Accounts whose `closed` flag an event of this call may change.
         if ((f & TB_TRANSFER_CLOSING_DEBIT) && dr.row != kNone32) {
@@ -375,7 +446,7 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
         res.timestamp = ts_event;
         res.status = TB_STATUS_CREATED;
         res.reserved = 0;
-        c.results[k] = res;
+        ingest_store_result(&c.results[k], res);
         if (pending && t.timeout > 0) need_commit = true;  // expires_at index
         if (c.bal_items && c.pair_shift) {
             const uint32_t ps = c.pair_shift;
@@ -478,7 +549,8 @@ __device__ inline void wave_lds_sync() {
 // event's fields, and go back out as the transfer rows (timestamp patched) with 8 coalesced
 // stores. The next chunk's loads are issued before the current chunk's table work, so the event
 // stream overlaps the claim / index round trip.
-__global__ void __launch_bounds__(kBlock, 4) tr_ingest(Tables T, Call<tb_transfer_t> c) {
+__global__ void __launch_bounds__(kBlock, TBG_INGEST_WG_PER_CU) tr_ingest(Tables T,
+                                                                         Call<tb_transfer_t> c) {
     __shared__ __attribute__((aligned(16))) uint8_t lds_ev[kIngestWaves][64 * kLdsEventStride];
     __shared__ uint64_t lds_ts[kIngestWaves][64];
     __shared__ unsigned int bucket_hist[kBucketsMax];
@@ -498,7 +570,17 @@ __global__ void __launch_bounds__(kBlock, 4) tr_ingest(Tables T, Call<tb_transfe
 #pragma unroll
         for (int i = 0; i < 8; i++) {
             const uint32_t idx = i * 64 + lane;
+#if TBG_INGEST_NT_LOADS
+            typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+            if (idx < parts) {
+                const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(&src[idx]));
+                q[i] = make_uint4(v.x, v.y, v.z, v.w);
+            } else {
+                q[i] = make_uint4(0, 0, 0, 0);
+            }
+#else
             q[i] = idx < parts ? src[idx] : make_uint4(0, 0, 0, 0);
+#endif
         }
     };
     uint32_t base = (blockIdx.x * kIngestWaves + wv) * 64;
@@ -537,6 +619,16 @@ __global__ void __launch_bounds__(kBlock, 4) tr_ingest(Tables T, Call<tb_transfe
             batch_imported = (c.events[bstart].flags & TB_TRANSFER_IMPORTED) != 0;
             first_of_batch = k == bstart;
         }
+        // ts_event (and the batch facts) may come from loads: wait for them here, before the
+        // row stores and the prefetch are issued -- a wait at their first use further down would
+        // have to drain the prefetch too (vmcnt counts in order). The asm redefines the registers,
+        // so the compiler places no later wait for them.
+        {
+            uint32_t fb = first_of_batch, bi = batch_imported;
+            asm volatile("s_waitcnt vmcnt(0)" : "+v"(ts_event), "+v"(fb), "+v"(bi));
+            first_of_batch = fb != 0;
+            batch_imported = bi != 0;
+        }
         if (straddle) {
             lds_ts[wv][lane] = active ? ts_event : 0;
             wave_lds_sync();
@@ -556,8 +648,23 @@ __global__ void __launch_bounds__(kBlock, 4) tr_ingest(Tables T, Call<tb_transfe
                 q[i].z = uint32_t(ts);
                 q[i].w = uint32_t(ts >> 32);
             }
-            if (full || i * 64 + lane < cnt * 8) dst[i * 64 + lane] = q[i];
+            if (full || i * 64 + lane < cnt * 8) {
+#if TBG_INGEST_NT
+                typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+                const v4u v = {q[i].x, q[i].y, q[i].z, q[i].w};
+                __builtin_nontemporal_store(v, reinterpret_cast<v4u*>(&dst[i * 64 + lane]));
+#else
+                dst[i * 64 + lane] = q[i];
+#endif
+            }
         }
+        const uint32_t next = base + nw * 64;
+#if TBG_INGEST_EARLY_PREFETCH
+        // The next chunk's loads overlap this chunk's claim and index round trips. (Issued
+        // unconditionally -- past the end the current chunk is reloaded and dropped -- so the
+        // compiler's wait counts stay exact and the claim does not wait for the prefetch.)
+        load_chunk(next < c.n ? next : ubase);
+#endif
         if (active) {
             const tb_transfer_t& t = *reinterpret_cast<const tb_transfer_t*>(my + lane * kLdsEventStride);
             const bool prev_linked =
@@ -571,8 +678,9 @@ __global__ void __launch_bounds__(kBlock, 4) tr_ingest(Tables T, Call<tb_transfe
             n_fast += fts != 0;
             ts_max = fts > ts_max ? fts : ts_max;
         }
-        const uint32_t next = base + nw * 64;
+#if !TBG_INGEST_EARLY_PREFETCH
         if (next < c.n) load_chunk(next);
+#endif
         wave_lds_sync();  // the LDS image is rewritten by the next chunk
     }
     flags = block_reduce(flags, OpOr());  // (its barriers also order the histogram adds)

@@ -154,7 +154,8 @@ def load(path: str = None):
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = path or LIB_PATH
+    # (TBG_LIB: an alternative build of the same library, for same-box A/B measurements)
+    p = path or os.environ.get("TBG_LIB") or LIB_PATH
     if not os.path.exists(p):
         raise OSError(f"libtbg.so not built: {p} (run __graft_entry__.build())")
     lib = ctypes.CDLL(p)
