@@ -3,8 +3,9 @@
  *
  * Mirrors `StateMachineType(Storage)` (src/state_machine.zig:222-2958) as consumed by
  * `ReplicaType(StateMachine, ...)` (src/vsr/replica.zig:144-152) for the operations of this path:
- * pulse, create_accounts, create_transfers, lookup_accounts, lookup_transfers and
- * get_change_events (the account_events groove's reader, CDC). Bodies are
+ * pulse, create_accounts, create_transfers, lookup_accounts, lookup_transfers,
+ * get_change_events (the account_events groove's reader, CDC) and the scans over the same tables:
+ * get_account_transfers, get_account_balances, query_accounts, query_transfers. Bodies are
  * multi-batch encoded exactly as src/vsr/multi_batch.zig; replies are multi-batch encoded the
  * same way. The executor underneath is pluggable (tb_executor): the product binds the HIP
  * executor (tbg.h) with tb_sm_open_gpu; tests may bind another executor with the same semantics.
@@ -38,6 +39,10 @@ enum {
     TB_OPERATION_GET_CHANGE_EVENTS = 137,
     TB_OPERATION_LOOKUP_ACCOUNTS = 140,
     TB_OPERATION_LOOKUP_TRANSFERS = 141,
+    TB_OPERATION_GET_ACCOUNT_TRANSFERS = 142,
+    TB_OPERATION_GET_ACCOUNT_BALANCES = 143,
+    TB_OPERATION_QUERY_ACCOUNTS = 144,
+    TB_OPERATION_QUERY_TRANSFERS = 145,
     TB_OPERATION_CREATE_ACCOUNTS = 146,
     TB_OPERATION_CREATE_TRANSFERS = 147,
 };
@@ -59,6 +64,15 @@ typedef struct tb_executor {
     /* ChangeEvents of the filter, at most min(filter->limit, limit_max); 0 if invalid. */
     int64_t (*get_change_events)(void* self, const tb_change_events_filter_t* filter,
                                  uint32_t limit_max, tb_change_event_t* out);
+    /* The scans of one filter, at most min(filter->limit, limit_max) results; 0 if invalid. */
+    int64_t (*get_account_transfers)(void* self, const tb_account_filter_t* filter,
+                                     uint32_t limit_max, tb_transfer_t* out);
+    int64_t (*get_account_balances)(void* self, const tb_account_filter_t* filter,
+                                    uint32_t limit_max, tb_account_balance_t* out);
+    int64_t (*query_accounts)(void* self, const tb_query_filter_t* filter, uint32_t limit_max,
+                              tb_account_t* out);
+    int64_t (*query_transfers)(void* self, const tb_query_filter_t* filter, uint32_t limit_max,
+                               tb_transfer_t* out);
 } tb_executor;
 
 typedef struct tb_sm tb_sm;

@@ -154,6 +154,58 @@ typedef struct tb_change_events_filter {
     uint8_t reserved[44];
 } tb_change_events_filter_t;
 
+/* AccountFilter, src/tigerbeetle.zig:563-611 -- 128 bytes: get_account_transfers and
+ * get_account_balances. Zero fields do not filter. */
+typedef struct tb_account_filter {
+    tb_uint128_t account_id;
+    tb_uint128_t user_data_128;
+    uint64_t user_data_64;
+    uint32_t user_data_32;
+    uint16_t code;
+    uint8_t reserved[58];
+    uint64_t timestamp_min; /* inclusive; 0: timestamp_min */
+    uint64_t timestamp_max; /* inclusive; 0: timestamp_max */
+    uint32_t limit;
+    uint32_t flags;         /* TB_ACCOUNT_FILTER_* */
+} tb_account_filter_t;
+
+enum {
+    TB_ACCOUNT_FILTER_DEBITS = 1u << 0,
+    TB_ACCOUNT_FILTER_CREDITS = 1u << 1,
+    TB_ACCOUNT_FILTER_REVERSED = 1u << 2,
+    TB_ACCOUNT_FILTER_PADDING_MASK = ~7u,
+};
+
+/* QueryFilter, src/tigerbeetle.zig:517-561 -- 64 bytes: query_accounts and query_transfers. */
+typedef struct tb_query_filter {
+    tb_uint128_t user_data_128;
+    uint64_t user_data_64;
+    uint32_t user_data_32;
+    uint32_t ledger;
+    uint16_t code;
+    uint8_t reserved[6];
+    uint64_t timestamp_min;
+    uint64_t timestamp_max;
+    uint32_t limit;
+    uint32_t flags;         /* TB_QUERY_FILTER_REVERSED */
+} tb_query_filter_t;
+
+enum {
+    TB_QUERY_FILTER_REVERSED = 1u << 0,
+    TB_QUERY_FILTER_PADDING_MASK = ~1u,
+};
+
+/* AccountBalance, src/tigerbeetle.zig:70-84 -- 128 bytes: an account's balances as they stood
+ * after one of its transfers (get_account_balances). */
+typedef struct tb_account_balance {
+    tb_uint128_t debits_pending;
+    tb_uint128_t debits_posted;
+    tb_uint128_t credits_pending;
+    tb_uint128_t credits_posted;
+    uint64_t timestamp;
+    uint8_t reserved[56];
+} tb_account_balance_t;
+
 /* AccountFlags, src/tigerbeetle.zig:45-68 (packed struct(u16), LSB first). */
 enum {
     TB_ACCOUNT_LINKED = 1u << 0,
@@ -340,10 +392,20 @@ static_assert(offsetof(tb_change_event_t, debit_account_id) == 128, "ChangeEvent
 static_assert(offsetof(tb_change_event_t, credit_account_id) == 240, "ChangeEvent layout");
 static_assert(offsetof(tb_change_event_t, timestamp) == 352, "ChangeEvent layout");
 static_assert(sizeof(tb_change_events_filter_t) == 64, "ChangeEventsFilter must be 64 bytes");
+static_assert(sizeof(tb_account_filter_t) == 128, "AccountFilter must be 128 bytes");
+static_assert(offsetof(tb_account_filter_t, timestamp_min) == 104, "AccountFilter layout");
+static_assert(sizeof(tb_query_filter_t) == 64, "QueryFilter must be 64 bytes");
+static_assert(offsetof(tb_query_filter_t, timestamp_min) == 40, "QueryFilter layout");
+static_assert(sizeof(tb_account_balance_t) == 128, "AccountBalance must be 128 bytes");
 #else
 _Static_assert(sizeof(tb_account_event_t) == 256, "AccountEvent must be 256 bytes");
 _Static_assert(sizeof(tb_change_event_t) == 384, "ChangeEvent must be 384 bytes");
 _Static_assert(sizeof(tb_change_events_filter_t) == 64, "ChangeEventsFilter must be 64 bytes");
+_Static_assert(sizeof(tb_account_filter_t) == 128, "AccountFilter must be 128 bytes");
+_Static_assert(offsetof(tb_account_filter_t, timestamp_min) == 104, "AccountFilter layout");
+_Static_assert(sizeof(tb_query_filter_t) == 64, "QueryFilter must be 64 bytes");
+_Static_assert(offsetof(tb_query_filter_t, timestamp_min) == 40, "QueryFilter layout");
+_Static_assert(sizeof(tb_account_balance_t) == 128, "AccountBalance must be 128 bytes");
 _Static_assert(sizeof(tb_account_t) == 128, "Account must be 128 bytes");
 _Static_assert(sizeof(tb_transfer_t) == 128, "Transfer must be 128 bytes");
 _Static_assert(sizeof(tb_create_result_t) == 16, "Create*Result must be 16 bytes");

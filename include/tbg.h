@@ -17,6 +17,8 @@
  *   tbg_lookup_transfers  <- execute_lookup_transfers           :3274-3292
  *   tbg_get_change_events <- execute_get_change_events          :3395-3527 (the account_events
  *                            groove written by account_event    :4384-4465)
+ *   tbg_get_account_transfers / _balances, tbg_query_accounts / _transfers <- the scans
+ *                            :1482-2123, :3294-3393 (below)
  * prefetch (:1146-1420) has no counterpart: every table is HBM-resident, nothing is staged.
  *
  * Batches: one call executes `n_batches` consecutive batches (a multi-batch body, or any sequence
@@ -146,6 +148,27 @@ int64_t tbg_get_change_events(tbg_ctx* ctx, const tb_change_events_filter_t* fil
 int64_t tbg_compact(tbg_ctx* ctx);
 int tbg_checkpoint(tbg_ctx* ctx, const char* path);
 tbg_ctx* tbg_open_checkpoint(const tbg_options* options, const char* path);
+
+/* The scans (state_machine.zig, prefetch_*_scan + execute_*): objects in timestamp order
+ * (descending with the filter's `reversed` flag) within [timestamp_min, timestamp_max], at most
+ * min(filter->limit, limit_max); 0 results for an invalid filter. Returns the count written.
+ *   tbg_get_account_transfers <- get_scan_from_account_filter :1737-1841 (the transfers whose
+ *                                debit and/or credit account is filter->account_id, AND the
+ *                                nonzero user_data_128/64/32 and code), execute :3294-3310
+ *   tbg_get_account_balances  <- prefetch_get_account_balances_scan :1608-1675 (the account must
+ *                                exist with flags.history; the same transfer scan, each mapped to
+ *                                its AccountEvent by timestamp), execute :3312-3357. Needs
+ *                                account_events_capacity > 0 (else TBG_EINVAL).
+ *   tbg_query_accounts        <- get_scan_from_query_filter :2054-2123 over the accounts groove
+ *   tbg_query_transfers       <- the same over the transfers groove (ledger, code, user data) */
+int64_t tbg_get_account_transfers(tbg_ctx* ctx, const tb_account_filter_t* filter,
+                                  uint32_t limit_max, tb_transfer_t* out);
+int64_t tbg_get_account_balances(tbg_ctx* ctx, const tb_account_filter_t* filter,
+                                 uint32_t limit_max, tb_account_balance_t* out);
+int64_t tbg_query_accounts(tbg_ctx* ctx, const tb_query_filter_t* filter, uint32_t limit_max,
+                           tb_account_t* out);
+int64_t tbg_query_transfers(tbg_ctx* ctx, const tb_query_filter_t* filter, uint32_t limit_max,
+                            tb_transfer_t* out);
 
 /* Test-harness `setup` action (src/state_machine_tests.zig:657-676). */
 int tbg_debug_set_account_balances(tbg_ctx* ctx, tb_uint128_t id, tb_uint128_t debits_pending,

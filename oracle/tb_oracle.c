@@ -1137,6 +1137,145 @@ int64_t tbo_get_change_events(const tbo_ctx* c, const tb_change_events_filter_t*
     return count;
 }
 
+/* ---- scans: get_account_transfers / get_account_balances / query_* ---------------------------
+ * get_scan_from_account_filter (state_machine.zig:1737-1841), get_scan_from_query_filter
+ * (:2054-2123), prefetch_get_account_balances_scan (:1608-1675), execute_* (:3294-3393). The
+ * grooves' index scans are restated as a walk over the objects in timestamp order (creation order:
+ * timestamps only grow, imported ones included), ascending or descending, keeping the objects every
+ * nonzero condition matches, up to the limit. */
+
+static int ts_in_range(uint64_t ts) { return ts >= TB_TIMESTAMP_MIN && ts <= TB_TIMESTAMP_MAX; }
+
+static int account_filter_valid(const tb_account_filter_t* f) {
+    int reserved_zero = 1;
+    for (int i = 0; i < 58; i++) reserved_zero &= f->reserved[i] == 0;
+    const u128 id = U(f->account_id);
+    return id != 0 && id != U128_MAX && (f->timestamp_min == 0 || ts_in_range(f->timestamp_min)) &&
+           (f->timestamp_max == 0 || ts_in_range(f->timestamp_max)) &&
+           (f->timestamp_max == 0 || f->timestamp_min <= f->timestamp_max) && f->limit != 0 &&
+           (f->flags & (TB_ACCOUNT_FILTER_DEBITS | TB_ACCOUNT_FILTER_CREDITS)) &&
+           !(f->flags & TB_ACCOUNT_FILTER_PADDING_MASK) && reserved_zero;
+}
+
+static int query_filter_valid(const tb_query_filter_t* f) {
+    int reserved_zero = 1;
+    for (int i = 0; i < 6; i++) reserved_zero &= f->reserved[i] == 0;
+    return (f->timestamp_min == 0 || ts_in_range(f->timestamp_min)) &&
+           (f->timestamp_max == 0 || ts_in_range(f->timestamp_max)) &&
+           (f->timestamp_max == 0 || f->timestamp_min <= f->timestamp_max) && f->limit != 0 &&
+           !(f->flags & TB_QUERY_FILTER_PADDING_MASK) && reserved_zero;
+}
+
+static int account_filter_match(const tb_account_filter_t* f, const tb_transfer_t* t) {
+    const u128 id = U(f->account_id);
+    const int on_side = ((f->flags & TB_ACCOUNT_FILTER_DEBITS) && U(t->debit_account_id) == id) ||
+                        ((f->flags & TB_ACCOUNT_FILTER_CREDITS) && U(t->credit_account_id) == id);
+    const uint64_t lo = f->timestamp_min ? f->timestamp_min : TB_TIMESTAMP_MIN;
+    const uint64_t hi = f->timestamp_max ? f->timestamp_max : TB_TIMESTAMP_MAX;
+    return on_side && t->timestamp >= lo && t->timestamp <= hi &&
+           (U(f->user_data_128) == 0 || U(f->user_data_128) == U(t->user_data_128)) &&
+           (f->user_data_64 == 0 || f->user_data_64 == t->user_data_64) &&
+           (f->user_data_32 == 0 || f->user_data_32 == t->user_data_32) &&
+           (f->code == 0 || f->code == t->code);
+}
+
+#define QUERY_MATCH(f, o)                                                                        \
+    ((o)->timestamp >= ((f)->timestamp_min ? (f)->timestamp_min : TB_TIMESTAMP_MIN) &&           \
+     (o)->timestamp <= ((f)->timestamp_max ? (f)->timestamp_max : TB_TIMESTAMP_MAX) &&           \
+     (U((f)->user_data_128) == 0 || U((f)->user_data_128) == U((o)->user_data_128)) &&           \
+     ((f)->user_data_64 == 0 || (f)->user_data_64 == (o)->user_data_64) &&                       \
+     ((f)->user_data_32 == 0 || (f)->user_data_32 == (o)->user_data_32) &&                       \
+     ((f)->ledger == 0 || (f)->ledger == (o)->ledger) && ((f)->code == 0 || (f)->code == (o)->code))
+
+/* The i-th object of the walk (ascending or descending). */
+static uint64_t walk_at(uint64_t n, uint64_t i, int reversed) { return reversed ? n - 1 - i : i; }
+
+int64_t tbo_get_account_transfers(const tbo_ctx* c, const tb_account_filter_t* filter,
+                                  uint32_t limit_max, tb_transfer_t* out) {
+    if (!account_filter_valid(filter)) return 0;
+    const uint32_t limit = filter->limit < limit_max ? filter->limit : limit_max;
+    const int rev = (filter->flags & TB_ACCOUNT_FILTER_REVERSED) != 0;
+    uint32_t count = 0;
+    for (uint64_t i = 0; i < c->n_transfers && count < limit; i++) {
+        const tb_transfer_t* t = &c->transfers[walk_at(c->n_transfers, i, rev)];
+        if (account_filter_match(filter, t)) out[count++] = *t;
+    }
+    return count;
+}
+
+int64_t tbo_get_account_balances(const tbo_ctx* c, const tb_account_filter_t* filter,
+                                 uint32_t limit_max, tb_account_balance_t* out) {
+    /* The account must exist and keep history (:1624-1626). */
+    const tb_account_t* a = get_account((tbo_ctx*)c, U(filter->account_id));
+    if (!a || !(a->flags & TB_ACCOUNT_HISTORY) || !account_filter_valid(filter)) return 0;
+    const uint32_t limit = filter->limit < limit_max ? filter->limit : limit_max;
+    const int rev = (filter->flags & TB_ACCOUNT_FILTER_REVERSED) != 0;
+    const u128 id = U(filter->account_id);
+    /* The groove keyed by timestamp (the log sorted, as get_change_events reads it). */
+    uint64_t* order = (uint64_t*)xrealloc(NULL, (c->n_events + 1) * sizeof(uint64_t));
+    for (uint64_t i = 0; i < c->n_events; i++) order[i] = i;
+    g_sort_ctx = c;
+    qsort(order, c->n_events, sizeof(uint64_t), event_index_cmp);
+    uint32_t count = 0;
+    for (uint64_t i = 0; i < c->n_transfers && count < limit; i++) {
+        const tb_transfer_t* t = &c->transfers[walk_at(c->n_transfers, i, rev)];
+        if (!account_filter_match(filter, t)) continue;
+        /* AccountBalancesScanLookup: the AccountEvent with the transfer's timestamp. */
+        uint64_t lo = 0, hi = c->n_events;
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) / 2;
+            if (c->events[order[mid]].timestamp < t->timestamp) lo = mid + 1;
+            else hi = mid;
+        }
+        if (lo == c->n_events || c->events[order[lo]].timestamp != t->timestamp) abort();
+        const tb_account_event_t* e = &c->events[order[lo]];
+        tb_account_balance_t* b = &out[count++];
+        memset(b, 0, sizeof(*b));
+        b->timestamp = e->timestamp;
+        if (U(e->dr_account_id) == id) {
+            b->debits_pending = e->dr_debits_pending;
+            b->debits_posted = e->dr_debits_posted;
+            b->credits_pending = e->dr_credits_pending;
+            b->credits_posted = e->dr_credits_posted;
+        } else if (U(e->cr_account_id) == id) {
+            b->debits_pending = e->cr_debits_pending;
+            b->debits_posted = e->cr_debits_posted;
+            b->credits_pending = e->cr_credits_pending;
+            b->credits_posted = e->cr_credits_posted;
+        } else {
+            abort();
+        }
+    }
+    free(order);
+    return count;
+}
+
+int64_t tbo_query_accounts(const tbo_ctx* c, const tb_query_filter_t* filter, uint32_t limit_max,
+                           tb_account_t* out) {
+    if (!query_filter_valid(filter)) return 0;
+    const uint32_t limit = filter->limit < limit_max ? filter->limit : limit_max;
+    const int rev = (filter->flags & TB_QUERY_FILTER_REVERSED) != 0;
+    uint32_t count = 0;
+    for (uint64_t i = 0; i < c->n_accounts && count < limit; i++) {
+        const tb_account_t* a = &c->accounts[walk_at(c->n_accounts, i, rev)];
+        if (QUERY_MATCH(filter, a)) out[count++] = *a;
+    }
+    return count;
+}
+
+int64_t tbo_query_transfers(const tbo_ctx* c, const tb_query_filter_t* filter,
+                            uint32_t limit_max, tb_transfer_t* out) {
+    if (!query_filter_valid(filter)) return 0;
+    const uint32_t limit = filter->limit < limit_max ? filter->limit : limit_max;
+    const int rev = (filter->flags & TB_QUERY_FILTER_REVERSED) != 0;
+    uint32_t count = 0;
+    for (uint64_t i = 0; i < c->n_transfers && count < limit; i++) {
+        const tb_transfer_t* t = &c->transfers[walk_at(c->n_transfers, i, rev)];
+        if (QUERY_MATCH(filter, t)) out[count++] = *t;
+    }
+    return count;
+}
+
 /* ---- executor binding (tb_state_machine.h) --------------------------------------------------*/
 
 static int ex_create_accounts(void* self, const tb_account_t* events, uint32_t n,
@@ -1174,6 +1313,23 @@ static int64_t ex_get_change_events(void* self, const tb_change_events_filter_t*
     return tbo_get_change_events((tbo_ctx*)self, filter, limit_max, out);
 }
 
+static int64_t ex_get_account_transfers(void* self, const tb_account_filter_t* f, uint32_t m,
+                                        tb_transfer_t* out) {
+    return tbo_get_account_transfers((tbo_ctx*)self, f, m, out);
+}
+static int64_t ex_get_account_balances(void* self, const tb_account_filter_t* f, uint32_t m,
+                                       tb_account_balance_t* out) {
+    return tbo_get_account_balances((tbo_ctx*)self, f, m, out);
+}
+static int64_t ex_query_accounts(void* self, const tb_query_filter_t* f, uint32_t m,
+                                 tb_account_t* out) {
+    return tbo_query_accounts((tbo_ctx*)self, f, m, out);
+}
+static int64_t ex_query_transfers(void* self, const tb_query_filter_t* f, uint32_t m,
+                                  tb_transfer_t* out) {
+    return tbo_query_transfers((tbo_ctx*)self, f, m, out);
+}
+
 void tbo_executor_fill(tbo_ctx* c, tb_executor* ex) {
     ex->self = c;
     ex->create_accounts = ex_create_accounts;
@@ -1183,4 +1339,8 @@ void tbo_executor_fill(tbo_ctx* c, tb_executor* ex) {
     ex->lookup_accounts = ex_lookup_accounts;
     ex->lookup_transfers = ex_lookup_transfers;
     ex->get_change_events = ex_get_change_events;
+    ex->get_account_transfers = ex_get_account_transfers;
+    ex->get_account_balances = ex_get_account_balances;
+    ex->query_accounts = ex_query_accounts;
+    ex->query_transfers = ex_query_transfers;
 }

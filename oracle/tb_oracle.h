@@ -80,6 +80,16 @@ uint64_t tbo_dump_account_events(const tbo_ctx* ctx, tb_account_event_t* out);
 int64_t tbo_get_change_events(const tbo_ctx* ctx, const tb_change_events_filter_t* filter,
                               uint32_t limit_max, tb_change_event_t* out);
 
+/* The scans (state_machine.zig:1482-2123, :3294-3393): see tbg.h. */
+int64_t tbo_get_account_transfers(const tbo_ctx* ctx, const tb_account_filter_t* filter,
+                                  uint32_t limit_max, tb_transfer_t* out);
+int64_t tbo_get_account_balances(const tbo_ctx* ctx, const tb_account_filter_t* filter,
+                                 uint32_t limit_max, tb_account_balance_t* out);
+int64_t tbo_query_accounts(const tbo_ctx* ctx, const tb_query_filter_t* filter,
+                           uint32_t limit_max, tb_account_t* out);
+int64_t tbo_query_transfers(const tbo_ctx* ctx, const tb_query_filter_t* filter,
+                            uint32_t limit_max, tb_transfer_t* out);
+
 /* Binds this oracle as a tb_executor (tb_state_machine.h) for the StateMachine mirror. */
 void tbo_executor_fill(tbo_ctx* ctx, tb_executor* ex);
 

@@ -32,6 +32,10 @@ _SIGS = [
     ("tbo_dump_account_events", ctypes.c_uint64, [vp, vp]),
     ("tbo_raise_key_max", None, [vp, ctypes.c_uint64, ctypes.c_uint64]),
     ("tbo_get_change_events", ctypes.c_int64, [vp, vp, ctypes.c_uint32, vp]),
+    ("tbo_get_account_transfers", ctypes.c_int64, [vp, vp, ctypes.c_uint32, vp]),
+    ("tbo_get_account_balances", ctypes.c_int64, [vp, vp, ctypes.c_uint32, vp]),
+    ("tbo_query_accounts", ctypes.c_int64, [vp, vp, ctypes.c_uint32, vp]),
+    ("tbo_query_transfers", ctypes.c_int64, [vp, vp, ctypes.c_uint32, vp]),
     ("tbo_executor_fill", None, [vp, ctypes.POINTER(native.Executor)]),
 ]
 

@@ -18,6 +18,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from tigerbeetle_amd import native  # noqa: E402
 from tigerbeetle_amd.types import (  # noqa: E402
     ACCOUNT_DTYPE, ACCOUNT_EVENT_DTYPE, CHANGE_EVENT_DTYPE, CHANGE_EVENTS_FILTER_DTYPE,
+    ACCOUNT_BALANCE_DTYPE, ACCOUNT_FILTER_DTYPE, QUERY_FILTER_DTYPE,
     RESULT_DTYPE, TRANSFER_DTYPE, TIMESTAMP_MAX, CreateAccountStatus, CreateTransferStatus)
 
 import oracle_binding  # noqa: E402
@@ -244,6 +245,35 @@ class Pair:
                                   f"first diff at {_first_diff(e_gpu, e_orc)}")
         return len(a_orc), len(t_orc)
 
+    def scan(self, kind, f, limit_max=8190):
+        """One scan on both sides (tbg_* vs tbo_*); they must agree byte for byte."""
+        dt = {"get_account_balances": ACCOUNT_BALANCE_DTYPE,
+              "query_accounts": ACCOUNT_DTYPE}.get(kind, TRANSFER_DTYPE)
+        g = np.zeros(limit_max, dtype=dt)
+        o = np.zeros(limit_max, dtype=dt)
+        ng = getattr(self.lib, "tbg_" + kind)(self.g, _ptr(f), limit_max, _ptr(g))
+        no = getattr(self.olib, "tbo_" + kind)(self.o, _ptr(f), limit_max, _ptr(o))
+        if ng != no or g[:max(ng, 0)].tobytes() != o[:no].tobytes():
+            raise ParityError(f"{kind} differs: gpu {ng}, oracle {no}, filter {f}; first diff at "
+                              f"{_first_diff(g[:max(ng, 0)], o[:no])}")
+        return no
+
+    def compare_scans(self, rng, n=40, limit_max=8190):
+        """`n` seeded filters over the current tables (random_scan_filters); returns the total
+        number of results compared."""
+        na = self.olib.tbo_account_count(self.o)
+        nt = self.olib.tbo_transfer_count(self.o)
+        a = np.zeros(na, dtype=ACCOUNT_DTYPE)
+        t = np.zeros(nt, dtype=TRANSFER_DTYPE)
+        self.olib.tbo_dump_accounts(self.o, _ptr(a))
+        self.olib.tbo_dump_transfers(self.o, _ptr(t))
+        total = 0
+        for kind, f in random_scan_filters(rng, a, t, n):
+            if kind == "get_account_balances" and not self.account_events:
+                continue
+            total += self.scan(kind, f, limit_max)
+        return total
+
     def change_events(self, timestamp_min=0, timestamp_max=0, limit=1 << 31, limit_max=8190):
         """get_change_events on both sides; they must agree byte for byte."""
         f = np.zeros(1, dtype=CHANGE_EVENTS_FILTER_DTYPE)
@@ -257,6 +287,61 @@ class Pair:
             raise ParityError(f"get_change_events differ: gpu {ng}, oracle {no}; first diff at "
                               f"{_first_diff(g[:ng], o[:no])}")
         return g[:ng]
+
+
+def _pick(rng, values, zero_p=0.5):
+    """0 (no condition) with probability zero_p, else one of `values` (or a random miss)."""
+    if len(values) == 0 or rng.random() < zero_p:
+        return 0
+    return int(values[rng.integers(0, len(values))]) if rng.random() < 0.9 else \
+        int(rng.integers(1, 1 << 30))
+
+
+def random_scan_filters(rng, accounts, transfers, n):
+    """Seeded AccountFilters and QueryFilters drawn from the objects that exist (so that most
+    conditions match something), with random timestamp ranges, limits, orders, and a few invalid
+    filters (zero limit, inverted range, no side, padding bits, reserved bytes)."""
+    ts = transfers["timestamp"] if len(transfers) else np.zeros(1, dtype=np.uint64)
+    ats = accounts["timestamp"] if len(accounts) else np.zeros(1, dtype=np.uint64)
+    out = []
+    for _ in range(n):
+        kind = rng.choice(["get_account_transfers", "get_account_balances", "query_accounts",
+                           "query_transfers"])
+        if kind.startswith("get_"):
+            f = np.zeros(1, dtype=ACCOUNT_FILTER_DTYPE)
+            src = accounts["id"][:, 0] if len(accounts) else np.zeros(1, dtype=np.uint64)
+            f["account_id"][0, 0] = src[rng.integers(0, len(src))] if rng.random() < 0.95 else 0
+            f["user_data_128"][0, 0] = _pick(rng, transfers["user_data_128"][:, 0], 0.8)
+            f["user_data_64"] = _pick(rng, transfers["user_data_64"], 0.85)
+            f["user_data_32"] = _pick(rng, transfers["user_data_32"], 0.85)
+            f["code"] = _pick(rng, transfers["code"], 0.8) & 0xFFFF
+            f["flags"] = int(rng.choice([1, 2, 3, 3, 5, 6, 7, 7, 0, 8]))
+            tsrc = ts
+        else:
+            f = np.zeros(1, dtype=QUERY_FILTER_DTYPE)
+            objs = accounts if kind == "query_accounts" else transfers
+            if len(objs):
+                f["user_data_128"][0, 0] = _pick(rng, objs["user_data_128"][:, 0], 0.7)
+                f["user_data_64"] = _pick(rng, objs["user_data_64"], 0.8)
+                f["user_data_32"] = _pick(rng, objs["user_data_32"], 0.8)
+                f["ledger"] = _pick(rng, objs["ledger"], 0.5)
+                f["code"] = _pick(rng, objs["code"], 0.7) & 0xFFFF
+            f["flags"] = int(rng.choice([0, 0, 1, 1, 2]))
+            tsrc = ats if kind == "query_accounts" else ts
+        r = rng.random()
+        if r < 0.5:
+            lo, hi = sorted(int(x) for x in rng.choice(tsrc, size=2))
+            f["timestamp_min"], f["timestamp_max"] = lo, hi
+        elif r < 0.6:
+            f["timestamp_min"] = int(rng.choice(tsrc))
+        elif r < 0.65:
+            lo, hi = sorted(int(x) for x in rng.choice(tsrc, size=2))
+            f["timestamp_min"], f["timestamp_max"] = hi + 1, lo  # inverted
+        f["limit"] = int(rng.choice([1, 2, 5, 30, 1000, 0xFFFFFFFF, 0]))
+        if rng.random() < 0.03:
+            f["reserved"][0, 0] = 1
+        out.append((kind, f))
+    return out
 
 
 def _first_diff(a, b):

@@ -9,8 +9,9 @@ derived by the harness rules (:704-735, :757-811).
 The StateMachine under test is bound to an executor: the CPU oracle (oracle/liboracle.so) or the
 HIP executor (libtbg.so). get_change_events (the account_events groove read back as
 ChangeEvents, :2396-2434, :3395-3527) is checked with the reference's own `match` rules
-(TestGetChangeEventsResult, :502-599). The other queries (get_account_transfers,
-get_account_balances, query_*) are outside this path and skipped: they do not change state.
+(TestGetChangeEventsResult, :502-599). The scans -- get_account_transfers, get_account_balances,
+query_accounts, query_transfers (TestAccountFilter / TestQueryFilter, :468-494, :863-1002) -- are
+submitted multi-batch encoded, one filter per commit, and their replies compared byte for byte.
 """
 import ctypes
 import os
@@ -24,7 +25,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from tigerbeetle_amd import native  # noqa: E402
 from tigerbeetle_amd.types import (  # noqa: E402
     ACCOUNT_DTYPE, CHANGE_EVENT_DTYPE, CHANGE_EVENTS_FILTER_DTYPE, RESULT_DTYPE, TRANSFER_DTYPE,
-    CreateAccountStatus, CreateTransferStatus, Operation, TIMESTAMP_MAX, U128_MAX, NS_PER_S)
+    CreateAccountStatus, CreateTransferStatus, Operation, TIMESTAMP_MAX, U128_MAX, NS_PER_S,
+    ACCOUNT_BALANCE_DTYPE, ACCOUNT_FILTER_DTYPE, QUERY_FILTER_DTYPE)
 
 TABLE_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "tables")
 
@@ -36,8 +38,11 @@ TEST_BATCH_SIZE_LIMIT = 30 * 128
 # = message_body_size_max / 128 (the unbatched encoding) = 30.
 TEST_PULSE_BATCH_MAX = TEST_MESSAGE_BODY_SIZE_MAX // 128
 
-SKIPPED_OPS = {"get_account_transfers", "get_account_balances", "query_accounts",
-               "query_transfers"}
+SKIPPED_OPS = set()
+SCAN_OPS = {"get_account_transfers": (Operation.get_account_transfers, 128, 128),
+            "get_account_balances": (Operation.get_account_balances, 128, 128),
+            "query_accounts": (Operation.query_accounts, 64, 128),
+            "query_transfers": (Operation.query_transfers, 64, 128)}
 
 
 # ---- row DSL (src/testing/table.zig) --------------------------------------------------------
@@ -186,6 +191,46 @@ def parse_row(line: str):
                 b[f] = parse_uint(t.next(), 128)
             b["closed"] = False if t.eat("_") else (t.next() == "CLSD")
             row[side] = b
+    elif kind in ("get_account_balances", "get_account_transfers"):
+        # TestAccountFilter (:468-482)
+        row["account_id"] = parse_uint(t.next(), 128)
+        for f, bits in (("user_data_128", 128), ("user_data_64", 64), ("user_data_32", 32),
+                        ("code", 16)):
+            row[f] = 0 if t.eat("_") else parse_uint(t.next(), bits)
+        row["min"] = None if t.eat("_") else parse_uint(t.next(), 128)
+        row["max"] = None if t.eat("_") else parse_uint(t.next(), 128)
+        row["limit"] = parse_uint(t.next(), 32)
+        for flag in ("DR", "CR", "REV"):
+            row[flag] = not t.eat("_")
+            if row[flag]:
+                assert t.next() == flag, line
+    elif kind in ("query_accounts", "query_transfers"):
+        # TestQueryFilter (:484-494)
+        for f, bits in (("user_data_128", 128), ("user_data_64", 64), ("user_data_32", 32),
+                        ("ledger", 32), ("code", 16)):
+            row[f] = parse_uint(t.next(), bits)
+        row["min"] = None if t.eat("_") else parse_uint(t.next(), 128)
+        row["max"] = None if t.eat("_") else parse_uint(t.next(), 128)
+        row["limit"] = parse_uint(t.next(), 32)
+        row["REV"] = not t.eat("_")
+        if row["REV"]:
+            assert t.next() == "REV", line
+    elif kind == "get_account_balances_result":
+        row["transfer_id"] = parse_uint(t.next(), 128)
+        for f in ("debits_pending", "debits_posted", "credits_pending", "credits_posted"):
+            row[f] = parse_uint(t.next(), 128)
+    elif kind in ("get_account_transfers_result", "query_transfers_result"):
+        row["id"] = parse_uint(t.next(), 128)
+    elif kind == "query_accounts_result":
+        row["id"] = parse_uint(t.next(), 128)
+        if t.eat("_"):
+            row["data"] = None
+        else:
+            d = {}
+            for f in ("debits_pending", "debits_posted", "credits_pending", "credits_posted"):
+                d[f] = parse_uint(t.next(), 128)
+            d["closed"] = False if t.eat("_") else (t.next() == "CLSD")
+            row["data"] = d
     elif kind.split("_result")[0] in SKIPPED_OPS or kind in SKIPPED_OPS:
         row["kind"] = "skip"
         row["op"] = kind
@@ -489,6 +534,53 @@ def run_table(handle: StateMachineHandle, rows, label=""):
         elif kind == "get_change_events_result":
             assert operation == "get_change_events"
             reply.append(row)
+        elif kind in ("get_account_balances", "get_account_transfers"):
+            assert operation is None
+            operation = kind
+            f = np.zeros(1, dtype=ACCOUNT_FILTER_DTYPE)[0]
+            _set_u128(f, "account_id", row["account_id"])
+            _set_u128(f, "user_data_128", row["user_data_128"])
+            f["user_data_64"] = row["user_data_64"]
+            f["user_data_32"] = row["user_data_32"]
+            f["code"] = row["code"]
+            f["timestamp_min"] = 0 if row["min"] is None else int(transfers[row["min"]]["timestamp"])
+            f["timestamp_max"] = 0 if row["max"] is None else int(transfers[row["max"]]["timestamp"])
+            f["limit"] = row["limit"]
+            f["flags"] = (1 if row["DR"] else 0) | (2 if row["CR"] else 0) | \
+                (4 if row["REV"] else 0)
+            request.append(f.tobytes())
+        elif kind in ("query_accounts", "query_transfers"):
+            assert operation is None
+            operation = kind
+            objects = accounts if kind == "query_accounts" else transfers
+            f = np.zeros(1, dtype=QUERY_FILTER_DTYPE)[0]
+            _set_u128(f, "user_data_128", row["user_data_128"])
+            for k in ("user_data_64", "user_data_32", "ledger", "code"):
+                f[k] = row[k]
+            f["timestamp_min"] = 0 if row["min"] is None else int(objects[row["min"]]["timestamp"])
+            f["timestamp_max"] = 0 if row["max"] is None else int(objects[row["max"]]["timestamp"])
+            f["limit"] = row["limit"]
+            f["flags"] = 1 if row["REV"] else 0
+            request.append(f.tobytes())
+        elif kind == "get_account_balances_result":
+            assert operation == "get_account_balances"
+            b = np.zeros(1, dtype=ACCOUNT_BALANCE_DTYPE)[0]
+            for k in ("debits_pending", "debits_posted", "credits_pending", "credits_posted"):
+                _set_u128(b, k, row[k])
+            b["timestamp"] = transfers[row["transfer_id"]]["timestamp"]
+            reply.append(b.tobytes())
+        elif kind in ("get_account_transfers_result", "query_transfers_result"):
+            assert operation == kind[:-len("_result")]
+            reply.append(transfers[row["id"]].tobytes())
+        elif kind == "query_accounts_result":
+            assert operation == "query_accounts"
+            a = accounts[row["id"]].copy()
+            d = row["data"]
+            if d is not None:
+                for k in ("debits_pending", "debits_posted", "credits_pending", "credits_posted"):
+                    _set_u128(a, k, d[k])
+                a["flags"] = (int(a["flags"]) & ~(1 << 5)) | ((1 << 5) if d["closed"] else 0)
+            reply.append(a.tobytes())
         elif kind == "commit":
             op_name = row["operation"]
             if op_name == "get_change_events":
@@ -524,6 +616,10 @@ def run_table(handle: StateMachineHandle, rows, label=""):
                 actual = ctx.submit(Operation.lookup_accounts, payload, 16, 128)
             elif op_name == "lookup_transfers":
                 actual = ctx.submit(Operation.lookup_transfers, payload, 16, 128)
+            elif op_name in SCAN_OPS:
+                assert len(request) == 1
+                code, event_size, result_size = SCAN_OPS[op_name]
+                actual = ctx.submit(code, payload, event_size, result_size)
             else:
                 raise ValueError(op_name)
             expected = b"".join(reply)
@@ -621,7 +717,8 @@ def describe_mismatch(label, commit_index, op_name, expected: bytes, actual: byt
             mark = "   " if es == as_ else ">>>"
             lines.append(f"{mark} [{i}] expected={es} actual={as_}")
     else:
-        dt = ACCOUNT_DTYPE if op_name == "lookup_accounts" else TRANSFER_DTYPE
+        dt = {"lookup_accounts": ACCOUNT_DTYPE, "query_accounts": ACCOUNT_DTYPE,
+              "get_account_balances": ACCOUNT_BALANCE_DTYPE}.get(op_name, TRANSFER_DTYPE)
         e = np.frombuffer(expected, dtype=dt)
         a = np.frombuffer(actual, dtype=dt)
         for i in range(max(len(e), len(a))):

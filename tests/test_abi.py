@@ -37,8 +37,14 @@ def test_struct_sizes():
     assert ACCOUNT_DTYPE.itemsize == 128 and TRANSFER_DTYPE.itemsize == 128
     assert RESULT_DTYPE.itemsize == 16
     assert ctypes.sizeof(native.TbgOptions) == 48
-    assert ctypes.sizeof(native.Executor) == 8 * 8
+    assert ctypes.sizeof(native.Executor) == 12 * 8
     from tigerbeetle_amd.types import (ACCOUNT_EVENT_DTYPE, CHANGE_EVENT_DTYPE,
                                        CHANGE_EVENTS_FILTER_DTYPE)
     assert ACCOUNT_EVENT_DTYPE.itemsize == 256 and CHANGE_EVENT_DTYPE.itemsize == 384
     assert CHANGE_EVENTS_FILTER_DTYPE.itemsize == 64
+    from tigerbeetle_amd.types import (ACCOUNT_BALANCE_DTYPE, ACCOUNT_FILTER_DTYPE,
+                                       QUERY_FILTER_DTYPE)
+    assert ACCOUNT_FILTER_DTYPE.itemsize == 128 and QUERY_FILTER_DTYPE.itemsize == 64
+    assert ACCOUNT_BALANCE_DTYPE.itemsize == 128
+    assert ACCOUNT_FILTER_DTYPE.fields["timestamp_min"][1] == 104
+    assert QUERY_FILTER_DTYPE.fields["timestamp_min"][1] == 40

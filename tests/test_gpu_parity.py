@@ -42,6 +42,63 @@ def test_fuzz(seed, force_replay):
             if step % 3 == 2:
                 p.tick(int(rng.integers(1, 3)) * NS_PER_S)
         p.compare_state()
+        assert p.compare_scans(rng, n=60) > 0
+    finally:
+        p.close()
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_scans_at_scale(seed):
+    """The scans (get_account_transfers / _balances, query_accounts / _transfers) over 12k accounts
+    with history and 100k transfers -- pending, posted, voided and single-phase, user data drawn
+    from small sets so that conditions intersect -- against the oracle, with the reply limit of
+    production (8190 results) and the reference's test configuration (29)."""
+    rng = np.random.default_rng(500 + seed)
+    p = Pair(account_capacity=1 << 15, transfer_capacity=1 << 18, batch_events_max=1 << 15)
+    try:
+        n_acc = 12_000
+        acc = workload.accounts(n_acc, seed=seed, ledger=1)
+        acc["flags"] = rng.choice([0, 8], size=n_acc).astype(np.uint16)  # history on half
+        acc["user_data_64"] = rng.integers(1, 20, size=n_acc).astype(np.uint64)
+        acc["code"] = rng.integers(1, 5, size=n_acc).astype(np.uint16)
+        acc["ledger"] = rng.integers(1, 3, size=n_acc).astype(np.uint32)
+        p.create_accounts(acc, _split(n_acc, rng, 8189))
+        # accounts of each ledger: transfers stay within one
+        by_ledger = {lg: np.nonzero(acc["ledger"] == lg)[0] + 1 for lg in (1, 2)}
+        for call in range(4):
+            n = 25_000
+            t = workload.transfers_uniform(n, 100, seed=seed * 10 + call, id_offset=call * n)
+            lg = rng.integers(1, 3, size=n)
+            for v in (1, 2):
+                ids = by_ledger[v]
+                m = lg == v
+                dr = rng.choice(ids[:200], size=m.sum())
+                cr = rng.choice(ids[:200], size=m.sum())
+                cr = np.where(cr == dr, ids[200], cr)
+                t["debit_account_id"][m, 0] = dr
+                t["credit_account_id"][m, 0] = cr
+            t["ledger"] = lg.astype(np.uint32)
+            t["user_data_128"][:, 0] = rng.integers(1, 7, size=n).astype(np.uint64)
+            t["user_data_128"][:, 1] = 0
+            t["user_data_64"] = rng.integers(1, 11, size=n).astype(np.uint64)
+            t["user_data_32"] = rng.integers(1, 4, size=n).astype(np.uint32)
+            t["code"] = rng.integers(1, 9, size=n).astype(np.uint16)
+            t["flags"] = np.where(rng.random(n) < 0.3, 2, 0).astype(np.uint16)  # pending
+            p.create_transfers(t, _split(n, rng, 8189))
+            if call:
+                prev = np.arange((call - 1) * n, call * n, dtype=np.uint64) + 1
+                pv = workload.transfers_uniform(4000, 100, seed=99 + call,
+                                                id_offset=10_000_000 + call * 4000)
+                pv["pending_id"][:, 0] = rng.choice(prev, size=4000, replace=False)
+                pv["debit_account_id"] = 0
+                pv["credit_account_id"] = 0
+                pv["ledger"] = 0
+                pv["code"] = 0
+                pv["amount"] = 0
+                pv["flags"] = rng.choice([4, 8], size=4000).astype(np.uint16)
+                p.create_transfers(pv, _split(4000, rng, 8189))
+        assert p.compare_scans(rng, n=60, limit_max=8190) > 1000
+        assert p.compare_scans(rng, n=60, limit_max=29) > 0
     finally:
         p.close()
 

@@ -18,6 +18,7 @@
 #include "lanes.hpp"
 #include "events.hpp"
 #include "durability.hpp"
+#include "queries.hpp"
 
 using namespace tbg;
 
@@ -1888,6 +1889,192 @@ tbg_ctx* tbg_open_checkpoint(const tbg_options* options, const char* path) {
     ctx->ae_sorted = h.ae_sorted != 0;
     ctx->acc_ts_stale = ctx->tr_ts_stale = true;
     return ctx;
+}
+
+}  // extern "C"
+
+// ---- Scans (queries.hpp) ---------------------------------------------------------------------------
+
+namespace {
+
+bool scan_ts_valid(uint64_t ts) { return ts >= TB_TIMESTAMP_MIN && ts <= TB_TIMESTAMP_MAX; }
+
+// get_scan_from_account_filter's validity (:1743-1753).
+bool account_filter_valid(const tb_account_filter_t* f) {
+    bool reserved_zero = true;
+    for (int i = 0; i < 58; i++) reserved_zero &= f->reserved[i] == 0;
+    const u128 id = U(f->account_id);
+    return id != 0 && id != kU128Max && (f->timestamp_min == 0 || scan_ts_valid(f->timestamp_min)) &&
+           (f->timestamp_max == 0 || scan_ts_valid(f->timestamp_max)) &&
+           (f->timestamp_max == 0 || f->timestamp_min <= f->timestamp_max) && f->limit != 0 &&
+           (f->flags & (TB_ACCOUNT_FILTER_DEBITS | TB_ACCOUNT_FILTER_CREDITS)) &&
+           !(f->flags & TB_ACCOUNT_FILTER_PADDING_MASK) && reserved_zero;
+}
+
+// get_scan_from_query_filter's validity (:2062-2070).
+bool query_filter_valid(const tb_query_filter_t* f) {
+    bool reserved_zero = true;
+    for (int i = 0; i < 6; i++) reserved_zero &= f->reserved[i] == 0;
+    return (f->timestamp_min == 0 || scan_ts_valid(f->timestamp_min)) &&
+           (f->timestamp_max == 0 || scan_ts_valid(f->timestamp_max)) &&
+           (f->timestamp_max == 0 || f->timestamp_min <= f->timestamp_max) && f->limit != 0 &&
+           !(f->flags & TB_QUERY_FILTER_PADDING_MASK) && reserved_zero;
+}
+
+template <typename F>
+ScanFilter scan_filter_common(const F* f) {
+    ScanFilter s{};
+    s.user_data_128 = U(f->user_data_128);
+    s.user_data_64 = f->user_data_64;
+    s.user_data_32 = f->user_data_32;
+    s.code = f->code;
+    s.ts_lo = f->timestamp_min ? f->timestamp_min : TB_TIMESTAMP_MIN;
+    s.ts_hi = f->timestamp_max ? f->timestamp_max : TB_TIMESTAMP_MAX;
+    return s;
+}
+
+// Matches one table's live rows (`launch` fills the match flags), selects them in row order and
+// returns their count; the selected rows are ctx->sel_buf[0 .. count).
+template <typename Launch>
+int64_t scan_select(tbg_ctx* ctx, uint64_t used, Launch launch) {
+    if (used == 0) return 0;
+    uint8_t* match = nullptr;
+    if (!dev_alloc(ctx, &match, used, false)) return TBG_ENOMEM;
+    launch(match);
+    unsigned int* d_count = &ctx->d_scalars->slow_count;
+    int rc = hip_ok(ctx, hipGetLastError(), "scan match") ? 0 : TBG_EHIP;
+    if (!rc) rc = select_flagged(ctx, match, used, ctx->sel_buf, d_count);
+    unsigned int count = 0;
+    if (!rc && !(hip_ok(ctx, hipMemcpyAsync(&count, d_count, 4, hipMemcpyDeviceToHost, ctx->stream),
+                        "scan count") &&
+                 hip_ok(ctx, hipStreamSynchronize(ctx->stream), "scan sync")))
+        rc = TBG_EHIP;
+    (void)hipFree(match);
+    return rc ? rc : int64_t(count);
+}
+
+// The first n (or, reversed, the last n) selected rows of `rows`, copied to the host.
+template <typename Row>
+int64_t scan_output(tbg_ctx* ctx, const Row* rows, uint32_t count, uint32_t n, bool reversed,
+                    Row* out) {
+    if (n == 0) return 0;
+    Row* d_out = nullptr;
+    if (!dev_alloc(ctx, &d_out, n, false)) return TBG_ENOMEM;
+    hipLaunchKernelGGL(scan_gather<Row>, dim3(grid_for(n)), dim3(kBlock), 0, ctx->stream, rows,
+                       ctx->sel_buf, count, n, reversed ? 1 : 0, d_out);
+    int64_t rc = n;
+    if (!hip_ok(ctx, hipGetLastError(), "scan gather") ||
+        !hip_ok(ctx, hipMemcpyAsync(out, d_out, size_t(n) * sizeof(Row), hipMemcpyDeviceToHost,
+                                    ctx->stream), "scan copy") ||
+        !hip_ok(ctx, hipStreamSynchronize(ctx->stream), "scan sync"))
+        rc = TBG_EHIP;
+    (void)hipFree(d_out);
+    return rc;
+}
+
+// The transfers an AccountFilter selects (get_account_transfers / get_account_balances).
+int64_t scan_account_transfers(tbg_ctx* ctx, const tb_account_filter_t* filter) {
+    ScanFilter f = scan_filter_common(filter);
+    f.account_id = U(filter->account_id);
+    f.sides = filter->flags & (TB_ACCOUNT_FILTER_DEBITS | TB_ACCOUNT_FILTER_CREDITS);
+    const uint64_t used = ctx->T.tr_rows_used;
+    return scan_select(ctx, used, [&](uint8_t* match) {
+        hipLaunchKernelGGL(scan_match_account_transfers, dim3(grid_for(used)), dim3(kBlock), 0,
+                           ctx->stream, ctx->T.tr_rows, ctx->T.tr_live, used, f, match);
+    });
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t tbg_get_account_transfers(tbg_ctx* ctx, const tb_account_filter_t* filter,
+                                  uint32_t limit_max, tb_transfer_t* out) {
+    if (!ctx || !filter) return TBG_EINVAL;
+    if (!account_filter_valid(filter)) return 0;
+    const int64_t count = scan_account_transfers(ctx, filter);
+    if (count <= 0) return count;
+    const uint32_t n = std::min<uint64_t>({uint64_t(count), filter->limit, limit_max});
+    return scan_output(ctx, ctx->T.tr_rows, uint32_t(count), n,
+                       (filter->flags & TB_ACCOUNT_FILTER_REVERSED) != 0, out);
+}
+
+int64_t tbg_get_account_balances(tbg_ctx* ctx, const tb_account_filter_t* filter,
+                                 uint32_t limit_max, tb_account_balance_t* out) {
+    if (!ctx || !filter) return TBG_EINVAL;
+    if (!ctx->ae_log) {
+        ctx->error = "get_account_balances needs account_events_capacity > 0";
+        return TBG_EINVAL;
+    }
+    // The account must exist and keep history (:1624-1626).
+    tb_account_t acc;
+    const int64_t found = lookup_impl(ctx, &filter->account_id, 1, &acc, true);
+    if (found < 0) return found;
+    if (found == 0 || !(acc.flags & TB_ACCOUNT_HISTORY) || !account_filter_valid(filter)) return 0;
+    const int64_t count = scan_account_transfers(ctx, filter);
+    if (count <= 0) return count;
+    const uint32_t n = std::min<uint64_t>({uint64_t(count), filter->limit, limit_max});
+    int rc = ae_sort_log(ctx);
+    if (rc) return rc;
+    tb_account_balance_t* d_out = nullptr;
+    unsigned int* d_missing = reinterpret_cast<unsigned int*>(ctx->ae_words);
+    if (!dev_alloc(ctx, &d_out, n, false)) return TBG_ENOMEM;
+    int64_t result = n;
+    unsigned int missing = 0;
+    if (!hip_ok(ctx, hipMemsetAsync(d_missing, 0, 4, ctx->stream), "memset")) result = TBG_EHIP;
+    if (result >= 0) {
+        hipLaunchKernelGGL(scan_balances, dim3(grid_for(n)), dim3(kBlock), 0, ctx->stream,
+                           ctx->T.tr_rows, ctx->sel_buf, uint32_t(count), n,
+                           (filter->flags & TB_ACCOUNT_FILTER_REVERSED) ? 1 : 0, ctx->ae_log,
+                           ctx->ae_used, U(filter->account_id), d_out, d_missing);
+        if (!hip_ok(ctx, hipGetLastError(), "scan balances") ||
+            !hip_ok(ctx, hipMemcpyAsync(out, d_out, size_t(n) * sizeof(tb_account_balance_t),
+                                        hipMemcpyDeviceToHost, ctx->stream), "balances copy") ||
+            !hip_ok(ctx, hipMemcpyAsync(&missing, d_missing, 4, hipMemcpyDeviceToHost,
+                                        ctx->stream), "missing") ||
+            !hip_ok(ctx, hipStreamSynchronize(ctx->stream), "sync"))
+            result = TBG_EHIP;
+    }
+    (void)hipFree(d_out);
+    if (result >= 0 && missing) {
+        ctx->error = "get_account_balances: a transfer without its AccountEvent";
+        result = TBG_EINVAL;
+    }
+    return result;
+}
+
+int64_t tbg_query_accounts(tbg_ctx* ctx, const tb_query_filter_t* filter, uint32_t limit_max,
+                           tb_account_t* out) {
+    if (!ctx || !filter) return TBG_EINVAL;
+    if (!query_filter_valid(filter)) return 0;
+    ScanFilter f = scan_filter_common(filter);
+    f.ledger = filter->ledger;
+    const uint64_t used = ctx->T.acc_rows_used;
+    const int64_t count = scan_select(ctx, used, [&](uint8_t* match) {
+        hipLaunchKernelGGL(scan_match_query<tb_account_t>, dim3(grid_for(used)), dim3(kBlock), 0,
+                           ctx->stream, ctx->T.acc_rows, ctx->T.acc_live, used, f, match);
+    });
+    if (count <= 0) return count;
+    const uint32_t n = std::min<uint64_t>({uint64_t(count), filter->limit, limit_max});
+    return scan_output(ctx, ctx->T.acc_rows, uint32_t(count), n,
+                       (filter->flags & TB_QUERY_FILTER_REVERSED) != 0, out);
+}
+
+int64_t tbg_query_transfers(tbg_ctx* ctx, const tb_query_filter_t* filter, uint32_t limit_max,
+                            tb_transfer_t* out) {
+    if (!ctx || !filter) return TBG_EINVAL;
+    if (!query_filter_valid(filter)) return 0;
+    ScanFilter f = scan_filter_common(filter);
+    f.ledger = filter->ledger;
+    const uint64_t used = ctx->T.tr_rows_used;
+    const int64_t count = scan_select(ctx, used, [&](uint8_t* match) {
+        hipLaunchKernelGGL(scan_match_query<tb_transfer_t>, dim3(grid_for(used)), dim3(kBlock), 0,
+                           ctx->stream, ctx->T.tr_rows, ctx->T.tr_live, used, f, match);
+    });
+    if (count <= 0) return count;
+    const uint32_t n = std::min<uint64_t>({uint64_t(count), filter->limit, limit_max});
+    return scan_output(ctx, ctx->T.tr_rows, uint32_t(count), n,
+                       (filter->flags & TB_QUERY_FILTER_REVERSED) != 0, out);
 }
 
 }  // extern "C"

@@ -9,6 +9,7 @@
 #include "../../include/tb_state_machine.h"
 
 #include <algorithm>
+#include <cstddef>
 #include <cstdlib>
 #include <cstring>
 #include <new>
@@ -35,8 +36,31 @@ bool operation_info(uint8_t operation, OperationInfo* info) {
         case TB_OPERATION_LOOKUP_ACCOUNTS: *info = {16, 128, true}; return true;
         case TB_OPERATION_LOOKUP_TRANSFERS: *info = {16, 128, true}; return true;
         case TB_OPERATION_GET_CHANGE_EVENTS: *info = {64, 384, false}; return true;
+        case TB_OPERATION_GET_ACCOUNT_TRANSFERS: *info = {128, 128, true}; return true;
+        case TB_OPERATION_GET_ACCOUNT_BALANCES: *info = {128, 128, true}; return true;
+        case TB_OPERATION_QUERY_ACCOUNTS: *info = {64, 128, true}; return true;
+        case TB_OPERATION_QUERY_TRANSFERS: *info = {64, 128, true}; return true;
         default: return false;
     }
+}
+
+// Operation.is_batchable (src/tigerbeetle.zig:787-815): the queries take one filter per batch.
+bool is_query(uint8_t operation) {
+    return operation == TB_OPERATION_GET_CHANGE_EVENTS ||
+           operation == TB_OPERATION_GET_ACCOUNT_TRANSFERS ||
+           operation == TB_OPERATION_GET_ACCOUNT_BALANCES ||
+           operation == TB_OPERATION_QUERY_ACCOUNTS || operation == TB_OPERATION_QUERY_TRANSFERS;
+}
+
+// A query filter's `limit` (Operation.result_count_expected, tigerbeetle.zig:966-990).
+uint32_t filter_limit(uint8_t operation, const uint8_t* filter) {
+    uint32_t limit = 0;
+    const size_t at = (operation == TB_OPERATION_QUERY_ACCOUNTS ||
+                       operation == TB_OPERATION_QUERY_TRANSFERS)
+                          ? offsetof(tb_query_filter_t, limit)
+                          : offsetof(tb_account_filter_t, limit);
+    std::memcpy(&limit, filter + at, 4);
+    return limit;
 }
 
 }  // namespace
@@ -140,10 +164,19 @@ struct tb_sm {
                         (options.message_body_size_max - reply_trailer_min) / info.result_size);
     }
 
+    // Operation.result_max (tigerbeetle.zig:907-931).
+    uint32_t result_max(uint8_t operation, const OperationInfo& info,
+                        uint32_t batch_size_limit) const {
+        if (!is_query(operation)) return event_max(info, batch_size_limit);
+        if (!info.multi_batch) return options.message_body_size_max / info.result_size;
+        return (options.message_body_size_max -
+                tb_multi_batch_trailer_total_size(info.result_size, 1)) / info.result_size;
+    }
+
     bool batch_valid(uint8_t operation, const OperationInfo& info, uint32_t batch_size) const {
         if (operation == TB_OPERATION_PULSE) return batch_size == 0;
         // Not batchable (queries): exactly one filter.
-        if (operation == TB_OPERATION_GET_CHANGE_EVENTS) return batch_size == info.event_size;
+        if (is_query(operation)) return batch_size == info.event_size;
         if (batch_size % info.event_size != 0) return false;
         return batch_size / info.event_size <= event_max(info, options.batch_size_limit);
     }
@@ -174,6 +207,21 @@ int64_t gpu_get_change_events(void* self, const tb_change_events_filter_t* filte
                               uint32_t limit_max, tb_change_event_t* out) {
     return tbg_get_change_events(static_cast<tbg_ctx*>(self), filter, limit_max, out);
 }
+int64_t gpu_get_account_transfers(void* self, const tb_account_filter_t* f, uint32_t m,
+                                  tb_transfer_t* out) {
+    return tbg_get_account_transfers(static_cast<tbg_ctx*>(self), f, m, out);
+}
+int64_t gpu_get_account_balances(void* self, const tb_account_filter_t* f, uint32_t m,
+                                 tb_account_balance_t* out) {
+    return tbg_get_account_balances(static_cast<tbg_ctx*>(self), f, m, out);
+}
+int64_t gpu_query_accounts(void* self, const tb_query_filter_t* f, uint32_t m, tb_account_t* out) {
+    return tbg_query_accounts(static_cast<tbg_ctx*>(self), f, m, out);
+}
+int64_t gpu_query_transfers(void* self, const tb_query_filter_t* f, uint32_t m,
+                            tb_transfer_t* out) {
+    return tbg_query_transfers(static_cast<tbg_ctx*>(self), f, m, out);
+}
 
 }  // namespace
 
@@ -200,6 +248,10 @@ tb_sm* bind_gpu(const tb_sm_options* options, tbg_ctx* ctx) {
     ex.lookup_accounts = gpu_lookup_accounts;
     ex.lookup_transfers = gpu_lookup_transfers;
     ex.get_change_events = gpu_get_change_events;
+    ex.get_account_transfers = gpu_get_account_transfers;
+    ex.get_account_balances = gpu_get_account_balances;
+    ex.query_accounts = gpu_query_accounts;
+    ex.query_transfers = gpu_query_transfers;
     tb_sm* sm = tb_sm_open(options, &ex);
     if (!sm) {
         tbg_close(ctx);
@@ -252,10 +304,13 @@ extern "C" int tb_sm_input_valid(const tb_sm* sm, uint8_t operation, const void*
                                        uint32_t(counts.size()), &payload);
     if (nb <= 0) return 0;
     uint64_t result_count_expected = 0;
-    uint32_t result_max = sm->event_max(info, sm->options.message_body_size_max);
+    const uint32_t result_max = sm->result_max(operation, info, sm->options.message_body_size_max);
+    const uint8_t* batch = static_cast<const uint8_t*>(body);
     for (int64_t b = 0; b < nb; b++) {
         if (!sm->batch_valid(operation, info, uint32_t(counts[b]) * info.event_size)) return 0;
-        result_count_expected += std::min<uint32_t>(counts[b], result_max);
+        const uint32_t expected = is_query(operation) ? filter_limit(operation, batch) : counts[b];
+        result_count_expected += std::min<uint32_t>(expected, result_max);
+        batch += uint32_t(counts[b]) * info.event_size;
     }
     uint64_t reply_trailer = tb_multi_batch_trailer_total_size(info.result_size, uint32_t(nb));
     if (sm->options.message_body_size_max < result_count_expected * info.result_size + reply_trailer)
@@ -363,6 +418,51 @@ extern "C" int64_t tb_sm_commit(tb_sm* sm, uint64_t client_lo, uint64_t client_h
                                                      uint32_t(nb), results);
         if (rc < 0) return rc;
         return tb_multi_batch_encode_trailer(out, n * 16u, 16, sm->counts.data(), uint32_t(nb));
+    }
+
+    if (is_query(operation)) {
+        // execute_query_multi_batch (:2823-2910): each batch is one filter, its results (at most
+        // min(filter.limit, result_max)) one reply batch.
+        const tb_executor& ex = sm->executor;
+        if (!ex.get_account_transfers || !ex.get_account_balances || !ex.query_accounts ||
+            !ex.query_transfers)
+            return TBG_EINVAL;
+        const uint32_t limit_max = sm->result_max(operation, info,
+                                                  sm->options.message_body_size_max);
+        const uint8_t* filter = static_cast<const uint8_t*>(body);
+        std::vector<uint16_t> reply_counts(static_cast<size_t>(nb));
+        uint32_t written = 0;
+        for (int64_t b = 0; b < nb; b++, filter += info.event_size) {
+            void* dst = out + written;
+            int64_t count = 0;
+            switch (operation) {
+                case TB_OPERATION_GET_ACCOUNT_TRANSFERS:
+                    count = ex.get_account_transfers(
+                        ex.self, reinterpret_cast<const tb_account_filter_t*>(filter), limit_max,
+                        static_cast<tb_transfer_t*>(dst));
+                    break;
+                case TB_OPERATION_GET_ACCOUNT_BALANCES:
+                    count = ex.get_account_balances(
+                        ex.self, reinterpret_cast<const tb_account_filter_t*>(filter), limit_max,
+                        static_cast<tb_account_balance_t*>(dst));
+                    break;
+                case TB_OPERATION_QUERY_ACCOUNTS:
+                    count = ex.query_accounts(ex.self,
+                                              reinterpret_cast<const tb_query_filter_t*>(filter),
+                                              limit_max, static_cast<tb_account_t*>(dst));
+                    break;
+                default:
+                    count = ex.query_transfers(ex.self,
+                                               reinterpret_cast<const tb_query_filter_t*>(filter),
+                                               limit_max, static_cast<tb_transfer_t*>(dst));
+                    break;
+            }
+            if (count < 0) return count;
+            reply_counts[b] = uint16_t(count);
+            written += uint32_t(count) * info.result_size;
+        }
+        return tb_multi_batch_encode_trailer(out, written, info.result_size, reply_counts.data(),
+                                             uint32_t(nb));
     }
 
     // lookup_accounts / lookup_transfers: per batch, found objects only (:3255-3292).

@@ -66,6 +66,10 @@ class Executor(ctypes.Structure):
         ("lookup_accounts", vp),
         ("lookup_transfers", vp),
         ("get_change_events", vp),
+        ("get_account_transfers", vp),
+        ("get_account_balances", vp),
+        ("query_accounts", vp),
+        ("query_transfers", vp),
     ]
 
 
@@ -101,6 +105,10 @@ SIGNATURES = [
     ("tbg_compact", ctypes.c_int64, [vp]),
     ("tbg_checkpoint", ctypes.c_int, [vp, ctypes.c_char_p]),
     ("tbg_open_checkpoint", vp, [ctypes.POINTER(TbgOptions), ctypes.c_char_p]),
+    ("tbg_get_account_transfers", ctypes.c_int64, [vp, vp, ctypes.c_uint32, vp]),
+    ("tbg_get_account_balances", ctypes.c_int64, [vp, vp, ctypes.c_uint32, vp]),
+    ("tbg_query_accounts", ctypes.c_int64, [vp, vp, ctypes.c_uint32, vp]),
+    ("tbg_query_transfers", ctypes.c_int64, [vp, vp, ctypes.c_uint32, vp]),
     ("tbg_debug_set_account_balances", ctypes.c_int, [vp, U128, U128, U128, U128, U128]),
     ("tbg_last_stats", ctypes.c_int, [vp, ctypes.POINTER(TbgStats)]),
     ("tbg_debug_force_replay", ctypes.c_int, [vp, ctypes.c_int]),

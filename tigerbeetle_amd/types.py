@@ -87,6 +87,25 @@ CHANGE_EVENT_DTYPE = np.dtype([
 CHANGE_EVENTS_FILTER_DTYPE = np.dtype([("timestamp_min", "<u8"), ("timestamp_max", "<u8"),
                                        ("limit", "<u4"), ("reserved", "u1", (44,))])
 
+# src/tigerbeetle.zig:563-611 (AccountFilter; flags: debits 1, credits 2, reversed 4)
+ACCOUNT_FILTER_DTYPE = np.dtype([
+    ("account_id", "<u8", (2,)), ("user_data_128", "<u8", (2,)), ("user_data_64", "<u8"),
+    ("user_data_32", "<u4"), ("code", "<u2"), ("reserved", "u1", (58,)),
+    ("timestamp_min", "<u8"), ("timestamp_max", "<u8"), ("limit", "<u4"), ("flags", "<u4"),
+])
+# src/tigerbeetle.zig:517-561 (QueryFilter; flags: reversed 1)
+QUERY_FILTER_DTYPE = np.dtype([
+    ("user_data_128", "<u8", (2,)), ("user_data_64", "<u8"), ("user_data_32", "<u4"),
+    ("ledger", "<u4"), ("code", "<u2"), ("reserved", "u1", (6,)), ("timestamp_min", "<u8"),
+    ("timestamp_max", "<u8"), ("limit", "<u4"), ("flags", "<u4"),
+])
+# src/tigerbeetle.zig:70-84 (AccountBalance)
+ACCOUNT_BALANCE_DTYPE = np.dtype([
+    ("debits_pending", "<u8", (2,)), ("debits_posted", "<u8", (2,)),
+    ("credits_pending", "<u8", (2,)), ("credits_posted", "<u8", (2,)), ("timestamp", "<u8"),
+    ("reserved", "u1", (56,)),
+])
+
 # src/tigerbeetle.zig:471-493
 RESULT_DTYPE = np.dtype([("timestamp", "<u8"), ("status", "<u4"), ("reserved", "<u4")])
 
@@ -246,6 +265,10 @@ class Operation(enum.IntEnum):
     create_transfers = 147
     lookup_accounts = 140
     lookup_transfers = 141
+    get_account_transfers = 142
+    get_account_balances = 143
+    query_accounts = 144
+    query_transfers = 145
 
 
 def u128_split(x: int):
