@@ -312,11 +312,13 @@ def u128_of(rec, name) -> int:
 class StateMachineHandle:
     """A tb_sm bound to an executor, plus the executor's `setup` hook."""
 
-    def __init__(self, lib, sm, set_balances, close):
+    def __init__(self, lib, sm, set_balances, close, after_commit=None):
         self.lib = lib
         self.sm = sm
         self.set_balances = set_balances
         self._close = close
+        # Optional hook run after every commit; it may replace self.sm (checkpoint + reopen).
+        self.after_commit = after_commit
         self.output = ctypes.create_string_buffer(TEST_MESSAGE_BODY_SIZE_MAX + 256)
 
     def close(self):
@@ -599,6 +601,9 @@ def run_table(handle: StateMachineHandle, rows, label=""):
                 request.clear()
                 reply.clear()
                 operation = None
+                if handle.after_commit:
+                    handle.after_commit()
+                    ctx.sm = sm = handle.sm
                 continue
             if operation == "skip" or op_name in SKIPPED_OPS:
                 request.clear()
@@ -628,6 +633,9 @@ def run_table(handle: StateMachineHandle, rows, label=""):
             request.clear()
             reply.clear()
             operation = None
+            if handle.after_commit:
+                handle.after_commit()
+                ctx.sm = sm = handle.sm
         else:
             raise ValueError(kind)
     assert operation is None and not request and not reply

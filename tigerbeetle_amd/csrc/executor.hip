@@ -8,6 +8,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -204,6 +205,24 @@ void tmark(tbg_ctx* ctx, const char* name) {
     if (!ctx->marks[ctx->n_marks]) (void)hipEventCreate(&ctx->marks[ctx->n_marks]);
     (void)hipEventRecord(ctx->marks[ctx->n_marks], ctx->stream);
     ctx->mark_names[ctx->n_marks++] = name;
+}
+
+// Host wall time of a phase of a host-buffer call (tbg_profile): accumulated like the marks.
+void hprof(tbg_ctx* ctx, const char* name, double ms) {
+    if (!ctx->timing) return;
+    size_t j = 0;
+    while (j < ctx->prof_names.size() && ctx->prof_names[j] != name) j++;
+    if (j == ctx->prof_names.size()) {
+        ctx->prof_names.push_back(name);
+        ctx->prof_ms.push_back(0);
+        ctx->prof_count.push_back(0);
+    }
+    ctx->prof_ms[j] += ms;
+    ctx->prof_count[j] += 1;
+}
+double now_ms() {
+    return std::chrono::duration<double, std::milli>(
+               std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
 // After the stream is synchronised: accumulate the time between consecutive marks per name.
@@ -1174,7 +1193,11 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
     if (replay && (ctx->h_scalars->flags & kFlagImported)) rc = check_imported_indexes(ctx, true);
     if (replay && !rc) rc = run_replay(ctx, c, true, false);
     if (!rc) rc = end_call(ctx, n, !replay);
-    if (!rc && ctx->ae_log) rc = ae_transfers(ctx, c);
+    if (!rc && ctx->ae_log) {
+        const double ta = ctx->timing ? now_ms() : 0;
+        rc = ae_transfers(ctx, c);
+        if (ctx->timing) hprof(ctx, "host:account_events", now_ms() - ta);
+    }
     ctx->stream = saved;
     ctx->T.tr_rows_used += n;  // rows are consumed whether or not the events created objects
     ctx->tr_ts_stale = true;
@@ -1261,17 +1284,25 @@ int tbg_create_transfers(tbg_ctx* ctx, const tb_transfer_t* events, uint32_t n,
                          tb_create_result_t* results) {
     if (!ctx || n > ctx->opt.batch_events_max) return TBG_EINVAL;
     if (n == 0) return 0;
+    const double t0 = ctx->timing ? now_ms() : 0;
     int rc = upload_batches(ctx, n, batch_lens, batch_ts, nb);
     if (rc) return rc;
     HIP_TRY(ctx, hipMemcpyAsync(ctx->d_events, events, size_t(n) * 128, hipMemcpyHostToDevice,
                                 ctx->stream));
+    const double t1 = ctx->timing ? now_ms() : 0;
     rc = tbg_create_transfers_device(ctx, reinterpret_cast<const tb_transfer_t*>(ctx->d_events), n,
                                      ctx->d_batch_ends, ctx->d_batch_ts, nb, ctx->d_results,
                                      nullptr);
     if (rc) return rc;
+    const double t2 = ctx->timing ? now_ms() : 0;
     HIP_TRY(ctx, hipMemcpyAsync(results, ctx->d_results, size_t(n) * 16, hipMemcpyDeviceToHost,
                                 ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (ctx->timing) {
+        hprof(ctx, "host:upload", t1 - t0);
+        hprof(ctx, "host:call", t2 - t1);
+        hprof(ctx, "host:download", now_ms() - t2);
+    }
     return 0;
 }
 

@@ -1542,20 +1542,45 @@ __global__ void pulse_collect(Tables T, uint64_t timestamp, uint64_t count, uint
                               uint64_t* cand_ts, uint64_t* cand_row,
                               unsigned long long* cand_count, unsigned long long* next_unexpired) {
     const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (i >= count) return;
-    const uint64_t row = T.expiry[i];
-    if (!T.tr_live[row] || T.tr_status[row] != TB_PENDING_PENDING) return;
-    const tb_transfer_t& p = T.tr_rows[row];
-    const uint64_t expires_at = p.timestamp + (uint64_t)p.timeout * TB_NS_PER_S;
-    keep[atomicAdd(keep_count, 1ull)] = row;
-    if (expires_at <= timestamp) {
-        const unsigned long long j = atomicAdd(cand_count, 1ull);
-        cand_expires[j] = expires_at;
-        cand_ts[j] = p.timestamp;
-        cand_row[j] = row;
-    } else {
-        atomicMin(next_unexpired, (unsigned long long)expires_at);
+    bool kept = false, cand = false;
+    uint64_t row = 0, expires_at = ~0ull, ts = 0;
+    if (i < count) {
+        row = T.expiry[i];
+        if (T.tr_live[row] && T.tr_status[row] == TB_PENDING_PENDING) {
+            const tb_transfer_t& p = T.tr_rows[row];
+            ts = p.timestamp;
+            expires_at = p.timestamp + (uint64_t)p.timeout * TB_NS_PER_S;
+            kept = true;
+            cand = expires_at <= timestamp;
+        }
     }
+    // One atomic per wave for each list (the appends of a whole wave), not one per entry: ~90k
+    // entries on one counter serialised at ~0.5 ns each.
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t keep_mask = __ballot(kept), cand_mask = __ballot(cand);
+    const uint64_t below = (1ull << lane) - 1;
+    unsigned long long keep_base = 0, cand_base = 0;
+    const int leader = keep_mask ? __ffsll((unsigned long long)keep_mask) - 1 : 0;
+    if (keep_mask && lane == uint32_t(leader)) {
+        keep_base = atomicAdd(keep_count, (unsigned long long)__popcll(keep_mask));
+        if (cand_mask) cand_base = atomicAdd(cand_count, (unsigned long long)__popcll(cand_mask));
+    }
+    keep_base = __shfl(keep_base, leader);
+    cand_base = __shfl(cand_base, leader);
+    if (kept) keep[keep_base + __popcll(keep_mask & below)] = row;
+    if (cand) {
+        const uint64_t j = cand_base + __popcll(cand_mask & below);
+        cand_expires[j] = expires_at;
+        cand_ts[j] = ts;
+        cand_row[j] = row;
+    }
+    // The earliest unexpired expiry: a wave minimum first.
+    uint64_t next = (kept && !cand) ? expires_at : ~0ull;
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t o = __shfl_xor(next, off);
+        next = o < next ? o : next;
+    }
+    if (lane == 0 && next != ~0ull) atomicMin(next_unexpired, (unsigned long long)next);
 }
 
 // The timestamps of the first n sorted candidates (their index keys' second half).

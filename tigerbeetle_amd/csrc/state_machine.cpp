@@ -9,6 +9,7 @@
 #include "../../include/tb_state_machine.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cstddef>
 #include <cstdlib>
 #include <cstring>
