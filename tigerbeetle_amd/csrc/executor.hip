@@ -16,7 +16,7 @@
 #include <vector>
 
 #include "../../include/tbg.h"
-#include "lanes.hpp"
+#include "group.hpp"
 #include "events.hpp"
 #include "durability.hpp"
 #include "queries.hpp"
@@ -46,29 +46,32 @@ struct PulseScratch {
     unsigned long long* counters = nullptr;
 };
 
-// Flow replay scratch (flow.hpp), grown on demand to the largest replay list seen.
+// Flow replay scratch (flow.hpp, group.hpp), grown on demand to the largest replay list seen.
 struct FlowScratch {
     uint64_t cap = 0;          // positions
+    uint64_t slots = 0;        // grouping hash slots
     uint8_t *head8 = nullptr, *barrier8 = nullptr;
     uint32_t *heads = nullptr, *unit_of = nullptr, *barriers = nullptr, *vals = nullptr,
-             *vals_sorted = nullptr, *pred = nullptr, *done = nullptr;
-    uint64_t *keys = nullptr, *keys_sorted = nullptr, *pnt_ops = nullptr, *pnt_scan = nullptr;
+             *vals_sorted = nullptr, *succ = nullptr, *indeg = nullptr;
+    uint64_t *keys_sorted = nullptr, *pnt_ops = nullptr, *pnt_scan = nullptr;
     Step* steps = nullptr;
     uint32_t* queue = nullptr;
-    uint8_t* ready8 = nullptr;
+    uint8_t* outcome = nullptr;  // account lanes' verdicts
+    // the grouping (group.hpp)
+    unsigned long long* hkeys = nullptr;
+    uint32_t *hcnt = nullptr, *hoff = nullptr, *loc = nullptr, *rank = nullptr;
+    uint4* big = nullptr;
     // account lanes (lanes.hpp)
     LaneRec* recs = nullptr;
     uint32_t *mailbox = nullptr, *owner_starts = nullptr, *mb_index = nullptr;
-    uint8_t* owner_head8 = nullptr;
     unsigned int* lane_counts = nullptr;
     uint32_t* dup_mark = nullptr;  // per event (batch_events_max)
-    unsigned int* counts = nullptr;
-    unsigned long long* pnt_fired = nullptr;
+    unsigned int* counts = nullptr;  // [0] units [1] barriers [2] ready [4] grouped pairs [5] listed
+    unsigned long long* words = nullptr;  // [0] pnt_fired [1] expiry_count at the plan's start
     UndoEntry* lane_undo = nullptr;
     unsigned int* engine = nullptr;  // flow engine queue counters
-    uint32_t *exp_flag = nullptr, *exp_index = nullptr;
+    uint32_t* exp_flag = nullptr;
     uint32_t* acc_free = nullptr;  // per account (lanes.hpp free owners)
-    u128 *contrib = nullptr, *prefix = nullptr;
 };
 
 }  // namespace
@@ -112,6 +115,12 @@ struct tbg_ctx {
     uint32_t idx_dirty_cap = 0;
     void* cub_temp = nullptr;
     size_t cub_temp_bytes = 0;
+    // chained scans (prims.hpp): per-tile status words, the tile ticket, launch sequence
+    unsigned long long* scan_status = nullptr;
+    uint64_t scan_tiles_cap = 0;
+    unsigned int* scan_ticket = nullptr;
+    uint32_t scan_ticket_base = 0;
+    uint32_t scan_seq = 0;
 
     // imported-timestamp indexes (rebuilt on demand)
     uint64_t* acc_ts_index = nullptr;
@@ -179,18 +188,38 @@ int ensure_cub_temp(tbg_ctx* ctx, size_t bytes) {
     return 0;
 }
 
-// Order-preserving selection of indices [0, n) whose flag is nonzero.
+// One chained scan (prims.hpp): `n` items, the op's emits and total.
+template <typename Op>
+int launch_scan(tbg_ctx* ctx, uint64_t n, const Op& op) {
+    const uint64_t tiles = n ? (n + kScanTile - 1) / kScanTile : 1;
+    if (tiles > 0xFFFFFFFFull) return TBG_EINVAL;
+    if (!ctx->scan_ticket) HIP_TRY(ctx, hipMalloc(&ctx->scan_ticket, sizeof(unsigned int)));
+    if (tiles > ctx->scan_tiles_cap) {
+        if (ctx->scan_status) {
+            HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+            HIP_TRY(ctx, hipFree(ctx->scan_status));
+            ctx->scan_status = nullptr;
+        }
+        const uint64_t cap = std::max<uint64_t>(next_pow2(tiles), 1024);
+        HIP_TRY(ctx, hipMalloc(&ctx->scan_status, cap * sizeof(unsigned long long)));
+        // zero words carry sequence 0, which no launch uses: "not ready"
+        HIP_TRY(ctx, hipMemsetAsync(ctx->scan_status, 0, cap * sizeof(unsigned long long), ctx->stream));
+        HIP_TRY(ctx, hipMemsetAsync(ctx->scan_ticket, 0, sizeof(unsigned int), ctx->stream));
+        ctx->scan_ticket_base = 0;
+        ctx->scan_tiles_cap = cap;
+    }
+    ctx->scan_seq = ctx->scan_seq % ((1u << 30) - 1) + 1;
+    ScanState st{ctx->scan_status, ctx->scan_ticket, ctx->scan_ticket_base, ctx->scan_seq};
+    ctx->scan_ticket_base += uint32_t(tiles);
+    hipLaunchKernelGGL(chained_scan<Op>, dim3(uint32_t(tiles)), dim3(kScanThreads), 0, ctx->stream,
+                       n, op, st);
+    return 0;
+}
+
+// Order-preserving selection of indices [0, n) whose flag is nonzero (one launch).
 int select_flagged(tbg_ctx* ctx, const uint8_t* flags, uint64_t n, uint32_t* out,
                    unsigned int* d_count) {
-    hipcub::CountingInputIterator<uint32_t> it(0);
-    size_t bytes = 0;
-    HIP_TRY(ctx, hipcub::DeviceSelect::Flagged(nullptr, bytes, it, flags, out, d_count, int(n),
-                                               ctx->stream));
-    int rc = ensure_cub_temp(ctx, bytes);
-    if (rc) return rc;
-    HIP_TRY(ctx, hipcub::DeviceSelect::Flagged(ctx->cub_temp, bytes, it, flags, out, d_count,
-                                               int(n), ctx->stream));
-    return 0;
+    return launch_scan(ctx, n, SelectFlags8{flags, out, d_count});
 }
 
 int sync_scalars(tbg_ctx* ctx) {
@@ -352,23 +381,23 @@ int end_call(tbg_ctx* ctx, uint32_t n, bool already_synced = false) {
 
 void free_flow(FlowScratch& F) {
     void* ptrs[] = {F.head8, F.barrier8, F.heads, F.unit_of, F.barriers, F.vals, F.vals_sorted,
-                    F.pred, F.done, F.keys, F.keys_sorted, F.pnt_ops, F.pnt_scan, F.steps,
-                    F.queue, F.ready8, F.recs, F.mailbox, F.owner_starts, F.owner_head8, F.mb_index,
-                    F.exp_flag, F.exp_index, F.contrib, F.prefix};
+                    F.succ, F.indeg, F.keys_sorted, F.pnt_ops, F.pnt_scan, F.steps, F.queue,
+                    F.outcome, F.recs, F.mailbox, F.owner_starts, F.mb_index, F.exp_flag,
+                    F.hkeys, F.hcnt, F.hoff, F.loc, F.rank, F.big};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
-    F.head8 = F.barrier8 = nullptr;
-    F.heads = F.unit_of = F.barriers = F.vals = F.vals_sorted = F.pred = F.done = nullptr;
-    F.keys = F.keys_sorted = F.pnt_ops = F.pnt_scan = nullptr;
+    F.head8 = F.barrier8 = F.outcome = nullptr;
+    F.heads = F.unit_of = F.barriers = F.vals = F.vals_sorted = F.succ = F.indeg = nullptr;
+    F.keys_sorted = F.pnt_ops = F.pnt_scan = nullptr;
     F.steps = nullptr;
     F.queue = nullptr;
-    F.ready8 = nullptr;
     F.recs = nullptr;
-    F.exp_flag = F.exp_index = nullptr;
-    F.contrib = F.prefix = nullptr;
+    F.exp_flag = nullptr;
     F.mailbox = F.owner_starts = F.mb_index = nullptr;
-    F.owner_head8 = nullptr;
-    F.cap = 0;
+    F.hkeys = nullptr;
+    F.hcnt = F.hoff = F.loc = F.rank = nullptr;
+    F.big = nullptr;
+    F.cap = F.slots = 0;
 }
 
 int ensure_flow(tbg_ctx* ctx, uint64_t m) {
@@ -376,7 +405,7 @@ int ensure_flow(tbg_ctx* ctx, uint64_t m) {
     bool ok = true;
     if (!F.dup_mark) {
         ok = dev_alloc(ctx, &F.dup_mark, ctx->opt.batch_events_max, true) &&
-             dev_alloc(ctx, &F.counts, 4, true) && dev_alloc(ctx, &F.pnt_fired, 1, true) &&
+             dev_alloc(ctx, &F.counts, 8, true) && dev_alloc(ctx, &F.words, 4, true) &&
              dev_alloc(ctx, &F.lane_counts, 4, true) &&
              dev_alloc(ctx, &F.lane_undo, uint64_t(kFlowLanesMax) * kFlowUndoPerLane, false) &&
              dev_alloc(ctx, &F.engine, kFlowEngineWords, true) &&
@@ -387,29 +416,32 @@ int ensure_flow(tbg_ctx* ctx, uint64_t m) {
     free_flow(F);
     const uint64_t cap = std::max<uint64_t>(next_pow2(m), 1u << 14);
     const uint64_t kc = kFlowKeys * cap;
+    const uint64_t slots = 2 * kc;  // grouping table load <= 0.5
     ok = dev_alloc(ctx, &F.head8, cap, false) && dev_alloc(ctx, &F.barrier8, cap, false) &&
          dev_alloc(ctx, &F.heads, cap, false) && dev_alloc(ctx, &F.unit_of, cap, false) &&
-         dev_alloc(ctx, &F.barriers, cap, false) && dev_alloc(ctx, &F.done, cap, true) &&
+         dev_alloc(ctx, &F.barriers, cap, false) && dev_alloc(ctx, &F.indeg, cap, true) &&
          dev_alloc(ctx, &F.pnt_ops, cap, false) && dev_alloc(ctx, &F.pnt_scan, cap, false) &&
          dev_alloc(ctx, &F.vals, kc, false) && dev_alloc(ctx, &F.vals_sorted, kc, false) &&
-         dev_alloc(ctx, &F.pred, kc, false) && dev_alloc(ctx, &F.keys, kc, false) &&
-         dev_alloc(ctx, &F.keys_sorted, kc, false) && dev_alloc(ctx, &F.steps, cap, false) &&
-         dev_alloc(ctx, &F.queue, cap, false) && dev_alloc(ctx, &F.ready8, cap + kFlowThreads, false) &&
-         dev_alloc(ctx, &F.recs, cap, false) && dev_alloc(ctx, &F.mailbox, cap, false) &&
-         dev_alloc(ctx, &F.mb_index, cap, false) &&
-         dev_alloc(ctx, &F.exp_flag, cap, false) && dev_alloc(ctx, &F.exp_index, cap, false) &&
-         dev_alloc(ctx, &F.contrib, kc, false) && dev_alloc(ctx, &F.prefix, kc, false) &&
-         dev_alloc(ctx, &F.owner_starts, kc, false) && dev_alloc(ctx, &F.owner_head8, kc, false);
+         dev_alloc(ctx, &F.succ, kc, false) && dev_alloc(ctx, &F.keys_sorted, kc, false) &&
+         dev_alloc(ctx, &F.steps, cap, false) && dev_alloc(ctx, &F.queue, cap, false) &&
+         dev_alloc(ctx, &F.outcome, cap, false) && dev_alloc(ctx, &F.recs, cap, false) &&
+         dev_alloc(ctx, &F.mailbox, cap, false) && dev_alloc(ctx, &F.mb_index, cap, false) &&
+         dev_alloc(ctx, &F.exp_flag, cap, false) && dev_alloc(ctx, &F.owner_starts, kc, false) &&
+         dev_alloc(ctx, &F.hkeys, slots, true) && dev_alloc(ctx, &F.hcnt, slots, true) &&
+         dev_alloc(ctx, &F.hoff, slots, false) && dev_alloc(ctx, &F.loc, kc, false) &&
+         dev_alloc(ctx, &F.rank, kc, false) && dev_alloc(ctx, &F.big, kc / kGroupSmall + 1, false);
     if (!ok) {
         free_flow(F);
         return TBG_EHIP;
     }
     F.cap = cap;
+    F.slots = slots;
     return 0;
 }
 
-// The flow replay of a create_transfers call (flow.hpp): plan the units and their keys, then
-// execute them on one workgroup; pulse_next_timestamp is resolved afterwards in post/void calls.
+// The flow replay of a create_transfers call (flow.hpp): plan the units and group their keys
+// (group.hpp), then run the account lanes (lanes.hpp) or the flow engine; pulse_next_timestamp is
+// resolved afterwards in post/void calls.
 int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned int call_flags) {
     int rc = ensure_flow(ctx, m);
     if (rc) return rc;
@@ -425,123 +457,103 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
     P.barrier8 = F.barrier8;
     P.barriers = F.barriers;
     P.dup_mark = F.dup_mark;
-    P.keys = F.keys;
-    P.vals = F.vals;
-    P.keys_sorted = F.keys_sorted;
-    P.vals_sorted = F.vals_sorted;
-    P.succ = F.pred;
-    P.indeg = F.done;
+    P.succ = F.succ;
+    P.indeg = F.indeg;
     P.queue = F.queue;
-    P.ready8 = F.ready8;
     const bool post_void = (call_flags & kFlagPostVoid) != 0;
     P.pnt_ops = post_void ? F.pnt_ops : nullptr;
     P.pnt_scan = F.pnt_scan;
-    P.pnt_fired = F.pnt_fired;
+    P.pnt_fired = &F.words[0];
     P.lane_undo = F.lane_undo;
     P.steps = F.steps;
     P.engine = F.engine;
     P.exp_flag = F.exp_flag;
-    P.exp_index = F.exp_index;
+    P.exp_base = &F.words[1];
+    P.lane_counts = F.lane_counts;
     // Additive accounts get no key (Replay::additive); TBG_NO_ADDITIVE keys every account.
     const bool lanes_possible =
         !(call_flags & (kFlagDuplicate | kFlagPostVoid | kFlagClosable | kFlagImported)) &&
         !c.force_replay && !getenv("TBG_NO_LANES");
     P.add_epoch = getenv("TBG_NO_ADDITIVE") ? 0 : c.epoch;
+
+    GroupPlan G{};
+    G.hmask = F.slots - 1;
+    G.hkeys = F.hkeys;
+    G.hcnt = F.hcnt;
+    G.hoff = F.hoff;
+    G.loc = F.loc;
+    G.rank = F.rank;
+    G.vals = F.vals;
+    G.vals_sorted = F.vals_sorted;
+    G.keys_sorted = F.keys_sorted;
+    G.big = F.big;
+    G.counts = F.counts + 4;
+    G.unit_of = F.unit_of;
+    G.succ = F.succ;
+    G.indeg = F.indeg;
+    G.lanes = lanes_possible;
+    G.free_owners = getenv("TBG_NO_FREE_OWNERS") == nullptr;
+    G.epoch = c.epoch;
+    G.owner_starts = F.owner_starts;
+    G.lane_counts = F.lane_counts;
+    G.recs = F.recs;
+    G.acc_free = F.acc_free;
+
+    LanePlan L{};
+    L.m = m;
+    L.keys_sorted = F.keys_sorted;
+    L.n_pairs = F.counts + 4;
+    L.steps = F.steps;
+    L.slow_list = c.slow_list;
+    L.recs = F.recs;
+    L.mailbox = F.mailbox;
+    L.mb_index = F.mb_index;
+    L.outcome = F.outcome;
+    L.owner_starts = F.owner_starts;
+    L.counts = F.lane_counts;
+    L.epoch = c.epoch;
+    L.acc_free = F.acc_free;
+
     const dim3 block(kBlock);
-    hipLaunchKernelGGL(flow_heads, dim3(grid_for(m)), block, 0, ctx->stream, ctx->T, c, P);
+    const uint64_t pairs = kFlowKeys * uint64_t(m);
+    hipLaunchKernelGGL(flow_heads, dim3(grid_for(std::max<uint64_t>(m, kFlowEngineWords))), block,
+                       0, ctx->stream, ctx->T, c, P);
     rc = select_flagged(ctx, F.head8, m, F.heads, &F.counts[0]);
     if (rc) return rc;
     hipLaunchKernelGGL(flow_units, dim3(grid_for(m)), block, 0, ctx->stream, P);
-    hipLaunchKernelGGL(flow_keys, dim3(grid_for(m)), block, 0, ctx->stream, ctx->T, c, P,
-                       call_flags);
-    {  // the planned expires_at entries
-        size_t sb = 0;
-        HIP_TRY(ctx, hipcub::DeviceScan::ExclusiveSum(nullptr, sb, F.exp_flag, F.exp_index, int(m),
-                                                      ctx->stream));
-        rc = ensure_cub_temp(ctx, sb);
-        if (rc) return rc;
-        HIP_TRY(ctx, hipcub::DeviceScan::ExclusiveSum(ctx->cub_temp, sb, F.exp_flag, F.exp_index,
-                                                      int(m), ctx->stream));
-        hipLaunchKernelGGL(flow_expiry, dim3(grid_for(m)), block, 0, ctx->stream, ctx->T, c, P);
-        hipLaunchKernelGGL(flow_expiry_count, dim3(1), dim3(64), 0, ctx->stream, ctx->T, P);
-    }
-    const int pairs = int(kFlowKeys * uint64_t(m));
-    size_t bytes = 0;
-    HIP_TRY(ctx, hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, F.keys, F.keys_sorted, F.vals,
-                                                    F.vals_sorted, pairs, 0, 64, ctx->stream));
-    rc = ensure_cub_temp(ctx, bytes);
+    hipLaunchKernelGGL(plan_keys, dim3((m + kPlanThreads - 1) / kPlanThreads), dim3(kPlanThreads), 0,
+                       ctx->stream, ctx->T, c, P, G, L, call_flags);
+    // the planned expires_at entries
+    rc = launch_scan(ctx, m,
+                     PlanExpiry{F.exp_flag, c.slow_list, ctx->T.expiry, ctx->T.expiry_capacity,
+                                c.row_base, &F.words[1],
+                                reinterpret_cast<unsigned long long*>(&ctx->T.scalars->expiry_count),
+                                &ctx->T.scalars->flags});
+    if (!rc) rc = launch_scan(ctx, F.slots, ExclusiveSumU32{F.hcnt, F.hoff, &F.counts[4]});
     if (rc) return rc;
-    HIP_TRY(ctx, hipcub::DeviceRadixSort::SortPairs(ctx->cub_temp, bytes, F.keys, F.keys_sorted,
-                                                    F.vals, F.vals_sorted, pairs, 0, 64,
-                                                    ctx->stream));
-    HIP_TRY(ctx, hipMemsetAsync(F.done, 0, uint64_t(m) * 4, ctx->stream));  // indeg
-    hipLaunchKernelGGL(flow_edges, dim3(grid_for(uint64_t(pairs))), block, 0, ctx->stream, P);
-    hipLaunchKernelGGL(flow_ready, dim3(grid_for(m)), block, 0, ctx->stream, P);
-    rc = select_flagged(ctx, F.barrier8, m, F.barriers, &F.counts[1]);
-    if (!rc) rc = select_flagged(ctx, F.ready8, m, F.queue, &F.counts[2]);
+    hipLaunchKernelGGL(group_scatter, dim3(grid_for(pairs)), block, 0, ctx->stream, G, pairs);
+    hipLaunchKernelGGL(group_small, dim3(grid_for(F.slots)), block, 0, ctx->stream, ctx->T, G,
+                       F.slots);
+    hipLaunchKernelGGL(group_big, dim3(kGroupBigBlocks), dim3(kGroupBigThreads), 0, ctx->stream,
+                       ctx->T, G);
+    rc = launch_scan(ctx, m, SelectReady{F.indeg, F.counts, F.queue, F.engine, &F.counts[2]});
+    if (!rc) rc = select_flagged(ctx, F.barrier8, m, F.barriers, &F.counts[1]);
     if (rc) return rc;
-    hipLaunchKernelGGL(flow_queue_init, dim3(grid_for(std::max<uint64_t>(m, kFlowEngineWords))), block, 0, ctx->stream, P);
-    if (post_void) {
-        HIP_TRY(ctx, hipMemsetAsync(F.pnt_ops, 0, uint64_t(m) * 8, ctx->stream));
-        HIP_TRY(ctx, hipMemsetAsync(F.pnt_fired, 0, 8, ctx->stream));
-    }
     // Calls of limit events only: the account lanes (lanes.hpp); the flow replay then skips.
     P.skip = nullptr;
     if (lanes_possible) {
-        LanePlan L{};
-        L.m = m;
-        L.keys_sorted = F.keys_sorted;
-        L.n_pairs = uint64_t(pairs);
-        L.steps = F.steps;
-        L.slow_list = c.slow_list;
-        L.recs = F.recs;
-        L.mailbox = F.mailbox;
-        L.mb_index = F.mb_index;
-        L.outcome = F.ready8;  // (free once the flow plan's queue is built)
-        L.owner_head8 = F.owner_head8;
-        L.owner_starts = F.owner_starts;
-        L.counts = F.lane_counts;
-        HIP_TRY(ctx, hipMemsetAsync(F.lane_counts, 0, 16, ctx->stream));
-        hipLaunchKernelGGL(lanes_check, dim3(grid_for(m)), block, 0, ctx->stream, ctx->T, c, P, L);
         // One-lane walk (lanes_replay): LDS mailbox indexes. Wave walk (lanes_walk, the
-        // default): a zeroed word per position in global memory.
+        // default): a zeroed word per position (plan_keys).
         const bool one_lane = getenv("TBG_LANES_ONE_LANE") != nullptr;
         if (one_lane) {
-            size_t sb = 0;
-            HIP_TRY(ctx, hipcub::DeviceScan::ExclusiveSum(nullptr, sb, F.mailbox, F.mb_index,
-                                                          int(m), ctx->stream));
-            rc = ensure_cub_temp(ctx, sb);
+            rc = launch_scan(ctx, m, ExclusiveSumU32{F.mailbox, F.mb_index, nullptr});
             if (rc) return rc;
-            HIP_TRY(ctx, hipcub::DeviceScan::ExclusiveSum(ctx->cub_temp, sb, F.mailbox,
-                                                          F.mb_index, int(m), ctx->stream));
             hipLaunchKernelGGL(lanes_mailboxes, dim3(grid_for(m)), block, 0, ctx->stream, L);
-        } else {
-            HIP_TRY(ctx, hipMemsetAsync(F.mb_index, 0, uint64_t(m) * 4, ctx->stream));
         }
-        hipLaunchKernelGGL(lanes_segments, dim3(grid_for(uint64_t(pairs))), block, 0, ctx->stream,
-                           ctx->T, L);
-        rc = select_flagged(ctx, F.owner_head8, uint64_t(pairs), F.owner_starts, &F.lane_counts[0]);
-        if (rc) return rc;
         tmark(ctx, "flow_plan");
-        // Free owners (lanes.hpp): contributions, their u128 prefix sums, the owners' verdicts,
-        // their events' owner bits.
-        L.epoch = c.epoch;
-        L.acc_free = F.acc_free;
-        L.contrib = F.contrib;
-        L.prefix = F.prefix;
-        if (!getenv("TBG_NO_FREE_OWNERS")) {
-            hipLaunchKernelGGL(lanes_contrib, dim3(grid_for(uint64_t(pairs))), block, 0, ctx->stream,
-                               ctx->T, L);
-            size_t pb = 0;
-            HIP_TRY(ctx, hipcub::DeviceScan::InclusiveSum(nullptr, pb, F.contrib, F.prefix, pairs,
-                                                          ctx->stream));
-            rc = ensure_cub_temp(ctx, pb);
-            if (rc) return rc;
-            HIP_TRY(ctx, hipcub::DeviceScan::InclusiveSum(ctx->cub_temp, pb, F.contrib, F.prefix,
-                                                          pairs, ctx->stream));
-            hipLaunchKernelGGL(lanes_owner_free, dim3(grid_for(2 * uint64_t(m))), block, 0, ctx->stream, ctx->T, L);
+        // Free owners (their verdicts: the grouping): their events' owner bits.
+        if (!getenv("TBG_NO_FREE_OWNERS"))
             hipLaunchKernelGGL(lanes_free, dim3(grid_for(m)), block, 0, ctx->stream, ctx->T, L);
-        }
         if (one_lane)
             hipLaunchKernelGGL(lanes_replay, dim3(1), dim3(kLanesMax), 0, ctx->stream, ctx->T, c, L);
         else {
@@ -593,13 +605,14 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
     if (debug) {
         unsigned int cnt[2] = {0, 0};
         unsigned long long d[12] = {};
-        unsigned int cnt3[3] = {};
-        (void)hipMemcpyAsync(cnt3, F.counts, 12, hipMemcpyDeviceToHost, ctx->stream);
+        unsigned int cnt3[8] = {};
+        (void)hipMemcpyAsync(cnt3, F.counts, 32, hipMemcpyDeviceToHost, ctx->stream);
         (void)hipMemcpyAsync(d, ctx->flow_debug, 96, hipMemcpyDeviceToHost, ctx->stream);
         cnt[0] = cnt3[0];
         cnt[1] = cnt3[1];
-        fprintf(stderr, "flow: initially ready %u\n", cnt3[2]);
         (void)hipStreamSynchronize(ctx->stream);
+        fprintf(stderr, "flow: initially ready %u grouped pairs %u listed segments %u longest id "
+                "key %u longest account key %u\n", cnt3[2], cnt3[4], cnt3[5], cnt3[6], cnt3[7]);
         // wall_clock64 runs at 100 MHz on MI300-class parts
         fprintf(stderr, "flow: m=%u units=%u barriers=%u flags=%#x lanes=%u iterations=%llu "
                 "events=%llu exec_us=%.1f engine_us=%.1f\n", m, cnt[0], cnt[1], call_flags, lanes,
@@ -1032,7 +1045,8 @@ void tbg_close(tbg_ctx* ctx) {
                     ctx->cub_temp, ctx->acc_ts_index, ctx->tr_ts_index, ctx->sel_buf,
                     ctx->pulse.keep, ctx->pulse.exp, ctx->pulse.ts, ctx->pulse.rows,
                     ctx->pulse.exp_b, ctx->pulse.rows_b, ctx->pulse.counters,
-                    ctx->flow.dup_mark, ctx->flow.counts, ctx->flow.pnt_fired, ctx->flow.lane_counts,
+                    ctx->flow.dup_mark, ctx->flow.counts, ctx->flow.words, ctx->flow.lane_counts,
+                    ctx->scan_status, ctx->scan_ticket,
                     ctx->flow.lane_undo, ctx->flow.engine, ctx->flow.acc_free,
                     ctx->ae_log, ctx->ae_ref, ctx->ae_flags, ctx->ae_list, ctx->ae_words,
                     ctx->ae.keys, ctx->ae.vals, ctx->ae.keys_sorted, ctx->ae.vals_sorted,

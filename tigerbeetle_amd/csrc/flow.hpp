@@ -24,8 +24,8 @@
 // handled in Replay (replay.hpp: key_range, pulse_next_timestamp, the expires_at list).
 //
 // Order. A unit may execute an event once, for each key of the event, the previous unit holding
-// that key (in call order) has finished -- its "predecessor", from a radix sort of (key, unit)
-// pairs. Waiting on the immediate predecessor is enough: it waited on its own. Units are taken in
+// that key (in call order) has finished -- its "predecessor", from the grouping of the (key, unit)
+// pairs by key (group.hpp). Waiting on the immediate predecessor is enough: it waited on its own. Units are taken in
 // call order, and each waits only on earlier units, so the earliest unfinished unit can always
 // run: the replay always progresses and every lane reaches the exit. A barrier unit runs alone:
 // every earlier unit has finished and no later unit starts until it has.
@@ -58,19 +58,14 @@ struct FlowPlan {
     const uint32_t* slow_list;
     uint8_t* head8;              // per position: starts a unit
     uint32_t* heads;             // per unit: its first position
-    unsigned int* counts;        // [0] units, [1] barriers
+    unsigned int* counts;        // [0] units, [1] barriers, [2] initially ready units
     uint32_t* unit_of;           // per position
     uint8_t* barrier8;           // per unit (positions >= units hold 0)
     uint32_t* barriers;          // barrier units, in order
     uint32_t* dup_mark;          // per event of the call: an in-call holder with later claimants
-    uint64_t* keys;              // kFlowKeys per position: (type:1 | index:32 | unit:31)
-    uint32_t* vals;              // kFlowKeys * position + j
-    uint64_t* keys_sorted;
-    uint32_t* vals_sorted;
     uint32_t* succ;              // kFlowKeys per position: successor unit or kNone32
     uint32_t* indeg;             // per unit: predecessors not yet finished
     uint32_t* queue;             // ready units (unit + 1; 0 = not yet pushed)
-    uint8_t* ready8;             // per unit: no predecessor
     uint64_t* pnt_ops;           // per position (post/void calls), else null
     uint64_t* pnt_scan;
     unsigned long long* pnt_fired;
@@ -78,7 +73,8 @@ struct FlowPlan {
     struct Step* steps;          // per position: what the engine prefetches before it waits
     const unsigned int* skip;    // nonzero: the account lanes replayed the call (lanes.hpp)
     uint32_t* exp_flag;          // per position: may append to the expires_at index
-    uint32_t* exp_index;         // exclusive prefix sum of exp_flag
+    unsigned long long* exp_base;  // expiry_count at the plan's start (flow_heads)
+    unsigned int* lane_counts;   // the account lanes' counters (zeroed by flow_heads)
     uint32_t add_epoch;          // nonzero: additive accounts get no key (Replay::additive)
     unsigned int* engine;        // [0] q_head, [32] q_tail, [64 + 32 j] units_done shard j
                                  // (kFlowDoneShards; one 128-byte line each)
@@ -106,6 +102,14 @@ __device__ inline uint32_t flow_id_key(const tb_uint128_t& id) { return uint32_t
 // Unit heads and duplicate holders.
 __global__ void flow_heads(Tables T, Call<tb_transfer_t> c, FlowPlan P) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    // Per-call counters, zeroed here (grid >= kFlowEngineWords): the engine's q_head, q_tail and
+    // done shards, the lanes' counters, the grouping's listed segments, pulse_next_timestamp's flag.
+    if (s < kFlowEngineWords) P.engine[s] = 0;
+    if (s < 4) P.lane_counts[s] = 0;
+    if (s == 0) {
+        P.counts[5] = P.counts[6] = P.counts[7] = 0;
+        *P.pnt_fired = 0;
+    }
     if (s >= P.m) return;
     const uint32_t k = P.slow_list[s];
     bool head = true;
@@ -115,6 +119,9 @@ __global__ void flow_heads(Tables T, Call<tb_transfer_t> c, FlowPlan P) {
         head = batch_start_of(c, b) == k;
     }
     P.head8[s] = head;
+    P.queue[s] = 0;  // (the ready units are selected into it after the grouping)
+    if (P.pnt_ops) P.pnt_ops[s] = 0;
+    if (s == 0) *P.exp_base = T.scalars->expiry_count;
     const uint32_t slot = c.ev_slot[k];
     if (slot != kNone32) {
         const uint64_t w = T.tr.slots[slot];
@@ -138,131 +145,6 @@ __global__ void flow_units(FlowPlan P) {
     const uint32_t end = u + 1 < units ? P.heads[u + 1] : P.m;
     for (uint32_t s = begin; s < end; s++) P.unit_of[s] = u;
     P.barrier8[u] = end - begin > kFlowChainMax;
-}
-
-// The keys of each replayed event.
-__global__ void flow_keys(Tables T, Call<tb_transfer_t> c, FlowPlan P, unsigned int call_flags) {
-    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= P.m) return;
-    const uint32_t k = P.slow_list[s];
-    const uint32_t u = P.unit_of[s];
-    const tb_transfer_t& t = c.events[k];
-    uint64_t key[kFlowKeys] = {kFlowNoKey, kFlowNoKey, kFlowNoKey, kFlowNoKey};
-    // Additive accounts need no ordering (Replay::additive, replay.hpp).
-    auto keyless = [&](uint64_t row) { return acc_additive(T, row, P.add_epoch); };
-    if (!u128_is_zero(t.id) && !u128_is_max(t.id)) key[0] = flow_key(0, flow_id_key(t.id), u);
-    if (t.flags & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) {
-        if (!u128_is_zero(t.pending_id) && !u128_is_max(t.pending_id)) {
-            key[1] = flow_key(0, flow_id_key(t.pending_id), u);
-            // The pending transfer's accounts: the committed row's, or its in-call creator's.
-            bool certain = true;
-            const tb_transfer_t* p = nullptr;
-            const uint64_t ps = transfer_slot_find(T, c, t.pending_id);
-            if (ps == kNone) {
-                // Not found now; with duplicate ids in the call a later claimant may create it.
-                certain = !(call_flags & kFlagDuplicate);
-            } else {
-                const uint64_t w = T.tr.slots[ps];
-                const uint64_t r = (w & kRefMask) - 1;
-                if (r < c.row_base) {
-                    if (!(w & kOrphanBit)) p = &T.tr_rows[r];
-                } else {
-                    const uint32_t j = uint32_t(r - c.row_base);
-                    if (P.dup_mark[j] == P.epoch) certain = false;
-                    else p = &c.events[j];
-                }
-            }
-            if (!certain) {
-                P.barrier8[u] = 1;
-            } else if (p) {
-                const uint64_t dr = account_find(T, p->debit_account_id);
-                const uint64_t cr = account_find(T, p->credit_account_id);
-                if (dr != kNone && !keyless(dr)) key[2] = flow_key(1, uint32_t(dr), u);
-                if (cr != kNone && !keyless(cr)) key[3] = flow_key(1, uint32_t(cr), u);
-            }
-        }
-    } else {
-        const uint32_t dr = c.ev_dr[k], cr = c.ev_cr[k];
-        if (dr != kNone32 && !keyless(dr)) key[2] = flow_key(1, dr, u);
-        if (cr != kNone32 && !keyless(cr)) key[3] = flow_key(1, cr, u);
-    }
-    // The expires_at entry a created pending transfer with a timeout appends (planned here: one
-    // slot per candidate position; a candidate that fails or whose chain is discarded leaves an
-    // entry of a row that is not live, dropped at the next pulse).
-    P.exp_flag[s] = (t.flags & TB_TRANSFER_PENDING) && t.timeout > 0 &&
-                    !(t.flags & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING));
-    const StepInfo si = step_info(c, k, uint16_t(TB_TRANSFER_IMPORTED));
-    const EvRefs x = ev_refs(c, k);
-    Step st;
-    st.ts_event = si.ts_event;
-    st.batch = si.batch;
-    st.flags = si.flags;
-    st.k = k;
-    st.slot = x.slot;
-    st.dr = x.dr;
-    st.cr = x.cr;
-    P.steps[s] = st;
-#pragma unroll
-    for (uint32_t j = 0; j < kFlowKeys; j++) {
-        P.keys[kFlowKeys * uint64_t(s) + j] = key[j];
-        P.vals[kFlowKeys * uint64_t(s) + j] = kFlowKeys * s + j;
-    }
-}
-
-// The planned expires_at entries (flow_keys): candidate s takes slot expiry_count + exp_index[s].
-__global__ void flow_expiry(Tables T, Call<tb_transfer_t> c, FlowPlan P) {
-    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= P.m || !P.exp_flag[s]) return;
-    const uint64_t i = T.scalars->expiry_count + P.exp_index[s];
-    if (i < T.expiry_capacity) T.expiry[i] = c.row_base + P.slow_list[s];
-    else atomicOr(&T.scalars->flags, kFlagTableFull);
-}
-__global__ void flow_expiry_count(Tables T, FlowPlan P) {
-    if (threadIdx.x != 0 || blockIdx.x != 0 || P.m == 0) return;
-    const uint64_t n = T.scalars->expiry_count + P.exp_index[P.m - 1] + P.exp_flag[P.m - 1];
-    T.scalars->expiry_count = n < T.expiry_capacity ? n : T.expiry_capacity;
-}
-
-// The edges of the unit graph, from the (key, unit) pairs in key order: a pair whose previous
-// pair has the same key and another unit gets an edge from that unit (its predecessor on the key);
-// the last pair of a (key, unit) group records the next unit on the key (its successor). A key
-// repeated within a chain yields one edge. indeg counts each unit's edges.
-__global__ void flow_edges(FlowPlan P) {
-    const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    const uint64_t n = kFlowKeys * uint64_t(P.m);
-    if (i >= n) return;
-    const uint64_t key = P.keys_sorted[i];
-    constexpr uint64_t kUnitMask = (1u << kFlowUnitBits) - 1;
-    uint32_t succ = kNone32;
-    if (key != kFlowNoKey) {
-        const uint32_t unit = uint32_t(key & kUnitMask);
-        if (i > 0) {
-            const uint64_t prev = P.keys_sorted[i - 1];
-            if ((prev >> kFlowUnitBits) == (key >> kFlowUnitBits) && uint32_t(prev & kUnitMask) != unit)
-                atomicAdd(&P.indeg[unit], 1u);
-        }
-        if (i + 1 < n) {
-            const uint64_t next = P.keys_sorted[i + 1];
-            if ((next >> kFlowUnitBits) == (key >> kFlowUnitBits) && uint32_t(next & kUnitMask) != unit)
-                succ = uint32_t(next & kUnitMask);
-        }
-    }
-    P.succ[P.vals_sorted[i]] = succ;
-}
-
-__global__ void flow_ready(FlowPlan P) {
-    const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
-    if (u >= P.m) return;
-    P.ready8[u] = u < P.counts[0] && P.indeg[u] == 0;
-}
-
-// Initially ready units (selected in order into the queue, raw) -> queue entries unit + 1; the
-// rest of the queue empty.
-__global__ void flow_queue_init(FlowPlan P) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < kFlowEngineWords) P.engine[i] = i == 32 ? P.counts[2] : 0;  // q_head, q_tail, done
-    if (i >= P.counts[0]) return;
-    P.queue[i] = i < P.counts[2] ? P.queue[i] + 1 : 0;
 }
 
 // The engine: lanes spread over `blocks` workgroups (see the header). A unit is ready once every

@@ -1,0 +1,580 @@
+// The flow plan's key grouping: each replayed event's keys (flow.hpp header) grouped by key, every
+// group in call order -- what the flow replay's edges and the account lanes' walks are read from.
+//
+// A library radix sort of the 64-bit (key, unit) words took ~20 launches per call (merge passes)
+// and the lanes' pre-passes another ~10; the grouping here is five launches, none of them a sort of
+// the whole pair array:
+//
+//   plan_keys      per replayed event: its keys (flow_keys' rules), its step record, the lanes'
+//                  eligibility and record (lanes_check's rules); each key is inserted into an HBM
+//                  hash table (key -> slot, CAS on an empty word) and counted. The counts of one
+//                  workgroup are first summed per slot in LDS, so a hot account's thousands of pairs
+//                  cost one global atomic per workgroup, and each pair keeps its arrival rank.
+//   chained_scan   the slots' exclusive sums: every key's segment in the grouped array.
+//   group_scatter  pair -> its segment at its rank (arrival order, not yet call order).
+//   group_small    per slot: a segment of <= 16 pairs is sorted in registers by pair index (pair
+//                  index 4 * position + j grows with the unit); larger ones are listed. Then the
+//                  segment's edges (a pair whose predecessor in the segment belongs to another
+//                  unit adds to that unit's in-degree; the last pair of a unit's run names the
+//                  next unit as its successor), its (key, unit) words, and -- for the account lanes
+//                  -- owner segments with their free-owner verdict (lanes.hpp). The slot is
+//                  cleared for the next call (the table is never memset).
+//   group_big      per listed segment, one workgroup: <= 8192 pairs by a bitonic sort in LDS,
+//                  more by bitmaps of 2^20 pair indices in LDS (set bits, prefix popcounts,
+//                  enumerate); then the same per-segment work.
+//
+// Segments are disjoint and each is in call order, which is all the consumers read: flow_replay
+// (succ / indeg), lanes_walk / lanes_replay (a segment ends where the key changes; the grouped
+// pair count bounds the array). The order of the segments themselves is arbitrary.
+#pragma once
+
+#include "lanes.hpp"
+#include "prims.hpp"
+
+namespace tbg {
+
+constexpr uint32_t kGroupSmall = 16;        // segments sorted in registers
+constexpr uint32_t kGroupBigThreads = 512;
+constexpr uint32_t kGroupMedium = 8192;     // segments sorted by an LDS bitonic sort
+constexpr uint32_t kGroupLdsWords = 32768;  // 128 KB: bitonic vals + units, or one bitmap window
+constexpr uint32_t kGroupWindowBits = kGroupLdsWords * 32;
+constexpr uint32_t kGroupBigBlocks = 256;
+constexpr uint32_t kGroupBatch = 8;         // pairs per lane per batch of loads (group_big)
+constexpr uint32_t kPlanThreads = 256;      // plan_keys workgroup: 1024 pairs
+constexpr uint32_t kPlanLdsSlots = 2048;    // LDS aggregation table (load <= 0.5)
+
+struct GroupPlan {
+    uint64_t hmask;                 // hash slots - 1
+    unsigned long long* hkeys;      // per slot: key + 1 (0 empty); key = type << 32 | index
+    uint32_t* hcnt;                 // per slot: pairs
+    uint32_t* hoff;                 // per slot: exclusive sum of hcnt
+    uint32_t* loc;                  // per pair: slot (kNone32: no key)
+    uint32_t* rank;                 // per pair: arrival rank within its slot
+    uint32_t* vals;                 // grouped pair indices (arrival order within a segment)
+    uint32_t* vals_sorted;          // large segments: pair indices in order
+    uint64_t* keys_sorted;          // grouped (key, unit) words: flow_key(type, index, unit)
+    uint4* big;                     // listed segments: {offset, count, key lo, key hi}
+    unsigned int* counts;           // [0] grouped pairs, [1] listed segments, [2] / [3] the
+                                    // longest id-key / account-key segment (pairs)
+    const uint32_t* unit_of;        // per position
+    uint32_t* succ;                 // per pair
+    uint32_t* indeg;                // per unit
+    // account lanes (lanes.hpp): owner segments and free owners; lanes == false: none
+    bool lanes;
+    bool free_owners;               // free-owner verdicts (TBG_NO_FREE_OWNERS: none)
+    uint32_t epoch;
+    uint32_t* owner_starts;
+    unsigned int* lane_counts;      // [0] owners, [1] ineligible events
+    const LaneRec* recs;            // per position
+    uint32_t* acc_free;             // per account row
+};
+
+__device__ inline uint64_t group_hash(uint64_t key) { return mix64(key ^ 0x94D049BB133111EBull); }
+
+// The slot of `key` in the grouping table (inserting it). Words only go 0 -> key + 1, so a stale 0
+// read is settled by the CAS and a nonzero read is final.
+__device__ inline uint32_t group_slot(const GroupPlan& G, uint64_t key) {
+    const unsigned long long tag = key + 1;
+    uint64_t s = group_hash(key) & G.hmask;
+    while (true) {
+        unsigned long long w = G.hkeys[s];
+        if (w == 0) {
+            w = atomicCAS(&G.hkeys[s], 0ull, tag);
+            if (w == 0) return uint32_t(s);
+        }
+        if (w == tag) return uint32_t(s);
+        s = (s + 1) & G.hmask;
+    }
+}
+
+// Everything per replayed event s (flow_keys' and lanes_check's rules); its keys' grouping slots
+// and ranks. Launched with kPlanThreads per workgroup.
+__global__ void __launch_bounds__(kPlanThreads) plan_keys(Tables T, Call<tb_transfer_t> c,
+                                                          FlowPlan P, GroupPlan G,
+                                                          LanePlan L, unsigned int call_flags) {
+    __shared__ uint32_t agg_slot[kPlanLdsSlots];
+    __shared__ uint32_t agg_count[kPlanLdsSlots];
+    for (uint32_t i = threadIdx.x; i < kPlanLdsSlots; i += kPlanThreads) {
+        agg_slot[i] = kNone32;
+        agg_count[i] = 0;
+    }
+    __syncthreads();
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t key[kFlowKeys] = {kFlowNoKey, kFlowNoKey, kFlowNoKey, kFlowNoKey};
+    uint32_t local[kFlowKeys] = {kNone32, kNone32, kNone32, kNone32};
+    uint32_t lrank[kFlowKeys] = {0, 0, 0, 0};
+    bool ineligible = false;
+    if (s < P.m) {
+        const uint32_t k = P.slow_list[s];
+        const uint32_t u = P.unit_of[s];
+        const tb_transfer_t& t = c.events[k];
+        auto keyless = [&](uint64_t row) { return acc_additive(T, row, P.add_epoch); };
+        if (!u128_is_zero(t.id) && !u128_is_max(t.id)) key[0] = flow_id_key(t.id);
+        if (t.flags & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) {
+            if (!u128_is_zero(t.pending_id) && !u128_is_max(t.pending_id)) {
+                key[1] = flow_id_key(t.pending_id);
+                // The pending transfer's accounts: the committed row's, or its in-call creator's.
+                bool certain = true;
+                const tb_transfer_t* p = nullptr;
+                const uint64_t ps = transfer_slot_find(T, c, t.pending_id);
+                if (ps == kNone) {
+                    // Not found now; with duplicate ids in the call a later claimant may create it.
+                    certain = !(call_flags & kFlagDuplicate);
+                } else {
+                    const uint64_t w = T.tr.slots[ps];
+                    const uint64_t r = (w & kRefMask) - 1;
+                    if (r < c.row_base) {
+                        if (!(w & kOrphanBit)) p = &T.tr_rows[r];
+                    } else {
+                        const uint32_t j = uint32_t(r - c.row_base);
+                        if (P.dup_mark[j] == P.epoch) certain = false;
+                        else p = &c.events[j];
+                    }
+                }
+                if (!certain) {
+                    P.barrier8[u] = 1;
+                } else if (p) {
+                    const uint64_t dr = account_find(T, p->debit_account_id);
+                    const uint64_t cr = account_find(T, p->credit_account_id);
+                    if (dr != kNone && !keyless(dr)) key[2] = (1ull << 32) | uint32_t(dr);
+                    if (cr != kNone && !keyless(cr)) key[3] = (1ull << 32) | uint32_t(cr);
+                }
+            }
+        } else {
+            const uint32_t dr = c.ev_dr[k], cr = c.ev_cr[k];
+            if (dr != kNone32 && !keyless(dr)) key[2] = (1ull << 32) | dr;
+            if (cr != kNone32 && !keyless(cr)) key[3] = (1ull << 32) | cr;
+        }
+        // The expires_at entry a created pending transfer with a timeout appends (planned: one
+        // slot per candidate position; a candidate that fails or whose chain is discarded leaves
+        // an entry of a row that is not live, dropped at the next pulse).
+        P.exp_flag[s] = (t.flags & TB_TRANSFER_PENDING) && t.timeout > 0 &&
+                        !(t.flags & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING));
+        const StepInfo si = step_info(c, k, uint16_t(TB_TRANSFER_IMPORTED));
+        const EvRefs x = ev_refs(c, k);
+        Step st;
+        st.ts_event = si.ts_event;
+        st.batch = si.batch;
+        st.flags = si.flags;
+        st.k = k;
+        st.slot = x.slot;
+        st.dr = x.dr;
+        st.cr = x.cr;
+        P.steps[s] = st;
+        P.indeg[s] = 0;  // (units < m)
+        *reinterpret_cast<uint4*>(G.succ + kFlowKeys * uint64_t(s)) =
+            make_uint4(kNone32, kNone32, kNone32, kNone32);
+        if (G.lanes) {
+            // lanes_check: a limit event (lanes.hpp header) or an ineligible one.
+            bool ok = st.dr != kNone32 && st.cr != kNone32 && st.slot != kNone32 && st.dr != st.cr;
+            ok = ok && P.heads[u] == s &&
+                 (u + 1 == P.counts[0] ? s + 1 == L.m : P.heads[u + 1] == s + 1);
+            ok = ok && t.flags == 0 && t.timeout == 0 && u128_is_zero(t.pending_id) &&
+                 t.amount.hi == 0 && t.timestamp == 0 && !(st.flags & StepInfo::kBatchImported);
+            uint32_t bits = 0;
+            if (ok) {
+                const uint64_t w = T.tr.slots[st.slot];
+                ok = w != kEmpty && w != kTomb && (w & kRefMask) == c.row_base + k + 1;
+                const tb_account_t& dr = T.acc_rows[st.dr];
+                const tb_account_t& cr = T.acc_rows[st.cr];
+                ok = ok && !((dr.flags | cr.flags) & TB_ACCOUNT_CLOSED) && lanes_low(dr) &&
+                     lanes_low(cr) && dr.ledger == cr.ledger && t.ledger == dr.ledger &&
+                     t.code != 0 && t.ledger != 0 && !u128_is_zero(t.id) && !u128_is_max(t.id);
+                if (lanes_owner(dr.flags)) bits |= kLaneDrOwner;
+                if (lanes_owner(cr.flags)) bits |= kLaneCrOwner;
+                if (dr.flags & TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS) bits |= kLaneDrDecides;
+                if (cr.flags & TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS) bits |= kLaneCrDecides;
+                ok = ok && (bits & (kLaneDrOwner | kLaneCrOwner)) != 0;
+            }
+            L.mailbox[s] = ok && (bits & (kLaneDrOwner | kLaneCrOwner)) ==
+                                     (kLaneDrOwner | kLaneCrOwner);
+            L.mb_index[s] = 0;  // the walk's verdict words (one-lane mode: rewritten)
+            ineligible = !ok;
+            if (ok) {
+                LaneRec r;
+                r.amount = t.amount.lo;
+                r.dr = st.dr;
+                r.bits = bits;
+                L.recs[s] = r;
+            }
+        }
+        // Grouping: the global slot, then this workgroup's count of the slot in LDS.
+#pragma unroll
+        for (uint32_t j = 0; j < kFlowKeys; j++) {
+            if (key[j] == kFlowNoKey) continue;
+            const uint32_t slot = group_slot(G, key[j]);
+            uint32_t h = uint32_t(mix64(slot)) & (kPlanLdsSlots - 1);
+            while (true) {
+                const uint32_t o = atomicCAS(&agg_slot[h], kNone32, slot);
+                if (o == kNone32 || o == slot) break;
+                h = (h + 1) & (kPlanLdsSlots - 1);
+            }
+            local[j] = h;
+            lrank[j] = atomicAdd(&agg_count[h], 1u);
+        }
+    }
+    if (G.lanes) {
+        const uint64_t bad = __ballot(ineligible);
+        if ((threadIdx.x & 63) == 0 && bad) atomicAdd(&L.counts[1], uint32_t(__popcll(bad)));
+    }
+    __syncthreads();
+    // One global add per slot of this workgroup: agg_count becomes the slot's base.
+    for (uint32_t i = threadIdx.x; i < kPlanLdsSlots; i += kPlanThreads) {
+        const uint32_t slot = agg_slot[i];
+        if (slot != kNone32) agg_count[i] = atomicAdd(&G.hcnt[slot], agg_count[i]);
+    }
+    __syncthreads();
+    if (s >= P.m) return;
+#pragma unroll
+    for (uint32_t j = 0; j < kFlowKeys; j++) {
+        const uint64_t pair = kFlowKeys * uint64_t(s) + j;
+        if (local[j] == kNone32) {
+            G.loc[pair] = kNone32;
+        } else {
+            G.loc[pair] = agg_slot[local[j]];
+            G.rank[pair] = agg_count[local[j]] + lrank[j];
+        }
+    }
+}
+
+__global__ void group_scatter(GroupPlan G, uint64_t pairs) {
+    const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= pairs) return;
+    const uint32_t slot = G.loc[i];
+    if (slot == kNone32) return;
+    G.vals[G.hoff[slot] + G.rank[i]] = uint32_t(i);
+}
+
+// Pair v of a segment at grouped position `at` (key `key`), its unit u, and the units of its
+// neighbours in the segment (kNone32 at the ends): the (key, unit) word, the successor, and the
+// in-degree edge.
+__device__ inline void group_emit(const GroupPlan& G, uint64_t at, uint64_t key, uint32_t v,
+                                  uint32_t u, uint32_t u_prev, uint32_t u_next) {
+    G.keys_sorted[at] = (key << kFlowUnitBits) | u;
+    G.succ[v] = (u_next != kNone32 && u_next != u) ? u_next : kNone32;
+    if (u_prev != kNone32 && u_prev != u) atomicAdd(&G.indeg[u], 1u);
+}
+
+// The free-owner verdict of an owner segment from the sum of the amounts its limit checks
+// (lanes.hpp, free owners).
+__device__ inline void group_owner_verdict(Tables T, const GroupPlan& G, uint32_t row, u128 sum) {
+    const tb_account_t& a = T.acc_rows[row];
+    const u128 dpe = U(a.debits_pending), dpo = U(a.debits_posted);
+    const u128 cpe = U(a.credits_pending), cpo = U(a.credits_posted);
+    // (every balance < 2^126 and the sum < 2^96 for an eligible call: no wrap below)
+    if (!G.free_owners) return;
+    bool free = true;
+    if (a.flags & TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS) free = free && dpe + dpo + sum <= cpo;
+    if (a.flags & TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS) free = free && cpe + cpo + sum <= dpo;
+    if (free) G.acc_free[row] = G.epoch;
+}
+
+// The amount owner `row` checks on pair v's event (0: none).
+__device__ inline uint64_t group_owner_contrib(const GroupPlan& G, uint32_t row, uint32_t v) {
+    const LaneRec r = G.recs[v / kFlowKeys];
+    const bool debit = r.dr == row;
+    return (debit ? (r.bits & kLaneDrDecides) : (r.bits & kLaneCrDecides)) ? r.amount : 0;
+}
+
+// Is this segment an account lanes owner of a call the lanes run (every replayed event eligible)?
+__device__ inline bool group_owner_probe(Tables T, const GroupPlan& G, uint64_t key) {
+    return G.lanes && (key >> 32) == 1 && G.lane_counts[1] == 0 &&
+           lanes_owner(T.acc_rows[uint32_t(key)].flags);
+}
+// Registers an owner segment (owner_starts; any order: one walk per owner).
+__device__ inline void group_owner_add(const GroupPlan& G, uint32_t off) {
+    G.owner_starts[atomicAdd(&G.lane_counts[0], 1u)] = off;
+}
+
+template <int N>
+__device__ inline void sort_network(uint32_t (&v)[N]) {
+#pragma unroll
+    for (int k = 2; k <= N; k <<= 1)
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1)
+#pragma unroll
+            for (int i = 0; i < N; i++) {
+                const int l = i ^ j;
+                if (l > i) {
+                    const bool up = (i & k) == 0;
+                    const uint32_t a = v[i], b = v[l];
+                    if ((a > b) == up) {
+                        v[i] = b;
+                        v[l] = a;
+                    }
+                }
+            }
+}
+
+__global__ void group_small(Tables T, GroupPlan G, uint64_t slots) {
+    const uint64_t h = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (h >= slots) return;
+    const uint32_t c = G.hcnt[h];
+    if (c == 0) return;
+    const uint64_t key = G.hkeys[h] - 1;
+    const uint32_t off = G.hoff[h];
+    G.hkeys[h] = 0;
+    G.hcnt[h] = 0;
+    if (c > 1) atomicMax(&G.counts[2 + (key >> 32)], c);
+    if (c > kGroupSmall) {
+        const uint32_t b = atomicAdd(&G.counts[1], 1u);
+        G.big[b] = make_uint4(off, c, uint32_t(key), uint32_t(key >> 32));
+        return;
+    }
+    if (c == 1) {
+        const uint32_t v = G.vals[off];
+        group_emit(G, off, key, v, G.unit_of[v / kFlowKeys], kNone32, kNone32);
+        if (group_owner_probe(T, G, key)) {
+            group_owner_add(G, off);
+            group_owner_verdict(T, G, uint32_t(key), group_owner_contrib(G, uint32_t(key), v));
+        }
+        return;
+    }
+    uint32_t v[kGroupSmall], u[kGroupSmall];
+#pragma unroll
+    for (uint32_t i = 0; i < kGroupSmall; i++) v[i] = i < c ? G.vals[off + i] : kNone32;
+    sort_network(v);
+#pragma unroll
+    for (uint32_t i = 0; i < kGroupSmall; i++) u[i] = i < c ? G.unit_of[v[i] / kFlowKeys] : kNone32;
+#pragma unroll
+    for (uint32_t i = 0; i < kGroupSmall; i++)
+        if (i < c)
+            group_emit(G, off + i, key, v[i], u[i], i > 0 ? u[i - 1] : kNone32,
+                       i + 1 < kGroupSmall ? u[i + 1] : kNone32);
+    if (group_owner_probe(T, G, key)) {
+        group_owner_add(G, off);
+        u128 sum = 0;
+#pragma unroll
+        for (uint32_t i = 0; i < kGroupSmall; i++)
+            if (i < c) sum += group_owner_contrib(G, uint32_t(key), v[i]);
+        group_owner_verdict(T, G, uint32_t(key), sum);
+    }
+}
+
+// Workgroup sums (kGroupBigThreads lanes).
+__device__ inline uint32_t group_block_exclusive(uint32_t x, uint32_t* total, uint32_t* scratch) {
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t incl = wave_inclusive_u32(x, lane);
+    if (lane == 63) scratch[wave] = incl;
+    __syncthreads();
+    uint32_t before = 0, all = 0;
+    for (uint32_t w = 0; w < kGroupBigThreads / 64; w++) {
+        if (w < wave) before += scratch[w];
+        all += scratch[w];
+    }
+    __syncthreads();
+    *total = all;
+    return before + incl - x;
+}
+
+__global__ void __launch_bounds__(kGroupBigThreads) group_big(Tables T, GroupPlan G) {
+    __shared__ uint32_t buf[kGroupLdsWords];
+    __shared__ uint32_t scratch[kGroupBigThreads / 64];
+    __shared__ uint32_t red_min[kGroupBigThreads / 64], red_max[kGroupBigThreads / 64];
+    __shared__ unsigned long long red_lo[kGroupBigThreads / 64], red_hi[kGroupBigThreads / 64];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t nbig = G.counts[1];
+    for (uint32_t b = blockIdx.x; b < nbig; b += gridDim.x) {
+        const uint4 e = G.big[b];
+        const uint32_t off = e.x, c = e.y;
+        const uint64_t key = (uint64_t(e.w) << 32) | e.z;
+        const bool owner = group_owner_probe(T, G, key);
+        const uint32_t row = uint32_t(key);
+        uint64_t sum_lo = 0, sum_hi = 0;
+        if (c <= kGroupMedium) {
+            uint32_t p2 = 32;
+            while (p2 < c) p2 <<= 1;
+            for (uint32_t i = tid; i < p2; i += kGroupBigThreads)
+                buf[i] = i < c ? G.vals[off + i] : kNone32;
+            __syncthreads();
+            for (uint32_t k = 2; k <= p2; k <<= 1)
+                for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                    for (uint32_t i = tid; i < p2; i += kGroupBigThreads) {
+                        const uint32_t l = i ^ j;
+                        if (l > i) {
+                            const uint32_t a = buf[i], bb = buf[l];
+                            if ((a > bb) == ((i & k) == 0)) {
+                                buf[i] = bb;
+                                buf[l] = a;
+                            }
+                        }
+                    }
+                    __syncthreads();
+                }
+            // (unit lookups: kGroupBatch independent loads in flight per lane)
+            uint32_t* units = buf + kGroupMedium;
+            for (uint32_t i0 = tid * kGroupBatch; i0 < c; i0 += kGroupBigThreads * kGroupBatch) {
+                uint32_t uu[kGroupBatch];
+                uint64_t aa[kGroupBatch];
+#pragma unroll
+                for (uint32_t j = 0; j < kGroupBatch; j++) {
+                    uu[j] = i0 + j < c ? G.unit_of[buf[i0 + j] / kFlowKeys] : 0u;
+                    aa[j] = owner && i0 + j < c ? group_owner_contrib(G, row, buf[i0 + j]) : 0u;
+                }
+#pragma unroll
+                for (uint32_t j = 0; j < kGroupBatch; j++) {
+                    if (i0 + j < c) units[i0 + j] = uu[j];
+                    sum_lo += aa[j];
+                    sum_hi += sum_lo < aa[j];
+                }
+            }
+            __syncthreads();
+            for (uint32_t i = tid; i < c; i += kGroupBigThreads) {
+                group_emit(G, off + i, key, buf[i], units[i], i > 0 ? units[i - 1] : kNone32,
+                           i + 1 < c ? units[i + 1] : kNone32);
+            }
+        } else {
+            // The segment's pair index range, then bitmap windows of kGroupWindowBits indices.
+            uint32_t lo = kNone32, hi = 0;
+            for (uint32_t i = tid; i < c; i += kGroupBigThreads) {
+                const uint32_t v = G.vals[off + i];
+                lo = min(lo, v);
+                hi = max(hi, v);
+            }
+            for (int d = 32; d >= 1; d >>= 1) {
+                lo = min(lo, uint32_t(__shfl_xor(lo, d, 64)));
+                hi = max(hi, uint32_t(__shfl_xor(hi, d, 64)));
+            }
+            if (lane == 0) {
+                red_min[wave] = lo;
+                red_max[wave] = hi;
+            }
+            __syncthreads();
+            lo = red_min[0];
+            hi = red_max[0];
+            for (uint32_t w = 1; w < kGroupBigThreads / 64; w++) {
+                lo = min(lo, red_min[w]);
+                hi = max(hi, red_max[w]);
+            }
+            uint32_t placed = 0;
+            for (uint64_t wb = lo; wb <= hi; wb += kGroupWindowBits) {
+                for (uint32_t i = tid; i < kGroupLdsWords; i += kGroupBigThreads) buf[i] = 0;
+                __syncthreads();
+                for (uint32_t i = tid; i < c; i += kGroupBigThreads) {
+                    const uint32_t v = G.vals[off + i];
+                    if (v >= wb && v - wb < kGroupWindowBits) {
+                        const uint32_t d = uint32_t(v - wb);
+                        atomicOr(&buf[d >> 5], 1u << (d & 31));
+                    }
+                }
+                __syncthreads();
+                constexpr uint32_t kWordsPerThread = kGroupLdsWords / kGroupBigThreads;
+                uint32_t mine = 0;
+                for (uint32_t w = 0; w < kWordsPerThread; w++)
+                    mine += __popc(buf[tid * kWordsPerThread + w]);
+                uint32_t total = 0;
+                uint32_t r = placed + group_block_exclusive(mine, &total, scratch);
+                for (uint32_t w = 0; w < kWordsPerThread; w++) {
+                    uint32_t bits = buf[tid * kWordsPerThread + w];
+                    while (bits) {
+                        const uint32_t bit = __builtin_ctz(bits);
+                        bits &= bits - 1;
+                        G.vals_sorted[off + r++] =
+                            uint32_t(wb + uint64_t(tid * kWordsPerThread + w) * 32 + bit);
+                    }
+                }
+                placed += total;
+                __syncthreads();
+            }
+            __threadfence();
+            __syncthreads();
+            // kGroupBatch consecutive pairs per lane, with both neighbours: every load of a batch
+            // is issued before any is used (two round trips per batch, not three per pair).
+            for (uint32_t i0 = tid * kGroupBatch; i0 < c; i0 += kGroupBigThreads * kGroupBatch) {
+                uint32_t v[kGroupBatch + 2], u[kGroupBatch + 2];
+#pragma unroll
+                for (uint32_t j = 0; j < kGroupBatch + 2; j++) {
+                    const int64_t at = int64_t(i0) + j - 1;
+                    v[j] = at >= 0 && at < int64_t(c) ? G.vals_sorted[off + at] : kNone32;
+                }
+                uint64_t aa[kGroupBatch + 2];
+#pragma unroll
+                for (uint32_t j = 0; j < kGroupBatch + 2; j++) {
+                    u[j] = v[j] != kNone32 ? G.unit_of[v[j] / kFlowKeys] : kNone32;
+                    aa[j] = owner && j >= 1 && j <= kGroupBatch && v[j] != kNone32
+                                ? group_owner_contrib(G, row, v[j]) : 0u;
+                }
+#pragma unroll
+                for (uint32_t j = 1; j <= kGroupBatch; j++) {
+                    if (i0 + j - 1 >= c) break;
+                    group_emit(G, off + i0 + j - 1, key, v[j], u[j], u[j - 1], u[j + 1]);
+                    sum_lo += aa[j];
+                    sum_hi += sum_lo < aa[j];
+                }
+            }
+        }
+        if (owner) {
+            for (int d = 32; d >= 1; d >>= 1) {
+                const uint64_t olo = __shfl_xor(sum_lo, d, 64);
+                const uint64_t ohi = __shfl_xor(sum_hi, d, 64);
+                const uint64_t nlo = sum_lo + olo;
+                sum_hi = sum_hi + ohi + (nlo < sum_lo ? 1u : 0u);
+                sum_lo = nlo;
+            }
+            if (lane == 0) {
+                red_lo[wave] = sum_lo;
+                red_hi[wave] = sum_hi;
+            }
+            __syncthreads();
+            if (tid == 0) {
+                u128 sum = 0;
+                for (uint32_t w = 0; w < kGroupBigThreads / 64; w++)
+                    sum += (u128(red_hi[w]) << 64) | red_lo[w];
+                group_owner_add(G, off);
+                group_owner_verdict(T, G, row, sum);
+            }
+        }
+        __syncthreads();  // (buf is reused by the next segment)
+    }
+}
+
+// Scan ops of the plan.
+
+// Initially ready units (no predecessor) -> the engine's queue (unit + 1), q_tail, counts[2].
+struct SelectReady {
+    static constexpr bool kEmitAll = false;
+    const uint32_t* indeg;
+    const unsigned int* counts;  // [0] units
+    uint32_t* queue;
+    unsigned int* engine;
+    unsigned int* ready_count;
+    __device__ void load(uint64_t base, uint64_t n, uint32_t* c) const {
+        const uint32_t units = counts[0];
+#pragma unroll
+        for (uint32_t i = 0; i < kScanItems; i++)
+            c[i] = base + i < n && base + i < units && indeg[base + i] == 0;
+    }
+    __device__ void emit(uint64_t u, uint32_t p) const { queue[p] = uint32_t(u) + 1; }
+    __device__ void total(uint32_t t) const {
+        engine[32] = t;
+        *ready_count = t;
+    }
+};
+
+// The planned expires_at entries: candidate s takes slot base + its exclusive rank.
+struct PlanExpiry {
+    static constexpr bool kEmitAll = false;
+    const uint32_t* exp_flag;
+    const uint32_t* slow_list;
+    uint64_t* expiry;
+    uint64_t expiry_capacity;
+    uint64_t row_base;
+    const unsigned long long* base;  // expiry_count at the plan's start (flow_heads)
+    unsigned long long* expiry_count;
+    unsigned int* scalar_flags;
+    __device__ void load(uint64_t b, uint64_t n, uint32_t* c) const {
+#pragma unroll
+        for (uint32_t i = 0; i < kScanItems; i++) c[i] = b + i < n ? exp_flag[b + i] : 0u;
+    }
+    __device__ void emit(uint64_t s, uint32_t p) const {
+        const uint64_t i = *base + p;
+        if (i < expiry_capacity) expiry[i] = row_base + slow_list[s];
+        else atomicOr(scalar_flags, kFlagTableFull);
+    }
+    __device__ void total(uint32_t t) const {
+        const uint64_t n = *base + t;
+        *expiry_count = n < expiry_capacity ? n : expiry_capacity;
+    }
+};
+
+}  // namespace tbg

@@ -53,22 +53,19 @@ constexpr uint32_t kLaneMbMax = kLaneMbWords * 8;
 
 struct LanePlan {
     uint32_t m;
-    const uint64_t* keys_sorted;  // the flow plan's (key, unit) pairs
-    uint64_t n_pairs;
+    const uint64_t* keys_sorted;  // the flow plan's grouped (key, unit) pairs (group.hpp)
+    const unsigned int* n_pairs;  // grouped pairs (device)
     const Step* steps;
     const uint32_t* slow_list;
     LaneRec* recs;            // per position
     uint32_t* mailbox;        // per position: 1 when both sides are owned (then its LDS index)
-    uint32_t* mb_index;       // exclusive prefix sum of `mailbox`
+    uint32_t* mb_index;       // exclusive prefix sum of `mailbox` (one-lane mode); the walk's
+                              // verdict words (zeroed by plan_keys)
     uint8_t* outcome;         // per position: the writer lane's verdict (kOut*)
-    uint8_t* owner_head8;     // per sorted pair: first pair of an owner's segment
-    uint32_t* owner_starts;   // selected
+    uint32_t* owner_starts;   // per owner: its segment's first grouped pair (any order)
     unsigned int* counts;     // [0] owners, [1] ineligible events, [2] handled (set by the engine)
-    // free owners (lanes_contrib .. lanes_free)
     uint32_t epoch;
     uint32_t* acc_free;       // per account row: epoch of the call in which it is a free owner
-    u128* contrib;            // per sorted pair: the amount its owner's limit checks, else 0
-    u128* prefix;             // inclusive prefix sums of contrib
 };
 
 // The rings' loads are inline asm, so the compiler inserts no wait for them: its wait analysis
@@ -103,46 +100,6 @@ __device__ inline bool lanes_low(const tb_account_t& a) {
            a.credits_posted.hi < kLim;
 }
 
-// Per replayed event: is it a limit event (else count it), and its record.
-__global__ void lanes_check(Tables T, Call<tb_transfer_t> c, FlowPlan F, LanePlan L) {
-    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= L.m) return;
-    const Step st = L.steps[s];
-    const uint32_t k = st.k;
-    const tb_transfer_t& t = c.events[k];
-    bool ok = st.dr != kNone32 && st.cr != kNone32 && st.slot != kNone32 && st.dr != st.cr;
-    // a unit of its own (no chain)
-    const uint32_t u = F.unit_of[s];
-    ok = ok && F.heads[u] == s && (u + 1 == F.counts[0] ? s + 1 == L.m : F.heads[u + 1] == s + 1);
-    ok = ok && (t.flags & ~uint16_t(0)) == 0 && t.timeout == 0 && u128_is_zero(t.pending_id) &&
-         t.amount.hi == 0 && t.timestamp == 0 && !(st.flags & StepInfo::kBatchImported);
-    uint32_t bits = 0;
-    if (ok) {
-        const uint64_t w = T.tr.slots[st.slot];
-        ok = w != kEmpty && w != kTomb && (w & kRefMask) == c.row_base + k + 1;
-        const tb_account_t& dr = T.acc_rows[st.dr];
-        const tb_account_t& cr = T.acc_rows[st.cr];
-        ok = ok && !((dr.flags | cr.flags) & TB_ACCOUNT_CLOSED) && lanes_low(dr) && lanes_low(cr) &&
-             dr.ledger == cr.ledger && t.ledger == dr.ledger && t.code != 0 && t.ledger != 0 &&
-             !u128_is_zero(t.id) && !u128_is_max(t.id);
-        if (lanes_owner(dr.flags)) bits |= kLaneDrOwner;
-        if (lanes_owner(cr.flags)) bits |= kLaneCrOwner;
-        if (dr.flags & TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS) bits |= kLaneDrDecides;
-        if (cr.flags & TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS) bits |= kLaneCrDecides;
-        ok = ok && (bits & (kLaneDrOwner | kLaneCrOwner)) != 0;
-    }
-    L.mailbox[s] = ok && (bits & (kLaneDrOwner | kLaneCrOwner)) == (kLaneDrOwner | kLaneCrOwner);
-    if (!ok) {
-        atomicAdd(&L.counts[1], 1u);
-        return;
-    }
-    LaneRec r;
-    r.amount = t.amount.lo;
-    r.dr = st.dr;
-    r.bits = bits;
-    L.recs[s] = r;
-}
-
 // The LDS mailbox index of each event with two owners (too many: the flow replay runs).
 __global__ void lanes_mailboxes(LanePlan L) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
@@ -150,20 +107,6 @@ __global__ void lanes_mailboxes(LanePlan L) {
     const uint32_t i = L.mb_index[s];
     if (i >= kLaneMbMax) atomicAdd(&L.counts[1], 1u);
     else L.recs[s].bits |= i << kLaneMbShift;
-}
-
-// The first pair of each owner account's segment in the sorted (key, unit) pairs.
-__global__ void lanes_segments(Tables T, LanePlan L) {
-    const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (i >= L.n_pairs) return;
-    const uint64_t key = L.keys_sorted[i];
-    bool head = false;
-    if (key != kFlowNoKey && (key >> 63) == 1 &&
-        (i == 0 || (L.keys_sorted[i - 1] >> kFlowUnitBits) != (key >> kFlowUnitBits))) {
-        const uint32_t row = uint32_t((key >> kFlowUnitBits) & 0xFFFFFFFFu);
-        head = lanes_owner(T.acc_rows[row].flags);
-    }
-    L.owner_head8[i] = head;
 }
 
 // Free owners. An owner whose limit passes even if every event it checks in the call is created
@@ -174,44 +117,7 @@ __global__ void lanes_segments(Tables T, LanePlan L) {
 // each event is then as good as unowned: no lane walks it (lanes_free clears its owner bits; the
 // post pass adds its amounts with atomics), and an event left without owners is created. Config 3
 // (hot accounts funded for most of the stream) needs no lane at all until an account nears its
-// limit. The sums: one contribution per sorted (key, unit) pair, an inclusive u128 scan, and the
-// difference across each owner's pairs (from its start to the next owner's: the pairs between are
-// other keys, which contribute 0).
-__global__ void lanes_contrib(Tables T, LanePlan L) {
-    const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (i >= L.n_pairs) return;
-    const uint64_t key = L.keys_sorted[i];
-    u128 v = 0;
-    if (key != kFlowNoKey && (key >> 63) == 1) {
-        const uint32_t row = uint32_t((key >> kFlowUnitBits) & 0xFFFFFFFFu);
-        const uint32_t s = uint32_t(key & ((1u << kFlowUnitBits) - 1));
-        if (s < L.m) {
-            const LaneRec r = L.recs[s];
-            const bool debit = r.dr == row;
-            if (debit ? (r.bits & kLaneDrDecides) : (r.bits & kLaneCrDecides)) v = r.amount;
-        }
-    }
-    L.contrib[i] = v;
-}
-
-__global__ void lanes_owner_free(Tables T, LanePlan L) {
-    const uint32_t o = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t owners = L.counts[0];
-    if (o >= owners || L.counts[1] != 0) return;
-    const uint64_t start = L.owner_starts[o];
-    const uint64_t end = o + 1 < owners ? L.owner_starts[o + 1] : L.n_pairs;
-    const u128 sum = L.prefix[end - 1] - (start ? L.prefix[start - 1] : u128(0));
-    const uint32_t row = uint32_t((L.keys_sorted[start] >> kFlowUnitBits) & 0xFFFFFFFFu);
-    const tb_account_t& a = T.acc_rows[row];
-    const u128 dpe = U(a.debits_pending), dpo = U(a.debits_posted);
-    const u128 cpe = U(a.credits_pending), cpo = U(a.credits_posted);
-    // (every balance < 2^126 and the sum < 2^96 for an eligible call: no wrap below)
-    bool free = true;
-    if (a.flags & TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS) free = free && dpe + dpo + sum <= cpo;
-    if (a.flags & TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS) free = free && cpe + cpo + sum <= dpo;
-    if (free) L.acc_free[row] = L.epoch;
-}
-
+// limit. The sums are taken per owner segment by the grouping (group.hpp: group_owner_verdict).
 __global__ void lanes_free(Tables T, LanePlan L) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= L.m || L.counts[1] != 0) return;
@@ -244,20 +150,19 @@ __global__ void __launch_bounds__(kLanesMax) lanes_replay(Tables T, Call<tb_tran
     for (uint32_t i = o; i < kLaneMbWords; i += blockDim.x) mbox[i] = 0;
     __syncthreads();
     bool alive = o < owners;
+    const uint64_t n_pairs = *L.n_pairs;
     uint64_t idx = alive ? L.owner_starts[o] : 0;
     const uint64_t my_key = alive ? (L.keys_sorted[idx] >> kFlowUnitBits) : 0;
     const uint32_t row = uint32_t(my_key & 0xFFFFFFFFu);
     const bool walks = alive && L.acc_free[row] != L.epoch;  // (free owners: lanes_free)
     alive = walks;
     u128 dpe = 0, dpo = 0, cpe = 0, cpo = 0;
-    uint16_t flags = 0;
     if (alive) {
         const tb_account_t& a = T.acc_rows[row];
         dpe = U(a.debits_pending);
         dpo = U(a.debits_posted);
         cpe = U(a.credits_pending);
         cpo = U(a.credits_posted);
-        flags = a.flags;
     }
     bool published = false;
     // The account's records in call order: record loads kAhead steps ahead, and the pair loads
@@ -275,8 +180,8 @@ __global__ void __launch_bounds__(kLanesMax) lanes_replay(Tables T, Call<tb_tran
     // the rings in flight instead of draining them every step.
     bool pre_valid[kAhead];
     auto fetch_pair = [&](uint32_t slot) {  // (an unconditional load: no select waits for it)
-        const uint64_t at = fetch_idx < L.n_pairs ? fetch_idx : L.n_pairs - 1;
-        pre_valid[slot] = fetch_idx < L.n_pairs;
+        const uint64_t at = fetch_idx < n_pairs ? fetch_idx : n_pairs - 1;
+        pre_valid[slot] = fetch_idx < n_pairs;
         pre_key[slot] = lane_load8(&L.keys_sorted[at]);
         fetch_idx++;
     };
@@ -457,6 +362,7 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
     const uint32_t o = walk_uniform(blockIdx.x * kWalkWaves + (threadIdx.x >> 6));
     if (o >= owners) return;
     const uint64_t start = walk_uniform64(L.owner_starts[o]);
+    const uint64_t n_pairs = walk_uniform(*L.n_pairs);
     const uint64_t my_key = walk_uniform64(L.keys_sorted[start]) >> kFlowUnitBits;
     const uint32_t row = uint32_t(my_key & 0xFFFFFFFFu);
     if (walk_uniform(L.acc_free[row]) == L.epoch) return;  // a free owner (lanes_free)
@@ -470,7 +376,7 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
 
     auto fetch_pairs = [&](uint64_t base, uint64_t* key) {
         const uint64_t p = base + lane;
-        *key = p < L.n_pairs ? L.keys_sorted[p] : ~0ull;
+        *key = p < n_pairs ? L.keys_sorted[p] : ~0ull;
     };
     auto fetch_recs = [&](uint64_t key, WalkWindow* w) {
         w->valid = key != ~0ull && (key >> kFlowUnitBits) == my_key;
