@@ -53,7 +53,7 @@ struct FlowScratch {
     uint8_t *head8 = nullptr, *barrier8 = nullptr;
     uint32_t *heads = nullptr, *unit_of = nullptr, *barriers = nullptr, *vals = nullptr,
              *vals_sorted = nullptr, *succ = nullptr, *indeg = nullptr;
-    uint64_t *keys_sorted = nullptr, *pnt_ops = nullptr, *pnt_scan = nullptr;
+    uint64_t* keys_sorted = nullptr;
     Step* steps = nullptr;
     uint32_t* queue = nullptr;
     uint8_t* outcome = nullptr;  // account lanes' verdicts
@@ -67,7 +67,7 @@ struct FlowScratch {
     unsigned int* lane_counts = nullptr;
     uint32_t* dup_mark = nullptr;  // per event (batch_events_max)
     unsigned int* counts = nullptr;  // [0] units [1] barriers [2] ready [4] grouped pairs [5] listed
-    unsigned long long* words = nullptr;  // [0] pnt_fired [1] expiry_count at the plan's start
+    unsigned long long* words = nullptr;  // [1] expiry_count at the plan's start
     UndoEntry* lane_undo = nullptr;
     unsigned int* engine = nullptr;  // flow engine queue counters
     uint32_t* exp_flag = nullptr;
@@ -100,6 +100,8 @@ struct tbg_ctx {
     uint8_t* ev_info = nullptr;
     uint8_t* ev_slow = nullptr;
     uint32_t* slow_list = nullptr;
+    uint64_t* pnt_call = nullptr;           // pulse_next_timestamp updates per event (post/void)
+    unsigned long long* pnt_fired = nullptr;
     // balance items (2 per event, packed u64) and their sorted copy
     uint64_t* bal_items = nullptr;
     uint4* chunk_info = nullptr;     // per 64-event chunk of a create_transfers call
@@ -341,6 +343,7 @@ Call<Event> make_call(tbg_ctx* ctx, const Event* d_events, uint32_t n, const uin
     c.ev_info = ctx->ev_info;
     c.ev_slow = ctx->ev_slow;
     c.slow_list = ctx->slow_list;
+    c.pnt_call = ctx->pnt_call;
     return c;
 }
 
@@ -381,14 +384,14 @@ int end_call(tbg_ctx* ctx, uint32_t n, bool already_synced = false) {
 
 void free_flow(FlowScratch& F) {
     void* ptrs[] = {F.head8, F.barrier8, F.heads, F.unit_of, F.barriers, F.vals, F.vals_sorted,
-                    F.succ, F.indeg, F.keys_sorted, F.pnt_ops, F.pnt_scan, F.steps, F.queue,
+                    F.succ, F.indeg, F.keys_sorted, F.steps, F.queue,
                     F.outcome, F.recs, F.mailbox, F.owner_starts, F.mb_index, F.exp_flag,
                     F.hkeys, F.hcnt, F.hoff, F.loc, F.rank, F.big};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     F.head8 = F.barrier8 = F.outcome = nullptr;
     F.heads = F.unit_of = F.barriers = F.vals = F.vals_sorted = F.succ = F.indeg = nullptr;
-    F.keys_sorted = F.pnt_ops = F.pnt_scan = nullptr;
+    F.keys_sorted = nullptr;
     F.steps = nullptr;
     F.queue = nullptr;
     F.recs = nullptr;
@@ -420,7 +423,6 @@ int ensure_flow(tbg_ctx* ctx, uint64_t m) {
     ok = dev_alloc(ctx, &F.head8, cap, false) && dev_alloc(ctx, &F.barrier8, cap, false) &&
          dev_alloc(ctx, &F.heads, cap, false) && dev_alloc(ctx, &F.unit_of, cap, false) &&
          dev_alloc(ctx, &F.barriers, cap, false) && dev_alloc(ctx, &F.indeg, cap, true) &&
-         dev_alloc(ctx, &F.pnt_ops, cap, false) && dev_alloc(ctx, &F.pnt_scan, cap, false) &&
          dev_alloc(ctx, &F.vals, kc, false) && dev_alloc(ctx, &F.vals_sorted, kc, false) &&
          dev_alloc(ctx, &F.succ, kc, false) && dev_alloc(ctx, &F.keys_sorted, kc, false) &&
          dev_alloc(ctx, &F.steps, cap, false) && dev_alloc(ctx, &F.queue, cap, false) &&
@@ -461,9 +463,7 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
     P.indeg = F.indeg;
     P.queue = F.queue;
     const bool post_void = (call_flags & kFlagPostVoid) != 0;
-    P.pnt_ops = post_void ? F.pnt_ops : nullptr;
-    P.pnt_scan = F.pnt_scan;
-    P.pnt_fired = &F.words[0];
+    P.pnt_ops = post_void ? c.pnt_call : nullptr;
     P.lane_undo = F.lane_undo;
     P.steps = F.steps;
     P.engine = F.engine;
@@ -620,22 +620,30 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
         fprintf(stderr, "flow: continuations %llu stall: head %llu tail %llu done %llu pos %llu\n",
                 d[4], d[8], d[9], d[10], d[11]);
     }
-    if (post_void) {
-        hipLaunchKernelGGL(flow_pnt_prep, dim3(grid_for(m)), block, 0, ctx->stream, P);
-        // prefix minima into keys_sorted (free after the plan)
-        size_t sb = 0;
-        HIP_TRY(ctx, hipcub::DeviceScan::InclusiveScan(nullptr, sb, F.pnt_scan, F.keys_sorted,
-                                                       hipcub::Min(), int(m), ctx->stream));
-        rc = ensure_cub_temp(ctx, sb);
-        if (rc) return rc;
-        HIP_TRY(ctx, hipcub::DeviceScan::InclusiveScan(ctx->cub_temp, sb, F.pnt_scan,
-                                                       F.keys_sorted, hipcub::Min(), int(m),
-                                                       ctx->stream));
-        hipLaunchKernelGGL(flow_pnt_check, dim3(grid_for(m)), block, 0, ctx->stream, ctx->T, P,
-                           F.keys_sorted);
-        hipLaunchKernelGGL(flow_pnt_final, dim3(1), dim3(64), 0, ctx->stream, ctx->T, P,
-                           F.keys_sorted);
-    }
+    HIP_TRY(ctx, hipGetLastError());
+    return 0;
+}
+
+// pulse_next_timestamp of a call with post/void: its recorded updates in call order (kernels.hpp
+// pnt_*). The scratch is the balance items' (consumed before the replay).
+int pnt_resolve(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
+    const uint32_t n = c.n;
+    uint64_t* mins = ctx->bal_items;
+    uint64_t* prefix = ctx->bal_items + n;
+    const dim3 block(kBlock);
+    hipLaunchKernelGGL(pnt_prep, dim3(grid_for(n)), block, 0, ctx->stream, c.pnt_call, n, mins);
+    size_t sb = 0;
+    HIP_TRY(ctx, hipcub::DeviceScan::InclusiveScan(nullptr, sb, mins, prefix, hipcub::Min(), int(n),
+                                                   ctx->stream));
+    int rc = ensure_cub_temp(ctx, sb);
+    if (rc) return rc;
+    HIP_TRY(ctx, hipcub::DeviceScan::InclusiveScan(ctx->cub_temp, sb, mins, prefix, hipcub::Min(),
+                                                   int(n), ctx->stream));
+    hipLaunchKernelGGL(pnt_check, dim3(grid_for(n)), block, 0, ctx->stream, ctx->T, c.pnt_call, n,
+                       prefix, ctx->pnt_fired);
+    hipLaunchKernelGGL(pnt_final, dim3(1), dim3(64), 0, ctx->stream, ctx->T, n, prefix,
+                       ctx->pnt_fired);
+    tmark(ctx, "pnt_resolve");
     HIP_TRY(ctx, hipGetLastError());
     return 0;
 }
@@ -983,7 +991,8 @@ tbg_ctx* tbg_open(const tbg_options* options) {
          dev_alloc(ctx, &ctx->ev_slot, ev_max, false) && dev_alloc(ctx, &ctx->ev_dr, ev_max, false) &&
          dev_alloc(ctx, &ctx->ev_cr, ev_max, false) && dev_alloc(ctx, &ctx->ev_amount, ev_max, false) &&
          dev_alloc(ctx, &ctx->ev_info, ev_max, false) && dev_alloc(ctx, &ctx->ev_slow, ev_max, false) &&
-         dev_alloc(ctx, &ctx->slow_list, ev_max, false);
+         dev_alloc(ctx, &ctx->slow_list, ev_max, false) &&
+         dev_alloc(ctx, &ctx->pnt_call, ev_max, false) && dev_alloc(ctx, &ctx->pnt_fired, 1, true);
     // (2 * ev_max items, at least ev_max u64 of lookup scratch)
     ok = ok && dev_alloc(ctx, &ctx->bal_items, 2 * ev_max, false) &&
          dev_alloc(ctx, &ctx->chunk_info, (ev_max + 63) / 64 + 1, false);
@@ -1040,6 +1049,7 @@ void tbg_close(tbg_ctx* ctx) {
                     ctx->T.tr_status, ctx->T.expiry, ctx->d_scalars, ctx->T.undo, ctx->d_events,
                     ctx->d_results, ctx->d_batch_ends, ctx->d_batch_ts, ctx->ev_slot, ctx->ev_dr,
                     ctx->ev_cr, ctx->ev_amount, ctx->ev_info, ctx->ev_slow, ctx->slow_list,
+                    ctx->pnt_call, ctx->pnt_fired,
                     ctx->bal_items, ctx->chunk_info, ctx->bal_items_sorted, ctx->bucket_words, ctx->bucket_partials,
                     ctx->window_partials, ctx->window_carry,
                     ctx->cub_temp, ctx->acc_ts_index, ctx->tr_ts_index, ctx->sel_buf,
@@ -1206,6 +1216,7 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
     const bool replay = !rc && ctx->h_scalars->stats[0] > 0;
     if (replay && (ctx->h_scalars->flags & kFlagImported)) rc = check_imported_indexes(ctx, true);
     if (replay && !rc) rc = run_replay(ctx, c, true, false);
+    if (!rc && (ctx->h_scalars->flags & kFlagPostVoid)) rc = pnt_resolve(ctx, c);
     if (!rc) rc = end_call(ctx, n, !replay);
     if (!rc && ctx->ae_log) {
         const double ta = ctx->timing ? now_ms() : 0;

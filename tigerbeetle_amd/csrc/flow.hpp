@@ -66,9 +66,7 @@ struct FlowPlan {
     uint32_t* succ;              // kFlowKeys per position: successor unit or kNone32
     uint32_t* indeg;             // per unit: predecessors not yet finished
     uint32_t* queue;             // ready units (unit + 1; 0 = not yet pushed)
-    uint64_t* pnt_ops;           // per position (post/void calls), else null
-    uint64_t* pnt_scan;
-    unsigned long long* pnt_fired;
+    uint64_t* pnt_ops;           // post/void calls: Call::pnt_call (per event), else null
     UndoEntry* lane_undo;        // kFlowUndoPerLane per lane
     struct Step* steps;          // per position: what the engine prefetches before it waits
     const unsigned int* skip;    // nonzero: the account lanes replayed the call (lanes.hpp)
@@ -108,7 +106,6 @@ __global__ void flow_heads(Tables T, Call<tb_transfer_t> c, FlowPlan P) {
     if (s < 4) P.lane_counts[s] = 0;
     if (s == 0) {
         P.counts[5] = P.counts[6] = P.counts[7] = 0;
-        *P.pnt_fired = 0;
     }
     if (s >= P.m) return;
     const uint32_t k = P.slow_list[s];
@@ -120,7 +117,6 @@ __global__ void flow_heads(Tables T, Call<tb_transfer_t> c, FlowPlan P) {
     }
     P.head8[s] = head;
     P.queue[s] = 0;  // (the ready units are selected into it after the grouping)
-    if (P.pnt_ops) P.pnt_ops[s] = 0;
     if (s == 0) *P.exp_base = T.scalars->expiry_count;
     const uint32_t slot = c.ev_slot[k];
     if (slot != kNone32) {
@@ -191,6 +187,7 @@ __global__ void __launch_bounds__(kFlowThreads) flow_replay(Tables T, Call<tb_tr
         if (block == 0 && tid == 0) {
             Replay R(T);
             R.expiry_planned = true;
+            R.pnt_ops = P.pnt_ops;
             for (uint32_t s = 0; s < P.m; s++) {
                 replay_chain_step<tb_transfer_t>(R, c, P.slow_list[s], true, chain_open,
                                                  chain_start, chain_broken);
@@ -228,7 +225,6 @@ __global__ void __launch_bounds__(kFlowThreads) flow_replay(Tables T, Call<tb_tr
             si.ts_event = st.ts_event;
             si.batch = st.batch;
             si.flags = st.flags;
-            R.pos = s;
             replay_chain_step_at<tb_transfer_t>(R, c, st.k, ev, si, EvRefs{st.slot, st.dr, st.cr},
                                                 true, chain_open, chain_start, chain_broken);
             if (R.overflow) {
@@ -357,35 +353,6 @@ __global__ void __launch_bounds__(kFlowThreads) flow_replay(Tables T, Call<tb_tr
         T.scalars->stats[2] = P.m;
         if (P.debug) P.debug[3] = wall_clock64() - t_start;
     }
-}
-
-// pulse_next_timestamp after a flow replay of a call with post/void: the recorded updates in
-// replay order. `min` updates lower it; a reset fires when the value before it (the start value
-// and every earlier `min`, while no reset has fired) equals its expiry, after which the value is
-// timestamp_min, which no later update changes.
-__global__ void flow_pnt_prep(FlowPlan P) {
-    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= P.m) return;
-    const uint64_t op = P.pnt_ops[s];
-    P.pnt_scan[s] = (op == 0 || (op & kPntReset)) ? ~0ull : op;
-}
-
-__global__ void flow_pnt_check(Tables T, FlowPlan P, const uint64_t* prefix_min) {
-    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= P.m) return;
-    const uint64_t op = P.pnt_ops[s];
-    if (!(op & kPntReset)) return;
-    uint64_t before = T.scalars->pulse_next_timestamp;
-    if (s > 0 && prefix_min[s - 1] < before) before = prefix_min[s - 1];
-    if (before == (op & ~kPntReset)) atomicOr(P.pnt_fired, 1ull);
-}
-
-__global__ void flow_pnt_final(Tables T, FlowPlan P, const uint64_t* prefix_min) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    uint64_t v = T.scalars->pulse_next_timestamp;
-    if (*P.pnt_fired) v = TB_TIMESTAMP_MIN;
-    else if (P.m && prefix_min[P.m - 1] < v) v = prefix_min[P.m - 1];
-    T.scalars->pulse_next_timestamp = v;
 }
 
 }  // namespace tbg

@@ -714,6 +714,7 @@ __device__ inline void commit_event(const Tables& T, const Call<tb_transfer_t>& 
     const uint8_t cls = info & kInfoClassMask;
     const uint64_t row = c.row_base + k;
     const uint64_t ref = row + 1;
+    if (call_flags & kFlagPostVoid) c.pnt_call[k] = 0;  // (the replay records its own)
     bool slow = cls == kClassSlow || (call_flags & kFlagImported);
     if (cls == kClassFast) {
         uint32_t s = kNone32, dr, cr;
@@ -750,8 +751,7 @@ __device__ inline void commit_event(const Tables& T, const Call<tb_transfer_t>& 
              (s == kNone32 || (T.tr.slots[s] & kRefMask) != ref)) ||
             ((call_flags & kFlagClosable) &&
              (T.acc_closable[dr] == c.epoch || T.acc_closable[cr] == c.epoch)) ||
-            ((call_flags & kFlagHot) && (T.acc_hot[dr] == c.epoch || T.acc_hot[cr] == c.epoch)) ||
-            ((info & kInfoPending) && (info & kInfoTimeout) && (call_flags & kFlagPostVoid))) {
+            ((call_flags & kFlagHot) && (T.acc_hot[dr] == c.epoch || T.acc_hot[cr] == c.epoch))) {
             // Demoted: undo the speculative liveness and balance items; the replay decides.
             slow = true;
             T.tr_live[row] = 0;
@@ -781,9 +781,12 @@ __device__ inline void commit_event(const Tables& T, const Call<tb_transfer_t>& 
             }
             if (pending && (info & kInfoTimeout)) {
                 expiry_append(T, row, false);
-                const uint64_t timeout = T.tr_rows[row].timeout;
-                atomicMin(&T.scalars->pulse_next_timestamp,
-                          (unsigned long long)(ts_applied + timeout * TB_NS_PER_S));
+                const uint64_t expires_at = ts_applied + T.tr_rows[row].timeout * TB_NS_PER_S;
+                // With post/void in the call the order of updates matters (a post/void resets
+                // pulse_next_timestamp when it names its expiry): recorded at the event, resolved
+                // in call order after the replay (pnt_resolve).
+                if (call_flags & kFlagPostVoid) c.pnt_call[k] = expires_at;
+                else atomicMin(&T.scalars->pulse_next_timestamp, (unsigned long long)expires_at);
             }
         }
     } else if (!slow && cls == kClassDone) {
@@ -1246,6 +1249,7 @@ __device__ inline void replay_chain_step_at(Replay& R, const Call<Event>& c, uin
     const uint16_t f = ev.flags;
     uint32_t status = 0;
     uint64_t ts_actual = ts_event;
+    R.pos = k;
 
     do {  // execute_create's loop body (:3030-3105)
         if (f & linked_flag) {
@@ -1351,6 +1355,7 @@ template <typename Event>
 __global__ void replay_kernel(Tables T, Call<Event> c, int is_transfers) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     Replay R(T);
+    if (is_transfers && (T.scalars->flags & kFlagPostVoid)) R.pnt_ops = c.pnt_call;
     bool chain_open = false, chain_broken = false;
     uint32_t chain_start = 0;
     const uint32_t n = T.scalars->slow_count;
@@ -1363,6 +1368,37 @@ __global__ void replay_kernel(Tables T, Call<Event> c, int is_transfers) {
         }
     }
     T.scalars->stats[2] = n;
+}
+
+// pulse_next_timestamp of a call with post/void, from the updates recorded per event (Call::
+// pnt_call) in call order. `min` updates lower it; a reset fires when the value before it (the
+// start value and every earlier `min`, while no reset has fired) equals its expiry, after which the
+// value is timestamp_min, which no later update changes. So: prefix minima of the `min` updates,
+// then "does any reset meet its prefix?"
+__global__ void pnt_prep(const uint64_t* ops, uint32_t n, uint64_t* mins) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const uint64_t op = ops[k];
+    mins[k] = (op == 0 || (op & kPntReset)) ? ~0ull : op;
+}
+__global__ void pnt_check(Tables T, const uint64_t* ops, uint32_t n, const uint64_t* prefix_min,
+                          unsigned long long* fired) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const uint64_t op = ops[k];
+    if (!(op & kPntReset)) return;
+    uint64_t before = T.scalars->pulse_next_timestamp;
+    if (k > 0 && prefix_min[k - 1] < before) before = prefix_min[k - 1];
+    if (before == (op & ~kPntReset)) atomicOr(fired, 1ull);
+}
+__global__ void pnt_final(Tables T, uint32_t n, const uint64_t* prefix_min,
+                          unsigned long long* fired) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    uint64_t v = T.scalars->pulse_next_timestamp;
+    if (*fired) v = TB_TIMESTAMP_MIN;
+    else if (n && prefix_min[n - 1] < v) v = prefix_min[n - 1];
+    T.scalars->pulse_next_timestamp = v;
+    *fired = 0;
 }
 
 // Id slots and liveness of events: created -> object, transient -> orphan, else tombstone.

@@ -126,6 +126,9 @@ struct Call {
     // Per-event timestamps (a ledger shard's slice of a routed call: its events keep their global
     // timestamps, which are not contiguous); nullptr: batch_ts[b] - batch_ends[b] + k + 1.
     const uint64_t* event_ts;
+    // Calls with post/void: every pulse_next_timestamp update, per event (0: none; expires_at:
+    // min; expires_at | kPntReset: reset-if-equal), resolved in call order after the replay.
+    uint64_t* pnt_call;
 };
 
 constexpr uint32_t kNone32 = 0xFFFFFFFFu;
@@ -249,8 +252,8 @@ struct Replay {
     uint64_t undo_cap;
     // flow mode
     bool concurrent = false;
-    uint64_t* pnt_ops = nullptr;  // per replay position: 0, expires_at (min) or | kPntReset
-    uint32_t pos = 0;             // replay position of the executing event
+    uint64_t* pnt_ops = nullptr;  // calls with post/void: Call::pnt_call (per event)
+    uint32_t pos = 0;             // the executing event (its index in the call)
     uint64_t key_max = 0, key_max_scope = 0;
     uint32_t add_epoch = 0;       // nonzero: additive accounts of this call (additive())
     bool expiry_planned = false;  // the flow plan wrote this call's expires_at entries
@@ -374,25 +377,21 @@ struct Replay {
         }
     }
     // create_transfer :3975-3982: pulse_next_timestamp = min(pulse_next_timestamp, expires_at).
+    // In calls with post/void every update is recorded at its event (FAST pending transfers with
+    // a timeout record theirs in tr_commit) and resolved in call order afterwards (pnt_resolve);
+    // otherwise only `min` updates exist, which commute.
     __device__ void pulse_min(uint64_t expires_at) {
-        if (!concurrent) {
+        if (pnt_ops) {
+            pnt_ops[pos] = expires_at;
+        } else if (!concurrent) {
             if (expires_at < T.scalars->pulse_next_timestamp)
                 T.scalars->pulse_next_timestamp = expires_at;
-        } else if (pnt_ops) {
-            pnt_ops[pos] = expires_at;
         } else {
             atomicMin(&T.scalars->pulse_next_timestamp, (unsigned long long)expires_at);
         }
     }
     // post_or_void_pending_transfer :4227-4229: reset to timestamp_min if it names this expiry.
-    __device__ void pulse_reset(uint64_t expires_at) {
-        if (!concurrent) {
-            if (T.scalars->pulse_next_timestamp == expires_at)
-                T.scalars->pulse_next_timestamp = TB_TIMESTAMP_MIN;
-        } else {
-            pnt_ops[pos] = expires_at | kPntReset;
-        }
-    }
+    __device__ void pulse_reset(uint64_t expires_at) { pnt_ops[pos] = expires_at | kPntReset; }
 };
 
 // ---- transfers --------------------------------------------------------------------------------
