@@ -619,6 +619,28 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
                 d[0], d[1], d[2] / 100.0, d[3] / 100.0);
         fprintf(stderr, "flow: continuations %llu stall: head %llu tail %llu done %llu pos %llu\n",
                 d[4], d[8], d[9], d[10], d[11]);
+        // The critical path: units in order are a topological order (edges go to later units).
+        const uint32_t units = cnt3[0];
+        std::vector<uint32_t> heads(units), succ(uint64_t(kFlowKeys) * m);
+        (void)hipMemcpy(heads.data(), F.heads, units * 4ull, hipMemcpyDeviceToHost);
+        (void)hipMemcpy(succ.data(), F.succ, succ.size() * 4, hipMemcpyDeviceToHost);
+        std::vector<uint64_t> start(units, 0), depth(units, 0);
+        uint64_t longest = 0, longest_units = 0;
+        for (uint32_t u = 0; u < units; u++) {
+            const uint32_t b = heads[u], e = u + 1 < units ? heads[u + 1] : m;
+            const uint64_t fin = start[u] + (e - b);
+            const uint64_t dep = depth[u] + 1;
+            longest = std::max(longest, fin);
+            longest_units = std::max(longest_units, dep);
+            for (uint64_t i = uint64_t(kFlowKeys) * b; i < uint64_t(kFlowKeys) * e; i++) {
+                const uint32_t v = succ[i];
+                if (v == kNone32 || v >= units) continue;
+                start[v] = std::max(start[v], fin);
+                depth[v] = std::max(depth[v], dep);
+            }
+        }
+        fprintf(stderr, "flow: critical path %llu events, %llu units\n",
+                (unsigned long long)longest, (unsigned long long)longest_units);
     }
     HIP_TRY(ctx, hipGetLastError());
     return 0;

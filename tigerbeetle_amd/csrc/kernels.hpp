@@ -310,7 +310,7 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
                                             bool prev_linked, uint64_t* fast_ts,
                                             unsigned int* bucket_hist) {
     bool imported = false, post_void = false, dup = false, closable = false, hot = false;
-    bool need_commit = false;
+    bool need_commit = false, chain_fast = false;
     const uint16_t f = t.flags;
     imported = (f & TB_TRANSFER_IMPORTED) != 0;
     post_void = (f & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) != 0;
@@ -322,8 +322,8 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
     uint32_t status = 0;
     uint64_t ts_out = ts_event;
     uint8_t info = 0, cls = kClassSlow;
-    bool pre_done = false;
-    if (!chain && !c.force_replay) {
+    bool pre_done = false, pre_fail = false;
+    if (!c.force_replay) {
         // execute_create's per-event checks before create_transfer (:3052-3081) and the
         // checks before the id lookup (:3729-3733): independent of every table.
         if (batch_imported != imported) {
@@ -338,6 +338,11 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
         } else if (!imported && !valid_id) {
             status = u128_is_zero(id) ? TB_CT_ID_MUST_NOT_BE_ZERO : TB_CT_ID_MUST_NOT_BE_INT_MAX;
             pre_done = true;
+        }
+        // A failing event of a linked chain fails the chain: the replay decides it.
+        if (chain && pre_done) {
+            pre_done = false;
+            pre_fail = true;
         }
     }
     uint64_t slot = kNone;
@@ -412,9 +417,14 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
                 }
             }
         }
-        if (!chain && !c.force_replay && !imported && slot != kNone) {
+        if (!c.force_replay && !pre_fail && !imported && slot != kNone) {
             cls = classify_after_lookup(T, c, k, ts_event, t, w_slot, dr, cr, &status, &ts_out,
                                         &info);
+            // Linked chains (execute_create :3033-3207): a chain whose every event is FAST
+            // creates every event -- tr_commit confirms that for the whole chain (commit_chain)
+            // or demotes all of it; a chain with any other event is replayed.
+            if (chain && cls != kClassFast) cls = kClassSlow;
+            chain_fast = chain && cls == kClassFast;
         }
     }
     info |= cls;
@@ -505,7 +515,7 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
     }
     return (imported ? kFlagImported : 0u) | (post_void ? kFlagPostVoid : 0u) |
            (dup ? kFlagDuplicate : 0u) | (closable ? kFlagClosable : 0u) | (hot ? kFlagHot : 0u) |
-           (need_commit ? kFlagNeedCommit : 0u);
+           (need_commit ? kFlagNeedCommit : 0u) | (chain_fast ? kFlagChain : 0u);
 }
 
 // Per 64-event chunk of a create_transfers call (one lane each): the batch b0 of its first event,
@@ -702,6 +712,111 @@ __device__ inline tb_uint128_t* account_field(tb_account_t* rows, uint32_t key) 
     return reinterpret_cast<tb_uint128_t*>(reinterpret_cast<uint8_t*>(a) + 16 + 16 * (key & 3));
 }
 
+// A FAST event's record as tr_commit reads it: its id slot (kNone32 unless re-probed or recorded),
+// account rows and amount.
+struct FastRec {
+    uint32_t s, dr, cr;
+    uint64_t amount;
+};
+__device__ inline FastRec fast_record(const Tables& T, const Call<tb_transfer_t>& c, uint32_t k,
+                                      unsigned int call_flags, uint8_t info) {
+    FastRec f;
+    f.s = kNone32;
+    const bool lean = (info & kInfoLean) != 0;
+    if (lean && c.pair_shift) {
+        const uint32_t ps = c.pair_shift;
+        const uint64_t x = c.bal_items[k];
+        f.dr = uint32_t(x & ((1ull << ps) - 1));
+        f.cr = uint32_t((x >> ps) & ((1ull << ps) - 1));
+        f.amount = x >> (2 * ps + 1);
+    } else if (lean) {
+        const uint64_t kmask = (1ull << c.key_bits) - 1;
+        const uint64_t* it = c.bal_items + 2 * uint64_t(k);
+        const uint64_t i0 = it[0], i1 = it[1];
+        f.dr = uint32_t((i0 & kmask) >> 2);
+        f.cr = uint32_t((i1 & kmask) >> 2);
+        f.amount = i0 >> c.key_bits;
+    } else {
+        f.s = c.ev_slot[k];
+        f.dr = c.ev_dr[k];
+        f.cr = c.ev_cr[k];
+        f.amount = c.ev_amount[k];
+    }
+    if (lean && (call_flags & (kFlagImported | kFlagDuplicate | kFlagClosable | kFlagHot |
+                               kFlagPostVoid | kFlagChain))) {
+        // The slot this event's id occupies (its own claim, or an earlier in-call holder's).
+        const uint64_t fs = transfer_slot_find(T, c, c.events[k].id);
+        f.s = fs == kNone ? kNone32 : uint32_t(fs);
+    }
+    return f;
+}
+
+// Does anything of the call invalidate FAST event k's speculative commit? Each re-check reads only
+// when ingest raised the flag that can make it fail.
+__device__ inline bool fast_demoted(const Tables& T, const Call<tb_transfer_t>& c, uint32_t k,
+                                    unsigned int call_flags, const FastRec& f) {
+    const uint64_t ref = c.row_base + k + 1;
+    return (call_flags & kFlagImported) ||
+           ((call_flags & kFlagDuplicate) &&
+            (f.s == kNone32 || (T.tr.slots[f.s] & kRefMask) != ref)) ||
+           ((call_flags & kFlagClosable) &&
+            (T.acc_closable[f.dr] == c.epoch || T.acc_closable[f.cr] == c.epoch)) ||
+           ((call_flags & kFlagHot) && (T.acc_hot[f.dr] == c.epoch || T.acc_hot[f.cr] == c.epoch));
+}
+
+// fast_demoted for another event j of the call, from what no thread of tr_commit writes: its id's
+// slot and its accounts looked up again (the same slot and rows ingest found -- accounts and the
+// refs of slots are fixed during tr_commit), not its balance items, which j's own thread may be
+// clearing.
+__device__ inline bool fast_demoted_peer(const Tables& T, const Call<tb_transfer_t>& c, uint32_t j,
+                                         unsigned int call_flags) {
+    if (call_flags & kFlagImported) return true;
+    const tb_transfer_t& e = c.events[j];
+    if (call_flags & kFlagDuplicate) {
+        const uint64_t s = transfer_slot_find(T, c, e.id);
+        if (s == kNone || (T.tr.slots[s] & kRefMask) != c.row_base + j + 1) return true;
+    }
+    if (call_flags & (kFlagClosable | kFlagHot)) {
+        const uint64_t dr = account_find(T, e.debit_account_id);
+        const uint64_t cr = account_find(T, e.credit_account_id);
+        if (dr == kNone || cr == kNone) return true;
+        if ((call_flags & kFlagClosable) &&
+            (T.acc_closable[dr] == c.epoch || T.acc_closable[cr] == c.epoch))
+            return true;
+        if ((call_flags & kFlagHot) && (T.acc_hot[dr] == c.epoch || T.acc_hot[cr] == c.epoch))
+            return true;
+    }
+    return false;
+}
+
+// A FAST event of a linked chain (execute_create :3033-3207): the chain creates every event iff
+// every event of it is FAST and none is demoted -- then no event fails, nothing is rolled back, and
+// each event's effects are those of a FAST event. Otherwise the whole chain replays. Every event of
+// the chain evaluates the same rule over the same events, so they agree. Chains longer than
+// kFastChainMax (or open at their batch's end: linked_event_chain_open) replay.
+constexpr uint32_t kFastChainMax = 32;
+__device__ inline bool chain_demoted(const Tables& T, const Call<tb_transfer_t>& c, uint32_t k,
+                                     unsigned int call_flags) {
+    const uint32_t b = batch_of_guess(c.batch_ends, c.n_batches, c.n, k);
+    const uint32_t bs = batch_start_of(c, b), be = c.batch_ends[b];
+    uint32_t x = k, y = k;
+    while (x > bs && (c.events[x - 1].flags & TB_TRANSFER_LINKED)) {
+        if (k - x >= kFastChainMax) return true;
+        x--;
+    }
+    while (c.events[y].flags & TB_TRANSFER_LINKED) {
+        if (y + 1 >= be) return true;  // linked_event_chain_open
+        if (y - k >= kFastChainMax) return true;
+        y++;
+    }
+    if (y - x >= kFastChainMax) return true;
+    for (uint32_t j = x; j <= y; j++)
+        if ((c.ev_info[j] & kInfoClassMask) != kClassFast) return true;
+    for (uint32_t j = x; j <= y; j++)
+        if (j != k && fast_demoted_peer(T, c, j, call_flags)) return true;
+    return false;
+}
+
 // One event of tr_commit: applied (committed FAST), done (final DONE), ts_applied (its timestamp).
 __device__ inline void commit_event(const Tables& T, const Call<tb_transfer_t>& c, uint32_t k,
                                     unsigned int call_flags, bool& applied, bool& done,
@@ -717,41 +832,17 @@ __device__ inline void commit_event(const Tables& T, const Call<tb_transfer_t>& 
     if (call_flags & kFlagPostVoid) c.pnt_call[k] = 0;  // (the replay records its own)
     bool slow = cls == kClassSlow || (call_flags & kFlagImported);
     if (cls == kClassFast) {
-        uint32_t s = kNone32, dr, cr;
-        uint64_t amount;
+        const FastRec fr = fast_record(T, c, k, call_flags, info);
+        const uint32_t s = fr.s, dr = fr.dr, cr = fr.cr;
+        const uint64_t amount = fr.amount;
         const bool lean = (info & kInfoLean) != 0;
-        if (lean && c.pair_shift) {
-            const uint32_t ps = c.pair_shift;
-            const uint64_t x = c.bal_items[k];
-            dr = uint32_t(x & ((1ull << ps) - 1));
-            cr = uint32_t((x >> ps) & ((1ull << ps) - 1));
-            amount = x >> (2 * ps + 1);
-        } else if (lean) {
-            const uint64_t kmask = (1ull << c.key_bits) - 1;
-            const uint64_t* it = c.bal_items + 2 * uint64_t(k);
-            const uint64_t i0 = it[0], i1 = it[1];
-            dr = uint32_t((i0 & kmask) >> 2);
-            cr = uint32_t((i1 & kmask) >> 2);
-            amount = i0 >> c.key_bits;
-        } else {
-            s = c.ev_slot[k];
-            dr = c.ev_dr[k];
-            cr = c.ev_cr[k];
-            amount = c.ev_amount[k];
-        }
-        if (lean && (slow || (call_flags & kFlagDuplicate) || (call_flags & kFlagClosable) ||
-                     (call_flags & kFlagHot) || (call_flags & kFlagPostVoid))) {
-            // The slot this event's id occupies (its own claim, or an earlier in-call holder's).
-            const uint64_t fs = transfer_slot_find(T, c, c.events[k].id);
-            s = fs == kNone ? kNone32 : uint32_t(fs);
-        }
-        // Each re-check reads only when ingest raised the flag that can make it fail.
-        if (slow ||
-            ((call_flags & kFlagDuplicate) &&
-             (s == kNone32 || (T.tr.slots[s] & kRefMask) != ref)) ||
-            ((call_flags & kFlagClosable) &&
-             (T.acc_closable[dr] == c.epoch || T.acc_closable[cr] == c.epoch)) ||
-            ((call_flags & kFlagHot) && (T.acc_hot[dr] == c.epoch || T.acc_hot[cr] == c.epoch))) {
+        const bool in_chain =
+            (call_flags & kFlagChain) &&
+            ((c.events[k].flags & TB_TRANSFER_LINKED) ||
+             (k > 0 && (c.events[k - 1].flags & TB_TRANSFER_LINKED) &&
+              k != batch_start_of(c, batch_of_guess(c.batch_ends, c.n_batches, c.n, k))));
+        if (slow || fast_demoted(T, c, k, call_flags, fr) ||
+            (in_chain && chain_demoted(T, c, k, call_flags))) {
             // Demoted: undo the speculative liveness and balance items; the replay decides.
             slow = true;
             T.tr_live[row] = 0;

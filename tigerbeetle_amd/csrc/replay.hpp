@@ -46,10 +46,11 @@ enum : unsigned int {
     kFlagClosable = 1u << 6,   // some account is marked closable
     kFlagNeedCommit = 1u << 7, // some event is not a plain FAST event (tr_commit must run)
     kFlagFlowStalled = 1u << 8, // the flow replay's watchdog fired (a bug: the call fails)
+    kFlagChain = 1u << 9,      // some linked chain's event is FAST (tr_commit decides the chain)
 };
 // Call flags under which tr_commit re-validates (and may demote) ingest's FAST events.
 constexpr unsigned int kCommitFlags = kFlagImported | kFlagPostVoid | kFlagDuplicate | kFlagHot |
-                                      kFlagClosable | kFlagNeedCommit;
+                                      kFlagClosable | kFlagNeedCommit | kFlagChain;
 
 enum : uint8_t { kClassDone = 0, kClassFast = 1, kClassSlow = 2 };
 
