@@ -102,6 +102,8 @@ struct tbg_ctx {
     uint32_t* slow_list = nullptr;
     uint64_t* pnt_call = nullptr;           // pulse_next_timestamp updates per event (post/void)
     unsigned long long* pnt_fired = nullptr;
+    unsigned long long* pv_slots = nullptr;  // pending-id claims of post/void events (kernels.hpp)
+    uint64_t pv_mask = 0;
     // balance items (2 per event, packed u64) and their sorted copy
     uint64_t* bal_items = nullptr;
     uint4* chunk_info = nullptr;     // per 64-event chunk of a create_transfers call
@@ -344,6 +346,9 @@ Call<Event> make_call(tbg_ctx* ctx, const Event* d_events, uint32_t n, const uin
     c.ev_slow = ctx->ev_slow;
     c.slow_list = ctx->slow_list;
     c.pnt_call = ctx->pnt_call;
+    // (TBG_NO_PV_FAST: every post/void replays)
+    c.pv_slots = getenv("TBG_NO_PV_FAST") ? nullptr : ctx->pv_slots;
+    c.pv_mask = ctx->pv_mask;
     return c;
 }
 
@@ -1014,7 +1019,9 @@ tbg_ctx* tbg_open(const tbg_options* options) {
          dev_alloc(ctx, &ctx->ev_cr, ev_max, false) && dev_alloc(ctx, &ctx->ev_amount, ev_max, false) &&
          dev_alloc(ctx, &ctx->ev_info, ev_max, false) && dev_alloc(ctx, &ctx->ev_slow, ev_max, false) &&
          dev_alloc(ctx, &ctx->slow_list, ev_max, false) &&
-         dev_alloc(ctx, &ctx->pnt_call, ev_max, false) && dev_alloc(ctx, &ctx->pnt_fired, 1, true);
+         dev_alloc(ctx, &ctx->pnt_call, ev_max, false) && dev_alloc(ctx, &ctx->pnt_fired, 1, true) &&
+         dev_alloc(ctx, &ctx->pv_slots, next_pow2(2 * uint64_t(ev_max)), true);
+    ctx->pv_mask = next_pow2(2 * uint64_t(ev_max)) - 1;
     // (2 * ev_max items, at least ev_max u64 of lookup scratch)
     ok = ok && dev_alloc(ctx, &ctx->bal_items, 2 * ev_max, false) &&
          dev_alloc(ctx, &ctx->chunk_info, (ev_max + 63) / 64 + 1, false);
@@ -1071,7 +1078,7 @@ void tbg_close(tbg_ctx* ctx) {
                     ctx->T.tr_status, ctx->T.expiry, ctx->d_scalars, ctx->T.undo, ctx->d_events,
                     ctx->d_results, ctx->d_batch_ends, ctx->d_batch_ts, ctx->ev_slot, ctx->ev_dr,
                     ctx->ev_cr, ctx->ev_amount, ctx->ev_info, ctx->ev_slow, ctx->slow_list,
-                    ctx->pnt_call, ctx->pnt_fired,
+                    ctx->pnt_call, ctx->pnt_fired, ctx->pv_slots,
                     ctx->bal_items, ctx->chunk_info, ctx->bal_items_sorted, ctx->bucket_words, ctx->bucket_partials,
                     ctx->window_partials, ctx->window_carry,
                     ctx->cub_temp, ctx->acc_ts_index, ctx->tr_ts_index, ctx->sel_buf,

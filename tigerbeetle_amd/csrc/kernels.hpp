@@ -194,6 +194,146 @@ __device__ inline AccSnap acc_probe_snap(const Tables& T, const AccProbe& p, con
     return a;
 }
 
+// ---- post / void on the parallel path ----------------------------------------------------------
+//
+// A post/void (post_or_void_pending_transfer, :4053-4300) of a committed pending transfer X whose
+// status is `pending` at the call's start is decided by the call's start state alone -- every check
+// reads X's immutable row, its TransferPending status, the event and the accounts' `closed` flags
+// -- unless an earlier event of the call changes X's status, which only a post/void of X does. So
+// the earliest post/void of X in the call (a claim on X's id, smallest event index wins) may be FAST
+// when it would succeed: its effects are X's status (posted / voided, written once), the accounts'
+// balance deltas (pending -= X.amount, posted += amount: u128 atomics, commutative), its own row,
+// and a pulse_next_timestamp reset recorded at the event (pnt_resolve). tr_commit confirms the claim
+// and the usual demotions (hot / closable accounts, duplicates). Later post/voids of X replay after
+// the FAST one's effects, exactly as in call order.
+__device__ inline uint64_t pv_home(const Call<tb_transfer_t>& c, const tb_uint128_t& x) {
+    return mix64(x.lo ^ mix64(x.hi ^ 0x5851F42D4C957F2Dull)) & c.pv_mask;
+}
+// Claims pending id `x` for event k (keeping the earliest claimant).
+__device__ inline void pv_claim(const Call<tb_transfer_t>& c, uint32_t k, const tb_uint128_t& x) {
+    const unsigned long long mine = (uint64_t(c.epoch) << 32) | (k + 1);
+    uint64_t s = pv_home(c, x);
+    for (uint64_t n = 0; n <= c.pv_mask; n++) {
+        unsigned long long w = c.pv_slots[s];
+        while ((w >> 32) != c.epoch) {  // free (another call's): take it
+            const unsigned long long o = atomicCAS(&c.pv_slots[s], w, mine);
+            if (o == w) return;
+            w = o;
+        }
+        if (u128_eq(c.events[uint32_t(w) - 1].pending_id, x)) {
+            if (mine < w) atomicMin(&c.pv_slots[s], mine);
+            return;
+        }
+        s = (s + 1) & c.pv_mask;
+    }
+}
+// Is event k the earliest post/void of pending id `x` in the call?
+__device__ inline bool pv_first(const Call<tb_transfer_t>& c, uint32_t k, const tb_uint128_t& x) {
+    uint64_t s = pv_home(c, x);
+    for (uint64_t n = 0; n <= c.pv_mask; n++) {
+        const unsigned long long w = c.pv_slots[s];
+        if ((w >> 32) != c.epoch) return false;
+        if (u128_eq(c.events[uint32_t(w) - 1].pending_id, x)) return uint32_t(w) == k + 1;
+        s = (s + 1) & c.pv_mask;
+    }
+    return false;
+}
+
+// The committed pending transfer a post/void names (kNone: not a committed, un-orphaned row).
+__device__ inline uint64_t pv_pending_row(const Tables& T, const Call<tb_transfer_t>& c,
+                                          const tb_uint128_t& pending_id) {
+    const uint64_t ps = transfer_slot_find(T, c, pending_id);
+    if (ps == kNone) return kNone;
+    const uint64_t w = T.tr.slots[ps];
+    const uint64_t r = (w & kRefMask) - 1;
+    if (r >= c.row_base || (w & kOrphanBit)) return kNone;
+    return r;
+}
+
+struct PvFast {
+    uint32_t dr, cr;  // the pending transfer's account rows
+    uint64_t amount;  // the amount posted (void: 0)
+};
+
+// post_or_void_pending_transfer's checks (:4053-4246) for a fresh, unique id; DONE where the
+// outcome is fixed by the call's start state, FAST where it succeeds if no earlier event of the
+// call posts / voids the same pending transfer (tr_commit: pv_first), else SLOW.
+__device__ inline uint8_t classify_post_void(const Tables& T, const Call<tb_transfer_t>& c,
+                                             uint32_t k, uint64_t ts_event, const tb_transfer_t& t,
+                                             uint32_t* status, PvFast* out) {
+    const uint16_t f = t.flags;
+    uint32_t st = 0;
+    if ((f & TB_TRANSFER_POST_PENDING) && (f & TB_TRANSFER_VOID_PENDING))
+        st = TB_CT_FLAGS_ARE_MUTUALLY_EXCLUSIVE;
+    else if (f & (TB_TRANSFER_PENDING | TB_TRANSFER_BALANCING_DEBIT | TB_TRANSFER_BALANCING_CREDIT |
+                  TB_TRANSFER_CLOSING_DEBIT | TB_TRANSFER_CLOSING_CREDIT))
+        st = TB_CT_FLAGS_ARE_MUTUALLY_EXCLUSIVE;
+    else if (u128_is_zero(t.pending_id)) st = TB_CT_PENDING_ID_MUST_NOT_BE_ZERO;
+    else if (u128_is_max(t.pending_id)) st = TB_CT_PENDING_ID_MUST_NOT_BE_INT_MAX;
+    else if (u128_eq(t.pending_id, t.id)) st = TB_CT_PENDING_ID_MUST_BE_DIFFERENT;
+    else if (t.timeout != 0) st = TB_CT_TIMEOUT_RESERVED_FOR_PENDING_TRANSFER;
+    if (st) {
+        *status = st;
+        return kClassDone;
+    }
+    // (not found now: an earlier event of the call may create it -- the replay decides)
+    const uint64_t ps = transfer_slot_find(T, c, t.pending_id);
+    if (ps == kNone) return kClassSlow;
+    const uint64_t pw = T.tr.slots[ps];
+    const uint64_t pr = (pw & kRefMask) - 1;
+    if (pr >= c.row_base) return kClassSlow;  // created in this call
+    if (pw & kOrphanBit) st = TB_CT_PENDING_TRANSFER_NOT_FOUND;
+    const tb_transfer_t& p = T.tr_rows[pr];  // committed rows are immutable
+    if (!st && !(p.flags & TB_TRANSFER_PENDING)) st = TB_CT_PENDING_TRANSFER_NOT_PENDING;
+    if (st) {
+        *status = st;
+        return kClassDone;
+    }
+    if (!u128_is_zero(t.debit_account_id) && !u128_eq(t.debit_account_id, p.debit_account_id))
+        st = TB_CT_PENDING_TRANSFER_HAS_DIFFERENT_DEBIT_ACCOUNT_ID;
+    else if (!u128_is_zero(t.credit_account_id) && !u128_eq(t.credit_account_id, p.credit_account_id))
+        st = TB_CT_PENDING_TRANSFER_HAS_DIFFERENT_CREDIT_ACCOUNT_ID;
+    else if (t.ledger > 0 && t.ledger != p.ledger) st = TB_CT_PENDING_TRANSFER_HAS_DIFFERENT_LEDGER;
+    else if (t.code > 0 && t.code != p.code) st = TB_CT_PENDING_TRANSFER_HAS_DIFFERENT_CODE;
+    const u128 p_amount = U(p.amount);
+    const u128 amount = (f & TB_TRANSFER_VOID_PENDING)
+                            ? (U(t.amount) == 0 ? p_amount : U(t.amount))
+                            : (U(t.amount) == kU128Max ? p_amount : U(t.amount));
+    if (!st && amount > p_amount) st = TB_CT_EXCEEDS_PENDING_TRANSFER_AMOUNT;
+    else if (!st && (f & TB_TRANSFER_VOID_PENDING) && amount < p_amount)
+        st = TB_CT_PENDING_TRANSFER_HAS_DIFFERENT_AMOUNT;
+    if (!st) {
+        switch (T.tr_status[pr]) {  // no event of the call makes a resolved transfer pending
+            case TB_PENDING_PENDING: break;
+            case TB_PENDING_POSTED: st = TB_CT_PENDING_TRANSFER_ALREADY_POSTED; break;
+            case TB_PENDING_VOIDED: st = TB_CT_PENDING_TRANSFER_ALREADY_VOIDED; break;
+            default: st = TB_CT_PENDING_TRANSFER_EXPIRED; break;
+        }
+    }
+    if (st) {
+        *status = st;
+        return kClassDone;
+    }
+    // From here the outcome depends on the status an earlier post/void of the call may set, and on
+    // `closed`: only the success path is parallel.
+    if (p.timeout != 0 && p.timestamp + uint64_t(p.timeout) * TB_NS_PER_S <= ts_event)
+        return kClassSlow;  // pending_transfer_expired, unless an earlier event resolved it
+    if (p_amount >> 64) return kClassSlow;
+    if ((f & TB_TRANSFER_VOID_PENDING) &&
+        (p.flags & (TB_TRANSFER_CLOSING_DEBIT | TB_TRANSFER_CLOSING_CREDIT)))
+        return kClassSlow;  // un-closes accounts (closable)
+    AccEntry ed, ec;
+    if (acc_index_find(T.acc_index, T.acc_rows, p.debit_account_id, &ed) == kNone ||
+        acc_index_find(T.acc_index, T.acc_rows, p.credit_account_id, &ec) == kNone)
+        return kClassSlow;
+    // (a hazard: possibly closed, balances near 2^126, or a wide entry -- the replay decides)
+    if (meta_hazard(ed.meta) || meta_hazard(ec.meta)) return kClassSlow;
+    out->dr = ed.ref - 1;
+    out->cr = ec.ref - 1;
+    out->amount = (f & TB_TRANSFER_POST_PENDING) ? uint64_t(amount) : 0;
+    return kClassFast;
+}
+
 // The checks after the id lookup (create_transfer, :3727-3873), on the ingest snapshot. `w` is
 // the word of the id's slot as this event observed it.
 __device__ inline uint8_t classify_after_lookup(const Tables& T, const Call<tb_transfer_t>& c,
@@ -201,7 +341,7 @@ __device__ inline uint8_t classify_after_lookup(const Tables& T, const Call<tb_t
                                                 const tb_transfer_t& t, uint64_t w,
                                                 const AccSnap& dr, const AccSnap& cr,
                                                 uint32_t* status, uint64_t* ts_out,
-                                                uint8_t* info) {
+                                                uint8_t* info, PvFast* pv) {
     const uint16_t f = t.flags;
     const uint64_t r = (w & kRefMask) - 1;
     if (r < c.row_base) {  // a committed id: the result is final for every event of the call
@@ -226,7 +366,8 @@ __device__ inline uint8_t classify_after_lookup(const Tables& T, const Call<tb_t
     if (r != c.row_base + k) return kClassSlow;  // a later duplicate of an in-call id
     // Provisionally the first occurrence: every DONE below is valid only if that holds.
     *info |= kInfoPostLookup;
-    if (f & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) return kClassSlow;
+    if (f & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING))
+        return c.pv_slots ? classify_post_void(T, c, k, ts_event, t, status, pv) : kClassSlow;
     uint32_t st = 0;
     if (u128_is_zero(t.debit_account_id)) st = TB_CT_DEBIT_ACCOUNT_ID_MUST_NOT_BE_ZERO;
     else if (u128_is_max(t.debit_account_id)) st = TB_CT_DEBIT_ACCOUNT_ID_MUST_NOT_BE_INT_MAX;
@@ -348,6 +489,7 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
     uint64_t slot = kNone;
     AccSnap dr, cr;
     dr.row = cr.row = kNone32;
+    PvFast pv{kNone32, kNone32, 0};
     if (pre_done) {
         cls = kClassDone;
     } else {
@@ -417,9 +559,13 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
                 }
             }
         }
+        // Every post/void claims its pending id: the earliest claimant may be FAST.
+        if (post_void && c.pv_slots && !c.force_replay && !u128_is_zero(t.pending_id) &&
+            !u128_is_max(t.pending_id))
+            pv_claim(c, k, t.pending_id);
         if (!c.force_replay && !pre_fail && !imported && slot != kNone) {
             cls = classify_after_lookup(T, c, k, ts_event, t, w_slot, dr, cr, &status, &ts_out,
-                                        &info);
+                                        &info, &pv);
             // Linked chains (execute_create :3033-3207): a chain whose every event is FAST
             // creates every event -- tr_commit confirms that for the whole chain (commit_chain)
             // or demotes all of it; a chain with any other event is replayed.
@@ -427,10 +573,17 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
             chain_fast = chain && cls == kClassFast;
         }
     }
+    // A FAST post/void: its record names the pending transfer's accounts and the posted amount;
+    // its effects are all tr_commit's (no balance items).
+    const bool pv_fast = cls == kClassFast && post_void;
+    if (pv_fast) {
+        dr.row = pv.dr;
+        cr.row = pv.cr;
+    }
     info |= cls;
     // A FAST event whose balance items are packed needs no per-event record: tr_commit decodes
     // the rows and amount from the items and re-probes the slot if it has to.
-    const bool lean = cls == kClassFast && c.bal_items && item_packable(c, t.amount.lo);
+    const bool lean = cls == kClassFast && !pv_fast && c.bal_items && item_packable(c, t.amount.lo);
     c.ev_info[k] = info | (lean ? kInfoLean : 0);
     if (!lean) {
         c.ev_slot[k] = slot == kNone ? kNone32 : uint32_t(slot);
@@ -450,7 +603,7 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
         const bool pending = (f & TB_TRANSFER_PENDING) != 0;
         if (pending) T.tr_status[row] = TB_PENDING_PENDING;  // fresh rows read TB_PENDING_NONE
         T.tr_live[row] = 1;
-        const uint64_t amount = t.amount.lo;
+        const uint64_t amount = pv_fast ? pv.amount : t.amount.lo;
         if (!lean) c.ev_amount[k] = amount;
         tb_create_result_t res;
         res.timestamp = ts_event;
@@ -458,7 +611,12 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
         res.reserved = 0;
         ingest_store_result(&c.results[k], res);
         if (pending && t.timeout > 0) need_commit = true;  // expires_at index
-        if (c.bal_items && c.pair_shift) {
+        if (pv_fast) {
+            need_commit = true;
+            if (c.bal_items && c.pair_shift) c.bal_items[k] = ~0ull;
+            else if (c.bal_items)
+                *reinterpret_cast<uint4*>(c.bal_items + 2 * uint64_t(k)) = make_uint4(~0u, ~0u, ~0u, ~0u);
+        } else if (c.bal_items && c.pair_shift) {
             const uint32_t ps = c.pair_shift;
             if (item_packable(c, amount)) {
                 c.bal_items[k] = (amount << (2 * ps + 1)) | (uint64_t(pending) << (2 * ps)) |
@@ -717,11 +875,13 @@ __device__ inline tb_uint128_t* account_field(tb_account_t* rows, uint32_t key) 
 struct FastRec {
     uint32_t s, dr, cr;
     uint64_t amount;
+    bool post_void;
 };
 __device__ inline FastRec fast_record(const Tables& T, const Call<tb_transfer_t>& c, uint32_t k,
                                       unsigned int call_flags, uint8_t info) {
     FastRec f;
     f.s = kNone32;
+    f.post_void = (c.events[k].flags & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) != 0;
     const bool lean = (info & kInfoLean) != 0;
     if (lean && c.pair_shift) {
         const uint32_t ps = c.pair_shift;
@@ -756,6 +916,7 @@ __device__ inline FastRec fast_record(const Tables& T, const Call<tb_transfer_t>
 __device__ inline bool fast_demoted(const Tables& T, const Call<tb_transfer_t>& c, uint32_t k,
                                     unsigned int call_flags, const FastRec& f) {
     const uint64_t ref = c.row_base + k + 1;
+    if (f.post_void && !pv_first(c, k, c.events[k].pending_id)) return true;
     return (call_flags & kFlagImported) ||
            ((call_flags & kFlagDuplicate) &&
             (f.s == kNone32 || (T.tr.slots[f.s] & kRefMask) != ref)) ||
@@ -776,9 +937,18 @@ __device__ inline bool fast_demoted_peer(const Tables& T, const Call<tb_transfer
         const uint64_t s = transfer_slot_find(T, c, e.id);
         if (s == kNone || (T.tr.slots[s] & kRefMask) != c.row_base + j + 1) return true;
     }
+    const bool post_void = (e.flags & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) != 0;
+    if (post_void && !pv_first(c, j, e.pending_id)) return true;
     if (call_flags & (kFlagClosable | kFlagHot)) {
-        const uint64_t dr = account_find(T, e.debit_account_id);
-        const uint64_t cr = account_find(T, e.credit_account_id);
+        // (a post/void's accounts are its pending transfer's)
+        const tb_transfer_t* a = &e;
+        if (post_void) {
+            const uint64_t pr = pv_pending_row(T, c, e.pending_id);
+            if (pr == kNone) return true;
+            a = &T.tr_rows[pr];
+        }
+        const uint64_t dr = account_find(T, a->debit_account_id);
+        const uint64_t cr = account_find(T, a->credit_account_id);
         if (dr == kNone || cr == kNone) return true;
         if ((call_flags & kFlagClosable) &&
             (T.acc_closable[dr] == c.epoch || T.acc_closable[cr] == c.epoch))
@@ -815,6 +985,45 @@ __device__ inline bool chain_demoted(const Tables& T, const Call<tb_transfer_t>&
     for (uint32_t j = x; j <= y; j++)
         if (j != k && fast_demoted_peer(T, c, j, call_flags)) return true;
     return false;
+}
+
+// The effects of a confirmed FAST post/void (post_or_void_pending_transfer :4193-4299): its row,
+// the pending transfer's status, the balance deltas on the pending transfer's accounts, and the
+// pulse_next_timestamp reset (recorded at the event: calls with post/void resolve them in order).
+__device__ inline void commit_post_void(const Tables& T, const Call<tb_transfer_t>& c, uint32_t k,
+                                        uint64_t row, uint64_t ts, uint32_t dr, uint32_t cr) {
+    const tb_transfer_t t = c.events[k];
+    const uint64_t pr = pv_pending_row(T, c, t.pending_id);
+    const tb_transfer_t p = T.tr_rows[pr];
+    const bool post = (t.flags & TB_TRANSFER_POST_PENDING) != 0;
+    const u128 p_amount = U(p.amount);
+    const u128 amount = post ? (U(t.amount) == kU128Max ? p_amount : U(t.amount)) : p_amount;
+    tb_transfer_t o;
+    o.id = t.id;
+    o.debit_account_id = p.debit_account_id;
+    o.credit_account_id = p.credit_account_id;
+    o.amount = W(amount);
+    o.pending_id = t.pending_id;
+    o.user_data_128 = U(t.user_data_128) > 0 ? t.user_data_128 : p.user_data_128;
+    o.user_data_64 = t.user_data_64 > 0 ? t.user_data_64 : p.user_data_64;
+    o.user_data_32 = t.user_data_32 > 0 ? t.user_data_32 : p.user_data_32;
+    o.timeout = 0;
+    o.ledger = p.ledger;
+    o.code = p.code;
+    o.flags = t.flags;
+    o.timestamp = ts;
+    T.tr_rows[row] = o;
+    T.tr_status[pr] = post ? TB_PENDING_POSTED : TB_PENDING_VOIDED;
+    atomic_sub_u128(&T.acc_rows[dr].debits_pending, p_amount);
+    atomic_sub_u128(&T.acc_rows[cr].credits_pending, p_amount);
+    if (post && amount) {
+        if (atomic_add_u128(&T.acc_rows[dr].debits_posted, amount) >= kHazardHiLimit)
+            acc_hazard_set(T.acc_index, T.acc_entry_of, dr, kHazardHigh);
+        if (atomic_add_u128(&T.acc_rows[cr].credits_posted, amount) >= kHazardHiLimit)
+            acc_hazard_set(T.acc_index, T.acc_entry_of, cr, kHazardHigh);
+    }
+    if (p.timeout != 0)
+        c.pnt_call[k] = (p.timestamp + uint64_t(p.timeout) * TB_NS_PER_S) | kPntReset;
 }
 
 // One event of tr_commit: applied (committed FAST), done (final DONE), ts_applied (its timestamp).
@@ -858,6 +1067,10 @@ __device__ inline void commit_event(const Tables& T, const Call<tb_transfer_t>& 
                 c.ev_dr[k] = dr;
                 c.ev_cr[k] = cr;
             }
+        } else if (fr.post_void) {
+            applied = true;
+            ts_applied = c.results[k].timestamp;
+            commit_post_void(T, c, k, row, ts_applied, dr, cr);
         } else {
             applied = true;
             ts_applied = c.results[k].timestamp;

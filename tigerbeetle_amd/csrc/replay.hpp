@@ -130,6 +130,10 @@ struct Call {
     // Calls with post/void: every pulse_next_timestamp update, per event (0: none; expires_at:
     // min; expires_at | kPntReset: reset-if-equal), resolved in call order after the replay.
     uint64_t* pnt_call;
+    // create_transfers: per-call claims of pending ids by post/void events (epoch:32 | event + 1;
+    // words of other epochs are free): the earliest post/void of a pending transfer in the call.
+    unsigned long long* pv_slots;
+    uint64_t pv_mask;
 };
 
 constexpr uint32_t kNone32 = 0xFFFFFFFFu;
