@@ -717,3 +717,94 @@ def test_change_events_imported_before_expiries():
         assert list(ev["type"]) == [1, 0, 0, 0, 4]
     finally:
         p.close()
+
+
+@pytest.mark.parametrize("mode", ["parallel", "no-pv-fast", "flow"])
+@pytest.mark.parametrize("seed", range(3))
+def test_fast_post_void_and_chains(seed, mode, monkeypatch):
+    """The parallel path's post/voids, linked chains and pulse_next_timestamp ordering against the
+    oracle: post/voids of committed pending transfers drawn from a small pool (many calls post or
+    void the same pending transfer several times: the earliest claimant may be FAST, the others
+    replay), full / partial / excess / maxInt amounts, voids with and without amounts, mismatched
+    accounts / ledgers / codes, pending transfers with timeouts of 0-3 s and some closing ones,
+    posts of pending transfers created in the same call, 4-event linked chains mixing all of these
+    (all-FAST chains commit in parallel, others replay), and pulses between calls."""
+    if mode == "no-pv-fast":
+        monkeypatch.setenv("TBG_NO_PV_FAST", "1")
+    rng = np.random.default_rng(700 + seed)
+    p = Pair(account_capacity=256, transfer_capacity=1 << 16, batch_events_max=1 << 13,
+             force_replay=(mode == "flow"))
+    try:
+        n_acc = 24
+        acc = workload.accounts(n_acc, seed=seed, ledger=1)
+        p.create_accounts(acc)
+        fund = [dict(id=1 + i, debit_account_id=1 + (i + 1) % n_acc, credit_account_id=1 + i,
+                     amount=10**12, ledger=1, code=1) for i in range(n_acc)]
+        p.create_transfers(_transfers(fund))
+        next_id = 1000
+        pool = []  # pending transfers of earlier calls: (id, amount)
+
+        def account_pair():
+            dr = int(rng.integers(1, n_acc + 1))
+            cr = int(rng.integers(1, n_acc + 1))
+            return dr, cr if cr != dr else 1 + dr % n_acc
+
+        def event(in_call_pending):
+            nonlocal next_id
+            next_id += 1
+            kind = rng.random()
+            if kind < 0.45 and (pool or in_call_pending):
+                if in_call_pending and (not pool or rng.random() < 0.1):
+                    pid, pamt = in_call_pending[int(rng.integers(0, len(in_call_pending)))]
+                else:
+                    pid, pamt = pool[int(rng.integers(0, len(pool)))]
+                post = rng.random() < 0.6
+                r = rng.random()
+                if post:
+                    amount = [(1 << 128) - 1, pamt, max(pamt // 3, 1), pamt + 1][int(r * 4)]
+                else:
+                    amount = [0, 0, pamt, max(pamt // 2, 1)][int(r * 4)]
+                ev = dict(id=next_id, pending_id=pid, amount=amount,
+                          flags=4 if post else 8)
+                m = rng.random()
+                if m < 0.05:
+                    ev["debit_account_id"] = int(rng.integers(1, n_acc + 1))
+                elif m < 0.08:
+                    ev["ledger"] = 2
+                elif m < 0.10:
+                    ev["code"] = 9
+                return ev
+            dr, cr = account_pair()
+            amount = int(rng.integers(1, 10**6))
+            if kind < 0.75:
+                flags = 2
+                if rng.random() < 0.03:
+                    flags |= 64 if rng.random() < 0.5 else 128  # closing_debit / closing_credit
+                ev = dict(id=next_id, debit_account_id=dr, credit_account_id=cr, amount=amount,
+                          ledger=1, code=1, flags=flags, timeout=int(rng.integers(0, 4)))
+                in_call_pending.append((next_id, amount))
+                return ev
+            return dict(id=next_id, debit_account_id=dr, credit_account_id=cr, amount=amount,
+                        ledger=1, code=1)
+
+        for call in range(6):
+            rows, in_call = [], []
+            while len(rows) < 3000:
+                if rng.random() < 0.12:
+                    chain = [event(in_call) for _ in range(4)]
+                    for ev in chain[:-1]:
+                        ev["flags"] = ev.get("flags", 0) | 1  # linked
+                    rows += chain
+                else:
+                    rows.append(event(in_call))
+            t = _transfers(rows)
+            r = p.create_transfers(t, [1500, len(rows) - 1500])
+            created = r["status"] == 0xFFFFFFFF
+            for i, ev in enumerate(rows):
+                if created[i] and (ev.get("flags", 0) & 2):
+                    pool.append((ev["id"], ev["amount"]))
+            pool = pool[-400:]
+            p.tick(int(rng.integers(1, 3)) * NS_PER_S)
+            p.compare_state()
+    finally:
+        p.close()

@@ -10,13 +10,15 @@
 // (u128 modular arithmetic: exact, since every true balance is in [0, 2^128)), and A's `closed`
 // after e is final(A).closed XOR (the parity of A's later closed flips: closing creations set it,
 // voids of closing transfers and expiries of closing transfers clear it). Each event touches two
-// accounts; the (account, event) touches are radix-sorted by account with events in descending
-// order, and an exclusive scan by key gives every touch the sum of its account's later deltas.
+// accounts; the (account, event) touches are grouped by account (group.hpp: an HBM hash table,
+// LDS-aggregated counts, a chained scan, a scatter), each account's touches put in event order
+// (registers for <= 16, else one workgroup: LDS bitonic sort or bitmap windows), and a suffix sum
+// over them gives every touch the sum of its account's later deltas.
 // Chains that were rolled back left no created event, so their events never appear (the groove's
 // scope discard). AccountEvents are in timestamp order within a call; the log is kept sorted.
 #pragma once
 
-#include "kernels.hpp"
+#include "group.hpp"
 
 namespace tbg {
 
@@ -34,42 +36,33 @@ struct AeDelta {
     uint64_t pad;
 };
 
-// The running sums scanned per account (the four balances and the closed flips).
+// The running sums of an account's later touches (the four balances and the closed flips).
 struct Bal5 {
     u128 dp, dpo, cp, cpo;
-    uint32_t flips, pad0;
-    uint64_t pad1;
+    uint32_t flips;
 };
-struct Bal5Add {
-    __device__ Bal5 operator()(const Bal5& a, const Bal5& b) const {
-        Bal5 r;
-        r.dp = a.dp + b.dp;
-        r.dpo = a.dpo + b.dpo;
-        r.cp = a.cp + b.cp;
-        r.cpo = a.cpo + b.cpo;
-        r.flips = a.flips + b.flips;
-        r.pad0 = 0;
-        r.pad1 = 0;
-        return r;
+__device__ inline void bal5_add(Bal5& a, const AeDelta& d) {
+    if (d.side == 0) {
+        a.dp += d.pending;
+        a.dpo += d.posted;
+    } else {
+        a.cp += d.pending;
+        a.cpo += d.posted;
     }
-};
+    a.flips += d.flip;
+}
 
 struct AeScratch {
-    uint64_t* keys;         // per touch: account row << 32 | ~event
-    uint32_t* vals;         // per touch: 2 * event + side
-    uint64_t* keys_sorted;
-    uint32_t* vals_sorted;
-    AeDelta* deltas;        // per touch (by 2 * event + side)
-    uint32_t* seg;          // per sorted touch: account row
-    Bal5* values;           // per sorted touch: its deltas placed in the four fields
-    Bal5* scanned;          // exclusive sums by account (the account's later events)
+    AeDelta* deltas;        // per touch (2 * event + side)
+    GroupPlan G;            // the touches grouped by account row (table, segments); G.counts:
+                            // [0] grouped touches, [1] listed accounts, [2] their chunks
+    uint32_t* chunk_seg;    // per chunk of a listed account: the account's entry in G.big
+    Bal5* chunk_tot;        // per chunk: the sums of its touches
 };
 
-__device__ inline void ae_side(const AeScratch& S, uint32_t i, uint32_t side, uint32_t row,
-                               u128 pending, u128 posted, uint32_t flip) {
+__device__ inline void ae_side(const AeScratch& S, uint32_t i, uint32_t side, u128 pending,
+                               u128 posted, uint32_t flip) {
     const uint32_t v = 2 * i + side;
-    S.keys[v] = (uint64_t(row) << 32) | (0xFFFFFFFFu - i);
-    S.vals[v] = v;
     AeDelta d;
     d.pending = pending;
     d.posted = posted;
@@ -109,12 +102,24 @@ __global__ void ae_created_flags(Call<tb_transfer_t> c, uint8_t* flags) {
     if (k < c.n) flags[k] = c.results[k].status == TB_STATUS_CREATED;
 }
 
-__global__ void ae_collect_transfers(Tables T, Call<tb_transfer_t> c, const uint32_t* list,
-                                     uint32_t m, AeScratch S, tb_account_event_t* log,
-                                     AeRef* refs) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= m) return;
-    const uint32_t k = list[i];
+// (Both collectors run kPlanThreads lanes per workgroup and group the event's two touches by
+// account row; lanes past the events write "no key" for their touches.)
+__device__ inline void ae_group_touches(const AeScratch& S, GroupBlock& B, uint32_t i, bool active,
+                                        uint32_t dr, uint32_t cr, uint32_t bound) {
+    uint32_t e0 = kNone32, e1 = kNone32, r0 = 0, r1 = 0;
+    if (active) {
+        e0 = group_block_add(S.G, B, dr, &r0);
+        e1 = group_block_add(S.G, B, cr, &r1);
+    }
+    group_block_publish(S.G, B);
+    if (i >= bound) return;
+    group_block_place(S.G, B, 2 * uint64_t(i), e0, r0);
+    group_block_place(S.G, B, 2 * uint64_t(i) + 1, e1, r1);
+}
+
+__device__ inline void ae_collect_transfer(Tables T, const Call<tb_transfer_t>& c, uint32_t k,
+                                           uint32_t i, const AeScratch& S, tb_account_event_t* log,
+                                           AeRef* refs, uint32_t* dr_out, uint32_t* cr_out) {
     const uint64_t row = c.row_base + k;
     const tb_transfer_t& t = T.tr_rows[row];  // the created transfer (amount actual, accounts)
     const uint16_t f = t.flags;
@@ -145,55 +150,73 @@ __global__ void ae_collect_transfers(Tables T, Call<tb_transfer_t> c, const uint
     } else {
         d_posted = amount;
     }
-    ae_side(S, i, 0, uint32_t(dr), d_pending, d_posted, flip_dr);
-    ae_side(S, i, 1, uint32_t(cr), d_pending, d_posted, flip_cr);
+    ae_side(S, i, 0, d_pending, d_posted, flip_dr);
+    ae_side(S, i, 1, d_pending, d_posted, flip_cr);
     ae_event_fields(&log[i], t.timestamp, f, status, p, c.events[k].amount, t.amount, t.ledger);
     refs[i] = AeRef{uint32_t(row), uint32_t(dr), uint32_t(cr), 0};
+    *dr_out = uint32_t(dr);
+    *cr_out = uint32_t(cr);
+}
+
+__global__ void __launch_bounds__(kPlanThreads)
+ae_collect_transfers(Tables T, Call<tb_transfer_t> c, const uint32_t* list,
+                     const unsigned int* count, AeScratch S, tb_account_event_t* log, AeRef* refs) {
+    __shared__ GroupBlock B;
+    group_block_init(B);
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) S.G.counts[1] = S.G.counts[2] = 0;  // listed accounts / chunks (ae_group_small)
+    const bool active = i < *count;
+    uint32_t dr_row = 0, cr_row = 0;
+    if (active) ae_collect_transfer(T, c, list[i], i, S, log, refs, &dr_row, &cr_row);
+    ae_group_touches(S, B, i, active, dr_row, cr_row, c.n);
 }
 
 // Expiries of a pulse (execute_expire_pending_transfers :4540-4626): rows[i] in expiry order,
 // event i stamped timestamp - m + i + 1.
-__global__ void ae_collect_expiry(Tables T, const uint64_t* rows, uint32_t m, uint64_t timestamp,
-                                  AeScratch S, tb_account_event_t* log, AeRef* refs) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= m) return;
-    const uint64_t row = rows[i];
+__device__ inline void ae_expiry_one(Tables T, uint64_t row, uint32_t m, uint32_t i,
+                                     uint64_t timestamp, const AeScratch& S,
+                                     tb_account_event_t* log, AeRef* refs, uint32_t* dr_out,
+                                     uint32_t* cr_out) {
     const tb_transfer_t& p = T.tr_rows[row];
     const uint64_t dr = account_find(T, p.debit_account_id);
     const uint64_t cr = account_find(T, p.credit_account_id);
     const u128 d_pending = u128(0) - U(p.amount);
-    ae_side(S, i, 0, uint32_t(dr), d_pending, 0, (p.flags & TB_TRANSFER_CLOSING_DEBIT) != 0);
-    ae_side(S, i, 1, uint32_t(cr), d_pending, 0, (p.flags & TB_TRANSFER_CLOSING_CREDIT) != 0);
+    ae_side(S, i, 0, d_pending, 0, (p.flags & TB_TRANSFER_CLOSING_DEBIT) != 0);
+    ae_side(S, i, 1, d_pending, 0, (p.flags & TB_TRANSFER_CLOSING_CREDIT) != 0);
     ae_event_fields(&log[i], timestamp - m + i + 1, 0, TB_PENDING_EXPIRED, &p,
                     tb_uint128_t{0, 0}, p.amount, p.ledger);
     refs[i] = AeRef{uint32_t(row), uint32_t(dr), uint32_t(cr), 0};
+    *dr_out = uint32_t(dr);
+    *cr_out = uint32_t(cr);
 }
 
-// Sorted touches -> their account (the scan key) and their deltas in the four fields.
-__global__ void ae_values(AeScratch S, uint32_t touches) {
-    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= touches) return;
-    const AeDelta d = S.deltas[S.vals_sorted[j]];
-    Bal5 b;
-    b.dp = d.side == 0 ? d.pending : 0;
-    b.dpo = d.side == 0 ? d.posted : 0;
-    b.cp = d.side == 1 ? d.pending : 0;
-    b.cpo = d.side == 1 ? d.posted : 0;
-    b.flips = d.flip;
-    b.pad0 = 0;
-    b.pad1 = 0;
-    S.values[j] = b;
-    S.seg[j] = uint32_t(S.keys_sorted[j] >> 32);
+__global__ void __launch_bounds__(kPlanThreads)
+ae_collect_expiry(Tables T, const uint64_t* rows, uint32_t m, uint64_t timestamp, AeScratch S,
+                  tb_account_event_t* log, AeRef* refs) {
+    __shared__ GroupBlock B;
+    group_block_init(B);
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) S.G.counts[1] = S.G.counts[2] = 0;  // listed accounts / chunks (ae_group_small)
+    uint32_t dr_row = 0, cr_row = 0;
+    if (i < m) ae_expiry_one(T, rows[i], m, i, timestamp, S, log, refs, &dr_row, &cr_row);
+    ae_group_touches(S, B, i, i < m, dr_row, cr_row, m);
 }
 
-// One sorted touch: its account after the event = final row - the later events' sums.
-__global__ void ae_emit(Tables T, AeScratch S, uint32_t touches, tb_account_event_t* log) {
-    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= touches) return;
-    const uint32_t v = S.vals_sorted[j];
+// The appended block's count and first / last timestamps (the log's order check).
+__global__ void ae_tail(const tb_account_event_t* log, const unsigned int* d_count, uint32_t n,
+                        unsigned long long* out) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const uint32_t m = d_count ? *d_count : n;
+    out[0] = m;
+    out[1] = m ? log[0].timestamp : 0;
+    out[2] = m ? log[m - 1].timestamp : 0;
+}
+
+// One touch's half of its AccountEvent: the account after the event = final row - the sums of
+// the account's later touches in the call.
+__device__ inline void ae_emit_touch(const tb_account_t& a, uint32_t v, const Bal5& later,
+                                     tb_account_event_t* log) {
     const uint32_t i = v >> 1, side = v & 1;
-    const tb_account_t& a = T.acc_rows[S.seg[j]];
-    const Bal5 later = S.scanned[j];
     tb_account_event_t* e = &log[i];
     const tb_uint128_t dp = W(U(a.debits_pending) - later.dp);
     const tb_uint128_t dpo = W(U(a.debits_posted) - later.dpo);
@@ -216,6 +239,245 @@ __global__ void ae_emit(Tables T, AeScratch S, uint32_t touches, tb_account_even
         e->cr_credits_posted = cpo;
         e->cr_account_timestamp = a.timestamp;
         e->cr_account_flags = flags;
+    }
+}
+
+// Listed accounts are processed in chunks of kAeChunk touches (kAeRun per lane of a workgroup).
+constexpr uint32_t kAeRun = 4;
+constexpr uint32_t kAeChunk = kGroupBigThreads * kAeRun;
+constexpr uint32_t kAeChunkBlocks = 512;  // ae_chunk_totals / ae_chunk_emit grid (grid-stride)
+
+// Per grouped account: <= kGroupSmall touches in registers (sorted, then emitted last to first with
+// the running sums); larger groups are listed for ae_group_sort / ae_chunk_*. Clears the slot.
+// A wave-sorted account (kGroupSmall < c <= kGroupMid touches in buf, event order): lane l takes
+// positions 4l .. 4l + 3; the later sums of its run = a suffix scan over the lanes after it.
+__device__ inline u128 wave_suffix_exclusive_u128(u128 x) {
+    const uint32_t lane = threadIdx.x & 63;
+    u128 f = x;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t lo = __shfl_down(uint64_t(f), d, 64), hi = __shfl_down(uint64_t(f >> 64), d, 64);
+        if (lane + d < 64) f += (u128(hi) << 64) | lo;
+    }
+    return f - x;
+}
+__device__ inline void ae_mid_account(Tables T, const AeScratch& S, uint32_t off, uint32_t c,
+                                      uint32_t row, uint32_t* buf, tb_account_event_t* log) {
+    const uint32_t lane = threadIdx.x & 63;
+    wave_rank_sort(S.G.vals, off, c, buf);
+    uint32_t v[4];
+    Bal5 run{};
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) {
+        v[j] = 4 * lane + j < c ? buf[4 * lane + j] : kNone32;
+        if (v[j] != kNone32) bal5_add(run, S.deltas[v[j]]);
+    }
+    Bal5 later;
+    later.dp = wave_suffix_exclusive_u128(run.dp);
+    later.dpo = wave_suffix_exclusive_u128(run.dpo);
+    later.cp = wave_suffix_exclusive_u128(run.cp);
+    later.cpo = wave_suffix_exclusive_u128(run.cpo);
+    later.flips = uint32_t(wave_suffix_exclusive_u128(run.flips));
+    const tb_account_t& a = T.acc_rows[row];
+#pragma unroll
+    for (int j = 3; j >= 0; j--) {
+        if (v[j] == kNone32) continue;
+        ae_emit_touch(a, v[j], later, log);
+        bal5_add(later, S.deltas[v[j]]);
+    }
+    wave_lds_sync();  // (buf is reused by the wave's next account)
+}
+
+// Per grouped account: <= kGroupSmall touches in registers (sorted, then emitted last to first with
+// the running sums), <= kGroupMid by the slot's wave (ae_mid_account); larger ones are listed for
+// ae_group_sort / ae_chunk_*. Clears the slot.
+__global__ void __launch_bounds__(kBlock) ae_group_small(Tables T, AeScratch S, uint64_t slots,
+                                                         tb_account_event_t* log) {
+    __shared__ uint32_t wave_buf[kBlock / 64][kGroupMid];
+    const GroupPlan& G = S.G;
+    const uint64_t h = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    uint32_t c = 0, off = 0, row = 0;
+    if (h < slots) {
+        c = G.hcnt[h];
+        if (c) {
+            row = uint32_t(G.hkeys[h] - 1);
+            off = G.hoff[h];
+            G.hkeys[h] = 0;
+            G.hcnt[h] = 0;
+        }
+    }
+    if (c > kGroupMid) {
+        const uint32_t b = atomicAdd(&G.counts[1], 1u);
+        const uint32_t chunks = (c + kAeChunk - 1) / kAeChunk;
+        const uint32_t cb = atomicAdd(&G.counts[2], chunks);
+        G.big[b] = make_uint4(off, c, row, cb);
+        for (uint32_t q = 0; q < chunks; q++) S.chunk_seg[cb + q] = b;
+    } else if (c >= 1 && c <= kGroupSmall) {
+        uint32_t v[kGroupSmall];
+#pragma unroll
+        for (uint32_t i = 0; i < kGroupSmall; i++) v[i] = i < c ? G.vals[off + i] : kNone32;
+        sort_network(v);
+        const tb_account_t& a = T.acc_rows[row];
+        Bal5 later{};
+#pragma unroll
+        for (int i = kGroupSmall - 1; i >= 0; i--) {
+            if (uint32_t(i) >= c) continue;
+            ae_emit_touch(a, v[i], later, log);
+            bal5_add(later, S.deltas[v[i]]);
+        }
+    }
+    uint64_t mids = __ballot(c > kGroupSmall && c <= kGroupMid);
+    while (mids) {
+        const int l = __ffsll((unsigned long long)mids) - 1;
+        mids &= mids - 1;
+        ae_mid_account(T, S, __shfl(off, l, 64), __shfl(c, l, 64), __shfl(row, l, 64),
+                       wave_buf[threadIdx.x >> 6], log);
+    }
+}
+
+// Sums across a workgroup of kGroupBigThreads: exclusive prefix over lanes (in lane order) and
+// the total, one u128 at a time (a Bal5 is five of them: registers stay low).
+struct Bal5Lds {
+    unsigned long long w[kGroupBigThreads / 64][2];
+};
+__device__ inline u128 block_exclusive_u128(u128 x, u128* total, Bal5Lds& L) {
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    u128 f = x;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t lo = __shfl_up(uint64_t(f), d, 64), hi = __shfl_up(uint64_t(f >> 64), d, 64);
+        if (lane >= uint32_t(d)) f += (u128(hi) << 64) | lo;
+    }
+    if (lane == 63) {
+        L.w[wave][0] = uint64_t(f);
+        L.w[wave][1] = uint64_t(f >> 64);
+    }
+    __syncthreads();
+    u128 before = 0, all = 0;
+    for (uint32_t w = 0; w < kGroupBigThreads / 64; w++) {
+        const u128 t = (u128(L.w[w][1]) << 64) | L.w[w][0];
+        if (w < wave) before += t;
+        all += t;
+    }
+    __syncthreads();
+    *total = all;
+    return before + f - x;
+}
+__device__ inline Bal5 bal5_block_exclusive(const Bal5& x, Bal5* total, Bal5Lds& L) {
+    Bal5 r;
+    r.dp = block_exclusive_u128(x.dp, &total->dp, L);
+    r.dpo = block_exclusive_u128(x.dpo, &total->dpo, L);
+    r.cp = block_exclusive_u128(x.cp, &total->cp, L);
+    r.cpo = block_exclusive_u128(x.cpo, &total->cpo, L);
+    u128 tf;
+    r.flips = uint32_t(block_exclusive_u128(x.flips, &tf, L));
+    total->flips = uint32_t(tf);
+    return r;
+}
+
+// Listed accounts, one workgroup each: the touches in event order into vals_sorted.
+__global__ void __launch_bounds__(kGroupBigThreads) ae_group_sort(AeScratch S) {
+    __shared__ SegmentLds L;
+    const GroupPlan& G = S.G;
+    const uint32_t nbig = G.counts[1];
+    for (uint32_t b = blockIdx.x; b < nbig; b += gridDim.x) {
+        const uint4 e = G.big[b];
+        segment_sort(G.vals, G.vals_sorted, e.x, e.y, L);
+    }
+}
+
+// Chunk q of a listed account holds the touches at positions (from the account's last touch
+// backwards) [q * kAeChunk, (q + 1) * kAeChunk); lane t the kAeRun of them from q * kAeChunk +
+// t * kAeRun. Loads the lane's run and returns its sums.
+__device__ inline Bal5 ae_chunk_run(const AeScratch& S, const uint4& e, uint32_t q,
+                                    uint32_t (&v)[kAeRun]) {
+    const uint32_t off = e.x, c = e.y;
+    const uint32_t r0 = q * kAeChunk + threadIdx.x * kAeRun;
+    Bal5 run{};
+#pragma unroll
+    for (uint32_t j = 0; j < kAeRun; j++)
+        v[j] = r0 + j < c ? S.G.vals_sorted[off + c - 1 - (r0 + j)] : kNone32;
+#pragma unroll
+    for (uint32_t j = 0; j < kAeRun; j++)
+        if (v[j] != kNone32) bal5_add(run, S.deltas[v[j]]);
+    return run;
+}
+
+// Every chunk's sums (one workgroup per chunk, grid-stride).
+__global__ void __launch_bounds__(kGroupBigThreads) ae_chunk_totals(AeScratch S) {
+    __shared__ Bal5Lds B;
+    const GroupPlan& G = S.G;
+    const uint32_t nchunks = G.counts[2];
+    for (uint32_t g = blockIdx.x; g < nchunks; g += gridDim.x) {
+        const uint32_t b = S.chunk_seg[g];
+        const uint4 e = G.big[b];
+        uint32_t v[kAeRun];
+        const Bal5 run = ae_chunk_run(S, e, g - e.w, v);
+        Bal5 total;
+        (void)bal5_block_exclusive(run, &total, B);
+        if (threadIdx.x == 0) S.chunk_tot[g] = total;
+    }
+}
+
+// Every chunk's touches emitted: later sums = the totals of the account's chunks before this one
+// (chunk 0 holds its last touches; summed by the first wave) + the lanes before in the chunk + the
+// run's touches after.
+__global__ void __launch_bounds__(kGroupBigThreads) ae_chunk_emit(Tables T, AeScratch S,
+                                                                 tb_account_event_t* log) {
+    __shared__ Bal5Lds B;
+    __shared__ Bal5 carry_lds;
+    const GroupPlan& G = S.G;
+    const uint32_t nchunks = G.counts[2];
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    for (uint32_t g = blockIdx.x; g < nchunks; g += gridDim.x) {
+        const uint32_t b = S.chunk_seg[g];
+        const uint4 e = G.big[b];
+        const uint32_t q = g - e.w;
+        if (tid < 64) {  // chunks 0 .. q - 1 (the later touches): lanes sum, the wave reduces
+            u128 f[4] = {0, 0, 0, 0};
+            uint32_t fl = 0;
+            for (uint32_t j = lane; j < q; j += 64) {
+                const Bal5 t = S.chunk_tot[e.w + j];
+                f[0] += t.dp;
+                f[1] += t.dpo;
+                f[2] += t.cp;
+                f[3] += t.cpo;
+                fl += t.flips;
+            }
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) {
+#pragma unroll
+                for (int x = 0; x < 4; x++) {
+                    const uint64_t lo = __shfl_xor(uint64_t(f[x]), d, 64);
+                    const uint64_t hi = __shfl_xor(uint64_t(f[x] >> 64), d, 64);
+                    f[x] += (u128(hi) << 64) | lo;
+                }
+                fl += __shfl_xor(fl, d, 64);
+            }
+            if (lane == 0) {
+                carry_lds.dp = f[0];
+                carry_lds.dpo = f[1];
+                carry_lds.cp = f[2];
+                carry_lds.cpo = f[3];
+                carry_lds.flips = fl;
+            }
+        }
+        uint32_t v[kAeRun];
+        const Bal5 run = ae_chunk_run(S, e, q, v);
+        Bal5 chunk;
+        Bal5 later = bal5_block_exclusive(run, &chunk, B);  // (its barriers publish carry_lds)
+        later.dp += carry_lds.dp;
+        later.dpo += carry_lds.dpo;
+        later.cp += carry_lds.cp;
+        later.cpo += carry_lds.cpo;
+        later.flips += carry_lds.flips;
+        const tb_account_t& a = T.acc_rows[e.z];
+        for (uint32_t j = 0; j < kAeRun; j++) {
+            if (v[j] == kNone32) break;
+            ae_emit_touch(a, v[j], later, log);
+            bal5_add(later, S.deltas[v[j]]);
+        }
+        __syncthreads();  // (carry_lds is rewritten by the next chunk)
     }
 }
 

@@ -61,12 +61,15 @@ struct FlowScratch {
     unsigned long long* hkeys = nullptr;
     uint32_t *hcnt = nullptr, *hoff = nullptr, *loc = nullptr, *rank = nullptr;
     uint4* big = nullptr;
+    uint32_t* chunk_seg = nullptr;
+    unsigned long long* chunk_sum = nullptr;
+    unsigned int* seg_done = nullptr;
     // account lanes (lanes.hpp)
     LaneRec* recs = nullptr;
     uint32_t *mailbox = nullptr, *owner_starts = nullptr, *mb_index = nullptr;
     unsigned int* lane_counts = nullptr;
     uint32_t* dup_mark = nullptr;  // per event (batch_events_max)
-    unsigned int* counts = nullptr;  // [0] units [1] barriers [2] ready [4] grouped pairs [5] listed
+    unsigned int* counts = nullptr;  // [0] units [1] barriers [2] ready; [4..8] the grouping's
     unsigned long long* words = nullptr;  // [1] expiry_count at the plan's start
     UndoEntry* lane_undo = nullptr;
     unsigned int* engine = nullptr;  // flow engine queue counters
@@ -391,7 +394,8 @@ void free_flow(FlowScratch& F) {
     void* ptrs[] = {F.head8, F.barrier8, F.heads, F.unit_of, F.barriers, F.vals, F.vals_sorted,
                     F.succ, F.indeg, F.keys_sorted, F.steps, F.queue,
                     F.outcome, F.recs, F.mailbox, F.owner_starts, F.mb_index, F.exp_flag,
-                    F.hkeys, F.hcnt, F.hoff, F.loc, F.rank, F.big};
+                    F.hkeys, F.hcnt, F.hoff, F.loc, F.rank, F.big, F.chunk_seg, F.chunk_sum,
+                    F.seg_done};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     F.head8 = F.barrier8 = F.outcome = nullptr;
@@ -405,6 +409,9 @@ void free_flow(FlowScratch& F) {
     F.hkeys = nullptr;
     F.hcnt = F.hoff = F.loc = F.rank = nullptr;
     F.big = nullptr;
+    F.chunk_seg = nullptr;
+    F.chunk_sum = nullptr;
+    F.seg_done = nullptr;
     F.cap = F.slots = 0;
 }
 
@@ -413,7 +420,7 @@ int ensure_flow(tbg_ctx* ctx, uint64_t m) {
     bool ok = true;
     if (!F.dup_mark) {
         ok = dev_alloc(ctx, &F.dup_mark, ctx->opt.batch_events_max, true) &&
-             dev_alloc(ctx, &F.counts, 8, true) && dev_alloc(ctx, &F.words, 4, true) &&
+             dev_alloc(ctx, &F.counts, 12, true) && dev_alloc(ctx, &F.words, 4, true) &&
              dev_alloc(ctx, &F.lane_counts, 4, true) &&
              dev_alloc(ctx, &F.lane_undo, uint64_t(kFlowLanesMax) * kFlowUndoPerLane, false) &&
              dev_alloc(ctx, &F.engine, kFlowEngineWords, true) &&
@@ -436,7 +443,10 @@ int ensure_flow(tbg_ctx* ctx, uint64_t m) {
          dev_alloc(ctx, &F.exp_flag, cap, false) && dev_alloc(ctx, &F.owner_starts, kc, false) &&
          dev_alloc(ctx, &F.hkeys, slots, true) && dev_alloc(ctx, &F.hcnt, slots, true) &&
          dev_alloc(ctx, &F.hoff, slots, false) && dev_alloc(ctx, &F.loc, kc, false) &&
-         dev_alloc(ctx, &F.rank, kc, false) && dev_alloc(ctx, &F.big, kc / kGroupSmall + 1, false);
+         dev_alloc(ctx, &F.rank, kc, false) && dev_alloc(ctx, &F.big, kc / kGroupSmall + 1, false) &&
+         dev_alloc(ctx, &F.chunk_seg, kc / kGroupChunk + kc / kGroupSmall + 1, false) &&
+         dev_alloc(ctx, &F.chunk_sum, 2 * (kc / kGroupChunk + kc / kGroupSmall + 1), false) &&
+         dev_alloc(ctx, &F.seg_done, kc / kGroupSmall + 1, false);
     if (!ok) {
         free_flow(F);
         return TBG_EHIP;
@@ -493,6 +503,9 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
     G.keys_sorted = F.keys_sorted;
     G.big = F.big;
     G.counts = F.counts + 4;
+    G.chunk_seg = F.chunk_seg;
+    G.chunk_sum = F.chunk_sum;
+    G.seg_done = F.seg_done;
     G.unit_of = F.unit_of;
     G.succ = F.succ;
     G.indeg = F.indeg;
@@ -539,7 +552,8 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
     hipLaunchKernelGGL(group_scatter, dim3(grid_for(pairs)), block, 0, ctx->stream, G, pairs);
     hipLaunchKernelGGL(group_small, dim3(grid_for(F.slots)), block, 0, ctx->stream, ctx->T, G,
                        F.slots);
-    hipLaunchKernelGGL(group_big, dim3(kGroupBigBlocks), dim3(kGroupBigThreads), 0, ctx->stream,
+    hipLaunchKernelGGL(group_sort, dim3(kGroupBigBlocks), dim3(kGroupBigThreads), 0, ctx->stream, G);
+    hipLaunchKernelGGL(group_chunk, dim3(kGroupChunkBlocks), dim3(kGroupBigThreads), 0, ctx->stream,
                        ctx->T, G);
     rc = launch_scan(ctx, m, SelectReady{F.indeg, F.counts, F.queue, F.engine, &F.counts[2]});
     if (!rc) rc = select_flagged(ctx, F.barrier8, m, F.barriers, &F.counts[1]);
@@ -767,76 +781,85 @@ int64_t dump_impl(tbg_ctx* ctx, const Row* rows, const uint8_t* live, uint64_t u
 
 // ---- AccountEvents (events.hpp) ---------------------------------------------------------------
 
-int ensure_ae_scratch(tbg_ctx* ctx, uint64_t touches) {
-    if (touches <= ctx->ae_touch_cap) return 0;
-    AeScratch& S = ctx->ae;
-    void* ptrs[] = {S.keys, S.vals, S.keys_sorted, S.vals_sorted, S.deltas, S.seg, S.values,
-                    S.scanned};
+void free_ae_scratch(AeScratch& S) {
+    GroupPlan& G = S.G;
+    void* ptrs[] = {S.deltas, G.hkeys, G.hcnt, G.hoff, G.loc, G.rank, G.vals, G.vals_sorted, G.big,
+                    G.counts, S.chunk_seg, S.chunk_tot};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     S = AeScratch{};
+}
+
+int ensure_ae_scratch(tbg_ctx* ctx, uint64_t touches) {
+    if (touches <= ctx->ae_touch_cap) return 0;
+    AeScratch& S = ctx->ae;
+    free_ae_scratch(S);
     ctx->ae_touch_cap = 0;
     const uint64_t cap = std::max<uint64_t>(next_pow2(touches), 1u << 14);
-    if (!(dev_alloc(ctx, &S.keys, cap, false) && dev_alloc(ctx, &S.vals, cap, false) &&
-          dev_alloc(ctx, &S.keys_sorted, cap, false) && dev_alloc(ctx, &S.vals_sorted, cap, false) &&
-          dev_alloc(ctx, &S.deltas, cap, false) && dev_alloc(ctx, &S.seg, cap, false) &&
-          dev_alloc(ctx, &S.values, cap, false) && dev_alloc(ctx, &S.scanned, cap, false)))
+    const uint64_t slots = 2 * cap;  // grouping table load <= 0.5
+    GroupPlan& G = S.G;
+    if (!(dev_alloc(ctx, &S.deltas, cap, false) && dev_alloc(ctx, &G.hkeys, slots, true) &&
+          dev_alloc(ctx, &G.hcnt, slots, true) && dev_alloc(ctx, &G.hoff, slots, false) &&
+          dev_alloc(ctx, &G.loc, cap, false) && dev_alloc(ctx, &G.rank, cap, false) &&
+          dev_alloc(ctx, &G.vals, cap, false) && dev_alloc(ctx, &G.vals_sorted, cap, false) &&
+          dev_alloc(ctx, &G.big, cap / kGroupSmall + 1, false) && dev_alloc(ctx, &G.counts, 4, true) &&
+          dev_alloc(ctx, &S.chunk_seg, cap / kAeChunk + cap / kGroupSmall + 1, false) &&
+          dev_alloc(ctx, &S.chunk_tot, cap / kAeChunk + cap / kGroupSmall + 1, false)))
         return TBG_ENOMEM;
+    G.hmask = slots - 1;
     ctx->ae_touch_cap = cap;
     return 0;
 }
 
-// Appends m AccountEvents: `collect` writes their event-level fields and both touches of each;
-// the account halves follow from the final rows and the later events' sums per account.
+// Appends the AccountEvents of up to `n_upper` events (the exact count at d_count, or n_upper
+// itself when d_count is null): `collect` writes their event-level fields and groups both touches
+// of each by account (events.hpp); the account halves follow from the final rows and the later
+// touches' sums per account. One host synchronisation, for the count and the timestamp bounds.
 template <typename Collect>
-int ae_append(tbg_ctx* ctx, uint32_t m, Collect collect) {
-    if (m == 0) return 0;
-    if (ctx->ae_used + m > ctx->ae_cap) {
-        ctx->error = "account_events capacity exceeded";
-        return TBG_ENOSPC;
+int ae_append(tbg_ctx* ctx, uint32_t n_upper, const unsigned int* d_count, Collect collect) {
+    if (n_upper == 0) return 0;
+    if (ctx->ae_used + n_upper > ctx->ae_cap) {
+        unsigned int m = n_upper;
+        if (d_count) {
+            HIP_TRY(ctx, hipMemcpyAsync(&m, d_count, 4, hipMemcpyDeviceToHost, ctx->stream));
+            HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        }
+        if (ctx->ae_used + m > ctx->ae_cap) {
+            ctx->error = "account_events capacity exceeded";
+            return TBG_ENOSPC;
+        }
     }
-    const uint64_t touches = 2 * uint64_t(m);
-    int rc = ensure_ae_scratch(ctx, touches);
+    int rc = ensure_ae_scratch(ctx, 2 * uint64_t(n_upper));
     if (rc) return rc;
     AeScratch& S = ctx->ae;
+    const uint64_t slots = S.G.hmask + 1;
     tb_account_event_t* log = ctx->ae_log + ctx->ae_used;
     collect(S, log, ctx->ae_ref + ctx->ae_used);
-    uint32_t row_bits = 1;
-    while ((1ull << row_bits) < ctx->T.acc_rows_used) row_bits++;
-    size_t bytes = 0;
-    HIP_TRY(ctx, hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, S.keys, S.keys_sorted, S.vals,
-                                                    S.vals_sorted, int(touches), 0,
-                                                    int(32 + row_bits), ctx->stream));
-    rc = ensure_cub_temp(ctx, bytes);
+    rc = launch_scan(ctx, slots, ExclusiveSumU32{S.G.hcnt, S.G.hoff, &S.G.counts[0]});
     if (rc) return rc;
-    HIP_TRY(ctx, hipcub::DeviceRadixSort::SortPairs(ctx->cub_temp, bytes, S.keys, S.keys_sorted,
-                                                    S.vals, S.vals_sorted, int(touches), 0,
-                                                    int(32 + row_bits), ctx->stream));
-    hipLaunchKernelGGL(ae_values, dim3(grid_for(touches)), dim3(kBlock), 0, ctx->stream, S,
-                       uint32_t(touches));
-    Bal5 zero{};
-    bytes = 0;
-    HIP_TRY(ctx, hipcub::DeviceScan::ExclusiveScanByKey(nullptr, bytes, S.seg, S.values, S.scanned,
-                                                        Bal5Add(), zero, int(touches),
-                                                        hipcub::Equality(), ctx->stream));
-    rc = ensure_cub_temp(ctx, bytes);
-    if (rc) return rc;
-    HIP_TRY(ctx, hipcub::DeviceScan::ExclusiveScanByKey(ctx->cub_temp, bytes, S.seg, S.values,
-                                                        S.scanned, Bal5Add(), zero, int(touches),
-                                                        hipcub::Equality(), ctx->stream));
-    hipLaunchKernelGGL(ae_emit, dim3(grid_for(touches)), dim3(kBlock), 0, ctx->stream, ctx->T, S,
-                       uint32_t(touches), log);
+    const uint64_t pairs = 2 * uint64_t(n_upper);
+    hipLaunchKernelGGL(group_scatter, dim3(grid_for(pairs)), dim3(kBlock), 0, ctx->stream, S.G, pairs);
+    hipLaunchKernelGGL(ae_group_small, dim3(grid_for(slots)), dim3(kBlock), 0, ctx->stream, ctx->T,
+                       S, slots, log);
+    hipLaunchKernelGGL(ae_group_sort, dim3(kGroupBigBlocks), dim3(kGroupBigThreads), 0, ctx->stream,
+                       S);
+    hipLaunchKernelGGL(ae_chunk_totals, dim3(kAeChunkBlocks), dim3(kGroupBigThreads), 0,
+                       ctx->stream, S);
+    hipLaunchKernelGGL(ae_chunk_emit, dim3(kAeChunkBlocks), dim3(kGroupBigThreads), 0, ctx->stream,
+                       ctx->T, S, log);
+    hipLaunchKernelGGL(ae_tail, dim3(1), dim3(64), 0, ctx->stream, log, d_count, n_upper,
+                       ctx->ae_words + 1);
     tmark(ctx, "account_events");
     HIP_TRY(ctx, hipGetLastError());
     // The log stays in timestamp order unless this block starts before the last one ended (an
     // imported batch after a pulse's expiries); then get_change_events sorts it first.
-    uint64_t first = 0, last = 0;
-    HIP_TRY(ctx, hipMemcpyAsync(&first, &log[0].timestamp, 8, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(ctx, hipMemcpyAsync(&last, &log[m - 1].timestamp, 8, hipMemcpyDeviceToHost,
-                                ctx->stream));
+    unsigned long long tail[3] = {0, 0, 0};  // count, first timestamp, last timestamp
+    HIP_TRY(ctx, hipMemcpyAsync(tail, ctx->ae_words + 1, 24, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    if (ctx->ae_used && first <= ctx->ae_last_ts) ctx->ae_sorted = false;
-    ctx->ae_last_ts = std::max(ctx->ae_last_ts, last);
+    const uint64_t m = tail[0];
+    if (m == 0) return 0;
+    if (ctx->ae_used && tail[1] <= ctx->ae_last_ts) ctx->ae_sorted = false;
+    ctx->ae_last_ts = std::max<uint64_t>(ctx->ae_last_ts, tail[2]);
     ctx->ae_used += m;
     return 0;
 }
@@ -848,22 +871,22 @@ int ae_transfers(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
     unsigned int* d_count = reinterpret_cast<unsigned int*>(ctx->ae_words);
     int rc = select_flagged(ctx, ctx->ae_flags, c.n, ctx->ae_list, d_count);
     if (rc) return rc;
-    unsigned int m = 0;
-    HIP_TRY(ctx, hipMemcpyAsync(&m, d_count, 4, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     const uint32_t* list = ctx->ae_list;
-    return ae_append(ctx, m, [&](const AeScratch& S, tb_account_event_t* log, AeRef* refs) {
-        hipLaunchKernelGGL(ae_collect_transfers, dim3(grid_for(m)), dim3(kBlock), 0, ctx->stream,
-                           ctx->T, c, list, m, S, log, refs);
+    return ae_append(ctx, c.n, d_count, [&](const AeScratch& S, tb_account_event_t* log,
+                                           AeRef* refs) {
+        hipLaunchKernelGGL(ae_collect_transfers, dim3((c.n + kPlanThreads - 1) / kPlanThreads),
+                           dim3(kPlanThreads), 0, ctx->stream, ctx->T, c, list, d_count, S, log,
+                           refs);
     });
 }
 
 // AccountEvents of a pulse: the expired rows in expiry order.
 int ae_expiry(tbg_ctx* ctx, const uint64_t* rows, uint64_t m, uint64_t timestamp) {
-    return ae_append(ctx, uint32_t(m), [&](const AeScratch& S, tb_account_event_t* log,
-                                           AeRef* refs) {
-        hipLaunchKernelGGL(ae_collect_expiry, dim3(grid_for(m)), dim3(kBlock), 0, ctx->stream,
-                           ctx->T, rows, uint32_t(m), timestamp, S, log, refs);
+    return ae_append(ctx, uint32_t(m), nullptr, [&](const AeScratch& S, tb_account_event_t* log,
+                                                    AeRef* refs) {
+        hipLaunchKernelGGL(ae_collect_expiry, dim3((uint32_t(m) + kPlanThreads - 1) / kPlanThreads),
+                           dim3(kPlanThreads), 0, ctx->stream, ctx->T, rows, uint32_t(m), timestamp,
+                           S, log, refs);
     });
 }
 
@@ -1087,9 +1110,8 @@ void tbg_close(tbg_ctx* ctx) {
                     ctx->flow.dup_mark, ctx->flow.counts, ctx->flow.words, ctx->flow.lane_counts,
                     ctx->scan_status, ctx->scan_ticket,
                     ctx->flow.lane_undo, ctx->flow.engine, ctx->flow.acc_free,
-                    ctx->ae_log, ctx->ae_ref, ctx->ae_flags, ctx->ae_list, ctx->ae_words,
-                    ctx->ae.keys, ctx->ae.vals, ctx->ae.keys_sorted, ctx->ae.vals_sorted,
-                    ctx->ae.deltas, ctx->ae.seg, ctx->ae.values, ctx->ae.scanned};
+                    ctx->ae_log, ctx->ae_ref, ctx->ae_flags, ctx->ae_list, ctx->ae_words};
+    free_ae_scratch(ctx->ae);
     free_flow(ctx->flow);
     for (void* p : ptrs)
         if (p) (void)hipFree(p);

@@ -105,7 +105,7 @@ __global__ void flow_heads(Tables T, Call<tb_transfer_t> c, FlowPlan P) {
     if (s < kFlowEngineWords) P.engine[s] = 0;
     if (s < 4) P.lane_counts[s] = 0;
     if (s == 0) {
-        P.counts[5] = P.counts[6] = P.counts[7] = 0;
+        P.counts[5] = P.counts[6] = P.counts[7] = P.counts[8] = 0;
     }
     if (s >= P.m) return;
     const uint32_t k = P.slow_list[s];

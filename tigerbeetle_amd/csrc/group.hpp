@@ -2,7 +2,7 @@
 // group in call order -- what the flow replay's edges and the account lanes' walks are read from.
 //
 // A library radix sort of the 64-bit (key, unit) words took ~20 launches per call (merge passes)
-// and the lanes' pre-passes another ~10; the grouping here is five launches, none of them a sort of
+// and the lanes' pre-passes another ~10; the grouping here is six launches, none of them a sort of
 // the whole pair array:
 //
 //   plan_keys      per replayed event: its keys (flow_keys' rules), its step record, the lanes'
@@ -13,15 +13,17 @@
 //   chained_scan   the slots' exclusive sums: every key's segment in the grouped array.
 //   group_scatter  pair -> its segment at its rank (arrival order, not yet call order).
 //   group_small    per slot: a segment of <= 16 pairs is sorted in registers by pair index (pair
-//                  index 4 * position + j grows with the unit); larger ones are listed. Then the
+//                  index 4 * position + j grows with the unit), one of <= 256 by the slot's wave
+//                  (a rank sort through LDS), larger ones are listed. Then the
 //                  segment's edges (a pair whose predecessor in the segment belongs to another
 //                  unit adds to that unit's in-degree; the last pair of a unit's run names the
 //                  next unit as its successor), its (key, unit) words, and -- for the account lanes
 //                  -- owner segments with their free-owner verdict (lanes.hpp). The slot is
 //                  cleared for the next call (the table is never memset).
-//   group_big      per listed segment, one workgroup: <= 8192 pairs by a bitonic sort in LDS,
-//                  more by bitmaps of 2^20 pair indices in LDS (set bits, prefix popcounts,
-//                  enumerate); then the same per-segment work.
+//   group_sort     per listed segment, one workgroup: bitmaps of up to 2^20 pair indices in LDS
+//                  over the segment's range (set bits, prefix popcounts, enumerate).
+//   group_chunk    per 2048-pair chunk of a listed segment, one workgroup: the same per-pair work;
+//                  an owner segment's last chunk adds up the chunks' contributions.
 //
 // Segments are disjoint and each is in call order, which is all the consumers read: flow_replay
 // (succ / indeg), lanes_walk / lanes_replay (a segment ends where the key changes; the grouped
@@ -34,12 +36,14 @@
 namespace tbg {
 
 constexpr uint32_t kGroupSmall = 16;        // segments sorted in registers
+constexpr uint32_t kGroupMid = 256;         // segments sorted by one wave (rank sort, LDS)
 constexpr uint32_t kGroupBigThreads = 512;
-constexpr uint32_t kGroupMedium = 8192;     // segments sorted by an LDS bitonic sort
-constexpr uint32_t kGroupLdsWords = 32768;  // 128 KB: bitonic vals + units, or one bitmap window
+constexpr uint32_t kGroupLdsWords = 32768;  // 128 KB: one bitmap window
 constexpr uint32_t kGroupWindowBits = kGroupLdsWords * 32;
 constexpr uint32_t kGroupBigBlocks = 256;
-constexpr uint32_t kGroupBatch = 8;         // pairs per lane per batch of loads (group_big)
+constexpr uint32_t kGroupBatch = 4;         // consecutive pairs per lane (group_chunk)
+constexpr uint32_t kGroupChunk = kGroupBigThreads * kGroupBatch;  // pairs per group_chunk workgroup
+constexpr uint32_t kGroupChunkBlocks = 512;  // group_chunk grid (grid-stride over the chunks)
 constexpr uint32_t kPlanThreads = 256;      // plan_keys workgroup: 1024 pairs
 constexpr uint32_t kPlanLdsSlots = 2048;    // LDS aggregation table (load <= 0.5)
 
@@ -55,7 +59,11 @@ struct GroupPlan {
     uint64_t* keys_sorted;          // grouped (key, unit) words: flow_key(type, index, unit)
     uint4* big;                     // listed segments: {offset, count, key lo, key hi}
     unsigned int* counts;           // [0] grouped pairs, [1] listed segments, [2] / [3] the
-                                    // longest id-key / account-key segment (pairs)
+                                    // longest id-key / account-key segment (pairs), [4] chunks
+                                    // of the listed segments
+    uint32_t* chunk_seg;            // per chunk of a listed segment: the segment's entry in big
+    unsigned long long* chunk_sum;  // per chunk: u128 {lo, hi} of its owner contributions
+    unsigned int* seg_done;         // per listed segment: chunks finished (group_chunk)
     const uint32_t* unit_of;        // per position
     uint32_t* succ;                 // per pair
     uint32_t* indeg;                // per unit
@@ -87,18 +95,61 @@ __device__ inline uint32_t group_slot(const GroupPlan& G, uint64_t key) {
     }
 }
 
+// Counting keys by slot within one workgroup (kPlanThreads lanes): each lane inserts its keys
+// (group_slot) and counts them in an LDS table of the workgroup's slots; then one global add per
+// slot turns the LDS counts into bases, and every pair gets its slot and rank. All lanes call the
+// three steps in order.
+struct GroupBlock {
+    uint32_t slot[kPlanLdsSlots];
+    uint32_t count[kPlanLdsSlots];
+};
+__device__ inline void group_block_init(GroupBlock& B) {
+    for (uint32_t i = threadIdx.x; i < kPlanLdsSlots; i += kPlanThreads) {
+        B.slot[i] = kNone32;
+        B.count[i] = 0;
+    }
+    __syncthreads();
+}
+// Counts `key` in the workgroup: returns its LDS entry (*lrank: its rank among the workgroup's).
+__device__ inline uint32_t group_block_add(const GroupPlan& G, GroupBlock& B, uint64_t key,
+                                           uint32_t* lrank) {
+    const uint32_t slot = group_slot(G, key);
+    uint32_t h = uint32_t(mix64(slot)) & (kPlanLdsSlots - 1);
+    while (true) {
+        const uint32_t o = atomicCAS(&B.slot[h], kNone32, slot);
+        if (o == kNone32 || o == slot) break;
+        h = (h + 1) & (kPlanLdsSlots - 1);
+    }
+    *lrank = atomicAdd(&B.count[h], 1u);
+    return h;
+}
+// One global add per slot of the workgroup: B.count becomes the slot's base.
+__device__ inline void group_block_publish(const GroupPlan& G, GroupBlock& B) {
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < kPlanLdsSlots; i += kPlanThreads) {
+        const uint32_t slot = B.slot[i];
+        if (slot != kNone32) B.count[i] = atomicAdd(&G.hcnt[slot], B.count[i]);
+    }
+    __syncthreads();
+}
+// Pair `pair`'s slot and rank (entry kNone32: no key).
+__device__ inline void group_block_place(const GroupPlan& G, const GroupBlock& B, uint64_t pair,
+                                         uint32_t entry, uint32_t lrank) {
+    if (entry == kNone32) {
+        G.loc[pair] = kNone32;
+    } else {
+        G.loc[pair] = B.slot[entry];
+        G.rank[pair] = B.count[entry] + lrank;
+    }
+}
+
 // Everything per replayed event s (flow_keys' and lanes_check's rules); its keys' grouping slots
 // and ranks. Launched with kPlanThreads per workgroup.
 __global__ void __launch_bounds__(kPlanThreads) plan_keys(Tables T, Call<tb_transfer_t> c,
                                                           FlowPlan P, GroupPlan G,
                                                           LanePlan L, unsigned int call_flags) {
-    __shared__ uint32_t agg_slot[kPlanLdsSlots];
-    __shared__ uint32_t agg_count[kPlanLdsSlots];
-    for (uint32_t i = threadIdx.x; i < kPlanLdsSlots; i += kPlanThreads) {
-        agg_slot[i] = kNone32;
-        agg_count[i] = 0;
-    }
-    __syncthreads();
+    __shared__ GroupBlock B;
+    group_block_init(B);
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     uint64_t key[kFlowKeys] = {kFlowNoKey, kFlowNoKey, kFlowNoKey, kFlowNoKey};
     uint32_t local[kFlowKeys] = {kNone32, kNone32, kNone32, kNone32};
@@ -200,41 +251,18 @@ __global__ void __launch_bounds__(kPlanThreads) plan_keys(Tables T, Call<tb_tran
         }
         // Grouping: the global slot, then this workgroup's count of the slot in LDS.
 #pragma unroll
-        for (uint32_t j = 0; j < kFlowKeys; j++) {
-            if (key[j] == kFlowNoKey) continue;
-            const uint32_t slot = group_slot(G, key[j]);
-            uint32_t h = uint32_t(mix64(slot)) & (kPlanLdsSlots - 1);
-            while (true) {
-                const uint32_t o = atomicCAS(&agg_slot[h], kNone32, slot);
-                if (o == kNone32 || o == slot) break;
-                h = (h + 1) & (kPlanLdsSlots - 1);
-            }
-            local[j] = h;
-            lrank[j] = atomicAdd(&agg_count[h], 1u);
-        }
+        for (uint32_t j = 0; j < kFlowKeys; j++)
+            if (key[j] != kFlowNoKey) local[j] = group_block_add(G, B, key[j], &lrank[j]);
     }
     if (G.lanes) {
         const uint64_t bad = __ballot(ineligible);
         if ((threadIdx.x & 63) == 0 && bad) atomicAdd(&L.counts[1], uint32_t(__popcll(bad)));
     }
-    __syncthreads();
-    // One global add per slot of this workgroup: agg_count becomes the slot's base.
-    for (uint32_t i = threadIdx.x; i < kPlanLdsSlots; i += kPlanThreads) {
-        const uint32_t slot = agg_slot[i];
-        if (slot != kNone32) agg_count[i] = atomicAdd(&G.hcnt[slot], agg_count[i]);
-    }
-    __syncthreads();
+    group_block_publish(G, B);
     if (s >= P.m) return;
 #pragma unroll
-    for (uint32_t j = 0; j < kFlowKeys; j++) {
-        const uint64_t pair = kFlowKeys * uint64_t(s) + j;
-        if (local[j] == kNone32) {
-            G.loc[pair] = kNone32;
-        } else {
-            G.loc[pair] = agg_slot[local[j]];
-            G.rank[pair] = agg_count[local[j]] + lrank[j];
-        }
-    }
+    for (uint32_t j = 0; j < kFlowKeys; j++)
+        group_block_place(G, B, kFlowKeys * uint64_t(s) + j, local[j], lrank[j]);
 }
 
 __global__ void group_scatter(GroupPlan G, uint64_t pairs) {
@@ -306,51 +334,6 @@ __device__ inline void sort_network(uint32_t (&v)[N]) {
             }
 }
 
-__global__ void group_small(Tables T, GroupPlan G, uint64_t slots) {
-    const uint64_t h = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (h >= slots) return;
-    const uint32_t c = G.hcnt[h];
-    if (c == 0) return;
-    const uint64_t key = G.hkeys[h] - 1;
-    const uint32_t off = G.hoff[h];
-    G.hkeys[h] = 0;
-    G.hcnt[h] = 0;
-    if (c > 1) atomicMax(&G.counts[2 + (key >> 32)], c);
-    if (c > kGroupSmall) {
-        const uint32_t b = atomicAdd(&G.counts[1], 1u);
-        G.big[b] = make_uint4(off, c, uint32_t(key), uint32_t(key >> 32));
-        return;
-    }
-    if (c == 1) {
-        const uint32_t v = G.vals[off];
-        group_emit(G, off, key, v, G.unit_of[v / kFlowKeys], kNone32, kNone32);
-        if (group_owner_probe(T, G, key)) {
-            group_owner_add(G, off);
-            group_owner_verdict(T, G, uint32_t(key), group_owner_contrib(G, uint32_t(key), v));
-        }
-        return;
-    }
-    uint32_t v[kGroupSmall], u[kGroupSmall];
-#pragma unroll
-    for (uint32_t i = 0; i < kGroupSmall; i++) v[i] = i < c ? G.vals[off + i] : kNone32;
-    sort_network(v);
-#pragma unroll
-    for (uint32_t i = 0; i < kGroupSmall; i++) u[i] = i < c ? G.unit_of[v[i] / kFlowKeys] : kNone32;
-#pragma unroll
-    for (uint32_t i = 0; i < kGroupSmall; i++)
-        if (i < c)
-            group_emit(G, off + i, key, v[i], u[i], i > 0 ? u[i - 1] : kNone32,
-                       i + 1 < kGroupSmall ? u[i + 1] : kNone32);
-    if (group_owner_probe(T, G, key)) {
-        group_owner_add(G, off);
-        u128 sum = 0;
-#pragma unroll
-        for (uint32_t i = 0; i < kGroupSmall; i++)
-            if (i < c) sum += group_owner_contrib(G, uint32_t(key), v[i]);
-        group_owner_verdict(T, G, uint32_t(key), sum);
-    }
-}
-
 // Workgroup sums (kGroupBigThreads lanes).
 __device__ inline uint32_t group_block_exclusive(uint32_t x, uint32_t* total, uint32_t* scratch) {
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -367,140 +350,250 @@ __device__ inline uint32_t group_block_exclusive(uint32_t x, uint32_t* total, ui
     return before + incl - x;
 }
 
-__global__ void __launch_bounds__(kGroupBigThreads) group_big(Tables T, GroupPlan G) {
-    __shared__ uint32_t buf[kGroupLdsWords];
-    __shared__ uint32_t scratch[kGroupBigThreads / 64];
-    __shared__ uint32_t red_min[kGroupBigThreads / 64], red_max[kGroupBigThreads / 64];
-    __shared__ unsigned long long red_lo[kGroupBigThreads / 64], red_hi[kGroupBigThreads / 64];
+// LDS of a segment-sorting workgroup.
+struct SegmentLds {
+    uint32_t buf[kGroupLdsWords];
+    uint32_t scratch[kGroupBigThreads / 64];
+    uint32_t red_min[kGroupBigThreads / 64], red_max[kGroupBigThreads / 64];
+};
+
+// Sorts the c distinct values in[off, off + c) ascending into out[off, off + c) (one workgroup of
+// kGroupBigThreads; visible to the whole workgroup on return): bitmap windows of up to
+// kGroupWindowBits values in LDS over the values' range -- set bits, prefix popcounts, enumerate.
+__device__ inline void segment_sort(const uint32_t* in, uint32_t* out, uint32_t off, uint32_t c,
+                                    SegmentLds& L) {
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    uint32_t* buf = L.buf;
+    uint32_t lo = kNone32, hi = 0;
+    for (uint32_t i = tid; i < c; i += kGroupBigThreads) {
+        const uint32_t v = in[off + i];
+        lo = min(lo, v);
+        hi = max(hi, v);
+    }
+    for (int d = 32; d >= 1; d >>= 1) {
+        lo = min(lo, uint32_t(__shfl_xor(lo, d, 64)));
+        hi = max(hi, uint32_t(__shfl_xor(hi, d, 64)));
+    }
+    if (lane == 0) {
+        L.red_min[wave] = lo;
+        L.red_max[wave] = hi;
+    }
+    __syncthreads();
+    lo = L.red_min[0];
+    hi = L.red_max[0];
+    for (uint32_t w = 1; w < kGroupBigThreads / 64; w++) {
+        lo = min(lo, L.red_min[w]);
+        hi = max(hi, L.red_max[w]);
+    }
+    uint32_t placed = 0;
+    for (uint64_t wb = lo; wb <= hi; wb += kGroupWindowBits) {
+        // the window's words, rounded up to whole lanes' shares
+        const uint64_t span = hi - wb + 1 < kGroupWindowBits ? hi - wb + 1 : kGroupWindowBits;
+        const uint32_t per = uint32_t((span + 32 * kGroupBigThreads - 1) / (32 * kGroupBigThreads));
+        const uint32_t words = per * kGroupBigThreads;
+        for (uint32_t i = tid; i < words; i += kGroupBigThreads) buf[i] = 0;
+        __syncthreads();
+        for (uint32_t i = tid; i < c; i += kGroupBigThreads) {
+            const uint32_t v = in[off + i];
+            if (v >= wb && v - wb < kGroupWindowBits) {
+                const uint32_t d = uint32_t(v - wb);
+                atomicOr(&buf[d >> 5], 1u << (d & 31));
+            }
+        }
+        __syncthreads();
+        uint32_t mine = 0;
+        for (uint32_t w = 0; w < per; w++) mine += __popc(buf[tid * per + w]);
+        uint32_t total = 0;
+        uint32_t r = placed + group_block_exclusive(mine, &total, L.scratch);
+        for (uint32_t w = 0; w < per; w++) {
+            uint32_t bits = buf[tid * per + w];
+            while (bits) {
+                const uint32_t bit = __builtin_ctz(bits);
+                bits &= bits - 1;
+                out[off + r++] = uint32_t(wb + uint64_t(tid * per + w) * 32 + bit);
+            }
+        }
+        placed += total;
+        __syncthreads();
+    }
+    __threadfence();
+    __syncthreads();
+}
+
+// A segment of kGroupSmall < c <= kGroupMid values sorted by one wave: lane l holds values
+// l + 64 j; each value's rank is the count of smaller values (every value broadcast once); the
+// values land in buf[rank]. All lanes of the wave call it with the same arguments.
+__device__ inline void wave_rank_sort(const uint32_t* in, uint32_t off, uint32_t c, uint32_t* buf) {
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t x[4], r[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) x[j] = lane + 64 * j < c ? in[off + lane + 64 * j] : kNone32;
+    for (uint32_t s = 0; s < c; s++) {
+        const uint32_t src = s < 64 ? x[0] : s < 128 ? x[1] : s < 192 ? x[2] : x[3];
+        const uint32_t y = __shfl(src, s & 63, 64);
+#pragma unroll
+        for (uint32_t j = 0; j < 4; j++) r[j] += y < x[j];
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++)
+        if (lane + 64 * j < c) buf[r[j]] = x[j];
+    wave_lds_sync();
+}
+
+// The flow plan's per-segment work for a wave-sorted segment (group_small's mid tier).
+__device__ inline void group_mid_segment(Tables T, const GroupPlan& G, uint32_t off, uint32_t c,
+                                         uint64_t key, uint32_t* buf) {
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t* units = buf + kGroupMid;
+    wave_rank_sort(G.vals, off, c, buf);
+    const bool owner = group_owner_probe(T, G, key);
+    const uint32_t row = uint32_t(key);
+    uint64_t sum_lo = 0, sum_hi = 0;
+    uint32_t uu[4];
+    uint64_t aa[4];
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) {
+        const uint32_t p = lane + 64 * j;
+        uu[j] = p < c ? G.unit_of[buf[p] / kFlowKeys] : 0u;
+        aa[j] = owner && p < c ? group_owner_contrib(G, row, buf[p]) : 0u;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) {
+        if (lane + 64 * j < c) units[lane + 64 * j] = uu[j];
+        sum_lo += aa[j];
+        sum_hi += sum_lo < aa[j];
+    }
+    wave_lds_sync();
+    for (uint32_t p = lane; p < c; p += 64)
+        group_emit(G, off + p, key, buf[p], units[p], p > 0 ? units[p - 1] : kNone32,
+                   p + 1 < c ? units[p + 1] : kNone32);
+    if (owner) {
+        for (int d = 32; d >= 1; d >>= 1) {
+            const uint64_t olo = __shfl_xor(sum_lo, d, 64);
+            const uint64_t ohi = __shfl_xor(sum_hi, d, 64);
+            const uint64_t nlo = sum_lo + olo;
+            sum_hi = sum_hi + ohi + (nlo < sum_lo ? 1u : 0u);
+            sum_lo = nlo;
+        }
+        if (lane == 0) {
+            group_owner_add(G, off);
+            group_owner_verdict(T, G, row, (u128(sum_hi) << 64) | sum_lo);
+        }
+    }
+    wave_lds_sync();  // (buf is reused by the wave's next segment)
+}
+
+__global__ void __launch_bounds__(kBlock) group_small(Tables T, GroupPlan G, uint64_t slots) {
+    __shared__ uint32_t wave_buf[kBlock / 64][2 * kGroupMid];
+    const uint64_t h = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    uint32_t c = 0, off = 0;
+    uint64_t key = 0;
+    if (h < slots) {
+        c = G.hcnt[h];
+        if (c) {
+            key = G.hkeys[h] - 1;
+            off = G.hoff[h];
+            G.hkeys[h] = 0;
+            G.hcnt[h] = 0;
+            if (c > 1) atomicMax(&G.counts[2 + (key >> 32)], c);
+        }
+    }
+    if (c > kGroupMid) {
+        // Listed: ordered by group_sort, emitted by group_chunk in chunks of kGroupChunk pairs.
+        const uint32_t b = atomicAdd(&G.counts[1], 1u);
+        const uint32_t chunks = (c + kGroupChunk - 1) / kGroupChunk;
+        const uint32_t cb = atomicAdd(&G.counts[4], chunks);
+        G.big[b] = make_uint4(off, c, uint32_t(key), (uint32_t(key >> 32) << 31) | cb);
+        G.seg_done[b] = 0;
+        for (uint32_t q = 0; q < chunks; q++) G.chunk_seg[cb + q] = b;
+    } else if (c == 1) {
+        const uint32_t v = G.vals[off];
+        group_emit(G, off, key, v, G.unit_of[v / kFlowKeys], kNone32, kNone32);
+        if (group_owner_probe(T, G, key)) {
+            group_owner_add(G, off);
+            group_owner_verdict(T, G, uint32_t(key), group_owner_contrib(G, uint32_t(key), v));
+        }
+    } else if (c > 1 && c <= kGroupSmall) {
+        uint32_t v[kGroupSmall], u[kGroupSmall];
+#pragma unroll
+        for (uint32_t i = 0; i < kGroupSmall; i++) v[i] = i < c ? G.vals[off + i] : kNone32;
+        sort_network(v);
+#pragma unroll
+        for (uint32_t i = 0; i < kGroupSmall; i++) u[i] = i < c ? G.unit_of[v[i] / kFlowKeys] : kNone32;
+#pragma unroll
+        for (uint32_t i = 0; i < kGroupSmall; i++)
+            if (i < c)
+                group_emit(G, off + i, key, v[i], u[i], i > 0 ? u[i - 1] : kNone32,
+                           i + 1 < kGroupSmall ? u[i + 1] : kNone32);
+        if (group_owner_probe(T, G, key)) {
+            group_owner_add(G, off);
+            u128 sum = 0;
+#pragma unroll
+            for (uint32_t i = 0; i < kGroupSmall; i++)
+                if (i < c) sum += group_owner_contrib(G, uint32_t(key), v[i]);
+            group_owner_verdict(T, G, uint32_t(key), sum);
+        }
+    }
+    // The wave's mid-size segments, one at a time by the whole wave.
+    uint64_t mids = __ballot(c > kGroupSmall && c <= kGroupMid);
+    while (mids) {
+        const int l = __ffsll((unsigned long long)mids) - 1;
+        mids &= mids - 1;
+        const uint32_t moff = __shfl(off, l, 64), mc = __shfl(c, l, 64);
+        const uint64_t mkey = (uint64_t(uint32_t(__shfl(uint32_t(key >> 32), l, 64))) << 32) |
+                              uint32_t(__shfl(uint32_t(key), l, 64));
+        group_mid_segment(T, G, moff, mc, mkey, wave_buf[threadIdx.x >> 6]);
+    }
+}
+
+// Listed segments, one workgroup each: the pairs in call order into vals_sorted.
+__global__ void __launch_bounds__(kGroupBigThreads) group_sort(GroupPlan G) {
+    __shared__ SegmentLds L;
     const uint32_t nbig = G.counts[1];
     for (uint32_t b = blockIdx.x; b < nbig; b += gridDim.x) {
         const uint4 e = G.big[b];
-        const uint32_t off = e.x, c = e.y;
-        const uint64_t key = (uint64_t(e.w) << 32) | e.z;
+        segment_sort(G.vals, G.vals_sorted, e.x, e.y, L);
+    }
+}
+
+// Chunks of the listed segments, one workgroup each (grid-stride): kGroupBatch consecutive pairs
+// per lane with both neighbours, every load of a batch issued before any is used; an owner
+// segment's chunks sum their contributions, and the segment's last chunk to finish (a counter,
+// release / acquire at agent scope) adds them up for the free verdict and registers the owner.
+__global__ void __launch_bounds__(kGroupBigThreads) group_chunk(Tables T, GroupPlan G) {
+    __shared__ unsigned long long red_lo[kGroupBigThreads / 64], red_hi[kGroupBigThreads / 64];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t nchunks = G.counts[4];
+    for (uint32_t g = blockIdx.x; g < nchunks; g += gridDim.x) {
+        const uint32_t b = G.chunk_seg[g];
+        const uint4 e = G.big[b];
+        const uint32_t off = e.x, c = e.y, cb = e.w & 0x7FFFFFFFu;
+        const uint64_t key = (uint64_t(e.w >> 31) << 32) | e.z;
+        const uint32_t row = e.z;
         const bool owner = group_owner_probe(T, G, key);
-        const uint32_t row = uint32_t(key);
+        const uint32_t q = g - cb, chunks = (c + kGroupChunk - 1) / kGroupChunk;
         uint64_t sum_lo = 0, sum_hi = 0;
-        if (c <= kGroupMedium) {
-            uint32_t p2 = 32;
-            while (p2 < c) p2 <<= 1;
-            for (uint32_t i = tid; i < p2; i += kGroupBigThreads)
-                buf[i] = i < c ? G.vals[off + i] : kNone32;
-            __syncthreads();
-            for (uint32_t k = 2; k <= p2; k <<= 1)
-                for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-                    for (uint32_t i = tid; i < p2; i += kGroupBigThreads) {
-                        const uint32_t l = i ^ j;
-                        if (l > i) {
-                            const uint32_t a = buf[i], bb = buf[l];
-                            if ((a > bb) == ((i & k) == 0)) {
-                                buf[i] = bb;
-                                buf[l] = a;
-                            }
-                        }
-                    }
-                    __syncthreads();
-                }
-            // (unit lookups: kGroupBatch independent loads in flight per lane)
-            uint32_t* units = buf + kGroupMedium;
-            for (uint32_t i0 = tid * kGroupBatch; i0 < c; i0 += kGroupBigThreads * kGroupBatch) {
-                uint32_t uu[kGroupBatch];
-                uint64_t aa[kGroupBatch];
+        const uint32_t i0 = q * kGroupChunk + tid * kGroupBatch;
+        if (i0 < c) {
+            uint32_t v[kGroupBatch + 2], u[kGroupBatch + 2];
 #pragma unroll
-                for (uint32_t j = 0; j < kGroupBatch; j++) {
-                    uu[j] = i0 + j < c ? G.unit_of[buf[i0 + j] / kFlowKeys] : 0u;
-                    aa[j] = owner && i0 + j < c ? group_owner_contrib(G, row, buf[i0 + j]) : 0u;
-                }
+            for (uint32_t j = 0; j < kGroupBatch + 2; j++) {
+                const int64_t at = int64_t(i0) + j - 1;
+                v[j] = at >= 0 && at < int64_t(c) ? G.vals_sorted[off + at] : kNone32;
+            }
+            uint64_t aa[kGroupBatch + 2];
 #pragma unroll
-                for (uint32_t j = 0; j < kGroupBatch; j++) {
-                    if (i0 + j < c) units[i0 + j] = uu[j];
-                    sum_lo += aa[j];
-                    sum_hi += sum_lo < aa[j];
-                }
+            for (uint32_t j = 0; j < kGroupBatch + 2; j++) {
+                u[j] = v[j] != kNone32 ? G.unit_of[v[j] / kFlowKeys] : kNone32;
+                aa[j] = owner && j >= 1 && j <= kGroupBatch && v[j] != kNone32
+                            ? group_owner_contrib(G, row, v[j]) : 0u;
             }
-            __syncthreads();
-            for (uint32_t i = tid; i < c; i += kGroupBigThreads) {
-                group_emit(G, off + i, key, buf[i], units[i], i > 0 ? units[i - 1] : kNone32,
-                           i + 1 < c ? units[i + 1] : kNone32);
-            }
-        } else {
-            // The segment's pair index range, then bitmap windows of kGroupWindowBits indices.
-            uint32_t lo = kNone32, hi = 0;
-            for (uint32_t i = tid; i < c; i += kGroupBigThreads) {
-                const uint32_t v = G.vals[off + i];
-                lo = min(lo, v);
-                hi = max(hi, v);
-            }
-            for (int d = 32; d >= 1; d >>= 1) {
-                lo = min(lo, uint32_t(__shfl_xor(lo, d, 64)));
-                hi = max(hi, uint32_t(__shfl_xor(hi, d, 64)));
-            }
-            if (lane == 0) {
-                red_min[wave] = lo;
-                red_max[wave] = hi;
-            }
-            __syncthreads();
-            lo = red_min[0];
-            hi = red_max[0];
-            for (uint32_t w = 1; w < kGroupBigThreads / 64; w++) {
-                lo = min(lo, red_min[w]);
-                hi = max(hi, red_max[w]);
-            }
-            uint32_t placed = 0;
-            for (uint64_t wb = lo; wb <= hi; wb += kGroupWindowBits) {
-                for (uint32_t i = tid; i < kGroupLdsWords; i += kGroupBigThreads) buf[i] = 0;
-                __syncthreads();
-                for (uint32_t i = tid; i < c; i += kGroupBigThreads) {
-                    const uint32_t v = G.vals[off + i];
-                    if (v >= wb && v - wb < kGroupWindowBits) {
-                        const uint32_t d = uint32_t(v - wb);
-                        atomicOr(&buf[d >> 5], 1u << (d & 31));
-                    }
-                }
-                __syncthreads();
-                constexpr uint32_t kWordsPerThread = kGroupLdsWords / kGroupBigThreads;
-                uint32_t mine = 0;
-                for (uint32_t w = 0; w < kWordsPerThread; w++)
-                    mine += __popc(buf[tid * kWordsPerThread + w]);
-                uint32_t total = 0;
-                uint32_t r = placed + group_block_exclusive(mine, &total, scratch);
-                for (uint32_t w = 0; w < kWordsPerThread; w++) {
-                    uint32_t bits = buf[tid * kWordsPerThread + w];
-                    while (bits) {
-                        const uint32_t bit = __builtin_ctz(bits);
-                        bits &= bits - 1;
-                        G.vals_sorted[off + r++] =
-                            uint32_t(wb + uint64_t(tid * kWordsPerThread + w) * 32 + bit);
-                    }
-                }
-                placed += total;
-                __syncthreads();
-            }
-            __threadfence();
-            __syncthreads();
-            // kGroupBatch consecutive pairs per lane, with both neighbours: every load of a batch
-            // is issued before any is used (two round trips per batch, not three per pair).
-            for (uint32_t i0 = tid * kGroupBatch; i0 < c; i0 += kGroupBigThreads * kGroupBatch) {
-                uint32_t v[kGroupBatch + 2], u[kGroupBatch + 2];
 #pragma unroll
-                for (uint32_t j = 0; j < kGroupBatch + 2; j++) {
-                    const int64_t at = int64_t(i0) + j - 1;
-                    v[j] = at >= 0 && at < int64_t(c) ? G.vals_sorted[off + at] : kNone32;
-                }
-                uint64_t aa[kGroupBatch + 2];
-#pragma unroll
-                for (uint32_t j = 0; j < kGroupBatch + 2; j++) {
-                    u[j] = v[j] != kNone32 ? G.unit_of[v[j] / kFlowKeys] : kNone32;
-                    aa[j] = owner && j >= 1 && j <= kGroupBatch && v[j] != kNone32
-                                ? group_owner_contrib(G, row, v[j]) : 0u;
-                }
-#pragma unroll
-                for (uint32_t j = 1; j <= kGroupBatch; j++) {
-                    if (i0 + j - 1 >= c) break;
-                    group_emit(G, off + i0 + j - 1, key, v[j], u[j], u[j - 1], u[j + 1]);
-                    sum_lo += aa[j];
-                    sum_hi += sum_lo < aa[j];
-                }
+            for (uint32_t j = 1; j <= kGroupBatch; j++) {
+                if (i0 + j - 1 >= c) break;
+                group_emit(G, off + i0 + j - 1, key, v[j], u[j], u[j - 1], u[j + 1]);
+                sum_lo += aa[j];
+                sum_hi += sum_lo < aa[j];
             }
         }
         if (owner) {
@@ -520,11 +613,25 @@ __global__ void __launch_bounds__(kGroupBigThreads) group_big(Tables T, GroupPla
                 u128 sum = 0;
                 for (uint32_t w = 0; w < kGroupBigThreads / 64; w++)
                     sum += (u128(red_hi[w]) << 64) | red_lo[w];
-                group_owner_add(G, off);
-                group_owner_verdict(T, G, row, sum);
+                G.chunk_sum[2 * uint64_t(g)] = uint64_t(sum);
+                G.chunk_sum[2 * uint64_t(g) + 1] = uint64_t(sum >> 64);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                if (atomicAdd(&G.seg_done[b], 1u) == chunks - 1) {
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    u128 all = 0;
+                    for (uint32_t j = 0; j < chunks; j++) {
+                        const uint64_t lo = __hip_atomic_load(&G.chunk_sum[2 * uint64_t(cb + j)],
+                                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        const uint64_t hi = __hip_atomic_load(&G.chunk_sum[2 * uint64_t(cb + j) + 1],
+                                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        all += (u128(hi) << 64) | lo;
+                    }
+                    group_owner_add(G, off);
+                    group_owner_verdict(T, G, row, all);
+                }
             }
+            __syncthreads();  // (red_* are rewritten by the next chunk)
         }
-        __syncthreads();  // (buf is reused by the next segment)
     }
 }
 
