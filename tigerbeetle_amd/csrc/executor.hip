@@ -644,22 +644,42 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
         (void)hipMemcpy(heads.data(), F.heads, units * 4ull, hipMemcpyDeviceToHost);
         (void)hipMemcpy(succ.data(), F.succ, succ.size() * 4, hipMemcpyDeviceToHost);
         std::vector<uint64_t> start(units, 0), depth(units, 0);
+        std::vector<uint32_t> via(units, kNone32), via_key(units, 0);  // the edge that set start
         uint64_t longest = 0, longest_units = 0;
+        uint32_t last = 0;
         for (uint32_t u = 0; u < units; u++) {
             const uint32_t b = heads[u], e = u + 1 < units ? heads[u + 1] : m;
             const uint64_t fin = start[u] + (e - b);
             const uint64_t dep = depth[u] + 1;
-            longest = std::max(longest, fin);
+            if (fin > longest) {
+                longest = fin;
+                last = u;
+            }
             longest_units = std::max(longest_units, dep);
             for (uint64_t i = uint64_t(kFlowKeys) * b; i < uint64_t(kFlowKeys) * e; i++) {
                 const uint32_t v = succ[i];
                 if (v == kNone32 || v >= units) continue;
-                start[v] = std::max(start[v], fin);
+                if (fin > start[v]) {
+                    start[v] = fin;
+                    via[v] = u;
+                    via_key[v] = uint32_t(i % kFlowKeys);
+                }
                 depth[v] = std::max(depth[v], dep);
             }
         }
-        fprintf(stderr, "flow: critical path %llu events, %llu units\n",
-                (unsigned long long)longest, (unsigned long long)longest_units);
+        // The path's edges by key kind: [0] id, [1] pending id, [2] debit account, [3] credit.
+        unsigned kinds[kFlowKeys] = {};
+        unsigned chain_units = 0, path_units = 0;
+        for (uint32_t u = last; u != kNone32; u = via[u]) {
+            path_units++;
+            const uint32_t b = heads[u], e = u + 1 < units ? heads[u + 1] : m;
+            chain_units += e - b > 1;
+            if (via[u] != kNone32) kinds[via_key[u]]++;
+        }
+        fprintf(stderr, "flow: critical path %llu events, %llu units (%u on the path, %u chains; "
+                "edges by key: id %u pending %u debit %u credit %u)\n",
+                (unsigned long long)longest, (unsigned long long)longest_units, path_units,
+                chain_units, kinds[0], kinds[1], kinds[2], kinds[3]);
     }
     HIP_TRY(ctx, hipGetLastError());
     return 0;

@@ -48,10 +48,18 @@ def kernel_ms(p):
 
 
 def line(name, p, n, t_wall, extra):
-    extra = dict(extra, kernels_ms=kernel_ms(p))
+    kms = kernel_ms(p)
+    extra = dict(extra, kernels_ms=kms)
     s = p.seconds
+    # Device time: the HIP-event spans of the calls' kernels plus the AccountEvents span (its
+    # kernels and one host sync); the other host:* entries (PCIe copies, the host-side parts of the
+    # calls) are left out.
+    dev_ms = sum(v for k, v in kms.items()
+                 if not k.startswith("host:") or k == "host:account_events")
     return {"config": name, "transfers": n, "validated": True,
             "gpu_transfers_per_s": round(n / s["gpu"], 1),
+            "device_ms": round(dev_ms, 3),
+            "device_transfers_per_s": round(n / (dev_ms / 1e3), 1) if dev_ms else None,
             "oracle_transfers_per_s": round(n / s["oracle"], 1), "oracle_cores": 1,
             "gpu_s": round(s["gpu"], 3), "oracle_s": round(s["oracle"], 3),
             "replayed": p.stats["replayed"], "fast": p.stats["fast"],
