@@ -44,6 +44,9 @@
 #ifndef TBG_INGEST_JOINT_PROBE
 #define TBG_INGEST_JOINT_PROBE 1
 #endif
+#ifndef TBG_INGEST_H1_FIRST
+#define TBG_INGEST_H1_FIRST 1  // account index: the first candidate only, the second on a miss
+#endif
 
 namespace tbg {
 
@@ -507,7 +510,26 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
         if (valid_id)
             w_seen = atomicCAS(&T.tr.slots[s_id], (unsigned long long)kEmpty,
                                (unsigned long long)tref);
-#if TBG_INGEST_JOINT_PROBE
+#if TBG_INGEST_H1_FIRST
+        {
+            // Most entries sit at their first candidate (load <= 0.25): one 16-byte load per
+            // account; the second candidate only for the lanes whose first one missed.
+            const AccIndex& x = T.acc_index;
+            const uint64_t d1 = vd ? acc_entry_h1(dr_id) & x.mask : 0;
+            const uint64_t c1 = vc ? acc_entry_h1(cr_id) & x.mask : 0;
+            AccProbe pd, pc;
+            pd.v1 = *reinterpret_cast<const uint4*>(&x.entries[d1]);
+            pc.v1 = *reinterpret_cast<const uint4*>(&x.entries[c1]);
+            const bool dm = vd && !acc_entry_match(pd.v1, T.acc_rows, dr_id);
+            const bool cm = vc && !acc_entry_match(pc.v1, T.acc_rows, cr_id);
+            pd.v2 = dm ? *reinterpret_cast<const uint4*>(&x.entries[acc_entry_h2(dr_id) & x.mask])
+                       : make_uint4(0, 0, 0, 0);
+            pc.v2 = cm ? *reinterpret_cast<const uint4*>(&x.entries[acc_entry_h2(cr_id) & x.mask])
+                       : make_uint4(0, 0, 0, 0);
+            dr = acc_probe_snap(T, pd, dr_id, vd, true);
+            cr = acc_probe_snap(T, pc, cr_id, vc, false);
+        }
+#elif TBG_INGEST_JOINT_PROBE
         const AccProbe pd = acc_probe_issue(T.acc_index, dr_id, vd);
         const AccProbe pc = acc_probe_issue(T.acc_index, cr_id, vc);
         dr = acc_probe_snap(T, pd, dr_id, vd, true);
