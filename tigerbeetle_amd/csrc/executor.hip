@@ -536,9 +536,8 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
     const uint64_t pairs = kFlowKeys * uint64_t(m);
     hipLaunchKernelGGL(flow_heads, dim3(grid_for(std::max<uint64_t>(m, kFlowEngineWords))), block,
                        0, ctx->stream, ctx->T, c, P);
-    rc = select_flagged(ctx, F.head8, m, F.heads, &F.counts[0]);
+    rc = launch_scan(ctx, m, SelectHeads{F.head8, F.heads, F.unit_of, &F.counts[0]});
     if (rc) return rc;
-    hipLaunchKernelGGL(flow_units, dim3(grid_for(m)), block, 0, ctx->stream, P);
     hipLaunchKernelGGL(plan_keys, dim3((m + kPlanThreads - 1) / kPlanThreads), dim3(kPlanThreads), 0,
                        ctx->stream, ctx->T, c, P, G, L, call_flags);
     // the planned expires_at entries

@@ -35,6 +35,7 @@
 #pragma once
 
 #include "kernels.hpp"
+#include "prims.hpp"
 
 namespace tbg {
 
@@ -116,6 +117,7 @@ __global__ void flow_heads(Tables T, Call<tb_transfer_t> c, FlowPlan P) {
         head = batch_start_of(c, b) == k;
     }
     P.head8[s] = head;
+    P.barrier8[s] = 0;  // (units < m: plan_keys sets the barriers)
     P.queue[s] = 0;  // (the ready units are selected into it after the grouping)
     if (s == 0) *P.exp_base = T.scalars->expiry_count;
     const uint32_t slot = c.ev_slot[k];
@@ -128,20 +130,24 @@ __global__ void flow_heads(Tables T, Call<tb_transfer_t> c, FlowPlan P) {
     }
 }
 
-// Positions of each unit; barrier flags of over-long chains.
-__global__ void flow_units(FlowPlan P) {
-    const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
-    if (u >= P.m) return;
-    const uint32_t units = P.counts[0];
-    if (u >= units) {
-        P.barrier8[u] = 0;
-        return;
+// Unit heads selected in order (heads[u] = the unit's first position) and every position's unit
+// (the inclusive count of heads up to it, minus one): one chained scan over head8.
+struct SelectHeads {
+    static constexpr bool kEmitAll = true;
+    const uint8_t* head8;
+    uint32_t* heads;
+    uint32_t* unit_of;
+    unsigned int* count;
+    __device__ void load(uint64_t base, uint64_t n, uint32_t* c) const {
+        SelectFlags8{head8, nullptr, nullptr}.load(base, n, c);
     }
-    const uint32_t begin = P.heads[u];
-    const uint32_t end = u + 1 < units ? P.heads[u + 1] : P.m;
-    for (uint32_t s = begin; s < end; s++) P.unit_of[s] = u;
-    P.barrier8[u] = end - begin > kFlowChainMax;
-}
+    __device__ void emit(uint64_t s, uint32_t p) const {
+        const bool head = head8[s] != 0;
+        if (head) heads[p] = uint32_t(s);
+        unit_of[s] = p + (head ? 1u : 0u) - 1u;
+    }
+    __device__ void total(uint32_t t) const { *count = t; }
+};
 
 // The engine: lanes spread over `blocks` workgroups (see the header). A unit is ready once every
 // predecessor has finished (indeg 0). Ready units wait in a queue; a lane pops one, runs it, and

@@ -159,6 +159,11 @@ __global__ void __launch_bounds__(kPlanThreads) plan_keys(Tables T, Call<tb_tran
         const uint32_t k = P.slow_list[s];
         const uint32_t u = P.unit_of[s];
         const tb_transfer_t& t = c.events[k];
+        // A chain longer than the lanes' undo logs is a barrier (the serial replay).
+        if (P.heads[u] == s) {
+            const uint32_t end = u + 1 < P.counts[0] ? P.heads[u + 1] : P.m;
+            if (end - s > kFlowChainMax) P.barrier8[u] = 1;
+        }
         auto keyless = [&](uint64_t row) { return acc_additive(T, row, P.add_epoch); };
         if (!u128_is_zero(t.id) && !u128_is_max(t.id)) key[0] = flow_id_key(t.id);
         if (t.flags & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) {
@@ -495,7 +500,18 @@ __global__ void __launch_bounds__(kBlock) group_small(Tables T, GroupPlan G, uin
             off = G.hoff[h];
             G.hkeys[h] = 0;
             G.hcnt[h] = 0;
-            if (c > 1) atomicMax(&G.counts[2 + (key >> 32)], c);
+        }
+    }
+    {  // the longest id-key / account-key segment (flow debug statistics): one atomic per wave
+        uint32_t id_max = (c > 1 && (key >> 32) == 0) ? c : 0u;
+        uint32_t acc_max = (c > 1 && (key >> 32) == 1) ? c : 0u;
+        for (int d = 32; d >= 1; d >>= 1) {
+            id_max = max(id_max, uint32_t(__shfl_xor(id_max, d, 64)));
+            acc_max = max(acc_max, uint32_t(__shfl_xor(acc_max, d, 64)));
+        }
+        if ((threadIdx.x & 63) == 0) {
+            if (id_max) atomicMax(&G.counts[2], id_max);
+            if (acc_max) atomicMax(&G.counts[3], acc_max);
         }
     }
     if (c > kGroupMid) {
@@ -513,7 +529,27 @@ __global__ void __launch_bounds__(kBlock) group_small(Tables T, GroupPlan G, uin
             group_owner_add(G, off);
             group_owner_verdict(T, G, uint32_t(key), group_owner_contrib(G, uint32_t(key), v));
         }
-    } else if (c > 1 && c <= kGroupSmall) {
+    } else if (c > 1 && c <= 4) {
+        uint32_t v[4], u[4];
+#pragma unroll
+        for (uint32_t i = 0; i < 4; i++) v[i] = i < c ? G.vals[off + i] : kNone32;
+        sort_network(v);
+#pragma unroll
+        for (uint32_t i = 0; i < 4; i++) u[i] = i < c ? G.unit_of[v[i] / kFlowKeys] : kNone32;
+#pragma unroll
+        for (uint32_t i = 0; i < 4; i++)
+            if (i < c)
+                group_emit(G, off + i, key, v[i], u[i], i > 0 ? u[i - 1] : kNone32,
+                           i + 1 < 4 ? u[i + 1] : kNone32);
+        if (group_owner_probe(T, G, key)) {
+            group_owner_add(G, off);
+            u128 sum = 0;
+#pragma unroll
+            for (uint32_t i = 0; i < 4; i++)
+                if (i < c) sum += group_owner_contrib(G, uint32_t(key), v[i]);
+            group_owner_verdict(T, G, uint32_t(key), sum);
+        }
+    } else if (c > 4 && c <= kGroupSmall) {
         uint32_t v[kGroupSmall], u[kGroupSmall];
 #pragma unroll
         for (uint32_t i = 0; i < kGroupSmall; i++) v[i] = i < c ? G.vals[off + i] : kNone32;
