@@ -355,11 +355,13 @@ Call<Event> make_call(tbg_ctx* ctx, const Event* d_events, uint32_t n, const uin
     return c;
 }
 
-int begin_call(tbg_ctx* ctx) {
+// zero_scalars: reset the per-call words of the scalars block (flags, slow_count, stats) here;
+// create_transfers resets them in its first kernel (tr_chunk_info) instead.
+int begin_call(tbg_ctx* ctx, bool zero_scalars = true) {
     ctx->n_marks = 0;
-    // Reset the per-call words of the scalars block: flags, slow_count, stats.
-    HIP_TRY(ctx, hipMemsetAsync(&ctx->d_scalars->flags, 0,
-                                sizeof(DevScalars) - offsetof(DevScalars, flags), ctx->stream));
+    if (zero_scalars)
+        HIP_TRY(ctx, hipMemsetAsync(&ctx->d_scalars->flags, 0,
+                                    sizeof(DevScalars) - offsetof(DevScalars, flags), ctx->stream));
     tmark(ctx, "begin");
     return 0;
 }
@@ -1160,7 +1162,7 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
     if (n == 0) return 0;
     hipStream_t saved = ctx->stream;
     if (stream) ctx->stream = static_cast<hipStream_t>(stream);
-    int rc = begin_call(ctx);
+    int rc = begin_call(ctx, false);
     Call<tb_transfer_t> c = make_call(ctx, d_events, n, d_batch_ends, d_batch_ts, n_batches,
                                       d_results, ctx->T.tr_rows_used);
     c.event_ts = d_event_ts;
@@ -1211,7 +1213,7 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
     if (!rc) {
         c.chunk_info = ctx->chunk_info;
         hipLaunchKernelGGL(tr_chunk_info, dim3(grid_for((n + 63) / 64)), block, 0, ctx->stream, c,
-                           ctx->chunk_info);
+                           ctx->chunk_info, ctx->d_scalars);
         hipLaunchKernelGGL(tr_ingest, dim3(ig), block, 0, ctx->stream, ctx->T, c);
         tmark(ctx, "tr_ingest");
         hipLaunchKernelGGL(tr_commit, grid, block, 0, ctx->stream, ctx->T, c);

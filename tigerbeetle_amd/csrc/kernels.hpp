@@ -708,8 +708,17 @@ constexpr uint32_t kChunkBatchMask = (1u << 30) - 1;
 constexpr uint32_t kChunkImported = 1u << 30;
 constexpr uint32_t kChunkPrevLinked = 1u << 31;
 
-__global__ void tr_chunk_info(Call<tb_transfer_t> c, uint4* out) {
+// (Also resets the call's words of the scalars block -- flags, counters -- for tr_ingest: the first
+// kernel of a create_transfers call, so the call needs no separate memset.)
+__global__ void tr_chunk_info(Call<tb_transfer_t> c, uint4* out, DevScalars* scalars) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) {
+        scalars->flags = 0;
+        scalars->slow_count = 0;
+        for (int j = 0; j < 4; j++) scalars->stats[j] = 0;
+        scalars->spec_fast = 0;
+        scalars->spec_ts_max = 0;
+    }
     const uint32_t base = i * 64;
     if (base >= c.n) return;
     const uint32_t b0 = batch_of_guess(c.batch_ends, c.n_batches, c.n, base);
