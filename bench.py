@@ -493,7 +493,7 @@ def per_commit(args, lib, dev, g, wl, prepare_ts, id_base):
         size = lib.tb_sm_commit(sm, 1, 0, op_counter[0], ts, operation, body, len(body), out)
         if size < 0:
             raise RuntimeError(f"tb_sm_commit: {size}")
-        return out.raw[:size]
+        return ctypes.string_at(out, size)
 
     if wl.name == "config2":
         accs = wl.acc

@@ -192,7 +192,8 @@ int tbg_debug_force_replay(tbg_ctx* ctx, int enable);
  * flow replay's exactness. */
 int tbg_debug_serial_replay(tbg_ctx* ctx, int enable);
 
-/* Per-kernel timing with HIP events on the call's stream (off by default; resets the totals).
+/* Per-kernel timing with HIP events on the call's stream (off by default; resets the totals);
+ * enable == 2 records only the host-wall phases of host-buffer calls (host:*), no HIP events.
  * tbg_profile_read returns 1 and fills name / accumulated milliseconds / launches for entry
  * `index`, or 0 past the last entry. */
 int tbg_profile(tbg_ctx* ctx, int enable);

@@ -58,6 +58,7 @@ struct AeScratch {
                             // [0] grouped touches, [1] listed accounts, [2] their chunks
     uint32_t* chunk_seg;    // per chunk of a listed account: the account's entry in G.big
     Bal5* chunk_tot;        // per chunk: the sums of its touches
+    unsigned long long* state;  // the log on device: [0] events, [1] last timestamp, [2] unsorted
 };
 
 __device__ inline void ae_side(const AeScratch& S, uint32_t i, uint32_t side, u128 pending,
@@ -97,10 +98,20 @@ __device__ inline uint64_t ae_transfer_row(const Tables& T, const tb_uint128_t& 
 }
 
 // Created events of a create_transfers call: list[i] = event index k (call order).
-__global__ void ae_created_flags(Call<tb_transfer_t> c, uint8_t* flags) {
-    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k < c.n) flags[k] = c.results[k].status == TB_STATUS_CREATED;
-}
+// The created events of a create_transfers call, in call order (one chained-scan launch).
+struct SelectCreated {
+    static constexpr bool kEmitAll = false;
+    const tb_create_result_t* results;
+    uint32_t* out;
+    unsigned int* count;
+    __device__ void load(uint64_t base, uint64_t n, uint32_t* c) const {
+#pragma unroll
+        for (uint32_t i = 0; i < kScanItems; i++)
+            c[i] = base + i < n && results[base + i].status == TB_STATUS_CREATED;
+    }
+    __device__ void emit(uint64_t i, uint32_t p) const { out[p] = uint32_t(i); }
+    __device__ void total(uint32_t t) const { *count = t; }
+};
 
 // (Both collectors run kPlanThreads lanes per workgroup and group the event's two touches by
 // account row; lanes past the events write "no key" for their touches.)
@@ -165,6 +176,8 @@ ae_collect_transfers(Tables T, Call<tb_transfer_t> c, const uint32_t* list,
     group_block_init(B);
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i == 0) S.G.counts[1] = S.G.counts[2] = 0;  // listed accounts / chunks (ae_group_small)
+    log += S.state[0];
+    refs += S.state[0];
     const bool active = i < *count;
     uint32_t dr_row = 0, cr_row = 0;
     if (active) ae_collect_transfer(T, c, list[i], i, S, log, refs, &dr_row, &cr_row);
@@ -197,19 +210,26 @@ ae_collect_expiry(Tables T, const uint64_t* rows, uint32_t m, uint64_t timestamp
     group_block_init(B);
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i == 0) S.G.counts[1] = S.G.counts[2] = 0;  // listed accounts / chunks (ae_group_small)
+    log += S.state[0];
+    refs += S.state[0];
     uint32_t dr_row = 0, cr_row = 0;
     if (i < m) ae_expiry_one(T, rows[i], m, i, timestamp, S, log, refs, &dr_row, &cr_row);
     ae_group_touches(S, B, i, i < m, dr_row, cr_row, m);
 }
 
-// The appended block's count and first / last timestamps (the log's order check).
+// Closes an appended block: the log's length and last timestamp advance on device (the host reads
+// them only when it needs them, ae_settle), and a block that starts at or before the previous
+// last timestamp marks the log unsorted (get_change_events sorts it first).
 __global__ void ae_tail(const tb_account_event_t* log, const unsigned int* d_count, uint32_t n,
-                        unsigned long long* out) {
+                        unsigned long long* state) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     const uint32_t m = d_count ? *d_count : n;
-    out[0] = m;
-    out[1] = m ? log[0].timestamp : 0;
-    out[2] = m ? log[m - 1].timestamp : 0;
+    if (m == 0) return;
+    const uint64_t used = state[0];
+    const uint64_t first = log[used].timestamp, last = log[used + m - 1].timestamp;
+    if (used && first <= state[1]) state[2] = 1;
+    state[1] = last > state[1] ? last : state[1];
+    state[0] = used + m;
 }
 
 // One touch's half of its AccountEvent: the account after the event = final row - the sums of
@@ -295,6 +315,7 @@ __global__ void __launch_bounds__(kBlock) ae_group_small(Tables T, AeScratch S, 
                                                          tb_account_event_t* log) {
     __shared__ uint32_t wave_buf[kBlock / 64][kGroupMid];
     const GroupPlan& G = S.G;
+    log += S.state[0];
     const uint64_t h = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     uint32_t c = 0, off = 0, row = 0;
     if (h < slots) {
@@ -427,6 +448,7 @@ __global__ void __launch_bounds__(kGroupBigThreads) ae_chunk_emit(Tables T, AeSc
     __shared__ Bal5Lds B;
     __shared__ Bal5 carry_lds;
     const GroupPlan& G = S.G;
+    log += S.state[0];
     const uint32_t nchunks = G.counts[2];
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     for (uint32_t g = blockIdx.x; g < nchunks; g += gridDim.x) {

@@ -86,6 +86,8 @@ struct tbg_ctx {
     Tables T{};
     DevScalars* d_scalars = nullptr;
     DevScalars* h_scalars = nullptr;  // pinned
+    tb_create_result_t* h_results = nullptr;  // pinned: host-buffer calls' results land here first
+    hipEvent_t results_ready = nullptr;
     uint32_t epoch = 0;
     bool force_replay = false;
     bool serial_replay = false;  // debug: every replay on one lane (replay_kernel)
@@ -141,11 +143,15 @@ struct tbg_ctx {
     // The account_events groove (events.hpp): AccountEvents in timestamp order + their references.
     tb_account_event_t* ae_log = nullptr;
     AeRef* ae_ref = nullptr;
-    uint64_t ae_cap = 0, ae_used = 0, ae_last_ts = 0;
-    bool ae_sorted = true;
+    // The log's length / last timestamp / order as of the last ae_settle; appends advance them on
+    // device (ae_words[4..6]) and ae_bound, an upper bound of the length, on the host.
+    uint64_t ae_cap = 0, ae_used = 0, ae_last_ts = 0, ae_bound = 0;
+    bool ae_sorted = true, ae_pending = false;
+    // Host-buffer create_transfers: its AccountEvents are launched after the results' download.
+    bool ae_defer = false, ae_deferred = false;
+    Call<tb_transfer_t> ae_call{};
     AeScratch ae{};
     uint64_t ae_touch_cap = 0;
-    uint8_t* ae_flags = nullptr;
     uint32_t* ae_list = nullptr;
     unsigned long long* ae_words = nullptr;  // bounds / counts
     unsigned long long* flow_debug = nullptr;
@@ -153,6 +159,7 @@ struct tbg_ctx {
 
     // Per-kernel timing (tbg_profile): HIP events recorded on the call's stream between launches.
     bool timing = false;
+    bool timing_host = false;  // host phases only (tbg_profile(ctx, 2): no HIP events)
     static constexpr int kMaxMarks = 32;
     hipEvent_t marks[kMaxMarks] = {};
     const char* mark_names[kMaxMarks] = {};
@@ -245,7 +252,7 @@ void tmark(tbg_ctx* ctx, const char* name) {
 
 // Host wall time of a phase of a host-buffer call (tbg_profile): accumulated like the marks.
 void hprof(tbg_ctx* ctx, const char* name, double ms) {
-    if (!ctx->timing) return;
+    if (!ctx->timing_host) return;
     size_t j = 0;
     while (j < ctx->prof_names.size() && ctx->prof_names[j] != name) j++;
     if (j == ctx->prof_names.size()) {
@@ -618,6 +625,7 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
     const uint32_t blocks = env_u("TBG_FLOW_BLOCKS", kFlowBlocks, 1,
                                   kFlowLanesMax / (waves * P.lanes_per_wave));
     P.xcd_stride = env_u("TBG_FLOW_XCD", 1, 1, 8);
+    P.backoff = env_u("TBG_FLOW_BACKOFF", 1, 0, 1);
     const uint32_t lanes = blocks * waves * P.lanes_per_wave;
     hipLaunchKernelGGL(flow_replay, dim3(blocks * P.xcd_stride), dim3(waves * 64), 0, ctx->stream,
                        ctx->T, c, P);
@@ -832,14 +840,41 @@ int ensure_ae_scratch(tbg_ctx* ctx, uint64_t touches) {
     return 0;
 }
 
+// The host's view of the log (ae_used / ae_last_ts / ae_sorted) after the appends in flight.
+int ae_settle(tbg_ctx* ctx) {
+    if (!ctx->ae_pending) return 0;
+    unsigned long long st[3] = {0, 0, 0};
+    HIP_TRY(ctx, hipMemcpyAsync(st, ctx->ae_words + 4, 24, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->ae_used = ctx->ae_bound = st[0];
+    ctx->ae_last_ts = st[1];
+    ctx->ae_sorted = st[2] == 0;
+    ctx->ae_pending = false;
+    return 0;
+}
+
+// Sets the device's view of the log from the host's (open / restore / after a sort).
+int ae_publish(tbg_ctx* ctx) {
+    const unsigned long long st[3] = {ctx->ae_used, ctx->ae_last_ts, ctx->ae_sorted ? 0ull : 1ull};
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->ae_words + 4, st, 24, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // (`st` is a stack value)
+    ctx->ae_bound = ctx->ae_used;
+    ctx->ae_pending = false;
+    return 0;
+}
+
 // Appends the AccountEvents of up to `n_upper` events (the exact count at d_count, or n_upper
 // itself when d_count is null): `collect` writes their event-level fields and groups both touches
 // of each by account (events.hpp); the account halves follow from the final rows and the later
-// touches' sums per account. One host synchronisation, for the count and the timestamp bounds.
+// touches' sums per account. No host synchronisation: the block's position in the log and the
+// log's length advance on device (ae_tail); the host synchronises only when the upper bound of
+// the length could pass the capacity.
 template <typename Collect>
 int ae_append(tbg_ctx* ctx, uint32_t n_upper, const unsigned int* d_count, Collect collect) {
     if (n_upper == 0) return 0;
-    if (ctx->ae_used + n_upper > ctx->ae_cap) {
+    if (ctx->ae_bound + n_upper > ctx->ae_cap) {
+        int rc = ae_settle(ctx);
+        if (rc) return rc;
         unsigned int m = n_upper;
         if (d_count) {
             HIP_TRY(ctx, hipMemcpyAsync(&m, d_count, 4, hipMemcpyDeviceToHost, ctx->stream));
@@ -853,9 +888,10 @@ int ae_append(tbg_ctx* ctx, uint32_t n_upper, const unsigned int* d_count, Colle
     int rc = ensure_ae_scratch(ctx, 2 * uint64_t(n_upper));
     if (rc) return rc;
     AeScratch& S = ctx->ae;
+    S.state = ctx->ae_words + 4;
     const uint64_t slots = S.G.hmask + 1;
-    tb_account_event_t* log = ctx->ae_log + ctx->ae_used;
-    collect(S, log, ctx->ae_ref + ctx->ae_used);
+    tb_account_event_t* log = ctx->ae_log;  // (+ the device length, read by each kernel)
+    collect(S, log, ctx->ae_ref);
     rc = launch_scan(ctx, slots, ExclusiveSumU32{S.G.hcnt, S.G.hoff, &S.G.counts[0]});
     if (rc) return rc;
     const uint64_t pairs = 2 * uint64_t(n_upper);
@@ -868,29 +904,18 @@ int ae_append(tbg_ctx* ctx, uint32_t n_upper, const unsigned int* d_count, Colle
                        ctx->stream, S);
     hipLaunchKernelGGL(ae_chunk_emit, dim3(kAeChunkBlocks), dim3(kGroupBigThreads), 0, ctx->stream,
                        ctx->T, S, log);
-    hipLaunchKernelGGL(ae_tail, dim3(1), dim3(64), 0, ctx->stream, log, d_count, n_upper,
-                       ctx->ae_words + 1);
+    hipLaunchKernelGGL(ae_tail, dim3(1), dim3(64), 0, ctx->stream, log, d_count, n_upper, S.state);
     tmark(ctx, "account_events");
     HIP_TRY(ctx, hipGetLastError());
-    // The log stays in timestamp order unless this block starts before the last one ended (an
-    // imported batch after a pulse's expiries); then get_change_events sorts it first.
-    unsigned long long tail[3] = {0, 0, 0};  // count, first timestamp, last timestamp
-    HIP_TRY(ctx, hipMemcpyAsync(tail, ctx->ae_words + 1, 24, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    const uint64_t m = tail[0];
-    if (m == 0) return 0;
-    if (ctx->ae_used && tail[1] <= ctx->ae_last_ts) ctx->ae_sorted = false;
-    ctx->ae_last_ts = std::max<uint64_t>(ctx->ae_last_ts, tail[2]);
-    ctx->ae_used += m;
+    ctx->ae_bound += n_upper;
+    ctx->ae_pending = true;
     return 0;
 }
 
 // AccountEvents of a create_transfers call: its created events in call order.
 int ae_transfers(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
-    hipLaunchKernelGGL(ae_created_flags, dim3(grid_for(c.n)), dim3(kBlock), 0, ctx->stream, c,
-                       ctx->ae_flags);
     unsigned int* d_count = reinterpret_cast<unsigned int*>(ctx->ae_words);
-    int rc = select_flagged(ctx, ctx->ae_flags, c.n, ctx->ae_list, d_count);
+    int rc = launch_scan(ctx, c.n, SelectCreated{c.results, ctx->ae_list, d_count});
     if (rc) return rc;
     const uint32_t* list = ctx->ae_list;
     return ae_append(ctx, c.n, d_count, [&](const AeScratch& S, tb_account_event_t* log,
@@ -913,16 +938,18 @@ int ae_expiry(tbg_ctx* ctx, const uint64_t* rows, uint64_t m, uint64_t timestamp
 
 // Restores timestamp order of the log (stable) when an append broke it.
 int ae_sort_log(tbg_ctx* ctx) {
-    if (ctx->ae_sorted || ctx->ae_used < 2) {
+    int rc = ae_settle(ctx);
+    if (rc) return rc;
+    if (ctx->ae_sorted) return 0;
+    if (ctx->ae_used < 2) {
         ctx->ae_sorted = true;
-        return 0;
+        return ae_publish(ctx);
     }
     const uint64_t n = ctx->ae_used;
     uint64_t *keys = nullptr, *keys2 = nullptr;
     uint32_t *idx = nullptr, *idx2 = nullptr;
     tb_account_event_t* log2 = nullptr;
     AeRef* ref2 = nullptr;
-    int rc = 0;
     if (!(dev_alloc(ctx, &keys, n, false) && dev_alloc(ctx, &keys2, n, false) &&
           dev_alloc(ctx, &idx, n, false) && dev_alloc(ctx, &idx2, n, false) &&
           dev_alloc(ctx, &log2, n, false) && dev_alloc(ctx, &ref2, n, false)))
@@ -951,8 +978,9 @@ int ae_sort_log(tbg_ctx* ctx) {
     }
     for (void* p : {(void*)keys, (void*)keys2, (void*)idx, (void*)idx2, (void*)log2, (void*)ref2})
         if (p) (void)hipFree(p);
-    if (!rc) ctx->ae_sorted = true;
-    return rc;
+    if (rc) return rc;
+    ctx->ae_sorted = true;
+    return ae_publish(ctx);
 }
 
 int upload_batches(tbg_ctx* ctx, uint32_t n, const uint32_t* batch_lens, const uint64_t* batch_ts,
@@ -1084,12 +1112,17 @@ tbg_ctx* tbg_open(const tbg_options* options) {
         ctx->ae_cap = options->account_events_capacity;
         ok = ok && dev_alloc(ctx, &ctx->ae_log, ctx->ae_cap, false) &&
              dev_alloc(ctx, &ctx->ae_ref, ctx->ae_cap, false) &&
-             dev_alloc(ctx, &ctx->ae_flags, std::max<uint64_t>(ev_max, options->pulse_batch_max), false) &&
              dev_alloc(ctx, &ctx->ae_list, std::max<uint64_t>(ev_max, options->pulse_batch_max), false) &&
-             dev_alloc(ctx, &ctx->ae_words, 4, true);
+             dev_alloc(ctx, &ctx->ae_words, 8, true);
     }
     ok = ok && hip_ok(ctx, hipHostMalloc(reinterpret_cast<void**>(&ctx->h_scalars),
                                          sizeof(DevScalars)), "hipHostMalloc");
+    ok = ok && hip_ok(ctx, hipEventCreateWithFlags(&ctx->results_ready, hipEventDisableTiming),
+                      "hipEventCreate");
+    ok = ok && hip_ok(ctx, hipHostMalloc(reinterpret_cast<void**>(&ctx->h_results),
+                                         size_t(std::max<uint64_t>(ev_max, 1)) *
+                                             sizeof(tb_create_result_t)),
+                      "hipHostMalloc");
     if (!ok) {
         fprintf(stderr, "tbg_open: %s\n", ctx->error.c_str());
         tbg_close(ctx);
@@ -1131,7 +1164,7 @@ void tbg_close(tbg_ctx* ctx) {
                     ctx->flow.dup_mark, ctx->flow.counts, ctx->flow.words, ctx->flow.lane_counts,
                     ctx->scan_status, ctx->scan_ticket,
                     ctx->flow.lane_undo, ctx->flow.engine, ctx->flow.acc_free,
-                    ctx->ae_log, ctx->ae_ref, ctx->ae_flags, ctx->ae_list, ctx->ae_words};
+                    ctx->ae_log, ctx->ae_ref, ctx->ae_list, ctx->ae_words};
     free_ae_scratch(ctx->ae);
     free_flow(ctx->flow);
     for (void* p : ptrs)
@@ -1139,6 +1172,8 @@ void tbg_close(tbg_ctx* ctx) {
     for (hipEvent_t e : ctx->marks)
         if (e) (void)hipEventDestroy(e);
     if (ctx->h_scalars) (void)hipHostFree(ctx->h_scalars);
+    if (ctx->h_results) (void)hipHostFree(ctx->h_results);
+    if (ctx->results_ready) (void)hipEventDestroy(ctx->results_ready);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -1290,14 +1325,37 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
     if (replay && !rc) rc = run_replay(ctx, c, true, false);
     if (!rc && (ctx->h_scalars->flags & kFlagPostVoid)) rc = pnt_resolve(ctx, c);
     if (!rc) rc = end_call(ctx, n, !replay);
-    if (!rc && ctx->ae_log) {
-        const double ta = ctx->timing ? now_ms() : 0;
+    if (!rc && ctx->ae_log && ctx->ae_defer) {
+        ctx->ae_call = c;  // launched by tbg_create_transfers once the results' copy is queued
+        ctx->ae_deferred = true;
+    } else if (!rc && ctx->ae_log) {
+        const double ta = ctx->timing_host ? now_ms() : 0;
         rc = ae_transfers(ctx, c);
-        if (ctx->timing) hprof(ctx, "host:account_events", now_ms() - ta);
+        hprof(ctx, "host:account_events", now_ms() - ta);
     }
     ctx->stream = saved;
     ctx->T.tr_rows_used += n;  // rows are consumed whether or not the events created objects
     ctx->tr_ts_stale = true;
+    return rc;
+}
+
+// Results of a host-buffer call: DMA into the pinned staging rows, then one host copy (a pageable
+// destination would take the driver's slower staged path). A create_transfers call's deferred
+// AccountEvents are launched behind the copy: the host waits for the results only, and the next
+// call's work queues behind the appends on the same stream.
+int download_results(tbg_ctx* ctx, tb_create_result_t* results, uint32_t n) {
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->h_results, ctx->d_results, size_t(n) * 16,
+                                hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipEventRecord(ctx->results_ready, ctx->stream));
+    int rc = 0;
+    if (ctx->ae_deferred) {
+        ctx->ae_deferred = false;
+        const double ta = ctx->timing_host ? now_ms() : 0;
+        rc = ae_transfers(ctx, ctx->ae_call);
+        hprof(ctx, "host:account_events", now_ms() - ta);
+    }
+    HIP_TRY(ctx, hipEventSynchronize(ctx->results_ready));
+    std::memcpy(results, ctx->h_results, size_t(n) * 16);
     return rc;
 }
 
@@ -1381,21 +1439,25 @@ int tbg_create_transfers(tbg_ctx* ctx, const tb_transfer_t* events, uint32_t n,
                          tb_create_result_t* results) {
     if (!ctx || n > ctx->opt.batch_events_max) return TBG_EINVAL;
     if (n == 0) return 0;
-    const double t0 = ctx->timing ? now_ms() : 0;
+    const double t0 = ctx->timing_host ? now_ms() : 0;
     int rc = upload_batches(ctx, n, batch_lens, batch_ts, nb);
     if (rc) return rc;
     HIP_TRY(ctx, hipMemcpyAsync(ctx->d_events, events, size_t(n) * 128, hipMemcpyHostToDevice,
                                 ctx->stream));
-    const double t1 = ctx->timing ? now_ms() : 0;
+    const double t1 = ctx->timing_host ? now_ms() : 0;
+    ctx->ae_defer = true;
     rc = tbg_create_transfers_device(ctx, reinterpret_cast<const tb_transfer_t*>(ctx->d_events), n,
                                      ctx->d_batch_ends, ctx->d_batch_ts, nb, ctx->d_results,
                                      nullptr);
+    ctx->ae_defer = false;
+    if (rc) {
+        ctx->ae_deferred = false;
+        return rc;
+    }
+    const double t2 = ctx->timing_host ? now_ms() : 0;
+    rc = download_results(ctx, results, n);
     if (rc) return rc;
-    const double t2 = ctx->timing ? now_ms() : 0;
-    HIP_TRY(ctx, hipMemcpyAsync(results, ctx->d_results, size_t(n) * 16, hipMemcpyDeviceToHost,
-                                ctx->stream));
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    if (ctx->timing) {
+    if (ctx->timing_host) {
         hprof(ctx, "host:upload", t1 - t0);
         hprof(ctx, "host:call", t2 - t1);
         hprof(ctx, "host:download", now_ms() - t2);
@@ -1415,9 +1477,8 @@ int tbg_create_accounts(tbg_ctx* ctx, const tb_account_t* events, uint32_t n,
     rc = tbg_create_accounts_device(ctx, reinterpret_cast<const tb_account_t*>(ctx->d_events), n,
                                     ctx->d_batch_ends, ctx->d_batch_ts, nb, ctx->d_results, nullptr);
     if (rc) return rc;
-    HIP_TRY(ctx, hipMemcpyAsync(results, ctx->d_results, size_t(n) * 16, hipMemcpyDeviceToHost,
-                                ctx->stream));
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    rc = download_results(ctx, results, n);
+    if (rc) return rc;
     return 0;
 }
 
@@ -1628,6 +1689,7 @@ int tbg_debug_set_account_balances(tbg_ctx* ctx, tb_uint128_t id, tb_uint128_t d
 
 int64_t tbg_dump_account_events(tbg_ctx* ctx, tb_account_event_t* out) {
     if (!ctx) return TBG_EINVAL;
+    if (int rc = ae_settle(ctx)) return rc;
     if (!out || ctx->ae_used == 0) return int64_t(ctx->ae_used);
     int rc = ae_sort_log(ctx);
     if (rc) return rc;
@@ -1647,6 +1709,7 @@ int64_t tbg_get_change_events(tbg_ctx* ctx, const tb_change_events_filter_t* fil
     const bool valid = (tmin == 0 || (tmin >= TB_TIMESTAMP_MIN && tmin <= TB_TIMESTAMP_MAX)) &&
                        (tmax == 0 || (tmax >= TB_TIMESTAMP_MIN && tmax <= TB_TIMESTAMP_MAX)) &&
                        (tmax == 0 || tmin <= tmax) && filter->limit != 0 && reserved_zero;
+    if (int rc = ae_settle(ctx)) return rc;
     if (!valid || ctx->ae_used == 0) return 0;
     int rc = ae_sort_log(ctx);
     if (rc) return rc;
@@ -1693,7 +1756,8 @@ int tbg_debug_serial_replay(tbg_ctx* ctx, int enable) {
 
 int tbg_profile(tbg_ctx* ctx, int enable) {
     if (!ctx) return TBG_EINVAL;
-    ctx->timing = enable != 0;
+    ctx->timing = enable == 1;
+    ctx->timing_host = enable != 0;
     ctx->prof_names.clear();
     ctx->prof_ms.clear();
     ctx->prof_count.clear();
@@ -1894,6 +1958,7 @@ int64_t tbg_compact(tbg_ctx* ctx) {
                 rc = TBG_EHIP;
         }
     }
+    if (!rc) rc = ae_settle(ctx);
     if (!rc && ctx->ae_used)
         hipLaunchKernelGGL(cmp_ae_refs, dim3(grid_for(ctx->ae_used)), dim3(kBlock), 0, ctx->stream,
                            ctx->ae_ref, ctx->ae_used, new_row);
@@ -2015,6 +2080,10 @@ tbg_ctx* tbg_open_checkpoint(const tbg_options* options, const char* path) {
     ctx->ae_used = h.ae_used;
     ctx->ae_last_ts = h.ae_last_ts;
     ctx->ae_sorted = h.ae_sorted != 0;
+    if (ctx->ae_log && ae_publish(ctx)) {
+        tbg_close(ctx);
+        return nullptr;
+    }
     ctx->acc_ts_stale = ctx->tr_ts_stale = true;
     return ctx;
 }

@@ -79,6 +79,7 @@ struct FlowPlan {
                                  // (kFlowDoneShards; one 128-byte line each)
     uint32_t lanes_per_wave;     // lanes of each engine wave that run units
     uint32_t xcd_stride;         // only workgroups blockIdx % xcd_stride == 0 run
+    uint32_t backoff;            // idle waves sleep longer the longer they find no unit
     unsigned long long* debug;   // optional: [0] loop iterations, [1] events, [2] cycles executing,
                                  // [3] cycles of the engine (lane 0)
 };
@@ -89,6 +90,7 @@ struct Step {
     uint64_t ts_event;
     uint32_t batch, flags;  // StepInfo
     uint32_t k, slot, dr, cr;  // the event and its EvRefs
+    uint32_t pslot, pad;       // EvRefs::pslot
 };
 
 __device__ inline uint64_t flow_key(uint32_t type, uint32_t index, uint32_t unit) {
@@ -231,7 +233,7 @@ __global__ void __launch_bounds__(kFlowThreads) flow_replay(Tables T, Call<tb_tr
             si.ts_event = st.ts_event;
             si.batch = st.batch;
             si.flags = st.flags;
-            replay_chain_step_at<tb_transfer_t>(R, c, st.k, ev, si, EvRefs{st.slot, st.dr, st.cr},
+            replay_chain_step_at<tb_transfer_t>(R, c, st.k, ev, si, EvRefs{st.slot, st.dr, st.cr, st.pslot},
                                                 true, chain_open, chain_start, chain_broken);
             if (R.overflow) {
                 atomicOr(&T.scalars->flags, kFlagUndoOverflow);
@@ -294,7 +296,7 @@ __global__ void __launch_bounds__(kFlowThreads) flow_replay(Tables T, Call<tb_tr
     };
     uint32_t u = kNone32;
     uint64_t spins = 0;
-    uint32_t last_seen = 0, polls = 0;
+    uint32_t last_seen = 0, polls = 0, idle = 0;
     bool alive = wave_lane < P.lanes_per_wave;
     uint32_t pos = alive ? atomicAdd(q_head, 1u) : 0;
     // The loop's exit is wave-uniform (a vote): inside it every lane only takes if/else paths, so
@@ -317,7 +319,8 @@ __global__ void __launch_bounds__(kFlowThreads) flow_replay(Tables T, Call<tb_tr
                     u = w - 1;
                     pos = atomicAdd(q_head, 1u);
                     spins = 0;
-                } else if ((++polls & 7) == 0) {  // the shards' sum, every 8th idle poll
+                    idle = 0;
+                } else if ((++idle, ++polls & 7) == 0) {  // the shards' sum, every 8th idle poll
                     uint32_t seen = 0;
                     for (uint32_t j = 0; j < kFlowDoneShards; j++)
                         seen += __hip_atomic_load(P.engine + 64 + 32 * j, __ATOMIC_RELAXED,
@@ -343,8 +346,17 @@ __global__ void __launch_bounds__(kFlowThreads) flow_replay(Tables T, Call<tb_tr
                 }
             }
         }
-        if (alive && u != kNone32) u = run_unit(u);
-        else if (alive) __builtin_amdgcn_s_sleep(1);
+        // A wave sleeps only when none of its lanes has a unit to run (s_sleep stalls the whole
+        // wave); the longer its lanes have been idle, the longer it sleeps, so that idle waves'
+        // polls do not crowd the memory system the running lanes' replays wait on.
+        const bool wave_runs = __any(alive && u != kNone32);
+        if (alive && u != kNone32) {
+            u = run_unit(u);
+        } else if (alive && !wave_runs) {
+            if (!P.backoff || idle < 16) __builtin_amdgcn_s_sleep(1);
+            else if (idle < 128) __builtin_amdgcn_s_sleep(4);
+            else __builtin_amdgcn_s_sleep(16);
+        }
     }
     if (lane_key_max)
         atomicMax(&T.scalars->transfers_key_max, (unsigned long long)lane_key_max);

@@ -165,6 +165,7 @@ __global__ void __launch_bounds__(kPlanThreads) plan_keys(Tables T, Call<tb_tran
             if (end - s > kFlowChainMax) P.barrier8[u] = 1;
         }
         auto keyless = [&](uint64_t row) { return acc_additive(T, row, P.add_epoch); };
+        uint32_t pslot = kPvNoHint, pdr = kNone32, pcr = kNone32;  // a post/void's pending
         if (!u128_is_zero(t.id) && !u128_is_max(t.id)) key[0] = flow_id_key(t.id);
         if (t.flags & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) {
             if (!u128_is_zero(t.pending_id) && !u128_is_max(t.pending_id)) {
@@ -189,11 +190,16 @@ __global__ void __launch_bounds__(kPlanThreads) plan_keys(Tables T, Call<tb_tran
                 }
                 if (!certain) {
                     P.barrier8[u] = 1;
-                } else if (p) {
-                    const uint64_t dr = account_find(T, p->debit_account_id);
-                    const uint64_t cr = account_find(T, p->credit_account_id);
-                    if (dr != kNone && !keyless(dr)) key[2] = (1ull << 32) | uint32_t(dr);
-                    if (cr != kNone && !keyless(cr)) key[3] = (1ull << 32) | uint32_t(cr);
+                } else {
+                    pslot = ps == kNone ? kNone32 : uint32_t(ps);
+                    if (p) {
+                        const uint64_t dr = account_find(T, p->debit_account_id);
+                        const uint64_t cr = account_find(T, p->credit_account_id);
+                        if (dr != kNone && !keyless(dr)) key[2] = (1ull << 32) | uint32_t(dr);
+                        if (cr != kNone && !keyless(cr)) key[3] = (1ull << 32) | uint32_t(cr);
+                        pdr = dr == kNone ? kNone32 : uint32_t(dr);
+                        pcr = cr == kNone ? kNone32 : uint32_t(cr);
+                    }
                 }
             }
         } else {
@@ -214,8 +220,11 @@ __global__ void __launch_bounds__(kPlanThreads) plan_keys(Tables T, Call<tb_tran
         st.flags = si.flags;
         st.k = k;
         st.slot = x.slot;
-        st.dr = x.dr;
-        st.cr = x.cr;
+        const bool pv = (t.flags & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) != 0;
+        st.dr = pv ? pdr : x.dr;  // (a post/void's own accounts are read only by the lanes
+        st.cr = pv ? pcr : x.cr;  // check, which a post/void never passes)
+        st.pslot = pslot;
+        st.pad = 0;
         P.steps[s] = st;
         P.indeg[s] = 0;  // (units < m)
         *reinterpret_cast<uint4*>(G.succ + kFlowKeys * uint64_t(s)) =

@@ -157,12 +157,18 @@ __device__ inline uint64_t slot_of(const C& c, uint32_t k) {
 }
 
 // An event's per-call records the replay reads: its id slot and account rows (kNone32 = none).
+// An event's id slot and account rows, found before the replay. For a post/void the flow plan
+// also resolves the pending transfer: `pslot` its id's slot (kNone32: not found) and dr / cr its
+// accounts' rows (kNone32: look them up); kPvNoHint: nothing resolved (the replay looks up all).
+constexpr uint32_t kPvNoHint = 0xFFFFFFFEu;
 struct EvRefs {
     uint32_t slot, dr, cr;
+    uint32_t pslot = kPvNoHint;
 };
 template <typename C>
 __device__ inline EvRefs ev_refs(const C& c, uint32_t k) {
-    return EvRefs{c.ev_slot[k], c.ev_dr ? c.ev_dr[k] : kNone32, c.ev_cr ? c.ev_cr[k] : kNone32};
+    return EvRefs{c.ev_slot[k], c.ev_dr ? c.ev_dr[k] : kNone32, c.ev_cr ? c.ev_cr[k] : kNone32,
+                  kPvNoHint};
 }
 // Batch facts of a replayed event (execute_multi_batch / execute_create): its timestamp, its batch,
 // whether it is the batch's last event (a linked flag there is linked_event_chain_open) and
@@ -515,7 +521,8 @@ __device__ inline void expiry_append(const Tables& T, uint64_t row, bool serial)
 
 template <typename C>
 __device__ uint32_t replay_post_or_void(Replay& R, const C& c, uint32_t k, uint64_t ts_event,
-                                        const tb_transfer_t& t, uint64_t* ts_out) {
+                                        const tb_transfer_t& t, const EvRefs& x,
+                                        uint64_t* ts_out) {
     const Tables& T = R.T;
     const uint16_t f = t.flags;
     if ((f & TB_TRANSFER_POST_PENDING) && (f & TB_TRANSFER_VOID_PENDING))
@@ -528,17 +535,30 @@ __device__ uint32_t replay_post_or_void(Replay& R, const C& c, uint32_t k, uint6
     if (u128_eq(t.pending_id, t.id)) return TB_CT_PENDING_ID_MUST_BE_DIFFERENT;
     if (t.timeout != 0) return TB_CT_TIMEOUT_RESERVED_FOR_PENDING_TRANSFER;
 
+    // With the plan's resolution the account rows load alongside the pending id's slot instead
+    // of after the pending row (the same rows: the pending transfer's accounts never change).
+    const bool hinted = x.pslot != kPvNoHint && x.dr != kNone32 && x.cr != kNone32;
+    tb_account_t dr, cr;
+    if (hinted) {
+        dr = T.acc_rows[x.dr];
+        cr = T.acc_rows[x.cr];
+    }
+    const uint64_t ps = x.pslot != kPvNoHint ? slot_or_none(x.pslot)
+                                             : transfer_slot_find(T, c, t.pending_id);
     uint64_t p_row = 0;
-    if (replay_get_transfer_at_slot(T, c, transfer_slot_find(T, c, t.pending_id), k, &p_row) != 1)
+    if (replay_get_transfer_at_slot(T, c, ps, k, &p_row) != 1)
         return TB_CT_PENDING_TRANSFER_NOT_FOUND;
     const tb_transfer_t p = T.tr_rows[p_row];
     if (!(p.flags & TB_TRANSFER_PENDING)) return TB_CT_PENDING_TRANSFER_NOT_PENDING;
 
-    uint64_t dr_row = account_find(T, p.debit_account_id);
-    uint64_t cr_row = account_find(T, p.credit_account_id);
-    if (dr_row == kNone || cr_row == kNone) return TB_CT_PENDING_TRANSFER_NOT_FOUND;  // unreachable
-    const tb_account_t dr = T.acc_rows[dr_row];
-    const tb_account_t cr = T.acc_rows[cr_row];
+    uint64_t dr_row = x.dr, cr_row = x.cr;
+    if (!hinted) {
+        dr_row = account_find(T, p.debit_account_id);
+        cr_row = account_find(T, p.credit_account_id);
+        if (dr_row == kNone || cr_row == kNone) return TB_CT_PENDING_TRANSFER_NOT_FOUND;  // unreachable
+        dr = T.acc_rows[dr_row];
+        cr = T.acc_rows[cr_row];
+    }
 
     if (!u128_is_zero(t.debit_account_id) && !u128_eq(t.debit_account_id, p.debit_account_id))
         return TB_CT_PENDING_TRANSFER_HAS_DIFFERENT_DEBIT_ACCOUNT_ID;
@@ -659,7 +679,7 @@ __device__ uint32_t replay_create_transfer(Replay& R, const C& c, uint32_t k, ui
     }
 
     if (f & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING))
-        return replay_post_or_void(R, c, k, ts_event, t, ts_out);
+        return replay_post_or_void(R, c, k, ts_event, t, x, ts_out);
 
     if (u128_is_zero(t.debit_account_id)) return TB_CT_DEBIT_ACCOUNT_ID_MUST_NOT_BE_ZERO;
     if (u128_is_max(t.debit_account_id)) return TB_CT_DEBIT_ACCOUNT_ID_MUST_NOT_BE_INT_MAX;

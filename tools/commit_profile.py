@@ -32,7 +32,7 @@ def kernel_ms(lib, g):
     return out
 
 
-def run_sm(lib, R, account_events):
+def run_sm(lib, R, account_events, mode=1):
     sm_opt = native.SmOptions()
     sm_opt.batch_size_limit = MBSM
     sm_opt.message_body_size_max = MBSM
@@ -83,7 +83,7 @@ def run_sm(lib, R, account_events):
         ev["id"][:, 0] += np.uint64(r * BATCH + 1)
         bodies.append(encode(ev))
     commit(147, bodies[0])  # warm
-    lib.tbg_profile(g, 1)
+    lib.tbg_profile(g, mode)
     t0 = time.perf_counter()
     for r in range(1, R):
         commit(147, bodies[r])
@@ -101,6 +101,9 @@ def main():
     lib = native.load()
     print(json.dumps({"state_machine_account_events": run_sm(lib, a.commits, True)}))
     print(json.dumps({"state_machine_no_account_events": run_sm(lib, a.commits, False)}))
+    # host phases only (no HIP events between launches): the undistorted split
+    print(json.dumps({"state_machine_account_events_host": run_sm(lib, a.commits, True, 2)}))
+    print(json.dumps({"state_machine_no_account_events_host": run_sm(lib, a.commits, False, 2)}))
 
 
 if __name__ == "__main__":

@@ -5,7 +5,7 @@ set -o pipefail
 tag=${1:-abflow}; out=gpurun_out/$tag; mkdir -p $out
 for i in 1 2; do
   for v in default knob; do
-    if [ $v = knob ]; then export $KNOB=1; else unset $KNOB; fi
+    if [ $v = knob ]; then export $KNOB=${KNOBVAL:-1}; else unset $KNOB; fi
     timeout -k 10 240 python -u tools/bench_configs.py --configs ${CONFIGS:-4} > $out/$v.$i.json 2> $out/$v.$i.err || { tail -5 $out/$v.$i.err; exit 1; }
     python3 -c "import json,sys
 for l in open(sys.argv[1]):
