@@ -90,7 +90,7 @@ struct Step {
     uint64_t ts_event;
     uint32_t batch, flags;  // StepInfo
     uint32_t k, slot, dr, cr;  // the event and its EvRefs
-    uint32_t pslot, pad;       // EvRefs::pslot
+    uint32_t pslot, add;       // EvRefs::pslot, EvRefs::add
 };
 
 __device__ inline uint64_t flow_key(uint32_t type, uint32_t index, uint32_t unit) {
@@ -233,7 +233,8 @@ __global__ void __launch_bounds__(kFlowThreads) flow_replay(Tables T, Call<tb_tr
             si.ts_event = st.ts_event;
             si.batch = st.batch;
             si.flags = st.flags;
-            replay_chain_step_at<tb_transfer_t>(R, c, st.k, ev, si, EvRefs{st.slot, st.dr, st.cr, st.pslot},
+            replay_chain_step_at<tb_transfer_t>(R, c, st.k, ev, si,
+                                                EvRefs{st.slot, st.dr, st.cr, st.pslot, st.add},
                                                 true, chain_open, chain_start, chain_broken);
             if (R.overflow) {
                 atomicOr(&T.scalars->flags, kFlagUndoOverflow);

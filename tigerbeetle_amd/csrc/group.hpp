@@ -166,6 +166,7 @@ __global__ void __launch_bounds__(kPlanThreads) plan_keys(Tables T, Call<tb_tran
         }
         auto keyless = [&](uint64_t row) { return acc_additive(T, row, P.add_epoch); };
         uint32_t pslot = kPvNoHint, pdr = kNone32, pcr = kNone32;  // a post/void's pending
+        uint32_t add = kAddKnown;  // the replay's additive verdicts (EvRefs::add)
         if (!u128_is_zero(t.id) && !u128_is_max(t.id)) key[0] = flow_id_key(t.id);
         if (t.flags & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) {
             if (!u128_is_zero(t.pending_id) && !u128_is_max(t.pending_id)) {
@@ -197,6 +198,8 @@ __global__ void __launch_bounds__(kPlanThreads) plan_keys(Tables T, Call<tb_tran
                         const uint64_t cr = account_find(T, p->credit_account_id);
                         if (dr != kNone && !keyless(dr)) key[2] = (1ull << 32) | uint32_t(dr);
                         if (cr != kNone && !keyless(cr)) key[3] = (1ull << 32) | uint32_t(cr);
+                        if (dr != kNone && keyless(dr)) add |= kAddDr;
+                        if (cr != kNone && keyless(cr)) add |= kAddCr;
                         pdr = dr == kNone ? kNone32 : uint32_t(dr);
                         pcr = cr == kNone ? kNone32 : uint32_t(cr);
                     }
@@ -206,6 +209,8 @@ __global__ void __launch_bounds__(kPlanThreads) plan_keys(Tables T, Call<tb_tran
             const uint32_t dr = c.ev_dr[k], cr = c.ev_cr[k];
             if (dr != kNone32 && !keyless(dr)) key[2] = (1ull << 32) | dr;
             if (cr != kNone32 && !keyless(cr)) key[3] = (1ull << 32) | cr;
+            if (dr != kNone32 && keyless(dr)) add |= kAddDr;
+            if (cr != kNone32 && keyless(cr)) add |= kAddCr;
         }
         // The expires_at entry a created pending transfer with a timeout appends (planned: one
         // slot per candidate position; a candidate that fails or whose chain is discarded leaves
@@ -224,7 +229,7 @@ __global__ void __launch_bounds__(kPlanThreads) plan_keys(Tables T, Call<tb_tran
         st.dr = pv ? pdr : x.dr;  // (a post/void's own accounts are read only by the lanes
         st.cr = pv ? pcr : x.cr;  // check, which a post/void never passes)
         st.pslot = pslot;
-        st.pad = 0;
+        st.add = add;
         P.steps[s] = st;
         P.indeg[s] = 0;  // (units < m)
         *reinterpret_cast<uint4*>(G.succ + kFlowKeys * uint64_t(s)) =

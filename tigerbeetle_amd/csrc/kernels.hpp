@@ -1035,7 +1035,7 @@ __device__ inline void commit_post_void(const Tables& T, const Call<tb_transfer_
     o.credit_account_id = p.credit_account_id;
     o.amount = W(amount);
     o.pending_id = t.pending_id;
-    o.user_data_128 = U(t.user_data_128) > 0 ? t.user_data_128 : p.user_data_128;
+    o.user_data_128 = W(U(t.user_data_128) > 0 ? U(t.user_data_128) : U(p.user_data_128));  // (scalar select: a struct select keeps both rows in scratch)
     o.user_data_64 = t.user_data_64 > 0 ? t.user_data_64 : p.user_data_64;
     o.user_data_32 = t.user_data_32 > 0 ? t.user_data_32 : p.user_data_32;
     o.timeout = 0;

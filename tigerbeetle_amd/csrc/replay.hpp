@@ -54,14 +54,28 @@ constexpr unsigned int kCommitFlags = kFlagImported | kFlagPostVoid | kFlagDupli
 
 enum : uint8_t { kClassDone = 0, kClassFast = 1, kClassSlow = 2 };
 
-struct UndoEntry {
+struct alignas(16) UndoEntry {
     uint64_t kind_index;  // kind in the top byte
-    tb_account_t row;     // kUndoAccount: the whole row before the update
+    uint64_t pad;         // (the row 16-B aligned: store_balances writes 16-B words)
+    tb_account_t row;     // kUndoAccount: the row's balances and flags before the update (the
+                          // only fields a create_transfers replay changes)
 };
 constexpr uint64_t kUndoAccount = 1ull << 56;
 constexpr uint64_t kUndoStatus = 2ull << 56;
 constexpr uint64_t kUndoDelta = 3ull << 56;   // balance deltas added atomically (row's 4 fields)
 constexpr uint64_t kUndoIndexMask = (1ull << 56) - 1;
+
+// The four balances (16-B stores) and the flags of `src` into the row at `dst`.
+__device__ inline void store_balances(tb_account_t* dst, const tb_account_t& src) {
+    auto q = [](const tb_uint128_t& v) {
+        return make_uint4(uint32_t(v.lo), uint32_t(v.lo >> 32), uint32_t(v.hi), uint32_t(v.hi >> 32));
+    };
+    *reinterpret_cast<uint4*>(&dst->debits_pending) = q(src.debits_pending);
+    *reinterpret_cast<uint4*>(&dst->debits_posted) = q(src.debits_posted);
+    *reinterpret_cast<uint4*>(&dst->credits_pending) = q(src.credits_pending);
+    *reinterpret_cast<uint4*>(&dst->credits_posted) = q(src.credits_posted);
+    dst->flags = src.flags;
+}
 
 // Everything a kernel needs, passed by value.
 struct Tables {
@@ -160,15 +174,19 @@ __device__ inline uint64_t slot_of(const C& c, uint32_t k) {
 // An event's id slot and account rows, found before the replay. For a post/void the flow plan
 // also resolves the pending transfer: `pslot` its id's slot (kNone32: not found) and dr / cr its
 // accounts' rows (kNone32: look them up); kPvNoHint: nothing resolved (the replay looks up all).
+// `add`: the flow plan's additive verdicts (Replay::additive) of dr (kAddDr) and cr (kAddCr),
+// valid with kAddKnown.
 constexpr uint32_t kPvNoHint = 0xFFFFFFFEu;
+constexpr uint32_t kAddDr = 1, kAddCr = 2, kAddKnown = 4;
 struct EvRefs {
     uint32_t slot, dr, cr;
     uint32_t pslot = kPvNoHint;
+    uint32_t add = 0;
 };
 template <typename C>
 __device__ inline EvRefs ev_refs(const C& c, uint32_t k) {
     return EvRefs{c.ev_slot[k], c.ev_dr ? c.ev_dr[k] : kNone32, c.ev_cr ? c.ev_cr[k] : kNone32,
-                  kPvNoHint};
+                  kPvNoHint, 0};
 }
 // Batch facts of a replayed event (execute_multi_batch / execute_create): its timestamp, its batch,
 // whether it is the batch's last event (a linked flag there is linked_event_chain_open) and
@@ -289,7 +307,7 @@ struct Replay {
                 uint64_t idx = u.kind_index & kUndoIndexMask;
                 const uint64_t kind = u.kind_index & ~kUndoIndexMask;
                 if (kind == kUndoAccount) {
-                    copy_row(&T.acc_rows[idx], &u.row);
+                    store_balances(&T.acc_rows[idx], u.row);
                 } else if (kind == kUndoDelta) {
                     tb_account_t& a = T.acc_rows[idx];
                     if (!u128_is_zero(u.row.debits_pending))
@@ -316,16 +334,6 @@ struct Replay {
         undo_len = scope.undo_len;
         scope.open = false;
     }
-    __device__ void log_account(uint64_t row) {
-        if (!scope.open) return;
-        if (undo_len >= undo_cap) {
-            overflow = true;
-            return;
-        }
-        undo[undo_len].kind_index = kUndoAccount | row;
-        copy_row(&undo[undo_len].row, &T.acc_rows[row]);
-        undo_len++;
-    }
     __device__ void log_status(uint64_t row) {
         if (!scope.open) return;
         if (undo_len >= undo_cap) {
@@ -336,9 +344,20 @@ struct Replay {
         undo[undo_len].row.timestamp = T.tr_status[row];
         undo_len++;
     }
-    __device__ void update_account(uint64_t row, const tb_account_t& next) {
-        log_account(row);
-        T.acc_rows[row] = next;
+    // (`old`: the row as this event read it, logged from registers). Only the balances and flags
+    // are written: nothing else of an account changes in a create_transfers call, and whole-row
+    // struct copies of register rows would go through scratch memory.
+    __device__ void update_account(uint64_t row, const tb_account_t& old, const tb_account_t& next) {
+        if (scope.open) {
+            if (undo_len >= undo_cap) {
+                overflow = true;
+            } else {
+                undo[undo_len].kind_index = kUndoAccount | row;
+                store_balances(&undo[undo_len].row, old);
+                undo_len++;
+            }
+        }
+        store_balances(&T.acc_rows[row], next);
         // A rollback restores the row but keeps the hazard bits: they only over-approximate.
         const uint16_t h = acc_hazard_of(next);
         if (h) acc_hazard_set(T.acc_index, T.acc_entry_of, row, h);
@@ -351,27 +370,59 @@ struct Replay {
     // so the flow plan gives them no account key (flow_keys) and the replay adds its deltas with
     // u128 atomics, logged as deltas for a chain's rollback.
     __device__ bool additive(uint64_t row) const { return acc_additive(T, row, add_epoch); }
-    // Adds the four (modular) deltas to the row's debits_pending, debits_posted, credits_pending,
-    // credits_posted.
-    __device__ void add_balances(uint64_t row, u128 d_dpe, u128 d_dpo, u128 d_cpe, u128 d_cpo) {
-        tb_account_t& a = T.acc_rows[row];
-        uint64_t hi = 0;
-        if (d_dpe) hi |= atomic_add_u128(&a.debits_pending, d_dpe);
-        if (d_dpo) hi |= atomic_add_u128(&a.debits_posted, d_dpo);
-        if (d_cpe) hi |= atomic_add_u128(&a.credits_pending, d_cpe);
-        if (d_cpo) hi |= atomic_add_u128(&a.credits_posted, d_cpo);
-        if (hi >= kHazardHiLimit) acc_hazard_set(T.acc_index, T.acc_entry_of, row, kHazardHigh);
+    __device__ bool additive(uint64_t row, const EvRefs& x, uint32_t bit) const {
+        return (x.add & kAddKnown) ? (x.add & bit) != 0 : additive(row);
+    }
+    // Adds the four (modular) deltas d[0..3] to debits_pending, debits_posted, credits_pending,
+    // credits_posted of row a (da) and of row b (db); kNone32 skips a row. Every low-word atomic
+    // goes out before any returns (one round trip to the point of coherence, not one per field),
+    // then the carries.
+    __device__ void add_balances2(uint32_t a, const u128 (&da)[4], uint32_t b, const u128 (&db)[4]) {
+        uint64_t old[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const uint32_t row = j < 4 ? a : b;
+            const u128 d = j < 4 ? da[j] : db[j - 4];
+            old[j] = 0;
+            if (row != kNone32 && uint64_t(d) != 0) {
+                tb_uint128_t* f = &T.acc_rows[row].debits_pending + (j & 3);
+                old[j] = atomicAdd((unsigned long long*)&f->lo, (unsigned long long)uint64_t(d));
+            }
+        }
+        uint64_t hi_a = 0, hi_b = 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const uint32_t row = j < 4 ? a : b;
+            const u128 d = j < 4 ? da[j] : db[j - 4];
+            if (row == kNone32) continue;
+            const uint64_t lo = uint64_t(d);
+            const uint64_t hi = uint64_t(d >> 64) + ((lo != 0 && old[j] + lo < old[j]) ? 1 : 0);
+            if (hi) {
+                tb_uint128_t* f = &T.acc_rows[row].debits_pending + (j & 3);
+                const uint64_t h = atomicAdd((unsigned long long*)&f->hi, (unsigned long long)hi) + hi;
+                if (j < 4) hi_a |= h;
+                else hi_b |= h;
+            }
+        }
+        if (a != kNone32 && hi_a >= kHazardHiLimit) acc_hazard_set(T.acc_index, T.acc_entry_of, a, kHazardHigh);
+        if (b != kNone32 && hi_b >= kHazardHiLimit) acc_hazard_set(T.acc_index, T.acc_entry_of, b, kHazardHigh);
         if (!scope.open) return;
-        if (undo_len >= undo_cap) {
+        if (undo_len + (a != kNone32) + (b != kNone32) > undo_cap) {
             overflow = true;
             return;
         }
-        UndoEntry& u = undo[undo_len++];
-        u.kind_index = kUndoDelta | row;
-        u.row.debits_pending = W(d_dpe);
-        u.row.debits_posted = W(d_dpo);
-        u.row.credits_pending = W(d_cpe);
-        u.row.credits_posted = W(d_cpo);
+#pragma unroll
+        for (int r = 0; r < 2; r++) {
+            const uint32_t row = r == 0 ? a : b;
+            if (row == kNone32) continue;
+            const u128* d = r == 0 ? da : db;
+            UndoEntry& u = undo[undo_len++];
+            u.kind_index = kUndoDelta | row;
+            u.row.debits_pending = W(d[0]);
+            u.row.debits_posted = W(d[1]);
+            u.row.credits_pending = W(d[2]);
+            u.row.credits_posted = W(d[3]);
+        }
     }
     __device__ void update_status(uint64_t row, uint8_t status) {
         log_status(row);
@@ -409,10 +460,16 @@ struct Replay {
 
 // groove.get for transfers as seen by in-call event k: 0 not found, 1 object (row), 2 orphaned.
 template <typename C>
+__device__ inline int replay_transfer_at_word(const C& c, uint64_t w, uint32_t k, uint64_t* row);
+template <typename C>
 __device__ inline int replay_get_transfer_at_slot(const Tables& T, const C& c, uint64_t s,
                                                   uint32_t k, uint64_t* row) {
     if (s == kNone) return 0;
-    uint64_t w = T.tr.slots[s];
+    return replay_transfer_at_word(c, T.tr.slots[s], k, row);
+}
+// The same from the slot's word (kEmpty: no slot).
+template <typename C>
+__device__ inline int replay_transfer_at_word(const C& c, uint64_t w, uint32_t k, uint64_t* row) {
     if (w == kEmpty || w == kTomb) return 0;
     uint64_t r = (w & kRefMask) - 1;
     if (r < c.row_base) {
@@ -608,7 +665,7 @@ __device__ uint32_t replay_post_or_void(Replay& R, const C& c, uint32_t k, uint6
     o.credit_account_id = p.credit_account_id;
     o.amount = W(amount);
     o.pending_id = t.pending_id;
-    o.user_data_128 = U(t.user_data_128) > 0 ? t.user_data_128 : p.user_data_128;
+    o.user_data_128 = W(U(t.user_data_128) > 0 ? U(t.user_data_128) : U(p.user_data_128));  // (scalar select: a struct select keeps both rows in scratch)
     o.user_data_64 = t.user_data_64 > 0 ? t.user_data_64 : p.user_data_64;
     o.user_data_32 = t.user_data_32 > 0 ? t.user_data_32 : p.user_data_32;
     o.timeout = 0;
@@ -635,16 +692,18 @@ __device__ uint32_t replay_post_or_void(Replay& R, const C& c, uint32_t k, uint6
         if (p.flags & TB_TRANSFER_CLOSING_CREDIT) cr_new.flags &= (uint16_t)~TB_ACCOUNT_CLOSED;
     }
     const u128 posted = (f & TB_TRANSFER_POST_PENDING) ? amount : u128(0);
-    if (R.additive(dr_row)) {  // (flags unchanged: a void of a closing transfer marks closable)
-        R.add_balances(dr_row, u128(0) - p_amount, posted, 0, 0);
-    } else if (amount > 0 || p_amount > 0 || dr_new.flags != dr.flags) {
-        R.update_account(dr_row, dr_new);
+    const EvRefs xa{x.slot, x.dr, x.cr, x.pslot, hinted ? x.add : 0u};
+    // (additive rows: flags unchanged -- a void of a closing transfer marks closable)
+    const bool add_dr = R.additive(dr_row, xa, kAddDr), add_cr = R.additive(cr_row, xa, kAddCr);
+    if (add_dr || add_cr) {
+        const u128 da[4] = {u128(0) - p_amount, posted, 0, 0};
+        const u128 db[4] = {0, 0, u128(0) - p_amount, posted};
+        R.add_balances2(add_dr ? uint32_t(dr_row) : kNone32, da, add_cr ? uint32_t(cr_row) : kNone32, db);
     }
-    if (R.additive(cr_row)) {
-        R.add_balances(cr_row, 0, 0, u128(0) - p_amount, posted);
-    } else if (amount > 0 || p_amount > 0 || cr_new.flags != cr.flags) {
-        R.update_account(cr_row, cr_new);
-    }
+    if (!add_dr && (amount > 0 || p_amount > 0 || dr_new.flags != dr.flags))
+        R.update_account(dr_row, dr, dr_new);
+    if (!add_cr && (amount > 0 || p_amount > 0 || cr_new.flags != cr.flags))
+        R.update_account(cr_row, cr, cr_new);
     *ts_out = ts_actual;
     return TB_STATUS_CREATED;
 }
@@ -655,12 +714,22 @@ __device__ uint32_t replay_create_transfer(Replay& R, const C& c, uint32_t k, ui
                                            uint64_t* ts_out) {
     const Tables& T = R.T;
     const uint16_t f = t.flags;
+    // Every load the outcome needs whose address is known goes out first (the id slot's word, then
+    // both account rows): the checks below overlap them instead of waiting on each in turn.
+    const uint64_t w_slot = x.slot != kNone32 ? T.tr.slots[x.slot] : kEmpty;
+    const bool rows_early = !(f & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) &&
+                            x.dr != kNone32 && x.cr != kNone32;
+    tb_account_t dr, cr;
+    if (rows_early) {
+        dr = T.acc_rows[x.dr];
+        cr = T.acc_rows[x.cr];
+    }
     if (f & TB_TRANSFER_PADDING_MASK) return TB_CT_RESERVED_FLAG;
     if (u128_is_zero(t.id)) return TB_CT_ID_MUST_NOT_BE_ZERO;
     if (u128_is_max(t.id)) return TB_CT_ID_MUST_NOT_BE_INT_MAX;
 
     uint64_t e_row = 0;
-    switch (replay_get_transfer_at_slot(T, c, slot_or_none(x.slot), k, &e_row)) {
+    switch (replay_transfer_at_word(c, w_slot, k, &e_row)) {
         case 1: {
             const tb_transfer_t e = T.tr_rows[e_row];
             if ((t.flags == e.flags) && U(t.pending_id) == U(e.pending_id) &&
@@ -699,8 +768,7 @@ __device__ uint32_t replay_create_transfer(Replay& R, const C& c, uint32_t k, ui
     if (dr_row == kNone32) return TB_CT_DEBIT_ACCOUNT_NOT_FOUND;
     const uint32_t cr_row = x.cr;
     if (cr_row == kNone32) return TB_CT_CREDIT_ACCOUNT_NOT_FOUND;
-    const tb_account_t dr = T.acc_rows[dr_row];
-    const tb_account_t cr = T.acc_rows[cr_row];
+    // (rows_early holds here: both rows are loaded)
     if (dr.ledger != cr.ledger) return TB_CT_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;
     if (t.ledger != dr.ledger) return TB_CT_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
 
@@ -771,16 +839,17 @@ __device__ uint32_t replay_create_transfer(Replay& R, const C& c, uint32_t k, ui
     if (f & TB_TRANSFER_CLOSING_DEBIT) dr_new.flags |= TB_ACCOUNT_CLOSED;
     if (f & TB_TRANSFER_CLOSING_CREDIT) cr_new.flags |= TB_ACCOUNT_CLOSED;
     const bool pend = (f & TB_TRANSFER_PENDING) != 0;
-    if (R.additive(dr_row)) {  // (not closing: a closing transfer marks closable)
-        R.add_balances(dr_row, pend ? amount : 0, pend ? 0 : amount, 0, 0);
-    } else if (amount > 0 || (dr_new.flags & TB_ACCOUNT_CLOSED)) {
-        R.update_account(dr_row, dr_new);
+    // (additive rows are never closing: a closing transfer marks closable)
+    const bool add_dr = R.additive(dr_row, x, kAddDr), add_cr = R.additive(cr_row, x, kAddCr);
+    if (add_dr || add_cr) {
+        const u128 da[4] = {pend ? amount : 0, pend ? 0 : amount, 0, 0};
+        const u128 db[4] = {0, 0, pend ? amount : 0, pend ? 0 : amount};
+        R.add_balances2(add_dr ? dr_row : kNone32, da, add_cr ? cr_row : kNone32, db);
     }
-    if (R.additive(cr_row)) {
-        R.add_balances(cr_row, 0, 0, pend ? amount : 0, pend ? 0 : amount);
-    } else if (amount > 0 || (cr_new.flags & TB_ACCOUNT_CLOSED)) {
-        R.update_account(cr_row, cr_new);
-    }
+    if (!add_dr && (amount > 0 || (dr_new.flags & TB_ACCOUNT_CLOSED)))
+        R.update_account(dr_row, dr, dr_new);
+    if (!add_cr && (amount > 0 || (cr_new.flags & TB_ACCOUNT_CLOSED)))
+        R.update_account(cr_row, cr, cr_new);
 
     if (t.timeout > 0) R.pulse_min(ts_actual + (uint64_t)t.timeout * TB_NS_PER_S);
     *ts_out = ts_actual;
