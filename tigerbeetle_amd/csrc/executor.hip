@@ -55,6 +55,7 @@ struct FlowScratch {
              *vals_sorted = nullptr, *succ = nullptr, *indeg = nullptr;
     uint64_t* keys_sorted = nullptr;
     Step* steps = nullptr;
+    tb_transfer_t* evs = nullptr;  // per position: its event (flow_replay loads it with the step)
     uint32_t* queue = nullptr;
     uint8_t* outcome = nullptr;  // account lanes' verdicts
     // the grouping (group.hpp)
@@ -401,7 +402,7 @@ int end_call(tbg_ctx* ctx, uint32_t n, bool already_synced = false) {
 
 void free_flow(FlowScratch& F) {
     void* ptrs[] = {F.head8, F.barrier8, F.heads, F.unit_of, F.barriers, F.vals, F.vals_sorted,
-                    F.succ, F.indeg, F.keys_sorted, F.steps, F.queue,
+                    F.succ, F.indeg, F.keys_sorted, F.steps, F.evs, F.queue,
                     F.outcome, F.recs, F.mailbox, F.owner_starts, F.mb_index, F.exp_flag,
                     F.hkeys, F.hcnt, F.hoff, F.loc, F.rank, F.big, F.chunk_seg, F.chunk_sum,
                     F.seg_done};
@@ -411,6 +412,7 @@ void free_flow(FlowScratch& F) {
     F.heads = F.unit_of = F.barriers = F.vals = F.vals_sorted = F.succ = F.indeg = nullptr;
     F.keys_sorted = nullptr;
     F.steps = nullptr;
+    F.evs = nullptr;
     F.queue = nullptr;
     F.recs = nullptr;
     F.exp_flag = nullptr;
@@ -446,7 +448,8 @@ int ensure_flow(tbg_ctx* ctx, uint64_t m) {
          dev_alloc(ctx, &F.barriers, cap, false) && dev_alloc(ctx, &F.indeg, cap, true) &&
          dev_alloc(ctx, &F.vals, kc, false) && dev_alloc(ctx, &F.vals_sorted, kc, false) &&
          dev_alloc(ctx, &F.succ, kc, false) && dev_alloc(ctx, &F.keys_sorted, kc, false) &&
-         dev_alloc(ctx, &F.steps, cap, false) && dev_alloc(ctx, &F.queue, cap, false) &&
+         dev_alloc(ctx, &F.steps, cap, false) && dev_alloc(ctx, &F.evs, cap, false) &&
+         dev_alloc(ctx, &F.queue, cap, false) &&
          dev_alloc(ctx, &F.outcome, cap, false) && dev_alloc(ctx, &F.recs, cap, false) &&
          dev_alloc(ctx, &F.mailbox, cap, false) && dev_alloc(ctx, &F.mb_index, cap, false) &&
          dev_alloc(ctx, &F.exp_flag, cap, false) && dev_alloc(ctx, &F.owner_starts, kc, false) &&
@@ -490,6 +493,7 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
     P.pnt_ops = post_void ? c.pnt_call : nullptr;
     P.lane_undo = F.lane_undo;
     P.steps = F.steps;
+    P.evs = F.evs;
     P.engine = F.engine;
     P.exp_flag = F.exp_flag;
     P.exp_base = &F.words[1];

@@ -70,6 +70,7 @@ struct FlowPlan {
     uint64_t* pnt_ops;           // post/void calls: Call::pnt_call (per event), else null
     UndoEntry* lane_undo;        // kFlowUndoPerLane per lane
     struct Step* steps;          // per position: what the engine prefetches before it waits
+    tb_transfer_t* evs;          // per position: its event (a copy, addressed by position)
     const unsigned int* skip;    // nonzero: the account lanes replayed the call (lanes.hpp)
     uint32_t* exp_flag;          // per position: may append to the expires_at index
     unsigned long long* exp_base;  // expiry_count at the plan's start (flow_heads)
@@ -226,9 +227,18 @@ __global__ void __launch_bounds__(kFlowThreads) flow_replay(Tables T, Call<tb_tr
         R.undo_len = 0;
         R.key_max = 0;
         const uint64_t t0 = P.debug ? wall_clock64() : 0;
+        // Step records and events are addressed by position and never written during the
+        // replay: a chain's next pair loads while the current event runs.
+        Step st = P.steps[begin];
+        tb_transfer_t ev = P.evs[begin];
         for (uint32_t s = begin; s < end; s++) {
-            const Step st = P.steps[s];
-            const tb_transfer_t ev = c.events[st.k];
+            const bool more = s + 1 < end;
+            Step st_next;
+            tb_transfer_t ev_next;
+            if (more) {
+                st_next = P.steps[s + 1];
+                ev_next = P.evs[s + 1];
+            }
             StepInfo si;
             si.ts_event = st.ts_event;
             si.batch = st.batch;
@@ -239,6 +249,10 @@ __global__ void __launch_bounds__(kFlowThreads) flow_replay(Tables T, Call<tb_tr
             if (R.overflow) {
                 atomicOr(&T.scalars->flags, kFlagUndoOverflow);
                 R.overflow = false;
+            }
+            if (more) {
+                st = st_next;
+                ev = ev_next;
             }
         }
         if (P.debug) {

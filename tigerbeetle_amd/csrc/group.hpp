@@ -231,6 +231,7 @@ __global__ void __launch_bounds__(kPlanThreads) plan_keys(Tables T, Call<tb_tran
         st.pslot = pslot;
         st.add = add;
         P.steps[s] = st;
+        copy_row(&P.evs[s], &c.events[k]);
         P.indeg[s] = 0;  // (units < m)
         *reinterpret_cast<uint4*>(G.succ + kFlowKeys * uint64_t(s)) =
             make_uint4(kNone32, kNone32, kNone32, kNone32);
