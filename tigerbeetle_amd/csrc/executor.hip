@@ -617,8 +617,11 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
         P.debug = ctx->flow_debug;
     }
     // Engine shape (flow.hpp): lanes per wave x waves per workgroup x workgroups; TBG_FLOW_XCD=8
-    // packs the running workgroups onto one XCD. Default (config 4 sweeps, profiles/r01_flow2):
-    // 8 lanes per wave, 4 waves x 256 workgroups (8192 lanes) over the whole chip.
+    // packs the running workgroups onto one XCD. Default (config 4 sweeps, profiles/r02_shapes):
+    // 1 lane per wave, 4 waves x 256 workgroups (1024 lanes) over the whole chip -- with the
+    // replay's per-event latency down to ~2.8 us, lanes sharing a wave (divergent branches take
+    // turns) cost more than the extra lanes gain: 8192 lanes (8 per wave) 5.9 ms per 1M events,
+    // 4096 (1 or 4 per wave) 5.3, 1024 (1 per wave) 4.8-5.2, 512 5.2-5.6.
     auto env_u = [](const char* name, uint32_t def, uint32_t lo, uint32_t hi) {
         const char* e = getenv(name);
         const uint32_t v = e ? uint32_t(atoi(e)) : def;

@@ -41,7 +41,7 @@ namespace tbg {
 
 constexpr uint32_t kFlowThreads = 512;      // threads of an engine workgroup
 constexpr uint32_t kFlowLanesMax = 8192;    // lanes running units, over all engine workgroups
-constexpr uint32_t kFlowLanesPerWave = 8;   // default engine shape (TBG_FLOW_LPW / _WAVES / _BLOCKS)
+constexpr uint32_t kFlowLanesPerWave = 1;   // default engine shape (TBG_FLOW_LPW / _WAVES / _BLOCKS)
 constexpr uint32_t kFlowWaves = 4;
 constexpr uint32_t kFlowBlocks = 256;
 constexpr uint32_t kFlowDoneShards = 16;    // units_done counter shards (one line each)
@@ -168,8 +168,10 @@ struct SelectHeads {
 // Measured on config 4: one lane per wave over the whole chip halved the replay's time against one
 // workgroup of 512 busy lanes (116 -> 56 ms per 300k events, every account keyed); packing onto one
 // XCD lost. With additive accounts unkeyed the replay has far more independent units, and more
-// lanes win: 8192 lanes (8 per wave, 256 workgroups) run 1M events in 7.0 ms, 4096 in 8.2 ms,
-// 512 in 19.9 ms.
+// lanes won while an event cost ~5 us (8192 lanes, 8 per wave: 7.0 ms per 1M events; 512: 19.9).
+// With an event at ~2.8 us (no scratch, one round trip for the row loads and one for the additive
+// atomics) the critical path dominates and sharing a wave costs more than lanes gain: 1024 lanes,
+// one per wave, is the default (executor.hip, profiles/r02_shapes).
 //
 // Hand-offs between lanes on different CUs follow the agent-scope model (MI355X_MICROARCH.md,
 // inter-workgroup visibility): a finishing unit runs one release fence (L2 write-back) before its
