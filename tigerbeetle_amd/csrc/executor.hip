@@ -273,6 +273,7 @@ double now_ms() {
 void tcollect(tbg_ctx* ctx) {
     if (!ctx->timing) return;
     for (int i = 1; i < ctx->n_marks; i++) {
+        if (ctx->mark_names[i][0] == '-') continue;  // a span start only
         float ms = 0;
         if (hipEventElapsedTime(&ms, ctx->marks[i - 1], ctx->marks[i]) != hipSuccess) continue;
         const std::string name = ctx->mark_names[i];
@@ -366,6 +367,10 @@ Call<Event> make_call(tbg_ctx* ctx, const Event* d_events, uint32_t n, const uin
 // zero_scalars: reset the per-call words of the scalars block (flags, slow_count, stats) here;
 // create_transfers resets them in its first kernel (tr_chunk_info) instead.
 int begin_call(tbg_ctx* ctx, bool zero_scalars = true) {
+    if (ctx->timing && ctx->n_marks > 1) {  // the previous call's AccountEvents (queued after it)
+        (void)hipStreamSynchronize(ctx->stream);
+        tcollect(ctx);
+    }
     ctx->n_marks = 0;
     if (zero_scalars)
         HIP_TRY(ctx, hipMemsetAsync(&ctx->d_scalars->flags, 0,
@@ -877,7 +882,8 @@ int ae_publish(tbg_ctx* ctx) {
 // log's length advance on device (ae_tail); the host synchronises only when the upper bound of
 // the length could pass the capacity.
 template <typename Collect>
-int ae_append(tbg_ctx* ctx, uint32_t n_upper, const unsigned int* d_count, Collect collect) {
+int ae_append(tbg_ctx* ctx, uint32_t n_upper, const unsigned int* d_count, Collect collect,
+              const char* mark = "account_events") {
     if (n_upper == 0) return 0;
     if (ctx->ae_bound + n_upper > ctx->ae_cap) {
         int rc = ae_settle(ctx);
@@ -898,6 +904,7 @@ int ae_append(tbg_ctx* ctx, uint32_t n_upper, const unsigned int* d_count, Colle
     S.state = ctx->ae_words + 4;
     const uint64_t slots = S.G.hmask + 1;
     tb_account_event_t* log = ctx->ae_log;  // (+ the device length, read by each kernel)
+    tmark(ctx, "-account_events");
     collect(S, log, ctx->ae_ref);
     rc = launch_scan(ctx, slots, ExclusiveSumU32{S.G.hcnt, S.G.hoff, &S.G.counts[0]});
     if (rc) return rc;
@@ -912,7 +919,7 @@ int ae_append(tbg_ctx* ctx, uint32_t n_upper, const unsigned int* d_count, Colle
     hipLaunchKernelGGL(ae_chunk_emit, dim3(kAeChunkBlocks), dim3(kGroupBigThreads), 0, ctx->stream,
                        ctx->T, S, log);
     hipLaunchKernelGGL(ae_tail, dim3(1), dim3(64), 0, ctx->stream, log, d_count, n_upper, S.state);
-    tmark(ctx, "account_events");
+    tmark(ctx, mark);
     HIP_TRY(ctx, hipGetLastError());
     ctx->ae_bound += n_upper;
     ctx->ae_pending = true;
@@ -940,7 +947,7 @@ int ae_expiry(tbg_ctx* ctx, const uint64_t* rows, uint64_t m, uint64_t timestamp
         hipLaunchKernelGGL(ae_collect_expiry, dim3((uint32_t(m) + kPlanThreads - 1) / kPlanThreads),
                            dim3(kPlanThreads), 0, ctx->stream, ctx->T, rows, uint32_t(m), timestamp,
                            S, log, refs);
-    });
+    }, "pulse:account_events");
 }
 
 // Restores timestamp order of the log (stable) when an append broke it.
@@ -1773,7 +1780,12 @@ int tbg_profile(tbg_ctx* ctx, int enable) {
 
 int tbg_profile_read(tbg_ctx* ctx, uint32_t index, char* name, uint32_t name_len,
                      double* total_ms, uint64_t* launches) {
-    if (!ctx || index >= ctx->prof_names.size()) return 0;
+    if (!ctx) return 0;
+    if (index == 0 && ctx->timing && ctx->n_marks > 1) {  // marks still pending (AccountEvents)
+        (void)hipStreamSynchronize(ctx->stream);
+        tcollect(ctx);
+    }
+    if (index >= ctx->prof_names.size()) return 0;
     if (name && name_len) snprintf(name, name_len, "%s", ctx->prof_names[index].c_str());
     if (total_ms) *total_ms = ctx->prof_ms[index];
     if (launches) *launches = ctx->prof_count[index];

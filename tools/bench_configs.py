@@ -51,11 +51,10 @@ def line(name, p, n, t_wall, extra):
     kms = kernel_ms(p)
     extra = dict(extra, kernels_ms=kms)
     s = p.seconds
-    # Device time: the HIP-event spans of the calls' kernels plus the AccountEvents span (its
-    # kernels and one host sync); the other host:* entries (PCIe copies, the host-side parts of the
-    # calls) are left out.
-    dev_ms = sum(v for k, v in kms.items()
-                 if not k.startswith("host:") or k == "host:account_events")
+    # Device time: the HIP-event spans of the calls' kernels, the AccountEvents appends included
+    # (`account_events`: queued behind each call's results); the host:* entries (PCIe copies, the
+    # host-side parts of the calls) and the pulses between calls (pulse:*) are left out.
+    dev_ms = sum(v for k, v in kms.items() if not k.startswith(("host:", "pulse:")))
     return {"config": name, "transfers": n, "validated": True,
             "gpu_transfers_per_s": round(n / s["gpu"], 1),
             "device_ms": round(dev_ms, 3),
