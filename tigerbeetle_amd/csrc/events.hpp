@@ -41,14 +41,15 @@ struct Bal5 {
     u128 dp, dpo, cp, cpo;
     uint32_t flips;
 };
+// (value selects, not a branch between fields: the compiler would pick a field pointer and keep
+// the sums in scratch)
 __device__ inline void bal5_add(Bal5& a, const AeDelta& d) {
-    if (d.side == 0) {
-        a.dp += d.pending;
-        a.dpo += d.posted;
-    } else {
-        a.cp += d.pending;
-        a.cpo += d.posted;
-    }
+    const bool dr = d.side == 0;
+    const u128 pending = d.pending, posted = d.posted;
+    a.dp += dr ? pending : u128(0);
+    a.dpo += dr ? posted : u128(0);
+    a.cp += dr ? u128(0) : pending;
+    a.cpo += dr ? u128(0) : posted;
     a.flips += d.flip;
 }
 
@@ -237,29 +238,27 @@ __global__ void ae_tail(const tb_account_event_t* log, const unsigned int* d_cou
 __device__ inline void ae_emit_touch(const tb_account_t& a, uint32_t v, const Bal5& later,
                                      tb_account_event_t* log) {
     const uint32_t i = v >> 1, side = v & 1;
-    tb_account_event_t* e = &log[i];
-    const tb_uint128_t dp = W(U(a.debits_pending) - later.dp);
-    const tb_uint128_t dpo = W(U(a.debits_posted) - later.dpo);
-    const tb_uint128_t cp = W(U(a.credits_pending) - later.cp);
-    const tb_uint128_t cpo = W(U(a.credits_posted) - later.cpo);
-    const uint16_t flags = uint16_t(a.flags ^ ((later.flips & 1) ? TB_ACCOUNT_CLOSED : 0));
-    if (side == 0) {
-        e->dr_account_id = a.id;
-        e->dr_debits_pending = dp;
-        e->dr_debits_posted = dpo;
-        e->dr_credits_pending = cp;
-        e->dr_credits_posted = cpo;
-        e->dr_account_timestamp = a.timestamp;
-        e->dr_account_flags = flags;
-    } else {
-        e->cr_account_id = a.id;
-        e->cr_debits_pending = dp;
-        e->cr_debits_posted = dpo;
-        e->cr_credits_pending = cp;
-        e->cr_credits_posted = cpo;
-        e->cr_account_timestamp = a.timestamp;
-        e->cr_account_flags = flags;
-    }
+    // The dr and cr halves share one layout (id and four balances: five 16-byte words, then the
+    // account timestamp and flags): one side's pointers, 16-byte stores (no struct copies, which
+    // the compiler stages through scratch).
+    uint8_t* e = reinterpret_cast<uint8_t*>(&log[i]);
+    uint4* w = reinterpret_cast<uint4*>(
+        e + (side ? offsetof(tb_account_event_t, cr_account_id) : offsetof(tb_account_event_t, dr_account_id)));
+    auto q = [](u128 x) {
+        return make_uint4(uint32_t(uint64_t(x)), uint32_t(uint64_t(x) >> 32), uint32_t(uint64_t(x >> 64)),
+                          uint32_t(uint64_t(x >> 64) >> 32));
+    };
+    w[0] = q(U(a.id));
+    w[1] = q(U(a.debits_pending) - later.dp);
+    w[2] = q(U(a.debits_posted) - later.dpo);
+    w[3] = q(U(a.credits_pending) - later.cp);
+    w[4] = q(U(a.credits_posted) - later.cpo);
+    *reinterpret_cast<uint64_t*>(e + (side ? offsetof(tb_account_event_t, cr_account_timestamp)
+                                           : offsetof(tb_account_event_t, dr_account_timestamp))) =
+        a.timestamp;
+    *reinterpret_cast<uint16_t*>(e + (side ? offsetof(tb_account_event_t, cr_account_flags)
+                                           : offsetof(tb_account_event_t, dr_account_flags))) =
+        uint16_t(a.flags ^ ((later.flips & 1) ? TB_ACCOUNT_CLOSED : 0));
 }
 
 // Listed accounts are processed in chunks of kAeChunk touches (kAeRun per lane of a workgroup).
