@@ -135,8 +135,15 @@ __device__ inline void ae_collect_transfer(Tables T, const Call<tb_transfer_t>& 
     const uint64_t row = c.row_base + k;
     const tb_transfer_t& t = T.tr_rows[row];  // the created transfer (amount actual, accounts)
     const uint16_t f = t.flags;
-    const uint64_t dr = account_find(T, t.debit_account_id);
-    const uint64_t cr = account_find(T, t.credit_account_id);
+    // A created transfer that is not a post/void has the event's own accounts, whose rows the
+    // ingest found (c.ev_dr / ev_cr, unless it packed them into balance items: kInfoLean); a
+    // post/void's are the pending transfer's.
+    const bool pv = (f & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) != 0;
+    const bool refs_ok = !pv && c.ev_dr && c.ev_cr && !(c.ev_info[k] & kInfoLean);
+    const uint32_t edr = refs_ok ? c.ev_dr[k] : kNone32;
+    const uint32_t ecr = refs_ok ? c.ev_cr[k] : kNone32;
+    const uint64_t dr = edr != kNone32 ? uint64_t(edr) : account_find(T, t.debit_account_id);
+    const uint64_t cr = ecr != kNone32 ? uint64_t(ecr) : account_find(T, t.credit_account_id);
     const u128 amount = U(t.amount);
     uint8_t status = TB_PENDING_NONE;
     const tb_transfer_t* p = nullptr;
