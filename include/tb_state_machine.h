@@ -5,12 +5,15 @@
  * `ReplicaType(StateMachine, ...)` (src/vsr/replica.zig:144-152) for the operations of this path:
  * pulse, create_accounts, create_transfers, lookup_accounts, lookup_transfers,
  * get_change_events (the account_events groove's reader, CDC) and the scans over the same tables:
- * get_account_transfers, get_account_balances, query_accounts, query_transfers. Bodies are
- * multi-batch encoded exactly as src/vsr/multi_batch.zig; replies are multi-batch encoded the
- * same way. The executor underneath is pluggable (tb_executor): the product binds the HIP
+ * get_account_transfers, get_account_balances, query_accounts, query_transfers -- and their
+ * deprecated encodings (the unbatched bodies and the sparse create results older clients send,
+ * execute :2671-2700, execute_create :3116-3194). Bodies are multi-batch encoded exactly as
+ * src/vsr/multi_batch.zig; replies are multi-batch encoded the same way. The executor underneath is pluggable (tb_executor): the product binds the HIP
  * executor (tbg.h) with tb_sm_open_gpu; tests may bind another executor with the same semantics.
  *
  *   tb_sm_input_valid     <- StateMachine.input_valid   :980-1032 (+ batch_valid :1036-1067)
+ *   tb_sm_event_max / tb_sm_result_max <- Operation.event_max / result_max
+ *                            (src/tigerbeetle.zig:853-931) under the bound message_body_size_max
  *   tb_sm_prepare         <- StateMachine.prepare       :1070-1101
  *   tb_sm_pulse_needed    <- StateMachine.pulse_needed  :1138-1144
  *   tb_sm_prefetch        <- StateMachine.prefetch      :1146-1226 (completes immediately:
@@ -33,10 +36,21 @@
 extern "C" {
 #endif
 
-/* Operation numbers (src/tigerbeetle.zig:685-716, vsr_operations_reserved = 128). */
+/* Operation numbers (src/tigerbeetle.zig:685-716, vsr_operations_reserved = 128): every operation
+ * of the reference's StateMachine, the deprecated encodings included (older clients). */
 enum {
     TB_OPERATION_PULSE = 128,
+    TB_OPERATION_DEPRECATED_CREATE_ACCOUNTS_UNBATCHED = 129,
+    TB_OPERATION_DEPRECATED_CREATE_TRANSFERS_UNBATCHED = 130,
+    TB_OPERATION_DEPRECATED_LOOKUP_ACCOUNTS_UNBATCHED = 131,
+    TB_OPERATION_DEPRECATED_LOOKUP_TRANSFERS_UNBATCHED = 132,
+    TB_OPERATION_DEPRECATED_GET_ACCOUNT_TRANSFERS_UNBATCHED = 133,
+    TB_OPERATION_DEPRECATED_GET_ACCOUNT_BALANCES_UNBATCHED = 134,
+    TB_OPERATION_DEPRECATED_QUERY_ACCOUNTS_UNBATCHED = 135,
+    TB_OPERATION_DEPRECATED_QUERY_TRANSFERS_UNBATCHED = 136,
     TB_OPERATION_GET_CHANGE_EVENTS = 137,
+    TB_OPERATION_DEPRECATED_CREATE_ACCOUNTS_SPARSE = 138,
+    TB_OPERATION_DEPRECATED_CREATE_TRANSFERS_SPARSE = 139,
     TB_OPERATION_LOOKUP_ACCOUNTS = 140,
     TB_OPERATION_LOOKUP_TRANSFERS = 141,
     TB_OPERATION_GET_ACCOUNT_TRANSFERS = 142,
@@ -95,6 +109,11 @@ void tb_sm_close(tb_sm* sm);
 tbg_ctx* tb_sm_executor_gpu(tb_sm* sm);
 
 int tb_sm_input_valid(const tb_sm* sm, uint8_t operation, const void* body, uint32_t size);
+/* Operation.event_max / result_max (tigerbeetle.zig:853-931) for this state machine's
+ * message_body_size_max; 0 for pulse, an unknown operation or a batch_size_limit outside
+ * (0, message_body_size_max]. */
+uint32_t tb_sm_event_max(const tb_sm* sm, uint8_t operation, uint32_t batch_size_limit);
+uint32_t tb_sm_result_max(const tb_sm* sm, uint8_t operation, uint32_t batch_size_limit);
 void tb_sm_prepare(tb_sm* sm, uint8_t operation, const void* body, uint32_t size);
 int tb_sm_pulse_needed(const tb_sm* sm, uint64_t timestamp);
 

@@ -184,6 +184,13 @@ typedef struct tbg_stats {
 } tbg_stats;
 int tbg_last_stats(tbg_ctx* ctx, tbg_stats* out);
 
+/* The executor's overflow predicate, sum_overflows (state_machine.zig:5144-5149), on `n` operand
+ * pairs of `bits` = 64 (low words only) or 128: out[i] = 1 iff a[i] + b[i] overflows. ctx NULL
+ * evaluates it on the host; otherwise a kernel on the ctx's device (the code the replay runs).
+ * Pins the predicate to the reference's "sum_overflows" test (:5151-5166). */
+int tbg_sum_overflows(tbg_ctx* ctx, uint32_t bits, const tb_uint128_t* a, const tb_uint128_t* b,
+                      uint32_t n, uint8_t* out);
+
 /* Forces every event through the ordered replay (self-check of the fast path). */
 int tbg_debug_force_replay(tbg_ctx* ctx, int enable);
 

@@ -39,10 +39,35 @@ TEST_BATCH_SIZE_LIMIT = 30 * 128
 TEST_PULSE_BATCH_MAX = TEST_MESSAGE_BODY_SIZE_MAX // 128
 
 SKIPPED_OPS = set()
-SCAN_OPS = {"get_account_transfers": (Operation.get_account_transfers, 128, 128),
-            "get_account_balances": (Operation.get_account_balances, 128, 128),
-            "query_accounts": (Operation.query_accounts, 64, 128),
-            "query_transfers": (Operation.query_transfers, 64, 128)}
+
+# TestContext.Operation.versions (state_machine_tests.zig:59-95): every table runs once per client
+# encoding -- the dense multi-batch operations, the sparse create results (multi-batch), and the
+# deprecated unbatched bodies. Per table operation: (operation number, event size, result size,
+# multi-batch encoded).
+VERSIONS = {
+    "dense": {
+        "create_accounts": (146, 128, 16, True), "create_transfers": (147, 128, 16, True),
+        "lookup_accounts": (140, 16, 128, True), "lookup_transfers": (141, 16, 128, True),
+        "get_account_transfers": (142, 128, 128, True),
+        "get_account_balances": (143, 128, 128, True),
+        "query_accounts": (144, 64, 128, True), "query_transfers": (145, 64, 128, True),
+    },
+    "sparse": {
+        "create_accounts": (138, 128, 8, True), "create_transfers": (139, 128, 8, True),
+        "lookup_accounts": (140, 16, 128, True), "lookup_transfers": (141, 16, 128, True),
+        "get_account_transfers": (142, 128, 128, True),
+        "get_account_balances": (143, 128, 128, True),
+        "query_accounts": (144, 64, 128, True), "query_transfers": (145, 64, 128, True),
+    },
+    "unbatched": {
+        "create_accounts": (129, 128, 8, False), "create_transfers": (130, 128, 8, False),
+        "lookup_accounts": (131, 16, 128, False), "lookup_transfers": (132, 16, 128, False),
+        "get_account_transfers": (133, 128, 128, False),
+        "get_account_balances": (134, 128, 128, False),
+        "query_accounts": (135, 64, 128, False), "query_transfers": (136, 64, 128, False),
+    },
+}
+SCAN_OPS = ("get_account_transfers", "get_account_balances", "query_accounts", "query_transfers")
 
 
 # ---- row DSL (src/testing/table.zig) --------------------------------------------------------
@@ -392,8 +417,9 @@ class TableContext:
         return reply
 
     # TestContext.submit (:178-228)
-    def submit(self, operation: int, payload: bytes, element_size: int, result_size: int) -> bytes:
-        body = encode_multi_batch(self.lib, payload, element_size)
+    def submit(self, operation: int, payload: bytes, element_size: int, result_size: int,
+               multi_batch: bool = True) -> bytes:
+        body = encode_multi_batch(self.lib, payload, element_size) if multi_batch else payload
         assert self.lib.tb_sm_input_valid(self.sm, operation, body, len(body)) == 1
         self.prepare(operation, body)
         pulse_needed = self.lib.tb_sm_pulse_needed(self.sm,
@@ -401,6 +427,8 @@ class TableContext:
         reply = self.execute(operation, body)
         if pulse_needed:
             self.pulse()
+        if not multi_batch:
+            return reply
         return decode_multi_batch_single(self.lib, reply, result_size)
 
 
@@ -408,8 +436,10 @@ class TableMismatch(AssertionError):
     pass
 
 
-def run_table(handle: StateMachineHandle, rows, label=""):
-    """check_version (state_machine_tests.zig:620-1079) for the dense create_* encoding."""
+def run_table(handle: StateMachineHandle, rows, label="", version="dense"):
+    """check_version (state_machine_tests.zig:620-1086) for one client encoding (VERSIONS)."""
+    ops = VERSIONS[version]
+    dense = version == "dense"
     ctx = TableContext(handle)
     lib, sm = ctx.lib, ctx.sm
     accounts = {}
@@ -454,7 +484,10 @@ def run_table(handle: StateMachineHandle, rows, label=""):
                     else linked_events_failed[row["id"]]
             else:
                 ts = timestamp_commit
-            reply.append(struct.pack("<QII", ts, int(status), 0))
+            if dense:
+                reply.append(struct.pack("<QII", ts, int(status), 0))
+            elif status != CreateAccountStatus.created:  # CreateAccountErrorResult (:738-746)
+                reply.append(struct.pack("<II", len(request) - 1, int(status)))
             if row["LNK"]:
                 if status == CreateAccountStatus.linked_event_failed:
                     assert row["id"] not in linked_events_failed
@@ -489,7 +522,10 @@ def run_table(handle: StateMachineHandle, rows, label=""):
                     else linked_events_failed[row["id"]]
             else:
                 ts = timestamp_commit
-            reply.append(struct.pack("<QII", ts, int(status), 0))
+            if dense:
+                reply.append(struct.pack("<QII", ts, int(status), 0))
+            elif status != CreateTransferStatus.created:  # CreateTransferErrorResult (:812-820)
+                reply.append(struct.pack("<II", len(request) - 1, int(status)))
             if row["LNK"]:
                 if status == CreateTransferStatus.linked_event_failed:
                     assert row["id"] not in linked_events_failed
@@ -613,23 +649,16 @@ def run_table(handle: StateMachineHandle, rows, label=""):
             assert operation in (None, op_name), (operation, op_name)
             commits += 1
             payload = b"".join(request)
-            if op_name == "create_accounts":
-                actual = ctx.submit(Operation.create_accounts, payload, 128, 16)
-            elif op_name == "create_transfers":
-                actual = ctx.submit(Operation.create_transfers, payload, 128, 16)
-            elif op_name == "lookup_accounts":
-                actual = ctx.submit(Operation.lookup_accounts, payload, 16, 128)
-            elif op_name == "lookup_transfers":
-                actual = ctx.submit(Operation.lookup_transfers, payload, 16, 128)
-            elif op_name in SCAN_OPS:
-                assert len(request) == 1
-                code, event_size, result_size = SCAN_OPS[op_name]
-                actual = ctx.submit(code, payload, event_size, result_size)
-            else:
+            if op_name not in ops:
                 raise ValueError(op_name)
+            if op_name in SCAN_OPS:
+                assert len(request) == 1
+            code, event_size, result_size, multi_batch = ops[op_name]
+            actual = ctx.submit(code, payload, event_size, result_size, multi_batch)
             expected = b"".join(reply)
             if actual != expected:
-                raise TableMismatch(describe_mismatch(label, commits, op_name, expected, actual))
+                raise TableMismatch(describe_mismatch(f"{label} [{version}]", commits, op_name,
+                                                      expected, actual, result_size))
             request.clear()
             reply.clear()
             operation = None
@@ -712,10 +741,15 @@ def change_event_mismatch(want, ev, accounts, transfers):
     return None
 
 
-def describe_mismatch(label, commit_index, op_name, expected: bytes, actual: bytes) -> str:
+def describe_mismatch(label, commit_index, op_name, expected: bytes, actual: bytes,
+                      result_size=16) -> str:
     lines = [f"{label}: commit #{commit_index} ({op_name}) reply mismatch "
              f"(expected {len(expected)} B, actual {len(actual)} B)"]
-    if op_name.startswith("create"):
+    if op_name.startswith("create") and result_size == 8:
+        e = np.frombuffer(expected, dtype=np.uint32).reshape(-1, 2)
+        a = np.frombuffer(actual, dtype=np.uint32).reshape(-1, 2)
+        lines.append(f"expected {e.tolist()}\nactual   {a.tolist()}")
+    elif op_name.startswith("create"):
         e = np.frombuffer(expected, dtype=RESULT_DTYPE)
         a = np.frombuffer(actual, dtype=RESULT_DTYPE)
         enum_t = CreateAccountStatus if op_name == "create_accounts" else CreateTransferStatus

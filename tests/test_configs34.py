@@ -1,0 +1,84 @@
+"""Configs 3 and 4 at BASELINE scale (10k accounts; 1M events per run) against the oracle.
+
+The order-dependent workloads of BASELINE.json (configs[2], configs[3]) as the builder's rate tool
+runs them (tests/configs34.py): commits of 16 x 8189 events (the executor's multi-batch calls) and
+one-batch commits of <= 8189 events (one replica prepare, tigerbeetle.zig:853-901). Every call's
+results byte for byte, then every Account / Transfer row, TransferPending status and AccountEvent
+(parity.Pair). Config 3 also runs with the one-lane account walk (TBG_LANES_ONE_LANE), config 4
+with every post/void replayed (TBG_NO_PV_FAST) on its one-batch form.
+"""
+import pytest
+
+import configs34
+from parity import Pair
+
+pytestmark = pytest.mark.gpu
+
+BATCH = configs34.BATCH
+
+
+def _pair(n, batches):
+    return Pair(account_capacity=1 << 14, transfer_capacity=n + (1 << 14),
+                batch_events_max=BATCH * batches, batch_count_max=batches)
+
+
+@pytest.mark.parametrize("walk", ["wave", "one_lane"])
+def test_config3_baseline_scale(walk, monkeypatch):
+    """10k accounts, 100 hot with debits_must_not_exceed_credits; 1M events as 8 calls of
+    16 x 8189 (the last one shorter), then one single-batch 8189-event call
+    (state_machine.zig:3903-3913 in serial order)."""
+    if walk == "one_lane":
+        monkeypatch.setenv("TBG_LANES_ONE_LANE", "1")
+    p = _pair(1_000_000 + BATCH, 16)
+    try:
+        s = configs34.config3(p, 1_000_000, batches_per_commit=16, tail_single=BATCH)
+        assert s["calls"] == 9
+        # ~20% of each hot account's debits find its credits exhausted
+        assert 0.1 * s["hot_debits"] < s["exceeds_credits"] < 0.35 * s["hot_debits"]
+        assert p.stats["replayed"] > 500_000  # the walk decides most of the stream
+        p.compare_state()
+    finally:
+        p.close()
+
+
+def test_config3_one_batch_commits():
+    """Config 3 as replica commits: 25 single-batch calls of 8189 events."""
+    p = _pair(25 * BATCH, 1)
+    try:
+        s = configs34.config3(p, 25 * BATCH, batches_per_commit=1)
+        assert s["calls"] == 25 and s["exceeds_credits"] > 0
+        p.compare_state()
+    finally:
+        p.close()
+
+
+def test_config4_baseline_scale():
+    """10k accounts; 1M events of pending / post / void / chains with injected failures /
+    resubmits in 8 calls of 16 x 8189, a 1-2 s tick and a pulse after each
+    (state_machine.zig:3033-3207, :4053-4299, :4511-4628)."""
+    p = _pair(1_000_000, 16)
+    try:
+        s = configs34.config4(p, 1_000_000, batches_per_commit=16)
+        assert s["commits"] == 8
+        # created, exceeds_credits, pending_transfer_already_posted / _voided, the ledger
+        # mismatch, and linked_event_failed all occur
+        for st in (0xFFFFFFFF, 54, 24, 32, 1):
+            assert st in s["statuses"], st
+        p.compare_state()
+    finally:
+        p.close()
+
+
+@pytest.mark.parametrize("pv", ["fast", "replayed"])
+def test_config4_one_batch_commits(pv, monkeypatch):
+    """Config 4 as replica commits: 30 single-batch calls of 8189 events with ticks and pulses;
+    post/voids FAST-claimed, or all replayed (TBG_NO_PV_FAST)."""
+    if pv == "replayed":
+        monkeypatch.setenv("TBG_NO_PV_FAST", "1")
+    p = _pair(30 * BATCH, 1)
+    try:
+        s = configs34.config4(p, 30 * BATCH, batches_per_commit=1)
+        assert s["commits"] == 30
+        p.compare_state()
+    finally:
+        p.close()

@@ -77,6 +77,19 @@ def test_gpu_table(table, force_replay):
         h.close()
 
 
+@pytest.mark.parametrize("version", ["sparse", "unbatched"])
+@pytest.mark.parametrize("table", tablerun.table_files())
+def test_gpu_table_deprecated_encodings(table, version):
+    """The reference runs every table in each client encoding (check, state_machine_tests.zig
+    :607-619): the sparse create results and the unbatched bodies through the HIP executor."""
+    rows = tablerun.load_table(f"{tablerun.TABLE_DIR}/{table}")
+    h = gpu_handle(False)
+    try:
+        tablerun.run_table(h, rows, table, version)
+    finally:
+        h.close()
+
+
 @pytest.mark.parametrize("durability", ["compact", "checkpoint"])
 @pytest.mark.parametrize("table", tablerun.table_files())
 def test_gpu_table_durability(table, durability, tmp_path):

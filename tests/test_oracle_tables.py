@@ -34,12 +34,14 @@ def oracle_handle():
     return tablerun.StateMachineHandle(lib, sm, set_balances, close)
 
 
+@pytest.mark.parametrize("version", list(tablerun.VERSIONS))
 @pytest.mark.parametrize("table", tablerun.table_files())
-def test_oracle_table(table):
+def test_oracle_table(table, version):
+    """check(): every table in each client encoding (state_machine_tests.zig:607-619)."""
     rows = tablerun.load_table(f"{tablerun.TABLE_DIR}/{table}")
     h = oracle_handle()
     try:
-        tablerun.run_table(h, rows, table)
+        tablerun.run_table(h, rows, table, version)
     finally:
         h.close()
 

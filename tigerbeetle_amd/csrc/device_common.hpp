@@ -40,6 +40,12 @@ __host__ __device__ inline tb_uint128_t W(u128 x) {
     r.hi = (uint64_t)(x >> 64);
     return r;
 }
+// sum_overflows (state_machine.zig:5144-5149): whether a + b overflows Int (std.math.add's
+// error), for the u64 and u128 widths the reference instantiates (:5163-5166).
+template <typename Int>
+__host__ __device__ inline bool sum_overflows(Int a, Int b) {
+    return Int(a + b) < a;
+}
 __host__ __device__ inline bool u128_eq(const tb_uint128_t& a, const tb_uint128_t& b) {
     return a.lo == b.lo && a.hi == b.hi;
 }

@@ -1756,6 +1756,56 @@ int tbg_last_stats(tbg_ctx* ctx, tbg_stats* out) {
     return 0;
 }
 
+}  // extern "C"
+
+namespace {
+
+__device__ __host__ inline uint8_t sum_overflows_bits(uint32_t bits, const tb_uint128_t& a,
+                                                      const tb_uint128_t& b) {
+    return bits == 64 ? uint8_t(sum_overflows<uint64_t>(a.lo, b.lo))
+                      : uint8_t(sum_overflows<u128>(U(a), U(b)));
+}
+
+__global__ void sum_overflows_kernel(uint32_t bits, const tb_uint128_t* a, const tb_uint128_t* b,
+                                     uint32_t n, uint8_t* out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = sum_overflows_bits(bits, a[i], b[i]);
+}
+
+}  // namespace
+
+extern "C" {
+
+int tbg_sum_overflows(tbg_ctx* ctx, uint32_t bits, const tb_uint128_t* a, const tb_uint128_t* b,
+                      uint32_t n, uint8_t* out) {
+    if ((bits != 64 && bits != 128) || (n && (!a || !b || !out))) return TBG_EINVAL;
+    if (!ctx) {
+        for (uint32_t i = 0; i < n; i++) out[i] = sum_overflows_bits(bits, a[i], b[i]);
+        return 0;
+    }
+    if (n == 0) return 0;
+    tb_uint128_t* d = nullptr;
+    uint8_t* d_out = nullptr;
+    int rc = dev_alloc(ctx, &d, 2 * uint64_t(n), false) && dev_alloc(ctx, &d_out, n, false)
+                 ? 0 : TBG_ENOMEM;
+    if (!rc && !(hip_ok(ctx, hipMemcpyAsync(d, a, n * 16ull, hipMemcpyHostToDevice, ctx->stream),
+                        "copy") &&
+                 hip_ok(ctx, hipMemcpyAsync(d + n, b, n * 16ull, hipMemcpyHostToDevice,
+                                            ctx->stream), "copy")))
+        rc = TBG_EHIP;
+    if (!rc) {
+        hipLaunchKernelGGL(sum_overflows_kernel, dim3(grid_for(n)), dim3(kBlock), 0, ctx->stream,
+                           bits, d, d + n, n, d_out);
+        if (!hip_ok(ctx, hipGetLastError(), "launch") ||
+            !hip_ok(ctx, hipMemcpyAsync(out, d_out, n, hipMemcpyDeviceToHost, ctx->stream), "copy") ||
+            !hip_ok(ctx, hipStreamSynchronize(ctx->stream), "sync"))
+            rc = TBG_EHIP;
+    }
+    if (d) (void)hipFree(d);
+    if (d_out) (void)hipFree(d_out);
+    return rc;
+}
+
 int tbg_debug_force_replay(tbg_ctx* ctx, int enable) {
     if (!ctx) return TBG_EINVAL;
     ctx->force_replay = enable != 0;

@@ -804,13 +804,13 @@ __device__ uint32_t replay_create_transfer(Replay& R, const C& c, uint32_t k, ui
     const u128 dpe = U(dr.debits_pending), dpo = U(dr.debits_posted);
     const u128 cpe = U(cr.credits_pending), cpo = U(cr.credits_posted);
     if (f & TB_TRANSFER_PENDING) {
-        if (amount + dpe < amount) return TB_CT_OVERFLOWS_DEBITS_PENDING;
-        if (amount + cpe < amount) return TB_CT_OVERFLOWS_CREDITS_PENDING;
+        if (sum_overflows(amount, dpe)) return TB_CT_OVERFLOWS_DEBITS_PENDING;
+        if (sum_overflows(amount, cpe)) return TB_CT_OVERFLOWS_CREDITS_PENDING;
     }
-    if (amount + dpo < amount) return TB_CT_OVERFLOWS_DEBITS_POSTED;
-    if (amount + cpo < amount) return TB_CT_OVERFLOWS_CREDITS_POSTED;
-    if (amount + (dpe + dpo) < amount) return TB_CT_OVERFLOWS_DEBITS;
-    if (amount + (cpe + cpo) < amount) return TB_CT_OVERFLOWS_CREDITS;
+    if (sum_overflows(amount, dpo)) return TB_CT_OVERFLOWS_DEBITS_POSTED;
+    if (sum_overflows(amount, cpo)) return TB_CT_OVERFLOWS_CREDITS_POSTED;
+    if (sum_overflows(amount, dpe + dpo)) return TB_CT_OVERFLOWS_DEBITS;
+    if (sum_overflows(amount, cpe + cpo)) return TB_CT_OVERFLOWS_CREDITS;
     if (ts_actual + (uint64_t)t.timeout * TB_NS_PER_S > TB_TIMESTAMP_MAX)
         return TB_CT_OVERFLOWS_TIMEOUT;
     if ((dr.flags & TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS) && dpe + dpo + amount > U(dr.credits_posted))

@@ -23,43 +23,74 @@ constexpr uint16_t kTrailerPadding = 0xFFFF;      // TrailerItem.padding
 
 uint32_t div_ceil(uint32_t a, uint32_t b) { return (a + b - 1) / b; }
 
+// Operation's comptime facts (src/tigerbeetle.zig:717-849): EventType / ResultType sizes,
+// is_batchable, is_multi_batch.
 struct OperationInfo {
     uint32_t event_size;
     uint32_t result_size;
+    bool batchable;
     bool multi_batch;
 };
 
 bool operation_info(uint8_t operation, OperationInfo* info) {
     switch (operation) {
-        case TB_OPERATION_PULSE: *info = {0, 1, false}; return true;
-        case TB_OPERATION_CREATE_ACCOUNTS: *info = {128, 16, true}; return true;
-        case TB_OPERATION_CREATE_TRANSFERS: *info = {128, 16, true}; return true;
-        case TB_OPERATION_LOOKUP_ACCOUNTS: *info = {16, 128, true}; return true;
-        case TB_OPERATION_LOOKUP_TRANSFERS: *info = {16, 128, true}; return true;
-        case TB_OPERATION_GET_CHANGE_EVENTS: *info = {64, 384, false}; return true;
-        case TB_OPERATION_GET_ACCOUNT_TRANSFERS: *info = {128, 128, true}; return true;
-        case TB_OPERATION_GET_ACCOUNT_BALANCES: *info = {128, 128, true}; return true;
-        case TB_OPERATION_QUERY_ACCOUNTS: *info = {64, 128, true}; return true;
-        case TB_OPERATION_QUERY_TRANSFERS: *info = {64, 128, true}; return true;
+        case TB_OPERATION_PULSE: *info = {0, 0, false, false}; return true;
+        case TB_OPERATION_DEPRECATED_CREATE_ACCOUNTS_UNBATCHED:
+        case TB_OPERATION_DEPRECATED_CREATE_TRANSFERS_UNBATCHED:
+            *info = {128, 8, true, false}; return true;
+        case TB_OPERATION_DEPRECATED_LOOKUP_ACCOUNTS_UNBATCHED:
+        case TB_OPERATION_DEPRECATED_LOOKUP_TRANSFERS_UNBATCHED:
+            *info = {16, 128, true, false}; return true;
+        case TB_OPERATION_DEPRECATED_GET_ACCOUNT_TRANSFERS_UNBATCHED:
+        case TB_OPERATION_DEPRECATED_GET_ACCOUNT_BALANCES_UNBATCHED:
+            *info = {128, 128, false, false}; return true;
+        case TB_OPERATION_DEPRECATED_QUERY_ACCOUNTS_UNBATCHED:
+        case TB_OPERATION_DEPRECATED_QUERY_TRANSFERS_UNBATCHED:
+            *info = {64, 128, false, false}; return true;
+        case TB_OPERATION_GET_CHANGE_EVENTS: *info = {64, 384, false, false}; return true;
+        case TB_OPERATION_DEPRECATED_CREATE_ACCOUNTS_SPARSE:
+        case TB_OPERATION_DEPRECATED_CREATE_TRANSFERS_SPARSE:
+            *info = {128, 8, true, true}; return true;
+        case TB_OPERATION_LOOKUP_ACCOUNTS:
+        case TB_OPERATION_LOOKUP_TRANSFERS: *info = {16, 128, true, true}; return true;
+        case TB_OPERATION_GET_ACCOUNT_TRANSFERS:
+        case TB_OPERATION_GET_ACCOUNT_BALANCES: *info = {128, 128, false, true}; return true;
+        case TB_OPERATION_QUERY_ACCOUNTS:
+        case TB_OPERATION_QUERY_TRANSFERS: *info = {64, 128, false, true}; return true;
+        case TB_OPERATION_CREATE_ACCOUNTS:
+        case TB_OPERATION_CREATE_TRANSFERS: *info = {128, 16, true, true}; return true;
         default: return false;
     }
 }
 
-// Operation.is_batchable (src/tigerbeetle.zig:787-815): the queries take one filter per batch.
-bool is_query(uint8_t operation) {
-    return operation == TB_OPERATION_GET_CHANGE_EVENTS ||
-           operation == TB_OPERATION_GET_ACCOUNT_TRANSFERS ||
-           operation == TB_OPERATION_GET_ACCOUNT_BALANCES ||
-           operation == TB_OPERATION_QUERY_ACCOUNTS || operation == TB_OPERATION_QUERY_TRANSFERS;
+bool is_create(uint8_t operation) {
+    switch (operation) {
+        case TB_OPERATION_CREATE_ACCOUNTS:
+        case TB_OPERATION_CREATE_TRANSFERS:
+        case TB_OPERATION_DEPRECATED_CREATE_ACCOUNTS_SPARSE:
+        case TB_OPERATION_DEPRECATED_CREATE_TRANSFERS_SPARSE:
+        case TB_OPERATION_DEPRECATED_CREATE_ACCOUNTS_UNBATCHED:
+        case TB_OPERATION_DEPRECATED_CREATE_TRANSFERS_UNBATCHED: return true;
+        default: return false;
+    }
 }
 
-// A query filter's `limit` (Operation.result_count_expected, tigerbeetle.zig:966-990).
+bool creates_accounts(uint8_t operation) {
+    return operation == TB_OPERATION_CREATE_ACCOUNTS ||
+           operation == TB_OPERATION_DEPRECATED_CREATE_ACCOUNTS_SPARSE ||
+           operation == TB_OPERATION_DEPRECATED_CREATE_ACCOUNTS_UNBATCHED;
+}
+
+// A query filter's `limit` (Operation.result_count_expected, tigerbeetle.zig:966-990): the
+// AccountFilter, QueryFilter or ChangeEventsFilter of the (non-batchable) operation.
 uint32_t filter_limit(uint8_t operation, const uint8_t* filter) {
     uint32_t limit = 0;
-    const size_t at = (operation == TB_OPERATION_QUERY_ACCOUNTS ||
-                       operation == TB_OPERATION_QUERY_TRANSFERS)
-                          ? offsetof(tb_query_filter_t, limit)
-                          : offsetof(tb_account_filter_t, limit);
+    size_t at = offsetof(tb_account_filter_t, limit);
+    if (operation == TB_OPERATION_QUERY_ACCOUNTS || operation == TB_OPERATION_QUERY_TRANSFERS ||
+        operation == TB_OPERATION_DEPRECATED_QUERY_ACCOUNTS_UNBATCHED ||
+        operation == TB_OPERATION_DEPRECATED_QUERY_TRANSFERS_UNBATCHED)
+        at = offsetof(tb_query_filter_t, limit);
+    if (operation == TB_OPERATION_GET_CHANGE_EVENTS) at = offsetof(tb_change_events_filter_t, limit);
     std::memcpy(&limit, filter + at, 4);
     return limit;
 }
@@ -154,32 +185,39 @@ struct tb_sm {
 
     // Operation.event_max (src/tigerbeetle.zig:853-901).
     uint32_t event_max(const OperationInfo& info, uint32_t batch_size_limit) const {
+        const uint32_t mbsm = options.message_body_size_max;
         if (!info.multi_batch) {
-            return info.event_size == 0 ? options.message_body_size_max / info.result_size
+            return info.event_size == 0 ? mbsm / info.result_size
                                         : std::min(batch_size_limit / info.event_size,
-                                                   options.message_body_size_max / info.result_size);
+                                                   mbsm / info.result_size);
         }
-        uint32_t reply_trailer_min = tb_multi_batch_trailer_total_size(info.result_size, 1);
-        uint32_t request_trailer_min = tb_multi_batch_trailer_total_size(info.event_size, 1);
+        const uint32_t reply_trailer_min = tb_multi_batch_trailer_total_size(info.result_size, 1);
+        if (info.event_size == 0) return (mbsm - reply_trailer_min) / info.result_size;
+        const uint32_t request_trailer_min = tb_multi_batch_trailer_total_size(info.event_size, 1);
         return std::min((batch_size_limit - request_trailer_min) / info.event_size,
-                        (options.message_body_size_max - reply_trailer_min) / info.result_size);
+                        (mbsm - reply_trailer_min) / info.result_size);
     }
 
     // Operation.result_max (tigerbeetle.zig:907-931).
-    uint32_t result_max(uint8_t operation, const OperationInfo& info,
-                        uint32_t batch_size_limit) const {
-        if (!is_query(operation)) return event_max(info, batch_size_limit);
-        if (!info.multi_batch) return options.message_body_size_max / info.result_size;
-        return (options.message_body_size_max -
-                tb_multi_batch_trailer_total_size(info.result_size, 1)) / info.result_size;
+    uint32_t result_max(const OperationInfo& info, uint32_t batch_size_limit) const {
+        if (info.batchable) return event_max(info, batch_size_limit);
+        const uint32_t mbsm = options.message_body_size_max;
+        if (!info.multi_batch) return mbsm / info.result_size;
+        return (mbsm - tb_multi_batch_trailer_total_size(info.result_size, 1)) / info.result_size;
     }
 
+    // StateMachine.batch_valid (state_machine.zig:1036-1067): one (decoded) batch.
     bool batch_valid(uint8_t operation, const OperationInfo& info, uint32_t batch_size) const {
         if (operation == TB_OPERATION_PULSE) return batch_size == 0;
-        // Not batchable (queries): exactly one filter.
-        if (is_query(operation)) return batch_size == info.event_size;
+        if (!info.batchable) return batch_size == info.event_size;
         if (batch_size % info.event_size != 0) return false;
         return batch_size / info.event_size <= event_max(info, options.batch_size_limit);
+    }
+
+    // prepare_delta_nanoseconds (:1106-1136): the logical time one batch advances.
+    uint64_t prepare_delta(uint8_t operation, uint32_t batch_size) const {
+        if (operation == TB_OPERATION_PULSE) return options.pulse_batch_max;
+        return is_create(operation) ? batch_size / 128u : 0;
     }
 };
 
@@ -292,8 +330,24 @@ extern "C" void tb_sm_close(tb_sm* sm) {
 
 extern "C" tbg_ctx* tb_sm_executor_gpu(tb_sm* sm) { return sm ? sm->gpu : nullptr; }
 
+extern "C" uint32_t tb_sm_event_max(const tb_sm* sm, uint8_t operation, uint32_t batch_size_limit) {
+    OperationInfo info;
+    if (!sm || !operation_info(operation, &info) || info.result_size == 0) return 0;
+    if (batch_size_limit == 0 || batch_size_limit > sm->options.message_body_size_max) return 0;
+    return sm->event_max(info, batch_size_limit);
+}
+
+extern "C" uint32_t tb_sm_result_max(const tb_sm* sm, uint8_t operation, uint32_t batch_size_limit) {
+    OperationInfo info;
+    if (!sm || !operation_info(operation, &info) || info.result_size == 0) return 0;
+    if (batch_size_limit == 0 || batch_size_limit > sm->options.message_body_size_max) return 0;
+    return sm->result_max(info, batch_size_limit);
+}
+
 extern "C" int tb_sm_input_valid(const tb_sm* sm, uint8_t operation, const void* body,
                                  uint32_t size) {
+    // StateMachine.input_valid (:980-1032). The reference asserts size <= batch_size_limit (the
+    // replica checked it); here an oversize body is simply invalid.
     OperationInfo info;
     if (!operation_info(operation, &info)) return 0;
     if (size > sm->options.batch_size_limit) return 0;
@@ -305,13 +359,17 @@ extern "C" int tb_sm_input_valid(const tb_sm* sm, uint8_t operation, const void*
                                        uint32_t(counts.size()), &payload);
     if (nb <= 0) return 0;
     uint64_t result_count_expected = 0;
-    const uint32_t result_max = sm->result_max(operation, info, sm->options.message_body_size_max);
+    // Replies are not constrained by the runtime batch_size_limit (:1013-1017).
+    const uint32_t result_max = sm->result_max(info, sm->options.message_body_size_max);
     const uint8_t* batch = static_cast<const uint8_t*>(body);
     for (int64_t b = 0; b < nb; b++) {
-        if (!sm->batch_valid(operation, info, uint32_t(counts[b]) * info.event_size)) return 0;
-        const uint32_t expected = is_query(operation) ? filter_limit(operation, batch) : counts[b];
+        const uint32_t batch_size = uint32_t(counts[b]) * info.event_size;
+        if (!sm->batch_valid(operation, info, batch_size)) return 0;
+        // Operation.result_count_expected (tigerbeetle.zig:936-992): one result per event, or
+        // up to the filter's limit.
+        const uint32_t expected = info.batchable ? counts[b] : filter_limit(operation, batch);
         result_count_expected += std::min<uint32_t>(expected, result_max);
-        batch += uint32_t(counts[b]) * info.event_size;
+        batch += batch_size;
     }
     uint64_t reply_trailer = tb_multi_batch_trailer_total_size(info.result_size, uint32_t(nb));
     if (sm->options.message_body_size_max < result_count_expected * info.result_size + reply_trailer)
@@ -320,18 +378,19 @@ extern "C" int tb_sm_input_valid(const tb_sm* sm, uint8_t operation, const void*
 }
 
 extern "C" void tb_sm_prepare(tb_sm* sm, uint8_t operation, const void* body, uint32_t size) {
+    // StateMachine.prepare (:1070-1101): the sum of the batches' deltas.
     OperationInfo info;
     if (!operation_info(operation, &info)) return;
     uint64_t delta = 0;
-    if (operation == TB_OPERATION_PULSE) {
-        delta = sm->options.pulse_batch_max;
-    } else if (operation == TB_OPERATION_CREATE_ACCOUNTS ||
-               operation == TB_OPERATION_CREATE_TRANSFERS) {
+    if (!info.multi_batch) {
+        delta = sm->prepare_delta(operation, size);
+    } else {
         uint32_t payload = 0;
         sm->counts.resize(kBatchCountMax);
         int64_t nb = tb_multi_batch_decode(body, size, info.event_size, sm->counts.data(),
                                            uint32_t(sm->counts.size()), &payload);
-        if (nb > 0) delta = payload / info.event_size;
+        for (int64_t b = 0; b < nb; b++)
+            delta += sm->prepare_delta(operation, uint32_t(sm->counts[b]) * info.event_size);
     }
     sm->prepare_timestamp += delta;
 }
@@ -353,6 +412,51 @@ extern "C" void tb_sm_prefetch(tb_sm* sm, tb_sm_prefetch_callback callback, void
     if (callback) callback(context);
 }
 
+namespace {
+
+// The sparse results of the deprecated create operations (CreateAccountErrorResult /
+// CreateTransferErrorResult, tigerbeetle.zig:496-515): execute_create (:3116-3194) appends
+// {index, status} for every event whose final status is not `created` -- a broken chain's earlier
+// events (linked_event_failed) are appended, in order, before the event that broke it -- which is
+// the dense results' non-created entries in index order. Returns the bytes written.
+uint32_t sparse_results(const tb_create_result_t* dense, uint32_t n, uint8_t* out) {
+    uint32_t count = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        if (dense[i].status == TB_STATUS_CREATED) continue;
+        const uint32_t entry[2] = {i, dense[i].status};
+        std::memcpy(out + 8u * count, entry, 8);
+        count++;
+    }
+    return 8u * count;
+}
+
+// One query filter's scan through the executor: results written to `dst`, their count returned
+// (at most min(filter.limit, limit_max); 0 for an invalid filter).
+int64_t execute_scan(const tb_executor& ex, uint8_t operation, const uint8_t* filter,
+                     uint32_t limit_max, void* dst) {
+    switch (operation) {
+        case TB_OPERATION_GET_ACCOUNT_TRANSFERS:
+        case TB_OPERATION_DEPRECATED_GET_ACCOUNT_TRANSFERS_UNBATCHED:
+            return ex.get_account_transfers(ex.self,
+                                            reinterpret_cast<const tb_account_filter_t*>(filter),
+                                            limit_max, static_cast<tb_transfer_t*>(dst));
+        case TB_OPERATION_GET_ACCOUNT_BALANCES:
+        case TB_OPERATION_DEPRECATED_GET_ACCOUNT_BALANCES_UNBATCHED:
+            return ex.get_account_balances(ex.self,
+                                           reinterpret_cast<const tb_account_filter_t*>(filter),
+                                           limit_max, static_cast<tb_account_balance_t*>(dst));
+        case TB_OPERATION_QUERY_ACCOUNTS:
+        case TB_OPERATION_DEPRECATED_QUERY_ACCOUNTS_UNBATCHED:
+            return ex.query_accounts(ex.self, reinterpret_cast<const tb_query_filter_t*>(filter),
+                                     limit_max, static_cast<tb_account_t*>(dst));
+        default:
+            return ex.query_transfers(ex.self, reinterpret_cast<const tb_query_filter_t*>(filter),
+                                      limit_max, static_cast<tb_transfer_t*>(dst));
+    }
+}
+
+}  // namespace
+
 extern "C" int64_t tb_sm_commit(tb_sm* sm, uint64_t client_lo, uint64_t client_hi, uint64_t op,
                                 uint64_t timestamp, uint8_t operation, const void* body,
                                 uint32_t size, void* output) {
@@ -361,10 +465,12 @@ extern "C" int64_t tb_sm_commit(tb_sm* sm, uint64_t client_lo, uint64_t client_h
     (void)op;
     OperationInfo info;
     if (!operation_info(operation, &info)) return TBG_EINVAL;
+    const tb_executor& ex = sm->executor;
+    uint8_t* out = static_cast<uint8_t*>(output);
     if (operation == TB_OPERATION_PULSE) {
         // execute_expire_pending_transfers (:4511-4628): scans with expires_at_max =
         // prefetch_timestamp (:2463); no output.
-        int64_t expired = sm->executor.pulse(sm->executor.self, timestamp);
+        int64_t expired = ex.pulse(ex.self, timestamp);
         if (expired < 0) return expired;
         if (expired > 0) sm->commit_timestamp = timestamp;
         return 0;
@@ -374,31 +480,39 @@ extern "C" int64_t tb_sm_commit(tb_sm* sm, uint64_t client_lo, uint64_t client_h
         // execute_query(.get_change_events) (:2770-2800, :3395-3422): not multi-batch; the scan
         // limit is capped by the reply size and the prefetches available per scanned result
         // (prefetch_get_change_events_scan, :2232-2265): transfers, and 2 accounts per event.
-        if (size != sizeof(tb_change_events_filter_t) || !sm->executor.get_change_events)
-            return TBG_EINVAL;
+        if (size != sizeof(tb_change_events_filter_t) || !ex.get_change_events) return TBG_EINVAL;
         tb_change_events_filter_t filter;
         std::memcpy(&filter, body, sizeof(filter));
-        const OperationInfo lookup{16, 128, false};  // deprecated_lookup_*_unbatched
+        const OperationInfo lookup{16, 128, true, false};  // deprecated_lookup_*_unbatched
         const uint32_t prefetch = sm->event_max(lookup, sm->options.batch_size_limit);
         const uint32_t limit_max = std::min({sm->options.message_body_size_max / 384u, prefetch,
                                              prefetch / 2});
         if (limit_max == 0) return 0;
-        int64_t count = sm->executor.get_change_events(sm->executor.self, &filter, limit_max,
-                                                       static_cast<tb_change_event_t*>(output));
+        int64_t count = ex.get_change_events(ex.self, &filter, limit_max,
+                                             static_cast<tb_change_event_t*>(output));
         return count < 0 ? count : count * int64_t(sizeof(tb_change_event_t));
     }
 
-    uint32_t payload = 0;
+    // The batches of the body: the multi-batch decoding, or the whole body as one batch for the
+    // deprecated unbatched operations (execute, :2671-2700; execute_query, :2764-2821).
+    uint32_t payload = size;
+    int64_t nb = 1;
     sm->counts.resize(kBatchCountMax);
-    int64_t nb = tb_multi_batch_decode(body, size, info.event_size, sm->counts.data(),
-                                       uint32_t(sm->counts.size()), &payload);
-    if (nb <= 0) return TBG_EINVAL;
+    if (info.multi_batch) {
+        nb = tb_multi_batch_decode(body, size, info.event_size, sm->counts.data(),
+                                   uint32_t(sm->counts.size()), &payload);
+        if (nb <= 0) return TBG_EINVAL;
+    } else {
+        if (size % info.event_size != 0 || (!info.batchable && size != info.event_size))
+            return TBG_EINVAL;
+        sm->counts[0] = uint16_t(size / info.event_size);
+    }
     const uint32_t n = payload / info.event_size;
-    uint8_t* out = static_cast<uint8_t*>(output);
 
-    if (operation == TB_OPERATION_CREATE_ACCOUNTS || operation == TB_OPERATION_CREATE_TRANSFERS) {
+    if (is_create(operation)) {
         // execute_multi_batch: execute_timestamp starts at timestamp - delta(payload) and each
-        // batch advances it by its own delta before executing (:2717-2737).
+        // batch advances it by its own delta before executing (:2717-2737); an unbatched body
+        // is one batch stamped `timestamp` (execute, :2671-2700).
         sm->lens.resize(size_t(nb));
         sm->batch_ts.resize(size_t(nb));
         uint64_t execute_timestamp = timestamp - n;
@@ -407,82 +521,75 @@ extern "C" int64_t tb_sm_commit(tb_sm* sm, uint64_t client_lo, uint64_t client_h
             execute_timestamp += sm->counts[b];
             sm->batch_ts[b] = execute_timestamp;
         }
+        const bool dense = info.result_size == sizeof(tb_create_result_t);
         tb_create_result_t* results = reinterpret_cast<tb_create_result_t*>(out);
-        int rc = operation == TB_OPERATION_CREATE_ACCOUNTS
-                     ? sm->executor.create_accounts(sm->executor.self,
-                                                    static_cast<const tb_account_t*>(body), n,
-                                                    sm->lens.data(), sm->batch_ts.data(),
-                                                    uint32_t(nb), results)
-                     : sm->executor.create_transfers(sm->executor.self,
-                                                     static_cast<const tb_transfer_t*>(body), n,
-                                                     sm->lens.data(), sm->batch_ts.data(),
-                                                     uint32_t(nb), results);
+        if (!dense) {
+            sm->results.resize(n);
+            results = sm->results.data();
+        }
+        int rc = n == 0 ? 0
+                 : creates_accounts(operation)
+                     ? ex.create_accounts(ex.self, static_cast<const tb_account_t*>(body), n,
+                                          sm->lens.data(), sm->batch_ts.data(), uint32_t(nb),
+                                          results)
+                     : ex.create_transfers(ex.self, static_cast<const tb_transfer_t*>(body), n,
+                                           sm->lens.data(), sm->batch_ts.data(), uint32_t(nb),
+                                           results);
         if (rc < 0) return rc;
-        return tb_multi_batch_encode_trailer(out, n * 16u, 16, sm->counts.data(), uint32_t(nb));
+        if (dense)
+            return tb_multi_batch_encode_trailer(out, n * 16u, 16, sm->counts.data(), uint32_t(nb));
+        // Sparse: each batch's errors, indexed within the batch (execute_create runs per batch).
+        uint32_t written = 0, offset = 0;
+        std::vector<uint16_t> reply_counts(static_cast<size_t>(nb));
+        for (int64_t b = 0; b < nb; b++) {
+            const uint32_t bytes = sparse_results(results + offset, sm->counts[b], out + written);
+            reply_counts[b] = uint16_t(bytes / 8);
+            written += bytes;
+            offset += sm->counts[b];
+        }
+        if (!info.multi_batch) return written;
+        return tb_multi_batch_encode_trailer(out, written, 8, reply_counts.data(), uint32_t(nb));
     }
 
-    if (is_query(operation)) {
-        // execute_query_multi_batch (:2823-2910): each batch is one filter, its results (at most
-        // min(filter.limit, result_max)) one reply batch.
-        const tb_executor& ex = sm->executor;
+    if (!info.batchable) {
+        // The scans (execute_query_multi_batch :2823-2910, execute_query :2764-2821): each batch
+        // is one filter, its results (at most min(filter.limit, result_max)) one reply batch.
         if (!ex.get_account_transfers || !ex.get_account_balances || !ex.query_accounts ||
             !ex.query_transfers)
             return TBG_EINVAL;
-        const uint32_t limit_max = sm->result_max(operation, info,
-                                                  sm->options.message_body_size_max);
+        const uint32_t limit_max = sm->result_max(info, sm->options.message_body_size_max);
         const uint8_t* filter = static_cast<const uint8_t*>(body);
         std::vector<uint16_t> reply_counts(static_cast<size_t>(nb));
         uint32_t written = 0;
         for (int64_t b = 0; b < nb; b++, filter += info.event_size) {
-            void* dst = out + written;
-            int64_t count = 0;
-            switch (operation) {
-                case TB_OPERATION_GET_ACCOUNT_TRANSFERS:
-                    count = ex.get_account_transfers(
-                        ex.self, reinterpret_cast<const tb_account_filter_t*>(filter), limit_max,
-                        static_cast<tb_transfer_t*>(dst));
-                    break;
-                case TB_OPERATION_GET_ACCOUNT_BALANCES:
-                    count = ex.get_account_balances(
-                        ex.self, reinterpret_cast<const tb_account_filter_t*>(filter), limit_max,
-                        static_cast<tb_account_balance_t*>(dst));
-                    break;
-                case TB_OPERATION_QUERY_ACCOUNTS:
-                    count = ex.query_accounts(ex.self,
-                                              reinterpret_cast<const tb_query_filter_t*>(filter),
-                                              limit_max, static_cast<tb_account_t*>(dst));
-                    break;
-                default:
-                    count = ex.query_transfers(ex.self,
-                                               reinterpret_cast<const tb_query_filter_t*>(filter),
-                                               limit_max, static_cast<tb_transfer_t*>(dst));
-                    break;
-            }
+            const int64_t count = execute_scan(ex, operation, filter, limit_max, out + written);
             if (count < 0) return count;
             reply_counts[b] = uint16_t(count);
             written += uint32_t(count) * info.result_size;
         }
+        if (!info.multi_batch) return written;
         return tb_multi_batch_encode_trailer(out, written, info.result_size, reply_counts.data(),
                                              uint32_t(nb));
     }
 
     // lookup_accounts / lookup_transfers: per batch, found objects only (:3255-3292).
+    const bool accounts = operation == TB_OPERATION_LOOKUP_ACCOUNTS ||
+                          operation == TB_OPERATION_DEPRECATED_LOOKUP_ACCOUNTS_UNBATCHED;
     const tb_uint128_t* ids = static_cast<const tb_uint128_t*>(body);
     uint32_t written = 0, offset = 0;
     std::vector<uint16_t> reply_counts(static_cast<size_t>(nb));
     for (int64_t b = 0; b < nb; b++) {
-        int64_t found = operation == TB_OPERATION_LOOKUP_ACCOUNTS
-                            ? sm->executor.lookup_accounts(
-                                  sm->executor.self, ids + offset, sm->counts[b],
-                                  reinterpret_cast<tb_account_t*>(out + written))
-                            : sm->executor.lookup_transfers(
-                                  sm->executor.self, ids + offset, sm->counts[b],
-                                  reinterpret_cast<tb_transfer_t*>(out + written));
+        int64_t found = sm->counts[b] == 0 ? 0
+                        : accounts ? ex.lookup_accounts(ex.self, ids + offset, sm->counts[b],
+                                                        reinterpret_cast<tb_account_t*>(out + written))
+                                   : ex.lookup_transfers(ex.self, ids + offset, sm->counts[b],
+                                                         reinterpret_cast<tb_transfer_t*>(out + written));
         if (found < 0) return found;
         reply_counts[b] = uint16_t(found);
         written += uint32_t(found) * 128u;
         offset += sm->counts[b];
     }
+    if (!info.multi_batch) return written;
     return tb_multi_batch_encode_trailer(out, written, 128, reply_counts.data(), uint32_t(nb));
 }
 

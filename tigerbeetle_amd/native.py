@@ -111,6 +111,7 @@ SIGNATURES = [
     ("tbg_query_transfers", ctypes.c_int64, [vp, vp, ctypes.c_uint32, vp]),
     ("tbg_debug_set_account_balances", ctypes.c_int, [vp, U128, U128, U128, U128, U128]),
     ("tbg_last_stats", ctypes.c_int, [vp, ctypes.POINTER(TbgStats)]),
+    ("tbg_sum_overflows", ctypes.c_int, [vp, ctypes.c_uint32, vp, vp, ctypes.c_uint32, vp]),
     ("tbg_debug_force_replay", ctypes.c_int, [vp, ctypes.c_int]),
     ("tbg_debug_serial_replay", ctypes.c_int, [vp, ctypes.c_int]),
     ("tbg_profile", ctypes.c_int, [vp, ctypes.c_int]),
@@ -135,6 +136,8 @@ SIGNATURES = [
     ("tb_sm_checkpoint", ctypes.c_int, [vp, ctypes.c_char_p]),
     ("tb_sm_executor_gpu", vp, [vp]),
     ("tb_sm_input_valid", ctypes.c_int, [vp, ctypes.c_uint8, vp, ctypes.c_uint32]),
+    ("tb_sm_event_max", ctypes.c_uint32, [vp, ctypes.c_uint8, ctypes.c_uint32]),
+    ("tb_sm_result_max", ctypes.c_uint32, [vp, ctypes.c_uint8, ctypes.c_uint32]),
     ("tb_sm_prepare", None, [vp, ctypes.c_uint8, vp, ctypes.c_uint32]),
     ("tb_sm_pulse_needed", ctypes.c_int, [vp, ctypes.c_uint64]),
     ("tb_sm_prefetch", None, [vp, PREFETCH_CALLBACK, vp, ctypes.c_uint64, ctypes.c_uint64,
