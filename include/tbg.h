@@ -92,6 +92,18 @@ int tbg_create_transfers_stamped_device(tbg_ctx* ctx, const tb_transfer_t* d_eve
                                         const uint64_t* d_event_timestamps,
                                         tb_create_result_t* d_results, void* stream);
 
+/* Pins a host buffer the caller reuses across calls (a replica's message bodies and reply
+ * buffers) for direct DMA: a host-buffer call whose events or results lie in a registered range
+ * skips the driver's staged copy of pageable memory (hipHostRegister). Unregistered at
+ * tbg_unregister_host or tbg_close. */
+int tbg_register_host(tbg_ctx* ctx, void* ptr, uint64_t size);
+int tbg_unregister_host(tbg_ctx* ctx, void* ptr);
+
+/* Waits for every kernel and copy the ctx has queued on its own stream (e.g. the AccountEvents
+ * appends a *_device call leaves behind it) -- for callers that reuse the call's device buffers
+ * from other streams. */
+int tbg_synchronize(tbg_ctx* ctx);
+
 /* Returns the number of pending transfers expired (<= pulse_batch_max). */
 int64_t tbg_pulse(tbg_ctx* ctx, uint64_t timestamp);
 uint64_t tbg_pulse_next_timestamp(tbg_ctx* ctx);
@@ -100,13 +112,18 @@ uint64_t tbg_pulse_next_timestamp(tbg_ctx* ctx);
  * ExpirePendingTransfersType :4875-5029, spans all shards): the count of this shard's
  * expired-eligible pending transfers at `timestamp` and the first `max` of their index keys
  * (expires_at, timestamp) in order; then the pulse that expires exactly this shard's entries up to
- * and including a cut key -- the pulse_batch_max-th key across all shards -- and sets
- * pulse_next_timestamp (the cut's expires_at: the scan's buffer filled). Both return a count or a
- * negative error. */
+ * and including a cut key -- the pulse_batch_max-th key across all shards, or the last key when
+ * fewer expire -- and sets pulse_next_timestamp to `pulse_next_timestamp` (the cut's expires_at:
+ * the scan's buffer filled), or, when it is 0, to this shard's first unexpired expires_at.
+ * `event_timestamps` (NULL: timestamp - m + i + 1 locally) stamps this shard's i-th expiry with
+ * its position in the pulse's expiry order over all shards, timestamp - E + position + 1
+ * (execute_expire_pending_transfers :4540-4546): its AccountEvent's timestamp. Both return a
+ * count or a negative error. */
 int64_t tbg_pulse_candidates(tbg_ctx* ctx, uint64_t timestamp, uint64_t* expires_at,
                              uint64_t* timestamps, uint32_t max);
 int64_t tbg_pulse_cut(tbg_ctx* ctx, uint64_t timestamp, uint64_t cut_expires_at,
-                      uint64_t cut_timestamp, uint64_t pulse_next_timestamp);
+                      uint64_t cut_timestamp, uint64_t pulse_next_timestamp,
+                      const uint64_t* event_timestamps);
 
 /* Sharded imported batches: raises the accounts / transfers objects trees' key_range.key_max
  * (read only by imported events' must_not_regress checks) to the maxima over every shard. */

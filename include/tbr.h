@@ -9,9 +9,12 @@
  * open-addressing tables probed like the executor's id tables.
  *
  * The device fast path (tbr_route_device) takes calls in which no event can observe another
- * shard's state: single (unlinked), non-imported, not post/void events whose two accounts are
- * known and on one shard and whose id is new to every shard and unique in the call. Any other
- * event is a *hazard*: the call is left to the exact router (tigerbeetle_amd/shard.py,
+ * shard's state: non-imported events whose id is new to every shard and unique in the call and
+ * whose two accounts are known and on one shard; events whose id already exists (decided by the
+ * id's holder, create_transfer_exists :3988-4051, before any account lookup); post/voids, on the
+ * shard of their pending transfer (in the directory or created earlier in the call) when it has
+ * no timeout; and linked chains whose events all go to one shard and end within their batch. Any
+ * other event is a *hazard*: the call is left to the exact router (tigerbeetle_amd/shard.py,
  * LedgerRouter), which reads the same directories through tbr_account_shards /
  * tbr_transfer_shards and records its outcome with tbr_record_*.
  *
@@ -53,9 +56,13 @@ int64_t tbr_route_device(tbr_ctx* ctx, const tb_transfer_t* d_events, uint32_t n
                          uint64_t* d_out_timestamps, uint32_t* d_out_positions,
                          uint32_t* shard_counts);
 /* The routed call's results (in shard order) back to call order; records the ids that now exist
- * on their shard (created, or orphaned by a transient failure) and releases the others. */
+ * on their shard (created, or orphaned by a transient failure) and releases the others.
+ * *created_timestamp_max (if not NULL) receives the largest timestamp of a created transfer (0 if
+ * none): the transfers objects tree's key_range.key_max the host router keeps for imported
+ * events' must_not_regress checks (:3808-3817). */
 int tbr_settle_device(tbr_ctx* ctx, const tb_create_result_t* d_shard_results,
-                      const uint32_t* d_positions, uint32_t n, tb_create_result_t* d_results);
+                      const uint32_t* d_positions, uint32_t n, tb_create_result_t* d_results,
+                      uint64_t* created_timestamp_max);
 
 #ifdef __cplusplus
 }

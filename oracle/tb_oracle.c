@@ -906,8 +906,11 @@ static uint64_t expiry_sorted(tbo_ctx* c, expiry_key_t** out) {
     return n_keys;
 }
 
-/* execute_expire_pending_transfers (:4540-4626) for the first `expired` keys. */
-static void expire_keys(tbo_ctx* c, const expiry_key_t* keys, uint64_t expired, uint64_t timestamp) {
+/* execute_expire_pending_transfers (:4540-4626) for the first `expired` keys; expiry k is stamped
+ * timestamp - expired + k + 1 (:4546), or stamps[k] (a shard's expiries stamped by their positions
+ * in the pulse over all shards). */
+static void expire_keys(tbo_ctx* c, const expiry_key_t* keys, uint64_t expired, uint64_t timestamp,
+                        const uint64_t* stamps) {
     for (uint64_t k = 0; k < expired; k++) {
         const tb_transfer_t* p = &c->transfers[keys[k].index];
         tb_account_t* dr = get_account(c, U(p->debit_account_id));
@@ -921,7 +924,7 @@ static void expire_keys(tbo_ctx* c, const expiry_key_t* keys, uint64_t expired, 
         *dr = dr_new;
         *cr = cr_new;
         c->pending_status[keys[k].index] = TB_PENDING_EXPIRED;
-        c->commit_timestamp = timestamp - expired + k + 1;
+        c->commit_timestamp = stamps ? stamps[k] : timestamp - expired + k + 1;
         account_event(c, c->commit_timestamp, &dr_new, &cr_new, 0, TB_PENDING_EXPIRED, p, 0,
                       U(p->amount));
     }
@@ -943,7 +946,7 @@ uint32_t tbo_pulse(tbo_ctx* c, uint64_t timestamp) {
     } else {
         c->pulse_next_timestamp = TB_TIMESTAMP_MAX;
     }
-    expire_keys(c, keys, expired, timestamp);
+    expire_keys(c, keys, expired, timestamp, NULL);
     free(keys);
     return (uint32_t)expired;
 }
@@ -965,7 +968,8 @@ uint64_t tbo_pulse_candidates(tbo_ctx* c, uint64_t timestamp, uint64_t* expires_
 }
 
 uint32_t tbo_pulse_cut(tbo_ctx* c, uint64_t timestamp, uint64_t cut_expires_at,
-                       uint64_t cut_timestamp, uint64_t pulse_next_timestamp) {
+                       uint64_t cut_timestamp, uint64_t pulse_next_timestamp,
+                       const uint64_t* stamps) {
     expiry_key_t* keys;
     const uint64_t n_keys = expiry_sorted(c, &keys);
     uint64_t expired = 0;
@@ -973,8 +977,10 @@ uint32_t tbo_pulse_cut(tbo_ctx* c, uint64_t timestamp, uint64_t cut_expires_at,
            (keys[expired].expires_at < cut_expires_at ||
             (keys[expired].expires_at == cut_expires_at && keys[expired].timestamp <= cut_timestamp)))
         expired++;
+    if (pulse_next_timestamp == 0) /* this shard's first unexpired (tbg_pulse_cut's rule) */
+        pulse_next_timestamp = expired < n_keys ? keys[expired].expires_at : TB_TIMESTAMP_MAX;
     c->pulse_next_timestamp = pulse_next_timestamp;
-    expire_keys(c, keys, expired, timestamp);
+    expire_keys(c, keys, expired, timestamp, stamps);
     free(keys);
     return (uint32_t)expired;
 }

@@ -46,7 +46,8 @@ uint32_t tbo_pulse(tbo_ctx* ctx, uint64_t timestamp);
 uint64_t tbo_pulse_candidates(tbo_ctx* ctx, uint64_t timestamp, uint64_t* expires_at,
                               uint64_t* timestamps, uint32_t max);
 uint32_t tbo_pulse_cut(tbo_ctx* ctx, uint64_t timestamp, uint64_t cut_expires_at,
-                       uint64_t cut_timestamp, uint64_t pulse_next_timestamp);
+                       uint64_t cut_timestamp, uint64_t pulse_next_timestamp,
+                       const uint64_t* stamps);
 int tbo_pulse_needed(const tbo_ctx* ctx, uint64_t timestamp);
 uint64_t tbo_pulse_next_timestamp(const tbo_ctx* ctx);
 

@@ -18,7 +18,7 @@ _SIGS = [
     ("tbo_pulse", ctypes.c_uint32, [vp, ctypes.c_uint64]),
     ("tbo_pulse_candidates", ctypes.c_uint64, [vp, ctypes.c_uint64, vp, vp, ctypes.c_uint32]),
     ("tbo_pulse_cut", ctypes.c_uint32, [vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
-                                        ctypes.c_uint64]),
+                                        ctypes.c_uint64, vp]),
     ("tbo_pulse_needed", ctypes.c_int, [vp, ctypes.c_uint64]),
     ("tbo_pulse_next_timestamp", ctypes.c_uint64, [vp]),
     ("tbo_lookup_accounts", ctypes.c_uint32, [vp, vp, ctypes.c_uint32, vp]),

@@ -18,8 +18,9 @@ BATCH = configs34.BATCH
 
 
 def _pair(n, batches):
+    # (batch_events_max also holds the 10k-account create_accounts call)
     return Pair(account_capacity=1 << 14, transfer_capacity=n + (1 << 14),
-                batch_events_max=BATCH * batches, batch_count_max=batches)
+                batch_events_max=max(BATCH * batches, 1 << 14), batch_count_max=batches)
 
 
 @pytest.mark.parametrize("walk", ["wave", "one_lane"])

@@ -4,9 +4,12 @@ union of the shards' final tables against the oracle's.
 
 Two ranks on the box's one GPU, over gloo (host staging; RCCL needs one GPU per rank): rank 0
 holds the client calls in HBM and the device router; each rank owns two of four ledgers. The
-calls mix the device fast path (interleaved ledgers, fresh ids) with calls the device router must
-hand to the exact host router (a transfer between two shards' accounts, a linked chain, resubmitted
-ids, post/void), and pending transfers that expire in sharded pulses.
+calls take the device path -- interleaved ledgers and fresh ids; a linked chain on one shard,
+resubmitted ids (on their holders) and posts / voids of untimed pending transfers (on their
+pending transfer's shard) -- except the one the device router must hand to the exact host router
+(a transfer between two shards' accounts); pending transfers expire in sharded pulses. Every shard
+records AccountEvents, and the union of the shards' logs must be the oracle's (the ADVICE item:
+the appends a device call leaves on the executor's stream read the call's buffers).
 """
 import multiprocessing as mp
 import os
@@ -65,8 +68,11 @@ def _calls(seed):
 
     fast1 = uniform(30_000, pending_frac=0.1)
     ops.append(("fast", fast1, [8189, 8189, 8189, 30_000 - 3 * 8189]))
+    cross = uniform(2_000)
+    # (ledgers 1, 2 on shard 0 and 3, 4 on shard 1: the credit account two ledgers over)
+    cross["credit_account_id"][5, 0] = ((int(cross["ledger"][5]) + 1) % LEDGERS) * PER_LEDGER + 8
+    ops.append(("host", cross, [2_000]))  # a transfer between two shards' accounts
     haz = uniform(3_000)
-    haz["credit_account_id"][5, 0] = ((int(haz["ledger"][5]) % LEDGERS) * PER_LEDGER) + 7  # 2 shards
     haz["flags"][10:13] |= 1  # a chain (same ledger: set its accounts)
     for j in range(10, 14):
         haz["ledger"][j] = 1
@@ -84,7 +90,7 @@ def _calls(seed):
         haz["ledger"][e] = 0
         haz["code"][e] = 0
         haz["timeout"][e] = 0
-    ops.append(("host", haz, [3_000]))
+    ops.append(("fast", haz, [3_000]))
     ops.append(("tick", 2_000_000_000))
     ops.append(("fast", uniform(20_000), [8189, 20_000 - 8189]))
     return ops
@@ -110,6 +116,7 @@ def _rank(rank, world, port, seed, q):
         o.pulse_batch_max = 8190
         o.device = 0
         o.pulse_next_timestamp_init = TIMESTAMP_MAX
+        o.account_events_capacity = 1 << 18
         rs = RoutedShards(o, events_max=1 << 16, router_transfer_capacity=1 << 19,
                           router_account_capacity=4096, ledgers=LEDGERS)
         ref = OracleShard() if rank == 0 else None
@@ -160,10 +167,17 @@ def _rank(rank, world, port, seed, q):
                 pulses += 1
         dumps = [None] * world
         dist.all_gather_object(dumps, rs.shard.dump())
+        events = [None] * world
+        dist.all_gather_object(events, rs.shard.dump_account_events())
         if rank == 0:
             assert all(len(d[1]) for d in dumps), "every shard holds transfers"
             assert_same_state(dumps, ref)
-            assert rs.fast_calls == 2 and rs.host_calls == 1, (rs.fast_calls, rs.host_calls)
+            got = np.concatenate(events)
+            got = got[np.argsort(got["timestamp"], kind="stable")]
+            want = ref.dump_account_events()
+            assert len(got) > 50_000 and got.tobytes() == want.tobytes(), \
+                f"account events differ ({len(got)} vs {len(want)})"
+            assert rs.fast_calls == 3 and rs.host_calls == 1, (rs.fast_calls, rs.host_calls)
             assert pulses > 0
         rs.close()
         dist.barrier()

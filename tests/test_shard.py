@@ -22,7 +22,7 @@ sys.path.insert(0, os.path.dirname(HERE))
 sys.path.insert(0, HERE)
 
 from tigerbeetle_amd import shard, workload  # noqa: E402
-from tigerbeetle_amd.types import (ACCOUNT_DTYPE, NS_PER_S, RESULT_DTYPE,  # noqa: E402
+from tigerbeetle_amd.types import (ACCOUNT_DTYPE, ACCOUNT_EVENT_DTYPE, NS_PER_S, RESULT_DTYPE,  # noqa: E402,E501
                                    TIMESTAMP_MAX, TRANSFER_DTYPE)
 import oracle_binding  # noqa: E402
 
@@ -74,9 +74,11 @@ class OracleShard:
         k = min(n, max_keys)
         return n, list(zip(e[:k].tolist(), t[:k].tolist()))
 
-    def pulse_cut(self, timestamp, cut_expires_at, cut_timestamp, pulse_next_timestamp):
+    def pulse_cut(self, timestamp, cut_expires_at, cut_timestamp, pulse_next_timestamp,
+                  stamps=None):
+        st = None if not stamps else np.ascontiguousarray(stamps, dtype=np.uint64)
         return int(self.lib.tbo_pulse_cut(self.o, timestamp, cut_expires_at, cut_timestamp,
-                                          pulse_next_timestamp))
+                                          pulse_next_timestamp, None if st is None else _ptr(st)))
 
     def pulse_next_timestamp(self):
         return int(self.lib.tbo_pulse_next_timestamp(self.o))
@@ -93,6 +95,12 @@ class OracleShard:
         self.lib.tbo_dump_transfers(self.o, _ptr(t))
         self.lib.tbo_dump_pending_status(self.o, _ptr(s))
         return a, t, s
+
+    def dump_account_events(self):
+        """The oracle's AccountEvents in timestamp order (the groove is keyed by timestamp)."""
+        e = np.zeros(self.lib.tbo_dump_account_events(self.o, None), dtype=ACCOUNT_EVENT_DTYPE)
+        self.lib.tbo_dump_account_events(self.o, _ptr(e))
+        return e[np.argsort(e["timestamp"], kind="stable")]
 
 
 def _split(rng, n, max_batch):
@@ -229,7 +237,10 @@ def drive(cluster, ref, ops, rank0=True, pbm=PBM, cuts=None):
     return pulses
 
 
-def assert_same_state(dumps, ref):
+def assert_same_state(dumps, ref, events=None):
+    """The union of the shards' tables in timestamp order equals the unsharded reference's; with
+    `events` (each shard's AccountEvents), so does the union of the account_events logs -- an
+    expiry's AccountEvent carries its position in the pulse across all shards."""
     a = np.concatenate([d[0] for d in dumps])
     t = np.concatenate([d[1] for d in dumps])
     s = np.concatenate([d[2] for d in dumps])
@@ -238,6 +249,11 @@ def assert_same_state(dumps, ref):
     for got, want, name in zip((a[oa], t[ot], s[ot]), ref.dump(),
                                ("accounts", "transfers", "TransferPending statuses")):
         assert got.tobytes() == want.tobytes(), f"{name} differ ({len(got)} vs {len(want)} rows)"
+    if events is not None:
+        e = np.concatenate(events)
+        e = e[np.argsort(e["timestamp"], kind="stable")]
+        want = ref.dump_account_events()
+        assert e.tobytes() == want.tobytes(), f"account events differ ({len(e)} vs {len(want)})"
 
 
 def _accounts(ids, ledgers):
@@ -359,7 +375,7 @@ def test_local_shards_match_unsharded(seed):
         assert drive(cluster, ref, scenario(seed)) > 0
         dumps = [s.dump() for s in shards]
         assert all(len(d[1]) for d in dumps), "every shard holds transfers"
-        assert_same_state(dumps, ref)
+        assert_same_state(dumps, ref, [s.dump_account_events() for s in shards])
     finally:
         for s in shards + [ref]:
             s.close()
@@ -384,7 +400,8 @@ def test_local_shards_pulse_cut(seed):
         cuts = []
         assert drive(cluster, ref, scenario(seed, calls=10), pbm=pbm, cuts=cuts) > 0
         assert cuts, "the scenario should expire more than pulse_batch_max at once"
-        assert_same_state([s.dump() for s in shards], ref)
+        assert_same_state([s.dump() for s in shards], ref,
+                          [s.dump_account_events() for s in shards])
     finally:
         for s in shards + [ref]:
             s.close()
@@ -407,9 +424,11 @@ def _gloo_rank(rank, world, port, seed, q, pbm=PBM):
             assert cuts, "the scenario should expire more than pulse_batch_max at once"
         dumps = [None] * world
         dist.all_gather_object(dumps, ex.dump())
+        events = [None] * world
+        dist.all_gather_object(events, ex.dump_account_events())
         if rank == 0:
             assert all(len(d[1]) for d in dumps), "every shard holds transfers"
-            assert_same_state(dumps, ref)
+            assert_same_state(dumps, ref, events)
         # A refused call fails on every rank and leaves the group usable.
         chain = _transfers([
             dict(id=10**9, debit_account_id=1, credit_account_id=5, amount=1, ledger=1, code=1,
@@ -458,12 +477,14 @@ def test_shard_group_gloo_world2(pbm):
 @pytest.mark.gpu
 def test_local_shards_gpu():
     """Two HBM executors on cuda:0 behind the router, against the unsharded oracle."""
-    shards = [shard.GpuShard(1 << 10, 1 << 14, batch_events_max=4096) for _ in range(2)]
+    shards = [shard.GpuShard(1 << 10, 1 << 14, batch_events_max=4096,
+                             account_events_capacity=1 << 15) for _ in range(2)]
     ref = OracleShard()
     try:
         cluster = shard.LocalShards(shard.LedgerRouter(2, ledgers=LEDGERS), shards, PBM)
         assert drive(cluster, ref, scenario(11)) > 0
-        assert_same_state([s.dump() for s in shards], ref)
+        assert_same_state([s.dump() for s in shards], ref,
+                          [s.dump_account_events() for s in shards])
     finally:
         for s in shards:
             s.close()
@@ -475,15 +496,16 @@ def test_local_shards_gpu_pulse_cut():
     """Two HBM executors with pulse_batch_max 6: the global pulse cut through tbg_pulse_candidates
     / tbg_pulse_cut, against the unsharded oracle."""
     pbm = 6
-    shards = [shard.GpuShard(1 << 10, 1 << 14, batch_events_max=4096, pulse_batch_max=pbm)
-              for _ in range(2)]
+    shards = [shard.GpuShard(1 << 10, 1 << 14, batch_events_max=4096, pulse_batch_max=pbm,
+                             account_events_capacity=1 << 15) for _ in range(2)]
     ref = OracleShard(pbm)
     try:
         cluster = shard.LocalShards(shard.LedgerRouter(2, ledgers=LEDGERS), shards, pbm)
         cuts = []
         assert drive(cluster, ref, scenario(12, calls=10), pbm=pbm, cuts=cuts) > 0
         assert cuts
-        assert_same_state([s.dump() for s in shards], ref)
+        assert_same_state([s.dump() for s in shards], ref,
+                          [s.dump_account_events() for s in shards])
     finally:
         for s in shards:
             s.close()

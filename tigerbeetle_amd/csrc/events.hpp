@@ -193,9 +193,10 @@ ae_collect_transfers(Tables T, Call<tb_transfer_t> c, const uint32_t* list,
 }
 
 // Expiries of a pulse (execute_expire_pending_transfers :4540-4626): rows[i] in expiry order,
-// event i stamped timestamp - m + i + 1.
+// event i stamped timestamp - m + i + 1 -- or stamps[i], a shard's expiries stamped by their
+// positions in the pulse's expiry order across all shards.
 __device__ inline void ae_expiry_one(Tables T, uint64_t row, uint32_t m, uint32_t i,
-                                     uint64_t timestamp, const AeScratch& S,
+                                     uint64_t timestamp, const uint64_t* stamps, const AeScratch& S,
                                      tb_account_event_t* log, AeRef* refs, uint32_t* dr_out,
                                      uint32_t* cr_out) {
     const tb_transfer_t& p = T.tr_rows[row];
@@ -204,7 +205,7 @@ __device__ inline void ae_expiry_one(Tables T, uint64_t row, uint32_t m, uint32_
     const u128 d_pending = u128(0) - U(p.amount);
     ae_side(S, i, 0, d_pending, 0, (p.flags & TB_TRANSFER_CLOSING_DEBIT) != 0);
     ae_side(S, i, 1, d_pending, 0, (p.flags & TB_TRANSFER_CLOSING_CREDIT) != 0);
-    ae_event_fields(&log[i], timestamp - m + i + 1, 0, TB_PENDING_EXPIRED, &p,
+    ae_event_fields(&log[i], stamps ? stamps[i] : timestamp - m + i + 1, 0, TB_PENDING_EXPIRED, &p,
                     tb_uint128_t{0, 0}, p.amount, p.ledger);
     refs[i] = AeRef{uint32_t(row), uint32_t(dr), uint32_t(cr), 0};
     *dr_out = uint32_t(dr);
@@ -212,8 +213,8 @@ __device__ inline void ae_expiry_one(Tables T, uint64_t row, uint32_t m, uint32_
 }
 
 __global__ void __launch_bounds__(kPlanThreads)
-ae_collect_expiry(Tables T, const uint64_t* rows, uint32_t m, uint64_t timestamp, AeScratch S,
-                  tb_account_event_t* log, AeRef* refs) {
+ae_collect_expiry(Tables T, const uint64_t* rows, uint32_t m, uint64_t timestamp,
+                  const uint64_t* stamps, AeScratch S, tb_account_event_t* log, AeRef* refs) {
     __shared__ GroupBlock B;
     group_block_init(B);
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -221,7 +222,7 @@ ae_collect_expiry(Tables T, const uint64_t* rows, uint32_t m, uint64_t timestamp
     log += S.state[0];
     refs += S.state[0];
     uint32_t dr_row = 0, cr_row = 0;
-    if (i < m) ae_expiry_one(T, rows[i], m, i, timestamp, S, log, refs, &dr_row, &cr_row);
+    if (i < m) ae_expiry_one(T, rows[i], m, i, timestamp, stamps, S, log, refs, &dr_row, &cr_row);
     ae_group_touches(S, B, i, i < m, dr_row, cr_row, m);
 }
 

@@ -89,6 +89,15 @@ struct tbg_ctx {
     DevScalars* h_scalars = nullptr;  // pinned
     tb_create_result_t* h_results = nullptr;  // pinned: host-buffer calls' results land here first
     hipEvent_t results_ready = nullptr;
+    // pinned staging of a host-buffer call's batch ends and timestamps (batch_count_max each)
+    uint32_t* h_batch_ends = nullptr;
+    uint64_t* h_batch_ts = nullptr;
+    // Host ranges the caller registered (tbg_register_host): DMA straight from / to them.
+    std::vector<std::pair<uintptr_t, uint64_t>> registered;
+    // A host-buffer create_transfers call queues its results' download before its one host
+    // synchronisation (create_transfers_impl); valid when the call needed no replay.
+    tb_create_result_t* early_dst = nullptr;
+    bool early_done = false;
     uint32_t epoch = 0;
     bool force_replay = false;
     bool serial_replay = false;  // debug: every replay on one lane (replay_kernel)
@@ -156,7 +165,6 @@ struct tbg_ctx {
     uint32_t* ae_list = nullptr;
     unsigned long long* ae_words = nullptr;  // bounds / counts
     unsigned long long* flow_debug = nullptr;
-    std::vector<uint32_t> h_ends;
 
     // Per-kernel timing (tbg_profile): HIP events recorded on the call's stream between launches.
     bool timing = false;
@@ -941,12 +949,13 @@ int ae_transfers(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
 }
 
 // AccountEvents of a pulse: the expired rows in expiry order.
-int ae_expiry(tbg_ctx* ctx, const uint64_t* rows, uint64_t m, uint64_t timestamp) {
+int ae_expiry(tbg_ctx* ctx, const uint64_t* rows, uint64_t m, uint64_t timestamp,
+              const uint64_t* d_stamps = nullptr) {
     return ae_append(ctx, uint32_t(m), nullptr, [&](const AeScratch& S, tb_account_event_t* log,
                                                     AeRef* refs) {
         hipLaunchKernelGGL(ae_collect_expiry, dim3((uint32_t(m) + kPlanThreads - 1) / kPlanThreads),
                            dim3(kPlanThreads), 0, ctx->stream, ctx->T, rows, uint32_t(m), timestamp,
-                           S, log, refs);
+                           d_stamps, S, log, refs);
     }, "pulse:account_events");
 }
 
@@ -997,19 +1006,27 @@ int ae_sort_log(tbg_ctx* ctx) {
     return ae_publish(ctx);
 }
 
+bool is_registered(const tbg_ctx* ctx, const void* p, uint64_t bytes) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    for (const auto& r : ctx->registered)
+        if (a >= r.first && a + bytes <= r.first + r.second) return true;
+    return false;
+}
+
 int upload_batches(tbg_ctx* ctx, uint32_t n, const uint32_t* batch_lens, const uint64_t* batch_ts,
                    uint32_t nb) {
     if (nb == 0 || nb > ctx->opt.batch_count_max) return TBG_EINVAL;
-    ctx->h_ends.resize(nb);
+    // (the pinned staging is free: the previous call's copies completed before it returned)
     uint64_t total = 0;
     for (uint32_t b = 0; b < nb; b++) {
         total += batch_lens[b];
-        ctx->h_ends[b] = uint32_t(total);
+        ctx->h_batch_ends[b] = uint32_t(total);
+        ctx->h_batch_ts[b] = batch_ts[b];
     }
     if (total != n) return TBG_EINVAL;
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->d_batch_ends, ctx->h_ends.data(), nb * 4,
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->d_batch_ends, ctx->h_batch_ends, nb * 4,
                                 hipMemcpyHostToDevice, ctx->stream));
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->d_batch_ts, batch_ts, nb * 8, hipMemcpyHostToDevice,
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->d_batch_ts, ctx->h_batch_ts, nb * 8, hipMemcpyHostToDevice,
                                 ctx->stream));
     return 0;
 }
@@ -1133,6 +1150,10 @@ tbg_ctx* tbg_open(const tbg_options* options) {
                                          sizeof(DevScalars)), "hipHostMalloc");
     ok = ok && hip_ok(ctx, hipEventCreateWithFlags(&ctx->results_ready, hipEventDisableTiming),
                       "hipEventCreate");
+    ok = ok && hip_ok(ctx, hipHostMalloc(reinterpret_cast<void**>(&ctx->h_batch_ends),
+                                         size_t(options->batch_count_max) * 4), "hipHostMalloc") &&
+         hip_ok(ctx, hipHostMalloc(reinterpret_cast<void**>(&ctx->h_batch_ts),
+                                   size_t(options->batch_count_max) * 8), "hipHostMalloc");
     ok = ok && hip_ok(ctx, hipHostMalloc(reinterpret_cast<void**>(&ctx->h_results),
                                          size_t(std::max<uint64_t>(ev_max, 1)) *
                                              sizeof(tb_create_result_t)),
@@ -1187,6 +1208,9 @@ void tbg_close(tbg_ctx* ctx) {
         if (e) (void)hipEventDestroy(e);
     if (ctx->h_scalars) (void)hipHostFree(ctx->h_scalars);
     if (ctx->h_results) (void)hipHostFree(ctx->h_results);
+    if (ctx->h_batch_ends) (void)hipHostFree(ctx->h_batch_ends);
+    if (ctx->h_batch_ts) (void)hipHostFree(ctx->h_batch_ts);
+    for (const auto& r : ctx->registered) (void)hipHostUnregister(reinterpret_cast<void*>(r.first));
     if (ctx->results_ready) (void)hipEventDestroy(ctx->results_ready);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -1328,6 +1352,14 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
             rc = hip_ok(ctx, hipGetLastError(), "launch") ? 0 : TBG_EHIP;
         }
     }
+    // A host-buffer call's results are queued for download here, so that one host
+    // synchronisation covers them when the call needs no replay (else they are downloaded again).
+    if (!rc && ctx->early_dst) {
+        tb_create_result_t* dst = is_registered(ctx, ctx->early_dst, uint64_t(n) * 16)
+                                      ? ctx->early_dst : ctx->h_results;
+        rc = hip_ok(ctx, hipMemcpyAsync(dst, d_results, size_t(n) * 16, hipMemcpyDeviceToHost,
+                                        ctx->stream), "results copy") ? 0 : TBG_EHIP;
+    }
     // One host synchronisation: does the call need the ordered replay (and, with imported events,
     // the accounts' timestamp index)?
     if (!rc) {
@@ -1335,6 +1367,7 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
         tmark(ctx, "host_sync");
     }
     const bool replay = !rc && ctx->h_scalars->stats[0] > 0;
+    ctx->early_done = !rc && ctx->early_dst && !replay;  // (only the replay rewrites results)
     if (replay && (ctx->h_scalars->flags & kFlagImported)) rc = check_imported_indexes(ctx, true);
     if (replay && !rc) rc = run_replay(ctx, c, true, false);
     if (!rc && (ctx->h_scalars->flags & kFlagPostVoid)) rc = pnt_resolve(ctx, c);
@@ -1353,14 +1386,18 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
     return rc;
 }
 
-// Results of a host-buffer call: DMA into the pinned staging rows, then one host copy (a pageable
-// destination would take the driver's slower staged path). A create_transfers call's deferred
-// AccountEvents are launched behind the copy: the host waits for the results only, and the next
-// call's work queues behind the appends on the same stream.
-int download_results(tbg_ctx* ctx, tb_create_result_t* results, uint32_t n) {
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->h_results, ctx->d_results, size_t(n) * 16,
-                                hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(ctx, hipEventRecord(ctx->results_ready, ctx->stream));
+// Results of a host-buffer call: DMA straight into a registered destination, else into the
+// pinned staging rows and one host copy (a pageable destination would take the driver's slower
+// staged path). A create_transfers call's deferred AccountEvents are launched behind the copy:
+// the host waits for the results only, and the next call's work queues behind the appends on the
+// same stream. `early`: the results were already downloaded before the call's synchronisation.
+int download_results(tbg_ctx* ctx, tb_create_result_t* results, uint32_t n, bool early = false) {
+    const bool direct = is_registered(ctx, results, uint64_t(n) * 16);
+    if (!early) {
+        HIP_TRY(ctx, hipMemcpyAsync(direct ? results : ctx->h_results, ctx->d_results,
+                                    size_t(n) * 16, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(ctx, hipEventRecord(ctx->results_ready, ctx->stream));
+    }
     int rc = 0;
     if (ctx->ae_deferred) {
         ctx->ae_deferred = false;
@@ -1368,8 +1405,8 @@ int download_results(tbg_ctx* ctx, tb_create_result_t* results, uint32_t n) {
         rc = ae_transfers(ctx, ctx->ae_call);
         hprof(ctx, "host:account_events", now_ms() - ta);
     }
-    HIP_TRY(ctx, hipEventSynchronize(ctx->results_ready));
-    std::memcpy(results, ctx->h_results, size_t(n) * 16);
+    if (!early) HIP_TRY(ctx, hipEventSynchronize(ctx->results_ready));
+    if (!direct) std::memcpy(results, ctx->h_results, size_t(n) * 16);
     return rc;
 }
 
@@ -1460,16 +1497,18 @@ int tbg_create_transfers(tbg_ctx* ctx, const tb_transfer_t* events, uint32_t n,
                                 ctx->stream));
     const double t1 = ctx->timing_host ? now_ms() : 0;
     ctx->ae_defer = true;
+    ctx->early_dst = results;
     rc = tbg_create_transfers_device(ctx, reinterpret_cast<const tb_transfer_t*>(ctx->d_events), n,
                                      ctx->d_batch_ends, ctx->d_batch_ts, nb, ctx->d_results,
                                      nullptr);
     ctx->ae_defer = false;
+    ctx->early_dst = nullptr;
     if (rc) {
         ctx->ae_deferred = false;
         return rc;
     }
     const double t2 = ctx->timing_host ? now_ms() : 0;
-    rc = download_results(ctx, results, n);
+    rc = download_results(ctx, results, n, ctx->early_done);
     if (rc) return rc;
     if (ctx->timing_host) {
         hprof(ctx, "host:upload", t1 - t0);
@@ -1586,6 +1625,32 @@ int pulse_keys(tbg_ctx* ctx, uint64_t n, std::vector<uint64_t>* exp, std::vector
 
 extern "C" {
 
+int tbg_register_host(tbg_ctx* ctx, void* ptr, uint64_t size) {
+    if (!ctx || !ptr || size == 0) return TBG_EINVAL;
+    if (is_registered(ctx, ptr, size)) return 0;
+    HIP_TRY(ctx, hipHostRegister(ptr, size, hipHostRegisterDefault));
+    ctx->registered.emplace_back(reinterpret_cast<uintptr_t>(ptr), size);
+    return 0;
+}
+
+int tbg_unregister_host(tbg_ctx* ctx, void* ptr) {
+    if (!ctx) return TBG_EINVAL;
+    for (size_t i = 0; i < ctx->registered.size(); i++) {
+        if (ctx->registered[i].first != reinterpret_cast<uintptr_t>(ptr)) continue;
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        HIP_TRY(ctx, hipHostUnregister(ptr));
+        ctx->registered.erase(ctx->registered.begin() + long(i));
+        return 0;
+    }
+    return TBG_EINVAL;
+}
+
+int tbg_synchronize(tbg_ctx* ctx) {
+    if (!ctx) return TBG_EINVAL;
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return 0;
+}
+
 int64_t tbg_pulse(tbg_ctx* ctx, uint64_t timestamp) {
     if (!ctx) return TBG_EINVAL;
     PulseGather G;
@@ -1628,7 +1693,8 @@ int64_t tbg_pulse_candidates(tbg_ctx* ctx, uint64_t timestamp, uint64_t* expires
 }
 
 int64_t tbg_pulse_cut(tbg_ctx* ctx, uint64_t timestamp, uint64_t cut_expires_at,
-                      uint64_t cut_timestamp, uint64_t pulse_next_timestamp) {
+                      uint64_t cut_timestamp, uint64_t pulse_next_timestamp,
+                      const uint64_t* event_timestamps) {
     if (!ctx) return TBG_EINVAL;
     PulseGather G;
     int rc = pulse_gather(ctx, timestamp, true, &G);
@@ -1641,8 +1707,22 @@ int64_t tbg_pulse_cut(tbg_ctx* ctx, uint64_t timestamp, uint64_t cut_expires_at,
     while (expired < e.size() && (e[expired] < cut_expires_at ||
                                   (e[expired] == cut_expires_at && t[expired] <= cut_timestamp)))
         expired++;
-    rc = pulse_finish(ctx, expired, G.kept, pulse_next_timestamp);
-    if (!rc && ctx->ae_log) rc = ae_expiry(ctx, ctx->pulse.rows, expired, timestamp);
+    // 0: this shard's own next expiry (every candidate at or before the cut expires), as tbg_pulse.
+    uint64_t pulse_next = pulse_next_timestamp;
+    if (pulse_next == 0) {
+        pulse_next = G.next_unexpired == ~0ull ? TB_TIMESTAMP_MAX : G.next_unexpired;
+        if (expired < e.size()) pulse_next = std::min(pulse_next, e[expired]);
+    }
+    // The AccountEvents' stamps: the expiries' positions across all shards.
+    uint64_t* d_stamps = nullptr;
+    if (event_timestamps && expired && ctx->ae_log) {
+        d_stamps = ctx->pulse.exp_b;  // (free after pulse_gather's sort)
+        HIP_TRY(ctx, hipMemcpyAsync(d_stamps, event_timestamps, expired * 8, hipMemcpyHostToDevice,
+                                    ctx->stream));
+    }
+    rc = pulse_finish(ctx, expired, G.kept, pulse_next);
+    if (!rc && ctx->ae_log) rc = ae_expiry(ctx, ctx->pulse.rows, expired, timestamp, d_stamps);
+    if (!rc && d_stamps) HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // (host stamps)
     return rc ? rc : int64_t(expired);
 }
 

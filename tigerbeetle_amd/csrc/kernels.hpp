@@ -443,6 +443,32 @@ __device__ inline void ingest_store_result(tb_create_result_t* p, const tb_creat
 #endif
 }
 
+// Balance-delta item: key = account_row * 4 + field (0 dp, 1 dpo, 2 cp, 3 cpo).
+__device__ inline tb_uint128_t* account_field(tb_account_t* rows, uint32_t key) {
+    tb_account_t* a = &rows[key >> 2];
+    return reinterpret_cast<tb_uint128_t*>(reinterpret_cast<uint8_t*>(a) + 16 + 16 * (key & 3));
+}
+
+// A FAST event's balance deltas as u128 atomics on its two rows (`undo`: subtracted again, for a
+// demoted event of a call without balance items, whose deltas ingest applied). An add that
+// takes a balance's high word to >= 2^62 raises the account's kHazardHigh bit; a subtraction
+// leaves the bits (they are a conservative, set-only summary).
+__device__ inline void apply_fast_deltas(const Tables& T, uint32_t dr, uint32_t cr, bool pending,
+                                         uint64_t amount, bool undo) {
+    if (!amount) return;
+    tb_uint128_t* fd = account_field(T.acc_rows, dr * 4 + (pending ? 0 : 1));
+    tb_uint128_t* fc = account_field(T.acc_rows, cr * 4 + (pending ? 2 : 3));
+    if (undo) {
+        atomic_sub_u128(fd, amount);
+        atomic_sub_u128(fc, amount);
+        return;
+    }
+    if (atomic_add_u128(fd, amount) >= kHazardHiLimit)
+        acc_hazard_set(T.acc_index, T.acc_entry_of, dr, kHazardHigh);
+    if (atomic_add_u128(fc, amount) >= kHazardHiLimit)
+        acc_hazard_set(T.acc_index, T.acc_entry_of, cr, kHazardHigh);
+}
+
 // One event of tr_ingest, `t` being the event as staged in LDS; returns the call flags it raises
 // (kFlag*). The row store is done by the caller (the whole wave's rows at once, coalesced).
 //
@@ -663,7 +689,11 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
                 need_commit = true;
             }
         } else {
-            need_commit = true;  // unsorted calls: u128 atomics in tr_commit
+            // Calls without balance items (below kSortThreshold events): the deltas go to the
+            // rows now, with u128 atomics (they commute with every other FAST delta, and nothing
+            // reads a balance before tr_commit); a FAST event tr_commit demotes subtracts them
+            // again (commit_event). A clean call then needs no tr_commit pass at all.
+            apply_fast_deltas(T, dr.row, cr.row, pending, amount, false);
         }
         *fast_ts = ts_event;
     } else {
@@ -895,11 +925,6 @@ __global__ void __launch_bounds__(kBlock, TBG_INGEST_WG_PER_CU) tr_ingest(Tables
     }
 }
 
-// Balance-delta item: key = account_row * 4 + field (0 dp, 1 dpo, 2 cp, 3 cpo).
-__device__ inline tb_uint128_t* account_field(tb_account_t* rows, uint32_t key) {
-    tb_account_t* a = &rows[key >> 2];
-    return reinterpret_cast<tb_uint128_t*>(reinterpret_cast<uint8_t*>(a) + 16 + 16 * (key & 3));
-}
 
 // A FAST event's record as tr_commit reads it: its id slot (kNone32 unless re-probed or recorded),
 // account rows and amount.
@@ -1083,9 +1108,12 @@ __device__ inline void commit_event(const Tables& T, const Call<tb_transfer_t>& 
               k != batch_start_of(c, batch_of_guess(c.batch_ends, c.n_batches, c.n, k))));
         if (slow || fast_demoted(T, c, k, call_flags, fr) ||
             (in_chain && chain_demoted(T, c, k, call_flags))) {
-            // Demoted: undo the speculative liveness and balance items; the replay decides.
+            // Demoted: undo the speculative liveness and balance items (or, in a call without
+            // items, the deltas ingest applied); the replay decides.
             slow = true;
             T.tr_live[row] = 0;
+            if (!c.bal_items && !fr.post_void)
+                apply_fast_deltas(T, dr, cr, (info & kInfoPending) != 0, amount, true);
             if (c.bal_items && c.pair_shift) {
                 c.bal_items[k] = ~0ull;
             } else if (c.bal_items) {
@@ -1106,14 +1134,9 @@ __device__ inline void commit_event(const Tables& T, const Call<tb_transfer_t>& 
             applied = true;
             ts_applied = c.results[k].timestamp;
             const bool pending = (info & kInfoPending) != 0;
-            if (amount && (!c.bal_items || !item_packable(c, amount))) {
-                if (atomic_add_u128(account_field(T.acc_rows, dr * 4 + (pending ? 0 : 1)),
-                                    amount) >= kHazardHiLimit)
-                    acc_hazard_set(T.acc_index, T.acc_entry_of, dr, kHazardHigh);
-                if (atomic_add_u128(account_field(T.acc_rows, cr * 4 + (pending ? 2 : 3)),
-                                    amount) >= kHazardHiLimit)
-                    acc_hazard_set(T.acc_index, T.acc_entry_of, cr, kHazardHigh);
-            }
+            // (a call without balance items: ingest applied the deltas)
+            if (c.bal_items && !item_packable(c, amount))
+                apply_fast_deltas(T, dr, cr, pending, amount, false);
             if (pending && (info & kInfoTimeout)) {
                 expiry_append(T, row, false);
                 const uint64_t expires_at = ts_applied + T.tr_rows[row].timeout * TB_NS_PER_S;

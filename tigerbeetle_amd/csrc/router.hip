@@ -6,9 +6,11 @@
 // transfer rows, and its slot claim is released at settle unless the id now exists on its shard.
 //
 // Fast path, per call of n events (one workgroup per 256 consecutive events, so the scatter is
-// stable): tbr_pass1 -- the hazard checks, both account lookups, the id claim, per-block counts
-// per shard; the host turns the counts into per-block offsets (shard-major exclusive sums);
-// tbr_pass2 -- each event copied to its slice with its global commit timestamp and its position.
+// stable): tbr_pass1 -- the hazard checks, the id claim, the shard pinned by the id's holder or
+// both accounts; tbr_pass_pv -- a post/void's shard from its pending transfer; tbr_pass_chains --
+// linked chains whole on one shard, per-block counts per shard; the host turns the counts into
+// per-block offsets (shard-major exclusive sums); tbr_pass2 -- each event copied to its slice with
+// its global commit timestamp and its position.
 
 #include <hip/hip_runtime.h>
 
@@ -73,30 +75,34 @@ __global__ void tbr_lookup(Dir d, const tb_uint128_t* q, uint32_t n, int32_t* ou
     out[i] = r == kNone ? -1 : int32_t(d.shard[r]);
 }
 
+// ev_shard codes besides a shard: the event is a hazard (the call goes to the host router), or a
+// post/void whose shard follows its pending transfer (resolved by tbr_pass_pv).
+constexpr uint8_t kShardHazard = 0xFF;
+constexpr uint8_t kShardPending = 0xFE;
+
+__device__ inline void raise_hazard(const RouteArgs& a, bool hazard) {
+    if (__any(hazard) && (threadIdx.x & 63) == 0) atomicOr(&a.flags[0], 1u);
+}
+
+// Pass 1, per event: the static hazards, the id claim, and the shard the event's own fields pin:
+// the holder's for an id that already exists (create_transfer_exists runs before any account
+// lookup, :3733-3760, so the holder decides it), the accounts' for a single-phase or pending
+// event (both known, on one shard), none yet for a post/void (its pending transfer's, pass 2).
 __global__ void __launch_bounds__(kRouteBlock) tbr_pass1(RouteArgs a) {
-    __shared__ unsigned int cnt[kShardsMax];
-    for (uint32_t s = threadIdx.x; s < a.shards; s += kRouteBlock) cnt[s] = 0;
-    __syncthreads();
     const uint32_t k = blockIdx.x * kRouteBlock + threadIdx.x;
     bool hazard = false;
     if (k < a.n) {
         const tb_transfer_t& t = a.events[k];
         const uint16_t f = t.flags;
-        uint8_t shard = 0xFF;
+        const bool post_void = (f & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) != 0;
+        uint8_t shard = kShardHazard;
         uint32_t slot = kNone32;
-        hazard = (f & (TB_TRANSFER_LINKED | TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING |
-                       TB_TRANSFER_IMPORTED | TB_TRANSFER_PADDING_MASK)) != 0 ||
+        hazard = (f & (TB_TRANSFER_IMPORTED | TB_TRANSFER_PADDING_MASK)) != 0 ||
                  t.timestamp != 0 || u128_is_zero(t.id) || u128_is_max(t.id);
         uint64_t sd = kNone;
         if (!hazard) {
-            const uint64_t rd = dir_find(a.acc, t.debit_account_id);
-            const uint64_t rc = dir_find(a.acc, t.credit_account_id);
-            hazard = rd == kNone || rc == kNone || a.acc.shard[rd] != a.acc.shard[rc];
-            if (!hazard) sd = a.acc.shard[rd];
-        }
-        if (!hazard) {
             // The id: new to every shard and unique in the call (the serial order's first
-            // occurrence keeps the slot; any repeat is a hazard).
+            // occurrence keeps the slot; an in-call repeat is a hazard), or held by one shard.
             const tb_transfer_t* ev = a.events;
             const tb_uint128_t* ids = a.tr.ids;
             const uint64_t base = a.base;
@@ -110,18 +116,104 @@ __global__ void __launch_bounds__(kRouteBlock) tbr_pass1(RouteArgs a) {
             } else {
                 slot = uint32_t(s);
                 const uint64_t owner = (a.tr.slots.slots[s] & kRefMask) - 1;
-                hazard = dup || owner != base + k;
-                shard = uint8_t(sd);
+                if (owner < base) {
+                    shard = uint8_t(a.tr.shard[owner] & 0x7Fu);  // exists: decided on its holder
+                    hazard = dup;
+                } else {
+                    hazard = dup || owner != base + k;
+                }
             }
         }
-        a.ev_shard[k] = hazard ? 0xFF : shard;
+        if (!hazard && shard == kShardHazard) {
+            if (post_void) {
+                shard = kShardPending;
+            } else {
+                const uint64_t rd = dir_find(a.acc, t.debit_account_id);
+                const uint64_t rc = dir_find(a.acc, t.credit_account_id);
+                hazard = rd == kNone || rc == kNone || a.acc.shard[rd] != a.acc.shard[rc];
+                if (!hazard) shard = a.acc.shard[rd];
+            }
+        }
+        if (!hazard && shard != kShardPending) sd = shard;
+        a.ev_shard[k] = hazard ? kShardHazard : shard;
         a.ev_slot[k] = slot;
         a.tr.ids[a.base + k] = t.id;
         const bool timed = (f & TB_TRANSFER_PENDING) && t.timeout > 0;
         a.tr.shard[a.base + k] = uint8_t(sd == kNone ? 0 : sd) | (timed ? TBR_TIMED : 0);
-        if (!hazard) atomicAdd(&cnt[shard], 1u);
     }
-    if (__any(hazard) && (threadIdx.x & 63) == 0) atomicOr(&a.flags[0], 1u);
+    raise_hazard(a, hazard);
+}
+
+// Pass 2, per post/void: the shard of its pending transfer -- the directory's holder, or the
+// in-call event that creates it (post_or_void_pending_transfer reads only the pending transfer,
+// its TransferPending status and its accounts, all on that shard, :4053-4299). A pending
+// transfer with a timeout is a hazard: its post/void resets pulse_next_timestamp on equality with
+// the global value (:4227-4229), which no shard holds; so is a pending id found nowhere (no
+// shard is pinned) or created in the call by another post/void.
+__global__ void __launch_bounds__(kRouteBlock) tbr_pass_pv(RouteArgs a) {
+    const uint32_t k = blockIdx.x * kRouteBlock + threadIdx.x;
+    bool hazard = false;
+    if (k < a.n && a.ev_shard[k] == kShardPending) {
+        const tb_transfer_t& t = a.events[k];
+        const tb_transfer_t* ev = a.events;
+        const tb_uint128_t* ids = a.tr.ids;
+        const uint64_t base = a.base;
+        const uint64_t s = probe_find(a.tr.slots, t.pending_id, [=](uint64_t r) {
+            return r >= base ? ev[r - base].id : ids[r];
+        });
+        uint8_t shard = kShardHazard;
+        if (s != kNone) {
+            const uint64_t r = (a.tr.slots.slots[s] & kRefMask) - 1;
+            if (r < base) {
+                const uint8_t v = a.tr.shard[r];
+                if (!(v & TBR_TIMED)) shard = v & 0x7Fu;
+            } else {
+                const tb_transfer_t& p = ev[r - base];
+                const bool p_pv = (p.flags & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) != 0;
+                const bool p_timed = (p.flags & TB_TRANSFER_PENDING) && p.timeout > 0;
+                const uint8_t ps = a.ev_shard[r - base];
+                if (!p_pv && !p_timed && ps < kShardPending) shard = ps;
+            }
+        }
+        hazard = shard == kShardHazard;
+        a.ev_shard[k] = shard;
+        if (!hazard) a.tr.shard[a.base + k] = shard;
+    }
+    raise_hazard(a, hazard);
+}
+
+// Pass 3, per event: linked chains (:3002-3213) are atomic, so a chain goes to a shard whole --
+// every event pinned to the same shard -- and a chain left open at its batch's end (the slice
+// is one batch on its shard) is a hazard. The chain's first event checks it. Then the per-block
+// counts per shard of the scatter.
+__global__ void __launch_bounds__(kRouteBlock) tbr_pass_chains(RouteArgs a) {
+    __shared__ unsigned int cnt[kShardsMax];
+    for (uint32_t s = threadIdx.x; s < a.shards; s += kRouteBlock) cnt[s] = 0;
+    __syncthreads();
+    const uint32_t k = blockIdx.x * kRouteBlock + threadIdx.x;
+    bool hazard = false;
+    if (k < a.n) {
+        const uint8_t sh = a.ev_shard[k];
+        hazard = sh >= kShardPending;
+        const bool linked = (a.events[k].flags & TB_TRANSFER_LINKED) != 0;
+        if (linked && !hazard) {
+            const uint32_t b = batch_of_guess(a.batch_ends, a.n_batches, a.n, k);
+            const uint32_t bstart = b ? a.batch_ends[b - 1] : 0, bend = a.batch_ends[b];
+            const bool head = k == bstart || !(a.events[k - 1].flags & TB_TRANSFER_LINKED);
+            if (head) {
+                uint32_t j = k + 1;
+                for (; j < bend; j++) {
+                    if (a.ev_shard[j] != sh) break;
+                    if (!(a.events[j].flags & TB_TRANSFER_LINKED)) break;
+                }
+                // ended by a non-linked event of the same shard; else another shard's event or
+                // the batch's end (chain open)
+                hazard = j >= bend || a.ev_shard[j] != sh;
+            }
+        }
+        if (!hazard) atomicAdd(&cnt[sh], 1u);
+    }
+    raise_hazard(a, hazard);
     __syncthreads();
     for (uint32_t s = threadIdx.x; s < a.shards; s += kRouteBlock)
         a.block_counts[uint64_t(s) * a.nblocks + blockIdx.x] = cnt[s];
@@ -168,15 +260,20 @@ __global__ void __launch_bounds__(kRouteBlock) tbr_pass2(RouteArgs a, const uint
 
 // Results back to call order; ids that exist now (created, or orphaned by a transient failure)
 // stay in the directory, the others are released.
+// The largest timestamp of a created transfer goes to key_max (the transfers objects tree's
+// key_range.key_max, which imported events on the host path read).
 __global__ void tbr_settle(RouteArgs a, const tb_create_result_t* shard_res, const uint32_t* pos,
-                           tb_create_result_t* results) {
+                           tb_create_result_t* results, unsigned long long* key_max) {
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= a.n) return;
     const uint32_t k = pos[j];
     const tb_create_result_t r = shard_res[j];
     results[k] = r;
     const uint64_t row = a.base + k;
-    if (r.status == TB_STATUS_CREATED) return;
+    if (r.status == TB_STATUS_CREATED) {
+        atomicMax(key_max, (unsigned long long)r.timestamp);
+        return;
+    }
     if (tb_transfer_status_transient(r.status)) {
         a.tr.shard[row] &= uint8_t(~TBR_TIMED);  // an orphan is no pending transfer
         return;
@@ -204,6 +301,7 @@ struct tbr_ctx {
     uint32_t* block_counts = nullptr;
     uint32_t* offsets = nullptr;
     unsigned int* flags = nullptr;
+    unsigned long long* key_max = nullptr;  // settle: created timestamps' maximum
     tb_uint128_t* q_ids = nullptr;  // lookup / record staging (events_max)
     int32_t* q_out = nullptr;
     // the routed call awaiting tbr_settle_device
@@ -303,7 +401,8 @@ tbr_ctx* tbr_open(uint32_t shards, uint64_t account_capacity, uint64_t transfer_
          alloc(&r->ev_slot, events_max, false, r->stream) &&
          alloc(&r->block_counts, uint64_t(shards) * nblocks, false, r->stream) &&
          alloc(&r->offsets, uint64_t(shards) * nblocks, false, r->stream) &&
-         alloc(&r->flags, 2, true, r->stream) && alloc(&r->q_ids, events_max, false, r->stream) &&
+         alloc(&r->flags, 2, true, r->stream) && alloc(&r->key_max, 1, true, r->stream) &&
+         alloc(&r->q_ids, events_max, false, r->stream) &&
          alloc(&r->q_out, events_max, false, r->stream);
     ok = ok && hipStreamSynchronize(r->stream) == hipSuccess;
     if (!ok) {
@@ -321,7 +420,7 @@ void tbr_close(tbr_ctx* r) {
     if (r->stream) (void)hipStreamSynchronize(r->stream);
     void* ptrs[] = {r->acc.slots.slots, r->acc.ids, r->acc.shard, r->tr.slots.slots, r->tr.ids,
                     r->tr.shard, r->ev_shard, r->ev_slot, r->block_counts, r->offsets, r->flags,
-                    r->q_ids, r->q_out};
+                    r->key_max, r->q_ids, r->q_out};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (r->stream) (void)hipStreamDestroy(r->stream);
@@ -358,6 +457,8 @@ int64_t tbr_route_device(tbr_ctx* r, const tb_transfer_t* d_events, uint32_t n,
     const dim3 grid(a.nblocks), block(kRouteBlock);
     if (hipMemsetAsync(r->flags, 0, 8, r->stream)) return -5;
     hipLaunchKernelGGL(tbr_pass1, grid, block, 0, r->stream, a);
+    hipLaunchKernelGGL(tbr_pass_pv, grid, block, 0, r->stream, a);
+    hipLaunchKernelGGL(tbr_pass_chains, grid, block, 0, r->stream, a);
     std::vector<uint32_t> counts(uint64_t(r->shards) * a.nblocks);
     unsigned int f[2] = {0, 0};
     if (hipMemcpyAsync(f, r->flags, 8, hipMemcpyDeviceToHost, r->stream) ||
@@ -394,13 +495,19 @@ int64_t tbr_route_device(tbr_ctx* r, const tb_transfer_t* d_events, uint32_t n,
 }
 
 int tbr_settle_device(tbr_ctx* r, const tb_create_result_t* d_shard_results,
-                      const uint32_t* d_positions, uint32_t n, tb_create_result_t* d_results) {
+                      const uint32_t* d_positions, uint32_t n, tb_create_result_t* d_results,
+                      uint64_t* created_timestamp_max) {
     if (!r || !r->pending || n != r->call_n) return -22;
     RouteArgs a = route_args(r, nullptr, n, nullptr, nullptr, 1);
     a.base = r->call_base;
+    unsigned long long km = 0;
+    if (hipMemsetAsync(r->key_max, 0, 8, r->stream)) return -5;
     hipLaunchKernelGGL(tbr_settle, dim3((n + 255) / 256), dim3(256), 0, r->stream, a,
-                       d_shard_results, d_positions, d_results);
-    if (hipGetLastError() || hipStreamSynchronize(r->stream)) return -5;
+                       d_shard_results, d_positions, d_results, r->key_max);
+    if (hipGetLastError() || hipMemcpyAsync(&km, r->key_max, 8, hipMemcpyDeviceToHost, r->stream) ||
+        hipStreamSynchronize(r->stream))
+        return -5;
+    if (created_timestamp_max) *created_timestamp_max = km;
     r->tr_used = r->call_base + n;
     r->pending = false;
     return 0;

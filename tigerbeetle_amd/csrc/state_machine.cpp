@@ -330,6 +330,11 @@ extern "C" void tb_sm_close(tb_sm* sm) {
 
 extern "C" tbg_ctx* tb_sm_executor_gpu(tb_sm* sm) { return sm ? sm->gpu : nullptr; }
 
+extern "C" int tb_sm_register_buffer(tb_sm* sm, void* ptr, uint64_t size) {
+    if (!sm) return TBG_EINVAL;
+    return sm->gpu ? tbg_register_host(sm->gpu, ptr, size) : 0;
+}
+
 extern "C" uint32_t tb_sm_event_max(const tb_sm* sm, uint8_t operation, uint32_t batch_size_limit) {
     OperationInfo info;
     if (!sm || !operation_info(operation, &info) || info.result_size == 0) return 0;

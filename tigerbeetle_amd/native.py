@@ -90,10 +90,13 @@ SIGNATURES = [
     ("tbg_create_transfers_device", ctypes.c_int, [vp, vp, ctypes.c_uint32, vp, vp,
                                                   ctypes.c_uint32, vp, vp]),
     ("tbg_create_transfers_stamped_device", ctypes.c_int, [vp, vp, ctypes.c_uint32, vp, vp, vp]),
+    ("tbg_register_host", ctypes.c_int, [vp, vp, ctypes.c_uint64]),
+    ("tbg_unregister_host", ctypes.c_int, [vp, vp]),
+    ("tbg_synchronize", ctypes.c_int, [vp]),
     ("tbg_pulse", ctypes.c_int64, [vp, ctypes.c_uint64]),
     ("tbg_pulse_candidates", ctypes.c_int64, [vp, ctypes.c_uint64, vp, vp, ctypes.c_uint32]),
     ("tbg_pulse_cut", ctypes.c_int64, [vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
-                                       ctypes.c_uint64]),
+                                       ctypes.c_uint64, vp]),
     ("tbg_pulse_next_timestamp", ctypes.c_uint64, [vp]),
     ("tbg_raise_key_max", ctypes.c_int, [vp, ctypes.c_uint64, ctypes.c_uint64]),
     ("tbg_lookup_accounts", ctypes.c_int64, [vp, vp, ctypes.c_uint32, vp]),
@@ -126,7 +129,7 @@ SIGNATURES = [
     ("tbr_transfer_shards", ctypes.c_int64, [vp, vp, ctypes.c_uint32, vp]),
     ("tbr_route_device", ctypes.c_int64, [vp, vp, ctypes.c_uint32, vp, vp, ctypes.c_uint32, vp, vp,
                                           vp, vp]),
-    ("tbr_settle_device", ctypes.c_int, [vp, vp, vp, ctypes.c_uint32, vp]),
+    ("tbr_settle_device", ctypes.c_int, [vp, vp, vp, ctypes.c_uint32, vp, c_u64p]),
     ("tb_sm_open", vp, [ctypes.POINTER(SmOptions), ctypes.POINTER(Executor)]),
     ("tb_sm_open_gpu", vp, [ctypes.POINTER(SmOptions), ctypes.POINTER(TbgOptions)]),
     ("tb_sm_open_gpu_checkpoint", vp, [ctypes.POINTER(SmOptions), ctypes.POINTER(TbgOptions),
@@ -135,6 +138,7 @@ SIGNATURES = [
     ("tb_sm_compact", ctypes.c_int, [vp, ctypes.c_uint64]),
     ("tb_sm_checkpoint", ctypes.c_int, [vp, ctypes.c_char_p]),
     ("tb_sm_executor_gpu", vp, [vp]),
+    ("tb_sm_register_buffer", ctypes.c_int, [vp, vp, ctypes.c_uint64]),
     ("tb_sm_input_valid", ctypes.c_int, [vp, ctypes.c_uint8, vp, ctypes.c_uint32]),
     ("tb_sm_event_max", ctypes.c_uint32, [vp, ctypes.c_uint8, ctypes.c_uint32]),
     ("tb_sm_result_max", ctypes.c_uint32, [vp, ctypes.c_uint8, ctypes.c_uint32]),

@@ -9,9 +9,11 @@ backend), every rank executes its slice with tbg_create_transfers_stamped_device
 results come back, and rank 0 puts them in call order (tbr_settle_device, which also records the
 ids that now exist on their shards).
 
-A call the device router cannot place -- any event that could observe another shard's state
-(chains, post/void, imported events, ids that exist or repeat, accounts unknown or on two shards)
--- is executed by the exact host router instead (shard.LedgerRouter over the same directories,
+The device router places single events, resubmitted ids (on their holder), post/voids (on
+their pending transfer's shard) and linked chains that stay on one shard (include/tbr.h). A call
+it cannot place -- any event that could observe another shard's state (imported events, ids that
+repeat within the call, accounts unknown or on two shards, chains across shards, post/voids of
+pending transfers with a timeout) -- is executed by the exact host router instead (shard.LedgerRouter over the same directories,
 through shard.ShardGroup): surrogates for cross-shard transfers, key-range sync for imported
 batches, refusal of the cases no shard can execute alone.
 """
@@ -158,10 +160,14 @@ class RoutedShards:
                 if r is not None:
                     r.wait()
             self.torch.cuda.synchronize(self.dev)
+            key_max = ctypes.c_uint64(0)
             rc = self.lib.tbr_settle_device(self.tbr, self.res.data_ptr(), self.pos.data_ptr(), n,
-                                            d_results)
+                                            d_results, ctypes.byref(key_max))
             if rc != 0:
                 raise RuntimeError(f"tbr_settle_device: {rc}")
+            # The transfers objects tree's key_max over every shard, as the host router's commit
+            # keeps it: a later imported call's must_not_regress checks read it (:3808-3817).
+            self.router.transfers_key_max = max(self.router.transfers_key_max, key_max.value)
         else:
             if mine:
                 self._recv(self.ev[:mine * 128], 0)
@@ -179,6 +185,11 @@ class RoutedShards:
         self.torch.cuda.synchronize(self.dev)
         rc = self.lib.tbg_create_transfers_stamped_device(self.g, ev.data_ptr(), n, ts.data_ptr(),
                                                           res.data_ptr(), None)
+        if rc == 0:
+            # The executor may leave work queued behind the call on its own stream (the
+            # AccountEvents appends read the call's events and results): the next call's receive
+            # into `ev` / `res` runs on torch's stream, so wait for it here.
+            rc = self.lib.tbg_synchronize(self.g)
         if rc != 0:
             raise RuntimeError(f"tbg_create_transfers_stamped_device: {rc} "
                                f"{self.lib.tbg_last_error(self.g)}")

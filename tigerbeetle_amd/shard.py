@@ -61,7 +61,9 @@ the first `pulse_batch_max` of their keys (an all-gather); below `pulse_batch_ma
 shard expires all of its own (and keeps its earliest unexpired expiry, whose minimum over shards
 is the reference's); otherwise the `pulse_batch_max`-th key across shards is the cut: each shard
 expires its entries up to it and sets `pulse_next_timestamp` to the cut's expiry. Timestamps are
-unique, so the cut expires exactly `pulse_batch_max` transfers -- the reference's.
+unique, so the cut expires exactly `pulse_batch_max` transfers -- the reference's. Each expiry is
+stamped with its position in the pulse's order over all shards (`pulse_plan`), as the reference
+stamps it (:4540-4546): its AccountEvent carries that timestamp.
 """
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Set
@@ -476,6 +478,26 @@ def pulse_cut(counts, key_lists, pulse_batch_max: int):
     return keys[pulse_batch_max - 1]
 
 
+def pulse_plan(counts, key_lists, pulse_batch_max: int, timestamp: int):
+    """One sharded pulse (module doc): (cut key, pulse_next_timestamp for tbg_pulse_cut -- the
+    cut's expires_at, or 0 for each shard's own next expiry when fewer than pulse_batch_max
+    expire --, per shard the timestamps of its expiries). The reference stamps expiry i of the
+    pulse's E (in (expires_at, timestamp) order over all shards) timestamp - E + i + 1
+    (execute_expire_pending_transfers :4540-4546); a shard's expiries are a prefix of its keys."""
+    cut = pulse_cut(counts, key_lists, pulse_batch_max)
+    merged = sorted((int(e), int(t), s) for s, ks in enumerate(key_lists) for e, t in ks)
+    if cut is not None:
+        merged = [m for m in merged if (m[0], m[1]) <= cut]
+    E = len(merged)
+    stamps = [[] for _ in key_lists]
+    for i, (_, _, s) in enumerate(merged):
+        stamps[s].append(timestamp - E + i + 1)
+    if cut is None:
+        cut = (merged[-1][0], merged[-1][1]) if merged else (0, 0)
+        return cut, 0, stamps
+    return cut, cut[0], stamps
+
+
 class LocalShards:
     """All shards in one process (one executor each: several HBM table sets on one GPU, or CPU
     executors in tests). `executors[s]` provides create_accounts / create_transfers
@@ -520,10 +542,10 @@ class LocalShards:
 
     def pulse(self, timestamp: int) -> int:
         cands = [ex.pulse_candidates(timestamp, self.pulse_batch_max) for ex in self.executors]
-        cut = pulse_cut([c for c, _ in cands], [k for _, k in cands], self.pulse_batch_max)
-        if cut is None:
-            return sum(int(ex.pulse(timestamp)) for ex in self.executors)
-        return sum(int(ex.pulse_cut(timestamp, cut[0], cut[1], cut[0])) for ex in self.executors)
+        cut, pnt, stamps = pulse_plan([c for c, _ in cands], [k for _, k in cands],
+                                      self.pulse_batch_max, timestamp)
+        return sum(int(ex.pulse_cut(timestamp, cut[0], cut[1], pnt, st))
+                   for ex, st in zip(self.executors, stamps))
 
 
 class ShardGroup:
@@ -681,11 +703,8 @@ class ShardGroup:
         counts = [int(p[0, 0]) for p in parts]
         key_lists = [[(int(e), int(t)) for e, t in p[1:1 + min(c, B)].tolist()]
                      for p, c in zip(parts, counts)]
-        cut = pulse_cut(counts, key_lists, B)
-        if cut is None:
-            local = int(self.executor.pulse(timestamp))
-        else:
-            local = int(self.executor.pulse_cut(timestamp, cut[0], cut[1], cut[0]))
+        cut, pnt, stamps = pulse_plan(counts, key_lists, B, timestamp)
+        local = int(self.executor.pulse_cut(timestamp, cut[0], cut[1], pnt, stamps[self.rank]))
         t = torch.tensor([local], dtype=torch.int64, device=self.device)
         self.dist.all_reduce(t, group=self.group)
         return int(t.item())
@@ -696,7 +715,7 @@ class GpuShard:
 
     def __init__(self, account_capacity, transfer_capacity, batch_events_max=1 << 16,
                  batch_count_max=4096, pulse_batch_max=8190, device=0,
-                 pulse_next_timestamp_init=(1 << 63) - 1):
+                 pulse_next_timestamp_init=(1 << 63) - 1, account_events_capacity=0):
         import ctypes
         from . import native
         self._c = ctypes
@@ -710,6 +729,7 @@ class GpuShard:
         o.pulse_batch_max = pulse_batch_max
         o.device = device
         o.pulse_next_timestamp_init = pulse_next_timestamp_init
+        o.account_events_capacity = account_events_capacity
         self.g = self.lib.tbg_open(ctypes.byref(o))
         if not self.g:
             raise RuntimeError("tbg_open failed")
@@ -764,9 +784,13 @@ class GpuShard:
         k = min(n, max_keys)
         return n, list(zip(e[:k].tolist(), t[:k].tolist()))
 
-    def pulse_cut(self, timestamp, cut_expires_at, cut_timestamp, pulse_next_timestamp):
+    def pulse_cut(self, timestamp, cut_expires_at, cut_timestamp, pulse_next_timestamp,
+                  stamps=None):
+        st = None if stamps is None else np.ascontiguousarray(stamps, dtype=np.uint64)
         n = int(self.lib.tbg_pulse_cut(self.g, timestamp, cut_expires_at, cut_timestamp,
-                                       pulse_next_timestamp))
+                                       pulse_next_timestamp,
+                                       None if st is None or len(st) == 0
+                                       else st.ctypes.data_as(self._c.c_void_p)))
         if n < 0:
             raise RuntimeError(f"libtbg: {n} {self.lib.tbg_last_error(self.g)}")
         return n
@@ -790,3 +814,12 @@ class GpuShard:
         self.lib.tbg_dump_transfers(self.g, t.ctypes.data_as(c.c_void_p),
                                     s.ctypes.data_as(c.c_void_p))
         return a, t, s
+
+    def dump_account_events(self):
+        """This shard's AccountEvents in timestamp order (tbg_dump_account_events)."""
+        from .types import ACCOUNT_EVENT_DTYPE
+        n = self.lib.tbg_dump_account_events(self.g, None)
+        e = np.zeros(max(n, 0), dtype=ACCOUNT_EVENT_DTYPE)
+        if n > 0:
+            self.lib.tbg_dump_account_events(self.g, e.ctypes.data_as(self._c.c_void_p))
+        return e

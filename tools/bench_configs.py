@@ -60,7 +60,7 @@ def line(name, p, n, t_wall, extra):
 def run(config, n, batches):
     t0 = time.perf_counter()
     p = Pair(account_capacity=1 << 14, transfer_capacity=n + (1 << 12),
-             batch_events_max=BATCH * batches, batch_count_max=batches)
+             batch_events_max=max(BATCH * batches, 1 << 14), batch_count_max=batches)
 
     def start():
         p.seconds = {"gpu": 0.0, "oracle": 0.0}
