@@ -154,14 +154,17 @@ int64_t tbg_get_change_events(tbg_ctx* ctx, const tb_change_events_filter_t* fil
  *                           consumed by every event), rebuilds the transfer id index without the
  *                           tombstones of failed claims, keeps row order (= timestamp order).
  *                           Returns the rows freed (>= 0) or an error. Results of later calls are
- *                           unchanged by it.
+ *                           unchanged by it. A failure once rows have begun to move leaves the
+ *                           tables undefined: every later call on the ctx returns TBG_EHIP.
  *   tbg_checkpoint       <- StateMachine.checkpoint (:2937-2958): writes an image of every
  *                           persistent table (accounts, transfers, TransferPending, expires_at,
- *                           AccountEvents, pulse_next_timestamp, key ranges) to `path`, replacing
- *                           it atomically (written to `path`.tmp, then renamed).
+ *                           AccountEvents, pulse_next_timestamp, key ranges) with a checksum of
+ *                           its header and of every section to `path`.tmp, fsyncs it, renames it
+ *                           over `path` and fsyncs the directory (an atomic, durable switch).
  *   tbg_open_checkpoint  <- StateMachine.open (:964-978): opens a ctx with `options` (the same
  *                           capacities as the ctx that wrote the image) and loads the image; NULL
- *                           if the image is unreadable or does not fit. */
+ *                           if the image is unreadable, does not fit, or fails a checksum
+ *                           (nothing of a torn image is installed). */
 int64_t tbg_compact(tbg_ctx* ctx);
 int tbg_checkpoint(tbg_ctx* ctx, const char* path);
 tbg_ctx* tbg_open_checkpoint(const tbg_options* options, const char* path);

@@ -91,3 +91,42 @@ def test_checkpoint_rejects_other_geometry(tmp_path):
     finally:
         p.opt.transfer_capacity = 1 << 12
         p.close()
+
+
+@pytest.mark.parametrize("damage", ["flip_row_byte", "flip_header_byte", "truncate", "no_footer"])
+def test_checkpoint_rejects_torn_or_corrupt_images(damage, tmp_path):
+    """Every section and the header carry a checksum: an image with one flipped byte, a cut-off
+    tail or a missing footer opens nothing (StateMachine.open must not install torn tables);
+    the intact image still opens and matches."""
+    import ctypes
+    import os
+    p = Pair(account_capacity=1 << 10, transfer_capacity=1 << 12, batch_events_max=1024)
+    try:
+        p.create_accounts(workload.accounts(64, seed=1, ledger=1))
+        p.create_transfers(workload.transfers_uniform(500, 64, seed=1, ledger=1))
+        path = tmp_path / "img"
+        assert p.lib.tbg_checkpoint(p.g, str(path).encode()) == 0
+        assert not os.path.exists(str(path) + ".tmp")
+        good = path.read_bytes()
+        g = p.lib.tbg_open_checkpoint(ctypes.byref(p.opt), str(path).encode())
+        assert g
+        p.lib.tbg_close(g)
+        bad = bytearray(good)
+        if damage == "flip_row_byte":
+            bad[len(bad) // 2] ^= 0x40
+        elif damage == "flip_header_byte":
+            bad[40] ^= 0x01
+        elif damage == "truncate":
+            bad = bad[:len(bad) - 1000]
+        else:
+            bad = bad[:len(bad) - 8]
+        path.write_bytes(bytes(bad))
+        assert not p.lib.tbg_open_checkpoint(ctypes.byref(p.opt), str(path).encode())
+        path.write_bytes(good)
+        g = p.lib.tbg_open_checkpoint(ctypes.byref(p.opt), str(path).encode())
+        assert g
+        p.lib.tbg_close(p.g)
+        p.g = g
+        p.compare_state()
+    finally:
+        p.close()

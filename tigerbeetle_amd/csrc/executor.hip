@@ -7,6 +7,9 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <fcntl.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -99,6 +102,9 @@ struct tbg_ctx {
     tb_create_result_t* early_dst = nullptr;
     bool early_done = false;
     uint32_t epoch = 0;
+    // Sticky: a compaction failed after it began moving rows; the tables are undefined and every
+    // later call fails (tbg_compact).
+    bool failed = false;
     bool force_replay = false;
     bool serial_replay = false;  // debug: every replay on one lane (replay_kernel)
     tbg_stats stats{};
@@ -187,6 +193,15 @@ bool hip_ok(tbg_ctx* ctx, hipError_t e, const char* what) {
     ctx->error = buf;
     return false;
 }
+
+// Every call on a ctx whose tables a failed compaction left undefined fails.
+#define FAILED_GUARD(ctx)                                                        \
+    do {                                                                         \
+        if ((ctx)->failed) {                                                     \
+            (ctx)->error = "tables undefined after a failed compaction";        \
+            return TBG_EHIP;                                                     \
+        }                                                                        \
+    } while (0)
 
 #define HIP_TRY(ctx, expr)                                  \
     do {                                                    \
@@ -1033,6 +1048,7 @@ int upload_batches(tbg_ctx* ctx, uint32_t n, const uint32_t* batch_lens, const u
 
 int64_t lookup_impl(tbg_ctx* ctx, const tb_uint128_t* ids, uint32_t n, void* out, bool accounts) {
     if (!ctx) return TBG_EINVAL;
+    FAILED_GUARD(ctx);
     if (n == 0) return 0;
     if (n > ctx->opt.batch_events_max) return TBG_EINVAL;
     // Scratch: ids and output rows in d_events; rows in bal_items; found flags in ev_slow.
@@ -1228,6 +1244,7 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
                           const uint64_t* d_event_ts) {
     if (!ctx || n > ctx->opt.batch_events_max || n_batches > ctx->opt.batch_count_max)
         return TBG_EINVAL;
+    FAILED_GUARD(ctx);
     if (ctx->T.tr_rows_used + n > ctx->opt.transfer_capacity) {
         ctx->error = "transfer capacity exceeded";
         return TBG_ENOSPC;
@@ -1443,6 +1460,7 @@ int tbg_create_accounts_device(tbg_ctx* ctx, const tb_account_t* d_events, uint3
                                uint32_t n_batches, tb_create_result_t* d_results, void* stream) {
     if (!ctx || n > ctx->opt.batch_events_max || n_batches > ctx->opt.batch_count_max)
         return TBG_EINVAL;
+    FAILED_GUARD(ctx);
     if (ctx->T.acc_rows_used + n > ctx->opt.account_capacity) {
         ctx->error = "account capacity exceeded";
         return TBG_ENOSPC;
@@ -1653,6 +1671,7 @@ int tbg_synchronize(tbg_ctx* ctx) {
 
 int64_t tbg_pulse(tbg_ctx* ctx, uint64_t timestamp) {
     if (!ctx) return TBG_EINVAL;
+    FAILED_GUARD(ctx);
     PulseGather G;
     const uint64_t batch_max = ctx->opt.pulse_batch_max;
     // AccountEvents are stamped in expiry order: the candidates must be in index order.
@@ -1928,7 +1947,9 @@ int tbg_profile_read(tbg_ctx* ctx, uint32_t index, char* name, uint32_t name_len
 
 namespace {
 
-// Checkpoint image: a header, then the persistent tables in a fixed order (tbg_checkpoint).
+// Checkpoint image: a header, the persistent tables in a fixed order, then a footer holding a
+// checksum of the header and of every section (tbg_checkpoint); tbg_open_checkpoint installs
+// nothing unless every checksum matches.
 struct CkptHeader {
     char magic[8];
     uint32_t version, epoch;
@@ -1938,11 +1959,46 @@ struct CkptHeader {
     uint32_t ae_sorted, pad;
     DevScalars scalars;
 };
-constexpr char kCkptMagic[8] = {'T', 'B', 'G', 'C', 'K', 'P', 'T', '1'};
-constexpr uint32_t kCkptVersion = 1;
+constexpr char kCkptMagic[8] = {'T', 'B', 'G', 'C', 'K', 'P', 'T', '2'};
+constexpr uint32_t kCkptVersion = 2;
+constexpr uint32_t kCkptSections = 12;
+struct CkptFooter {
+    char magic[8];
+    uint64_t header_checksum;
+    uint64_t section_checksum[kCkptSections];
+};
 constexpr size_t kStageBytes = size_t(64) << 20;
 
-// Device <-> file through one pinned staging buffer.
+// A streaming 64-bit checksum of a byte sequence (8 bytes per step, a multiply-rotate mix; the
+// tail bytes as one short word); the sequence's length is folded in by ck_finish.
+struct Checksum {
+    uint64_t h = 0x243F6A8885A308D3ull, len = 0;
+    void add(const uint8_t* p, size_t n) {
+        size_t i = 0;
+        for (; i + 8 <= n; i += 8) {
+            uint64_t w;
+            memcpy(&w, p + i, 8);
+            h = ((h << 29) | (h >> 35)) ^ w;
+            h *= 0x9E3779B97F4A7C15ull;
+        }
+        if (i < n) {  // (only at a section's end: staged chunks are multiples of 8 bytes)
+            uint64_t w = 0;
+            memcpy(&w, p + i, n - i);
+            h = ((h << 29) | (h >> 35)) ^ w;
+            h *= 0x9E3779B97F4A7C15ull;
+        }
+        len += n;
+    }
+    uint64_t finish() const {
+        uint64_t x = h ^ len;
+        x ^= x >> 33;
+        x *= 0xFF51AFD7ED558CCDull;
+        x ^= x >> 33;
+        return x;
+    }
+};
+
+// Device <-> file through one pinned staging buffer; each section's checksum as it passes.
 struct Stager {
     tbg_ctx* ctx;
     FILE* f;
@@ -1954,31 +2010,54 @@ struct Stager {
     ~Stager() {
         if (host) (void)hipHostFree(host);
     }
-    bool write(const void* dev, uint64_t bytes) {
+    bool write(const void* dev, uint64_t bytes, uint64_t* checksum) {
         const uint8_t* d = static_cast<const uint8_t*>(dev);
+        Checksum ck;
         for (uint64_t off = 0; ok && off < bytes; off += kStageBytes) {
             const size_t n = size_t(std::min<uint64_t>(kStageBytes, bytes - off));
             ok = hip_ok(ctx, hipMemcpyAsync(host, d + off, n, hipMemcpyDeviceToHost, ctx->stream),
                         "checkpoint copy") &&
                  hip_ok(ctx, hipStreamSynchronize(ctx->stream), "checkpoint sync") &&
                  fwrite(host, 1, n, f) == n;
+            if (ok) ck.add(host, n);
             if (!ok && ctx->error.empty()) ctx->error = "checkpoint write";
         }
+        *checksum = ck.finish();
         return ok;
     }
-    bool read(void* dev, uint64_t bytes) {
+    bool read(void* dev, uint64_t bytes, uint64_t* checksum) {
         uint8_t* d = static_cast<uint8_t*>(dev);
+        Checksum ck;
         for (uint64_t off = 0; ok && off < bytes; off += kStageBytes) {
             const size_t n = size_t(std::min<uint64_t>(kStageBytes, bytes - off));
             ok = fread(host, 1, n, f) == n &&
                  hip_ok(ctx, hipMemcpyAsync(d + off, host, n, hipMemcpyHostToDevice, ctx->stream),
-                        "restore copy") &&
-                 hip_ok(ctx, hipStreamSynchronize(ctx->stream), "restore sync");
+                        "restore copy");
+            if (ok) ck.add(host, n);
+            ok = ok && hip_ok(ctx, hipStreamSynchronize(ctx->stream), "restore sync");
             if (!ok && ctx->error.empty()) ctx->error = "checkpoint image truncated";
         }
+        *checksum = ck.finish();
         return ok;
     }
 };
+
+uint64_t header_checksum(const CkptHeader& h) {
+    Checksum ck;
+    ck.add(reinterpret_cast<const uint8_t*>(&h), sizeof(h));
+    return ck.finish();
+}
+
+// fsync of the directory holding `path` (a rename is durable once its directory is).
+bool fsync_parent(const std::string& path) {
+    const size_t slash = path.find_last_of('/');
+    const std::string dir = slash == std::string::npos ? "." : (slash == 0 ? "/" : path.substr(0, slash));
+    const int fd = open(dir.c_str(), O_RDONLY | O_DIRECTORY);
+    if (fd < 0) return false;
+    const bool ok = fsync(fd) == 0;
+    close(fd);
+    return ok;
+}
 
 uint64_t acc_slot_count(const tbg_ctx* ctx) { return ctx->T.acc.mask + 1; }
 uint64_t tr_slot_count(const tbg_ctx* ctx) { return ctx->T.tr.mask + 1; }
@@ -2011,6 +2090,7 @@ extern "C" {
 
 int64_t tbg_compact(tbg_ctx* ctx) {
     if (!ctx) return TBG_EINVAL;
+    FAILED_GUARD(ctx);
     Tables& T = ctx->T;
     const uint64_t used = T.tr_rows_used;
     if (used == 0) return 0;
@@ -2050,6 +2130,8 @@ int64_t tbg_compact(tbg_ctx* ctx) {
                      hip_ok(ctx, hipStreamSynchronize(ctx->stream), "sync")))
             rc = TBG_EHIP;
     }
+    // From the first row move on, a failure leaves the tables undefined (ctx->failed).
+    const bool mutating = !rc;
     // Rows move down in place, one chunk at a time: chunk [a, b)'s kept rows go to
     // [new_row[a], new_row[b]), which ends at or before b and starts after every earlier chunk's.
     for (uint64_t a = 0; !rc && a < used; a += chunk) {
@@ -2130,6 +2212,9 @@ int64_t tbg_compact(tbg_ctx* ctx) {
         T.tr_rows_used = kept;
         ctx->tr_ts_stale = true;
         rc = int64_t(used - kept);
+    } else if (mutating) {
+        ctx->failed = true;
+        ctx->error = "compaction failed after moving rows (" + ctx->error + "): tables undefined";
     }
     for (void* p : {(void*)keep32, (void*)new_row, (void*)sel, (void*)c_rows, (void*)c_live,
                     (void*)c_status, (void*)x_flags, (void*)x_out, (void*)d_words})
@@ -2139,6 +2224,7 @@ int64_t tbg_compact(tbg_ctx* ctx) {
 
 int tbg_checkpoint(tbg_ctx* ctx, const char* path) {
     if (!ctx || !path) return TBG_EINVAL;
+    FAILED_GUARD(ctx);  // (never persist undefined tables)
     HIP_TRY(ctx, hipMemcpyAsync(ctx->h_scalars, ctx->d_scalars, sizeof(DevScalars),
                                 hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
@@ -2167,17 +2253,24 @@ int tbg_checkpoint(tbg_ctx* ctx, const char* path) {
         return TBG_EINVAL;
     }
     bool ok = fwrite(&h, sizeof(h), 1, f) == 1;
+    CkptFooter foot{};
+    memcpy(foot.magic, kCkptMagic, 8);
+    foot.header_checksum = header_checksum(h);
     {
         Stager st(ctx, f);
         ok = ok && st.ok;
-        for (auto& sec : ckpt_sections(ctx, h.acc_rows_used, h.tr_rows_used,
-                                       h.scalars.expiry_count, h.ae_used))
-            ok = ok && st.write(sec.first, sec.second);
+        const auto secs = ckpt_sections(ctx, h.acc_rows_used, h.tr_rows_used,
+                                        h.scalars.expiry_count, h.ae_used);
+        for (size_t i = 0; i < secs.size(); i++)
+            ok = ok && st.write(secs[i].first, secs[i].second, &foot.section_checksum[i]);
     }
+    ok = ok && fwrite(&foot, sizeof(foot), 1, f) == 1;
+    // Durable before it becomes the image: the data (fsync), then the name (rename + the
+    // directory's fsync) -- the superblock's atomic switch.
     ok = fflush(f) == 0 && ok;
+    ok = ok && fsync(fileno(f)) == 0;
     ok = fclose(f) == 0 && ok;
-    // The image replaces the previous one only once complete (the superblock's atomic switch).
-    if (ok) ok = rename(tmp.c_str(), path) == 0;
+    if (ok) ok = rename(tmp.c_str(), path) == 0 && fsync_parent(path);
     if (!ok) {
         if (ctx->error.empty()) ctx->error = "checkpoint: write failed";
         remove(tmp.c_str());
@@ -2207,12 +2300,21 @@ tbg_ctx* tbg_open_checkpoint(const tbg_options* options, const char* path) {
               h.acc_rows_used <= options->account_capacity &&
               h.tr_rows_used <= options->transfer_capacity &&
               h.scalars.expiry_count <= ctx->T.expiry_capacity && h.ae_used <= ctx->ae_cap;
+    CkptFooter foot{};
     if (ok) {
         Stager st(ctx, f);
         ok = st.ok;
-        for (auto& sec : ckpt_sections(ctx, h.acc_rows_used, h.tr_rows_used,
-                                       h.scalars.expiry_count, h.ae_used))
-            ok = ok && st.read(sec.first, sec.second);
+        const auto secs = ckpt_sections(ctx, h.acc_rows_used, h.tr_rows_used,
+                                        h.scalars.expiry_count, h.ae_used);
+        uint64_t sums[kCkptSections] = {};
+        for (size_t i = 0; i < secs.size(); i++)
+            ok = ok && st.read(secs[i].first, secs[i].second, &sums[i]);
+        // Nothing is installed unless the header and every section match their checksums.
+        ok = ok && fread(&foot, sizeof(foot), 1, f) == 1 &&
+             memcmp(foot.magic, kCkptMagic, 8) == 0 &&
+             foot.header_checksum == header_checksum(h);
+        for (size_t i = 0; ok && i < secs.size(); i++) ok = foot.section_checksum[i] == sums[i];
+        if (!ok) fprintf(stderr, "tbg_open_checkpoint: %s: image corrupt or truncated\n", path);
     }
     fclose(f);
     if (ok)

@@ -818,10 +818,17 @@ __global__ void __launch_bounds__(kBlock, TBG_INGEST_WG_PER_CU) tr_ingest(Tables
         const uint32_t ubase = __builtin_amdgcn_readfirstlane(base);
         const uint4 ci = c.chunk_info[ubase >> 6];
         const uint32_t cnt = c.n - ubase < 64 ? c.n - ubase : 64;
+        // One ds_write_b128 per part: each 8-lane group writes one event's 128 contiguous bytes,
+        // which no two lanes share a bank of. (A uint4 store here was split into ds_write2_b64
+        // pairs, whose 16-lane groups put two events' rows 144 B apart on the same banks: 2-way
+        // conflicts, SQ_LDS_BANK_CONFLICT in profiles/r02_pmc.)
+        typedef unsigned int v4u_lds __attribute__((ext_vector_type(4)));
 #pragma unroll
         for (int i = 0; i < 8; i++) {
             const uint32_t e = i * 8 + (lane >> 3), part = lane & 7;
-            *reinterpret_cast<uint4*>(my + e * kLdsEventStride + part * 16) = q[i];
+            const v4u_lds v = {q[i].x, q[i].y, q[i].z, q[i].w};
+            *reinterpret_cast<v4u_lds*>(
+                __builtin_assume_aligned(my + e * kLdsEventStride + part * 16, 16)) = v;
         }
         wave_lds_sync();
         const uint32_t k = base + lane;
@@ -894,6 +901,10 @@ __global__ void __launch_bounds__(kBlock, TBG_INGEST_WG_PER_CU) tr_ingest(Tables
         // compiler's wait counts stay exact and the claim does not wait for the prefetch.)
         load_chunk(next < c.n ? next : ubase);
 #endif
+        // (The lane's fields are read from the LDS image where they are used: 16-byte fields with
+        // conflict-free ds_read_b128; the 2-8 byte ones put 2-4 lanes of a 32-lane group on a
+        // bank. A register copy of the event would avoid that but spills at this kernel's
+        // 128-VGPR budget.)
         if (active) {
             const tb_transfer_t& t = *reinterpret_cast<const tb_transfer_t*>(my + lane * kLdsEventStride);
             const bool prev_linked =
