@@ -56,7 +56,8 @@ METRIC = "validated create_transfers/sec (1/2/4/8 GPU) + % of HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # Measured HBM bytes per launch of each kernel (tools/pmc.sh: separate rocprofv3 --pmc passes of
 # this bench's default workload; FETCH_SIZE doubled per the gfx950 note + WRITE_SIZE).
-TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "traffic.json")  # config 2 (the default workload)
+TRAFFIC_FILE_CONFIG5 = os.path.join(ROOT, "profiles", "traffic_config5.json")
 BATCH = 8189           # Operation.create_transfers.event_max (src/tigerbeetle.zig:853-901)
 CREATED = 0xFFFFFFFF
 MESSAGE_BODY_SIZE_MAX = (1 << 20) - 256  # constants.message_body_size_max (constants.zig:234)
@@ -207,10 +208,10 @@ def event_timestamps(lens, batch_ts):
             + within.astype(np.uint64) + np.uint64(1))
 
 
-def measured_traffic(kernel):
-    """(HBM bytes per launch, source) of `kernel` from TRAFFIC_FILE, or (None, None)."""
+def measured_traffic(kernel, path=TRAFFIC_FILE):
+    """(HBM bytes per launch, source) of `kernel` from a tools/pmc.sh summary, or (None, None)."""
     try:
-        with open(TRAFFIC_FILE) as fh:
+        with open(path) as fh:
             d = json.load(fh)
         return float(d["kernels"][kernel]["hbm_bytes_per_launch"]), d.get("source")
     except (OSError, ValueError, KeyError, TypeError):
@@ -924,7 +925,9 @@ def main():
         avg_s = kms / kcount / 1e3
         kbytes = KERNEL_BYTES_PER_EVENT[kname] * N
         achieved = kbytes / avg_s / 1e9
-        traffic, traffic_src = measured_traffic(kname) if wl.default else (None, None)
+        traffic, traffic_src = (measured_traffic(kname) if wl.default else
+                                measured_traffic(kname, TRAFFIC_FILE_CONFIG5)
+                                if wl.name == "config5" else (None, None))
         roofline = {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 1),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                     "traffic": traffic, "traffic_source": traffic_src,

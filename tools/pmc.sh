@@ -9,7 +9,7 @@ out=$R/gpurun_out/$tag
 mkdir -p $out
 export TMPDIR=/tmp
 cd /tmp
-args="--no-cpu-baseline --no-validate --steps 2 --warmup 1 $*"
+args="--no-cpu-baseline --no-validate --commit-reps 0 --steps 2 --warmup 1 $*"
 i=0
 for ctrs in "FETCH_SIZE" "WRITE_SIZE" \
             "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" \
@@ -21,3 +21,5 @@ for ctrs in "FETCH_SIZE" "WRITE_SIZE" \
         python3 $R/bench.py $args > $out/p$i.log 2>&1 || { echo "pass $i ($ctrs) failed"; tail -5 $out/p$i.log; exit 1; }
 done
 cd $R && python3 tools/pmc_summary.py $out $out/traffic.json > $out/summary.txt && cat $out/traffic.json
+# (the per-launch averages cover only full-size bench steps: --commit-reps 0 runs no 8189-event
+# per-commit calls, whose launches would otherwise be averaged in)
