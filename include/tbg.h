@@ -218,6 +218,9 @@ int tbg_debug_force_replay(tbg_ctx* ctx, int enable);
  * of the flow replay (many lanes, units ordered by the keys they share): a self-check of the
  * flow replay's exactness. */
 int tbg_debug_serial_replay(tbg_ctx* ctx, int enable);
+/* Debug / A-B: 1 = every AccountEvents append on the call's stream (no side stream; the default
+ * hands a call of <= 8192 events' appends to a side stream behind the next call). */
+int tbg_debug_ae_sync(tbg_ctx* ctx, int enable);
 
 /* Per-kernel timing with HIP events on the call's stream (off by default; resets the totals);
  * enable == 2 records only the host-wall phases of host-buffer calls (host:*), no HIP events.

@@ -36,7 +36,7 @@ class Pair:
     def __init__(self, account_capacity=1 << 16, transfer_capacity=1 << 20,
                  batch_events_max=1 << 16, batch_count_max=4096, pulse_batch_max=8190,
                  pulse_next_timestamp_init=TIMESTAMP_MAX, force_replay=False, device=0,
-                 account_events=True):
+                 account_events=True, registered=False):
         self.lib = native.load()
         self.olib = oracle_binding.load()
         o = native.TbgOptions()
@@ -56,6 +56,19 @@ class Pair:
             raise RuntimeError("tbg_open failed")
         self._force_replay = force_replay
         self._apply_debug_modes()
+        # registered: create_transfers bodies and results go through one page-aligned host pool
+        # registered with the executor (tbg_register_host), as a replica's message pool: the
+        # kernels read the body and write the results over PCIe (hostio.hpp, tr_ingest).
+        self._pool = None
+        if registered:
+            ev_bytes = batch_events_max * 128
+            raw = np.zeros(ev_bytes + batch_events_max * 16 + 8192, dtype=np.uint8)
+            off = (-raw.ctypes.data) % 4096
+            self._pool_raw = raw
+            self._pool = raw[off:off + ev_bytes + batch_events_max * 16 + 4096]
+            assert self.lib.tbg_register_host(self.g, self._pool.ctypes.data,
+                                              self._pool.nbytes) == 0
+            self._pool_results = ev_bytes
         self.o = self.olib.tbo_open(pulse_batch_max, pulse_next_timestamp_init)
         self.prepare_timestamp = 0
         self._pulse_delta = pulse_batch_max
@@ -67,8 +80,9 @@ class Pair:
         force_replay = self._force_replay
         if force_replay:  # True: every event through the flow replay; "serial": on one lane
             self.lib.tbg_debug_force_replay(self.g, 1)
-        if force_replay == "serial":
+        if force_replay == "serial":  # (and the appends on the call's stream)
             self.lib.tbg_debug_serial_replay(self.g, 1)
+            self.lib.tbg_debug_ae_sync(self.g, 1)
 
     def compact(self):
         """tbg_compact on the executor (the oracle has nothing to compact); rows freed."""
@@ -157,9 +171,18 @@ class Pair:
         r_gpu = np.zeros(n, dtype=RESULT_DTYPE)
         r_orc = np.zeros(n, dtype=RESULT_DTYPE)
         t0 = time.perf_counter()
-        rc = self.lib.tbg_create_transfers(
-            self.g, _ptr(events), n, lens_a.ctypes.data_as(native.c_u32p),
-            batch_ts.ctypes.data_as(native.c_u64p), len(lens), _ptr(r_gpu))
+        if self._pool is not None:
+            body = self._pool[:n * 128]
+            body[:] = events.view(np.uint8).reshape(-1)
+            res = self._pool[self._pool_results:self._pool_results + n * 16]
+            rc = self.lib.tbg_create_transfers(
+                self.g, ctypes.c_void_p(body.ctypes.data), n, lens_a.ctypes.data_as(native.c_u32p),
+                batch_ts.ctypes.data_as(native.c_u64p), len(lens), ctypes.c_void_p(res.ctypes.data))
+            r_gpu[:] = res.view(RESULT_DTYPE)
+        else:
+            rc = self.lib.tbg_create_transfers(
+                self.g, _ptr(events), n, lens_a.ctypes.data_as(native.c_u32p),
+                batch_ts.ctypes.data_as(native.c_u64p), len(lens), _ptr(r_gpu))
         t1 = time.perf_counter()
         if rc != 0:
             raise RuntimeError(f"tbg_create_transfers: {rc} {self.lib.tbg_last_error(self.g)}")

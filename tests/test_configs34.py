@@ -17,10 +17,11 @@ pytestmark = pytest.mark.gpu
 BATCH = configs34.BATCH
 
 
-def _pair(n, batches):
+def _pair(n, batches, registered=False):
     # (batch_events_max also holds the 10k-account create_accounts call)
     return Pair(account_capacity=1 << 14, transfer_capacity=n + (1 << 14),
-                batch_events_max=max(BATCH * batches, 1 << 14), batch_count_max=batches)
+                batch_events_max=max(BATCH * batches, 1 << 14), batch_count_max=batches,
+                registered=registered)
 
 
 @pytest.mark.parametrize("walk", ["wave", "one_lane"])
@@ -42,9 +43,11 @@ def test_config3_baseline_scale(walk, monkeypatch):
         p.close()
 
 
-def test_config3_one_batch_commits():
-    """Config 3 as replica commits: 25 single-batch calls of 8189 events."""
-    p = _pair(25 * BATCH, 1)
+@pytest.mark.parametrize("registered", [False, True], ids=["pageable", "registered"])
+def test_config3_one_batch_commits(registered):
+    """Config 3 as replica commits: 25 single-batch calls of 8189 events (bodies and replies in a
+    registered host pool: read and written by the kernels over PCIe)."""
+    p = _pair(25 * BATCH, 1, registered)
     try:
         s = configs34.config3(p, 25 * BATCH, batches_per_commit=1)
         assert s["calls"] == 25 and s["exceeds_credits"] > 0
@@ -70,13 +73,14 @@ def test_config4_baseline_scale():
         p.close()
 
 
-@pytest.mark.parametrize("pv", ["fast", "replayed"])
+@pytest.mark.parametrize("pv", ["fast", "replayed", "registered"])
 def test_config4_one_batch_commits(pv, monkeypatch):
     """Config 4 as replica commits: 30 single-batch calls of 8189 events with ticks and pulses;
-    post/voids FAST-claimed, or all replayed (TBG_NO_PV_FAST)."""
+    post/voids FAST-claimed, or all replayed (TBG_NO_PV_FAST), or FAST with the bodies and
+    replies in a registered host pool."""
     if pv == "replayed":
         monkeypatch.setenv("TBG_NO_PV_FAST", "1")
-    p = _pair(30 * BATCH, 1)
+    p = _pair(30 * BATCH, 1, registered=pv == "registered")
     try:
         s = configs34.config4(p, 30 * BATCH, batches_per_commit=1)
         assert s["commits"] == 30

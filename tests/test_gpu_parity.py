@@ -18,13 +18,16 @@ def _split(n, rng, max_batch):
     return lens
 
 
+@pytest.mark.parametrize("registered", [False, True], ids=["pageable", "registered"])
 @pytest.mark.parametrize("force_replay", [False, True, "serial"], ids=["parallel", "flow", "serial"])
 @pytest.mark.parametrize("seed", range(6))
-def test_fuzz(seed, force_replay):
+def test_fuzz(seed, force_replay, registered):
+    """Executor-level fuzzing against the oracle; `registered`: bodies and results in a registered
+    host pool (the kernels read / write them over PCIe, the appends on the side stream)."""
     rng = np.random.default_rng(1000 + seed)
     p = Pair(account_capacity=1 << 12, transfer_capacity=1 << 15, batch_events_max=4096,
              pulse_batch_max=16, pulse_next_timestamp_init=TIMESTAMP_MAX,
-             force_replay=force_replay)
+             force_replay=force_replay, registered=registered)
     try:
         n_acc = 24
         a = workload.fuzz_accounts(rng, 40, n_acc)
@@ -647,8 +650,9 @@ def test_long_linked_chains(length, force_replay):
         p.close()
 
 
+@pytest.mark.parametrize("registered", [False, True], ids=["pageable", "registered"])
 @pytest.mark.parametrize("force_replay", [False, True, "serial"], ids=["parallel", "flow", "serial"])
-def test_change_events(force_replay):
+def test_change_events(force_replay, registered):
     """AccountEvents (state_machine.zig:4384-4465) and get_change_events (:3395-3527) against the
     oracle: single-phase, pending, posted (partial), voided (also of closing transfers) and
     expired events, balancing amounts, rolled-back chains; then filters by timestamp range and
@@ -656,7 +660,7 @@ def test_change_events(force_replay):
     rng = np.random.default_rng(31)
     p = Pair(account_capacity=1 << 10, transfer_capacity=1 << 15, batch_events_max=4096,
              pulse_batch_max=16, pulse_next_timestamp_init=TIMESTAMP_MAX,
-             force_replay=force_replay)
+             force_replay=force_replay, registered=registered)
     try:
         acc = workload.accounts(30, seed=3, ledger=1)
         acc["flags"] = rng.choice([0, 0, 2, 4, 8], size=30).astype(np.uint16)

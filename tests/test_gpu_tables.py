@@ -35,8 +35,9 @@ def gpu_handle(force_replay: bool, durability=None, tmp_path=None):
     def debug_modes(g):
         if force_replay:
             lib.tbg_debug_force_replay(g, 1)
-        if force_replay == "serial":
+        if force_replay == "serial":  # (and the appends on the call's stream: both append paths)
             lib.tbg_debug_serial_replay(g, 1)
+            lib.tbg_debug_ae_sync(g, 1)
 
     debug_modes(lib.tb_sm_executor_gpu(sm))
     h = None

@@ -16,6 +16,11 @@
 // over them gives every touch the sum of its account's later deltas.
 // Chains that were rolled back left no created event, so their events never appear (the groove's
 // scope discard). AccountEvents are in timestamp order within a call; the log is kept sorted.
+//
+// The collection pass writes each touch's half as the account's final row (id, balances, account
+// timestamp, flags); the emit passes subtract the later touches' sums from it in place. Nothing
+// after the collection reads the accounts, which lets a small call's appends run on a side stream
+// behind the next call (ae_snapshot below).
 #pragma once
 
 #include "group.hpp"
@@ -60,6 +65,9 @@ struct AeScratch {
     uint32_t* chunk_seg;    // per chunk of a listed account: the account's entry in G.big
     Bal5* chunk_tot;        // per chunk: the sums of its touches
     unsigned long long* state;  // the log on device: [0] events, [1] last timestamp, [2] unsorted
+    // Touch v's event is v >> 1: its log position is pos[v >> 1] (the side stream's appends,
+    // whose touches are numbered by call event), or v >> 1 itself when pos is null.
+    const uint32_t* pos;
 };
 
 __device__ inline void ae_side(const AeScratch& S, uint32_t i, uint32_t side, u128 pending,
@@ -88,6 +96,80 @@ __device__ inline void ae_event_fields(tb_account_event_t* e, uint64_t timestamp
     e->ledger = ledger;
     e->transfer_pending_status = status;
     for (int j = 0; j < 11; j++) e->reserved[j] = 0;
+}
+
+// A touch's half of its AccountEvent. The dr and cr halves share one layout (id and four
+// balances: five 16-byte words, then the account timestamp and flags): one side's pointers,
+// 16-byte stores (no struct copies, which the compiler stages through scratch).
+__device__ inline uint4 ae_q(u128 x) {
+    return make_uint4(uint32_t(uint64_t(x)), uint32_t(uint64_t(x) >> 32), uint32_t(uint64_t(x >> 64)),
+                      uint32_t(uint64_t(x >> 64) >> 32));
+}
+__device__ inline u128 ae_u(uint4 v) {
+    return (u128((uint64_t(v.w) << 32) | v.z) << 64) | ((uint64_t(v.y) << 32) | v.x);
+}
+__device__ inline uint4* ae_half_words(tb_account_event_t* log, uint32_t i, uint32_t side) {
+    uint8_t* e = reinterpret_cast<uint8_t*>(&log[i]);
+    return reinterpret_cast<uint4*>(e + (side ? offsetof(tb_account_event_t, cr_account_id)
+                                              : offsetof(tb_account_event_t, dr_account_id)));
+}
+__device__ inline uint16_t* ae_half_flags(tb_account_event_t* log, uint32_t i, uint32_t side) {
+    uint8_t* e = reinterpret_cast<uint8_t*>(&log[i]);
+    return reinterpret_cast<uint16_t*>(e + (side ? offsetof(tb_account_event_t, cr_account_flags)
+                                                 : offsetof(tb_account_event_t, dr_account_flags)));
+}
+__device__ inline uint64_t* ae_half_timestamp(tb_account_event_t* log, uint32_t i, uint32_t side) {
+    uint8_t* e = reinterpret_cast<uint8_t*>(&log[i]);
+    return reinterpret_cast<uint64_t*>(e + (side ? offsetof(tb_account_event_t, cr_account_timestamp)
+                                                 : offsetof(tb_account_event_t, dr_account_timestamp)));
+}
+
+// An account's final state as a touch's half starts out (collection) -- also the snapshot's form.
+struct AeFinal {
+    uint4 id, dp, dpo, cp, cpo;
+    uint64_t timestamp;
+    uint32_t flags, pad;
+};
+static_assert(sizeof(AeFinal) == 96, "AeFinal layout");
+__device__ inline AeFinal ae_final_of(const tb_account_t& a) {
+    AeFinal f;
+    const uint4* w = reinterpret_cast<const uint4*>(&a);  // id, debits_pending .. credits_posted
+    f.id = w[0];
+    f.dp = w[1];
+    f.dpo = w[2];
+    f.cp = w[3];
+    f.cpo = w[4];
+    f.timestamp = a.timestamp;
+    f.flags = a.flags;
+    f.pad = 0;
+    return f;
+}
+__device__ inline void ae_write_final(tb_account_event_t* log, uint32_t i, uint32_t side,
+                                      const AeFinal& f) {
+    uint4* w = ae_half_words(log, i, side);
+    w[0] = f.id;
+    w[1] = f.dp;
+    w[2] = f.dpo;
+    w[3] = f.cp;
+    w[4] = f.cpo;
+    *ae_half_timestamp(log, i, side) = f.timestamp;
+    *ae_half_flags(log, i, side) = uint16_t(f.flags);
+}
+
+// One touch's half: the account after the event = its final state (written by the collection) -
+// the sums of the account's later touches in the call.
+__device__ inline void ae_emit_touch(uint32_t v, const Bal5& later, tb_account_event_t* log,
+                                     const uint32_t* pos) {
+    const uint32_t i = pos ? pos[v >> 1] : v >> 1, side = v & 1;
+    uint4* w = ae_half_words(log, i, side);
+    const uint4 dp = w[1], dpo = w[2], cp = w[3], cpo = w[4];
+    uint16_t* fl = ae_half_flags(log, i, side);
+    const uint16_t flags = *fl;
+    w[1] = ae_q(ae_u(dp) - later.dp);
+    w[2] = ae_q(ae_u(dpo) - later.dpo);
+    w[3] = ae_q(ae_u(cp) - later.cp);
+    w[4] = ae_q(ae_u(cpo) - later.cpo);
+    if (later.flips & 1) *fl = uint16_t(flags ^ TB_ACCOUNT_CLOSED);
 }
 
 __device__ inline uint64_t ae_transfer_row(const Tables& T, const tb_uint128_t& id) {
@@ -120,8 +202,10 @@ __device__ inline void ae_group_touches(const AeScratch& S, GroupBlock& B, uint3
                                         uint32_t dr, uint32_t cr, uint32_t bound) {
     uint32_t e0 = kNone32, e1 = kNone32, r0 = 0, r1 = 0;
     if (active) {
-        e0 = group_block_add(S.G, B, dr, &r0);
-        e1 = group_block_add(S.G, B, cr, &r1);
+        uint32_t s0, s1;
+        group_slot2(S.G, dr, cr, &s0, &s1);
+        e0 = group_block_count(B, s0, &r0);
+        e1 = group_block_count(B, s1, &r1);
     }
     group_block_publish(S.G, B);
     if (i >= bound) return;
@@ -129,29 +213,16 @@ __device__ inline void ae_group_touches(const AeScratch& S, GroupBlock& B, uint3
     group_block_place(S.G, B, 2 * uint64_t(i) + 1, e1, r1);
 }
 
-__device__ inline void ae_collect_transfer(Tables T, const Call<tb_transfer_t>& c, uint32_t k,
-                                           uint32_t i, const AeScratch& S, tb_account_event_t* log,
-                                           AeRef* refs, uint32_t* dr_out, uint32_t* cr_out) {
-    const uint64_t row = c.row_base + k;
-    const tb_transfer_t& t = T.tr_rows[row];  // the created transfer (amount actual, accounts)
+// Both sides' deltas of created transfer t (p: its pending transfer, for a post/void); returns the
+// event's TransferPendingStatus.
+__device__ inline uint8_t ae_transfer_sides(const AeScratch& S, uint32_t i, const tb_transfer_t& t,
+                                            const tb_transfer_t* p) {
     const uint16_t f = t.flags;
-    // A created transfer that is not a post/void has the event's own accounts, whose rows the
-    // ingest found (c.ev_dr / ev_cr, unless it packed them into balance items: kInfoLean); a
-    // post/void's are the pending transfer's.
-    const bool pv = (f & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) != 0;
-    const bool refs_ok = !pv && c.ev_dr && c.ev_cr && !(c.ev_info[k] & kInfoLean);
-    const uint32_t edr = refs_ok ? c.ev_dr[k] : kNone32;
-    const uint32_t ecr = refs_ok ? c.ev_cr[k] : kNone32;
-    const uint64_t dr = edr != kNone32 ? uint64_t(edr) : account_find(T, t.debit_account_id);
-    const uint64_t cr = ecr != kNone32 ? uint64_t(ecr) : account_find(T, t.credit_account_id);
     const u128 amount = U(t.amount);
     uint8_t status = TB_PENDING_NONE;
-    const tb_transfer_t* p = nullptr;
     u128 d_pending = 0, d_posted = 0;
     uint32_t flip_dr = 0, flip_cr = 0;
-    if (f & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) {
-        const uint64_t pr = ae_transfer_row(T, t.pending_id);
-        p = &T.tr_rows[pr];
+    if (p) {
         d_pending = u128(0) - U(p->amount);
         if (f & TB_TRANSFER_POST_PENDING) {
             status = TB_PENDING_POSTED;
@@ -171,7 +242,30 @@ __device__ inline void ae_collect_transfer(Tables T, const Call<tb_transfer_t>& 
     }
     ae_side(S, i, 0, d_pending, d_posted, flip_dr);
     ae_side(S, i, 1, d_pending, d_posted, flip_cr);
+    return status;
+}
+
+__device__ inline void ae_collect_transfer(Tables T, const Call<tb_transfer_t>& c, uint32_t k,
+                                           uint32_t i, const AeScratch& S, tb_account_event_t* log,
+                                           AeRef* refs, uint32_t* dr_out, uint32_t* cr_out) {
+    const uint64_t row = c.row_base + k;
+    const tb_transfer_t& t = T.tr_rows[row];  // the created transfer (amount actual, accounts)
+    const uint16_t f = t.flags;
+    // A created transfer that is not a post/void has the event's own accounts, whose rows the
+    // ingest found (c.ev_dr / ev_cr, unless it packed them into balance items: kInfoLean); a
+    // post/void's are the pending transfer's.
+    const bool pv = (f & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) != 0;
+    const bool refs_ok = !pv && c.ev_dr && c.ev_cr && !(c.ev_info[k] & kInfoLean);
+    const uint32_t edr = refs_ok ? c.ev_dr[k] : kNone32;
+    const uint32_t ecr = refs_ok ? c.ev_cr[k] : kNone32;
+    const uint64_t dr = edr != kNone32 ? uint64_t(edr) : account_find(T, t.debit_account_id);
+    const uint64_t cr = ecr != kNone32 ? uint64_t(ecr) : account_find(T, t.credit_account_id);
+    const tb_transfer_t* p =
+        pv ? &T.tr_rows[ae_transfer_row(T, t.pending_id)] : nullptr;
+    const uint8_t status = ae_transfer_sides(S, i, t, p);
     ae_event_fields(&log[i], t.timestamp, f, status, p, c.events[k].amount, t.amount, t.ledger);
+    ae_write_final(log, i, 0, ae_final_of(T.acc_rows[dr]));
+    ae_write_final(log, i, 1, ae_final_of(T.acc_rows[cr]));
     refs[i] = AeRef{uint32_t(row), uint32_t(dr), uint32_t(cr), 0};
     *dr_out = uint32_t(dr);
     *cr_out = uint32_t(cr);
@@ -192,6 +286,110 @@ ae_collect_transfers(Tables T, Call<tb_transfer_t> c, const uint32_t* list,
     ae_group_touches(S, B, i, active, dr_row, cr_row, c.n);
 }
 
+// ---- Small calls: the appends behind the next call --------------------------------------------
+//
+// A create_transfers call of at most kAeAsyncMax events hands its appends to a side stream
+// (executor: ae_transfers_async). The staging pass runs on the call's stream (fused into its
+// stage_out), before the next call can change anything: per created event k it writes the finished
+// AccountEvent but for the later touches' sums -- event fields and both accounts' final state --
+// its reference, both sides' deltas (touches 2k, 2k + 1) and a created flag. The side stream then
+// numbers the created events (a chained scan), copies each record to its log position and groups
+// the touches by account, and the emit passes subtract the later sums in place. It reads only
+// the staging (and writes only the log), so the next call runs beside it.
+constexpr uint32_t kAeAsyncMax = 8192;
+
+struct AeStage {
+    tb_account_event_t* rec;  // per event
+    AeRef* ref;               // per event
+    AeDelta* delta;           // per touch (2k + side)
+    uint8_t* created;         // per event
+};
+
+struct AeSnapJob {
+    Tables T;
+    Call<tb_transfer_t> c;
+    AeStage st;
+    bool on;
+};
+__device__ inline void ae_snapshot_one(const AeSnapJob& J, uint32_t k) {
+    const Tables& T = J.T;
+    const Call<tb_transfer_t>& c = J.c;
+    const bool made = k < c.n && c.results[k].status == TB_STATUS_CREATED;
+    J.st.created[k] = made;
+    if (!made) return;
+    const uint64_t row = c.row_base + k;
+    const tb_transfer_t& t = T.tr_rows[row];
+    const uint16_t f = t.flags;
+    const bool pv = (f & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) != 0;
+    const bool refs_ok = !pv && c.ev_dr && c.ev_cr && !(c.ev_info[k] & kInfoLean);
+    const uint32_t edr = refs_ok ? c.ev_dr[k] : kNone32;
+    const uint32_t ecr = refs_ok ? c.ev_cr[k] : kNone32;
+    const uint64_t dr = edr != kNone32 ? uint64_t(edr) : account_find(T, t.debit_account_id);
+    const uint64_t cr = ecr != kNone32 ? uint64_t(ecr) : account_find(T, t.credit_account_id);
+    const uint64_t pr = pv ? ae_transfer_row(T, t.pending_id) : kNone;
+    if (dr == kNone || cr == kNone || (pv && pr == kNone)) {  // (never for a final result)
+        J.st.created[k] = 0;
+        return;
+    }
+    const tb_transfer_t* p = pv ? &T.tr_rows[pr] : nullptr;
+    AeScratch D{};
+    D.deltas = J.st.delta;
+    const uint8_t status = ae_transfer_sides(D, k, t, p);
+    tb_account_event_t* rec = J.st.rec;
+    ae_event_fields(&rec[k], t.timestamp, f, status, p, c.events[k].amount, t.amount, t.ledger);
+    ae_write_final(rec, k, 0, ae_final_of(T.acc_rows[dr]));
+    ae_write_final(rec, k, 1, ae_final_of(T.acc_rows[cr]));
+    J.st.ref[k] = AeRef{uint32_t(row), uint32_t(dr), uint32_t(cr), 0};
+}
+
+// The staging on its own (a call whose replay ran after stage_out).
+__global__ void ae_snapshot(AeSnapJob J) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < kAeAsyncMax) ae_snapshot_one(J, k);
+}
+
+// u8 flags -> pos[i] = the number of flagged items before i (flagged items only); the count.
+struct PositionsOf8 {
+    static constexpr bool kEmitAll = false;
+    const uint8_t* flags;
+    uint32_t* pos;
+    unsigned int* count;
+    __device__ void load(uint64_t base, uint64_t n, uint32_t* c) const {
+        const uint4 v = *reinterpret_cast<const uint4*>(flags + base);  // (n: a multiple of 16)
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (uint32_t i = 0; i < kScanItems; i++) c[i] = ((w[i >> 2] >> (8 * (i & 3))) & 0xFF) != 0;
+        (void)n;
+    }
+    __device__ void emit(uint64_t i, uint32_t p) const { pos[i] = p; }
+    __device__ void total(uint32_t t) const { *count = t; }
+};
+
+// One lane per call event: a created event's record and reference to its log position, its
+// touches (2k, 2k + 1) into the grouping.
+__global__ void __launch_bounds__(kPlanThreads)
+ae_copy_group(AeStage st, const uint32_t* pos, AeScratch S, tb_account_event_t* log, AeRef* refs) {
+    __shared__ GroupBlock B;
+    group_block_init(B);
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k == 0) S.G.counts[1] = S.G.counts[2] = 0;  // listed accounts / chunks (ae_group_small)
+    const uint64_t used = S.state[0];
+    const bool active = k < kAeAsyncMax && st.created[k];
+    uint32_t dr_row = 0, cr_row = 0;
+    if (active) {
+        const uint64_t i = used + pos[k];
+        const uint4* src = reinterpret_cast<const uint4*>(&st.rec[k]);
+        uint4* dst = reinterpret_cast<uint4*>(&log[i]);
+#pragma unroll
+        for (int w = 0; w < 16; w++) dst[w] = src[w];
+        const AeRef r = st.ref[k];
+        refs[i] = r;
+        dr_row = r.dr_row;
+        cr_row = r.cr_row;
+    }
+    ae_group_touches(S, B, k, active, dr_row, cr_row, kAeAsyncMax);
+}
+
 // Expiries of a pulse (execute_expire_pending_transfers :4540-4626): rows[i] in expiry order,
 // event i stamped timestamp - m + i + 1 -- or stamps[i], a shard's expiries stamped by their
 // positions in the pulse's expiry order across all shards.
@@ -207,14 +405,18 @@ __device__ inline void ae_expiry_one(Tables T, uint64_t row, uint32_t m, uint32_
     ae_side(S, i, 1, d_pending, 0, (p.flags & TB_TRANSFER_CLOSING_CREDIT) != 0);
     ae_event_fields(&log[i], stamps ? stamps[i] : timestamp - m + i + 1, 0, TB_PENDING_EXPIRED, &p,
                     tb_uint128_t{0, 0}, p.amount, p.ledger);
+    ae_write_final(log, i, 0, ae_final_of(T.acc_rows[dr]));
+    ae_write_final(log, i, 1, ae_final_of(T.acc_rows[cr]));
     refs[i] = AeRef{uint32_t(row), uint32_t(dr), uint32_t(cr), 0};
     *dr_out = uint32_t(dr);
     *cr_out = uint32_t(cr);
 }
 
 __global__ void __launch_bounds__(kPlanThreads)
-ae_collect_expiry(Tables T, const uint64_t* rows, uint32_t m, uint64_t timestamp,
-                  const uint64_t* stamps, AeScratch S, tb_account_event_t* log, AeRef* refs) {
+ae_collect_expiry(Tables T, const uint64_t* rows, uint32_t m_upper, const unsigned int* m_dev,
+                  uint64_t timestamp, const uint64_t* stamps, AeScratch S, tb_account_event_t* log,
+                  AeRef* refs) {
+    const uint32_t m = m_dev ? *m_dev : m_upper;  // (the pulse's count, on device)
     __shared__ GroupBlock B;
     group_block_init(B);
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -223,7 +425,7 @@ ae_collect_expiry(Tables T, const uint64_t* rows, uint32_t m, uint64_t timestamp
     refs += S.state[0];
     uint32_t dr_row = 0, cr_row = 0;
     if (i < m) ae_expiry_one(T, rows[i], m, i, timestamp, stamps, S, log, refs, &dr_row, &cr_row);
-    ae_group_touches(S, B, i, i < m, dr_row, cr_row, m);
+    ae_group_touches(S, B, i, i < m, dr_row, cr_row, m_upper);
 }
 
 // Closes an appended block: the log's length and last timestamp advance on device (the host reads
@@ -241,33 +443,6 @@ __global__ void ae_tail(const tb_account_event_t* log, const unsigned int* d_cou
     state[0] = used + m;
 }
 
-// One touch's half of its AccountEvent: the account after the event = final row - the sums of
-// the account's later touches in the call.
-__device__ inline void ae_emit_touch(const tb_account_t& a, uint32_t v, const Bal5& later,
-                                     tb_account_event_t* log) {
-    const uint32_t i = v >> 1, side = v & 1;
-    // The dr and cr halves share one layout (id and four balances: five 16-byte words, then the
-    // account timestamp and flags): one side's pointers, 16-byte stores (no struct copies, which
-    // the compiler stages through scratch).
-    uint8_t* e = reinterpret_cast<uint8_t*>(&log[i]);
-    uint4* w = reinterpret_cast<uint4*>(
-        e + (side ? offsetof(tb_account_event_t, cr_account_id) : offsetof(tb_account_event_t, dr_account_id)));
-    auto q = [](u128 x) {
-        return make_uint4(uint32_t(uint64_t(x)), uint32_t(uint64_t(x) >> 32), uint32_t(uint64_t(x >> 64)),
-                          uint32_t(uint64_t(x >> 64) >> 32));
-    };
-    w[0] = q(U(a.id));
-    w[1] = q(U(a.debits_pending) - later.dp);
-    w[2] = q(U(a.debits_posted) - later.dpo);
-    w[3] = q(U(a.credits_pending) - later.cp);
-    w[4] = q(U(a.credits_posted) - later.cpo);
-    *reinterpret_cast<uint64_t*>(e + (side ? offsetof(tb_account_event_t, cr_account_timestamp)
-                                           : offsetof(tb_account_event_t, dr_account_timestamp))) =
-        a.timestamp;
-    *reinterpret_cast<uint16_t*>(e + (side ? offsetof(tb_account_event_t, cr_account_flags)
-                                           : offsetof(tb_account_event_t, dr_account_flags))) =
-        uint16_t(a.flags ^ ((later.flips & 1) ? TB_ACCOUNT_CLOSED : 0));
-}
 
 // Listed accounts are processed in chunks of kAeChunk touches (kAeRun per lane of a workgroup).
 constexpr uint32_t kAeRun = 4;
@@ -305,11 +480,12 @@ __device__ inline void ae_mid_account(Tables T, const AeScratch& S, uint32_t off
     later.cp = wave_suffix_exclusive_u128(run.cp);
     later.cpo = wave_suffix_exclusive_u128(run.cpo);
     later.flips = uint32_t(wave_suffix_exclusive_u128(run.flips));
-    const tb_account_t& a = T.acc_rows[row];
+    (void)T;
+    (void)row;
 #pragma unroll
     for (int j = 3; j >= 0; j--) {
         if (v[j] == kNone32) continue;
-        ae_emit_touch(a, v[j], later, log);
+        ae_emit_touch(v[j], later, log, S.pos);
         bal5_add(later, S.deltas[v[j]]);
     }
     wave_lds_sync();  // (buf is reused by the wave's next account)
@@ -345,12 +521,11 @@ __global__ void __launch_bounds__(kBlock) ae_group_small(Tables T, AeScratch S, 
 #pragma unroll
         for (uint32_t i = 0; i < kGroupSmall; i++) v[i] = i < c ? G.vals[off + i] : kNone32;
         sort_network(v);
-        const tb_account_t& a = T.acc_rows[row];
         Bal5 later{};
 #pragma unroll
         for (int i = kGroupSmall - 1; i >= 0; i--) {
             if (uint32_t(i) >= c) continue;
-            ae_emit_touch(a, v[i], later, log);
+            ae_emit_touch(v[i], later, log, S.pos);
             bal5_add(later, S.deltas[v[i]]);
         }
     }
@@ -500,13 +675,84 @@ __global__ void __launch_bounds__(kGroupBigThreads) ae_chunk_emit(Tables T, AeSc
         later.cp += carry_lds.cp;
         later.cpo += carry_lds.cpo;
         later.flips += carry_lds.flips;
-        const tb_account_t& a = T.acc_rows[e.z];
+        (void)T;
         for (uint32_t j = 0; j < kAeRun; j++) {
             if (v[j] == kNone32) break;
-            ae_emit_touch(a, v[j], later, log);
+            ae_emit_touch(v[j], later, log, S.pos);
             bal5_add(later, S.deltas[v[j]]);
         }
         __syncthreads();  // (carry_lds is rewritten by the next chunk)
+    }
+}
+
+// ---- The side stream's graph (small calls) ---------------------------------------------------
+
+// group_scatter + the log's tail (ae_tail) + the graph's scan words cleared for its next replay.
+// The block's base position in the log is kept at base[0] for the emit kernels that follow (the
+// tail advances the log's length first).
+__global__ void ae_scatter_tail(GroupPlan G, uint64_t pairs, const tb_account_event_t* log,
+                                const unsigned int* d_count, unsigned long long* state,
+                                unsigned long long* base, unsigned long long* scan_words,
+                                uint32_t n_scan_words) {
+    const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (blockIdx.x == 0) {
+        for (uint32_t w = threadIdx.x; w < n_scan_words; w += blockDim.x) scan_words[w] = 0;
+        if (threadIdx.x == 0) {
+            const uint32_t m = *d_count;
+            const uint64_t used = state[0];
+            base[0] = used;
+            if (m) {
+                const uint64_t first = log[used].timestamp, last = log[used + m - 1].timestamp;
+                if (used && first <= state[1]) state[2] = 1;
+                state[1] = last > state[1] ? last : state[1];
+                state[0] = used + m;
+            }
+        }
+    }
+    if (i >= pairs) return;
+    const uint32_t slot = G.loc[i];
+    if (slot == kNone32) return;
+    G.vals[G.hoff[slot] + G.rank[i]] = uint32_t(i);
+}
+
+// Listed accounts of a small call, one workgroup each from sort to emission: the touches in event
+// order (segment_sort), then the chunks from the last touch backwards with the later chunks' sums
+// carried in registers (ae_group_sort + ae_chunk_totals + ae_chunk_emit in one launch; a small
+// call's listed accounts hold at most 2 * kAeAsyncMax touches between them).
+__global__ void __launch_bounds__(kGroupBigThreads) ae_group_big_serial(AeScratch S,
+                                                                      tb_account_event_t* log) {
+    __shared__ SegmentLds L;
+    __shared__ Bal5Lds B;
+    const GroupPlan& G = S.G;
+    log += S.state[0];
+    const uint32_t nbig = G.counts[1];
+    for (uint32_t b = blockIdx.x; b < nbig; b += gridDim.x) {
+        const uint4 e = G.big[b];
+        segment_sort(G.vals, G.vals_sorted, e.x, e.y, L);
+        const uint32_t chunks = (e.y + kAeChunk - 1) / kAeChunk;
+        Bal5 carry{};
+        for (uint32_t q = 0; q < chunks; q++) {
+            uint32_t v[kAeRun];
+            const Bal5 run = ae_chunk_run(S, e, q, v);
+            Bal5 chunk;
+            Bal5 later = bal5_block_exclusive(run, &chunk, B);
+            later.dp += carry.dp;
+            later.dpo += carry.dpo;
+            later.cp += carry.cp;
+            later.cpo += carry.cpo;
+            later.flips += carry.flips;
+            for (uint32_t j = 0; j < kAeRun; j++) {
+                if (v[j] == kNone32) break;
+                ae_emit_touch(v[j], later, log, S.pos);
+                bal5_add(later, S.deltas[v[j]]);
+            }
+            carry.dp += chunk.dp;
+            carry.dpo += chunk.dpo;
+            carry.cp += chunk.cp;
+            carry.cpo += chunk.cpo;
+            carry.flips += chunk.flips;
+        }
+        __syncthreads();  // (L is reused by the next listed account)
     }
 }
 

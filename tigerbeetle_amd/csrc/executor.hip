@@ -23,6 +23,8 @@
 #include "events.hpp"
 #include "durability.hpp"
 #include "queries.hpp"
+#include "hostio.hpp"
+#include "pulse.hpp"
 
 using namespace tbg;
 
@@ -41,12 +43,16 @@ constexpr uint32_t kSortThreshold = 1u << 16;
 // Balance items use u128 atomics instead of the sort when the key space has more than this many
 // account fields per item.
 constexpr uint64_t kAtomicKeysPerItem = 8;
+// Calls up to this many events find their chunks' batch bounds inside tr_ingest.
+constexpr uint32_t kInlineChunkMax = 1u << 16;
 
 struct PulseScratch {
-    uint64_t capacity = 0;
+    uint64_t capacity = 0;  // a multiple of kPulseRun (pulse.hpp's sorted runs)
     uint64_t *keep = nullptr, *exp = nullptr, *ts = nullptr, *rows = nullptr;
     uint64_t *exp_b = nullptr, *rows_b = nullptr;
-    unsigned long long* counters = nullptr;
+    uint32_t* run_len = nullptr;  // two arrays of capacity / kPulseRun + 1
+    unsigned long long* counters = nullptr;  // kept, candidates, earliest unexpired, expired
+    unsigned int* expired = nullptr;
 };
 
 // Flow replay scratch (flow.hpp, group.hpp), grown on demand to the largest replay list seen.
@@ -95,12 +101,28 @@ struct tbg_ctx {
     // pinned staging of a host-buffer call's batch ends and timestamps (batch_count_max each)
     uint32_t* h_batch_ends = nullptr;
     uint64_t* h_batch_ts = nullptr;
-    // Host ranges the caller registered (tbg_register_host): DMA straight from / to them.
-    std::vector<std::pair<uintptr_t, uint64_t>> registered;
+    // The pinned blocks as the GPU addresses them (hostio.hpp kernels read / write them).
+    DevScalars* dh_scalars = nullptr;
+    tb_create_result_t* dh_results = nullptr;
+    uint32_t* dh_batch_ends = nullptr;
+    uint64_t* dh_batch_ts = nullptr;
+    // Host ranges the caller registered (tbg_register_host), mapped for the GPU: bodies are read
+    // and results written by kernels over PCIe (hostio.hpp).
+    struct Mapped {
+        uintptr_t host;
+        uint64_t size;
+        uintptr_t dev;
+    };
+    std::vector<Mapped> registered;
     // A host-buffer create_transfers call queues its results' download before its one host
     // synchronisation (create_transfers_impl); valid when the call needed no replay.
     tb_create_result_t* early_dst = nullptr;
     bool early_done = false;
+    // The next create_transfers call's scalar words were reset by its staging kernel.
+    bool scalars_reset = false;
+    // ... and its body is read by tr_ingest from mapped host memory (the GPU's address), null: the
+    // body is in d_events.
+    const tb_transfer_t* events_host = nullptr;
     uint32_t epoch = 0;
     // Sticky: a compaction failed after it began moving rows; the tables are undefined and every
     // later call fails (tbg_compact).
@@ -170,6 +192,24 @@ struct tbg_ctx {
     uint64_t ae_touch_cap = 0;
     uint32_t* ae_list = nullptr;
     unsigned long long* ae_words = nullptr;  // bounds / counts
+    // Small create_transfers calls hand their appends to a side stream (ae_transfers_async): a
+    // staging buffer per parity, the side stream's own positions and grouping scratch. Every other
+    // use of the log joins the side stream first (ae_join).
+    hipStream_t ae_stream = nullptr;
+    AeStage ae_stage[2] = {};
+    uint32_t* ae_pos = nullptr;
+    hipEvent_t ae_snap_ready[2] = {}, ae_done[2] = {};
+    bool ae_done_recorded[2] = {};
+    uint32_t ae_parity = 0;
+    bool ae_async_pending = false;
+    bool ae_async = true;  // tbg_debug_ae_sync(ctx, 1) / TBG_AE_SYNC=1: every append on the call's stream
+    bool ae_async_ready = false;
+    AeScratch ae_g{};
+    // The call's stage_out took its staging and the side stream's appends were queued behind it,
+    // before the host's synchronisation (valid unless a replay followed: then stage_out wrote no
+    // created flags and the appends found nothing).
+    bool ae_snap_early = false;
+    unsigned long long* ae_g_words = nullptr;  // [0] created count; [8..] the graph's scan words
     unsigned long long* flow_debug = nullptr;
 
     // Per-kernel timing (tbg_profile): HIP events recorded on the call's stream between launches.
@@ -260,9 +300,12 @@ int select_flagged(tbg_ctx* ctx, const uint8_t* flags, uint64_t n, uint32_t* out
     return launch_scan(ctx, n, SelectFlags8{flags, out, d_count});
 }
 
+int stage_call_outputs(tbg_ctx* ctx, const tb_create_result_t* d_results, tb_create_result_t* dst,
+                       uint32_t n, bool scalars, const AeSnapJob* snap = nullptr);
+// The scalars block to the host (a kernel writes the mapped pinned copy: no DMA hand-off).
 int sync_scalars(tbg_ctx* ctx) {
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->h_scalars, ctx->d_scalars, sizeof(DevScalars),
-                                hipMemcpyDeviceToHost, ctx->stream));
+    int rc = stage_call_outputs(ctx, nullptr, nullptr, 0, true);
+    if (rc) return rc;
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     return 0;
 }
@@ -381,6 +424,7 @@ Call<Event> make_call(tbg_ctx* ctx, const Event* d_events, uint32_t n, const uin
     c.ev_slow = ctx->ev_slow;
     c.slow_list = ctx->slow_list;
     c.pnt_call = ctx->pnt_call;
+    c.events_out = nullptr;
     // (TBG_NO_PV_FAST: every post/void replays)
     c.pv_slots = getenv("TBG_NO_PV_FAST") ? nullptr : ctx->pv_slots;
     c.pv_mask = ctx->pv_mask;
@@ -733,21 +777,12 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
 // pnt_*). The scratch is the balance items' (consumed before the replay).
 int pnt_resolve(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
     const uint32_t n = c.n;
-    uint64_t* mins = ctx->bal_items;
-    uint64_t* prefix = ctx->bal_items + n;
-    const dim3 block(kBlock);
-    hipLaunchKernelGGL(pnt_prep, dim3(grid_for(n)), block, 0, ctx->stream, c.pnt_call, n, mins);
-    size_t sb = 0;
-    HIP_TRY(ctx, hipcub::DeviceScan::InclusiveScan(nullptr, sb, mins, prefix, hipcub::Min(), int(n),
-                                                   ctx->stream));
-    int rc = ensure_cub_temp(ctx, sb);
-    if (rc) return rc;
-    HIP_TRY(ctx, hipcub::DeviceScan::InclusiveScan(ctx->cub_temp, sb, mins, prefix, hipcub::Min(),
-                                                   int(n), ctx->stream));
-    hipLaunchKernelGGL(pnt_check, dim3(grid_for(n)), block, 0, ctx->stream, ctx->T, c.pnt_call, n,
-                       prefix, ctx->pnt_fired);
-    hipLaunchKernelGGL(pnt_final, dim3(1), dim3(64), 0, ctx->stream, ctx->T, n, prefix,
-                       ctx->pnt_fired);
+    const uint32_t tiles = std::max<uint32_t>(1, (n + kPntTile - 1) / kPntTile);
+    uint64_t* tile_min = ctx->bal_items;  // (free after the balance application)
+    hipLaunchKernelGGL(pnt_tile_min, dim3(tiles), dim3(kPntThreads), 0, ctx->stream, c.pnt_call, n,
+                       tile_min);
+    hipLaunchKernelGGL(pnt_tile_resolve, dim3(tiles), dim3(kPntThreads), 0, ctx->stream, ctx->T,
+                       c.pnt_call, n, tile_min, ctx->pnt_fired);
     tmark(ctx, "pnt_resolve");
     HIP_TRY(ctx, hipGetLastError());
     return 0;
@@ -791,14 +826,16 @@ int ensure_pulse_scratch(tbg_ctx* ctx, uint64_t count) {
     PulseScratch& S = ctx->pulse;
     if (S.counters && count <= S.capacity) return 0;
     for (void* p : {(void*)S.keep, (void*)S.exp, (void*)S.ts, (void*)S.rows, (void*)S.exp_b,
-                    (void*)S.rows_b, (void*)S.counters})
+                    (void*)S.rows_b, (void*)S.counters, (void*)S.run_len, (void*)S.expired})
         if (p) (void)hipFree(p);
     S = PulseScratch();
-    const uint64_t cap = std::max<uint64_t>(count + count / 2, 1024);
+    const uint64_t want = std::max<uint64_t>(count + count / 2, 1024);
+    const uint64_t cap = (want + kPulseRun - 1) / kPulseRun * kPulseRun;
     if (!(dev_alloc(ctx, &S.keep, cap, false) && dev_alloc(ctx, &S.exp, cap, false) &&
           dev_alloc(ctx, &S.ts, cap, false) && dev_alloc(ctx, &S.rows, cap, false) &&
           dev_alloc(ctx, &S.exp_b, cap, false) && dev_alloc(ctx, &S.rows_b, cap, false) &&
-          dev_alloc(ctx, &S.counters, 3, false)))
+          dev_alloc(ctx, &S.run_len, 2 * (cap / kPulseRun + 1), false) &&
+          dev_alloc(ctx, &S.expired, 1, true) && dev_alloc(ctx, &S.counters, 4, false)))
         return TBG_ENOMEM;
     S.capacity = cap;
     return 0;
@@ -854,12 +891,7 @@ void free_ae_scratch(AeScratch& S) {
     S = AeScratch{};
 }
 
-int ensure_ae_scratch(tbg_ctx* ctx, uint64_t touches) {
-    if (touches <= ctx->ae_touch_cap) return 0;
-    AeScratch& S = ctx->ae;
-    free_ae_scratch(S);
-    ctx->ae_touch_cap = 0;
-    const uint64_t cap = std::max<uint64_t>(next_pow2(touches), 1u << 14);
+int alloc_ae_scratch(tbg_ctx* ctx, AeScratch& S, uint64_t cap) {
     const uint64_t slots = 2 * cap;  // grouping table load <= 0.5
     GroupPlan& G = S.G;
     if (!(dev_alloc(ctx, &S.deltas, cap, false) && dev_alloc(ctx, &G.hkeys, slots, true) &&
@@ -871,12 +903,31 @@ int ensure_ae_scratch(tbg_ctx* ctx, uint64_t touches) {
           dev_alloc(ctx, &S.chunk_tot, cap / kAeChunk + cap / kGroupSmall + 1, false)))
         return TBG_ENOMEM;
     G.hmask = slots - 1;
+    return 0;
+}
+
+int ensure_ae_scratch(tbg_ctx* ctx, uint64_t touches) {
+    if (touches <= ctx->ae_touch_cap) return 0;
+    free_ae_scratch(ctx->ae);
+    ctx->ae_touch_cap = 0;
+    const uint64_t cap = std::max<uint64_t>(next_pow2(touches), 1u << 14);
+    int rc = alloc_ae_scratch(ctx, ctx->ae, cap);
+    if (rc) return rc;
     ctx->ae_touch_cap = cap;
+    return 0;
+}
+
+// The call's stream waits for the side stream's appends (GPU-side; no host synchronisation).
+int ae_join(tbg_ctx* ctx) {
+    if (!ctx->ae_async_pending) return 0;
+    HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ae_done[ctx->ae_parity ^ 1], 0));
+    ctx->ae_async_pending = false;
     return 0;
 }
 
 // The host's view of the log (ae_used / ae_last_ts / ae_sorted) after the appends in flight.
 int ae_settle(tbg_ctx* ctx) {
+    if (int rc = ae_join(ctx)) return rc;
     if (!ctx->ae_pending) return 0;
     unsigned long long st[3] = {0, 0, 0};
     HIP_TRY(ctx, hipMemcpyAsync(st, ctx->ae_words + 4, 24, hipMemcpyDeviceToHost, ctx->stream));
@@ -890,6 +941,7 @@ int ae_settle(tbg_ctx* ctx) {
 
 // Sets the device's view of the log from the host's (open / restore / after a sort).
 int ae_publish(tbg_ctx* ctx) {
+    if (int rc = ae_join(ctx)) return rc;
     const unsigned long long st[3] = {ctx->ae_used, ctx->ae_last_ts, ctx->ae_sorted ? 0ull : 1ull};
     HIP_TRY(ctx, hipMemcpyAsync(ctx->ae_words + 4, st, 24, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // (`st` is a stack value)
@@ -908,6 +960,7 @@ template <typename Collect>
 int ae_append(tbg_ctx* ctx, uint32_t n_upper, const unsigned int* d_count, Collect collect,
               const char* mark = "account_events") {
     if (n_upper == 0) return 0;
+    if (int rc = ae_join(ctx)) return rc;
     if (ctx->ae_bound + n_upper > ctx->ae_cap) {
         int rc = ae_settle(ctx);
         if (rc) return rc;
@@ -949,8 +1002,123 @@ int ae_append(tbg_ctx* ctx, uint32_t n_upper, const unsigned int* d_count, Colle
     return 0;
 }
 
+// The side stream's appends of staging buffer p (ae_append's sequence over the staging, at its
+// fixed upper bound kAeAsyncMax): number the created events, copy and group, place, emit. The two
+// chained scans use their own status words and ticket (ae_g_words[7 ..]), which ae_scatter_tail
+// clears for the next append.
+int ae_launch_appends(tbg_ctx* ctx, uint32_t p) {
+    AeScratch S = ctx->ae_g;
+    S.state = ctx->ae_words + 4;
+    S.pos = nullptr;
+    AeScratch Se = S;  // the emit kernels: the block's base (kept by ae_scatter_tail), event-
+    Se.state = ctx->ae_g_words + 2;  // numbered touches and the staged deltas
+    Se.pos = ctx->ae_pos;
+    Se.deltas = ctx->ae_stage[p].delta;
+    unsigned int* d_count = reinterpret_cast<unsigned int*>(ctx->ae_g_words);
+    unsigned long long* scan_words = ctx->ae_g_words + 8;
+    unsigned int* ticket = reinterpret_cast<unsigned int*>(ctx->ae_g_words + 7);
+    const uint64_t slots = S.G.hmask + 1;
+    const uint32_t tiles1 = (kAeAsyncMax + kScanTile - 1) / kScanTile;
+    const uint32_t tiles2 = uint32_t((slots + kScanTile - 1) / kScanTile);
+    hipStream_t st = ctx->ae_stream;
+    hipLaunchKernelGGL(chained_scan<PositionsOf8>, dim3(tiles1), dim3(kScanThreads), 0, st,
+                       uint64_t(kAeAsyncMax), PositionsOf8{ctx->ae_stage[p].created, ctx->ae_pos, d_count},
+                       ScanState{scan_words, ticket, 0, 1});
+    hipLaunchKernelGGL(ae_copy_group, dim3((kAeAsyncMax + kPlanThreads - 1) / kPlanThreads),
+                       dim3(kPlanThreads), 0, st, ctx->ae_stage[p], ctx->ae_pos, S, ctx->ae_log,
+                       ctx->ae_ref);
+    hipLaunchKernelGGL(chained_scan<ExclusiveSumU32>, dim3(tiles2), dim3(kScanThreads), 0, st,
+                       slots, ExclusiveSumU32{S.G.hcnt, S.G.hoff, &S.G.counts[0]},
+                       ScanState{scan_words + tiles1, ticket, tiles1, 2});
+    const uint64_t pairs = 2 * uint64_t(kAeAsyncMax);
+    hipLaunchKernelGGL(ae_scatter_tail, dim3(grid_for(pairs)), dim3(kBlock), 0, st, S.G, pairs,
+                       ctx->ae_log, d_count, S.state, ctx->ae_g_words + 2, ctx->ae_g_words + 7,
+                       1 + tiles1 + tiles2);
+    hipLaunchKernelGGL(ae_group_small, dim3(grid_for(slots)), dim3(kBlock), 0, st, ctx->T, Se, slots,
+                       ctx->ae_log);
+    hipLaunchKernelGGL(ae_group_big_serial, dim3(2 * kAeAsyncMax / (kGroupMid + 1) + 1),
+                       dim3(kGroupBigThreads), 0, st, Se, ctx->ae_log);
+    HIP_TRY(ctx, hipGetLastError());
+    return 0;
+}
+
+int ensure_ae_async(tbg_ctx* ctx) {
+    if (ctx->ae_async_ready) return 0;
+    const uint64_t cap = 2 * uint64_t(kAeAsyncMax);
+    for (int p = 0; p < 2; p++) {
+        AeStage& st = ctx->ae_stage[p];
+        if (!(dev_alloc(ctx, &st.rec, kAeAsyncMax, false) && dev_alloc(ctx, &st.ref, kAeAsyncMax, false) &&
+              dev_alloc(ctx, &st.delta, 2 * kAeAsyncMax, false) &&
+              dev_alloc(ctx, &st.created, kAeAsyncMax, true)))
+            return TBG_ENOMEM;
+    }
+    if (!(dev_alloc(ctx, &ctx->ae_pos, kAeAsyncMax, false) && dev_alloc(ctx, &ctx->ae_g_words, 64, true)))
+        return TBG_ENOMEM;
+    if (int rc = alloc_ae_scratch(ctx, ctx->ae_g, cap)) return rc;
+    // (the scans' words: 8 + tiles of both scans)
+    if ((cap * 2 + kScanTile - 1) / kScanTile + (kAeAsyncMax + kScanTile - 1) / kScanTile + 8 > 64)
+        return TBG_EINVAL;
+    HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->ae_stream, hipStreamNonBlocking));
+    for (int p = 0; p < 2; p++) {
+        HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ae_snap_ready[p], hipEventDisableTiming));
+        HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ae_done[p], hipEventDisableTiming));
+    }
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // (the scratch's zeroing)
+    ctx->ae_async_ready = true;
+    return 0;
+}
+
+// Can call c's appends go to the side stream? (a small call; the log's capacity checked on the
+// host's upper bound; not while kernels are being timed)
+bool ae_async_ok(const tbg_ctx* ctx, uint32_t n) {
+    return ctx->ae_log && ctx->ae_async && !ctx->timing && n <= kAeAsyncMax &&
+           ctx->ae_bound + n <= ctx->ae_cap;
+}
+
+// The snapshot job of the next small call (buffer ctx->ae_parity), after the call's stream waited
+// for that buffer's previous graph.
+int ae_snap_job(tbg_ctx* ctx, const Call<tb_transfer_t>& c, AeSnapJob* J) {
+    if (int rc = ensure_ae_async(ctx)) return rc;
+    const uint32_t p = ctx->ae_parity;
+    if (ctx->ae_done_recorded[p]) HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ae_done[p], 0));
+    *J = AeSnapJob{ctx->T, c, ctx->ae_stage[p], true};
+    return 0;
+}
+
+// The side stream appends staging buffer p once the call's stream reaches this point.
+int ae_launch_graph(tbg_ctx* ctx) {
+    const uint32_t p = ctx->ae_parity;
+    HIP_TRY(ctx, hipEventRecord(ctx->ae_snap_ready[p], ctx->stream));
+    HIP_TRY(ctx, hipStreamWaitEvent(ctx->ae_stream, ctx->ae_snap_ready[p], 0));
+    if (int rc = ae_launch_appends(ctx, p)) return rc;
+    HIP_TRY(ctx, hipEventRecord(ctx->ae_done[p], ctx->ae_stream));
+    ctx->ae_done_recorded[p] = true;
+    ctx->ae_parity = p ^ 1;
+    ctx->ae_async_pending = true;
+    return 0;
+}
+
+// AccountEvents of a small create_transfers call behind the next call. When no replay ran, the
+// call's stage_out took the snapshot and the graph is already queued behind it; else the snapshot
+// is taken now (the speculative graph found no created flags and appended nothing).
+int ae_transfers_async(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
+    if (!ctx->ae_snap_early) {
+        AeSnapJob J;
+        if (int rc = ae_snap_job(ctx, c, &J)) return rc;
+        hipLaunchKernelGGL(ae_snapshot, dim3(kAeAsyncMax / kBlock), dim3(kBlock), 0, ctx->stream, J);
+        HIP_TRY(ctx, hipGetLastError());
+        if (int rc = ae_launch_graph(ctx)) return rc;
+    }
+    ctx->ae_snap_early = false;
+    ctx->ae_bound += c.n;
+    ctx->ae_pending = true;
+    return 0;
+}
+
 // AccountEvents of a create_transfers call: its created events in call order.
 int ae_transfers(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
+    if (ae_async_ok(ctx, c.n)) return ae_transfers_async(ctx, c);
+    ctx->ae_snap_early = false;
     unsigned int* d_count = reinterpret_cast<unsigned int*>(ctx->ae_words);
     int rc = launch_scan(ctx, c.n, SelectCreated{c.results, ctx->ae_list, d_count});
     if (rc) return rc;
@@ -964,13 +1132,14 @@ int ae_transfers(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
 }
 
 // AccountEvents of a pulse: the expired rows in expiry order.
+// (m: the count, or its upper bound when d_count holds it on device)
 int ae_expiry(tbg_ctx* ctx, const uint64_t* rows, uint64_t m, uint64_t timestamp,
-              const uint64_t* d_stamps = nullptr) {
-    return ae_append(ctx, uint32_t(m), nullptr, [&](const AeScratch& S, tb_account_event_t* log,
+              const uint64_t* d_stamps = nullptr, const unsigned int* d_count = nullptr) {
+    return ae_append(ctx, uint32_t(m), d_count, [&](const AeScratch& S, tb_account_event_t* log,
                                                     AeRef* refs) {
         hipLaunchKernelGGL(ae_collect_expiry, dim3((uint32_t(m) + kPlanThreads - 1) / kPlanThreads),
-                           dim3(kPlanThreads), 0, ctx->stream, ctx->T, rows, uint32_t(m), timestamp,
-                           d_stamps, S, log, refs);
+                           dim3(kPlanThreads), 0, ctx->stream, ctx->T, rows, uint32_t(m), d_count,
+                           timestamp, d_stamps, S, log, refs);
     }, "pulse:account_events");
 }
 
@@ -1021,15 +1190,62 @@ int ae_sort_log(tbg_ctx* ctx) {
     return ae_publish(ctx);
 }
 
-bool is_registered(const tbg_ctx* ctx, const void* p, uint64_t bytes) {
+// The GPU's address of host range [p, p + bytes) if it lies in a registered range, else null.
+template <typename T>
+T* mapped(const tbg_ctx* ctx, T* p, uint64_t bytes) {
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);
     for (const auto& r : ctx->registered)
-        if (a >= r.first && a + bytes <= r.first + r.second) return true;
-    return false;
+        if (a >= r.host && a + bytes <= r.host + r.size) return reinterpret_cast<T*>(r.dev + (a - r.host));
+    return nullptr;
+}
+bool is_registered(const tbg_ctx* ctx, const void* p, uint64_t bytes) {
+    return mapped(ctx, p, bytes) != nullptr;
+}
+
+// A host-buffer call's inputs into HBM: the batch ends / timestamps from the pinned staging and,
+// when the body lies in a registered range, the body itself -- one kernel on the call's stream
+// (hostio.hpp); an unregistered body takes hipMemcpyAsync.
+int stage_call_inputs(tbg_ctx* ctx, const void* events, uint64_t bytes, uint32_t nb,
+                      bool reset_scalars, bool ingest_reads_host = false) {
+    const uint4* src = mapped(ctx, static_cast<const uint4*>(events), bytes);
+    ctx->events_host = nullptr;
+    if (src && ingest_reads_host) {  // (tr_ingest reads the body itself and leaves the copy)
+        ctx->events_host = reinterpret_cast<const tb_transfer_t*>(src);
+        src = nullptr;
+        bytes = 0;
+    }
+    if (!src && bytes)
+        HIP_TRY(ctx, hipMemcpyAsync(ctx->d_events, events, bytes, hipMemcpyHostToDevice, ctx->stream));
+    StageIn s{src, reinterpret_cast<uint4*>(ctx->d_events), bytes / 16, ctx->dh_batch_ends,
+              ctx->d_batch_ends, ctx->dh_batch_ts, ctx->d_batch_ts, nb,
+              reset_scalars ? ctx->d_scalars : nullptr};
+    const uint64_t per_block = uint64_t(kStageThreads) * kStageWords;
+    const uint32_t grid = src ? uint32_t(std::max<uint64_t>(1, (s.words + per_block - 1) / per_block)) : 1;
+    hipLaunchKernelGGL(stage_in, dim3(grid), dim3(kStageThreads), 0, ctx->stream, s);
+    HIP_TRY(ctx, hipGetLastError());
+    return 0;
+}
+
+// Results (n > 0) and / or the scalars block to mapped host memory, as one kernel on the stream.
+int stage_call_outputs(tbg_ctx* ctx, const tb_create_result_t* d_results, tb_create_result_t* dst,
+                       uint32_t n, bool scalars, const AeSnapJob* snap) {
+    StageOut s{reinterpret_cast<const uint4*>(d_results), reinterpret_cast<uint4*>(dst), n,
+               scalars ? reinterpret_cast<const unsigned long long*>(ctx->d_scalars) : nullptr,
+               reinterpret_cast<unsigned long long*>(ctx->dh_scalars),
+               uint32_t(sizeof(DevScalars) / 8)};
+    if (!dst || !n) s.src = nullptr;
+    AeSnapJob J{};
+    if (snap) J = *snap;
+    const uint32_t items = std::max<uint32_t>(n, snap ? kAeAsyncMax : 0);
+    const uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>((items + kStageThreads - 1) / kStageThreads, 1024));
+    hipLaunchKernelGGL(stage_out, dim3(grid), dim3(kStageThreads), 0, ctx->stream, s, J);
+    HIP_TRY(ctx, hipGetLastError());
+    return 0;
 }
 
 int upload_batches(tbg_ctx* ctx, uint32_t n, const uint32_t* batch_lens, const uint64_t* batch_ts,
-                   uint32_t nb) {
+                   uint32_t nb, const void* events, uint64_t event_bytes, bool reset_scalars,
+                   bool ingest_reads_host = false) {
     if (nb == 0 || nb > ctx->opt.batch_count_max) return TBG_EINVAL;
     // (the pinned staging is free: the previous call's copies completed before it returned)
     uint64_t total = 0;
@@ -1039,11 +1255,8 @@ int upload_batches(tbg_ctx* ctx, uint32_t n, const uint32_t* batch_lens, const u
         ctx->h_batch_ts[b] = batch_ts[b];
     }
     if (total != n) return TBG_EINVAL;
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->d_batch_ends, ctx->h_batch_ends, nb * 4,
-                                hipMemcpyHostToDevice, ctx->stream));
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->d_batch_ts, ctx->h_batch_ts, nb * 8, hipMemcpyHostToDevice,
-                                ctx->stream));
-    return 0;
+    return stage_call_inputs(ctx, events, uint64_t(n) * event_bytes, nb, reset_scalars,
+                             ingest_reads_host);
 }
 
 int64_t lookup_impl(tbg_ctx* ctx, const tb_uint128_t* ids, uint32_t n, void* out, bool accounts) {
@@ -1093,7 +1306,7 @@ extern "C" {
 tbg_ctx* tbg_open(const tbg_options* options) {
     if (!options || options->account_capacity == 0 || options->transfer_capacity == 0 ||
         options->batch_events_max == 0 || options->batch_count_max == 0 ||
-        options->pulse_batch_max == 0)
+        options->pulse_batch_max == 0 || options->pulse_batch_max > kPulseRun)
         return nullptr;
     // Slots and rows are addressed with 32-bit indexes in per-event scratch.
     if (options->account_capacity >= (1ull << 31) || options->transfer_capacity >= (1ull << 31))
@@ -1138,7 +1351,7 @@ tbg_ctx* tbg_open(const tbg_options* options) {
          dev_alloc(ctx, &ctx->ev_cr, ev_max, false) && dev_alloc(ctx, &ctx->ev_amount, ev_max, false) &&
          dev_alloc(ctx, &ctx->ev_info, ev_max, false) && dev_alloc(ctx, &ctx->ev_slow, ev_max, false) &&
          dev_alloc(ctx, &ctx->slow_list, ev_max, false) &&
-         dev_alloc(ctx, &ctx->pnt_call, ev_max, false) && dev_alloc(ctx, &ctx->pnt_fired, 1, true) &&
+         dev_alloc(ctx, &ctx->pnt_call, ev_max, false) && dev_alloc(ctx, &ctx->pnt_fired, 2, true) &&
          dev_alloc(ctx, &ctx->pv_slots, next_pow2(2 * uint64_t(ev_max)), true);
     ctx->pv_mask = next_pow2(2 * uint64_t(ev_max)) - 1;
     // (2 * ev_max items, at least ev_max u64 of lookup scratch)
@@ -1174,6 +1387,14 @@ tbg_ctx* tbg_open(const tbg_options* options) {
                                          size_t(std::max<uint64_t>(ev_max, 1)) *
                                              sizeof(tb_create_result_t)),
                       "hipHostMalloc");
+    ok = ok && hip_ok(ctx, hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->dh_scalars),
+                                                   ctx->h_scalars, 0), "hipHostGetDevicePointer") &&
+         hip_ok(ctx, hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->dh_results),
+                                             ctx->h_results, 0), "hipHostGetDevicePointer") &&
+         hip_ok(ctx, hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->dh_batch_ends),
+                                             ctx->h_batch_ends, 0), "hipHostGetDevicePointer") &&
+         hip_ok(ctx, hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->dh_batch_ts),
+                                             ctx->h_batch_ts, 0), "hipHostGetDevicePointer");
     if (!ok) {
         fprintf(stderr, "tbg_open: %s\n", ctx->error.c_str());
         tbg_close(ctx);
@@ -1185,6 +1406,7 @@ tbg_ctx* tbg_open(const tbg_options* options) {
     T.expiry_capacity = tr_cap;
     T.undo_capacity = undo_cap;
     T.scalars = ctx->d_scalars;
+    ctx->ae_async = getenv("TBG_AE_SYNC") == nullptr;
     T.acc_ts_index = ctx->acc_ts_index;
     T.tr_ts_index = ctx->tr_ts_index;
     DevScalars init{};
@@ -1200,7 +1422,19 @@ tbg_ctx* tbg_open(const tbg_options* options) {
 
 void tbg_close(tbg_ctx* ctx) {
     if (!ctx) return;
+    if (ctx->ae_stream) (void)hipStreamSynchronize(ctx->ae_stream);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    for (int p = 0; p < 2; p++) {
+        if (ctx->ae_snap_ready[p]) (void)hipEventDestroy(ctx->ae_snap_ready[p]);
+        if (ctx->ae_done[p]) (void)hipEventDestroy(ctx->ae_done[p]);
+        for (void* q : {(void*)ctx->ae_stage[p].rec, (void*)ctx->ae_stage[p].ref,
+                        (void*)ctx->ae_stage[p].delta, (void*)ctx->ae_stage[p].created})
+            if (q) (void)hipFree(q);
+    }
+    if (ctx->ae_pos) (void)hipFree(ctx->ae_pos);
+    if (ctx->ae_g_words) (void)hipFree(ctx->ae_g_words);
+    free_ae_scratch(ctx->ae_g);
+    if (ctx->ae_stream) (void)hipStreamDestroy(ctx->ae_stream);
     void* ptrs[] = {ctx->idx_dirty, ctx->idx_counters, ctx->T.acc_index.entries, ctx->T.acc_entry_of, ctx->T.acc.slots, ctx->T.acc_rows, ctx->T.acc_live, ctx->T.acc_hot,
                     ctx->T.acc_closable, ctx->T.tr.slots, ctx->T.tr_rows, ctx->T.tr_live,
                     ctx->T.tr_status, ctx->T.expiry, ctx->d_scalars, ctx->T.undo, ctx->d_events,
@@ -1212,6 +1446,7 @@ void tbg_close(tbg_ctx* ctx) {
                     ctx->cub_temp, ctx->acc_ts_index, ctx->tr_ts_index, ctx->sel_buf,
                     ctx->pulse.keep, ctx->pulse.exp, ctx->pulse.ts, ctx->pulse.rows,
                     ctx->pulse.exp_b, ctx->pulse.rows_b, ctx->pulse.counters,
+                    ctx->pulse.run_len, ctx->pulse.expired,
                     ctx->flow.dup_mark, ctx->flow.counts, ctx->flow.words, ctx->flow.lane_counts,
                     ctx->scan_status, ctx->scan_ticket,
                     ctx->flow.lane_undo, ctx->flow.engine, ctx->flow.acc_free,
@@ -1226,7 +1461,7 @@ void tbg_close(tbg_ctx* ctx) {
     if (ctx->h_results) (void)hipHostFree(ctx->h_results);
     if (ctx->h_batch_ends) (void)hipHostFree(ctx->h_batch_ends);
     if (ctx->h_batch_ts) (void)hipHostFree(ctx->h_batch_ts);
-    for (const auto& r : ctx->registered) (void)hipHostUnregister(reinterpret_cast<void*>(r.first));
+    for (const auto& r : ctx->registered) (void)hipHostUnregister(reinterpret_cast<void*>(r.host));
     if (ctx->results_ready) (void)hipEventDestroy(ctx->results_ready);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -1300,7 +1535,23 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
                                         ctx->stream), "memset") ? 0 : TBG_EHIP;
     }
     if (!rc && n_batches > kChunkBatchMask) rc = TBG_EINVAL;
-    if (!rc) {
+    // Small calls whose scalar words the host-buffer staging already reset: each ingest wave
+    // finds its chunk's batch bounds itself (no tr_chunk_info launch).
+    const bool inline_chunks = ctx->scalars_reset && n <= kInlineChunkMax;
+    ctx->scalars_reset = false;
+    if (!rc && inline_chunks) {
+        c.chunk_info = nullptr;
+        Call<tb_transfer_t> ci = c;
+        if (ctx->events_host) {
+            ci.events = ctx->events_host;
+            ci.events_out = const_cast<tb_transfer_t*>(c.events);
+        }
+        hipLaunchKernelGGL(tr_ingest, dim3(ig), block, 0, ctx->stream, ctx->T, ci);
+        tmark(ctx, "tr_ingest");
+        hipLaunchKernelGGL(tr_commit, grid, block, 0, ctx->stream, ctx->T, c);
+        tmark(ctx, "tr_commit");
+        rc = hip_ok(ctx, hipGetLastError(), "launch") ? 0 : TBG_EHIP;
+    } else if (!rc) {
         c.chunk_info = ctx->chunk_info;
         hipLaunchKernelGGL(tr_chunk_info, dim3(grid_for((n + 63) / 64)), block, 0, ctx->stream, c,
                            ctx->chunk_info, ctx->d_scalars);
@@ -1371,19 +1622,27 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
     }
     // A host-buffer call's results are queued for download here, so that one host
     // synchronisation covers them when the call needs no replay (else they are downloaded again).
-    if (!rc && ctx->early_dst) {
-        tb_create_result_t* dst = is_registered(ctx, ctx->early_dst, uint64_t(n) * 16)
-                                      ? ctx->early_dst : ctx->h_results;
-        rc = hip_ok(ctx, hipMemcpyAsync(dst, d_results, size_t(n) * 16, hipMemcpyDeviceToHost,
-                                        ctx->stream), "results copy") ? 0 : TBG_EHIP;
-    }
     // One host synchronisation: does the call need the ordered replay (and, with imported events,
-    // the accounts' timestamp index)?
+    // the accounts' timestamp index)? One kernel writes the scalars and, for a host-buffer call,
+    // its results to mapped host memory (the registered destination, or the pinned staging).
     if (!rc) {
-        rc = sync_scalars(ctx);
+        tb_create_result_t* dst = nullptr;
+        if (ctx->early_dst) {
+            dst = mapped(ctx, ctx->early_dst, uint64_t(n) * 16);
+            if (!dst) dst = ctx->dh_results;
+        }
+        // (a small call's AccountEvents snapshot rides along: final unless a replay follows)
+        AeSnapJob J;
+        const bool snap = ae_async_ok(ctx, n) && !(rc = ae_snap_job(ctx, c, &J));
+        if (!rc) rc = stage_call_outputs(ctx, d_results, dst, dst ? n : 0, true, snap ? &J : nullptr);
+        // (its graph queued now: the host's launch calls overlap the call's kernels)
+        if (!rc && snap) rc = ae_launch_graph(ctx);
+        ctx->ae_snap_early = snap && !rc;
+        if (!rc) rc = hip_ok(ctx, hipStreamSynchronize(ctx->stream), "sync") ? 0 : TBG_EHIP;
         tmark(ctx, "host_sync");
     }
     const bool replay = !rc && ctx->h_scalars->stats[0] > 0;
+    if (replay) ctx->ae_snap_early = false;
     ctx->early_done = !rc && ctx->early_dst && !replay;  // (only the replay rewrites results)
     if (replay && (ctx->h_scalars->flags & kFlagImported)) rc = check_imported_indexes(ctx, true);
     if (replay && !rc) rc = run_replay(ctx, c, true, false);
@@ -1409,10 +1668,11 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
 // the host waits for the results only, and the next call's work queues behind the appends on the
 // same stream. `early`: the results were already downloaded before the call's synchronisation.
 int download_results(tbg_ctx* ctx, tb_create_result_t* results, uint32_t n, bool early = false) {
-    const bool direct = is_registered(ctx, results, uint64_t(n) * 16);
+    tb_create_result_t* dst = mapped(ctx, results, uint64_t(n) * 16);
+    const bool direct = dst != nullptr;
     if (!early) {
-        HIP_TRY(ctx, hipMemcpyAsync(direct ? results : ctx->h_results, ctx->d_results,
-                                    size_t(n) * 16, hipMemcpyDeviceToHost, ctx->stream));
+        int rc = stage_call_outputs(ctx, ctx->d_results, direct ? dst : ctx->dh_results, n, false);
+        if (rc) return rc;
         HIP_TRY(ctx, hipEventRecord(ctx->results_ready, ctx->stream));
     }
     int rc = 0;
@@ -1509,10 +1769,11 @@ int tbg_create_transfers(tbg_ctx* ctx, const tb_transfer_t* events, uint32_t n,
     if (!ctx || n > ctx->opt.batch_events_max) return TBG_EINVAL;
     if (n == 0) return 0;
     const double t0 = ctx->timing_host ? now_ms() : 0;
-    int rc = upload_batches(ctx, n, batch_lens, batch_ts, nb);
+    // (stage_in resets the call's scalar words: no tr_chunk_info launch for a small call)
+    int rc = upload_batches(ctx, n, batch_lens, batch_ts, nb, events, 128, n <= kInlineChunkMax,
+                            n <= kInlineChunkMax);
     if (rc) return rc;
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->d_events, events, size_t(n) * 128, hipMemcpyHostToDevice,
-                                ctx->stream));
+    ctx->scalars_reset = n <= kInlineChunkMax;
     const double t1 = ctx->timing_host ? now_ms() : 0;
     ctx->ae_defer = true;
     ctx->early_dst = results;
@@ -1521,6 +1782,8 @@ int tbg_create_transfers(tbg_ctx* ctx, const tb_transfer_t* events, uint32_t n,
                                      nullptr);
     ctx->ae_defer = false;
     ctx->early_dst = nullptr;
+    ctx->scalars_reset = false;
+    ctx->events_host = nullptr;
     if (rc) {
         ctx->ae_deferred = false;
         return rc;
@@ -1541,10 +1804,8 @@ int tbg_create_accounts(tbg_ctx* ctx, const tb_account_t* events, uint32_t n,
                         tb_create_result_t* results) {
     if (!ctx || n > ctx->opt.batch_events_max) return TBG_EINVAL;
     if (n == 0) return 0;
-    int rc = upload_batches(ctx, n, batch_lens, batch_ts, nb);
+    int rc = upload_batches(ctx, n, batch_lens, batch_ts, nb, events, 128, false);
     if (rc) return rc;
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->d_events, events, size_t(n) * 128, hipMemcpyHostToDevice,
-                                ctx->stream));
     rc = tbg_create_accounts_device(ctx, reinterpret_cast<const tb_account_t*>(ctx->d_events), n,
                                     ctx->d_batch_ends, ctx->d_batch_ts, nb, ctx->d_results, nullptr);
     if (rc) return rc;
@@ -1564,42 +1825,49 @@ namespace {
 struct PulseGather {
     uint64_t cands = 0, kept = 0, next_unexpired = ~0ull;
 };
-int pulse_gather(tbg_ctx* ctx, uint64_t timestamp, bool sort, PulseGather* out) {
+// The expired candidates, their first min(candidates, k) in (expires_at, timestamp) order at
+// S.exp / S.rows (pulse.hpp: LDS-sorted runs, pairwise merges keeping the first k); the entries still
+// pending at S.keep; the counters on device. `out`: the counters on the host too (one sync).
+int pulse_select(tbg_ctx* ctx, uint64_t timestamp, uint32_t k, PulseGather* out) {
     int rc = sync_scalars(ctx);
     if (rc) return rc;
     const uint64_t count = std::min<uint64_t>(ctx->h_scalars->expiry_count, ctx->T.expiry_capacity);
     rc = ensure_pulse_scratch(ctx, count);
     if (rc) return rc;
     PulseScratch& S = ctx->pulse;
-    unsigned long long h_counters[3] = {0, 0, ~0ull};  // kept, candidates, next unexpired
-    HIP_TRY(ctx, hipMemcpyAsync(S.counters, h_counters, sizeof(h_counters), hipMemcpyHostToDevice,
-                                ctx->stream));
-    if (count)
+    hipLaunchKernelGGL(pulse_reset_counters, dim3(1), dim3(64), 0, ctx->stream, S.counters);
+    if (count) {
         hipLaunchKernelGGL(pulse_collect, dim3(grid_for(count)), dim3(kBlock), 0, ctx->stream,
                            ctx->T, timestamp, count, S.keep, &S.counters[0], S.exp, S.ts, S.rows,
                            &S.counters[1], &S.counters[2]);
+        const uint32_t runs = uint32_t((count + kPulseRun - 1) / kPulseRun);
+        const uint64_t lens = S.capacity / kPulseRun + 1;
+        PulseRuns A{S.exp, S.rows, S.run_len}, B{S.exp_b, S.rows_b, S.run_len + lens};
+        hipLaunchKernelGGL(pulse_sort_chunks, dim3(runs), dim3(kPulseThreads), 0, ctx->stream, A,
+                           S.counters, k);
+        uint32_t live = runs;
+        bool swapped = false;
+        while (live > 1) {
+            const uint32_t next = (live + 1) / 2;
+            hipLaunchKernelGGL(pulse_merge, dim3(next), dim3(kPulseThreads), 0, ctx->stream, A,
+                               live, k, B);
+            std::swap(A, B);
+            swapped = !swapped;
+            live = next;
+        }
+        if (swapped) {  // (the result is in the second buffers: they become the first)
+            std::swap(S.exp, S.exp_b);
+            std::swap(S.rows, S.rows_b);
+        }
+    }
     HIP_TRY(ctx, hipGetLastError());
-    HIP_TRY(ctx, hipMemcpyAsync(h_counters, S.counters, sizeof(h_counters), hipMemcpyDeviceToHost,
-                                ctx->stream));
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    out->kept = h_counters[0];
-    out->cands = h_counters[1];
-    out->next_unexpired = h_counters[2];
-    const uint64_t cands = out->cands;
-    if (sort && cands > 1) {
-        size_t bytes = 0, bytes2 = 0;
-        HIP_TRY(ctx, hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, S.rows, S.rows_b, S.exp,
-                                                        S.exp_b, int(cands), 0, 64, ctx->stream));
-        HIP_TRY(ctx, hipcub::DeviceRadixSort::SortPairs(nullptr, bytes2, S.exp_b, S.exp, S.rows_b,
-                                                        S.rows, int(cands), 0, 64, ctx->stream));
-        rc = ensure_cub_temp(ctx, std::max(bytes, bytes2));
-        if (rc) return rc;
-        HIP_TRY(ctx, hipcub::DeviceRadixSort::SortPairs(ctx->cub_temp, bytes, S.rows, S.rows_b,
-                                                        S.exp, S.exp_b, int(cands), 0, 64,
-                                                        ctx->stream));
-        HIP_TRY(ctx, hipcub::DeviceRadixSort::SortPairs(ctx->cub_temp, bytes2, S.exp_b, S.exp,
-                                                        S.rows_b, S.rows, int(cands), 0, 64,
-                                                        ctx->stream));
+    if (out) {
+        unsigned long long h[3];
+        HIP_TRY(ctx, hipMemcpyAsync(h, S.counters, sizeof(h), hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        out->kept = h[0];
+        out->cands = h[1];
+        out->next_unexpired = h[2];
     }
     return 0;
 }
@@ -1610,7 +1878,7 @@ int pulse_finish(tbg_ctx* ctx, uint64_t expired, uint64_t kept, uint64_t pulse_n
     PulseScratch& S = ctx->pulse;
     if (expired)
         hipLaunchKernelGGL(pulse_apply, dim3(grid_for(expired)), dim3(kBlock), 0, ctx->stream,
-                           ctx->T, S.rows, expired);
+                           ctx->T, S.rows, expired, nullptr);
     HIP_TRY(ctx, hipGetLastError());
     // The index keeps the entries still pending (the ones just expired are dropped next time).
     if (kept)
@@ -1646,15 +1914,21 @@ extern "C" {
 int tbg_register_host(tbg_ctx* ctx, void* ptr, uint64_t size) {
     if (!ctx || !ptr || size == 0) return TBG_EINVAL;
     if (is_registered(ctx, ptr, size)) return 0;
-    HIP_TRY(ctx, hipHostRegister(ptr, size, hipHostRegisterDefault));
-    ctx->registered.emplace_back(reinterpret_cast<uintptr_t>(ptr), size);
+    HIP_TRY(ctx, hipHostRegister(ptr, size, hipHostRegisterMapped));
+    void* dev = nullptr;
+    if (hipHostGetDevicePointer(&dev, ptr, 0) != hipSuccess || !dev) {
+        (void)hipHostUnregister(ptr);
+        ctx->error = "hipHostGetDevicePointer";
+        return TBG_EHIP;
+    }
+    ctx->registered.push_back({reinterpret_cast<uintptr_t>(ptr), size, reinterpret_cast<uintptr_t>(dev)});
     return 0;
 }
 
 int tbg_unregister_host(tbg_ctx* ctx, void* ptr) {
     if (!ctx) return TBG_EINVAL;
     for (size_t i = 0; i < ctx->registered.size(); i++) {
-        if (ctx->registered[i].first != reinterpret_cast<uintptr_t>(ptr)) continue;
+        if (ctx->registered[i].host != reinterpret_cast<uintptr_t>(ptr)) continue;
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
         HIP_TRY(ctx, hipHostUnregister(ptr));
         ctx->registered.erase(ctx->registered.begin() + long(i));
@@ -1672,37 +1946,39 @@ int tbg_synchronize(tbg_ctx* ctx) {
 int64_t tbg_pulse(tbg_ctx* ctx, uint64_t timestamp) {
     if (!ctx) return TBG_EINVAL;
     FAILED_GUARD(ctx);
-    PulseGather G;
-    const uint64_t batch_max = ctx->opt.pulse_batch_max;
-    // AccountEvents are stamped in expiry order: the candidates must be in index order.
-    int rc = pulse_gather(ctx, timestamp, ctx->ae_log != nullptr, &G);
+    const uint32_t k = uint32_t(ctx->opt.pulse_batch_max);
+    // The scan stops with buffer_finished after batch_max values (:4969-4999): the first batch_max
+    // candidates in index order expire; everything after the host's first sync stays on device.
+    int rc = pulse_select(ctx, timestamp, k, nullptr);
     if (rc) return rc;
-    uint64_t expired = std::min<uint64_t>(G.cands, batch_max);
-    uint64_t pulse_next = G.next_unexpired == ~0ull ? TB_TIMESTAMP_MAX : G.next_unexpired;
-    if (G.cands >= batch_max) {
-        // The scan stops with buffer_finished after batch_max values: expire the first batch_max
-        // in index order; pulse_next_timestamp is the last one's expires_at (:4969-4999).
-        rc = pulse_gather(ctx, timestamp, true, &G);
-        if (rc) return rc;
-        uint64_t last = 0;
-        HIP_TRY(ctx, hipMemcpyAsync(&last, ctx->pulse.exp + (batch_max - 1), 8,
-                                    hipMemcpyDeviceToHost, ctx->stream));
-        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-        pulse_next = last;
+    PulseScratch& S = ctx->pulse;
+    const uint64_t count = std::min<uint64_t>(ctx->h_scalars->expiry_count, ctx->T.expiry_capacity);
+    const uint32_t upper = uint32_t(std::min<uint64_t>(count, k));
+    hipLaunchKernelGGL(pulse_settle, dim3(1), dim3(64), 0, ctx->stream, ctx->T, S.exp, S.counters,
+                       S.expired, k);
+    if (count) {
+        hipLaunchKernelGGL(pulse_keep_copy, dim3(std::min<uint32_t>(grid_for(count), kMaxGrid)),
+                           dim3(kBlock), 0, ctx->stream, ctx->T, S.keep, S.counters);
+        hipLaunchKernelGGL(pulse_apply, dim3(grid_for(upper)), dim3(kBlock), 0, ctx->stream, ctx->T,
+                           S.rows, uint64_t(upper), S.expired);
     }
-    rc = pulse_finish(ctx, expired, G.kept, pulse_next);
-    if (!rc && ctx->ae_log) rc = ae_expiry(ctx, ctx->pulse.rows, expired, timestamp);
-    return rc ? rc : int64_t(expired);
+    HIP_TRY(ctx, hipGetLastError());
+    if (ctx->ae_log && upper) rc = ae_expiry(ctx, S.rows, upper, timestamp, nullptr, S.expired);
+    if (rc) return rc;
+    unsigned int expired = 0;
+    HIP_TRY(ctx, hipMemcpyAsync(&expired, S.expired, 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return int64_t(expired);
 }
 
 int64_t tbg_pulse_candidates(tbg_ctx* ctx, uint64_t timestamp, uint64_t* expires_at,
                              uint64_t* timestamps, uint32_t max) {
     if (!ctx) return TBG_EINVAL;
     PulseGather G;
-    int rc = pulse_gather(ctx, timestamp, true, &G);
+    int rc = pulse_select(ctx, timestamp, std::min<uint32_t>(max, kPulseRun), &G);
     if (rc) return rc;
     std::vector<uint64_t> e, t;
-    rc = pulse_keys(ctx, std::min<uint64_t>(G.cands, max), &e, &t);
+    rc = pulse_keys(ctx, std::min<uint64_t>({G.cands, max, kPulseRun}), &e, &t);
     if (rc) return rc;
     for (size_t i = 0; i < e.size(); i++) {
         if (expires_at) expires_at[i] = e[i];
@@ -1716,7 +1992,7 @@ int64_t tbg_pulse_cut(tbg_ctx* ctx, uint64_t timestamp, uint64_t cut_expires_at,
                       const uint64_t* event_timestamps) {
     if (!ctx) return TBG_EINVAL;
     PulseGather G;
-    int rc = pulse_gather(ctx, timestamp, true, &G);
+    int rc = pulse_select(ctx, timestamp, uint32_t(ctx->opt.pulse_batch_max), &G);
     if (rc) return rc;
     // The cut is at most the global batch_max-th key: this shard expires at most that many.
     std::vector<uint64_t> e, t;
@@ -1917,6 +2193,12 @@ int tbg_debug_serial_replay(tbg_ctx* ctx, int enable) {
     return 0;
 }
 
+int tbg_debug_ae_sync(tbg_ctx* ctx, int enable) {
+    if (!ctx) return TBG_EINVAL;
+    ctx->ae_async = enable == 0;
+    return 0;
+}
+
 int tbg_profile(tbg_ctx* ctx, int enable) {
     if (!ctx) return TBG_EINVAL;
     ctx->timing = enable == 1;
@@ -2094,6 +2376,7 @@ int64_t tbg_compact(tbg_ctx* ctx) {
     Tables& T = ctx->T;
     const uint64_t used = T.tr_rows_used;
     if (used == 0) return 0;
+    if (int rc = ae_join(ctx)) return rc;  // (the side stream's appends read transfer rows)
     HIP_TRY(ctx, hipMemcpyAsync(ctx->h_scalars, ctx->d_scalars, sizeof(DevScalars),
                                 hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
@@ -2116,15 +2399,8 @@ int64_t tbg_compact(tbg_ctx* ctx) {
     if (!rc) {
         hipLaunchKernelGGL(cmp_mark, dim3(grid_for(tr_slot_count(ctx))), dim3(kBlock), 0,
                            ctx->stream, T.tr, used, keep32);
-        size_t bytes = 0;
-        // (keep32[used] = 0: new_row[used] is the kept count)
-        if (hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, keep32, new_row, int(used + 1),
-                                             ctx->stream) != hipSuccess)
-            rc = TBG_EHIP;
-        if (!rc) rc = ensure_cub_temp(ctx, bytes);
-        if (!rc && hipcub::DeviceScan::ExclusiveSum(ctx->cub_temp, bytes, keep32, new_row,
-                                                    int(used + 1), ctx->stream) != hipSuccess)
-            rc = TBG_EHIP;
+        // (keep32[used] = 0: new_row[used] is the kept count; one chained scan, prims.hpp)
+        rc = launch_scan(ctx, used + 1, ExclusiveSumU32{keep32, new_row, nullptr});
         if (!rc && !(hip_ok(ctx, hipMemcpyAsync(&kept, new_row + used, 4, hipMemcpyDeviceToHost,
                                                 ctx->stream), "kept") &&
                      hip_ok(ctx, hipStreamSynchronize(ctx->stream), "sync")))
@@ -2225,6 +2501,7 @@ int64_t tbg_compact(tbg_ctx* ctx) {
 int tbg_checkpoint(tbg_ctx* ctx, const char* path) {
     if (!ctx || !path) return TBG_EINVAL;
     FAILED_GUARD(ctx);  // (never persist undefined tables)
+    if (int rc = ae_join(ctx)) return rc;
     HIP_TRY(ctx, hipMemcpyAsync(ctx->h_scalars, ctx->d_scalars, sizeof(DevScalars),
                                 hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));

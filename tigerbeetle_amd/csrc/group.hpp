@@ -95,6 +95,21 @@ __device__ inline uint32_t group_slot(const GroupPlan& G, uint64_t key) {
     }
 }
 
+// The slots of two keys: both home words are read (and, when empty, claimed) together -- one round
+// trip for the common case instead of one per key; collisions continue in group_slot.
+__device__ inline void group_slot2(const GroupPlan& G, uint64_t key0, uint64_t key1, uint32_t* s0,
+                                   uint32_t* s1) {
+    const unsigned long long tag0 = key0 + 1, tag1 = key1 + 1;
+    const uint64_t h0 = group_hash(key0) & G.hmask, h1 = group_hash(key1) & G.hmask;
+    unsigned long long w0 = G.hkeys[h0], w1 = G.hkeys[h1];
+    if (w0 == 0) w0 = atomicCAS(&G.hkeys[h0], 0ull, tag0);
+    if (w1 == 0 && !(h1 == h0 && tag1 == tag0)) w1 = atomicCAS(&G.hkeys[h1], 0ull, tag1);
+    else if (h1 == h0 && tag1 == tag0) w1 = 0;  // (the same key: w0's outcome decides both)
+    *s0 = (w0 == 0 || w0 == tag0) ? uint32_t(h0) : group_slot(G, key0);
+    if (h1 == h0 && tag1 == tag0) *s1 = *s0;
+    else *s1 = (w1 == 0 || w1 == tag1) ? uint32_t(h1) : group_slot(G, key1);
+}
+
 // Counting keys by slot within one workgroup (kPlanThreads lanes): each lane inserts its keys
 // (group_slot) and counts them in an LDS table of the workgroup's slots; then one global add per
 // slot turns the LDS counts into bases, and every pair gets its slot and rank. All lanes call the
@@ -111,9 +126,7 @@ __device__ inline void group_block_init(GroupBlock& B) {
     __syncthreads();
 }
 // Counts `key` in the workgroup: returns its LDS entry (*lrank: its rank among the workgroup's).
-__device__ inline uint32_t group_block_add(const GroupPlan& G, GroupBlock& B, uint64_t key,
-                                           uint32_t* lrank) {
-    const uint32_t slot = group_slot(G, key);
+__device__ inline uint32_t group_block_count(GroupBlock& B, uint32_t slot, uint32_t* lrank) {
     uint32_t h = uint32_t(mix64(slot)) & (kPlanLdsSlots - 1);
     while (true) {
         const uint32_t o = atomicCAS(&B.slot[h], kNone32, slot);
@@ -123,13 +136,24 @@ __device__ inline uint32_t group_block_add(const GroupPlan& G, GroupBlock& B, ui
     *lrank = atomicAdd(&B.count[h], 1u);
     return h;
 }
+__device__ inline uint32_t group_block_add(const GroupPlan& G, GroupBlock& B, uint64_t key,
+                                           uint32_t* lrank) {
+    return group_block_count(B, group_slot(G, key), lrank);
+}
 // One global add per slot of the workgroup: B.count becomes the slot's base.
+// (each lane's adds are issued together, then their results stored: one round trip per lane)
 __device__ inline void group_block_publish(const GroupPlan& G, GroupBlock& B) {
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < kPlanLdsSlots; i += kPlanThreads) {
+    constexpr uint32_t kPer = kPlanLdsSlots / kPlanThreads;
+    uint32_t base[kPer];
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; j++) {
+        const uint32_t i = threadIdx.x + j * kPlanThreads;
         const uint32_t slot = B.slot[i];
-        if (slot != kNone32) B.count[i] = atomicAdd(&G.hcnt[slot], B.count[i]);
+        base[j] = slot != kNone32 ? atomicAdd(&G.hcnt[slot], B.count[i]) : 0u;
     }
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; j++) B.count[threadIdx.x + j * kPlanThreads] = base[j];
     __syncthreads();
 }
 // Pair `pair`'s slot and rank (entry kNone32: no key).

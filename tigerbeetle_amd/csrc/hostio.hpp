@@ -1,0 +1,85 @@
+// Host-buffer calls without DMA-engine hand-offs. A replica's message bodies and replies live in
+// host memory (the message pool, tigerbeetle.zig:853-901); registered with the executor
+// (tbg_register_host) they are mapped into the GPU's address space, and these kernels move a call's
+// body into HBM and its results (plus the call's scalars block) back over PCIe on the call's own
+// stream. A hipMemcpyAsync between host and device memory runs on a DMA engine: each hand-off
+// between it and the compute queue costs ~8-10 us of idle time per copy, more than the 1 MB body
+// takes to cross PCIe (profiles/r03_commit/timeline.txt).
+#pragma once
+
+#include "events.hpp"
+
+namespace tbg {
+
+constexpr uint32_t kStageThreads = 256;
+constexpr uint32_t kStageWords = 4;  // 16-byte words per lane per pass (all loads issued first)
+
+struct StageIn {
+    const uint4* src;  // mapped host body, or null (the body came by hipMemcpyAsync)
+    uint4* dst;
+    uint64_t words;    // 16-byte words of the body
+    const uint32_t* ends_src;  // mapped pinned staging -> the call's device copies
+    uint32_t* ends_dst;
+    const uint64_t* ts_src;
+    uint64_t* ts_dst;
+    uint32_t nb;
+    DevScalars* reset;  // the call's scalar words to zero (the first kernel of a call), or null
+};
+
+__global__ void __launch_bounds__(kStageThreads) stage_in(StageIn s) {
+    const uint64_t tid = uint64_t(blockIdx.x) * kStageThreads + threadIdx.x;
+    const uint64_t stride = uint64_t(gridDim.x) * kStageThreads;
+    if (tid == 0 && s.reset) reset_call_scalars(s.reset);
+    if (blockIdx.x == 0)
+        for (uint32_t b = threadIdx.x; b < s.nb; b += kStageThreads) {
+            s.ends_dst[b] = s.ends_src[b];
+            s.ts_dst[b] = s.ts_src[b];
+        }
+    if (!s.src) return;
+    for (uint64_t w = tid; w < s.words; w += stride * kStageWords) {
+        uint4 v[kStageWords];
+#pragma unroll
+        for (uint32_t j = 0; j < kStageWords; j++) {
+            const uint64_t x = w + j * stride;
+            v[j] = x < s.words ? s.src[x] : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < kStageWords; j++) {
+            const uint64_t x = w + j * stride;
+            if (x < s.words) s.dst[x] = v[j];
+        }
+    }
+}
+
+struct StageOut {
+    const uint4* src;  // the call's results (16 B each), or null
+    uint4* dst;        // mapped host destination
+    uint32_t n;
+    const unsigned long long* scalars_src;  // the scalars block, or null
+    unsigned long long* scalars_dst;        // mapped pinned copy
+    uint32_t scalar_words;
+};
+
+// (+ a small call's AccountEvents staging, events.hpp, when J.on: the call's state is final here
+// unless its replay follows, in which case the executor stages it again after the replay)
+__global__ void __launch_bounds__(kStageThreads) stage_out(StageOut s, AeSnapJob J) {
+    const uint32_t tid = blockIdx.x * kStageThreads + threadIdx.x;
+    // Only when no event replays (stats[0], set by tr_commit): a replayed event's result is not
+    // final yet -- its slot may still read `created` from the speculation -- and the executor
+    // takes the snapshot again after the replay.
+    // (The graph behind it is already queued: with a replay pending it must find no created flag.)
+    if (J.on) {
+        const bool final = J.T.scalars->stats[0] == 0;
+        for (uint32_t k = tid; k < kAeAsyncMax; k += gridDim.x * kStageThreads) {
+            if (final) ae_snapshot_one(J, k);
+            else J.st.created[k] = 0;
+        }
+    }
+    if (s.scalars_src && blockIdx.x == 0)
+        for (uint32_t w = threadIdx.x; w < s.scalar_words; w += kStageThreads)
+            s.scalars_dst[w] = s.scalars_src[w];
+    if (s.src)
+        for (uint32_t i = tid; i < s.n; i += gridDim.x * kStageThreads) s.dst[i] = s.src[i];
+}
+
+}  // namespace tbg

@@ -738,19 +738,7 @@ constexpr uint32_t kChunkBatchMask = (1u << 30) - 1;
 constexpr uint32_t kChunkImported = 1u << 30;
 constexpr uint32_t kChunkPrevLinked = 1u << 31;
 
-// (Also resets the call's words of the scalars block -- flags, counters -- for tr_ingest: the first
-// kernel of a create_transfers call, so the call needs no separate memset.)
-__global__ void tr_chunk_info(Call<tb_transfer_t> c, uint4* out, DevScalars* scalars) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i == 0) {
-        scalars->flags = 0;
-        scalars->slow_count = 0;
-        for (int j = 0; j < 4; j++) scalars->stats[j] = 0;
-        scalars->spec_fast = 0;
-        scalars->spec_ts_max = 0;
-    }
-    const uint32_t base = i * 64;
-    if (base >= c.n) return;
+__device__ inline uint4 chunk_info_of(const Call<tb_transfer_t>& c, uint32_t base) {
     const uint32_t b0 = batch_of_guess(c.batch_ends, c.n_batches, c.n, base);
     const uint32_t end0 = c.batch_ends[b0];
     const uint32_t bstart0 = batch_start_of(c, b0);
@@ -758,7 +746,26 @@ __global__ void tr_chunk_info(Call<tb_transfer_t> c, uint4* out, DevScalars* sca
     uint32_t w = b0;
     if (c.events[bstart0].flags & TB_TRANSFER_IMPORTED) w |= kChunkImported;
     if (base > bstart0 && (c.events[base - 1].flags & TB_TRANSFER_LINKED)) w |= kChunkPrevLinked;
-    out[i] = make_uint4(w, end0, uint32_t(ts_base), uint32_t(ts_base >> 32));
+    return make_uint4(w, end0, uint32_t(ts_base), uint32_t(ts_base >> 32));
+}
+
+// The call's words of the scalars block (flags, counters), zero before tr_ingest.
+__device__ inline void reset_call_scalars(DevScalars* scalars) {
+    scalars->flags = 0;
+    scalars->slow_count = 0;
+    for (int j = 0; j < 4; j++) scalars->stats[j] = 0;
+    scalars->spec_fast = 0;
+    scalars->spec_ts_max = 0;
+}
+
+// (Also resets the call's words of the scalars block for tr_ingest: the first kernel of a
+// create_transfers call, so the call needs no separate memset.)
+__global__ void tr_chunk_info(Call<tb_transfer_t> c, uint4* out, DevScalars* scalars) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) reset_call_scalars(scalars);
+    const uint32_t base = i * 64;
+    if (base >= c.n) return;
+    out[i] = chunk_info_of(c, base);
 }
 
 // LDS image of a wave's 64 events: 144 bytes per event (128 + 16 of padding), so the lanes'
@@ -816,7 +823,8 @@ __global__ void __launch_bounds__(kBlock, TBG_INGEST_WG_PER_CU) tr_ingest(Tables
     if (base < c.n) load_chunk(base);
     for (; base < c.n; base += nw * 64) {
         const uint32_t ubase = __builtin_amdgcn_readfirstlane(base);
-        const uint4 ci = c.chunk_info[ubase >> 6];
+        // (small calls: the wave finds its chunk's bounds itself -- one launch fewer)
+        const uint4 ci = c.chunk_info ? c.chunk_info[ubase >> 6] : chunk_info_of(c, ubase);
         const uint32_t cnt = c.n - ubase < 64 ? c.n - ubase : 64;
         // One ds_write_b128 per part: each 8-lane group writes one event's 128 contiguous bytes,
         // which no two lanes share a bank of. (A uint4 store here was split into ds_write2_b64
@@ -876,6 +884,12 @@ __global__ void __launch_bounds__(kBlock, TBG_INGEST_WG_PER_CU) tr_ingest(Tables
         // completion (vmcnt(0)) before the second, serialising the 8 stores.
         uint4* dst = reinterpret_cast<uint4*>(T.tr_rows + c.row_base + base);
         const bool full = cnt == 64;
+        if (c.events_out) {  // (the body as submitted, for the call's later kernels)
+            uint4* cp = reinterpret_cast<uint4*>(c.events_out + base);
+#pragma unroll
+            for (int i = 0; i < 8; i++)
+                if (full || i * 64 + lane < cnt * 8) cp[i * 64 + lane] = q[i];
+        }
         const uint64_t ts_lane = ts_base + ubase + (lane >> 3);  // + 8 i: event i * 8 + lane / 8
 #pragma unroll
         for (int i = 0; i < 8; i++) {
@@ -1995,9 +2009,10 @@ __global__ void pulse_key_timestamps(Tables T, const uint64_t* rows, uint64_t n,
 }
 
 // execute_expire_pending_transfers (:4540-4626) for the selected rows.
-__global__ void pulse_apply(Tables T, const uint64_t* rows, uint64_t n) {
+// (n_dev: the count on device, n its upper bound)
+__global__ void pulse_apply(Tables T, const uint64_t* rows, uint64_t n, const unsigned int* n_dev) {
     const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+    if (i >= n || (n_dev && i >= *n_dev)) return;
     const uint64_t row = rows[i];
     const tb_transfer_t& p = T.tr_rows[row];
     const uint64_t dr_row = account_find(T, p.debit_account_id);

@@ -144,6 +144,9 @@ struct Call {
     // Calls with post/void: every pulse_next_timestamp update, per event (0: none; expires_at:
     // min; expires_at | kPntReset: reset-if-equal), resolved in call order after the replay.
     uint64_t* pnt_call;
+    // tr_ingest of a small host-buffer call reads the body straight from mapped host memory
+    // (`events`) and leaves a copy here for the call's later kernels (null: no copy).
+    tb_transfer_t* events_out;
     // create_transfers: per-call claims of pending ids by post/void events (epoch:32 | event + 1;
     // words of other epochs are free): the earliest post/void of a pending transfer in the call.
     unsigned long long* pv_slots;

@@ -117,6 +117,7 @@ SIGNATURES = [
     ("tbg_sum_overflows", ctypes.c_int, [vp, ctypes.c_uint32, vp, vp, ctypes.c_uint32, vp]),
     ("tbg_debug_force_replay", ctypes.c_int, [vp, ctypes.c_int]),
     ("tbg_debug_serial_replay", ctypes.c_int, [vp, ctypes.c_int]),
+    ("tbg_debug_ae_sync", ctypes.c_int, [vp, ctypes.c_int]),
     ("tbg_profile", ctypes.c_int, [vp, ctypes.c_int]),
     ("tbg_profile_read", ctypes.c_int, [vp, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32,
                                        ctypes.POINTER(ctypes.c_double), c_u64p]),

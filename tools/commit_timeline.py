@@ -125,7 +125,8 @@ def timeline(kernel_csv, copy_csv, last=6):
                              f"COPY {kind} {r.get('Size', '')}"))
     rows.sort()
     # the last `last` commits: from the last `last` tr_chunk_info launches on
-    starts = [i for i, r in enumerate(rows) if r[2].startswith("tr_chunk_info")]
+    anchor = "stage_in" if any(r[2].startswith("stage_in") for r in rows) else "tr_chunk_info"
+    starts = [i for i, r in enumerate(rows) if r[2].startswith(anchor)]
     if len(starts) < last + 1:
         return
     i0 = starts[-last - 1]
