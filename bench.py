@@ -85,6 +85,8 @@ def parse_args():
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="bounded CPU-oracle sample (rank 0, N=1)")
+    ap.add_argument("--no-account-events-line", action="store_true",
+                    help="skip the with_account_events measurement")
     ap.add_argument("--commit-reps", type=int, default=200,
                     help="8189-event commits timed for `per_commit` (0: skip)")
     ap.add_argument("--account-events", action="store_true",
@@ -454,6 +456,8 @@ def per_commit(args, lib, dev, g, wl, prepare_ts, id_base):
     device = {"events_per_commit": n, "commits": R, "transfers_per_s": round(n * R / t_all, 1),
               "us_per_commit_mean": round(t_all / R * 1e6, 1),
               "us_per_commit_p50": round(float(np.median(lat)) * 1e6, 1),
+              "us_per_commit_p90": round(float(np.percentile(lat, 90)) * 1e6, 1),
+              "us_per_commit_max": round(float(lat.max()) * 1e6, 1),
               "validated": bool(ok),
               "validation": "every result (status and timestamp), every transfer row",
               "note": "tbg_create_transfers_device, the body resident in HBM, one synchronous "
@@ -466,13 +470,13 @@ def per_commit(args, lib, dev, g, wl, prepare_ts, id_base):
     sm_opt.pulse_batch_max = 8190
     topt = native.TbgOptions()
     topt.account_capacity = wl.A if wl.name == "config2" else 1 << 21
-    topt.transfer_capacity = (R + 2) * n
+    topt.transfer_capacity = (R + 3) * n
     topt.batch_events_max = BATCH
     topt.batch_count_max = 64
     topt.pulse_batch_max = 8190
     topt.device = 0
     topt.pulse_next_timestamp_init = 1
-    topt.account_events_capacity = (R + 2) * n  # the drop-in records AccountEvents (CDC)
+    topt.account_events_capacity = (R + 3) * n  # the drop-in records AccountEvents (CDC)
     sm = lib.tb_sm_open_gpu(ctypes.byref(sm_opt), ctypes.byref(topt))
     if not sm:
         return {"device": device, "state_machine": None}, prepare_ts
@@ -517,16 +521,22 @@ def per_commit(args, lib, dev, g, wl, prepare_ts, id_base):
     # for direct DMA (tb_sm_register_buffer): one page-aligned pool holding every body here.
     first = encode(body_events)
     stride = (len(first) + 4095) // 4096 * 4096
-    pool_raw = np.zeros(R * stride + 4096, dtype=np.uint8)
+    # (body 0: one untimed warmup commit; bodies 1 .. R timed)
+    pool_raw = np.zeros((R + 1) * stride + 4096, dtype=np.uint8)
     off0 = (-pool_raw.ctypes.data) % 4096
-    pool = pool_raw[off0:off0 + R * stride]
-    for r in range(R):
+    pool = pool_raw[off0:off0 + (R + 1) * stride]
+    for r in range(R + 1):
         ev = body_events.copy()
         ev["id"][:, 0] += np.uint64(r * n + 1)
         b = encode(ev)
         pool[r * stride:r * stride + len(b)] = np.frombuffer(b, dtype=np.uint8)
     assert lib.tb_sm_register_buffer(sm, pool.ctypes.data, pool.nbytes) == 0
-    assert lib.tb_sm_register_buffer(sm, ctypes.addressof(out), len(out)) == 0
+    # (and one reply buffer per commit, so nothing is copied out inside the timed loop)
+    reply_stride = (16 * n + 256 + 4095) // 4096 * 4096
+    replies_raw = np.zeros((R + 1) * reply_stride + 4096, dtype=np.uint8)
+    off1 = (-replies_raw.ctypes.data) % 4096
+    replies_pool = replies_raw[off1:off1 + (R + 1) * reply_stride]
+    assert lib.tb_sm_register_buffer(sm, replies_pool.ctypes.data, replies_pool.nbytes) == 0
     body_size = len(first)
 
     def commit_pooled(r):
@@ -540,21 +550,23 @@ def per_commit(args, lib, dev, g, wl, prepare_ts, id_base):
         lib.tb_sm_prefetch(sm, cb, None, op_counter[0], op_counter[0], OP_CREATE_TRANSFERS, body,
                            body_size)
         size = lib.tb_sm_commit(sm, 1, 0, op_counter[0], ts, OP_CREATE_TRANSFERS, body, body_size,
-                                out)
+                                ctypes.c_void_p(replies_pool.ctypes.data + r * reply_stride))
         if size < 0:
             raise RuntimeError(f"tb_sm_commit: {size}")
         return ts
 
-    lat_sm = np.zeros(R)
-    commit_ts = np.zeros(R, dtype=np.uint64)
-    replies = np.zeros((R, 16 * n), dtype=np.uint8)
+    lat_sm = np.zeros(R + 1)
+    commit_ts = np.zeros(R + 1, dtype=np.uint64)
+    commit_ts[0] = commit_pooled(0)  # warmup (untimed)
+    lib.tbg_synchronize(lib.tb_sm_executor_gpu(sm))
     t_all = time.perf_counter()
-    for r in range(R):
+    for r in range(1, R + 1):
         t0 = time.perf_counter()
         commit_ts[r] = commit_pooled(r)
         lat_sm[r] = time.perf_counter() - t0
-        ctypes.memmove(replies[r].ctypes.data, out, 16 * n)
     t_all = time.perf_counter() - t_all
+    lat_sm = lat_sm[1:]
+    replies = replies_pool.reshape(R + 1, reply_stride)[:, :16 * n]
     # Validation after timing: every reply (each event created at ts - n + i + 1), every transfer
     # row (the event as submitted, stamped), and every touched account's balances (the exact
     # sums over the R bodies).
@@ -562,7 +574,7 @@ def per_commit(args, lib, dev, g, wl, prepare_ts, id_base):
     within = np.arange(n, dtype=np.uint64)
     ids = np.zeros((n, 2), dtype=np.uint64)
     rows = np.zeros(n, dtype=TRANSFER_DTYPE)
-    for r in range(R):
+    for r in range(R + 1):
         res = replies[r].view(RESULT_DTYPE)
         want_ts = commit_ts[r] - np.uint64(n) + within + np.uint64(1)
         sm_ok &= bool((res["status"] == CREATED).all() and (res["timestamp"] == want_ts).all())
@@ -589,15 +601,18 @@ def per_commit(args, lib, dev, g, wl, prepare_ts, id_base):
         z = min(len(touched), a + BATCH)
         sm_ok &= lib.tbg_lookup_accounts(g_sm, acc_ids[a:z].ctypes.data_as(ctypes.c_void_p), z - a,
                                          acc_rows[a:z].ctypes.data_as(ctypes.c_void_p)) == z - a
-    sm_ok &= bool((acc_rows["debits_posted"][:, 0] == exp_d * np.uint64(R)).all() and
-                  (acc_rows["credits_posted"][:, 0] == exp_c * np.uint64(R)).all() and
+    sm_ok &= bool((acc_rows["debits_posted"][:, 0] == exp_d * np.uint64(R + 1)).all() and
+                  (acc_rows["credits_posted"][:, 0] == exp_c * np.uint64(R + 1)).all() and
                   (acc_rows["debits_pending"] == 0).all() and (acc_rows["credits_pending"] == 0).all())
     n_events = lib.tbg_dump_account_events(g_sm, None)
-    sm_ok &= n_events == R * n  # one AccountEvent per created transfer
+    sm_ok &= n_events == (R + 1) * n  # one AccountEvent per created transfer
     lib.tb_sm_close(sm)
     smr = {"events_per_commit": n, "commits": R, "transfers_per_s": round(n * R / t_all, 1),
            "us_per_commit_mean": round(t_all / R * 1e6, 1),
            "us_per_commit_p50": round(float(np.median(lat_sm)) * 1e6, 1),
+           "us_per_commit_p90": round(float(np.percentile(lat_sm, 90)) * 1e6, 1),
+           "us_per_commit_p99": round(float(np.percentile(lat_sm, 99)) * 1e6, 1),
+           "us_per_commit_max": round(float(lat_sm.max()) * 1e6, 1),
            "body_bytes": body_size, "validated": bool(sm_ok),
            "validation": "every reply (status and timestamp), every transfer row byte for byte, "
                          "every touched account's balances, one AccountEvent per transfer",
@@ -606,6 +621,76 @@ def per_commit(args, lib, dev, g, wl, prepare_ts, id_base):
                    "the reply buffer registered once, tb_sm_register_buffer), AccountEvents "
                    "recorded"}
     return {"device": device, "state_machine": smr}, prepare_ts
+
+
+def account_events_line(args, lib, dev, wl, steps, d_ends, lens, N, A):
+    """Config 2's step with the AccountEvents groove recorded: a second executor, the same
+    accounts and the first three steps' inputs (HBM-resident, their own ids and timestamps), one
+    warmup + two timed steps. Validated: every result created, exactly one AccountEvent per
+    transfer. (The AccountEvents' contents are pinned by the GPU parity tests.)"""
+    opt = native.TbgOptions()
+    opt.account_capacity = A
+    opt.transfer_capacity = 3 * N
+    opt.batch_events_max = max(N, wl.chunk)
+    opt.batch_count_max = len(lens)
+    opt.pulse_batch_max = 8190
+    opt.device = 0
+    opt.pulse_next_timestamp_init = 1
+    opt.account_events_capacity = 3 * N
+    g2 = lib.tbg_open(ctypes.byref(opt))
+    if not g2:
+        return None
+    try:
+        prepare_ts = 0
+        for acc in wl.account_chunks():
+            res = np.zeros(len(acc), dtype=RESULT_DTYPE)
+            a_lens = np.asarray([len(acc)], dtype=np.uint32)
+            a_ts, prepare_ts = global_step_timestamps(prepare_ts, [len(acc)], 1, 0)
+            rc = lib.tbg_create_accounts(g2, acc.ctypes.data_as(ctypes.c_void_p), len(acc),
+                                         a_lens.ctypes.data_as(native.c_u32p),
+                                         a_ts.ctypes.data_as(native.c_u64p), 1,
+                                         res.ctypes.data_as(ctypes.c_void_p))
+            if rc != 0:
+                return None
+
+        def step(s):
+            d_ev, d_ts, d_res, _ = steps[s]
+            rc = lib.tbg_create_transfers_device(g2, d_ev, N, d_ends, d_ts, len(lens), d_res, None)
+            if rc != 0:
+                raise RuntimeError(f"with_account_events: {rc} {lib.tbg_last_error(g2)}")
+
+        step(0)
+        lib.tbg_profile(g2, 1)
+        lib.tbg_synchronize(g2)
+        t0 = time.perf_counter()
+        step(1)
+        step(2)
+        lib.tbg_synchronize(g2)
+        t = time.perf_counter() - t0
+        kms = {}
+        i = 0
+        name = ctypes.create_string_buffer(64)
+        ms, cnt = ctypes.c_double(), ctypes.c_uint64()
+        while lib.tbg_profile_read(g2, i, name, 64, ctypes.byref(ms), ctypes.byref(cnt)):
+            kms[name.value.decode()] = round(ms.value / 2, 4)
+            i += 1
+        lib.tbg_profile(g2, 0)
+        ok = True
+        r = np.zeros(N, dtype=RESULT_DTYPE)
+        for s in range(3):
+            dev.download(steps[s][2], r)
+            ok &= bool((r["status"] == CREATED).all())
+        n_ae = lib.tbg_dump_account_events(g2, None)
+        ok &= n_ae == 3 * N
+        return {"value": round(2 * N / t, 1), "unit": "transfers/s", "steps": 2, "warmup": 1,
+                "ms_per_step": round(t / 2 * 1e3, 3), "account_events_per_step": N,
+                "account_events_ms_per_step": kms.get("account_events"),
+                "kernels_ms_per_step": kms, "validated": bool(ok),
+                "validation": "every result created; one AccountEvent per transfer (3 steps)",
+                "note": "config 2's step with the account_events groove recorded (256-B "
+                        "AccountEvent per created transfer), a second executor"}
+    finally:
+        lib.tbg_close(g2)
 
 
 def routed_call(n_per_shard, world, accounts, seed, step):
@@ -908,6 +993,15 @@ def main():
                 "note": "one step through tbg_create_transfers with host buffers (events in, "
                         "results out over PCIe)"}
 
+    # The integrated drop-in records an AccountEvent for every created transfer
+    # (state_machine.zig:4417, "For CDC we always insert the history"): the same steps on a second
+    # executor with the account_events groove on (SURVEY.md §8d prices the 256-B AccountEvent
+    # separately, so `value` above is the executor without it).
+    with_ae = None
+    if (rank == 0 and world == 1 and not args.no_validate and not args.account_events and
+            wl.name == "config2" and W + K >= 3 and not args.no_account_events_line):
+        with_ae = account_events_line(args, lib, dev, wl, steps, d_ends, lens, N, A)
+
     commits = None
     if R > 0:
         commits, prepare_ts = per_commit(args, lib, dev, g, wl, prepare_ts,
@@ -974,6 +1068,7 @@ def main():
             "cpu_baseline": cpu,
             "pcie_inclusive": pcie,
             "per_commit": commits,
+            "with_account_events": with_ae,
         }
         if world > 1:
             line["routed"] = routed

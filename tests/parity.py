@@ -75,6 +75,7 @@ class Pair:
         self.calls = 0
         self.stats = {"events": 0, "fast": 0, "replayed": 0, "static_fail": 0}
         self.seconds = {"gpu": 0.0, "oracle": 0.0}  # wall time of each side's create_* calls
+        self.pulses = []  # per tbg_pulse: (wall seconds, transfers expired)
 
     def _apply_debug_modes(self):
         force_replay = self._force_replay
@@ -221,7 +222,9 @@ class Pair:
             # prepare(pulse): prepare_ts += 1 + batch_max.create_transfers (:1113).
             self.prepare_timestamp += 1 + self._pulse_delta
             ts = self.prepare_timestamp
+            t0 = time.perf_counter()
             eg = self.lib.tbg_pulse(self.g, ts)
+            self.pulses.append((time.perf_counter() - t0, eg))  # (wall seconds, expired)
             eo = self.olib.tbo_pulse(self.o, ts)
             if eg != eo:
                 raise ParityError(f"pulse at {ts}: gpu expired {eg}, oracle {eo}")

@@ -120,6 +120,10 @@ struct tbg_ctx {
     bool early_done = false;
     // The next create_transfers call's scalar words were reset by its staging kernel.
     bool scalars_reset = false;
+    // The call's scalar words are zero on device: the last create_transfers call queued
+    // tr_reset_scalars at its end and nothing has written them since (create_accounts and the
+    // other entry points that may clear this flag).
+    bool scalars_clean = true;
     // ... and its body is read by tr_ingest from mapped host memory (the GPU's address), null: the
     // body is in d_events.
     const tb_transfer_t* events_host = nullptr;
@@ -434,6 +438,7 @@ Call<Event> make_call(tbg_ctx* ctx, const Event* d_events, uint32_t n, const uin
 // zero_scalars: reset the per-call words of the scalars block (flags, slow_count, stats) here;
 // create_transfers resets them in its first kernel (tr_chunk_info) instead.
 int begin_call(tbg_ctx* ctx, bool zero_scalars = true) {
+    if (zero_scalars) ctx->scalars_clean = false;  // (the call's kernels write its scalar words)
     if (ctx->timing && ctx->n_marks > 1) {  // the previous call's AccountEvents (queued after it)
         (void)hipStreamSynchronize(ctx->stream);
         tcollect(ctx);
@@ -1417,6 +1422,12 @@ tbg_ctx* tbg_open(const tbg_options* options) {
         tbg_close(ctx);
         return nullptr;
     }
+    // (the side stream's staging and scratch now, not in the first small call)
+    if (ctx->ae_log && ctx->ae_async && ensure_ae_async(ctx) != 0) {
+        fprintf(stderr, "tbg_open: %s\n", ctx->error.c_str());
+        tbg_close(ctx);
+        return nullptr;
+    }
     return ctx;
 }
 
@@ -1537,8 +1548,9 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
     if (!rc && n_batches > kChunkBatchMask) rc = TBG_EINVAL;
     // Small calls whose scalar words the host-buffer staging already reset: each ingest wave
     // finds its chunk's batch bounds itself (no tr_chunk_info launch).
-    const bool inline_chunks = ctx->scalars_reset && n <= kInlineChunkMax;
+    const bool inline_chunks = (ctx->scalars_reset || ctx->scalars_clean) && n <= kInlineChunkMax;
     ctx->scalars_reset = false;
+    ctx->scalars_clean = false;
     if (!rc && inline_chunks) {
         c.chunk_info = nullptr;
         Call<tb_transfer_t> ci = c;
@@ -1655,6 +1667,10 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
         const double ta = ctx->timing_host ? now_ms() : 0;
         rc = ae_transfers(ctx, c);
         hprof(ctx, "host:account_events", now_ms() - ta);
+    }
+    if (!rc) {
+        hipLaunchKernelGGL(tr_reset_scalars, dim3(1), dim3(64), 0, ctx->stream, ctx->d_scalars);
+        ctx->scalars_clean = hip_ok(ctx, hipGetLastError(), "reset");
     }
     ctx->stream = saved;
     ctx->T.tr_rows_used += n;  // rows are consumed whether or not the events created objects

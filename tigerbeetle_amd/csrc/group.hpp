@@ -403,7 +403,8 @@ struct SegmentLds {
 
 // Sorts the c distinct values in[off, off + c) ascending into out[off, off + c) (one workgroup of
 // kGroupBigThreads; visible to the whole workgroup on return): bitmap windows of up to
-// kGroupWindowBits values in LDS over the values' range -- set bits, prefix popcounts, enumerate.
+// kGroupWindowBits values in LDS over the values' range -- set bits, prefix popcounts, enumerate --
+// or, for a sparse segment, an LDS bitonic sort of the values themselves.
 __device__ inline void segment_sort(const uint32_t* in, uint32_t* out, uint32_t off, uint32_t c,
                                     SegmentLds& L) {
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -428,6 +429,32 @@ __device__ inline void segment_sort(const uint32_t* in, uint32_t* out, uint32_t 
     for (uint32_t w = 1; w < kGroupBigThreads / 64; w++) {
         lo = min(lo, L.red_min[w]);
         hi = max(hi, L.red_max[w]);
+    }
+    // A sparse segment (its range many times its count: a call's touches of one account spread
+    // over the whole call) sorts faster as values than as a bitmap of its range: LDS bitonic
+    // sort of the next power of two >= c (kNone32 padding), when it fits the buffer.
+    uint32_t pw = 1;
+    while (pw < c) pw <<= 1;
+    if (pw <= kGroupLdsWords && uint64_t(hi - lo) + 1 > 64ull * pw) {
+        for (uint32_t i = tid; i < pw; i += kGroupBigThreads) buf[i] = i < c ? in[off + i] : kNone32;
+        __syncthreads();
+        for (uint32_t size = 2; size <= pw; size <<= 1) {
+            for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+                for (uint32_t t = tid; t < pw / 2; t += kGroupBigThreads) {
+                    const uint32_t a = 2 * t - (t & (stride - 1)), b = a + stride;
+                    const uint32_t x = buf[a], y = buf[b];
+                    if ((x > y) == ((a & size) == 0)) {
+                        buf[a] = y;
+                        buf[b] = x;
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        for (uint32_t i = tid; i < c; i += kGroupBigThreads) out[off + i] = buf[i];
+        __threadfence();
+        __syncthreads();
+        return;
     }
     uint32_t placed = 0;
     for (uint64_t wb = lo; wb <= hi; wb += kGroupWindowBits) {

@@ -758,6 +758,12 @@ __device__ inline void reset_call_scalars(DevScalars* scalars) {
     scalars->spec_ts_max = 0;
 }
 
+// The call's scalar words zeroed at the end of a call (queued behind it, while the host returns):
+// the next small call needs neither tr_chunk_info nor a memset before its tr_ingest.
+__global__ void tr_reset_scalars(DevScalars* scalars) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) reset_call_scalars(scalars);
+}
+
 // (Also resets the call's words of the scalars block for tr_ingest: the first kernel of a
 // create_transfers call, so the call needs no separate memset.)
 __global__ void tr_chunk_info(Call<tb_transfer_t> c, uint4* out, DevScalars* scalars) {

@@ -39,6 +39,19 @@ def kernel_ms(p):
     return out
 
 
+def pulse_line(p):
+    """The pulses between the calls (tbg_pulse, host-timed: the call's own synchronisations
+    included): how many, the transfers they expired, the mean wall time per pulse."""
+    if not p.pulses:
+        return None
+    secs = [t for t, _ in p.pulses]
+    expired = sum(e for _, e in p.pulses)
+    return {"pulses": len(p.pulses), "expired": expired,
+            "us_per_pulse_mean": round(sum(secs) / len(secs) * 1e6, 1),
+            "us_per_pulse_max": round(max(secs) * 1e6, 1),
+            "expired_per_s": round(expired / sum(secs), 1) if sum(secs) else None}
+
+
 def line(name, p, n, t_wall, extra):
     kms = kernel_ms(p)
     extra = dict(extra, kernels_ms=kms)
@@ -54,7 +67,8 @@ def line(name, p, n, t_wall, extra):
             "oracle_transfers_per_s": round(n / s["oracle"], 1), "oracle_cores": 1,
             "gpu_s": round(s["gpu"], 3), "oracle_s": round(s["oracle"], 3),
             "replayed": p.stats["replayed"], "fast": p.stats["fast"],
-            "static_fail": p.stats["static_fail"], "wall_s": round(t_wall, 1), **extra}
+            "static_fail": p.stats["static_fail"], "wall_s": round(t_wall, 1),
+            "pulse": pulse_line(p), **extra}
 
 
 def run(config, n, batches):
@@ -65,6 +79,7 @@ def run(config, n, batches):
     def start():
         p.seconds = {"gpu": 0.0, "oracle": 0.0}
         p.stats = {k: 0 for k in p.stats}
+        p.pulses = []
         p.lib.tbg_profile(p.g, 1)
 
     try:
