@@ -812,3 +812,72 @@ def test_fast_post_void_and_chains(seed, mode, monkeypatch):
             p.compare_state()
     finally:
         p.close()
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_doomed_debits(seed, monkeypatch):
+    """The flow plan's doomed debits (group.hpp: a replayed debit of a debits_must_not_exceed_credits
+    account that fails in any order gets no key on that account): limited accounts with some
+    starting credit, debits above and below what the call's credits could ever cover, credits to
+    them in the same call (bounding the rule), pending debits, posts / voids of their pending
+    transfers (which turn the rule off for the account), linked chains holding doomed debits --
+    every call against the oracle, and once more with the rule off (TBG_NO_DOOM)."""
+    rng = np.random.default_rng(500 + seed)
+    for doom in (True, False):
+        if not doom:
+            monkeypatch.setenv("TBG_NO_DOOM", "1")
+        p = Pair(account_capacity=256, transfer_capacity=1 << 14, batch_events_max=4096)
+        try:
+            n_acc = 40
+            acc = workload.accounts(n_acc, seed=seed, ledger=1)
+            acc["flags"][:8] |= 2  # accounts 1..8: debits_must_not_exceed_credits
+            p.create_accounts(acc)
+            # starting credits of the limited accounts (from unlimited accounts 20..39)
+            p.create_transfers(_transfers([dict(id=10 + i, debit_account_id=20 + i,
+                                                credit_account_id=1 + i, amount=1000 * (i + 1),
+                                                ledger=1, code=1) for i in range(8)]))
+            pend = [dict(id=100 + i, debit_account_id=1 + i % 8, credit_account_id=30 + i % 5,
+                         amount=50 + i, ledger=1, code=1, flags=2) for i in range(16)]
+            p.create_transfers(_transfers(pend))
+            next_id = 1000
+            for step in range(5):
+                rows = []
+                for _ in range(600):
+                    r = rng.random()
+                    dr = int(rng.integers(1, n_acc + 1))
+                    cr = int(rng.integers(1, n_acc + 1))
+                    if cr == dr:
+                        cr = dr % n_acc + 1
+                    row = dict(id=next_id, debit_account_id=dr, credit_account_id=cr, ledger=1,
+                               code=1, amount=int(rng.choice([10, 300, 2000, 9000, 50_000])))
+                    if r < 0.35:
+                        row["debit_account_id"] = int(rng.integers(1, 9))  # a limited debit
+                        if row["credit_account_id"] == row["debit_account_id"]:
+                            row["credit_account_id"] = 20
+                    elif r < 0.45:
+                        row["credit_account_id"] = int(rng.integers(1, 9))  # credit a limited one
+                        if row["credit_account_id"] == row["debit_account_id"]:
+                            row["debit_account_id"] = 21
+                    elif r < 0.5:
+                        row["flags"] = 2  # pending
+                    rows.append(row)
+                    next_id += 1
+                # posts / voids of the limited accounts' pending transfers (some accounts only)
+                if step in (1, 3):
+                    for i in range(step, 16, 5):
+                        rows.insert(int(rng.integers(0, len(rows))),
+                                    dict(id=next_id, pending_id=100 + i,
+                                         flags=4 if i % 2 else 8, amount=0))
+                        next_id += 1
+                else:  # a post / void forces the flow replay (no account lanes)
+                    rows.insert(0, dict(id=next_id, pending_id=999_999, flags=4, amount=0))
+                    next_id += 1
+                # linked chains ending in a limited debit
+                for _ in range(30):
+                    at = int(rng.integers(0, len(rows) - 4))
+                    for j in range(3):
+                        rows[at + j]["flags"] = rows[at + j].get("flags", 0) | 1
+                p.create_transfers(_transfers(rows), [len(rows) // 2, len(rows) - len(rows) // 2])
+            p.compare_state()
+        finally:
+            p.close()

@@ -85,6 +85,8 @@ struct FlowScratch {
     unsigned int* engine = nullptr;  // flow engine queue counters
     uint32_t* exp_flag = nullptr;
     uint32_t* acc_free = nullptr;  // per account (lanes.hpp free owners)
+    unsigned long long* acc_pot = nullptr;  // per account (group.hpp doomed debits)
+    uint32_t* doom_off = nullptr;
 };
 
 }  // namespace
@@ -512,7 +514,9 @@ int ensure_flow(tbg_ctx* ctx, uint64_t m) {
              dev_alloc(ctx, &F.lane_counts, 4, true) &&
              dev_alloc(ctx, &F.lane_undo, uint64_t(kFlowLanesMax) * kFlowUndoPerLane, false) &&
              dev_alloc(ctx, &F.engine, kFlowEngineWords, true) &&
-             dev_alloc(ctx, &F.acc_free, ctx->opt.account_capacity, true);
+             dev_alloc(ctx, &F.acc_free, ctx->opt.account_capacity, true) &&
+             dev_alloc(ctx, &F.acc_pot, ctx->opt.account_capacity, true) &&
+             dev_alloc(ctx, &F.doom_off, 1, true);
         if (!ok) return TBG_EHIP;
     }
     if (m <= F.cap) return 0;
@@ -580,6 +584,11 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
         !(call_flags & (kFlagDuplicate | kFlagPostVoid | kFlagClosable | kFlagImported)) &&
         !c.force_replay && !getenv("TBG_NO_LANES");
     P.add_epoch = getenv("TBG_NO_ADDITIVE") ? 0 : c.epoch;
+    // Doomed debits (group.hpp): not with duplicate ids (a post/void's pending transfer may be a
+    // later claimant's) nor with the account lanes (which decide limit events themselves).
+    const bool doom = !lanes_possible && !(call_flags & kFlagDuplicate) && !getenv("TBG_NO_DOOM");
+    P.acc_pot = doom ? F.acc_pot : nullptr;
+    P.doom_off = F.doom_off;
 
     GroupPlan G{};
     G.hmask = F.slots - 1;
@@ -628,6 +637,8 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
                        0, ctx->stream, ctx->T, c, P);
     rc = launch_scan(ctx, m, SelectHeads{F.head8, F.heads, F.unit_of, &F.counts[0]});
     if (rc) return rc;
+    if (doom)
+        hipLaunchKernelGGL(flow_credit_pot, dim3(grid_for(m)), block, 0, ctx->stream, ctx->T, c, P);
     hipLaunchKernelGGL(plan_keys, dim3((m + kPlanThreads - 1) / kPlanThreads), dim3(kPlanThreads), 0,
                        ctx->stream, ctx->T, c, P, G, L, call_flags);
     // the planned expires_at entries
@@ -1461,6 +1472,7 @@ void tbg_close(tbg_ctx* ctx) {
                     ctx->flow.dup_mark, ctx->flow.counts, ctx->flow.words, ctx->flow.lane_counts,
                     ctx->scan_status, ctx->scan_ticket,
                     ctx->flow.lane_undo, ctx->flow.engine, ctx->flow.acc_free,
+                    ctx->flow.acc_pot, ctx->flow.doom_off,
                     ctx->ae_log, ctx->ae_ref, ctx->ae_list, ctx->ae_words};
     free_ae_scratch(ctx->ae);
     free_flow(ctx->flow);

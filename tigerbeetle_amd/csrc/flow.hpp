@@ -83,6 +83,11 @@ struct FlowPlan {
     uint32_t backoff;            // idle waves sleep longer the longer they find no unit
     unsigned long long* debug;   // optional: [0] loop iterations, [1] events, [2] cycles executing,
                                  // [3] cycles of the engine (lane 0)
+    // Doomed debits (group.hpp: flow_credit_pot): null, or per account row the call's credit
+    // potential (epoch:32 | sum:32, sum all-ones: unbounded) and a word set to the epoch when the
+    // call cannot bound it (a post/void whose pending transfer is uncertain).
+    unsigned long long* acc_pot;
+    uint32_t* doom_off;
 };
 
 // Per position, everything the replay reads that no other unit writes, so the engine loads it

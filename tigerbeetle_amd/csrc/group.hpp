@@ -167,6 +167,93 @@ __device__ inline void group_block_place(const GroupPlan& G, const GroupBlock& B
     }
 }
 
+// ---- Doomed debits ------------------------------------------------------------------------------
+//
+// An account L with debits_must_not_exceed_credits fails a debit of `amount` (exceeds_credits,
+// create_transfer :3907-3909) whenever dpe + dpo + amount > cpo. Within one call, dpe and dpo of L
+// only grow unless a post / void resolves a pending transfer of L, and cpo grows at most by the
+// posted credits the call's replayed events carry to L (every event touching L replays: L's limit
+// marks it hot, so no FAST event touches it). So a replayed debit of L with
+//     dpe0 + dpo0 + amount > cpo0 + (the call's replayed posted credits to L)
+// (balances at the plan, after the FAST deltas) fails at whatever point of the call it runs, and
+// its unit needs no ordering with the other units of L: plan_keys gives it no key on L. (The
+// account lanes decide such events themselves; calls with duplicate ids never drop keys.)
+constexpr uint32_t kPotUnbounded = 0xFFFFFFFFu;
+
+__device__ inline bool pot_limited(const tb_account_t& a) {
+    return (a.flags & TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS) != 0;
+}
+// Adds `amount` to L's potential for this call (saturating: all-ones = unbounded).
+__device__ inline void pot_add(unsigned long long* w, uint32_t epoch, uint64_t amount) {
+    unsigned long long old = *w;
+    while (true) {
+        const uint32_t e = uint32_t(old >> 32), sum = e == epoch ? uint32_t(old) : 0u;
+        const uint64_t add = sum == kPotUnbounded ? 0 : amount;
+        const uint64_t next_sum = uint64_t(sum) + add >= kPotUnbounded ? kPotUnbounded : sum + add;
+        const unsigned long long want = (uint64_t(epoch) << 32) | next_sum;
+        if (want == old) return;
+        const unsigned long long seen = atomicCAS(w, old, want);
+        if (seen == old) return;
+        old = seen;
+    }
+}
+// L's potential this call (0 when no replayed event credits it).
+__device__ inline uint32_t pot_of(const unsigned long long* w, uint32_t epoch) {
+    const unsigned long long v = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return uint32_t(v >> 32) == epoch ? uint32_t(v) : 0u;
+}
+
+__global__ void flow_credit_pot(Tables T, Call<tb_transfer_t> c, FlowPlan P) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= P.m) return;
+    const uint32_t k = P.slow_list[s];
+    const tb_transfer_t& t = c.events[k];
+    if (t.flags & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) {
+        // A post / void changes its pending transfer's accounts' dpe (and dpo, cpo): both sides,
+        // if limited, are unbounded; an uncertain pending transfer turns the rule off.
+        if (u128_is_zero(t.pending_id) || u128_is_max(t.pending_id)) return;
+        const uint64_t ps = transfer_slot_find(T, c, t.pending_id);
+        if (ps == kNone) return;  // (not found: fails; duplicates turn the rule off on the host)
+        const uint64_t w = T.tr.slots[ps];
+        const uint64_t r = (w & kRefMask) - 1;
+        const tb_transfer_t* p = nullptr;
+        if (r < c.row_base) {
+            if (!(w & kOrphanBit)) p = &T.tr_rows[r];
+        } else {
+            p = &c.events[uint32_t(r - c.row_base)];
+        }
+        if (!p) return;
+        const uint64_t dr = account_find(T, p->debit_account_id);
+        const uint64_t cr = account_find(T, p->credit_account_id);
+        if (dr != kNone && pot_limited(T.acc_rows[dr])) pot_add(&P.acc_pot[dr], P.epoch, kPotUnbounded);
+        if (cr != kNone && pot_limited(T.acc_rows[cr])) pot_add(&P.acc_pot[cr], P.epoch, kPotUnbounded);
+        return;
+    }
+    if (t.flags & TB_TRANSFER_PENDING) return;  // (a pending credit adds to cpe, not cpo)
+    const uint32_t cr = c.ev_cr[k];
+    if (cr == kNone32 || !pot_limited(T.acc_rows[cr])) return;
+    pot_add(&P.acc_pot[cr], P.epoch, t.amount.hi ? kPotUnbounded : t.amount.lo);
+}
+
+// Is replayed event t (debit account row dr) doomed (the rule above)?
+__device__ inline bool doomed_debit(const Tables& T, const FlowPlan& P, const tb_transfer_t& t,
+                                   uint32_t dr) {
+    if (!P.acc_pot || dr == kNone32 || *P.doom_off == P.epoch) return false;
+    if (t.flags & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING | TB_TRANSFER_BALANCING_DEBIT |
+                   TB_TRANSFER_BALANCING_CREDIT | TB_TRANSFER_IMPORTED))
+        return false;
+    if (t.amount.hi != 0 || t.amount.lo >= (1ull << 56)) return false;
+    const tb_account_t& a = T.acc_rows[dr];
+    if (!pot_limited(a) || T.acc_closable[dr] == P.epoch) return false;
+    constexpr uint64_t kLim = 1ull << 62;
+    if (a.debits_pending.hi || a.debits_posted.hi || a.credits_posted.hi ||
+        a.debits_pending.lo >= kLim || a.debits_posted.lo >= kLim || a.credits_posted.lo >= kLim)
+        return false;
+    const uint32_t pot = pot_of(&P.acc_pot[dr], P.epoch);
+    if (pot == kPotUnbounded) return false;
+    return a.debits_pending.lo + a.debits_posted.lo + t.amount.lo > a.credits_posted.lo + pot;
+}
+
 // Everything per replayed event s (flow_keys' and lanes_check's rules); its keys' grouping slots
 // and ranks. Launched with kPlanThreads per workgroup.
 __global__ void __launch_bounds__(kPlanThreads) plan_keys(Tables T, Call<tb_transfer_t> c,
@@ -231,7 +318,9 @@ __global__ void __launch_bounds__(kPlanThreads) plan_keys(Tables T, Call<tb_tran
             }
         } else {
             const uint32_t dr = c.ev_dr[k], cr = c.ev_cr[k];
-            if (dr != kNone32 && !keyless(dr)) key[2] = (1ull << 32) | dr;
+            // (a doomed debit reads L's balances in any order: no key on L)
+            if (dr != kNone32 && !keyless(dr) && !(!G.lanes && doomed_debit(T, P, t, dr)))
+                key[2] = (1ull << 32) | dr;
             if (cr != kNone32 && !keyless(cr)) key[3] = (1ull << 32) | cr;
             if (dr != kNone32 && keyless(dr)) add |= kAddDr;
             if (cr != kNone32 && keyless(cr)) add |= kAddCr;
