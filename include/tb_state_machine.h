@@ -108,7 +108,9 @@ void tb_sm_close(tb_sm* sm);
 /* The bound HIP executor of a tb_sm_open_gpu state machine (NULL otherwise). */
 tbg_ctx* tb_sm_executor_gpu(tb_sm* sm);
 /* Registers a host buffer the replica passes as bodies or reply outputs (its message pool) with
- * the HIP executor for direct DMA (tbg_register_host); a no-op returning 0 for another executor. */
+ * the HIP executor (tbg_register_host): page-locked and mapped, so the executor's kernels read a
+ * body and write a reply over PCIe on the call's stream, with no DMA-engine hand-off; a no-op
+ * returning 0 for another executor. */
 int tb_sm_register_buffer(tb_sm* sm, void* ptr, uint64_t size);
 
 int tb_sm_input_valid(const tb_sm* sm, uint8_t operation, const void* body, uint32_t size);

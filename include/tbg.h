@@ -92,10 +92,11 @@ int tbg_create_transfers_stamped_device(tbg_ctx* ctx, const tb_transfer_t* d_eve
                                         const uint64_t* d_event_timestamps,
                                         tb_create_result_t* d_results, void* stream);
 
-/* Pins a host buffer the caller reuses across calls (a replica's message bodies and reply
- * buffers) for direct DMA: a host-buffer call whose events or results lie in a registered range
- * skips the driver's staged copy of pageable memory (hipHostRegister). Unregistered at
- * tbg_unregister_host or tbg_close. */
+/* Pins and maps a host buffer the caller reuses across calls (a replica's message bodies and
+ * reply buffers; hipHostRegister, mapped): a host-buffer call whose events or results lie in a
+ * registered range has its kernels read the body (tr_ingest, small calls) and write the results
+ * over PCIe on the call's own stream -- no staged copy of pageable memory and no DMA-engine
+ * hand-off. Unregistered at tbg_unregister_host or tbg_close. */
 int tbg_register_host(tbg_ctx* ctx, void* ptr, uint64_t size);
 int tbg_unregister_host(tbg_ctx* ctx, void* ptr);
 

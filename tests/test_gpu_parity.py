@@ -872,6 +872,12 @@ def test_doomed_debits(seed, monkeypatch):
                 else:  # a post / void forces the flow replay (no account lanes)
                     rows.insert(0, dict(id=next_id, pending_id=999_999, flags=4, amount=0))
                     next_id += 1
+                # in-call duplicate ids (every claimant's credits bound the rule; an uncertain
+                # pending transfer turns it off)
+                if step % 2 == 0:
+                    for _ in range(12):
+                        a_i, b_i = rng.integers(0, len(rows), size=2)
+                        rows[int(b_i)]["id"] = rows[int(a_i)]["id"]
                 # linked chains ending in a limited debit
                 for _ in range(30):
                     at = int(rng.integers(0, len(rows) - 4))

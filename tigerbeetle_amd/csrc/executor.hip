@@ -584,9 +584,8 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
         !(call_flags & (kFlagDuplicate | kFlagPostVoid | kFlagClosable | kFlagImported)) &&
         !c.force_replay && !getenv("TBG_NO_LANES");
     P.add_epoch = getenv("TBG_NO_ADDITIVE") ? 0 : c.epoch;
-    // Doomed debits (group.hpp): not with duplicate ids (a post/void's pending transfer may be a
-    // later claimant's) nor with the account lanes (which decide limit events themselves).
-    const bool doom = !lanes_possible && !(call_flags & kFlagDuplicate) && !getenv("TBG_NO_DOOM");
+    // Doomed debits (group.hpp): not with the account lanes (which decide limit events themselves).
+    const bool doom = !lanes_possible && !getenv("TBG_NO_DOOM");
     P.acc_pot = doom ? F.acc_pot : nullptr;
     P.doom_off = F.doom_off;
 
@@ -638,7 +637,8 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
     rc = launch_scan(ctx, m, SelectHeads{F.head8, F.heads, F.unit_of, &F.counts[0]});
     if (rc) return rc;
     if (doom)
-        hipLaunchKernelGGL(flow_credit_pot, dim3(grid_for(m)), block, 0, ctx->stream, ctx->T, c, P);
+        hipLaunchKernelGGL(flow_credit_pot, dim3(grid_for(m)), block, 0, ctx->stream, ctx->T, c, P,
+                           call_flags);
     hipLaunchKernelGGL(plan_keys, dim3((m + kPlanThreads - 1) / kPlanThreads), dim3(kPlanThreads), 0,
                        ctx->stream, ctx->T, c, P, G, L, call_flags);
     // the planned expires_at entries

@@ -177,7 +177,8 @@ __device__ inline void group_block_place(const GroupPlan& G, const GroupBlock& B
 //     dpe0 + dpo0 + amount > cpo0 + (the call's replayed posted credits to L)
 // (balances at the plan, after the FAST deltas) fails at whatever point of the call it runs, and
 // its unit needs no ordering with the other units of L: plan_keys gives it no key on L. (The
-// account lanes decide such events themselves; calls with duplicate ids never drop keys.)
+// account lanes decide such events themselves. Duplicate ids add every claimant's credits; a
+// post/void whose pending transfer is uncertain -- plan_keys' rule -- turns it off for the call.)
 constexpr uint32_t kPotUnbounded = 0xFFFFFFFFu;
 
 __device__ inline bool pot_limited(const tb_account_t& a) {
@@ -203,7 +204,8 @@ __device__ inline uint32_t pot_of(const unsigned long long* w, uint32_t epoch) {
     return uint32_t(v >> 32) == epoch ? uint32_t(v) : 0u;
 }
 
-__global__ void flow_credit_pot(Tables T, Call<tb_transfer_t> c, FlowPlan P) {
+__global__ void flow_credit_pot(Tables T, Call<tb_transfer_t> c, FlowPlan P,
+                                unsigned int call_flags) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= P.m) return;
     const uint32_t k = P.slow_list[s];
@@ -211,16 +213,26 @@ __global__ void flow_credit_pot(Tables T, Call<tb_transfer_t> c, FlowPlan P) {
     if (t.flags & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) {
         // A post / void changes its pending transfer's accounts' dpe (and dpo, cpo): both sides,
         // if limited, are unbounded; an uncertain pending transfer turns the rule off.
+        // (plan_keys' certainty rule: with duplicate ids a pending id not found now, or held in
+        // the call by an event with later claimants, may be another event's -- the rule is off)
         if (u128_is_zero(t.pending_id) || u128_is_max(t.pending_id)) return;
         const uint64_t ps = transfer_slot_find(T, c, t.pending_id);
-        if (ps == kNone) return;  // (not found: fails; duplicates turn the rule off on the host)
+        if (ps == kNone) {
+            if (call_flags & kFlagDuplicate) *P.doom_off = P.epoch;
+            return;
+        }
         const uint64_t w = T.tr.slots[ps];
         const uint64_t r = (w & kRefMask) - 1;
         const tb_transfer_t* p = nullptr;
         if (r < c.row_base) {
             if (!(w & kOrphanBit)) p = &T.tr_rows[r];
         } else {
-            p = &c.events[uint32_t(r - c.row_base)];
+            const uint32_t j = uint32_t(r - c.row_base);
+            if (P.dup_mark[j] == P.epoch) {
+                *P.doom_off = P.epoch;
+                return;
+            }
+            p = &c.events[j];
         }
         if (!p) return;
         const uint64_t dr = account_find(T, p->debit_account_id);
