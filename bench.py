@@ -1018,6 +1018,12 @@ def main():
         kname, (kms, kcount) = dom
         avg_s = kms / kcount / 1e3
         kbytes = KERNEL_BYTES_PER_EVENT[kname] * N
+        # A sparse key space (config 5): tr_ingest also applies the balance deltas itself (u128
+        # atomics on the accounts' rows; no bal_* kernel ran), so it does the path's per-account
+        # work too: SURVEY.md §8d's 256 B per distinct account (row read + write).
+        ingest_balances = kname == "tr_ingest" and not any(k.startswith("bal") for k in kernels)
+        if ingest_balances:
+            kbytes += 256 * distinct
         achieved = kbytes / avg_s / 1e9
         traffic, traffic_src = (measured_traffic(kname) if wl.default else
                                 measured_traffic(kname, TRAFFIC_FILE_CONFIG5)
@@ -1027,7 +1033,9 @@ def main():
                     "traffic": traffic, "traffic_source": traffic_src,
                     "alg_bytes_per_launch": kbytes,
                     "alg_bytes_basis": "SURVEY.md §8d: 288 B per event (event 128 R, result 16 W, "
-                                       "transfer row 128 W, id-key probe 16)",
+                                       "transfer row 128 W, id-key probe 16)" +
+                                       (" + 256 B per distinct account (the kernel applies the "
+                                        "balances: row read + write)" if ingest_balances else ""),
                     "avg_launch_ms": round(kms / kcount, 4),
                     "path": {"alg_bytes_per_step": path_bytes,
                              "alg_bytes_basis": "SURVEY.md §8d: 288 N + 256 D "

@@ -887,3 +887,52 @@ def test_doomed_debits(seed, monkeypatch):
             p.compare_state()
         finally:
             p.close()
+
+
+@pytest.mark.parametrize("mode", ["parallel", "no-pv-fast", "flow"])
+def test_later_post_void_claims(mode, monkeypatch):
+    """Later posts / voids of a pending transfer whose first post / void in the call is a single
+    FAST event fail with already_posted / already_voided without replaying (tr_commit:
+    later_claim_status), also inside linked chains (the chain fails there: linked_event_failed for
+    the rest); a winner inside a chain (which may roll back), a second winner and duplicate ids
+    keep the ordered replay. Every call against the oracle."""
+    if mode == "no-pv-fast":
+        monkeypatch.setenv("TBG_NO_PV_FAST", "1")
+    rng = np.random.default_rng(77)
+    p = Pair(account_capacity=256, transfer_capacity=1 << 14, batch_events_max=4096,
+             force_replay=mode == "flow")
+    try:
+        acc = workload.accounts(30, seed=5, ledger=1)
+        p.create_accounts(acc)
+        pend = [dict(id=100 + i, debit_account_id=1 + i % 30, credit_account_id=1 + (i + 7) % 30,
+                     amount=1000 + i, ledger=1, code=1, flags=2) for i in range(300)]
+        p.create_transfers(_transfers(pend))
+        next_id = 10_000
+        for step in range(4):
+            rows = []
+            for _ in range(500):
+                r = rng.random()
+                if r < 0.6:  # a post / void of one of a few pending transfers: many later claims
+                    x = 100 + int(rng.integers(step * 70, step * 70 + 60))
+                    post = rng.random() < 0.6
+                    rows.append(dict(id=next_id, pending_id=x, flags=4 if post else 8,
+                                     amount=(2**128 - 1) if post else 0))
+                else:
+                    dr, cr = rng.integers(1, 31, size=2)
+                    if dr == cr:
+                        cr = dr % 30 + 1
+                    rows.append(dict(id=next_id, debit_account_id=int(dr), credit_account_id=int(cr),
+                                     amount=int(rng.integers(1, 100)), ledger=1, code=1))
+                next_id += 1
+            for _ in range(40):  # chains of 2-4 events
+                at = int(rng.integers(0, len(rows) - 5))
+                for j in range(int(rng.integers(1, 4))):
+                    rows[at + j]["flags"] = rows[at + j].get("flags", 0) | 1
+            if step == 2:
+                for _ in range(8):  # in-call duplicate ids
+                    a_i, b_i = rng.integers(0, len(rows), size=2)
+                    rows[int(b_i)]["id"] = rows[int(a_i)]["id"]
+            p.create_transfers(_transfers(rows), [len(rows) // 3, len(rows) - len(rows) // 3])
+        p.compare_state()
+    finally:
+        p.close()

@@ -149,6 +149,7 @@ struct tbg_ctx {
     uint8_t* ev_info = nullptr;
     uint8_t* ev_slow = nullptr;
     uint32_t* slow_list = nullptr;
+    uint32_t* fix_slots = nullptr;  // tr_commit's fixed failures' id slots (Call::fix_slots)
     uint64_t* pnt_call = nullptr;           // pulse_next_timestamp updates per event (post/void)
     unsigned long long* pnt_fired = nullptr;
     unsigned long long* pv_slots = nullptr;  // pending-id claims of post/void events (kernels.hpp)
@@ -307,7 +308,8 @@ int select_flagged(tbg_ctx* ctx, const uint8_t* flags, uint64_t n, uint32_t* out
 }
 
 int stage_call_outputs(tbg_ctx* ctx, const tb_create_result_t* d_results, tb_create_result_t* dst,
-                       uint32_t n, bool scalars, const AeSnapJob* snap = nullptr);
+                       uint32_t n, bool scalars, const AeSnapJob* snap = nullptr,
+                       bool fixes = false);
 // The scalars block to the host (a kernel writes the mapped pinned copy: no DMA hand-off).
 int sync_scalars(tbg_ctx* ctx) {
     int rc = stage_call_outputs(ctx, nullptr, nullptr, 0, true);
@@ -431,6 +433,7 @@ Call<Event> make_call(tbg_ctx* ctx, const Event* d_events, uint32_t n, const uin
     c.slow_list = ctx->slow_list;
     c.pnt_call = ctx->pnt_call;
     c.events_out = nullptr;
+    c.fix_slots = ctx->fix_slots;
     // (TBG_NO_PV_FAST: every post/void replays)
     c.pv_slots = getenv("TBG_NO_PV_FAST") ? nullptr : ctx->pv_slots;
     c.pv_mask = ctx->pv_mask;
@@ -1244,11 +1247,12 @@ int stage_call_inputs(tbg_ctx* ctx, const void* events, uint64_t bytes, uint32_t
 
 // Results (n > 0) and / or the scalars block to mapped host memory, as one kernel on the stream.
 int stage_call_outputs(tbg_ctx* ctx, const tb_create_result_t* d_results, tb_create_result_t* dst,
-                       uint32_t n, bool scalars, const AeSnapJob* snap) {
+                       uint32_t n, bool scalars, const AeSnapJob* snap, bool fixes) {
     StageOut s{reinterpret_cast<const uint4*>(d_results), reinterpret_cast<uint4*>(dst), n,
                scalars ? reinterpret_cast<const unsigned long long*>(ctx->d_scalars) : nullptr,
                reinterpret_cast<unsigned long long*>(ctx->dh_scalars),
-               uint32_t(sizeof(DevScalars) / 8)};
+               uint32_t(sizeof(DevScalars) / 8), fixes ? ctx->fix_slots : nullptr,
+               ctx->T.tr.slots, ctx->d_scalars};
     if (!dst || !n) s.src = nullptr;
     AeSnapJob J{};
     if (snap) J = *snap;
@@ -1367,6 +1371,7 @@ tbg_ctx* tbg_open(const tbg_options* options) {
          dev_alloc(ctx, &ctx->ev_cr, ev_max, false) && dev_alloc(ctx, &ctx->ev_amount, ev_max, false) &&
          dev_alloc(ctx, &ctx->ev_info, ev_max, false) && dev_alloc(ctx, &ctx->ev_slow, ev_max, false) &&
          dev_alloc(ctx, &ctx->slow_list, ev_max, false) &&
+         dev_alloc(ctx, &ctx->fix_slots, ev_max, false) &&
          dev_alloc(ctx, &ctx->pnt_call, ev_max, false) && dev_alloc(ctx, &ctx->pnt_fired, 2, true) &&
          dev_alloc(ctx, &ctx->pv_slots, next_pow2(2 * uint64_t(ev_max)), true);
     ctx->pv_mask = next_pow2(2 * uint64_t(ev_max)) - 1;
@@ -1462,6 +1467,7 @@ void tbg_close(tbg_ctx* ctx) {
                     ctx->T.tr_status, ctx->T.expiry, ctx->d_scalars, ctx->T.undo, ctx->d_events,
                     ctx->d_results, ctx->d_batch_ends, ctx->d_batch_ts, ctx->ev_slot, ctx->ev_dr,
                     ctx->ev_cr, ctx->ev_amount, ctx->ev_info, ctx->ev_slow, ctx->slow_list,
+                    ctx->fix_slots,
                     ctx->pnt_call, ctx->pnt_fired, ctx->pv_slots,
                     ctx->bal_items, ctx->chunk_info, ctx->bal_items_sorted, ctx->bucket_words, ctx->bucket_partials,
                     ctx->window_partials, ctx->window_carry,
@@ -1539,9 +1545,13 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
     // 1M-event calls): u128 atomics per item instead of the sort; collisions are rare.
     const bool use_atomic = use_sort && !use_window && !use_buckets &&
                             uint64_t(key_end) > kAtomicKeysPerItem * 2 * uint64_t(n);
+    // Sparse key spaces: tr_ingest applies each FAST event's deltas with u128 atomics itself (as
+    // in small calls; a demotion subtracts them) -- no items written, read back and applied by a
+    // second kernel. TBG_NO_INGEST_ATOMICS: items and bal_atomic_apply.
+    const bool ingest_atomics = use_atomic && !getenv("TBG_NO_INGEST_ATOMICS");
     if (use_buckets && key_bits < 16) key_bits = 16;
     BucketPlan plan{};
-    if (use_sort) {
+    if (use_sort && !ingest_atomics) {
         c.bal_items = ctx->bal_items;
         c.key_bits = key_bits;
         if (use_window) c.pair_shift = pair_shift;
@@ -1617,12 +1627,12 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
                            target, plan, ctx->bucket_partials, key_end);
         tmark(ctx, "bal_apply");
         rc = hip_ok(ctx, hipGetLastError(), "launch") ? 0 : TBG_EHIP;
-    } else if (!rc && use_atomic) {
+    } else if (!rc && use_atomic && !ingest_atomics) {
         hipLaunchKernelGGL(bal_atomic_apply, dim3(grid_for(uint64_t(items) / 2)), block, 0,
                            ctx->stream, target, ctx->bal_items, uint64_t(items), key_bits, key_end);
         tmark(ctx, "bal_atomic");
         rc = hip_ok(ctx, hipGetLastError(), "launch") ? 0 : TBG_EHIP;
-    } else if (!rc && use_sort) {
+    } else if (!rc && use_sort && !ingest_atomics) {
         // Balance deltas: sort the packed items by field key, reduce runs in u128.
         size_t bytes = 0;
         rc = hip_ok(ctx, hipcub::DeviceRadixSort::SortKeys(nullptr, bytes, ctx->bal_items,
@@ -1658,7 +1668,8 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
         // (a small call's AccountEvents snapshot rides along: final unless a replay follows)
         AeSnapJob J;
         const bool snap = ae_async_ok(ctx, n) && !(rc = ae_snap_job(ctx, c, &J));
-        if (!rc) rc = stage_call_outputs(ctx, d_results, dst, dst ? n : 0, true, snap ? &J : nullptr);
+        if (!rc)
+            rc = stage_call_outputs(ctx, d_results, dst, dst ? n : 0, true, snap ? &J : nullptr, true);
         // (its graph queued now: the host's launch calls overlap the call's kernels)
         if (!rc && snap) rc = ae_launch_graph(ctx);
         ctx->ae_snap_early = snap && !rc;
@@ -2270,7 +2281,7 @@ struct CkptHeader {
     DevScalars scalars;
 };
 constexpr char kCkptMagic[8] = {'T', 'B', 'G', 'C', 'K', 'P', 'T', '2'};
-constexpr uint32_t kCkptVersion = 2;
+constexpr uint32_t kCkptVersion = 3;  // (3: DevScalars::fixed)
 constexpr uint32_t kCkptSections = 12;
 struct CkptFooter {
     char magic[8];

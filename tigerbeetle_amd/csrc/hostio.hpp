@@ -58,12 +58,22 @@ struct StageOut {
     const unsigned long long* scalars_src;  // the scalars block, or null
     unsigned long long* scalars_dst;        // mapped pinned copy
     uint32_t scalar_words;
+    // A create_transfers call's first stage_out: tr_commit's fixed failures' id slots become
+    // tombstones here (null: none to release).
+    const uint32_t* fix_slots;
+    unsigned long long* id_slots;
+    const DevScalars* scalars;
 };
 
 // (+ a small call's AccountEvents staging, events.hpp, when J.on: the call's state is final here
 // unless its replay follows, in which case the executor stages it again after the replay)
 __global__ void __launch_bounds__(kStageThreads) stage_out(StageOut s, AeSnapJob J) {
     const uint32_t tid = blockIdx.x * kStageThreads + threadIdx.x;
+    if (s.fix_slots) {
+        const uint64_t nfix = s.scalars->fixed;
+        for (uint64_t i = tid; i < nfix; i += uint64_t(gridDim.x) * kStageThreads)
+            s.id_slots[s.fix_slots[i]] = kTomb;
+    }
     // Only when no event replays (stats[0], set by tr_commit): a replayed event's result is not
     // final yet -- its slot may still read `created` from the speculation -- and the executor
     // takes the snapshot again after the replay.

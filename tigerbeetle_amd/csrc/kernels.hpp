@@ -242,6 +242,18 @@ __device__ inline bool pv_first(const Call<tb_transfer_t>& c, uint32_t k, const 
     return false;
 }
 
+// The earliest post/void of pending id `x` in the call (kNone32: no claim this call).
+__device__ inline uint32_t pv_winner(const Call<tb_transfer_t>& c, const tb_uint128_t& x) {
+    uint64_t s = pv_home(c, x);
+    for (uint64_t n = 0; n <= c.pv_mask; n++) {
+        const unsigned long long w = c.pv_slots[s];
+        if ((w >> 32) != c.epoch) return kNone32;
+        if (u128_eq(c.events[uint32_t(w) - 1].pending_id, x)) return uint32_t(w) - 1;
+        s = (s + 1) & c.pv_mask;
+    }
+    return kNone32;
+}
+
 // The committed pending transfer a post/void names (kNone: not a committed, un-orphaned row).
 __device__ inline uint64_t pv_pending_row(const Tables& T, const Call<tb_transfer_t>& c,
                                           const tb_uint128_t& pending_id) {
@@ -756,6 +768,7 @@ __device__ inline void reset_call_scalars(DevScalars* scalars) {
     for (int j = 0; j < 4; j++) scalars->stats[j] = 0;
     scalars->spec_fast = 0;
     scalars->spec_ts_max = 0;
+    scalars->fixed = 0;
 }
 
 // The call's scalar words zeroed at the end of a call (queued behind it, while the host returns):
@@ -1046,12 +1059,74 @@ __device__ inline bool fast_demoted_peer(const Tables& T, const Call<tb_transfer
     return false;
 }
 
+constexpr uint32_t kFastChainMax = 32;  // (chain_demoted below)
+
+// A later post/void k of a pending transfer X whose first post/void in the call (the winner of X's
+// claim) is a single FAST event that tr_commit confirms: X is posted / voided before k runs, and
+// k -- FAST at ingest, so every check before the status switch (post_or_void_pending_transfer
+// :4166-4226) passed on X's immutable row -- fails with pending_transfer_already_posted /
+// _voided in any order. (A winner inside a chain may roll back: then k replays.) 0: not such an
+// event. Reads only what no tr_commit thread writes.
+__device__ inline uint32_t later_claim_status(const Tables& T, const Call<tb_transfer_t>& c,
+                                              uint32_t k, unsigned int call_flags) {
+    const tb_transfer_t& e = c.events[k];
+    if (!(e.flags & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) || !c.pv_slots ||
+        (call_flags & kFlagImported))
+        return 0;
+    const uint32_t j = pv_winner(c, e.pending_id);
+    if (j == kNone32 || j >= k) return 0;
+    if ((c.ev_info[j] & kInfoClassMask) != kClassFast) return 0;
+    const tb_transfer_t& w = c.events[j];
+    if (w.flags & TB_TRANSFER_LINKED) return 0;
+    if (j > 0 && (c.events[j - 1].flags & TB_TRANSFER_LINKED) &&
+        j != batch_start_of(c, batch_of_guess(c.batch_ends, c.n_batches, c.n, j)))
+        return 0;
+    if (fast_demoted_peer(T, c, j, call_flags)) return 0;
+    // k itself must hold its id (a later duplicate's outcome follows the earlier holder's).
+    if (call_flags & kFlagDuplicate) {
+        const uint64_t s = transfer_slot_find(T, c, e.id);
+        if (s == kNone || (T.tr.slots[s] & kRefMask) != c.row_base + k + 1) return 0;
+    }
+    return (w.flags & TB_TRANSFER_POST_PENDING) ? TB_CT_PENDING_TRANSFER_ALREADY_POSTED
+                                                : TB_CT_PENDING_TRANSFER_ALREADY_VOIDED;
+}
+
+// A chain whose every event is FAST at ingest and whose first event that is not an undemoted FAST
+// event is a later claim (above) fails there in any order: that event takes the claim's status,
+// every other event of the chain linked_event_failed (execute_create :3116-3194), nothing is
+// applied. Returns that status for event k (0: not such a chain). Every event of the chain
+// evaluates the same rule over the same data, so they agree.
+__device__ inline uint32_t chain_fail_status(const Tables& T, const Call<tb_transfer_t>& c,
+                                             uint32_t k, unsigned int call_flags) {
+    const uint32_t b = batch_of_guess(c.batch_ends, c.n_batches, c.n, k);
+    const uint32_t bs = batch_start_of(c, b), be = c.batch_ends[b];
+    uint32_t x = k, y = k;
+    while (x > bs && (c.events[x - 1].flags & TB_TRANSFER_LINKED)) {
+        if (k - x >= kFastChainMax) return 0;
+        x--;
+    }
+    while (c.events[y].flags & TB_TRANSFER_LINKED) {
+        if (y + 1 >= be) return 0;  // linked_event_chain_open: the replay decides
+        if (y - k >= kFastChainMax) return 0;
+        y++;
+    }
+    if (y - x >= kFastChainMax) return 0;
+    for (uint32_t j = x; j <= y; j++)
+        if ((c.ev_info[j] & kInfoClassMask) != kClassFast) return 0;
+    for (uint32_t j = x; j <= y; j++) {
+        if (!fast_demoted_peer(T, c, j, call_flags)) continue;
+        const uint32_t st = later_claim_status(T, c, j, call_flags);
+        if (!st) return 0;
+        return j == k ? st : uint32_t(TB_CT_LINKED_EVENT_FAILED);
+    }
+    return 0;  // (no failure: the chain is confirmed)
+}
+
 // A FAST event of a linked chain (execute_create :3033-3207): the chain creates every event iff
 // every event of it is FAST and none is demoted -- then no event fails, nothing is rolled back, and
 // each event's effects are those of a FAST event. Otherwise the whole chain replays. Every event of
 // the chain evaluates the same rule over the same events, so they agree. Chains longer than
 // kFastChainMax (or open at their batch's end: linked_event_chain_open) replay.
-constexpr uint32_t kFastChainMax = 32;
 __device__ inline bool chain_demoted(const Tables& T, const Call<tb_transfer_t>& c, uint32_t k,
                                      unsigned int call_flags) {
     const uint32_t b = batch_of_guess(c.batch_ends, c.n_batches, c.n, k);
@@ -1137,8 +1212,33 @@ __device__ inline void commit_event(const Tables& T, const Call<tb_transfer_t>& 
             ((c.events[k].flags & TB_TRANSFER_LINKED) ||
              (k > 0 && (c.events[k - 1].flags & TB_TRANSFER_LINKED) &&
               k != batch_start_of(c, batch_of_guess(c.batch_ends, c.n_batches, c.n, k))));
-        if (slow || fast_demoted(T, c, k, call_flags, fr) ||
-            (in_chain && chain_demoted(T, c, k, call_flags))) {
+        // Fixed failures of post/voids racing an earlier FAST one (later_claim_status): DONE.
+        uint32_t fixed = 0;
+        if (!slow && (call_flags & kFlagPostVoid))
+            fixed = in_chain ? chain_fail_status(T, c, k, call_flags)
+                             : (fr.post_void && !pv_first(c, k, c.events[k].pending_id)
+                                    ? later_claim_status(T, c, k, call_flags) : 0u);
+        if (fixed) {
+            // Undo the speculative liveness and balance effects (as a demotion does), release
+            // the id (neither status is transient: the slot becomes a tombstone).
+            done = true;
+            T.tr_live[row] = 0;
+            if (!c.bal_items && !fr.post_void)
+                apply_fast_deltas(T, dr, cr, (info & kInfoPending) != 0, amount, true);
+            if (c.bal_items && c.pair_shift) {
+                c.bal_items[k] = ~0ull;
+            } else if (c.bal_items) {
+                uint64_t* it = c.bal_items + 2 * uint64_t(k);
+                it[0] = ~0ull;
+                it[1] = ~0ull;
+            }
+            c.results[k].status = fixed;
+            // (the id's release waits for stage_out: other threads of this kernel read slots)
+            const uint64_t fs = s != kNone32 ? uint64_t(s) : transfer_slot_find(T, c, c.events[k].id);
+            if (fs != kNone && (T.tr.slots[fs] & kRefMask) == ref)
+                c.fix_slots[atomicAdd(&T.scalars->fixed, 1ull)] = uint32_t(fs);
+        } else if (slow || fast_demoted(T, c, k, call_flags, fr) ||
+                   (in_chain && chain_demoted(T, c, k, call_flags))) {
             // Demoted: undo the speculative liveness and balance items (or, in a call without
             // items, the deltas ingest applied); the replay decides.
             slow = true;

@@ -34,6 +34,7 @@ struct DevScalars {
     unsigned long long stats[4];           // per call: slow, fast, replayed, static
     unsigned long long spec_fast;          // per call: FAST events as ingest classified them
     unsigned long long spec_ts_max;        // per call: their largest timestamp
+    unsigned long long fixed;              // per call: tr_commit's fixed failures (Call::fix_slots)
 };
 
 enum : unsigned int {
@@ -147,6 +148,9 @@ struct Call {
     // tr_ingest of a small host-buffer call reads the body straight from mapped host memory
     // (`events`) and leaves a copy here for the call's later kernels (null: no copy).
     tb_transfer_t* events_out;
+    // tr_commit's fixed failures (later_claim_status): the id slots they release, tombstoned by
+    // the next kernel (stage_out) -- tr_commit's threads read other events' slots.
+    uint32_t* fix_slots;
     // create_transfers: per-call claims of pending ids by post/void events (epoch:32 | event + 1;
     // words of other epochs are free): the earliest post/void of a pending transfer in the call.
     unsigned long long* pv_slots;
