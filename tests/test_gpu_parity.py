@@ -162,6 +162,52 @@ def test_atomic_path_sparse_keys():
         p.close()
 
 
+@pytest.mark.parametrize("lean", [True, False], ids=["lean", "records"])
+def test_atomic_path_sparse_demotions(lean, monkeypatch):
+    """Sparse key spaces (config 5's shape, >= 65,536 events): tr_ingest applies the FAST deltas
+    itself and, `lean`, writes no per-event record (tr_commit looks the accounts up again). A call
+    that makes tr_commit demote and fix events: limit-flag accounts, duplicate ids, closing flags,
+    post/voids (several of one pending transfer) -- TBG_NO_LEAN_LOOKUP writes the records."""
+    if not lean:
+        monkeypatch.setenv("TBG_NO_LEAN_LOOKUP", "1")
+    rng = np.random.default_rng(21)
+    p = Pair(account_capacity=1 << 19, transfer_capacity=1 << 19, batch_events_max=1 << 17)
+    try:
+        n_acc = 300_000
+        acc = workload.accounts(n_acc, seed=7)
+        acc["flags"][rng.random(n_acc) < 0.01] |= 2  # debits_must_not_exceed_credits
+        for i in range(0, n_acc, 100_000):
+            p.create_accounts(acc[i:i + 100_000], [8189] * 12 + [100_000 - 12 * 8189])
+        n = 70_000
+        split = [8189] * 8 + [n - 8 * 8189]
+        t = workload.transfers_uniform(n, n_acc, seed=7)
+        pend = rng.random(n) < 0.1
+        t["flags"][pend] |= 2
+        t["timeout"][pend & (rng.random(n) < 0.5)] = 5
+        r = p.create_transfers(t, split)
+        pending_ids = t["id"][pend & (r["status"] == 0xFFFFFFFF), 0]
+        u = workload.transfers_uniform(n, n_acc, seed=8, id_offset=1_000_000)
+        dup = rng.random(n) < 0.005
+        u["id"][dup] = u["id"][rng.integers(0, n, size=int(dup.sum()))]
+        u["flags"][rng.random(n) < 0.002] |= 64   # closing_debit
+        u["flags"][rng.random(n) < 0.002] |= 128  # closing_credit
+        u["flags"][rng.random(n) < 0.01] |= 2     # pending
+        pv = rng.random(n) < 0.03
+        u["flags"][pv] = np.where(rng.random(int(pv.sum())) < 0.5, 4, 8)  # post / void
+        u["pending_id"][pv, 0] = pending_ids[rng.integers(0, len(pending_ids) // 4,
+                                                          size=int(pv.sum()))]
+        u["debit_account_id"][pv] = 0
+        u["credit_account_id"][pv] = 0
+        u["ledger"][pv] = 0
+        u["code"][pv] = 0
+        u["amount"][pv, 0] = np.where(rng.random(int(pv.sum())) < 0.5, 0, 2**64 - 1)
+        u["amount"][pv, 1] = np.where(u["amount"][pv, 0] == 0, 0, 2**64 - 1)
+        p.create_transfers(u, split)
+        p.compare_state()
+    finally:
+        p.close()
+
+
 @pytest.mark.parametrize("window", [True, False], ids=["window", "buckets"])
 def test_bucket_path_hot_skew(window, monkeypatch):
     """One call of >= 65,536 events over hot limited accounts: window (pair items, LDS counters)

@@ -420,6 +420,7 @@ Call<Event> make_call(tbg_ctx* ctx, const Event* d_events, uint32_t n, const uin
     c.bal_items = nullptr;
     c.key_bits = 0;
     c.pair_shift = 0;
+    c.lean_lookup = 0;
     c.bucket_counts = nullptr;
     c.n_buckets = 0;
     c.chunk_info = nullptr;
@@ -1551,6 +1552,7 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
     const bool ingest_atomics = use_atomic && !getenv("TBG_NO_INGEST_ATOMICS");
     if (use_buckets && key_bits < 16) key_bits = 16;
     BucketPlan plan{};
+    c.lean_lookup = ingest_atomics && !getenv("TBG_NO_LEAN_LOOKUP");
     if (use_sort && !ingest_atomics) {
         c.bal_items = ctx->bal_items;
         c.key_bits = key_bits;

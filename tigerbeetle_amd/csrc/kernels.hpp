@@ -643,7 +643,8 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
     info |= cls;
     // A FAST event whose balance items are packed needs no per-event record: tr_commit decodes
     // the rows and amount from the items and re-probes the slot if it has to.
-    const bool lean = cls == kClassFast && !pv_fast && c.bal_items && item_packable(c, t.amount.lo);
+    const bool lean = cls == kClassFast && !pv_fast &&
+                      (c.bal_items ? item_packable(c, t.amount.lo) : c.lean_lookup != 0);
     c.ev_info[k] = info | (lean ? kInfoLean : 0);
     if (!lean) {
         c.ev_slot[k] = slot == kNone ? kNone32 : uint32_t(slot);
@@ -983,7 +984,13 @@ __device__ inline FastRec fast_record(const Tables& T, const Call<tb_transfer_t>
     f.s = kNone32;
     f.post_void = (c.events[k].flags & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) != 0;
     const bool lean = (info & kInfoLean) != 0;
-    if (lean && c.pair_shift) {
+    if (lean && !c.bal_items) {
+        // (Call::lean_lookup: the accounts are fixed during the call; FAST means both exist)
+        const tb_transfer_t& e = c.events[k];
+        f.dr = uint32_t(account_find(T, e.debit_account_id));
+        f.cr = uint32_t(account_find(T, e.credit_account_id));
+        f.amount = e.amount.lo;
+    } else if (lean && c.pair_shift) {
         const uint32_t ps = c.pair_shift;
         const uint64_t x = c.bal_items[k];
         f.dr = uint32_t(x & ((1ull << ps) - 1));

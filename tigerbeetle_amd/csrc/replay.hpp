@@ -134,6 +134,9 @@ struct Call {
     // Pair items (the balance window path, key spaces of <= 2^14 accounts): pair_shift = s > 0,
     // one item per event, (amount << 2s + 1) | (pending << 2s) | (cr << s) | dr; ~0 = none.
     uint32_t pair_shift;
+    // Calls whose ingest applies the FAST deltas itself (no balance items, sparse key spaces):
+    // FAST events write no record either (kInfoLean); tr_commit looks their accounts up again.
+    uint32_t lean_lookup;
     // Bucketed balance path (small key spaces): per-bucket item counts, bucket = key >> 13.
     unsigned int* bucket_counts;
     uint32_t n_buckets;
@@ -167,8 +170,9 @@ enum : uint8_t {
     kInfoPending = 1 << 4,     // flags.pending
     kInfoTimeout = 1 << 5,     // timeout > 0
     kInfoClaimed = 1 << 6,     // the event claimed / found its id slot
-    kInfoLean = 1 << 7,        // FAST with packed balance items: ev_slot / ev_dr / ev_cr /
-                               // ev_amount were not written (the items hold rows and amount)
+    kInfoLean = 1 << 7,        // FAST without a record: ev_slot / ev_dr / ev_cr / ev_amount
+                               // were not written (the packed balance items hold rows and
+                               // amount, or, Call::lean_lookup, tr_commit looks them up)
 };
 
 template <typename C>
