@@ -464,21 +464,25 @@ def test_flow_replay_stress(seed):
         p.close()
 
 
-@pytest.mark.parametrize("walk", ["wave", "one-lane"])
+@pytest.mark.parametrize("walk", ["wave", "wave-seq", "one-lane"])
 @pytest.mark.parametrize("n_acc", [200, 700], ids=["lanes", "over-lanes"])
 def test_account_lanes_limits(n_acc, walk, monkeypatch):
     """Calls whose replayed events are all limit events run on the account lanes (one lane per
     limited account): debits_must_not_exceed_credits and credits_must_not_exceed_debits on both
     sides, transfers between two limited accounts (both verdicts needed), between a limited and an
     unlimited account, and funding; 700 limited accounts exceed the lanes (the flow replay runs).
-    `walk`: one wave per walked owner (lanes_walk) or one lane (lanes_replay)."""
+    `walk`: one wave per walked owner (lanes_walk; wave-wide steps or, TBG_WALK_SEQ, event by
+    event) or one lane (lanes_replay)."""
     if walk == "one-lane":
         monkeypatch.setenv("TBG_LANES_ONE_LANE", "1")
+    if walk == "wave-seq":  # the walk event by event (no wave-wide steps)
+        monkeypatch.setenv("TBG_WALK_SEQ", "1")
     rng = np.random.default_rng(n_acc)
     p = Pair(account_capacity=1 << 12, transfer_capacity=1 << 17, batch_events_max=1 << 15)
     try:
         acc = workload.accounts(n_acc, seed=11, ledger=2)
-        acc["flags"] = rng.choice([0, 2, 4], size=n_acc, p=[0.2, 0.4, 0.4]).astype(np.uint16)
+        # (6: both limits -- such an owner walks event by event)
+        acc["flags"] = rng.choice([0, 2, 4, 6], size=n_acc, p=[0.2, 0.35, 0.35, 0.1]).astype(np.uint16)
         acc["flags"][0] = 0  # an unlimited source
         p.create_accounts(acc, _split(n_acc, rng, 512))
         fund = workload.funding_transfers(n_acc - 1, 50_000, id_offset=1 << 30)
@@ -562,7 +566,7 @@ def test_flow_additive_accounts(additive, monkeypatch):
         p.close()
 
 
-@pytest.mark.parametrize("walk", ["wave", "one-lane"])
+@pytest.mark.parametrize("walk", ["wave", "wave-seq", "one-lane"])
 @pytest.mark.parametrize("free_owners", [True, False], ids=["free", "walked"])
 def test_account_lanes_free_owners(free_owners, walk, monkeypatch):
     """Account lanes with free owners (lanes.hpp): limited accounts funded beyond every amount
@@ -574,6 +578,8 @@ def test_account_lanes_free_owners(free_owners, walk, monkeypatch):
         monkeypatch.setenv("TBG_NO_FREE_OWNERS", "1")
     if walk == "one-lane":
         monkeypatch.setenv("TBG_LANES_ONE_LANE", "1")
+    if walk == "wave-seq":  # the walk event by event (no wave-wide steps)
+        monkeypatch.setenv("TBG_WALK_SEQ", "1")
     rng = np.random.default_rng(91)
     p = Pair(account_capacity=64, transfer_capacity=1 << 14, batch_events_max=1 << 12)
     try:
@@ -607,7 +613,7 @@ def test_account_lanes_free_owners(free_owners, walk, monkeypatch):
         p.close()
 
 
-@pytest.mark.parametrize("walk", ["wave", "one-lane"])
+@pytest.mark.parametrize("walk", ["wave", "wave-seq", "one-lane"])
 def test_account_walk_long_owner(walk, monkeypatch):
     """One walked owner with ~100k events in a single call (its funding runs out a third of the
     way), a second walked owner in another wave with a few hundred events, transfers between them
@@ -616,6 +622,8 @@ def test_account_walk_long_owner(walk, monkeypatch):
     ADVICE r1)."""
     if walk == "one-lane":
         monkeypatch.setenv("TBG_LANES_ONE_LANE", "1")
+    if walk == "wave-seq":  # the walk event by event (no wave-wide steps)
+        monkeypatch.setenv("TBG_WALK_SEQ", "1")
     rng = np.random.default_rng(4242)
     p = Pair(account_capacity=64, transfer_capacity=1 << 18, batch_events_max=1 << 17)
     try:

@@ -633,6 +633,7 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
     L.counts = F.lane_counts;
     L.epoch = c.epoch;
     L.acc_free = F.acc_free;
+    L.walk_seq = getenv("TBG_WALK_SEQ") != nullptr;
 
     const dim3 block(kBlock);
     const uint64_t pairs = kFlowKeys * uint64_t(m);

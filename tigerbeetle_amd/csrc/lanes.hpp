@@ -66,6 +66,7 @@ struct LanePlan {
     unsigned int* counts;     // [0] owners, [1] ineligible events, [2] handled (set by the engine)
     uint32_t epoch;
     uint32_t* acc_free;       // per account row: epoch of the call in which it is a free owner
+    uint32_t walk_seq;        // lanes_walk: every window event by event (TBG_WALK_SEQ)
 };
 
 // The rings' loads are inline asm, so the compiler inserts no wait for them: its wait analysis
@@ -369,6 +370,10 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
     unsigned int* progress = &L.counts[3];
 
     const tb_account_t& acc0 = T.acc_rows[row];
+    const uint32_t oflags = walk_uniform(acc0.flags);
+    const bool owner_dm = (oflags & TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS) != 0;
+    const bool owner_cm = (oflags & TB_ACCOUNT_CREDITS_MUST_NOT_EXCEED_DEBITS) != 0;
+    const bool one_limit = owner_dm != owner_cm && !L.walk_seq;
     const u128 dpe = walk_uniform128(acc0.debits_pending);
     const u128 cpe = walk_uniform128(acc0.credits_pending);
     u128 dpo = walk_uniform128(acc0.debits_posted);
@@ -451,6 +456,33 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
         const bool narrow = __ballot(cur.valid && cur.amt_hi >= (1u << 24)) == 0 &&
                             (dpe >> 62) == 0 && (dpo >> 62) == 0 && (cpe >> 62) == 0 &&
                             (cpo >> 62) == 0;
+        // The other side's verdict of window event j (not in the snapshot): poll its word.
+        auto wait_verdict = [&](uint32_t j, bool debit) -> bool {
+            const uint64_t tp0 = dbg ? wall_clock64() : 0;
+            n_poll++;
+            publish();  // (an owner this one waits on may wait on these)
+            const uint32_t sj = __builtin_amdgcn_readlane(cur.s, j);
+            const uint32_t need = debit ? kMbCrSet : kMbDrSet;
+            uint32_t mb = 0;
+            while (!stalled) {
+                mb = walk_uniform(__hip_atomic_load(&mbox[sj], __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT));
+                if (mb & need) break;
+                __builtin_amdgcn_s_sleep(1);
+                if ((++spins & 255) == 0) {
+                    const unsigned int p = walk_uniform(__hip_atomic_load(
+                        progress, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                    if (p != seen) {
+                        seen = p;
+                        spins = 0;
+                    } else if (spins > kFlowSpinLimit) {
+                        stalled = true;
+                    }
+                }
+            }
+            if (dbg) t_poll += wall_clock64() - tp0;
+            return (mb & (debit ? kMbCrOk : kMbDrOk)) != 0;
+        };
         auto walk_events = [&](auto dpe_v, auto& dpo_v, auto cpe_v, auto& cpo_v) {
             using V = decltype(dpe_v);
             for (uint32_t j = 0; j < cnt; j++) {
@@ -474,34 +506,11 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
                 }
                 bool other_ok = true;
                 if (other_m & bit) {
-                    uint32_t mb = 0;
                     if (snap_set & bit) {
                         other_ok = (snap_ok & bit) != 0;
                         n_snap++;
                     } else {
-                        const uint64_t tp0 = dbg ? wall_clock64() : 0;
-                        n_poll++;
-                        publish();  // (an owner this one waits on may wait on these)
-                        const uint32_t sj = __builtin_amdgcn_readlane(cur.s, j);
-                        const uint32_t need = debit ? kMbCrSet : kMbDrSet;
-                        while (!stalled) {
-                            mb = walk_uniform(__hip_atomic_load(&mbox[sj], __ATOMIC_RELAXED,
-                                                                __HIP_MEMORY_SCOPE_AGENT));
-                            if (mb & need) break;
-                            __builtin_amdgcn_s_sleep(1);
-                            if ((++spins & 255) == 0) {
-                                const unsigned int p = walk_uniform(__hip_atomic_load(
-                                    progress, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-                                if (p != seen) {
-                                    seen = p;
-                                    spins = 0;
-                                } else if (spins > kFlowSpinLimit) {
-                                    stalled = true;
-                                }
-                            }
-                        }
-                        other_ok = (mb & (debit ? kMbCrOk : kMbDrOk)) != 0;
-                        if (dbg) t_poll += wall_clock64() - tp0;
+                        other_ok = wait_verdict(j, debit);
                     }
                 }
                 const bool dr_fail = debit ? !my_ok : !other_ok;
@@ -515,7 +524,101 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
                 }
             }
         };
-        if (narrow) {
+        if (narrow && one_limit) {
+            // An owner with one limit flag: its checked ("mine") events all test used + amount <=
+            // cap -- debits_must_not_exceed_credits: used = dpe + dpo, cap = cpo; credits_must_
+            // not_exceed_debits: used = cpe + cpo, cap = dpo -- a created mine event adds to
+            // `used`, a created other event to `cap`. The window resolves in wave-wide steps:
+            // (A) if used + (every mine amount) <= cap, every mine check passes whatever the
+            // other events do; (B) else, with the state fixed, every event up to the first one
+            // that would be created (or whose other verdict is unknown) is not created -- a
+            // ballot finds it, it is applied, and the scan resumes after it. Steps are created
+            // events + polls, not events: config 3's exhausted owners fail most of theirs.
+            const uint64_t dpe64 = uint64_t(dpe), cpe64 = uint64_t(cpe);
+            uint64_t used = owner_dm ? dpe64 + uint64_t(dpo) : cpe64 + uint64_t(cpo);
+            uint64_t cap = owner_dm ? uint64_t(cpo) : uint64_t(dpo);
+            const uint64_t used0 = used, cap0 = cap;
+            const uint64_t amt = cur.valid ? walk_u64(cur.amt_lo, cur.amt_hi) : 0;
+            const bool l_mine = (mine_m >> lane) & 1, l_other = (other_m >> lane) & 1;
+            uint64_t known = snap_set & other_m, known_ok = snap_ok & other_m;
+            n_snap += __popcll(known);
+            uint64_t mine_sum = l_mine ? amt : 0;
+            for (int off = 32; off > 0; off >>= 1) mine_sum += __shfl_xor(mine_sum, off);
+            mine_sum = walk_uniform64(mine_sum);
+            if (used + mine_sum <= cap) {
+                decided = mine_m;
+                myok_m = mine_m;
+                publish();
+                for (uint64_t u = other_m & ~known; u != 0; u &= u - 1) {
+                    const uint32_t j = uint32_t(__builtin_ctzll(u));
+                    known |= 1ull << j;
+                    if (wait_verdict(j, (debit_m >> j) & 1)) known_ok |= 1ull << j;
+                }
+                created_m = vmask & (~other_m | known_ok);
+                drfail_m = vmask & ~created_m & ~debit_m;  // (credit events: the debit side failed)
+                uint64_t add_used = ((created_m & mine_m) >> lane) & 1 ? amt : 0;
+                uint64_t add_cap = ((created_m & ~mine_m) >> lane) & 1 ? amt : 0;
+                for (int off = 32; off > 0; off >>= 1) {
+                    add_used += __shfl_xor(add_used, off);
+                    add_cap += __shfl_xor(add_cap, off);
+                }
+                used += walk_uniform64(add_used);
+                cap += walk_uniform64(add_cap);
+            } else {
+                uint64_t rem = vmask;
+                while (rem != 0 && !stalled) {
+                    const bool in = (rem >> lane) & 1;
+                    const bool ok_mine = !l_mine || used + amt <= cap;
+                    const bool unknown = l_other && !((known >> lane) & 1);
+                    const bool creates = ok_mine && (!l_other || ((known_ok >> lane) & 1));
+                    const uint64_t brk = __ballot(in && (unknown || creates));
+                    const uint64_t okm = __ballot(in && l_mine && ok_mine);
+                    // (not created: a debit event's debit side fails when it is the owner's check,
+                    // a credit event's when the other owner said so)
+                    const uint64_t drf = __ballot(in && ((l_mine && !ok_mine && ((debit_m >> lane) & 1)) ||
+                                                         (l_other && !((debit_m >> lane) & 1) &&
+                                                          !((known_ok >> lane) & 1))));
+                    const uint64_t before = brk ? ((brk & (0 - brk)) - 1) & rem : rem;
+                    decided |= before & mine_m;
+                    myok_m |= before & okm;
+                    drfail_m |= before & drf;
+                    rem &= ~before;
+                    if (brk == 0) break;
+                    const uint32_t j = uint32_t(__builtin_ctzll(brk));
+                    const uint64_t bit = 1ull << j;
+                    if ((other_m & bit) && !(known & bit)) {
+                        // Its own check first (the state is final up to j): the other owner may
+                        // be waiting on this very verdict.
+                        if (mine_m & bit) {
+                            decided |= bit;
+                            if ((okm >> j) & 1) myok_m |= bit;
+                        }
+                        known |= bit;
+                        if (wait_verdict(j, (debit_m & bit) != 0)) known_ok |= bit;
+                        continue;
+                    }
+                    const uint64_t a = walk_u64(__builtin_amdgcn_readlane(cur.amt_lo, j),
+                                                __builtin_amdgcn_readlane(cur.amt_hi, j));
+                    created_m |= bit;
+                    if (mine_m & bit) {
+                        decided |= bit;
+                        myok_m |= bit;
+                        used += a;
+                    } else {
+                        cap += a;
+                    }
+                    rem &= ~bit;
+                    publish();
+                }
+            }
+            if (owner_dm) {
+                dpo = u128(uint64_t(dpo) + (used - used0));
+                cpo = u128(uint64_t(cpo) + (cap - cap0));
+            } else {
+                cpo = u128(uint64_t(cpo) + (used - used0));
+                dpo = u128(uint64_t(dpo) + (cap - cap0));
+            }
+        } else if (narrow) {
             uint64_t dpo64 = uint64_t(dpo), cpo64 = uint64_t(cpo);
             walk_events(uint64_t(dpe), dpo64, uint64_t(cpe), cpo64);
             dpo = dpo64;
