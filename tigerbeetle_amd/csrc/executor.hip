@@ -699,6 +699,9 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
             }
         }
         hipLaunchKernelGGL(lanes_finish, dim3(grid_for(m)), block, 0, ctx->stream, ctx->T, c, L);
+        if (!getenv("TBG_NO_FREE_OWNERS"))
+            hipLaunchKernelGGL(lanes_free_sums, dim3(grid_for(pairs)), block, 0, ctx->stream,
+                               ctx->T, L, pairs);
         tmark(ctx, "tr_lanes");
         P.skip = &F.lane_counts[2];
     }

@@ -42,6 +42,7 @@ enum : uint32_t {
     kLaneDrOwner = 1, kLaneCrOwner = 2,  // the account has a limit flag
     kLaneDrDecides = 4,                  // dr has debits_must_not_exceed_credits
     kLaneCrDecides = 8,                  // cr has credits_must_not_exceed_debits
+    kLaneDrFree = 16, kLaneCrFree = 32,  // the side's owner is free (lanes_free_sums adds it)
 };
 // mailbox bits per event
 enum : uint32_t { kMbDrSet = 1, kMbDrOk = 2, kMbCrSet = 4, kMbCrOk = 8 };
@@ -126,9 +127,9 @@ __global__ void lanes_free(Tables T, LanePlan L) {
     const uint32_t cr = L.steps[s].cr;
     uint32_t bits = r.bits;
     if ((bits & kLaneDrOwner) && L.acc_free[r.dr] == L.epoch)
-        bits &= ~uint32_t(kLaneDrOwner | kLaneDrDecides);
+        bits = (bits & ~uint32_t(kLaneDrOwner | kLaneDrDecides)) | kLaneDrFree;
     if ((bits & kLaneCrOwner) && L.acc_free[cr] == L.epoch)
-        bits &= ~uint32_t(kLaneCrOwner | kLaneCrDecides);
+        bits = (bits & ~uint32_t(kLaneCrOwner | kLaneCrDecides)) | kLaneCrFree;
     if (bits == r.bits) return;
     L.recs[s].bits = bits;
     if (!(bits & (kLaneDrOwner | kLaneCrOwner))) L.outcome[s] = kOutCreated;
@@ -666,12 +667,13 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
 // After the lanes, one lane per event: the result (timestamp, verdict), the sides of created
 // events that no lane owns (u128 atomics: their balances are never read in the call), and the
 // transfers key_max.
-// Adds `amount` to balance field `key` (kNone32: nothing) with one u128 atomic per distinct key
-// of the wave: lanes with equal keys are summed first. (Free owners' sides go through here; config
-// 3's hottest account takes ~20k adds per call on one field.) Every lane of the wave calls it.
-__device__ inline void wave_add_field(const BalTarget& B, uint32_t key, uint64_t amount) {
+// Adds `amount` to balance field `key` (kNone32: nothing) with u128 atomics: the lanes sharing the
+// key of the first pending lane are summed first (`rounds` times; a key that dominates the wave
+// takes one atomic), the rest add their own. Every lane of the wave calls it.
+__device__ inline void wave_add_field(const BalTarget& B, uint32_t key, uint64_t amount,
+                                      int rounds = 64) {
     const uint32_t lane = threadIdx.x & 63;
-    while (true) {
+    for (int r = 0; r < rounds; r++) {
         const uint64_t pend = __ballot(key != kNone32);
         if (pend == 0) break;
         const int leader = __ffsll((unsigned long long)pend) - 1;
@@ -687,6 +689,53 @@ __device__ inline void wave_add_field(const BalTarget& B, uint32_t key, uint64_t
         }
         if (lane == uint32_t(leader)) add_field(B, lkey, (u128(hi) << 64) | lo, true);
         if (mine) key = kNone32;
+    }
+    if (key != kNone32) add_field(B, key, u128(amount), true);
+}
+
+// Free owners' sides (lanes_free): every created event's amount on the owner's posted field, one
+// u128 atomic per run of the owner's grouped pairs in a wave (the pairs are grouped by account, so
+// a segmented sum over 64 consecutive pairs; config 3's hottest free owner takes ~20k events per
+// call on one field -- as per-event atomics, contention).
+__global__ void lanes_free_sums(Tables T, LanePlan L, uint64_t pairs) {
+    const uint64_t p = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63;
+    uint64_t run = ~0ull;  // the account key (tag | row) of the pair; ~0: none
+    uint64_t dlo = 0, dhi = 0, clo = 0, chi = 0;
+    const bool ok = L.counts[2] && !(T.scalars->flags & kFlagFlowStalled);
+    if (ok && p < pairs && p < *L.n_pairs) {
+        const uint64_t key = L.keys_sorted[p];
+        run = key >> kFlowUnitBits;
+        const uint32_t row = uint32_t(run & 0xFFFFFFFFu);
+        if ((run >> 32) == 1 && L.acc_free[row] == L.epoch) {
+            const uint32_t s = uint32_t(key & ((1u << kFlowUnitBits) - 1));
+            if (s < L.m && L.outcome[s] == kOutCreated) {
+                const LaneRec r = L.recs[s];
+                if (r.dr == row && (r.bits & kLaneDrFree)) dlo = r.amount;
+                else if (r.dr != row && (r.bits & kLaneCrFree)) clo = r.amount;
+            }
+        }
+    }
+    // Segmented inclusive sums over the wave (runs of equal `run` are contiguous).
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint64_t orun = __shfl_up(run, off);
+        const uint64_t odlo = __shfl_up(dlo, off), odhi = __shfl_up(dhi, off);
+        const uint64_t oclo = __shfl_up(clo, off), ochi = __shfl_up(chi, off);
+        if (lane >= uint32_t(off) && orun == run) {
+            const uint64_t nd = dlo + odlo, nc = clo + oclo;
+            dhi += odhi + (nd < dlo ? 1u : 0u);
+            chi += ochi + (nc < clo ? 1u : 0u);
+            dlo = nd;
+            clo = nc;
+        }
+    }
+    const uint64_t next = __shfl_down(run, 1);
+    const bool last = lane == 63 || next != run;
+    if (last && run != ~0ull) {
+        const BalTarget B{T.acc_rows, T.acc_index, T.acc_entry_of};
+        const uint32_t row = uint32_t(run & 0xFFFFFFFFu);
+        add_field(B, row * 4 + 1, (u128(dhi) << 64) | dlo, true);
+        add_field(B, row * 4 + 3, (u128(chi) << 64) | clo, true);
     }
 }
 
@@ -710,13 +759,14 @@ __global__ void lanes_finish(Tables T, Call<tb_transfer_t> c, LanePlan L) {
         if (out == kOutCreated) {
             ts_max = st.ts_event;
             amount = rec.amount;
-            if (!(rec.bits & kLaneDrOwner)) dr_key = st.dr * 4 + 1;
-            if (!(rec.bits & kLaneCrOwner)) cr_key = st.cr * 4 + 3;
+            if (!(rec.bits & (kLaneDrOwner | kLaneDrFree))) dr_key = st.dr * 4 + 1;
+            if (!(rec.bits & (kLaneCrOwner | kLaneCrFree))) cr_key = st.cr * 4 + 3;
         }
     }
+    // (sides of free owners: lanes_free_sums; the unowned sides here are mostly distinct)
     const BalTarget B{T.acc_rows, T.acc_index, T.acc_entry_of};
-    wave_add_field(B, dr_key, amount);
-    wave_add_field(B, cr_key, amount);
+    wave_add_field(B, dr_key, amount, 2);
+    wave_add_field(B, cr_key, amount, 2);
     ts_max = block_reduce(ts_max, OpMax());
     if (threadIdx.x == 0 && ts_max)
         atomicMax(&T.scalars->transfers_key_max, (unsigned long long)ts_max);
