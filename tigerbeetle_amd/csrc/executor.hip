@@ -45,6 +45,7 @@ constexpr uint32_t kSortThreshold = 1u << 16;
 constexpr uint64_t kAtomicKeysPerItem = 8;
 // Calls up to this many events find their chunks' batch bounds inside tr_ingest.
 constexpr uint32_t kInlineChunkMax = 1u << 16;
+constexpr size_t kFlowDebugBytes = 8 * (16 + 8 * 1000);  // TBG_FLOW_DEBUG counters (+ per owner)
 
 struct PulseScratch {
     uint64_t capacity = 0;  // a multiple of kPulseRun (pulse.hpp's sorted runs)
@@ -683,8 +684,8 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
         else {
             const bool dbg = getenv("TBG_FLOW_DEBUG") != nullptr;
             if (dbg) {
-                if (!ctx->flow_debug) HIP_TRY(ctx, hipMalloc(&ctx->flow_debug, 128));
-                HIP_TRY(ctx, hipMemsetAsync(ctx->flow_debug, 0, 128, ctx->stream));
+                if (!ctx->flow_debug) HIP_TRY(ctx, hipMalloc(&ctx->flow_debug, kFlowDebugBytes));
+                HIP_TRY(ctx, hipMemsetAsync(ctx->flow_debug, 0, kFlowDebugBytes, ctx->stream));
             }
             hipLaunchKernelGGL(lanes_walk, dim3(kLanesMax / kWalkWaves), dim3(kWalkWaves * 64), 0,
                                ctx->stream, ctx->T, c, L, F.mb_index,
@@ -696,6 +697,19 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
                 fprintf(stderr, "walk: m=%u walks=%llu windows=%llu events=%llu polls=%llu "
                         "poll_us=%.1f snapshot_hits=%llu longest_walk_us=%.1f\n", m, d[6], d[0],
                         d[1], d[2], d[3] / 100.0, d[5], d[4] / 100.0);
+                std::vector<unsigned long long> o(8 * 1000);
+                (void)hipMemcpy(o.data(), ctx->flow_debug + 16, o.size() * 8, hipMemcpyDeviceToHost);
+                std::vector<uint32_t> idx;
+                for (uint32_t i = 0; i < 1000; i++)
+                    if (o[8 * i]) idx.push_back(i);
+                std::sort(idx.begin(), idx.end(),
+                          [&](uint32_t a, uint32_t b) { return o[8 * a] > o[8 * b]; });
+                for (size_t i = 0; i < idx.size() && i < 3; i++) {
+                    const unsigned long long* w = &o[8 * idx[i]];
+                    fprintf(stderr, "  owner %u: events=%llu windows=%llu all_pass=%llu iters=%llu "
+                            "polls=%llu poll_us=%.1f walk_us=%.1f\n", idx[i], w[0], w[4], w[6],
+                            w[5], w[1], w[2] / 100.0, w[3] / 100.0);
+                }
             }
         }
         hipLaunchKernelGGL(lanes_finish, dim3(grid_for(m)), block, 0, ctx->stream, ctx->T, c, L);
@@ -708,7 +722,7 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
     tmark(ctx, "flow_plan");
     const bool debug = getenv("TBG_FLOW_DEBUG") != nullptr;
     if (debug) {
-        if (!ctx->flow_debug) HIP_TRY(ctx, hipMalloc(&ctx->flow_debug, 128));
+        if (!ctx->flow_debug) HIP_TRY(ctx, hipMalloc(&ctx->flow_debug, kFlowDebugBytes));
         HIP_TRY(ctx, hipMemsetAsync(ctx->flow_debug, 0, 128, ctx->stream));
         P.debug = ctx->flow_debug;
     }

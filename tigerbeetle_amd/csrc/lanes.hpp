@@ -351,7 +351,7 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
     // dbg (TBG_FLOW_DEBUG): [0] windows, [1] events, [2] live polls, [3] poll cycles,
     // [4] max walk cycles, [5] verdicts found in snapshots, [6] walks (100 MHz wall clock)
     const uint64_t t_walk0 = wall_clock64();
-    uint64_t n_win = 0, n_ev = 0, n_poll = 0, t_poll = 0, n_snap = 0;
+    uint64_t n_win = 0, n_ev = 0, n_poll = 0, t_poll = 0, n_snap = 0, n_iter = 0, n_alla = 0;
     const uint32_t owners = L.counts[0];
     const bool run = L.counts[1] == 0 && owners != 0 && owners <= kLanesMax;
     if (blockIdx.x == 0 && threadIdx.x == 0 && run) {
@@ -384,11 +384,26 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
         const uint64_t p = base + lane;
         *key = p < n_pairs ? L.keys_sorted[p] : ~0ull;
     };
-    auto fetch_recs = [&](uint64_t key, WalkWindow* w) {
+    // A window as loaded: nothing computed from the loads here, so that no load waits for another
+    // (the snapshot word is loaded for every valid event, needed or not).
+    struct WalkRaw {
+        uint32_t s;
+        LaneRec r;
+        uint32_t mb;
+        bool valid;
+    };
+    auto fetch_recs = [&](uint64_t key, WalkRaw* w) {
         w->valid = key != ~0ull && (key >> kFlowUnitBits) == my_key;
         const uint32_t s = uint32_t(key & ((1u << kFlowUnitBits) - 1));
         w->s = w->valid && s < L.m ? s : 0u;
-        const LaneRec r = L.recs[w->s];
+        w->r = L.recs[w->s];
+        w->mb = w->valid ? __hip_atomic_load(&mbox[w->s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                         : 0u;
+    };
+    auto decode = [&](const WalkRaw& x, WalkWindow* w) {
+        w->valid = x.valid;
+        w->s = x.s;
+        const LaneRec r = x.r;
         const bool debit = r.dr == row;
         const bool dec_dr = (r.bits & kLaneDrDecides) != 0, dec_cr = (r.bits & kLaneCrDecides) != 0;
         const bool mine = debit ? dec_dr : dec_cr;
@@ -399,24 +414,67 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
                   (other_owner && mine ? kWalkOtherOwner : 0u) | (writer ? kWalkWriter : 0u);
         w->amt_lo = uint32_t(r.amount);
         w->amt_hi = uint32_t(r.amount >> 32);
-        w->mb = other && w->valid
-                    ? __hip_atomic_load(&mbox[w->s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                    : 0u;
+        w->mb = other && w->valid ? x.mb : 0u;
     };
 
+    // Super windows of four windows (256 events): the records (and snapshot) of super window W + 1
+    // are issued as W starts, their pairs one super window earlier -- one memory round trip per
+    // four windows, overlapped with W's work. (Loads whose address is a loaded value wait for
+    // everything issued before them: a deeper ring of single windows waits as often.)
     uint64_t base = start;
-    uint64_t key_cur, key_next;
-    fetch_pairs(base, &key_cur);
-    WalkWindow cur;
-    fetch_recs(key_cur, &cur);
-    fetch_pairs(base + 64, &key_next);
+    WalkRaw b0, b1, b2, b3;
+    uint64_t k0, k1, k2, k3;  // the pairs of the next super window
+    {
+        uint64_t p0, p1, p2, p3;
+        fetch_pairs(base, &p0);
+        fetch_pairs(base + 64, &p1);
+        fetch_pairs(base + 128, &p2);
+        fetch_pairs(base + 192, &p3);
+        fetch_recs(p0, &b0);
+        fetch_recs(p1, &b1);
+        fetch_recs(p2, &b2);
+        fetch_recs(p3, &b3);
+        fetch_pairs(base + 256, &k0);
+        fetch_pairs(base + 320, &k1);
+        fetch_pairs(base + 384, &k2);
+        fetch_pairs(base + 448, &k3);
+    }
     uint64_t spins = 0;
     unsigned int seen = 0;
     bool stalled = false;
-    while (true) {
+    bool done = false;
+    while (!done) {
+        const bool more_super = (__ballot(b3.valid) >> 63) & 1;
+        WalkRaw n0, n1, n2, n3;
+        n0.valid = n1.valid = n2.valid = n3.valid = false;
+        uint64_t q0 = ~0ull, q1 = ~0ull, q2 = ~0ull, q3 = ~0ull;
+        if (more_super) {
+            fetch_recs(k0, &n0);
+            fetch_recs(k1, &n1);
+            fetch_recs(k2, &n2);
+            fetch_recs(k3, &n3);
+            fetch_pairs(base + 512, &q0);
+            fetch_pairs(base + 576, &q1);
+            fetch_pairs(base + 640, &q2);
+            fetch_pairs(base + 704, &q3);
+        }
+      for (uint32_t sub = 0; sub < 4; sub++) {
+        // (field by field: a select of whole structs goes through scratch)
+        WalkRaw x;
+        x.s = sub == 0 ? b0.s : sub == 1 ? b1.s : sub == 2 ? b2.s : b3.s;
+        x.r.amount = sub == 0 ? b0.r.amount : sub == 1 ? b1.r.amount : sub == 2 ? b2.r.amount : b3.r.amount;
+        x.r.dr = sub == 0 ? b0.r.dr : sub == 1 ? b1.r.dr : sub == 2 ? b2.r.dr : b3.r.dr;
+        x.r.bits = sub == 0 ? b0.r.bits : sub == 1 ? b1.r.bits : sub == 2 ? b2.r.bits : b3.r.bits;
+        x.mb = sub == 0 ? b0.mb : sub == 1 ? b1.mb : sub == 2 ? b2.mb : b3.mb;
+        x.valid = sub == 0 ? b0.valid : sub == 1 ? b1.valid : sub == 2 ? b2.valid : b3.valid;
+        WalkWindow cur;
+        decode(x, &cur);
         // The window as scalar masks (one bit per event, in call order).
         const uint64_t vmask = __ballot(cur.valid);
-        if (vmask == 0) break;
+        if (vmask == 0) {
+            done = true;
+            break;
+        }
         const uint64_t debit_m = __ballot(cur.valid && (cur.bits & kWalkDebit));
         const uint64_t mine_m = __ballot(cur.valid && (cur.bits & kWalkMine));
         const uint64_t other_m = __ballot(cur.valid && (cur.bits & kWalkOther));
@@ -426,14 +484,6 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
             __ballot((cur.mb & (my_debit ? kMbCrSet : kMbDrSet)) != 0);
         const uint64_t snap_ok = __ballot((cur.mb & (my_debit ? kMbCrOk : kMbDrOk)) != 0);
         const bool more = (vmask >> 63) & 1;  // the segment continues past this window
-        // Prefetch: the next window's records and snapshot, the pairs after it.
-        WalkWindow nxt;
-        nxt.valid = false;
-        uint64_t key_after = ~0ull;
-        if (more) {
-            fetch_recs(key_next, &nxt);
-            fetch_pairs(base + 128, &key_after);
-        }
         const uint32_t cnt = uint32_t(__popcll(vmask));
         uint64_t created_m = 0, drfail_m = 0, myok_m = 0, published = 0;
         // Verdicts this owner owes are published with one vector atomic per flush: before any
@@ -543,13 +593,28 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
             const bool l_mine = (mine_m >> lane) & 1, l_other = (other_m >> lane) & 1;
             uint64_t known = snap_set & other_m, known_ok = snap_ok & other_m;
             n_snap += __popcll(known);
+            // The words of the window events in `want` read again, all at once (the snapshot is
+            // two windows old): one round trip instead of a poll per event.
+            auto refresh = [&](uint64_t want) {
+                publish();
+                const bool w = (want >> lane) & 1;
+                const uint32_t mb2 = w ? __hip_atomic_load(&mbox[cur.s], __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT)
+                                       : 0u;
+                const uint64_t set = __ballot(w && (mb2 & (my_debit ? kMbCrSet : kMbDrSet)));
+                const uint64_t ok = __ballot(w && (mb2 & (my_debit ? kMbCrOk : kMbDrOk)));
+                known |= set;
+                known_ok |= ok & set;
+            };
             uint64_t mine_sum = l_mine ? amt : 0;
             for (int off = 32; off > 0; off >>= 1) mine_sum += __shfl_xor(mine_sum, off);
             mine_sum = walk_uniform64(mine_sum);
             if (used + mine_sum <= cap) {
+                n_alla++;
                 decided = mine_m;
                 myok_m = mine_m;
                 publish();
+                if (other_m & ~known) refresh(other_m & ~known);
                 for (uint64_t u = other_m & ~known; u != 0; u &= u - 1) {
                     const uint32_t j = uint32_t(__builtin_ctzll(u));
                     known |= 1ull << j;
@@ -568,11 +633,15 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
             } else {
                 uint64_t rem = vmask;
                 while (rem != 0 && !stalled) {
+                    n_iter++;
                     const bool in = (rem >> lane) & 1;
                     const bool ok_mine = !l_mine || used + amt <= cap;
                     const bool unknown = l_other && !((known >> lane) & 1);
                     const bool creates = ok_mine && (!l_other || ((known_ok >> lane) & 1));
-                    const uint64_t brk = __ballot(in && (unknown || creates));
+                    // (an unknown verdict matters only when the own check passes: else the event
+                    // is not created, and a credit event's other side is a walked owner -- the
+                    // writer of its outcome)
+                    const uint64_t brk = __ballot(in && ((unknown && ok_mine) || creates));
                     const uint64_t okm = __ballot(in && l_mine && ok_mine);
                     // (not created: a debit event's debit side fails when it is the owner's check,
                     // a credit event's when the other owner said so)
@@ -594,8 +663,11 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
                             decided |= bit;
                             if ((okm >> j) & 1) myok_m |= bit;
                         }
-                        known |= bit;
-                        if (wait_verdict(j, (debit_m & bit) != 0)) known_ok |= bit;
+                        refresh(other_m & ~known & rem);
+                        if (!(known & bit)) {
+                            known |= bit;
+                            if (wait_verdict(j, (debit_m & bit) != 0)) known_ok |= bit;
+                        }
                         continue;
                     }
                     const uint64_t a = walk_u64(__builtin_amdgcn_readlane(cur.amt_lo, j),
@@ -641,10 +713,21 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
         if (lane == 0) atomicAdd(progress, 1u);
         n_win++;
         n_ev += cnt;
-        if (!more) break;
-        base += 64;
-        cur = nxt;
-        key_next = key_after;
+        if (!more) {
+            done = true;
+            break;
+        }
+      }
+        if (done) break;
+        base += 256;
+        b0 = n0;
+        b1 = n1;
+        b2 = n2;
+        b3 = n3;
+        k0 = q0;
+        k1 = q1;
+        k2 = q2;
+        k3 = q3;
     }
     if (lane == 0) {
         tb_account_t& acc = T.acc_rows[row];
@@ -660,6 +743,17 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
             atomicMax(&dbg[4], wall_clock64() - t_walk0);
             atomicAdd(&dbg[5], n_snap);
             atomicAdd(&dbg[6], 1ull);
+            if (o < 1000) {  // per owner: events, polls, poll time, walk time, windows, step
+                             // B iterations, all-pass windows
+                unsigned long long* w = &dbg[16 + 8 * o];
+                w[0] = n_ev;
+                w[1] = n_poll;
+                w[2] = t_poll;
+                w[3] = wall_clock64() - t_walk0;
+                w[4] = n_win;
+                w[5] = n_iter;
+                w[6] = n_alla;
+            }
         }
     }
 }
