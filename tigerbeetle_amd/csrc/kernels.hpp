@@ -1009,9 +1009,10 @@ __device__ inline FastRec fast_record(const Tables& T, const Call<tb_transfer_t>
         f.cr = c.ev_cr[k];
         f.amount = c.ev_amount[k];
     }
-    if (lean && (call_flags & (kFlagImported | kFlagDuplicate | kFlagClosable | kFlagHot |
-                               kFlagPostVoid | kFlagChain))) {
-        // The slot this event's id occupies (its own claim, or an earlier in-call holder's).
+    if (lean && (call_flags & kFlagDuplicate)) {
+        // The slot this event's id occupies (its own claim, or an earlier in-call holder's): the
+        // duplicate check reads it. (Otherwise only a demoted or fixed event needs it: looked up
+        // there.)
         const uint64_t fs = transfer_slot_find(T, c, c.events[k].id);
         f.s = fs == kNone ? kNone32 : uint32_t(fs);
     }
@@ -1156,6 +1157,64 @@ __device__ inline bool chain_demoted(const Tables& T, const Call<tb_transfer_t>&
     return false;
 }
 
+// chain_demoted / chain_fail_status of a wave's events at once (tr_commit): every FAST chain event
+// evaluates fast_demoted_peer (and, when demoted, later_claim_status) for itself once, and the
+// lanes of a chain that lies inside the wave combine them by ballot -- instead of each event
+// re-evaluating every other event of its chain. valid == false: not a chain event, or a chain that
+// crosses the wave's edge (commit_event evaluates it alone). Every lane of the wave calls it.
+struct ChainPre {
+    bool valid;
+    bool demoted;   // chain_demoted
+    uint32_t fail;  // chain_fail_status (calls with post/void)
+};
+__device__ inline ChainPre chain_pre_wave(const Tables& T, const Call<tb_transfer_t>& c,
+                                          uint32_t k, bool active, unsigned int call_flags) {
+    ChainPre p{false, false, 0};
+    if (!(call_flags & kFlagChain)) return p;
+    const uint32_t lane = threadIdx.x & 63;
+    bool linked = false, prev_linked = false, open = false;
+    uint8_t cls = 0;
+    if (active) {
+        const uint32_t b = batch_of_guess(c.batch_ends, c.n_batches, c.n, k);
+        const uint32_t bs = batch_start_of(c, b), be = c.batch_ends[b];
+        linked = (c.events[k].flags & TB_TRANSFER_LINKED) != 0;
+        prev_linked = k > bs && (c.events[k - 1].flags & TB_TRANSFER_LINKED);
+        open = linked && k + 1 >= be;  // linked_event_chain_open
+        cls = c.ev_info[k] & kInfoClassMask;
+    }
+    const bool in_chain = active && (linked || prev_linked);
+    const uint64_t head_m = __ballot(active && !prev_linked);
+    const uint64_t end_m = __ballot(active && (!linked || open));
+    const uint64_t open_m = __ballot(open);
+    const uint64_t fast_m = __ballot(active && cls == kClassFast);
+    bool pd = false;
+    uint32_t lc = 0;
+    if (in_chain && cls == kClassFast) {
+        pd = fast_demoted_peer(T, c, k, call_flags);
+        if (pd && (call_flags & kFlagPostVoid)) lc = later_claim_status(T, c, k, call_flags);
+    }
+    const uint64_t pd_m = __ballot(pd);
+    const uint64_t below = head_m & ((2ull << lane) - 1);       // (lane 63: all ones)
+    const uint64_t above = end_m & ~((1ull << lane) - 1);
+    const bool inside = in_chain && below != 0 && above != 0;
+    const uint32_t x = inside ? 63u - uint32_t(__builtin_clzll(below)) : lane;
+    const uint32_t y = inside ? uint32_t(__builtin_ctzll(above)) : lane;
+    const uint64_t chain_m = inside ? ((y == 63 ? ~0ull : (2ull << y) - 1) & ~((1ull << x) - 1)) : 0;
+    const uint64_t pm = pd_m & chain_m;
+    const uint32_t j = pm ? uint32_t(__builtin_ctzll(pm)) : lane;
+    const uint32_t lc_j = __shfl(lc, int(j));
+    if (!inside) return p;
+    p.valid = true;
+    if (y - x >= kFastChainMax || ((open_m >> y) & 1) || (fast_m & chain_m) != chain_m) {
+        p.demoted = true;
+        return p;
+    }
+    if (pm && (call_flags & kFlagPostVoid) && lc_j)
+        p.fail = j == lane ? lc_j : uint32_t(TB_CT_LINKED_EVENT_FAILED);
+    p.demoted = (pm & ~(1ull << lane)) != 0;
+    return p;
+}
+
 // The effects of a confirmed FAST post/void (post_or_void_pending_transfer :4193-4299): its row,
 // the pending transfer's status, the balance deltas on the pending transfer's accounts, and the
 // pulse_next_timestamp reset (recorded at the event: calls with post/void resolve them in order).
@@ -1198,7 +1257,8 @@ __device__ inline void commit_post_void(const Tables& T, const Call<tb_transfer_
 // One event of tr_commit: applied (committed FAST), done (final DONE), ts_applied (its timestamp).
 __device__ inline void commit_event(const Tables& T, const Call<tb_transfer_t>& c, uint32_t k,
                                     unsigned int call_flags, bool& applied, bool& done,
-                                    bool& slow_out, uint64_t& ts_applied) {
+                                    bool& slow_out, uint64_t& ts_applied,
+                                    const ChainPre pre, uint64_t* expiry_row) {
     applied = false;
     done = false;
     slow_out = false;
@@ -1222,7 +1282,7 @@ __device__ inline void commit_event(const Tables& T, const Call<tb_transfer_t>& 
         // Fixed failures of post/voids racing an earlier FAST one (later_claim_status): DONE.
         uint32_t fixed = 0;
         if (!slow && (call_flags & kFlagPostVoid))
-            fixed = in_chain ? chain_fail_status(T, c, k, call_flags)
+            fixed = in_chain ? (pre.valid ? pre.fail : chain_fail_status(T, c, k, call_flags))
                              : (fr.post_void && !pv_first(c, k, c.events[k].pending_id)
                                     ? later_claim_status(T, c, k, call_flags) : 0u);
         if (fixed) {
@@ -1245,7 +1305,7 @@ __device__ inline void commit_event(const Tables& T, const Call<tb_transfer_t>& 
             if (fs != kNone && (T.tr.slots[fs] & kRefMask) == ref)
                 c.fix_slots[atomicAdd(&T.scalars->fixed, 1ull)] = uint32_t(fs);
         } else if (slow || fast_demoted(T, c, k, call_flags, fr) ||
-                   (in_chain && chain_demoted(T, c, k, call_flags))) {
+                   (in_chain && (pre.valid ? pre.demoted : chain_demoted(T, c, k, call_flags)))) {
             // Demoted: undo the speculative liveness and balance items (or, in a call without
             // items, the deltas ingest applied); the replay decides.
             slow = true;
@@ -1260,7 +1320,8 @@ __device__ inline void commit_event(const Tables& T, const Call<tb_transfer_t>& 
                 it[1] = ~0ull;
             }
             if (lean) {  // the replay reads the record
-                c.ev_slot[k] = s;
+                const uint64_t fs = s != kNone32 ? uint64_t(s) : transfer_slot_find(T, c, c.events[k].id);
+                c.ev_slot[k] = fs == kNone ? kNone32 : uint32_t(fs);
                 c.ev_dr[k] = dr;
                 c.ev_cr[k] = cr;
             }
@@ -1276,7 +1337,7 @@ __device__ inline void commit_event(const Tables& T, const Call<tb_transfer_t>& 
             if (c.bal_items && !item_packable(c, amount))
                 apply_fast_deltas(T, dr, cr, pending, amount, false);
             if (pending && (info & kInfoTimeout)) {
-                expiry_append(T, row, false);
+                *expiry_row = row;  // (appended by the wave: tr_commit)
                 const uint64_t expires_at = ts_applied + T.tr_rows[row].timeout * TB_NS_PER_S;
                 // With post/void in the call the order of updates matters (a post/void resets
                 // pulse_next_timestamp when it names its expiry): recorded at the event, resolved
@@ -1326,15 +1387,39 @@ __global__ void tr_commit(Tables T, Call<tb_transfer_t> c) {
         return;
     }
     uint64_t n_applied = 0, n_done = 0, n_slow = 0, ts_max = 0;
-    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < c.n;
-         k += gridDim.x * blockDim.x) {
-        bool applied, done, slow;
-        uint64_t ts;
-        commit_event(T, c, k, call_flags, applied, done, slow, ts);
-        n_applied += applied;
-        n_done += done;
-        n_slow += slow;
-        ts_max = ts > ts_max ? ts : ts_max;
+    // (wave-uniform loop: chain_pre_wave combines the wave's lanes)
+    const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+    for (uint64_t kb = uint64_t(blockIdx.x) * blockDim.x + (threadIdx.x & ~63u); kb < c.n;
+         kb += stride) {
+        const uint32_t k = uint32_t(kb) + (threadIdx.x & 63);
+        const bool active = k < c.n;
+        const ChainPre pre = chain_pre_wave(T, c, k, active, call_flags);
+        uint64_t exp_row = kNone;
+        if (active) {
+            bool applied, done, slow;
+            uint64_t ts;
+            commit_event(T, c, k, call_flags, applied, done, slow, ts, pre, &exp_row);
+            n_applied += applied;
+            n_done += done;
+            n_slow += slow;
+            ts_max = ts > ts_max ? ts : ts_max;
+        }
+        // The wave's expires_at entries with one counter add (a returning add per entry on one
+        // word serialises: config 4 appends ~30k per 131k-event call).
+        const uint64_t want = __ballot(exp_row != kNone);
+        if (want) {
+            const uint32_t lane = threadIdx.x & 63;
+            const int leader = __ffsll((unsigned long long)want) - 1;
+            unsigned long long base = 0;
+            if (lane == uint32_t(leader))
+                base = atomicAdd(&T.scalars->expiry_count, (unsigned long long)__popcll(want));
+            base = __shfl(base, leader);
+            if (exp_row != kNone) {
+                const uint64_t i = base + __popcll(want & ((1ull << lane) - 1));
+                if (i < T.expiry_capacity) T.expiry[i] = exp_row;
+                else atomicOr(&T.scalars->flags, kFlagTableFull);
+            }
+        }
     }
     // transfers objects tree key_range (groove.zig:1780): the largest committed timestamp.
     n_applied = block_reduce(n_applied, OpAdd());
