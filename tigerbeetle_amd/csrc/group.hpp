@@ -70,6 +70,7 @@ struct GroupPlan {
     // account lanes (lanes.hpp): owner segments and free owners; lanes == false: none
     bool lanes;
     bool free_owners;               // free-owner verdicts (TBG_NO_FREE_OWNERS: none)
+    bool sort_values;               // group_sort: every segment that fits LDS sorts as values
     uint32_t epoch;
     uint32_t* owner_starts;
     unsigned int* lane_counts;      // [0] owners, [1] ineligible events
@@ -507,7 +508,7 @@ struct SegmentLds {
 // kGroupWindowBits values in LDS over the values' range -- set bits, prefix popcounts, enumerate --
 // or, for a sparse segment, an LDS bitonic sort of the values themselves.
 __device__ inline void segment_sort(const uint32_t* in, uint32_t* out, uint32_t off, uint32_t c,
-                                    SegmentLds& L) {
+                                    SegmentLds& L, bool values = false) {
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint32_t* buf = L.buf;
     uint32_t lo = kNone32, hi = 0;
@@ -536,7 +537,7 @@ __device__ inline void segment_sort(const uint32_t* in, uint32_t* out, uint32_t 
     // sort of the next power of two >= c (kNone32 padding), when it fits the buffer.
     uint32_t pw = 1;
     while (pw < c) pw <<= 1;
-    if (pw <= kGroupLdsWords && uint64_t(hi - lo) + 1 > 64ull * pw) {
+    if (pw <= kGroupLdsWords && (values || uint64_t(hi - lo) + 1 > 64ull * pw)) {
         for (uint32_t i = tid; i < pw; i += kGroupBigThreads) buf[i] = i < c ? in[off + i] : kNone32;
         __syncthreads();
         for (uint32_t size = 2; size <= pw; size <<= 1) {
@@ -755,7 +756,7 @@ __global__ void __launch_bounds__(kGroupBigThreads) group_sort(GroupPlan G) {
     const uint32_t nbig = G.counts[1];
     for (uint32_t b = blockIdx.x; b < nbig; b += gridDim.x) {
         const uint4 e = G.big[b];
-        segment_sort(G.vals, G.vals_sorted, e.x, e.y, L);
+        segment_sort(G.vals, G.vals_sorted, e.x, e.y, L, G.sort_values);
     }
 }
 
