@@ -1164,25 +1164,36 @@ __device__ inline bool chain_demoted(const Tables& T, const Call<tb_transfer_t>&
 // crosses the wave's edge (commit_event evaluates it alone). Every lane of the wave calls it.
 struct ChainPre {
     bool valid;
-    bool demoted;   // chain_demoted
-    uint32_t fail;  // chain_fail_status (calls with post/void)
+    bool demoted;     // chain_demoted
+    uint32_t fail;    // chain_fail_status (calls with post/void)
+    int8_t in_chain;  // commit_event's in_chain (-1: not evaluated)
+    bool has_fr;      // fr: the event's FastRec (FAST chain events)
+    FastRec fr;
 };
 __device__ inline ChainPre chain_pre_wave(const Tables& T, const Call<tb_transfer_t>& c,
                                           uint32_t k, bool active, unsigned int call_flags) {
-    ChainPre p{false, false, 0};
-    if (!(call_flags & kFlagChain)) return p;
+    ChainPre p{false, false, 0, -1, false, FastRec{}};
+    if (!(call_flags & kFlagChain)) {
+        p.in_chain = 0;
+        return p;
+    }
     const uint32_t lane = threadIdx.x & 63;
     bool linked = false, prev_linked = false, open = false;
-    uint8_t cls = 0;
+    uint8_t cls = 0, info = 0;
     if (active) {
-        const uint32_t b = batch_of_guess(c.batch_ends, c.n_batches, c.n, k);
-        const uint32_t bs = batch_start_of(c, b), be = c.batch_ends[b];
         linked = (c.events[k].flags & TB_TRANSFER_LINKED) != 0;
-        prev_linked = k > bs && (c.events[k - 1].flags & TB_TRANSFER_LINKED);
-        open = linked && k + 1 >= be;  // linked_event_chain_open
-        cls = c.ev_info[k] & kInfoClassMask;
+        const bool pl = k > 0 && (c.events[k - 1].flags & TB_TRANSFER_LINKED);
+        if (linked || pl) {  // (the batch bounds only for events next to a linked one)
+            const uint32_t b = batch_of_guess(c.batch_ends, c.n_batches, c.n, k);
+            const uint32_t bs = batch_start_of(c, b), be = c.batch_ends[b];
+            prev_linked = pl && k > bs;
+            open = linked && k + 1 >= be;  // linked_event_chain_open
+        }
+        info = c.ev_info[k];
+        cls = info & kInfoClassMask;
     }
     const bool in_chain = active && (linked || prev_linked);
+    p.in_chain = in_chain ? 1 : 0;
     const uint64_t head_m = __ballot(active && !prev_linked);
     const uint64_t end_m = __ballot(active && (!linked || open));
     const uint64_t open_m = __ballot(open);
@@ -1190,7 +1201,11 @@ __device__ inline ChainPre chain_pre_wave(const Tables& T, const Call<tb_transfe
     bool pd = false;
     uint32_t lc = 0;
     if (in_chain && cls == kClassFast) {
-        pd = fast_demoted_peer(T, c, k, call_flags);
+        // (its own record: this thread has not touched it yet -- the same verdict the peers'
+        // fast_demoted_peer reaches from lookups)
+        p.fr = fast_record(T, c, k, call_flags, info);
+        p.has_fr = true;
+        pd = fast_demoted(T, c, k, call_flags, p.fr);
         if (pd && (call_flags & kFlagPostVoid)) lc = later_claim_status(T, c, k, call_flags);
     }
     const uint64_t pd_m = __ballot(pd);
@@ -1270,15 +1285,17 @@ __device__ inline void commit_event(const Tables& T, const Call<tb_transfer_t>& 
     if (call_flags & kFlagPostVoid) c.pnt_call[k] = 0;  // (the replay records its own)
     bool slow = cls == kClassSlow || (call_flags & kFlagImported);
     if (cls == kClassFast) {
-        const FastRec fr = fast_record(T, c, k, call_flags, info);
+        const FastRec fr = pre.has_fr ? pre.fr : fast_record(T, c, k, call_flags, info);
         const uint32_t s = fr.s, dr = fr.dr, cr = fr.cr;
         const uint64_t amount = fr.amount;
         const bool lean = (info & kInfoLean) != 0;
         const bool in_chain =
-            (call_flags & kFlagChain) &&
-            ((c.events[k].flags & TB_TRANSFER_LINKED) ||
-             (k > 0 && (c.events[k - 1].flags & TB_TRANSFER_LINKED) &&
-              k != batch_start_of(c, batch_of_guess(c.batch_ends, c.n_batches, c.n, k))));
+            pre.in_chain >= 0
+                ? pre.in_chain != 0
+                : (call_flags & kFlagChain) &&
+                      ((c.events[k].flags & TB_TRANSFER_LINKED) ||
+                       (k > 0 && (c.events[k - 1].flags & TB_TRANSFER_LINKED) &&
+                        k != batch_start_of(c, batch_of_guess(c.batch_ends, c.n_batches, c.n, k))));
         // Fixed failures of post/voids racing an earlier FAST one (later_claim_status): DONE.
         uint32_t fixed = 0;
         if (!slow && (call_flags & kFlagPostVoid))
