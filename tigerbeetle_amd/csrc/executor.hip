@@ -106,6 +106,13 @@ struct tbg_ctx {
     uint64_t* h_batch_ts = nullptr;
     // The pinned blocks as the GPU addresses them (hostio.hpp kernels read / write them).
     DevScalars* dh_scalars = nullptr;
+    // A call's end as the host sees it without the runtime's stream synchronisation: stage_out's
+    // last workgroup writes the call's sequence number into a pinned word (spin_wait).
+    unsigned int* h_seq = nullptr;
+    unsigned int* dh_seq = nullptr;
+    unsigned int* d_stage_done = nullptr;  // stage_out's finished workgroups
+    unsigned int seq = 0;
+    bool spin_sync = false;
     tb_create_result_t* dh_results = nullptr;
     uint32_t* dh_batch_ends = nullptr;
     uint64_t* dh_batch_ts = nullptr;
@@ -310,7 +317,7 @@ int select_flagged(tbg_ctx* ctx, const uint8_t* flags, uint64_t n, uint32_t* out
 
 int stage_call_outputs(tbg_ctx* ctx, const tb_create_result_t* d_results, tb_create_result_t* dst,
                        uint32_t n, bool scalars, const AeSnapJob* snap = nullptr,
-                       bool fixes = false);
+                       bool fixes = false, unsigned int seq = 0);
 // The scalars block to the host (a kernel writes the mapped pinned copy: no DMA hand-off).
 int sync_scalars(tbg_ctx* ctx) {
     int rc = stage_call_outputs(ctx, nullptr, nullptr, 0, true);
@@ -1266,13 +1273,33 @@ int stage_call_inputs(tbg_ctx* ctx, const void* events, uint64_t bytes, uint32_t
 }
 
 // Results (n > 0) and / or the scalars block to mapped host memory, as one kernel on the stream.
+// Waits for stage_out's sequence word (every kernel before it has finished: the scalars and
+// results it wrote are visible). The stream is queried now and then, so that a fault or a hang
+// surfaces as the runtime reports it.
+int spin_wait(tbg_ctx* ctx, unsigned int seq) {
+    for (uint64_t spins = 1;; spins++) {
+        if (__atomic_load_n(ctx->h_seq, __ATOMIC_ACQUIRE) == seq) return 0;
+        if ((spins & 4095) == 0) {
+            const hipError_t q = hipStreamQuery(ctx->stream);
+            if (q == hipSuccess) {
+                if (__atomic_load_n(ctx->h_seq, __ATOMIC_ACQUIRE) == seq) return 0;
+                return hip_ok(ctx, hipStreamSynchronize(ctx->stream), "sync") ? 0 : TBG_EHIP;
+            }
+            if (q != hipErrorNotReady) return hip_ok(ctx, q, "sync") ? 0 : TBG_EHIP;
+        }
+        __builtin_ia32_pause();
+    }
+}
+
 int stage_call_outputs(tbg_ctx* ctx, const tb_create_result_t* d_results, tb_create_result_t* dst,
-                       uint32_t n, bool scalars, const AeSnapJob* snap, bool fixes) {
+                       uint32_t n, bool scalars, const AeSnapJob* snap, bool fixes,
+                       unsigned int seq) {
     StageOut s{reinterpret_cast<const uint4*>(d_results), reinterpret_cast<uint4*>(dst), n,
                scalars ? reinterpret_cast<const unsigned long long*>(ctx->d_scalars) : nullptr,
                reinterpret_cast<unsigned long long*>(ctx->dh_scalars),
                uint32_t(sizeof(DevScalars) / 8), fixes ? ctx->fix_slots : nullptr,
-               ctx->T.tr.slots, ctx->d_scalars};
+               ctx->T.tr.slots, ctx->d_scalars, seq ? ctx->d_stage_done : nullptr,
+               seq ? ctx->dh_seq : nullptr, seq};
     if (!dst || !n) s.src = nullptr;
     AeSnapJob J{};
     if (snap) J = *snap;
@@ -1418,6 +1445,12 @@ tbg_ctx* tbg_open(const tbg_options* options) {
     }
     ok = ok && hip_ok(ctx, hipHostMalloc(reinterpret_cast<void**>(&ctx->h_scalars),
                                          sizeof(DevScalars)), "hipHostMalloc");
+    ok = ok && hip_ok(ctx, hipHostMalloc(reinterpret_cast<void**>(&ctx->h_seq), 64), "hipHostMalloc") &&
+         hip_ok(ctx, hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->dh_seq), ctx->h_seq, 0),
+                "hipHostGetDevicePointer") &&
+         dev_alloc(ctx, &ctx->d_stage_done, 1, true);
+    if (ok) *ctx->h_seq = 0;
+    ctx->spin_sync = getenv("TBG_NO_SPIN_SYNC") == nullptr;
     ok = ok && hip_ok(ctx, hipEventCreateWithFlags(&ctx->results_ready, hipEventDisableTiming),
                       "hipEventCreate");
     ok = ok && hip_ok(ctx, hipHostMalloc(reinterpret_cast<void**>(&ctx->h_batch_ends),
@@ -1487,7 +1520,7 @@ void tbg_close(tbg_ctx* ctx) {
                     ctx->T.tr_status, ctx->T.expiry, ctx->d_scalars, ctx->T.undo, ctx->d_events,
                     ctx->d_results, ctx->d_batch_ends, ctx->d_batch_ts, ctx->ev_slot, ctx->ev_dr,
                     ctx->ev_cr, ctx->ev_amount, ctx->ev_info, ctx->ev_slow, ctx->slow_list,
-                    ctx->fix_slots,
+                    ctx->fix_slots, ctx->d_stage_done,
                     ctx->pnt_call, ctx->pnt_fired, ctx->pv_slots,
                     ctx->bal_items, ctx->chunk_info, ctx->bal_items_sorted, ctx->bucket_words, ctx->bucket_partials,
                     ctx->window_partials, ctx->window_carry,
@@ -1507,6 +1540,7 @@ void tbg_close(tbg_ctx* ctx) {
     for (hipEvent_t e : ctx->marks)
         if (e) (void)hipEventDestroy(e);
     if (ctx->h_scalars) (void)hipHostFree(ctx->h_scalars);
+    if (ctx->h_seq) (void)hipHostFree(ctx->h_seq);
     if (ctx->h_results) (void)hipHostFree(ctx->h_results);
     if (ctx->h_batch_ends) (void)hipHostFree(ctx->h_batch_ends);
     if (ctx->h_batch_ts) (void)hipHostFree(ctx->h_batch_ts);
@@ -1689,12 +1723,16 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
         // (a small call's AccountEvents snapshot rides along: final unless a replay follows)
         AeSnapJob J;
         const bool snap = ae_async_ok(ctx, n) && !(rc = ae_snap_job(ctx, c, &J));
+        const bool spin = ctx->spin_sync && !ctx->timing;
+        const unsigned int seq = spin ? (++ctx->seq ? ctx->seq : ++ctx->seq) : 0u;
         if (!rc)
-            rc = stage_call_outputs(ctx, d_results, dst, dst ? n : 0, true, snap ? &J : nullptr, true);
+            rc = stage_call_outputs(ctx, d_results, dst, dst ? n : 0, true, snap ? &J : nullptr, true,
+                                    seq);
         // (its graph queued now: the host's launch calls overlap the call's kernels)
         if (!rc && snap) rc = ae_launch_graph(ctx);
         ctx->ae_snap_early = snap && !rc;
-        if (!rc) rc = hip_ok(ctx, hipStreamSynchronize(ctx->stream), "sync") ? 0 : TBG_EHIP;
+        if (!rc) rc = spin ? spin_wait(ctx, seq)
+                           : (hip_ok(ctx, hipStreamSynchronize(ctx->stream), "sync") ? 0 : TBG_EHIP);
         tmark(ctx, "host_sync");
     }
     const bool replay = !rc && ctx->h_scalars->stats[0] > 0;

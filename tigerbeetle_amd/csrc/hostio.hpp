@@ -63,6 +63,11 @@ struct StageOut {
     const uint32_t* fix_slots;
     unsigned long long* id_slots;
     const DevScalars* scalars;
+    // The call's end for a spinning host (null: none): the last workgroup to finish writes `seq`
+    // into the pinned word after every workgroup's writes (system-scope fences).
+    unsigned int* done;
+    unsigned int* host_seq;
+    unsigned int seq;
 };
 
 // (+ a small call's AccountEvents staging, events.hpp, when J.on: the call's state is final here
@@ -90,6 +95,17 @@ __global__ void __launch_bounds__(kStageThreads) stage_out(StageOut s, AeSnapJob
             s.scalars_dst[w] = s.scalars_src[w];
     if (s.src)
         for (uint32_t i = tid; i < s.n; i += gridDim.x * kStageThreads) s.dst[i] = s.src[i];
+    if (s.host_seq) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __threadfence_system();
+            if (atomicAdd(s.done, 1u) == gridDim.x - 1) {
+                atomicExch(s.done, 0u);
+                __threadfence_system();
+                __hip_atomic_store(s.host_seq, s.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+    }
 }
 
 }  // namespace tbg
