@@ -11,11 +11,14 @@ export TMPDIR=/tmp
 cd /tmp
 args="--no-cpu-baseline --no-validate --commit-reps 0 --steps 2 --warmup 1 $*"
 i=0
-for ctrs in "FETCH_SIZE" "WRITE_SIZE" \
+# PMC_TRAFFIC_ONLY=1: the two HBM traffic passes only (what roofline.traffic reads).
+passes=("FETCH_SIZE" "WRITE_SIZE" \
             "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" \
             "TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE GRBM_COUNT" \
             "TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAIT_INST_LDS" \
-            "TCP_TCC_READ_REQ_sum TCP_TCC_WRITE_REQ_sum TCP_TCC_ATOMIC_WITH_RET_REQ_sum TCC_ATOMIC_sum"; do
+            "TCP_TCC_READ_REQ_sum TCP_TCC_WRITE_REQ_sum TCP_TCC_ATOMIC_WITH_RET_REQ_sum TCC_ATOMIC_sum")
+[ -n "$PMC_TRAFFIC_ONLY" ] && passes=("FETCH_SIZE" "WRITE_SIZE")
+for ctrs in "${passes[@]}"; do
     i=$((i+1))
     timeout -s KILL 120 rocprofv3 --pmc $ctrs --output-format csv -d $out/p$i -o run -- \
         python3 $R/bench.py $args > $out/p$i.log 2>&1 || { echo "pass $i ($ctrs) failed"; tail -5 $out/p$i.log; exit 1; }
