@@ -616,14 +616,69 @@ __device__ inline Bal5 bal5_block_exclusive(const Bal5& x, Bal5* total, Bal5Lds&
     return r;
 }
 
-// Listed accounts, one workgroup each: the touches in event order into vals_sorted.
+// A segment of at most kWaveSortMax values sorted by one wave: an LDS bitonic sort of the next
+// power of two (kNone32 padding) with wave-level barriers only. All lanes of the wave call it.
+constexpr uint32_t kWaveSortMax = 2048;
+__device__ inline void wave_bitonic_sort(const uint32_t* in, uint32_t* out, uint32_t off, uint32_t c,
+                                         uint32_t* buf) {
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t pw = 64;
+    while (pw < c) pw <<= 1;
+    for (uint32_t i = lane; i < pw; i += 64) buf[i] = i < c ? in[off + i] : kNone32;
+    wave_lds_sync();
+    // (each stage's reads all issue before any compare: one LDS round trip per stage)
+    constexpr uint32_t kPer = kWaveSortMax / 128;
+    const uint32_t pairs = pw / 2;
+    for (uint32_t size = 2; size <= pw; size <<= 1) {
+        for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+            uint32_t xs[kPer], ys[kPer];
+#pragma unroll
+            for (uint32_t j = 0; j < kPer; j++) {
+                const uint32_t t = lane + 64 * j;
+                const uint32_t a = 2 * t - (t & (stride - 1)), b = a + stride;
+                if (t < pairs) {
+                    xs[j] = buf[a];
+                    ys[j] = buf[b];
+                }
+            }
+#pragma unroll
+            for (uint32_t j = 0; j < kPer; j++) {
+                const uint32_t t = lane + 64 * j;
+                const uint32_t a = 2 * t - (t & (stride - 1)), b = a + stride;
+                if (t < pairs && (xs[j] > ys[j]) == ((a & size) == 0)) {
+                    buf[a] = ys[j];
+                    buf[b] = xs[j];
+                }
+            }
+            wave_lds_sync();
+        }
+    }
+    for (uint32_t i = lane; i < c; i += 64) out[off + i] = buf[i];
+    wave_lds_sync();  // (buf is reused by the wave's next segment)
+}
+
+// Listed accounts: the touches in event order into vals_sorted -- an account of at most
+// kWaveSortMax touches by one wave (the workgroup's eight waves sort eight of them at once), a
+// larger one by the whole workgroup (segment_sort). (One workgroup per account sorted config 2's
+// 10k accounts of ~2,000 touches forty at a time per CU: 2.4 ms per 10M-event step.)
 __global__ void __launch_bounds__(kGroupBigThreads) ae_group_sort(AeScratch S) {
     __shared__ SegmentLds L;
+    static_assert(kGroupBigThreads / 64 * kWaveSortMax <= kGroupLdsWords, "wave sort slices");
     const GroupPlan& G = S.G;
     const uint32_t nbig = G.counts[1];
+    const uint32_t wave = threadIdx.x >> 6, waves = kGroupBigThreads / 64;
+    // (only when there are many more accounts than workgroups: with a few hundred, one workgroup
+    // each finishes sooner -- the large ones would wait behind the waves' share)
+    const bool by_waves = nbig > 4 * gridDim.x;
+    uint32_t* slice = L.buf + wave * kWaveSortMax;
+    for (uint32_t b = blockIdx.x * waves + wave; by_waves && b < nbig; b += gridDim.x * waves) {
+        const uint4 e = G.big[b];
+        if (e.y <= kWaveSortMax) wave_bitonic_sort(G.vals, G.vals_sorted, e.x, e.y, slice);
+    }
+    __syncthreads();
     for (uint32_t b = blockIdx.x; b < nbig; b += gridDim.x) {
         const uint4 e = G.big[b];
-        segment_sort(G.vals, G.vals_sorted, e.x, e.y, L);
+        if (!by_waves || e.y > kWaveSortMax) segment_sort(G.vals, G.vals_sorted, e.x, e.y, L);
     }
 }
 
