@@ -118,6 +118,35 @@ def test_uniform_config2_small():
         r = p.create_transfers(t, lens)
         assert (r["status"] == 0xFFFFFFFF).all()
         assert p.stats["replayed"] == 0
+        assert p.stats["ae_window"] == 1  # (the one-pass AccountEvents)
+        p.compare_state()
+    finally:
+        p.close()
+
+
+@pytest.mark.parametrize("spin", [True, False], ids=["spin", "stream-sync"])
+def test_many_small_registered_calls(spin, monkeypatch):
+    """The host's end-of-call wait: stage_out's last workgroup publishes a sequence word after every
+    workgroup's results and scalar words (each thread releases its stores at system scope). 300
+    small calls from a registered pool, each reply compared with the oracle as soon as the call
+    returns (Pair checks every result); TBG_NO_SPIN_SYNC (a stream synchronisation) is the
+    control."""
+    if not spin:
+        monkeypatch.setenv("TBG_NO_SPIN_SYNC", "1")
+    rng = np.random.default_rng(31)
+    p = Pair(account_capacity=1 << 12, transfer_capacity=1 << 20, batch_events_max=8189,
+             registered=True)
+    try:
+        n_acc = 500
+        p.create_accounts(workload.accounts(n_acc, seed=4))
+        off = 0
+        for call in range(300):
+            n = int(rng.integers(1, 3000)) if call % 10 else 8189
+            t = workload.transfers_uniform(n, n_acc, seed=call, id_offset=off)
+            off += n
+            bad = rng.random(n) < 0.05
+            t["id"][bad] = 0
+            p.create_transfers(t, _split(n, rng, 8189))
         p.compare_state()
     finally:
         p.close()
@@ -265,6 +294,70 @@ def test_balance_window_edges(n_acc):
             r = p.create_transfers(t, _split(n, rng, 8189))
             assert (r["status"] == 0xFFFFFFFF).mean() > 0.9
         p.compare_state()
+    finally:
+        p.close()
+
+
+@pytest.mark.parametrize("case", ["window", "no-window", "skew", "wide-rows"])
+def test_account_events_window(case, monkeypatch):
+    """AccountEvents of balance-window calls in one pass (events.hpp ae_window_emit): calls of
+    >= 65,536 events over <= 12,288 accounts whose created events are plain single-phase, with
+    statically failed events between them (ids 0, same accounts, existing ids of an earlier call:
+    no record), interleaved with small calls (side-stream appends) and a pulse, compared with the
+    oracle's log byte for byte and through get_change_events. `skew`: 90 % of the touches on 8
+    accounts (long per-round lists); `no-window`: TBG_NO_AE_WINDOW (the general appends);
+    `wide-rows`: 13,000 accounts (above the window emit's LDS) take the general appends; calls with
+    pending transfers or wide amounts fall back in every case."""
+    if case == "no-window":
+        monkeypatch.setenv("TBG_NO_AE_WINDOW", "1")
+    rng = np.random.default_rng(77)
+    n_acc = 13_000 if case == "wide-rows" else 10_000
+    p = Pair(account_capacity=1 << 14, transfer_capacity=1 << 20, batch_events_max=1 << 17,
+             pulse_batch_max=64, pulse_next_timestamp_init=TIMESTAMP_MAX)
+    try:
+        acc = workload.accounts(n_acc, seed=3)
+        p.create_accounts(acc, _split(n_acc, rng, 8189))
+        off = 0
+        windows = 0
+        for call in range(4):
+            n = 70_000 + 10_000 * call
+            t = workload.transfers_uniform(n, n_acc, seed=100 + call, id_offset=off)
+            off += n
+            if case == "skew":
+                hot = rng.random(n) < 0.9
+                t["debit_account_id"][hot, 0] = rng.integers(1, 5, size=int(hot.sum()))
+                hot = rng.random(n) < 0.9
+                t["credit_account_id"][hot, 0] = rng.integers(5, 9, size=int(hot.sum()))
+            fail = rng.random(n)
+            t["id"][fail < 0.01] = 0                                    # id_must_not_be_zero
+            same = (fail >= 0.01) & (fail < 0.02)
+            t["credit_account_id"][same] = t["debit_account_id"][same]  # accounts_must_be_different
+            if call:
+                old = (fail >= 0.02) & (fail < 0.03)                    # exists / exists_with_*
+                t["id"][old, 0] = rng.integers(1, off - n, size=int(old.sum()))
+            if call == 2:
+                pend = fail >= 0.995                                    # pending: general appends
+                t["flags"][pend] |= 2
+            w0 = p.stats["ae_window"]
+            r = p.create_transfers(t, _split(n, rng, 8189))
+            assert (r["status"] == 0xFFFFFFFF).mean() > 0.9
+            took = p.stats["ae_window"] > w0
+            if case in ("no-window", "wide-rows") or call == 2:
+                assert not took
+            mid_ts = int(r["timestamp"][n // 2])
+            windows += took
+            # small calls (side stream) and a pulse between the window calls
+            s = workload.transfers_uniform(3_000, n_acc, seed=200 + call, id_offset=off)
+            off += 3_000
+            s["flags"][rng.random(3_000) < 0.2] |= 2
+            s["timeout"][s["flags"] & 2 != 0] = 1
+            p.create_transfers(s, _split(3_000, rng, 1000))
+            p.tick(2 * NS_PER_S)
+        p.compare_state()
+        assert len(p.change_events()) > 0
+        assert len(p.change_events(timestamp_min=mid_ts)) > 0  # (inside the last window call)
+        if case in ("window", "skew"):
+            assert windows >= 2  # (calls with in-call duplicates of failed ids replay)
     finally:
         p.close()
 

@@ -849,6 +849,246 @@ __global__ void __launch_bounds__(kGroupBigThreads) ae_group_big_serial(AeScratc
     }
 }
 
+// ---- AccountEvents of balance-window calls in one pass ------------------------------------------
+//
+// A create_transfers call on the balance window path (kernels.hpp: pair items, <= 2^14 accounts)
+// whose created events are all plain single-phase FAST events -- no replay, no linked chain,
+// post/void or imported event, no pending transfer, every amount packed in its item (no
+// kFlagChain / kFlagPostVoid / kFlagImported / kFlagAeSlow) and every window sum below 2^32 (no
+// kFlagWideSums) -- changes nothing of an account but its posted balances, each created event by
+// its item's amount. The AccountEvent of created event e (account_event :4384-4465) then carries,
+// for each of its accounts A,
+//     A's posted balances after e = A's final posted balances - A's deltas of the events after e
+// and A's final row for everything else (pending balances, `closed`, timestamp, id). The later
+// deltas come from the window's per-workgroup partial sums: ae_window_suffix turns them into
+// suffix sums over the slices (partials[w][key] = the key's deltas in slices w, w + 1, ...), and
+// ae_window_emit walks slice w (bal_window_accumulate's) in rounds of 1024 events with the slice's
+// suffix sums in LDS, one u32 per account and side (R). Within a round the later deltas of event
+// e on account A are R[A] minus A's deltas of the round's events up to and including e: every
+// touch pushes itself on its account's LDS list (an exchange of the list head; a node is an event
+// and a side) and e walks both of its accounts' lists, summing the nodes of events <= e (config 2
+// puts ~0.2 touches on an account per round: the lists are short). After the round R drops by the
+// round's deltas. Each record is written once, as 16 non-temporal 16-byte stores; no grouping,
+// sorting or returning global atomics. The records' positions: the slices' created counts (from
+// bal_window_accumulate) and a ballot scan per round. The final account rows are L2-resident at
+// these key spaces; an event's timestamp is its result's.
+constexpr uint32_t kAeWinThreads = 1024;
+constexpr uint32_t kAeWinRowsMax = 12288;  // 12 B of LDS per account (R debit, R credit, list head)
+constexpr uint32_t kAeWinNil = 0xFFFFFFFFu;
+
+struct AeWindow {
+    const uint64_t* items;               // the call's pair items (~0: none)
+    const tb_create_result_t* results;
+    const tb_account_t* acc_rows;
+    uint32_t n, ps, rows, nwg, wkeys;
+    uint64_t row_base;
+    uint32_t* suffix;                    // the window partials, [workgroup][key]: suffix sums
+    const unsigned int* slice_count;     // per workgroup: its slice's created events
+    unsigned long long* slice_ts;        // per workgroup: its first and last created timestamp
+    unsigned int* done;                  // finished workgroups (the last one closes the block)
+    tb_account_event_t* log;
+    AeRef* refs;
+    unsigned long long* state;           // the log on device: [0] length, [1] last ts, [2] unsorted
+};
+
+// One lane per (account, side) key in use: partials[w][key] = sum over w' >= w (in place).
+__global__ void ae_window_suffix(AeWindow W) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= 2 * W.rows) return;
+    const uint32_t key = t < W.rows ? t : ((1u << W.ps) | (t - W.rows));
+    uint32_t* p = W.suffix + key;
+    const uint64_t stride = W.wkeys;
+    uint32_t s = 0;
+    int64_t w = int64_t(W.nwg) - 1;
+    for (; w >= 7; w -= 8) {  // (eight loads in flight)
+        uint32_t v[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) v[j] = p[uint64_t(w - j) * stride];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            s += v[j];
+            p[uint64_t(w - j) * stride] = s;
+        }
+    }
+    for (; w >= 0; w--) {
+        s += p[uint64_t(w) * stride];
+        p[uint64_t(w) * stride] = s;
+    }
+}
+
+__device__ inline void ae_nt_store(uint4* p, uint4 v) {
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    const v4u x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, reinterpret_cast<v4u*>(p));
+}
+__device__ inline uint4 ae_sub_u32(uint4 balance, uint32_t d) {
+    return ae_q(ae_u(balance) - u128(d));
+}
+
+__global__ void __launch_bounds__(kAeWinThreads) ae_window_emit(AeWindow W) {
+    __shared__ uint32_t Rd[kAeWinRowsMax];    // debits_posted deltas of the events from the round on
+    __shared__ uint32_t Rc[kAeWinRowsMax];    // credits_posted
+    __shared__ uint32_t head[kAeWinRowsMax];  // the round's touch lists (node 2e + side)
+    __shared__ uint16_t next[2 * kAeWinThreads];
+    __shared__ uint32_t amt[kAeWinThreads];
+    __shared__ uint32_t wave_cnt[kAeWinThreads / 64];
+    __shared__ unsigned long long ts_lds[2];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, w = blockIdx.x;
+    const uint32_t per = window_slice_per(W.n, W.nwg);
+    const uint32_t b0 = w * per;
+    const uint32_t b1 = b0 + per < W.n ? b0 + per : W.n;
+    // created events of the earlier slices
+    uint32_t before = 0;
+    for (uint32_t j = tid; j < w; j += kAeWinThreads) before += W.slice_count[j];
+    for (int off = 32; off > 0; off >>= 1) before += __shfl_xor(before, off);
+    if (lane == 0) wave_cnt[wv] = before;
+    const uint32_t* suf = W.suffix + uint64_t(w) * W.wkeys;
+    for (uint32_t a = tid; a < W.rows; a += kAeWinThreads) {
+        Rd[a] = suf[a];
+        Rc[a] = suf[(1u << W.ps) + a];
+        head[a] = kAeWinNil;
+    }
+    if (tid == 0) {
+        ts_lds[0] = ~0ull;
+        ts_lds[1] = 0;
+    }
+    const uint64_t used = W.state[0];
+    __syncthreads();
+    uint64_t pos = used;
+    for (uint32_t j = 0; j < kAeWinThreads / 64; j++) pos += wave_cnt[j];
+    __syncthreads();
+    const uint32_t ps = W.ps;
+    const uint64_t rmask = (1ull << ps) - 1;
+    uint64_t ts_min = ~0ull, ts_max = 0;
+    for (uint32_t r0 = b0; r0 < b1; r0 += kAeWinThreads) {
+        const uint32_t e = r0 + tid;
+        const uint64_t x = e < b1 ? W.items[e] : ~0ull;
+        const bool valid = x != ~0ull;
+        uint32_t dr = 0, cr = 0, a = 0;
+        uint4 D[6], C[6];
+        uint64_t ts = 0;
+        if (valid) {
+            dr = uint32_t(x & rmask);
+            cr = uint32_t((x >> ps) & rmask);
+            a = uint32_t(x >> (2 * ps + 1));  // (< 2^32: no kFlagWideSums)
+            // the record's loads first: the rows' id and balances (words 0-4) and their ledger,
+            // flags and timestamp (word 7), the event's timestamp
+            const uint4* pd = reinterpret_cast<const uint4*>(&W.acc_rows[dr]);
+            const uint4* pc = reinterpret_cast<const uint4*>(&W.acc_rows[cr]);
+#pragma unroll
+            for (int j = 0; j < 5; j++) {
+                D[j] = pd[j];
+                C[j] = pc[j];
+            }
+            D[5] = pd[7];
+            C[5] = pc[7];
+            ts = W.results[e].timestamp;
+            next[2 * tid] = uint16_t(atomicExch(&head[dr], 2 * tid));
+            next[2 * tid + 1] = uint16_t(atomicExch(&head[cr], 2 * tid + 1));
+            amt[tid] = a;
+        }
+        const uint64_t bal = __ballot(valid);
+        const uint32_t rank = lane ? __popcll(bal & (~0ull >> (64 - lane))) : 0;
+        if (lane == 0) wave_cnt[wv] = uint32_t(__popcll(bal));
+        __syncthreads();
+        uint64_t my = pos + rank;
+        uint32_t round_total = 0;
+        for (uint32_t j = 0; j < kAeWinThreads / 64; j++) {
+            const uint32_t cj = wave_cnt[j];
+            my += j < wv ? cj : 0;
+            round_total += cj;
+        }
+        // later deltas: [0] the debit account's debits_posted, [1] its credits_posted, [2] / [3]
+        // the credit account's
+        uint32_t later[4] = {0, 0, 0, 0};
+        if (valid) {
+#pragma unroll
+            for (int side = 0; side < 2; side++) {
+                const uint32_t acc = side ? cr : dr;
+                uint32_t sd = 0, sc = 0;
+                for (uint32_t nd = head[acc]; nd != kAeWinNil;) {
+                    if ((nd >> 1) <= tid) {
+                        const uint32_t v = amt[nd >> 1];
+                        if (nd & 1) sc += v;
+                        else sd += v;
+                    }
+                    const uint32_t nx = next[nd];
+                    nd = nx == 0xFFFFu ? kAeWinNil : nx;
+                }
+                later[2 * side] = Rd[acc] - sd;
+                later[2 * side + 1] = Rc[acc] - sc;
+            }
+        }
+        __syncthreads();  // (every list walked and R read before the round's updates)
+        if (valid) {
+            head[dr] = kAeWinNil;
+            head[cr] = kAeWinNil;
+            atomicSub(&Rd[dr], a);
+            atomicSub(&Rc[cr], a);
+            ts_min = ts < ts_min ? ts : ts_min;
+            ts_max = ts > ts_max ? ts : ts_max;
+            // row word 7: ledger, code | flags << 16, timestamp
+            uint4* out = reinterpret_cast<uint4*>(&W.log[my]);
+            ae_nt_store(out + 0, D[0]);
+            ae_nt_store(out + 1, D[1]);
+            ae_nt_store(out + 2, ae_sub_u32(D[2], later[0]));
+            ae_nt_store(out + 3, D[3]);
+            ae_nt_store(out + 4, ae_sub_u32(D[4], later[1]));
+            ae_nt_store(out + 5, C[0]);
+            ae_nt_store(out + 6, C[1]);
+            ae_nt_store(out + 7, ae_sub_u32(C[2], later[2]));
+            ae_nt_store(out + 8, C[3]);
+            ae_nt_store(out + 9, ae_sub_u32(C[4], later[3]));
+            ae_nt_store(out + 10, make_uint4(uint32_t(ts), uint32_t(ts >> 32), D[5].z, D[5].w));
+            ae_nt_store(out + 11, make_uint4(C[5].z, C[5].w, (D[5].y >> 16) | (C[5].y & 0xFFFF0000u), 0u));
+            ae_nt_store(out + 12, make_uint4(0, 0, 0, 0));
+            ae_nt_store(out + 13, make_uint4(a, 0, 0, 0));
+            ae_nt_store(out + 14, make_uint4(a, 0, 0, 0));
+            ae_nt_store(out + 15, make_uint4(D[5].x, uint32_t(TB_PENDING_NONE), 0, 0));
+            ae_nt_store(reinterpret_cast<uint4*>(&W.refs[my]),
+                        make_uint4(uint32_t(W.row_base + e), dr, cr, 0));
+        }
+        pos += round_total;
+        __syncthreads();  // (the lists are empty and R is current for the next round)
+    }
+    // The slice's first and last created timestamps; the last workgroup closes the block.
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t a = __shfl_xor(ts_min, off), b = __shfl_xor(ts_max, off);
+        ts_min = a < ts_min ? a : ts_min;
+        ts_max = b > ts_max ? b : ts_max;
+    }
+    if (lane == 0) {
+        atomicMin(&ts_lds[0], ts_min);
+        atomicMax(&ts_lds[1], ts_max);
+    }
+    __syncthreads();
+    if (tid != 0) return;
+    W.slice_ts[2 * w] = ts_lds[0];
+    W.slice_ts[2 * w + 1] = ts_lds[1];
+    __threadfence();
+    if (atomicAdd(W.done, 1u) != gridDim.x - 1) return;
+    __threadfence();
+    uint64_t total = 0, first = 0, last = 0;
+    bool any = false;
+    const volatile unsigned int* counts = W.slice_count;  // (other workgroups' words: no cached copy)
+    const volatile unsigned long long* sts = W.slice_ts;
+    for (uint32_t j = 0; j < gridDim.x; j++) {
+        const uint32_t cj = counts[j];
+        if (!cj) continue;
+        const uint64_t f = sts[2 * j], l = sts[2 * j + 1];
+        if (!any) first = f;
+        any = true;
+        last = l;
+        total += cj;
+    }
+    if (total) {
+        if (used && first <= W.state[1]) W.state[2] = 1;
+        if (last > W.state[1]) W.state[1] = last;
+        W.state[0] = used + total;
+    }
+    *W.done = 0;
+}
+
 // ---- get_change_events ---------------------------------------------------------------------
 
 // The first log position with timestamp >= lo, and the first with timestamp > hi.

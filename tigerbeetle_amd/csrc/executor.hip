@@ -14,7 +14,9 @@
 #include <chrono>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -43,6 +45,9 @@ constexpr uint32_t kSortThreshold = 1u << 16;
 // Balance items use u128 atomics instead of the sort when the key space has more than this many
 // account fields per item.
 constexpr uint64_t kAtomicKeysPerItem = 8;
+// The pinned blocks kernels write for the spinning host (scalars, results, the sequence word):
+// coherent, so that their write-back does not depend on the memory type.
+constexpr unsigned int kCoherentHost = hipHostMallocMapped | hipHostMallocCoherent;
 // Calls up to this many events find their chunks' batch bounds inside tr_ingest.
 constexpr uint32_t kInlineChunkMax = 1u << 16;
 constexpr size_t kFlowDebugBytes = 8 * (16 + 8 * 1000);  // TBG_FLOW_DEBUG counters (+ per owner)
@@ -113,6 +118,7 @@ struct tbg_ctx {
     unsigned int* d_stage_done = nullptr;  // stage_out's finished workgroups
     unsigned int seq = 0;
     bool spin_sync = false;
+    double call_timeout_ms = 60000;  // spin_wait's bound (TBG_CALL_TIMEOUT_MS)
     tb_create_result_t* dh_results = nullptr;
     uint32_t* dh_batch_ends = nullptr;
     uint64_t* dh_batch_ts = nullptr;
@@ -171,6 +177,12 @@ struct tbg_ctx {
     uint64_t bucket_slices_max = 0;
     uint32_t* window_partials = nullptr;   // balance window: per workgroup, kWindowKeys u32 sums
     unsigned long long* window_carry = nullptr;  // per window key (zero between calls)
+    unsigned int* window_counts = nullptr;  // per workgroup: its slice's items; [kWindowGridMax] done
+    unsigned long long* window_ts = nullptr;  // per workgroup: first / last created timestamp
+    // The last create_transfers call's balance window (its AccountEvents may take ae_window_emit).
+    struct WindowCall {
+        uint32_t epoch = 0, nwg = 0, ps = 0, wkeys = 0;
+    } win;
     // account index build (cuckoo insertion + repair)
     uint32_t* idx_dirty = nullptr;
     unsigned int* idx_counters = nullptr;
@@ -218,6 +230,7 @@ struct tbg_ctx {
     uint32_t ae_parity = 0;
     bool ae_async_pending = false;
     bool ae_async = true;  // tbg_debug_ae_sync(ctx, 1) / TBG_AE_SYNC=1: every append on the call's stream
+    bool ae_window_on = true;  // TBG_NO_AE_WINDOW=1: window calls take the general appends
     bool ae_async_ready = false;
     AeScratch ae_g{};
     // The call's stage_out took its staging and the side stream's appends were queued behind it,
@@ -473,6 +486,7 @@ int end_call(tbg_ctx* ctx, uint32_t n, bool already_synced = false) {
     tcollect(ctx);
     const DevScalars& s = *ctx->h_scalars;
     ctx->stats.events = n;
+    ctx->stats.ae_window = 0;
     ctx->stats.fast = s.stats[1];
     ctx->stats.replayed = s.stats[2];
     ctx->stats.static_fail = s.stats[3];
@@ -1131,9 +1145,13 @@ int ae_snap_job(tbg_ctx* ctx, const Call<tb_transfer_t>& c, AeSnapJob* J) {
     return 0;
 }
 
-// The side stream appends staging buffer p once the call's stream reaches this point.
-int ae_launch_graph(tbg_ctx* ctx) {
+// The side stream appends staging buffer p (at most n AccountEvents) once the call's stream
+// reaches this point. The log's bound grows as the graph is queued: a call that fails later still
+// leaves a graph that may append.
+int ae_launch_graph(tbg_ctx* ctx, uint32_t n) {
     const uint32_t p = ctx->ae_parity;
+    ctx->ae_bound += n;
+    ctx->ae_pending = true;
     HIP_TRY(ctx, hipEventRecord(ctx->ae_snap_ready[p], ctx->stream));
     HIP_TRY(ctx, hipStreamWaitEvent(ctx->ae_stream, ctx->ae_snap_ready[p], 0));
     if (int rc = ae_launch_appends(ctx, p)) return rc;
@@ -1153,9 +1171,52 @@ int ae_transfers_async(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
         if (int rc = ae_snap_job(ctx, c, &J)) return rc;
         hipLaunchKernelGGL(ae_snapshot, dim3(kAeAsyncMax / kBlock), dim3(kBlock), 0, ctx->stream, J);
         HIP_TRY(ctx, hipGetLastError());
-        if (int rc = ae_launch_graph(ctx)) return rc;
+        if (int rc = ae_launch_graph(ctx, c.n)) return rc;
     }
     ctx->ae_snap_early = false;
+    return 0;
+}
+
+// AccountEvents of a balance-window call in one pass (events.hpp, ae_window_emit), when the call
+// qualifies: its window partials are still current (nothing ran since), no replay ran, and no
+// flag says an event or a sum is outside what the window emit tracks. Returns 1 when not taken.
+int ae_window(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
+    const DevScalars& h = *ctx->h_scalars;
+    constexpr unsigned int kNot = kFlagChain | kFlagPostVoid | kFlagImported | kFlagAeSlow |
+                                  kFlagWideSums;
+    if (ctx->win.epoch != c.epoch || ctx->epoch != c.epoch || (h.flags & kNot) || h.stats[0] ||
+        ctx->T.acc_rows_used > kAeWinRowsMax || !ctx->ae_window_on)
+        return 1;
+    if (int rc = ae_join(ctx)) return rc;
+    if (ctx->ae_bound + c.n > ctx->ae_cap) {
+        if (int rc = ae_settle(ctx)) return rc;
+        if (ctx->ae_used + c.n > ctx->ae_cap) return 1;  // (the general path counts exactly)
+    }
+    AeWindow W{};
+    W.items = ctx->bal_items;
+    W.results = c.results;
+    W.acc_rows = ctx->T.acc_rows;
+    W.n = c.n;
+    W.ps = ctx->win.ps;
+    W.rows = uint32_t(ctx->T.acc_rows_used);
+    W.nwg = ctx->win.nwg;
+    W.wkeys = ctx->win.wkeys;
+    W.row_base = c.row_base;
+    W.suffix = ctx->window_partials;
+    W.slice_count = ctx->window_counts;
+    W.slice_ts = ctx->window_ts;
+    W.done = ctx->window_counts + kWindowGridMax;
+    W.log = ctx->ae_log;
+    W.refs = ctx->ae_ref;
+    W.state = ctx->ae_words + 4;
+    tmark(ctx, "-account_events");
+    hipLaunchKernelGGL(ae_window_suffix, dim3((2 * W.rows + kBlock - 1) / kBlock), dim3(kBlock), 0,
+                       ctx->stream, W);
+    hipLaunchKernelGGL(ae_window_emit, dim3(W.nwg), dim3(kAeWinThreads), 0, ctx->stream, W);
+    tmark(ctx, "account_events");
+    HIP_TRY(ctx, hipGetLastError());
+    ctx->win.epoch = 0;  // (the partials are suffix sums now)
+    ctx->stats.ae_window = 1;
     ctx->ae_bound += c.n;
     ctx->ae_pending = true;
     return 0;
@@ -1163,6 +1224,12 @@ int ae_transfers_async(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
 
 // AccountEvents of a create_transfers call: its created events in call order.
 int ae_transfers(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
+    if (ctx->ae_snap_early) {  // (stage_out took the snapshot and its graph is queued)
+        ctx->ae_snap_early = false;
+        return 0;
+    }
+    const int wrc = ae_window(ctx, c);
+    if (wrc <= 0) return wrc;
     if (ae_async_ok(ctx, c.n)) return ae_transfers_async(ctx, c);
     ctx->ae_snap_early = false;
     unsigned int* d_count = reinterpret_cast<unsigned int*>(ctx->ae_words);
@@ -1248,6 +1315,65 @@ bool is_registered(const tbg_ctx* ctx, const void* p, uint64_t bytes) {
     return mapped(ctx, p, bytes) != nullptr;
 }
 
+// Process-wide registrations of host ranges (tbg_register_host): one hipHostRegister per range
+// start, counted over the ctxs using it. A range that HIP reports as already registered by
+// someone else (not through this registry) is used but never unregistered here.
+struct HostPin {
+    uint64_t size;
+    uintptr_t dev;
+    uint32_t users;
+    bool owned;
+};
+std::mutex& host_pins_mu() {
+    static std::mutex m;
+    return m;
+}
+std::map<uintptr_t, HostPin>& host_pins() {
+    static std::map<uintptr_t, HostPin> m;
+    return m;
+}
+
+bool host_pin_acquire(tbg_ctx* ctx, void* ptr, uint64_t size, uintptr_t* dev_out) {
+    std::lock_guard<std::mutex> g(host_pins_mu());
+    auto& pins = host_pins();
+    const uintptr_t a = reinterpret_cast<uintptr_t>(ptr);
+    auto it = pins.find(a);
+    if (it != pins.end()) {
+        if (size > it->second.size) {
+            ctx->error = "tbg_register_host: range overlaps a smaller registration at the same start";
+            return false;
+        }
+        it->second.users++;
+        *dev_out = it->second.dev;
+        return true;
+    }
+    const hipError_t e = hipHostRegister(ptr, size, hipHostRegisterMapped);
+    const bool owned = e == hipSuccess;
+    if (!owned) {
+        (void)hipGetLastError();  // (clears the error for later calls)
+        if (e != hipErrorHostMemoryAlreadyRegistered) return hip_ok(ctx, e, "hipHostRegister");
+    }
+    void* dev = nullptr;
+    if (hipHostGetDevicePointer(&dev, ptr, 0) != hipSuccess || !dev) {
+        (void)hipGetLastError();
+        if (owned) (void)hipHostUnregister(ptr);
+        ctx->error = "hipHostGetDevicePointer";
+        return false;
+    }
+    pins[a] = HostPin{size, reinterpret_cast<uintptr_t>(dev), 1, owned};
+    *dev_out = reinterpret_cast<uintptr_t>(dev);
+    return true;
+}
+
+void host_pin_release(void* ptr) {
+    std::lock_guard<std::mutex> g(host_pins_mu());
+    auto& pins = host_pins();
+    auto it = pins.find(reinterpret_cast<uintptr_t>(ptr));
+    if (it == pins.end() || --it->second.users) return;
+    if (it->second.owned) (void)hipHostUnregister(ptr);
+    pins.erase(it);
+}
+
 // A host-buffer call's inputs into HBM: the batch ends / timestamps from the pinned staging and,
 // when the body lies in a registered range, the body itself -- one kernel on the call's stream
 // (hostio.hpp); an unregistered body takes hipMemcpyAsync.
@@ -1276,7 +1402,10 @@ int stage_call_inputs(tbg_ctx* ctx, const void* events, uint64_t bytes, uint32_t
 // Waits for stage_out's sequence word (every kernel before it has finished: the scalars and
 // results it wrote are visible). The stream is queried now and then, so that a fault or a hang
 // surfaces as the runtime reports it.
+// The wait is bounded (TBG_CALL_TIMEOUT_MS, default 60 s): a kernel that hangs instead of faulting
+// ends the call with TBG_EHIP and leaves the ctx failed (its tables are undefined).
 int spin_wait(tbg_ctx* ctx, unsigned int seq) {
+    const double deadline = now_ms() + ctx->call_timeout_ms;
     for (uint64_t spins = 1;; spins++) {
         if (__atomic_load_n(ctx->h_seq, __ATOMIC_ACQUIRE) == seq) return 0;
         if ((spins & 4095) == 0) {
@@ -1286,6 +1415,14 @@ int spin_wait(tbg_ctx* ctx, unsigned int seq) {
                 return hip_ok(ctx, hipStreamSynchronize(ctx->stream), "sync") ? 0 : TBG_EHIP;
             }
             if (q != hipErrorNotReady) return hip_ok(ctx, q, "sync") ? 0 : TBG_EHIP;
+            if (now_ms() > deadline) {
+                char buf[160];
+                snprintf(buf, sizeof(buf), "sync: the call did not finish within %.0f ms "
+                         "(a kernel hangs; the ctx is unusable)", ctx->call_timeout_ms);
+                ctx->error = buf;
+                ctx->failed = true;
+                return TBG_EHIP;
+            }
         }
         __builtin_ia32_pause();
     }
@@ -1431,7 +1568,9 @@ tbg_ctx* tbg_open(const tbg_options* options) {
              dev_alloc(ctx, &ctx->bucket_words, 4 * (kBucketsMax + 1), true) &&
              dev_alloc(ctx, &ctx->bucket_partials, ctx->bucket_slices_max * kBucketKeys, false) &&
              dev_alloc(ctx, &ctx->window_partials, uint64_t(kWindowGridMax) * kWindowKeys, false) &&
-             dev_alloc(ctx, &ctx->window_carry, kWindowKeys, true);
+             dev_alloc(ctx, &ctx->window_carry, kWindowKeys, true) &&
+             dev_alloc(ctx, &ctx->window_counts, kWindowGridMax + 1, true) &&
+             dev_alloc(ctx, &ctx->window_ts, 2 * kWindowGridMax, false);
     }
     ok = ok && dev_alloc(ctx, &ctx->acc_ts_index, acc_cap, false) &&
          dev_alloc(ctx, &ctx->tr_ts_index, tr_cap, false) &&
@@ -1444,13 +1583,14 @@ tbg_ctx* tbg_open(const tbg_options* options) {
              dev_alloc(ctx, &ctx->ae_words, 8, true);
     }
     ok = ok && hip_ok(ctx, hipHostMalloc(reinterpret_cast<void**>(&ctx->h_scalars),
-                                         sizeof(DevScalars)), "hipHostMalloc");
-    ok = ok && hip_ok(ctx, hipHostMalloc(reinterpret_cast<void**>(&ctx->h_seq), 64), "hipHostMalloc") &&
+                                         sizeof(DevScalars), kCoherentHost), "hipHostMalloc");
+    ok = ok && hip_ok(ctx, hipHostMalloc(reinterpret_cast<void**>(&ctx->h_seq), 64, kCoherentHost), "hipHostMalloc") &&
          hip_ok(ctx, hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->dh_seq), ctx->h_seq, 0),
                 "hipHostGetDevicePointer") &&
          dev_alloc(ctx, &ctx->d_stage_done, 1, true);
     if (ok) *ctx->h_seq = 0;
     ctx->spin_sync = getenv("TBG_NO_SPIN_SYNC") == nullptr;
+    if (const char* e = getenv("TBG_CALL_TIMEOUT_MS")) ctx->call_timeout_ms = std::max(1.0, atof(e));
     ok = ok && hip_ok(ctx, hipEventCreateWithFlags(&ctx->results_ready, hipEventDisableTiming),
                       "hipEventCreate");
     ok = ok && hip_ok(ctx, hipHostMalloc(reinterpret_cast<void**>(&ctx->h_batch_ends),
@@ -1459,7 +1599,7 @@ tbg_ctx* tbg_open(const tbg_options* options) {
                                    size_t(options->batch_count_max) * 8), "hipHostMalloc");
     ok = ok && hip_ok(ctx, hipHostMalloc(reinterpret_cast<void**>(&ctx->h_results),
                                          size_t(std::max<uint64_t>(ev_max, 1)) *
-                                             sizeof(tb_create_result_t)),
+                                             sizeof(tb_create_result_t), kCoherentHost),
                       "hipHostMalloc");
     ok = ok && hip_ok(ctx, hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->dh_scalars),
                                                    ctx->h_scalars, 0), "hipHostGetDevicePointer") &&
@@ -1481,6 +1621,7 @@ tbg_ctx* tbg_open(const tbg_options* options) {
     T.undo_capacity = undo_cap;
     T.scalars = ctx->d_scalars;
     ctx->ae_async = getenv("TBG_AE_SYNC") == nullptr;
+    ctx->ae_window_on = getenv("TBG_NO_AE_WINDOW") == nullptr;
     T.acc_ts_index = ctx->acc_ts_index;
     T.tr_ts_index = ctx->tr_ts_index;
     DevScalars init{};
@@ -1523,7 +1664,7 @@ void tbg_close(tbg_ctx* ctx) {
                     ctx->fix_slots, ctx->d_stage_done,
                     ctx->pnt_call, ctx->pnt_fired, ctx->pv_slots,
                     ctx->bal_items, ctx->chunk_info, ctx->bal_items_sorted, ctx->bucket_words, ctx->bucket_partials,
-                    ctx->window_partials, ctx->window_carry,
+                    ctx->window_partials, ctx->window_carry, ctx->window_counts, ctx->window_ts,
                     ctx->cub_temp, ctx->acc_ts_index, ctx->tr_ts_index, ctx->sel_buf,
                     ctx->pulse.keep, ctx->pulse.exp, ctx->pulse.ts, ctx->pulse.rows,
                     ctx->pulse.exp_b, ctx->pulse.rows_b, ctx->pulse.counters,
@@ -1544,7 +1685,7 @@ void tbg_close(tbg_ctx* ctx) {
     if (ctx->h_results) (void)hipHostFree(ctx->h_results);
     if (ctx->h_batch_ends) (void)hipHostFree(ctx->h_batch_ends);
     if (ctx->h_batch_ts) (void)hipHostFree(ctx->h_batch_ts);
-    for (const auto& r : ctx->registered) (void)hipHostUnregister(reinterpret_cast<void*>(r.host));
+    for (const auto& r : ctx->registered) host_pin_release(reinterpret_cast<void*>(r.host));
     if (ctx->results_ready) (void)hipEventDestroy(ctx->results_ready);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -1658,12 +1799,16 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
         const uint32_t wkeys = std::min<uint32_t>(kWindowKeys, 4u << pair_shift);
         hipLaunchKernelGGL(bal_window_accumulate, dim3(nwg), dim3(kWindowThreads), 0, ctx->stream,
                            target, ctx->bal_items, n, pair_shift, wkeys, ctx->window_partials,
-                           ctx->window_carry);
+                           ctx->window_carry, ctx->window_counts, &ctx->d_scalars->flags);
         tmark(ctx, "bal_window");
         hipLaunchKernelGGL(bal_window_apply, dim3((wkeys + 63) / 64), dim3(kApplyThreads), 0,
                            ctx->stream, target,
                            ctx->window_partials, nwg, pair_shift, wkeys, ctx->T.acc_rows_used,
-                           ctx->window_carry);
+                           ctx->window_carry, &ctx->d_scalars->flags);
+        ctx->win.epoch = c.epoch;
+        ctx->win.nwg = nwg;
+        ctx->win.ps = pair_shift;
+        ctx->win.wkeys = wkeys;
         tmark(ctx, "bal_apply");
         rc = hip_ok(ctx, hipGetLastError(), "launch") ? 0 : TBG_EHIP;
     } else if (!rc && use_buckets) {
@@ -1729,7 +1874,7 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
             rc = stage_call_outputs(ctx, d_results, dst, dst ? n : 0, true, snap ? &J : nullptr, true,
                                     seq);
         // (its graph queued now: the host's launch calls overlap the call's kernels)
-        if (!rc && snap) rc = ae_launch_graph(ctx);
+        if (!rc && snap) rc = ae_launch_graph(ctx, n);
         ctx->ae_snap_early = snap && !rc;
         if (!rc) rc = spin ? spin_wait(ctx, seq)
                            : (hip_ok(ctx, hipStreamSynchronize(ctx->stream), "sync") ? 0 : TBG_EHIP);
@@ -2012,14 +2157,11 @@ extern "C" {
 int tbg_register_host(tbg_ctx* ctx, void* ptr, uint64_t size) {
     if (!ctx || !ptr || size == 0) return TBG_EINVAL;
     if (is_registered(ctx, ptr, size)) return 0;
-    HIP_TRY(ctx, hipHostRegister(ptr, size, hipHostRegisterMapped));
-    void* dev = nullptr;
-    if (hipHostGetDevicePointer(&dev, ptr, 0) != hipSuccess || !dev) {
-        (void)hipHostUnregister(ptr);
-        ctx->error = "hipHostGetDevicePointer";
-        return TBG_EHIP;
-    }
-    ctx->registered.push_back({reinterpret_cast<uintptr_t>(ptr), size, reinterpret_cast<uintptr_t>(dev)});
+    // Several ctxs of one process (shards, state machines) may register the same message pool:
+    // registrations are counted process-wide and the last user unregisters (host_pin_release).
+    uintptr_t dev = 0;
+    if (!host_pin_acquire(ctx, ptr, size, &dev)) return TBG_EHIP;
+    ctx->registered.push_back({reinterpret_cast<uintptr_t>(ptr), size, dev});
     return 0;
 }
 
@@ -2027,8 +2169,9 @@ int tbg_unregister_host(tbg_ctx* ctx, void* ptr) {
     if (!ctx) return TBG_EINVAL;
     for (size_t i = 0; i < ctx->registered.size(); i++) {
         if (ctx->registered[i].host != reinterpret_cast<uintptr_t>(ptr)) continue;
+        if (int rc = ae_join(ctx)) return rc;
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-        HIP_TRY(ctx, hipHostUnregister(ptr));
+        host_pin_release(ptr);
         ctx->registered.erase(ctx->registered.begin() + long(i));
         return 0;
     }
@@ -2037,6 +2180,8 @@ int tbg_unregister_host(tbg_ctx* ctx, void* ptr) {
 
 int tbg_synchronize(tbg_ctx* ctx) {
     if (!ctx) return TBG_EINVAL;
+    // (the side stream's AccountEvents appends too: the call's stream waits for them first)
+    if (int rc = ae_join(ctx)) return rc;
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     return 0;
 }

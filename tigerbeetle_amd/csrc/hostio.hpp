@@ -96,9 +96,12 @@ __global__ void __launch_bounds__(kStageThreads) stage_out(StageOut s, AeSnapJob
     if (s.src)
         for (uint32_t i = tid; i < s.n; i += gridDim.x * kStageThreads) s.dst[i] = s.src[i];
     if (s.host_seq) {
+        // Every thread releases its own stores at system scope before the barrier (a fence orders
+        // only the issuing wave's stores; a workgroup barrier waits at workgroup scope only): the
+        // workgroup's count then covers every result and scalar word it wrote.
+        __threadfence_system();
         __syncthreads();
         if (threadIdx.x == 0) {
-            __threadfence_system();
             if (atomicAdd(s.done, 1u) == gridDim.x - 1) {
                 atomicExch(s.done, 0u);
                 __threadfence_system();

@@ -492,7 +492,7 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
                                             bool prev_linked, uint64_t* fast_ts,
                                             unsigned int* bucket_hist) {
     bool imported = false, post_void = false, dup = false, closable = false, hot = false;
-    bool need_commit = false, chain_fast = false;
+    bool need_commit = false, chain_fast = false, ae_slow = false;
     const uint16_t f = t.flags;
     imported = (f & TB_TRANSFER_IMPORTED) != 0;
     post_void = (f & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) != 0;
@@ -679,10 +679,12 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
                 *reinterpret_cast<uint4*>(c.bal_items + 2 * uint64_t(k)) = make_uint4(~0u, ~0u, ~0u, ~0u);
         } else if (c.bal_items && c.pair_shift) {
             const uint32_t ps = c.pair_shift;
+            ae_slow = pending;  // (the AccountEvents window tracks posted balances only)
             if (item_packable(c, amount)) {
                 c.bal_items[k] = (amount << (2 * ps + 1)) | (uint64_t(pending) << (2 * ps)) |
                                  (uint64_t(cr.row) << ps) | dr.row;
             } else {
+                ae_slow = true;
                 c.bal_items[k] = ~0ull;  // too wide to pack: atomics in tr_commit
                 need_commit = true;
             }
@@ -738,7 +740,8 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
     }
     return (imported ? kFlagImported : 0u) | (post_void ? kFlagPostVoid : 0u) |
            (dup ? kFlagDuplicate : 0u) | (closable ? kFlagClosable : 0u) | (hot ? kFlagHot : 0u) |
-           (need_commit ? kFlagNeedCommit : 0u) | (chain_fast ? kFlagChain : 0u);
+           (need_commit ? kFlagNeedCommit : 0u) | (chain_fast ? kFlagChain : 0u) |
+           (ae_slow ? kFlagAeSlow : 0u);
 }
 
 // Per 64-event chunk of a create_transfers call (one lane each): the batch b0 of its first event,
@@ -1621,29 +1624,45 @@ __device__ inline void window_field_add(const BalTarget& B, uint32_t row, uint32
     if (hi >= kHazardHiLimit) acc_hazard_set(B.index, B.entry_of, row, kHazardHigh);
 }
 
+// A workgroup's slice of the items: [b0, b1) with `per` even (uint4 loads). The AccountEvents
+// emit of window calls (events.hpp, ae_window_emit) walks the same slices.
+__host__ __device__ inline uint32_t window_slice_per(uint32_t n, uint32_t nwg) {
+    return ((n + nwg - 1) / nwg + 1) & ~1u;
+}
+
+// (+ per workgroup: the count of its slice's items -- the created events of a call the
+// AccountEvents window takes -- and kFlagWideSums when a u32 window counter carried)
 __global__ void __launch_bounds__(kWindowThreads) bal_window_accumulate(
     BalTarget B, const uint64_t* items, uint32_t n, uint32_t ps, uint32_t wkeys,
-    uint32_t* partials, unsigned long long* carry) {
+    uint32_t* partials, unsigned long long* carry, unsigned int* slice_count,
+    unsigned int* call_flags) {
     __shared__ uint32_t acc[kWindowKeys];
+    __shared__ uint32_t wave_items[kWindowThreads / 64];
     for (uint32_t i = threadIdx.x; i < wkeys; i += kWindowThreads) acc[i] = 0;
     __syncthreads();
-    const uint32_t per = ((n + gridDim.x - 1) / gridDim.x + 1) & ~1u;  // even: uint4 loads
+    const uint32_t per = window_slice_per(n, gridDim.x);
     const uint32_t b0 = blockIdx.x * per;
     const uint32_t b1 = b0 + per < n ? b0 + per : n;
     const uint64_t rmask = (1ull << ps) - 1;
+    uint32_t n_items = 0;
+    bool wide = false;
     auto add = [&](uint32_t f, uint32_t row, uint64_t amount) {
         const uint32_t key = (f << ps) | row;
         if (key < wkeys) {
             const uint32_t lo = uint32_t(amount);
             const uint32_t old = atomicAdd(&acc[key], lo);
             const uint64_t hi = (amount >> 32) + (uint32_t(old + lo) < old ? 1 : 0);
-            if (hi) atomicAdd(&carry[key], (unsigned long long)hi);
+            if (hi) {
+                atomicAdd(&carry[key], (unsigned long long)hi);
+                wide = true;
+            }
         } else {
             window_field_add(B, row, f, amount, true);
         }
     };
     auto item = [&](uint64_t x) {
         if (x == ~0ull) return;
+        n_items++;
         const uint32_t dr = uint32_t(x & rmask), cr = uint32_t((x >> ps) & rmask);
         const uint32_t pend = uint32_t(x >> (2 * ps)) & 1u;
         const uint64_t amount = x >> (2 * ps + 1);
@@ -1667,7 +1686,15 @@ __global__ void __launch_bounds__(kWindowThreads) bal_window_accumulate(
         item(items[i]);
         if (i + 1 < b1) item(items[i + 1]);
     }
+    if (__any(wide) && (threadIdx.x & 63) == 0) atomicOr(call_flags, kFlagWideSums);
+    for (int off = 32; off > 0; off >>= 1) n_items += __shfl_xor(n_items, off);
+    if ((threadIdx.x & 63) == 0) wave_items[threadIdx.x >> 6] = n_items;
     __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (uint32_t w = 0; w < kWindowThreads / 64; w++) t += wave_items[w];
+        slice_count[blockIdx.x] = t;
+    }
     uint32_t* out = partials + uint64_t(blockIdx.x) * wkeys;
     for (uint32_t k = threadIdx.x; k < wkeys; k += kWindowThreads) out[k] = acc[k];
 }
@@ -1676,9 +1703,10 @@ __global__ void __launch_bounds__(kWindowThreads) bal_window_accumulate(
 // those keys (coalesced 256-B rows), then LDS combines them -- 5,000 waves over the chip instead
 // of one lane walking all partials of a key.
 constexpr uint32_t kApplyThreads = 1024;
+// (kFlagWideSums when a key's total reaches 2^32: the AccountEvents window keeps u32 sums)
 __global__ void __launch_bounds__(kApplyThreads) bal_window_apply(
     BalTarget B, const uint32_t* partials, uint32_t nwg, uint32_t ps, uint32_t wkeys,
-    uint64_t rows_used, unsigned long long* carry) {
+    uint64_t rows_used, unsigned long long* carry, unsigned int* call_flags) {
     __shared__ uint64_t part[kApplyThreads / 64][64];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t k = blockIdx.x * 64 + lane;
@@ -1707,6 +1735,7 @@ __global__ void __launch_bounds__(kApplyThreads) bal_window_apply(
         sum += u128(c) << 32;
         carry[k] = 0;
     }
+    if (c || (s >> 32)) atomicOr(call_flags, kFlagWideSums);
     window_field_add(B, row, f, sum, false);
 }
 

@@ -48,6 +48,10 @@ enum : unsigned int {
     kFlagNeedCommit = 1u << 7, // some event is not a plain FAST event (tr_commit must run)
     kFlagFlowStalled = 1u << 8, // the flow replay's watchdog fired (a bug: the call fails)
     kFlagChain = 1u << 9,      // some linked chain's event is FAST (tr_commit decides the chain)
+    // AccountEvents (events.hpp): the window emit takes calls whose created events are all plain
+    // single-phase FAST events with a pair item and whose window sums stay below 2^32.
+    kFlagAeSlow = 1u << 10,    // a FAST event the AccountEvents window cannot take
+    kFlagWideSums = 1u << 11,  // a window key's sum reached 2^32
 };
 // Call flags under which tr_commit re-validates (and may demote) ingest's FAST events.
 constexpr unsigned int kCommitFlags = kFlagImported | kFlagPostVoid | kFlagDuplicate | kFlagHot |

@@ -44,6 +44,7 @@ class TbgStats(ctypes.Structure):
         ("fast", ctypes.c_uint64),
         ("replayed", ctypes.c_uint64),
         ("static_fail", ctypes.c_uint64),
+        ("ae_window", ctypes.c_uint64),
     ]
 
 
