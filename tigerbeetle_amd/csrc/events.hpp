@@ -1166,14 +1166,63 @@ __global__ void ae_change_events(Tables T, const tb_account_event_t* log, const 
     out[i] = o;
 }
 
-// Log order repair (imported transfers may postdate... precede earlier expiries): the log sorted by
-// timestamp, stable.
+// ---- Log order repair -------------------------------------------------------------------------
+//
+// The log is a sequence of appended blocks, each in timestamp order; an imported transfer (whose
+// timestamp precedes a pulse's expiries already in the log) breaks the order between blocks.
+// ae_sort_log (executor) restores it by merging the log's natural runs: ae_run_flags marks each
+// run's first position (a timestamp below its predecessor's), a selection lists the runs, and each
+// ae_merge_pass merges runs 2j and 2j + 1 (every lane finds its first output's split by a merge-path
+// binary search, then merges kMergePer outputs), ceil(log2(runs)) passes; the resulting
+// permutation gathers the records and references (ae_permute). Timestamps are unique, so the
+// order is total (no library sort).
 __global__ void ae_sort_keys(const tb_account_event_t* log, uint64_t n, uint64_t* keys,
-                             uint32_t* idx) {
+                             uint32_t* idx, uint8_t* run_first) {
     const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    keys[i] = log[i].timestamp;
+    const uint64_t ts = log[i].timestamp;
+    keys[i] = ts;
     idx[i] = uint32_t(i);
+    run_first[i] = i == 0 || ts < log[i - 1].timestamp;
+}
+
+constexpr uint32_t kMergePer = 8;
+// starts[0 .. runs]: the runs' first positions, starts[runs] = n.
+__global__ void ae_merge_pass(const uint64_t* key, const uint32_t* val, const uint64_t* starts,
+                              uint32_t runs, uint64_t n, uint64_t* key_out, uint32_t* val_out) {
+    uint64_t d = (uint64_t(blockIdx.x) * blockDim.x + threadIdx.x) * kMergePer;
+    if (d >= n) return;
+    const uint64_t d_end = d + kMergePer < n ? d + kMergePer : n;
+    // the pair of runs holding output d: the last p with starts[2p] <= d
+    const uint32_t pairs = (runs + 1) / 2;
+    uint32_t lo = 0, hi = pairs;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (starts[2 * mid] <= d) lo = mid;
+        else hi = mid;
+    }
+    for (uint32_t p = lo; d < d_end && p < pairs; p++) {
+        const uint64_t a0 = starts[2 * p];
+        const uint64_t a1 = starts[2 * p + 1 < runs ? 2 * p + 1 : runs];
+        const uint64_t b1 = starts[2 * p + 2 < runs ? 2 * p + 2 : runs];
+        const uint64_t b0 = a1, la = a1 - a0, lb = b1 - b0;
+        // of the pair's first k outputs, the number taken from run a
+        const uint64_t k = d - a0;
+        uint64_t l = k > lb ? k - lb : 0, h = k < la ? k : la;
+        while (l < h) {
+            const uint64_t m = (l + h) >> 1;
+            if (key[b0 + (k - 1 - m)] < key[a0 + m]) h = m;
+            else l = m + 1;
+        }
+        uint64_t i = a0 + l, j = b0 + (k - l);
+        const uint64_t stop = d_end < b1 ? d_end : b1;
+        for (; d < stop; d++) {
+            const bool take_a = j >= b1 || (i < a1 && key[i] < key[j]);
+            const uint64_t src = take_a ? i++ : j++;
+            key_out[d] = key[src];
+            val_out[d] = val[src];
+        }
+    }
 }
 __global__ void ae_permute(const tb_account_event_t* log, const AeRef* refs, const uint32_t* idx,
                            uint64_t n, tb_account_event_t* log_out, AeRef* refs_out) {

@@ -5,7 +5,6 @@
 // ingest pass, to learn whether the call holds imported events, which need timestamp indexes).
 
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include <fcntl.h>
 #include <unistd.h>
@@ -187,8 +186,6 @@ struct tbg_ctx {
     uint32_t* idx_dirty = nullptr;
     unsigned int* idx_counters = nullptr;
     uint32_t idx_dirty_cap = 0;
-    void* cub_temp = nullptr;
-    size_t cub_temp_bytes = 0;
     // chained scans (prims.hpp): per-tile status words, the tile ticket, launch sequence
     unsigned long long* scan_status = nullptr;
     uint64_t scan_tiles_cap = 0;
@@ -282,16 +279,6 @@ bool dev_alloc(tbg_ctx* ctx, T** p, uint64_t count, bool zero) {
     if (!hip_ok(ctx, hipMalloc(reinterpret_cast<void**>(p), bytes), "hipMalloc")) return false;
     if (zero && !hip_ok(ctx, hipMemsetAsync(*p, 0, bytes, ctx->stream), "hipMemset")) return false;
     return true;
-}
-
-int ensure_cub_temp(tbg_ctx* ctx, size_t bytes) {
-    if (bytes <= ctx->cub_temp_bytes) return 0;
-    if (ctx->cub_temp) (void)hipFree(ctx->cub_temp);
-    ctx->cub_temp = nullptr;
-    ctx->cub_temp_bytes = 0;
-    HIP_TRY(ctx, hipMalloc(&ctx->cub_temp, bytes));
-    ctx->cub_temp_bytes = bytes;
-    return 0;
 }
 
 // One chained scan (prims.hpp): `n` items, the op's emits and total.
@@ -1266,28 +1253,52 @@ int ae_sort_log(tbg_ctx* ctx) {
         return ae_publish(ctx);
     }
     const uint64_t n = ctx->ae_used;
-    uint64_t *keys = nullptr, *keys2 = nullptr;
-    uint32_t *idx = nullptr, *idx2 = nullptr;
+    uint64_t *keys = nullptr, *keys2 = nullptr, *starts = nullptr;
+    uint32_t *idx = nullptr, *idx2 = nullptr, *list = nullptr;
+    uint8_t* run_first = nullptr;
     tb_account_event_t* log2 = nullptr;
     AeRef* ref2 = nullptr;
     if (!(dev_alloc(ctx, &keys, n, false) && dev_alloc(ctx, &keys2, n, false) &&
           dev_alloc(ctx, &idx, n, false) && dev_alloc(ctx, &idx2, n, false) &&
+          dev_alloc(ctx, &run_first, n, false) && dev_alloc(ctx, &list, n, false) &&
+          dev_alloc(ctx, &starts, n + 1, false) &&
           dev_alloc(ctx, &log2, n, false) && dev_alloc(ctx, &ref2, n, false)))
         rc = TBG_ENOMEM;
     if (!rc) {
+        // the natural runs (each appended block is in order), merged pairwise
         hipLaunchKernelGGL(ae_sort_keys, dim3(grid_for(n)), dim3(kBlock), 0, ctx->stream,
-                           ctx->ae_log, n, keys, idx);
-        size_t bytes = 0;
-        if (hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, keys, keys2, idx, idx2, int(n), 0,
-                                               64, ctx->stream) != hipSuccess)
+                           ctx->ae_log, n, keys, idx, run_first);
+        unsigned int* d_count = &ctx->d_scalars->slow_count;  // scratch word (between calls)
+        rc = select_flagged(ctx, run_first, n, list, d_count);
+        unsigned int runs = 0;
+        if (!rc && (hipMemcpyAsync(&runs, d_count, 4, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+                    hipStreamSynchronize(ctx->stream) != hipSuccess))
             rc = TBG_EHIP;
-        if (!rc) rc = ensure_cub_temp(ctx, bytes);
-        if (!rc && hipcub::DeviceRadixSort::SortPairs(ctx->cub_temp, bytes, keys, keys2, idx, idx2,
-                                                      int(n), 0, 64, ctx->stream) != hipSuccess)
+        std::vector<uint32_t> first(runs);
+        if (!rc && runs && hipMemcpy(first.data(), list, runs * 4ull, hipMemcpyDeviceToHost) != hipSuccess)
             rc = TBG_EHIP;
+        std::vector<uint64_t> st(first.begin(), first.end());
+        st.push_back(n);
+        while (!rc && runs > 1) {
+            if (hipMemcpy(starts, st.data(), st.size() * 8, hipMemcpyHostToDevice) != hipSuccess) {
+                rc = TBG_EHIP;
+                break;
+            }
+            const uint64_t lanes = (n + kMergePer - 1) / kMergePer;
+            hipLaunchKernelGGL(ae_merge_pass, dim3(grid_for(lanes)), dim3(kBlock), 0, ctx->stream,
+                               keys, idx, starts, runs, n, keys2, idx2);
+            if (hipStreamSynchronize(ctx->stream) != hipSuccess) rc = TBG_EHIP;
+            std::swap(keys, keys2);
+            std::swap(idx, idx2);
+            std::vector<uint64_t> next;
+            for (uint32_t r = 0; r < runs; r += 2) next.push_back(st[r]);
+            next.push_back(n);
+            st.swap(next);
+            runs = (runs + 1) / 2;
+        }
         if (!rc) {
             hipLaunchKernelGGL(ae_permute, dim3(grid_for(n)), dim3(kBlock), 0, ctx->stream,
-                               ctx->ae_log, ctx->ae_ref, idx2, n, log2, ref2);
+                               ctx->ae_log, ctx->ae_ref, idx, n, log2, ref2);
             if (hipMemcpyAsync(ctx->ae_log, log2, n * sizeof(tb_account_event_t),
                                hipMemcpyDeviceToDevice, ctx->stream) != hipSuccess ||
                 hipMemcpyAsync(ctx->ae_ref, ref2, n * sizeof(AeRef), hipMemcpyDeviceToDevice,
@@ -1296,6 +1307,8 @@ int ae_sort_log(tbg_ctx* ctx) {
                 rc = TBG_EHIP;
         }
     }
+    for (void* p : {(void*)run_first, (void*)list, (void*)starts})
+        if (p) (void)hipFree(p);
     for (void* p : {(void*)keys, (void*)keys2, (void*)idx, (void*)idx2, (void*)log2, (void*)ref2})
         if (p) (void)hipFree(p);
     if (rc) return rc;
@@ -1665,7 +1678,7 @@ void tbg_close(tbg_ctx* ctx) {
                     ctx->pnt_call, ctx->pnt_fired, ctx->pv_slots,
                     ctx->bal_items, ctx->chunk_info, ctx->bal_items_sorted, ctx->bucket_words, ctx->bucket_partials,
                     ctx->window_partials, ctx->window_carry, ctx->window_counts, ctx->window_ts,
-                    ctx->cub_temp, ctx->acc_ts_index, ctx->tr_ts_index, ctx->sel_buf,
+                    ctx->acc_ts_index, ctx->tr_ts_index, ctx->sel_buf,
                     ctx->pulse.keep, ctx->pulse.exp, ctx->pulse.ts, ctx->pulse.rows,
                     ctx->pulse.exp_b, ctx->pulse.rows_b, ctx->pulse.counters,
                     ctx->pulse.run_len, ctx->pulse.expired,
@@ -1722,15 +1735,14 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
     { const char* e = getenv("TBG_INGEST_GRID"); if (e) ig = std::min(grid_for(n), uint32_t(atoi(e))); }
     const bool use_sort = n >= kSortThreshold && ctx->bal_items_sorted;
     // Balance items pack (amount << key_bits) | field key into a u64; the all-ones key is the
-    // "no item" sentinel, so key_bits covers 4 * accounts + 1 values. The key sits in the low
-    // bits: rocPRIM (ROCm 7.2) radix-sorts u64 keys wrongly for begin_bit > 0 with end_bit = 64
-    // on its small-input path (tools/sorttest.hip: 200k items, bits [48, 64)).
+    // "no item" sentinel, so key_bits covers 4 * accounts + 1 values.
     const uint32_t key_end = uint32_t(4 * ctx->T.acc_rows_used);
     uint32_t key_bits = 1;
     while ((1ull << key_bits) <= key_end) key_bits++;
     // Key spaces of <= 2^14 accounts take the balance window (pair items, LDS counters; config
-    // 2); up to 65,536 accounts the bucketed path, whose LDS sums need amounts < 2^48 (key_bits
-    // >= 16); larger ones the radix sort + run reduction.
+    // 2); up to 262,144 accounts the bucketed path, whose LDS sums need amounts < 2^48 (key_bits
+    // >= 16); larger ones per-workgroup LDS hash tables (bal_hash_apply), or u128 atomics when
+    // the key space is sparse.
     uint32_t pair_shift = 1;
     while ((1ull << pair_shift) < ctx->T.acc_rows_used) pair_shift++;
     const bool use_window = use_sort && ctx->window_partials && pair_shift <= kWindowShiftMax &&
@@ -1833,26 +1845,12 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
         tmark(ctx, "bal_atomic");
         rc = hip_ok(ctx, hipGetLastError(), "launch") ? 0 : TBG_EHIP;
     } else if (!rc && use_sort && !ingest_atomics) {
-        // Balance deltas: sort the packed items by field key, reduce runs in u128.
-        size_t bytes = 0;
-        rc = hip_ok(ctx, hipcub::DeviceRadixSort::SortKeys(nullptr, bytes, ctx->bal_items,
-                                                           ctx->bal_items_sorted, items, 0,
-                                                           int(key_bits), ctx->stream), "sort size")
-                 ? 0 : TBG_EHIP;
-        if (!rc) rc = ensure_cub_temp(ctx, bytes);
-        if (!rc)
-            rc = hip_ok(ctx, hipcub::DeviceRadixSort::SortKeys(ctx->cub_temp, bytes, ctx->bal_items,
-                                                               ctx->bal_items_sorted, items,
-                                                               0, int(key_bits), ctx->stream), "sort")
-                     ? 0 : TBG_EHIP;
-        tmark(ctx, "bal_sort");
-        if (!rc) {
-            const uint64_t tiles = (uint64_t(items) + kReduceTile - 1) / kReduceTile;
-            hipLaunchKernelGGL(bal_reduce_tiles, dim3(uint32_t(tiles)), block, 0, ctx->stream,
-                               target, ctx->bal_items_sorted, uint64_t(items), key_bits, key_end);
-            tmark(ctx, "bal_reduce");
-            rc = hip_ok(ctx, hipGetLastError(), "launch") ? 0 : TBG_EHIP;
-        }
+        // Balance deltas: items summed per account field in per-workgroup LDS hash tables.
+        const uint64_t blocks = (uint64_t(items) + kHashSliceItems - 1) / kHashSliceItems;
+        hipLaunchKernelGGL(bal_hash_apply, dim3(uint32_t(blocks)), dim3(kHashThreads), 0,
+                           ctx->stream, target, ctx->bal_items, uint64_t(items), key_bits, key_end);
+        tmark(ctx, "bal_hash");
+        rc = hip_ok(ctx, hipGetLastError(), "launch") ? 0 : TBG_EHIP;
     }
     // A host-buffer call's results are queued for download here, so that one host
     // synchronisation covers them when the call needs no replay (else they are downloaded again).

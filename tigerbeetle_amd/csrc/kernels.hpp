@@ -14,9 +14,9 @@
 //                the call for pending-with-timeout) and commits FAST events (status, liveness,
 //                expires_at entry, pulse_next_timestamp, balance deltas) or demotes them to SLOW;
 //                finalises the id slots of DONE events (orphan / tombstone).
-//   balances     FAST balance deltas as (account field, amount) items, radix-sorted by field
-//                (hipcub) and reduced per run into u128 sums (bal_reduce_tiles); small calls use
-//                u128 atomics in tr_commit instead.
+//   balances     FAST balance deltas as (account field, amount) items summed per account field in
+//                LDS (the balance window, the buckets, or per-workgroup hash tables: bal_hash_apply)
+//                and added to the rows; sparse key spaces and small calls use u128 atomics.
 //   replay       the SLOW events in serial order on one lane (replay.hpp), then their id slots.
 //
 // Exactness argument: DESIGN.md §4.
@@ -1454,15 +1454,6 @@ __global__ void tr_commit(Tables T, Call<tb_transfer_t> c) {
     }
 }
 
-// Sorted balance items -> u128 sums added to the account fields, one tile of kReduceTile items
-// per block. An item is (amount << key_bits) | field key; keys >= key_end are the "no item"
-// sentinel. Each lane reduces 16 consecutive items (vector loads); lane-edge runs are merged in
-// order through LDS by lane 0. A run that touches neither tile edge is owned by this block: plain
-// read-modify-write. The tile's first and last runs may continue in a neighbour tile: u128 atomics
-// (at most two per tile).
-constexpr uint32_t kReducePerLane = 16;
-constexpr uint32_t kReduceTile = kBlock * kReducePerLane;
-
 struct BalTarget {
     tb_account_t* rows;
     AccIndex index;
@@ -1483,90 +1474,63 @@ __device__ inline void add_field(const BalTarget& B, uint32_t key, u128 sum, boo
     if (hi >= kHazardHiLimit) acc_hazard_set(B.index, B.entry_of, key >> 2, kHazardHigh);
 }
 
-__global__ void bal_reduce_tiles(BalTarget rows, const uint64_t* items, uint64_t n,
-                                 uint32_t key_bits, uint32_t key_end) {
-    __shared__ uint32_t first_key[kBlock], last_key[kBlock];
-    __shared__ uint64_t first_lo[kBlock], first_hi[kBlock], last_lo[kBlock], last_hi[kBlock];
-    __shared__ uint8_t single[kBlock];
-    const uint64_t kmask = (1ull << key_bits) - 1;
-    const uint64_t tile = uint64_t(blockIdx.x) * kReduceTile;
-    const uint64_t begin = tile + uint64_t(threadIdx.x) * kReducePerLane;
-    const uint64_t tile_end = tile + kReduceTile < n ? tile + kReduceTile : n;
-    uint32_t fk = key_end, lk = key_end;
-    u128 fs = 0, ls = 0;
-    bool one = true;
-    if (begin < tile_end) {
-        const uint64_t end = begin + kReducePerLane < tile_end ? begin + kReducePerLane : tile_end;
-        uint64_t it[kReducePerLane];
-        if (end - begin == kReducePerLane) {
-            const uint4* p = reinterpret_cast<const uint4*>(items + begin);
-#pragma unroll
-            for (int i = 0; i < 8; i++) {
-                uint4 q = p[i];
-                it[2 * i] = (uint64_t(q.y) << 32) | q.x;
-                it[2 * i + 1] = (uint64_t(q.w) << 32) | q.z;
-            }
-        } else {
-#pragma unroll
-            for (int i = 0; i < (int)kReducePerLane; i++) it[i] = begin + i < end ? items[begin + i] : ~0ull;
-        }
-        auto key_of = [&](uint64_t x) {
-            const uint64_t kk = x & kmask;
-            return kk < key_end ? uint32_t(kk) : key_end;
-        };
-        uint32_t cur = key_of(it[0]);
-        u128 sum = 0;
-        bool first_run = true;
-#pragma unroll
-        for (int i = 0; i < (int)kReducePerLane; i++) {
-            const uint32_t kk = key_of(it[i]);
-            if (kk != cur) {
-                if (first_run) {
-                    fk = cur;
-                    fs = sum;
-                    first_run = false;
-                    one = false;
-                } else if (cur < key_end) {
-                    add_field(rows, cur, sum, false);  // interior run of this lane: owned
-                }
-                cur = kk;
-                sum = 0;
-            }
-            sum += it[i] >> key_bits;
-        }
-        if (first_run) {
-            fk = cur;
-            fs = sum;
-        }
-        lk = cur;
-        ls = sum;
+// Key spaces too large for the buckets and not sparse (bal_hash_apply): each workgroup sums a slice
+// of kHashSliceItems items per account field in an LDS hash table (open addressing on the key,
+// u64 sums: amounts < 2^46 at these key widths, 2^11 items per slice) and adds every field's slice
+// sum to its row with u128 atomics -- a hot account costs one atomic per workgroup instead of one
+// per item, a cold one what bal_atomic_apply pays. An item whose probe window is full takes its
+// atomic at once. (This replaces a library radix sort of the items and a run reduction.)
+constexpr uint32_t kHashThreads = 256;
+constexpr uint32_t kHashSlots = 4096;
+constexpr uint32_t kHashItemsPerLane = 8;
+constexpr uint32_t kHashSliceItems = kHashThreads * kHashItemsPerLane;
+constexpr uint32_t kHashProbes = 32;
+constexpr uint32_t kHashEmpty = 0xFFFFFFFFu;
+
+__global__ void __launch_bounds__(kHashThreads) bal_hash_apply(BalTarget rows, const uint64_t* items,
+                                                               uint64_t n, uint32_t key_bits,
+                                                               uint32_t key_end) {
+    __shared__ uint32_t hkey[kHashSlots];
+    __shared__ unsigned long long hsum[kHashSlots];
+    for (uint32_t i = threadIdx.x; i < kHashSlots; i += kHashThreads) {
+        hkey[i] = kHashEmpty;
+        hsum[i] = 0;
     }
-    first_key[threadIdx.x] = fk;
-    last_key[threadIdx.x] = lk;
-    first_lo[threadIdx.x] = uint64_t(fs);
-    first_hi[threadIdx.x] = uint64_t(fs >> 64);
-    last_lo[threadIdx.x] = uint64_t(ls);
-    last_hi[threadIdx.x] = uint64_t(ls >> 64);
-    single[threadIdx.x] = one;
     __syncthreads();
-    // Lane-edge runs: the lane where a run starts adds it, walking forward over the lanes that
-    // continue it. A run that touches the tile's first item (it may continue from the previous
-    // tile) or its last (it may continue into the next) is shared: u128 atomics.
-    const uint32_t t = threadIdx.x;
-    auto finish = [&](uint32_t key, u128 sum, bool shared) {
-        uint32_t q = t + 1;
-        for (; q < kBlock && first_key[q] == key; q++) {
-            sum += ((u128)first_hi[q] << 64) | first_lo[q];
-            if (!single[q]) break;  // the run ends inside lane q
-        }
-        if (q == kBlock) shared = true;
-        if (key < key_end) add_field(rows, key, sum, shared);
-    };
-    if (t == 0 || last_key[t - 1] != fk) {
-        if (one) finish(fk, fs, t == 0);
-        else if (fk < key_end) add_field(rows, fk, fs, t == 0);
+    const uint64_t kmask = (1ull << key_bits) - 1;
+    const uint64_t base = uint64_t(blockIdx.x) * kHashSliceItems;
+    // items base + 2 (t + j * kHashThreads), + 1: coalesced 16-byte loads (n is even)
+    uint64_t it[kHashItemsPerLane];
+#pragma unroll
+    for (uint32_t j = 0; j < kHashItemsPerLane / 2; j++) {
+        const uint64_t i = base + 2 * (uint64_t(threadIdx.x) + uint64_t(j) * kHashThreads);
+        uint4 q = make_uint4(~0u, ~0u, ~0u, ~0u);
+        if (i < n) q = *reinterpret_cast<const uint4*>(items + i);
+        it[2 * j] = (uint64_t(q.y) << 32) | q.x;
+        it[2 * j + 1] = (uint64_t(q.w) << 32) | q.z;
     }
-    if (!one) finish(lk, ls, false);
+#pragma unroll
+    for (uint32_t j = 0; j < kHashItemsPerLane; j++) {
+        const uint64_t k64 = it[j] & kmask;
+        if (k64 >= key_end) continue;
+        const uint32_t key = uint32_t(k64);
+        const uint64_t amount = it[j] >> key_bits;
+        uint32_t h = (key * 0x9E3779B1u) >> (32 - 12);
+        bool placed = false;
+        for (uint32_t p = 0; p < kHashProbes && !placed; p++, h = (h + 1) & (kHashSlots - 1)) {
+            uint32_t cur = hkey[h];
+            if (cur == kHashEmpty) cur = atomicCAS(&hkey[h], kHashEmpty, key);
+            if (cur == kHashEmpty || cur == key) {
+                atomicAdd(&hsum[h], (unsigned long long)amount);
+                placed = true;
+            }
+        }
+        if (!placed) add_field(rows, key, amount, true);
+    }
+    static_assert(kHashSlots == 1u << 12, "hash width");
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < kHashSlots; i += kHashThreads)
+        if (hkey[i] != kHashEmpty) add_field(rows, hkey[i], hsum[i], true);
 }
 
 // Sparse key spaces (far more account fields than items): the FAST events' packed balance items

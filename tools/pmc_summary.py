@@ -14,7 +14,7 @@ from collections import defaultdict
 
 def short(name):
     n = name.split("(")[0]
-    for key in ("tr_ingest", "tr_commit", "bal_reduce_tiles", "bal_bucket_scatter",
+    for key in ("tr_ingest", "tr_commit", "bal_hash_apply", "bal_bucket_scatter",
                 "bal_bucket_accumulate", "bal_bucket_apply", "onesweep_iteration",
                 "onesweep_global_offsets", "acc_prepare", "acc_classify", "replay_kernel"):
         if key in name:
