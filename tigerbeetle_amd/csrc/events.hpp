@@ -965,37 +965,24 @@ __global__ void __launch_bounds__(kAeWinThreads) ae_window_emit(AeWindow W) {
         const uint64_t x = e < b1 ? W.items[e] : ~0ull;
         const bool valid = x != ~0ull;
         uint32_t dr = 0, cr = 0, a = 0;
-        uint4 D[6], C[6];
         uint64_t ts = 0;
         if (valid) {
             dr = uint32_t(x & rmask);
             cr = uint32_t((x >> ps) & rmask);
             a = uint32_t(x >> (2 * ps + 1));  // (< 2^32: no kFlagWideSums)
-            // the record's loads first: the rows' id and balances (words 0-4) and their ledger,
-            // flags and timestamp (word 7), the event's timestamp
-            const uint4* pd = reinterpret_cast<const uint4*>(&W.acc_rows[dr]);
-            const uint4* pc = reinterpret_cast<const uint4*>(&W.acc_rows[cr]);
-#pragma unroll
-            for (int j = 0; j < 5; j++) {
-                D[j] = pd[j];
-                C[j] = pc[j];
-            }
-            D[5] = pd[7];
-            C[5] = pc[7];
             ts = W.results[e].timestamp;
             next[2 * tid] = uint16_t(atomicExch(&head[dr], 2 * tid));
             next[2 * tid + 1] = uint16_t(atomicExch(&head[cr], 2 * tid + 1));
             amt[tid] = a;
         }
         const uint64_t bal = __ballot(valid);
-        const uint32_t rank = lane ? __popcll(bal & (~0ull >> (64 - lane))) : 0;
         if (lane == 0) wave_cnt[wv] = uint32_t(__popcll(bal));
         __syncthreads();
-        uint64_t my = pos + rank;
+        uint64_t wave_pos = pos;  // the wave's first record
         uint32_t round_total = 0;
         for (uint32_t j = 0; j < kAeWinThreads / 64; j++) {
             const uint32_t cj = wave_cnt[j];
-            my += j < wv ? cj : 0;
+            wave_pos += j < wv ? cj : 0;
             round_total += cj;
         }
         // later deltas: [0] the debit account's debits_posted, [1] its credits_posted, [2] / [3]
@@ -1027,26 +1014,44 @@ __global__ void __launch_bounds__(kAeWinThreads) ae_window_emit(AeWindow W) {
             atomicSub(&Rc[cr], a);
             ts_min = ts < ts_min ? ts : ts_min;
             ts_max = ts > ts_max ? ts : ts_max;
-            // row word 7: ledger, code | flags << 16, timestamp
-            uint4* out = reinterpret_cast<uint4*>(&W.log[my]);
-            ae_nt_store(out + 0, D[0]);
-            ae_nt_store(out + 1, D[1]);
-            ae_nt_store(out + 2, ae_sub_u32(D[2], later[0]));
-            ae_nt_store(out + 3, D[3]);
-            ae_nt_store(out + 4, ae_sub_u32(D[4], later[1]));
-            ae_nt_store(out + 5, C[0]);
-            ae_nt_store(out + 6, C[1]);
-            ae_nt_store(out + 7, ae_sub_u32(C[2], later[2]));
-            ae_nt_store(out + 8, C[3]);
-            ae_nt_store(out + 9, ae_sub_u32(C[4], later[3]));
-            ae_nt_store(out + 10, make_uint4(uint32_t(ts), uint32_t(ts >> 32), D[5].z, D[5].w));
-            ae_nt_store(out + 11, make_uint4(C[5].z, C[5].w, (D[5].y >> 16) | (C[5].y & 0xFFFF0000u), 0u));
-            ae_nt_store(out + 12, make_uint4(0, 0, 0, 0));
-            ae_nt_store(out + 13, make_uint4(a, 0, 0, 0));
-            ae_nt_store(out + 14, make_uint4(a, 0, 0, 0));
-            ae_nt_store(out + 15, make_uint4(D[5].x, uint32_t(TB_PENDING_NONE), 0, 0));
-            ae_nt_store(reinterpret_cast<uint4*>(&W.refs[my]),
+            const uint32_t rank = lane ? __popcll(bal & (~0ull >> (64 - lane))) : 0;
+            ae_nt_store(reinterpret_cast<uint4*>(&W.refs[wave_pos + rank]),
                         make_uint4(uint32_t(W.row_base + e), dr, cr, 0));
+        }
+        // The wave's records, four at a time (one 1 KB store per instruction when the four are
+        // consecutive): lane L writes word L % 16 of the record of event lane 4 j + L / 16,
+        // loading the one row word it needs (L2) and the event lane's values by lane shuffles.
+        //   words 0-4 / 5-9: the debit / credit account's id and balances (posted ones less the
+        //   later deltas); 10: timestamps; 11: the credit account's timestamp and both flags;
+        //   12: pending id (0); 13, 14: amount requested and amount; 15: ledger, status (none).
+        const uint32_t wd = lane & 15, sub = lane >> 4;
+        const bool credit_half = (wd >= 5 && wd < 10) || wd == 11;
+        const uint32_t k = wd < 5 ? wd : wd < 10 ? wd - 5 : 7;
+        for (uint32_t j = 0; j < 16; j++) {
+            if (((bal >> (4 * j)) & 0xF) == 0) continue;  // (wave-uniform)
+            const uint32_t src = 4 * j + sub;
+            const uint32_t s_dr = __shfl(dr, src), s_cr = __shfl(cr, src), s_a = __shfl(a, src);
+            // (a shuffle reads the source lane's value of the expression: select after it)
+            const uint32_t l0 = __shfl(later[0], src), l1 = __shfl(later[1], src);
+            const uint32_t l2 = __shfl(later[2], src), l3 = __shfl(later[3], src);
+            const uint32_t l_dpo = credit_half ? l2 : l0, l_cpo = credit_half ? l3 : l1;
+            const uint32_t ts_lo = __shfl(uint32_t(ts), src), ts_hi = __shfl(uint32_t(ts >> 32), src);
+            const bool v = (bal >> src) & 1;
+            uint4 q = make_uint4(0, 0, 0, 0);
+            if (v) q = reinterpret_cast<const uint4*>(&W.acc_rows[credit_half ? s_cr : s_dr])[k];
+            // word 11 takes the debit account's flags from word 10's lane (its row word 7)
+            const uint32_t dflags = __shfl(q.y, lane > 0 ? lane - 1 : 0);
+            if (!v) continue;
+            uint4 o = q;
+            if (k == 2) o = ae_sub_u32(q, l_dpo);
+            else if (k == 4) o = ae_sub_u32(q, l_cpo);
+            else if (wd == 10) o = make_uint4(ts_lo, ts_hi, q.z, q.w);
+            else if (wd == 11) o = make_uint4(q.z, q.w, (dflags >> 16) | (q.y & 0xFFFF0000u), 0u);
+            else if (wd == 12) o = make_uint4(0, 0, 0, 0);
+            else if (wd == 13 || wd == 14) o = make_uint4(s_a, 0, 0, 0);
+            else if (wd == 15) o = make_uint4(q.x, uint32_t(TB_PENDING_NONE), 0, 0);
+            const uint64_t at = wave_pos + uint64_t(__popcll(bal & ((1ull << src) - 1)));
+            ae_nt_store(reinterpret_cast<uint4*>(&W.log[at]) + wd, o);
         }
         pos += round_total;
         __syncthreads();  // (the lists are empty and R is current for the next round)
