@@ -60,6 +60,10 @@ __device__ inline void bal5_add(Bal5& a, const AeDelta& d) {
 
 struct AeScratch {
     AeDelta* deltas;        // per touch (2 * event + side)
+    // The kernels do nothing when *skip == skip_if (a small call's appends that ae_small_emit
+    // took over; null: never).
+    const unsigned int* skip = nullptr;
+    uint32_t skip_if = 0;
     GroupPlan G;            // the touches grouped by account row (table, segments); G.counts:
                             // [0] grouped touches, [1] listed accounts, [2] their chunks
     uint32_t* chunk_seg;    // per chunk of a listed account: the account's entry in G.big
@@ -343,7 +347,13 @@ struct AeStage {
     AeRef* ref;               // per event
     AeDelta* delta;           // per touch (2k + side)
     uint8_t* created;         // per event
+    // [0] the epoch of the last call whose staging holds an event ae_small_emit cannot take;
+    // [1] the epoch of the last call whose appends ae_small_emit made (the graph then skips)
+    unsigned int* words;
 };
+// An event ae_small_emit takes: created single-phase (its deltas are posted balances only, no
+// `closed` flip) with an amount below 2^19 (u32 sums over <= 8192 events cannot wrap).
+constexpr uint64_t kAeSmallAmountMax = 1ull << 19;
 
 struct AeSnapJob {
     Tables T;
@@ -375,6 +385,8 @@ __device__ inline void ae_snapshot_one(const AeSnapJob& J, uint32_t k) {
     AeScratch D{};
     D.deltas = J.st.delta;
     const uint8_t status = ae_transfer_sides(D, k, t, p);
+    if (status != TB_PENDING_NONE || t.amount.hi != 0 || t.amount.lo >= kAeSmallAmountMax)
+        J.st.words[0] = c.epoch;  // (ae_small_emit leaves this call to the general appends)
     tb_account_event_t* rec = J.st.rec;
     ae_write_record(&rec[k], ae_final_of(T.acc_rows[dr]), ae_final_of(T.acc_rows[cr]), t.timestamp,
                     f, status, p, c.events[k].amount, t.amount, t.ledger);
@@ -409,6 +421,7 @@ struct PositionsOf8 {
 __global__ void __launch_bounds__(kPlanThreads)
 ae_copy_group(AeStage st, const uint32_t* pos, AeScratch S, tb_account_event_t* log, AeRef* refs) {
     __shared__ GroupBlock B;
+    if (S.skip && *S.skip == S.skip_if) return;
     group_block_init(B);
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k == 0) S.G.counts[1] = S.G.counts[2] = 0;  // listed accounts / chunks (ae_group_small)
@@ -535,6 +548,7 @@ __device__ inline void ae_mid_account(Tables T, const AeScratch& S, uint32_t off
 __global__ void __launch_bounds__(kBlock) ae_group_small(Tables T, AeScratch S, uint64_t slots,
                                                          tb_account_event_t* log) {
     __shared__ uint32_t wave_buf[kBlock / 64][kGroupMid];
+    if (S.skip && *S.skip == S.skip_if) return;
     const GroupPlan& G = S.G;
     log += S.state[0];
     const uint64_t h = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -786,7 +800,8 @@ __global__ void __launch_bounds__(kGroupBigThreads) ae_chunk_emit(Tables T, AeSc
 __global__ void ae_scatter_tail(GroupPlan G, uint64_t pairs, const tb_account_event_t* log,
                                 const unsigned int* d_count, unsigned long long* state,
                                 unsigned long long* base, unsigned long long* scan_words,
-                                uint32_t n_scan_words) {
+                                uint32_t n_scan_words, const unsigned int* skip, uint32_t skip_if) {
+    if (skip && *skip == skip_if) return;
     const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     if (blockIdx.x == 0) {
         for (uint32_t w = threadIdx.x; w < n_scan_words; w += blockDim.x) scan_words[w] = 0;
@@ -816,6 +831,7 @@ __global__ void __launch_bounds__(kGroupBigThreads) ae_group_big_serial(AeScratc
                                                                       tb_account_event_t* log) {
     __shared__ SegmentLds L;
     __shared__ Bal5Lds B;
+    if (S.skip && *S.skip == S.skip_if) return;
     const GroupPlan& G = S.G;
     log += S.state[0];
     const uint32_t nbig = G.counts[1];
@@ -1092,6 +1108,169 @@ __global__ void __launch_bounds__(kAeWinThreads) ae_window_emit(AeWindow W) {
         W.state[0] = used + total;
     }
     *W.done = 0;
+}
+
+// ---- AccountEvents of small calls in one pass ----------------------------------------------------
+//
+// A small create_transfers call's appends (the side stream, behind the next call) when every
+// created event is single-phase with an amount below 2^19 and the key space is dense enough for
+// the LDS (<= kAeWinRowsMax accounts): the staged records (stage_out's snapshot: the finished
+// AccountEvent with both accounts' final state) need only their posted balances lowered by the
+// later events' deltas. One launch of kAeSmallWgs workgroups, one per 1024 staged events; each
+// sums the posted deltas of the events from its own first one on into LDS (R, the accounts' later
+// deltas at its start), then resolves its 1024 events as one round of ae_window_emit (touch lists
+// in LDS) and copies the records into the log with the balances patched, four records per 1 KB
+// store. The last workgroup closes the block (length, last timestamp, order). Calls it cannot take
+// go to the general appends queued behind it (their kernels skip the calls it took).
+constexpr uint32_t kAeSmallWgs = 8;
+static_assert(kAeSmallWgs * kAeWinThreads == 8192, "one round per workgroup over the staging");
+
+struct AeSmall {
+    AeStage st;
+    uint32_t epoch;
+    uint32_t rows;
+    tb_account_event_t* log;
+    AeRef* refs;
+    unsigned long long* state;     // the log on device (AeWindow::state)
+    unsigned int* counts;          // [kAeSmallWgs] created per workgroup, [kAeSmallWgs] done
+    unsigned long long* slice_ts;  // [2 * kAeSmallWgs]
+};
+
+__global__ void __launch_bounds__(kAeWinThreads) ae_small_emit(AeSmall A) {
+    __shared__ uint32_t Rd[kAeWinRowsMax];
+    __shared__ uint32_t Rc[kAeWinRowsMax];
+    __shared__ uint32_t head[kAeWinRowsMax];
+    __shared__ uint16_t next[2 * kAeWinThreads];
+    __shared__ uint32_t amt[kAeWinThreads];
+    __shared__ uint32_t wave_cnt[kAeWinThreads / 64];
+    __shared__ uint32_t before_lds;
+    __shared__ unsigned long long ts_lds[2];
+    if (A.st.words[0] == A.epoch) return;  // (an event the general appends take)
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, w = blockIdx.x;
+    if (w == 0 && tid == 0) A.st.words[1] = A.epoch;  // (the general appends skip)
+    for (uint32_t a = tid; a < A.rows; a += kAeWinThreads) {
+        Rd[a] = 0;
+        Rc[a] = 0;
+        head[a] = kAeWinNil;
+    }
+    if (tid == 0) {
+        before_lds = 0;
+        ts_lds[0] = ~0ull;
+        ts_lds[1] = 0;
+    }
+    __syncthreads();
+    // R: the posted deltas of the staged events from this workgroup's first one on; the created
+    // events before it (the block's positions).
+    const uint32_t e0 = w * kAeWinThreads;
+    uint32_t before = 0;
+    for (uint32_t e = tid; e < kAeAsyncMax; e += kAeWinThreads) {
+        if (!A.st.created[e]) continue;
+        if (e < e0) {
+            before++;
+            continue;
+        }
+        const AeRef r = A.st.ref[e];
+        const uint32_t a = uint32_t(A.st.delta[2 * e].posted);
+        atomicAdd(&Rd[r.dr_row], a);
+        atomicAdd(&Rc[r.cr_row], a);
+    }
+    for (int off = 32; off > 0; off >>= 1) before += __shfl_xor(before, off);
+    if (lane == 0 && before) atomicAdd(&before_lds, before);
+    // this workgroup's round: its events' touches on the accounts' lists
+    const uint32_t e = e0 + tid;
+    const bool valid = A.st.created[e] != 0;
+    uint32_t dr = 0, cr = 0, a = 0;
+    uint64_t ts = 0;
+    if (valid) {
+        const AeRef r = A.st.ref[e];
+        dr = r.dr_row;
+        cr = r.cr_row;
+        a = uint32_t(A.st.delta[2 * e].posted);
+        ts = A.st.rec[e].timestamp;
+        next[2 * tid] = uint16_t(atomicExch(&head[dr], 2 * tid));
+        next[2 * tid + 1] = uint16_t(atomicExch(&head[cr], 2 * tid + 1));
+        amt[tid] = a;
+    }
+    const uint64_t bal = __ballot(valid);
+    if (lane == 0) wave_cnt[wv] = uint32_t(__popcll(bal));
+    __syncthreads();
+    uint64_t wave_pos = A.state[0] + before_lds;
+    uint32_t total = 0;
+    for (uint32_t j = 0; j < kAeWinThreads / 64; j++) {
+        const uint32_t cj = wave_cnt[j];
+        wave_pos += j < wv ? cj : 0;
+        total += cj;
+    }
+    uint32_t later[4] = {0, 0, 0, 0};
+    if (valid) {
+#pragma unroll
+        for (int side = 0; side < 2; side++) {
+            const uint32_t acc = side ? cr : dr;
+            uint32_t sd = 0, sc = 0;
+            for (uint32_t nd = head[acc]; nd != kAeWinNil;) {
+                if ((nd >> 1) <= tid) {
+                    const uint32_t v = amt[nd >> 1];
+                    if (nd & 1) sc += v;
+                    else sd += v;
+                }
+                const uint32_t nx = next[nd];
+                nd = nx == 0xFFFFu ? kAeWinNil : nx;
+            }
+            later[2 * side] = Rd[acc] - sd;
+            later[2 * side + 1] = Rc[acc] - sc;
+        }
+        atomicMin(&ts_lds[0], ts);
+        atomicMax(&ts_lds[1], ts);
+        const uint32_t rank = lane ? __popcll(bal & (~0ull >> (64 - lane))) : 0;
+        ae_nt_store(reinterpret_cast<uint4*>(&A.refs[wave_pos + rank]),
+                    *reinterpret_cast<const uint4*>(&A.st.ref[e]));
+    }
+    // The records, four per 1 KB store: lane L copies word L % 16 of event lane 4 j + L / 16's
+    // staged record, the posted balances (words 2, 4 / 7, 9) lowered by the later deltas.
+    const uint32_t wd = lane & 15, sub = lane >> 4;
+    const bool credit_half = wd >= 5 && wd < 10;
+    const uint32_t k = credit_half ? wd - 5 : wd;
+    const uint4* recs = reinterpret_cast<const uint4*>(A.st.rec);
+    for (uint32_t j = 0; j < 16; j++) {
+        if (((bal >> (4 * j)) & 0xF) == 0) continue;  // (wave-uniform)
+        const uint32_t src = 4 * j + sub;
+        const uint32_t l0 = __shfl(later[0], src), l1 = __shfl(later[1], src);
+        const uint32_t l2 = __shfl(later[2], src), l3 = __shfl(later[3], src);
+        if (!((bal >> src) & 1)) continue;
+        const uint32_t es = e0 + (tid & ~63u) + src;
+        uint4 q = recs[uint64_t(es) * 16 + wd];
+        if (wd < 10 && k == 2) q = ae_sub_u32(q, credit_half ? l2 : l0);
+        else if (wd < 10 && k == 4) q = ae_sub_u32(q, credit_half ? l3 : l1);
+        const uint64_t at = wave_pos + uint64_t(__popcll(bal & ((1ull << src) - 1)));
+        ae_nt_store(reinterpret_cast<uint4*>(&A.log[at]) + wd, q);
+    }
+    __syncthreads();
+    if (tid != 0) return;
+    A.counts[w] = total;
+    A.slice_ts[2 * w] = ts_lds[0];
+    A.slice_ts[2 * w + 1] = ts_lds[1];
+    __threadfence();
+    if (atomicAdd(&A.counts[kAeSmallWgs], 1u) != gridDim.x - 1) return;
+    __threadfence();
+    const volatile unsigned int* counts = A.counts;
+    const volatile unsigned long long* sts = A.slice_ts;
+    uint64_t all = 0, first = 0, last = 0;
+    bool any = false;
+    for (uint32_t j = 0; j < gridDim.x; j++) {
+        const uint32_t cj = counts[j];
+        if (!cj) continue;
+        if (!any) first = sts[2 * j];
+        any = true;
+        last = sts[2 * j + 1];
+        all += cj;
+    }
+    const uint64_t used = A.state[0];
+    if (all) {
+        if (used && first <= A.state[1]) A.state[2] = 1;
+        if (last > A.state[1]) A.state[1] = last;
+        A.state[0] = used + all;
+    }
+    A.counts[kAeSmallWgs] = 0;
 }
 
 // ---- get_change_events ---------------------------------------------------------------------

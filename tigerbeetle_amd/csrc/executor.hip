@@ -235,6 +235,8 @@ struct tbg_ctx {
     // created flags and the appends found nothing).
     bool ae_snap_early = false;
     unsigned long long* ae_g_words = nullptr;  // [0] created count; [8..] the graph's scan words
+    unsigned int* ae_small_counts = nullptr;   // ae_small_emit: per workgroup, then done
+    unsigned long long* ae_small_ts = nullptr;
     unsigned long long* flow_debug = nullptr;
 
     // Per-kernel timing (tbg_profile): HIP events recorded on the call's stream between launches.
@@ -1053,10 +1055,22 @@ int ae_append(tbg_ctx* ctx, uint32_t n_upper, const unsigned int* d_count, Colle
 // fixed upper bound kAeAsyncMax): number the created events, copy and group, place, emit. The two
 // chained scans use their own status words and ticket (ae_g_words[7 ..]), which ae_scatter_tail
 // clears for the next append.
-int ae_launch_appends(tbg_ctx* ctx, uint32_t p) {
+int ae_launch_appends(tbg_ctx* ctx, uint32_t p, uint32_t epoch) {
+    hipStream_t st = ctx->ae_stream;
+    // The one-pass appends first (ae_small_emit); they take the call unless the staging holds an
+    // event they cannot, and then every kernel below skips it.
+    const bool small = ctx->ae_window_on && ctx->T.acc_rows_used <= kAeWinRowsMax;
+    const unsigned int* handled = ctx->ae_stage[p].words + 1;
+    if (small) {
+        AeSmall A{ctx->ae_stage[p], epoch, uint32_t(ctx->T.acc_rows_used), ctx->ae_log, ctx->ae_ref,
+                  ctx->ae_words + 4, ctx->ae_small_counts, ctx->ae_small_ts};
+        hipLaunchKernelGGL(ae_small_emit, dim3(kAeSmallWgs), dim3(kAeWinThreads), 0, st, A);
+    }
     AeScratch S = ctx->ae_g;
     S.state = ctx->ae_words + 4;
     S.pos = nullptr;
+    S.skip = small ? handled : nullptr;
+    S.skip_if = epoch;
     AeScratch Se = S;  // the emit kernels: the block's base (kept by ae_scatter_tail), event-
     Se.state = ctx->ae_g_words + 2;  // numbered touches and the staged deltas
     Se.pos = ctx->ae_pos;
@@ -1067,20 +1081,19 @@ int ae_launch_appends(tbg_ctx* ctx, uint32_t p) {
     const uint64_t slots = S.G.hmask + 1;
     const uint32_t tiles1 = (kAeAsyncMax + kScanTile - 1) / kScanTile;
     const uint32_t tiles2 = uint32_t((slots + kScanTile - 1) / kScanTile);
-    hipStream_t st = ctx->ae_stream;
     hipLaunchKernelGGL(chained_scan<PositionsOf8>, dim3(tiles1), dim3(kScanThreads), 0, st,
                        uint64_t(kAeAsyncMax), PositionsOf8{ctx->ae_stage[p].created, ctx->ae_pos, d_count},
-                       ScanState{scan_words, ticket, 0, 1});
+                       ScanState{scan_words, ticket, 0, 1, S.skip, epoch});
     hipLaunchKernelGGL(ae_copy_group, dim3((kAeAsyncMax + kPlanThreads - 1) / kPlanThreads),
                        dim3(kPlanThreads), 0, st, ctx->ae_stage[p], ctx->ae_pos, S, ctx->ae_log,
                        ctx->ae_ref);
     hipLaunchKernelGGL(chained_scan<ExclusiveSumU32>, dim3(tiles2), dim3(kScanThreads), 0, st,
                        slots, ExclusiveSumU32{S.G.hcnt, S.G.hoff, &S.G.counts[0]},
-                       ScanState{scan_words + tiles1, ticket, tiles1, 2});
+                       ScanState{scan_words + tiles1, ticket, tiles1, 2, S.skip, epoch});
     const uint64_t pairs = 2 * uint64_t(kAeAsyncMax);
     hipLaunchKernelGGL(ae_scatter_tail, dim3(grid_for(pairs)), dim3(kBlock), 0, st, S.G, pairs,
                        ctx->ae_log, d_count, S.state, ctx->ae_g_words + 2, ctx->ae_g_words + 7,
-                       1 + tiles1 + tiles2);
+                       1 + tiles1 + tiles2, S.skip, epoch);
     hipLaunchKernelGGL(ae_group_small, dim3(grid_for(slots)), dim3(kBlock), 0, st, ctx->T, Se, slots,
                        ctx->ae_log);
     hipLaunchKernelGGL(ae_group_big_serial, dim3(2 * kAeAsyncMax / (kGroupMid + 1) + 1),
@@ -1096,10 +1109,12 @@ int ensure_ae_async(tbg_ctx* ctx) {
         AeStage& st = ctx->ae_stage[p];
         if (!(dev_alloc(ctx, &st.rec, kAeAsyncMax, false) && dev_alloc(ctx, &st.ref, kAeAsyncMax, false) &&
               dev_alloc(ctx, &st.delta, 2 * kAeAsyncMax, false) &&
-              dev_alloc(ctx, &st.created, kAeAsyncMax, true)))
+              dev_alloc(ctx, &st.created, kAeAsyncMax, true) && dev_alloc(ctx, &st.words, 4, true)))
             return TBG_ENOMEM;
     }
-    if (!(dev_alloc(ctx, &ctx->ae_pos, kAeAsyncMax, false) && dev_alloc(ctx, &ctx->ae_g_words, 64, true)))
+    if (!(dev_alloc(ctx, &ctx->ae_pos, kAeAsyncMax, false) && dev_alloc(ctx, &ctx->ae_g_words, 64, true) &&
+          dev_alloc(ctx, &ctx->ae_small_counts, kAeSmallWgs + 1, true) &&
+          dev_alloc(ctx, &ctx->ae_small_ts, 2 * kAeSmallWgs, false)))
         return TBG_ENOMEM;
     if (int rc = alloc_ae_scratch(ctx, ctx->ae_g, cap)) return rc;
     // (the scans' words: 8 + tiles of both scans)
@@ -1135,13 +1150,13 @@ int ae_snap_job(tbg_ctx* ctx, const Call<tb_transfer_t>& c, AeSnapJob* J) {
 // The side stream appends staging buffer p (at most n AccountEvents) once the call's stream
 // reaches this point. The log's bound grows as the graph is queued: a call that fails later still
 // leaves a graph that may append.
-int ae_launch_graph(tbg_ctx* ctx, uint32_t n) {
+int ae_launch_graph(tbg_ctx* ctx, uint32_t n, uint32_t epoch) {
     const uint32_t p = ctx->ae_parity;
     ctx->ae_bound += n;
     ctx->ae_pending = true;
     HIP_TRY(ctx, hipEventRecord(ctx->ae_snap_ready[p], ctx->stream));
     HIP_TRY(ctx, hipStreamWaitEvent(ctx->ae_stream, ctx->ae_snap_ready[p], 0));
-    if (int rc = ae_launch_appends(ctx, p)) return rc;
+    if (int rc = ae_launch_appends(ctx, p, epoch)) return rc;
     HIP_TRY(ctx, hipEventRecord(ctx->ae_done[p], ctx->ae_stream));
     ctx->ae_done_recorded[p] = true;
     ctx->ae_parity = p ^ 1;
@@ -1158,7 +1173,7 @@ int ae_transfers_async(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
         if (int rc = ae_snap_job(ctx, c, &J)) return rc;
         hipLaunchKernelGGL(ae_snapshot, dim3(kAeAsyncMax / kBlock), dim3(kBlock), 0, ctx->stream, J);
         HIP_TRY(ctx, hipGetLastError());
-        if (int rc = ae_launch_graph(ctx, c.n)) return rc;
+        if (int rc = ae_launch_graph(ctx, c.n, c.epoch)) return rc;
     }
     ctx->ae_snap_early = false;
     return 0;
@@ -1662,11 +1677,14 @@ void tbg_close(tbg_ctx* ctx) {
         if (ctx->ae_snap_ready[p]) (void)hipEventDestroy(ctx->ae_snap_ready[p]);
         if (ctx->ae_done[p]) (void)hipEventDestroy(ctx->ae_done[p]);
         for (void* q : {(void*)ctx->ae_stage[p].rec, (void*)ctx->ae_stage[p].ref,
-                        (void*)ctx->ae_stage[p].delta, (void*)ctx->ae_stage[p].created})
+                        (void*)ctx->ae_stage[p].delta, (void*)ctx->ae_stage[p].created,
+                        (void*)ctx->ae_stage[p].words})
             if (q) (void)hipFree(q);
     }
     if (ctx->ae_pos) (void)hipFree(ctx->ae_pos);
     if (ctx->ae_g_words) (void)hipFree(ctx->ae_g_words);
+    for (void* q : {(void*)ctx->ae_small_counts, (void*)ctx->ae_small_ts})
+        if (q) (void)hipFree(q);
     free_ae_scratch(ctx->ae_g);
     if (ctx->ae_stream) (void)hipStreamDestroy(ctx->ae_stream);
     void* ptrs[] = {ctx->idx_dirty, ctx->idx_counters, ctx->T.acc_index.entries, ctx->T.acc_entry_of, ctx->T.acc.slots, ctx->T.acc_rows, ctx->T.acc_live, ctx->T.acc_hot,
@@ -1872,7 +1890,7 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
             rc = stage_call_outputs(ctx, d_results, dst, dst ? n : 0, true, snap ? &J : nullptr, true,
                                     seq);
         // (its graph queued now: the host's launch calls overlap the call's kernels)
-        if (!rc && snap) rc = ae_launch_graph(ctx, n);
+        if (!rc && snap) rc = ae_launch_graph(ctx, n, c.epoch);
         ctx->ae_snap_early = snap && !rc;
         if (!rc) rc = spin ? spin_wait(ctx, seq)
                            : (hip_ok(ctx, hipStreamSynchronize(ctx->stream), "sync") ? 0 : TBG_EHIP);

@@ -36,6 +36,10 @@ struct ScanState {
     unsigned int* ticket;        // monotone tile ticket counter
     uint32_t ticket_base;        // the ticket of this launch's first tile
     uint32_t seq;                // this launch's sequence number (1 .. 2^30 - 1)
+    // The launch does nothing when *skip == skip_if (a queued launch whose work another kernel
+    // took over; every launch sharing its status words and ticket must skip alike).
+    const unsigned int* skip = nullptr;
+    uint32_t skip_if = 0;
 };
 
 __device__ inline unsigned long long scan_word(uint32_t seq, uint64_t flag, uint32_t v) {
@@ -62,6 +66,7 @@ template <typename Op>
 __global__ void __launch_bounds__(kScanThreads) chained_scan(uint64_t n, Op op, ScanState st) {
     __shared__ uint32_t s_tile, s_prefix;
     __shared__ uint32_t s_wave[kScanThreads / 64];
+    if (st.skip && *st.skip == st.skip_if) return;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (tid == 0) s_tile = atomicAdd(st.ticket, 1u) - st.ticket_base;
     __syncthreads();
