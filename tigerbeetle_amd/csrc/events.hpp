@@ -359,7 +359,11 @@ struct AeSnapJob {
     Tables T;
     Call<tb_transfer_t> c;
     AeStage st;
-    bool on;
+    // Taken right after the call (before the host knows whether a replay follows): with a replay
+    // pending (stats[0], set by tr_commit) nothing is final yet -- a replayed event's slot may still
+    // read `created` from the speculation -- so the staging holds no created event (the side
+    // stream's appends, already queued, find none) and the executor stages again after the replay.
+    bool speculative;
 };
 __device__ inline void ae_snapshot_one(const AeSnapJob& J, uint32_t k) {
     const Tables& T = J.T;
@@ -393,10 +397,11 @@ __device__ inline void ae_snapshot_one(const AeSnapJob& J, uint32_t k) {
     J.st.ref[k] = AeRef{uint32_t(row), uint32_t(dr), uint32_t(cr), 0};
 }
 
-// The staging on its own (a call whose replay ran after stage_out).
 __global__ void ae_snapshot(AeSnapJob J) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k < kAeAsyncMax) ae_snapshot_one(J, k);
+    if (k >= kAeAsyncMax) return;
+    if (J.speculative && J.T.scalars->stats[0] != 0) J.st.created[k] = 0;
+    else ae_snapshot_one(J, k);
 }
 
 // u8 flags -> pos[i] = the number of flagged items before i (flagged items only); the count.

@@ -1143,7 +1143,7 @@ int ae_snap_job(tbg_ctx* ctx, const Call<tb_transfer_t>& c, AeSnapJob* J) {
     if (int rc = ensure_ae_async(ctx)) return rc;
     const uint32_t p = ctx->ae_parity;
     if (ctx->ae_done_recorded[p]) HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ae_done[p], 0));
-    *J = AeSnapJob{ctx->T, c, ctx->ae_stage[p], true};
+    *J = AeSnapJob{ctx->T, c, ctx->ae_stage[p], false};
     return 0;
 }
 
@@ -1466,11 +1466,9 @@ int stage_call_outputs(tbg_ctx* ctx, const tb_create_result_t* d_results, tb_cre
                ctx->T.tr.slots, ctx->d_scalars, seq ? ctx->d_stage_done : nullptr,
                seq ? ctx->dh_seq : nullptr, seq};
     if (!dst || !n) s.src = nullptr;
-    AeSnapJob J{};
-    if (snap) J = *snap;
-    const uint32_t items = std::max<uint32_t>(n, snap ? kAeAsyncMax : 0);
-    const uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>((items + kStageThreads - 1) / kStageThreads, 1024));
-    hipLaunchKernelGGL(stage_out, dim3(grid), dim3(kStageThreads), 0, ctx->stream, s, J);
+    (void)snap;
+    const uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>((n + kStageThreads - 1) / kStageThreads, 1024));
+    hipLaunchKernelGGL(stage_out, dim3(grid), dim3(kStageThreads), 0, ctx->stream, s);
     HIP_TRY(ctx, hipGetLastError());
     return 0;
 }
@@ -1881,16 +1879,24 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
             dst = mapped(ctx, ctx->early_dst, uint64_t(n) * 16);
             if (!dst) dst = ctx->dh_results;
         }
-        // (a small call's AccountEvents snapshot rides along: final unless a replay follows)
-        AeSnapJob J;
-        const bool snap = ae_async_ok(ctx, n) && !(rc = ae_snap_job(ctx, c, &J));
+        const bool snap = ae_async_ok(ctx, n);
         const bool spin = ctx->spin_sync && !ctx->timing;
         const unsigned int seq = spin ? (++ctx->seq ? ctx->seq : ++ctx->seq) : 0u;
-        if (!rc)
-            rc = stage_call_outputs(ctx, d_results, dst, dst ? n : 0, true, snap ? &J : nullptr, true,
-                                    seq);
-        // (its graph queued now: the host's launch calls overlap the call's kernels)
-        if (!rc && snap) rc = ae_launch_graph(ctx, n, c.epoch);
+        rc = stage_call_outputs(ctx, d_results, dst, dst ? n : 0, true, nullptr, true, seq);
+        // A small call's AccountEvents snapshot follows stage_out (the host's wait ends at
+        // stage_out): final unless a replay follows, then it stages nothing. Its appends are queued
+        // on the side stream now, so that the host's launch calls overlap the call's kernels.
+        if (!rc && snap) {
+            AeSnapJob J;
+            rc = ae_snap_job(ctx, c, &J);
+            if (!rc) {
+                J.speculative = true;
+                hipLaunchKernelGGL(ae_snapshot, dim3(kAeAsyncMax / kBlock), dim3(kBlock), 0,
+                                   ctx->stream, J);
+                rc = hip_ok(ctx, hipGetLastError(), "launch") ? 0 : TBG_EHIP;
+            }
+            if (!rc) rc = ae_launch_graph(ctx, n, c.epoch);
+        }
         ctx->ae_snap_early = snap && !rc;
         if (!rc) rc = spin ? spin_wait(ctx, seq)
                            : (hip_ok(ctx, hipStreamSynchronize(ctx->stream), "sync") ? 0 : TBG_EHIP);

@@ -70,25 +70,14 @@ struct StageOut {
     unsigned int seq;
 };
 
-// (+ a small call's AccountEvents staging, events.hpp, when J.on: the call's state is final here
-// unless its replay follows, in which case the executor stages it again after the replay)
-__global__ void __launch_bounds__(kStageThreads) stage_out(StageOut s, AeSnapJob J) {
+// (A small call's AccountEvents staging follows in its own kernel, ae_snapshot: the host's wait
+// ends here.)
+__global__ void __launch_bounds__(kStageThreads) stage_out(StageOut s) {
     const uint32_t tid = blockIdx.x * kStageThreads + threadIdx.x;
     if (s.fix_slots) {
         const uint64_t nfix = s.scalars->fixed;
         for (uint64_t i = tid; i < nfix; i += uint64_t(gridDim.x) * kStageThreads)
             s.id_slots[s.fix_slots[i]] = kTomb;
-    }
-    // Only when no event replays (stats[0], set by tr_commit): a replayed event's result is not
-    // final yet -- its slot may still read `created` from the speculation -- and the executor
-    // takes the snapshot again after the replay.
-    // (The graph behind it is already queued: with a replay pending it must find no created flag.)
-    if (J.on) {
-        const bool final = J.T.scalars->stats[0] == 0;
-        for (uint32_t k = tid; k < kAeAsyncMax; k += gridDim.x * kStageThreads) {
-            if (final) ae_snapshot_one(J, k);
-            else J.st.created[k] = 0;
-        }
     }
     if (s.scalars_src && blockIdx.x == 0)
         for (uint32_t w = threadIdx.x; w < s.scalar_words; w += kStageThreads)
