@@ -404,6 +404,43 @@ __global__ void ae_snapshot(AeSnapJob J) {
     else ae_snapshot_one(J, k);
 }
 
+// A pulse's expiries staged like a small call (ae_expiry_one's records, ae_collect_expiry's
+// order and stamps): the first m of `rows` (m on device), expiry i stamped timestamp - m + i + 1.
+// ae_small_emit takes a pulse whose expiries release pending amounts below 2^19 and close no
+// account (else the general appends, words[0]).
+struct AeExpirySnap {
+    Tables T;
+    const uint64_t* rows;
+    const unsigned int* m_dev;
+    uint64_t timestamp;
+    AeStage st;
+    uint32_t epoch;
+};
+__global__ void ae_expiry_snapshot(AeExpirySnap J) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= kAeAsyncMax) return;
+    const uint32_t m = *J.m_dev;
+    J.st.created[i] = i < m;
+    if (i >= m) return;
+    const Tables& T = J.T;
+    const uint64_t row = J.rows[i];
+    const tb_transfer_t& p = T.tr_rows[row];
+    const uint64_t dr = account_find(T, p.debit_account_id);
+    const uint64_t cr = account_find(T, p.credit_account_id);
+    const u128 d_pending = u128(0) - U(p.amount);
+    const uint32_t fd = (p.flags & TB_TRANSFER_CLOSING_DEBIT) != 0;
+    const uint32_t fc = (p.flags & TB_TRANSFER_CLOSING_CREDIT) != 0;
+    AeScratch D{};
+    D.deltas = J.st.delta;
+    ae_side(D, i, 0, d_pending, 0, fd);
+    ae_side(D, i, 1, d_pending, 0, fc);
+    ae_write_record(&J.st.rec[i], ae_final_of(T.acc_rows[dr]), ae_final_of(T.acc_rows[cr]),
+                    J.timestamp - m + i + 1, 0, TB_PENDING_EXPIRED, &p, tb_uint128_t{0, 0},
+                    p.amount, p.ledger);
+    J.st.ref[i] = AeRef{uint32_t(row), uint32_t(dr), uint32_t(cr), 0};
+    if (fd || fc || p.amount.hi != 0 || p.amount.lo >= kAeSmallAmountMax) J.st.words[0] = J.epoch;
+}
+
 // u8 flags -> pos[i] = the number of flagged items before i (flagged items only); the count.
 struct PositionsOf8 {
     static constexpr bool kEmitAll = false;
@@ -1134,12 +1171,25 @@ struct AeSmall {
     AeStage st;
     uint32_t epoch;
     uint32_t rows;
+    // 0: created transfers (posted deltas, words 2 / 4 lowered); 1: a pulse's expiries (pending
+    // deltas -amount, words 1 / 3 raised by the later expiries' amounts)
+    uint32_t pending;
     tb_account_event_t* log;
     AeRef* refs;
     unsigned long long* state;     // the log on device (AeWindow::state)
     unsigned int* counts;          // [kAeSmallWgs] created per workgroup, [kAeSmallWgs] done
     unsigned long long* slice_ts;  // [2 * kAeSmallWgs]
 };
+
+// A staged event's amount on both of its accounts (every staged event moves the same amount on
+// its two sides): posted for created transfers, the pending amount released by an expiry.
+__device__ inline uint32_t ae_small_amount(const AeSmall& A, uint32_t e) {
+    return A.pending ? uint32_t(0u - uint32_t(A.st.delta[2 * e].pending))
+                     : uint32_t(A.st.delta[2 * e].posted);
+}
+__device__ inline uint4 ae_add_u32(uint4 balance, uint32_t d) {
+    return ae_q(ae_u(balance) + u128(d));
+}
 
 __global__ void __launch_bounds__(kAeWinThreads) ae_small_emit(AeSmall A) {
     __shared__ uint32_t Rd[kAeWinRowsMax];
@@ -1175,7 +1225,7 @@ __global__ void __launch_bounds__(kAeWinThreads) ae_small_emit(AeSmall A) {
             continue;
         }
         const AeRef r = A.st.ref[e];
-        const uint32_t a = uint32_t(A.st.delta[2 * e].posted);
+        const uint32_t a = ae_small_amount(A, e);
         atomicAdd(&Rd[r.dr_row], a);
         atomicAdd(&Rc[r.cr_row], a);
     }
@@ -1190,7 +1240,7 @@ __global__ void __launch_bounds__(kAeWinThreads) ae_small_emit(AeSmall A) {
         const AeRef r = A.st.ref[e];
         dr = r.dr_row;
         cr = r.cr_row;
-        a = uint32_t(A.st.delta[2 * e].posted);
+        a = ae_small_amount(A, e);
         ts = A.st.rec[e].timestamp;
         next[2 * tid] = uint16_t(atomicExch(&head[dr], 2 * tid));
         next[2 * tid + 1] = uint16_t(atomicExch(&head[cr], 2 * tid + 1));
@@ -1244,8 +1294,10 @@ __global__ void __launch_bounds__(kAeWinThreads) ae_small_emit(AeSmall A) {
         if (!((bal >> src) & 1)) continue;
         const uint32_t es = e0 + (tid & ~63u) + src;
         uint4 q = recs[uint64_t(es) * 16 + wd];
-        if (wd < 10 && k == 2) q = ae_sub_u32(q, credit_half ? l2 : l0);
-        else if (wd < 10 && k == 4) q = ae_sub_u32(q, credit_half ? l3 : l1);
+        const uint32_t kd = A.pending ? 1 : 2, kc = A.pending ? 3 : 4;  // the patched words
+        const uint32_t l = wd >= 10 ? 0u : k == kd ? (credit_half ? l2 : l0)
+                                      : k == kc ? (credit_half ? l3 : l1) : 0u;
+        if (l) q = A.pending ? ae_add_u32(q, l) : ae_sub_u32(q, l);
         const uint64_t at = wave_pos + uint64_t(__popcll(bal & ((1ull << src) - 1)));
         ae_nt_store(reinterpret_cast<uint4*>(&A.log[at]) + wd, q);
     }

@@ -118,6 +118,12 @@ struct tbg_ctx {
     unsigned int seq = 0;
     bool spin_sync = false;
     double call_timeout_ms = 60000;  // spin_wait's bound (TBG_CALL_TIMEOUT_MS)
+    // The expires_at index's length as of the last create_transfers call or pulse (the pulse's
+    // first kernels need no synchronisation for it); cleared by anything else that changes it.
+    bool expiry_known = false;
+    uint64_t expiry_host = 0;
+    unsigned long long* h_pulse = nullptr;   // pinned: a pulse's expired count, the index length
+    unsigned long long* dh_pulse = nullptr;
     tb_create_result_t* dh_results = nullptr;
     uint32_t* dh_batch_ends = nullptr;
     uint64_t* dh_batch_ts = nullptr;
@@ -474,6 +480,8 @@ int end_call(tbg_ctx* ctx, uint32_t n, bool already_synced = false) {
     }
     tcollect(ctx);
     const DevScalars& s = *ctx->h_scalars;
+    ctx->expiry_host = s.expiry_count;
+    ctx->expiry_known = true;
     ctx->stats.events = n;
     ctx->stats.ae_window = 0;
     ctx->stats.fast = s.stats[1];
@@ -1055,15 +1063,16 @@ int ae_append(tbg_ctx* ctx, uint32_t n_upper, const unsigned int* d_count, Colle
 // fixed upper bound kAeAsyncMax): number the created events, copy and group, place, emit. The two
 // chained scans use their own status words and ticket (ae_g_words[7 ..]), which ae_scatter_tail
 // clears for the next append.
-int ae_launch_appends(tbg_ctx* ctx, uint32_t p, uint32_t epoch) {
+int ae_launch_appends(tbg_ctx* ctx, uint32_t p, uint32_t epoch, bool pending) {
     hipStream_t st = ctx->ae_stream;
     // The one-pass appends first (ae_small_emit); they take the call unless the staging holds an
     // event they cannot, and then every kernel below skips it.
     const bool small = ctx->ae_window_on && ctx->T.acc_rows_used <= kAeWinRowsMax;
     const unsigned int* handled = ctx->ae_stage[p].words + 1;
     if (small) {
-        AeSmall A{ctx->ae_stage[p], epoch, uint32_t(ctx->T.acc_rows_used), ctx->ae_log, ctx->ae_ref,
-                  ctx->ae_words + 4, ctx->ae_small_counts, ctx->ae_small_ts};
+        AeSmall A{ctx->ae_stage[p], epoch, uint32_t(ctx->T.acc_rows_used), pending ? 1u : 0u,
+                  ctx->ae_log, ctx->ae_ref, ctx->ae_words + 4, ctx->ae_small_counts,
+                  ctx->ae_small_ts};
         hipLaunchKernelGGL(ae_small_emit, dim3(kAeSmallWgs), dim3(kAeWinThreads), 0, st, A);
     }
     AeScratch S = ctx->ae_g;
@@ -1139,24 +1148,31 @@ bool ae_async_ok(const tbg_ctx* ctx, uint32_t n) {
 
 // The snapshot job of the next small call (buffer ctx->ae_parity), after the call's stream waited
 // for that buffer's previous graph.
-int ae_snap_job(tbg_ctx* ctx, const Call<tb_transfer_t>& c, AeSnapJob* J) {
+// The staging buffer of the next appends (ctx->ae_parity), once the call's stream waited for its
+// previous appends.
+int ae_stage_acquire(tbg_ctx* ctx) {
     if (int rc = ensure_ae_async(ctx)) return rc;
     const uint32_t p = ctx->ae_parity;
     if (ctx->ae_done_recorded[p]) HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ae_done[p], 0));
-    *J = AeSnapJob{ctx->T, c, ctx->ae_stage[p], false};
+    return 0;
+}
+
+int ae_snap_job(tbg_ctx* ctx, const Call<tb_transfer_t>& c, AeSnapJob* J) {
+    if (int rc = ae_stage_acquire(ctx)) return rc;
+    *J = AeSnapJob{ctx->T, c, ctx->ae_stage[ctx->ae_parity], false};
     return 0;
 }
 
 // The side stream appends staging buffer p (at most n AccountEvents) once the call's stream
 // reaches this point. The log's bound grows as the graph is queued: a call that fails later still
 // leaves a graph that may append.
-int ae_launch_graph(tbg_ctx* ctx, uint32_t n, uint32_t epoch) {
+int ae_launch_graph(tbg_ctx* ctx, uint32_t n, uint32_t epoch, bool pending = false) {
     const uint32_t p = ctx->ae_parity;
     ctx->ae_bound += n;
     ctx->ae_pending = true;
     HIP_TRY(ctx, hipEventRecord(ctx->ae_snap_ready[p], ctx->stream));
     HIP_TRY(ctx, hipStreamWaitEvent(ctx->ae_stream, ctx->ae_snap_ready[p], 0));
-    if (int rc = ae_launch_appends(ctx, p, epoch)) return rc;
+    if (int rc = ae_launch_appends(ctx, p, epoch, pending)) return rc;
     HIP_TRY(ctx, hipEventRecord(ctx->ae_done[p], ctx->ae_stream));
     ctx->ae_done_recorded[p] = true;
     ctx->ae_parity = p ^ 1;
@@ -1256,6 +1272,18 @@ int ae_expiry(tbg_ctx* ctx, const uint64_t* rows, uint64_t m, uint64_t timestamp
                            dim3(kPlanThreads), 0, ctx->stream, ctx->T, rows, uint32_t(m), d_count,
                            timestamp, d_stamps, S, log, refs);
     }, "pulse:account_events");
+}
+
+// A pulse's AccountEvents behind the next call (the side stream, as small create_transfers calls):
+// the expiries staged on the call's stream right after pulse_apply, the appends queued.
+int ae_expiry_async(tbg_ctx* ctx, const uint64_t* rows, uint32_t upper, uint64_t timestamp,
+                    const unsigned int* d_count) {
+    if (int rc = ae_stage_acquire(ctx)) return rc;
+    const uint32_t epoch = ++ctx->epoch;
+    AeExpirySnap J{ctx->T, rows, d_count, timestamp, ctx->ae_stage[ctx->ae_parity], epoch};
+    hipLaunchKernelGGL(ae_expiry_snapshot, dim3(kAeAsyncMax / kBlock), dim3(kBlock), 0, ctx->stream, J);
+    HIP_TRY(ctx, hipGetLastError());
+    return ae_launch_graph(ctx, upper, epoch, true);
 }
 
 // Restores timestamp order of the log (stable) when an append broke it.
@@ -1610,6 +1638,9 @@ tbg_ctx* tbg_open(const tbg_options* options) {
     }
     ok = ok && hip_ok(ctx, hipHostMalloc(reinterpret_cast<void**>(&ctx->h_scalars),
                                          sizeof(DevScalars), kCoherentHost), "hipHostMalloc");
+    ok = ok && hip_ok(ctx, hipHostMalloc(reinterpret_cast<void**>(&ctx->h_pulse), 64, kCoherentHost), "hipHostMalloc") &&
+         hip_ok(ctx, hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->dh_pulse), ctx->h_pulse, 0),
+                "hipHostGetDevicePointer");
     ok = ok && hip_ok(ctx, hipHostMalloc(reinterpret_cast<void**>(&ctx->h_seq), 64, kCoherentHost), "hipHostMalloc") &&
          hip_ok(ctx, hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->dh_seq), ctx->h_seq, 0),
                 "hipHostGetDevicePointer") &&
@@ -1711,6 +1742,7 @@ void tbg_close(tbg_ctx* ctx) {
         if (e) (void)hipEventDestroy(e);
     if (ctx->h_scalars) (void)hipHostFree(ctx->h_scalars);
     if (ctx->h_seq) (void)hipHostFree(ctx->h_seq);
+    if (ctx->h_pulse) (void)hipHostFree(ctx->h_pulse);
     if (ctx->h_results) (void)hipHostFree(ctx->h_results);
     if (ctx->h_batch_ends) (void)hipHostFree(ctx->h_batch_ends);
     if (ctx->h_batch_ts) (void)hipHostFree(ctx->h_batch_ts);
@@ -1740,6 +1772,7 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
     if (n == 0) return 0;
     hipStream_t saved = ctx->stream;
     if (stream) ctx->stream = static_cast<hipStream_t>(stream);
+    ctx->expiry_known = false;  // (end_call learns it again)
     int rc = begin_call(ctx, false);
     Call<tb_transfer_t> c = make_call(ctx, d_events, n, d_batch_ends, d_batch_ts, n_batches,
                                       d_results, ctx->T.tr_rows_used);
@@ -2094,9 +2127,15 @@ struct PulseGather {
 // S.exp / S.rows (pulse.hpp: LDS-sorted runs, pairwise merges keeping the first k); the entries still
 // pending at S.keep; the counters on device. `out`: the counters on the host too (one sync).
 int pulse_select(tbg_ctx* ctx, uint64_t timestamp, uint32_t k, PulseGather* out) {
-    int rc = sync_scalars(ctx);
-    if (rc) return rc;
-    const uint64_t count = std::min<uint64_t>(ctx->h_scalars->expiry_count, ctx->T.expiry_capacity);
+    int rc = 0;
+    // The index length: known on the host since the last call or pulse (else one synchronisation).
+    if (!ctx->expiry_known) {
+        rc = sync_scalars(ctx);
+        if (rc) return rc;
+        ctx->expiry_host = ctx->h_scalars->expiry_count;
+        ctx->expiry_known = true;
+    }
+    const uint64_t count = std::min<uint64_t>(ctx->expiry_host, ctx->T.expiry_capacity);
     rc = ensure_pulse_scratch(ctx, count);
     if (rc) return rc;
     PulseScratch& S = ctx->pulse;
@@ -2155,6 +2194,8 @@ int pulse_finish(tbg_ctx* ctx, uint64_t expired, uint64_t kept, uint64_t pulse_n
     HIP_TRY(ctx, hipMemcpyAsync(&ctx->d_scalars->pulse_next_timestamp, &next_ull, 8,
                                 hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->expiry_host = kept;
+    ctx->expiry_known = true;
     return 0;
 }
 
@@ -2214,10 +2255,12 @@ int64_t tbg_pulse(tbg_ctx* ctx, uint64_t timestamp) {
     const uint32_t k = uint32_t(ctx->opt.pulse_batch_max);
     // The scan stops with buffer_finished after batch_max values (:4969-4999): the first batch_max
     // candidates in index order expire; everything after the host's first sync stays on device.
+    tmark(ctx, "-pulse");
     int rc = pulse_select(ctx, timestamp, k, nullptr);
     if (rc) return rc;
+    tmark(ctx, "pulse:select");
     PulseScratch& S = ctx->pulse;
-    const uint64_t count = std::min<uint64_t>(ctx->h_scalars->expiry_count, ctx->T.expiry_capacity);
+    const uint64_t count = std::min<uint64_t>(ctx->expiry_host, ctx->T.expiry_capacity);
     const uint32_t upper = uint32_t(std::min<uint64_t>(count, k));
     hipLaunchKernelGGL(pulse_settle, dim3(1), dim3(64), 0, ctx->stream, ctx->T, S.exp, S.counters,
                        S.expired, k);
@@ -2228,12 +2271,27 @@ int64_t tbg_pulse(tbg_ctx* ctx, uint64_t timestamp) {
                            S.rows, uint64_t(upper), S.expired);
     }
     HIP_TRY(ctx, hipGetLastError());
-    if (ctx->ae_log && upper) rc = ae_expiry(ctx, S.rows, upper, timestamp, nullptr, S.expired);
+    tmark(ctx, "pulse:apply");
+    ctx->expiry_known = false;
+    // The expiries' AccountEvents behind the next call (the side stream), or here.
+    if (ctx->ae_log && upper) {
+        if (ae_async_ok(ctx, upper) && !getenv("TBG_PULSE_AE_SYNC"))
+            rc = ae_expiry_async(ctx, S.rows, upper, timestamp, S.expired);
+        else
+            rc = ae_expiry(ctx, S.rows, upper, timestamp, nullptr, S.expired);
+    }
     if (rc) return rc;
-    unsigned int expired = 0;
-    HIP_TRY(ctx, hipMemcpyAsync(&expired, S.expired, 4, hipMemcpyDeviceToHost, ctx->stream));
+    // The count expired and the index's new length, written into mapped pinned memory by a kernel
+    // (no copy-engine hand-off), one synchronisation.
+    hipLaunchKernelGGL(pulse_report, dim3(1), dim3(64), 0, ctx->stream, S.expired, S.counters,
+                       ctx->dh_pulse);
+    HIP_TRY(ctx, hipGetLastError());
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    return int64_t(expired);
+    tmark(ctx, "pulse:report");
+    tcollect(ctx);
+    ctx->expiry_host = ctx->h_pulse[1];
+    ctx->expiry_known = true;
+    return int64_t(ctx->h_pulse[0]);
 }
 
 int64_t tbg_pulse_candidates(tbg_ctx* ctx, uint64_t timestamp, uint64_t* expires_at,
@@ -2636,6 +2694,7 @@ std::vector<std::pair<void*, uint64_t>> ckpt_sections(tbg_ctx* ctx, uint64_t acc
 extern "C" {
 
 int64_t tbg_compact(tbg_ctx* ctx) {
+    if (ctx) ctx->expiry_known = false;  // (compaction renumbers and drops index entries)
     if (!ctx) return TBG_EINVAL;
     FAILED_GUARD(ctx);
     Tables& T = ctx->T;

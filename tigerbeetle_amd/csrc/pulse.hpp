@@ -151,6 +151,15 @@ __global__ void pulse_settle(Tables T, const uint64_t* exp, unsigned long long* 
     *expired_out = uint32_t(expired);
 }
 
+// The pulse's outcome for the host: the count expired and the index's new length.
+__global__ void pulse_report(const unsigned int* expired, const unsigned long long* counters,
+                             unsigned long long* out) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    out[0] = *expired;
+    out[1] = counters[0];
+    __threadfence_system();
+}
+
 // The index keeps the entries still pending (the ones just expired are dropped at the next pulse).
 __global__ void pulse_keep_copy(Tables T, const uint64_t* keep, const unsigned long long* counters) {
     const uint64_t n = counters[0];

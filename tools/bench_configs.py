@@ -71,7 +71,7 @@ def line(name, p, n, t_wall, extra):
             "pulse": pulse_line(p), **extra}
 
 
-def run(config, n, batches):
+def run(config, n, batches, profile=True):
     t0 = time.perf_counter()
     p = Pair(account_capacity=1 << 14, transfer_capacity=n + (1 << 12),
              batch_events_max=max(BATCH * batches, 1 << 14), batch_count_max=batches)
@@ -80,7 +80,7 @@ def run(config, n, batches):
         p.seconds = {"gpu": 0.0, "oracle": 0.0}
         p.stats = {k: 0 for k in p.stats}
         p.pulses = []
-        p.lib.tbg_profile(p.g, 1)
+        p.lib.tbg_profile(p.g, 1 if profile else 0)
 
     try:
         drive = configs34.config3 if config == "config3" else configs34.config4
@@ -96,9 +96,14 @@ def main():
     ap.add_argument("--transfers", type=int, default=1_000_000)
     ap.add_argument("--batches", type=int, default=16, help="8189-event batches per commit")
     ap.add_argument("--configs", default="3,4")
+    ap.add_argument("--no-profile", action="store_true",
+                    help="no per-kernel HIP events: the executor's asynchronous paths (the "
+                         "AccountEvents appends behind the next call) run as in production; "
+                         "host-timed rates only")
     args = ap.parse_args()
     for c in args.configs.split(","):
-        print(json.dumps(run("config" + c.strip(), args.transfers, args.batches)), flush=True)
+        print(json.dumps(run("config" + c.strip(), args.transfers, args.batches,
+                             profile=not args.no_profile)), flush=True)
 
 
 if __name__ == "__main__":
