@@ -202,7 +202,9 @@ typedef struct tbg_stats {
     uint64_t fast;         /* applied by the parallel path */
     uint64_t replayed;     /* executed by the ordered replay */
     uint64_t static_fail;  /* failed on checks that depend on no in-call state */
-    uint64_t ae_window;    /* 1: the call's AccountEvents were written in one pass (balance window) */
+    uint64_t ae_window;    /* the call's AccountEvents in one pass: 1 balance-window emit, 2 dense
+                            * emit (general calls, dense key spaces); 0 the general appends or the
+                            * side stream (small calls) */
 } tbg_stats;
 int tbg_last_stats(tbg_ctx* ctx, tbg_stats* out);
 

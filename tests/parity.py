@@ -140,6 +140,7 @@ class Pair:
     def _stats(self):
         s = native.TbgStats()
         self.lib.tbg_last_stats(self.g, ctypes.byref(s))
+        self.last_stats = {k: getattr(s, k) for k in self.stats}
         for k in self.stats:
             self.stats[k] += getattr(s, k)
 

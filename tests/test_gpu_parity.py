@@ -306,8 +306,8 @@ def test_account_events_window(case, monkeypatch):
     no record), interleaved with small calls (side-stream appends) and a pulse, compared with the
     oracle's log byte for byte and through get_change_events. `skew`: 90 % of the touches on 8
     accounts (long per-round lists); `no-window`: TBG_NO_AE_WINDOW (the general appends);
-    `wide-rows`: 13,000 accounts (above the window emit's LDS) take the general appends; calls with
-    pending transfers or wide amounts fall back in every case."""
+    `wide-rows`: 13,000 accounts (above the window emit's LDS) take the general appends; a call with
+    pending transfers takes the dense emit (ae_dense_*)."""
     if case == "no-window":
         monkeypatch.setenv("TBG_NO_AE_WINDOW", "1")
     rng = np.random.default_rng(77)
@@ -338,14 +338,15 @@ def test_account_events_window(case, monkeypatch):
             if call == 2:
                 pend = fail >= 0.995                                    # pending: general appends
                 t["flags"][pend] |= 2
-            w0 = p.stats["ae_window"]
             r = p.create_transfers(t, _split(n, rng, 8189))
             assert (r["status"] == 0xFFFFFFFF).mean() > 0.9
-            took = p.stats["ae_window"] > w0
-            if case in ("no-window", "wide-rows") or call == 2:
-                assert not took
+            path = p.last_stats["ae_window"]  # 1: window emit, 2: dense emit, 0: general
+            if case in ("no-window", "wide-rows"):
+                assert path == 0
+            elif call == 2:
+                assert path == 2  # (pending transfers: the dense emit)
             mid_ts = int(r["timestamp"][n // 2])
-            windows += took
+            windows += path == 1
             # small calls (side stream) and a pulse between the window calls
             s = workload.transfers_uniform(3_000, n_acc, seed=200 + call, id_offset=off)
             off += 3_000
@@ -358,6 +359,58 @@ def test_account_events_window(case, monkeypatch):
         assert len(p.change_events(timestamp_min=mid_ts)) > 0  # (inside the last window call)
         if case in ("window", "skew"):
             assert windows >= 2  # (calls with in-call duplicates of failed ids replay)
+    finally:
+        p.close()
+
+
+@pytest.mark.parametrize("case", ["dense", "closing", "wide", "no-window"])
+def test_account_events_dense(case, monkeypatch):
+    """AccountEvents of general calls in one pass (events.hpp ae_dense_*): calls of > 8,192 events
+    with pending transfers, posts and voids of them (replayed and FAST), linked chains with
+    injected failures and limited accounts, against the oracle's log byte for byte. `closing`:
+    pending transfers that close accounts (a `closed` flip) and `wide`: amounts of 2^19 and more
+    make the call take the general appends; `no-window`: TBG_NO_AE_WINDOW."""
+    if case == "no-window":
+        monkeypatch.setenv("TBG_NO_AE_WINDOW", "1")
+    rng = np.random.default_rng(91)
+    p = Pair(account_capacity=1 << 12, transfer_capacity=1 << 18, batch_events_max=1 << 16,
+             pulse_batch_max=8190)
+    try:
+        acc = workload.accounts(2_000, seed=5)
+        acc["flags"][:8] |= 2
+        p.create_accounts(acc)
+        pending, seen = np.zeros(0, dtype=np.uint64), np.zeros(0, dtype=np.uint64)
+        resolved = np.zeros(0, dtype=np.uint64)
+        offset = 0
+        paths = []
+        for step in range(5):
+            n = 20_000
+            t = workload.transfers_two_phase(n, 2_000, seed=70 + step, id_offset=offset,
+                                             prior_pending_ids=pending, prior_ids=seen,
+                                             prior_resolved_ids=resolved, n_limited=8)
+            offset += n
+            if case == "closing" and step == 3:
+                pend = np.nonzero((t["flags"] & 2) != 0)[0][:20]
+                t["flags"][pend] |= 64  # closing_debit
+            if case == "wide" and step == 3:
+                single = np.nonzero(t["flags"] == 0)[0][:20]
+                t["amount"][single, 0] = 1 << 20
+            r = p.create_transfers(t, _split(n, rng, 8189))
+            paths.append(p.last_stats["ae_window"])
+            made = r["status"] == 0xFFFFFFFF
+            ids = t["id"][:, 0]
+            pending = np.concatenate([pending, ids[made & ((t["flags"] & 2) != 0)]])[-20_000:]
+            resolved = np.concatenate([resolved, t["pending_id"][made & ((t["flags"] & 12) != 0), 0]])
+            seen = np.concatenate([seen, ids])[-20_000:]
+            p.tick(NS_PER_S)
+        if case == "no-window":
+            assert paths == [0] * 5
+        elif case == "dense":
+            assert paths == [2] * 5
+        else:
+            assert paths[3] == 0 and paths.count(2) == 4
+        p.compare_state()
+        assert len(p.change_events()) > 0
     finally:
         p.close()
 

@@ -1330,6 +1330,375 @@ __global__ void __launch_bounds__(kAeWinThreads) ae_small_emit(AeSmall A) {
     A.counts[kAeSmallWgs] = 0;
 }
 
+// ---- AccountEvents of general calls in one pass (dense key spaces) ------------------------------
+//
+// A create_transfers call of any shape -- replayed events, pending transfers, posts and voids --
+// over <= kAeWinRowsMax accounts, when no created event flips `closed` and every amount moved is
+// below 2^19: every created event moves the same pending delta (a pending transfer's amount, or
+// minus the amount a post / void releases) and posted delta (the amount posted) on both of its
+// accounts. The record of created event e carries, for each account A of e,
+//     A's balance after e = A's final balance - A's deltas of the created events after e
+// for all four balances, and A's final row otherwise. The call is cut into slices of
+// kAeDenseSlice events:
+//   ae_dense_stage     per event: its touch (rows, deltas; absent unless created) and the record's
+//                      event words, from the transfer row (and the pending transfer's);
+//                      kFlagAeWide-style refusal in *fail (a flip, an amount >= 2^19)
+//   ae_dense_partials  per slice and balance pair (pending / posted): the slice's deltas per
+//                      account (LDS sums), and its created count
+//   ae_dense_suffix    per pair and account key: the partials summed over the later slices (i64;
+//                      refusal when a sum leaves the i32 range)
+//   ae_dense_emit      per slice: its events' later pending deltas, then posted deltas, one
+//                      round of 1024 events at a time (ae_window_emit's touch lists in LDS), and
+//                      the records from the final rows, four per 1 KB store.
+// The host checks the refusal word between the suffix and the emit; a refused call takes the
+// general appends.
+constexpr uint32_t kAeDenseRounds = 4;
+constexpr uint32_t kAeDenseSlice = kAeDenseRounds * kAeWinThreads;
+
+struct AeTouch {
+    uint32_t dr, cr;  // account rows (kNone32: the event created nothing)
+    uint32_t dpe, dpo;  // pending / posted delta on both accounts (i32 as u32)
+};
+
+struct AeDense {
+    Tables T;
+    Call<tb_transfer_t> c;
+    uint32_t rows, slices;
+    AeTouch* touch;           // per event
+    uint4* ev;                // per event, 5 words: pending id, amount requested, amount,
+                              // (ts lo, ts hi, transfer flags | pending flags << 16, ledger),
+                              // (status, 0, 0, 0)
+    uint32_t* partials;       // [pair][slice][2 * rows]: debit-side then credit-side sums
+    unsigned int* slice_count;  // [slices] created events; [slices] done
+    unsigned long long* slice_ts;  // [2 * slices]
+    unsigned int* fail;       // == epoch: the call takes the general appends
+    uint32_t epoch;
+    tb_account_event_t* log;
+    AeRef* refs;
+    unsigned long long* state;
+};
+
+__global__ void ae_dense_stage(AeDense A) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    const Call<tb_transfer_t>& c = A.c;
+    AeTouch o{kNone32, kNone32, 0, 0};
+    bool bad = false;
+    if (k < c.n && c.results[k].status == TB_STATUS_CREATED) {
+        const Tables& T = A.T;
+        const uint64_t row = c.row_base + k;
+        const tb_transfer_t& t = T.tr_rows[row];
+        const uint16_t f = t.flags;
+        const bool pv = (f & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) != 0;
+        const bool refs_ok = !pv && c.ev_dr && c.ev_cr && !(c.ev_info[k] & kInfoLean);
+        const uint32_t edr = refs_ok ? c.ev_dr[k] : kNone32;
+        const uint32_t ecr = refs_ok ? c.ev_cr[k] : kNone32;
+        const uint64_t dr = edr != kNone32 ? uint64_t(edr) : account_find(T, t.debit_account_id);
+        const uint64_t cr = ecr != kNone32 ? uint64_t(ecr) : account_find(T, t.credit_account_id);
+        const tb_transfer_t* p = pv ? &T.tr_rows[ae_transfer_row(T, t.pending_id)] : nullptr;
+        uint8_t status = TB_PENDING_NONE;
+        u128 dpe = 0, dpo = 0;
+        bool flip = false;
+        if (p) {
+            dpe = u128(0) - U(p->amount);
+            if (f & TB_TRANSFER_POST_PENDING) {
+                status = TB_PENDING_POSTED;
+                dpo = U(t.amount);
+            } else {
+                status = TB_PENDING_VOIDED;
+                flip = (p->flags & (TB_TRANSFER_CLOSING_DEBIT | TB_TRANSFER_CLOSING_CREDIT)) != 0;
+            }
+        } else if (f & TB_TRANSFER_PENDING) {
+            status = TB_PENDING_PENDING;
+            dpe = U(t.amount);
+            flip = (f & (TB_TRANSFER_CLOSING_DEBIT | TB_TRANSFER_CLOSING_CREDIT)) != 0;
+        } else {
+            dpo = U(t.amount);
+        }
+        const u128 mag = (dpe >> 127) ? u128(0) - dpe : dpe;
+        bad = flip || mag >= kAeSmallAmountMax || dpo >= kAeSmallAmountMax;
+        o = AeTouch{uint32_t(dr), uint32_t(cr), uint32_t(uint64_t(dpe)), uint32_t(uint64_t(dpo))};
+        const uint32_t pf = p ? p->flags : 0u;
+        uint4* e = A.ev + uint64_t(k) * 5;
+        e[0] = p ? ae_q128(p->id) : make_uint4(0, 0, 0, 0);
+        e[1] = ae_q128(c.events[k].amount);
+        e[2] = ae_q128(t.amount);
+        e[3] = make_uint4(uint32_t(t.timestamp), uint32_t(t.timestamp >> 32),
+                          uint32_t(f) | (pf << 16), t.ledger);
+        e[4] = make_uint4(status, 0, 0, 0);
+    }
+    if (__any(bad) && (threadIdx.x & 63) == 0) *A.fail = A.epoch;
+    if (k < c.n) A.touch[k] = o;
+}
+
+// Workgroup 2 s + q: slice s, pair q (0 pending, 1 posted).
+__global__ void __launch_bounds__(kAeWinThreads) ae_dense_partials(AeDense A) {
+    __shared__ uint32_t Rd[kAeWinRowsMax];
+    __shared__ uint32_t Rc[kAeWinRowsMax];
+    __shared__ uint32_t wave_cnt[kAeWinThreads / 64];
+    const uint32_t tid = threadIdx.x, s = blockIdx.x >> 1, q = blockIdx.x & 1;
+    for (uint32_t a = tid; a < A.rows; a += kAeWinThreads) {
+        Rd[a] = 0;
+        Rc[a] = 0;
+    }
+    __syncthreads();
+    const uint32_t e0 = s * kAeDenseSlice;
+    const uint32_t e1 = e0 + kAeDenseSlice < A.c.n ? e0 + kAeDenseSlice : A.c.n;
+    uint32_t made = 0;
+    for (uint32_t e = e0 + tid; e < e1; e += kAeWinThreads) {
+        const AeTouch t = A.touch[e];
+        if (t.dr == kNone32) continue;
+        made++;
+        const uint32_t d = q ? t.dpo : t.dpe;
+        if (d) {
+            atomicAdd(&Rd[t.dr], d);
+            atomicAdd(&Rc[t.cr], d);
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) made += __shfl_xor(made, off);
+    if ((tid & 63) == 0) wave_cnt[tid >> 6] = made;
+    __syncthreads();
+    uint32_t* out = A.partials + (uint64_t(q) * A.slices + s) * 2 * A.rows;
+    for (uint32_t a = tid; a < A.rows; a += kAeWinThreads) {
+        out[a] = Rd[a];
+        out[A.rows + a] = Rc[a];
+    }
+    if (q == 0 && tid == 0) {
+        uint32_t total = 0;
+        for (uint32_t w = 0; w < kAeWinThreads / 64; w++) total += wave_cnt[w];
+        A.slice_count[s] = total;
+    }
+}
+
+// One lane per (pair, account key): partials[pair][s][key] = the sum over slices >= s (i64; a sum
+// outside the i32 range refuses the call).
+__global__ void ae_dense_suffix(AeDense A) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t keys = 2 * A.rows;
+    if (t >= 2 * keys) return;
+    const uint32_t q = t / keys, key = t % keys;
+    uint32_t* p = A.partials + uint64_t(q) * A.slices * keys + key;
+    int64_t acc = 0;
+    bool wide = false;
+    for (int64_t s = int64_t(A.slices) - 1; s >= 0; s--) {
+        acc += int32_t(p[uint64_t(s) * keys]);
+        wide |= acc >= (int64_t(1) << 31) || acc < -(int64_t(1) << 31);
+        p[uint64_t(s) * keys] = uint32_t(int32_t(acc));
+    }
+    if (wide) *A.fail = A.epoch;
+}
+
+// The refusal word for the host (mapped pinned memory).
+__global__ void ae_dense_report(const unsigned int* fail, unsigned long long* out) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        *out = *fail;
+        __threadfence_system();
+    }
+}
+
+__device__ inline uint4 ae_sub_i32(uint4 balance, uint32_t d) {
+    return ae_q(ae_u(balance) - u128(int64_t(int32_t(d))));  // (sign-extended: u128 wraps)
+}
+
+// Per round: the touch lists of its events, and each event's later deltas of the pair on both of
+// its accounts (ae_window_emit's procedure); R drops by the round's deltas afterwards.
+struct AeDenseLds {
+    uint32_t Rd[kAeWinRowsMax];
+    uint32_t Rc[kAeWinRowsMax];
+    uint32_t head[kAeWinRowsMax];
+    uint16_t next[2 * kAeWinThreads];
+    uint32_t amt[kAeWinThreads];
+    uint32_t wave_cnt[2][kAeWinThreads / 64];  // (by round parity: a wave may run a round ahead)
+    unsigned long long ts[2];
+};
+__device__ inline void ae_dense_round(AeDenseLds& L, bool valid, uint32_t dr, uint32_t cr,
+                                      uint32_t d, uint32_t later[4]) {
+    const uint32_t tid = threadIdx.x;
+    if (valid) {
+        L.next[2 * tid] = uint16_t(atomicExch(&L.head[dr], 2 * tid));
+        L.next[2 * tid + 1] = uint16_t(atomicExch(&L.head[cr], 2 * tid + 1));
+        L.amt[tid] = d;
+    }
+    __syncthreads();
+    if (valid) {
+#pragma unroll
+        for (int side = 0; side < 2; side++) {
+            const uint32_t acc = side ? cr : dr;
+            uint32_t sd = 0, sc = 0;
+            for (uint32_t nd = L.head[acc]; nd != kAeWinNil;) {
+                if ((nd >> 1) <= tid) {
+                    const uint32_t v = L.amt[nd >> 1];
+                    if (nd & 1) sc += v;
+                    else sd += v;
+                }
+                const uint32_t nx = L.next[nd];
+                nd = nx == 0xFFFFu ? kAeWinNil : nx;
+            }
+            later[2 * side] = L.Rd[acc] - sd;
+            later[2 * side + 1] = L.Rc[acc] - sc;
+        }
+    }
+    __syncthreads();
+    if (valid) {
+        L.head[dr] = kAeWinNil;
+        L.head[cr] = kAeWinNil;
+        atomicSub(&L.Rd[dr], d);
+        atomicSub(&L.Rc[cr], d);
+    }
+    __syncthreads();
+}
+
+__device__ inline void ae_dense_load_r(AeDenseLds& L, const AeDense& A, uint32_t q, uint32_t s) {
+    const uint32_t* suf = A.partials + (uint64_t(q) * A.slices + s) * 2 * A.rows;
+    for (uint32_t a = threadIdx.x; a < A.rows; a += kAeWinThreads) {
+        L.Rd[a] = suf[a];
+        L.Rc[a] = suf[A.rows + a];
+        L.head[a] = kAeWinNil;
+    }
+    __syncthreads();
+}
+
+__global__ void __launch_bounds__(kAeWinThreads) ae_dense_emit(AeDense A) {
+    __shared__ AeDenseLds L;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, s = blockIdx.x;
+    const uint32_t e0 = s * kAeDenseSlice;
+    // created events of the earlier slices
+    uint32_t before = 0;
+    for (uint32_t j = tid; j < s; j += kAeWinThreads) before += A.slice_count[j];
+    for (int off = 32; off > 0; off >>= 1) before += __shfl_xor(before, off);
+    if (lane == 0) L.wave_cnt[0][wv] = before;
+    if (tid == 0) {
+        L.ts[0] = ~0ull;
+        L.ts[1] = 0;
+    }
+    const uint64_t used = A.state[0];
+    __syncthreads();
+    uint64_t pos = used;
+    for (uint32_t j = 0; j < kAeWinThreads / 64; j++) pos += L.wave_cnt[0][j];
+    __syncthreads();
+    AeTouch t[kAeDenseRounds];
+#pragma unroll
+    for (uint32_t r = 0; r < kAeDenseRounds; r++) {
+        const uint32_t e = e0 + r * kAeWinThreads + tid;
+        t[r] = e < A.c.n ? A.touch[e] : AeTouch{kNone32, kNone32, 0, 0};
+    }
+    // pass 1: later pending deltas (kept in registers)
+    uint32_t lpe[kAeDenseRounds][4];
+    ae_dense_load_r(L, A, 0, s);
+#pragma unroll
+    for (uint32_t r = 0; r < kAeDenseRounds; r++) {
+        lpe[r][0] = lpe[r][1] = lpe[r][2] = lpe[r][3] = 0;
+        ae_dense_round(L, t[r].dr != kNone32, t[r].dr, t[r].cr, t[r].dpe, lpe[r]);
+    }
+    // pass 2: later posted deltas, and the records
+    ae_dense_load_r(L, A, 1, s);
+    uint64_t ts_min = ~0ull, ts_max = 0;
+    const uint32_t wd = lane & 15, sub = lane >> 4;
+    const bool credit_half = (wd >= 5 && wd < 10) || wd == 11;
+    const uint32_t kw = wd < 5 ? wd : wd < 10 ? wd - 5 : 7;
+#pragma unroll
+    for (uint32_t r = 0; r < kAeDenseRounds; r++) {
+        const uint32_t e = e0 + r * kAeWinThreads + tid;
+        const bool valid = t[r].dr != kNone32;
+        uint32_t lpo[4] = {0, 0, 0, 0};
+        // (the round's positions: this round's ballot counts before the lists' barriers)
+        const uint64_t bal = __ballot(valid);
+        if (lane == 0) L.wave_cnt[r & 1][wv] = uint32_t(__popcll(bal));
+        ae_dense_round(L, valid, t[r].dr, t[r].cr, t[r].dpo, lpo);
+        uint64_t wave_pos = pos;
+        uint32_t round_total = 0;
+        for (uint32_t j = 0; j < kAeWinThreads / 64; j++) {
+            const uint32_t cj = L.wave_cnt[r & 1][j];
+            wave_pos += j < wv ? cj : 0;
+            round_total += cj;
+        }
+        if (valid) {
+            const uint32_t rank = lane ? __popcll(bal & (~0ull >> (64 - lane))) : 0;
+            ae_nt_store(reinterpret_cast<uint4*>(&A.refs[wave_pos + rank]),
+                        make_uint4(uint32_t(A.c.row_base + e), t[r].dr, t[r].cr, 0));
+            const uint4 w3 = A.ev[uint64_t(e) * 5 + 3];
+            const uint64_t ts = (uint64_t(w3.y) << 32) | w3.x;
+            ts_min = ts < ts_min ? ts : ts_min;
+            ts_max = ts > ts_max ? ts : ts_max;
+        }
+        // The records, four per 1 KB store (lane L: word L % 16 of event lane 4 j + L / 16):
+        //   0-4 / 5-9 the debit / credit account's id and balances less the later deltas,
+        //   10 timestamps, 11 the credit account's timestamp and the flags, 12-14 the event's
+        //   pending id and amounts, 15 ledger and status.
+        for (uint32_t j = 0; j < 16; j++) {
+            if (((bal >> (4 * j)) & 0xF) == 0) continue;  // (wave-uniform)
+            const uint32_t src = 4 * j + sub;
+            const uint32_t s_dr = __shfl(t[r].dr, src), s_cr = __shfl(t[r].cr, src);
+            const uint32_t a0 = __shfl(lpe[r][0], src), a1 = __shfl(lpe[r][1], src);
+            const uint32_t a2 = __shfl(lpe[r][2], src), a3 = __shfl(lpe[r][3], src);
+            const uint32_t b0 = __shfl(lpo[0], src), b1 = __shfl(lpo[1], src);
+            const uint32_t b2 = __shfl(lpo[2], src), b3 = __shfl(lpo[3], src);
+            const bool v = (bal >> src) & 1;
+            const uint32_t es = e0 + r * kAeWinThreads + (tid & ~63u) + src;
+            uint4 qw = make_uint4(0, 0, 0, 0);
+            if (v && (wd < 12 || wd == 15))
+                qw = reinterpret_cast<const uint4*>(&A.T.acc_rows[credit_half ? s_cr : s_dr])[kw];
+            const uint32_t dflags = __shfl(qw.y, lane > 0 ? lane - 1 : 0);
+            if (!v) continue;
+            const uint4* ev = A.ev + uint64_t(es) * 5;
+            uint4 o = qw;
+            if (wd < 10) {
+                // (words 1 / 3: debits / credits pending; 2 / 4: posted; the account's own deltas)
+                const uint32_t le = kw == 1 ? (credit_half ? a2 : a0) : kw == 3 ? (credit_half ? a3 : a1) : 0u;
+                const uint32_t lo = kw == 2 ? (credit_half ? b2 : b0) : kw == 4 ? (credit_half ? b3 : b1) : 0u;
+                if (le) o = ae_sub_i32(o, le);
+                if (lo) o = ae_sub_i32(o, lo);
+            } else if (wd == 10) {
+                const uint4 x = ev[3];
+                o = make_uint4(x.x, x.y, qw.z, qw.w);
+            } else if (wd == 11) {
+                const uint4 x = ev[3];
+                o = make_uint4(qw.z, qw.w, (dflags >> 16) | (qw.y & 0xFFFF0000u), x.z);
+            } else if (wd < 15) {
+                o = ev[wd - 12];
+            } else {
+                o = make_uint4(qw.x, ev[4].x, 0, 0);
+            }
+            const uint64_t at = wave_pos + uint64_t(__popcll(bal & ((1ull << src) - 1)));
+            ae_nt_store(reinterpret_cast<uint4*>(&A.log[at]) + wd, o);
+        }
+        pos += round_total;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t x = __shfl_xor(ts_min, off), y = __shfl_xor(ts_max, off);
+        ts_min = x < ts_min ? x : ts_min;
+        ts_max = y > ts_max ? y : ts_max;
+    }
+    if (lane == 0) {
+        atomicMin(&L.ts[0], ts_min);
+        atomicMax(&L.ts[1], ts_max);
+    }
+    __syncthreads();
+    if (tid != 0) return;
+    A.slice_ts[2 * s] = L.ts[0];
+    A.slice_ts[2 * s + 1] = L.ts[1];
+    __threadfence();
+    if (atomicAdd(&A.slice_count[A.slices], 1u) != gridDim.x - 1) return;
+    __threadfence();
+    const volatile unsigned int* counts = A.slice_count;
+    const volatile unsigned long long* sts = A.slice_ts;
+    uint64_t total = 0, first = 0, last = 0;
+    bool any = false;
+    for (uint32_t j = 0; j < gridDim.x; j++) {
+        const uint32_t cj = counts[j];
+        if (!cj) continue;
+        if (!any) first = sts[2 * j];
+        any = true;
+        last = sts[2 * j + 1];
+        total += cj;
+    }
+    if (total) {
+        if (used && first <= A.state[1]) A.state[2] = 1;
+        if (last > A.state[1]) A.state[1] = last;
+        A.state[0] = used + total;
+    }
+    A.slice_count[A.slices] = 0;
+}
+
 // ---- get_change_events ---------------------------------------------------------------------
 
 // The first log position with timestamp >= lo, and the first with timestamp > hi.

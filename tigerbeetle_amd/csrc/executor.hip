@@ -242,6 +242,13 @@ struct tbg_ctx {
     bool ae_snap_early = false;
     unsigned long long* ae_g_words = nullptr;  // [0] created count; [8..] the graph's scan words
     unsigned int* ae_small_counts = nullptr;   // ae_small_emit: per workgroup, then done
+    // ae_dense_* scratch (allocated at the first general call they take)
+    uint4* ae_dense_touch = nullptr;
+    uint4* ae_dense_ev = nullptr;
+    uint32_t* ae_dense_partials = nullptr;
+    unsigned int* ae_dense_counts = nullptr;
+    unsigned long long* ae_dense_ts = nullptr;
+    unsigned int* ae_dense_fail = nullptr;
     unsigned long long* ae_small_ts = nullptr;
     unsigned long long* flow_debug = nullptr;
 
@@ -1240,6 +1247,64 @@ int ae_window(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
     return 0;
 }
 
+// AccountEvents of a general call in one pass over dense key spaces (events.hpp, ae_dense_*):
+// staged, summed per slice, suffix-summed; the call is refused (1: the general appends take it)
+// when an event flips `closed` or moves 2^19 or more, or a later-delta sum leaves the i32 range.
+constexpr uint32_t kAeDenseMax = 1u << 18;  // events per call
+int ae_dense(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
+    if (!ctx->ae_window_on || ctx->T.acc_rows_used > kAeWinRowsMax || c.n > kAeDenseMax ||
+        c.n > ctx->opt.batch_events_max)
+        return 1;
+    if (!ctx->ae_dense_touch) {
+        const uint64_t cap = std::min<uint64_t>(kAeDenseMax, ctx->opt.batch_events_max);
+        const uint64_t slices = (cap + kAeDenseSlice - 1) / kAeDenseSlice;
+        if (!(dev_alloc(ctx, &ctx->ae_dense_touch, cap, false) &&
+              dev_alloc(ctx, &ctx->ae_dense_ev, 5 * cap, false) &&
+              dev_alloc(ctx, &ctx->ae_dense_partials, 2 * slices * 2 * kAeWinRowsMax, false) &&
+              dev_alloc(ctx, &ctx->ae_dense_counts, slices + 1, true) &&
+              dev_alloc(ctx, &ctx->ae_dense_ts, 2 * slices, false) &&
+              dev_alloc(ctx, &ctx->ae_dense_fail, 1, true)))
+            return TBG_ENOMEM;
+    }
+    if (int rc = ae_join(ctx)) return rc;
+    if (ctx->ae_bound + c.n > ctx->ae_cap) {
+        if (int rc = ae_settle(ctx)) return rc;
+        if (ctx->ae_used + c.n > ctx->ae_cap) return 1;  // (the general path counts exactly)
+    }
+    AeDense A{};
+    A.T = ctx->T;
+    A.c = c;
+    A.rows = uint32_t(ctx->T.acc_rows_used);
+    A.slices = (c.n + kAeDenseSlice - 1) / kAeDenseSlice;
+    A.touch = reinterpret_cast<AeTouch*>(ctx->ae_dense_touch);
+    A.ev = ctx->ae_dense_ev;
+    A.partials = ctx->ae_dense_partials;
+    A.slice_count = ctx->ae_dense_counts;
+    A.slice_ts = ctx->ae_dense_ts;
+    A.fail = ctx->ae_dense_fail;
+    A.epoch = c.epoch;
+    A.log = ctx->ae_log;
+    A.refs = ctx->ae_ref;
+    A.state = ctx->ae_words + 4;
+    tmark(ctx, "-account_events");
+    hipLaunchKernelGGL(ae_dense_stage, dim3(grid_for(c.n)), dim3(kBlock), 0, ctx->stream, A);
+    hipLaunchKernelGGL(ae_dense_partials, dim3(2 * A.slices), dim3(kAeWinThreads), 0, ctx->stream, A);
+    hipLaunchKernelGGL(ae_dense_suffix, dim3((4 * A.rows + kBlock - 1) / kBlock), dim3(kBlock), 0,
+                       ctx->stream, A);
+    hipLaunchKernelGGL(ae_dense_report, dim3(1), dim3(64), 0, ctx->stream, ctx->ae_dense_fail,
+                       ctx->dh_pulse + 2);
+    HIP_TRY(ctx, hipGetLastError());
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (ctx->h_pulse[2] == c.epoch) return 1;
+    hipLaunchKernelGGL(ae_dense_emit, dim3(A.slices), dim3(kAeWinThreads), 0, ctx->stream, A);
+    tmark(ctx, "account_events");
+    HIP_TRY(ctx, hipGetLastError());
+    ctx->stats.ae_window = 2;
+    ctx->ae_bound += c.n;
+    ctx->ae_pending = true;
+    return 0;
+}
+
 // AccountEvents of a create_transfers call: its created events in call order.
 int ae_transfers(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
     if (ctx->ae_snap_early) {  // (stage_out took the snapshot and its graph is queued)
@@ -1249,6 +1314,8 @@ int ae_transfers(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
     const int wrc = ae_window(ctx, c);
     if (wrc <= 0) return wrc;
     if (ae_async_ok(ctx, c.n)) return ae_transfers_async(ctx, c);
+    const int drc = ae_dense(ctx, c);
+    if (drc <= 0) return drc;
     ctx->ae_snap_early = false;
     unsigned int* d_count = reinterpret_cast<unsigned int*>(ctx->ae_words);
     int rc = launch_scan(ctx, c.n, SelectCreated{c.results, ctx->ae_list, d_count});
@@ -1712,7 +1779,9 @@ void tbg_close(tbg_ctx* ctx) {
     }
     if (ctx->ae_pos) (void)hipFree(ctx->ae_pos);
     if (ctx->ae_g_words) (void)hipFree(ctx->ae_g_words);
-    for (void* q : {(void*)ctx->ae_small_counts, (void*)ctx->ae_small_ts})
+    for (void* q : {(void*)ctx->ae_small_counts, (void*)ctx->ae_small_ts, (void*)ctx->ae_dense_touch,
+                    (void*)ctx->ae_dense_ev, (void*)ctx->ae_dense_partials,
+                    (void*)ctx->ae_dense_counts, (void*)ctx->ae_dense_ts, (void*)ctx->ae_dense_fail})
         if (q) (void)hipFree(q);
     free_ae_scratch(ctx->ae_g);
     if (ctx->ae_stream) (void)hipStreamDestroy(ctx->ae_stream);
