@@ -68,11 +68,19 @@ struct AeScratch {
                             // [0] grouped touches, [1] listed accounts, [2] their chunks
     uint32_t* chunk_seg;    // per chunk of a listed account: the account's entry in G.big
     Bal5* chunk_tot;        // per chunk: the sums of its touches
-    unsigned long long* state;  // the log on device: [0] events, [1] last timestamp, [2] unsorted
+    unsigned long long* state;  // the log on device: [0] events, [1] last timestamp, [2] unsorted,
+                                // [3] overflowed (sticky: an append found no room, wrote nothing)
+    uint64_t cap = ~0ull;       // the log's capacity (records)
     // Touch v's event is v >> 1: its log position is pos[v >> 1] (the side stream's appends,
     // whose touches are numbered by call event), or v >> 1 itself when pos is null.
     const uint32_t* pos;
 };
+
+// Room in the log for m more records? Every append checks before it writes (the host's bound is
+// an upper bound; this makes an error of it a reported overflow, never a write past the log).
+__device__ inline bool ae_room(const unsigned long long* state, uint64_t cap, uint64_t m) {
+    return state[3] == 0 && state[0] + m <= cap;
+}
 
 __device__ inline void ae_side(const AeScratch& S, uint32_t i, uint32_t side, u128 pending,
                                u128 posted, uint32_t flip) {
@@ -322,9 +330,11 @@ ae_collect_transfers(Tables T, Call<tb_transfer_t> c, const uint32_t* list,
     group_block_init(B);
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i == 0) S.G.counts[1] = S.G.counts[2] = 0;  // listed accounts / chunks (ae_group_small)
+    const bool room = ae_room(S.state, S.cap, *count);
     log += S.state[0];
     refs += S.state[0];
-    const bool active = i < *count;
+    if (!room && i == 0) S.state[3] = 1;
+    const bool active = room && i < *count;
     uint32_t dr_row = 0, cr_row = 0;
     if (active) ae_collect_transfer(T, c, list[i], i, S, log, refs, &dr_row, &cr_row);
     ae_group_touches(S, B, i, active, dr_row, cr_row, c.n);
@@ -461,14 +471,17 @@ struct PositionsOf8 {
 // One lane per call event: a created event's record and reference to its log position, its
 // touches (2k, 2k + 1) into the grouping.
 __global__ void __launch_bounds__(kPlanThreads)
-ae_copy_group(AeStage st, const uint32_t* pos, AeScratch S, tb_account_event_t* log, AeRef* refs) {
+ae_copy_group(AeStage st, const uint32_t* pos, const unsigned int* m_dev, AeScratch S,
+              tb_account_event_t* log, AeRef* refs) {
     __shared__ GroupBlock B;
     if (S.skip && *S.skip == S.skip_if) return;
     group_block_init(B);
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k == 0) S.G.counts[1] = S.G.counts[2] = 0;  // listed accounts / chunks (ae_group_small)
+    const bool room = ae_room(S.state, S.cap, *m_dev);
+    if (!room && k == 0) S.state[3] = 1;
     const uint64_t used = S.state[0];
-    const bool active = k < kAeAsyncMax && st.created[k];
+    const bool active = room && k < kAeAsyncMax && st.created[k];
     uint32_t dr_row = 0, cr_row = 0;
     if (active) {
         const uint64_t i = used + pos[k];
@@ -514,11 +527,14 @@ ae_collect_expiry(Tables T, const uint64_t* rows, uint32_t m_upper, const unsign
     group_block_init(B);
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i == 0) S.G.counts[1] = S.G.counts[2] = 0;  // listed accounts / chunks (ae_group_small)
+    const bool room = ae_room(S.state, S.cap, m);
+    if (!room && i == 0) S.state[3] = 1;
     log += S.state[0];
     refs += S.state[0];
+    const bool active = room && i < m;
     uint32_t dr_row = 0, cr_row = 0;
-    if (i < m) ae_expiry_one(T, rows[i], m, i, timestamp, stamps, S, log, refs, &dr_row, &cr_row);
-    ae_group_touches(S, B, i, i < m, dr_row, cr_row, m_upper);
+    if (active) ae_expiry_one(T, rows[i], m, i, timestamp, stamps, S, log, refs, &dr_row, &cr_row);
+    ae_group_touches(S, B, i, active, dr_row, cr_row, m_upper);
 }
 
 // Closes an appended block: the log's length and last timestamp advance on device (the host reads
@@ -528,7 +544,7 @@ __global__ void ae_tail(const tb_account_event_t* log, const unsigned int* d_cou
                         unsigned long long* state) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     const uint32_t m = d_count ? *d_count : n;
-    if (m == 0) return;
+    if (m == 0 || state[3]) return;  // (an overflowed append wrote nothing)
     const uint64_t used = state[0];
     const uint64_t first = log[used].timestamp, last = log[used + m - 1].timestamp;
     if (used && first <= state[1]) state[2] = 1;
@@ -851,7 +867,7 @@ __global__ void ae_scatter_tail(GroupPlan G, uint64_t pairs, const tb_account_ev
             const uint32_t m = *d_count;
             const uint64_t used = state[0];
             base[0] = used;
-            if (m) {
+            if (m && !state[3]) {
                 const uint64_t first = log[used].timestamp, last = log[used + m - 1].timestamp;
                 if (used && first <= state[1]) state[2] = 1;
                 state[1] = last > state[1] ? last : state[1];
@@ -946,7 +962,8 @@ struct AeWindow {
     unsigned int* done;                  // finished workgroups (the last one closes the block)
     tb_account_event_t* log;
     AeRef* refs;
-    unsigned long long* state;           // the log on device: [0] length, [1] last ts, [2] unsorted
+    unsigned long long* state;           // the log on device (AeScratch::state)
+    uint64_t cap;
 };
 
 // One lane per (account, side) key in use: partials[w][key] = sum over w' >= w (in place).
@@ -995,10 +1012,20 @@ __global__ void __launch_bounds__(kAeWinThreads) ae_window_emit(AeWindow W) {
     const uint32_t per = window_slice_per(W.n, W.nwg);
     const uint32_t b0 = w * per;
     const uint32_t b1 = b0 + per < W.n ? b0 + per : W.n;
-    // created events of the earlier slices
-    uint32_t before = 0;
-    for (uint32_t j = tid; j < w; j += kAeWinThreads) before += W.slice_count[j];
-    for (int off = 32; off > 0; off >>= 1) before += __shfl_xor(before, off);
+    // created events of the earlier slices; of all (the room in the log: else nothing is written)
+    uint32_t before = 0, all = 0;
+    for (uint32_t j = tid; j < W.nwg; j += kAeWinThreads) {
+        before += j < w ? W.slice_count[j] : 0;
+        all += W.slice_count[j];
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        before += __shfl_xor(before, off);
+        all += __shfl_xor(all, off);
+    }
+    if (!__syncthreads_and(ae_room(W.state, W.cap, all))) {
+        if (tid == 0) W.state[3] = 1;
+        return;
+    }
     if (lane == 0) wave_cnt[wv] = before;
     const uint32_t* suf = W.suffix + uint64_t(w) * W.wkeys;
     for (uint32_t a = tid; a < W.rows; a += kAeWinThreads) {
@@ -1176,9 +1203,10 @@ struct AeSmall {
     uint32_t pending;
     tb_account_event_t* log;
     AeRef* refs;
-    unsigned long long* state;     // the log on device (AeWindow::state)
+    unsigned long long* state;     // the log on device (AeScratch::state)
     unsigned int* counts;          // [kAeSmallWgs] created per workgroup, [kAeSmallWgs] done
     unsigned long long* slice_ts;  // [2 * kAeSmallWgs]
+    uint64_t cap;
 };
 
 // A staged event's amount on both of its accounts (every staged event moves the same amount on
@@ -1198,7 +1226,7 @@ __global__ void __launch_bounds__(kAeWinThreads) ae_small_emit(AeSmall A) {
     __shared__ uint16_t next[2 * kAeWinThreads];
     __shared__ uint32_t amt[kAeWinThreads];
     __shared__ uint32_t wave_cnt[kAeWinThreads / 64];
-    __shared__ uint32_t before_lds;
+    __shared__ uint32_t before_lds, all_lds;
     __shared__ unsigned long long ts_lds[2];
     if (A.st.words[0] == A.epoch) return;  // (an event the general appends take)
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, w = blockIdx.x;
@@ -1210,6 +1238,7 @@ __global__ void __launch_bounds__(kAeWinThreads) ae_small_emit(AeSmall A) {
     }
     if (tid == 0) {
         before_lds = 0;
+        all_lds = 0;
         ts_lds[0] = ~0ull;
         ts_lds[1] = 0;
     }
@@ -1217,9 +1246,10 @@ __global__ void __launch_bounds__(kAeWinThreads) ae_small_emit(AeSmall A) {
     // R: the posted deltas of the staged events from this workgroup's first one on; the created
     // events before it (the block's positions).
     const uint32_t e0 = w * kAeWinThreads;
-    uint32_t before = 0;
+    uint32_t before = 0, all = 0;
     for (uint32_t e = tid; e < kAeAsyncMax; e += kAeWinThreads) {
         if (!A.st.created[e]) continue;
+        all++;
         if (e < e0) {
             before++;
             continue;
@@ -1229,8 +1259,17 @@ __global__ void __launch_bounds__(kAeWinThreads) ae_small_emit(AeSmall A) {
         atomicAdd(&Rd[r.dr_row], a);
         atomicAdd(&Rc[r.cr_row], a);
     }
-    for (int off = 32; off > 0; off >>= 1) before += __shfl_xor(before, off);
+    for (int off = 32; off > 0; off >>= 1) {
+        before += __shfl_xor(before, off);
+        all += __shfl_xor(all, off);
+    }
     if (lane == 0 && before) atomicAdd(&before_lds, before);
+    if (lane == 0 && all) atomicAdd(&all_lds, all);
+    __syncthreads();
+    if (!ae_room(A.state, A.cap, all_lds)) {  // (uniform: the same counts in every workgroup)
+        if (tid == 0) A.state[3] = 1;
+        return;
+    }
     // this workgroup's round: its events' touches on the accounts' lists
     const uint32_t e = e0 + tid;
     const bool valid = A.st.created[e] != 0;
@@ -1311,7 +1350,7 @@ __global__ void __launch_bounds__(kAeWinThreads) ae_small_emit(AeSmall A) {
     __threadfence();
     const volatile unsigned int* counts = A.counts;
     const volatile unsigned long long* sts = A.slice_ts;
-    uint64_t all = 0, first = 0, last = 0;
+    uint64_t appended = 0, first = 0, last = 0;
     bool any = false;
     for (uint32_t j = 0; j < gridDim.x; j++) {
         const uint32_t cj = counts[j];
@@ -1319,13 +1358,13 @@ __global__ void __launch_bounds__(kAeWinThreads) ae_small_emit(AeSmall A) {
         if (!any) first = sts[2 * j];
         any = true;
         last = sts[2 * j + 1];
-        all += cj;
+        appended += cj;
     }
     const uint64_t used = A.state[0];
-    if (all) {
+    if (appended) {
         if (used && first <= A.state[1]) A.state[2] = 1;
         if (last > A.state[1]) A.state[1] = last;
-        A.state[0] = used + all;
+        A.state[0] = used + appended;
     }
     A.counts[kAeSmallWgs] = 0;
 }
@@ -1376,6 +1415,7 @@ struct AeDense {
     tb_account_event_t* log;
     AeRef* refs;
     unsigned long long* state;
+    uint64_t cap;
 };
 
 __global__ void ae_dense_stage(AeDense A) {
@@ -1561,10 +1601,20 @@ __global__ void __launch_bounds__(kAeWinThreads) ae_dense_emit(AeDense A) {
     __shared__ AeDenseLds L;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, s = blockIdx.x;
     const uint32_t e0 = s * kAeDenseSlice;
-    // created events of the earlier slices
-    uint32_t before = 0;
-    for (uint32_t j = tid; j < s; j += kAeWinThreads) before += A.slice_count[j];
-    for (int off = 32; off > 0; off >>= 1) before += __shfl_xor(before, off);
+    // created events of the earlier slices; of all (the room in the log: else nothing is written)
+    uint32_t before = 0, all = 0;
+    for (uint32_t j = tid; j < A.slices; j += kAeWinThreads) {
+        before += j < s ? A.slice_count[j] : 0;
+        all += A.slice_count[j];
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        before += __shfl_xor(before, off);
+        all += __shfl_xor(all, off);
+    }
+    if (!__syncthreads_and(ae_room(A.state, A.cap, all))) {
+        if (tid == 0) A.state[3] = 1;
+        return;
+    }
     if (lane == 0) L.wave_cnt[0][wv] = before;
     if (tid == 0) {
         L.ts[0] = ~0ull;

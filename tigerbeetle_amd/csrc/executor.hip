@@ -993,9 +993,14 @@ int ae_join(tbg_ctx* ctx) {
 int ae_settle(tbg_ctx* ctx) {
     if (int rc = ae_join(ctx)) return rc;
     if (!ctx->ae_pending) return 0;
-    unsigned long long st[3] = {0, 0, 0};
-    HIP_TRY(ctx, hipMemcpyAsync(st, ctx->ae_words + 4, 24, hipMemcpyDeviceToHost, ctx->stream));
+    unsigned long long st[4] = {0, 0, 0, 0};
+    HIP_TRY(ctx, hipMemcpyAsync(st, ctx->ae_words + 4, 32, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (st[3]) {  // (an append found no room on device and wrote nothing: the bound was wrong)
+        ctx->error = "account_events capacity exceeded (device check)";
+        ctx->failed = true;
+        return TBG_ENOSPC;
+    }
     ctx->ae_used = ctx->ae_bound = st[0];
     ctx->ae_last_ts = st[1];
     ctx->ae_sorted = st[2] == 0;
@@ -1042,6 +1047,7 @@ int ae_append(tbg_ctx* ctx, uint32_t n_upper, const unsigned int* d_count, Colle
     if (rc) return rc;
     AeScratch& S = ctx->ae;
     S.state = ctx->ae_words + 4;
+    S.cap = ctx->ae_cap;
     const uint64_t slots = S.G.hmask + 1;
     tb_account_event_t* log = ctx->ae_log;  // (+ the device length, read by each kernel)
     tmark(ctx, "-account_events");
@@ -1079,11 +1085,12 @@ int ae_launch_appends(tbg_ctx* ctx, uint32_t p, uint32_t epoch, bool pending) {
     if (small) {
         AeSmall A{ctx->ae_stage[p], epoch, uint32_t(ctx->T.acc_rows_used), pending ? 1u : 0u,
                   ctx->ae_log, ctx->ae_ref, ctx->ae_words + 4, ctx->ae_small_counts,
-                  ctx->ae_small_ts};
+                  ctx->ae_small_ts, ctx->ae_cap};
         hipLaunchKernelGGL(ae_small_emit, dim3(kAeSmallWgs), dim3(kAeWinThreads), 0, st, A);
     }
     AeScratch S = ctx->ae_g;
     S.state = ctx->ae_words + 4;
+    S.cap = ctx->ae_cap;
     S.pos = nullptr;
     S.skip = small ? handled : nullptr;
     S.skip_if = epoch;
@@ -1101,7 +1108,7 @@ int ae_launch_appends(tbg_ctx* ctx, uint32_t p, uint32_t epoch, bool pending) {
                        uint64_t(kAeAsyncMax), PositionsOf8{ctx->ae_stage[p].created, ctx->ae_pos, d_count},
                        ScanState{scan_words, ticket, 0, 1, S.skip, epoch});
     hipLaunchKernelGGL(ae_copy_group, dim3((kAeAsyncMax + kPlanThreads - 1) / kPlanThreads),
-                       dim3(kPlanThreads), 0, st, ctx->ae_stage[p], ctx->ae_pos, S, ctx->ae_log,
+                       dim3(kPlanThreads), 0, st, ctx->ae_stage[p], ctx->ae_pos, d_count, S, ctx->ae_log,
                        ctx->ae_ref);
     hipLaunchKernelGGL(chained_scan<ExclusiveSumU32>, dim3(tiles2), dim3(kScanThreads), 0, st,
                        slots, ExclusiveSumU32{S.G.hcnt, S.G.hoff, &S.G.counts[0]},
@@ -1234,6 +1241,7 @@ int ae_window(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
     W.log = ctx->ae_log;
     W.refs = ctx->ae_ref;
     W.state = ctx->ae_words + 4;
+    W.cap = ctx->ae_cap;
     tmark(ctx, "-account_events");
     hipLaunchKernelGGL(ae_window_suffix, dim3((2 * W.rows + kBlock - 1) / kBlock), dim3(kBlock), 0,
                        ctx->stream, W);
@@ -1286,6 +1294,7 @@ int ae_dense(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
     A.log = ctx->ae_log;
     A.refs = ctx->ae_ref;
     A.state = ctx->ae_words + 4;
+    A.cap = ctx->ae_cap;
     tmark(ctx, "-account_events");
     hipLaunchKernelGGL(ae_dense_stage, dim3(grid_for(c.n)), dim3(kBlock), 0, ctx->stream, A);
     hipLaunchKernelGGL(ae_dense_partials, dim3(2 * A.slices), dim3(kAeWinThreads), 0, ctx->stream, A);
