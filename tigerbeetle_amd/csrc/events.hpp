@@ -1408,7 +1408,8 @@ struct AeDense {
                               // (ts lo, ts hi, transfer flags | pending flags << 16, ledger),
                               // (status, 0, 0, 0)
     uint32_t* partials;       // [pair][slice][2 * rows]: debit-side then credit-side sums
-    unsigned int* slice_count;  // [slices] created events; [slices] done
+    unsigned int* slice_count;  // [slices] created events
+    unsigned int* done;         // finished emit workgroups (a word of its own: zero between calls)
     unsigned long long* slice_ts;  // [2 * slices]
     unsigned int* fail;       // == epoch: the call takes the general appends
     uint32_t epoch;
@@ -1727,7 +1728,7 @@ __global__ void __launch_bounds__(kAeWinThreads) ae_dense_emit(AeDense A) {
     A.slice_ts[2 * s] = L.ts[0];
     A.slice_ts[2 * s + 1] = L.ts[1];
     __threadfence();
-    if (atomicAdd(&A.slice_count[A.slices], 1u) != gridDim.x - 1) return;
+    if (atomicAdd(A.done, 1u) != gridDim.x - 1) return;
     __threadfence();
     const volatile unsigned int* counts = A.slice_count;
     const volatile unsigned long long* sts = A.slice_ts;
@@ -1746,7 +1747,7 @@ __global__ void __launch_bounds__(kAeWinThreads) ae_dense_emit(AeDense A) {
         if (last > A.state[1]) A.state[1] = last;
         A.state[0] = used + total;
     }
-    A.slice_count[A.slices] = 0;
+    *A.done = 0;
 }
 
 // ---- get_change_events ---------------------------------------------------------------------

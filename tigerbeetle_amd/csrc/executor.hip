@@ -1288,6 +1288,8 @@ int ae_dense(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
     A.ev = ctx->ae_dense_ev;
     A.partials = ctx->ae_dense_partials;
     A.slice_count = ctx->ae_dense_counts;
+    A.done = ctx->ae_dense_counts + (std::min<uint64_t>(kAeDenseMax, ctx->opt.batch_events_max) +
+                                     kAeDenseSlice - 1) / kAeDenseSlice;
     A.slice_ts = ctx->ae_dense_ts;
     A.fail = ctx->ae_dense_fail;
     A.epoch = c.epoch;
