@@ -130,6 +130,22 @@ int64_t tbg_pulse_cut(tbg_ctx* ctx, uint64_t timestamp, uint64_t cut_expires_at,
  * (read only by imported events' must_not_regress checks) to the maxima over every shard. */
 int tbg_raise_key_max(tbg_ctx* ctx, uint64_t accounts_key_max, uint64_t transfers_key_max);
 
+/* Sharded pulse_next_timestamp (one executor per ledger shard). A post/void of a pending transfer
+ * with a timeout resets pulse_next_timestamp when it equals the transfer's expiry
+ * (post_or_void_pending_transfer :4227-4229): a comparison against the value over *all* shards at
+ * that point of the call. With tbg_set_pnt_sharded(ctx, 1) every create_transfers call records
+ * each update at its event -- min(expires_at) of a pending transfer with a timeout
+ * (create_transfer :3975-3982) or a reset-if-equal of a post/void -- applies the mins only, and
+ * tbg_pnt_ops returns the last call's updates as (event timestamp, op) pairs in call order (op:
+ * expires_at, with bit 63 set for a reset) and the value at the call's start. The caller merges
+ * the shards' updates by timestamp, replays them from the minimum of the starts and, when a reset
+ * fires, sets every shard's value to timestamp_min (tbg_set_pulse_next_timestamp). Returns the
+ * count (at most `max` copied) or a negative error. */
+int tbg_set_pnt_sharded(tbg_ctx* ctx, int on);
+int64_t tbg_pnt_ops(tbg_ctx* ctx, uint64_t* timestamps, uint64_t* ops, uint64_t max,
+                    uint64_t* start);
+int tbg_set_pulse_next_timestamp(tbg_ctx* ctx, uint64_t value);
+
 /* Found objects only, in request order; returns the count written. */
 int64_t tbg_lookup_accounts(tbg_ctx* ctx, const tb_uint128_t* ids, uint32_t n, tb_account_t* out);
 int64_t tbg_lookup_transfers(tbg_ctx* ctx, const tb_uint128_t* ids, uint32_t n,

@@ -12,8 +12,8 @@
  * shard's state: non-imported events whose id is new to every shard and unique in the call and
  * whose two accounts are known and on one shard; events whose id already exists (decided by the
  * id's holder, create_transfer_exists :3988-4051, before any account lookup); post/voids, on the
- * shard of their pending transfer (in the directory or created earlier in the call) when it has
- * no timeout; and linked chains whose events all go to one shard and end within their batch. Any
+ * shard of their pending transfer (in the directory or created earlier in the call); and linked
+ * chains whose events all go to one shard and end within their batch. Any
  * other event is a *hazard*: the call is left to the exact router (tigerbeetle_amd/shard.py,
  * LedgerRouter), which reads the same directories through tbr_account_shards /
  * tbr_transfer_shards and records its outcome with tbr_record_*.
@@ -49,7 +49,10 @@ int64_t tbr_transfer_shards(tbr_ctx* ctx, const tb_uint128_t* ids, uint32_t n, i
  * shard order at d_out_events / d_out_timestamps (event i of shard s at offset
  * sum(shard_counts[< s]) + i), d_out_positions = each slice event's position in the call,
  * shard_counts[shards] on the host; the call's ids are held for it until tbr_settle_device.
- * Returns 1 when the call holds a hazard (nothing routed, nothing held); < 0 on error. */
+ * Returns 2 instead of 0 when the call posts or voids: its shards' pulse_next_timestamp updates
+ * are then resolved across shards after it (tbg_pnt_ops, post_or_void_pending_transfer
+ * :4227-4229). Returns 1 when the call holds a hazard (nothing routed, nothing held); < 0 on
+ * error. */
 int64_t tbr_route_device(tbr_ctx* ctx, const tb_transfer_t* d_events, uint32_t n,
                          const uint32_t* d_batch_ends, const uint64_t* d_batch_timestamps,
                          uint32_t n_batches, tb_transfer_t* d_out_events,

@@ -173,6 +173,15 @@ struct tbo_ctx {
     uint32_t pulse_batch_max;
     uint64_t commit_timestamp;
 
+    /* Sharded pulse_next_timestamp (tbo_pnt_sharded): every update is logged with its event's
+     * timestamp -- `min` updates applied, reset-if-equal ones only logged (the reset compares
+     * against the value across all shards, which the caller resolves). */
+    int pnt_sharded;
+    uint64_t* pnt_ts;
+    uint64_t* pnt_op;
+    uint64_t n_pnt, cap_pnt;
+    uint64_t pnt_start; /* pulse_next_timestamp before the logged updates */
+
     /* The account_events groove (state_machine.zig:104-220), in insertion order. */
     tb_account_event_t* events;
     uint64_t n_events, cap_events;
@@ -184,6 +193,36 @@ struct tbo_ctx {
     undo_t* undo;
     uint64_t n_undo, cap_undo;
 };
+
+/* Test instrumentation for sharded calls (not a reference mechanism): the pulse_next_timestamp
+ * updates of post_or_void_pending_transfer (:4227-4229) and create_transfer (:3975-3982). */
+#define TBO_PNT_RESET (1ull << 63)
+static void pnt_log(tbo_ctx* c, uint64_t ts, uint64_t op) {
+    if (c->n_pnt == 0) c->pnt_start = c->pulse_next_timestamp;
+    if (c->n_pnt == c->cap_pnt) {
+        c->cap_pnt = c->cap_pnt ? 2 * c->cap_pnt : 1024;
+        c->pnt_ts = (uint64_t*)xrealloc(c->pnt_ts, c->cap_pnt * sizeof(uint64_t));
+        c->pnt_op = (uint64_t*)xrealloc(c->pnt_op, c->cap_pnt * sizeof(uint64_t));
+    }
+    c->pnt_ts[c->n_pnt] = ts;
+    c->pnt_op[c->n_pnt] = op;
+    c->n_pnt++;
+}
+
+void tbo_pnt_sharded(tbo_ctx* c, int on) { c->pnt_sharded = on; }
+
+uint64_t tbo_pnt_ops(tbo_ctx* c, uint64_t* ts, uint64_t* ops, uint64_t* start) {
+    const uint64_t n = c->n_pnt;
+    if (start) *start = n ? c->pnt_start : c->pulse_next_timestamp;
+    for (uint64_t i = 0; i < n; i++) {
+        if (ts) ts[i] = c->pnt_ts[i];
+        if (ops) ops[i] = c->pnt_op[i];
+    }
+    if (ts || ops) c->n_pnt = 0;
+    return n;
+}
+
+void tbo_set_pulse_next_timestamp(tbo_ctx* c, uint64_t v) { c->pulse_next_timestamp = v; }
 
 tbo_ctx* tbo_open(uint32_t pulse_batch_max, uint64_t pulse_next_timestamp_init) {
     tbo_ctx* c = (tbo_ctx*)calloc(1, sizeof(tbo_ctx));
@@ -204,6 +243,8 @@ void tbo_close(tbo_ctx* c) {
     free(c->expiry);
     free(c->undo);
     free(c->events);
+    free(c->pnt_ts);
+    free(c->pnt_op);
     map_free(&c->account_by_id);
     map_free(&c->account_by_ts);
     map_free(&c->transfer_by_id);
@@ -610,7 +651,8 @@ static uint32_t post_or_void_pending_transfer(tbo_ctx* c, uint64_t timestamp_eve
 
     if (has_expiry) {
         /* The expires_at index entry is removed (status below); reset the pulse flag. */
-        if (c->pulse_next_timestamp == expires_at) c->pulse_next_timestamp = TB_TIMESTAMP_MIN;
+        if (c->pnt_sharded) pnt_log(c, timestamp_actual, expires_at | TBO_PNT_RESET);
+        else if (c->pulse_next_timestamp == expires_at) c->pulse_next_timestamp = TB_TIMESTAMP_MIN;
     }
     update_pending_status(c, pi, (f & TB_TRANSFER_POST_PENDING) ? TB_PENDING_POSTED
                                                                  : TB_PENDING_VOIDED);
@@ -760,6 +802,7 @@ static uint32_t create_transfer(tbo_ctx* c, uint64_t timestamp_event, const tb_t
 
     if (t->timeout > 0) {
         uint64_t expires_at = timestamp_actual + (uint64_t)t->timeout * TB_NS_PER_S;
+        if (c->pnt_sharded) pnt_log(c, timestamp_actual, expires_at);
         if (expires_at < c->pulse_next_timestamp) c->pulse_next_timestamp = expires_at;
     }
     c->commit_timestamp = timestamp_actual;

@@ -91,6 +91,16 @@ int64_t tbo_query_accounts(const tbo_ctx* ctx, const tb_query_filter_t* filter,
 int64_t tbo_query_transfers(const tbo_ctx* ctx, const tb_query_filter_t* filter,
                             uint32_t limit_max, tb_transfer_t* out);
 
+/* Sharded pulse_next_timestamp (test instrumentation for the ledger shards, shard.py): with
+ * `on`, every update of create_transfer (:3975-3982, `min`, applied) and of
+ * post_or_void_pending_transfer (:4227-4229, reset-if-equal: logged, not applied) is logged with
+ * its event's timestamp; tbo_pnt_ops returns the log since the last read (count; with ts / ops
+ * non-null it copies and clears) and the value before its first entry; the caller resolves the
+ * resets across shards and sets the value. Op encoding: expires_at, | 1 << 63 for a reset. */
+void tbo_pnt_sharded(tbo_ctx* ctx, int on);
+uint64_t tbo_pnt_ops(tbo_ctx* ctx, uint64_t* ts, uint64_t* ops, uint64_t* start);
+void tbo_set_pulse_next_timestamp(tbo_ctx* ctx, uint64_t value);
+
 /* Binds this oracle as a tb_executor (tb_state_machine.h) for the StateMachine mirror. */
 void tbo_executor_fill(tbo_ctx* ctx, tb_executor* ex);
 

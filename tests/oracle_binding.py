@@ -31,6 +31,9 @@ _SIGS = [
     ("tbo_dump_pending_status", ctypes.c_uint64, [vp, vp]),
     ("tbo_dump_account_events", ctypes.c_uint64, [vp, vp]),
     ("tbo_raise_key_max", None, [vp, ctypes.c_uint64, ctypes.c_uint64]),
+    ("tbo_pnt_sharded", None, [vp, ctypes.c_int]),
+    ("tbo_pnt_ops", ctypes.c_uint64, [vp, vp, vp, ctypes.POINTER(ctypes.c_uint64)]),
+    ("tbo_set_pulse_next_timestamp", None, [vp, ctypes.c_uint64]),
     ("tbo_get_change_events", ctypes.c_int64, [vp, vp, ctypes.c_uint32, vp]),
     ("tbo_get_account_transfers", ctypes.c_int64, [vp, vp, ctypes.c_uint32, vp]),
     ("tbo_get_account_balances", ctypes.c_int64, [vp, vp, ctypes.c_uint32, vp]),

@@ -5,9 +5,11 @@ union of the shards' final tables against the oracle's.
 Two ranks on the box's one GPU, over gloo (host staging; RCCL needs one GPU per rank): rank 0
 holds the client calls in HBM and the device router; each rank owns two of four ledgers. The
 calls take the device path -- interleaved ledgers and fresh ids; a linked chain on one shard,
-resubmitted ids (on their holders) and posts / voids of untimed pending transfers (on their
-pending transfer's shard) -- except the one the device router must hand to the exact host router
-(a transfer between two shards' accounts); pending transfers expire in sharded pulses. Every shard
+resubmitted ids (on their holders), posts / voids of pending transfers (on their pending
+transfer's shard), with and without a timeout: a post/void of the earliest-expiring one resets
+pulse_next_timestamp, resolved across the shards after the call -- except the one the device
+router must hand to the exact host router (a transfer between two shards' accounts); pending
+transfers expire in sharded pulses. Every shard
 records AccountEvents, and the union of the shards' logs must be the oracle's (the ADVICE item:
 the appends a device call leaves on the executor's stream read the call's buffers).
 """
@@ -91,6 +93,21 @@ def _calls(seed):
         haz["code"][e] = 0
         haz["timeout"][e] = 0
     ops.append(("fast", haz, [3_000]))
+    # posts / voids of pending transfers with a timeout, the earliest-expiring one first (its
+    # expiry is pulse_next_timestamp: the reset fires), among new pending transfers and transfers
+    timed_ids = fast1["id"][(fast1["flags"] == 2) & (fast1["timeout"] == 1), 0][:40]
+    tpv = uniform(4_000, pending_frac=0.2)
+    for j, pid in enumerate(timed_ids):
+        e = 50 + 37 * j
+        tpv["pending_id"][e, 0] = pid
+        tpv["flags"][e] = 8 if j % 3 == 0 else 4
+        tpv["amount"][e] = [0, 0] if j % 3 == 0 else [2**64 - 1, 2**64 - 1]
+        tpv["debit_account_id"][e] = 0
+        tpv["credit_account_id"][e] = 0
+        tpv["ledger"][e] = 0
+        tpv["code"][e] = 0
+        tpv["timeout"][e] = 0
+    ops.append(("fast", tpv, [4_000]))
     ops.append(("tick", 2_000_000_000))
     ops.append(("fast", uniform(20_000), [8189, 20_000 - 8189]))
     return ops
@@ -177,7 +194,7 @@ def _rank(rank, world, port, seed, q):
             want = ref.dump_account_events()
             assert len(got) > 50_000 and got.tobytes() == want.tobytes(), \
                 f"account events differ ({len(got)} vs {len(want)})"
-            assert rs.fast_calls == 3 and rs.host_calls == 1, (rs.fast_calls, rs.host_calls)
+            assert rs.fast_calls == 4 and rs.host_calls == 1, (rs.fast_calls, rs.host_calls)
             assert pulses > 0
         rs.close()
         dist.barrier()

@@ -62,6 +62,9 @@ class OracleShard:
 
     def create_transfers(self, events, lens, batch_ts):
         ev = np.ascontiguousarray(events, dtype=TRANSFER_DTYPE)
+        n = int(self.lib.tbo_pnt_ops(self.o, None, None, None))  # (the log starts with this call)
+        z = np.zeros(max(n, 1), dtype=np.uint64)
+        self.lib.tbo_pnt_ops(self.o, _ptr(z), _ptr(z.copy()), None)
         return self._run(self.lib.tbo_create_transfers, ev, lens, batch_ts)
 
     def pulse(self, timestamp):
@@ -82,6 +85,21 @@ class OracleShard:
 
     def pulse_next_timestamp(self):
         return int(self.lib.tbo_pulse_next_timestamp(self.o))
+
+    def set_pnt_sharded(self, on):
+        self.lib.tbo_pnt_sharded(self.o, 1 if on else 0)
+
+    def pnt_ops(self):
+        """The updates recorded since the last create_transfers call began: (start, pairs)."""
+        start = ctypes.c_uint64()
+        n = int(self.lib.tbo_pnt_ops(self.o, None, None, ctypes.byref(start)))
+        ts = np.zeros(max(n, 1), dtype=np.uint64)
+        ops = np.zeros(max(n, 1), dtype=np.uint64)
+        self.lib.tbo_pnt_ops(self.o, _ptr(ts), _ptr(ops), ctypes.byref(start))
+        return int(start.value), list(zip(ts[:n].tolist(), ops[:n].tolist()))
+
+    def set_pulse_next_timestamp(self, value):
+        self.lib.tbo_set_pulse_next_timestamp(self.o, int(value))
 
     def raise_key_max(self, accounts_key_max, transfers_key_max):
         self.lib.tbo_raise_key_max(self.o, accounts_key_max, transfers_key_max)
@@ -112,11 +130,11 @@ def _split(rng, n, max_batch):
     return lens
 
 
-def scenario(seed, calls=8, n_acc=48):
-    """A call sequence the router can shard: transfers and chains stay within one ledger and
-    post/void target pending transfers created without a timeout; with resubmitted ids, failing
-    chains, limit failures, missing accounts, chains cut by batch ends and pending transfers that
-    expire in pulses."""
+def scenario(seed, calls=8, n_acc=48, timed_post_void=True):
+    """A call sequence the router can shard: transfers and chains stay within one ledger; with
+    resubmitted ids, failing chains, limit failures, missing accounts, chains cut by batch ends,
+    pending transfers that expire in pulses, and post/voids of pending transfers -- with a timeout
+    too (`timed_post_void`: their reset of pulse_next_timestamp is resolved across shards)."""
     rng = np.random.default_rng(seed)
     acc = workload.accounts(n_acc, seed=seed)
     ids = np.arange(1, n_acc + 1)
@@ -168,6 +186,8 @@ def scenario(seed, calls=8, n_acc=48):
                         t["flags"][e] = 2
                         if rng.random() < 0.5:
                             t["timeout"][e] = int(rng.integers(1, 3))
+                            if timed_post_void:
+                                untimed.append(tid)
                         else:
                             untimed.append(tid)
                 if j < span - 1:
@@ -356,14 +376,26 @@ def test_router_routes_and_refuses():
     timed = _transfers([dict(id=17, debit_account_id=1, credit_account_id=2, amount=5, ledger=1,
                              code=1, flags=2, timeout=1)])
     r.commit(r.plan_transfers(timed, [1], [70]), timed, _created(1, 70))
-    with pytest.raises(shard.RouteError, match="timeout"):
-        r.plan_transfers(_transfers([dict(id=18, pending_id=17, flags=4, amount=(1 << 128) - 1)]),
-                         [1], [80])
+    # a post/void of a pending transfer with a timeout goes to its shard (its reset of
+    # pulse_next_timestamp is resolved across shards after the call)
+    pv = r.plan_transfers(_transfers([dict(id=18, pending_id=17, flags=4, amount=(1 << 128) - 1)]),
+                          [1], [80])
+    assert pv.shard_of.tolist() == [0] and pv.post_void
     untimed = _transfers([dict(id=19, debit_account_id=3, credit_account_id=4, amount=5,
                                ledger=3, code=1, flags=2)])
     r.commit(r.plan_transfers(untimed, [1], [90]), untimed, _created(1, 90))
     post = _transfers([dict(id=20, pending_id=19, flags=4, amount=(1 << 128) - 1)])
     assert r.plan_transfers(post, [1], [100]).shard_of.tolist() == [1]
+
+
+def test_pnt_resets_fire():
+    """The reset-if-equal of a post/void (:4227-4229) fires against the value over all shards in
+    call order: a `min` recorded by another shard before it can prevent it."""
+    R = shard.PNT_RESET
+    assert shard.pnt_resets_fire([100, 50], [[], [(10, 50 | R)]])
+    assert not shard.pnt_resets_fire([100, 60], [[(5, 40)], [(10, 60 | R)]])
+    assert not shard.pnt_resets_fire([100, 60], [[(15, 40)], [(10, 50 | R)]])
+    assert shard.pnt_resets_fire([100, 100], [[(5, 40)], [(10, 40 | R)]])
 
 
 @pytest.mark.parametrize("seed", [0, 1, 2])

@@ -170,6 +170,9 @@ struct tbg_ctx {
     uint32_t* slow_list = nullptr;
     uint32_t* fix_slots = nullptr;  // tr_commit's fixed failures' id slots (Call::fix_slots)
     uint64_t* pnt_call = nullptr;           // pulse_next_timestamp updates per event (post/void)
+    bool pnt_sharded = false;               // tbg_set_pnt_sharded: every call records its updates
+    Call<tb_transfer_t> pnt_last{};         // the last create_transfers call (tbg_pnt_ops)
+    bool pnt_last_valid = false;
     unsigned long long* pnt_fired = nullptr;
     unsigned long long* pv_slots = nullptr;  // pending-id claims of post/void events (kernels.hpp)
     uint64_t pv_mask = 0;
@@ -461,6 +464,7 @@ Call<Event> make_call(tbg_ctx* ctx, const Event* d_events, uint32_t n, const uin
     // (TBG_NO_PV_FAST: every post/void replays)
     c.pv_slots = getenv("TBG_NO_PV_FAST") ? nullptr : ctx->pv_slots;
     c.pv_mask = ctx->pv_mask;
+    c.pnt_force = ctx->pnt_sharded ? 1 : 0;
     return c;
 }
 
@@ -601,7 +605,7 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
     P.indeg = F.indeg;
     P.queue = F.queue;
     const bool post_void = (call_flags & kFlagPostVoid) != 0;
-    P.pnt_ops = post_void ? c.pnt_call : nullptr;
+    P.pnt_ops = post_void || c.pnt_force ? c.pnt_call : nullptr;
     P.lane_undo = F.lane_undo;
     P.steps = F.steps;
     P.evs = F.evs;
@@ -846,7 +850,7 @@ int pnt_resolve(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
     hipLaunchKernelGGL(pnt_tile_min, dim3(tiles), dim3(kPntThreads), 0, ctx->stream, c.pnt_call, n,
                        tile_min);
     hipLaunchKernelGGL(pnt_tile_resolve, dim3(tiles), dim3(kPntThreads), 0, ctx->stream, ctx->T,
-                       c.pnt_call, n, tile_min, ctx->pnt_fired);
+                       c.pnt_call, n, tile_min, ctx->pnt_fired, c.pnt_force);
     tmark(ctx, "pnt_resolve");
     HIP_TRY(ctx, hipGetLastError());
     return 0;
@@ -1688,7 +1692,7 @@ tbg_ctx* tbg_open(const tbg_options* options) {
          dev_alloc(ctx, &ctx->ev_info, ev_max, false) && dev_alloc(ctx, &ctx->ev_slow, ev_max, false) &&
          dev_alloc(ctx, &ctx->slow_list, ev_max, false) &&
          dev_alloc(ctx, &ctx->fix_slots, ev_max, false) &&
-         dev_alloc(ctx, &ctx->pnt_call, ev_max, false) && dev_alloc(ctx, &ctx->pnt_fired, 2, true) &&
+         dev_alloc(ctx, &ctx->pnt_call, ev_max, false) && dev_alloc(ctx, &ctx->pnt_fired, 4, true) &&
          dev_alloc(ctx, &ctx->pv_slots, next_pow2(2 * uint64_t(ev_max)), true);
     ctx->pv_mask = next_pow2(2 * uint64_t(ev_max)) - 1;
     // (2 * ev_max items, at least ev_max u64 of lookup scratch)
@@ -2020,7 +2024,11 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
     ctx->early_done = !rc && ctx->early_dst && !replay;  // (only the replay rewrites results)
     if (replay && (ctx->h_scalars->flags & kFlagImported)) rc = check_imported_indexes(ctx, true);
     if (replay && !rc) rc = run_replay(ctx, c, true, false);
-    if (!rc && (ctx->h_scalars->flags & kFlagPostVoid)) rc = pnt_resolve(ctx, c);
+    if (!rc && ((ctx->h_scalars->flags & kFlagPostVoid) || c.pnt_force)) rc = pnt_resolve(ctx, c);
+    if (!rc) {
+        ctx->pnt_last = c;
+        ctx->pnt_last_valid = c.pnt_force != 0;
+    }
     if (!rc) rc = end_call(ctx, n, !replay);
     if (!rc && ctx->ae_log && ctx->ae_defer) {
         ctx->ae_call = c;  // launched by tbg_create_transfers once the results' copy is queued
@@ -2443,6 +2451,57 @@ int tbg_raise_key_max(tbg_ctx* ctx, uint64_t accounts_key_max, uint64_t transfer
 uint64_t tbg_pulse_next_timestamp(tbg_ctx* ctx) {
     if (!ctx || sync_scalars(ctx)) return 0;
     return ctx->h_scalars->pulse_next_timestamp;
+}
+
+int tbg_set_pnt_sharded(tbg_ctx* ctx, int on) {
+    if (!ctx) return TBG_EINVAL;
+    ctx->pnt_sharded = on != 0;
+    ctx->pnt_last_valid = false;
+    return 0;
+}
+
+int64_t tbg_pnt_ops(tbg_ctx* ctx, uint64_t* timestamps, uint64_t* ops, uint64_t max,
+                    uint64_t* start) {
+    if (!ctx) return TBG_EINVAL;
+    FAILED_GUARD(ctx);
+    if (!ctx->pnt_last_valid) {  // (no sharded call since: nothing recorded)
+        if (start) *start = tbg_pulse_next_timestamp(ctx);
+        return 0;
+    }
+    const Call<tb_transfer_t>& c = ctx->pnt_last;
+    hipLaunchKernelGGL(pnt_flags, dim3(grid_for(c.n)), dim3(kBlock), 0, ctx->stream, c.pnt_call,
+                       c.n, ctx->ev_slow);
+    unsigned int* d_count = &ctx->d_scalars->slow_count;  // scratch word (between calls)
+    int rc = select_flagged(ctx, ctx->ev_slow, c.n, ctx->slow_list, d_count);
+    if (rc) return rc;
+    hipLaunchKernelGGL(pnt_gather, dim3(grid_for(c.n)), dim3(kBlock), 0, ctx->stream, c,
+                       ctx->slow_list, d_count, ctx->bal_items);
+    HIP_TRY(ctx, hipGetLastError());
+    rc = sync_scalars(ctx);
+    if (rc) return rc;
+    const uint64_t m = ctx->h_scalars->slow_count;
+    unsigned long long st = 0;
+    HIP_TRY(ctx, hipMemcpy(&st, ctx->pnt_fired + 2, 8, hipMemcpyDeviceToHost));
+    if (start) *start = st;
+    if (m && (timestamps || ops)) {
+        std::vector<uint64_t> pairs(2 * m);
+        HIP_TRY(ctx, hipMemcpy(pairs.data(), ctx->bal_items, 16 * m, hipMemcpyDeviceToHost));
+        for (uint64_t i = 0; i < std::min(m, max); i++) {
+            if (timestamps) timestamps[i] = pairs[2 * i];
+            if (ops) ops[i] = pairs[2 * i + 1];
+        }
+    }
+    return int64_t(m);
+}
+
+int tbg_set_pulse_next_timestamp(tbg_ctx* ctx, uint64_t value) {
+    if (!ctx) return TBG_EINVAL;
+    FAILED_GUARD(ctx);
+    const unsigned long long v = value;
+    HIP_TRY(ctx, hipMemcpyAsync(&ctx->d_scalars->pulse_next_timestamp, &v, 8,
+                                hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // (`v` is a stack value)
+    return 0;
 }
 
 int64_t tbg_lookup_accounts(tbg_ctx* ctx, const tb_uint128_t* ids, uint32_t n, tb_account_t* out) {

@@ -493,6 +493,7 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
                                             unsigned int* bucket_hist) {
     bool imported = false, post_void = false, dup = false, closable = false, hot = false;
     bool need_commit = false, chain_fast = false, ae_slow = false;
+    if (c.pnt_force) c.pnt_call[k] = 0;  // (sharded calls record every update: none yet)
     const uint16_t f = t.flags;
     imported = (f & TB_TRANSFER_IMPORTED) != 0;
     post_void = (f & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) != 0;
@@ -1285,7 +1286,8 @@ __device__ inline void commit_event(const Tables& T, const Call<tb_transfer_t>& 
     const uint8_t cls = info & kInfoClassMask;
     const uint64_t row = c.row_base + k;
     const uint64_t ref = row + 1;
-    if (call_flags & kFlagPostVoid) c.pnt_call[k] = 0;  // (the replay records its own)
+    const bool pnt_rec = (call_flags & kFlagPostVoid) || c.pnt_force;
+    if (pnt_rec) c.pnt_call[k] = 0;  // (the replay records its own)
     bool slow = cls == kClassSlow || (call_flags & kFlagImported);
     if (cls == kClassFast) {
         const FastRec fr = pre.has_fr ? pre.fr : fast_record(T, c, k, call_flags, info);
@@ -1362,7 +1364,7 @@ __device__ inline void commit_event(const Tables& T, const Call<tb_transfer_t>& 
                 // With post/void in the call the order of updates matters (a post/void resets
                 // pulse_next_timestamp when it names its expiry): recorded at the event, resolved
                 // in call order after the replay (pnt_resolve).
-                if (call_flags & kFlagPostVoid) c.pnt_call[k] = expires_at;
+                if (pnt_rec) c.pnt_call[k] = expires_at;
                 else atomicMin(&T.scalars->pulse_next_timestamp, (unsigned long long)expires_at);
             }
         }
@@ -1946,7 +1948,7 @@ template <typename Event>
 __global__ void replay_kernel(Tables T, Call<Event> c, int is_transfers) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     Replay R(T);
-    if (is_transfers && (T.scalars->flags & kFlagPostVoid)) R.pnt_ops = c.pnt_call;
+    if (is_transfers && ((T.scalars->flags & kFlagPostVoid) || c.pnt_force)) R.pnt_ops = c.pnt_call;
     bool chain_open = false, chain_broken = false;
     uint32_t chain_start = 0;
     const uint32_t n = T.scalars->slow_count;

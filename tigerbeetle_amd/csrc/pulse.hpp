@@ -151,6 +151,33 @@ __global__ void pulse_settle(Tables T, const uint64_t* exp, unsigned long long* 
     *expired_out = uint32_t(expired);
 }
 
+// A sharded call's recorded updates for the caller (tbg_pnt_ops): event k's flag.
+__global__ void pnt_flags(const uint64_t* ops, uint32_t n, uint8_t* flags) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < n) flags[k] = ops[k] != 0;
+}
+// ... and the selected ones as (timestamp, op) pairs, in call order.
+__global__ void pnt_gather(Call<tb_transfer_t> c, const uint32_t* list, const unsigned int* count,
+                           uint64_t* out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= *count) return;
+    const uint32_t k = list[i];
+    uint64_t ts;
+    if (c.event_ts) {
+        ts = c.event_ts[k];
+    } else {
+        uint32_t lo = 0, hi = c.n_batches - 1;  // the batch holding k: the first end > k
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (c.batch_ends[mid] > k) hi = mid;
+            else lo = mid + 1;
+        }
+        ts = c.batch_ts[lo] - c.batch_ends[lo] + k + 1;
+    }
+    out[2 * i] = ts;
+    out[2 * i + 1] = c.pnt_call[k];
+}
+
 // The pulse's outcome for the host: the count expired and the index's new length.
 __global__ void pulse_report(const unsigned int* expired, const unsigned long long* counters,
                              unsigned long long* out) {
@@ -206,15 +233,19 @@ __global__ void __launch_bounds__(kPntThreads) pnt_tile_min(const uint64_t* ops,
     if (threadIdx.x == 0) tile_min[blockIdx.x] = m;
 }
 
-// words: [0] fired, [1] finished tiles (both zero between calls: the last tile clears them).
+// words: [0] fired, [1] finished tiles (both zero between calls: the last tile clears them),
+// [2] the value at the call's start. `mins_only` (a sharded call): resets are not applied here
+// (they compare against the value across all shards: the caller resolves them).
 __global__ void __launch_bounds__(kPntThreads) pnt_tile_resolve(Tables T, const uint64_t* ops,
                                                                uint32_t n, const uint64_t* tile_min,
-                                                               unsigned long long* words) {
+                                                               unsigned long long* words,
+                                                               uint32_t mins_only) {
     __shared__ uint64_t lds[kPntThreads / 64];
     __shared__ uint64_t thread_min[kPntThreads];
     __shared__ bool last;
     const uint32_t tid = threadIdx.x, tile = blockIdx.x, tiles = gridDim.x;
     const uint64_t start = T.scalars->pulse_next_timestamp;
+    if (tile == 0 && tid == 0) words[2] = start;
     // The minimum before this tile: the value at the call's start and the earlier tiles' minima.
     uint64_t before = ~0ull;
     for (uint32_t t = tid; t < tile; t += kPntThreads) before = tile_min[t] < before ? tile_min[t] : before;
@@ -236,7 +267,7 @@ __global__ void __launch_bounds__(kPntThreads) pnt_tile_resolve(Tables T, const 
     bool fired = false;
     for (uint32_t i = 0; i < kPntItems; i++) {
         const uint64_t op = ops_l[i];
-        if (op & kPntReset) fired |= run == (op & ~kPntReset);
+        if ((op & kPntReset) && !mins_only) fired |= run == (op & ~kPntReset);
         const uint64_t v = pnt_min_of(op);
         run = v < run ? v : run;
     }

@@ -152,6 +152,9 @@ struct Call {
     // Calls with post/void: every pulse_next_timestamp update, per event (0: none; expires_at:
     // min; expires_at | kPntReset: reset-if-equal), resolved in call order after the replay.
     uint64_t* pnt_call;
+    // Sharded calls (tbg_set_pnt_sharded): every update is recorded, whatever the call's flags,
+    // and the resets are resolved across shards by the caller (pnt_resolve applies the mins).
+    uint32_t pnt_force;
     // tr_ingest of a small host-buffer call reads the body straight from mapped host memory
     // (`events`) and leaves a copy here for the call's later kernels (null: no copy).
     tb_transfer_t* events_out;

@@ -48,7 +48,7 @@ struct RouteArgs {
     uint8_t* ev_shard;      // per event: its shard, 0xFF for a hazard
     uint32_t* ev_slot;      // per event: its claimed slot (kNone32: none)
     uint32_t* block_counts; // [shard][block]
-    unsigned int* flags;    // [0] hazard, [1] table full
+    unsigned int* flags;    // [0] hazard, [1] table full, [2] the call posts or voids
 };
 
 __device__ inline uint64_t dir_find(const Dir& d, const tb_uint128_t& id) {
@@ -90,7 +90,7 @@ __device__ inline void raise_hazard(const RouteArgs& a, bool hazard) {
 // event (both known, on one shard), none yet for a post/void (its pending transfer's, pass 2).
 __global__ void __launch_bounds__(kRouteBlock) tbr_pass1(RouteArgs a) {
     const uint32_t k = blockIdx.x * kRouteBlock + threadIdx.x;
-    bool hazard = false;
+    bool hazard = false, pv_any = false;
     if (k < a.n) {
         const tb_transfer_t& t = a.events[k];
         const uint16_t f = t.flags;
@@ -140,16 +140,19 @@ __global__ void __launch_bounds__(kRouteBlock) tbr_pass1(RouteArgs a) {
         a.tr.ids[a.base + k] = t.id;
         const bool timed = (f & TB_TRANSFER_PENDING) && t.timeout > 0;
         a.tr.shard[a.base + k] = uint8_t(sd == kNone ? 0 : sd) | (timed ? TBR_TIMED : 0);
+        pv_any = post_void;
     }
+    if (__any(pv_any) && (threadIdx.x & 63) == 0) atomicOr(&a.flags[2], 1u);
     raise_hazard(a, hazard);
 }
 
 // Pass 2, per post/void: the shard of its pending transfer -- the directory's holder, or the
 // in-call event that creates it (post_or_void_pending_transfer reads only the pending transfer,
-// its TransferPending status and its accounts, all on that shard, :4053-4299). A pending
-// transfer with a timeout is a hazard: its post/void resets pulse_next_timestamp on equality with
-// the global value (:4227-4229), which no shard holds; so is a pending id found nowhere (no
-// shard is pinned) or created in the call by another post/void.
+// its TransferPending status and its accounts, all on that shard, :4053-4299). A pending id
+// found nowhere (no shard is pinned) or created in the call by another post/void is a hazard.
+// (A post/void of a pending transfer with a timeout resets pulse_next_timestamp on equality with
+// the value over all shards, :4227-4229: the shards record their updates and the caller
+// resolves them after the call -- tbg_pnt_ops.)
 __global__ void __launch_bounds__(kRouteBlock) tbr_pass_pv(RouteArgs a) {
     const uint32_t k = blockIdx.x * kRouteBlock + threadIdx.x;
     bool hazard = false;
@@ -165,14 +168,12 @@ __global__ void __launch_bounds__(kRouteBlock) tbr_pass_pv(RouteArgs a) {
         if (s != kNone) {
             const uint64_t r = (a.tr.slots.slots[s] & kRefMask) - 1;
             if (r < base) {
-                const uint8_t v = a.tr.shard[r];
-                if (!(v & TBR_TIMED)) shard = v & 0x7Fu;
+                shard = a.tr.shard[r] & 0x7Fu;
             } else {
                 const tb_transfer_t& p = ev[r - base];
                 const bool p_pv = (p.flags & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) != 0;
-                const bool p_timed = (p.flags & TB_TRANSFER_PENDING) && p.timeout > 0;
                 const uint8_t ps = a.ev_shard[r - base];
-                if (!p_pv && !p_timed && ps < kShardPending) shard = ps;
+                if (!p_pv && ps < kShardPending) shard = ps;
             }
         }
         hazard = shard == kShardHazard;
@@ -401,7 +402,7 @@ tbr_ctx* tbr_open(uint32_t shards, uint64_t account_capacity, uint64_t transfer_
          alloc(&r->ev_slot, events_max, false, r->stream) &&
          alloc(&r->block_counts, uint64_t(shards) * nblocks, false, r->stream) &&
          alloc(&r->offsets, uint64_t(shards) * nblocks, false, r->stream) &&
-         alloc(&r->flags, 2, true, r->stream) && alloc(&r->key_max, 1, true, r->stream) &&
+         alloc(&r->flags, 4, true, r->stream) && alloc(&r->key_max, 1, true, r->stream) &&
          alloc(&r->q_ids, events_max, false, r->stream) &&
          alloc(&r->q_out, events_max, false, r->stream);
     ok = ok && hipStreamSynchronize(r->stream) == hipSuccess;
@@ -455,13 +456,13 @@ int64_t tbr_route_device(tbr_ctx* r, const tb_transfer_t* d_events, uint32_t n,
     if (r->tr_used + n > r->tr_cap) return -28;
     RouteArgs a = route_args(r, d_events, n, d_batch_ends, d_batch_ts, n_batches);
     const dim3 grid(a.nblocks), block(kRouteBlock);
-    if (hipMemsetAsync(r->flags, 0, 8, r->stream)) return -5;
+    if (hipMemsetAsync(r->flags, 0, 16, r->stream)) return -5;
     hipLaunchKernelGGL(tbr_pass1, grid, block, 0, r->stream, a);
     hipLaunchKernelGGL(tbr_pass_pv, grid, block, 0, r->stream, a);
     hipLaunchKernelGGL(tbr_pass_chains, grid, block, 0, r->stream, a);
     std::vector<uint32_t> counts(uint64_t(r->shards) * a.nblocks);
-    unsigned int f[2] = {0, 0};
-    if (hipMemcpyAsync(f, r->flags, 8, hipMemcpyDeviceToHost, r->stream) ||
+    unsigned int f[4] = {0, 0, 0, 0};
+    if (hipMemcpyAsync(f, r->flags, 16, hipMemcpyDeviceToHost, r->stream) ||
         hipMemcpyAsync(counts.data(), r->block_counts, counts.size() * 4, hipMemcpyDeviceToHost,
                        r->stream) ||
         hipStreamSynchronize(r->stream))
@@ -491,7 +492,7 @@ int64_t tbr_route_device(tbr_ctx* r, const tb_transfer_t* d_events, uint32_t n,
     r->pending = true;
     r->call_base = a.base;
     r->call_n = n;
-    return 0;
+    return f[2] ? 2 : 0;
 }
 
 int tbr_settle_device(tbr_ctx* r, const tb_create_result_t* d_shard_results,

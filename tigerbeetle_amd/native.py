@@ -100,6 +100,9 @@ SIGNATURES = [
                                        ctypes.c_uint64, vp]),
     ("tbg_pulse_next_timestamp", ctypes.c_uint64, [vp]),
     ("tbg_raise_key_max", ctypes.c_int, [vp, ctypes.c_uint64, ctypes.c_uint64]),
+    ("tbg_set_pnt_sharded", ctypes.c_int, [vp, ctypes.c_int]),
+    ("tbg_pnt_ops", ctypes.c_int64, [vp, vp, vp, ctypes.c_uint64, c_u64p]),
+    ("tbg_set_pulse_next_timestamp", ctypes.c_int, [vp, ctypes.c_uint64]),
     ("tbg_lookup_accounts", ctypes.c_int64, [vp, vp, ctypes.c_uint32, vp]),
     ("tbg_lookup_transfers", ctypes.c_int64, [vp, vp, ctypes.c_uint32, vp]),
     ("tbg_dump_accounts", ctypes.c_int64, [vp, vp]),

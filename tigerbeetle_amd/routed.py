@@ -12,10 +12,15 @@ ids that now exist on their shards).
 The device router places single events, resubmitted ids (on their holder), post/voids (on
 their pending transfer's shard) and linked chains that stay on one shard (include/tbr.h). A call
 it cannot place -- any event that could observe another shard's state (imported events, ids that
-repeat within the call, accounts unknown or on two shards, chains across shards, post/voids of
-pending transfers with a timeout) -- is executed by the exact host router instead (shard.LedgerRouter over the same directories,
+repeat within the call, accounts unknown or on two shards, chains across shards) -- is executed
+by the exact host router instead (shard.LedgerRouter over the same directories,
 through shard.ShardGroup): surrogates for cross-shard transfers, key-range sync for imported
 batches, refusal of the cases no shard can execute alone.
+
+A routed call that posts or voids (the router's mode 2) resolves pulse_next_timestamp across the
+shards after it (shard.ShardGroup.resolve_pnt: every shard's recorded updates gathered at rank 0,
+replayed in call order, the outcome broadcast): a post/void of a pending transfer with a timeout
+resets it against the value over all shards (post_or_void_pending_transfer :4227-4229).
 """
 import ctypes
 
@@ -128,6 +133,9 @@ class RoutedShards:
             words = [0] * (W + 1)
         words = self._bcast(words)
         mode, counts = words[0], words[1:]
+        resolve = mode == 2
+        if mode == 2:
+            mode = 0
         if mode == 1:
             self.host_calls += 1
             if self.rank == 0:
@@ -177,6 +185,8 @@ class RoutedShards:
                 r = self._isend(self.res[:mine * 16], 0)
                 if r is not None:
                     r.wait()
+        if resolve:
+            self.host.resolve_pnt(executed=mine > 0)
         return 0
 
     def _execute(self, ev, ts, res, n):

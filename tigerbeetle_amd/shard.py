@@ -34,10 +34,17 @@ alone:
   cross-shard transfer whose id repeats an id of the call;
 * imported events whose outcome depends on another shard: a timestamp at or below an imported
   timestamp of an earlier event of the call on another shard, or at or below the other groove's
-  key maximum (a possible timestamp collision, :3660, :3812);
-* a post/void of a pending transfer that has a timeout: it resets `pulse_next_timestamp` when
-  that equals the pending transfer's expiry (:4227-4229), a comparison against the *global*
-  value at that point of the call, which no shard holds.
+  key maximum (a possible timestamp collision, :3660, :3812).
+
+A post/void of a pending transfer that has a timeout resets `pulse_next_timestamp` when that
+equals the pending transfer's expiry (:4227-4229) -- a comparison against the *global* value at
+that point of the call, which no shard holds. The shards run with sharded pulse_next_timestamp
+(`set_pnt_sharded`): each records every update at its event (min of a pending transfer's expiry,
+applied; reset-if-equal of a post/void, only recorded) with the event's global timestamp. After a
+call holding a post/void the updates of every shard are gathered, merged by timestamp and replayed
+from the minimum of the shards' values at the call's start (`pnt_resets_fire`); when a reset
+fires, every shard's value becomes timestamp_min -- the reference's value. No event's outcome
+reads the value (only pulses do, between calls), so the call itself runs unchanged.
 
 Events whose outcome is decided before any shard-local lookup can fail (`id_must_not_be_zero`,
 accounts not found anywhere, pending transfer not found anywhere) go to the shard of their ledger.
@@ -84,6 +91,24 @@ _ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER = 23
 _CLOSING_TRANSFER_MUST_BE_PENDING = 64
 
 
+PNT_RESET = 1 << 63  # a recorded update that is a reset-if-equal (post/void of an expiry)
+TIMESTAMP_MIN = 1
+
+
+def pnt_resets_fire(starts, op_lists) -> bool:
+    """Does a reset of pulse_next_timestamp fire in the call's order across shards? `starts`: the
+    shards' values at the call's start; `op_lists`: per shard, its recorded updates as (event
+    timestamp, op) -- op an expiry (a `min`), or an expiry | PNT_RESET (reset-if-equal)."""
+    value = min(int(x) for x in starts)
+    for _, op in sorted((int(t), int(o)) for ops in op_lists for t, o in ops):
+        if op & PNT_RESET:
+            if value == op & ~PNT_RESET:
+                return True  # (timestamp_min from here on: every later `min` keeps it)
+        elif op < value:
+            value = op
+    return False
+
+
 class RouteError(RuntimeError):
     """The call holds an event that no single shard can execute exactly (see the module doc)."""
 
@@ -110,6 +135,7 @@ class Plan:
     # cross-shard transfers: event index -> the reference's status (the shard runs a surrogate)
     cross: Dict[int, int] = field(default_factory=dict)
     imported: bool = False                  # the call holds imported events (key ranges synced)
+    post_void: bool = False                 # ... posts or voids (pulse_next_timestamp resolved)
 
     def shard_events(self, events: np.ndarray) -> np.ndarray:
         """The events as the shards execute them: cross-shard transfers as their surrogates."""
@@ -394,8 +420,6 @@ class LedgerRouter:
                 pins.add(in_call[i])
             if fl[k] & post_void:
                 p = pids[k]
-                if (p in tr_known and tr_known[p][1]) or p in in_call_timed:
-                    raise RouteError(f"event {k} posts/voids a pending transfer with a timeout")
                 if p in tr_known:
                     pins.add(tr_known[p][0])
                 elif p in in_call:
@@ -423,7 +447,8 @@ class LedgerRouter:
             self._check_imported(imported, events["timestamp"], lens, batch_ts, shard_of,
                                  self.accounts_key_max, "transfer")
         return Plan("transfers", shard_of, split_runs(shard_of, lens, batch_ts, self.shards),
-                    cross=cross, imported=bool(n and imported.any()))
+                    cross=cross, imported=bool(n and imported.any()),
+                    post_void=bool(n and ((flags & post_void) != 0).any()))
 
     # -- directories --------------------------------------------------------------------------
 
@@ -509,6 +534,8 @@ class LocalShards:
         self.router = router
         self.executors = executors
         self.pulse_batch_max = pulse_batch_max
+        for ex in executors:
+            ex.set_pnt_sharded(True)
 
     def _run(self, kind, events, lens, batch_ts):
         dtype = ACCOUNT_DTYPE if kind == "accounts" else TRANSFER_DTYPE
@@ -529,6 +556,12 @@ class LocalShards:
                            np.asarray(sl.batch_ts, dtype=np.uint64)))
         results = plan.patch(gather_results(plan, outs, len(events)))
         self.router.commit(plan, events, results)
+        if plan.post_void:  # (a shard that executed nothing of the call: its value alone)
+            recorded = [ex.pnt_ops() if o is not None else (int(ex.pulse_next_timestamp()), [])
+                        for ex, o in zip(self.executors, outs)]
+            if pnt_resets_fire([s for s, _ in recorded], [ops for _, ops in recorded]):
+                for ex in self.executors:
+                    ex.set_pulse_next_timestamp(TIMESTAMP_MIN)
         return results
 
     def create_accounts(self, events, lens, batch_ts):
@@ -569,6 +602,7 @@ class ShardGroup:
         self.executor = executor
         self.device = device
         self.pulse_batch_max = pulse_batch_max
+        executor.set_pnt_sharded(True)
 
     def _peer(self, r: int) -> int:
         return r if self.group is None else self.dist.get_global_rank(self.group, r)
@@ -609,11 +643,13 @@ class ShardGroup:
                         else self.router.plan_transfers)(events, lens, batch_ts)
             except RouteError as e:
                 err = e
-        # Status word: refused, or the global key maxima an imported call needs on every shard.
+        # Status word: refused, the global key maxima an imported call needs on every shard, and
+        # whether the call posts or voids (pulse_next_timestamp resolved across shards after it).
         word = self._bcast_words([0 if err is None else 1,
                                   int(plan is not None and plan.imported),
                                   self.router.accounts_key_max if self.rank == 0 else 0,
-                                  self.router.transfers_key_max if self.rank == 0 else 0])
+                                  self.router.transfers_key_max if self.rank == 0 else 0,
+                                  int(plan is not None and plan.post_void)])
         if word[0]:  # every rank fails a refused call
             raise err if err is not None else RouteError("refused by the router on rank 0")
         if word[1]:
@@ -659,11 +695,36 @@ class ShardGroup:
             if failure is not None:
                 raise failure
             raise RuntimeError("a shard's executor failed; the shards' state is undefined")
+        if word[4]:
+            self.resolve_pnt(executed=len(mine[0]) > 0)
         if self.rank != 0:
             return None
         results = plan.patch(gather_results(plan, outs, len(events)))
         self.router.commit(plan, events, results)
         return results
+
+    def resolve_pnt(self, executed=True):
+        """Collective, after a call that posts or voids: every shard's recorded
+        pulse_next_timestamp updates to rank 0 (its start value, then (timestamp, op) pairs; a
+        shard that executed nothing of the call sends its value alone), replayed in call order
+        there; the outcome broadcast."""
+        if executed:
+            start, ops = self.executor.pnt_ops()
+        else:
+            start, ops = int(self.executor.pulse_next_timestamp()), []
+        mine = np.asarray([start] + [x for pair in ops for x in pair], dtype=np.uint64)
+        if self.rank != 0:
+            self._send(mine, 0)
+            fired = self._bcast(0)
+        else:
+            starts, lists = [start], [ops]
+            for s in range(1, self.world):
+                a = self._recv(s, np.uint64)
+                starts.append(int(a[0]))
+                lists.append(list(zip(a[1::2].tolist(), a[2::2].tolist())))
+            fired = self._bcast(int(pnt_resets_fire(starts, lists)))
+        if fired:
+            self.executor.set_pulse_next_timestamp(TIMESTAMP_MIN)
 
     def _bcast_words(self, words):
         import torch
@@ -797,6 +858,28 @@ class GpuShard:
 
     def pulse_next_timestamp(self):
         return int(self.lib.tbg_pulse_next_timestamp(self.g))
+
+    def set_pnt_sharded(self, on):
+        self.lib.tbg_set_pnt_sharded(self.g, 1 if on else 0)
+
+    def pnt_ops(self):
+        """The last call's recorded pulse_next_timestamp updates: (start, [(timestamp, op)])."""
+        c = self._c
+        start = c.c_uint64()
+        n = int(self.lib.tbg_pnt_ops(self.g, None, None, 0, c.byref(start)))
+        if n < 0:
+            raise RuntimeError(f"libtbg: {n} {self.lib.tbg_last_error(self.g)}")
+        ts = np.zeros(max(n, 1), dtype=np.uint64)
+        ops = np.zeros(max(n, 1), dtype=np.uint64)
+        if n:
+            self.lib.tbg_pnt_ops(self.g, ts.ctypes.data_as(c.c_void_p),
+                                 ops.ctypes.data_as(c.c_void_p), n, c.byref(start))
+        return int(start.value), list(zip(ts[:n].tolist(), ops[:n].tolist()))
+
+    def set_pulse_next_timestamp(self, value):
+        rc = self.lib.tbg_set_pulse_next_timestamp(self.g, int(value))
+        if rc != 0:
+            raise RuntimeError(f"libtbg: {rc} {self.lib.tbg_last_error(self.g)}")
 
     def raise_key_max(self, accounts_key_max, transfers_key_max):
         rc = self.lib.tbg_raise_key_max(self.g, accounts_key_max, transfers_key_max)
