@@ -407,8 +407,8 @@ def test_account_events_dense(case, monkeypatch):
             assert paths == [0] * 5
         elif case == "dense":
             assert paths == [2] * 5
-        else:
-            assert paths[3] == 0 and paths.count(2) == 4
+        else:  # (after the closing step, voids of its closing transfers flip `closed` back too)
+            assert paths[:3] == [2] * 3 and paths[3] == 0
         p.compare_state()
         assert len(p.change_events()) > 0
     finally:
