@@ -44,6 +44,9 @@
 #ifndef TBG_INGEST_JOINT_PROBE
 #define TBG_INGEST_JOINT_PROBE 1
 #endif
+#ifndef TBG_INGEST_NARROW_B128
+#define TBG_INGEST_NARROW_B128 1  // the event's narrow fields by 16-byte LDS reads (EvNarrow)
+#endif
 #ifndef TBG_INGEST_H1_FIRST
 #define TBG_INGEST_H1_FIRST 1  // account index: the first candidate only, the second on a miss
 #endif
@@ -351,13 +354,47 @@ __device__ inline uint8_t classify_post_void(const Tables& T, const Call<tb_tran
 
 // The checks after the id lookup (create_transfer, :3727-3873), on the ingest snapshot. `w` is
 // the word of the id's slot as this event observed it.
+// The narrow fields of a staged event, taken from its LDS image with 16-byte reads (words 3, 6, 7:
+// amount, timeout, ledger / code / flags / timestamp). Read one by one at the image's 144-byte
+// stride, the 4- and 8-byte fields put 4 lanes of a 32-lane group on one bank
+// (SQ_LDS_BANK_CONFLICT, profiles/r03_final_pmc); the 16-byte reads are conflict-free.
+struct EvNarrow {
+    const uint4* w;  // the event's LDS image (16-byte words)
+#if TBG_INGEST_NARROW_B128
+    __device__ uint16_t flags() const { return uint16_t(w[7].y >> 16); }
+    __device__ uint16_t code() const { return uint16_t(w[7].y); }
+    __device__ uint32_t ledger() const { return w[7].x; }
+    __device__ uint32_t timeout() const { return w[6].w; }
+    __device__ uint64_t timestamp() const { const uint4 q = w[7]; return (uint64_t(q.w) << 32) | q.z; }
+    __device__ uint64_t amount_lo() const { const uint4 q = w[3]; return (uint64_t(q.y) << 32) | q.x; }
+    __device__ uint64_t amount_hi() const { const uint4 q = w[3]; return (uint64_t(q.w) << 32) | q.z; }
+#else  // (the fields one by one: same-box A/B builds)
+    __device__ const tb_transfer_t& t() const { return *reinterpret_cast<const tb_transfer_t*>(w); }
+    __device__ uint16_t flags() const { return t().flags; }
+    __device__ uint16_t code() const { return t().code; }
+    __device__ uint32_t ledger() const { return t().ledger; }
+    __device__ uint32_t timeout() const { return t().timeout; }
+    __device__ uint64_t timestamp() const { return t().timestamp; }
+    __device__ uint64_t amount_lo() const { return t().amount.lo; }
+    __device__ uint64_t amount_hi() const { return t().amount.hi; }
+#endif
+};
+__device__ inline EvNarrow ev_narrow(const tb_transfer_t& t) {
+    return EvNarrow{reinterpret_cast<const uint4*>(&t)};
+}
+static_assert(offsetof(tb_transfer_t, amount) == 48 && offsetof(tb_transfer_t, timeout) == 108 &&
+                  offsetof(tb_transfer_t, ledger) == 112 && offsetof(tb_transfer_t, code) == 116 &&
+                  offsetof(tb_transfer_t, flags) == 118 && offsetof(tb_transfer_t, timestamp) == 120,
+              "Transfer layout");
+
 __device__ inline uint8_t classify_after_lookup(const Tables& T, const Call<tb_transfer_t>& c,
                                                 uint32_t k, uint64_t ts_event,
-                                                const tb_transfer_t& t, uint64_t w,
+                                                const tb_transfer_t& t, const EvNarrow& tn,
+                                                uint64_t w,
                                                 const AccSnap& dr, const AccSnap& cr,
                                                 uint32_t* status, uint64_t* ts_out,
                                                 uint8_t* info, PvFast* pv) {
-    const uint16_t f = t.flags;
+    const uint16_t f = tn.flags();
     const uint64_t r = (w & kRefMask) - 1;
     if (r < c.row_base) {  // a committed id: the result is final for every event of the call
         if (w & kOrphanBit) {
@@ -366,8 +403,8 @@ __device__ inline uint8_t classify_after_lookup(const Tables& T, const Call<tb_t
         }
         const tb_transfer_t& e = T.tr_rows[r];  // committed rows are immutable
         const tb_transfer_t* p = nullptr;
-        if (t.flags == e.flags && U(t.pending_id) == U(e.pending_id) && t.timeout == e.timeout &&
-            (t.flags & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING))) {
+        if (f == e.flags && U(t.pending_id) == U(e.pending_id) && tn.timeout() == e.timeout &&
+            (f & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING))) {
             const uint64_t ps = transfer_slot_find(T, c, t.pending_id);
             if (ps == kNone) return kClassSlow;
             const uint64_t pw = T.tr.slots[ps];
@@ -390,17 +427,17 @@ __device__ inline uint8_t classify_after_lookup(const Tables& T, const Call<tb_t
     else if (u128_is_max(t.credit_account_id)) st = TB_CT_CREDIT_ACCOUNT_ID_MUST_NOT_BE_INT_MAX;
     else if (u128_eq(t.credit_account_id, t.debit_account_id)) st = TB_CT_ACCOUNTS_MUST_BE_DIFFERENT;
     else if (!u128_is_zero(t.pending_id)) st = TB_CT_PENDING_ID_MUST_BE_ZERO;
-    else if (!(f & TB_TRANSFER_PENDING) && t.timeout != 0)
+    else if (!(f & TB_TRANSFER_PENDING) && tn.timeout() != 0)
         st = TB_CT_TIMEOUT_RESERVED_FOR_PENDING_TRANSFER;
     else if (!(f & TB_TRANSFER_PENDING) &&
              (f & (TB_TRANSFER_CLOSING_DEBIT | TB_TRANSFER_CLOSING_CREDIT)))
         st = TB_CT_CLOSING_TRANSFER_MUST_BE_PENDING;
-    else if (t.ledger == 0) st = TB_CT_LEDGER_MUST_NOT_BE_ZERO;
-    else if (t.code == 0) st = TB_CT_CODE_MUST_NOT_BE_ZERO;
+    else if (tn.ledger() == 0) st = TB_CT_LEDGER_MUST_NOT_BE_ZERO;
+    else if (tn.code() == 0) st = TB_CT_CODE_MUST_NOT_BE_ZERO;
     else if (dr.row == kNone32) st = TB_CT_DEBIT_ACCOUNT_NOT_FOUND;
     else if (cr.row == kNone32) st = TB_CT_CREDIT_ACCOUNT_NOT_FOUND;
     else if (dr.ledger != cr.ledger) st = TB_CT_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;
-    else if (t.ledger != dr.ledger) st = TB_CT_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
+    else if (tn.ledger() != dr.ledger) st = TB_CT_TRANSFER_MUST_HAVE_THE_SAME_LEDGER_AS_ACCOUNTS;
     if (st) {
         *status = st;
         return kClassDone;
@@ -413,7 +450,7 @@ __device__ inline uint8_t classify_after_lookup(const Tables& T, const Call<tb_t
               TB_TRANSFER_CLOSING_DEBIT | TB_TRANSFER_CLOSING_CREDIT)) != 0;
     // Overflow is impossible when every balance is < 2^126 and every amount < 2^64.
     constexpr uint64_t kHiLimit = 1ull << 62;
-    const bool overflow_possible = t.amount.hi != 0 || dr.hi_pending >= kHiLimit ||
+    const bool overflow_possible = tn.amount_hi() != 0 || dr.hi_pending >= kHiLimit ||
                                    dr.hi_posted >= kHiLimit || cr.hi_pending >= kHiLimit ||
                                    cr.hi_posted >= kHiLimit;
     const bool limited = (dr.flags & TB_ACCOUNT_DEBITS_MUST_NOT_EXCEED_CREDITS) ||
@@ -428,13 +465,13 @@ __device__ inline uint8_t classify_after_lookup(const Tables& T, const Call<tb_t
         return kClassDone;
     }
     if (balancing_or_closing || overflow_possible) return kClassSlow;
-    if (ts_event + (uint64_t)t.timeout * TB_NS_PER_S > TB_TIMESTAMP_MAX) {
+    if (ts_event + (uint64_t)tn.timeout() * TB_NS_PER_S > TB_TIMESTAMP_MAX) {
         *status = TB_CT_OVERFLOWS_TIMEOUT;
         return kClassDone;
     }
     if (limited) return kClassSlow;
     if (f & TB_TRANSFER_PENDING) *info |= kInfoPending;
-    if (t.timeout > 0) *info |= kInfoTimeout;
+    if (tn.timeout() > 0) *info |= kInfoTimeout;
     return kClassFast;
 }
 
@@ -491,10 +528,11 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
                                             bool batch_imported, uint64_t ts_event,
                                             bool prev_linked, uint64_t* fast_ts,
                                             unsigned int* bucket_hist) {
+    const EvNarrow tn = ev_narrow(t);
     bool imported = false, post_void = false, dup = false, closable = false, hot = false;
     bool need_commit = false, chain_fast = false, ae_slow = false;
     if (c.pnt_force) c.pnt_call[k] = 0;  // (sharded calls record every update: none yet)
-    const uint16_t f = t.flags;
+    const uint16_t f = tn.flags();
     imported = (f & TB_TRANSFER_IMPORTED) != 0;
     post_void = (f & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) != 0;
     const tb_uint128_t id = t.id;
@@ -512,7 +550,7 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
         if (batch_imported != imported) {
             status = imported ? TB_CT_IMPORTED_EVENT_NOT_EXPECTED : TB_CT_IMPORTED_EVENT_EXPECTED;
             pre_done = true;
-        } else if (!imported && t.timestamp != 0) {
+        } else if (!imported && tn.timestamp() != 0) {
             status = TB_CT_TIMESTAMP_MUST_BE_ZERO;
             pre_done = true;
         } else if (!imported && (f & TB_TRANSFER_PADDING_MASK)) {
@@ -625,7 +663,7 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
             !u128_is_max(t.pending_id))
             pv_claim(c, k, t.pending_id);
         if (!c.force_replay && !pre_fail && !imported && slot != kNone) {
-            cls = classify_after_lookup(T, c, k, ts_event, t, w_slot, dr, cr, &status, &ts_out,
+            cls = classify_after_lookup(T, c, k, ts_event, t, tn, w_slot, dr, cr, &status, &ts_out,
                                         &info, &pv);
             // Linked chains (execute_create :3033-3207): a chain whose every event is FAST
             // creates every event -- tr_commit confirms that for the whole chain (commit_chain)
@@ -645,7 +683,7 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
     // A FAST event whose balance items are packed needs no per-event record: tr_commit decodes
     // the rows and amount from the items and re-probes the slot if it has to.
     const bool lean = cls == kClassFast && !pv_fast &&
-                      (c.bal_items ? item_packable(c, t.amount.lo) : c.lean_lookup != 0);
+                      (c.bal_items ? item_packable(c, tn.amount_lo()) : c.lean_lookup != 0);
     c.ev_info[k] = info | (lean ? kInfoLean : 0);
     if (!lean) {
         c.ev_slot[k] = slot == kNone ? kNone32 : uint32_t(slot);
@@ -665,14 +703,14 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
         const bool pending = (f & TB_TRANSFER_PENDING) != 0;
         if (pending) T.tr_status[row] = TB_PENDING_PENDING;  // fresh rows read TB_PENDING_NONE
         T.tr_live[row] = 1;
-        const uint64_t amount = pv_fast ? pv.amount : t.amount.lo;
+        const uint64_t amount = pv_fast ? pv.amount : tn.amount_lo();
         if (!lean) c.ev_amount[k] = amount;
         tb_create_result_t res;
         res.timestamp = ts_event;
         res.status = TB_STATUS_CREATED;
         res.reserved = 0;
         ingest_store_result(&c.results[k], res);
-        if (pending && t.timeout > 0) need_commit = true;  // expires_at index
+        if (pending && tn.timeout() > 0) need_commit = true;  // expires_at index
         if (pv_fast) {
             need_commit = true;
             if (c.bal_items && c.pair_shift) c.bal_items[k] = ~0ull;
@@ -719,7 +757,7 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
         // only writes needs no mark: every FAST delta is applied before the replay and the
         // replay's own deltas commute with them. (post/void read no balance, :4053-4300; `closed`
         // is ordered by the closable marks.)
-        const bool ovf = t.amount.hi != 0 || dr.hi_pending >= kHazardHiLimit ||
+        const bool ovf = tn.amount_hi() != 0 || dr.hi_pending >= kHazardHiLimit ||
                          dr.hi_posted >= kHazardHiLimit || cr.hi_pending >= kHazardHiLimit ||
                          cr.hi_posted >= kHazardHiLimit;
         const bool read_dr = dr.row != kNone32 &&
