@@ -415,6 +415,32 @@ def test_account_events_dense(case, monkeypatch):
         p.close()
 
 
+def test_account_events_dense_hot():
+    """The one-pass AccountEvents (ae_dense_emit's sorted touches) under config 3's skew: a
+    Zipfian hot account takes ~1 in 6 debits (hundreds of touches per 2,048-event slice), limited
+    accounts run out of credits mid-call; the log against the oracle's byte for byte."""
+    rng = np.random.default_rng(33)
+    p = Pair(account_capacity=1 << 14, transfer_capacity=1 << 17, batch_events_max=1 << 16)
+    try:
+        acc = workload.accounts(3_000, seed=8)
+        acc["flags"][1:101] |= 2
+        p.create_accounts(acc)
+        p.create_transfers(workload.funding_transfers(100, 300_000, id_offset=10_000_000))
+        paths = []
+        for step in range(3):
+            n = 30_000
+            t = workload.transfers_hot_limits(n, n_accounts=3_000, n_hot=100, seed=50 + step,
+                                              id_offset=step * n)
+            r = p.create_transfers(t, _split(n, rng, 8189))
+            paths.append(p.last_stats["ae_window"])
+            assert (r["status"] == 54).sum() > 0 or step == 0
+        assert paths == [2] * 3
+        p.compare_state()
+        assert len(p.change_events()) > 0
+    finally:
+        p.close()
+
+
 def test_hot_limits_config3_small():
     """Config 3 shape at small scale: Zipfian hot accounts with debits_must_not_exceed_credits."""
     p = Pair(account_capacity=1 << 14, transfer_capacity=1 << 16, batch_events_max=1 << 15)

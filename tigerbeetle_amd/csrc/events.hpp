@@ -378,16 +378,27 @@ struct AeSnapJob {
 __device__ inline void ae_snapshot_one(const AeSnapJob& J, uint32_t k) {
     const Tables& T = J.T;
     const Call<tb_transfer_t>& c = J.c;
-    const bool made = k < c.n && c.results[k].status == TB_STATUS_CREATED;
-    J.st.created[k] = made;
-    if (!made) return;
+    if (k >= c.n) {
+        J.st.created[k] = 0;
+        return;
+    }
+    // (the result, the row's flags and the event's account refs loaded together, before the
+    // created test: one round trip before the account rows instead of three)
     const uint64_t row = c.row_base + k;
     const tb_transfer_t& t = T.tr_rows[row];
+    const bool have_refs = c.ev_dr && c.ev_cr;
+    const uint32_t status_k = c.results[k].status;
     const uint16_t f = t.flags;
+    const uint32_t info = have_refs ? c.ev_info[k] : 0u;
+    const uint32_t edr0 = have_refs ? c.ev_dr[k] : kNone32;
+    const uint32_t ecr0 = have_refs ? c.ev_cr[k] : kNone32;
+    const bool made = status_k == TB_STATUS_CREATED;
+    J.st.created[k] = made;
+    if (!made) return;
     const bool pv = (f & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) != 0;
-    const bool refs_ok = !pv && c.ev_dr && c.ev_cr && !(c.ev_info[k] & kInfoLean);
-    const uint32_t edr = refs_ok ? c.ev_dr[k] : kNone32;
-    const uint32_t ecr = refs_ok ? c.ev_cr[k] : kNone32;
+    const bool refs_ok = !pv && have_refs && !(info & kInfoLean);
+    const uint32_t edr = refs_ok ? edr0 : kNone32;
+    const uint32_t ecr = refs_ok ? ecr0 : kNone32;
     const uint64_t dr = edr != kNone32 ? uint64_t(edr) : account_find(T, t.debit_account_id);
     const uint64_t cr = ecr != kNone32 ? uint64_t(ecr) : account_find(T, t.credit_account_id);
     const uint64_t pr = pv ? ae_transfer_row(T, t.pending_id) : kNone;
@@ -1000,6 +1011,12 @@ __device__ inline uint4 ae_sub_u32(uint4 balance, uint32_t d) {
     return ae_q(ae_u(balance) - u128(d));
 }
 
+// Record groups whose loads issue together in ae_small_emit and ae_dense_emit: every row / staged
+// word load of a batch goes out before its stores (the compiler cannot tell the log from the rows
+// it reads, so one group at a time paid a full load latency per four records). (ae_window_emit,
+// 1024 lanes at most 128 registers each, spills with a batch: it keeps one group at a time.)
+constexpr uint32_t kAeRecBatch = 4;
+
 __global__ void __launch_bounds__(kAeWinThreads) ae_window_emit(AeWindow W) {
     __shared__ uint32_t Rd[kAeWinRowsMax];    // debits_posted deltas of the events from the round on
     __shared__ uint32_t Rc[kAeWinRowsMax];    // credits_posted
@@ -1185,14 +1202,15 @@ __global__ void __launch_bounds__(kAeWinThreads) ae_window_emit(AeWindow W) {
 // created event is single-phase with an amount below 2^19 and the key space is dense enough for
 // the LDS (<= kAeWinRowsMax accounts): the staged records (stage_out's snapshot: the finished
 // AccountEvent with both accounts' final state) need only their posted balances lowered by the
-// later events' deltas. One launch of kAeSmallWgs workgroups, one per 1024 staged events; each
+// later events' deltas. One launch of kAeSmallWgs workgroups, one per 256 staged events; each
 // sums the posted deltas of the events from its own first one on into LDS (R, the accounts' later
 // deltas at its start), then resolves its 1024 events as one round of ae_window_emit (touch lists
 // in LDS) and copies the records into the log with the balances patched, four records per 1 KB
 // store. The last workgroup closes the block (length, last timestamp, order). Calls it cannot take
 // go to the general appends queued behind it (their kernels skip the calls it took).
-constexpr uint32_t kAeSmallWgs = 8;
-static_assert(kAeSmallWgs * kAeWinThreads == 8192, "one round per workgroup over the staging");
+constexpr uint32_t kAeSmallThreads = 256;
+constexpr uint32_t kAeSmallWgs = 32;  // (32 CUs of waves in flight; 8 of 1024 lanes: 35 us a call)
+static_assert(kAeSmallWgs * kAeSmallThreads == kAeAsyncMax, "one round per workgroup over the staging");
 
 struct AeSmall {
     AeStage st;
@@ -1219,19 +1237,19 @@ __device__ inline uint4 ae_add_u32(uint4 balance, uint32_t d) {
     return ae_q(ae_u(balance) + u128(d));
 }
 
-__global__ void __launch_bounds__(kAeWinThreads) ae_small_emit(AeSmall A) {
+__global__ void __launch_bounds__(kAeSmallThreads) ae_small_emit(AeSmall A) {
     __shared__ uint32_t Rd[kAeWinRowsMax];
     __shared__ uint32_t Rc[kAeWinRowsMax];
     __shared__ uint32_t head[kAeWinRowsMax];
-    __shared__ uint16_t next[2 * kAeWinThreads];
-    __shared__ uint32_t amt[kAeWinThreads];
-    __shared__ uint32_t wave_cnt[kAeWinThreads / 64];
+    __shared__ uint16_t next[2 * kAeSmallThreads];
+    __shared__ uint32_t amt[kAeSmallThreads];
+    __shared__ uint32_t wave_cnt[kAeSmallThreads / 64];
     __shared__ uint32_t before_lds, all_lds;
     __shared__ unsigned long long ts_lds[2];
     if (A.st.words[0] == A.epoch) return;  // (an event the general appends take)
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, w = blockIdx.x;
     if (w == 0 && tid == 0) A.st.words[1] = A.epoch;  // (the general appends skip)
-    for (uint32_t a = tid; a < A.rows; a += kAeWinThreads) {
+    for (uint32_t a = tid; a < A.rows; a += kAeSmallThreads) {
         Rd[a] = 0;
         Rc[a] = 0;
         head[a] = kAeWinNil;
@@ -1245,19 +1263,36 @@ __global__ void __launch_bounds__(kAeWinThreads) ae_small_emit(AeSmall A) {
     __syncthreads();
     // R: the posted deltas of the staged events from this workgroup's first one on; the created
     // events before it (the block's positions).
-    const uint32_t e0 = w * kAeWinThreads;
+    const uint32_t e0 = w * kAeSmallThreads;
     uint32_t before = 0, all = 0;
-    for (uint32_t e = tid; e < kAeAsyncMax; e += kAeWinThreads) {
-        if (!A.st.created[e]) continue;
-        all++;
-        if (e < e0) {
-            before++;
-            continue;
+    // (8 events a lane at a time, their staged words loaded unconditionally and all at once: the
+    // staging is always readable, and a load per event in sequence waited a latency each)
+    constexpr uint32_t kU = 8;
+    static_assert(kAeAsyncMax % (kAeSmallThreads * kU) == 0, "whole passes");
+    for (uint32_t eb = tid; eb < kAeAsyncMax; eb += kAeSmallThreads * kU) {
+        uint8_t made[kU];
+        uint32_t rdr[kU], rcr[kU], am[kU];
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++) {
+            const uint32_t e = eb + u * kAeSmallThreads;
+            made[u] = A.st.created[e];
+            const AeRef r = A.st.ref[e];
+            rdr[u] = r.dr_row;
+            rcr[u] = r.cr_row;
+            am[u] = ae_small_amount(A, e);
         }
-        const AeRef r = A.st.ref[e];
-        const uint32_t a = ae_small_amount(A, e);
-        atomicAdd(&Rd[r.dr_row], a);
-        atomicAdd(&Rc[r.cr_row], a);
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++) {
+            const uint32_t e = eb + u * kAeSmallThreads;
+            if (!made[u]) continue;
+            all++;
+            if (e < e0) {
+                before++;
+                continue;
+            }
+            atomicAdd(&Rd[rdr[u]], am[u]);
+            atomicAdd(&Rc[rcr[u]], am[u]);
+        }
     }
     for (int off = 32; off > 0; off >>= 1) {
         before += __shfl_xor(before, off);
@@ -1290,7 +1325,7 @@ __global__ void __launch_bounds__(kAeWinThreads) ae_small_emit(AeSmall A) {
     __syncthreads();
     uint64_t wave_pos = A.state[0] + before_lds;
     uint32_t total = 0;
-    for (uint32_t j = 0; j < kAeWinThreads / 64; j++) {
+    for (uint32_t j = 0; j < kAeSmallThreads / 64; j++) {
         const uint32_t cj = wave_cnt[j];
         wave_pos += j < wv ? cj : 0;
         total += cj;
@@ -1325,20 +1360,29 @@ __global__ void __launch_bounds__(kAeWinThreads) ae_small_emit(AeSmall A) {
     const bool credit_half = wd >= 5 && wd < 10;
     const uint32_t k = credit_half ? wd - 5 : wd;
     const uint4* recs = reinterpret_cast<const uint4*>(A.st.rec);
-    for (uint32_t j = 0; j < 16; j++) {
-        if (((bal >> (4 * j)) & 0xF) == 0) continue;  // (wave-uniform)
-        const uint32_t src = 4 * j + sub;
-        const uint32_t l0 = __shfl(later[0], src), l1 = __shfl(later[1], src);
-        const uint32_t l2 = __shfl(later[2], src), l3 = __shfl(later[3], src);
-        if (!((bal >> src) & 1)) continue;
-        const uint32_t es = e0 + (tid & ~63u) + src;
-        uint4 q = recs[uint64_t(es) * 16 + wd];
-        const uint32_t kd = A.pending ? 1 : 2, kc = A.pending ? 3 : 4;  // the patched words
-        const uint32_t l = wd >= 10 ? 0u : k == kd ? (credit_half ? l2 : l0)
-                                      : k == kc ? (credit_half ? l3 : l1) : 0u;
-        if (l) q = A.pending ? ae_add_u32(q, l) : ae_sub_u32(q, l);
-        const uint64_t at = wave_pos + uint64_t(__popcll(bal & ((1ull << src) - 1)));
-        ae_nt_store(reinterpret_cast<uint4*>(&A.log[at]) + wd, q);
+    const uint32_t kd = A.pending ? 1 : 2, kc = A.pending ? 3 : 4;  // the patched words
+    for (uint32_t j0 = 0; j0 < 16; j0 += kAeRecBatch) {
+        if (((bal >> (4 * j0)) & ((1ull << (4 * kAeRecBatch)) - 1)) == 0) continue;  // (uniform)
+        uint4 qs[kAeRecBatch];
+#pragma unroll
+        for (uint32_t u = 0; u < kAeRecBatch; u++) {
+            const uint32_t src = 4 * (j0 + u) + sub;
+            const uint32_t es = e0 + (tid & ~63u) + src;
+            qs[u] = ((bal >> src) & 1) ? recs[uint64_t(es) * 16 + wd] : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kAeRecBatch; u++) {
+            const uint32_t src = 4 * (j0 + u) + sub;
+            const uint32_t l0 = __shfl(later[0], src), l1 = __shfl(later[1], src);
+            const uint32_t l2 = __shfl(later[2], src), l3 = __shfl(later[3], src);
+            if (!((bal >> src) & 1)) continue;
+            uint4 q = qs[u];
+            const uint32_t l = wd >= 10 ? 0u : k == kd ? (credit_half ? l2 : l0)
+                                          : k == kc ? (credit_half ? l3 : l1) : 0u;
+            if (l) q = A.pending ? ae_add_u32(q, l) : ae_sub_u32(q, l);
+            const uint64_t at = wave_pos + uint64_t(__popcll(bal & ((1ull << src) - 1)));
+            ae_nt_store(reinterpret_cast<uint4*>(&A.log[at]) + wd, q);
+        }
     }
     __syncthreads();
     if (tid != 0) return;
@@ -1385,14 +1429,27 @@ __global__ void __launch_bounds__(kAeWinThreads) ae_small_emit(AeSmall A) {
 //   ae_dense_partials  per slice and balance pair (pending / posted): the slice's deltas per
 //                      account (LDS sums), and its created count
 //   ae_dense_suffix    per pair and account key: the partials summed over the later slices (i64;
-//                      refusal when a sum leaves the i32 range)
-//   ae_dense_emit      per slice: its events' later pending deltas, then posted deltas, one
-//                      round of 1024 events at a time (ae_window_emit's touch lists in LDS), and
-//                      the records from the final rows, four per 1 KB store.
+//                      refusal when a sum reaches 2^30: a later delta is then a suffix less at
+//                      most kAeDenseSlice * 2^19 = 2^30, inside the i32 range)
+//   ae_dense_later     per slice: its touches (account, event, side) sorted in registers
+//                      (block_bitonic_sort), one segmented scan of the four deltas (pending /
+//                      posted on the debit / credit side) along the sorted order gives every touch
+//                      its account's sums up to its event, the slice's suffix less those is its
+//                      later deltas; with each event's position in the block.
+//                      (Touch lists walked per event cost O(L^2) in a round's L touches of one
+//                      hot account; the sort costs the same for any key distribution.)
+//   ae_dense_records   per 256 events: the records from the final rows, four per 1 KB store
+//                      (a kernel of its own: small workgroups keep enough waves in flight for the
+//                      row loads, which the sort's 64 large workgroups did not).
 // The host checks the refusal word between the suffix and the emit; a refused call takes the
 // general appends.
-constexpr uint32_t kAeDenseRounds = 4;
-constexpr uint32_t kAeDenseSlice = kAeDenseRounds * kAeWinThreads;
+constexpr uint32_t kAeDenseSlice = 2048;
+constexpr uint32_t kAeDenseEmitThreads = 512;
+constexpr uint32_t kAeDenseEv = kAeDenseSlice / kAeDenseEmitThreads;  // events per lane
+constexpr uint32_t kAeDenseKeys = 2 * kAeDenseEv;                      // touches per lane
+constexpr uint32_t kAeDenseTixBits = 12;                               // log2(2 * kAeDenseSlice)
+static_assert(2 * kAeDenseSlice == (1u << kAeDenseTixBits), "touch index bits");
+static_assert(kAeWinRowsMax < (1u << (32 - kAeDenseTixBits)), "account row bits");
 
 struct AeTouch {
     uint32_t dr, cr;  // account rows (kNone32: the event created nothing)
@@ -1409,8 +1466,10 @@ struct AeDense {
                               // (status, 0, 0, 0)
     uint32_t* partials;       // [pair][slice][2 * rows]: debit-side then credit-side sums
     unsigned int* slice_count;  // [slices] created events
-    unsigned int* done;         // finished emit workgroups (a word of its own: zero between calls)
-    unsigned long long* slice_ts;  // [2 * slices]
+    unsigned int* done;         // finished record workgroups (a word of its own: zero between calls)
+    unsigned long long* slice_ts;  // [0] / [1]: the first / last created timestamp (~0 / 0 between calls)
+    uint4* later;               // per event, two words (ae_dense_later)
+    uint32_t* pos;              // per event: its position among the call's created events
     unsigned int* fail;       // == epoch: the call takes the general appends
     uint32_t epoch;
     tb_account_event_t* log;
@@ -1511,7 +1570,7 @@ __global__ void __launch_bounds__(kAeWinThreads) ae_dense_partials(AeDense A) {
 }
 
 // One lane per (pair, account key): partials[pair][s][key] = the sum over slices >= s (i64; a sum
-// outside the i32 range refuses the call).
+// of magnitude 2^30 or more refuses the call).
 __global__ void ae_dense_suffix(AeDense A) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t keys = 2 * A.rows;
@@ -1520,10 +1579,25 @@ __global__ void ae_dense_suffix(AeDense A) {
     uint32_t* p = A.partials + uint64_t(q) * A.slices * keys + key;
     int64_t acc = 0;
     bool wide = false;
-    for (int64_t s = int64_t(A.slices) - 1; s >= 0; s--) {
-        acc += int32_t(p[uint64_t(s) * keys]);
-        wide |= acc >= (int64_t(1) << 31) || acc < -(int64_t(1) << 31);
-        p[uint64_t(s) * keys] = uint32_t(int32_t(acc));
+    // (eight slices' loads in flight before their stores: one at a time waited a full load
+    // latency per slice)
+    constexpr int kB = 8;
+    for (int64_t s1 = int64_t(A.slices); s1 > 0; s1 -= kB) {
+        uint32_t v[kB];
+#pragma unroll
+        for (int j = 0; j < kB; j++) {
+            const int64_t s = s1 - 1 - j;
+            v[j] = s >= 0 ? p[uint64_t(s) * keys] : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < kB; j++) {
+            const int64_t s = s1 - 1 - j;
+            if (s >= 0) {
+                acc += int32_t(v[j]);
+                wide |= acc >= (int64_t(1) << 30) || acc <= -(int64_t(1) << 30);
+                p[uint64_t(s) * keys] = uint32_t(int32_t(acc));
+            }
+        }
     }
     if (wide) *A.fail = A.epoch;
 }
@@ -1540,213 +1614,261 @@ __device__ inline uint4 ae_sub_i32(uint4 balance, uint32_t d) {
     return ae_q(ae_u(balance) - u128(int64_t(int32_t(d))));  // (sign-extended: u128 wraps)
 }
 
-// Per round: the touch lists of its events, and each event's later deltas of the pair on both of
-// its accounts (ae_window_emit's procedure); R drops by the round's deltas afterwards.
+// ae_dense_later's LDS: the sort's stages, the slice's deltas by event, the later deltas by touch.
 struct AeDenseLds {
-    uint32_t Rd[kAeWinRowsMax];
-    uint32_t Rc[kAeWinRowsMax];
-    uint32_t head[kAeWinRowsMax];
-    uint16_t next[2 * kAeWinThreads];
-    uint32_t amt[kAeWinThreads];
-    uint32_t wave_cnt[2][kAeWinThreads / 64];  // (by round parity: a wave may run a round ahead)
-    unsigned long long ts[2];
+    uint32_t keys[2 * kAeDenseSlice];
+    uint32_t pe[kAeDenseSlice], po[kAeDenseSlice];
+    uint4 later[2 * kAeDenseSlice];  // (pending debit-side, credit-side; posted debit, credit)
+    uint32_t scan_f[kAeDenseEmitThreads / 64];
+    uint4 scan_v[kAeDenseEmitThreads / 64];
+    uint32_t wave_cnt[kAeDenseEv][kAeDenseEmitThreads / 64];
+    uint32_t before;
 };
-__device__ inline void ae_dense_round(AeDenseLds& L, bool valid, uint32_t dr, uint32_t cr,
-                                      uint32_t d, uint32_t later[4]) {
-    const uint32_t tid = threadIdx.x;
-    if (valid) {
-        L.next[2 * tid] = uint16_t(atomicExch(&L.head[dr], 2 * tid));
-        L.next[2 * tid + 1] = uint16_t(atomicExch(&L.head[cr], 2 * tid + 1));
-        L.amt[tid] = d;
-    }
-    __syncthreads();
-    if (valid) {
-#pragma unroll
-        for (int side = 0; side < 2; side++) {
-            const uint32_t acc = side ? cr : dr;
-            uint32_t sd = 0, sc = 0;
-            for (uint32_t nd = L.head[acc]; nd != kAeWinNil;) {
-                if ((nd >> 1) <= tid) {
-                    const uint32_t v = L.amt[nd >> 1];
-                    if (nd & 1) sc += v;
-                    else sd += v;
-                }
-                const uint32_t nx = L.next[nd];
-                nd = nx == 0xFFFFu ? kAeWinNil : nx;
-            }
-            later[2 * side] = L.Rd[acc] - sd;
-            later[2 * side + 1] = L.Rc[acc] - sc;
-        }
-    }
-    __syncthreads();
-    if (valid) {
-        L.head[dr] = kAeWinNil;
-        L.head[cr] = kAeWinNil;
-        atomicSub(&L.Rd[dr], d);
-        atomicSub(&L.Rc[cr], d);
-    }
-    __syncthreads();
+
+__device__ inline uint4 ae_add4(uint4 a, uint4 b) {
+    return make_uint4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+__device__ inline uint4 ae_shfl_up4(uint4 v, int d) {
+    return make_uint4(__shfl_up(v.x, d, 64), __shfl_up(v.y, d, 64), __shfl_up(v.z, d, 64),
+                      __shfl_up(v.w, d, 64));
 }
 
-__device__ inline void ae_dense_load_r(AeDenseLds& L, const AeDense& A, uint32_t q, uint32_t s) {
-    const uint32_t* suf = A.partials + (uint64_t(q) * A.slices + s) * 2 * A.rows;
-    for (uint32_t a = threadIdx.x; a < A.rows; a += kAeWinThreads) {
-        L.Rd[a] = suf[a];
-        L.Rc[a] = suf[A.rows + a];
-        L.head[a] = kAeWinNil;
-    }
-    __syncthreads();
-}
-
-__global__ void __launch_bounds__(kAeWinThreads) ae_dense_emit(AeDense A) {
+// Per slice: every created event's later deltas (A.later[2 e]: pending, debit account's debits /
+// credits then the credit account's; [2 e + 1]: posted) and its position among the call's created
+// events (A.pos[e]).
+__global__ void __launch_bounds__(kAeDenseEmitThreads) ae_dense_later(AeDense A) {
+    constexpr uint32_t kWaves = kAeDenseEmitThreads / 64, N = kAeDenseKeys;
+    constexpr uint32_t kTixMask = (1u << kAeDenseTixBits) - 1;
     __shared__ AeDenseLds L;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, s = blockIdx.x;
     const uint32_t e0 = s * kAeDenseSlice;
-    // created events of the earlier slices; of all (the room in the log: else nothing is written)
-    uint32_t before = 0, all = 0;
-    for (uint32_t j = tid; j < A.slices; j += kAeWinThreads) {
-        before += j < s ? A.slice_count[j] : 0;
-        all += A.slice_count[j];
+    // created events of the earlier slices
+    uint32_t before = 0;
+    for (uint32_t j = tid; j < s; j += kAeDenseEmitThreads) before += A.slice_count[j];
+    for (int off = 32; off > 0; off >>= 1) before += __shfl_xor(before, off);
+    if (tid == 0) L.before = 0;
+    __syncthreads();
+    if (lane == 0 && before) atomicAdd(&L.before, before);
+    // The slice's touches as sort keys (account row, then touch = 2 event + side; none: ~0), the
+    // deltas by event. Lane tid takes events j * kAeDenseEmitThreads + tid.
+    AeTouch t[kAeDenseEv];
+    uint32_t k[N];
+#pragma unroll
+    for (uint32_t j = 0; j < kAeDenseEv; j++) {
+        const uint32_t le = j * kAeDenseEmitThreads + tid, e = e0 + le;
+        t[j] = e < A.c.n ? A.touch[e] : AeTouch{kNone32, kNone32, 0, 0};
+        const bool valid = t[j].dr != kNone32;
+        k[2 * j] = valid ? (t[j].dr << kAeDenseTixBits) | (2 * le) : ~0u;
+        k[2 * j + 1] = valid ? (t[j].cr << kAeDenseTixBits) | (2 * le + 1) : ~0u;
+        L.pe[le] = t[j].dpe;
+        L.po[le] = t[j].dpo;
     }
-    for (int off = 32; off > 0; off >>= 1) {
-        before += __shfl_xor(before, off);
-        all += __shfl_xor(all, off);
+    block_bitonic_sort<N, kAeDenseEmitThreads>(k, L.keys);
+#pragma unroll
+    for (uint32_t m = 0; m < N; m++) L.keys[tid * N + m] = k[m];
+    __syncthreads();
+    // Segmented inclusive sums along the sorted order (a segment: one account), four deltas at
+    // once: (start flag, sums) pairs combine as (f1 | f2, f2 ? v2 : v1 + v2).
+    const uint32_t prev_key = tid ? L.keys[tid * N - 1] : ~0u;
+    bool f[N];
+    uint4 v[N];
+#pragma unroll
+    for (uint32_t m = 0; m < N; m++) {
+        const uint32_t key = k[m], pk = m ? k[m - 1] : prev_key;
+        f[m] = (tid == 0 && m == 0) || (key >> kAeDenseTixBits) != (pk >> kAeDenseTixBits);
+        v[m] = make_uint4(0, 0, 0, 0);
+        if (key != ~0u) {
+            const uint32_t tix = key & kTixMask, le = tix >> 1;
+            const uint32_t dpe = L.pe[le], dpo = L.po[le];
+            v[m] = (tix & 1) ? make_uint4(0, dpe, 0, dpo) : make_uint4(dpe, 0, dpo, 0);
+        }
+    }
+    bool F = false;
+    uint4 V = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (uint32_t m = 0; m < N; m++) {
+        V = f[m] ? v[m] : ae_add4(V, v[m]);
+        F |= f[m];
+    }
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t fo = __shfl_up(uint32_t(F), d, 64);
+        const uint4 vo = ae_shfl_up4(V, d);
+        if (lane >= uint32_t(d)) {
+            if (!F) V = ae_add4(V, vo);
+            F |= fo != 0;
+        }
+    }
+    if (lane == 63) {
+        L.scan_f[wv] = F;
+        L.scan_v[wv] = V;
+    }
+    uint32_t fx = __shfl_up(uint32_t(F), 1, 64);
+    uint4 vx = ae_shfl_up4(V, 1);
+    if (lane == 0) {
+        fx = 0;
+        vx = make_uint4(0, 0, 0, 0);
+    }
+    __syncthreads();
+    uint4 carry = make_uint4(0, 0, 0, 0);
+    for (uint32_t w = 0; w < wv; w++) carry = L.scan_f[w] ? L.scan_v[w] : ae_add4(carry, L.scan_v[w]);
+    uint4 run = fx ? vx : ae_add4(carry, vx);
+    // Every touch's later deltas: the suffix from this slice less its account's sums so far.
+    const uint32_t* suf_pe = A.partials + (uint64_t(0) * A.slices + s) * 2 * A.rows;
+    const uint32_t* suf_po = A.partials + (uint64_t(1) * A.slices + s) * 2 * A.rows;
+#pragma unroll
+    for (uint32_t m = 0; m < N; m++) {
+        run = f[m] ? v[m] : ae_add4(run, v[m]);
+        const uint32_t key = k[m];
+        if (key == ~0u) continue;
+        const uint32_t acc = key >> kAeDenseTixBits;
+        L.later[key & kTixMask] = make_uint4(suf_pe[acc] - run.x, suf_pe[A.rows + acc] - run.y,
+                                             suf_po[acc] - run.z, suf_po[A.rows + acc] - run.w);
+    }
+    uint64_t bals[kAeDenseEv];
+#pragma unroll
+    for (uint32_t j = 0; j < kAeDenseEv; j++) {
+        bals[j] = __ballot(t[j].dr != kNone32);
+        if (lane == 0) L.wave_cnt[j][wv] = uint32_t(__popcll(bals[j]));
+    }
+    __syncthreads();
+    uint32_t pos = L.before;
+#pragma unroll
+    for (uint32_t r = 0; r < kAeDenseEv; r++) {
+        const uint32_t le = r * kAeDenseEmitThreads + tid, e = e0 + le;
+        uint32_t wave_pos = pos, round_total = 0;
+        for (uint32_t j = 0; j < kWaves; j++) {
+            const uint32_t cj = L.wave_cnt[r][j];
+            wave_pos += j < wv ? cj : 0;
+            round_total += cj;
+        }
+        if (t[r].dr != kNone32) {
+            const uint4 d = L.later[2 * le], c = L.later[2 * le + 1];
+            A.later[2 * uint64_t(e)] = make_uint4(d.x, d.y, c.x, c.y);
+            A.later[2 * uint64_t(e) + 1] = make_uint4(d.z, d.w, c.z, c.w);
+            const uint32_t rank = lane ? __popcll(bals[r] & (~0ull >> (64 - lane))) : 0;
+            A.pos[e] = wave_pos + rank;
+        }
+        pos += round_total;
+    }
+}
+
+// The records: 256 lanes a workgroup, a wave's 64 events at a time (enough waves in flight to hide
+// the row loads), four records per 1 KB store; the last workgroup closes the block.
+constexpr uint32_t kAeDenseRecThreads = 256;
+
+__global__ void __launch_bounds__(kAeDenseRecThreads) ae_dense_records(AeDense A) {
+    __shared__ unsigned long long ts_lds[2];
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    // the call's created events (the room in the log: else nothing is written)
+    uint32_t all = 0;
+    for (uint32_t j = tid; j < A.slices; j += kAeDenseRecThreads) all += A.slice_count[j];
+    for (int off = 32; off > 0; off >>= 1) all += __shfl_xor(all, off);
+    if (tid == 0) {
+        ts_lds[0] = ~0ull;
+        ts_lds[1] = 0;
     }
     if (!__syncthreads_and(ae_room(A.state, A.cap, all))) {
         if (tid == 0) A.state[3] = 1;
         return;
     }
-    if (lane == 0) L.wave_cnt[0][wv] = before;
-    if (tid == 0) {
-        L.ts[0] = ~0ull;
-        L.ts[1] = 0;
-    }
     const uint64_t used = A.state[0];
-    __syncthreads();
-    uint64_t pos = used;
-    for (uint32_t j = 0; j < kAeWinThreads / 64; j++) pos += L.wave_cnt[0][j];
-    __syncthreads();
-    AeTouch t[kAeDenseRounds];
-#pragma unroll
-    for (uint32_t r = 0; r < kAeDenseRounds; r++) {
-        const uint32_t e = e0 + r * kAeWinThreads + tid;
-        t[r] = e < A.c.n ? A.touch[e] : AeTouch{kNone32, kNone32, 0, 0};
-    }
-    // pass 1: later pending deltas (kept in registers)
-    uint32_t lpe[kAeDenseRounds][4];
-    ae_dense_load_r(L, A, 0, s);
-#pragma unroll
-    for (uint32_t r = 0; r < kAeDenseRounds; r++) {
-        lpe[r][0] = lpe[r][1] = lpe[r][2] = lpe[r][3] = 0;
-        ae_dense_round(L, t[r].dr != kNone32, t[r].dr, t[r].cr, t[r].dpe, lpe[r]);
-    }
-    // pass 2: later posted deltas, and the records
-    ae_dense_load_r(L, A, 1, s);
+    const uint32_t e = blockIdx.x * kAeDenseRecThreads + tid;
+    const AeTouch t = e < A.c.n ? A.touch[e] : AeTouch{kNone32, kNone32, 0, 0};
+    const bool valid = t.dr != kNone32;
+    const uint64_t bal = __ballot(valid);
+    uint4 lpe = make_uint4(0, 0, 0, 0), lpo = make_uint4(0, 0, 0, 0);
+    uint32_t my_pos = 0;
     uint64_t ts_min = ~0ull, ts_max = 0;
+    if (valid) {
+        lpe = A.later[2 * uint64_t(e)];
+        lpo = A.later[2 * uint64_t(e) + 1];
+        my_pos = A.pos[e];
+        ae_nt_store(reinterpret_cast<uint4*>(&A.refs[used + my_pos]),
+                    make_uint4(uint32_t(A.c.row_base + e), t.dr, t.cr, 0));
+        const uint4 w3 = A.ev[uint64_t(e) * 5 + 3];
+        ts_min = ts_max = (uint64_t(w3.y) << 32) | w3.x;
+    }
+    // The records, four per 1 KB store (lane L: word L % 16 of event lane 4 j + L / 16):
+    //   0-4 / 5-9 the debit / credit account's id and balances less the later deltas,
+    //   10 timestamps, 11 the credit account's timestamp and the flags, 12-14 the event's
+    //   pending id and amounts, 15 ledger and status.
     const uint32_t wd = lane & 15, sub = lane >> 4;
     const bool credit_half = (wd >= 5 && wd < 10) || wd == 11;
     const uint32_t kw = wd < 5 ? wd : wd < 10 ? wd - 5 : 7;
+    const uint32_t ew0 = e - lane;  // the wave's first event
+    for (uint32_t j0 = 0; j0 < 16; j0 += kAeRecBatch) {
+        if (((bal >> (4 * j0)) & ((1ull << (4 * kAeRecBatch)) - 1)) == 0) continue;  // (uniform)
+        uint4 qw[kAeRecBatch], xw[kAeRecBatch];
 #pragma unroll
-    for (uint32_t r = 0; r < kAeDenseRounds; r++) {
-        const uint32_t e = e0 + r * kAeWinThreads + tid;
-        const bool valid = t[r].dr != kNone32;
-        uint32_t lpo[4] = {0, 0, 0, 0};
-        // (the round's positions: this round's ballot counts before the lists' barriers)
-        const uint64_t bal = __ballot(valid);
-        if (lane == 0) L.wave_cnt[r & 1][wv] = uint32_t(__popcll(bal));
-        ae_dense_round(L, valid, t[r].dr, t[r].cr, t[r].dpo, lpo);
-        uint64_t wave_pos = pos;
-        uint32_t round_total = 0;
-        for (uint32_t j = 0; j < kAeWinThreads / 64; j++) {
-            const uint32_t cj = L.wave_cnt[r & 1][j];
-            wave_pos += j < wv ? cj : 0;
-            round_total += cj;
-        }
-        if (valid) {
-            const uint32_t rank = lane ? __popcll(bal & (~0ull >> (64 - lane))) : 0;
-            ae_nt_store(reinterpret_cast<uint4*>(&A.refs[wave_pos + rank]),
-                        make_uint4(uint32_t(A.c.row_base + e), t[r].dr, t[r].cr, 0));
-            const uint4 w3 = A.ev[uint64_t(e) * 5 + 3];
-            const uint64_t ts = (uint64_t(w3.y) << 32) | w3.x;
-            ts_min = ts < ts_min ? ts : ts_min;
-            ts_max = ts > ts_max ? ts : ts_max;
-        }
-        // The records, four per 1 KB store (lane L: word L % 16 of event lane 4 j + L / 16):
-        //   0-4 / 5-9 the debit / credit account's id and balances less the later deltas,
-        //   10 timestamps, 11 the credit account's timestamp and the flags, 12-14 the event's
-        //   pending id and amounts, 15 ledger and status.
-        for (uint32_t j = 0; j < 16; j++) {
-            if (((bal >> (4 * j)) & 0xF) == 0) continue;  // (wave-uniform)
-            const uint32_t src = 4 * j + sub;
-            const uint32_t s_dr = __shfl(t[r].dr, src), s_cr = __shfl(t[r].cr, src);
-            const uint32_t a0 = __shfl(lpe[r][0], src), a1 = __shfl(lpe[r][1], src);
-            const uint32_t a2 = __shfl(lpe[r][2], src), a3 = __shfl(lpe[r][3], src);
-            const uint32_t b0 = __shfl(lpo[0], src), b1 = __shfl(lpo[1], src);
-            const uint32_t b2 = __shfl(lpo[2], src), b3 = __shfl(lpo[3], src);
+        for (uint32_t u = 0; u < kAeRecBatch; u++) {
+            const uint32_t src = 4 * (j0 + u) + sub;
             const bool v = (bal >> src) & 1;
-            const uint32_t es = e0 + r * kAeWinThreads + (tid & ~63u) + src;
-            uint4 qw = make_uint4(0, 0, 0, 0);
+            const uint32_t s_dr = __shfl(t.dr, src), s_cr = __shfl(t.cr, src);
+            qw[u] = make_uint4(0, 0, 0, 0);
+            xw[u] = make_uint4(0, 0, 0, 0);
             if (v && (wd < 12 || wd == 15))
-                qw = reinterpret_cast<const uint4*>(&A.T.acc_rows[credit_half ? s_cr : s_dr])[kw];
-            const uint32_t dflags = __shfl(qw.y, lane > 0 ? lane - 1 : 0);
-            if (!v) continue;
-            const uint4* ev = A.ev + uint64_t(es) * 5;
-            uint4 o = qw;
+                qw[u] = reinterpret_cast<const uint4*>(&A.T.acc_rows[credit_half ? s_cr : s_dr])[kw];
+            if (v && wd >= 10)
+                xw[u] = A.ev[uint64_t(ew0 + src) * 5 + (wd <= 11 ? 3 : wd == 15 ? 4 : wd - 12)];
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kAeRecBatch; u++) {
+            const uint32_t src = 4 * (j0 + u) + sub;
+            const uint32_t a0 = __shfl(lpe.x, src), a1 = __shfl(lpe.y, src);
+            const uint32_t a2 = __shfl(lpe.z, src), a3 = __shfl(lpe.w, src);
+            const uint32_t b0 = __shfl(lpo.x, src), b1 = __shfl(lpo.y, src);
+            const uint32_t b2 = __shfl(lpo.z, src), b3 = __shfl(lpo.w, src);
+            const uint32_t at_pos = __shfl(my_pos, src);
+            const uint4 q = qw[u], x = xw[u];
+            const uint32_t dflags = __shfl(q.y, lane > 0 ? lane - 1 : 0);
+            if (!((bal >> src) & 1)) continue;
+            uint4 o = q;
             if (wd < 10) {
                 // (words 1 / 3: debits / credits pending; 2 / 4: posted; the account's own deltas)
-                const uint32_t le = kw == 1 ? (credit_half ? a2 : a0) : kw == 3 ? (credit_half ? a3 : a1) : 0u;
+                const uint32_t le2 = kw == 1 ? (credit_half ? a2 : a0) : kw == 3 ? (credit_half ? a3 : a1) : 0u;
                 const uint32_t lo = kw == 2 ? (credit_half ? b2 : b0) : kw == 4 ? (credit_half ? b3 : b1) : 0u;
-                if (le) o = ae_sub_i32(o, le);
+                if (le2) o = ae_sub_i32(o, le2);
                 if (lo) o = ae_sub_i32(o, lo);
             } else if (wd == 10) {
-                const uint4 x = ev[3];
-                o = make_uint4(x.x, x.y, qw.z, qw.w);
+                o = make_uint4(x.x, x.y, q.z, q.w);
             } else if (wd == 11) {
-                const uint4 x = ev[3];
-                o = make_uint4(qw.z, qw.w, (dflags >> 16) | (qw.y & 0xFFFF0000u), x.z);
+                o = make_uint4(q.z, q.w, (dflags >> 16) | (q.y & 0xFFFF0000u), x.z);
             } else if (wd < 15) {
-                o = ev[wd - 12];
+                o = x;
             } else {
-                o = make_uint4(qw.x, ev[4].x, 0, 0);
+                o = make_uint4(q.x, x.x, 0, 0);
             }
-            const uint64_t at = wave_pos + uint64_t(__popcll(bal & ((1ull << src) - 1)));
-            ae_nt_store(reinterpret_cast<uint4*>(&A.log[at]) + wd, o);
+            ae_nt_store(reinterpret_cast<uint4*>(&A.log[used + at_pos]) + wd, o);
         }
-        pos += round_total;
     }
     for (int off = 32; off > 0; off >>= 1) {
         const uint64_t x = __shfl_xor(ts_min, off), y = __shfl_xor(ts_max, off);
         ts_min = x < ts_min ? x : ts_min;
         ts_max = y > ts_max ? y : ts_max;
     }
-    if (lane == 0) {
-        atomicMin(&L.ts[0], ts_min);
-        atomicMax(&L.ts[1], ts_max);
+    if (lane == 0 && bal) {
+        atomicMin(&ts_lds[0], ts_min);
+        atomicMax(&ts_lds[1], ts_max);
     }
     __syncthreads();
     if (tid != 0) return;
-    A.slice_ts[2 * s] = L.ts[0];
-    A.slice_ts[2 * s + 1] = L.ts[1];
+    if (ts_lds[1]) {
+        atomicMin(&A.slice_ts[0], ts_lds[0]);
+        atomicMax(&A.slice_ts[1], ts_lds[1]);
+    }
     __threadfence();
     if (atomicAdd(A.done, 1u) != gridDim.x - 1) return;
     __threadfence();
-    const volatile unsigned int* counts = A.slice_count;
-    const volatile unsigned long long* sts = A.slice_ts;
-    uint64_t total = 0, first = 0, last = 0;
-    bool any = false;
-    for (uint32_t j = 0; j < gridDim.x; j++) {
-        const uint32_t cj = counts[j];
-        if (!cj) continue;
-        if (!any) first = sts[2 * j];
-        any = true;
-        last = sts[2 * j + 1];
-        total += cj;
-    }
-    if (total) {
+    volatile unsigned long long* sts = A.slice_ts;
+    const uint64_t first = sts[0], last = sts[1];
+    if (all) {
         if (used && first <= A.state[1]) A.state[2] = 1;
         if (last > A.state[1]) A.state[1] = last;
-        A.state[0] = used + total;
+        A.state[0] = used + all;
     }
+    sts[0] = ~0ull;
+    sts[1] = 0;
     *A.done = 0;
 }
 

@@ -55,7 +55,7 @@ struct PulseScratch {
     uint64_t capacity = 0;  // a multiple of kPulseRun (pulse.hpp's sorted runs)
     uint64_t *keep = nullptr, *exp = nullptr, *ts = nullptr, *rows = nullptr;
     uint64_t *exp_b = nullptr, *rows_b = nullptr;
-    uint32_t* run_len = nullptr;  // two arrays of capacity / kPulseRun + 1
+    uint32_t* run_len = nullptr;  // two arrays of capacity / kPulseSortRun + 1
     unsigned long long* counters = nullptr;  // kept, candidates, earliest unexpired, expired
     unsigned int* expired = nullptr;
 };
@@ -209,6 +209,7 @@ struct tbg_ctx {
     uint32_t* sel_buf = nullptr;  // selection output for dumps / indexes (max rows)
 
     PulseScratch pulse;
+    uint32_t pulse_row_bits = 1;  // bits of a transfer row (pulse.hpp PulsePack)
     FlowScratch flow;
 
     // The account_events groove (events.hpp): AccountEvents in timestamp order + their references.
@@ -251,6 +252,8 @@ struct tbg_ctx {
     uint32_t* ae_dense_partials = nullptr;
     unsigned int* ae_dense_counts = nullptr;
     unsigned long long* ae_dense_ts = nullptr;
+    uint4* ae_dense_later = nullptr;
+    uint32_t* ae_dense_pos = nullptr;
     unsigned int* ae_dense_fail = nullptr;
     unsigned long long* ae_small_ts = nullptr;
     unsigned long long* flow_debug = nullptr;
@@ -897,13 +900,15 @@ int ensure_pulse_scratch(tbg_ctx* ctx, uint64_t count) {
                     (void*)S.rows_b, (void*)S.counters, (void*)S.run_len, (void*)S.expired})
         if (p) (void)hipFree(p);
     S = PulseScratch();
-    const uint64_t want = std::max<uint64_t>(count + count / 2, 1024);
+    // (merged runs sit at strides up to kPulseRun: a level's runs may reach past the candidates
+    // by one stride)
+    const uint64_t want = count + count / 2 + 2 * kPulseRun;
     const uint64_t cap = (want + kPulseRun - 1) / kPulseRun * kPulseRun;
     if (!(dev_alloc(ctx, &S.keep, cap, false) && dev_alloc(ctx, &S.exp, cap, false) &&
           dev_alloc(ctx, &S.ts, cap, false) && dev_alloc(ctx, &S.rows, cap, false) &&
           dev_alloc(ctx, &S.exp_b, cap, false) && dev_alloc(ctx, &S.rows_b, cap, false) &&
-          dev_alloc(ctx, &S.run_len, 2 * (cap / kPulseRun + 1), false) &&
-          dev_alloc(ctx, &S.expired, 1, true) && dev_alloc(ctx, &S.counters, 4, false)))
+          dev_alloc(ctx, &S.run_len, 2 * (cap / kPulseSortRun + 1), false) &&
+          dev_alloc(ctx, &S.expired, 1, true) && dev_alloc(ctx, &S.counters, 8, false)))
         return TBG_ENOMEM;
     S.capacity = cap;
     return 0;
@@ -1090,7 +1095,7 @@ int ae_launch_appends(tbg_ctx* ctx, uint32_t p, uint32_t epoch, bool pending) {
         AeSmall A{ctx->ae_stage[p], epoch, uint32_t(ctx->T.acc_rows_used), pending ? 1u : 0u,
                   ctx->ae_log, ctx->ae_ref, ctx->ae_words + 4, ctx->ae_small_counts,
                   ctx->ae_small_ts, ctx->ae_cap};
-        hipLaunchKernelGGL(ae_small_emit, dim3(kAeSmallWgs), dim3(kAeWinThreads), 0, st, A);
+        hipLaunchKernelGGL(ae_small_emit, dim3(kAeSmallWgs), dim3(kAeSmallThreads), 0, st, A);
     }
     AeScratch S = ctx->ae_g;
     S.state = ctx->ae_words + 4;
@@ -1274,9 +1279,13 @@ int ae_dense(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
               dev_alloc(ctx, &ctx->ae_dense_ev, 5 * cap, false) &&
               dev_alloc(ctx, &ctx->ae_dense_partials, 2 * slices * 2 * kAeWinRowsMax, false) &&
               dev_alloc(ctx, &ctx->ae_dense_counts, slices + 1, true) &&
-              dev_alloc(ctx, &ctx->ae_dense_ts, 2 * slices, false) &&
+              dev_alloc(ctx, &ctx->ae_dense_ts, 2, false) &&
+              dev_alloc(ctx, &ctx->ae_dense_later, 2 * cap, false) &&
+              dev_alloc(ctx, &ctx->ae_dense_pos, cap, false) &&
               dev_alloc(ctx, &ctx->ae_dense_fail, 1, true)))
             return TBG_ENOMEM;
+        const unsigned long long ts_init[2] = {~0ull, 0};  // (ae_dense_records: min / max)
+        HIP_TRY(ctx, hipMemcpy(ctx->ae_dense_ts, ts_init, sizeof(ts_init), hipMemcpyHostToDevice));
     }
     if (int rc = ae_join(ctx)) return rc;
     if (ctx->ae_bound + c.n > ctx->ae_cap) {
@@ -1295,6 +1304,8 @@ int ae_dense(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
     A.done = ctx->ae_dense_counts + (std::min<uint64_t>(kAeDenseMax, ctx->opt.batch_events_max) +
                                      kAeDenseSlice - 1) / kAeDenseSlice;
     A.slice_ts = ctx->ae_dense_ts;
+    A.later = ctx->ae_dense_later;
+    A.pos = ctx->ae_dense_pos;
     A.fail = ctx->ae_dense_fail;
     A.epoch = c.epoch;
     A.log = ctx->ae_log;
@@ -1311,7 +1322,9 @@ int ae_dense(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
     HIP_TRY(ctx, hipGetLastError());
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     if (ctx->h_pulse[2] == c.epoch) return 1;
-    hipLaunchKernelGGL(ae_dense_emit, dim3(A.slices), dim3(kAeWinThreads), 0, ctx->stream, A);
+    hipLaunchKernelGGL(ae_dense_later, dim3(A.slices), dim3(kAeDenseEmitThreads), 0, ctx->stream, A);
+    hipLaunchKernelGGL(ae_dense_records, dim3((c.n + kAeDenseRecThreads - 1) / kAeDenseRecThreads),
+                       dim3(kAeDenseRecThreads), 0, ctx->stream, A);
     tmark(ctx, "account_events");
     HIP_TRY(ctx, hipGetLastError());
     ctx->stats.ae_window = 2;
@@ -1358,14 +1371,15 @@ int ae_expiry(tbg_ctx* ctx, const uint64_t* rows, uint64_t m, uint64_t timestamp
 
 // A pulse's AccountEvents behind the next call (the side stream, as small create_transfers calls):
 // the expiries staged on the call's stream right after pulse_apply, the appends queued.
-int ae_expiry_async(tbg_ctx* ctx, const uint64_t* rows, uint32_t upper, uint64_t timestamp,
-                    const unsigned int* d_count) {
+int ae_expiry_snapshot_async(tbg_ctx* ctx, const uint64_t* rows, uint64_t timestamp,
+                             const unsigned int* d_count, uint32_t* epoch_out) {
     if (int rc = ae_stage_acquire(ctx)) return rc;
     const uint32_t epoch = ++ctx->epoch;
     AeExpirySnap J{ctx->T, rows, d_count, timestamp, ctx->ae_stage[ctx->ae_parity], epoch};
     hipLaunchKernelGGL(ae_expiry_snapshot, dim3(kAeAsyncMax / kBlock), dim3(kBlock), 0, ctx->stream, J);
     HIP_TRY(ctx, hipGetLastError());
-    return ae_launch_graph(ctx, upper, epoch, true);
+    *epoch_out = epoch;
+    return 0;
 }
 
 // Restores timestamp order of the log (stable) when an append broke it.
@@ -1519,7 +1533,11 @@ int stage_call_inputs(tbg_ctx* ctx, const void* events, uint64_t bytes, uint32_t
                       bool reset_scalars, bool ingest_reads_host = false) {
     const uint4* src = mapped(ctx, static_cast<const uint4*>(events), bytes);
     ctx->events_host = nullptr;
-    if (src && ingest_reads_host) {  // (tr_ingest reads the body itself and leaves the copy)
+    // (TBG_INGEST_READS_HOST=0: stage_in copies the body first -- 32 workgroups of coalesced 16-B
+    // reads, the PCIe read rate's best shape (tools/pciebench.hip) -- and tr_ingest reads HBM)
+    static const bool ingest_host_ok = !getenv("TBG_INGEST_READS_HOST") ||
+                                       atoi(getenv("TBG_INGEST_READS_HOST")) != 0;
+    if (src && ingest_reads_host && ingest_host_ok) {  // (tr_ingest reads the body and leaves the copy)
         ctx->events_host = reinterpret_cast<const tb_transfer_t*>(src);
         src = nullptr;
         bytes = 0;
@@ -1530,7 +1548,7 @@ int stage_call_inputs(tbg_ctx* ctx, const void* events, uint64_t bytes, uint32_t
               ctx->d_batch_ends, ctx->dh_batch_ts, ctx->d_batch_ts, nb,
               reset_scalars ? ctx->d_scalars : nullptr};
     const uint64_t per_block = uint64_t(kStageThreads) * kStageWords;
-    const uint32_t grid = src ? uint32_t(std::max<uint64_t>(1, (s.words + per_block - 1) / per_block)) : 1;
+    const uint32_t grid = src ? uint32_t(std::min<uint64_t>(kStageInGridMax, std::max<uint64_t>(1, (s.words + per_block - 1) / per_block))) : 1;
     hipLaunchKernelGGL(stage_in, dim3(grid), dim3(kStageThreads), 0, ctx->stream, s);
     HIP_TRY(ctx, hipGetLastError());
     return 0;
@@ -1653,6 +1671,8 @@ tbg_ctx* tbg_open(const tbg_options* options) {
         return nullptr;
     tbg_ctx* ctx = new tbg_ctx();
     ctx->opt = *options;
+    ctx->pulse_row_bits = options->transfer_capacity > 1
+                              ? uint32_t(64 - __builtin_clzll(options->transfer_capacity - 1)) : 1u;
     bool ok = hip_ok(ctx, hipSetDevice(int(options->device)), "hipSetDevice") &&
               hip_ok(ctx, hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking),
                      "hipStreamCreate");
@@ -1796,7 +1816,8 @@ void tbg_close(tbg_ctx* ctx) {
     if (ctx->ae_g_words) (void)hipFree(ctx->ae_g_words);
     for (void* q : {(void*)ctx->ae_small_counts, (void*)ctx->ae_small_ts, (void*)ctx->ae_dense_touch,
                     (void*)ctx->ae_dense_ev, (void*)ctx->ae_dense_partials,
-                    (void*)ctx->ae_dense_counts, (void*)ctx->ae_dense_ts, (void*)ctx->ae_dense_fail})
+                    (void*)ctx->ae_dense_counts, (void*)ctx->ae_dense_ts, (void*)ctx->ae_dense_fail,
+                    (void*)ctx->ae_dense_later, (void*)ctx->ae_dense_pos})
         if (q) (void)hipFree(q);
     free_ae_scratch(ctx->ae_g);
     if (ctx->ae_stream) (void)hipStreamDestroy(ctx->ae_stream);
@@ -2214,7 +2235,8 @@ struct PulseGather {
 // The expired candidates, their first min(candidates, k) in (expires_at, timestamp) order at
 // S.exp / S.rows (pulse.hpp: LDS-sorted runs, pairwise merges keeping the first k); the entries still
 // pending at S.keep; the counters on device. `out`: the counters on the host too (one sync).
-int pulse_select(tbg_ctx* ctx, uint64_t timestamp, uint32_t k, PulseGather* out) {
+int pulse_select(tbg_ctx* ctx, uint64_t timestamp, uint32_t k, PulseGather* out,
+                 bool settle = false) {
     int rc = 0;
     // The index length: known on the host since the last call or pulse (else one synchronisation).
     if (!ctx->expiry_known) {
@@ -2227,31 +2249,46 @@ int pulse_select(tbg_ctx* ctx, uint64_t timestamp, uint32_t k, PulseGather* out)
     rc = ensure_pulse_scratch(ctx, count);
     if (rc) return rc;
     PulseScratch& S = ctx->pulse;
+    uint32_t levels = 0;
     hipLaunchKernelGGL(pulse_reset_counters, dim3(1), dim3(64), 0, ctx->stream, S.counters);
     if (count) {
-        hipLaunchKernelGGL(pulse_collect, dim3(grid_for(count)), dim3(kBlock), 0, ctx->stream,
+        hipLaunchKernelGGL(pulse_collect, dim3(uint32_t((count + kPulseCollectTile - 1) / kPulseCollectTile)),
+                           dim3(kPulseCollectThreads), 0, ctx->stream,
                            ctx->T, timestamp, count, S.keep, &S.counters[0], S.exp, S.ts, S.rows,
-                           &S.counters[1], &S.counters[2]);
-        const uint32_t runs = uint32_t((count + kPulseRun - 1) / kPulseRun);
-        const uint64_t lens = S.capacity / kPulseRun + 1;
-        PulseRuns A{S.exp, S.rows, S.run_len}, B{S.exp_b, S.rows_b, S.run_len + lens};
-        hipLaunchKernelGGL(pulse_sort_chunks, dim3(runs), dim3(kPulseThreads), 0, ctx->stream, A,
-                           S.counters, k);
+                           &S.counters[1], &S.counters[2], &S.counters[4]);
+        // Sorted runs of kPulseSortRun, then pairwise merges (each keeping the first k): run r of
+        // a level at r * stride, the stride doubling up to kPulseRun.
+        const uint32_t runs = uint32_t((count + kPulseSortRun - 1) / kPulseSortRun);
+        const uint64_t lens = S.capacity / kPulseSortRun + 1;
+        const uint32_t row_bits = ctx->pulse_row_bits;
+        PulseRuns A{S.exp, S.rows, S.run_len, kPulseSortRun};
+        PulseRuns B{S.exp_b, S.rows_b, S.run_len + lens, kPulseSortRun};
+        hipLaunchKernelGGL(pulse_sort_chunks, dim3(runs), dim3(kPulseSortThreads), 0, ctx->stream, A,
+                           S.counters, k, timestamp, row_bits);
+        const PulseRuns first = A, second = B;
         uint32_t live = runs;
         bool swapped = false;
         while (live > 1) {
             const uint32_t next = (live + 1) / 2;
+            B.stride = std::min<uint32_t>(2 * A.stride, kPulseRun);
             hipLaunchKernelGGL(pulse_merge, dim3(next), dim3(kPulseThreads), 0, ctx->stream, A,
-                               live, k, B);
+                               live, k, B, S.counters, timestamp, row_bits, levels);
             std::swap(A, B);
             swapped = !swapped;
             live = next;
+            levels++;
         }
+        if (levels)  // (moves the result where the host reads it; settles a pulse)
+            hipLaunchKernelGGL(pulse_final_copy, dim3(1), dim3(kPulseThreads), 0, ctx->stream, first,
+                               second, S.counters, levels, ctx->T, S.expired, k, uint32_t(settle));
         if (swapped) {  // (the result is in the second buffers: they become the first)
             std::swap(S.exp, S.exp_b);
             std::swap(S.rows, S.rows_b);
         }
     }
+    if (settle && levels == 0)
+        hipLaunchKernelGGL(pulse_settle, dim3(1), dim3(64), 0, ctx->stream, ctx->T, S.exp, S.counters,
+                           S.expired, k);
     HIP_TRY(ctx, hipGetLastError());
     if (out) {
         unsigned long long h[3];
@@ -2344,14 +2381,12 @@ int64_t tbg_pulse(tbg_ctx* ctx, uint64_t timestamp) {
     // The scan stops with buffer_finished after batch_max values (:4969-4999): the first batch_max
     // candidates in index order expire; everything after the host's first sync stays on device.
     tmark(ctx, "-pulse");
-    int rc = pulse_select(ctx, timestamp, k, nullptr);
+    int rc = pulse_select(ctx, timestamp, k, nullptr, true);
     if (rc) return rc;
     tmark(ctx, "pulse:select");
     PulseScratch& S = ctx->pulse;
     const uint64_t count = std::min<uint64_t>(ctx->expiry_host, ctx->T.expiry_capacity);
     const uint32_t upper = uint32_t(std::min<uint64_t>(count, k));
-    hipLaunchKernelGGL(pulse_settle, dim3(1), dim3(64), 0, ctx->stream, ctx->T, S.exp, S.counters,
-                       S.expired, k);
     if (count) {
         hipLaunchKernelGGL(pulse_keep_copy, dim3(std::min<uint32_t>(grid_for(count), kMaxGrid)),
                            dim3(kBlock), 0, ctx->stream, ctx->T, S.keep, S.counters);
@@ -2361,22 +2396,30 @@ int64_t tbg_pulse(tbg_ctx* ctx, uint64_t timestamp) {
     HIP_TRY(ctx, hipGetLastError());
     tmark(ctx, "pulse:apply");
     ctx->expiry_known = false;
-    // The expiries' AccountEvents behind the next call (the side stream), or here.
-    if (ctx->ae_log && upper) {
-        if (ae_async_ok(ctx, upper) && !getenv("TBG_PULSE_AE_SYNC"))
-            rc = ae_expiry_async(ctx, S.rows, upper, timestamp, S.expired);
-        else
-            rc = ae_expiry(ctx, S.rows, upper, timestamp, nullptr, S.expired);
-    }
+    // The expiries' AccountEvents behind the next call (the side stream: the snapshot here, the
+    // appends queued after the report, so the host's queueing overlaps the report), or here.
+    const bool ae_async = ctx->ae_log && upper && ae_async_ok(ctx, upper) && !getenv("TBG_PULSE_AE_SYNC");
+    uint32_t ae_epoch = 0;
+    if (ae_async)
+        rc = ae_expiry_snapshot_async(ctx, S.rows, timestamp, S.expired, &ae_epoch);
+    else if (ctx->ae_log && upper)
+        rc = ae_expiry(ctx, S.rows, upper, timestamp, nullptr, S.expired);
     if (rc) return rc;
     // The count expired and the index's new length, written into mapped pinned memory by a kernel
     // (no copy-engine hand-off), one synchronisation.
     hipLaunchKernelGGL(pulse_report, dim3(1), dim3(64), 0, ctx->stream, S.expired, S.counters,
                        ctx->dh_pulse);
     HIP_TRY(ctx, hipGetLastError());
+    if (ae_async && (rc = ae_launch_graph(ctx, upper, ae_epoch, true))) return rc;
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     tmark(ctx, "pulse:report");
     tcollect(ctx);
+    if (getenv("TBG_PULSE_TRACE")) {  // (diagnostics: the index and candidate counts)
+        unsigned long long h[3];
+        HIP_TRY(ctx, hipMemcpy(h, S.counters, sizeof(h), hipMemcpyDeviceToHost));
+        fprintf(stderr, "pulse index=%llu candidates=%llu kept=%llu expired=%llu\n",
+                (unsigned long long)count, h[1], h[0], ctx->h_pulse[0]);
+    }
     ctx->expiry_host = ctx->h_pulse[1];
     ctx->expiry_known = true;
     return int64_t(ctx->h_pulse[0]);

@@ -13,6 +13,9 @@ namespace tbg {
 
 constexpr uint32_t kStageThreads = 256;
 constexpr uint32_t kStageWords = 4;  // 16-byte words per lane per pass (all loads issued first)
+// A body read across PCIe peaks with few requests in flight: 32 workgroups of 256 lanes read 1 MB
+// in ~23 us (45 GB/s); 256 or more workgroups took ~29 us (tools/pciebench.hip).
+constexpr uint32_t kStageInGridMax = 32;
 
 struct StageIn {
     const uint4* src;  // mapped host body, or null (the body came by hipMemcpyAsync)

@@ -24,6 +24,7 @@
 
 #include "device_common.hpp"
 #include "replay.hpp"
+#include "prims.hpp"
 
 // tr_ingest build knobs (same-box A/B builds: csrc/Makefile `variant`).
 #ifndef TBG_INGEST_EARLY_PREFETCH
@@ -2202,52 +2203,93 @@ __global__ void acc_index_repair(Tables T, IndexBuild B) {
 
 // ================================ pulse ======================================================
 
-// One lane per expires_at entry: drop entries that left the index (posted / voided / expired /
-// rolled back), collect the expired ones, and find the earliest unexpired expiry.
-__global__ void pulse_collect(Tables T, uint64_t timestamp, uint64_t count, uint64_t* keep,
-                              unsigned long long* keep_count, uint64_t* cand_expires,
-                              uint64_t* cand_ts, uint64_t* cand_row,
-                              unsigned long long* cand_count, unsigned long long* next_unexpired) {
-    const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    bool kept = false, cand = false;
-    uint64_t row = 0, expires_at = ~0ull, ts = 0;
-    if (i < count) {
-        row = T.expiry[i];
-        if (T.tr_live[row] && T.tr_status[row] == TB_PENDING_PENDING) {
-            const tb_transfer_t& p = T.tr_rows[row];
-            ts = p.timestamp;
-            expires_at = p.timestamp + (uint64_t)p.timeout * TB_NS_PER_S;
-            kept = true;
-            cand = expires_at <= timestamp;
+// kPulseCollectItems expires_at entries per lane (independent loads in flight): drop entries that
+// left the index (posted / voided / expired / rolled back), collect the expired ones, and find the
+// earliest unexpired expiry. One atomic per workgroup for each list (a counter taken once per wave
+// serialised ~5k appends at the L2 for a 300k-entry index).
+constexpr uint32_t kPulseCollectThreads = 256, kPulseCollectItems = 4;
+constexpr uint32_t kPulseCollectTile = kPulseCollectThreads * kPulseCollectItems;
+
+__global__ void __launch_bounds__(kPulseCollectThreads) pulse_collect(
+    Tables T, uint64_t timestamp, uint64_t count, uint64_t* keep, unsigned long long* keep_count,
+    uint64_t* cand_expires, uint64_t* cand_ts, uint64_t* cand_row, unsigned long long* cand_count,
+    unsigned long long* next_unexpired, unsigned long long* cand_min) {
+    constexpr uint32_t kWaves = kPulseCollectThreads / 64;
+    __shared__ uint32_t s_keep[kWaves], s_cand[kWaves];
+    __shared__ unsigned long long s_base[2], s_next[kWaves], s_min[kWaves];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint64_t base = uint64_t(blockIdx.x) * kPulseCollectTile;
+    uint64_t row[kPulseCollectItems], exp[kPulseCollectItems], ts[kPulseCollectItems];
+    bool kept[kPulseCollectItems], cand[kPulseCollectItems];
+    uint32_t nk = 0, nc = 0;
+    uint64_t next = ~0ull, first = ~0ull;
+#pragma unroll
+    for (uint32_t j = 0; j < kPulseCollectItems; j++) {
+        const uint64_t i = base + j * kPulseCollectThreads + tid;
+        row[j] = i < count ? T.expiry[i] : 0;
+        kept[j] = i < count && T.tr_live[row[j]] && T.tr_status[row[j]] == TB_PENDING_PENDING;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kPulseCollectItems; j++) {
+        exp[j] = ~0ull;
+        ts[j] = 0;
+        cand[j] = false;
+        if (kept[j]) {
+            const tb_transfer_t& p = T.tr_rows[row[j]];
+            ts[j] = p.timestamp;
+            exp[j] = p.timestamp + (uint64_t)p.timeout * TB_NS_PER_S;
+            cand[j] = exp[j] <= timestamp;
+            if (!cand[j]) next = exp[j] < next ? exp[j] : next;
+            else first = exp[j] < first ? exp[j] : first;
+        }
+        nk += kept[j];
+        nc += cand[j];
+    }
+    const uint32_t ik = wave_inclusive_u32(nk, lane), ic = wave_inclusive_u32(nc, lane);
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t o = __shfl_xor(next, off), f = __shfl_xor(first, off);
+        next = o < next ? o : next;
+        first = f < first ? f : first;
+    }
+    if (lane == 63) {
+        s_keep[wv] = ik;
+        s_cand[wv] = ic;
+    }
+    if (lane == 0) {
+        s_next[wv] = next;
+        s_min[wv] = first;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t tk = 0, tc = 0;
+        uint64_t tn = ~0ull, tf = ~0ull;
+        for (uint32_t w = 0; w < kWaves; w++) {
+            tk += s_keep[w];
+            tc += s_cand[w];
+            tn = s_next[w] < tn ? s_next[w] : tn;
+            tf = s_min[w] < tf ? s_min[w] : tf;
+        }
+        if (tf != ~0ull) atomicMin(cand_min, (unsigned long long)tf);
+        s_base[0] = tk ? atomicAdd(keep_count, (unsigned long long)tk) : 0;
+        s_base[1] = tc ? atomicAdd(cand_count, (unsigned long long)tc) : 0;
+        if (tn != ~0ull) atomicMin(next_unexpired, (unsigned long long)tn);
+    }
+    __syncthreads();
+    uint64_t pk = s_base[0] + ik - nk, pc = s_base[1] + ic - nc;
+    for (uint32_t w = 0; w < wv; w++) {
+        pk += s_keep[w];
+        pc += s_cand[w];
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kPulseCollectItems; j++) {
+        if (kept[j]) keep[pk++] = row[j];
+        if (cand[j]) {
+            cand_expires[pc] = exp[j];
+            cand_ts[pc] = ts[j];
+            cand_row[pc] = row[j];
+            pc++;
         }
     }
-    // One atomic per wave for each list (the appends of a whole wave), not one per entry: ~90k
-    // entries on one counter serialised at ~0.5 ns each.
-    const uint32_t lane = threadIdx.x & 63;
-    const uint64_t keep_mask = __ballot(kept), cand_mask = __ballot(cand);
-    const uint64_t below = (1ull << lane) - 1;
-    unsigned long long keep_base = 0, cand_base = 0;
-    const int leader = keep_mask ? __ffsll((unsigned long long)keep_mask) - 1 : 0;
-    if (keep_mask && lane == uint32_t(leader)) {
-        keep_base = atomicAdd(keep_count, (unsigned long long)__popcll(keep_mask));
-        if (cand_mask) cand_base = atomicAdd(cand_count, (unsigned long long)__popcll(cand_mask));
-    }
-    keep_base = __shfl(keep_base, leader);
-    cand_base = __shfl(cand_base, leader);
-    if (kept) keep[keep_base + __popcll(keep_mask & below)] = row;
-    if (cand) {
-        const uint64_t j = cand_base + __popcll(cand_mask & below);
-        cand_expires[j] = expires_at;
-        cand_ts[j] = ts;
-        cand_row[j] = row;
-    }
-    // The earliest unexpired expiry: a wave minimum first.
-    uint64_t next = (kept && !cand) ? expires_at : ~0ull;
-    for (int off = 32; off > 0; off >>= 1) {
-        const uint64_t o = __shfl_xor(next, off);
-        next = o < next ? o : next;
-    }
-    if (lane == 0 && next != ~0ull) atomicMin(next_unexpired, (unsigned long long)next);
 }
 
 // The timestamps of the first n sorted candidates (their index keys' second half).

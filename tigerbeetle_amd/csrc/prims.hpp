@@ -138,6 +138,137 @@ __global__ void __launch_bounds__(kScanThreads) chained_scan(uint64_t n, Op op, 
     if (tid == 0 && tile == tiles - 1) op.total(s_prefix + agg);
 }
 
+// ---- workgroup sort in registers -----------------------------------------------------------------
+//
+// A bitonic network over THREADS * N keys, N per lane, lane-major (lane t holds elements
+// t N .. t N + N - 1): strides below N are compare-exchanges between a lane's own registers, strides
+// below 64 N between lanes of a wave (one shuffle per key), and only the longer strides go through
+// LDS (`lds`: THREADS * N keys), a barrier each. Ascending; on return every lane holds its N sorted
+// elements. Every lane of the workgroup must call it (it has barriers). A key type supplies
+// sort_less(a, b) and sort_shfl_xor(k, mask).
+__device__ inline bool sort_less(uint32_t a, uint32_t b) { return a < b; }
+__device__ inline uint32_t sort_shfl_xor(uint32_t k, int mask) { return __shfl_xor(k, mask, 64); }
+__device__ inline bool sort_less(uint64_t a, uint64_t b) { return a < b; }
+__device__ inline uint64_t sort_shfl_xor(uint64_t k, int mask) { return __shfl_xor(k, mask, 64); }
+
+template <uint32_t N, uint32_t THREADS, typename K>
+__device__ void block_bitonic_sort(K (&k)[N], K* lds) {
+    static_assert((N & (N - 1)) == 0 && (THREADS & (THREADS - 1)) == 0 && THREADS >= 64);
+    constexpr uint32_t kWave = 64 * N, kTotal = N * THREADS;
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t size = 2; size <= kTotal; size <<= 1) {
+        uint32_t stride = size >> 1;
+        if (stride >= kWave) {
+#pragma unroll
+            for (uint32_t m = 0; m < N; m++) lds[tid * N + m] = k[m];
+            __syncthreads();
+            for (; stride >= kWave; stride >>= 1) {
+                for (uint32_t p = tid; p < kTotal / 2; p += THREADS) {
+                    const uint32_t lo = 2 * p - (p & (stride - 1)), hi = lo + stride;
+                    const bool ascending = (lo & size) == 0;
+                    const K a = lds[lo], b = lds[hi];
+                    if (sort_less(b, a) == ascending) {
+                        lds[lo] = b;
+                        lds[hi] = a;
+                    }
+                }
+                __syncthreads();
+            }
+#pragma unroll
+            for (uint32_t m = 0; m < N; m++) k[m] = lds[tid * N + m];
+            __syncthreads();  // (the next LDS stage rewrites the array)
+        }
+        for (; stride >= N; stride >>= 1) {
+#pragma unroll
+            for (uint32_t m = 0; m < N; m++) {
+                const K o = sort_shfl_xor(k[m], int(stride / N));
+                const uint32_t i = tid * N + m;
+                const bool keep_min = ((i & stride) == 0) == ((i & size) == 0);
+                const bool o_less = sort_less(o, k[m]);
+                if (keep_min == o_less) k[m] = o;
+            }
+        }
+        // (strides below N: unrolled over constant strides, so the keys stay in registers)
+#pragma unroll
+        for (uint32_t st = N / 2; st > 0; st >>= 1) {
+            if (st > stride) continue;
+#pragma unroll
+            for (uint32_t m = 0; m < N; m++) {
+                if (m & st) continue;
+                const uint32_t p = m | st;
+                const bool ascending = ((tid * N + m) & size) == 0;
+                if (sort_less(k[p], k[m]) == ascending) {
+                    const K x = k[m];
+                    k[m] = k[p];
+                    k[p] = x;
+                }
+            }
+        }
+    }
+}
+
+// The same contract by merging: every lane sorts its N keys in registers (a bitonic network, no
+// communication), then log2(THREADS) rounds merge pairs of sorted runs through LDS -- each lane
+// finds where its N outputs start by a merge-path binary search and merges them into registers,
+// one barrier before and after the write-back. Keys must be distinct.
+template <uint32_t N, typename K>
+__device__ inline void lane_sort(K (&k)[N]) {
+#pragma unroll
+    for (uint32_t size = 2; size <= N; size <<= 1)
+#pragma unroll
+        for (uint32_t st = size >> 1; st > 0; st >>= 1)
+#pragma unroll
+            for (uint32_t m = 0; m < N; m++) {
+                if (m & st) continue;
+                const uint32_t p = m | st;
+                const bool ascending = (m & size) == 0;
+                if (sort_less(k[p], k[m]) == ascending) {
+                    const K x = k[m];
+                    k[m] = k[p];
+                    k[p] = x;
+                }
+            }
+}
+
+template <uint32_t N, uint32_t THREADS, typename K>
+__device__ void block_merge_sort(K (&k)[N], K* lds) {
+    constexpr uint32_t kTotal = N * THREADS;
+    const uint32_t tid = threadIdx.x;
+    lane_sort<N>(k);
+#pragma unroll
+    for (uint32_t m = 0; m < N; m++) lds[tid * N + m] = k[m];
+    __syncthreads();
+    for (uint32_t L = N; L < kTotal; L <<= 1) {
+        const uint32_t o0 = tid * N, base = o0 & ~(2 * L - 1), d = o0 - base;
+        const K* A = lds + base;
+        const K* B = lds + base + L;
+        uint32_t lo = d > L ? d - L : 0, hi = d < L ? d : L;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (sort_less(B[d - 1 - mid], A[mid])) hi = mid;
+            else lo = mid + 1;
+        }
+        uint32_t i = lo, j = d - lo;
+        K a = A[i < L ? i : L - 1], b = B[j < L ? j : L - 1];
+#pragma unroll
+        for (uint32_t m = 0; m < N; m++) {
+            const bool take_a = j >= L || (i < L && sort_less(a, b));
+            k[m] = take_a ? a : b;
+            if (take_a) {
+                i++;
+                if (i < L) a = A[i];
+            } else {
+                j++;
+                if (j < L) b = B[j];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t m = 0; m < N; m++) lds[o0 + m] = k[m];
+        __syncthreads();
+    }
+}
+
 // Ops.
 
 // u8 flags -> the indices of the nonzero ones, in order; the count to *count.

@@ -7,10 +7,11 @@
 // batch_max values, and pulse_next_timestamp becomes the last one's expiry). Here pulse_collect
 // (kernels.hpp) gathers the expired candidates (expires_at, row) -- rows are appended in timestamp
 // order, so (expires_at, row) orders exactly as (expires_at, timestamp) -- and:
-//   * pulse_sort_chunks sorts each run of kPulseRun candidates in LDS (bitonic, 128 KB) and keeps
-//     its first k (k = the batch);
-//   * pulse_merge merges the sorted runs pairwise, keeping only the first k of each pair (merge
-//     path: every lane finds its diagonal by binary search, then merges its outputs);
+//   * pulse_sort_chunks sorts each run of kPulseSortRun candidates (prims.hpp block_bitonic_sort:
+//     4 keys per lane in registers, shuffles within a wave, LDS across waves; one-word keys when
+//     the candidates' expiry span allows, PulsePack) and keeps its first k (k = the batch);
+//   * pulse_merge merges the sorted runs pairwise, keeping only the first k of each pair (every
+//     element's rank: its index plus a binary search in the other run, staged in LDS);
 // ceil(log2(runs)) merge rounds leave the first min(candidates, k) in order. pulse_settle then
 // sets the index's new length and pulse_next_timestamp on device, pulse_keep_copy compacts the
 // index, pulse_apply expires the selected rows.
@@ -24,17 +25,22 @@
 #pragma once
 
 #include "kernels.hpp"
+#include "prims.hpp"
 
 namespace tbg {
 
-constexpr uint32_t kPulseRun = 8192;      // candidates per LDS-sorted run (the batch is <= this)
-constexpr uint32_t kPulseThreads = 1024;
+constexpr uint32_t kPulseRun = 8192;         // the longest merged run (the batch is <= this)
+constexpr uint32_t kPulseThreads = 1024;     // (pulse_merge)
+constexpr uint32_t kPulseSortRun = 2048;     // candidates per sorted run (pulse_sort_chunks)
+constexpr uint32_t kPulseSortThreads = 512;
+constexpr uint32_t kPulseSortItems = kPulseSortRun / kPulseSortThreads;
 
-// Sorted runs of (expires_at, row): run r at [r * kPulseRun, r * kPulseRun + len[r]).
+// Sorted runs of (expires_at, row): run r at [r * stride, r * stride + len[r]).
 struct PulseRuns {
     uint64_t* exp;
     uint64_t* row;
     uint32_t* len;
+    uint32_t stride;
 };
 
 __device__ inline bool pulse_less(uint64_t ea, uint64_t ra, uint64_t eb, uint64_t rb) {
@@ -47,100 +53,279 @@ __global__ void pulse_reset_counters(unsigned long long* counters) {
         counters[1] = 0;      // candidates
         counters[2] = ~0ull;  // earliest unexpired expiry
         counters[3] = 0;      // expired (pulse_settle)
+        counters[4] = ~0ull;  // earliest candidate expiry
     }
 }
 
-// One workgroup per run: the run's candidates sorted in place, truncated to the first k.
-__global__ void __launch_bounds__(kPulseThreads) pulse_sort_chunks(PulseRuns R,
-                                                                  const unsigned long long* counters,
-                                                                  uint32_t k) {
-    __shared__ uint64_t se[kPulseRun];
-    __shared__ uint64_t sr[kPulseRun];
+// A candidate's sort key: (expires_at, row).
+struct PulseKey {
+    uint64_t e;
+    uint32_t r, pad;
+};
+__device__ inline bool sort_less(const PulseKey& a, const PulseKey& b) {
+    return a.e < b.e || (a.e == b.e && a.r < b.r);
+}
+__device__ inline PulseKey sort_shfl_xor(const PulseKey& k, int mask) {
+    return PulseKey{__shfl_xor(k.e, mask, 64), __shfl_xor(k.r, mask, 64), 0};
+}
+
+// Candidates expire at or before the pulse's timestamp and after the earliest candidate expiry
+// (counters[4], pulse_collect): when that span fits, (expires_at - earliest) << row_bits | row is
+// one u64 that orders as (expires_at, row) -- the sorts and merges move and compare one 8-byte
+// word (a third of the LDS traffic and shuffles of the two-word key, measured 3x faster:
+// tools/sortbench.hip); else they take the two-word key.
+struct PulsePack {
+    uint64_t base;
+    uint32_t row_bits;
+    bool packed;
+    __device__ uint64_t key(uint64_t e, uint64_t r) const { return ((e - base) << row_bits) | r; }
+};
+__device__ inline PulsePack pulse_pack(const unsigned long long* counters, uint64_t timestamp,
+                                       uint32_t row_bits) {
+    const uint64_t lo = counters[4];
+    const uint64_t span = timestamp >= lo ? timestamp - lo : ~0ull;
+    return PulsePack{lo, row_bits, lo != ~0ull && (span >> (63 - row_bits)) == 0};
+}
+
+// A run of candidates sorted in one workgroup (kPulseSortRun keys, 4 per lane, prims.hpp
+// block_bitonic_sort), truncated to the first k, in place.
+template <typename K, typename Pack, typename Unpack>
+__device__ void pulse_sort_run(PulseRuns R, uint64_t base, uint32_t n, uint32_t k, K* lds, K none,
+                               Pack pack, Unpack unpack) {
     const uint32_t tid = threadIdx.x;
+    K key[kPulseSortItems];
+#pragma unroll
+    for (uint32_t m = 0; m < kPulseSortItems; m++) {  // (any placement: coalesced loads)
+        const uint32_t i = m * kPulseSortThreads + tid;
+        key[m] = i < n ? pack(R.exp[base + i], R.row[base + i]) : none;
+    }
+    block_bitonic_sort<kPulseSortItems, kPulseSortThreads>(key, lds);
+#pragma unroll
+    for (uint32_t m = 0; m < kPulseSortItems; m++) lds[tid * kPulseSortItems + m] = key[m];
+    __syncthreads();
+    const uint32_t m_out = n < k ? n : k;
+    for (uint32_t i = tid; i < m_out; i += kPulseSortThreads) unpack(lds[i], &R.exp[base + i], &R.row[base + i]);
+}
+
+__global__ void __launch_bounds__(kPulseSortThreads) pulse_sort_chunks(PulseRuns R,
+                                                                      const unsigned long long* counters,
+                                                                      uint32_t k, uint64_t timestamp,
+                                                                      uint32_t row_bits) {
+    __shared__ union {
+        uint64_t u[kPulseSortRun];
+        PulseKey p[kPulseSortRun];
+    } lds;
     const uint64_t C = counters[1];
-    const uint64_t base = uint64_t(blockIdx.x) * kPulseRun;
+    const uint64_t base = uint64_t(blockIdx.x) * kPulseSortRun;
     if (base >= C) {
-        if (tid == 0) R.len[blockIdx.x] = 0;
+        if (threadIdx.x == 0) R.len[blockIdx.x] = 0;
         return;
     }
-    const uint32_t n = uint32_t(C - base < kPulseRun ? C - base : kPulseRun);
-    for (uint32_t i = tid; i < kPulseRun; i += kPulseThreads) {
-        se[i] = i < n ? R.exp[base + i] : ~0ull;
-        sr[i] = i < n ? R.row[base + i] : ~0ull;
+    const uint32_t n = uint32_t(C - base < kPulseSortRun ? C - base : kPulseSortRun);
+    const PulsePack P = pulse_pack(counters, timestamp, row_bits);
+    if (P.packed) {
+        const uint64_t mask = (1ull << row_bits) - 1;
+        pulse_sort_run<uint64_t>(
+            R, base, n, k, lds.u, ~0ull, [&](uint64_t e, uint64_t r) { return P.key(e, r); },
+            [&](uint64_t v, uint64_t* e, uint64_t* r) {
+                *e = P.base + (v >> row_bits);
+                *r = v & mask;
+            });
+    } else {
+        pulse_sort_run<PulseKey>(
+            R, base, n, k, lds.p, PulseKey{~0ull, ~0u, 0},
+            [](uint64_t e, uint64_t r) { return PulseKey{e, uint32_t(r), 0}; },
+            [](const PulseKey& v, uint64_t* e, uint64_t* r) {
+                *e = v.e;
+                *r = v.r;
+            });
     }
-    __syncthreads();
-    for (uint32_t size = 2; size <= kPulseRun; size <<= 1) {
-        for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
-            for (uint32_t t = tid; t < kPulseRun / 2; t += kPulseThreads) {
-                const uint32_t lo = 2 * t - (t & (stride - 1)), hi = lo + stride;
-                const bool ascending = (lo & size) == 0;
-                const uint64_t el = se[lo], rl = sr[lo], eh = se[hi], rh = sr[hi];
-                if (pulse_less(eh, rh, el, rl) == ascending) {
-                    se[lo] = eh;
-                    sr[lo] = rh;
-                    se[hi] = el;
-                    sr[hi] = rl;
-                }
-            }
-            __syncthreads();
-        }
-    }
-    const uint32_t m = n < k ? n : k;
-    for (uint32_t i = tid; i < m; i += kPulseThreads) {
-        R.exp[base + i] = se[i];
-        R.row[base + i] = sr[i];
-    }
-    if (tid == 0) R.len[blockIdx.x] = m;
+    if (threadIdx.x == 0) R.len[blockIdx.x] = n < k ? n : k;
 }
 
 // Runs 2r and 2r + 1 of `in` (runs_in of them) -> run r of `out`: the first min(k, sum) in order.
-__global__ void __launch_bounds__(kPulseThreads) pulse_merge(PulseRuns in, uint32_t runs_in,
-                                                            uint32_t k, PulseRuns out) {
-    const uint32_t r = blockIdx.x, tid = threadIdx.x;
-    const uint32_t a = 2 * r, b = 2 * r + 1;
-    const uint32_t la = a < runs_in ? in.len[a] : 0, lb = b < runs_in ? in.len[b] : 0;
-    const uint32_t L = la + lb < k ? la + lb : k;
-    const uint64_t* ae = in.exp + uint64_t(a) * kPulseRun;
-    const uint64_t* ar = in.row + uint64_t(a) * kPulseRun;
-    const uint64_t* be = in.exp + uint64_t(b) * kPulseRun;
-    const uint64_t* br = in.row + uint64_t(b) * kPulseRun;
-    uint64_t* oe = out.exp + uint64_t(r) * kPulseRun;
-    uint64_t* orow = out.row + uint64_t(r) * kPulseRun;
-    const uint32_t per = (L + kPulseThreads - 1) / kPulseThreads;
-    const uint32_t d0 = tid * per, d1 = d0 + per < L ? d0 + per : L;
-    if (d0 < d1) {
-        // The number of the first d0 outputs taken from a: the smallest i with a[i] after
-        // b[d0 - 1 - i] (keys are distinct: rows are).
-        uint32_t lo = d0 > lb ? d0 - lb : 0, hi = d0 < la ? d0 : la;
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi) >> 1;
-            const uint32_t j = d0 - 1 - mid;
-            if (pulse_less(be[j], br[j], ae[mid], ar[mid])) hi = mid;
-            else lo = mid + 1;
+// Every element's output position is its index plus the number of the other run's keys before it
+// (keys are distinct: rows are), by binary search in the other run staged in LDS. A lane holds its
+// kPulseMergeItems elements of each run in registers: every global load of a phase is in flight at
+// once, and so are its searches' LDS reads (one element at a time waited a load latency each).
+constexpr uint32_t kPulseMergeItems = kPulseRun / kPulseThreads;
+
+template <typename K, typename Pack>
+__device__ void pulse_merge_pair(PulseRuns in, uint32_t a, uint32_t b, uint32_t la, uint32_t lb,
+                                 uint32_t L, PulseRuns out, uint32_t r, K* other, Pack pack) {
+    const uint32_t tid = threadIdx.x;
+    uint64_t* oe = out.exp + uint64_t(r) * out.stride;
+    uint64_t* orow = out.row + uint64_t(r) * out.stride;
+    const uint64_t* ae = in.exp + uint64_t(a) * in.stride;
+    const uint64_t* ar = in.row + uint64_t(a) * in.stride;
+    const uint64_t* be = in.exp + uint64_t(b) * in.stride;
+    const uint64_t* br = in.row + uint64_t(b) * in.stride;
+    uint64_t xa_e[kPulseMergeItems], xa_r[kPulseMergeItems], xb_e[kPulseMergeItems], xb_r[kPulseMergeItems];
+#pragma unroll
+    for (uint32_t j = 0; j < kPulseMergeItems; j++) {
+        const uint32_t i = j * kPulseThreads + tid;
+        xa_e[j] = i < la ? ae[i] : 0;
+        xa_r[j] = i < la ? ar[i] : 0;
+        xb_e[j] = i < lb ? be[i] : 0;
+        xb_r[j] = i < lb ? br[i] : 0;
+    }
+    for (uint32_t phase = 0; phase < 2; phase++) {
+        const uint32_t lm = phase ? lb : la, lo = phase ? la : lb;
+        if (phase) __syncthreads();  // (phase 0's searches are done with the LDS copy)
+#pragma unroll
+        for (uint32_t j = 0; j < kPulseMergeItems; j++) {
+            const uint32_t i = j * kPulseThreads + tid;
+            if (i < lo) other[i] = phase ? pack(xa_e[j], xa_r[j]) : pack(xb_e[j], xb_r[j]);
         }
-        uint32_t i = lo, j = d0 - lo;
-        for (uint32_t d = d0; d < d1; d++) {
-            const bool take_a = j >= lb || (i < la && pulse_less(ae[i], ar[i], be[j], br[j]));
-            if (take_a) {
-                oe[d] = ae[i];
-                orow[d] = ar[i];
-                i++;
-            } else {
-                oe[d] = be[j];
-                orow[d] = br[j];
-                j++;
+        __syncthreads();
+        const uint32_t lim = lm < L ? lm : L;  // (an element at index >= L lands at >= L)
+        uint32_t top = 0;
+        if (lo) top = 1u << (31 - __builtin_clz(lo));
+        K x[kPulseMergeItems];
+        uint32_t pos[kPulseMergeItems];
+#pragma unroll
+        for (uint32_t j = 0; j < kPulseMergeItems; j++) {
+            x[j] = phase ? pack(xb_e[j], xb_r[j]) : pack(xa_e[j], xa_r[j]);
+            pos[j] = 0;
+        }
+        for (uint32_t step = top; step > 0; step >>= 1)
+#pragma unroll
+            for (uint32_t j = 0; j < kPulseMergeItems; j++)
+                if (pos[j] + step <= lo && sort_less(other[pos[j] + step - 1], x[j])) pos[j] += step;
+#pragma unroll
+        for (uint32_t j = 0; j < kPulseMergeItems; j++) {
+            const uint32_t i = j * kPulseThreads + tid, p = i + pos[j];
+            if (i < lim && p < L) {
+                oe[p] = phase ? xb_e[j] : xa_e[j];
+                orow[p] = phase ? xb_r[j] : xa_r[j];
             }
         }
     }
-    if (tid == 0) out.len[r] = L;
+}
+
+// The one-word keys' merge: both runs staged in LDS (2 x 64 KB), every lane finds where its
+// kPulseMergeItems outputs start on the merge path (one binary search) and merges them from LDS.
+// (Ranking every element by its own binary search costs eight random-address searches per lane:
+// bank conflicts made the merge LDS-bound, ~11 us a level.)
+__device__ void pulse_merge_path(PulseRuns in, uint32_t a, uint32_t b, uint32_t la, uint32_t lb,
+                                 uint32_t L, PulseRuns out, uint32_t r, uint64_t* A, uint64_t* B,
+                                 const PulsePack& P) {
+    const uint32_t tid = threadIdx.x;
+    const uint64_t* ae = in.exp + uint64_t(a) * in.stride;
+    const uint64_t* ar = in.row + uint64_t(a) * in.stride;
+    const uint64_t* be = in.exp + uint64_t(b) * in.stride;
+    const uint64_t* br = in.row + uint64_t(b) * in.stride;
+    uint64_t va[kPulseMergeItems], vb[kPulseMergeItems];
+#pragma unroll
+    for (uint32_t j = 0; j < kPulseMergeItems; j++) {
+        const uint32_t i = j * kPulseThreads + tid;
+        va[j] = i < la ? P.key(ae[i], ar[i]) : 0;
+        vb[j] = i < lb ? P.key(be[i], br[i]) : 0;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kPulseMergeItems; j++) {
+        const uint32_t i = j * kPulseThreads + tid;
+        if (i < la) A[i] = va[j];
+        if (i < lb) B[i] = vb[j];
+    }
+    __syncthreads();
+    const uint32_t d = tid * kPulseMergeItems;
+    if (d >= L) return;
+    // the number of A's keys among the first d outputs: the smallest i with A[i] after B[d-1-i]
+    uint32_t lo = d > lb ? d - lb : 0, hi = d < la ? d : la;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (B[d - 1 - mid] < A[mid]) hi = mid;
+        else lo = mid + 1;
+    }
+    uint32_t i = lo, j = d - lo;
+    uint64_t x = i < la ? A[i] : ~0ull, y = j < lb ? B[j] : ~0ull;
+    uint64_t* oe = out.exp + uint64_t(r) * out.stride;
+    uint64_t* orow = out.row + uint64_t(r) * out.stride;
+    const uint64_t mask = (1ull << P.row_bits) - 1;
+#pragma unroll
+    for (uint32_t m = 0; m < kPulseMergeItems; m++) {
+        const uint32_t o = d + m;
+        if (o >= L) break;
+        const bool take_a = x < y;  // (distinct keys; an exhausted run reads as ~0)
+        const uint64_t v = take_a ? x : y;
+        oe[o] = P.base + (v >> P.row_bits);
+        orow[o] = v & mask;
+        if (take_a) {
+            i++;
+            x = i < la ? A[i] : ~0ull;
+        } else {
+            j++;
+            y = j < lb ? B[j] : ~0ull;
+        }
+    }
+}
+
+// The merge levels past the candidates' own runs (the host launches levels for the index length,
+// an upper bound of the candidate count) do nothing: pulse_final_copy moves the result to the
+// buffer the host expects after all levels.
+__device__ inline uint32_t pulse_live_runs(const unsigned long long* counters) {
+    return uint32_t((counters[1] + kPulseSortRun - 1) / kPulseSortRun);
+}
+__device__ inline uint32_t pulse_levels(uint32_t live) {
+    return live <= 1 ? 0u : 32u - __builtin_clz(live - 1);  // ceil(log2(live))
+}
+
+__global__ void __launch_bounds__(kPulseThreads) pulse_merge(PulseRuns in, uint32_t runs_in,
+                                                            uint32_t k, PulseRuns out,
+                                                            const unsigned long long* counters,
+                                                            uint64_t timestamp, uint32_t row_bits,
+                                                            uint32_t level) {
+    if (level >= pulse_levels(pulse_live_runs(counters))) return;
+    __shared__ union {
+        uint64_t u[2][kPulseRun];
+        PulseKey p[kPulseRun];
+    } lds;
+    const uint32_t r = blockIdx.x;
+    const uint32_t a = 2 * r, b = 2 * r + 1;
+    const uint32_t la = a < runs_in ? in.len[a] : 0, lb = b < runs_in ? in.len[b] : 0;
+    const uint32_t L = la + lb < k ? la + lb : k;
+    if (threadIdx.x == 0) out.len[r] = L;
+    if (L == 0) return;
+    const PulsePack P = pulse_pack(counters, timestamp, row_bits);
+    if (P.packed)
+        pulse_merge_path(in, a, b, la, lb, L, out, r, lds.u[0], lds.u[1], P);
+    else
+        pulse_merge_pair<PulseKey>(in, a, b, la, lb, L, out, r, lds.p,
+                                   [](uint64_t e, uint64_t rw) { return PulseKey{e, uint32_t(rw), 0}; });
+}
+
+// After `levels` merge launches the host reads the result from the first buffers when `levels` is
+// even, else from the second: when the levels that ran leave it in the other one, run 0 moves.
+// Then pulse_settle's work (one launch less).
+__device__ void pulse_settle_one(Tables T, const uint64_t* exp, unsigned long long* counters,
+                                 unsigned int* expired_out, uint32_t k);
+
+__global__ void __launch_bounds__(kPulseThreads) pulse_final_copy(PulseRuns first, PulseRuns second,
+                                                                 unsigned long long* counters,
+                                                                 uint32_t levels, Tables T,
+                                                                 unsigned int* expired_out,
+                                                                 uint32_t k, uint32_t settle) {
+    const uint32_t ran = pulse_levels(pulse_live_runs(counters));
+    const PulseRuns dst = (levels & 1) ? second : first;
+    if ((ran & 1) != (levels & 1)) {
+        const PulseRuns src = (ran & 1) ? second : first;
+        const uint32_t n = src.len[0];
+        for (uint32_t i = threadIdx.x; i < n; i += kPulseThreads) {
+            dst.exp[i] = src.exp[i];
+            dst.row[i] = src.row[i];
+        }
+        if (threadIdx.x == 0) dst.len[0] = n;
+        __syncthreads();
+    }
+    if (settle && threadIdx.x == 0) pulse_settle_one(T, dst.exp, counters, expired_out, k);
 }
 
 // After the selection (the first min(candidates, k) in order at exp / rows): the number expired,
 // the index's new length (the entries still pending) and pulse_next_timestamp -- the k-th expiry
 // when the scan filled its batch, else the earliest unexpired one (timestamp_max if none).
-__global__ void pulse_settle(Tables T, const uint64_t* exp, unsigned long long* counters,
-                             unsigned int* expired_out, uint32_t k) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+__device__ void pulse_settle_one(Tables T, const uint64_t* exp, unsigned long long* counters,
+                                 unsigned int* expired_out, uint32_t k) {
     const uint64_t C = counters[1];
     const uint64_t expired = C < k ? C : k;
     uint64_t next = counters[2] == ~0ull ? TB_TIMESTAMP_MAX : counters[2];
@@ -149,6 +334,10 @@ __global__ void pulse_settle(Tables T, const uint64_t* exp, unsigned long long* 
     T.scalars->expiry_count = counters[0];
     counters[3] = expired;
     *expired_out = uint32_t(expired);
+}
+__global__ void pulse_settle(Tables T, const uint64_t* exp, unsigned long long* counters,
+                             unsigned int* expired_out, uint32_t k) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) pulse_settle_one(T, exp, counters, expired_out, k);
 }
 
 // A sharded call's recorded updates for the caller (tbg_pnt_ops): event k's flag.
