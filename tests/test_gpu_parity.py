@@ -458,6 +458,42 @@ def test_hot_limits_config3_small():
         p.close()
 
 
+@pytest.mark.parametrize("registered", [True, False], ids=["registered", "pageable"])
+def test_small_calls_alternating_with_pulses(registered):
+    """The round-3 fault's shape (config 4's single-batch commits): small calls whose
+    AccountEvents appends run on the side stream behind the next call, alternating with pulses
+    whose expiries touch the same few accounts while those appends are in flight (the staging
+    buffers reused two calls back, the pulse's own staged expiries between them); the log and
+    every row against the oracle."""
+    rng = np.random.default_rng(13)
+    p = Pair(account_capacity=1 << 10, transfer_capacity=1 << 19, batch_events_max=8189,
+             pulse_batch_max=8190, registered=registered)
+    try:
+        n_acc = 64  # (every call and every pulse touch the same accounts)
+        p.create_accounts(workload.accounts(n_acc, seed=13))
+        pending, seen = np.zeros(0, dtype=np.uint64), np.zeros(0, dtype=np.uint64)
+        resolved = np.zeros(0, dtype=np.uint64)
+        offset = 0
+        for step in range(40):
+            n = 8189 if step % 3 == 0 else int(rng.integers(500, 8189))
+            t = workload.transfers_two_phase(n, n_acc, seed=300 + step, id_offset=offset,
+                                             prior_pending_ids=pending, prior_ids=seen,
+                                             prior_resolved_ids=resolved, n_limited=0)
+            offset += n
+            r = p.create_transfers(t, [n])
+            created = r["status"] == 0xFFFFFFFF
+            is_pending = (t["flags"] & 2) != 0
+            pv = (t["flags"] & 12) != 0
+            pending = np.concatenate([pending, t["id"][created & is_pending, 0]])[-8_000:]
+            resolved = np.concatenate([resolved, t["pending_id"][created & pv, 0]])[-8_000:]
+            seen = np.concatenate([seen, t["id"][:, 0]])[-20_000:]
+            p.tick(int(rng.integers(1, 3)) * NS_PER_S)
+        p.compare_state()
+        assert len(p.change_events()) > 0
+    finally:
+        p.close()
+
+
 def test_two_phase_config4_small():
     """Config 4 shape: pending with timeouts, post/void, linked chains with failures, resubmits,
     pulses."""

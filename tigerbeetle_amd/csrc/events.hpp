@@ -1444,7 +1444,7 @@ __global__ void __launch_bounds__(kAeSmallThreads) ae_small_emit(AeSmall A) {
 // The host checks the refusal word between the suffix and the emit; a refused call takes the
 // general appends.
 constexpr uint32_t kAeDenseSlice = 2048;
-constexpr uint32_t kAeDenseEmitThreads = 512;
+constexpr uint32_t kAeDenseEmitThreads = 1024;
 constexpr uint32_t kAeDenseEv = kAeDenseSlice / kAeDenseEmitThreads;  // events per lane
 constexpr uint32_t kAeDenseKeys = 2 * kAeDenseEv;                      // touches per lane
 constexpr uint32_t kAeDenseTixBits = 12;                               // log2(2 * kAeDenseSlice)

@@ -1533,8 +1533,11 @@ int stage_call_inputs(tbg_ctx* ctx, const void* events, uint64_t bytes, uint32_t
                       bool reset_scalars, bool ingest_reads_host = false) {
     const uint4* src = mapped(ctx, static_cast<const uint4*>(events), bytes);
     ctx->events_host = nullptr;
-    // (TBG_INGEST_READS_HOST=0: stage_in copies the body first -- 32 workgroups of coalesced 16-B
-    // reads, the PCIe read rate's best shape (tools/pciebench.hip) -- and tr_ingest reads HBM)
+    // TBG_INGEST_READS_HOST=0: stage_in copies the body first -- 32 workgroups of coalesced 16-B
+    // reads, the PCIe read rate's best shape (45 GB/s, tools/pciebench.hip) -- and tr_ingest reads
+    // HBM. A commit without AccountEvents took 55-56 us that way against 58-60 with tr_ingest
+    // reading its events across PCIe itself (27 GB/s: one event's 128 B per lane); with
+    // AccountEvents (the drop-in's case) 70-77 against 70-72, so the direct reads stay the default.
     static const bool ingest_host_ok = !getenv("TBG_INGEST_READS_HOST") ||
                                        atoi(getenv("TBG_INGEST_READS_HOST")) != 0;
     if (src && ingest_reads_host && ingest_host_ok) {  // (tr_ingest reads the body and leaves the copy)
