@@ -1602,6 +1602,13 @@ __global__ void ae_dense_suffix(AeDense A) {
     if (wide) *A.fail = A.epoch;
 }
 
+__global__ void ae_dense_ts_init(unsigned long long* ts) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        ts[0] = ~0ull;
+        ts[1] = 0;
+    }
+}
+
 // The refusal word for the host (mapped pinned memory).
 __global__ void ae_dense_report(const unsigned int* fail, unsigned long long* out) {
     if (threadIdx.x == 0 && blockIdx.x == 0) {

@@ -56,6 +56,7 @@ struct PulseScratch {
     uint64_t *keep = nullptr, *exp = nullptr, *ts = nullptr, *rows = nullptr;
     uint64_t *exp_b = nullptr, *rows_b = nullptr;
     uint32_t* run_len = nullptr;  // two arrays of capacity / kPulseSortRun + 1
+    bool counters_clean = false;  // (tbg_pulse's report clears them for the next pulse)
     unsigned long long* counters = nullptr;  // kept, candidates, earliest unexpired, expired
     unsigned int* expired = nullptr;
 };
@@ -221,6 +222,12 @@ struct tbg_ctx {
     bool ae_sorted = true, ae_pending = false;
     // Host-buffer create_transfers: its AccountEvents are launched after the results' download.
     bool ae_defer = false, ae_deferred = false;
+    // A pulse's appends, queued later (ae_flush_graph): by the next call once its first kernels
+    // are queued (the host's launches then overlap the GPU), or by whatever joins the side stream
+    // or takes a staging buffer first.
+    bool ae_graph_deferred = false;
+    uint32_t ae_def_parity = 0, ae_def_epoch = 0;
+    bool ae_def_pending = false;
     Call<tb_transfer_t> ae_call{};
     AeScratch ae{};
     uint64_t ae_touch_cap = 0;
@@ -991,7 +998,10 @@ int ensure_ae_scratch(tbg_ctx* ctx, uint64_t touches) {
 }
 
 // The call's stream waits for the side stream's appends (GPU-side; no host synchronisation).
+int ae_flush_graph(tbg_ctx* ctx);
+
 int ae_join(tbg_ctx* ctx) {
+    if (int rc = ae_flush_graph(ctx)) return rc;
     if (!ctx->ae_async_pending) return 0;
     HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ae_done[ctx->ae_parity ^ 1], 0));
     ctx->ae_async_pending = false;
@@ -1173,7 +1183,10 @@ bool ae_async_ok(const tbg_ctx* ctx, uint32_t n) {
 // for that buffer's previous graph.
 // The staging buffer of the next appends (ctx->ae_parity), once the call's stream waited for its
 // previous appends.
+int ae_flush_graph(tbg_ctx* ctx);
+
 int ae_stage_acquire(tbg_ctx* ctx) {
+    if (int rc = ae_flush_graph(ctx)) return rc;
     if (int rc = ensure_ae_async(ctx)) return rc;
     const uint32_t p = ctx->ae_parity;
     if (ctx->ae_done_recorded[p]) HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ae_done[p], 0));
@@ -1199,6 +1212,32 @@ int ae_launch_graph(tbg_ctx* ctx, uint32_t n, uint32_t epoch, bool pending = fal
     HIP_TRY(ctx, hipEventRecord(ctx->ae_done[p], ctx->ae_stream));
     ctx->ae_done_recorded[p] = true;
     ctx->ae_parity = p ^ 1;
+    ctx->ae_async_pending = true;
+    return 0;
+}
+
+// ae_launch_graph in two halves: the bound, the snapshot's event and the parity now; the side
+// stream's launches at ae_flush_graph.
+int ae_defer_graph(tbg_ctx* ctx, uint32_t n, uint32_t epoch, bool pending) {
+    const uint32_t p = ctx->ae_parity;
+    ctx->ae_bound += n;
+    ctx->ae_pending = true;
+    HIP_TRY(ctx, hipEventRecord(ctx->ae_snap_ready[p], ctx->stream));
+    ctx->ae_graph_deferred = true;
+    ctx->ae_def_parity = p;
+    ctx->ae_def_epoch = epoch;
+    ctx->ae_def_pending = pending;
+    ctx->ae_parity = p ^ 1;
+    return 0;
+}
+int ae_flush_graph(tbg_ctx* ctx) {
+    if (!ctx->ae_graph_deferred) return 0;
+    ctx->ae_graph_deferred = false;
+    const uint32_t p = ctx->ae_def_parity;
+    HIP_TRY(ctx, hipStreamWaitEvent(ctx->ae_stream, ctx->ae_snap_ready[p], 0));
+    if (int rc = ae_launch_appends(ctx, p, ctx->ae_def_epoch, ctx->ae_def_pending)) return rc;
+    HIP_TRY(ctx, hipEventRecord(ctx->ae_done[p], ctx->ae_stream));
+    ctx->ae_done_recorded[p] = true;
     ctx->ae_async_pending = true;
     return 0;
 }
@@ -1284,8 +1323,9 @@ int ae_dense(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
               dev_alloc(ctx, &ctx->ae_dense_pos, cap, false) &&
               dev_alloc(ctx, &ctx->ae_dense_fail, 1, true)))
             return TBG_ENOMEM;
-        const unsigned long long ts_init[2] = {~0ull, 0};  // (ae_dense_records: min / max)
-        HIP_TRY(ctx, hipMemcpy(ctx->ae_dense_ts, ts_init, sizeof(ts_init), hipMemcpyHostToDevice));
+        // (ae_dense_records' min / max words; a kernel on the stream: a synchronous copy waited for
+        // every stream, ~10 ms inside config 4's first dense call)
+        hipLaunchKernelGGL(ae_dense_ts_init, dim3(1), dim3(64), 0, ctx->stream, ctx->ae_dense_ts);
     }
     if (int rc = ae_join(ctx)) return rc;
     if (ctx->ae_bound + c.n > ctx->ae_cap) {
@@ -1369,18 +1409,6 @@ int ae_expiry(tbg_ctx* ctx, const uint64_t* rows, uint64_t m, uint64_t timestamp
     }, "pulse:account_events");
 }
 
-// A pulse's AccountEvents behind the next call (the side stream, as small create_transfers calls):
-// the expiries staged on the call's stream right after pulse_apply, the appends queued.
-int ae_expiry_snapshot_async(tbg_ctx* ctx, const uint64_t* rows, uint64_t timestamp,
-                             const unsigned int* d_count, uint32_t* epoch_out) {
-    if (int rc = ae_stage_acquire(ctx)) return rc;
-    const uint32_t epoch = ++ctx->epoch;
-    AeExpirySnap J{ctx->T, rows, d_count, timestamp, ctx->ae_stage[ctx->ae_parity], epoch};
-    hipLaunchKernelGGL(ae_expiry_snapshot, dim3(kAeAsyncMax / kBlock), dim3(kBlock), 0, ctx->stream, J);
-    HIP_TRY(ctx, hipGetLastError());
-    *epoch_out = epoch;
-    return 0;
-}
 
 // Restores timestamp order of the log (stable) when an append broke it.
 int ae_sort_log(tbg_ctx* ctx) {
@@ -1950,6 +1978,7 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
         hipLaunchKernelGGL(tr_commit, grid, block, 0, ctx->stream, ctx->T, c);
         tmark(ctx, "tr_commit");
         rc = hip_ok(ctx, hipGetLastError(), "launch") ? 0 : TBG_EHIP;
+        if (!rc) rc = ae_flush_graph(ctx);  // (a pulse's appends, while this call runs)
     } else if (!rc) {
         c.chunk_info = ctx->chunk_info;
         hipLaunchKernelGGL(tr_chunk_info, dim3(grid_for((n + 63) / 64)), block, 0, ctx->stream, c,
@@ -1959,6 +1988,7 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
         hipLaunchKernelGGL(tr_commit, grid, block, 0, ctx->stream, ctx->T, c);
         tmark(ctx, "tr_commit");
         rc = hip_ok(ctx, hipGetLastError(), "launch") ? 0 : TBG_EHIP;
+        if (!rc) rc = ae_flush_graph(ctx);
     }
     const int items = int(2 * uint64_t(n));
     const BalTarget target{ctx->T.acc_rows, ctx->T.acc_index, ctx->T.acc_entry_of};
@@ -2253,7 +2283,9 @@ int pulse_select(tbg_ctx* ctx, uint64_t timestamp, uint32_t k, PulseGather* out,
     if (rc) return rc;
     PulseScratch& S = ctx->pulse;
     uint32_t levels = 0;
-    hipLaunchKernelGGL(pulse_reset_counters, dim3(1), dim3(64), 0, ctx->stream, S.counters);
+    if (!S.counters_clean)
+        hipLaunchKernelGGL(pulse_reset_counters, dim3(1), dim3(64), 0, ctx->stream, S.counters);
+    S.counters_clean = false;
     if (count) {
         hipLaunchKernelGGL(pulse_collect, dim3(uint32_t((count + kPulseCollectTile - 1) / kPulseCollectTile)),
                            dim3(kPulseCollectThreads), 0, ctx->stream,
@@ -2384,7 +2416,20 @@ int64_t tbg_pulse(tbg_ctx* ctx, uint64_t timestamp) {
     // The scan stops with buffer_finished after batch_max values (:4969-4999): the first batch_max
     // candidates in index order expire; everything after the host's first sync stays on device.
     tmark(ctx, "-pulse");
-    int rc = pulse_select(ctx, timestamp, k, nullptr, true);
+    // The expiries' AccountEvents: decided (and their staging acquired) before the pulse's
+    // launches, so no host work sits between pulse_apply and the snapshot.
+    const uint64_t count0 = ctx->expiry_known ? std::min<uint64_t>(ctx->expiry_host, ctx->T.expiry_capacity)
+                                              : ctx->T.expiry_capacity;
+    const uint32_t upper0 = uint32_t(std::min<uint64_t>(count0, k));
+    bool ae_async = ctx->ae_log && upper0 && ae_async_ok(ctx, upper0) && !getenv("TBG_PULSE_AE_SYNC");
+    uint32_t ae_epoch = 0;
+    int rc = 0;
+    if (ae_async) {
+        rc = ae_stage_acquire(ctx);
+        if (rc) return rc;
+        ae_epoch = ++ctx->epoch;
+    }
+    rc = pulse_select(ctx, timestamp, k, nullptr, true);
     if (rc) return rc;
     tmark(ctx, "pulse:select");
     PulseScratch& S = ctx->pulse;
@@ -2400,29 +2445,28 @@ int64_t tbg_pulse(tbg_ctx* ctx, uint64_t timestamp) {
     tmark(ctx, "pulse:apply");
     ctx->expiry_known = false;
     // The expiries' AccountEvents behind the next call (the side stream: the snapshot here, the
-    // appends queued after the report, so the host's queueing overlaps the report), or here.
-    const bool ae_async = ctx->ae_log && upper && ae_async_ok(ctx, upper) && !getenv("TBG_PULSE_AE_SYNC");
-    uint32_t ae_epoch = 0;
-    if (ae_async)
-        rc = ae_expiry_snapshot_async(ctx, S.rows, timestamp, S.expired, &ae_epoch);
-    else if (ctx->ae_log && upper)
+    // appends queued by the next call once its own kernels are queued), or here.
+    if (ae_async && upper) {
+        AeExpirySnap J{ctx->T, S.rows, S.expired, timestamp, ctx->ae_stage[ctx->ae_parity], ae_epoch};
+        hipLaunchKernelGGL(ae_expiry_snapshot, dim3(kAeAsyncMax / kBlock), dim3(kBlock), 0, ctx->stream, J);
+        HIP_TRY(ctx, hipGetLastError());
+    } else if (ctx->ae_log && upper) {
+        ae_async = false;
         rc = ae_expiry(ctx, S.rows, upper, timestamp, nullptr, S.expired);
+    } else {
+        ae_async = false;
+    }
     if (rc) return rc;
     // The count expired and the index's new length, written into mapped pinned memory by a kernel
     // (no copy-engine hand-off), one synchronisation.
     hipLaunchKernelGGL(pulse_report, dim3(1), dim3(64), 0, ctx->stream, S.expired, S.counters,
                        ctx->dh_pulse);
     HIP_TRY(ctx, hipGetLastError());
-    if (ae_async && (rc = ae_launch_graph(ctx, upper, ae_epoch, true))) return rc;
+    S.counters_clean = true;
+    if (ae_async) ae_defer_graph(ctx, upper, ae_epoch, true);
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     tmark(ctx, "pulse:report");
     tcollect(ctx);
-    if (getenv("TBG_PULSE_TRACE")) {  // (diagnostics: the index and candidate counts)
-        unsigned long long h[3];
-        HIP_TRY(ctx, hipMemcpy(h, S.counters, sizeof(h), hipMemcpyDeviceToHost));
-        fprintf(stderr, "pulse index=%llu candidates=%llu kept=%llu expired=%llu\n",
-                (unsigned long long)count, h[1], h[0], ctx->h_pulse[0]);
-    }
     ctx->expiry_host = ctx->h_pulse[1];
     ctx->expiry_known = true;
     return int64_t(ctx->h_pulse[0]);

@@ -47,14 +47,15 @@ __device__ inline bool pulse_less(uint64_t ea, uint64_t ra, uint64_t eb, uint64_
     return ea < eb || (ea == eb && ra < rb);
 }
 
+__device__ inline void pulse_counters_clear(unsigned long long* counters) {
+    counters[0] = 0;      // kept
+    counters[1] = 0;      // candidates
+    counters[2] = ~0ull;  // earliest unexpired expiry
+    counters[3] = 0;      // expired (pulse_settle)
+    counters[4] = ~0ull;  // earliest candidate expiry
+}
 __global__ void pulse_reset_counters(unsigned long long* counters) {
-    if (threadIdx.x == 0 && blockIdx.x == 0) {
-        counters[0] = 0;      // kept
-        counters[1] = 0;      // candidates
-        counters[2] = ~0ull;  // earliest unexpired expiry
-        counters[3] = 0;      // expired (pulse_settle)
-        counters[4] = ~0ull;  // earliest candidate expiry
-    }
+    if (threadIdx.x == 0 && blockIdx.x == 0) pulse_counters_clear(counters);
 }
 
 // A candidate's sort key: (expires_at, row).
@@ -229,35 +230,48 @@ __device__ void pulse_merge_path(PulseRuns in, uint32_t a, uint32_t b, uint32_t 
         if (i < lb) B[i] = vb[j];
     }
     __syncthreads();
+    // This lane's outputs d .. d + kPulseMergeItems - 1, merged into registers, then through LDS
+    // (over A, once every lane is done reading) to coalesced stores: a lane storing its own
+    // consecutive outputs made every store instruction touch 64 lines.
     const uint32_t d = tid * kPulseMergeItems;
-    if (d >= L) return;
-    // the number of A's keys among the first d outputs: the smallest i with A[i] after B[d-1-i]
-    uint32_t lo = d > lb ? d - lb : 0, hi = d < la ? d : la;
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (B[d - 1 - mid] < A[mid]) hi = mid;
-        else lo = mid + 1;
+    uint64_t o[kPulseMergeItems];
+    if (d < L) {
+        // the number of A's keys among the first d outputs: the smallest i with A[i] after B[d-1-i]
+        uint32_t lo = d > lb ? d - lb : 0, hi = d < la ? d : la;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (B[d - 1 - mid] < A[mid]) hi = mid;
+            else lo = mid + 1;
+        }
+        uint32_t i = lo, j = d - lo;
+        uint64_t x = i < la ? A[i] : ~0ull, y = j < lb ? B[j] : ~0ull;
+#pragma unroll
+        for (uint32_t m = 0; m < kPulseMergeItems; m++) {
+            const bool take_a = x < y;  // (distinct keys; an exhausted run reads as ~0)
+            o[m] = take_a ? x : y;
+            if (take_a) {
+                i++;
+                x = i < la ? A[i] : ~0ull;
+            } else {
+                j++;
+                y = j < lb ? B[j] : ~0ull;
+            }
+        }
     }
-    uint32_t i = lo, j = d - lo;
-    uint64_t x = i < la ? A[i] : ~0ull, y = j < lb ? B[j] : ~0ull;
+    __syncthreads();
+    if (d < L) {
+#pragma unroll
+        for (uint32_t m = 0; m < kPulseMergeItems; m++)
+            if (d + m < L) A[d + m] = o[m];
+    }
+    __syncthreads();
     uint64_t* oe = out.exp + uint64_t(r) * out.stride;
     uint64_t* orow = out.row + uint64_t(r) * out.stride;
     const uint64_t mask = (1ull << P.row_bits) - 1;
-#pragma unroll
-    for (uint32_t m = 0; m < kPulseMergeItems; m++) {
-        const uint32_t o = d + m;
-        if (o >= L) break;
-        const bool take_a = x < y;  // (distinct keys; an exhausted run reads as ~0)
-        const uint64_t v = take_a ? x : y;
-        oe[o] = P.base + (v >> P.row_bits);
-        orow[o] = v & mask;
-        if (take_a) {
-            i++;
-            x = i < la ? A[i] : ~0ull;
-        } else {
-            j++;
-            y = j < lb ? B[j] : ~0ull;
-        }
+    for (uint32_t q = tid; q < L; q += kPulseThreads) {
+        const uint64_t v = A[q];
+        oe[q] = P.base + (v >> P.row_bits);
+        orow[q] = v & mask;
     }
 }
 
@@ -368,12 +382,13 @@ __global__ void pnt_gather(Call<tb_transfer_t> c, const uint32_t* list, const un
 }
 
 // The pulse's outcome for the host: the count expired and the index's new length.
-__global__ void pulse_report(const unsigned int* expired, const unsigned long long* counters,
+__global__ void pulse_report(const unsigned int* expired, unsigned long long* counters,
                              unsigned long long* out) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     out[0] = *expired;
     out[1] = counters[0];
     __threadfence_system();
+    pulse_counters_clear(counters);  // (the next pulse starts clean: no reset launch)
 }
 
 // The index keeps the entries still pending (the ones just expired are dropped at the next pulse).
