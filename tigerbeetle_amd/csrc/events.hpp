@@ -436,6 +436,9 @@ struct AeExpirySnap {
     uint64_t timestamp;
     AeStage st;
     uint32_t epoch;
+    // Mapped pinned word: the epoch when an expiry needs the general appends (the host reads it
+    // after the pulse's synchronisation and queues only the appends the pulse needs), or null.
+    unsigned long long* host_general;
 };
 __global__ void ae_expiry_snapshot(AeExpirySnap J) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -459,7 +462,12 @@ __global__ void ae_expiry_snapshot(AeExpirySnap J) {
                     J.timestamp - m + i + 1, 0, TB_PENDING_EXPIRED, &p, tb_uint128_t{0, 0},
                     p.amount, p.ledger);
     J.st.ref[i] = AeRef{uint32_t(row), uint32_t(dr), uint32_t(cr), 0};
-    if (fd || fc || p.amount.hi != 0 || p.amount.lo >= kAeSmallAmountMax) J.st.words[0] = J.epoch;
+    if (fd || fc || p.amount.hi != 0 || p.amount.lo >= kAeSmallAmountMax) {
+        J.st.words[0] = J.epoch;
+        if (J.host_general)
+            __hip_atomic_store(J.host_general, (unsigned long long)J.epoch, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 // u8 flags -> pos[i] = the number of flagged items before i (flagged items only); the count.

@@ -902,16 +902,20 @@ int run_replay(tbg_ctx* ctx, Call<Event>& c, bool is_transfers, bool finalize_ev
 
 int ensure_pulse_scratch(tbg_ctx* ctx, uint64_t count) {
     PulseScratch& S = ctx->pulse;
+    // keep: expiry_capacity entries, once (tbg_pulse swaps it with the index: it never shrinks)
+    if (!S.keep && !dev_alloc(ctx, &S.keep, ctx->T.expiry_capacity, false)) return TBG_ENOMEM;
     if (S.counters && count <= S.capacity) return 0;
-    for (void* p : {(void*)S.keep, (void*)S.exp, (void*)S.ts, (void*)S.rows, (void*)S.exp_b,
-                    (void*)S.rows_b, (void*)S.counters, (void*)S.run_len, (void*)S.expired})
+    for (void* p : {(void*)S.exp, (void*)S.ts, (void*)S.rows, (void*)S.exp_b, (void*)S.rows_b,
+                    (void*)S.counters, (void*)S.run_len, (void*)S.expired})
         if (p) (void)hipFree(p);
+    uint64_t* keep = S.keep;
     S = PulseScratch();
-    // (merged runs sit at strides up to kPulseRun: a level's runs may reach past the candidates
-    // by one stride)
-    const uint64_t want = count + count / 2 + 2 * kPulseRun;
+    S.keep = keep;
+    // (twice the index length: a growing index reallocates -- synchronously -- rarely; merged runs
+    // sit at strides up to kPulseRun, so a level's runs may reach past the candidates by one stride)
+    const uint64_t want = std::max<uint64_t>(2 * count, 1u << 18) + 2 * kPulseRun;
     const uint64_t cap = (want + kPulseRun - 1) / kPulseRun * kPulseRun;
-    if (!(dev_alloc(ctx, &S.keep, cap, false) && dev_alloc(ctx, &S.exp, cap, false) &&
+    if (!(dev_alloc(ctx, &S.exp, cap, false) &&
           dev_alloc(ctx, &S.ts, cap, false) && dev_alloc(ctx, &S.rows, cap, false) &&
           dev_alloc(ctx, &S.exp_b, cap, false) && dev_alloc(ctx, &S.rows_b, cap, false) &&
           dev_alloc(ctx, &S.run_len, 2 * (cap / kPulseSortRun + 1), false) &&
@@ -1095,17 +1099,24 @@ int ae_append(tbg_ctx* ctx, uint32_t n_upper, const unsigned int* d_count, Colle
 // fixed upper bound kAeAsyncMax): number the created events, copy and group, place, emit. The two
 // chained scans use their own status words and ticket (ae_g_words[7 ..]), which ae_scatter_tail
 // clears for the next append.
-int ae_launch_appends(tbg_ctx* ctx, uint32_t p, uint32_t epoch, bool pending) {
+// which: 0 both paths (ae_small_emit takes the staging unless an event needs the general appends,
+// which then run; else they skip), 1 ae_small_emit only, 2 the general appends only (the host
+// knows from the snapshot which one the staging needs).
+int ae_launch_appends(tbg_ctx* ctx, uint32_t p, uint32_t epoch, bool pending, int which = 0) {
     hipStream_t st = ctx->ae_stream;
     // The one-pass appends first (ae_small_emit); they take the call unless the staging holds an
     // event they cannot, and then every kernel below skips it.
-    const bool small = ctx->ae_window_on && ctx->T.acc_rows_used <= kAeWinRowsMax;
+    const bool small = which != 2 && ctx->ae_window_on && ctx->T.acc_rows_used <= kAeWinRowsMax;
     const unsigned int* handled = ctx->ae_stage[p].words + 1;
     if (small) {
         AeSmall A{ctx->ae_stage[p], epoch, uint32_t(ctx->T.acc_rows_used), pending ? 1u : 0u,
                   ctx->ae_log, ctx->ae_ref, ctx->ae_words + 4, ctx->ae_small_counts,
                   ctx->ae_small_ts, ctx->ae_cap};
         hipLaunchKernelGGL(ae_small_emit, dim3(kAeSmallWgs), dim3(kAeSmallThreads), 0, st, A);
+        if (which == 1) {
+            HIP_TRY(ctx, hipGetLastError());
+            return 0;
+        }
     }
     AeScratch S = ctx->ae_g;
     S.state = ctx->ae_words + 4;
@@ -1235,7 +1246,10 @@ int ae_flush_graph(tbg_ctx* ctx) {
     ctx->ae_graph_deferred = false;
     const uint32_t p = ctx->ae_def_parity;
     HIP_TRY(ctx, hipStreamWaitEvent(ctx->ae_stream, ctx->ae_snap_ready[p], 0));
-    if (int rc = ae_launch_appends(ctx, p, ctx->ae_def_epoch, ctx->ae_def_pending)) return rc;
+    // (the pulse synchronised after its snapshot: the pinned word says which appends it needs)
+    const bool small_ok = ctx->ae_window_on && ctx->T.acc_rows_used <= kAeWinRowsMax;
+    const int which = !small_ok ? 0 : ctx->h_pulse[3] == ctx->ae_def_epoch ? 2 : 1;
+    if (int rc = ae_launch_appends(ctx, p, ctx->ae_def_epoch, ctx->ae_def_pending, which)) return rc;
     HIP_TRY(ctx, hipEventRecord(ctx->ae_done[p], ctx->ae_stream));
     ctx->ae_done_recorded[p] = true;
     ctx->ae_async_pending = true;
@@ -1828,6 +1842,12 @@ tbg_ctx* tbg_open(const tbg_options* options) {
         tbg_close(ctx);
         return nullptr;
     }
+    // (and the pulse's scratch: a first pulse that allocates waits on every stream)
+    if (ensure_pulse_scratch(ctx, 0) != 0) {
+        fprintf(stderr, "tbg_open: pulse scratch\n");
+        tbg_close(ctx);
+        return nullptr;
+    }
     return ctx;
 }
 
@@ -2269,7 +2289,7 @@ struct PulseGather {
 // S.exp / S.rows (pulse.hpp: LDS-sorted runs, pairwise merges keeping the first k); the entries still
 // pending at S.keep; the counters on device. `out`: the counters on the host too (one sync).
 int pulse_select(tbg_ctx* ctx, uint64_t timestamp, uint32_t k, PulseGather* out,
-                 bool settle = false) {
+                 bool settle = false, unsigned long long* report = nullptr) {
     int rc = 0;
     // The index length: known on the host since the last call or pulse (else one synchronisation).
     if (!ctx->expiry_known) {
@@ -2282,7 +2302,6 @@ int pulse_select(tbg_ctx* ctx, uint64_t timestamp, uint32_t k, PulseGather* out,
     rc = ensure_pulse_scratch(ctx, count);
     if (rc) return rc;
     PulseScratch& S = ctx->pulse;
-    uint32_t levels = 0;
     if (!S.counters_clean)
         hipLaunchKernelGGL(pulse_reset_counters, dim3(1), dim3(64), 0, ctx->stream, S.counters);
     S.counters_clean = false;
@@ -2301,7 +2320,7 @@ int pulse_select(tbg_ctx* ctx, uint64_t timestamp, uint32_t k, PulseGather* out,
         hipLaunchKernelGGL(pulse_sort_chunks, dim3(runs), dim3(kPulseSortThreads), 0, ctx->stream, A,
                            S.counters, k, timestamp, row_bits);
         const PulseRuns first = A, second = B;
-        uint32_t live = runs;
+        uint32_t live = runs, levels = 0;
         bool swapped = false;
         while (live > 1) {
             const uint32_t next = (live + 1) / 2;
@@ -2315,15 +2334,19 @@ int pulse_select(tbg_ctx* ctx, uint64_t timestamp, uint32_t k, PulseGather* out,
         }
         if (levels)  // (moves the result where the host reads it; settles a pulse)
             hipLaunchKernelGGL(pulse_final_copy, dim3(1), dim3(kPulseThreads), 0, ctx->stream, first,
-                               second, S.counters, levels, ctx->T, S.expired, k, uint32_t(settle));
+                               second, S.counters, levels, ctx->T, S.expired, k, uint32_t(settle),
+                               report);
+        else if (settle)
+            hipLaunchKernelGGL(pulse_settle, dim3(1), dim3(64), 0, ctx->stream, ctx->T, S.exp,
+                               S.counters, S.expired, k, report);
         if (swapped) {  // (the result is in the second buffers: they become the first)
             std::swap(S.exp, S.exp_b);
             std::swap(S.rows, S.rows_b);
         }
-    }
-    if (settle && levels == 0)
+    } else if (settle) {
         hipLaunchKernelGGL(pulse_settle, dim3(1), dim3(64), 0, ctx->stream, ctx->T, S.exp, S.counters,
-                           S.expired, k);
+                           S.expired, k, report);
+    }
     HIP_TRY(ctx, hipGetLastError());
     if (out) {
         unsigned long long h[3];
@@ -2416,6 +2439,8 @@ int64_t tbg_pulse(tbg_ctx* ctx, uint64_t timestamp) {
     // The scan stops with buffer_finished after batch_max values (:4969-4999): the first batch_max
     // candidates in index order expire; everything after the host's first sync stays on device.
     tmark(ctx, "-pulse");
+    static const bool htrace = getenv("TBG_PULSE_HOST_TRACE") != nullptr;
+    double ht[8] = {htrace ? now_ms() : 0};
     // The expiries' AccountEvents: decided (and their staging acquired) before the pulse's
     // launches, so no host work sits between pulse_apply and the snapshot.
     const uint64_t count0 = ctx->expiry_known ? std::min<uint64_t>(ctx->expiry_host, ctx->T.expiry_capacity)
@@ -2424,20 +2449,25 @@ int64_t tbg_pulse(tbg_ctx* ctx, uint64_t timestamp) {
     bool ae_async = ctx->ae_log && upper0 && ae_async_ok(ctx, upper0) && !getenv("TBG_PULSE_AE_SYNC");
     uint32_t ae_epoch = 0;
     int rc = 0;
+    if (htrace) ht[1] = now_ms();
+    rc = pulse_select(ctx, timestamp, k, nullptr, true, ctx->dh_pulse);
+    if (rc) return rc;
+    if (htrace) ht[2] = now_ms();
+    // (after the selection's launches: a previous pulse's deferred appends are queued while the
+    // selection runs; then this pulse's staging buffer)
     if (ae_async) {
         rc = ae_stage_acquire(ctx);
         if (rc) return rc;
         ae_epoch = ++ctx->epoch;
     }
-    rc = pulse_select(ctx, timestamp, k, nullptr, true);
-    if (rc) return rc;
     tmark(ctx, "pulse:select");
     PulseScratch& S = ctx->pulse;
     const uint64_t count = std::min<uint64_t>(ctx->expiry_host, ctx->T.expiry_capacity);
     const uint32_t upper = uint32_t(std::min<uint64_t>(count, k));
     if (count) {
-        hipLaunchKernelGGL(pulse_keep_copy, dim3(std::min<uint32_t>(grid_for(count), kMaxGrid)),
-                           dim3(kBlock), 0, ctx->stream, ctx->T, S.keep, S.counters);
+        // The index keeps the entries still pending: pulse_collect wrote them to S.keep, which
+        // becomes the index (the old one the next pulse's scratch; both hold expiry_capacity).
+        std::swap(ctx->T.expiry, S.keep);
         hipLaunchKernelGGL(pulse_apply, dim3(grid_for(upper)), dim3(kBlock), 0, ctx->stream, ctx->T,
                            S.rows, uint64_t(upper), S.expired);
     }
@@ -2447,7 +2477,9 @@ int64_t tbg_pulse(tbg_ctx* ctx, uint64_t timestamp) {
     // The expiries' AccountEvents behind the next call (the side stream: the snapshot here, the
     // appends queued by the next call once its own kernels are queued), or here.
     if (ae_async && upper) {
-        AeExpirySnap J{ctx->T, S.rows, S.expired, timestamp, ctx->ae_stage[ctx->ae_parity], ae_epoch};
+        ctx->h_pulse[3] = 0;
+        AeExpirySnap J{ctx->T, S.rows, S.expired, timestamp, ctx->ae_stage[ctx->ae_parity], ae_epoch,
+                       ctx->dh_pulse + 3};
         hipLaunchKernelGGL(ae_expiry_snapshot, dim3(kAeAsyncMax / kBlock), dim3(kBlock), 0, ctx->stream, J);
         HIP_TRY(ctx, hipGetLastError());
     } else if (ctx->ae_log && upper) {
@@ -2457,14 +2489,19 @@ int64_t tbg_pulse(tbg_ctx* ctx, uint64_t timestamp) {
         ae_async = false;
     }
     if (rc) return rc;
-    // The count expired and the index's new length, written into mapped pinned memory by a kernel
-    // (no copy-engine hand-off), one synchronisation.
-    hipLaunchKernelGGL(pulse_report, dim3(1), dim3(64), 0, ctx->stream, S.expired, S.counters,
-                       ctx->dh_pulse);
-    HIP_TRY(ctx, hipGetLastError());
+    // The count expired and the index's new length came to mapped pinned memory with the
+    // settlement (pulse_final_copy / pulse_settle: no copy-engine hand-off), which also cleared the
+    // counters; one synchronisation.
     S.counters_clean = true;
+    if (htrace) ht[3] = now_ms();
     if (ae_async) ae_defer_graph(ctx, upper, ae_epoch, true);
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (htrace) {
+        ht[4] = now_ms();
+        fprintf(stderr, "pulse host us: prep %.1f select %.1f rest %.1f sync %.1f\n",
+                (ht[1] - ht[0]) * 1e3, (ht[2] - ht[1]) * 1e3, (ht[3] - ht[2]) * 1e3,
+                (ht[4] - ht[3]) * 1e3);
+    }
     tmark(ctx, "pulse:report");
     tcollect(ctx);
     ctx->expiry_host = ctx->h_pulse[1];

@@ -10,11 +10,11 @@
 //   * pulse_sort_chunks sorts each run of kPulseSortRun candidates (prims.hpp block_bitonic_sort:
 //     4 keys per lane in registers, shuffles within a wave, LDS across waves; one-word keys when
 //     the candidates' expiry span allows, PulsePack) and keeps its first k (k = the batch);
-//   * pulse_merge merges the sorted runs pairwise, keeping only the first k of each pair (every
-//     element's rank: its index plus a binary search in the other run, staged in LDS);
-// ceil(log2(runs)) merge rounds leave the first min(candidates, k) in order. pulse_settle then
-// sets the index's new length and pulse_next_timestamp on device, pulse_keep_copy compacts the
-// index, pulse_apply expires the selected rows.
+//   * pulse_merge merges the sorted runs pairwise, a launch per level, keeping only the first k of
+//     each pair (merge path in LDS, outputs through LDS to coalesced stores);
+// ceil(log2(runs)) merge levels leave the first min(candidates, k) in order. The root then sets
+// the index's new length and pulse_next_timestamp on device and reports to the host (the kept
+// entries, written by pulse_collect, become the index), pulse_apply expires the selected rows.
 //
 // pulse_next_timestamp of a create_transfers call with post/void (pnt_*): every update was
 // recorded at its event -- min(expires_at) or reset-if-equal -- and a reset fires iff the running
@@ -275,9 +275,7 @@ __device__ void pulse_merge_path(PulseRuns in, uint32_t a, uint32_t b, uint32_t 
     }
 }
 
-// The merge levels past the candidates' own runs (the host launches levels for the index length,
-// an upper bound of the candidate count) do nothing: pulse_final_copy moves the result to the
-// buffer the host expects after all levels.
+// The runs holding candidates, and the merge levels over them.
 __device__ inline uint32_t pulse_live_runs(const unsigned long long* counters) {
     return uint32_t((counters[1] + kPulseSortRun - 1) / kPulseSortRun);
 }
@@ -285,6 +283,17 @@ __device__ inline uint32_t pulse_levels(uint32_t live) {
     return live <= 1 ? 0u : 32u - __builtin_clz(live - 1);  // ceil(log2(live))
 }
 
+
+__device__ void pulse_settle_one(Tables T, const uint64_t* exp, unsigned long long* counters,
+                                 unsigned int* expired_out, uint32_t k);
+__device__ inline void pulse_report_one(unsigned long long* counters, unsigned long long* report);
+
+
+// The merge levels, a launch each (levels past the candidates' own runs return at once), and
+// pulse_final_copy, which moves the result where the host reads it after all levels and settles
+// the pulse. (One launch for the whole tree, the second child of a pair to finish merging it, took
+// 77 us against ~45: every hand-off between workgroups paid an agent-scope release and acquire --
+// the L2 written back and invalidated -- where a kernel boundary pays it once.)
 __global__ void __launch_bounds__(kPulseThreads) pulse_merge(PulseRuns in, uint32_t runs_in,
                                                             uint32_t k, PulseRuns out,
                                                             const unsigned long long* counters,
@@ -311,15 +320,13 @@ __global__ void __launch_bounds__(kPulseThreads) pulse_merge(PulseRuns in, uint3
 
 // After `levels` merge launches the host reads the result from the first buffers when `levels` is
 // even, else from the second: when the levels that ran leave it in the other one, run 0 moves.
-// Then pulse_settle's work (one launch less).
-__device__ void pulse_settle_one(Tables T, const uint64_t* exp, unsigned long long* counters,
-                                 unsigned int* expired_out, uint32_t k);
-
+// Then the settlement (and, for tbg_pulse, the report).
 __global__ void __launch_bounds__(kPulseThreads) pulse_final_copy(PulseRuns first, PulseRuns second,
                                                                  unsigned long long* counters,
                                                                  uint32_t levels, Tables T,
                                                                  unsigned int* expired_out,
-                                                                 uint32_t k, uint32_t settle) {
+                                                                 uint32_t k, uint32_t settle,
+                                                                 unsigned long long* report) {
     const uint32_t ran = pulse_levels(pulse_live_runs(counters));
     const PulseRuns dst = (levels & 1) ? second : first;
     if ((ran & 1) != (levels & 1)) {
@@ -332,7 +339,10 @@ __global__ void __launch_bounds__(kPulseThreads) pulse_final_copy(PulseRuns firs
         if (threadIdx.x == 0) dst.len[0] = n;
         __syncthreads();
     }
-    if (settle && threadIdx.x == 0) pulse_settle_one(T, dst.exp, counters, expired_out, k);
+    if (settle && threadIdx.x == 0) {
+        pulse_settle_one(T, dst.exp, counters, expired_out, k);
+        if (report) pulse_report_one(counters, report);
+    }
 }
 
 // After the selection (the first min(candidates, k) in order at exp / rows): the number expired,
@@ -349,9 +359,19 @@ __device__ void pulse_settle_one(Tables T, const uint64_t* exp, unsigned long lo
     counters[3] = expired;
     *expired_out = uint32_t(expired);
 }
+// tbg_pulse's end (report != null): the count expired and the index's new length into mapped
+// pinned memory for the host, and the counters cleared for the next pulse.
+__device__ inline void pulse_report_one(unsigned long long* counters, unsigned long long* report) {
+    report[0] = counters[3];
+    report[1] = counters[0];
+    __threadfence_system();
+    pulse_counters_clear(counters);
+}
 __global__ void pulse_settle(Tables T, const uint64_t* exp, unsigned long long* counters,
-                             unsigned int* expired_out, uint32_t k) {
-    if (threadIdx.x == 0 && blockIdx.x == 0) pulse_settle_one(T, exp, counters, expired_out, k);
+                             unsigned int* expired_out, uint32_t k, unsigned long long* report) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    pulse_settle_one(T, exp, counters, expired_out, k);
+    if (report) pulse_report_one(counters, report);
 }
 
 // A sharded call's recorded updates for the caller (tbg_pnt_ops): event k's flag.
@@ -381,23 +401,7 @@ __global__ void pnt_gather(Call<tb_transfer_t> c, const uint32_t* list, const un
     out[2 * i + 1] = c.pnt_call[k];
 }
 
-// The pulse's outcome for the host: the count expired and the index's new length.
-__global__ void pulse_report(const unsigned int* expired, unsigned long long* counters,
-                             unsigned long long* out) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    out[0] = *expired;
-    out[1] = counters[0];
-    __threadfence_system();
-    pulse_counters_clear(counters);  // (the next pulse starts clean: no reset launch)
-}
 
-// The index keeps the entries still pending (the ones just expired are dropped at the next pulse).
-__global__ void pulse_keep_copy(Tables T, const uint64_t* keep, const unsigned long long* counters) {
-    const uint64_t n = counters[0];
-    for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
-         i += uint64_t(gridDim.x) * blockDim.x)
-        T.expiry[i] = keep[i];
-}
 
 // ---- pulse_next_timestamp of a call with post/void -------------------------------------------
 
