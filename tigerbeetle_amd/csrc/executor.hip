@@ -225,6 +225,8 @@ struct tbg_ctx {
     // A pulse's appends, queued later (ae_flush_graph): by the next call once its first kernels
     // are queued (the host's launches then overlap the GPU), or by whatever joins the side stream
     // or takes a staging buffer first.
+    const void* prefetch_events = nullptr;  // tbg_prefetch_body's body, in d_events
+    uint64_t prefetch_bytes = 0;
     bool ae_graph_deferred = false;
     uint32_t ae_def_parity = 0, ae_def_epoch = 0;
     bool ae_def_pending = false;
@@ -1575,6 +1577,14 @@ int stage_call_inputs(tbg_ctx* ctx, const void* events, uint64_t bytes, uint32_t
                       bool reset_scalars, bool ingest_reads_host = false) {
     const uint4* src = mapped(ctx, static_cast<const uint4*>(events), bytes);
     ctx->events_host = nullptr;
+    // (a body tbg_prefetch_body already moved into HBM)
+    const bool prefetched = ctx->prefetch_events == events && ctx->prefetch_bytes == bytes && bytes;
+    ctx->prefetch_events = nullptr;
+    ctx->prefetch_bytes = 0;
+    if (prefetched) {
+        src = nullptr;
+        bytes = 0;
+    }
     // TBG_INGEST_READS_HOST=0: stage_in copies the body first -- 32 workgroups of coalesced 16-B
     // reads, the PCIe read rate's best shape (45 GB/s, tools/pciebench.hip) -- and tr_ingest reads
     // HBM. A commit without AccountEvents took 55-56 us that way against 58-60 with tr_ingest
@@ -1597,6 +1607,21 @@ int stage_call_inputs(tbg_ctx* ctx, const void* events, uint64_t bytes, uint32_t
     hipLaunchKernelGGL(stage_in, dim3(grid), dim3(kStageThreads), 0, ctx->stream, s);
     HIP_TRY(ctx, hipGetLastError());
     return 0;
+}
+
+// The prefetch's body copy alone (StageIn with no batch ends or scalar reset).
+int prefetch_body(tbg_ctx* ctx, const void* events, uint64_t bytes) {
+    const uint4* src = mapped(ctx, static_cast<const uint4*>(events), bytes);
+    if (!src || bytes % 16 || bytes > uint64_t(ctx->opt.batch_events_max) * 128) return 0;
+    StageIn s{src, reinterpret_cast<uint4*>(ctx->d_events), bytes / 16, nullptr, nullptr, nullptr,
+              nullptr, 0, nullptr};
+    const uint64_t per_block = uint64_t(kStageThreads) * kStageWords;
+    const uint32_t grid = uint32_t(std::min<uint64_t>(kStageInGridMax, std::max<uint64_t>(1, (s.words + per_block - 1) / per_block)));
+    hipLaunchKernelGGL(stage_in, dim3(grid), dim3(kStageThreads), 0, ctx->stream, s);
+    HIP_TRY(ctx, hipGetLastError());
+    ctx->prefetch_events = events;
+    ctx->prefetch_bytes = bytes;
+    return 1;
 }
 
 // Results (n > 0) and / or the scalars block to mapped host memory, as one kernel on the stream.
@@ -1668,6 +1693,8 @@ int64_t lookup_impl(tbg_ctx* ctx, const tb_uint128_t* ids, uint32_t n, void* out
     if (n == 0) return 0;
     if (n > ctx->opt.batch_events_max) return TBG_EINVAL;
     // Scratch: ids and output rows in d_events; rows in bal_items; found flags in ev_slow.
+    ctx->prefetch_events = nullptr;  // (a prefetched body there is overwritten)
+    ctx->prefetch_bytes = 0;
     HIP_TRY(ctx, hipMemcpyAsync(ctx->d_events, ids, size_t(n) * 16, hipMemcpyHostToDevice,
                                 ctx->stream));
     const tb_uint128_t* d_ids = reinterpret_cast<const tb_uint128_t*>(ctx->d_events);
@@ -2399,6 +2426,16 @@ int pulse_keys(tbg_ctx* ctx, uint64_t n, std::vector<uint64_t>* exp, std::vector
 }  // namespace
 
 extern "C" {
+
+int tbg_prefetch_body(tbg_ctx* ctx, const void* events, uint64_t bytes) {
+    if (!ctx || !events) return TBG_EINVAL;
+    FAILED_GUARD(ctx);
+    // (off unless TBG_PREFETCH_BODY=1: with the prefetch and the commit back to back, the staged
+    // copy plus an HBM ingest took 73-81 us a commit with AccountEvents against 68-73 with tr_ingest
+    // reading the registered body itself -- tools/commit_timeline.py, same box)
+    static const bool on = getenv("TBG_PREFETCH_BODY") && atoi(getenv("TBG_PREFETCH_BODY")) != 0;
+    return on ? prefetch_body(ctx, events, bytes) : 0;
+}
 
 int tbg_register_host(tbg_ctx* ctx, void* ptr, uint64_t size) {
     if (!ctx || !ptr || size == 0) return TBG_EINVAL;

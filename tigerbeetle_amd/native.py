@@ -93,6 +93,7 @@ SIGNATURES = [
     ("tbg_create_transfers_stamped_device", ctypes.c_int, [vp, vp, ctypes.c_uint32, vp, vp, vp]),
     ("tbg_register_host", ctypes.c_int, [vp, vp, ctypes.c_uint64]),
     ("tbg_unregister_host", ctypes.c_int, [vp, vp]),
+    ("tbg_prefetch_body", ctypes.c_int, [vp, vp, ctypes.c_uint64]),
     ("tbg_synchronize", ctypes.c_int, [vp]),
     ("tbg_pulse", ctypes.c_int64, [vp, ctypes.c_uint64]),
     ("tbg_pulse_candidates", ctypes.c_int64, [vp, ctypes.c_uint64, vp, vp, ctypes.c_uint32]),
