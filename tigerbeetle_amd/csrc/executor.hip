@@ -225,6 +225,20 @@ struct tbg_ctx {
     // A pulse's appends, queued later (ae_flush_graph): by the next call once its first kernels
     // are queued (the host's launches then overlap the GPU), or by whatever joins the side stream
     // or takes a staging buffer first.
+    // The body buffer of the current host-buffer call (d_events, or d_events_alt for a small
+    // create_transfers call while a deferred snapshot still reads d_events).
+    uint8_t* body_dst = nullptr;
+    uint8_t* d_events_alt = nullptr;  // kAeAsyncMax events
+    // A small call's AccountEvents snapshot on the side stream (ae_snap_defer): queued by the next
+    // call just before its tr_ingest (the call's stream waits for it there: everything before --
+    // the body's upload -- runs beside it), its appends after the next call's kernels.
+    bool ae_snap_def = false, ae_snap_def_appends = false;
+    AeSnapJob ae_snap_def_job{};
+    uint32_t ae_snap_def_p = 0, ae_snap_def_epoch = 0;
+    const uint8_t* ae_snap_body = nullptr;  // the body buffer the deferred snapshot reads
+    hipEvent_t ae_snap_done = nullptr;
+    bool ae_side_snap = false;
+    bool ae_snap_side = false;  // (this call's snapshot goes to the side stream)
     const void* prefetch_events = nullptr;  // tbg_prefetch_body's body, in d_events
     uint64_t prefetch_bytes = 0;
     bool ae_graph_deferred = false;
@@ -239,6 +253,7 @@ struct tbg_ctx {
     // staging buffer per parity, the side stream's own positions and grouping scratch. Every other
     // use of the log joins the side stream first (ae_join).
     hipStream_t ae_stream = nullptr;
+    hipStream_t snap_stream = nullptr;  // the deferred snapshots (not behind the appends)
     AeStage ae_stage[2] = {};
     uint32_t* ae_pos = nullptr;
     hipEvent_t ae_snap_ready[2] = {}, ae_done[2] = {};
@@ -1005,9 +1020,10 @@ int ensure_ae_scratch(tbg_ctx* ctx, uint64_t touches) {
 
 // The call's stream waits for the side stream's appends (GPU-side; no host synchronisation).
 int ae_flush_graph(tbg_ctx* ctx);
+int ae_flush_all(tbg_ctx* ctx);
 
 int ae_join(tbg_ctx* ctx) {
-    if (int rc = ae_flush_graph(ctx)) return rc;
+    if (int rc = ae_flush_all(ctx)) return rc;
     if (!ctx->ae_async_pending) return 0;
     HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ae_done[ctx->ae_parity ^ 1], 0));
     ctx->ae_async_pending = false;
@@ -1176,11 +1192,14 @@ int ensure_ae_async(tbg_ctx* ctx) {
     if ((cap * 2 + kScanTile - 1) / kScanTile + (kAeAsyncMax + kScanTile - 1) / kScanTile + 8 > 64)
         return TBG_EINVAL;
     HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->ae_stream, hipStreamNonBlocking));
+    HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->snap_stream, hipStreamNonBlocking));
     for (int p = 0; p < 2; p++) {
         HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ae_snap_ready[p], hipEventDisableTiming));
         HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ae_done[p], hipEventDisableTiming));
     }
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // (the scratch's zeroing)
+    HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ae_snap_done, hipEventDisableTiming));
+    if (!dev_alloc(ctx, &ctx->d_events_alt, uint64_t(kAeAsyncMax) * 128, false)) return TBG_ENOMEM;
     ctx->ae_async_ready = true;
     return 0;
 }
@@ -1197,9 +1216,10 @@ bool ae_async_ok(const tbg_ctx* ctx, uint32_t n) {
 // The staging buffer of the next appends (ctx->ae_parity), once the call's stream waited for its
 // previous appends.
 int ae_flush_graph(tbg_ctx* ctx);
+int ae_flush_all(tbg_ctx* ctx);
 
 int ae_stage_acquire(tbg_ctx* ctx) {
-    if (int rc = ae_flush_graph(ctx)) return rc;
+    if (int rc = ae_flush_all(ctx)) return rc;
     if (int rc = ensure_ae_async(ctx)) return rc;
     const uint32_t p = ctx->ae_parity;
     if (ctx->ae_done_recorded[p]) HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ae_done[p], 0));
@@ -1255,6 +1275,62 @@ int ae_flush_graph(tbg_ctx* ctx) {
     HIP_TRY(ctx, hipEventRecord(ctx->ae_done[p], ctx->ae_stream));
     ctx->ae_done_recorded[p] = true;
     ctx->ae_async_pending = true;
+    return 0;
+}
+
+// A small call's snapshot on the side stream (ae_snap_defer), in two halves: the snapshot and the
+// call stream's wait for it (before anything writes the rows, results or body it reads), then its
+// appends.
+int ae_snap_flush1(tbg_ctx* ctx) {
+    if (!ctx->ae_snap_def) return 0;
+    ctx->ae_snap_def = false;
+    const uint32_t p = ctx->ae_snap_def_p;
+    // (a stream of its own: on the side stream it queued behind the previous call's appends; it
+    // waits only for the call's end and for the appends that last read its staging buffer)
+    HIP_TRY(ctx, hipStreamWaitEvent(ctx->snap_stream, ctx->ae_snap_ready[p], 0));
+    if (ctx->ae_done_recorded[p])
+        HIP_TRY(ctx, hipStreamWaitEvent(ctx->snap_stream, ctx->ae_done[p], 0));
+    hipLaunchKernelGGL(ae_snapshot, dim3(kAeAsyncMax / kBlock), dim3(kBlock), 0, ctx->snap_stream,
+                       ctx->ae_snap_def_job);
+    HIP_TRY(ctx, hipGetLastError());
+    HIP_TRY(ctx, hipEventRecord(ctx->ae_snap_done, ctx->snap_stream));
+    HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ae_snap_done, 0));
+    ctx->ae_snap_body = nullptr;
+    ctx->ae_snap_def_appends = true;
+    return 0;
+}
+int ae_snap_flush2(tbg_ctx* ctx) {
+    if (!ctx->ae_snap_def_appends) return 0;
+    ctx->ae_snap_def_appends = false;
+    const uint32_t p = ctx->ae_snap_def_p;
+    HIP_TRY(ctx, hipStreamWaitEvent(ctx->ae_stream, ctx->ae_snap_done, 0));
+    if (int rc = ae_launch_appends(ctx, p, ctx->ae_snap_def_epoch, false)) return rc;
+    HIP_TRY(ctx, hipEventRecord(ctx->ae_done[p], ctx->ae_stream));
+    ctx->ae_done_recorded[p] = true;
+    ctx->ae_async_pending = true;
+    return 0;
+}
+// Every deferred side-stream job, in the order they were deferred (at most one of each kind is
+// pending, and each defer flushes the other kind first).
+int ae_flush_all(tbg_ctx* ctx) {
+    if (int rc = ae_snap_flush1(ctx)) return rc;
+    if (int rc = ae_snap_flush2(ctx)) return rc;
+    return ae_flush_graph(ctx);
+}
+// After a small call with no replay: the snapshot, final now, deferred to the side stream.
+int ae_snap_defer(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
+    if (int rc = ae_flush_all(ctx)) return rc;
+    if (int rc = ensure_ae_async(ctx)) return rc;
+    const uint32_t p = ctx->ae_parity;
+    HIP_TRY(ctx, hipEventRecord(ctx->ae_snap_ready[p], ctx->stream));
+    ctx->ae_snap_def_job = AeSnapJob{ctx->T, c, ctx->ae_stage[p], false};
+    ctx->ae_snap_def = true;
+    ctx->ae_snap_def_p = p;
+    ctx->ae_snap_def_epoch = c.epoch;
+    ctx->ae_snap_body = reinterpret_cast<const uint8_t*>(c.events);
+    ctx->ae_bound += c.n;
+    ctx->ae_pending = true;
+    ctx->ae_parity = p ^ 1;
     return 0;
 }
 
@@ -1573,12 +1649,27 @@ void host_pin_release(void* ptr) {
 // A host-buffer call's inputs into HBM: the batch ends / timestamps from the pinned staging and,
 // when the body lies in a registered range, the body itself -- one kernel on the call's stream
 // (hostio.hpp); an unregistered body takes hipMemcpyAsync.
+int ae_snap_flush1(tbg_ctx* ctx);
+int ae_flush_all(tbg_ctx* ctx);
+
+// Chooses the host-buffer call's body buffer (ctx->body_dst).
+int body_buffer(tbg_ctx* ctx, bool small) {
+    ctx->body_dst = ctx->d_events;
+    if (ctx->ae_snap_body != ctx->d_events) return 0;
+    if (small && ctx->d_events_alt) {
+        ctx->body_dst = ctx->d_events_alt;
+        return 0;
+    }
+    return ae_flush_all(ctx);
+}
+
 int stage_call_inputs(tbg_ctx* ctx, const void* events, uint64_t bytes, uint32_t nb,
                       bool reset_scalars, bool ingest_reads_host = false) {
     const uint4* src = mapped(ctx, static_cast<const uint4*>(events), bytes);
     ctx->events_host = nullptr;
     // (a body tbg_prefetch_body already moved into HBM)
-    const bool prefetched = ctx->prefetch_events == events && ctx->prefetch_bytes == bytes && bytes;
+    const bool prefetched = ctx->prefetch_events == events && ctx->prefetch_bytes == bytes && bytes &&
+                            ctx->body_dst == ctx->d_events;
     ctx->prefetch_events = nullptr;
     ctx->prefetch_bytes = 0;
     if (prefetched) {
@@ -1598,8 +1689,8 @@ int stage_call_inputs(tbg_ctx* ctx, const void* events, uint64_t bytes, uint32_t
         bytes = 0;
     }
     if (!src && bytes)
-        HIP_TRY(ctx, hipMemcpyAsync(ctx->d_events, events, bytes, hipMemcpyHostToDevice, ctx->stream));
-    StageIn s{src, reinterpret_cast<uint4*>(ctx->d_events), bytes / 16, ctx->dh_batch_ends,
+        HIP_TRY(ctx, hipMemcpyAsync(ctx->body_dst, events, bytes, hipMemcpyHostToDevice, ctx->stream));
+    StageIn s{src, reinterpret_cast<uint4*>(ctx->body_dst), bytes / 16, ctx->dh_batch_ends,
               ctx->d_batch_ends, ctx->dh_batch_ts, ctx->d_batch_ts, nb,
               reset_scalars ? ctx->d_scalars : nullptr};
     const uint64_t per_block = uint64_t(kStageThreads) * kStageWords;
@@ -1613,6 +1704,7 @@ int stage_call_inputs(tbg_ctx* ctx, const void* events, uint64_t bytes, uint32_t
 int prefetch_body(tbg_ctx* ctx, const void* events, uint64_t bytes) {
     const uint4* src = mapped(ctx, static_cast<const uint4*>(events), bytes);
     if (!src || bytes % 16 || bytes > uint64_t(ctx->opt.batch_events_max) * 128) return 0;
+    if (ctx->ae_snap_body == ctx->d_events) return 0;  // (a deferred snapshot reads it)
     StageIn s{src, reinterpret_cast<uint4*>(ctx->d_events), bytes / 16, nullptr, nullptr, nullptr,
               nullptr, 0, nullptr};
     const uint64_t per_block = uint64_t(kStageThreads) * kStageWords;
@@ -1695,6 +1787,8 @@ int64_t lookup_impl(tbg_ctx* ctx, const tb_uint128_t* ids, uint32_t n, void* out
     // Scratch: ids and output rows in d_events; rows in bal_items; found flags in ev_slow.
     ctx->prefetch_events = nullptr;  // (a prefetched body there is overwritten)
     ctx->prefetch_bytes = 0;
+    if (ctx->ae_snap_body == ctx->d_events)
+        if (int rc = ae_flush_all(ctx)) return rc;
     HIP_TRY(ctx, hipMemcpyAsync(ctx->d_events, ids, size_t(n) * 16, hipMemcpyHostToDevice,
                                 ctx->stream));
     const tb_uint128_t* d_ids = reinterpret_cast<const tb_uint128_t*>(ctx->d_events);
@@ -1853,6 +1947,11 @@ tbg_ctx* tbg_open(const tbg_options* options) {
     T.scalars = ctx->d_scalars;
     ctx->ae_async = getenv("TBG_AE_SYNC") == nullptr;
     ctx->ae_window_on = getenv("TBG_NO_AE_WINDOW") == nullptr;
+    // (TBG_AE_SIDE_SNAP=1: a small call's snapshot on a stream of its own, the next call's ingest
+    // waiting for it: 83-96 us a commit against 69-74 on the call's stream -- the two cross-stream
+    // event waits on the critical path cost more than the 11 us snapshot they hide)
+    ctx->ae_side_snap = getenv("TBG_AE_SIDE_SNAP") && atoi(getenv("TBG_AE_SIDE_SNAP")) != 0;
+    ctx->body_dst = nullptr;
     T.acc_ts_index = ctx->acc_ts_index;
     T.tr_ts_index = ctx->tr_ts_index;
     DevScalars init{};
@@ -1881,6 +1980,7 @@ tbg_ctx* tbg_open(const tbg_options* options) {
 void tbg_close(tbg_ctx* ctx) {
     if (!ctx) return;
     if (ctx->ae_stream) (void)hipStreamSynchronize(ctx->ae_stream);
+    if (ctx->snap_stream) (void)hipStreamSynchronize(ctx->snap_stream);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     for (int p = 0; p < 2; p++) {
         if (ctx->ae_snap_ready[p]) (void)hipEventDestroy(ctx->ae_snap_ready[p]);
@@ -1895,10 +1995,12 @@ void tbg_close(tbg_ctx* ctx) {
     for (void* q : {(void*)ctx->ae_small_counts, (void*)ctx->ae_small_ts, (void*)ctx->ae_dense_touch,
                     (void*)ctx->ae_dense_ev, (void*)ctx->ae_dense_partials,
                     (void*)ctx->ae_dense_counts, (void*)ctx->ae_dense_ts, (void*)ctx->ae_dense_fail,
-                    (void*)ctx->ae_dense_later, (void*)ctx->ae_dense_pos})
+                    (void*)ctx->ae_dense_later, (void*)ctx->ae_dense_pos, (void*)ctx->d_events_alt})
         if (q) (void)hipFree(q);
     free_ae_scratch(ctx->ae_g);
+    if (ctx->ae_snap_done) (void)hipEventDestroy(ctx->ae_snap_done);
     if (ctx->ae_stream) (void)hipStreamDestroy(ctx->ae_stream);
+    if (ctx->snap_stream) (void)hipStreamDestroy(ctx->snap_stream);
     void* ptrs[] = {ctx->idx_dirty, ctx->idx_counters, ctx->T.acc_index.entries, ctx->T.acc_entry_of, ctx->T.acc.slots, ctx->T.acc_rows, ctx->T.acc_live, ctx->T.acc_hot,
                     ctx->T.acc_closable, ctx->T.tr.slots, ctx->T.tr_rows, ctx->T.tr_live,
                     ctx->T.tr_status, ctx->T.expiry, ctx->d_scalars, ctx->T.undo, ctx->d_events,
@@ -2020,22 +2122,24 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
             ci.events = ctx->events_host;
             ci.events_out = const_cast<tb_transfer_t*>(c.events);
         }
+        if (int frc = ae_snap_flush1(ctx)) return frc;  // (the previous call's snapshot)
         hipLaunchKernelGGL(tr_ingest, dim3(ig), block, 0, ctx->stream, ctx->T, ci);
         tmark(ctx, "tr_ingest");
         hipLaunchKernelGGL(tr_commit, grid, block, 0, ctx->stream, ctx->T, c);
         tmark(ctx, "tr_commit");
         rc = hip_ok(ctx, hipGetLastError(), "launch") ? 0 : TBG_EHIP;
-        if (!rc) rc = ae_flush_graph(ctx);  // (a pulse's appends, while this call runs)
+        if (!rc) rc = ae_flush_all(ctx);  // (deferred appends, while this call runs)
     } else if (!rc) {
         c.chunk_info = ctx->chunk_info;
         hipLaunchKernelGGL(tr_chunk_info, dim3(grid_for((n + 63) / 64)), block, 0, ctx->stream, c,
                            ctx->chunk_info, ctx->d_scalars);
+        if (int frc = ae_snap_flush1(ctx)) return frc;
         hipLaunchKernelGGL(tr_ingest, dim3(ig), block, 0, ctx->stream, ctx->T, c);
         tmark(ctx, "tr_ingest");
         hipLaunchKernelGGL(tr_commit, grid, block, 0, ctx->stream, ctx->T, c);
         tmark(ctx, "tr_commit");
         rc = hip_ok(ctx, hipGetLastError(), "launch") ? 0 : TBG_EHIP;
-        if (!rc) rc = ae_flush_graph(ctx);
+        if (!rc) rc = ae_flush_all(ctx);
     }
     const int items = int(2 * uint64_t(n));
     const BalTarget target{ctx->T.acc_rows, ctx->T.acc_index, ctx->T.acc_entry_of};
@@ -2104,7 +2208,7 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
         // A small call's AccountEvents snapshot follows stage_out (the host's wait ends at
         // stage_out): final unless a replay follows, then it stages nothing. Its appends are queued
         // on the side stream now, so that the host's launch calls overlap the call's kernels.
-        if (!rc && snap) {
+        if (!rc && snap && !ctx->ae_side_snap) {
             AeSnapJob J;
             rc = ae_snap_job(ctx, c, &J);
             if (!rc) {
@@ -2115,13 +2219,19 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
             }
             if (!rc) rc = ae_launch_graph(ctx, n, c.epoch);
         }
-        ctx->ae_snap_early = snap && !rc;
+        ctx->ae_snap_early = snap && !rc && !ctx->ae_side_snap;
+        ctx->ae_snap_side = snap && !rc && ctx->ae_side_snap;
         if (!rc) rc = spin ? spin_wait(ctx, seq)
                            : (hip_ok(ctx, hipStreamSynchronize(ctx->stream), "sync") ? 0 : TBG_EHIP);
         tmark(ctx, "host_sync");
     }
     const bool replay = !rc && ctx->h_scalars->stats[0] > 0;
     if (replay) ctx->ae_snap_early = false;
+    if (!rc && ctx->ae_snap_side && !replay) {  // (no replay: the snapshot is final)
+        rc = ae_snap_defer(ctx, c);
+        ctx->ae_snap_early = !rc;
+    }
+    ctx->ae_snap_side = false;
     ctx->early_done = !rc && ctx->early_dst && !replay;  // (only the replay rewrites results)
     if (replay && (ctx->h_scalars->flags & kFlagImported)) rc = check_imported_indexes(ctx, true);
     if (replay && !rc) rc = run_replay(ctx, c, true, false);
@@ -2256,15 +2366,19 @@ int tbg_create_transfers(tbg_ctx* ctx, const tb_transfer_t* events, uint32_t n,
     if (!ctx || n > ctx->opt.batch_events_max) return TBG_EINVAL;
     if (n == 0) return 0;
     const double t0 = ctx->timing_host ? now_ms() : 0;
+    // The body's buffer: d_events, unless a deferred snapshot still reads it (then a small call
+    // takes the second buffer, a larger one queues that snapshot first).
+    int rc = body_buffer(ctx, n <= kAeAsyncMax);
+    if (rc) return rc;
     // (stage_in resets the call's scalar words: no tr_chunk_info launch for a small call)
-    int rc = upload_batches(ctx, n, batch_lens, batch_ts, nb, events, 128, n <= kInlineChunkMax,
-                            n <= kInlineChunkMax);
+    rc = upload_batches(ctx, n, batch_lens, batch_ts, nb, events, 128, n <= kInlineChunkMax,
+                        n <= kInlineChunkMax);
     if (rc) return rc;
     ctx->scalars_reset = n <= kInlineChunkMax;
     const double t1 = ctx->timing_host ? now_ms() : 0;
     ctx->ae_defer = true;
     ctx->early_dst = results;
-    rc = tbg_create_transfers_device(ctx, reinterpret_cast<const tb_transfer_t*>(ctx->d_events), n,
+    rc = tbg_create_transfers_device(ctx, reinterpret_cast<const tb_transfer_t*>(ctx->body_dst), n,
                                      ctx->d_batch_ends, ctx->d_batch_ts, nb, ctx->d_results,
                                      nullptr);
     ctx->ae_defer = false;
@@ -2291,9 +2405,11 @@ int tbg_create_accounts(tbg_ctx* ctx, const tb_account_t* events, uint32_t n,
                         tb_create_result_t* results) {
     if (!ctx || n > ctx->opt.batch_events_max) return TBG_EINVAL;
     if (n == 0) return 0;
-    int rc = upload_batches(ctx, n, batch_lens, batch_ts, nb, events, 128, false);
+    int rc = body_buffer(ctx, false);
     if (rc) return rc;
-    rc = tbg_create_accounts_device(ctx, reinterpret_cast<const tb_account_t*>(ctx->d_events), n,
+    rc = upload_batches(ctx, n, batch_lens, batch_ts, nb, events, 128, false);
+    if (rc) return rc;
+    rc = tbg_create_accounts_device(ctx, reinterpret_cast<const tb_account_t*>(ctx->body_dst), n,
                                     ctx->d_batch_ends, ctx->d_batch_ts, nb, ctx->d_results, nullptr);
     if (rc) return rc;
     rc = download_results(ctx, results, n);
@@ -2490,8 +2606,11 @@ int64_t tbg_pulse(tbg_ctx* ctx, uint64_t timestamp) {
     rc = pulse_select(ctx, timestamp, k, nullptr, true, ctx->dh_pulse);
     if (rc) return rc;
     if (htrace) ht[2] = now_ms();
-    // (after the selection's launches: a previous pulse's deferred appends are queued while the
-    // selection runs; then this pulse's staging buffer)
+    // (after the selection's launches: deferred side-stream work -- a call's snapshot, which reads
+    // the rows pulse_apply writes, and appends -- is queued while the selection runs; then this
+    // pulse's staging buffer)
+    rc = ae_flush_all(ctx);
+    if (rc) return rc;
     if (ae_async) {
         rc = ae_stage_acquire(ctx);
         if (rc) return rc;
@@ -2692,6 +2811,7 @@ int tbg_debug_set_account_balances(tbg_ctx* ctx, tb_uint128_t id, tb_uint128_t d
                                    tb_uint128_t debits_posted, tb_uint128_t credits_pending,
                                    tb_uint128_t credits_posted) {
     if (!ctx) return TBG_EINVAL;
+    if (int rc = ae_flush_all(ctx)) return rc;  // (a deferred snapshot reads the rows)
     int* d_rc = reinterpret_cast<int*>(&ctx->d_scalars->slow_count);
     hipLaunchKernelGGL(set_balances_kernel, dim3(1), dim3(1), 0, ctx->stream, ctx->T, id,
                        debits_pending, debits_posted, credits_pending, credits_posted, d_rc);
