@@ -238,6 +238,7 @@ struct tbg_ctx {
     const uint8_t* ae_snap_body = nullptr;  // the body buffer the deferred snapshot reads
     hipEvent_t ae_snap_done = nullptr;
     bool ae_side_snap = false;
+    bool ae_no_query = false;  // (TBG_AE_NO_QUERY: always wait on the append events)
     bool ae_snap_side = false;  // (this call's snapshot goes to the side stream)
     const void* prefetch_events = nullptr;  // tbg_prefetch_body's body, in d_events
     uint64_t prefetch_bytes = 0;
@@ -1025,7 +1026,8 @@ int ae_flush_all(tbg_ctx* ctx);
 int ae_join(tbg_ctx* ctx) {
     if (int rc = ae_flush_all(ctx)) return rc;
     if (!ctx->ae_async_pending) return 0;
-    HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ae_done[ctx->ae_parity ^ 1], 0));
+    if (ctx->ae_no_query || hipEventQuery(ctx->ae_done[ctx->ae_parity ^ 1]) != hipSuccess)
+        HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ae_done[ctx->ae_parity ^ 1], 0));
     ctx->ae_async_pending = false;
     return 0;
 }
@@ -1222,9 +1224,16 @@ int ae_stage_acquire(tbg_ctx* ctx) {
     if (int rc = ae_flush_all(ctx)) return rc;
     if (int rc = ensure_ae_async(ctx)) return rc;
     const uint32_t p = ctx->ae_parity;
-    if (ctx->ae_done_recorded[p]) HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ae_done[p], 0));
+    // (a wait on an event that has already completed still puts a barrier packet on the call's
+    // stream: skipped when the appends two calls back are done)
+    if (ctx->ae_done_recorded[p] && (ctx->ae_no_query || hipEventQuery(ctx->ae_done[p]) != hipSuccess))
+        HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ae_done[p], 0));
     return 0;
 }
+
+// (the snapshots: one wave a workgroup, 128 workgroups -- the event's dependent loads spread over
+// more CUs than 32 workgroups of four waves)
+constexpr uint32_t kSnapThreads = 64;
 
 int ae_snap_job(tbg_ctx* ctx, const Call<tb_transfer_t>& c, AeSnapJob* J) {
     if (int rc = ae_stage_acquire(ctx)) return rc;
@@ -1290,7 +1299,7 @@ int ae_snap_flush1(tbg_ctx* ctx) {
     HIP_TRY(ctx, hipStreamWaitEvent(ctx->snap_stream, ctx->ae_snap_ready[p], 0));
     if (ctx->ae_done_recorded[p])
         HIP_TRY(ctx, hipStreamWaitEvent(ctx->snap_stream, ctx->ae_done[p], 0));
-    hipLaunchKernelGGL(ae_snapshot, dim3(kAeAsyncMax / kBlock), dim3(kBlock), 0, ctx->snap_stream,
+    hipLaunchKernelGGL(ae_snapshot, dim3(kAeAsyncMax / kSnapThreads), dim3(kSnapThreads), 0, ctx->snap_stream,
                        ctx->ae_snap_def_job);
     HIP_TRY(ctx, hipGetLastError());
     HIP_TRY(ctx, hipEventRecord(ctx->ae_snap_done, ctx->snap_stream));
@@ -1341,7 +1350,7 @@ int ae_transfers_async(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
     if (!ctx->ae_snap_early) {
         AeSnapJob J;
         if (int rc = ae_snap_job(ctx, c, &J)) return rc;
-        hipLaunchKernelGGL(ae_snapshot, dim3(kAeAsyncMax / kBlock), dim3(kBlock), 0, ctx->stream, J);
+        hipLaunchKernelGGL(ae_snapshot, dim3(kAeAsyncMax / kSnapThreads), dim3(kSnapThreads), 0, ctx->stream, J);
         HIP_TRY(ctx, hipGetLastError());
         if (int rc = ae_launch_graph(ctx, c.n, c.epoch)) return rc;
     }
@@ -1951,6 +1960,7 @@ tbg_ctx* tbg_open(const tbg_options* options) {
     // waiting for it: 83-96 us a commit against 69-74 on the call's stream -- the two cross-stream
     // event waits on the critical path cost more than the 11 us snapshot they hide)
     ctx->ae_side_snap = getenv("TBG_AE_SIDE_SNAP") && atoi(getenv("TBG_AE_SIDE_SNAP")) != 0;
+    ctx->ae_no_query = getenv("TBG_AE_NO_QUERY") != nullptr;
     ctx->body_dst = nullptr;
     T.acc_ts_index = ctx->acc_ts_index;
     T.tr_ts_index = ctx->tr_ts_index;
@@ -2213,7 +2223,7 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
             rc = ae_snap_job(ctx, c, &J);
             if (!rc) {
                 J.speculative = true;
-                hipLaunchKernelGGL(ae_snapshot, dim3(kAeAsyncMax / kBlock), dim3(kBlock), 0,
+                hipLaunchKernelGGL(ae_snapshot, dim3(kAeAsyncMax / kSnapThreads), dim3(kSnapThreads), 0,
                                    ctx->stream, J);
                 rc = hip_ok(ctx, hipGetLastError(), "launch") ? 0 : TBG_EHIP;
             }
@@ -2636,7 +2646,7 @@ int64_t tbg_pulse(tbg_ctx* ctx, uint64_t timestamp) {
         ctx->h_pulse[3] = 0;
         AeExpirySnap J{ctx->T, S.rows, S.expired, timestamp, ctx->ae_stage[ctx->ae_parity], ae_epoch,
                        ctx->dh_pulse + 3};
-        hipLaunchKernelGGL(ae_expiry_snapshot, dim3(kAeAsyncMax / kBlock), dim3(kBlock), 0, ctx->stream, J);
+        hipLaunchKernelGGL(ae_expiry_snapshot, dim3(kAeAsyncMax / kSnapThreads), dim3(kSnapThreads), 0, ctx->stream, J);
         HIP_TRY(ctx, hipGetLastError());
     } else if (ctx->ae_log && upper) {
         ae_async = false;
