@@ -278,6 +278,8 @@ struct tbg_ctx {
     unsigned int* ae_dense_counts = nullptr;
     unsigned long long* ae_dense_ts = nullptr;
     uint4* ae_dense_later = nullptr;
+    AeDense ae_dense_job{};           // (ae_dense_prefix -> ae_dense)
+    uint32_t ae_dense_prefixed = 0;   // the epoch whose prefix is queued
     uint32_t* ae_dense_pos = nullptr;
     unsigned int* ae_dense_fail = nullptr;
     unsigned long long* ae_small_ts = nullptr;
@@ -1408,7 +1410,10 @@ int ae_window(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
 // staged, summed per slice, suffix-summed; the call is refused (1: the general appends take it)
 // when an event flips `closed` or moves 2^19 or more, or a later-delta sum leaves the i32 range.
 constexpr uint32_t kAeDenseMax = 1u << 18;  // events per call
-int ae_dense(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
+// Its first half (stage, partials, suffix, the refusal word to pinned memory), launched before the
+// host's next synchronisation: by create_transfers after a replay, right before end_call's sync, so
+// the refusal is known without a synchronisation of its own. 1: not eligible.
+int ae_dense_prefix(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
     if (!ctx->ae_window_on || ctx->T.acc_rows_used > kAeWinRowsMax || c.n > kAeDenseMax ||
         c.n > ctx->opt.batch_events_max)
         return 1;
@@ -1433,7 +1438,8 @@ int ae_dense(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
         if (int rc = ae_settle(ctx)) return rc;
         if (ctx->ae_used + c.n > ctx->ae_cap) return 1;  // (the general path counts exactly)
     }
-    AeDense A{};
+    AeDense& A = ctx->ae_dense_job;
+    A = AeDense{};
     A.T = ctx->T;
     A.c = c;
     A.rows = uint32_t(ctx->T.acc_rows_used);
@@ -1460,9 +1466,22 @@ int ae_dense(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
                        ctx->stream, A);
     hipLaunchKernelGGL(ae_dense_report, dim3(1), dim3(64), 0, ctx->stream, ctx->ae_dense_fail,
                        ctx->dh_pulse + 2);
+    tmark(ctx, "account_events");
     HIP_TRY(ctx, hipGetLastError());
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    ctx->ae_dense_prefixed = c.epoch;
+    return 0;
+}
+
+int ae_dense(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
+    if (ctx->ae_dense_prefixed != c.epoch) {
+        const int rc = ae_dense_prefix(ctx, c);
+        if (rc) return rc;
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    }
+    ctx->ae_dense_prefixed = 0;
     if (ctx->h_pulse[2] == c.epoch) return 1;
+    const AeDense& A = ctx->ae_dense_job;
+    tmark(ctx, "-account_events");
     hipLaunchKernelGGL(ae_dense_later, dim3(A.slices), dim3(kAeDenseEmitThreads), 0, ctx->stream, A);
     hipLaunchKernelGGL(ae_dense_records, dim3((c.n + kAeDenseRecThreads - 1) / kAeDenseRecThreads),
                        dim3(kAeDenseRecThreads), 0, ctx->stream, A);
@@ -2249,6 +2268,12 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
     if (!rc) {
         ctx->pnt_last = c;
         ctx->pnt_last_valid = c.pnt_force != 0;
+    }
+    // (a replayed call's one-pass AccountEvents start now: end_call's synchronisation then covers
+    // their refusal word)
+    if (!rc && replay && ctx->ae_log && !ae_async_ok(ctx, n)) {
+        const int prc = ae_dense_prefix(ctx, c);
+        if (prc < 0) rc = prc;
     }
     if (!rc) rc = end_call(ctx, n, !replay);
     if (!rc && ctx->ae_log && ctx->ae_defer) {
