@@ -494,6 +494,38 @@ def test_small_calls_alternating_with_pulses(registered):
         p.close()
 
 
+@pytest.mark.parametrize("span", ["packed", "wide"])
+def test_pulse_many_candidates(span):
+    """Pulses over ~45k expired pending transfers with pulse_batch_max 8,190: 22 sorted runs, five
+    merge levels of several workgroups per pair, each pulse taking the first 8,190 in
+    (expires_at, timestamp) order. `packed`: timeouts of 1-600 s (one-word keys); `wide`: timeouts
+    up to 2^32 - 1 s, an expiry span past the one-word key's reach (the two-word path). The
+    expired counts, pulse_next_timestamp, rows and AccountEvents against the oracle."""
+    rng = np.random.default_rng(71 if span == "packed" else 72)
+    p = Pair(account_capacity=1 << 10, transfer_capacity=1 << 17, batch_events_max=1 << 14,
+             pulse_batch_max=8190)
+    try:
+        p.create_accounts(workload.accounts(200, seed=71))
+        hi = 600 if span == "packed" else (1 << 32) - 1
+        for step in range(3):
+            n = 15_000
+            t = workload.transfers_uniform(n, 200, seed=710 + step, id_offset=step * n)
+            t["flags"] |= 2  # pending
+            t["timeout"] = rng.integers(1, hi, size=n, dtype=np.int64)
+            t["timeout"][rng.random(n) < 0.3] = int(rng.integers(1, 4))  # (equal expiries: ties)
+            r = p.create_transfers(t, [8189, n - 8189])
+            assert (r["status"] == 0xFFFFFFFF).all()
+        before = len(p.pulses)
+        p.tick(hi * NS_PER_S + NS_PER_S)
+        for _ in range(8):
+            p.tick(1)
+        expired = [e for _, e in p.pulses[before:]]
+        assert expired[:5] == [8190] * 5 and sum(expired) == 45_000, expired
+        p.compare_state()
+    finally:
+        p.close()
+
+
 def test_two_phase_config4_small():
     """Config 4 shape: pending with timeouts, post/void, linked chains with failures, resubmits,
     pulses."""

@@ -1577,33 +1577,59 @@ __global__ void __launch_bounds__(kAeWinThreads) ae_dense_partials(AeDense A) {
     }
 }
 
-// One lane per (pair, account key): partials[pair][s][key] = the sum over slices >= s (i64; a sum
-// of magnitude 2^30 or more refuses the call).
-__global__ void ae_dense_suffix(AeDense A) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+// partials[pair][s][key] = the sum over slices >= s (i64; a sum of magnitude 2^30 or more
+// refuses the call). A workgroup takes 64 (pair, key) columns and splits each column's slices
+// into kAeSufGroups ranges, one wave per range: each wave sums its range, the ranges' totals
+// meet in LDS, and each wave then writes its range's suffixes from the total of the ranges
+// above it. (One lane per column walking every slice was a chain of slices/8 dependent load
+// batches: 20 us for a 1M-event call's 489 slices.)
+constexpr int kAeSufGroups = 16;
+constexpr int kAeSufThreads = 64 * kAeSufGroups;
+
+// (Holding a range in registers between the passes, 32 loads in flight a lane, took 16 us: 78
+// VGPRs left room for one 1,024-lane workgroup per CU, and capping them spilled.)
+__global__ __launch_bounds__(kAeSufThreads) void ae_dense_suffix(AeDense A) {
+    __shared__ long long total[kAeSufGroups][64];
+    const uint32_t lane = threadIdx.x & 63, g = threadIdx.x >> 6;
     const uint32_t keys = 2 * A.rows;
-    if (t >= 2 * keys) return;
-    const uint32_t q = t / keys, key = t % keys;
+    const uint32_t t = blockIdx.x * 64 + lane;
+    const bool live = t < 2 * keys;
+    const uint32_t q = live ? t / keys : 0, key = live ? t % keys : 0;
     uint32_t* p = A.partials + uint64_t(q) * A.slices * keys + key;
-    int64_t acc = 0;
-    bool wide = false;
-    // (eight slices' loads in flight before their stores: one at a time waited a full load
-    // latency per slice)
-    constexpr int kB = 8;
-    for (int64_t s1 = int64_t(A.slices); s1 > 0; s1 -= kB) {
-        uint32_t v[kB];
+    const uint32_t per = (A.slices + kAeSufGroups - 1) / kAeSufGroups;
+    const uint32_t lo = min(g * per, A.slices), hi = min(lo + per, A.slices);
+    constexpr int kB = 8;  // (loads in flight before their uses)
+    int64_t sum = 0;
+    if (live) {
+        for (uint32_t s0 = lo; s0 < hi; s0 += kB) {
+            uint32_t v[kB];
 #pragma unroll
-        for (int j = 0; j < kB; j++) {
-            const int64_t s = s1 - 1 - j;
-            v[j] = s >= 0 ? p[uint64_t(s) * keys] : 0u;
+            for (int j = 0; j < kB; j++) v[j] = s0 + j < hi ? p[uint64_t(s0 + j) * keys] : 0u;
+#pragma unroll
+            for (int j = 0; j < kB; j++) sum += int32_t(v[j]);
         }
+    }
+    total[g][lane] = sum;
+    __syncthreads();
+    int64_t acc = 0;
+    for (uint32_t h = g + 1; h < kAeSufGroups; h++) acc += total[h][lane];
+    bool wide = false;
+    if (live) {
+        for (int64_t s1 = hi; s1 > int64_t(lo); s1 -= kB) {
+            uint32_t v[kB];
 #pragma unroll
-        for (int j = 0; j < kB; j++) {
-            const int64_t s = s1 - 1 - j;
-            if (s >= 0) {
-                acc += int32_t(v[j]);
-                wide |= acc >= (int64_t(1) << 30) || acc <= -(int64_t(1) << 30);
-                p[uint64_t(s) * keys] = uint32_t(int32_t(acc));
+            for (int j = 0; j < kB; j++) {
+                const int64_t s = s1 - 1 - j;
+                v[j] = s >= int64_t(lo) ? p[uint64_t(s) * keys] : 0u;
+            }
+#pragma unroll
+            for (int j = 0; j < kB; j++) {
+                const int64_t s = s1 - 1 - j;
+                if (s >= int64_t(lo)) {
+                    acc += int32_t(v[j]);
+                    wide |= acc >= (int64_t(1) << 30) || acc <= -(int64_t(1) << 30);
+                    p[uint64_t(s) * keys] = uint32_t(int32_t(acc));
+                }
             }
         }
     }

@@ -1462,7 +1462,7 @@ int ae_dense_prefix(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
     tmark(ctx, "-account_events");
     hipLaunchKernelGGL(ae_dense_stage, dim3(grid_for(c.n)), dim3(kBlock), 0, ctx->stream, A);
     hipLaunchKernelGGL(ae_dense_partials, dim3(2 * A.slices), dim3(kAeWinThreads), 0, ctx->stream, A);
-    hipLaunchKernelGGL(ae_dense_suffix, dim3((4 * A.rows + kBlock - 1) / kBlock), dim3(kBlock), 0,
+    hipLaunchKernelGGL(ae_dense_suffix, dim3((4 * A.rows + 63) / 64), dim3(kAeSufThreads), 0,
                        ctx->stream, A);
     hipLaunchKernelGGL(ae_dense_report, dim3(1), dim3(64), 0, ctx->stream, ctx->ae_dense_fail,
                        ctx->dh_pulse + 2);
@@ -2503,7 +2503,7 @@ int pulse_select(tbg_ctx* ctx, uint64_t timestamp, uint32_t k, PulseGather* out,
         while (live > 1) {
             const uint32_t next = (live + 1) / 2;
             B.stride = std::min<uint32_t>(2 * A.stride, kPulseRun);
-            hipLaunchKernelGGL(pulse_merge, dim3(next), dim3(kPulseThreads), 0, ctx->stream, A,
+            hipLaunchKernelGGL(pulse_merge, dim3(next * kPulseSegs), dim3(kPulseSegThreads), 0, ctx->stream, A,
                                live, k, B, S.counters, timestamp, row_bits, levels);
             std::swap(A, B);
             swapped = !swapped;

@@ -2223,21 +2223,28 @@ __global__ void __launch_bounds__(kPulseCollectThreads) pulse_collect(
     bool kept[kPulseCollectItems], cand[kPulseCollectItems];
     uint32_t nk = 0, nc = 0;
     uint64_t next = ~0ull, first = ~0ull;
+    // (an entry's row fields are loaded with its live / status bytes, not after them: two rounds
+    // of dependent loads, not three -- a dropped entry's row is read for nothing)
+    uint32_t tmo[kPulseCollectItems];
 #pragma unroll
     for (uint32_t j = 0; j < kPulseCollectItems; j++) {
         const uint64_t i = base + j * kPulseCollectThreads + tid;
         row[j] = i < count ? T.expiry[i] : 0;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kPulseCollectItems; j++) {
+        const uint64_t i = base + j * kPulseCollectThreads + tid;
         kept[j] = i < count && T.tr_live[row[j]] && T.tr_status[row[j]] == TB_PENDING_PENDING;
+        ts[j] = i < count ? T.tr_rows[row[j]].timestamp : 0;
+        tmo[j] = i < count ? T.tr_rows[row[j]].timeout : 0;
     }
 #pragma unroll
     for (uint32_t j = 0; j < kPulseCollectItems; j++) {
         exp[j] = ~0ull;
-        ts[j] = 0;
         cand[j] = false;
+        if (!kept[j]) ts[j] = 0;
         if (kept[j]) {
-            const tb_transfer_t& p = T.tr_rows[row[j]];
-            ts[j] = p.timestamp;
-            exp[j] = p.timestamp + (uint64_t)p.timeout * TB_NS_PER_S;
+            exp[j] = ts[j] + (uint64_t)tmo[j] * TB_NS_PER_S;
             cand[j] = exp[j] <= timestamp;
             if (!cand[j]) next = exp[j] < next ? exp[j] : next;
             else first = exp[j] < first ? exp[j] : first;

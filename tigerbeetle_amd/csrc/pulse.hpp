@@ -11,7 +11,8 @@
 //     4 keys per lane in registers, shuffles within a wave, LDS across waves; one-word keys when
 //     the candidates' expiry span allows, PulsePack) and keeps its first k (k = the batch);
 //   * pulse_merge merges the sorted runs pairwise, a launch per level, keeping only the first k of
-//     each pair (merge path in LDS, outputs through LDS to coalesced stores);
+//     each pair (kPulseSegs workgroups per pair: merge-path diagonals, inputs in LDS, outputs
+//     through LDS to coalesced stores);
 // ceil(log2(runs)) merge levels leave the first min(candidates, k) in order. The root then sets
 // the index's new length and pulse_next_timestamp on device and reports to the host (the kept
 // entries, written by pulse_collect, become the index), pulse_apply expires the selected rows.
@@ -144,135 +145,97 @@ __global__ void __launch_bounds__(kPulseSortThreads) pulse_sort_chunks(PulseRuns
     if (threadIdx.x == 0) R.len[blockIdx.x] = n < k ? n : k;
 }
 
-// Runs 2r and 2r + 1 of `in` (runs_in of them) -> run r of `out`: the first min(k, sum) in order.
-// Every element's output position is its index plus the number of the other run's keys before it
-// (keys are distinct: rows are), by binary search in the other run staged in LDS. A lane holds its
-// kPulseMergeItems elements of each run in registers: every global load of a phase is in flight at
-// once, and so are its searches' LDS reads (one element at a time waited a load latency each).
-constexpr uint32_t kPulseMergeItems = kPulseRun / kPulseThreads;
+// Runs 2r and 2r + 1 of `in` (runs_in of them) -> run r of `out`: the first L = min(k, sum) in
+// order, kPulseSegs workgroups per pair, workgroup s writing outputs [s * kPulseSeg, (s + 1) *
+// kPulseSeg) of L. Its two merge-path diagonals are found by 64-ary searches over the runs in
+// global memory (a wave per diagonal, one probe per lane: 3 rounds of loads for 8,192 keys), its
+// inputs -- at most kPulseSeg keys of the two runs together -- are staged in LDS, every lane merges
+// kPulseSegItems outputs from its own diagonal (binary search in LDS) and the outputs go through
+// LDS to coalesced stores. Keys are distinct (rows are). (One 1,024-lane workgroup per pair took
+// ~12 us a level once the levels were down to a few pairs: a latency chain over 8,192 outputs.)
+constexpr uint32_t kPulseSeg = 1024;
+constexpr uint32_t kPulseSegThreads = 256;
+constexpr uint32_t kPulseSegItems = kPulseSeg / kPulseSegThreads;
+constexpr uint32_t kPulseSegs = kPulseRun / kPulseSeg;
 
-template <typename K, typename Pack>
-__device__ void pulse_merge_pair(PulseRuns in, uint32_t a, uint32_t b, uint32_t la, uint32_t lb,
-                                 uint32_t L, PulseRuns out, uint32_t r, K* other, Pack pack) {
-    const uint32_t tid = threadIdx.x;
-    uint64_t* oe = out.exp + uint64_t(r) * out.stride;
-    uint64_t* orow = out.row + uint64_t(r) * out.stride;
-    const uint64_t* ae = in.exp + uint64_t(a) * in.stride;
-    const uint64_t* ar = in.row + uint64_t(a) * in.stride;
-    const uint64_t* be = in.exp + uint64_t(b) * in.stride;
-    const uint64_t* br = in.row + uint64_t(b) * in.stride;
-    uint64_t xa_e[kPulseMergeItems], xa_r[kPulseMergeItems], xb_e[kPulseMergeItems], xb_r[kPulseMergeItems];
-#pragma unroll
-    for (uint32_t j = 0; j < kPulseMergeItems; j++) {
-        const uint32_t i = j * kPulseThreads + tid;
-        xa_e[j] = i < la ? ae[i] : 0;
-        xa_r[j] = i < la ? ar[i] : 0;
-        xb_e[j] = i < lb ? be[i] : 0;
-        xb_r[j] = i < lb ? br[i] : 0;
-    }
-    for (uint32_t phase = 0; phase < 2; phase++) {
-        const uint32_t lm = phase ? lb : la, lo = phase ? la : lb;
-        if (phase) __syncthreads();  // (phase 0's searches are done with the LDS copy)
-#pragma unroll
-        for (uint32_t j = 0; j < kPulseMergeItems; j++) {
-            const uint32_t i = j * kPulseThreads + tid;
-            if (i < lo) other[i] = phase ? pack(xa_e[j], xa_r[j]) : pack(xb_e[j], xb_r[j]);
-        }
-        __syncthreads();
-        const uint32_t lim = lm < L ? lm : L;  // (an element at index >= L lands at >= L)
-        uint32_t top = 0;
-        if (lo) top = 1u << (31 - __builtin_clz(lo));
-        K x[kPulseMergeItems];
-        uint32_t pos[kPulseMergeItems];
-#pragma unroll
-        for (uint32_t j = 0; j < kPulseMergeItems; j++) {
-            x[j] = phase ? pack(xb_e[j], xb_r[j]) : pack(xa_e[j], xa_r[j]);
-            pos[j] = 0;
-        }
-        for (uint32_t step = top; step > 0; step >>= 1)
-#pragma unroll
-            for (uint32_t j = 0; j < kPulseMergeItems; j++)
-                if (pos[j] + step <= lo && sort_less(other[pos[j] + step - 1], x[j])) pos[j] += step;
-#pragma unroll
-        for (uint32_t j = 0; j < kPulseMergeItems; j++) {
-            const uint32_t i = j * kPulseThreads + tid, p = i + pos[j];
-            if (i < lim && p < L) {
-                oe[p] = phase ? xb_e[j] : xa_e[j];
-                orow[p] = phase ? xb_r[j] : xa_r[j];
-            }
+// The number of run a's keys among the first d outputs of merging runs a and b: the smallest i in
+// [max(0, d - lb), min(d, la)] with B[d - 1 - i] < A[i] (the predicate rises once along i). One
+// wave, 64 probes a round.
+template <typename K, typename LoadA, typename LoadB>
+__device__ __forceinline__ uint32_t pulse_diagonal(uint32_t d, uint32_t la, uint32_t lb, LoadA load_a, LoadB load_b) {
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t lo = d > lb ? d - lb : 0, hi = d < la ? d : la;
+    while (lo < hi) {
+        const uint32_t step = (hi - lo + 63) / 64;
+        const uint32_t i = lo + lane * step;
+        bool p = true;
+        if (i < hi) p = sort_less(load_b(d - 1 - i), load_a(i));
+        const uint64_t m = __ballot(p);
+        if (m == 0) {
+            lo = lo + 63 * step + 1;
+        } else {
+            const uint32_t f = uint32_t(__builtin_ctzll(m));
+            const uint32_t nhi = lo + f * step < hi ? lo + f * step : hi;
+            if (f > 0) lo = lo + (f - 1) * step + 1;
+            hi = nhi;
         }
     }
+    return lo;
 }
 
-// The one-word keys' merge: both runs staged in LDS (2 x 64 KB), every lane finds where its
-// kPulseMergeItems outputs start on the merge path (one binary search) and merges them from LDS.
-// (Ranking every element by its own binary search costs eight random-address searches per lane:
-// bank conflicts made the merge LDS-bound, ~11 us a level.)
-__device__ void pulse_merge_path(PulseRuns in, uint32_t a, uint32_t b, uint32_t la, uint32_t lb,
-                                 uint32_t L, PulseRuns out, uint32_t r, uint64_t* A, uint64_t* B,
-                                 const PulsePack& P) {
-    const uint32_t tid = threadIdx.x;
+template <typename K, typename Pack, typename Unpack>
+__device__ __forceinline__ void pulse_merge_seg(PulseRuns in, uint32_t a, uint32_t b, uint32_t la, uint32_t lb,
+                                uint32_t L, PulseRuns out, uint32_t r, uint32_t d0, K* A, K* B, K* O,
+                                uint32_t* cut, K none, Pack pack, Unpack unpack) {
+    const uint32_t tid = threadIdx.x, wave = tid >> 6;
     const uint64_t* ae = in.exp + uint64_t(a) * in.stride;
     const uint64_t* ar = in.row + uint64_t(a) * in.stride;
     const uint64_t* be = in.exp + uint64_t(b) * in.stride;
     const uint64_t* br = in.row + uint64_t(b) * in.stride;
-    uint64_t va[kPulseMergeItems], vb[kPulseMergeItems];
-#pragma unroll
-    for (uint32_t j = 0; j < kPulseMergeItems; j++) {
-        const uint32_t i = j * kPulseThreads + tid;
-        va[j] = i < la ? P.key(ae[i], ar[i]) : 0;
-        vb[j] = i < lb ? P.key(be[i], br[i]) : 0;
-    }
-#pragma unroll
-    for (uint32_t j = 0; j < kPulseMergeItems; j++) {
-        const uint32_t i = j * kPulseThreads + tid;
-        if (i < la) A[i] = va[j];
-        if (i < lb) B[i] = vb[j];
+    const uint32_t d1 = d0 + kPulseSeg < L ? d0 + kPulseSeg : L;
+    if (wave < 2) {
+        const uint32_t d = wave ? d1 : d0;
+        const uint32_t i = pulse_diagonal<K>(
+            d, la, lb, [=](uint32_t x) { return pack(ae[x], ar[x]); },
+            [=](uint32_t x) { return pack(be[x], br[x]); });
+        if ((tid & 63) == 0) cut[wave] = i;
     }
     __syncthreads();
-    // This lane's outputs d .. d + kPulseMergeItems - 1, merged into registers, then through LDS
-    // (over A, once every lane is done reading) to coalesced stores: a lane storing its own
-    // consecutive outputs made every store instruction touch 64 lines.
-    const uint32_t d = tid * kPulseMergeItems;
-    uint64_t o[kPulseMergeItems];
-    if (d < L) {
-        // the number of A's keys among the first d outputs: the smallest i with A[i] after B[d-1-i]
-        uint32_t lo = d > lb ? d - lb : 0, hi = d < la ? d : la;
+    const uint32_t i0 = cut[0], i1 = cut[1];
+    const uint32_t j0 = d0 - i0, j1 = d1 - i1;
+    const uint32_t na = i1 - i0, nb = j1 - j0;
+    for (uint32_t x = tid; x < na; x += kPulseSegThreads) A[x] = pack(ae[i0 + x], ar[i0 + x]);
+    for (uint32_t x = tid; x < nb; x += kPulseSegThreads) B[x] = pack(be[j0 + x], br[j0 + x]);
+    __syncthreads();
+    const uint32_t n = d1 - d0, dd = tid * kPulseSegItems;
+    if (dd < n) {
+        uint32_t lo = dd > nb ? dd - nb : 0, hi = dd < na ? dd : na;
         while (lo < hi) {
             const uint32_t mid = (lo + hi) >> 1;
-            if (B[d - 1 - mid] < A[mid]) hi = mid;
+            if (sort_less(B[dd - 1 - mid], A[mid])) hi = mid;
             else lo = mid + 1;
         }
-        uint32_t i = lo, j = d - lo;
-        uint64_t x = i < la ? A[i] : ~0ull, y = j < lb ? B[j] : ~0ull;
+        uint32_t i = lo, j = dd - lo;
+        K x = i < na ? A[i] : none, y = j < nb ? B[j] : none;
 #pragma unroll
-        for (uint32_t m = 0; m < kPulseMergeItems; m++) {
-            const bool take_a = x < y;  // (distinct keys; an exhausted run reads as ~0)
-            o[m] = take_a ? x : y;
+        for (uint32_t m = 0; m < kPulseSegItems; m++) {
+            if (dd + m >= n) break;
+            const bool take_a = j >= nb || (i < na && sort_less(x, y));
             if (take_a) {
+                O[dd + m] = x;
                 i++;
-                x = i < la ? A[i] : ~0ull;
+                if (i < na) x = A[i];
             } else {
+                O[dd + m] = y;
                 j++;
-                y = j < lb ? B[j] : ~0ull;
+                if (j < nb) y = B[j];
             }
         }
     }
     __syncthreads();
-    if (d < L) {
-#pragma unroll
-        for (uint32_t m = 0; m < kPulseMergeItems; m++)
-            if (d + m < L) A[d + m] = o[m];
-    }
-    __syncthreads();
-    uint64_t* oe = out.exp + uint64_t(r) * out.stride;
-    uint64_t* orow = out.row + uint64_t(r) * out.stride;
-    const uint64_t mask = (1ull << P.row_bits) - 1;
-    for (uint32_t q = tid; q < L; q += kPulseThreads) {
-        const uint64_t v = A[q];
-        oe[q] = P.base + (v >> P.row_bits);
-        orow[q] = v & mask;
-    }
+    uint64_t* oe = out.exp + uint64_t(r) * out.stride + d0;
+    uint64_t* orow = out.row + uint64_t(r) * out.stride + d0;
+    for (uint32_t q = tid; q < n; q += kPulseSegThreads) unpack(O[q], &oe[q], &orow[q]);
 }
 
 // The runs holding candidates, and the merge levels over them.
@@ -294,28 +257,43 @@ __device__ inline void pulse_report_one(unsigned long long* counters, unsigned l
 // the pulse. (One launch for the whole tree, the second child of a pair to finish merging it, took
 // 77 us against ~45: every hand-off between workgroups paid an agent-scope release and acquire --
 // the L2 written back and invalidated -- where a kernel boundary pays it once.)
-__global__ void __launch_bounds__(kPulseThreads) pulse_merge(PulseRuns in, uint32_t runs_in,
-                                                            uint32_t k, PulseRuns out,
-                                                            const unsigned long long* counters,
-                                                            uint64_t timestamp, uint32_t row_bits,
-                                                            uint32_t level) {
+__global__ void __launch_bounds__(kPulseSegThreads) pulse_merge(PulseRuns in, uint32_t runs_in,
+                                                               uint32_t k, PulseRuns out,
+                                                               const unsigned long long* counters,
+                                                               uint64_t timestamp, uint32_t row_bits,
+                                                               uint32_t level) {
     if (level >= pulse_levels(pulse_live_runs(counters))) return;
     __shared__ union {
-        uint64_t u[2][kPulseRun];
-        PulseKey p[kPulseRun];
+        uint64_t u[3][kPulseSeg];
+        PulseKey p[3][kPulseSeg];
     } lds;
-    const uint32_t r = blockIdx.x;
+    __shared__ uint32_t cut[2];
+    const uint32_t r = blockIdx.x / kPulseSegs, s = blockIdx.x % kPulseSegs;
     const uint32_t a = 2 * r, b = 2 * r + 1;
     const uint32_t la = a < runs_in ? in.len[a] : 0, lb = b < runs_in ? in.len[b] : 0;
     const uint32_t L = la + lb < k ? la + lb : k;
-    if (threadIdx.x == 0) out.len[r] = L;
-    if (L == 0) return;
+    if (s == 0 && threadIdx.x == 0) out.len[r] = L;
+    const uint32_t d0 = s * kPulseSeg;
+    if (d0 >= L) return;
     const PulsePack P = pulse_pack(counters, timestamp, row_bits);
-    if (P.packed)
-        pulse_merge_path(in, a, b, la, lb, L, out, r, lds.u[0], lds.u[1], P);
-    else
-        pulse_merge_pair<PulseKey>(in, a, b, la, lb, L, out, r, lds.p,
-                                   [](uint64_t e, uint64_t rw) { return PulseKey{e, uint32_t(rw), 0}; });
+    if (P.packed) {
+        const uint64_t mask = (1ull << row_bits) - 1;
+        pulse_merge_seg<uint64_t>(
+            in, a, b, la, lb, L, out, r, d0, lds.u[0], lds.u[1], lds.u[2], cut, ~0ull,
+            [=](uint64_t e, uint64_t rw) { return P.key(e, rw); },
+            [=](uint64_t v, uint64_t* e, uint64_t* rw) {
+                *e = P.base + (v >> row_bits);
+                *rw = v & mask;
+            });
+    } else {
+        pulse_merge_seg<PulseKey>(
+            in, a, b, la, lb, L, out, r, d0, lds.p[0], lds.p[1], lds.p[2], cut, PulseKey{~0ull, ~0u, 0},
+            [](uint64_t e, uint64_t rw) { return PulseKey{e, uint32_t(rw), 0}; },
+            [](const PulseKey& v, uint64_t* e, uint64_t* rw) {
+                *e = v.e;
+                *rw = v.r;
+            });
+    }
 }
 
 // After `levels` merge launches the host reads the result from the first buffers when `levels` is
