@@ -58,7 +58,11 @@ struct PulseScratch {
     uint32_t* run_len = nullptr;  // two arrays of capacity / kPulseSortRun + 1
     bool counters_clean = false;  // (tbg_pulse's report clears them for the next pulse)
     unsigned long long* counters = nullptr;  // kept, candidates, earliest unexpired, expired
+    unsigned long long* counters_next = nullptr;  // (the other set of two: tbg_pulse alternates)
+    unsigned long long* counters_base = nullptr;  // (the allocation holding both)
     unsigned int* expired = nullptr;
+    uint64_t* sel = nullptr;  // tbg_pulse's expired rows, in order (kPulseRun)
+    PulseRuns first{}, second{};  // the last selection's buffers (pulse_apply_root)
 };
 
 // Flow replay scratch (flow.hpp, group.hpp), grown on demand to the largest replay list seen.
@@ -926,7 +930,7 @@ int ensure_pulse_scratch(tbg_ctx* ctx, uint64_t count) {
     if (!S.keep && !dev_alloc(ctx, &S.keep, ctx->T.expiry_capacity, false)) return TBG_ENOMEM;
     if (S.counters && count <= S.capacity) return 0;
     for (void* p : {(void*)S.exp, (void*)S.ts, (void*)S.rows, (void*)S.exp_b, (void*)S.rows_b,
-                    (void*)S.counters, (void*)S.run_len, (void*)S.expired})
+                    (void*)S.counters_base, (void*)S.run_len, (void*)S.expired, (void*)S.sel})
         if (p) (void)hipFree(p);
     uint64_t* keep = S.keep;
     S = PulseScratch();
@@ -939,8 +943,11 @@ int ensure_pulse_scratch(tbg_ctx* ctx, uint64_t count) {
           dev_alloc(ctx, &S.ts, cap, false) && dev_alloc(ctx, &S.rows, cap, false) &&
           dev_alloc(ctx, &S.exp_b, cap, false) && dev_alloc(ctx, &S.rows_b, cap, false) &&
           dev_alloc(ctx, &S.run_len, 2 * (cap / kPulseSortRun + 1), false) &&
-          dev_alloc(ctx, &S.expired, 1, true) && dev_alloc(ctx, &S.counters, 8, false)))
+          dev_alloc(ctx, &S.expired, 1, true) && dev_alloc(ctx, &S.counters_base, 16, false) &&
+          dev_alloc(ctx, &S.sel, kPulseRun, false)))
         return TBG_ENOMEM;
+    S.counters = S.counters_base;
+    S.counters_next = S.counters_base + 8;
     S.capacity = cap;
     return 0;
 }
@@ -2467,7 +2474,7 @@ struct PulseGather {
 // S.exp / S.rows (pulse.hpp: LDS-sorted runs, pairwise merges keeping the first k); the entries still
 // pending at S.keep; the counters on device. `out`: the counters on the host too (one sync).
 int pulse_select(tbg_ctx* ctx, uint64_t timestamp, uint32_t k, PulseGather* out,
-                 bool settle = false, unsigned long long* report = nullptr) {
+                 bool settle = false, unsigned long long* report = nullptr, bool fused = false) {
     int rc = 0;
     // The index length: known on the host since the last call or pulse (else one synchronisation).
     if (!ctx->expiry_known) {
@@ -2510,17 +2517,24 @@ int pulse_select(tbg_ctx* ctx, uint64_t timestamp, uint32_t k, PulseGather* out,
             live = next;
             levels++;
         }
-        if (levels)  // (moves the result where the host reads it; settles a pulse)
+        S.first = first;
+        S.second = second;
+        if (fused) {
+            // (pulse_apply_root reads the result where the levels that ran left it)
+        } else if (levels)  // (moves the result where the host reads it; settles a pulse)
             hipLaunchKernelGGL(pulse_final_copy, dim3(1), dim3(kPulseThreads), 0, ctx->stream, first,
                                second, S.counters, levels, ctx->T, S.expired, k, uint32_t(settle),
                                report);
         else if (settle)
             hipLaunchKernelGGL(pulse_settle, dim3(1), dim3(64), 0, ctx->stream, ctx->T, S.exp,
                                S.counters, S.expired, k, report);
-        if (swapped) {  // (the result is in the second buffers: they become the first)
+        if (swapped && !fused) {  // (the result is in the second buffers: they become the first)
             std::swap(S.exp, S.exp_b);
             std::swap(S.rows, S.rows_b);
         }
+    } else if (fused) {
+        S.first = PulseRuns{S.exp, S.rows, S.run_len, kPulseSortRun};
+        S.second = S.first;
     } else if (settle) {
         hipLaunchKernelGGL(pulse_settle, dim3(1), dim3(64), 0, ctx->stream, ctx->T, S.exp, S.counters,
                            S.expired, k, report);
@@ -2638,7 +2652,7 @@ int64_t tbg_pulse(tbg_ctx* ctx, uint64_t timestamp) {
     uint32_t ae_epoch = 0;
     int rc = 0;
     if (htrace) ht[1] = now_ms();
-    rc = pulse_select(ctx, timestamp, k, nullptr, true, ctx->dh_pulse);
+    rc = pulse_select(ctx, timestamp, k, nullptr, false, nullptr, true);
     if (rc) return rc;
     if (htrace) ht[2] = now_ms();
     // (after the selection's launches: deferred side-stream work -- a call's snapshot, which reads
@@ -2655,34 +2669,35 @@ int64_t tbg_pulse(tbg_ctx* ctx, uint64_t timestamp) {
     PulseScratch& S = ctx->pulse;
     const uint64_t count = std::min<uint64_t>(ctx->expiry_host, ctx->T.expiry_capacity);
     const uint32_t upper = uint32_t(std::min<uint64_t>(count, k));
-    if (count) {
-        // The index keeps the entries still pending: pulse_collect wrote them to S.keep, which
-        // becomes the index (the old one the next pulse's scratch; both hold expiry_capacity).
-        std::swap(ctx->T.expiry, S.keep);
-        hipLaunchKernelGGL(pulse_apply, dim3(grid_for(upper)), dim3(kBlock), 0, ctx->stream, ctx->T,
-                           S.rows, uint64_t(upper), S.expired);
-    }
+    // The index keeps the entries still pending: pulse_collect wrote them to S.keep, which becomes
+    // the index (the old one the next pulse's scratch; both hold expiry_capacity).
+    if (count) std::swap(ctx->T.expiry, S.keep);
+    // Expire, settle, report; the counters' other set cleared for the next pulse.
+    hipLaunchKernelGGL(pulse_apply_root, dim3(upper ? grid_for(upper) : 1), dim3(kBlock), 0,
+                       ctx->stream, S.first, S.second, S.counters, S.counters_next, ctx->T, k,
+                       S.sel, S.expired, ctx->dh_pulse);
     HIP_TRY(ctx, hipGetLastError());
+    std::swap(S.counters, S.counters_next);
     tmark(ctx, "pulse:apply");
     ctx->expiry_known = false;
     // The expiries' AccountEvents behind the next call (the side stream: the snapshot here, the
     // appends queued by the next call once its own kernels are queued), or here.
     if (ae_async && upper) {
         ctx->h_pulse[3] = 0;
-        AeExpirySnap J{ctx->T, S.rows, S.expired, timestamp, ctx->ae_stage[ctx->ae_parity], ae_epoch,
+        AeExpirySnap J{ctx->T, S.sel, S.expired, timestamp, ctx->ae_stage[ctx->ae_parity], ae_epoch,
                        ctx->dh_pulse + 3};
         hipLaunchKernelGGL(ae_expiry_snapshot, dim3(kAeAsyncMax / kSnapThreads), dim3(kSnapThreads), 0, ctx->stream, J);
         HIP_TRY(ctx, hipGetLastError());
     } else if (ctx->ae_log && upper) {
         ae_async = false;
-        rc = ae_expiry(ctx, S.rows, upper, timestamp, nullptr, S.expired);
+        rc = ae_expiry(ctx, S.sel, upper, timestamp, nullptr, S.expired);
     } else {
         ae_async = false;
     }
     if (rc) return rc;
     // The count expired and the index's new length came to mapped pinned memory with the
-    // settlement (pulse_final_copy / pulse_settle: no copy-engine hand-off), which also cleared the
-    // counters; one synchronisation.
+    // settlement (pulse_apply_root: no copy-engine hand-off), which also cleared the counters the
+    // next pulse takes; one synchronisation.
     S.counters_clean = true;
     if (htrace) ht[3] = now_ms();
     if (ae_async) ae_defer_graph(ctx, upper, ae_epoch, true);

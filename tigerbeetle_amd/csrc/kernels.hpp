@@ -2307,10 +2307,7 @@ __global__ void pulse_key_timestamps(Tables T, const uint64_t* rows, uint64_t n,
 
 // execute_expire_pending_transfers (:4540-4626) for the selected rows.
 // (n_dev: the count on device, n its upper bound)
-__global__ void pulse_apply(Tables T, const uint64_t* rows, uint64_t n, const unsigned int* n_dev) {
-    const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (i >= n || (n_dev && i >= *n_dev)) return;
-    const uint64_t row = rows[i];
+__device__ inline void pulse_apply_one(Tables T, uint64_t row) {
     const tb_transfer_t& p = T.tr_rows[row];
     const uint64_t dr_row = account_find(T, p.debit_account_id);
     const uint64_t cr_row = account_find(T, p.credit_account_id);
@@ -2327,6 +2324,12 @@ __global__ void pulse_apply(Tables T, const uint64_t* rows, uint64_t n, const un
     if (p.flags & TB_TRANSFER_CLOSING_CREDIT)
         atomicAnd(account_code_flags_word(cr), ~(uint32_t(TB_ACCOUNT_CLOSED) << 16));
     T.tr_status[row] = TB_PENDING_EXPIRED;
+}
+
+__global__ void pulse_apply(Tables T, const uint64_t* rows, uint64_t n, const unsigned int* n_dev) {
+    const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i >= n || (n_dev && i >= *n_dev)) return;
+    pulse_apply_one(T, rows[i]);
 }
 
 // ================================ lookups, dumps, indexes ===================================

@@ -323,6 +323,40 @@ __global__ void __launch_bounds__(kPulseThreads) pulse_final_copy(PulseRuns firs
     }
 }
 
+// tbg_pulse's last selection launch, in place of pulse_final_copy + pulse_apply: the selection is
+// where the merge levels that ran left it (the first buffers after an even number, else the
+// second); its first min(candidates, k) rows expire and are copied to `sel` (the expiries'
+// AccountEvents read them there), and workgroup 0 settles the pulse (pulse_settle_one's values),
+// reports to the host and clears `next_counters`, the set the next pulse takes (tbg_pulse
+// alternates two: this pulse's own is still being read here).
+__global__ void pulse_apply_root(PulseRuns first, PulseRuns second,
+                                 const unsigned long long* counters,
+                                 unsigned long long* next_counters, Tables T, uint32_t k,
+                                 uint64_t* sel, unsigned int* expired_out,
+                                 unsigned long long* report) {
+    const uint32_t ran = pulse_levels(pulse_live_runs(counters));
+    const PulseRuns src = (ran & 1) ? second : first;
+    const uint64_t C = counters[1];
+    const uint64_t n = C < k ? C : k;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        uint64_t next = counters[2] == ~0ull ? TB_TIMESTAMP_MAX : counters[2];
+        if (C >= k && k > 0) next = src.exp[k - 1];
+        T.scalars->pulse_next_timestamp = next;
+        T.scalars->expiry_count = counters[0];
+        *expired_out = uint32_t(n);
+        report[0] = n;
+        report[1] = counters[0];
+        __threadfence_system();
+        pulse_counters_clear(next_counters);
+    }
+    const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i < n) {
+        const uint64_t row = src.row[i];
+        sel[i] = row;
+        pulse_apply_one(T, row);
+    }
+}
+
 // After the selection (the first min(candidates, k) in order at exp / rows): the number expired,
 // the index's new length (the entries still pending) and pulse_next_timestamp -- the k-th expiry
 // when the scan filled its batch, else the earliest unexpired one (timestamp_max if none).
