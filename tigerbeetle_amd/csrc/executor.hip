@@ -170,6 +170,7 @@ struct tbg_ctx {
     uint32_t* ev_dr = nullptr;
     uint32_t* ev_cr = nullptr;
     uint64_t* ev_amount = nullptr;
+    uint64_t* ev_prow = nullptr;
     uint8_t* ev_info = nullptr;
     uint8_t* ev_slow = nullptr;
     uint32_t* slow_list = nullptr;
@@ -489,6 +490,7 @@ Call<Event> make_call(tbg_ctx* ctx, const Event* d_events, uint32_t n, const uin
     c.ev_dr = ctx->ev_dr;
     c.ev_cr = ctx->ev_cr;
     c.ev_amount = ctx->ev_amount;
+    c.ev_prow = ctx->ev_prow;
     c.ev_info = ctx->ev_info;
     c.ev_slow = ctx->ev_slow;
     c.slow_list = ctx->slow_list;
@@ -1910,6 +1912,7 @@ tbg_ctx* tbg_open(const tbg_options* options) {
          dev_alloc(ctx, &ctx->d_batch_ts, options->batch_count_max, false) &&
          dev_alloc(ctx, &ctx->ev_slot, ev_max, false) && dev_alloc(ctx, &ctx->ev_dr, ev_max, false) &&
          dev_alloc(ctx, &ctx->ev_cr, ev_max, false) && dev_alloc(ctx, &ctx->ev_amount, ev_max, false) &&
+         dev_alloc(ctx, &ctx->ev_prow, ev_max, false) &&
          dev_alloc(ctx, &ctx->ev_info, ev_max, false) && dev_alloc(ctx, &ctx->ev_slow, ev_max, false) &&
          dev_alloc(ctx, &ctx->slow_list, ev_max, false) &&
          dev_alloc(ctx, &ctx->fix_slots, ev_max, false) &&
@@ -2041,7 +2044,7 @@ void tbg_close(tbg_ctx* ctx) {
                     ctx->T.acc_closable, ctx->T.tr.slots, ctx->T.tr_rows, ctx->T.tr_live,
                     ctx->T.tr_status, ctx->T.expiry, ctx->d_scalars, ctx->T.undo, ctx->d_events,
                     ctx->d_results, ctx->d_batch_ends, ctx->d_batch_ts, ctx->ev_slot, ctx->ev_dr,
-                    ctx->ev_cr, ctx->ev_amount, ctx->ev_info, ctx->ev_slow, ctx->slow_list,
+                    ctx->ev_cr, ctx->ev_amount, ctx->ev_prow, ctx->ev_info, ctx->ev_slow, ctx->slow_list,
                     ctx->fix_slots, ctx->d_stage_done,
                     ctx->pnt_call, ctx->pnt_fired, ctx->pv_slots,
                     ctx->bal_items, ctx->chunk_info, ctx->bal_items_sorted, ctx->bucket_words, ctx->bucket_partials,

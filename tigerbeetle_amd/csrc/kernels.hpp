@@ -272,6 +272,7 @@ __device__ inline uint64_t pv_pending_row(const Tables& T, const Call<tb_transfe
 struct PvFast {
     uint32_t dr, cr;  // the pending transfer's account rows
     uint64_t amount;  // the amount posted (void: 0)
+    uint64_t prow;    // the pending transfer's row
 };
 
 // post_or_void_pending_transfer's checks (:4053-4246) for a fresh, unique id; DONE where the
@@ -350,6 +351,7 @@ __device__ inline uint8_t classify_post_void(const Tables& T, const Call<tb_tran
     out->dr = ed.ref - 1;
     out->cr = ec.ref - 1;
     out->amount = (f & TB_TRANSFER_POST_PENDING) ? uint64_t(amount) : 0;
+    out->prow = pr;
     return kClassFast;
 }
 
@@ -570,7 +572,7 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
     uint64_t slot = kNone;
     AccSnap dr, cr;
     dr.row = cr.row = kNone32;
-    PvFast pv{kNone32, kNone32, 0};
+    PvFast pv{kNone32, kNone32, 0, kNone};
     if (pre_done) {
         cls = kClassDone;
     } else {
@@ -714,6 +716,7 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
         if (pending && tn.timeout() > 0) need_commit = true;  // expires_at index
         if (pv_fast) {
             need_commit = true;
+            c.ev_prow[k] = pv.prow;  // (tr_commit applies it without looking the pending id up)
             if (c.bal_items && c.pair_shift) c.bal_items[k] = ~0ull;
             else if (c.bal_items)
                 *reinterpret_cast<uint4*>(c.bal_items + 2 * uint64_t(k)) = make_uint4(~0u, ~0u, ~0u, ~0u);
@@ -1279,7 +1282,7 @@ __device__ inline ChainPre chain_pre_wave(const Tables& T, const Call<tb_transfe
 __device__ inline void commit_post_void(const Tables& T, const Call<tb_transfer_t>& c, uint32_t k,
                                         uint64_t row, uint64_t ts, uint32_t dr, uint32_t cr) {
     const tb_transfer_t t = c.events[k];
-    const uint64_t pr = pv_pending_row(T, c, t.pending_id);
+    const uint64_t pr = c.ev_prow[k];  // (ingest's lookup: committed slots and rows are fixed)
     const tb_transfer_t p = T.tr_rows[pr];
     const bool post = (t.flags & TB_TRANSFER_POST_PENDING) != 0;
     const u128 p_amount = U(p.amount);
@@ -1300,12 +1303,29 @@ __device__ inline void commit_post_void(const Tables& T, const Call<tb_transfer_
     o.timestamp = ts;
     T.tr_rows[row] = o;
     T.tr_status[pr] = post ? TB_PENDING_POSTED : TB_PENDING_VOIDED;
-    atomic_sub_u128(&T.acc_rows[dr].debits_pending, p_amount);
-    atomic_sub_u128(&T.acc_rows[cr].credits_pending, p_amount);
-    if (post && amount) {
-        if (atomic_add_u128(&T.acc_rows[dr].debits_posted, amount) >= kHazardHiLimit)
+    // The balance words as atomic_sub_u128 / atomic_add_u128 would update them, the four low-word
+    // adds in flight together and their carries after (FAST: both amounts are < 2^64,
+    // classify_post_void): one atomic round trip on the event's path instead of four in sequence.
+    const uint64_t pa = uint64_t(p_amount), am = uint64_t(amount);
+    const bool posts = post && am != 0;
+    tb_account_t* A = T.acc_rows;
+    unsigned long long* dpe = reinterpret_cast<unsigned long long*>(&A[dr].debits_pending);
+    unsigned long long* cpe = reinterpret_cast<unsigned long long*>(&A[cr].credits_pending);
+    unsigned long long* dpo = reinterpret_cast<unsigned long long*>(&A[dr].debits_posted);
+    unsigned long long* cpo = reinterpret_cast<unsigned long long*>(&A[cr].credits_posted);
+    const uint64_t o_dpe = atomicAdd(dpe, 0ull - pa);
+    const uint64_t o_cpe = atomicAdd(cpe, 0ull - pa);
+    uint64_t o_dpo = 0, o_cpo = 0;
+    if (posts) {
+        o_dpo = atomicAdd(dpo, am);
+        o_cpo = atomicAdd(cpo, am);
+    }
+    if (o_dpe < pa) atomicAdd(dpe + 1, ~0ull);  // (borrows: the hi word less one)
+    if (o_cpe < pa) atomicAdd(cpe + 1, ~0ull);
+    if (posts) {
+        if (o_dpo + am < o_dpo && atomicAdd(dpo + 1, 1ull) + 1 >= kHazardHiLimit)
             acc_hazard_set(T.acc_index, T.acc_entry_of, dr, kHazardHigh);
-        if (atomic_add_u128(&T.acc_rows[cr].credits_posted, amount) >= kHazardHiLimit)
+        if (o_cpo + am < o_cpo && atomicAdd(cpo + 1, 1ull) + 1 >= kHazardHiLimit)
             acc_hazard_set(T.acc_index, T.acc_entry_of, cr, kHazardHigh);
     }
     if (p.timeout != 0)

@@ -128,6 +128,7 @@ struct Call {
     uint32_t* ev_dr;       // account rows (create_transfers)
     uint32_t* ev_cr;
     uint64_t* ev_amount;   // amount low word of parallel-path candidates
+    uint64_t* ev_prow;     // FAST post/void: its pending transfer's row (classify_post_void)
     uint8_t* ev_info;      // kInfo* bits
     uint8_t* ev_slow;      // 1 = executes in the ordered replay
     const uint32_t* slow_list;
