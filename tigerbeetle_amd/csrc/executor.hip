@@ -175,6 +175,7 @@ struct tbg_ctx {
     uint8_t* ev_slow = nullptr;
     uint32_t* slow_list = nullptr;
     uint32_t* fix_slots = nullptr;  // tr_commit's fixed failures' id slots (Call::fix_slots)
+    unsigned long long* chain_planes = nullptr;  // (Call::chain_planes, calls past kInlineChunkMax)
     uint64_t* pnt_call = nullptr;           // pulse_next_timestamp updates per event (post/void)
     bool pnt_sharded = false;               // tbg_set_pnt_sharded: every call records its updates
     Call<tb_transfer_t> pnt_last{};         // the last create_transfers call (tbg_pnt_ops)
@@ -497,6 +498,7 @@ Call<Event> make_call(tbg_ctx* ctx, const Event* d_events, uint32_t n, const uin
     c.pnt_call = ctx->pnt_call;
     c.events_out = nullptr;
     c.fix_slots = ctx->fix_slots;
+    c.chain_planes = nullptr;
     // (TBG_NO_PV_FAST: every post/void replays)
     c.pv_slots = getenv("TBG_NO_PV_FAST") ? nullptr : ctx->pv_slots;
     c.pv_mask = ctx->pv_mask;
@@ -1916,6 +1918,7 @@ tbg_ctx* tbg_open(const tbg_options* options) {
          dev_alloc(ctx, &ctx->ev_info, ev_max, false) && dev_alloc(ctx, &ctx->ev_slow, ev_max, false) &&
          dev_alloc(ctx, &ctx->slow_list, ev_max, false) &&
          dev_alloc(ctx, &ctx->fix_slots, ev_max, false) &&
+         dev_alloc(ctx, &ctx->chain_planes, (uint64_t(ev_max) + 63) / 64 * kPlWords, false) &&
          dev_alloc(ctx, &ctx->pnt_call, ev_max, false) && dev_alloc(ctx, &ctx->pnt_fired, 4, true) &&
          dev_alloc(ctx, &ctx->pv_slots, next_pow2(2 * uint64_t(ev_max)), true);
     ctx->pv_mask = next_pow2(2 * uint64_t(ev_max)) - 1;
@@ -2045,7 +2048,7 @@ void tbg_close(tbg_ctx* ctx) {
                     ctx->T.tr_status, ctx->T.expiry, ctx->d_scalars, ctx->T.undo, ctx->d_events,
                     ctx->d_results, ctx->d_batch_ends, ctx->d_batch_ts, ctx->ev_slot, ctx->ev_dr,
                     ctx->ev_cr, ctx->ev_amount, ctx->ev_prow, ctx->ev_info, ctx->ev_slow, ctx->slow_list,
-                    ctx->fix_slots, ctx->d_stage_done,
+                    ctx->fix_slots, ctx->chain_planes, ctx->d_stage_done,
                     ctx->pnt_call, ctx->pnt_fired, ctx->pv_slots,
                     ctx->bal_items, ctx->chunk_info, ctx->bal_items_sorted, ctx->bucket_words, ctx->bucket_partials,
                     ctx->window_partials, ctx->window_carry, ctx->window_counts, ctx->window_ts,
@@ -2175,6 +2178,13 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
         if (int frc = ae_snap_flush1(ctx)) return frc;
         hipLaunchKernelGGL(tr_ingest, dim3(ig), block, 0, ctx->stream, ctx->T, c);
         tmark(ctx, "tr_ingest");
+        // (large calls: chains resolved from bit planes -- a launch that returns at once when the
+        // call has no chain to confirm; TBG_NO_CHAIN_PLANES: tr_commit walks them itself)
+        static const bool planes = getenv("TBG_NO_CHAIN_PLANES") == nullptr;
+        if (planes) {
+            c.chain_planes = ctx->chain_planes;
+            hipLaunchKernelGGL(tr_chain_planes, grid, block, 0, ctx->stream, ctx->T, c);
+        }
         hipLaunchKernelGGL(tr_commit, grid, block, 0, ctx->stream, ctx->T, c);
         tmark(ctx, "tr_commit");
         rc = hip_ok(ctx, hipGetLastError(), "launch") ? 0 : TBG_EHIP;

@@ -1216,6 +1216,63 @@ struct ChainPre {
     bool has_fr;      // fr: the event's FastRec (FAST chain events)
     FastRec fr;
 };
+// Bit planes of a large call's linked chains (tr_chain_planes, before tr_commit): per 64-event
+// group, one word each of chain heads, chain ends, open ends, FAST events, demoted FAST chain
+// events (fast_demoted) and their later-claim statuses. Computed before tr_commit writes anything,
+// so from the state fast_demoted_peer reads. tr_commit then resolves every chain from the words of
+// three groups -- also chains that cross its wave's edges, which otherwise walked the chain event
+// by event with a chain of lookups each (config 4: ~100 us tails a 131k-event call).
+enum : uint32_t {
+    kPlHead, kPlEnd, kPlOpen, kPlFast, kPlDemoted, kPlPosted, kPlVoided, kPlWords = 8
+};
+
+// A chain event's ChainPre from the planes: the 64-event window whose bit 32 is event k (group
+// g = (k - lane) / 64 and its neighbours), chain bounds x <= 32 <= y, then chain_demoted /
+// chain_fail_status's rules. Every lane of the wave calls it.
+__device__ inline ChainPre chain_pre_planes(const Call<tb_transfer_t>& c, uint32_t kb, uint32_t lane,
+                                            bool in_chain, unsigned int call_flags, ChainPre p) {
+    const uint64_t g = kb / 64, groups = (uint64_t(c.n) + 63) / 64;
+    const unsigned long long* P = c.chain_planes;
+    auto win = [&](uint32_t plane) -> uint64_t {
+        const uint64_t b = P[g * kPlWords + plane];
+        if (lane < 32) {
+            const uint64_t a = g > 0 ? P[(g - 1) * kPlWords + plane] : 0ull;
+            return (a >> (32 + lane)) | (b << (32 - lane));
+        }
+        const uint64_t cw = g + 1 < groups ? P[(g + 1) * kPlWords + plane] : 0ull;
+        const uint32_t s = lane - 32;
+        return s ? (b >> s) | (cw << (64 - s)) : b;
+    };
+    const uint64_t H = win(kPlHead), E = win(kPlEnd), O = win(kPlOpen), F = win(kPlFast),
+                   D = win(kPlDemoted), LP = win(kPlPosted), LV = win(kPlVoided);
+    if (!in_chain) return p;
+    p.valid = true;
+    const uint64_t hb = H & ((2ull << 32) - 1);   // heads at or before this event
+    const uint64_t eb = E & ~((1ull << 32) - 1);  // ends at or after it
+    const uint32_t x = hb ? 63u - uint32_t(__builtin_clzll(hb)) : 0u;
+    const uint32_t y = eb ? uint32_t(__builtin_ctzll(eb)) : 63u;
+    // (x == 0: the head is kFastChainMax or more events back; eb == 0: the end is that far on)
+    if (x == 0 || !eb || y - x >= kFastChainMax || ((O >> y) & 1)) {
+        p.demoted = true;
+        return p;
+    }
+    const uint64_t cm = (y == 63 ? ~0ull : (2ull << y) - 1) & ~((1ull << x) - 1);
+    if ((F & cm) != cm) {
+        p.demoted = true;
+        return p;
+    }
+    const uint64_t pm = D & cm;
+    if (pm && (call_flags & kFlagPostVoid)) {
+        const uint32_t j = uint32_t(__builtin_ctzll(pm));
+        const uint32_t lc = ((LP >> j) & 1) ? uint32_t(TB_CT_PENDING_TRANSFER_ALREADY_POSTED)
+                            : ((LV >> j) & 1) ? uint32_t(TB_CT_PENDING_TRANSFER_ALREADY_VOIDED)
+                                              : 0u;
+        if (lc) p.fail = j == 32 ? lc : uint32_t(TB_CT_LINKED_EVENT_FAILED);
+    }
+    p.demoted = (pm & ~(1ull << 32)) != 0;
+    return p;
+}
+
 __device__ inline ChainPre chain_pre_wave(const Tables& T, const Call<tb_transfer_t>& c,
                                           uint32_t k, bool active, unsigned int call_flags) {
     ChainPre p{false, false, 0, -1, false, FastRec{}};
@@ -1240,6 +1297,7 @@ __device__ inline ChainPre chain_pre_wave(const Tables& T, const Call<tb_transfe
     }
     const bool in_chain = active && (linked || prev_linked);
     p.in_chain = in_chain ? 1 : 0;
+    if (c.chain_planes) return chain_pre_planes(c, k - lane, lane, in_chain, call_flags, p);
     const uint64_t head_m = __ballot(active && !prev_linked);
     const uint64_t end_m = __ballot(active && (!linked || open));
     const uint64_t open_m = __ballot(open);
@@ -1452,6 +1510,59 @@ __device__ inline void commit_event(const Tables& T, const Call<tb_transfer_t>& 
     }
     c.ev_slow[k] = slow;
     slow_out = slow;
+}
+
+// The planes (chain_pre_planes) of a call that raised a commit flag and has linked chains: the
+// per-event facts chain_pre_wave gathers, one ballot per plane.
+__global__ void tr_chain_planes(Tables T, Call<tb_transfer_t> c) {
+    const unsigned int call_flags = T.scalars->flags;
+    if (!(call_flags & kCommitFlags) || !(call_flags & kFlagChain)) return;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+    for (uint64_t kb = uint64_t(blockIdx.x) * blockDim.x + (threadIdx.x & ~63u); kb < c.n;
+         kb += stride) {
+        const uint32_t k = uint32_t(kb) + lane;
+        const bool active = k < c.n;
+        bool linked = false, prev_linked = false, open = false;
+        uint8_t cls = 0, info = 0;
+        if (active) {
+            linked = (c.events[k].flags & TB_TRANSFER_LINKED) != 0;
+            const bool pl = k > 0 && (c.events[k - 1].flags & TB_TRANSFER_LINKED);
+            if (linked || pl) {
+                const uint32_t b = batch_of_guess(c.batch_ends, c.n_batches, c.n, k);
+                const uint32_t bs = batch_start_of(c, b), be = c.batch_ends[b];
+                prev_linked = pl && k > bs;
+                open = linked && k + 1 >= be;  // linked_event_chain_open
+            }
+            info = c.ev_info[k];
+            cls = info & kInfoClassMask;
+        }
+        const bool in_chain = active && (linked || prev_linked);
+        bool pd = false;
+        uint32_t lc = 0;
+        if (in_chain && cls == kClassFast) {
+            const FastRec fr = fast_record(T, c, k, call_flags, info);
+            pd = fast_demoted(T, c, k, call_flags, fr);
+            if (pd && (call_flags & kFlagPostVoid)) lc = later_claim_status(T, c, k, call_flags);
+        }
+        const uint64_t w0 = __ballot(active && !prev_linked);
+        const uint64_t w1 = __ballot(active && (!linked || open));
+        const uint64_t w2 = __ballot(open);
+        const uint64_t w3 = __ballot(active && cls == kClassFast);
+        const uint64_t w4 = __ballot(pd);
+        const uint64_t w5 = __ballot(lc == TB_CT_PENDING_TRANSFER_ALREADY_POSTED);
+        const uint64_t w6 = __ballot(lc == TB_CT_PENDING_TRANSFER_ALREADY_VOIDED);
+        if (lane == 0) {
+            unsigned long long* o = c.chain_planes + (kb / 64) * kPlWords;
+            o[kPlHead] = w0;
+            o[kPlEnd] = w1;
+            o[kPlOpen] = w2;
+            o[kPlFast] = w3;
+            o[kPlDemoted] = w4;
+            o[kPlPosted] = w5;
+            o[kPlVoided] = w6;
+        }
+    }
 }
 
 // tr_commit: when ingest raised no commit flag, every event is a confirmed FAST event whose

@@ -162,6 +162,7 @@ struct Call {
     // tr_commit's fixed failures (later_claim_status): the id slots they release, tombstoned by
     // the next kernel (stage_out) -- tr_commit's threads read other events' slots.
     uint32_t* fix_slots;
+    unsigned long long* chain_planes;  // tr_chain_planes's words (null: tr_commit walks chains itself)
     // create_transfers: per-call claims of pending ids by post/void events (epoch:32 | event + 1;
     // words of other epochs are free): the earliest post/void of a pending transfer in the call.
     unsigned long long* pv_slots;
