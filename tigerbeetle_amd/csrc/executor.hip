@@ -176,6 +176,7 @@ struct tbg_ctx {
     uint32_t* slow_list = nullptr;
     uint32_t* fix_slots = nullptr;  // tr_commit's fixed failures' id slots (Call::fix_slots)
     unsigned long long* chain_planes = nullptr;  // (Call::chain_planes, calls past kInlineChunkMax)
+    bool chain_hint = true;  // the last large call had linked chains (tr_chain_planes is launched)
     uint64_t* pnt_call = nullptr;           // pulse_next_timestamp updates per event (post/void)
     bool pnt_sharded = false;               // tbg_set_pnt_sharded: every call records its updates
     Call<tb_transfer_t> pnt_last{};         // the last create_transfers call (tbg_pnt_ops)
@@ -2180,8 +2181,10 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
         tmark(ctx, "tr_ingest");
         // (large calls: chains resolved from bit planes -- a launch that returns at once when the
         // call has no chain to confirm; TBG_NO_CHAIN_PLANES: tr_commit walks them itself)
+        // (only while the calls have chains: the planes' launch alone costs ~5 us a call, and
+        // tr_commit is exact either way -- without planes it walks the chains)
         static const bool planes = getenv("TBG_NO_CHAIN_PLANES") == nullptr;
-        if (planes) {
+        if (planes && ctx->chain_hint) {
             c.chain_planes = ctx->chain_planes;
             hipLaunchKernelGGL(tr_chain_planes, grid, block, 0, ctx->stream, ctx->T, c);
         }
@@ -2275,6 +2278,7 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
         tmark(ctx, "host_sync");
     }
     const bool replay = !rc && ctx->h_scalars->stats[0] > 0;
+    if (!rc && n > kInlineChunkMax) ctx->chain_hint = (ctx->h_scalars->flags & kFlagChain) != 0;
     if (replay) ctx->ae_snap_early = false;
     if (!rc && ctx->ae_snap_side && !replay) {  // (no replay: the snapshot is final)
         rc = ae_snap_defer(ctx, c);
