@@ -2718,7 +2718,17 @@ int64_t tbg_pulse(tbg_ctx* ctx, uint64_t timestamp) {
     S.counters_clean = true;
     if (htrace) ht[3] = now_ms();
     if (ae_async) ae_defer_graph(ctx, upper, ae_epoch, true);
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    // (the host spins on a pinned word, as a call's end does: a stream synchronisation's wake-up
+    // is the slower path)
+    if (ctx->spin_sync && !ctx->timing) {
+        const unsigned int seq = ++ctx->seq ? ctx->seq : ++ctx->seq;
+        hipLaunchKernelGGL(host_signal, dim3(1), dim3(64), 0, ctx->stream, ctx->dh_seq, seq);
+        HIP_TRY(ctx, hipGetLastError());
+        rc = spin_wait(ctx, seq);
+        if (rc) return rc;
+    } else {
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    }
     if (htrace) {
         ht[4] = now_ms();
         fprintf(stderr, "pulse host us: prep %.1f select %.1f rest %.1f sync %.1f\n",

@@ -75,6 +75,15 @@ struct StageOut {
 
 // (A small call's AccountEvents staging follows in its own kernel, ae_snapshot: the host's wait
 // ends here.)
+// The end of a stream's work for a spinning host (tbg_pulse): `seq` into the pinned word, a
+// system-scope release after every earlier kernel of the stream.
+__global__ void host_signal(unsigned int* host_seq, unsigned int seq) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        __threadfence_system();
+        __hip_atomic_store(host_seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 __global__ void __launch_bounds__(kStageThreads) stage_out(StageOut s) {
     const uint32_t tid = blockIdx.x * kStageThreads + threadIdx.x;
     if (s.fix_slots) {
