@@ -1023,11 +1023,13 @@ struct FastRec {
     uint32_t s, dr, cr;
     uint64_t amount;
     bool post_void;
+    int8_t first = -1;  // a post/void: pv_first, when its caller already knows it (-1: not known)
 };
 __device__ inline FastRec fast_record(const Tables& T, const Call<tb_transfer_t>& c, uint32_t k,
                                       unsigned int call_flags, uint8_t info) {
     FastRec f;
     f.s = kNone32;
+    f.first = -1;
     f.post_void = (c.events[k].flags & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) != 0;
     const bool lean = (info & kInfoLean) != 0;
     if (lean && !c.bal_items) {
@@ -1070,7 +1072,8 @@ __device__ inline FastRec fast_record(const Tables& T, const Call<tb_transfer_t>
 __device__ inline bool fast_demoted(const Tables& T, const Call<tb_transfer_t>& c, uint32_t k,
                                     unsigned int call_flags, const FastRec& f) {
     const uint64_t ref = c.row_base + k + 1;
-    if (f.post_void && !pv_first(c, k, c.events[k].pending_id)) return true;
+    if (f.post_void && !(f.first >= 0 ? f.first != 0 : pv_first(c, k, c.events[k].pending_id)))
+        return true;
     return (call_flags & kFlagImported) ||
            ((call_flags & kFlagDuplicate) &&
             (f.s == kNone32 || (T.tr.slots[f.s] & kRefMask) != ref)) ||
@@ -1407,7 +1410,7 @@ __device__ inline void commit_event(const Tables& T, const Call<tb_transfer_t>& 
     if (pnt_rec) c.pnt_call[k] = 0;  // (the replay records its own)
     bool slow = cls == kClassSlow || (call_flags & kFlagImported);
     if (cls == kClassFast) {
-        const FastRec fr = pre.has_fr ? pre.fr : fast_record(T, c, k, call_flags, info);
+        FastRec fr = pre.has_fr ? pre.fr : fast_record(T, c, k, call_flags, info);
         const uint32_t s = fr.s, dr = fr.dr, cr = fr.cr;
         const uint64_t amount = fr.amount;
         const bool lean = (info & kInfoLean) != 0;
@@ -1420,10 +1423,15 @@ __device__ inline void commit_event(const Tables& T, const Call<tb_transfer_t>& 
                         k != batch_start_of(c, batch_of_guess(c.batch_ends, c.n_batches, c.n, k))));
         // Fixed failures of post/voids racing an earlier FAST one (later_claim_status): DONE.
         uint32_t fixed = 0;
-        if (!slow && (call_flags & kFlagPostVoid))
-            fixed = in_chain ? (pre.valid ? pre.fail : chain_fail_status(T, c, k, call_flags))
-                             : (fr.post_void && !pv_first(c, k, c.events[k].pending_id)
-                                    ? later_claim_status(T, c, k, call_flags) : 0u);
+        if (!slow && (call_flags & kFlagPostVoid)) {
+            if (in_chain) {
+                fixed = pre.valid ? pre.fail : chain_fail_status(T, c, k, call_flags);
+            } else if (fr.post_void) {
+                // (pv_first once: fast_demoted below reads it from the record)
+                fr.first = pv_first(c, k, c.events[k].pending_id) ? 1 : 0;
+                fixed = fr.first ? 0u : later_claim_status(T, c, k, call_flags);
+            }
+        }
         if (fixed) {
             // Undo the speculative liveness and balance effects (as a demotion does), release
             // the id (neither status is transient: the slot becomes a tombstone).
