@@ -1582,7 +1582,7 @@ __global__ void __launch_bounds__(kAeWinThreads) ae_dense_partials(AeDense A) {
 // into kAeSufGroups ranges, one wave per range: each wave sums its range, the ranges' totals
 // meet in LDS, and each wave then writes its range's suffixes from the total of the ranges
 // above it. (One lane per column walking every slice was a chain of slices/8 dependent load
-// batches: 20 us for a 1M-event call's 489 slices.)
+// batches: 20 us for a 131k-event call's 64 slices.)
 constexpr int kAeSufGroups = 16;
 constexpr int kAeSufThreads = 64 * kAeSufGroups;
 
