@@ -2453,11 +2453,19 @@ __device__ inline void pulse_apply_one(Tables T, uint64_t row) {
     if (dr_row == kNone || cr_row == kNone) return;
     tb_account_t* dr = &T.acc_rows[dr_row];
     tb_account_t* cr = &T.acc_rows[cr_row];
+    // (atomic_sub_u128 on both sides, the two low-word adds in flight together, borrows after)
     const u128 amount = U(p.amount);
-    if (amount) {
-        atomic_sub_u128(&dr->debits_pending, amount);
-        atomic_sub_u128(&cr->credits_pending, amount);
+    const uint64_t lo = uint64_t(amount), hi = uint64_t(amount >> 64);
+    unsigned long long* d = reinterpret_cast<unsigned long long*>(&dr->debits_pending);
+    unsigned long long* cw = reinterpret_cast<unsigned long long*>(&cr->credits_pending);
+    uint64_t od = 0, oc = 0;
+    if (lo) {
+        od = atomicAdd(d, 0ull - lo);
+        oc = atomicAdd(cw, 0ull - lo);
     }
+    const uint64_t hd = hi + (lo && od < lo ? 1u : 0u), hc = hi + (lo && oc < lo ? 1u : 0u);
+    if (hd) atomicAdd(d + 1, 0ull - hd);
+    if (hc) atomicAdd(cw + 1, 0ull - hc);
     if (p.flags & TB_TRANSFER_CLOSING_DEBIT)
         atomicAnd(account_code_flags_word(dr), ~(uint32_t(TB_ACCOUNT_CLOSED) << 16));
     if (p.flags & TB_TRANSFER_CLOSING_CREDIT)
