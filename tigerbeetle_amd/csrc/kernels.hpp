@@ -45,6 +45,9 @@
 #ifndef TBG_INGEST_JOINT_PROBE
 #define TBG_INGEST_JOINT_PROBE 1
 #endif
+#ifndef TBG_INGEST_PREV_SHFL
+#define TBG_INGEST_PREV_SHFL 1  // the previous event's flags by a lane shuffle (tr_ingest)
+#endif
 #ifndef TBG_INGEST_NARROW_B128
 #define TBG_INGEST_NARROW_B128 1  // the event's narrow fields by 16-byte LDS reads (EvNarrow)
 #endif
@@ -985,12 +988,21 @@ __global__ void __launch_bounds__(kBlock, TBG_INGEST_WG_PER_CU) tr_ingest(Tables
         // conflict-free ds_read_b128; the 2-8 byte ones put 2-4 lanes of a 32-lane group on a
         // bank. A register copy of the event would avoid that but spills at this kernel's
         // 128-VGPR budget.)
+        // (the previous event's flags from its lane: a 2-byte LDS read of its image at the
+        // 144-byte stride put 4 lanes on a bank)
+#if TBG_INGEST_PREV_SHFL
+        const uint32_t own_flags =
+            ev_narrow(*reinterpret_cast<const tb_transfer_t*>(my + lane * kLdsEventStride)).flags();
+        const uint32_t up_flags = __shfl_up(own_flags, 1, 64);
+#endif
         if (active) {
             const tb_transfer_t& t = *reinterpret_cast<const tb_transfer_t*>(my + lane * kLdsEventStride);
+#if !TBG_INGEST_PREV_SHFL
+            const uint32_t up_flags =
+                lane > 0 ? reinterpret_cast<const tb_transfer_t*>(my + (lane - 1) * kLdsEventStride)->flags : 0u;
+#endif
             const bool prev_linked =
-                lane > 0 ? !first_of_batch &&
-                               (reinterpret_cast<const tb_transfer_t*>(my + (lane - 1) * kLdsEventStride)
-                                    ->flags & TB_TRANSFER_LINKED) != 0
+                lane > 0 ? !first_of_batch && (up_flags & TB_TRANSFER_LINKED) != 0
                          : (w0 & kChunkPrevLinked) != 0;
             uint64_t fts = 0;
             flags |= ingest_event(T, c, k, t, batch_imported, ts_event, prev_linked, &fts,
