@@ -177,6 +177,7 @@ struct tbg_ctx {
     uint32_t* fix_slots = nullptr;  // tr_commit's fixed failures' id slots (Call::fix_slots)
     unsigned long long* chain_planes = nullptr;  // (Call::chain_planes, calls past kInlineChunkMax)
     bool chain_hint = true;  // the last large call had linked chains (tr_chain_planes is launched)
+    bool replay_hint = false;  // the last large call replayed (its results were downloaded twice)
     uint64_t* pnt_call = nullptr;           // pulse_next_timestamp updates per event (post/void)
     bool pnt_sharded = false;               // tbg_set_pnt_sharded: every call records its updates
     Call<tb_transfer_t> pnt_last{};         // the last create_transfers call (tbg_pnt_ops)
@@ -2278,7 +2279,10 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
         tmark(ctx, "host_sync");
     }
     const bool replay = !rc && ctx->h_scalars->stats[0] > 0;
-    if (!rc && n > kInlineChunkMax) ctx->chain_hint = (ctx->h_scalars->flags & kFlagChain) != 0;
+    if (!rc && n > kInlineChunkMax) {
+        ctx->chain_hint = (ctx->h_scalars->flags & kFlagChain) != 0;
+        ctx->replay_hint = replay;
+    }
     if (replay) ctx->ae_snap_early = false;
     if (!rc && ctx->ae_snap_side && !replay) {  // (no replay: the snapshot is final)
         rc = ae_snap_defer(ctx, c);
@@ -2436,7 +2440,10 @@ int tbg_create_transfers(tbg_ctx* ctx, const tb_transfer_t* events, uint32_t n,
     ctx->scalars_reset = n <= kInlineChunkMax;
     const double t1 = ctx->timing_host ? now_ms() : 0;
     ctx->ae_defer = true;
-    ctx->early_dst = results;
+    // (the results go to the host with the call's end unless the last large call replayed: a
+    // replay rewrites them, and the early copy -- ~70 us of PCIe writes for 131k results -- is then
+    // made for nothing; they are downloaded after the call instead)
+    ctx->early_dst = n > kInlineChunkMax && ctx->replay_hint ? nullptr : results;
     rc = tbg_create_transfers_device(ctx, reinterpret_cast<const tb_transfer_t*>(ctx->body_dst), n,
                                      ctx->d_batch_ends, ctx->d_batch_ts, nb, ctx->d_results,
                                      nullptr);
