@@ -92,6 +92,37 @@ int tbg_create_transfers_stamped_device(tbg_ctx* ctx, const tb_transfer_t* d_eve
                                         const uint64_t* d_event_timestamps,
                                         tb_create_result_t* d_results, void* stream);
 
+/* The same with host buffers, synchronous, for create_accounts too: the router's exact path
+ * (shard.py) sends a shard its events of an imported batch, or its part of a linked chain that
+ * spans shards, this way -- every event keeps its global timestamp and the events are one batch.
+ * `batch_timestamp` is the batch's `timestamp` (execute_create :3002-3104: imported events'
+ * must_not_advance bound; 0 = the last event's). Timestamps must be nonzero and increasing (else
+ * TBG_EINVAL). `options`: TBG_ONE_CHAIN -- the batch is one linked chain closed at its last event,
+ * whatever the events' linked flags (which are stored and compared unchanged): a shard's part of a
+ * chain across shards, probed with a failing last event or committed (executed by the ordered
+ * replay on one lane). */
+#define TBG_ONE_CHAIN 1u
+int tbg_create_transfers_stamped(tbg_ctx* ctx, const tb_transfer_t* events, uint32_t n,
+                                 const uint64_t* event_timestamps, uint64_t batch_timestamp,
+                                 uint32_t options, tb_create_result_t* results);
+int tbg_create_accounts_stamped(tbg_ctx* ctx, const tb_account_t* events, uint32_t n,
+                                const uint64_t* event_timestamps, uint64_t batch_timestamp,
+                                uint32_t options, tb_create_result_t* results);
+
+/* Sharded linked chains (shard.py): a shard probes its part of a chain that spans shards, and the
+ * chain's first failure across shards decides it (execute_create :3116-3172). An event the probe
+ * executed past that failure may have orphaned its id (transient_error :3215-3252) although the
+ * reference never executes it: tbg_forget_orphans returns such ids to unknown (a tombstone, as a
+ * failed claim leaves). Returns the count forgotten (ids not orphaned are left alone). */
+int64_t tbg_forget_orphans(tbg_ctx* ctx, const tb_uint128_t* ids, uint32_t n);
+
+/* Sharded imported events: whether a live object of a groove (transfers != 0: transfers, else
+ * accounts) holds each timestamp -- the `indirect_lookup` by timestamp that imported events'
+ * must_not_regress checks make into the *other* groove (:3661-3665, :3813-3817), asked of every
+ * shard by the router. out[i] = 0/1; returns the count found. */
+int64_t tbg_timestamps_exist(tbg_ctx* ctx, int transfers, const uint64_t* timestamps, uint32_t n,
+                             uint8_t* out);
+
 /* Pins and maps a host buffer the caller reuses across calls (a replica's message bodies and
  * reply buffers; hipHostRegister, mapped): a host-buffer call whose events or results lie in a
  * registered range has its kernels read the body (tr_ingest, small calls) and write the results
@@ -139,6 +170,8 @@ int64_t tbg_pulse_cut(tbg_ctx* ctx, uint64_t timestamp, uint64_t cut_expires_at,
 /* Sharded imported batches: raises the accounts / transfers objects trees' key_range.key_max
  * (read only by imported events' must_not_regress checks) to the maxima over every shard. */
 int tbg_raise_key_max(tbg_ctx* ctx, uint64_t accounts_key_max, uint64_t transfers_key_max);
+/* ... and reads this shard's (0: no key range yet), which the router raises every shard to. */
+int tbg_key_max(tbg_ctx* ctx, uint64_t* accounts_key_max, uint64_t* transfers_key_max);
 
 /* Sharded pulse_next_timestamp (one executor per ledger shard). A post/void of a pending transfer
  * with a timeout resets pulse_next_timestamp when it equals the transfer's expiry

@@ -812,8 +812,13 @@ static uint32_t create_transfer(tbo_ctx* c, uint64_t timestamp_event, const tb_t
 
 /* ---- execute_create (state_machine.zig:3002-3213) ------------------------------------------*/
 
+/* `stamps` (test instrumentation for sharded calls, NULL in the reference's form): event i is
+ * stamped stamps[i] instead of timestamp - n + i + 1 -- a shard's part of a linked chain that spans
+ * shards keeps its events' global timestamps. `one_chain`: the batch is one linked chain closed at
+ * its last event, whatever the events' linked flags (tbg.h TBG_ONE_CHAIN). */
 static void execute_create(tbo_ctx* c, int is_transfers, const void* events_, uint32_t n,
-                           uint64_t timestamp, tb_create_result_t* results) {
+                           uint64_t timestamp, const uint64_t* stamps, int one_chain,
+                           tb_create_result_t* results) {
     const tb_account_t* accounts = (const tb_account_t*)events_;
     const tb_transfer_t* transfers = (const tb_transfer_t*)events_;
     int64_t chain = -1;
@@ -826,17 +831,18 @@ static void execute_create(tbo_ctx* c, int is_transfers, const void* events_, ui
     for (uint32_t index = 0; index < n; index++) {
         uint16_t flags = is_transfers ? transfers[index].flags : accounts[index].flags;
         uint64_t ev_ts = is_transfers ? transfers[index].timestamp : accounts[index].timestamp;
-        const uint64_t timestamp_event = timestamp - n + index + 1;
+        const uint64_t timestamp_event = stamps ? stamps[index] : timestamp - n + index + 1;
         uint32_t status;
         uint64_t timestamp_actual = timestamp_event;
 
+        const int linked = one_chain || (flags & linked_flag);
         do {
-            if (flags & linked_flag) {
+            if (linked) {
                 if (chain < 0) {
                     chain = index;
                     scope_open(c);
                 }
-                if (index == n - 1) {
+                if (index == n - 1 && !one_chain) {
                     status = TB_CT_LINKED_EVENT_CHAIN_OPEN; /* same value for accounts */
                     break;
                 }
@@ -896,7 +902,8 @@ static void execute_create(tbo_ctx* c, int is_transfers, const void* events_, ui
         results[index].status = status;
         results[index].reserved = 0;
 
-        if (chain >= 0 && (!(flags & linked_flag) || status == TB_CT_LINKED_EVENT_CHAIN_OPEN)) {
+        if (chain >= 0 && (!linked || status == TB_CT_LINKED_EVENT_CHAIN_OPEN ||
+                           (one_chain && index == n - 1))) {
             if (!chain_broken) scope_close(c, 0);
             chain = -1;
             chain_broken = 0;
@@ -906,12 +913,80 @@ static void execute_create(tbo_ctx* c, int is_transfers, const void* events_, ui
 
 void tbo_create_accounts(tbo_ctx* c, const tb_account_t* events, uint32_t n, uint64_t timestamp,
                          tb_create_result_t* results) {
-    execute_create(c, 0, events, n, timestamp, results);
+    execute_create(c, 0, events, n, timestamp, NULL, 0, results);
 }
 
 void tbo_create_transfers(tbo_ctx* c, const tb_transfer_t* events, uint32_t n,
                           uint64_t timestamp, tb_create_result_t* results) {
-    execute_create(c, 1, events, n, timestamp, results);
+    if (c->pnt_sharded) c->n_pnt = 0; /* tbo_pnt_ops: this call's updates (tbg_pnt_ops' contract) */
+    execute_create(c, 1, events, n, timestamp, NULL, 0, results);
+}
+
+/* tbg_create_*'s multi-batch form: batch b holds lens[b] events, stamped as execute_create stamps
+ * them with timestamp batch_ts[b]; a sharded call's pulse_next_timestamp log covers the call. */
+void tbo_create_accounts_batches(tbo_ctx* c, const tb_account_t* events, const uint32_t* lens,
+                                 const uint64_t* batch_ts, uint32_t nb,
+                                 tb_create_result_t* results) {
+    uint64_t off = 0;
+    for (uint32_t b = 0; b < nb; b++) {
+        execute_create(c, 0, events + off, lens[b], batch_ts[b], NULL, 0, results + off);
+        off += lens[b];
+    }
+}
+
+void tbo_create_transfers_batches(tbo_ctx* c, const tb_transfer_t* events, const uint32_t* lens,
+                                  const uint64_t* batch_ts, uint32_t nb,
+                                  tb_create_result_t* results) {
+    if (c->pnt_sharded) c->n_pnt = 0;
+    uint64_t off = 0;
+    for (uint32_t b = 0; b < nb; b++) {
+        execute_create(c, 1, events + off, lens[b], batch_ts[b], NULL, 0, results + off);
+        off += lens[b];
+    }
+}
+
+/* Test instrumentation for sharded calls (tbg_create_*_stamped, tbg_forget_orphans,
+ * tbg_timestamps_exist in include/tbg.h): per-event timestamps; `timestamp` is the batch's. */
+void tbo_create_accounts_stamped(tbo_ctx* c, const tb_account_t* events, uint32_t n,
+                                 const uint64_t* stamps, uint64_t timestamp, uint32_t options,
+                                 tb_create_result_t* results) {
+    execute_create(c, 0, events, n, timestamp ? timestamp : (n ? stamps[n - 1] : 0), stamps,
+                   (options & 1) != 0, results);
+}
+
+void tbo_create_transfers_stamped(tbo_ctx* c, const tb_transfer_t* events, uint32_t n,
+                                  const uint64_t* stamps, uint64_t timestamp, uint32_t options,
+                                  tb_create_result_t* results) {
+    if (c->pnt_sharded) c->n_pnt = 0;
+    execute_create(c, 1, events, n, timestamp ? timestamp : (n ? stamps[n - 1] : 0), stamps,
+                   (options & 1) != 0, results);
+}
+
+void tbo_key_max(const tbo_ctx* c, uint64_t* accounts_key_max, uint64_t* transfers_key_max) {
+    *accounts_key_max = c->accounts_range.has ? c->accounts_range.key_max : 0;
+    *transfers_key_max = c->transfers_range.has ? c->transfers_range.key_max : 0;
+}
+
+uint64_t tbo_forget_orphans(tbo_ctx* c, const tb_uint128_t* ids, uint32_t n) {
+    uint64_t forgotten = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        uint64_t v;
+        if (map_get(&c->transfer_by_id, U(ids[i]), &v) && v == ORPHAN) {
+            map_del(&c->transfer_by_id, U(ids[i]));
+            forgotten++;
+        }
+    }
+    return forgotten;
+}
+
+uint64_t tbo_timestamps_exist(const tbo_ctx* c, int transfers, const uint64_t* ts, uint32_t n,
+                              uint8_t* out) {
+    uint64_t found = 0;
+    for (uint32_t i = 0; i < n; i++) {
+        out[i] = (uint8_t)map_get(transfers ? &c->transfer_by_ts : &c->account_by_ts, ts[i], NULL);
+        found += out[i];
+    }
+    return found;
 }
 
 /* ---- pulse ----------------------------------------------------------------------------------*/

@@ -35,6 +35,29 @@ void tbo_create_accounts(tbo_ctx* ctx, const tb_account_t* events, uint32_t n, u
 void tbo_create_transfers(tbo_ctx* ctx, const tb_transfer_t* events, uint32_t n,
                           uint64_t timestamp, tb_create_result_t* results);
 
+/* Sharded calls (test instrumentation; the shard executor contract of tigerbeetle_amd/shard.py,
+ * include/tbg.h): a multi-batch call (batch b: lens[b] events, timestamp batch_ts[b]) whose
+ * pulse_next_timestamp log (tbo_pnt_ops) covers the call; a one-batch call whose events carry
+ * their own timestamps `stamps` (`timestamp` = the batch's, 0 = the last stamp; options bit 0: one
+ * linked chain closed at the last event, whatever the linked flags); orphaned ids
+ * returned to unknown; whether live objects of a groove hold timestamps (out[i] = 0/1). */
+void tbo_create_accounts_batches(tbo_ctx* ctx, const tb_account_t* events, const uint32_t* lens,
+                                 const uint64_t* batch_ts, uint32_t nb,
+                                 tb_create_result_t* results);
+void tbo_create_transfers_batches(tbo_ctx* ctx, const tb_transfer_t* events, const uint32_t* lens,
+                                  const uint64_t* batch_ts, uint32_t nb,
+                                  tb_create_result_t* results);
+void tbo_create_accounts_stamped(tbo_ctx* ctx, const tb_account_t* events, uint32_t n,
+                                 const uint64_t* stamps, uint64_t timestamp, uint32_t options,
+                                 tb_create_result_t* results);
+void tbo_create_transfers_stamped(tbo_ctx* ctx, const tb_transfer_t* events, uint32_t n,
+                                  const uint64_t* stamps, uint64_t timestamp, uint32_t options,
+                                  tb_create_result_t* results);
+uint64_t tbo_forget_orphans(tbo_ctx* ctx, const tb_uint128_t* ids, uint32_t n);
+void tbo_key_max(const tbo_ctx* ctx, uint64_t* accounts_key_max, uint64_t* transfers_key_max);
+uint64_t tbo_timestamps_exist(const tbo_ctx* ctx, int transfers, const uint64_t* ts, uint32_t n,
+                              uint8_t* out);
+
 /* pulse: prefetch_expire_pending_transfers + execute_expire_pending_transfers
  * (state_machine.zig:2436-2562, :4511-4628, :4875-5029). Returns the number expired. */
 uint32_t tbo_pulse(tbo_ctx* ctx, uint64_t timestamp);

@@ -15,6 +15,15 @@ _SIGS = [
     ("tbo_close", None, [vp]),
     ("tbo_create_accounts", None, [vp, vp, ctypes.c_uint32, ctypes.c_uint64, vp]),
     ("tbo_create_transfers", None, [vp, vp, ctypes.c_uint32, ctypes.c_uint64, vp]),
+    ("tbo_create_accounts_batches", None, [vp, vp, vp, vp, ctypes.c_uint32, vp]),
+    ("tbo_create_transfers_batches", None, [vp, vp, vp, vp, ctypes.c_uint32, vp]),
+    ("tbo_create_accounts_stamped", None, [vp, vp, ctypes.c_uint32, vp, ctypes.c_uint64,
+                                           ctypes.c_uint32, vp]),
+    ("tbo_create_transfers_stamped", None, [vp, vp, ctypes.c_uint32, vp, ctypes.c_uint64,
+                                            ctypes.c_uint32, vp]),
+    ("tbo_forget_orphans", ctypes.c_uint64, [vp, vp, ctypes.c_uint32]),
+    ("tbo_key_max", None, [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
+    ("tbo_timestamps_exist", ctypes.c_uint64, [vp, ctypes.c_int, vp, ctypes.c_uint32, vp]),
     ("tbo_pulse", ctypes.c_uint32, [vp, ctypes.c_uint64]),
     ("tbo_pulse_candidates", ctypes.c_uint64, [vp, ctypes.c_uint64, vp, vp, ctypes.c_uint32]),
     ("tbo_pulse_cut", ctypes.c_uint32, [vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,

@@ -49,23 +49,65 @@ class OracleShard:
 
     def _run(self, fn, events, lens, batch_ts):
         out = np.zeros(len(events), dtype=RESULT_DTYPE)
-        off = 0
-        for ln, ts in zip(lens, batch_ts):
-            ln = int(ln)
-            fn(self.o, _ptr(events[off:off + ln]), ln, int(ts), _ptr(out[off:off + ln]))
-            off += ln
+        ln = np.ascontiguousarray(lens, dtype=np.uint32)
+        ts = np.ascontiguousarray(batch_ts, dtype=np.uint64)
+        fn(self.o, _ptr(events), _ptr(ln), _ptr(ts), len(ln), _ptr(out))
         return out
 
     def create_accounts(self, events, lens, batch_ts):
         ev = np.ascontiguousarray(events, dtype=ACCOUNT_DTYPE)
-        return self._run(self.lib.tbo_create_accounts, ev, lens, batch_ts)
+        return self._run(self.lib.tbo_create_accounts_batches, ev, lens, batch_ts)
 
     def create_transfers(self, events, lens, batch_ts):
         ev = np.ascontiguousarray(events, dtype=TRANSFER_DTYPE)
-        n = int(self.lib.tbo_pnt_ops(self.o, None, None, None))  # (the log starts with this call)
-        z = np.zeros(max(n, 1), dtype=np.uint64)
-        self.lib.tbo_pnt_ops(self.o, _ptr(z), _ptr(z.copy()), None)
-        return self._run(self.lib.tbo_create_transfers, ev, lens, batch_ts)
+        return self._run(self.lib.tbo_create_transfers_batches, ev, lens, batch_ts)
+
+    def _stamped(self, fn, events, stamps, batch_timestamp, options):
+        out = np.zeros(len(events), dtype=RESULT_DTYPE)
+        st = np.ascontiguousarray(stamps, dtype=np.uint64)
+        fn(self.o, _ptr(events), len(events), _ptr(st), int(batch_timestamp), int(options),
+           _ptr(out))
+        return out
+
+    def create_accounts_stamped(self, events, stamps, batch_timestamp=0, options=0):
+        ev = np.ascontiguousarray(events, dtype=ACCOUNT_DTYPE)
+        return self._stamped(self.lib.tbo_create_accounts_stamped, ev, stamps, batch_timestamp,
+                             options)
+
+    def create_transfers_stamped(self, events, stamps, batch_timestamp=0, options=0):
+        ev = np.ascontiguousarray(events, dtype=TRANSFER_DTYPE)
+        return self._stamped(self.lib.tbo_create_transfers_stamped, ev, stamps, batch_timestamp,
+                             options)
+
+    def forget_orphans(self, ids):
+        a = shard._u128_array(list(ids))
+        return int(self.lib.tbo_forget_orphans(self.o, _ptr(a), len(a)))
+
+    def timestamps_exist(self, transfers, ts):
+        ts = np.ascontiguousarray(ts, dtype=np.uint64)
+        out = np.zeros(len(ts), dtype=np.uint8)
+        self.lib.tbo_timestamps_exist(self.o, int(bool(transfers)), _ptr(ts), len(ts), _ptr(out))
+        return out.astype(bool)
+
+    def key_max(self):
+        a, t = ctypes.c_uint64(), ctypes.c_uint64()
+        self.lib.tbo_key_max(self.o, ctypes.byref(a), ctypes.byref(t))
+        return int(a.value), int(t.value)
+
+    def _lookup(self, fn, ids, dtype):
+        ids = list(ids)
+        if not ids:
+            return {}
+        a = shard._u128_array(ids)
+        out = np.zeros(len(ids), dtype=dtype)
+        n = int(fn(self.o, _ptr(a), len(ids), _ptr(out)))
+        return {int(r["id"][0]) | (int(r["id"][1]) << 64): r for r in out[:n]}
+
+    def lookup_accounts(self, ids):
+        return self._lookup(self.lib.tbo_lookup_accounts, ids, ACCOUNT_DTYPE)
+
+    def lookup_transfers(self, ids):
+        return self._lookup(self.lib.tbo_lookup_transfers, ids, TRANSFER_DTYPE)
 
     def pulse(self, timestamp):
         return int(self.lib.tbo_pulse(self.o, timestamp))
@@ -119,6 +161,155 @@ class OracleShard:
         e = np.zeros(self.lib.tbo_dump_account_events(self.o, None), dtype=ACCOUNT_EVENT_DTYPE)
         self.lib.tbo_dump_account_events(self.o, _ptr(e))
         return e[np.argsort(e["timestamp"], kind="stable")]
+
+
+def cross_scenario(seed, calls=10, n_acc=60):
+    """A call sequence full of what no shard can execute alone (module doc of shard.py): linked
+    chains across ledgers (shards) that succeed or fail at every position -- transiently
+    (exceeds_credits, accounts / pending transfers not found) or not (ledger mismatch, id 0,
+    exists, surrogates for transfers between shards) --, chains left open across shards at batch
+    ends, timed pending transfers and their posts / voids inside such chains, ids repeated on
+    another shard's accounts within a call (first occurrence created, failed transiently or not),
+    account chains across ledgers, imported batches whose timestamps regress across shards,
+    collide with the other groove's objects on other shards, advance past the batch, or mismatch
+    the batch's imported flag."""
+    rng = np.random.default_rng(seed)
+    acc = workload.accounts(n_acc, seed=seed)
+    ids = np.arange(1, n_acc + 1)
+    acc["ledger"] = 1 + (ids - 1) % LEDGERS
+    acc["flags"] = rng.choice([0, 0, 2, 4], size=n_acc).astype(np.uint16)
+    pools = {lg: ids[acc["ledger"] == lg] for lg in range(1, LEDGERS + 1)}
+    ops = [("accounts", acc, _split(rng, n_acc, 24))]
+    # an account chain across ledgers with a failure (and one without)
+    ach = workload.accounts(6, seed=seed + 1, id_offset=5_000)
+    ach["ledger"] = [1, 3, 4, 2, 3, 1]
+    ach["flags"] = [1, 1, 1, 0, 1, 0]
+    ach["code"][4] = 0  # code_must_not_be_zero: the first chain of two survives, the second fails
+    ops.append(("accounts", ach, [6]))
+    seen, pend, failed_ids = [], [], []
+    next_id = [100_000]
+
+    def fresh():
+        next_id[0] += 1
+        return next_id[0]
+
+    def plain(t, e, ledger, amount=None):
+        dr, cr = rng.choice(pools[ledger], size=2, replace=False)
+        t["debit_account_id"][e, 0] = dr
+        t["credit_account_id"][e, 0] = cr
+        t["amount"][e, 0] = int(rng.integers(1, 300)) if amount is None else amount
+        t["ledger"][e] = ledger
+        t["code"][e] = 1
+
+    for c in range(calls):
+        n = int(rng.integers(60, 140))
+        t = np.zeros(n, dtype=TRANSFER_DTYPE)
+        k = 0
+        while k < n:
+            span = min(n - k, int(rng.integers(2, 7)) if rng.random() < 0.45 else 1)
+            for j in range(span):
+                e = k + j
+                ledger = int(rng.integers(1, LEDGERS + 1))
+                r = rng.random()
+                t["id"][e, 0] = fresh()
+                if r < 0.06 and seen:  # an id of an earlier call: exists / id_already_failed
+                    t["id"][e, 0] = int(rng.choice(seen + failed_ids))
+                    plain(t, e, ledger)
+                elif r < 0.12 and e > 0:  # an id of this call, on any ledger
+                    t["id"][e, 0] = int(t["id"][int(rng.integers(0, e)), 0])
+                    plain(t, e, ledger)
+                elif r < 0.18 and pend:  # post / void (maybe of a transfer gone)
+                    t["pending_id"][e, 0] = int(rng.choice(pend)) if rng.random() < 0.9 \
+                        else 9_999_999
+                    t["flags"][e] = 4 if rng.random() < 0.6 else 8
+                    if t["flags"][e] == 4:
+                        t["amount"][e] = [2**64 - 1, 2**64 - 1]
+                elif r < 0.22:  # accounts of two ledgers (two shards, mostly)
+                    plain(t, e, ledger)
+                    t["credit_account_id"][e, 0] = int(rng.choice(pools[1 + ledger % LEDGERS]))
+                elif r < 0.25:
+                    plain(t, e, ledger)
+                    t["debit_account_id"][e, 0] = 77_777  # debit_account_not_found (transient)
+                elif r < 0.28:
+                    plain(t, e, ledger)
+                    t["ledger"][e] = 1 + ledger % LEDGERS  # not the accounts' ledger
+                elif r < 0.30:
+                    t["id"][e] = 0
+                    plain(t, e, ledger)
+                elif r < 0.36:
+                    plain(t, e, ledger, amount=10**7)  # exceeds_credits on a limited account
+                else:
+                    plain(t, e, ledger)
+                    if rng.random() < 0.3:
+                        t["flags"][e] = 2
+                        if rng.random() < 0.6:
+                            t["timeout"][e] = int(rng.integers(1, 4))
+                        pend.append(int(t["id"][e, 0]))
+                if j < span - 1:
+                    t["flags"][e] |= 1
+            k += span
+        if rng.random() < 0.5:
+            t["flags"][n - 1] |= 1  # a chain left open at the call's last batch end
+        seen.extend(int(x) for x in t["id"][:, 0] if x)
+        failed_ids.extend(int(x) for x in t["id"][rng.integers(0, n, size=3), 0] if x)
+        ops.append(("transfers", t, _split(rng, n, 40)))
+        if c % 3 == 1:
+            ops.append(("tick", int(rng.integers(1, 3)) * NS_PER_S))
+        if c % 3 == 2:
+            ops.extend(_imported_ops(rng, pools, fresh, seed + c))
+    return ops
+
+
+def _imported_ops(rng, pools, fresh, seed):
+    """Imported calls (drive's "imported2"): new accounts on every ledger (their timestamps
+    collide with the latest transfers), then transfers whose timestamps regress across shards,
+    collide with those accounts' timestamps, advance past the batch, or mismatch the batch's
+    imported flag."""
+    m = 8
+    a = workload.accounts(m, seed=seed, id_offset=int(fresh()) * 10)
+    a["ledger"] = 1 + np.arange(m) % LEDGERS
+    a["flags"] = 16
+    a["flags"][int(rng.integers(0, m))] |= 1  # a chain across ledgers (two events)
+
+    def fix_acc(ev, lo, ref):
+        ev["timestamp"] = lo + np.arange(len(ev), dtype=np.uint64)
+        if ref is not None and rng.random() < 0.7:  # a transfer's timestamp (a later one)
+            tr = ref.dump()[1]
+            if len(tr):
+                j = int(rng.integers(0, len(ev)))
+                ev["timestamp"][j] = int(tr["timestamp"][-1 - int(rng.integers(0, min(3, len(tr))))])
+        if rng.random() < 0.5:
+            ev["timestamp"] = ev["timestamp"][rng.permutation(len(ev))]
+
+    n = 24
+    t = np.zeros(n, dtype=TRANSFER_DTYPE)
+    for e in range(n):
+        ledger = 1 + e % LEDGERS
+        dr, cr = rng.choice(pools[ledger], size=2, replace=False)
+        t["id"][e, 0] = fresh()
+        t["debit_account_id"][e, 0] = dr
+        t["credit_account_id"][e, 0] = cr
+        t["amount"][e, 0] = int(rng.integers(1, 50))
+        t["ledger"][e] = ledger
+        t["code"][e] = 1
+        t["flags"][e] = 256 | (1 if rng.random() < 0.2 else 0)
+
+    def fix_tr(ev, lo, ref):
+        ts = lo + np.arange(len(ev), dtype=np.uint64)
+        swap = rng.integers(0, len(ev), size=(4, 2))
+        for x, y in swap:
+            ts[[x, y]] = ts[[y, x]]
+        ev["timestamp"] = ts
+        if ref is not None:
+            accs = ref.dump()[0]
+            j = int(rng.integers(0, len(ev)))
+            ev["timestamp"][j] = int(accs["timestamp"][-1 - int(rng.integers(0, 4))])
+        ev["timestamp"][int(rng.integers(0, len(ev)))] = (1 << 62)  # must_not_advance
+        x = int(rng.integers(1, len(ev)))
+        ev["flags"][x] &= ~np.uint16(256)  # imported_event_expected
+
+    return [("imported2", "accounts", a, [m], fix_acc),
+            ("imported2", "transfers", t, [12, 12], fix_tr)]
 
 
 def _split(rng, n, max_batch):
@@ -226,7 +417,15 @@ def drive(cluster, ref, ops, rank0=True, pbm=PBM, cuts=None):
         if op[0] == "tick":
             ts += op[1]
         else:
-            kind, ev, lens = op
+            if op[0] == "imported2":  # timestamps chosen by the op in a gap before the call
+                _, kind, ev, lens, fix = op
+                lo = ts + 1
+                ts += len(ev)
+                if rank0:
+                    ev = ev.copy()
+                    fix(ev, lo, ref)
+            else:
+                kind, ev, lens = op
             if kind == "imported":  # timestamps after every object so far, before the batch's
                 ev = ev.copy()
                 ev["timestamp"] = ts + 1 + np.arange(len(ev), dtype=np.uint64)
@@ -303,89 +502,80 @@ def _created(n, ts):
     return r
 
 
-def test_split_runs_keep_global_timestamps():
-    rng = np.random.default_rng(0)
-    lens = [7, 1, 12, 5, 30]
-    batch_ts = np.array([100, 150, 400, 1000, 5000], dtype=np.uint64)
-    n = sum(lens)
-    shard_of = rng.integers(0, 3, size=n).astype(np.int32)
-    slices = shard.split_runs(shard_of, lens, batch_ts, 3)
-    want = np.concatenate([int(ts) - ln + np.arange(1, ln + 1)
-                           for ln, ts in zip(lens, batch_ts)])
-    got = np.zeros(n, dtype=np.int64)
-    for s, sl in enumerate(slices):
-        assert (shard_of[sl.index] == s).all()
-        off = 0
-        for ln, ts in zip(sl.lens, sl.batch_ts):
-            got[sl.index[off:off + ln]] = ts - ln + np.arange(1, ln + 1)
-            off += ln
-        assert off == len(sl.index)
-    assert (got == want).all()
-    assert sorted(np.concatenate([sl.index for sl in slices]).tolist()) == list(range(n))
+def _plan(router, kind, events, lens, batch_ts, known=None, collisions=None):
+    """Segments the planner cuts a call into, as (start, end, chain, shard_of) -- planned against
+    fixed directories (no segment executes in between)."""
+    c = shard._Call(kind, np.ascontiguousarray(events, dtype=kind.dtype), lens, batch_ts)
+    kn = known or shard._Known()
+    p = shard.Planner(router, c, kn, collisions or {})
+    out, pos = [], 0
+    while pos < c.n:
+        seg = p.plan(pos)
+        out.append((seg.start, seg.end, seg.chain, [seg.shard_of[k] for k in range(seg.start,
+                                                                                     seg.end)]))
+        pos = seg.end
+    return out, c
 
 
-def test_router_routes_and_refuses():
+def test_planner_places_and_segments():
     r = shard.LedgerRouter(2, ledgers=4)  # ledgers 1, 2 -> shard 0; 3, 4 -> shard 1
-    acc = _accounts([1, 2, 3, 4], [1, 1, 3, 3])
-    plan = r.plan_accounts(acc, [4], [10])
-    r.commit(plan, acc, _created(4, 10))
-    assert r.dir.accounts == {1: 0, 2: 0, 3: 1, 4: 1}
+    kn = shard._Known(accounts={1: 0, 2: 0, 3: 1, 4: 1})
+    T = shard.TRANSFERS
     ok = _transfers([dict(id=10, debit_account_id=1, credit_account_id=2, amount=1, ledger=1, code=1),
                      dict(id=11, debit_account_id=3, credit_account_id=4, amount=1, ledger=3, code=1),
                      dict(id=12, debit_account_id=99, credit_account_id=4, amount=1, ledger=3,
                           code=1)])  # missing debit account: the credit account's shard
-    p = r.plan_transfers(ok, [3], [20])
-    assert p.shard_of.tolist() == [0, 1, 1]
-    assert [sl.lens for sl in p.slices] == [[1], [2]]
-    r.commit(p, ok, _created(3, 20))
+    segs, _ = _plan(r, T, ok, [3], [20], kn)
+    assert segs == [(0, 3, False, [0, 1, 1])]
     # an existing id goes to its holder, whatever accounts it names
+    kn.transfers[11] = (1, False)
     again = _transfers([dict(id=11, debit_account_id=1, credit_account_id=2, amount=1, ledger=1,
                              code=1)])
-    assert r.plan_transfers(again, [1], [30]).shard_of.tolist() == [1]
-    # accounts on two shards: a surrogate on the debit account's shard, the reference's status
+    assert _plan(r, T, again, [1], [30], kn)[0] == [(0, 1, False, [1])]
+    # accounts on two shards: a surrogate with the reference's status
     cross = _transfers([dict(id=13, debit_account_id=1, credit_account_id=3, amount=1, ledger=1,
                              code=1),
                         dict(id=14, debit_account_id=1, credit_account_id=3, amount=1, ledger=0,
                              code=1)])
-    p = r.plan_transfers(cross, [2], [40])
-    assert p.cross == {0: 23, 1: 19}  # accounts_must_have_the_same_ledger, ledger_must_not_be_zero
-    sur = p.shard_events(cross)
-    assert (sur["credit_account_id"] == sur["debit_account_id"]).all()
-    got = _created(2, 40)
-    got["status"] = 12  # the surrogates fail with accounts_must_be_different
-    assert p.patch(got)["status"].tolist() == [23, 19]
+    c = shard._Call(T, cross, [2], [40])
+    seg = shard.Planner(r, c, kn, {}).plan(0)
+    assert seg.cross == {0: 23, 1: 19}  # accounts_must_have_the_same_ledger, ledger_must_not_be_zero
+    # a linked chain across shards: a segment of its own, between the segments around it
     chain = _transfers([
-        dict(id=14, debit_account_id=1, credit_account_id=2, amount=1, ledger=1, code=1, flags=1),
-        dict(id=15, debit_account_id=3, credit_account_id=4, amount=1, ledger=3, code=1)])
-    with pytest.raises(shard.RouteError, match="linked chain"):
-        r.plan_transfers(chain, [2], [50])
-    # the same events with a batch end between them are two chains (the first one left open)
-    assert r.plan_transfers(chain, [1, 1], [49, 50]).shard_of.tolist() == [0, 1]
-    with pytest.raises(shard.RouteError, match="imported"):  # may collide with an account
-        r.plan_transfers(_transfers([dict(id=16, debit_account_id=1, credit_account_id=2,
-                                          amount=1, ledger=1, code=1, flags=256,
-                                          timestamp=5)]), [1], [60])
-    imp = _transfers([dict(id=16, debit_account_id=1, credit_account_id=2, amount=1, ledger=1,
+        dict(id=20, debit_account_id=1, credit_account_id=2, amount=1, ledger=1, code=1),
+        dict(id=21, debit_account_id=1, credit_account_id=2, amount=1, ledger=1, code=1, flags=1),
+        dict(id=22, debit_account_id=3, credit_account_id=4, amount=1, ledger=3, code=1),
+        dict(id=23, debit_account_id=3, credit_account_id=4, amount=1, ledger=3, code=1)])
+    assert _plan(r, T, chain, [4], [50], kn)[0] == [(0, 1, False, [0]), (1, 3, True, [0, 1]),
+                                                    (3, 4, False, [1])]
+    # the same events with a batch end between them: two chains (the first one left open)
+    assert _plan(r, T, chain, [2, 2], [49, 50], kn)[0] == [(0, 4, False, [0, 0, 1, 1])]
+    # an id repeated on another shard's accounts: the repeat waits for the first one's outcome
+    rep = _transfers([dict(id=30, debit_account_id=1, credit_account_id=2, amount=1, ledger=1, code=1),
+                      dict(id=30, debit_account_id=3, credit_account_id=4, amount=1, ledger=3,
+                           code=1)])
+    assert _plan(r, T, rep, [2], [60], kn)[0] == [(0, 1, False, [0]), (1, 2, False, [1])]
+    # ... but within one chain it runs where the first one did (the chain reaches it only if the
+    # first occurrence created the id: create_transfer_exists decides it there)
+    rep["flags"][0] = 1
+    assert _plan(r, T, rep, [2], [60], kn)[0] == [(0, 2, False, [0, 0])]
+    # imported events that may regress past another shard's: a new segment
+    imp = _transfers([dict(id=40, debit_account_id=1, credit_account_id=2, amount=1, ledger=1,
                            code=1, flags=256, timestamp=55),
-                      dict(id=17, debit_account_id=3, credit_account_id=4, amount=1, ledger=3,
+                      dict(id=41, debit_account_id=3, credit_account_id=4, amount=1, ledger=3,
                            code=1, flags=256, timestamp=56)])
-    assert r.plan_transfers(imp, [2], [60]).imported
-    imp["timestamp"] = [56, 55]  # the second may regress past the first, on another shard
-    with pytest.raises(shard.RouteError, match="regress"):
-        r.plan_transfers(imp, [2], [60])
-    timed = _transfers([dict(id=17, debit_account_id=1, credit_account_id=2, amount=5, ledger=1,
-                             code=1, flags=2, timeout=1)])
-    r.commit(r.plan_transfers(timed, [1], [70]), timed, _created(1, 70))
-    # a post/void of a pending transfer with a timeout goes to its shard (its reset of
-    # pulse_next_timestamp is resolved across shards after the call)
-    pv = r.plan_transfers(_transfers([dict(id=18, pending_id=17, flags=4, amount=(1 << 128) - 1)]),
-                          [1], [80])
-    assert pv.shard_of.tolist() == [0] and pv.post_void
-    untimed = _transfers([dict(id=19, debit_account_id=3, credit_account_id=4, amount=5,
-                               ledger=3, code=1, flags=2)])
-    r.commit(r.plan_transfers(untimed, [1], [90]), untimed, _created(1, 90))
-    post = _transfers([dict(id=20, pending_id=19, flags=4, amount=(1 << 128) - 1)])
-    assert r.plan_transfers(post, [1], [100]).shard_of.tolist() == [1]
+    assert len(_plan(r, T, imp, [2], [70], kn)[0]) == 1
+    imp["timestamp"] = [56, 55]
+    assert len(_plan(r, T, imp, [2], [70], kn)[0]) == 2
+    # an imported timestamp of an account on another shard: a timestamp surrogate
+    imp["timestamp"] = [55, 56]
+    c = shard._Call(T, imp, [2], [70])
+    seg = shard.Planner(r, c, kn, {56: {0}}).plan(0)
+    assert seg.tprime == {1: 1}
+    # a mismatched imported flag: the router's status (execute_create :3052-3064)
+    imp["flags"][1] = 0
+    c = shard._Call(T, imp, [2], [70])
+    assert c.pre == {1: int(shard._CT.imported_event_expected)}
 
 
 def test_pnt_resets_fire():
@@ -419,6 +609,24 @@ def _free_port():
         return s.getsockname()[1]
 
 
+@pytest.mark.parametrize("seed", list(range(6)))
+def test_local_shards_cross_shard_calls(seed):
+    """cross_scenario through three shards: every call the router once refused, executed
+    exactly -- results call by call, pulse_next_timestamp, pulses and the final tables and
+    AccountEvents against the unsharded oracle."""
+    shards = [OracleShard() for _ in range(3)]
+    ref = OracleShard()
+    try:
+        cluster = shard.LocalShards(shard.LedgerRouter(3, ledgers=LEDGERS), shards, PBM)
+        drive(cluster, ref, cross_scenario(seed))
+        assert cluster.engine.chain_segments > 0
+        assert_same_state([s.dump() for s in shards], ref,
+                          [s.dump_account_events() for s in shards])
+    finally:
+        for s in shards + [ref]:
+            s.close()
+
+
 @pytest.mark.parametrize("seed", [3, 4])
 def test_local_shards_pulse_cut(seed):
     """pulse_batch_max 6: pulses whose expired transfers span shards and exceed the batch take
@@ -439,7 +647,7 @@ def test_local_shards_pulse_cut(seed):
             s.close()
 
 
-def _gloo_rank(rank, world, port, seed, q, pbm=PBM):
+def _gloo_rank(rank, world, port, seed, q, pbm=PBM, cross=False):
     try:
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(port)
@@ -450,10 +658,13 @@ def _gloo_rank(rank, world, port, seed, q, pbm=PBM):
         group = shard.ShardGroup(ex, router, device="cpu", pulse_batch_max=pbm)
         ref = OracleShard(pbm) if rank == 0 else None
         cuts = []
-        pulses = drive(group, ref, scenario(seed, calls=10 if pbm < PBM else 8),
-                       rank0=rank == 0, pbm=pbm, cuts=cuts)
+        ops = cross_scenario(seed, calls=8) if cross else \
+            scenario(seed, calls=10 if pbm < PBM else 8)
+        pulses = drive(group, ref, ops, rank0=rank == 0, pbm=pbm, cuts=cuts)
         if rank == 0 and pbm < PBM:
             assert cuts, "the scenario should expire more than pulse_batch_max at once"
+        if rank == 0 and cross:
+            assert group.engine.chain_segments > 0
         dumps = [None] * world
         dist.all_gather_object(dumps, ex.dump())
         events = [None] * world
@@ -461,19 +672,16 @@ def _gloo_rank(rank, world, port, seed, q, pbm=PBM):
         if rank == 0:
             assert all(len(d[1]) for d in dumps), "every shard holds transfers"
             assert_same_state(dumps, ref, events)
-        # A refused call fails on every rank and leaves the group usable.
-        chain = _transfers([
-            dict(id=10**9, debit_account_id=1, credit_account_id=5, amount=1, ledger=1, code=1,
-                 flags=1),
-            dict(id=10**9 + 1, debit_account_id=3, credit_account_id=7, amount=1, ledger=3,
-                 code=1)])
+        # A call that fails on rank 0 (an invalid batch layout) fails on every rank and leaves
+        # the group usable.
         try:
             if rank == 0:
-                group.create_transfers(chain, [2], np.array([10**15], dtype=np.uint64))
+                group.create_transfers(np.zeros(2, dtype=TRANSFER_DTYPE), [3],
+                                       np.array([10**15], dtype=np.uint64))
             else:
                 group.create_transfers()
-            raise AssertionError("the cross-shard chain was not refused")
-        except shard.RouteError:
+            raise AssertionError("the invalid call did not fail")
+        except (ValueError, RuntimeError):
             pass
         assert group.pulse_next_timestamp() > 0
         dist.barrier()
@@ -483,12 +691,14 @@ def _gloo_rank(rank, world, port, seed, q, pbm=PBM):
         q.put((rank, traceback.format_exc(), 0))
 
 
-@pytest.mark.parametrize("pbm", [PBM, 6], ids=["pbm8190", "pbm6-cuts"])
-def test_shard_group_gloo_world2(pbm):
+@pytest.mark.parametrize("pbm,cross", [(PBM, False), (6, False), (PBM, True)],
+                         ids=["pbm8190", "pbm6-cuts", "cross-shard"])
+def test_shard_group_gloo_world2(pbm, cross):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_gloo_rank, args=(r, 2, port, 5, q, pbm)) for r in range(2)]
+    procs = [ctx.Process(target=_gloo_rank, args=(r, 2, port, 5, q, pbm, cross))
+             for r in range(2)]
     for p in procs:
         p.start()
     out = {}
@@ -503,7 +713,7 @@ def test_shard_group_gloo_world2(pbm):
                 p.kill()
     for rank, (err, _) in sorted(out.items()):
         assert err is None, f"rank {rank}:\n{err}"
-    assert out[0][1] > 0
+    assert out[0][1] > 0 or cross
 
 
 @pytest.mark.gpu
@@ -536,6 +746,27 @@ def test_local_shards_gpu_pulse_cut():
         cuts = []
         assert drive(cluster, ref, scenario(12, calls=10), pbm=pbm, cuts=cuts) > 0
         assert cuts
+        assert_same_state([s.dump() for s in shards], ref,
+                          [s.dump_account_events() for s in shards])
+    finally:
+        for s in shards:
+            s.close()
+        ref.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_local_shards_gpu_cross_shard(seed):
+    """cross_scenario through three HBM executors on cuda:0 (stamped calls, TBG_ONE_CHAIN probes
+    and commits, tbg_forget_orphans, tbg_timestamps_exist, tbg_key_max), against the unsharded
+    oracle."""
+    shards = [shard.GpuShard(1 << 12, 1 << 16, batch_events_max=4096,
+                             account_events_capacity=1 << 16) for _ in range(3)]
+    ref = OracleShard()
+    try:
+        cluster = shard.LocalShards(shard.LedgerRouter(3, ledgers=LEDGERS), shards, PBM)
+        drive(cluster, ref, cross_scenario(seed))
+        assert cluster.engine.chain_segments > 0
         assert_same_state([s.dump() for s in shards], ref,
                           [s.dump_account_events() for s in shards])
     finally:

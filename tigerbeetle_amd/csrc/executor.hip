@@ -159,6 +159,7 @@ struct tbg_ctx {
     bool failed = false;
     bool force_replay = false;
     bool serial_replay = false;  // debug: every replay on one lane (replay_kernel)
+    bool call_one_chain = false;  // the next call is one chain (TBG_ONE_CHAIN): serial replay
     tbg_stats stats{};
 
     // per-call scratch (capacity batch_events_max)
@@ -183,6 +184,8 @@ struct tbg_ctx {
     Call<tb_transfer_t> pnt_last{};         // the last create_transfers call (tbg_pnt_ops)
     bool pnt_last_valid = false;
     unsigned long long* pnt_fired = nullptr;
+    uint64_t* pnt_tiles = nullptr;          // pnt_resolve's per-tile minima (its own scratch)
+    uint64_t* d_stamps = nullptr;           // per-event timestamps of a host stamped call
     unsigned long long* pv_slots = nullptr;  // pending-id claims of post/void events (kernels.hpp)
     uint64_t pv_mask = 0;
     // balance items (2 per event, packed u64) and their sorted copy
@@ -480,7 +483,8 @@ Call<Event> make_call(tbg_ctx* ctx, const Event* d_events, uint32_t n, const uin
     c.results = d_results;
     c.row_base = row_base;
     c.epoch = ++ctx->epoch;
-    c.force_replay = ctx->force_replay ? 1 : 0;
+    c.one_chain = ctx->call_one_chain ? 1 : 0;
+    c.force_replay = ctx->force_replay || ctx->call_one_chain ? 1 : 0;
     c.bal_items = nullptr;
     c.key_bits = 0;
     c.pair_shift = 0;
@@ -886,7 +890,9 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
 int pnt_resolve(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
     const uint32_t n = c.n;
     const uint32_t tiles = std::max<uint32_t>(1, (n + kPntTile - 1) / kPntTile);
-    uint64_t* tile_min = ctx->bal_items;  // (free after the balance application)
+    // (not bal_items: a sharded call without post/void resolves too, and its AccountEvents balance
+    // window reads the pair items there afterwards)
+    uint64_t* tile_min = ctx->pnt_tiles;
     hipLaunchKernelGGL(pnt_tile_min, dim3(tiles), dim3(kPntThreads), 0, ctx->stream, c.pnt_call, n,
                        tile_min);
     hipLaunchKernelGGL(pnt_tile_resolve, dim3(tiles), dim3(kPntThreads), 0, ctx->stream, ctx->T,
@@ -905,7 +911,7 @@ int run_replay(tbg_ctx* ctx, Call<Event>& c, bool is_transfers, bool finalize_ev
     const unsigned int call_flags = ctx->h_scalars->flags;
     const uint64_t m = ctx->h_scalars->stats[0];
     if constexpr (__is_same(Event, tb_transfer_t)) {
-        if (!ctx->serial_replay && !(call_flags & kFlagImported) && m > 1 &&
+        if (!ctx->serial_replay && !c.one_chain && !(call_flags & kFlagImported) && m > 1 &&
             m < (1ull << kFlowUnitBits)) {
             rc = run_flow_replay(ctx, c, uint32_t(m), call_flags);
             if (rc) return rc;
@@ -1922,6 +1928,8 @@ tbg_ctx* tbg_open(const tbg_options* options) {
          dev_alloc(ctx, &ctx->fix_slots, ev_max, false) &&
          dev_alloc(ctx, &ctx->chain_planes, (uint64_t(ev_max) + 63) / 64 * kPlWords, false) &&
          dev_alloc(ctx, &ctx->pnt_call, ev_max, false) && dev_alloc(ctx, &ctx->pnt_fired, 4, true) &&
+         dev_alloc(ctx, &ctx->pnt_tiles, (uint64_t(ev_max) + kPntTile - 1) / kPntTile + 1, false) &&
+         dev_alloc(ctx, &ctx->d_stamps, ev_max + 1, false) &&
          dev_alloc(ctx, &ctx->pv_slots, next_pow2(2 * uint64_t(ev_max)), true);
     ctx->pv_mask = next_pow2(2 * uint64_t(ev_max)) - 1;
     // (2 * ev_max items, at least ev_max u64 of lookup scratch)
@@ -2051,7 +2059,7 @@ void tbg_close(tbg_ctx* ctx) {
                     ctx->d_results, ctx->d_batch_ends, ctx->d_batch_ts, ctx->ev_slot, ctx->ev_dr,
                     ctx->ev_cr, ctx->ev_amount, ctx->ev_prow, ctx->ev_info, ctx->ev_slow, ctx->slow_list,
                     ctx->fix_slots, ctx->chain_planes, ctx->d_stage_done,
-                    ctx->pnt_call, ctx->pnt_fired, ctx->pv_slots,
+                    ctx->pnt_call, ctx->pnt_fired, ctx->pnt_tiles, ctx->d_stamps, ctx->pv_slots,
                     ctx->bal_items, ctx->chunk_info, ctx->bal_items_sorted, ctx->bucket_words, ctx->bucket_partials,
                     ctx->window_partials, ctx->window_carry, ctx->window_counts, ctx->window_ts,
                     ctx->acc_ts_index, ctx->tr_ts_index, ctx->sel_buf,
@@ -2375,9 +2383,14 @@ int tbg_create_transfers_stamped_device(tbg_ctx* ctx, const tb_transfer_t* d_eve
                                  d_results, stream, d_event_timestamps);
 }
 
-int tbg_create_accounts_device(tbg_ctx* ctx, const tb_account_t* d_events, uint32_t n,
-                               const uint32_t* d_batch_ends, const uint64_t* d_batch_ts,
-                               uint32_t n_batches, tb_create_result_t* d_results, void* stream) {
+}  // extern "C"
+
+namespace {
+
+int create_accounts_impl(tbg_ctx* ctx, const tb_account_t* d_events, uint32_t n,
+                         const uint32_t* d_batch_ends, const uint64_t* d_batch_ts,
+                         uint32_t n_batches, tb_create_result_t* d_results, void* stream,
+                         const uint64_t* d_event_ts) {
     if (!ctx || n > ctx->opt.batch_events_max || n_batches > ctx->opt.batch_count_max)
         return TBG_EINVAL;
     FAILED_GUARD(ctx);
@@ -2391,6 +2404,7 @@ int tbg_create_accounts_device(tbg_ctx* ctx, const tb_account_t* d_events, uint3
     int rc = begin_call(ctx);
     Call<tb_account_t> c = make_call(ctx, d_events, n, d_batch_ends, d_batch_ts, n_batches,
                                      d_results, ctx->T.acc_rows_used);
+    c.event_ts = d_event_ts;
     const dim3 grid(grid_for(n)), block(kBlock);
     if (!rc) {
         hipLaunchKernelGGL(acc_prepare, grid, block, 0, ctx->stream, ctx->T, c);
@@ -2420,6 +2434,78 @@ int tbg_create_accounts_device(tbg_ctx* ctx, const tb_account_t* d_events, uint3
     ctx->stream = saved;
     ctx->T.acc_rows_used += n;
     ctx->acc_ts_stale = true;
+    return rc;
+}
+
+// Validates a stamped call's per-event timestamps (nonzero, increasing); its batch timestamp
+// (0: the last event's) in *bts.
+int stamps_ok(const uint64_t* ts, uint32_t n, uint64_t batch_timestamp, uint64_t* bts) {
+    if (!ts) return TBG_EINVAL;
+    for (uint32_t i = 0; i < n; i++)
+        if (ts[i] == 0 || (i && ts[i] <= ts[i - 1])) return TBG_EINVAL;
+    *bts = batch_timestamp ? batch_timestamp : ts[n - 1];
+    return 0;
+}
+
+// A host stamped call's inputs: the body and one batch (its end, its timestamp) through the
+// host-buffer staging, the per-event timestamps to d_stamps.
+int upload_stamped(tbg_ctx* ctx, const void* events, uint32_t n, const uint64_t* ts, uint64_t bts) {
+    int rc = body_buffer(ctx, false);
+    if (rc) return rc;
+    const uint32_t len = n;
+    rc = upload_batches(ctx, n, &len, &bts, 1, events, 128, false);
+    if (rc) return rc;
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->d_stamps, ts, size_t(n) * 8, hipMemcpyHostToDevice,
+                                ctx->stream));
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int tbg_create_accounts_device(tbg_ctx* ctx, const tb_account_t* d_events, uint32_t n,
+                               const uint32_t* d_batch_ends, const uint64_t* d_batch_ts,
+                               uint32_t n_batches, tb_create_result_t* d_results, void* stream) {
+    return create_accounts_impl(ctx, d_events, n, d_batch_ends, d_batch_ts, n_batches, d_results,
+                                stream, nullptr);
+}
+
+int tbg_create_transfers_stamped(tbg_ctx* ctx, const tb_transfer_t* events, uint32_t n,
+                                 const uint64_t* event_timestamps, uint64_t batch_timestamp,
+                                 uint32_t options, tb_create_result_t* results) {
+    if (!ctx || n > ctx->opt.batch_events_max || (options & ~TBG_ONE_CHAIN)) return TBG_EINVAL;
+    if (n == 0) return 0;
+    FAILED_GUARD(ctx);
+    uint64_t bts = 0;
+    int rc = stamps_ok(event_timestamps, n, batch_timestamp, &bts);
+    if (!rc) rc = upload_stamped(ctx, events, n, event_timestamps, bts);
+    ctx->call_one_chain = (options & TBG_ONE_CHAIN) != 0;
+    if (!rc)
+        rc = create_transfers_impl(ctx, reinterpret_cast<const tb_transfer_t*>(ctx->body_dst), n,
+                                   ctx->d_batch_ends, ctx->d_batch_ts, 1, ctx->d_results, nullptr,
+                                   ctx->d_stamps);
+    ctx->call_one_chain = false;
+    if (!rc) rc = download_results(ctx, results, n);
+    return rc;
+}
+
+int tbg_create_accounts_stamped(tbg_ctx* ctx, const tb_account_t* events, uint32_t n,
+                                const uint64_t* event_timestamps, uint64_t batch_timestamp,
+                                uint32_t options, tb_create_result_t* results) {
+    if (!ctx || n > ctx->opt.batch_events_max || (options & ~TBG_ONE_CHAIN)) return TBG_EINVAL;
+    if (n == 0) return 0;
+    FAILED_GUARD(ctx);
+    uint64_t bts = 0;
+    int rc = stamps_ok(event_timestamps, n, batch_timestamp, &bts);
+    if (!rc) rc = upload_stamped(ctx, events, n, event_timestamps, bts);
+    ctx->call_one_chain = (options & TBG_ONE_CHAIN) != 0;
+    if (!rc)
+        rc = create_accounts_impl(ctx, reinterpret_cast<const tb_account_t*>(ctx->body_dst), n,
+                                  ctx->d_batch_ends, ctx->d_batch_ts, 1, ctx->d_results, nullptr,
+                                  ctx->d_stamps);
+    ctx->call_one_chain = false;
+    if (!rc) rc = download_results(ctx, results, n);
     return rc;
 }
 
@@ -2812,6 +2898,65 @@ int tbg_raise_key_max(tbg_ctx* ctx, uint64_t accounts_key_max, uint64_t transfer
     HIP_TRY(ctx, hipMemcpyAsync(&ctx->d_scalars->transfers_key_max, &t, 8, hipMemcpyHostToDevice,
                                 ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return 0;
+}
+
+int64_t tbg_forget_orphans(tbg_ctx* ctx, const tb_uint128_t* ids, uint32_t n) {
+    if (!ctx || n > ctx->opt.batch_events_max || (n && !ids)) return TBG_EINVAL;
+    FAILED_GUARD(ctx);
+    if (n == 0) return 0;
+    ctx->prefetch_events = nullptr;  // (d_events is the scratch)
+    ctx->prefetch_bytes = 0;
+    if (ctx->ae_snap_body == ctx->d_events)
+        if (int rc = ae_flush_all(ctx)) return rc;
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->d_events, ids, size_t(n) * 16, hipMemcpyHostToDevice,
+                                ctx->stream));
+    unsigned int* d_count = &ctx->d_scalars->slow_count;  // scratch word (between calls)
+    HIP_TRY(ctx, hipMemsetAsync(d_count, 0, 4, ctx->stream));
+    hipLaunchKernelGGL(forget_orphans_kernel, dim3(grid_for(n)), dim3(kBlock), 0, ctx->stream,
+                       ctx->T, reinterpret_cast<const tb_uint128_t*>(ctx->d_events), n, d_count);
+    HIP_TRY(ctx, hipGetLastError());
+    HIP_TRY(ctx, hipMemcpyAsync(&ctx->h_scalars->slow_count, d_count, 4, hipMemcpyDeviceToHost,
+                                ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return ctx->h_scalars->slow_count;
+}
+
+int64_t tbg_timestamps_exist(tbg_ctx* ctx, int transfers, const uint64_t* timestamps, uint32_t n,
+                             uint8_t* out) {
+    if (!ctx || n > ctx->opt.batch_events_max || (n && (!timestamps || !out))) return TBG_EINVAL;
+    FAILED_GUARD(ctx);
+    if (n == 0) return 0;
+    // (check_imported_indexes rebuilds the index an imported call of the *other* groove reads)
+    int rc = check_imported_indexes(ctx, transfers == 0);
+    if (rc) return rc;
+    ctx->prefetch_events = nullptr;
+    ctx->prefetch_bytes = 0;
+    if (ctx->ae_snap_body == ctx->d_events)
+        if ((rc = ae_flush_all(ctx))) return rc;
+    uint64_t* d_ts = reinterpret_cast<uint64_t*>(ctx->d_events);
+    uint8_t* d_out = reinterpret_cast<uint8_t*>(d_ts + n);
+    HIP_TRY(ctx, hipMemcpyAsync(d_ts, timestamps, size_t(n) * 8, hipMemcpyHostToDevice,
+                                ctx->stream));
+    const uint64_t* index = transfers ? ctx->tr_ts_index : ctx->acc_ts_index;
+    const uint64_t count = transfers ? ctx->T.tr_ts_count : ctx->T.acc_ts_count;
+    hipLaunchKernelGGL(timestamps_exist_kernel, dim3(grid_for(n)), dim3(kBlock), 0, ctx->stream,
+                       index, count, d_ts, n, d_out);
+    HIP_TRY(ctx, hipGetLastError());
+    HIP_TRY(ctx, hipMemcpyAsync(out, d_out, n, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    int64_t found = 0;
+    for (uint32_t i = 0; i < n; i++) found += out[i];
+    return found;
+}
+
+int tbg_key_max(tbg_ctx* ctx, uint64_t* accounts_key_max, uint64_t* transfers_key_max) {
+    if (!ctx) return TBG_EINVAL;
+    FAILED_GUARD(ctx);
+    int rc = sync_scalars(ctx);
+    if (rc) return rc;
+    if (accounts_key_max) *accounts_key_max = ctx->h_scalars->accounts_key_max;
+    if (transfers_key_max) *transfers_key_max = ctx->h_scalars->transfers_key_max;
     return 0;
 }
 

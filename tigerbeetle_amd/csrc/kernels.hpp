@@ -2033,16 +2033,19 @@ __device__ inline void replay_chain_step_at(Replay& R, const Call<Event>& c, uin
     uint32_t status = 0;
     uint64_t ts_actual = ts_event;
     R.pos = k;
+    // (one_chain: every event links to the next, and the batch's last event closes the chain)
+    const bool linked = c.one_chain || (f & linked_flag);
+    const bool last = (si.flags & StepInfo::kLastOfBatch) != 0;
 
     do {  // execute_create's loop body (:3030-3105)
-        if (f & linked_flag) {
+        if (linked) {
             if (!chain_open) {
                 chain_open = true;
                 chain_start = k;
                 chain_broken = false;
                 R.scope_open();
             }
-            if (si.flags & StepInfo::kLastOfBatch) {
+            if (last && !c.one_chain) {
                 status = TB_CT_LINKED_EVENT_CHAIN_OPEN;
                 break;
             }
@@ -2103,7 +2106,8 @@ __device__ inline void replay_chain_step_at(Replay& R, const Call<Event>& c, uin
     res.status = status;
     res.reserved = 0;
     c.results[k] = res;
-    if (chain_open && (!(f & linked_flag) || status == TB_CT_LINKED_EVENT_CHAIN_OPEN)) {
+    if (chain_open && (!linked || status == TB_CT_LINKED_EVENT_CHAIN_OPEN ||
+                       (c.one_chain && last))) {
         if (!chain_broken) R.scope_close(false);
         chain_open = false;
         chain_broken = false;
@@ -2515,6 +2519,29 @@ __global__ void lookup_transfers_kernel(Tables T, const tb_uint128_t* ids, uint3
     }
     found[i] = r != kNone;
     rows[i] = r;
+}
+
+// Orphaned ids back to unknown (a tombstone): a sharded call's probe of a linked chain across
+// shards executed an event the reference never reaches (tigerbeetle_amd/shard.py).
+__global__ void forget_orphans_kernel(Tables T, const tb_uint128_t* ids, uint32_t n,
+                                      unsigned int* forgotten) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const tb_transfer_t* trs = T.tr_rows;
+    const uint64_t s = probe_find(T.tr, ids[i], [&](uint64_t r) { return trs[r].id; });
+    if (s == kNone) return;
+    const uint64_t w = T.tr.slots[s];
+    if (w == kTomb || !(w & kOrphanBit)) return;
+    T.tr.slots[s] = kTomb;
+    atomicAdd(forgotten, 1u);
+}
+
+// Whether a live object of a groove has each timestamp (its sorted timestamp index).
+__global__ void timestamps_exist_kernel(const uint64_t* index, uint64_t count, const uint64_t* ts,
+                                        uint32_t n, uint8_t* out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    out[i] = ts_index_contains(index, count, ts[i]) ? 1 : 0;
 }
 
 template <typename Row>

@@ -123,6 +123,9 @@ struct Call {
     uint64_t row_base;
     uint32_t epoch;
     uint32_t force_replay;
+    // The whole call is one linked chain closed at its last event, whatever the events' linked
+    // flags (tbg_create_*_stamped with TBG_ONE_CHAIN: a shard's part of a chain across shards).
+    uint32_t one_chain;
     // per-event scratch (structure of arrays; kNone32 = absent)
     uint32_t* ev_slot;     // slot of the event's id in the id table
     uint32_t* ev_dr;       // account rows (create_transfers)

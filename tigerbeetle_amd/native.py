@@ -91,6 +91,12 @@ SIGNATURES = [
     ("tbg_create_transfers_device", ctypes.c_int, [vp, vp, ctypes.c_uint32, vp, vp,
                                                   ctypes.c_uint32, vp, vp]),
     ("tbg_create_transfers_stamped_device", ctypes.c_int, [vp, vp, ctypes.c_uint32, vp, vp, vp]),
+    ("tbg_create_transfers_stamped", ctypes.c_int, [vp, vp, ctypes.c_uint32, vp, ctypes.c_uint64,
+                                                   ctypes.c_uint32, vp]),
+    ("tbg_create_accounts_stamped", ctypes.c_int, [vp, vp, ctypes.c_uint32, vp, ctypes.c_uint64,
+                                                  ctypes.c_uint32, vp]),
+    ("tbg_forget_orphans", ctypes.c_int64, [vp, vp, ctypes.c_uint32]),
+    ("tbg_timestamps_exist", ctypes.c_int64, [vp, ctypes.c_int, vp, ctypes.c_uint32, vp]),
     ("tbg_register_host", ctypes.c_int, [vp, vp, ctypes.c_uint64]),
     ("tbg_unregister_host", ctypes.c_int, [vp, vp]),
     ("tbg_prefetch_body", ctypes.c_int, [vp, vp, ctypes.c_uint64]),
@@ -101,6 +107,7 @@ SIGNATURES = [
                                        ctypes.c_uint64, vp]),
     ("tbg_pulse_next_timestamp", ctypes.c_uint64, [vp]),
     ("tbg_raise_key_max", ctypes.c_int, [vp, ctypes.c_uint64, ctypes.c_uint64]),
+    ("tbg_key_max", ctypes.c_int, [vp, c_u64p, c_u64p]),
     ("tbg_set_pnt_sharded", ctypes.c_int, [vp, ctypes.c_int]),
     ("tbg_pnt_ops", ctypes.c_int64, [vp, vp, vp, ctypes.c_uint64, c_u64p]),
     ("tbg_set_pulse_next_timestamp", ctypes.c_int, [vp, ctypes.c_uint64]),

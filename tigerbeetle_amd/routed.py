@@ -13,9 +13,9 @@ The device router places single events, resubmitted ids (on their holder), post/
 their pending transfer's shard) and linked chains that stay on one shard (include/tbr.h). A call
 it cannot place -- any event that could observe another shard's state (imported events, ids that
 repeat within the call, accounts unknown or on two shards, chains across shards) -- is executed
-by the exact host router instead (shard.LedgerRouter over the same directories,
-through shard.ShardGroup): surrogates for cross-shard transfers, key-range sync for imported
-batches, refusal of the cases no shard can execute alone.
+by the exact host engine instead (shard.Engine over the same directories, through
+shard.ShardGroup): surrogates for cross-shard transfers, segments, the chain protocol for linked
+chains across shards, key-range sync for imported batches -- every call executes exactly.
 
 A routed call that posts or voids (the router's mode 2) resolves pulse_next_timestamp across the
 shards after it (shard.ShardGroup.resolve_pnt: every shard's recorded updates gathered at rank 0,
@@ -168,14 +168,10 @@ class RoutedShards:
                 if r is not None:
                     r.wait()
             self.torch.cuda.synchronize(self.dev)
-            key_max = ctypes.c_uint64(0)
             rc = self.lib.tbr_settle_device(self.tbr, self.res.data_ptr(), self.pos.data_ptr(), n,
-                                            d_results, ctypes.byref(key_max))
+                                            d_results, None)
             if rc != 0:
                 raise RuntimeError(f"tbr_settle_device: {rc}")
-            # The transfers objects tree's key_max over every shard, as the host router's commit
-            # keeps it: a later imported call's must_not_regress checks read it (:3808-3817).
-            self.router.transfers_key_max = max(self.router.transfers_key_max, key_max.value)
         else:
             if mine:
                 self._recv(self.ev[:mine * 128], 0)
