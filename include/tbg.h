@@ -131,16 +131,6 @@ int64_t tbg_timestamps_exist(tbg_ctx* ctx, int transfers, const uint64_t* timest
 int tbg_register_host(tbg_ctx* ctx, void* ptr, uint64_t size);
 int tbg_unregister_host(tbg_ctx* ctx, void* ptr);
 
-/* The StateMachine's prefetch of a create body (state_machine.zig:1146-1226 prefetch; here the
- * tables are resident, so the body itself is what is fetched): when `events` lies in a registered
- * range, queues its copy into HBM on the ctx's stream (32 workgroups of coalesced 16-byte reads:
- * the PCIe read's best shape) and returns 1; the next create call on the same events and bytes
- * then reads HBM instead of the host body. 0: nothing queued (the call moves the body itself).
- * Stream-ordered: the caller may complete its prefetch callback at once. Off (returns 0) unless
- * TBG_PREFETCH_BODY=1: back to back with the commit it measured slower than tr_ingest reading the
- * registered body itself. */
-int tbg_prefetch_body(tbg_ctx* ctx, const void* events, uint64_t bytes);
-
 /* Waits for every kernel and copy the ctx has queued on its own stream (e.g. the AccountEvents
  * appends a *_device call leaves behind it) -- for callers that reuse the call's device buffers
  * from other streams. */

@@ -9,14 +9,16 @@
  * open-addressing tables probed like the executor's id tables.
  *
  * The device fast path (tbr_route_device) takes calls in which no event can observe another
- * shard's state: non-imported events whose id is new to every shard and unique in the call and
- * whose two accounts are known and on one shard; events whose id already exists (decided by the
+ * shard's state: events whose id is new to every shard and unique in the call and whose two
+ * accounts are known and on one shard; events whose id already exists (decided by the
  * id's holder, create_transfer_exists :3988-4051, before any account lookup); post/voids, on the
  * shard of their pending transfer (in the directory or created earlier in the call); and linked
- * chains whose events all go to one shard and end within their batch. Any
- * other event is a *hazard*: the call is left to the exact router (tigerbeetle_amd/shard.py,
- * LedgerRouter), which reads the same directories through tbr_account_shards /
- * tbr_transfer_shards and records its outcome with tbr_record_*.
+ * chains whose events all go to one shard and end within their batch; imported events when every
+ * event of the call is imported, their timestamps increase through the call, lie below their own
+ * commit timestamps and above the imported floor (tbr_set_imported_floor). Any other event is a
+ * *hazard*: the call is left to the exact engine (tigerbeetle_amd/shard.py, Engine), which reads
+ * the same directories through tbr_account_shards / tbr_transfer_shards and records its outcome
+ * with tbr_record_*.
  *
  * Reference: the shard boundary follows `accounts_must_have_the_same_ledger` /
  * `transfer_must_have_the_same_ledger_as_accounts` (src/state_machine.zig:3795-3798); transfer
@@ -44,6 +46,15 @@ int tbr_record_accounts(tbr_ctx* ctx, const tb_uint128_t* ids, const uint8_t* sh
 int tbr_record_transfers(tbr_ctx* ctx, const tb_uint128_t* ids, const uint8_t* shards, uint32_t n);
 int64_t tbr_account_shards(tbr_ctx* ctx, const tb_uint128_t* ids, uint32_t n, int32_t* out);
 int64_t tbr_transfer_shards(tbr_ctx* ctx, const tb_uint128_t* ids, uint32_t n, int32_t* out);
+
+/* Imported events on the fast path (execute_create :3066-3078, create_transfer :3800-3830): their
+ * must_not_regress checks read the objects trees' key ranges and the accounts' timestamps over all
+ * shards. The caller keeps `floor` at or above the largest timestamp of any account or transfer on
+ * any shard (tbg_key_max over the shards; raised by the created_timestamp_max of each settled
+ * call); an imported timestamp above it, in a call whose imported timestamps increase, collides
+ * with nothing and regresses past nothing on any shard. UINT64_MAX (the initial value): every
+ * imported event is a hazard. */
+int tbr_set_imported_floor(tbr_ctx* ctx, uint64_t floor);
 
 /* The fast path (device pointers, synchronous). Returns 0 when the call was routed: slices in
  * shard order at d_out_events / d_out_timestamps (event i of shard s at offset

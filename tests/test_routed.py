@@ -110,6 +110,25 @@ def _calls(seed):
     ops.append(("fast", tpv, [4_000]))
     ops.append(("tick", 2_000_000_000))
     ops.append(("fast", uniform(20_000), [8189, 20_000 - 8189]))
+    # a linked chain across the two shards, failing transiently on its second shard: the host
+    # engine's chain protocol (probe, the first failure across shards, the orphan kept)
+    xc = uniform(1_000)
+    for j, lg in zip(range(300, 304), (1, 3, 3, 2)):
+        xc["flags"][j] |= 1 if j < 303 else 0
+        xc["ledger"][j] = lg
+        xc["debit_account_id"][j, 0] = (lg - 1) * PER_LEDGER + 1 + j % 7
+        xc["credit_account_id"][j, 0] = (lg - 1) * PER_LEDGER + 20 + j % 5
+    xc["debit_account_id"][302, 0] = 999_999  # debit_account_not_found
+    ops.append(("host", xc, [1_000]))
+    # imported calls (timestamps in a gap before the call, increasing): on the device path above
+    # the floor; then with a regress across shards on the host engine
+    imp = uniform(3_000)
+    imp["flags"] |= 256
+    ops.append(("fast-imported", imp, [1_500, 1_500]))
+    imp2 = uniform(500)
+    imp2["flags"] |= 256
+    ops.append(("host-imported", imp2, [500]))
+    ops.append(("fast", uniform(5_000), [5_000]))
     return ops
 
 
@@ -144,6 +163,13 @@ def _rank(rank, world, port, seed, q):
             else:
                 kind, ev, lens = op
                 n = len(ev)
+                if kind.endswith("-imported"):  # timestamps in a gap before the call
+                    ev = ev.copy()
+                    ev["timestamp"] = ts + 1 + np.arange(n, dtype=np.uint64)
+                    if kind.startswith("host"):
+                        ev["timestamp"][[10, 11]] = ev["timestamp"][[11, 10]]  # a regress
+                    ts += n
+                    kind = kind.split("-")[0]
                 ts += 1 + n
                 batch_ts = (ts - n + np.cumsum(lens)).astype(np.uint64)
                 if kind == "accounts":
@@ -194,7 +220,7 @@ def _rank(rank, world, port, seed, q):
             want = ref.dump_account_events()
             assert len(got) > 50_000 and got.tobytes() == want.tobytes(), \
                 f"account events differ ({len(got)} vs {len(want)})"
-            assert rs.fast_calls == 4 and rs.host_calls == 1, (rs.fast_calls, rs.host_calls)
+            assert rs.fast_calls == 6 and rs.host_calls == 3, (rs.fast_calls, rs.host_calls)
             assert pulses > 0
         rs.close()
         dist.barrier()

@@ -236,23 +236,8 @@ struct tbg_ctx {
     // A pulse's appends, queued later (ae_flush_graph): by the next call once its first kernels
     // are queued (the host's launches then overlap the GPU), or by whatever joins the side stream
     // or takes a staging buffer first.
-    // The body buffer of the current host-buffer call (d_events, or d_events_alt for a small
-    // create_transfers call while a deferred snapshot still reads d_events).
+    // The body buffer of the current host-buffer call (d_events).
     uint8_t* body_dst = nullptr;
-    uint8_t* d_events_alt = nullptr;  // kAeAsyncMax events
-    // A small call's AccountEvents snapshot on the side stream (ae_snap_defer): queued by the next
-    // call just before its tr_ingest (the call's stream waits for it there: everything before --
-    // the body's upload -- runs beside it), its appends after the next call's kernels.
-    bool ae_snap_def = false, ae_snap_def_appends = false;
-    AeSnapJob ae_snap_def_job{};
-    uint32_t ae_snap_def_p = 0, ae_snap_def_epoch = 0;
-    const uint8_t* ae_snap_body = nullptr;  // the body buffer the deferred snapshot reads
-    hipEvent_t ae_snap_done = nullptr;
-    bool ae_side_snap = false;
-    bool ae_no_query = false;  // (TBG_AE_NO_QUERY: always wait on the append events)
-    bool ae_snap_side = false;  // (this call's snapshot goes to the side stream)
-    const void* prefetch_events = nullptr;  // tbg_prefetch_body's body, in d_events
-    uint64_t prefetch_bytes = 0;
     bool ae_graph_deferred = false;
     uint32_t ae_def_parity = 0, ae_def_epoch = 0;
     bool ae_def_pending = false;
@@ -265,14 +250,13 @@ struct tbg_ctx {
     // staging buffer per parity, the side stream's own positions and grouping scratch. Every other
     // use of the log joins the side stream first (ae_join).
     hipStream_t ae_stream = nullptr;
-    hipStream_t snap_stream = nullptr;  // the deferred snapshots (not behind the appends)
     AeStage ae_stage[2] = {};
     uint32_t* ae_pos = nullptr;
     hipEvent_t ae_snap_ready[2] = {}, ae_done[2] = {};
     bool ae_done_recorded[2] = {};
     uint32_t ae_parity = 0;
     bool ae_async_pending = false;
-    bool ae_async = true;  // tbg_debug_ae_sync(ctx, 1) / TBG_AE_SYNC=1: every append on the call's stream
+    bool ae_async = true;  // tbg_debug_ae_sync(ctx, 1): every append on the call's stream
     bool ae_window_on = true;  // TBG_NO_AE_WINDOW=1: window calls take the general appends
     bool ae_async_ready = false;
     AeScratch ae_g{};
@@ -687,7 +671,6 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
     G.indeg = F.indeg;
     G.lanes = lanes_possible;
     G.free_owners = getenv("TBG_NO_FREE_OWNERS") == nullptr;
-    G.sort_values = getenv("TBG_SEG_VALUES") != nullptr;
     G.epoch = c.epoch;
     G.owner_starts = F.owner_starts;
     G.lane_counts = F.lane_counts;
@@ -1047,7 +1030,7 @@ int ae_flush_all(tbg_ctx* ctx);
 int ae_join(tbg_ctx* ctx) {
     if (int rc = ae_flush_all(ctx)) return rc;
     if (!ctx->ae_async_pending) return 0;
-    if (ctx->ae_no_query || hipEventQuery(ctx->ae_done[ctx->ae_parity ^ 1]) != hipSuccess)
+    if (hipEventQuery(ctx->ae_done[ctx->ae_parity ^ 1]) != hipSuccess)
         HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ae_done[ctx->ae_parity ^ 1], 0));
     ctx->ae_async_pending = false;
     return 0;
@@ -1215,14 +1198,11 @@ int ensure_ae_async(tbg_ctx* ctx) {
     if ((cap * 2 + kScanTile - 1) / kScanTile + (kAeAsyncMax + kScanTile - 1) / kScanTile + 8 > 64)
         return TBG_EINVAL;
     HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->ae_stream, hipStreamNonBlocking));
-    HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->snap_stream, hipStreamNonBlocking));
     for (int p = 0; p < 2; p++) {
         HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ae_snap_ready[p], hipEventDisableTiming));
         HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ae_done[p], hipEventDisableTiming));
     }
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // (the scratch's zeroing)
-    HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->ae_snap_done, hipEventDisableTiming));
-    if (!dev_alloc(ctx, &ctx->d_events_alt, uint64_t(kAeAsyncMax) * 128, false)) return TBG_ENOMEM;
     ctx->ae_async_ready = true;
     return 0;
 }
@@ -1247,7 +1227,7 @@ int ae_stage_acquire(tbg_ctx* ctx) {
     const uint32_t p = ctx->ae_parity;
     // (a wait on an event that has already completed still puts a barrier packet on the call's
     // stream: skipped when the appends two calls back are done)
-    if (ctx->ae_done_recorded[p] && (ctx->ae_no_query || hipEventQuery(ctx->ae_done[p]) != hipSuccess))
+    if (ctx->ae_done_recorded[p] && (hipEventQuery(ctx->ae_done[p]) != hipSuccess))
         HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ae_done[p], 0));
     return 0;
 }
@@ -1308,61 +1288,8 @@ int ae_flush_graph(tbg_ctx* ctx) {
     return 0;
 }
 
-// A small call's snapshot on the side stream (ae_snap_defer), in two halves: the snapshot and the
-// call stream's wait for it (before anything writes the rows, results or body it reads), then its
-// appends.
-int ae_snap_flush1(tbg_ctx* ctx) {
-    if (!ctx->ae_snap_def) return 0;
-    ctx->ae_snap_def = false;
-    const uint32_t p = ctx->ae_snap_def_p;
-    // (a stream of its own: on the side stream it queued behind the previous call's appends; it
-    // waits only for the call's end and for the appends that last read its staging buffer)
-    HIP_TRY(ctx, hipStreamWaitEvent(ctx->snap_stream, ctx->ae_snap_ready[p], 0));
-    if (ctx->ae_done_recorded[p])
-        HIP_TRY(ctx, hipStreamWaitEvent(ctx->snap_stream, ctx->ae_done[p], 0));
-    hipLaunchKernelGGL(ae_snapshot, dim3(kAeAsyncMax / kSnapThreads), dim3(kSnapThreads), 0, ctx->snap_stream,
-                       ctx->ae_snap_def_job);
-    HIP_TRY(ctx, hipGetLastError());
-    HIP_TRY(ctx, hipEventRecord(ctx->ae_snap_done, ctx->snap_stream));
-    HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->ae_snap_done, 0));
-    ctx->ae_snap_body = nullptr;
-    ctx->ae_snap_def_appends = true;
-    return 0;
-}
-int ae_snap_flush2(tbg_ctx* ctx) {
-    if (!ctx->ae_snap_def_appends) return 0;
-    ctx->ae_snap_def_appends = false;
-    const uint32_t p = ctx->ae_snap_def_p;
-    HIP_TRY(ctx, hipStreamWaitEvent(ctx->ae_stream, ctx->ae_snap_done, 0));
-    if (int rc = ae_launch_appends(ctx, p, ctx->ae_snap_def_epoch, false)) return rc;
-    HIP_TRY(ctx, hipEventRecord(ctx->ae_done[p], ctx->ae_stream));
-    ctx->ae_done_recorded[p] = true;
-    ctx->ae_async_pending = true;
-    return 0;
-}
-// Every deferred side-stream job, in the order they were deferred (at most one of each kind is
-// pending, and each defer flushes the other kind first).
-int ae_flush_all(tbg_ctx* ctx) {
-    if (int rc = ae_snap_flush1(ctx)) return rc;
-    if (int rc = ae_snap_flush2(ctx)) return rc;
-    return ae_flush_graph(ctx);
-}
-// After a small call with no replay: the snapshot, final now, deferred to the side stream.
-int ae_snap_defer(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
-    if (int rc = ae_flush_all(ctx)) return rc;
-    if (int rc = ensure_ae_async(ctx)) return rc;
-    const uint32_t p = ctx->ae_parity;
-    HIP_TRY(ctx, hipEventRecord(ctx->ae_snap_ready[p], ctx->stream));
-    ctx->ae_snap_def_job = AeSnapJob{ctx->T, c, ctx->ae_stage[p], false};
-    ctx->ae_snap_def = true;
-    ctx->ae_snap_def_p = p;
-    ctx->ae_snap_def_epoch = c.epoch;
-    ctx->ae_snap_body = reinterpret_cast<const uint8_t*>(c.events);
-    ctx->ae_bound += c.n;
-    ctx->ae_pending = true;
-    ctx->ae_parity = p ^ 1;
-    return 0;
-}
+// Every deferred side-stream job (a pulse's appends).
+int ae_flush_all(tbg_ctx* ctx) { return ae_flush_graph(ctx); }
 
 // AccountEvents of a small create_transfers call behind the next call. When no replay ran, the
 // call's stage_out took the snapshot and the graph is already queued behind it; else the snapshot
@@ -1696,41 +1623,22 @@ void host_pin_release(void* ptr) {
 // A host-buffer call's inputs into HBM: the batch ends / timestamps from the pinned staging and,
 // when the body lies in a registered range, the body itself -- one kernel on the call's stream
 // (hostio.hpp); an unregistered body takes hipMemcpyAsync.
-int ae_snap_flush1(tbg_ctx* ctx);
 int ae_flush_all(tbg_ctx* ctx);
 
 // Chooses the host-buffer call's body buffer (ctx->body_dst).
-int body_buffer(tbg_ctx* ctx, bool small) {
+int body_buffer(tbg_ctx* ctx) {
     ctx->body_dst = ctx->d_events;
-    if (ctx->ae_snap_body != ctx->d_events) return 0;
-    if (small && ctx->d_events_alt) {
-        ctx->body_dst = ctx->d_events_alt;
-        return 0;
-    }
-    return ae_flush_all(ctx);
+    return 0;
 }
 
 int stage_call_inputs(tbg_ctx* ctx, const void* events, uint64_t bytes, uint32_t nb,
                       bool reset_scalars, bool ingest_reads_host = false) {
     const uint4* src = mapped(ctx, static_cast<const uint4*>(events), bytes);
     ctx->events_host = nullptr;
-    // (a body tbg_prefetch_body already moved into HBM)
-    const bool prefetched = ctx->prefetch_events == events && ctx->prefetch_bytes == bytes && bytes &&
-                            ctx->body_dst == ctx->d_events;
-    ctx->prefetch_events = nullptr;
-    ctx->prefetch_bytes = 0;
-    if (prefetched) {
-        src = nullptr;
-        bytes = 0;
-    }
-    // TBG_INGEST_READS_HOST=0: stage_in copies the body first -- 32 workgroups of coalesced 16-B
-    // reads, the PCIe read rate's best shape (45 GB/s, tools/pciebench.hip) -- and tr_ingest reads
-    // HBM. A commit without AccountEvents took 55-56 us that way against 58-60 with tr_ingest
-    // reading its events across PCIe itself (27 GB/s: one event's 128 B per lane); with
-    // AccountEvents (the drop-in's case) 70-77 against 70-72, so the direct reads stay the default.
-    static const bool ingest_host_ok = !getenv("TBG_INGEST_READS_HOST") ||
-                                       atoi(getenv("TBG_INGEST_READS_HOST")) != 0;
-    if (src && ingest_reads_host && ingest_host_ok) {  // (tr_ingest reads the body and leaves the copy)
+    // A small create_transfers call's registered body is read by tr_ingest itself across PCIe
+    // (it leaves the HBM copy for the later kernels): with AccountEvents this measured 70-72 us a
+    // commit against 70-77 with stage_in copying the body first.
+    if (src && ingest_reads_host) {
         ctx->events_host = reinterpret_cast<const tb_transfer_t*>(src);
         src = nullptr;
         bytes = 0;
@@ -1747,21 +1655,6 @@ int stage_call_inputs(tbg_ctx* ctx, const void* events, uint64_t bytes, uint32_t
     return 0;
 }
 
-// The prefetch's body copy alone (StageIn with no batch ends or scalar reset).
-int prefetch_body(tbg_ctx* ctx, const void* events, uint64_t bytes) {
-    const uint4* src = mapped(ctx, static_cast<const uint4*>(events), bytes);
-    if (!src || bytes % 16 || bytes > uint64_t(ctx->opt.batch_events_max) * 128) return 0;
-    if (ctx->ae_snap_body == ctx->d_events) return 0;  // (a deferred snapshot reads it)
-    StageIn s{src, reinterpret_cast<uint4*>(ctx->d_events), bytes / 16, nullptr, nullptr, nullptr,
-              nullptr, 0, nullptr};
-    const uint64_t per_block = uint64_t(kStageThreads) * kStageWords;
-    const uint32_t grid = uint32_t(std::min<uint64_t>(kStageInGridMax, std::max<uint64_t>(1, (s.words + per_block - 1) / per_block)));
-    hipLaunchKernelGGL(stage_in, dim3(grid), dim3(kStageThreads), 0, ctx->stream, s);
-    HIP_TRY(ctx, hipGetLastError());
-    ctx->prefetch_events = events;
-    ctx->prefetch_bytes = bytes;
-    return 1;
-}
 
 // Results (n > 0) and / or the scalars block to mapped host memory, as one kernel on the stream.
 // Waits for stage_out's sequence word (every kernel before it has finished: the scalars and
@@ -1832,10 +1725,6 @@ int64_t lookup_impl(tbg_ctx* ctx, const tb_uint128_t* ids, uint32_t n, void* out
     if (n == 0) return 0;
     if (n > ctx->opt.batch_events_max) return TBG_EINVAL;
     // Scratch: ids and output rows in d_events; rows in bal_items; found flags in ev_slow.
-    ctx->prefetch_events = nullptr;  // (a prefetched body there is overwritten)
-    ctx->prefetch_bytes = 0;
-    if (ctx->ae_snap_body == ctx->d_events)
-        if (int rc = ae_flush_all(ctx)) return rc;
     HIP_TRY(ctx, hipMemcpyAsync(ctx->d_events, ids, size_t(n) * 16, hipMemcpyHostToDevice,
                                 ctx->stream));
     const tb_uint128_t* d_ids = reinterpret_cast<const tb_uint128_t*>(ctx->d_events);
@@ -1996,13 +1885,10 @@ tbg_ctx* tbg_open(const tbg_options* options) {
     T.expiry_capacity = tr_cap;
     T.undo_capacity = undo_cap;
     T.scalars = ctx->d_scalars;
-    ctx->ae_async = getenv("TBG_AE_SYNC") == nullptr;
     ctx->ae_window_on = getenv("TBG_NO_AE_WINDOW") == nullptr;
     // (TBG_AE_SIDE_SNAP=1: a small call's snapshot on a stream of its own, the next call's ingest
     // waiting for it: 83-96 us a commit against 69-74 on the call's stream -- the two cross-stream
     // event waits on the critical path cost more than the 11 us snapshot they hide)
-    ctx->ae_side_snap = getenv("TBG_AE_SIDE_SNAP") && atoi(getenv("TBG_AE_SIDE_SNAP")) != 0;
-    ctx->ae_no_query = getenv("TBG_AE_NO_QUERY") != nullptr;
     ctx->body_dst = nullptr;
     T.acc_ts_index = ctx->acc_ts_index;
     T.tr_ts_index = ctx->tr_ts_index;
@@ -2032,7 +1918,6 @@ tbg_ctx* tbg_open(const tbg_options* options) {
 void tbg_close(tbg_ctx* ctx) {
     if (!ctx) return;
     if (ctx->ae_stream) (void)hipStreamSynchronize(ctx->ae_stream);
-    if (ctx->snap_stream) (void)hipStreamSynchronize(ctx->snap_stream);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     for (int p = 0; p < 2; p++) {
         if (ctx->ae_snap_ready[p]) (void)hipEventDestroy(ctx->ae_snap_ready[p]);
@@ -2047,12 +1932,10 @@ void tbg_close(tbg_ctx* ctx) {
     for (void* q : {(void*)ctx->ae_small_counts, (void*)ctx->ae_small_ts, (void*)ctx->ae_dense_touch,
                     (void*)ctx->ae_dense_ev, (void*)ctx->ae_dense_partials,
                     (void*)ctx->ae_dense_counts, (void*)ctx->ae_dense_ts, (void*)ctx->ae_dense_fail,
-                    (void*)ctx->ae_dense_later, (void*)ctx->ae_dense_pos, (void*)ctx->d_events_alt})
+                    (void*)ctx->ae_dense_later, (void*)ctx->ae_dense_pos})
         if (q) (void)hipFree(q);
     free_ae_scratch(ctx->ae_g);
-    if (ctx->ae_snap_done) (void)hipEventDestroy(ctx->ae_snap_done);
     if (ctx->ae_stream) (void)hipStreamDestroy(ctx->ae_stream);
-    if (ctx->snap_stream) (void)hipStreamDestroy(ctx->snap_stream);
     void* ptrs[] = {ctx->idx_dirty, ctx->idx_counters, ctx->T.acc_index.entries, ctx->T.acc_entry_of, ctx->T.acc.slots, ctx->T.acc_rows, ctx->T.acc_live, ctx->T.acc_hot,
                     ctx->T.acc_closable, ctx->T.tr.slots, ctx->T.tr_rows, ctx->T.tr_live,
                     ctx->T.tr_status, ctx->T.expiry, ctx->d_scalars, ctx->T.undo, ctx->d_events,
@@ -2118,7 +2001,6 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
     // tr_ingest: 12,288 workgroups (48 per CU) beat the grid-stride default of 4,096 by 3 % on
     // config 2 (0.707 vs 0.728 ms per 10M events); 32,768 and more lose 40 %.
     uint32_t ig = std::min(grid_for(n), kIngestGrid);
-    { const char* e = getenv("TBG_INGEST_GRID"); if (e) ig = std::min(grid_for(n), uint32_t(atoi(e))); }
     const bool use_sort = n >= kSortThreshold && ctx->bal_items_sorted;
     // Balance items pack (amount << key_bits) | field key into a u64; the all-ones key is the
     // "no item" sentinel, so key_bits covers 4 * accounts + 1 values.
@@ -2140,8 +2022,8 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
                             uint64_t(key_end) > kAtomicKeysPerItem * 2 * uint64_t(n);
     // Sparse key spaces: tr_ingest applies each FAST event's deltas with u128 atomics itself (as
     // in small calls; a demotion subtracts them) -- no items written, read back and applied by a
-    // second kernel. TBG_NO_INGEST_ATOMICS: items and bal_atomic_apply.
-    const bool ingest_atomics = use_atomic && !getenv("TBG_NO_INGEST_ATOMICS");
+    // second kernel.
+    const bool ingest_atomics = use_atomic;
     if (use_buckets && key_bits < 16) key_bits = 16;
     BucketPlan plan{};
     c.lean_lookup = ingest_atomics && !getenv("TBG_NO_LEAN_LOOKUP");
@@ -2174,7 +2056,6 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
             ci.events = ctx->events_host;
             ci.events_out = const_cast<tb_transfer_t*>(c.events);
         }
-        if (int frc = ae_snap_flush1(ctx)) return frc;  // (the previous call's snapshot)
         hipLaunchKernelGGL(tr_ingest, dim3(ig), block, 0, ctx->stream, ctx->T, ci);
         tmark(ctx, "tr_ingest");
         hipLaunchKernelGGL(tr_commit, grid, block, 0, ctx->stream, ctx->T, c);
@@ -2185,15 +2066,13 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
         c.chunk_info = ctx->chunk_info;
         hipLaunchKernelGGL(tr_chunk_info, dim3(grid_for((n + 63) / 64)), block, 0, ctx->stream, c,
                            ctx->chunk_info, ctx->d_scalars);
-        if (int frc = ae_snap_flush1(ctx)) return frc;
         hipLaunchKernelGGL(tr_ingest, dim3(ig), block, 0, ctx->stream, ctx->T, c);
         tmark(ctx, "tr_ingest");
         // (large calls: chains resolved from bit planes -- a launch that returns at once when the
-        // call has no chain to confirm; TBG_NO_CHAIN_PLANES: tr_commit walks them itself)
-        // (only while the calls have chains: the planes' launch alone costs ~5 us a call, and
-        // tr_commit is exact either way -- without planes it walks the chains)
-        static const bool planes = getenv("TBG_NO_CHAIN_PLANES") == nullptr;
-        if (planes && ctx->chain_hint) {
+        // call has no chain to confirm -- only while the calls have chains: the planes' launch
+        // alone costs ~5 us a call, and tr_commit is exact either way: without planes it walks
+        // the chains)
+        if (ctx->chain_hint) {
             c.chain_planes = ctx->chain_planes;
             hipLaunchKernelGGL(tr_chain_planes, grid, block, 0, ctx->stream, ctx->T, c);
         }
@@ -2238,11 +2117,6 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
                            target, plan, ctx->bucket_partials, key_end);
         tmark(ctx, "bal_apply");
         rc = hip_ok(ctx, hipGetLastError(), "launch") ? 0 : TBG_EHIP;
-    } else if (!rc && use_atomic && !ingest_atomics) {
-        hipLaunchKernelGGL(bal_atomic_apply, dim3(grid_for(uint64_t(items) / 2)), block, 0,
-                           ctx->stream, target, ctx->bal_items, uint64_t(items), key_bits, key_end);
-        tmark(ctx, "bal_atomic");
-        rc = hip_ok(ctx, hipGetLastError(), "launch") ? 0 : TBG_EHIP;
     } else if (!rc && use_sort && !ingest_atomics) {
         // Balance deltas: items summed per account field in per-workgroup LDS hash tables.
         const uint64_t blocks = (uint64_t(items) + kHashSliceItems - 1) / kHashSliceItems;
@@ -2269,7 +2143,7 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
         // A small call's AccountEvents snapshot follows stage_out (the host's wait ends at
         // stage_out): final unless a replay follows, then it stages nothing. Its appends are queued
         // on the side stream now, so that the host's launch calls overlap the call's kernels.
-        if (!rc && snap && !ctx->ae_side_snap) {
+        if (!rc && snap) {
             AeSnapJob J;
             rc = ae_snap_job(ctx, c, &J);
             if (!rc) {
@@ -2280,8 +2154,7 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
             }
             if (!rc) rc = ae_launch_graph(ctx, n, c.epoch);
         }
-        ctx->ae_snap_early = snap && !rc && !ctx->ae_side_snap;
-        ctx->ae_snap_side = snap && !rc && ctx->ae_side_snap;
+        ctx->ae_snap_early = snap && !rc;
         if (!rc) rc = spin ? spin_wait(ctx, seq)
                            : (hip_ok(ctx, hipStreamSynchronize(ctx->stream), "sync") ? 0 : TBG_EHIP);
         tmark(ctx, "host_sync");
@@ -2292,11 +2165,6 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
         ctx->replay_hint = replay;
     }
     if (replay) ctx->ae_snap_early = false;
-    if (!rc && ctx->ae_snap_side && !replay) {  // (no replay: the snapshot is final)
-        rc = ae_snap_defer(ctx, c);
-        ctx->ae_snap_early = !rc;
-    }
-    ctx->ae_snap_side = false;
     ctx->early_done = !rc && ctx->early_dst && !replay;  // (only the replay rewrites results)
     if (replay && (ctx->h_scalars->flags & kFlagImported)) rc = check_imported_indexes(ctx, true);
     if (replay && !rc) rc = run_replay(ctx, c, true, false);
@@ -2450,7 +2318,7 @@ int stamps_ok(const uint64_t* ts, uint32_t n, uint64_t batch_timestamp, uint64_t
 // A host stamped call's inputs: the body and one batch (its end, its timestamp) through the
 // host-buffer staging, the per-event timestamps to d_stamps.
 int upload_stamped(tbg_ctx* ctx, const void* events, uint32_t n, const uint64_t* ts, uint64_t bts) {
-    int rc = body_buffer(ctx, false);
+    int rc = body_buffer(ctx);
     if (rc) return rc;
     const uint32_t len = n;
     rc = upload_batches(ctx, n, &len, &bts, 1, events, 128, false);
@@ -2517,7 +2385,7 @@ int tbg_create_transfers(tbg_ctx* ctx, const tb_transfer_t* events, uint32_t n,
     const double t0 = ctx->timing_host ? now_ms() : 0;
     // The body's buffer: d_events, unless a deferred snapshot still reads it (then a small call
     // takes the second buffer, a larger one queues that snapshot first).
-    int rc = body_buffer(ctx, n <= kAeAsyncMax);
+    int rc = body_buffer(ctx);
     if (rc) return rc;
     // (stage_in resets the call's scalar words: no tr_chunk_info launch for a small call)
     rc = upload_batches(ctx, n, batch_lens, batch_ts, nb, events, 128, n <= kInlineChunkMax,
@@ -2557,7 +2425,7 @@ int tbg_create_accounts(tbg_ctx* ctx, const tb_account_t* events, uint32_t n,
                         tb_create_result_t* results) {
     if (!ctx || n > ctx->opt.batch_events_max) return TBG_EINVAL;
     if (n == 0) return 0;
-    int rc = body_buffer(ctx, false);
+    int rc = body_buffer(ctx);
     if (rc) return rc;
     rc = upload_batches(ctx, n, batch_lens, batch_ts, nb, events, 128, false);
     if (rc) return rc;
@@ -2702,15 +2570,6 @@ int pulse_keys(tbg_ctx* ctx, uint64_t n, std::vector<uint64_t>* exp, std::vector
 
 extern "C" {
 
-int tbg_prefetch_body(tbg_ctx* ctx, const void* events, uint64_t bytes) {
-    if (!ctx || !events) return TBG_EINVAL;
-    FAILED_GUARD(ctx);
-    // (off unless TBG_PREFETCH_BODY=1: with the prefetch and the commit back to back, the staged
-    // copy plus an HBM ingest took 73-81 us a commit with AccountEvents against 68-73 with tr_ingest
-    // reading the registered body itself -- tools/commit_timeline.py, same box)
-    static const bool on = getenv("TBG_PREFETCH_BODY") && atoi(getenv("TBG_PREFETCH_BODY")) != 0;
-    return on ? prefetch_body(ctx, events, bytes) : 0;
-}
 
 int tbg_register_host(tbg_ctx* ctx, void* ptr, uint64_t size) {
     if (!ctx || !ptr || size == 0) return TBG_EINVAL;
@@ -2758,7 +2617,7 @@ int64_t tbg_pulse(tbg_ctx* ctx, uint64_t timestamp) {
     const uint64_t count0 = ctx->expiry_known ? std::min<uint64_t>(ctx->expiry_host, ctx->T.expiry_capacity)
                                               : ctx->T.expiry_capacity;
     const uint32_t upper0 = uint32_t(std::min<uint64_t>(count0, k));
-    bool ae_async = ctx->ae_log && upper0 && ae_async_ok(ctx, upper0) && !getenv("TBG_PULSE_AE_SYNC");
+    bool ae_async = ctx->ae_log && upper0 && ae_async_ok(ctx, upper0) ;
     uint32_t ae_epoch = 0;
     int rc = 0;
     if (htrace) ht[1] = now_ms();
@@ -2905,10 +2764,6 @@ int64_t tbg_forget_orphans(tbg_ctx* ctx, const tb_uint128_t* ids, uint32_t n) {
     if (!ctx || n > ctx->opt.batch_events_max || (n && !ids)) return TBG_EINVAL;
     FAILED_GUARD(ctx);
     if (n == 0) return 0;
-    ctx->prefetch_events = nullptr;  // (d_events is the scratch)
-    ctx->prefetch_bytes = 0;
-    if (ctx->ae_snap_body == ctx->d_events)
-        if (int rc = ae_flush_all(ctx)) return rc;
     HIP_TRY(ctx, hipMemcpyAsync(ctx->d_events, ids, size_t(n) * 16, hipMemcpyHostToDevice,
                                 ctx->stream));
     unsigned int* d_count = &ctx->d_scalars->slow_count;  // scratch word (between calls)
@@ -2930,10 +2785,6 @@ int64_t tbg_timestamps_exist(tbg_ctx* ctx, int transfers, const uint64_t* timest
     // (check_imported_indexes rebuilds the index an imported call of the *other* groove reads)
     int rc = check_imported_indexes(ctx, transfers == 0);
     if (rc) return rc;
-    ctx->prefetch_events = nullptr;
-    ctx->prefetch_bytes = 0;
-    if (ctx->ae_snap_body == ctx->d_events)
-        if ((rc = ae_flush_all(ctx))) return rc;
     uint64_t* d_ts = reinterpret_cast<uint64_t*>(ctx->d_events);
     uint8_t* d_out = reinterpret_cast<uint8_t*>(d_ts + n);
     HIP_TRY(ctx, hipMemcpyAsync(d_ts, timestamps, size_t(n) * 8, hipMemcpyHostToDevice,

@@ -70,7 +70,6 @@ struct GroupPlan {
     // account lanes (lanes.hpp): owner segments and free owners; lanes == false: none
     bool lanes;
     bool free_owners;               // free-owner verdicts (TBG_NO_FREE_OWNERS: none)
-    bool sort_values;               // group_sort: every segment that fits LDS sorts as values
     uint32_t epoch;
     uint32_t* owner_starts;
     unsigned int* lane_counts;      // [0] owners, [1] ineligible events
@@ -756,7 +755,7 @@ __global__ void __launch_bounds__(kGroupBigThreads) group_sort(GroupPlan G) {
     const uint32_t nbig = G.counts[1];
     for (uint32_t b = blockIdx.x; b < nbig; b += gridDim.x) {
         const uint4 e = G.big[b];
-        segment_sort(G.vals, G.vals_sorted, e.x, e.y, L, G.sort_values);
+        segment_sort(G.vals, G.vals_sorted, e.x, e.y, L);
     }
 }
 

@@ -1670,7 +1670,7 @@ __device__ inline void add_field(const BalTarget& B, uint32_t key, u128 sum, boo
 // of kHashSliceItems items per account field in an LDS hash table (open addressing on the key,
 // u64 sums: amounts < 2^46 at these key widths, 2^11 items per slice) and adds every field's slice
 // sum to its row with u128 atomics -- a hot account costs one atomic per workgroup instead of one
-// per item, a cold one what bal_atomic_apply pays. An item whose probe window is full takes its
+// per item, a cold one a u128 atomic on the row. An item whose probe window is full takes its
 // atomic at once. (This replaces a library radix sort of the items and a run reduction.)
 constexpr uint32_t kHashThreads = 256;
 constexpr uint32_t kHashSlots = 4096;
@@ -1723,22 +1723,6 @@ __global__ void __launch_bounds__(kHashThreads) bal_hash_apply(BalTarget rows, c
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < kHashSlots; i += kHashThreads)
         if (hkey[i] != kHashEmpty) add_field(rows, hkey[i], hsum[i], true);
-}
-
-// Sparse key spaces (far more account fields than items): the FAST events' packed balance items
-// applied with u128 atomics, two items per lane -- collisions are rare, no sort is needed.
-__global__ void bal_atomic_apply(BalTarget rows, const uint64_t* items, uint64_t n,
-                                 uint32_t key_bits, uint32_t key_end) {
-    const uint64_t i = 2 * (uint64_t(blockIdx.x) * blockDim.x + threadIdx.x);
-    if (i >= n) return;
-    const uint64_t kmask = (1ull << key_bits) - 1;
-    const uint4 q = *reinterpret_cast<const uint4*>(items + i);  // n is even (2 per event)
-    const uint64_t it[2] = {(uint64_t(q.y) << 32) | q.x, (uint64_t(q.w) << 32) | q.z};
-#pragma unroll
-    for (int j = 0; j < 2; j++) {
-        const uint64_t key = it[j] & kmask;
-        if (key < key_end) add_field(rows, uint32_t(key), it[j] >> key_bits, true);
-    }
 }
 
 // ---- the balance window path (key spaces of <= 2^14 accounts, e.g. config 2) -----

@@ -48,7 +48,9 @@ struct RouteArgs {
     uint8_t* ev_shard;      // per event: its shard, 0xFF for a hazard
     uint32_t* ev_slot;      // per event: its claimed slot (kNone32: none)
     uint32_t* block_counts; // [shard][block]
-    unsigned int* flags;    // [0] hazard, [1] table full, [2] the call posts or voids
+    unsigned int* flags;    // [0] hazard, [1] table full, [2] the call posts or voids,
+                            // [3] bit 0: an imported event, bit 1: a non-imported one
+    uint64_t imported_floor;  // imported timestamps at or below it are hazards (tbr.h)
 };
 
 __device__ inline uint64_t dir_find(const Dir& d, const tb_uint128_t& id) {
@@ -91,14 +93,30 @@ __device__ inline void raise_hazard(const RouteArgs& a, bool hazard) {
 __global__ void __launch_bounds__(kRouteBlock) tbr_pass1(RouteArgs a) {
     const uint32_t k = blockIdx.x * kRouteBlock + threadIdx.x;
     bool hazard = false, pv_any = false;
+    unsigned int kinds = 0;
     if (k < a.n) {
         const tb_transfer_t& t = a.events[k];
         const uint16_t f = t.flags;
         const bool post_void = (f & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) != 0;
+        const bool imported = (f & TB_TRANSFER_IMPORTED) != 0;
         uint8_t shard = kShardHazard;
         uint32_t slot = kNone32;
-        hazard = (f & (TB_TRANSFER_IMPORTED | TB_TRANSFER_PADDING_MASK)) != 0 ||
-                 t.timestamp != 0 || u128_is_zero(t.id) || u128_is_max(t.id);
+        hazard = (f & TB_TRANSFER_PADDING_MASK) != 0 || (!imported && t.timestamp != 0) ||
+                 u128_is_zero(t.id) || u128_is_max(t.id);
+        // Imported events (execute_create :3066-3078, must_not_regress :3808-3817): routed when
+        // the whole call is imported (flags[3]; each shard's slice is one batch), their
+        // timestamps increase through the call (no event can regress past another shard's) and
+        // lie above every object of both grooves (the floor: no key range or timestamp of another
+        // shard can decide them) and below their own commit timestamps (must_not_advance holds
+        // on every shard as in the reference).
+        if (imported) {
+            const uint32_t b = batch_of_guess(a.batch_ends, a.n_batches, a.n, k);
+            const uint64_t stamp = a.batch_ts[b] - a.batch_ends[b] + k + 1;
+            hazard = hazard || t.timestamp < TB_TIMESTAMP_MIN || t.timestamp >= stamp ||
+                     t.timestamp <= a.imported_floor ||
+                     (k > 0 && t.timestamp <= a.events[k - 1].timestamp);
+        }
+        kinds = imported ? 1u : 2u;
         uint64_t sd = kNone;
         if (!hazard) {
             // The id: new to every shard and unique in the call (the serial order's first
@@ -143,6 +161,9 @@ __global__ void __launch_bounds__(kRouteBlock) tbr_pass1(RouteArgs a) {
         pv_any = post_void;
     }
     if (__any(pv_any) && (threadIdx.x & 63) == 0) atomicOr(&a.flags[2], 1u);
+    const uint64_t any_imported = __ballot(kinds & 1u), any_plain = __ballot(kinds & 2u);
+    if ((threadIdx.x & 63) == 0 && (any_imported || any_plain))
+        atomicOr(&a.flags[3], (any_imported ? 1u : 0u) | (any_plain ? 2u : 0u));
     raise_hazard(a, hazard);
 }
 
@@ -303,6 +324,7 @@ struct tbr_ctx {
     uint32_t* offsets = nullptr;
     unsigned int* flags = nullptr;
     unsigned long long* key_max = nullptr;  // settle: created timestamps' maximum
+    uint64_t imported_floor = ~0ull;        // tbr_set_imported_floor (none yet: every import)
     tb_uint128_t* q_ids = nullptr;  // lookup / record staging (events_max)
     int32_t* q_out = nullptr;
     // the routed call awaiting tbr_settle_device
@@ -338,6 +360,7 @@ RouteArgs route_args(tbr_ctx* r, const tb_transfer_t* ev, uint32_t n, const uint
     a.ev_slot = r->ev_slot;
     a.block_counts = r->block_counts;
     a.flags = r->flags;
+    a.imported_floor = r->imported_floor;
     return a;
 }
 
@@ -467,6 +490,7 @@ int64_t tbr_route_device(tbr_ctx* r, const tb_transfer_t* d_events, uint32_t n,
                        r->stream) ||
         hipStreamSynchronize(r->stream))
         return -5;
+    if (f[3] == 3u) f[0] = 1;  // imported and non-imported events in one call
     if (f[0] || f[1]) {
         hipLaunchKernelGGL(tbr_release, grid, block, 0, r->stream, a);
         if (hipStreamSynchronize(r->stream)) return -5;
@@ -493,6 +517,12 @@ int64_t tbr_route_device(tbr_ctx* r, const tb_transfer_t* d_events, uint32_t n,
     r->call_base = a.base;
     r->call_n = n;
     return f[2] ? 2 : 0;
+}
+
+int tbr_set_imported_floor(tbr_ctx* r, uint64_t floor) {
+    if (!r) return -22;
+    r->imported_floor = floor;
+    return 0;
 }
 
 int tbr_settle_device(tbr_ctx* r, const tb_create_result_t* d_shard_results,

@@ -407,24 +407,15 @@ extern "C" int tb_sm_pulse_needed(const tb_sm* sm, uint64_t timestamp) {
 extern "C" void tb_sm_prefetch(tb_sm* sm, tb_sm_prefetch_callback callback, void* context,
                                uint64_t op, uint64_t snapshot, uint8_t operation,
                                const void* body, uint32_t size) {
+    (void)sm;
     (void)op;
     (void)snapshot;
-    // Every table is resident in HBM; what a commit still fetches is the body. A create body in a
-    // registered message pool starts its copy into HBM now (tbg_prefetch_body), and the commit's
-    // create call finds it there. The copy is ordered before the commit on the executor's stream,
-    // so the callback completes at once.
-    OperationInfo info;
-    if (sm && sm->gpu && body && is_create(operation) && operation_info(operation, &info) &&
-        operation == TB_OPERATION_CREATE_TRANSFERS) {
-        uint32_t payload = size;
-        bool ok = true;
-        if (info.multi_batch) {
-            sm->counts.resize(kBatchCountMax);
-            ok = tb_multi_batch_decode(body, size, info.event_size, sm->counts.data(),
-                                       uint32_t(sm->counts.size()), &payload) > 0;
-        }
-        if (ok && payload) (void)tbg_prefetch_body(sm->gpu, body, payload);
-    }
+    (void)operation;
+    (void)body;
+    (void)size;
+    // Every table is resident in HBM: nothing is staged. (The body itself is read by the commit's
+    // create kernel across PCIe from the registered message pool; a copy started here measured
+    // slower back to back with the commit -- DESIGN.md §13.)
     if (callback) callback(context);
 }
 

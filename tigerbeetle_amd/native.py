@@ -99,7 +99,6 @@ SIGNATURES = [
     ("tbg_timestamps_exist", ctypes.c_int64, [vp, ctypes.c_int, vp, ctypes.c_uint32, vp]),
     ("tbg_register_host", ctypes.c_int, [vp, vp, ctypes.c_uint64]),
     ("tbg_unregister_host", ctypes.c_int, [vp, vp]),
-    ("tbg_prefetch_body", ctypes.c_int, [vp, vp, ctypes.c_uint64]),
     ("tbg_synchronize", ctypes.c_int, [vp]),
     ("tbg_pulse", ctypes.c_int64, [vp, ctypes.c_uint64]),
     ("tbg_pulse_candidates", ctypes.c_int64, [vp, ctypes.c_uint64, vp, vp, ctypes.c_uint32]),
@@ -143,6 +142,7 @@ SIGNATURES = [
     ("tbr_route_device", ctypes.c_int64, [vp, vp, ctypes.c_uint32, vp, vp, ctypes.c_uint32, vp, vp,
                                           vp, vp]),
     ("tbr_settle_device", ctypes.c_int, [vp, vp, vp, ctypes.c_uint32, vp, c_u64p]),
+    ("tbr_set_imported_floor", ctypes.c_int, [vp, ctypes.c_uint64]),
     ("tb_sm_open", vp, [ctypes.POINTER(SmOptions), ctypes.POINTER(Executor)]),
     ("tb_sm_open_gpu", vp, [ctypes.POINTER(SmOptions), ctypes.POINTER(TbgOptions)]),
     ("tb_sm_open_gpu_checkpoint", vp, [ctypes.POINTER(SmOptions), ctypes.POINTER(TbgOptions),

@@ -17,6 +17,11 @@ by the exact host engine instead (shard.Engine over the same directories, throug
 shard.ShardGroup): surrogates for cross-shard transfers, segments, the chain protocol for linked
 chains across shards, key-range sync for imported batches -- every call executes exactly.
 
+Imported calls take the device path when every event is imported, their timestamps increase and
+lie above the imported floor -- the largest timestamp of any object on any shard, kept by rank 0
+(the shards' key maxima after every host-path call, raised by each routed call's created
+timestamps; tbr_set_imported_floor).
+
 A routed call that posts or voids (the router's mode 2) resolves pulse_next_timestamp across the
 shards after it (shard.ShardGroup.resolve_pnt: every shard's recorded updates gathered at rank 0,
 replayed in call order, the outcome broadcast): a post/void of a pending transfer with a timeout
@@ -71,6 +76,7 @@ class RoutedShards:
             else None
         self.fast_calls = 0
         self.host_calls = 0
+        self.floor = None  # the imported floor (rank 0; None: unknown until a host-path call)
 
     def close(self):
         if self.tbr:
@@ -107,8 +113,23 @@ class RoutedShards:
 
     # -- calls --------------------------------------------------------------------------------------
 
+    def _set_floor(self, floor):
+        if self.rank == 0:
+            self.floor = floor
+            rc = self.lib.tbr_set_imported_floor(self.tbr, (1 << 64) - 1 if floor is None
+                                                 else int(floor))
+            if rc != 0:
+                raise RuntimeError(f"tbr_set_imported_floor: {rc}")
+
+    def _refresh_floor(self):
+        """Collective: the key maxima over all shards (raised on every shard) as the floor."""
+        a, t = self.host.sync_key_max_collective()
+        self._set_floor(max(a, t))
+
     def record_accounts(self, ids: np.ndarray, shards: np.ndarray):
-        """Rank 0: accounts that already exist on their shards (created there directly)."""
+        """Rank 0: accounts that already exist on their shards (created there directly; the
+        imported floor is unknown until the next host-path call)."""
+        self._set_floor(None)
         rc = self.lib.tbr_record_accounts(self.tbr, np.ascontiguousarray(ids).ctypes.data_as(
             ctypes.c_void_p), np.ascontiguousarray(shards, dtype=np.uint8).ctypes.data_as(
             ctypes.c_void_p), len(ids))
@@ -148,6 +169,7 @@ class RoutedShards:
                 self._copy_to_ptr(buf, d_results)
             else:
                 self.host.create_transfers()
+            self._refresh_floor()
             return 1
         self.fast_calls += 1
         offs = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
@@ -168,10 +190,13 @@ class RoutedShards:
                 if r is not None:
                     r.wait()
             self.torch.cuda.synchronize(self.dev)
+            km = ctypes.c_uint64(0)
             rc = self.lib.tbr_settle_device(self.tbr, self.res.data_ptr(), self.pos.data_ptr(), n,
-                                            d_results, None)
+                                            d_results, ctypes.byref(km))
             if rc != 0:
                 raise RuntimeError(f"tbr_settle_device: {rc}")
+            if self.floor is not None:
+                self._set_floor(max(self.floor, km.value))
         else:
             if mine:
                 self._recv(self.ev[:mine * 128], 0)
@@ -209,7 +234,9 @@ class RoutedShards:
 
     # pulses and host-router calls go through the host group (collective)
     def create_accounts(self, events=None, lens=None, batch_ts=None):
-        return self.host.create_accounts(events, lens, batch_ts)
+        res = self.host.create_accounts(events, lens, batch_ts)
+        self._refresh_floor()
+        return res
 
     def pulse_next_timestamp(self):
         return self.host.pulse_next_timestamp()
