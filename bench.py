@@ -83,6 +83,9 @@ def parse_args():
     ap.add_argument("--accounts", type=int, default=None,
                     help="accounts per GPU (config2: 10k, config5: 125M = 1B / 8)")
     ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--amounts", choices=["exp", "wide"], default="exp",
+                    help="config2 amounts: exp = Exp(10k) +| 1 (benchmark_load.zig); wide = "
+                         "log-uniform over [1, 2^63) (every result still created)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="bounded CPU-oracle sample (rank 0, N=1)")
     ap.add_argument("--no-account-events-line", action="store_true",
@@ -177,6 +180,20 @@ class Device:
         for p in self.ptrs:
             self.hip.hipFree(p)
         self.ptrs = []
+
+
+def u128_sums(idx, amt, n_out, reps):
+    """Exact u128 sums of u64 amounts by index, times reps: (n_out, 2) u64 [lo, hi] words (the
+    32-bit halves summed apart, so no u64 sum wraps for amounts up to 2^64 over < 2^32 events)."""
+    lo = np.zeros(n_out, dtype=np.uint64)
+    hi = np.zeros(n_out, dtype=np.uint64)
+    np.add.at(lo, idx, amt & np.uint64(0xFFFFFFFF))
+    np.add.at(hi, idx, amt >> np.uint64(32))
+    out = np.zeros((n_out, 2), dtype=np.uint64)
+    for i, (a, b) in enumerate(zip(lo.tolist(), hi.tolist())):
+        v = (a + (b << 32)) * reps
+        out[i] = (v & 0xFFFFFFFFFFFFFFFF, v >> 64)
+    return out
 
 
 def batch_plan(n):
@@ -301,7 +318,7 @@ class Config2:
         self.base = workload.transfers_uniform(self.N, self.A, seed=args.seed + rank,
                                                id_offset=rank * self.N,
                                                account_id_offset=rank * self.A,
-                                               ledger=self.ledger)
+                                               ledger=self.ledger, amounts=args.amounts)
         self.dr = self.base["debit_account_id"][:, 0].astype(np.int64) - 1 - rank * self.A
         self.cr = self.base["credit_account_id"][:, 0].astype(np.int64) - 1 - rank * self.A
         self.chunk = self.A
@@ -313,6 +330,8 @@ class Config2:
                                       f" (one client stream of {world} x 1222 batches, batch g "
                                       f"on ledger 2 + g mod {world})"),
                        "transfers_per_step_per_gpu": self.N, "accounts_per_gpu": self.A}
+        if args.amounts != "exp":
+            self.config["amounts"] = "log-uniform over [1, 2^63)"
 
     def account_chunks(self):
         yield self.acc
@@ -328,9 +347,7 @@ class Config2:
         want["timestamp"] = self.account_ts
         # (exact integer sums: bincount's float64 weights would round past 2^53)
         for col, idx in (("debits_posted", self.dr), ("credits_posted", self.cr)):
-            s = np.zeros(self.A, dtype=np.uint64)
-            np.add.at(s, idx, amt)
-            want[col][:, 0] = s * np.uint64(reps)
+            want[col] = u128_sums(idx, amt, self.A, reps)
         ok = dump.tobytes() == want.tobytes()
         return ok, "" if ok else "account rows differ"
 
@@ -589,10 +606,10 @@ def per_commit(args, lib, dev, g, wl, prepare_ts, id_base):
     amt = body_events["amount"][:, 0].astype(np.uint64)
     touched = np.unique(np.concatenate([dr_i, cr_i]))
     pos = {int(a): i for i, a in enumerate(touched)}
-    exp_d = np.zeros(len(touched), dtype=np.uint64)
-    exp_c = np.zeros(len(touched), dtype=np.uint64)
-    np.add.at(exp_d, np.fromiter((pos[int(x)] for x in dr_i), dtype=np.int64, count=n), amt)
-    np.add.at(exp_c, np.fromiter((pos[int(x)] for x in cr_i), dtype=np.int64, count=n), amt)
+    exp_d = u128_sums(np.fromiter((pos[int(x)] for x in dr_i), dtype=np.int64, count=n), amt,
+                      len(touched), R + 1)
+    exp_c = u128_sums(np.fromiter((pos[int(x)] for x in cr_i), dtype=np.int64, count=n), amt,
+                      len(touched), R + 1)
     acc_ids = np.zeros((len(touched), 2), dtype=np.uint64)
     acc_ids[:, 0] = (wl.acc["id"][touched, 0] if wl.name == "config2" else
                      workload.config5_global_index(touched, wl.rank, wl.world) + 1)
@@ -601,8 +618,8 @@ def per_commit(args, lib, dev, g, wl, prepare_ts, id_base):
         z = min(len(touched), a + BATCH)
         sm_ok &= lib.tbg_lookup_accounts(g_sm, acc_ids[a:z].ctypes.data_as(ctypes.c_void_p), z - a,
                                          acc_rows[a:z].ctypes.data_as(ctypes.c_void_p)) == z - a
-    sm_ok &= bool((acc_rows["debits_posted"][:, 0] == exp_d * np.uint64(R + 1)).all() and
-                  (acc_rows["credits_posted"][:, 0] == exp_c * np.uint64(R + 1)).all() and
+    sm_ok &= bool((acc_rows["debits_posted"] == exp_d).all() and
+                  (acc_rows["credits_posted"] == exp_c).all() and
                   (acc_rows["debits_pending"] == 0).all() and (acc_rows["credits_pending"] == 0).all())
     n_events = lib.tbg_dump_account_events(g_sm, None)
     sm_ok &= n_events == (R + 1) * n  # one AccountEvent per created transfer

@@ -30,7 +30,7 @@ def commit_lens(m, batch=BATCH):
 
 
 def config3(p, n, batches_per_commit=16, tail_single=0, accounts=10_000, n_hot=100, seed=3,
-            before_calls=None):
+            before_calls=None, amounts="exp"):
     """Config 3 on Pair `p` (capacities: accounts + 1, n + tail_single + n_hot transfers).
     `tail_single` more events follow as one single-batch call (one replica commit of <= 8189
     events). `before_calls` (if given) runs after setup, before the measured calls. Returns a
@@ -38,7 +38,8 @@ def config3(p, n, batches_per_commit=16, tail_single=0, accounts=10_000, n_hot=1
     acc = workload.accounts(accounts, seed=seed)
     acc["flags"][1:n_hot + 1] |= 2  # debits_must_not_exceed_credits
     p.create_accounts(acc)
-    t = workload.transfers_hot_limits(n + tail_single, n_accounts=accounts, n_hot=n_hot, seed=seed)
+    t = workload.transfers_hot_limits(n + tail_single, n_accounts=accounts, n_hot=n_hot, seed=seed,
+                                      amounts=amounts)
     p.create_transfers(workload.funding_transfers(
         n_hot, workload.hot_funding_amounts(t[:n], n_hot, 0.8), id_offset=1 << 40))
     if before_calls:
@@ -61,7 +62,7 @@ def config3(p, n, batches_per_commit=16, tail_single=0, accounts=10_000, n_hot=1
 
 
 def config4(p, n, batches_per_commit=16, accounts=10_000, seed=4, n_limited=16,
-            before_calls=None):
+            before_calls=None, amounts="exp"):
     """Config 4 on Pair `p`: commits of `batches_per_commit` x 8189 events, each followed by a
     1-2 s tick (the pulse runs when pulse_needed). Returns a summary dict with the statuses
     seen."""
@@ -80,7 +81,8 @@ def config4(p, n, batches_per_commit=16, accounts=10_000, seed=4, n_limited=16,
         m = min(per_commit, n - off)
         t = workload.transfers_two_phase(m, accounts, seed=10 * seed + step, id_offset=off,
                                          prior_pending_ids=pending, prior_ids=seen,
-                                         prior_resolved_ids=resolved, n_limited=n_limited)
+                                         prior_resolved_ids=resolved, n_limited=n_limited,
+                                         amounts=amounts)
         r = p.create_transfers(t, commit_lens(m))
         statuses |= set(int(x) for x in np.unique(r["status"]))
         created = r["status"] == 0xFFFFFFFF

@@ -38,13 +38,19 @@ def _codes(rng, n):
     return np.minimum(r + 1, 0xFFFF).astype(np.uint16)  # rand(u16) +| 1
 
 
-def _amounts(rng, n, mean=10_000):
+def _amounts(rng, n, mean=10_000, amounts="exp"):
+    """Exp(mean) +| 1 (benchmark_load.zig's), or with amounts="wide" log-uniform over
+    [1, 2^63): most above 2^19, a ledger in cents moving up to ~$10^16 a transfer."""
+    if amounts == "wide":
+        e = np.floor(np.exp2(rng.uniform(0.0, 63.0, size=n)))
+        return np.minimum(e, float(2**63 - 1024)).astype(U64)
     e = np.floor(rng.exponential(mean, size=n)).astype(np.int64)
     return (e + 1).astype(U64)  # Exp(mean) +| 1
 
 
 def transfers_uniform(n: int, n_accounts: int, seed: int = 42, id_offset: int = 0,
-                      account_id_offset: int = 0, ledger: int = 2) -> np.ndarray:
+                      account_id_offset: int = 0, ledger: int = 2,
+                      amounts: str = "exp") -> np.ndarray:
     """Config 1/2: uniform debit/credit over the accounts, no pending (benchmark_load.zig:965)."""
     rng = np.random.default_rng(seed)
     t = np.zeros(n, dtype=TRANSFER_DTYPE)
@@ -59,7 +65,7 @@ def transfers_uniform(n: int, n_accounts: int, seed: int = 42, id_offset: int = 
     t["user_data_32"] = rng.integers(0, 2**32, size=n, dtype=np.int64).astype(np.uint32)
     t["ledger"] = ledger
     t["code"] = _codes(rng, n)
-    _u128_col(t, "amount", _amounts(rng, n))
+    _u128_col(t, "amount", _amounts(rng, n, amounts=amounts))
     return t
 
 
@@ -88,10 +94,11 @@ def hot_limits_setup(n_accounts: int = 10_000, n_hot: int = 100, seed: int = 42,
 
 def transfers_hot_limits(n: int, n_accounts: int = 10_000, n_hot: int = 100, seed: int = 42,
                          id_offset: int = 0, theta: float = 0.99, hot_debit_ratio: float = 0.9,
-                         hot_credit_ratio: float = 0.1, amount_mean: int = 10_000) -> np.ndarray:
+                         hot_credit_ratio: float = 0.1, amount_mean: int = 10_000,
+                         amounts: str = "exp") -> np.ndarray:
     """Config 3: 90% of debits from Zipf-chosen hot (limited) accounts, ~10% of credits to hot."""
     rng = np.random.default_rng(seed)
-    t = transfers_uniform(n, n_accounts, seed=seed + 1, id_offset=id_offset)
+    t = transfers_uniform(n, n_accounts, seed=seed + 1, id_offset=id_offset, amounts=amounts)
     cold_lo, cold_n = n_hot + 1, n_accounts - n_hot - 1  # cold indices [n_hot+1, n_accounts)
     hot = rng.random(n) < hot_debit_ratio
     dr = np.where(hot, 1 + zipf_indices(rng, n_hot, theta, n),
@@ -102,7 +109,7 @@ def transfers_hot_limits(n: int, n_accounts: int = 10_000, n_hot: int = 100, see
     cr = np.where(cr == dr, np.where(cr + 1 < n_accounts, cr + 1, cold_lo), cr)
     _u128_col(t, "debit_account_id", (dr + 1).astype(U64))
     _u128_col(t, "credit_account_id", (cr + 1).astype(U64))
-    _u128_col(t, "amount", _amounts(rng, n, amount_mean))
+    _u128_col(t, "amount", _amounts(rng, n, amount_mean, amounts))
     return t
 
 
@@ -113,7 +120,11 @@ def funding_transfers(n_hot: int, amount, id_offset: int, source_index: int = 0)
     _u128_col(t, "id", np.arange(id_offset + 1, id_offset + n_hot + 1, dtype=U64))
     _u128_col(t, "debit_account_id", np.full(n_hot, source_index + 1, dtype=U64))
     _u128_col(t, "credit_account_id", np.arange(2, n_hot + 2, dtype=U64))
-    _u128_col(t, "amount", np.broadcast_to(np.asarray(amount, dtype=U64), (n_hot,)).copy())
+    if isinstance(amount, (list, tuple)):  # u128 Python ints
+        t["amount"][:, 0] = [a & 0xFFFFFFFFFFFFFFFF for a in amount]
+        t["amount"][:, 1] = [a >> 64 for a in amount]
+    else:
+        _u128_col(t, "amount", np.broadcast_to(np.asarray(amount, dtype=U64), (n_hot,)).copy())
     t["ledger"] = 2
     t["code"] = 1
     return t
@@ -129,14 +140,17 @@ def hot_funding_amounts(t: np.ndarray, n_hot: int = 100, fraction: float = 0.8) 
     hot_d, hot_c = (dr >= 0) & (dr < n_hot), (cr >= 0) & (cr < n_hot)
     debits = np.bincount(dr[hot_d], weights=amt[hot_d], minlength=n_hot)
     credits = np.bincount(cr[hot_c], weights=amt[hot_c], minlength=n_hot)
-    return np.maximum(fraction * debits - credits, 0).astype(U64)
+    f = np.maximum(fraction * debits - credits, 0)
+    if f.max() >= 2.0**63:  # (wide amounts: u128 funding, as Python ints)
+        return [int(x) for x in f]
+    return f.astype(U64)
 
 
 def transfers_two_phase(n: int, n_accounts: int, seed: int, id_offset: int,
                         prior_pending_ids: np.ndarray, pending_ratio=0.3, chain_ratio=0.3,
                         chain_len=8, fail_ratio=0.1, resubmit_ratio=0.01,
                         prior_ids: np.ndarray = None, prior_resolved_ids: np.ndarray = None,
-                        n_limited: int = 0) -> np.ndarray:
+                        n_limited: int = 0, amounts: str = "exp") -> np.ndarray:
     """Config 4: pending transfers with 1-5 s timeouts; posts (67%: half of them
     the full amount via maxInt, half a quarter of it) and voids (33%: 70% amount 0, 30% a nonzero
     amount, which fails with pending_transfer_has_different_amount when below the pending amount)
@@ -147,7 +161,7 @@ def transfers_two_phase(n: int, n_accounts: int, seed: int, id_offset: int,
     n_limited > 0) or a post of a pending transfer already posted or voided (`prior_resolved_ids`)
     -- and `resubmit_ratio` of ids resubmitted (exists / id_already_failed)."""
     rng = np.random.default_rng(seed)
-    t = transfers_uniform(n, n_accounts, seed=seed, id_offset=id_offset)
+    t = transfers_uniform(n, n_accounts, seed=seed, id_offset=id_offset, amounts=amounts)
     if n_limited:  # plain transfers never touch the limited accounts (their failures are injected)
         for col in ("debit_account_id", "credit_account_id"):
             low = t[col][:, 0] <= U64(n_limited)

@@ -71,7 +71,7 @@ def line(name, p, n, t_wall, extra):
             "pulse": pulse_line(p), **extra}
 
 
-def run(config, n, batches, profile=True):
+def run(config, n, batches, profile=True, amounts="exp"):
     t0 = time.perf_counter()
     p = Pair(account_capacity=1 << 14, transfer_capacity=n + (1 << 12),
              batch_events_max=max(BATCH * batches, 1 << 14), batch_count_max=batches)
@@ -84,9 +84,9 @@ def run(config, n, batches, profile=True):
 
     try:
         drive = configs34.config3 if config == "config3" else configs34.config4
-        extra = drive(p, n, batches_per_commit=batches, before_calls=start)
+        extra = drive(p, n, batches_per_commit=batches, before_calls=start, amounts=amounts)
         p.compare_state()
-        return line(config, p, n, time.perf_counter() - t0, extra)
+        return line(config, p, n, time.perf_counter() - t0, dict(extra, amounts=amounts))
     finally:
         p.close()
 
@@ -100,10 +100,12 @@ def main():
                     help="no per-kernel HIP events: the executor's asynchronous paths (the "
                          "AccountEvents appends behind the next call) run as in production; "
                          "host-timed rates only")
+    ap.add_argument("--amounts", choices=["exp", "wide"], default="exp",
+                    help="exp: Exp(10k) +| 1 (benchmark_load.zig); wide: log-uniform up to 2^63")
     args = ap.parse_args()
     for c in args.configs.split(","):
         print(json.dumps(run("config" + c.strip(), args.transfers, args.batches,
-                             profile=not args.no_profile)), flush=True)
+                             profile=not args.no_profile, amounts=args.amounts)), flush=True)
 
 
 if __name__ == "__main__":
