@@ -87,3 +87,21 @@ def test_config4_one_batch_commits(pv, monkeypatch):
         p.compare_state()
     finally:
         p.close()
+
+
+@pytest.mark.parametrize("config", ["config3", "config4"])
+def test_configs34_wide_amounts(config):
+    """Amounts log-uniform over [1, 2^63) (workload amounts="wide"): the account lanes' windows
+    on u128 (owners' balances past 2^62), balance items too wide to pack (tr_commit's atomics),
+    AccountEvents past the one-pass paths' 2^19 gate; 300k events, every result, row and
+    AccountEvent against the oracle."""
+    n = 300_000
+    p = _pair(n + BATCH, 16)
+    try:
+        drive = configs34.config3 if config == "config3" else configs34.config4
+        s = drive(p, n, batches_per_commit=16, amounts="wide")
+        if config == "config3":
+            assert s["exceeds_credits"] > 0
+        p.compare_state()
+    finally:
+        p.close()

@@ -106,6 +106,29 @@ def test_scans_at_scale(seed):
         p.close()
 
 
+@pytest.mark.parametrize("amounts", ["exp", "wide"])
+def test_uniform_config2_full_size(amounts):
+    """BASELINE configs[1] at its own size against the oracle: 10k accounts, ONE call of 10M
+    uniform create_transfers in 8189-event batches (the bench's step), every result, row and
+    AccountEvent compared (Pair.compare_state). `wide`: amounts log-uniform over [1, 2^63) --
+    beyond the packed balance items (tr_commit's atomics) and the one-pass AccountEvents."""
+    n = 10_000_000
+    p = Pair(account_capacity=1 << 14, transfer_capacity=n + (1 << 14), batch_events_max=n,
+             batch_count_max=1 << 11)
+    try:
+        acc = workload.accounts(10_000, seed=42)
+        r = p.create_accounts(acc, [8189, 10_000 - 8189])
+        assert (r["status"] == 0xFFFFFFFF).all()
+        t = workload.transfers_uniform(n, 10_000, seed=42, amounts=amounts)
+        lens = [8189] * (n // 8189) + [n % 8189]
+        r = p.create_transfers(t, lens)
+        assert (r["status"] == 0xFFFFFFFF).all()
+        assert p.stats["replayed"] == 0
+        p.compare_state()
+    finally:
+        p.close()
+
+
 def test_uniform_config2_small():
     """Config 2 shape at small scale: 10k accounts, 8189-event batches; all `created`."""
     p = Pair(account_capacity=1 << 14, transfer_capacity=1 << 17, batch_events_max=1 << 17)

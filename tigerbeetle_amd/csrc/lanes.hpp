@@ -344,6 +344,20 @@ __device__ inline uint64_t walk_uniform64(uint64_t v) {
 __device__ inline u128 walk_uniform128(const tb_uint128_t& x) {
     return (u128(walk_uniform64(x.hi)) << 64) | walk_uniform64(x.lo);
 }
+// The window sums of lanes_walk in u64 (narrow owners and amounts) or u128 (wide ones).
+__device__ inline uint64_t walk_uniform_v(uint64_t v) { return walk_uniform64(v); }
+__device__ inline u128 walk_uniform_v(u128 v) {
+    return (u128(walk_uniform64(uint64_t(v >> 64))) << 64) | walk_uniform64(uint64_t(v));
+}
+__device__ inline uint64_t walk_shfl_xor(uint64_t v, int off) { return __shfl_xor(v, off); }
+__device__ inline u128 walk_shfl_xor(u128 v, int off) {
+    return (u128(__shfl_xor(uint64_t(v >> 64), off)) << 64) | __shfl_xor(uint64_t(v), off);
+}
+template <typename V>
+__device__ inline V walk_wave_sum(V v) {
+    for (int off = 32; off > 0; off >>= 1) v += walk_shfl_xor(v, off);
+    return walk_uniform_v(v);
+}
 
 __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_transfer_t> c,
                                                                LanePlan L, uint32_t* mbox,
@@ -575,7 +589,10 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
                 }
             }
         };
-        if (narrow && one_limit) {
+        // An owner with one limit flag resolves its window in wave-wide steps, on u64 when its
+        // balances and the window's amounts are narrow (no sum below can wrap), else on u128.
+        auto one_limit_window = [&](auto zero) {
+            using V = decltype(zero);
             // An owner with one limit flag: its checked ("mine") events all test used + amount <=
             // cap -- debits_must_not_exceed_credits: used = dpe + dpo, cap = cpo; credits_must_
             // not_exceed_debits: used = cpe + cpo, cap = dpo -- a created mine event adds to
@@ -585,11 +602,10 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
             // that would be created (or whose other verdict is unknown) is not created -- a
             // ballot finds it, it is applied, and the scan resumes after it. Steps are created
             // events + polls, not events: config 3's exhausted owners fail most of theirs.
-            const uint64_t dpe64 = uint64_t(dpe), cpe64 = uint64_t(cpe);
-            uint64_t used = owner_dm ? dpe64 + uint64_t(dpo) : cpe64 + uint64_t(cpo);
-            uint64_t cap = owner_dm ? uint64_t(cpo) : uint64_t(dpo);
-            const uint64_t used0 = used, cap0 = cap;
-            const uint64_t amt = cur.valid ? walk_u64(cur.amt_lo, cur.amt_hi) : 0;
+            V used = owner_dm ? V(dpe) + V(dpo) : V(cpe) + V(cpo);
+            V cap = owner_dm ? V(cpo) : V(dpo);
+            const V used0 = used, cap0 = cap;
+            const V amt = cur.valid ? V(walk_u64(cur.amt_lo, cur.amt_hi)) : V(0);
             const bool l_mine = (mine_m >> lane) & 1, l_other = (other_m >> lane) & 1;
             uint64_t known = snap_set & other_m, known_ok = snap_ok & other_m;
             n_snap += __popcll(known);
@@ -606,9 +622,7 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
                 known |= set;
                 known_ok |= ok & set;
             };
-            uint64_t mine_sum = l_mine ? amt : 0;
-            for (int off = 32; off > 0; off >>= 1) mine_sum += __shfl_xor(mine_sum, off);
-            mine_sum = walk_uniform64(mine_sum);
+            const V mine_sum = walk_wave_sum(l_mine ? amt : V(0));
             if (used + mine_sum <= cap) {
                 n_alla++;
                 decided = mine_m;
@@ -622,14 +636,8 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
                 }
                 created_m = vmask & (~other_m | known_ok);
                 drfail_m = vmask & ~created_m & ~debit_m;  // (credit events: the debit side failed)
-                uint64_t add_used = ((created_m & mine_m) >> lane) & 1 ? amt : 0;
-                uint64_t add_cap = ((created_m & ~mine_m) >> lane) & 1 ? amt : 0;
-                for (int off = 32; off > 0; off >>= 1) {
-                    add_used += __shfl_xor(add_used, off);
-                    add_cap += __shfl_xor(add_cap, off);
-                }
-                used += walk_uniform64(add_used);
-                cap += walk_uniform64(add_cap);
+                used += walk_wave_sum(((created_m & mine_m) >> lane) & 1 ? amt : V(0));
+                cap += walk_wave_sum(((created_m & ~mine_m) >> lane) & 1 ? amt : V(0));
             } else {
                 uint64_t rem = vmask;
                 while (rem != 0 && !stalled) {
@@ -670,8 +678,8 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
                         }
                         continue;
                     }
-                    const uint64_t a = walk_u64(__builtin_amdgcn_readlane(cur.amt_lo, j),
-                                                __builtin_amdgcn_readlane(cur.amt_hi, j));
+                    const V a = V(walk_u64(__builtin_amdgcn_readlane(cur.amt_lo, j),
+                                           __builtin_amdgcn_readlane(cur.amt_hi, j)));
                     created_m |= bit;
                     if (mine_m & bit) {
                         decided |= bit;
@@ -685,12 +693,17 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
                 }
             }
             if (owner_dm) {
-                dpo = u128(uint64_t(dpo) + (used - used0));
-                cpo = u128(uint64_t(cpo) + (cap - cap0));
+                dpo += u128(used - used0);
+                cpo += u128(cap - cap0);
             } else {
-                cpo = u128(uint64_t(cpo) + (used - used0));
-                dpo = u128(uint64_t(dpo) + (cap - cap0));
+                cpo += u128(used - used0);
+                dpo += u128(cap - cap0);
             }
+        };
+        if (one_limit && narrow) {
+            one_limit_window(uint64_t(0));
+        } else if (one_limit) {
+            one_limit_window(u128(0));
         } else if (narrow) {
             uint64_t dpo64 = uint64_t(dpo), cpo64 = uint64_t(cpo);
             walk_events(uint64_t(dpe), dpo64, uint64_t(cpe), cpo64);
