@@ -2088,7 +2088,8 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
         const uint32_t nwg = std::max<uint32_t>(1, std::min<uint32_t>(kWindowGridMax, n / 8192));
         const uint32_t wkeys = std::min<uint32_t>(kWindowKeys, 4u << pair_shift);
         hipLaunchKernelGGL(bal_window_accumulate, dim3(nwg), dim3(kWindowThreads), 0, ctx->stream,
-                           target, ctx->bal_items, n, pair_shift, wkeys, ctx->window_partials,
+                           target, ctx->bal_items, c.ev_amount, n, pair_shift, wkeys,
+                           ctx->window_partials,
                            ctx->window_carry, ctx->window_counts, &ctx->d_scalars->flags);
         tmark(ctx, "bal_window");
         hipLaunchKernelGGL(bal_window_apply, dim3((wkeys + 63) / 64), dim3(kApplyThreads), 0,

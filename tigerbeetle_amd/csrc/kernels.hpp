@@ -483,8 +483,11 @@ __device__ inline uint8_t classify_after_lookup(const Tables& T, const Call<tb_t
 
 // Does a FAST event's amount fit its call's balance item(s)? (Else tr_commit adds it with u128
 // atomics.)
+// A pair item's amount field (63 - 2 pair_shift bits); all ones marks a *wide* item, whose
+// amount the balance window reads from the event's record (ev_amount).
+__device__ inline uint64_t pair_amount_mask(uint32_t ps) { return (1ull << (63 - 2 * ps)) - 1; }
 __device__ inline bool item_packable(const Call<tb_transfer_t>& c, uint64_t amount) {
-    return c.pair_shift ? (amount >> (63 - 2 * c.pair_shift)) == 0
+    return c.pair_shift ? amount < pair_amount_mask(c.pair_shift)
                         : (amount >> (64 - c.key_bits)) == 0;
 }
 
@@ -726,14 +729,12 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
         } else if (c.bal_items && c.pair_shift) {
             const uint32_t ps = c.pair_shift;
             ae_slow = pending;  // (the AccountEvents window tracks posted balances only)
-            if (item_packable(c, amount)) {
-                c.bal_items[k] = (amount << (2 * ps + 1)) | (uint64_t(pending) << (2 * ps)) |
-                                 (uint64_t(cr.row) << ps) | dr.row;
-            } else {
-                ae_slow = true;
-                c.bal_items[k] = ~0ull;  // too wide to pack: atomics in tr_commit
-                need_commit = true;
-            }
+            // (too wide to pack: a wide item, its amount in ev_amount -- the event is not lean --
+            // which the AccountEvents window does not take)
+            const bool packed = item_packable(c, amount);
+            ae_slow |= !packed;
+            c.bal_items[k] = ((packed ? amount : pair_amount_mask(ps)) << (2 * ps + 1)) |
+                             (uint64_t(pending) << (2 * ps)) | (uint64_t(cr.row) << ps) | dr.row;
         } else if (c.bal_items) {
             uint4* it = reinterpret_cast<uint4*>(c.bal_items + 2 * uint64_t(k));
             if ((amount >> (64 - c.key_bits)) == 0) {
@@ -1492,8 +1493,9 @@ __device__ inline void commit_event(const Tables& T, const Call<tb_transfer_t>& 
             applied = true;
             ts_applied = c.results[k].timestamp;
             const bool pending = (info & kInfoPending) != 0;
-            // (a call without balance items: ingest applied the deltas)
-            if (c.bal_items && !item_packable(c, amount))
+            // (a call without balance items: ingest applied the deltas; a wide pair item is the
+            // balance window's)
+            if (c.bal_items && !c.pair_shift && !item_packable(c, amount))
                 apply_fast_deltas(T, dr, cr, pending, amount, false);
             if (pending && (info & kInfoTimeout)) {
                 *expiry_row = row;  // (appended by the wave: tr_commit)
@@ -1773,8 +1775,8 @@ __host__ __device__ inline uint32_t window_slice_per(uint32_t n, uint32_t nwg) {
 // (+ per workgroup: the count of its slice's items -- the created events of a call the
 // AccountEvents window takes -- and kFlagWideSums when a u32 window counter carried)
 __global__ void __launch_bounds__(kWindowThreads) bal_window_accumulate(
-    BalTarget B, const uint64_t* items, uint32_t n, uint32_t ps, uint32_t wkeys,
-    uint32_t* partials, unsigned long long* carry, unsigned int* slice_count,
+    BalTarget B, const uint64_t* items, const uint64_t* wide_amounts, uint32_t n, uint32_t ps,
+    uint32_t wkeys, uint32_t* partials, unsigned long long* carry, unsigned int* slice_count,
     unsigned int* call_flags) {
     __shared__ uint32_t acc[kWindowKeys];
     __shared__ uint32_t wave_items[kWindowThreads / 64];
@@ -1784,6 +1786,7 @@ __global__ void __launch_bounds__(kWindowThreads) bal_window_accumulate(
     const uint32_t b0 = blockIdx.x * per;
     const uint32_t b1 = b0 + per < n ? b0 + per : n;
     const uint64_t rmask = (1ull << ps) - 1;
+    const uint64_t amask = pair_amount_mask(ps);
     uint32_t n_items = 0;
     bool wide = false;
     auto add = [&](uint32_t f, uint32_t row, uint64_t amount) {
@@ -1800,12 +1803,13 @@ __global__ void __launch_bounds__(kWindowThreads) bal_window_accumulate(
             window_field_add(B, row, f, amount, true);
         }
     };
-    auto item = [&](uint64_t x) {
+    auto item = [&](uint64_t x, uint32_t e) {
         if (x == ~0ull) return;
         n_items++;
         const uint32_t dr = uint32_t(x & rmask), cr = uint32_t((x >> ps) & rmask);
         const uint32_t pend = uint32_t(x >> (2 * ps)) & 1u;
-        const uint64_t amount = x >> (2 * ps + 1);
+        uint64_t amount = x >> (2 * ps + 1);
+        if (amount == amask) amount = wide_amounts[e];
         add(pend ? 2 : 0, dr, amount);
         add(pend ? 3 : 1, cr, amount);
     };
@@ -1818,13 +1822,13 @@ __global__ void __launch_bounds__(kWindowThreads) bal_window_accumulate(
         for (int j = 0; j < 4; j++) q[j] = *reinterpret_cast<const uint4*>(items + i + j * kStep);
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-            item((uint64_t(q[j].y) << 32) | q[j].x);
-            item((uint64_t(q[j].w) << 32) | q[j].z);
+            item((uint64_t(q[j].y) << 32) | q[j].x, i + j * kStep);
+            item((uint64_t(q[j].w) << 32) | q[j].z, i + j * kStep + 1);
         }
     }
     for (; i < b1; i += kStep) {
-        item(items[i]);
-        if (i + 1 < b1) item(items[i + 1]);
+        item(items[i], i);
+        if (i + 1 < b1) item(items[i + 1], i + 1);
     }
     if (__any(wide) && (threadIdx.x & 63) == 0) atomicOr(call_flags, kFlagWideSums);
     for (int off = 32; off > 0; off >>= 1) n_items += __shfl_xor(n_items, off);
