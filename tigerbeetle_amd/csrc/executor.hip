@@ -2085,7 +2085,9 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
     const BalTarget target{ctx->T.acc_rows, ctx->T.acc_index, ctx->T.acc_entry_of};
     if (!rc && use_window) {
         // Balance deltas: pair items summed per workgroup in LDS counters, partials applied.
-        const uint32_t nwg = std::max<uint32_t>(1, std::min<uint32_t>(kWindowGridMax, n / 8192));
+        // (even: a call with wide items pairs the workgroups, one per posted field and slice)
+        const uint32_t nwg =
+            std::max<uint32_t>(2, std::min<uint32_t>(kWindowGridMax, n / 8192)) & ~1u;
         const uint32_t wkeys = std::min<uint32_t>(kWindowKeys, 4u << pair_shift);
         hipLaunchKernelGGL(bal_window_accumulate, dim3(nwg), dim3(kWindowThreads), 0, ctx->stream,
                            target, ctx->bal_items, c.ev_amount, n, pair_shift, wkeys,

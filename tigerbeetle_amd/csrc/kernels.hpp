@@ -539,7 +539,7 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
                                             unsigned int* bucket_hist) {
     const EvNarrow tn = ev_narrow(t);
     bool imported = false, post_void = false, dup = false, closable = false, hot = false;
-    bool need_commit = false, chain_fast = false, ae_slow = false;
+    bool need_commit = false, chain_fast = false, ae_slow = false, wide_item = false;
     if (c.pnt_force) c.pnt_call[k] = 0;  // (sharded calls record every update: none yet)
     const uint16_t f = tn.flags();
     imported = (f & TB_TRANSFER_IMPORTED) != 0;
@@ -733,6 +733,7 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
             // which the AccountEvents window does not take)
             const bool packed = item_packable(c, amount);
             ae_slow |= !packed;
+            wide_item = !packed;
             c.bal_items[k] = ((packed ? amount : pair_amount_mask(ps)) << (2 * ps + 1)) |
                              (uint64_t(pending) << (2 * ps)) | (uint64_t(cr.row) << ps) | dr.row;
         } else if (c.bal_items) {
@@ -788,7 +789,7 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
     return (imported ? kFlagImported : 0u) | (post_void ? kFlagPostVoid : 0u) |
            (dup ? kFlagDuplicate : 0u) | (closable ? kFlagClosable : 0u) | (hot ? kFlagHot : 0u) |
            (need_commit ? kFlagNeedCommit : 0u) | (chain_fast ? kFlagChain : 0u) |
-           (ae_slow ? kFlagAeSlow : 0u);
+           (ae_slow ? kFlagAeSlow : 0u) | (wide_item ? kFlagWideItems : 0u);
 }
 
 // Per 64-event chunk of a create_transfers call (one lane each): the batch b0 of its first event,
@@ -1774,19 +1775,34 @@ __host__ __device__ inline uint32_t window_slice_per(uint32_t n, uint32_t nwg) {
 
 // (+ per workgroup: the count of its slice's items -- the created events of a call the
 // AccountEvents window takes -- and kFlagWideSums when a u32 window counter carried)
+// Calls with a wide item (kFlagWideItems: an amount too wide to pack, up to 2^64) take the wide
+// layout instead: workgroup 2 w + f sums slice w of the items into field f (0 debits_posted, 1
+// credits_posted) only, an amount's low and high 32 bits in two u32 LDS counters per account (the
+// same 128 KB; a low counter's wrap carries into the high one, a high counter's wrap -- 2^64 --
+// takes a global atomic), and writes both as partials. No AccountEvents window takes such a call.
+constexpr uint32_t kWindowHalf = kWindowKeys / 2;  // accounts per field in the wide layout
+
+// (+ per workgroup: the count of its slice's items -- the created events of a call the
+// AccountEvents window takes -- and kFlagWideSums when a u32 window counter carried)
 __global__ void __launch_bounds__(kWindowThreads) bal_window_accumulate(
     BalTarget B, const uint64_t* items, const uint64_t* wide_amounts, uint32_t n, uint32_t ps,
     uint32_t wkeys, uint32_t* partials, unsigned long long* carry, unsigned int* slice_count,
     unsigned int* call_flags) {
     __shared__ uint32_t acc[kWindowKeys];
     __shared__ uint32_t wave_items[kWindowThreads / 64];
-    for (uint32_t i = threadIdx.x; i < wkeys; i += kWindowThreads) acc[i] = 0;
+    const bool wide_layout = (*call_flags & kFlagWideItems) != 0;
+    for (uint32_t i = threadIdx.x; i < kWindowKeys; i += kWindowThreads) acc[i] = 0;
     __syncthreads();
-    const uint32_t per = window_slice_per(n, gridDim.x);
-    const uint32_t b0 = blockIdx.x * per;
+    const uint32_t slices = wide_layout ? (gridDim.x + 1) / 2 : gridDim.x;
+    const uint32_t w = wide_layout ? blockIdx.x >> 1 : blockIdx.x;
+    const uint32_t wf = blockIdx.x & 1;  // (wide layout: this workgroup's field)
+    const uint32_t per = window_slice_per(n, slices);
+    const uint32_t b0 = min(w * per, n);
     const uint32_t b1 = b0 + per < n ? b0 + per : n;
     const uint64_t rmask = (1ull << ps) - 1;
     const uint64_t amask = pair_amount_mask(ps);
+    uint32_t* lo_acc = acc;
+    uint32_t* hi_acc = acc + kWindowHalf;
     uint32_t n_items = 0;
     bool wide = false;
     auto add = [&](uint32_t f, uint32_t row, uint64_t amount) {
@@ -1803,6 +1819,16 @@ __global__ void __launch_bounds__(kWindowThreads) bal_window_accumulate(
             window_field_add(B, row, f, amount, true);
         }
     };
+    auto add_wide = [&](uint32_t row, uint64_t amount) {  // field wf, row < kWindowHalf
+        const uint32_t lo = uint32_t(amount);
+        const uint32_t old = atomicAdd(&lo_acc[row], lo);
+        const uint32_t hi = uint32_t(amount >> 32) + (uint32_t(old + lo) < old ? 1u : 0u);
+        if (hi) {
+            const uint32_t old_hi = atomicAdd(&hi_acc[row], hi);
+            if (uint32_t(old_hi + hi) < old_hi)  // (2^64)
+                atomicAdd(&carry[(wf << ps) | row], 1ull << 32);
+        }
+    };
     auto item = [&](uint64_t x, uint32_t e) {
         if (x == ~0ull) return;
         n_items++;
@@ -1810,6 +1836,11 @@ __global__ void __launch_bounds__(kWindowThreads) bal_window_accumulate(
         const uint32_t pend = uint32_t(x >> (2 * ps)) & 1u;
         uint64_t amount = x >> (2 * ps + 1);
         if (amount == amask) amount = wide_amounts[e];
+        if (wide_layout) {
+            if (pend) window_field_add(B, wf ? cr : dr, wf ? 3 : 2, amount, true);
+            else add_wide(wf ? cr : dr, amount);
+            return;
+        }
         add(pend ? 2 : 0, dr, amount);
         add(pend ? 3 : 1, cr, amount);
     };
@@ -1836,8 +1867,18 @@ __global__ void __launch_bounds__(kWindowThreads) bal_window_accumulate(
     __syncthreads();
     if (threadIdx.x == 0) {
         uint32_t t = 0;
-        for (uint32_t w = 0; w < kWindowThreads / 64; w++) t += wave_items[w];
+        for (uint32_t v = 0; v < kWindowThreads / 64; v++) t += wave_items[v];
         slice_count[blockIdx.x] = t;
+    }
+    if (wide_layout) {
+        // partials of workgroup g: [g][0, rows) low sums, [g][kWindowHalf, + rows) high sums
+        uint32_t* out = partials + uint64_t(blockIdx.x) * kWindowKeys;
+        const uint32_t rows = 1u << ps;
+        for (uint32_t k = threadIdx.x; k < rows; k += kWindowThreads) {
+            out[k] = lo_acc[k];
+            out[kWindowHalf + k] = hi_acc[k];
+        }
+        return;
     }
     uint32_t* out = partials + uint64_t(blockIdx.x) * wkeys;
     for (uint32_t k = threadIdx.x; k < wkeys; k += kWindowThreads) out[k] = acc[k];
@@ -1852,10 +1893,13 @@ __global__ void __launch_bounds__(kApplyThreads) bal_window_apply(
     BalTarget B, const uint32_t* partials, uint32_t nwg, uint32_t ps, uint32_t wkeys,
     uint64_t rows_used, unsigned long long* carry, unsigned int* call_flags) {
     __shared__ uint64_t part[kApplyThreads / 64][64];
+    __shared__ uint64_t part_hi[kApplyThreads / 64][64];
+    const bool wide_layout = (*call_flags & kFlagWideItems) != 0;
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t k = blockIdx.x * 64 + lane;
-    uint64_t s = 0;
-    if (k < wkeys) {
+    const uint32_t row = k & ((1u << ps) - 1), f = k >> ps;
+    uint64_t s = 0, sh = 0;
+    if (k < wkeys && !wide_layout) {
         uint32_t w = wv;
         for (; w + 3 * (kApplyThreads / 64) < nwg; w += 4 * (kApplyThreads / 64)) {
             uint32_t x[4];
@@ -1866,20 +1910,30 @@ __global__ void __launch_bounds__(kApplyThreads) bal_window_apply(
             for (int j = 0; j < 4; j++) s += x[j];
         }
         for (; w < nwg; w += kApplyThreads / 64) s += partials[uint64_t(w) * wkeys + k];
+    } else if (k < wkeys && f < 2) {
+        // (wide layout: the workgroups 2 w + f of field f, low and high sums; the pending fields
+        // took atomics)
+        for (uint32_t g = 2 * wv + f; g < nwg; g += 2 * (kApplyThreads / 64)) {
+            s += partials[uint64_t(g) * kWindowKeys + row];
+            sh += partials[uint64_t(g) * kWindowKeys + kWindowHalf + row];
+        }
     }
     part[wv][lane] = s;
+    part_hi[wv][lane] = sh;
     __syncthreads();
     if (wv != 0 || k >= wkeys) return;
-    for (uint32_t j = 1; j < kApplyThreads / 64; j++) s += part[j][lane];
-    const uint32_t row = k & ((1u << ps) - 1), f = k >> ps;
+    for (uint32_t j = 1; j < kApplyThreads / 64; j++) {
+        s += part[j][lane];
+        sh += part_hi[j][lane];
+    }
     if (row >= rows_used) return;
-    u128 sum = s;
+    u128 sum = u128(s) + (u128(sh) << 32);
     const unsigned long long c = carry[k];
     if (c) {
         sum += u128(c) << 32;
         carry[k] = 0;
     }
-    if (c || (s >> 32)) atomicOr(call_flags, kFlagWideSums);
+    if (c || (s >> 32) || sh) atomicOr(call_flags, kFlagWideSums);
     window_field_add(B, row, f, sum, false);
 }
 

@@ -52,6 +52,7 @@ enum : unsigned int {
     // single-phase FAST events with a pair item and whose window sums stay below 2^32.
     kFlagAeSlow = 1u << 10,    // a FAST event the AccountEvents window cannot take
     kFlagWideSums = 1u << 11,  // a window key's sum reached 2^32
+    kFlagWideItems = 1u << 12, // a pair item too wide to pack (the balance window's wide layout)
 };
 // Call flags under which tr_commit re-validates (and may demote) ingest's FAST events.
 constexpr unsigned int kCommitFlags = kFlagImported | kFlagPostVoid | kFlagDuplicate | kFlagHot |
