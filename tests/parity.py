@@ -73,7 +73,8 @@ class Pair:
         self.prepare_timestamp = 0
         self._pulse_delta = pulse_batch_max
         self.calls = 0
-        self.stats = {"events": 0, "fast": 0, "replayed": 0, "static_fail": 0, "ae_window": 0}
+        self.stats = {"events": 0, "fast": 0, "replayed": 0, "static_fail": 0, "ae_window": 0,
+                      "ingest_finished": 0}
         self.seconds = {"gpu": 0.0, "oracle": 0.0}  # wall time of each side's create_* calls
         self.pulses = []  # per tbg_pulse: (wall seconds, transfers expired)
 

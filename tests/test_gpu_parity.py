@@ -147,15 +147,18 @@ def test_uniform_config2_small():
         p.close()
 
 
-@pytest.mark.parametrize("spin", [True, False], ids=["spin", "stream-sync"])
-def test_many_small_registered_calls(spin, monkeypatch):
-    """The host's end-of-call wait: stage_out's last workgroup publishes a sequence word after every
-    workgroup's results and scalar words (each thread releases its stores at system scope). 300
-    small calls from a registered pool, each reply compared with the oracle as soon as the call
-    returns (Pair checks every result); TBG_NO_SPIN_SYNC (a stream synchronisation) is the
-    control."""
-    if not spin:
+@pytest.mark.parametrize("mode", ["spin", "stream-sync", "no-ingest-finish"])
+def test_many_small_registered_calls(mode, monkeypatch):
+    """The host's end-of-call wait: the last workgroup of tr_ingest (a call whose events are all
+    FAST) or of stage_out publishes a sequence word after every workgroup's results and scalar
+    words (each thread releases its stores at system scope). 300 small calls from a registered
+    pool, every third one clean, each reply compared with the oracle as soon as the call returns
+    (Pair checks every result); TBG_NO_SPIN_SYNC (a stream synchronisation) and
+    TBG_NO_INGEST_FINISH (stage_out ends every call) are the controls."""
+    if mode == "stream-sync":
         monkeypatch.setenv("TBG_NO_SPIN_SYNC", "1")
+    if mode == "no-ingest-finish":
+        monkeypatch.setenv("TBG_NO_INGEST_FINISH", "1")
     rng = np.random.default_rng(31)
     p = Pair(account_capacity=1 << 12, transfer_capacity=1 << 20, batch_events_max=8189,
              registered=True)
@@ -167,9 +170,15 @@ def test_many_small_registered_calls(spin, monkeypatch):
             n = int(rng.integers(1, 3000)) if call % 10 else 8189
             t = workload.transfers_uniform(n, n_acc, seed=call, id_offset=off)
             off += n
-            bad = rng.random(n) < 0.05
-            t["id"][bad] = 0
+            if call % 3:
+                bad = rng.random(n) < 0.05
+                t["id"][bad] = 0
             p.create_transfers(t, _split(n, rng, 8189))
+        # (every third call is clean: ~100 end in tr_ingest)
+        if mode == "no-ingest-finish":
+            assert p.stats["ingest_finished"] == 0
+        else:
+            assert p.stats["ingest_finished"] >= 90
         p.compare_state()
     finally:
         p.close()

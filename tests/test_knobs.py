@@ -5,7 +5,7 @@ another exact path or engine shape for the same results: the order-dependent wor
 3 and 4 (tests/configs34.py: limit accounts, pending / post / void, linked chains with injected
 failures) run under each setting and every result, row, TransferPending status and AccountEvent is
 compared with the oracle (parity.Pair). Knobs covered elsewhere: TBG_LANES_ONE_LANE and
-TBG_NO_PV_FAST (test_configs34.py), TBG_NO_SPIN_SYNC, TBG_NO_LEAN_LOOKUP, TBG_NO_WINDOW,
+TBG_NO_PV_FAST (test_configs34.py), TBG_NO_SPIN_SYNC, TBG_NO_INGEST_FINISH, TBG_NO_LEAN_LOOKUP, TBG_NO_WINDOW,
 TBG_NO_AE_WINDOW, TBG_WALK_SEQ, TBG_NO_ADDITIVE, TBG_NO_DOOM, TBG_NO_FREE_OWNERS
 (test_gpu_parity.py). Diagnostics that change no path: TBG_CALL_TIMEOUT_MS (the host's wait bound)
 and TBG_PULSE_HOST_TRACE (a printed trace).

@@ -71,7 +71,7 @@ struct FlowScratch {
     uint64_t slots = 0;        // grouping hash slots
     uint8_t *head8 = nullptr, *barrier8 = nullptr;
     uint32_t *heads = nullptr, *unit_of = nullptr, *barriers = nullptr, *vals = nullptr,
-             *vals_sorted = nullptr, *succ = nullptr, *indeg = nullptr;
+             *vals_sorted = nullptr, *succ = nullptr, *indeg = nullptr, *indeg0 = nullptr;
     uint64_t* keys_sorted = nullptr;
     Step* steps = nullptr;
     tb_transfer_t* evs = nullptr;  // per position: its event (flow_replay loads it with the step)
@@ -119,7 +119,7 @@ struct tbg_ctx {
     // last workgroup writes the call's sequence number into a pinned word (spin_wait).
     unsigned int* h_seq = nullptr;
     unsigned int* dh_seq = nullptr;
-    unsigned int* d_stage_done = nullptr;  // stage_out's finished workgroups
+    unsigned int* d_stage_done = nullptr;  // stage_out's finished workgroups; [1] tr_ingest's
     unsigned int seq = 0;
     bool spin_sync = false;
     double call_timeout_ms = 60000;  // spin_wait's bound (TBG_CALL_TIMEOUT_MS)
@@ -324,10 +324,8 @@ bool dev_alloc(tbg_ctx* ctx, T** p, uint64_t count, bool zero) {
     return true;
 }
 
-// One chained scan (prims.hpp): `n` items, the op's emits and total.
-template <typename Op>
-int launch_scan(tbg_ctx* ctx, uint64_t n, const Op& op) {
-    const uint64_t tiles = n ? (n + kScanTile - 1) / kScanTile : 1;
+// Tile words for `tiles` tiles and this launch's ScanState (prims.hpp).
+int scan_state(tbg_ctx* ctx, uint64_t tiles, ScanState* out) {
     if (tiles > 0xFFFFFFFFull) return TBG_EINVAL;
     if (!ctx->scan_ticket) HIP_TRY(ctx, hipMalloc(&ctx->scan_ticket, sizeof(unsigned int)));
     if (tiles > ctx->scan_tiles_cap) {
@@ -345,10 +343,32 @@ int launch_scan(tbg_ctx* ctx, uint64_t n, const Op& op) {
         ctx->scan_tiles_cap = cap;
     }
     ctx->scan_seq = ctx->scan_seq % ((1u << 30) - 1) + 1;
-    ScanState st{ctx->scan_status, ctx->scan_ticket, ctx->scan_ticket_base, ctx->scan_seq};
+    *out = ScanState{ctx->scan_status, ctx->scan_ticket, ctx->scan_ticket_base, ctx->scan_seq};
     ctx->scan_ticket_base += uint32_t(tiles);
+    return 0;
+}
+
+uint64_t scan_tiles(uint64_t n) { return n ? (n + kScanTile - 1) / kScanTile : 1; }
+
+// One chained scan (prims.hpp): `n` items, the op's emits and total.
+template <typename Op>
+int launch_scan(tbg_ctx* ctx, uint64_t n, const Op& op) {
+    const uint64_t tiles = scan_tiles(n);
+    ScanState st;
+    if (int rc = scan_state(ctx, tiles, &st)) return rc;
     hipLaunchKernelGGL(chained_scan<Op>, dim3(uint32_t(tiles)), dim3(kScanThreads), 0, ctx->stream,
                        n, op, st);
+    return 0;
+}
+
+// Two independent chained scans in one launch (chained_scan2).
+template <typename Op1, typename Op2>
+int launch_scan2(tbg_ctx* ctx, uint64_t n1, const Op1& op1, uint64_t n2, const Op2& op2) {
+    const uint64_t t1 = scan_tiles(n1), t2 = scan_tiles(n2);
+    ScanState st;
+    if (int rc = scan_state(ctx, t1 + t2, &st)) return rc;
+    hipLaunchKernelGGL((chained_scan2<Op1, Op2>), dim3(uint32_t(t1 + t2)), dim3(kScanThreads), 0,
+                       ctx->stream, n1, op1, n2, op2, uint32_t(t1), st);
     return 0;
 }
 
@@ -360,7 +380,7 @@ int select_flagged(tbg_ctx* ctx, const uint8_t* flags, uint64_t n, uint32_t* out
 
 int stage_call_outputs(tbg_ctx* ctx, const tb_create_result_t* d_results, tb_create_result_t* dst,
                        uint32_t n, bool scalars, const AeSnapJob* snap = nullptr,
-                       bool fixes = false, unsigned int seq = 0);
+                       bool fixes = false, unsigned int seq = 0, uint32_t skip_epoch = 0);
 // The scalars block to the host (a kernel writes the mapped pinned copy: no DMA hand-off).
 int sync_scalars(tbg_ctx* ctx) {
     int rc = stage_call_outputs(ctx, nullptr, nullptr, 0, true);
@@ -493,6 +513,11 @@ Call<Event> make_call(tbg_ctx* ctx, const Event* d_events, uint32_t n, const uin
     c.pv_slots = getenv("TBG_NO_PV_FAST") ? nullptr : ctx->pv_slots;
     c.pv_mask = ctx->pv_mask;
     c.pnt_force = ctx->pnt_sharded ? 1 : 0;
+    c.finish_done = nullptr;
+    c.finish_scalars = nullptr;
+    c.finish_results = nullptr;
+    c.finish_seq = nullptr;
+    c.seq = 0;
     return c;
 }
 
@@ -523,6 +548,7 @@ int end_call(tbg_ctx* ctx, uint32_t n, bool already_synced = false) {
     ctx->expiry_known = true;
     ctx->stats.events = n;
     ctx->stats.ae_window = 0;
+    ctx->stats.ingest_finished = (s.flags & kFlagFinished) ? 1 : 0;
     ctx->stats.fast = s.stats[1];
     ctx->stats.replayed = s.stats[2];
     ctx->stats.static_fail = s.stats[3];
@@ -543,14 +569,14 @@ int end_call(tbg_ctx* ctx, uint32_t n, bool already_synced = false) {
 
 void free_flow(FlowScratch& F) {
     void* ptrs[] = {F.head8, F.barrier8, F.heads, F.unit_of, F.barriers, F.vals, F.vals_sorted,
-                    F.succ, F.indeg, F.keys_sorted, F.steps, F.evs, F.queue,
+                    F.succ, F.indeg, F.indeg0, F.keys_sorted, F.steps, F.evs, F.queue,
                     F.outcome, F.recs, F.mailbox, F.owner_starts, F.mb_index, F.exp_flag,
                     F.hkeys, F.hcnt, F.hoff, F.loc, F.rank, F.big, F.chunk_seg, F.chunk_sum,
                     F.seg_done};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     F.head8 = F.barrier8 = F.outcome = nullptr;
-    F.heads = F.unit_of = F.barriers = F.vals = F.vals_sorted = F.succ = F.indeg = nullptr;
+    F.heads = F.unit_of = F.barriers = F.vals = F.vals_sorted = F.succ = F.indeg = F.indeg0 = nullptr;
     F.keys_sorted = nullptr;
     F.steps = nullptr;
     F.evs = nullptr;
@@ -588,7 +614,7 @@ int ensure_flow(tbg_ctx* ctx, uint64_t m) {
     const uint64_t slots = 2 * kc;  // grouping table load <= 0.5
     ok = dev_alloc(ctx, &F.head8, cap, false) && dev_alloc(ctx, &F.barrier8, cap, false) &&
          dev_alloc(ctx, &F.heads, cap, false) && dev_alloc(ctx, &F.unit_of, cap, false) &&
-         dev_alloc(ctx, &F.barriers, cap, false) && dev_alloc(ctx, &F.indeg, cap, true) &&
+         dev_alloc(ctx, &F.barriers, cap, false) && dev_alloc(ctx, &F.indeg, cap, true) && dev_alloc(ctx, &F.indeg0, cap, false) &&
          dev_alloc(ctx, &F.vals, kc, false) && dev_alloc(ctx, &F.vals_sorted, kc, false) &&
          dev_alloc(ctx, &F.succ, kc, false) && dev_alloc(ctx, &F.keys_sorted, kc, false) &&
          dev_alloc(ctx, &F.steps, cap, false) && dev_alloc(ctx, &F.evs, cap, false) &&
@@ -631,6 +657,7 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
     P.dup_mark = F.dup_mark;
     P.succ = F.succ;
     P.indeg = F.indeg;
+    P.indeg0 = F.indeg0;
     P.queue = F.queue;
     const bool post_void = (call_flags & kFlagPostVoid) != 0;
     P.pnt_ops = post_void || c.pnt_force ? c.pnt_call : nullptr;
@@ -652,7 +679,10 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
     P.doom_off = F.doom_off;
 
     GroupPlan G{};
-    G.hmask = F.slots - 1;
+    // The grouping table sized for this call (load <= 0.5 at kFlowKeys keys per event): a prefix
+    // of the allocation, which group_small leaves clear after every call.
+    const uint64_t slots = std::min<uint64_t>(F.slots, std::max<uint64_t>(next_pow2(2 * kFlowKeys * uint64_t(m)), 1u << 15));
+    G.hmask = slots - 1;
     G.hkeys = F.hkeys;
     G.hcnt = F.hcnt;
     G.hoff = F.hoff;
@@ -704,22 +734,23 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
                            call_flags);
     hipLaunchKernelGGL(plan_keys, dim3((m + kPlanThreads - 1) / kPlanThreads), dim3(kPlanThreads), 0,
                        ctx->stream, ctx->T, c, P, G, L, call_flags);
-    // the planned expires_at entries
-    rc = launch_scan(ctx, m,
-                     PlanExpiry{F.exp_flag, c.slow_list, ctx->T.expiry, ctx->T.expiry_capacity,
-                                c.row_base, &F.words[1],
-                                reinterpret_cast<unsigned long long*>(&ctx->T.scalars->expiry_count),
-                                &ctx->T.scalars->flags});
-    if (!rc) rc = launch_scan(ctx, F.slots, ExclusiveSumU32{F.hcnt, F.hoff, &F.counts[4]});
+    // the planned expires_at entries, and the slots' segments (one launch)
+    rc = launch_scan2(ctx, m,
+                      PlanExpiry{F.exp_flag, c.slow_list, ctx->T.expiry, ctx->T.expiry_capacity,
+                                 c.row_base, &F.words[1],
+                                 reinterpret_cast<unsigned long long*>(&ctx->T.scalars->expiry_count),
+                                 &ctx->T.scalars->flags},
+                      slots, ExclusiveSumU32{F.hcnt, F.hoff, &F.counts[4]});
     if (rc) return rc;
     hipLaunchKernelGGL(group_scatter, dim3(grid_for(pairs)), block, 0, ctx->stream, G, pairs);
-    hipLaunchKernelGGL(group_small, dim3(grid_for(F.slots)), block, 0, ctx->stream, ctx->T, G,
-                       F.slots);
+    hipLaunchKernelGGL(group_small, dim3(grid_for(slots)), block, 0, ctx->stream, ctx->T, G,
+                       slots);
     hipLaunchKernelGGL(group_sort, dim3(kGroupBigBlocks), dim3(kGroupBigThreads), 0, ctx->stream, G);
     hipLaunchKernelGGL(group_chunk, dim3(kGroupChunkBlocks), dim3(kGroupBigThreads), 0, ctx->stream,
                        ctx->T, G);
-    rc = launch_scan(ctx, m, SelectReady{F.indeg, F.counts, F.queue, F.engine, &F.counts[2]});
-    if (!rc) rc = select_flagged(ctx, F.barrier8, m, F.barriers, &F.counts[1]);
+    // the initially ready units, and the barrier events (one launch)
+    rc = launch_scan2(ctx, m, SelectReady{F.indeg, F.counts, F.queue, F.engine, &F.counts[2], F.indeg0}, m,
+                      SelectFlags8{F.barrier8, F.barriers, &F.counts[1]});
     if (rc) return rc;
     // Calls of limit events only: the account lanes (lanes.hpp); the flow replay then skips.
     P.skip = nullptr;
@@ -1688,13 +1719,14 @@ int spin_wait(tbg_ctx* ctx, unsigned int seq) {
 
 int stage_call_outputs(tbg_ctx* ctx, const tb_create_result_t* d_results, tb_create_result_t* dst,
                        uint32_t n, bool scalars, const AeSnapJob* snap, bool fixes,
-                       unsigned int seq) {
+                       unsigned int seq, uint32_t skip_epoch) {
     StageOut s{reinterpret_cast<const uint4*>(d_results), reinterpret_cast<uint4*>(dst), n,
                scalars ? reinterpret_cast<const unsigned long long*>(ctx->d_scalars) : nullptr,
                reinterpret_cast<unsigned long long*>(ctx->dh_scalars),
                uint32_t(sizeof(DevScalars) / 8), fixes ? ctx->fix_slots : nullptr,
                ctx->T.tr.slots, ctx->d_scalars, seq ? ctx->d_stage_done : nullptr,
-               seq ? ctx->dh_seq : nullptr, seq};
+               seq ? ctx->dh_seq : nullptr, seq,
+               skip_epoch ? ctx->d_stage_done + 2 : nullptr, skip_epoch};
     if (!dst || !n) s.src = nullptr;
     (void)snap;
     const uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>((n + kStageThreads - 1) / kStageThreads, 1024));
@@ -1852,7 +1884,8 @@ tbg_ctx* tbg_open(const tbg_options* options) {
     ok = ok && hip_ok(ctx, hipHostMalloc(reinterpret_cast<void**>(&ctx->h_seq), 64, kCoherentHost), "hipHostMalloc") &&
          hip_ok(ctx, hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->dh_seq), ctx->h_seq, 0),
                 "hipHostGetDevicePointer") &&
-         dev_alloc(ctx, &ctx->d_stage_done, 1, true);
+         // stage_out's and tr_ingest's finished workgroups, the epoch of the call tr_ingest ended
+         dev_alloc(ctx, &ctx->d_stage_done, 4, true);
     if (ok) *ctx->h_seq = 0;
     ctx->spin_sync = getenv("TBG_NO_SPIN_SYNC") == nullptr;
     if (const char* e = getenv("TBG_CALL_TIMEOUT_MS")) ctx->call_timeout_ms = std::max(1.0, atof(e));
@@ -2049,8 +2082,27 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
     const bool inline_chunks = (ctx->scalars_reset || ctx->scalars_clean) && n <= kInlineChunkMax;
     ctx->scalars_reset = false;
     ctx->scalars_clean = false;
+    // The call's outputs for the host: a host-buffer call's results go to mapped host memory (the
+    // registered destination, or the pinned staging); a spinning host waits for a sequence word.
+    tb_create_result_t* dst = nullptr;
+    if (ctx->early_dst) {
+        dst = mapped(ctx, ctx->early_dst, uint64_t(n) * 16);
+        if (!dst) dst = ctx->dh_results;
+    }
+    const bool spin = ctx->spin_sync && !ctx->timing;
+    const unsigned int seq = spin ? (++ctx->seq ? ctx->seq : ++ctx->seq) : 0u;
+    // A small call without balance items may end in its last tr_ingest workgroup (Call::
+    // finish_done); tr_commit and stage_out are queued all the same and return at once then.
+    const bool finish = inline_chunks && !use_sort && !getenv("TBG_NO_INGEST_FINISH");
     if (!rc && inline_chunks) {
         c.chunk_info = nullptr;
+        if (finish) {
+            c.finish_done = ctx->d_stage_done + 1;
+            c.finish_scalars = reinterpret_cast<unsigned long long*>(ctx->dh_scalars);
+            c.finish_results = dst;
+            c.finish_seq = seq ? ctx->dh_seq : nullptr;
+            c.seq = seq;
+        }
         Call<tb_transfer_t> ci = c;
         if (ctx->events_host) {
             ci.events = ctx->events_host;
@@ -2134,15 +2186,9 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
     // the accounts' timestamp index)? One kernel writes the scalars and, for a host-buffer call,
     // its results to mapped host memory (the registered destination, or the pinned staging).
     if (!rc) {
-        tb_create_result_t* dst = nullptr;
-        if (ctx->early_dst) {
-            dst = mapped(ctx, ctx->early_dst, uint64_t(n) * 16);
-            if (!dst) dst = ctx->dh_results;
-        }
         const bool snap = ae_async_ok(ctx, n);
-        const bool spin = ctx->spin_sync && !ctx->timing;
-        const unsigned int seq = spin ? (++ctx->seq ? ctx->seq : ++ctx->seq) : 0u;
-        rc = stage_call_outputs(ctx, d_results, dst, dst ? n : 0, true, nullptr, true, seq);
+        rc = stage_call_outputs(ctx, d_results, dst, dst ? n : 0, true, nullptr, true, seq,
+                                finish ? c.epoch : 0u);
         // A small call's AccountEvents snapshot follows stage_out (the host's wait ends at
         // stage_out): final unless a replay follows, then it stages nothing. Its appends are queued
         // on the side stream now, so that the host's launch calls overlap the call's kernels.
@@ -2191,7 +2237,9 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
         rc = ae_transfers(ctx, c);
         hprof(ctx, "host:account_events", now_ms() - ta);
     }
-    if (!rc) {
+    if (!rc && (ctx->h_scalars->flags & kFlagFinished)) {
+        ctx->scalars_clean = true;  // (tr_ingest's last workgroup cleared them)
+    } else if (!rc) {
         hipLaunchKernelGGL(tr_reset_scalars, dim3(1), dim3(64), 0, ctx->stream, ctx->d_scalars);
         ctx->scalars_clean = hip_ok(ctx, hipGetLastError(), "reset");
     }

@@ -66,6 +66,7 @@ struct FlowPlan {
     uint32_t* dup_mark;          // per event of the call: an in-call holder with later claimants
     uint32_t* succ;              // kFlowKeys per position: successor unit or kNone32
     uint32_t* indeg;             // per unit: predecessors not yet finished
+    const uint32_t* indeg0;      // per unit: its predecessors (edges) at the start (SelectReady)
     uint32_t* queue;             // ready units (unit + 1; 0 = not yet pushed)
     uint64_t* pnt_ops;           // post/void calls: Call::pnt_call (per event), else null
     UndoEntry* lane_undo;        // kFlowUndoPerLane per lane
@@ -272,10 +273,31 @@ __global__ void __launch_bounds__(kFlowThreads) flow_replay(Tables T, Call<tb_tr
         // Release: this unit's writes reach the point of coherence before any decrement. A unit
         // without successors skips it (the L2 write-back is the costliest step of a short unit,
         // and nothing in this kernel reads what it wrote; the kernel's end releases it).
-        bool any_succ = false;
+        bool any_succ = false, several = false;
+        uint32_t only = kNone32, edges = 0;
         for (uint32_t s = begin; s < end; s++) {
             const uint4 sc = *reinterpret_cast<const uint4*>(P.succ + kFlowKeys * uint64_t(s));
             any_succ |= (sc.x & sc.y & sc.z & sc.w) != kNone32;
+            const uint32_t vs[kFlowKeys] = {sc.x, sc.y, sc.z, sc.w};
+#pragma unroll
+            for (uint32_t q = 0; q < kFlowKeys; q++) {
+                if (vs[q] == kNone32) continue;
+                if (only == kNone32) only = vs[q];
+                if (vs[q] == only) edges++;
+                else several = true;
+            }
+        }
+        // A private hand-off: every edge into the one successor v comes from this unit (its
+        // in-degree at the start is this unit's edges to it), so no other lane waits on v or on
+        // this unit's writes before v has run. This lane runs v next with no release, decrement or
+        // acquire: v reads this unit's writes through the lane's own CU and XCD L2, and v's own
+        // release (or the kernel's end) publishes both units' writes to their later readers, all
+        // of which follow v. (v's in-degree word is reset for the next call's plan.)
+        if (any_succ && !several && P.indeg0[only] == edges) {
+            P.indeg[only] = 0;
+            __hip_atomic_fetch_add(done_shard, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            conts++;
+            return only;
         }
         uint32_t next = kNone32;
         bool pushed = false;

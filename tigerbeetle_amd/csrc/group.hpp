@@ -110,6 +110,44 @@ __device__ inline void group_slot2(const GroupPlan& G, uint64_t key0, uint64_t k
     else *s1 = (w1 == 0 || w1 == tag1) ? uint32_t(h1) : group_slot(G, key1);
 }
 
+// The slots of up to kFlowKeys keys (kFlowNoKey: none): every home word is read, and every empty
+// one claimed, before any result is waited on -- one or two round trips for the event instead of
+// one per key; equal keys share the first one's slot, collisions continue in group_slot.
+template <uint32_t N>
+__device__ inline void group_slots(const GroupPlan& G, const uint64_t (&key)[N], uint64_t none,
+                                   uint32_t (&slot)[N]) {
+    uint64_t h[N];
+    unsigned long long w[N];
+#pragma unroll
+    for (uint32_t j = 0; j < N; j++) {
+        h[j] = group_hash(key[j]) & G.hmask;
+        w[j] = key[j] != none ? G.hkeys[h[j]] : 1ull;
+    }
+    bool same[N];
+#pragma unroll
+    for (uint32_t j = 0; j < N; j++) {
+        same[j] = false;
+#pragma unroll
+        for (uint32_t i = 0; i < j; i++) same[j] |= key[i] == key[j];
+        if (key[j] != none && !same[j] && w[j] == 0)
+            w[j] = atomicCAS(&G.hkeys[h[j]], 0ull, (unsigned long long)(key[j] + 1));
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < N; j++) {
+        slot[j] = kNone32;
+        if (key[j] == none) continue;
+        if (same[j]) {
+            for (uint32_t i = 0; i < j; i++)
+                if (key[i] == key[j]) {
+                    slot[j] = slot[i];
+                    break;
+                }
+            continue;
+        }
+        slot[j] = (w[j] == 0 || w[j] == key[j] + 1) ? uint32_t(h[j]) : group_slot(G, key[j]);
+    }
+}
+
 // Counting keys by slot within one workgroup (kPlanThreads lanes): each lane inserts its keys
 // (group_slot) and counts them in an LDS table of the workgroup's slots; then one global add per
 // slot turns the LDS counts into bases, and every pair gets its slot and rank. All lanes call the
@@ -394,10 +432,12 @@ __global__ void __launch_bounds__(kPlanThreads) plan_keys(Tables T, Call<tb_tran
                 L.recs[s] = r;
             }
         }
-        // Grouping: the global slot, then this workgroup's count of the slot in LDS.
+        // Grouping: the global slots, then this workgroup's count of each slot in LDS.
+        uint32_t gs[kFlowKeys];
+        group_slots(G, key, kFlowNoKey, gs);
 #pragma unroll
         for (uint32_t j = 0; j < kFlowKeys; j++)
-            if (key[j] != kFlowNoKey) local[j] = group_block_add(G, B, key[j], &lrank[j]);
+            if (key[j] != kFlowNoKey) local[j] = group_block_count(B, gs[j], &lrank[j]);
     }
     if (G.lanes) {
         const uint64_t bad = __ballot(ineligible);
@@ -848,11 +888,16 @@ struct SelectReady {
     uint32_t* queue;
     unsigned int* engine;
     unsigned int* ready_count;
+    uint32_t* indeg0;            // the in-degrees' copy (FlowPlan::indeg0)
     __device__ void load(uint64_t base, uint64_t n, uint32_t* c) const {
         const uint32_t units = counts[0];
 #pragma unroll
-        for (uint32_t i = 0; i < kScanItems; i++)
-            c[i] = base + i < n && base + i < units && indeg[base + i] == 0;
+        for (uint32_t i = 0; i < kScanItems; i++) {
+            const bool unit = base + i < n && base + i < units;
+            const uint32_t d = unit ? indeg[base + i] : 1u;
+            if (unit) indeg0[base + i] = d;
+            c[i] = d == 0;
+        }
     }
     __device__ void emit(uint64_t u, uint32_t p) const { queue[p] = uint32_t(u) + 1; }
     __device__ void total(uint32_t t) const {

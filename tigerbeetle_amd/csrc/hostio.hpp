@@ -71,6 +71,10 @@ struct StageOut {
     unsigned int* done;
     unsigned int* host_seq;
     unsigned int seq;
+    // When *finished == finished_epoch (tr_ingest ended the call: Call::finish_done) the kernel
+    // returns at once. Null: never.
+    const unsigned int* finished;
+    unsigned int finished_epoch;
 };
 
 // (A small call's AccountEvents staging follows in its own kernel, ae_snapshot: the host's wait
@@ -86,6 +90,7 @@ __global__ void host_signal(unsigned int* host_seq, unsigned int seq) {
 
 __global__ void __launch_bounds__(kStageThreads) stage_out(StageOut s) {
     const uint32_t tid = blockIdx.x * kStageThreads + threadIdx.x;
+    if (s.finished && *s.finished == s.finished_epoch) return;
     if (s.fix_slots) {
         const uint64_t nfix = s.scalars->fixed;
         for (uint64_t i = tid; i < nfix; i += uint64_t(gridDim.x) * kStageThreads)

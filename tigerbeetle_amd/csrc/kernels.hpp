@@ -45,6 +45,9 @@
 #ifndef TBG_INGEST_JOINT_PROBE
 #define TBG_INGEST_JOINT_PROBE 1
 #endif
+#ifndef TBG_INGEST_HOST_HALVES
+#define TBG_INGEST_HOST_HALVES 0  // a body read from host memory: two waves of 4 loads a lane
+#endif
 #ifndef TBG_INGEST_PREV_SHFL
 #define TBG_INGEST_PREV_SHFL 1  // the previous event's flags by a lane shuffle (tr_ingest)
 #endif
@@ -839,6 +842,71 @@ __global__ void tr_chunk_info(Call<tb_transfer_t> c, uint4* out, DevScalars* sca
     out[i] = chunk_info_of(c, base);
 }
 
+// The end of a small call by tr_ingest's last workgroup (Call::finish_done), when no event raised a
+// commit flag: what tr_commit's clean branch, stage_out and tr_reset_scalars would do, two launches
+// earlier. A workgroup is counted after its stores are released: with results for the host every
+// thread releases at system scope (mapped host memory, as in stage_out); else every wave waits for
+// its stores and lane 0 releases at agent scope (MI355X_MICROARCH.md, inter-workgroup visibility).
+// The last workgroup acquires, sums the call's counters, copies the scalars block to its mapped
+// copy, clears the call's scalar words for the next call, marks the call finished for the queued
+// tr_commit and stage_out (finish_done[1] = epoch: they return at once), and then publishes the
+// sequence word.
+__device__ inline void ingest_finish(const Tables& T, const Call<tb_transfer_t>& c) {
+    __shared__ unsigned int last;  // 0: not the last workgroup; else the call's flags | 1 << 31
+    DevScalars* S = T.scalars;
+    if (c.finish_results) {
+        // The wave's results to the host (the lane re-reads what it wrote; final if the call
+        // finishes here, else stage_out writes them all again).
+        const uint32_t waves = blockDim.x / 64, nw = gridDim.x * waves;
+        for (uint32_t k = (blockIdx.x * waves + (threadIdx.x >> 6)) * 64 + (threadIdx.x & 63);
+             k < c.n; k += nw * 64)
+            c.finish_results[k] = c.results[k];
+        __threadfence_system();
+    } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (!c.finish_results) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        last = 0;
+        if (atomicAdd(c.finish_done, 1u) == gridDim.x - 1) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            atomicExch(c.finish_done, 0u);
+            last = __hip_atomic_load(&S->flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) | (1u << 31);
+        }
+    }
+    __syncthreads();
+    const unsigned int flags = last;
+    // (tr_commit and stage_out end a call with a commit flag)
+    if (!(flags >> 31) || (flags & kCommitFlags)) return;
+    auto load = [](const unsigned long long* p) {
+        return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    if (threadIdx.x == 0) {
+        // tr_commit's clean branch: transfers key_range and the FAST count
+        const unsigned long long ts = load(&S->spec_ts_max);
+        if (ts > load(&S->transfers_key_max)) atomicMax(&S->transfers_key_max, ts);
+        atomicAdd(&S->stats[1], load(&S->spec_fast));
+        atomicOr(&S->flags, kFlagFinished);
+        c.finish_done[1] = c.epoch;
+        __threadfence();
+    }
+    __syncthreads();
+    const uint32_t words = uint32_t(sizeof(DevScalars) / 8);
+    const unsigned long long* src = reinterpret_cast<const unsigned long long*>(S);
+    for (uint32_t w = threadIdx.x; w < words; w += blockDim.x) c.finish_scalars[w] = load(src + w);
+    __syncthreads();  // (every word is read before the call's words are cleared)
+    if (threadIdx.x == 0) reset_call_scalars(S);
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0 && c.finish_seq)
+        __hip_atomic_store(c.finish_seq, c.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // LDS image of a wave's 64 events: 144 bytes per event (128 + 16 of padding), so the lanes'
 // 16-byte field reads (one event per lane) fall on distinct banks.
 constexpr uint32_t kLdsEventStride = 144;
@@ -876,6 +944,10 @@ __global__ void __launch_bounds__(kBlock, TBG_INGEST_WG_PER_CU) tr_ingest(Tables
         const uint32_t parts = (c.n - base < 64 ? c.n - base : 64) * 8;
 #pragma unroll
         for (int i = 0; i < 8; i++) {
+#if TBG_INGEST_HOST_HALVES
+            // (PCIe reads peak with fewer requests in flight: tools/pciebench.hip)
+            if (i == 4 && c.events_out) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
             const uint32_t idx = i * 64 + lane;
 #if TBG_INGEST_NT_LOADS
             typedef unsigned int v4u __attribute__((ext_vector_type(4)));
@@ -1028,6 +1100,7 @@ __global__ void __launch_bounds__(kBlock, TBG_INGEST_WG_PER_CU) tr_ingest(Tables
         if (n_fast) atomicAdd(&T.scalars->spec_fast, (unsigned long long)n_fast);
         if (ts_max) atomicMax(&T.scalars->spec_ts_max, (unsigned long long)ts_max);
     }
+    if (c.finish_done) ingest_finish(T, c);
 }
 
 
@@ -1592,6 +1665,7 @@ __global__ void tr_chain_planes(Tables T, Call<tb_transfer_t> c) {
 // effects ingest already wrote; only the call's counters remain (from ingest's speculative
 // ones). Otherwise every event is re-validated.
 __global__ void tr_commit(Tables T, Call<tb_transfer_t> c) {
+    if (c.finish_done && c.finish_done[1] == c.epoch) return;  // (tr_ingest ended the call)
     const unsigned int call_flags = T.scalars->flags;
     if (!(call_flags & kCommitFlags)) {
         if (blockIdx.x == 0 && threadIdx.x == 0) {

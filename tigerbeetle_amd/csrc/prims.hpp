@@ -62,15 +62,14 @@ __device__ inline uint32_t wave_inclusive_u32(uint32_t v, uint32_t lane) {
     return v;
 }
 
+// One tile of a chained scan: `status` the scan's tile words, `tile` its tile (by ticket).
 template <typename Op>
-__global__ void __launch_bounds__(kScanThreads) chained_scan(uint64_t n, Op op, ScanState st) {
-    __shared__ uint32_t s_tile, s_prefix;
+__device__ inline void scan_tile(uint64_t n, const Op& op, unsigned long long* status, uint32_t seq,
+                                 uint32_t tile) {
+    __shared__ uint32_t s_prefix;
     __shared__ uint32_t s_wave[kScanThreads / 64];
-    if (st.skip && *st.skip == st.skip_if) return;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if (tid == 0) s_tile = atomicAdd(st.ticket, 1u) - st.ticket_base;
-    __syncthreads();
-    const uint32_t tile = s_tile;
+    ScanState st{status, nullptr, 0, seq};
     const uint64_t base = uint64_t(tile) * kScanTile + uint64_t(tid) * kScanItems;
     uint32_t c[kScanItems];
     op.load(base, n, c);
@@ -136,6 +135,30 @@ __global__ void __launch_bounds__(kScanThreads) chained_scan(uint64_t n, Op op, 
     }
     const uint64_t tiles = n ? (n + kScanTile - 1) / kScanTile : 1;
     if (tid == 0 && tile == tiles - 1) op.total(s_prefix + agg);
+}
+
+template <typename Op>
+__global__ void __launch_bounds__(kScanThreads) chained_scan(uint64_t n, Op op, ScanState st) {
+    __shared__ uint32_t s_tile;
+    if (st.skip && *st.skip == st.skip_if) return;
+    if (threadIdx.x == 0) s_tile = atomicAdd(st.ticket, 1u) - st.ticket_base;
+    __syncthreads();
+    scan_tile(n, op, st.status, st.seq, s_tile);
+}
+
+// Two independent scans in one launch: tickets [0, tiles1) are the first scan's tiles, the rest
+// the second's (its tile words follow the first's). A tile waits only on earlier tiles of its own
+// scan, which hold earlier tickets: the look-back progresses as in chained_scan.
+template <typename Op1, typename Op2>
+__global__ void __launch_bounds__(kScanThreads) chained_scan2(uint64_t n1, Op1 op1, uint64_t n2,
+                                                              Op2 op2, uint32_t tiles1,
+                                                              ScanState st) {
+    __shared__ uint32_t s_tile;
+    if (threadIdx.x == 0) s_tile = atomicAdd(st.ticket, 1u) - st.ticket_base;
+    __syncthreads();
+    const uint32_t t = s_tile;
+    if (t < tiles1) scan_tile(n1, op1, st.status, st.seq, t);
+    else scan_tile(n2, op2, st.status + tiles1, st.seq, t - tiles1);
 }
 
 // ---- workgroup sort in registers -----------------------------------------------------------------

@@ -53,6 +53,7 @@ enum : unsigned int {
     kFlagAeSlow = 1u << 10,    // a FAST event the AccountEvents window cannot take
     kFlagWideSums = 1u << 11,  // a window key's sum reached 2^32
     kFlagWideItems = 1u << 12, // a pair item too wide to pack (the balance window's wide layout)
+    kFlagFinished = 1u << 13,  // tr_ingest ended the call (Call::finish_done)
 };
 // Call flags under which tr_commit re-validates (and may demote) ingest's FAST events.
 constexpr unsigned int kCommitFlags = kFlagImported | kFlagPostVoid | kFlagDuplicate | kFlagHot |
@@ -171,6 +172,16 @@ struct Call {
     // words of other epochs are free): the earliest post/void of a pending transfer in the call.
     unsigned long long* pv_slots;
     uint64_t pv_mask;
+    // Small calls without balance items: the last tr_ingest workgroup to finish ends a call that
+    // raised no commit flag (every event FAST, its effects all written) -- the call's counters,
+    // the scalars block to its mapped copy, the sequence word for a spinning host -- and sets
+    // kFlagFinished, on which tr_commit and stage_out return at once. Its FAST results also go
+    // to the mapped host destination as they are made. finish_done = null: no such ending.
+    unsigned int* finish_done;       // ingest's finished workgroups (zero between calls)
+    unsigned long long* finish_scalars;  // mapped pinned copy of the scalars block
+    tb_create_result_t* finish_results;  // mapped host destination of the results, or null
+    unsigned int* finish_seq;        // the pinned sequence word, or null (the host synchronises)
+    unsigned int seq;
 };
 
 constexpr uint32_t kNone32 = 0xFFFFFFFFu;

@@ -45,6 +45,7 @@ class TbgStats(ctypes.Structure):
         ("replayed", ctypes.c_uint64),
         ("static_fail", ctypes.c_uint64),
         ("ae_window", ctypes.c_uint64),
+        ("ingest_finished", ctypes.c_uint64),
     ]
 
 
