@@ -773,3 +773,78 @@ def test_local_shards_gpu_cross_shard(seed):
         for s in shards:
             s.close()
         ref.close()
+
+
+def window_scenario(seed, n=150_000, n_acc=2_000):
+    """Large sharded calls (each shard's part >= 65,536 events over <= 2^14 accounts: the balance
+    window path, pnt_resolve on every sharded call): plain transfers (the one-pass AccountEvents
+    window), then a call with timed pending transfers (their pulse_next_timestamp minimums resolved
+    across shards; AccountEvents from the general path), then plain transfers again, with ticks so
+    that pulses expire some of the pending ones."""
+    rng = np.random.default_rng(seed)
+    acc = workload.accounts(n_acc, seed=seed)
+    ids = np.arange(1, n_acc + 1)
+    acc["ledger"] = 1 + (ids - 1) % LEDGERS
+    acc["flags"] = 0
+    pools = {lg: ids[acc["ledger"] == lg] for lg in range(1, LEDGERS + 1)}
+    ops = [("accounts", acc, [n_acc])]
+    next_id = 10_000_000
+    for c, pending in enumerate((0.0, 0.2, 0.0)):
+        t = np.zeros(n, dtype=TRANSFER_DTYPE)
+        ledger = rng.integers(1, LEDGERS + 1, size=n)
+        for lg in range(1, LEDGERS + 1):
+            sel = np.nonzero(ledger == lg)[0]
+            pair = rng.choice(len(pools[lg]), size=(len(sel), 2))
+            pair[:, 1] = (pair[:, 0] + 1 + pair[:, 1] % (len(pools[lg]) - 1)) % len(pools[lg])
+            t["debit_account_id"][sel, 0] = pools[lg][pair[:, 0]]
+            t["credit_account_id"][sel, 0] = pools[lg][pair[:, 1]]
+        t["id"][:, 0] = next_id + np.arange(n)
+        next_id += n
+        t["amount"][:, 0] = rng.integers(1, 1_000, size=n)
+        t["ledger"] = ledger
+        t["code"] = 1
+        if pending:
+            p = rng.random(n) < pending
+            t["flags"][p] = 2
+            t["timeout"][p] = rng.integers(1, 4, size=int(p.sum()))
+        ops.append(("transfers", t, [8189] * (n // 8189) + ([n % 8189] if n % 8189 else [])))
+        ops.append(("tick", 2 * NS_PER_S))
+    return ops
+
+
+@pytest.mark.gpu
+def test_local_shards_gpu_window_calls():
+    """window_scenario through two HBM executors: every shard's part of a call takes the balance
+    window and pnt_resolve (sharded calls record every pulse_next_timestamp update); results,
+    tables and AccountEvents against the unsharded oracle (pnt_resolve's scratch must
+    not be the balance items the AccountEvents window reads)."""
+    shards = [shard.GpuShard(1 << 12, 1 << 19, batch_events_max=1 << 18,
+                             account_events_capacity=1 << 20) for _ in range(2)]
+    ref = OracleShard()
+    try:
+        cluster = shard.LocalShards(shard.LedgerRouter(2, ledgers=LEDGERS), shards, PBM)
+        drive(cluster, ref, window_scenario(3))
+        assert_same_state([s.dump() for s in shards], ref,
+                          [s.dump_account_events() for s in shards])
+    finally:
+        for s in shards:
+            s.close()
+        ref.close()
+
+
+def test_local_shards_batch_cap():
+    """A shard's runs of a call whose ledgers interleave event by event become many short batches:
+    the engine splits them over sub-calls of at most max_batches batches (the executors'
+    batch_count_max), results and state unchanged."""
+    shards = [OracleShard() for _ in range(2)]
+    ref = OracleShard()
+    try:
+        cluster = shard.LocalShards(shard.LedgerRouter(2, ledgers=LEDGERS), shards, PBM)
+        cluster.engine.max_batches = 64
+        drive(cluster, ref, window_scenario(4, n=20_000, n_acc=200))
+        assert_same_state([s.dump() for s in shards], ref,
+                          [s.dump_account_events() for s in shards])
+    finally:
+        for s in shards:
+            s.close()
+        ref.close()

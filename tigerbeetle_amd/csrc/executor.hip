@@ -701,6 +701,7 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
     G.indeg = F.indeg;
     G.lanes = lanes_possible;
     G.free_owners = getenv("TBG_NO_FREE_OWNERS") == nullptr;
+    G.stats = getenv("TBG_FLOW_DEBUG") != nullptr;
     G.epoch = c.epoch;
     G.owner_starts = F.owner_starts;
     G.lane_counts = F.lane_counts;

@@ -70,6 +70,7 @@ struct GroupPlan {
     // account lanes (lanes.hpp): owner segments and free owners; lanes == false: none
     bool lanes;
     bool free_owners;               // free-owner verdicts (TBG_NO_FREE_OWNERS: none)
+    bool stats;                     // counts[2] / [3] (TBG_FLOW_DEBUG)
     uint32_t epoch;
     uint32_t* owner_starts;
     unsigned int* lane_counts;      // [0] owners, [1] ineligible events
@@ -576,7 +577,11 @@ __device__ inline void segment_sort(const uint32_t* in, uint32_t* out, uint32_t 
     // sort of the next power of two >= c (kNone32 padding), when it fits the buffer.
     uint32_t pw = 1;
     while (pw < c) pw <<= 1;
-    if (pw <= kGroupLdsWords && (values || uint64_t(hi - lo) + 1 > 64ull * pw)) {
+    // (A range within one bitmap window takes the bitmap whatever its density: clearing, setting,
+    // counting and enumerating 2^20 bits costs a few microseconds, an LDS bitonic sort of 32k
+    // values ~40 -- config 3's hot accounts.)
+    const uint64_t range = uint64_t(hi - lo) + 1;
+    if (pw <= kGroupLdsWords && (values || (range > kGroupWindowBits && range > 64ull * pw))) {
         for (uint32_t i = tid; i < pw; i += kGroupBigThreads) buf[i] = i < c ? in[off + i] : kNone32;
         __syncthreads();
         for (uint32_t size = 2; size <= pw; size <<= 1) {
@@ -709,7 +714,7 @@ __global__ void __launch_bounds__(kBlock) group_small(Tables T, GroupPlan G, uin
             G.hcnt[h] = 0;
         }
     }
-    {  // the longest id-key / account-key segment (flow debug statistics): one atomic per wave
+    if (G.stats) {  // the longest id-key / account-key segment (flow debug): one atomic per wave
         uint32_t id_max = (c > 1 && (key >> 32) == 0) ? c : 0u;
         uint32_t acc_max = (c > 1 && (key >> 32) == 1) ? c : 0u;
         for (int d = 32; d >= 1; d >>= 1) {

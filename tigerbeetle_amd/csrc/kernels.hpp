@@ -45,9 +45,6 @@
 #ifndef TBG_INGEST_JOINT_PROBE
 #define TBG_INGEST_JOINT_PROBE 1
 #endif
-#ifndef TBG_INGEST_HOST_HALVES
-#define TBG_INGEST_HOST_HALVES 0  // a body read from host memory: two waves of 4 loads a lane
-#endif
 #ifndef TBG_INGEST_PREV_SHFL
 #define TBG_INGEST_PREV_SHFL 1  // the previous event's flags by a lane shuffle (tr_ingest)
 #endif
@@ -944,10 +941,9 @@ __global__ void __launch_bounds__(kBlock, TBG_INGEST_WG_PER_CU) tr_ingest(Tables
         const uint32_t parts = (c.n - base < 64 ? c.n - base : 64) * 8;
 #pragma unroll
         for (int i = 0; i < 8; i++) {
-#if TBG_INGEST_HOST_HALVES
-            // (PCIe reads peak with fewer requests in flight: tools/pciebench.hip)
+            // A body read from host memory: two rounds of 4 loads a lane (PCIe reads peak with
+            // fewer requests in flight, tools/pciebench.hip; 77 -> 73 us a commit, r05_h A/B).
             if (i == 4 && c.events_out) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
             const uint32_t idx = i * 64 + lane;
 #if TBG_INGEST_NT_LOADS
             typedef unsigned int v4u __attribute__((ext_vector_type(4)));

@@ -631,9 +631,12 @@ class Engine:
     """Executes a call across shards exactly (module doc). `ops` is the shard group: LocalShards
     (all shards in this process) or ShardGroup (one per rank, run from rank 0)."""
 
-    def __init__(self, router: LedgerRouter, ops):
+    def __init__(self, router: LedgerRouter, ops, max_batches: int = 4096):
         self.router = router
         self.ops = ops
+        # Batches per "batches" sub-call (the executors' batch_count_max): a shard's runs of a
+        # call whose ledgers interleave event by event are many short batches.
+        self.max_batches = max_batches
         self.segments = 0       # statistics: segments executed, of them chains across shards
         self.chain_segments = 0
 
@@ -755,6 +758,8 @@ class Engine:
                     j = k
                     while j < hi and seg.shard_of[j] == s:
                         j += 1
+                    if pending[s] is not None and len(pending[s][1]) >= self.max_batches:
+                        flush(s)  # (a sub-call holds at most the executor's batch_count_max)
                     if pending[s] is None:
                         pending[s] = ([], [], [])
                     pending[s][0].extend(range(k, j))
