@@ -32,11 +32,47 @@ class ParityError(AssertionError):
     pass
 
 
+class _DeviceBuffers:
+    """hipMalloc'd body / batch bounds / results for Pair(device_calls=True)."""
+
+    def __init__(self, events_max, batches_max):
+        self.hip = ctypes.CDLL("libamdhip64.so")
+        self.hip.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
+        self.hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                       ctypes.c_int]
+        self.hip.hipFree.argtypes = [ctypes.c_void_p]
+        self.hip.hipDeviceSynchronize.argtypes = []
+        self.ev = self._alloc(events_max * 128)
+        self.res = self._alloc(events_max * 16)
+        self.ends = self._alloc(batches_max * 4)
+        self.ts = self._alloc(batches_max * 8)
+
+    def _alloc(self, nbytes):
+        p = ctypes.c_void_p()
+        assert self.hip.hipMalloc(ctypes.byref(p), nbytes) == 0, "hipMalloc"
+        return p
+
+    def put(self, p, a):
+        # (the previous call's queued work -- AccountEvents appends read its body -- has finished:
+        # the device call's contract is the stream's order)
+        assert self.hip.hipDeviceSynchronize() == 0
+        a = np.ascontiguousarray(a)
+        assert self.hip.hipMemcpy(p, a.ctypes.data_as(ctypes.c_void_p), a.nbytes, 1) == 0
+
+    def get(self, p, a):
+        assert self.hip.hipDeviceSynchronize() == 0
+        assert self.hip.hipMemcpy(a.ctypes.data_as(ctypes.c_void_p), p, a.nbytes, 2) == 0
+
+    def free(self):
+        for p in (self.ev, self.res, self.ends, self.ts):
+            self.hip.hipFree(p)
+
+
 class Pair:
     def __init__(self, account_capacity=1 << 16, transfer_capacity=1 << 20,
                  batch_events_max=1 << 16, batch_count_max=4096, pulse_batch_max=8190,
                  pulse_next_timestamp_init=TIMESTAMP_MAX, force_replay=False, device=0,
-                 account_events=True, registered=False):
+                 account_events=True, registered=False, device_calls=False):
         self.lib = native.load()
         self.olib = oracle_binding.load()
         o = native.TbgOptions()
@@ -69,6 +105,9 @@ class Pair:
             assert self.lib.tbg_register_host(self.g, self._pool.ctypes.data,
                                               self._pool.nbytes) == 0
             self._pool_results = ev_bytes
+        # device_calls: create_transfers through tbg_create_transfers_device, body, batch bounds
+        # and results in HBM (hipMalloc'd here), results copied back after the call.
+        self._dev = _DeviceBuffers(batch_events_max, batch_count_max) if device_calls else None
         self.o = self.olib.tbo_open(pulse_batch_max, pulse_next_timestamp_init)
         self.prepare_timestamp = 0
         self._pulse_delta = pulse_batch_max
@@ -105,6 +144,9 @@ class Pair:
         self._apply_debug_modes()
 
     def close(self):
+        if self._dev is not None:
+            self._dev.free()
+            self._dev = None
         if self.g:
             self.lib.tbg_close(self.g)
             self.g = None
@@ -174,7 +216,16 @@ class Pair:
         r_gpu = np.zeros(n, dtype=RESULT_DTYPE)
         r_orc = np.zeros(n, dtype=RESULT_DTYPE)
         t0 = time.perf_counter()
-        if self._pool is not None:
+        if self._dev is not None:
+            D = self._dev
+            D.put(D.ev, events)
+            D.put(D.ends, np.cumsum(lens_a, dtype=np.uint32))
+            D.put(D.ts, batch_ts)
+            rc = self.lib.tbg_create_transfers_device(self.g, D.ev, n, D.ends, D.ts, len(lens),
+                                                      D.res, None)
+            if rc == 0:
+                D.get(D.res, r_gpu)
+        elif self._pool is not None:
             body = self._pool[:n * 128]
             body[:] = events.view(np.uint8).reshape(-1)
             res = self._pool[self._pool_results:self._pool_results + n * 16]

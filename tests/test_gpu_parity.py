@@ -147,18 +147,15 @@ def test_uniform_config2_small():
         p.close()
 
 
-@pytest.mark.parametrize("mode", ["spin", "stream-sync", "no-ingest-finish"])
+@pytest.mark.parametrize("mode", ["spin", "stream-sync"])
 def test_many_small_registered_calls(mode, monkeypatch):
-    """The host's end-of-call wait: the last workgroup of tr_ingest (a call whose events are all
-    FAST) or of stage_out publishes a sequence word after every workgroup's results and scalar
-    words (each thread releases its stores at system scope). 300 small calls from a registered
-    pool, every third one clean, each reply compared with the oracle as soon as the call returns
-    (Pair checks every result); TBG_NO_SPIN_SYNC (a stream synchronisation) and
-    TBG_NO_INGEST_FINISH (stage_out ends every call) are the controls."""
+    """The host's end-of-call wait: stage_out's last workgroup publishes a sequence word after every
+    workgroup's results and scalar words (each thread releases its stores at system scope). 300
+    small calls from a registered pool, every third one clean, each reply compared with the oracle
+    as soon as the call returns (Pair checks every result); TBG_NO_SPIN_SYNC (a stream
+    synchronisation) is the control."""
     if mode == "stream-sync":
         monkeypatch.setenv("TBG_NO_SPIN_SYNC", "1")
-    if mode == "no-ingest-finish":
-        monkeypatch.setenv("TBG_NO_INGEST_FINISH", "1")
     rng = np.random.default_rng(31)
     p = Pair(account_capacity=1 << 12, transfer_capacity=1 << 20, batch_events_max=8189,
              registered=True)
@@ -174,11 +171,7 @@ def test_many_small_registered_calls(mode, monkeypatch):
                 bad = rng.random(n) < 0.05
                 t["id"][bad] = 0
             p.create_transfers(t, _split(n, rng, 8189))
-        # (every third call is clean: ~100 end in tr_ingest)
-        if mode == "no-ingest-finish":
-            assert p.stats["ingest_finished"] == 0
-        else:
-            assert p.stats["ingest_finished"] >= 90
+        assert p.stats["ingest_finished"] == 0  # (host-buffer calls end in stage_out)
         p.compare_state()
     finally:
         p.close()
@@ -1259,6 +1252,40 @@ def test_later_post_void_claims(mode, monkeypatch):
                     a_i, b_i = rng.integers(0, len(rows), size=2)
                     rows[int(b_i)]["id"] = rows[int(a_i)]["id"]
             p.create_transfers(_transfers(rows), [len(rows) // 3, len(rows) - len(rows) // 3])
+        p.compare_state()
+    finally:
+        p.close()
+
+
+@pytest.mark.parametrize("mode", ["finish", "no-ingest-finish"])
+def test_many_small_device_calls(mode, monkeypatch):
+    """tbg_create_transfers_device, the body and results in HBM (a replica's per-commit path on
+    device buffers): a call whose events are all FAST ends in tr_ingest's last workgroup (the
+    counters, the scalars block, the call's scalar words cleared, the sequence word; the queued
+    tr_commit and stage_out return at once). 300 small calls, every third one clean, each compared
+    with the oracle as it returns; TBG_NO_INGEST_FINISH (tr_commit and stage_out end every call) is
+    the control."""
+    if mode == "no-ingest-finish":
+        monkeypatch.setenv("TBG_NO_INGEST_FINISH", "1")
+    rng = np.random.default_rng(37)
+    p = Pair(account_capacity=1 << 12, transfer_capacity=1 << 20, batch_events_max=8189,
+             device_calls=True)
+    try:
+        n_acc = 500
+        p.create_accounts(workload.accounts(n_acc, seed=4))
+        off = 0
+        for call in range(300):
+            n = int(rng.integers(1, 3000)) if call % 10 else 8189
+            t = workload.transfers_uniform(n, n_acc, seed=call, id_offset=off)
+            off += n
+            if call % 3:
+                bad = rng.random(n) < 0.05
+                t["id"][bad] = 0
+            p.create_transfers(t, _split(n, rng, 8189))
+        if mode == "finish":
+            assert p.stats["ingest_finished"] >= 90
+        else:
+            assert p.stats["ingest_finished"] == 0
         p.compare_state()
     finally:
         p.close()

@@ -251,16 +251,17 @@ struct SelectCreated {
 
 // (Both collectors run kPlanThreads lanes per workgroup and group the event's two touches by
 // account row; lanes past the events write "no key" for their touches.)
-__device__ inline void ae_group_touches(const AeScratch& S, GroupBlock& B, uint32_t i, bool active,
-                                        uint32_t dr, uint32_t cr, uint32_t bound) {
+// (counted by account in LDS first, one global probe and add per distinct account of the
+// workgroup: group_key_publish)
+using AeGroupBlock = GroupKeyBlockT<kPlanThreads, kPlanLdsSlots>;
+__device__ inline void ae_group_touches(const AeScratch& S, AeGroupBlock& B, uint32_t i,
+                                        bool active, uint32_t dr, uint32_t cr, uint32_t bound) {
     uint32_t e0 = kNone32, e1 = kNone32, r0 = 0, r1 = 0;
     if (active) {
-        uint32_t s0, s1;
-        group_slot2(S.G, dr, cr, &s0, &s1);
-        e0 = group_block_count(B, s0, &r0);
-        e1 = group_block_count(B, s1, &r1);
+        e0 = group_key_count(B, dr, &r0);
+        e1 = group_key_count(B, cr, &r1);
     }
-    group_block_publish(S.G, B);
+    group_key_publish(S.G, B);
     if (i >= bound) return;
     group_block_place(S.G, B, 2 * uint64_t(i), e0, r0);
     group_block_place(S.G, B, 2 * uint64_t(i) + 1, e1, r1);
@@ -326,8 +327,8 @@ __device__ inline void ae_collect_transfer(Tables T, const Call<tb_transfer_t>& 
 __global__ void __launch_bounds__(kPlanThreads)
 ae_collect_transfers(Tables T, Call<tb_transfer_t> c, const uint32_t* list,
                      const unsigned int* count, AeScratch S, tb_account_event_t* log, AeRef* refs) {
-    __shared__ GroupBlock B;
-    group_block_init(B);
+    __shared__ AeGroupBlock B;
+    group_key_init(B);
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i == 0) S.G.counts[1] = S.G.counts[2] = 0;  // listed accounts / chunks (ae_group_small)
     const bool room = ae_room(S.state, S.cap, *count);
@@ -492,9 +493,9 @@ struct PositionsOf8 {
 __global__ void __launch_bounds__(kPlanThreads)
 ae_copy_group(AeStage st, const uint32_t* pos, const unsigned int* m_dev, AeScratch S,
               tb_account_event_t* log, AeRef* refs) {
-    __shared__ GroupBlock B;
+    __shared__ AeGroupBlock B;
     if (S.skip && *S.skip == S.skip_if) return;
-    group_block_init(B);
+    group_key_init(B);
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k == 0) S.G.counts[1] = S.G.counts[2] = 0;  // listed accounts / chunks (ae_group_small)
     const bool room = ae_room(S.state, S.cap, *m_dev);
@@ -542,8 +543,8 @@ ae_collect_expiry(Tables T, const uint64_t* rows, uint32_t m_upper, const unsign
                   uint64_t timestamp, const uint64_t* stamps, AeScratch S, tb_account_event_t* log,
                   AeRef* refs) {
     const uint32_t m = m_dev ? *m_dev : m_upper;  // (the pulse's count, on device)
-    __shared__ GroupBlock B;
-    group_block_init(B);
+    __shared__ AeGroupBlock B;
+    group_key_init(B);
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i == 0) S.G.counts[1] = S.G.counts[2] = 0;  // listed accounts / chunks (ae_group_small)
     const bool room = ae_room(S.state, S.cap, m);

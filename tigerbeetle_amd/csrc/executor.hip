@@ -153,6 +153,9 @@ struct tbg_ctx {
     // ... and its body is read by tr_ingest from mapped host memory (the GPU's address), null: the
     // body is in d_events.
     const tb_transfer_t* events_host = nullptr;
+    // ... and so are its batch bounds, from the pinned staging (dh_batch_ends / dh_batch_ts): the
+    // call has no stage_in launch.
+    bool batches_host = false;
     uint32_t epoch = 0;
     // Sticky: a compaction failed after it began moving rows; the tables are undefined and every
     // later call fails (tbg_compact).
@@ -507,6 +510,8 @@ Call<Event> make_call(tbg_ctx* ctx, const Event* d_events, uint32_t n, const uin
     c.slow_list = ctx->slow_list;
     c.pnt_call = ctx->pnt_call;
     c.events_out = nullptr;
+    c.ends_out = nullptr;
+    c.ts_out = nullptr;
     c.fix_slots = ctx->fix_slots;
     c.chain_planes = nullptr;
     // (TBG_NO_PV_FAST: every post/void replays)
@@ -515,7 +520,6 @@ Call<Event> make_call(tbg_ctx* ctx, const Event* d_events, uint32_t n, const uin
     c.pnt_force = ctx->pnt_sharded ? 1 : 0;
     c.finish_done = nullptr;
     c.finish_scalars = nullptr;
-    c.finish_results = nullptr;
     c.finish_seq = nullptr;
     c.seq = 0;
     return c;
@@ -702,6 +706,7 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
     G.lanes = lanes_possible;
     G.free_owners = getenv("TBG_NO_FREE_OWNERS") == nullptr;
     G.stats = getenv("TBG_FLOW_DEBUG") != nullptr;
+    G.pairs = uint32_t(std::min<uint64_t>(uint64_t(kFlowKeys) * m, 0xFFFFFFFFull));
     G.epoch = c.epoch;
     G.owner_starts = F.owner_starts;
     G.lane_counts = F.lane_counts;
@@ -733,7 +738,7 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
     if (doom)
         hipLaunchKernelGGL(flow_credit_pot, dim3(grid_for(m)), block, 0, ctx->stream, ctx->T, c, P,
                            call_flags);
-    hipLaunchKernelGGL(plan_keys, dim3((m + kPlanThreads - 1) / kPlanThreads), dim3(kPlanThreads), 0,
+    hipLaunchKernelGGL(plan_keys, dim3((m + kPlanKeysThreads - 1) / kPlanKeysThreads), dim3(kPlanKeysThreads), 0,
                        ctx->stream, ctx->T, c, P, G, L, call_flags);
     // the planned expires_at entries, and the slots' segments (one launch)
     rc = launch_scan2(ctx, m,
@@ -1667,6 +1672,7 @@ int stage_call_inputs(tbg_ctx* ctx, const void* events, uint64_t bytes, uint32_t
                       bool reset_scalars, bool ingest_reads_host = false) {
     const uint4* src = mapped(ctx, static_cast<const uint4*>(events), bytes);
     ctx->events_host = nullptr;
+    ctx->batches_host = false;
     // A small create_transfers call's registered body is read by tr_ingest itself across PCIe
     // (it leaves the HBM copy for the later kernels): with AccountEvents this measured 70-72 us a
     // commit against 70-77 with stage_in copying the body first.
@@ -1674,6 +1680,12 @@ int stage_call_inputs(tbg_ctx* ctx, const void* events, uint64_t bytes, uint32_t
         ctx->events_host = reinterpret_cast<const tb_transfer_t*>(src);
         src = nullptr;
         bytes = 0;
+        // ... and so are the batch bounds, when the call's scalar words are already clear (the
+        // last call's end cleared them): no stage_in launch at all.
+        if (!reset_scalars || ctx->scalars_clean) {
+            ctx->batches_host = true;
+            return 0;
+        }
     }
     if (!src && bytes)
         HIP_TRY(ctx, hipMemcpyAsync(ctx->body_dst, events, bytes, hipMemcpyHostToDevice, ctx->stream));
@@ -1727,11 +1739,15 @@ int stage_call_outputs(tbg_ctx* ctx, const tb_create_result_t* d_results, tb_cre
                uint32_t(sizeof(DevScalars) / 8), fixes ? ctx->fix_slots : nullptr,
                ctx->T.tr.slots, ctx->d_scalars, seq ? ctx->d_stage_done : nullptr,
                seq ? ctx->dh_seq : nullptr, seq,
-               skip_epoch ? ctx->d_stage_done + 2 : nullptr, skip_epoch};
+               skip_epoch ? ctx->d_stage_done + 2 : nullptr, skip_epoch, snap != nullptr, {}};
+    if (snap) s.snap = *snap;
     if (!dst || !n) s.src = nullptr;
-    (void)snap;
-    const uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>((n + kStageThreads - 1) / kStageThreads, 1024));
-    hipLaunchKernelGGL(stage_out, dim3(grid), dim3(kStageThreads), 0, ctx->stream, s);
+    // (with a snapshot: one 64-lane wave a workgroup, kAeAsyncMax lanes at least -- an event's
+    // dependent loads spread over more CUs, as ae_snapshot's)
+    const uint32_t threads = snap ? kSnapThreads : kStageThreads;
+    uint32_t grid = std::max<uint32_t>(1, std::min<uint32_t>((n + threads - 1) / threads, 1024));
+    if (snap) grid = std::max<uint32_t>(grid, kAeAsyncMax / kSnapThreads);
+    hipLaunchKernelGGL(stage_out, dim3(grid), dim3(threads), 0, ctx->stream, s);
     HIP_TRY(ctx, hipGetLastError());
     return 0;
 }
@@ -2092,15 +2108,17 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
     }
     const bool spin = ctx->spin_sync && !ctx->timing;
     const unsigned int seq = spin ? (++ctx->seq ? ctx->seq : ++ctx->seq) : 0u;
-    // A small call without balance items may end in its last tr_ingest workgroup (Call::
-    // finish_done); tr_commit and stage_out are queued all the same and return at once then.
-    const bool finish = inline_chunks && !use_sort && !getenv("TBG_NO_INGEST_FINISH");
+    // A small device-buffer call without balance items may end in its last tr_ingest workgroup
+    // (Call::finish_done); tr_commit and stage_out are queued all the same and return at once then
+    // (device per-commit 27.7 -> 24.5 us, r05_g / r05_i). Host-buffer calls keep stage_out: with
+    // the results' PCIe writes in tr_ingest's workgroups a commit took 71-77 us against 64-68
+    // (r05_i A/B).
+    const bool finish = inline_chunks && !use_sort && !dst && !getenv("TBG_NO_INGEST_FINISH");
     if (!rc && inline_chunks) {
         c.chunk_info = nullptr;
         if (finish) {
             c.finish_done = ctx->d_stage_done + 1;
             c.finish_scalars = reinterpret_cast<unsigned long long*>(ctx->dh_scalars);
-            c.finish_results = dst;
             c.finish_seq = seq ? ctx->dh_seq : nullptr;
             c.seq = seq;
         }
@@ -2108,6 +2126,12 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
         if (ctx->events_host) {
             ci.events = ctx->events_host;
             ci.events_out = const_cast<tb_transfer_t*>(c.events);
+        }
+        if (ctx->batches_host) {
+            ci.batch_ends = ctx->dh_batch_ends;
+            ci.batch_ts = ctx->dh_batch_ts;
+            ci.ends_out = const_cast<uint32_t*>(c.batch_ends);
+            ci.ts_out = const_cast<uint64_t*>(c.batch_ts);
         }
         hipLaunchKernelGGL(tr_ingest, dim3(ig), block, 0, ctx->stream, ctx->T, ci);
         tmark(ctx, "tr_ingest");
@@ -2188,22 +2212,19 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
     // its results to mapped host memory (the registered destination, or the pinned staging).
     if (!rc) {
         const bool snap = ae_async_ok(ctx, n);
-        rc = stage_call_outputs(ctx, d_results, dst, dst ? n : 0, true, nullptr, true, seq,
-                                finish ? c.epoch : 0u);
-        // A small call's AccountEvents snapshot follows stage_out (the host's wait ends at
-        // stage_out): final unless a replay follows, then it stages nothing. Its appends are queued
-        // on the side stream now, so that the host's launch calls overlap the call's kernels.
-        if (!rc && snap) {
-            AeSnapJob J;
+        // A small call's AccountEvents snapshot is taken by stage_out's workgroups once they are
+        // counted (the host's wait ends at the sequence word): final unless a replay follows, then
+        // it stages nothing. Its appends are queued on the side stream now, so that the host's
+        // launch calls overlap the call's kernels.
+        AeSnapJob J;
+        if (snap) {
             rc = ae_snap_job(ctx, c, &J);
-            if (!rc) {
-                J.speculative = true;
-                hipLaunchKernelGGL(ae_snapshot, dim3(kAeAsyncMax / kSnapThreads), dim3(kSnapThreads), 0,
-                                   ctx->stream, J);
-                rc = hip_ok(ctx, hipGetLastError(), "launch") ? 0 : TBG_EHIP;
-            }
-            if (!rc) rc = ae_launch_graph(ctx, n, c.epoch);
+            J.speculative = true;
         }
+        if (!rc)
+            rc = stage_call_outputs(ctx, d_results, dst, dst ? n : 0, true, snap ? &J : nullptr,
+                                    true, seq, finish ? c.epoch : 0u);
+        if (!rc && snap) rc = ae_launch_graph(ctx, n, c.epoch);
         ctx->ae_snap_early = snap && !rc;
         if (!rc) rc = spin ? spin_wait(ctx, seq)
                            : (hip_ok(ctx, hipStreamSynchronize(ctx->stream), "sync") ? 0 : TBG_EHIP);
@@ -2457,6 +2478,7 @@ int tbg_create_transfers(tbg_ctx* ctx, const tb_transfer_t* events, uint32_t n,
     ctx->early_dst = nullptr;
     ctx->scalars_reset = false;
     ctx->events_host = nullptr;
+    ctx->batches_host = false;
     if (rc) {
         ctx->ae_deferred = false;
         return rc;

@@ -6,10 +6,11 @@
 // the whole pair array:
 //
 //   plan_keys      per replayed event: its keys (flow_keys' rules), its step record, the lanes'
-//                  eligibility and record (lanes_check's rules); each key is inserted into an HBM
-//                  hash table (key -> slot, CAS on an empty word) and counted. The counts of one
-//                  workgroup are first summed per slot in LDS, so a hot account's thousands of pairs
-//                  cost one global atomic per workgroup, and each pair keeps its arrival rank.
+//                  eligibility and record (lanes_check's rules); each key is counted in an LDS
+//                  table of the workgroup's distinct keys, and each distinct key then takes its
+//                  slot in an HBM hash table (key -> slot, CAS on an empty word) and its range in
+//                  the slot with one add -- a hot account's thousands of pairs cost one probe and
+//                  one add per workgroup -- and each pair keeps its arrival rank.
 //   chained_scan   the slots' exclusive sums: every key's segment in the grouped array.
 //   group_scatter  pair -> its segment at its rank (arrival order, not yet call order).
 //   group_small    per slot: a segment of <= 16 pairs is sorted in registers by pair index (pair
@@ -46,6 +47,10 @@ constexpr uint32_t kGroupChunk = kGroupBigThreads * kGroupBatch;  // pairs per g
 constexpr uint32_t kGroupChunkBlocks = 512;  // group_chunk grid (grid-stride over the chunks)
 constexpr uint32_t kPlanThreads = 256;      // plan_keys workgroup: 1024 pairs
 constexpr uint32_t kPlanLdsSlots = 2048;    // LDS aggregation table (load <= 0.5)
+// plan_keys' workgroup (512 / 1024 lanes, fewer global adds per hot slot: 46 / 58 us a plan
+// against 43, profiles/r05_commit/ab_plan_keys.txt)
+constexpr uint32_t kPlanKeysThreads = 256;
+constexpr uint32_t kPlanKeysSlots = 8 * kPlanKeysThreads;  // (kFlowKeys per lane, load <= 0.5)
 
 struct GroupPlan {
     uint64_t hmask;                 // hash slots - 1
@@ -71,6 +76,7 @@ struct GroupPlan {
     bool lanes;
     bool free_owners;               // free-owner verdicts (TBG_NO_FREE_OWNERS: none)
     bool stats;                     // counts[2] / [3] (TBG_FLOW_DEBUG)
+    uint32_t pairs;                 // kFlowKeys * m: every pair index is below it
     uint32_t epoch;
     uint32_t* owner_starts;
     unsigned int* lane_counts;      // [0] owners, [1] ineligible events
@@ -94,21 +100,6 @@ __device__ inline uint32_t group_slot(const GroupPlan& G, uint64_t key) {
         if (w == tag) return uint32_t(s);
         s = (s + 1) & G.hmask;
     }
-}
-
-// The slots of two keys: both home words are read (and, when empty, claimed) together -- one round
-// trip for the common case instead of one per key; collisions continue in group_slot.
-__device__ inline void group_slot2(const GroupPlan& G, uint64_t key0, uint64_t key1, uint32_t* s0,
-                                   uint32_t* s1) {
-    const unsigned long long tag0 = key0 + 1, tag1 = key1 + 1;
-    const uint64_t h0 = group_hash(key0) & G.hmask, h1 = group_hash(key1) & G.hmask;
-    unsigned long long w0 = G.hkeys[h0], w1 = G.hkeys[h1];
-    if (w0 == 0) w0 = atomicCAS(&G.hkeys[h0], 0ull, tag0);
-    if (w1 == 0 && !(h1 == h0 && tag1 == tag0)) w1 = atomicCAS(&G.hkeys[h1], 0ull, tag1);
-    else if (h1 == h0 && tag1 == tag0) w1 = 0;  // (the same key: w0's outcome decides both)
-    *s0 = (w0 == 0 || w0 == tag0) ? uint32_t(h0) : group_slot(G, key0);
-    if (h1 == h0 && tag1 == tag0) *s1 = *s0;
-    else *s1 = (w1 == 0 || w1 == tag1) ? uint32_t(h1) : group_slot(G, key1);
 }
 
 // The slots of up to kFlowKeys keys (kFlowNoKey: none): every home word is read, and every empty
@@ -149,54 +140,9 @@ __device__ inline void group_slots(const GroupPlan& G, const uint64_t (&key)[N],
     }
 }
 
-// Counting keys by slot within one workgroup (kPlanThreads lanes): each lane inserts its keys
-// (group_slot) and counts them in an LDS table of the workgroup's slots; then one global add per
-// slot turns the LDS counts into bases, and every pair gets its slot and rank. All lanes call the
-// three steps in order.
-struct GroupBlock {
-    uint32_t slot[kPlanLdsSlots];
-    uint32_t count[kPlanLdsSlots];
-};
-__device__ inline void group_block_init(GroupBlock& B) {
-    for (uint32_t i = threadIdx.x; i < kPlanLdsSlots; i += kPlanThreads) {
-        B.slot[i] = kNone32;
-        B.count[i] = 0;
-    }
-    __syncthreads();
-}
-// Counts `key` in the workgroup: returns its LDS entry (*lrank: its rank among the workgroup's).
-__device__ inline uint32_t group_block_count(GroupBlock& B, uint32_t slot, uint32_t* lrank) {
-    uint32_t h = uint32_t(mix64(slot)) & (kPlanLdsSlots - 1);
-    while (true) {
-        const uint32_t o = atomicCAS(&B.slot[h], kNone32, slot);
-        if (o == kNone32 || o == slot) break;
-        h = (h + 1) & (kPlanLdsSlots - 1);
-    }
-    *lrank = atomicAdd(&B.count[h], 1u);
-    return h;
-}
-__device__ inline uint32_t group_block_add(const GroupPlan& G, GroupBlock& B, uint64_t key,
-                                           uint32_t* lrank) {
-    return group_block_count(B, group_slot(G, key), lrank);
-}
-// One global add per slot of the workgroup: B.count becomes the slot's base.
-// (each lane's adds are issued together, then their results stored: one round trip per lane)
-__device__ inline void group_block_publish(const GroupPlan& G, GroupBlock& B) {
-    __syncthreads();
-    constexpr uint32_t kPer = kPlanLdsSlots / kPlanThreads;
-    uint32_t base[kPer];
-#pragma unroll
-    for (uint32_t j = 0; j < kPer; j++) {
-        const uint32_t i = threadIdx.x + j * kPlanThreads;
-        const uint32_t slot = B.slot[i];
-        base[j] = slot != kNone32 ? atomicAdd(&G.hcnt[slot], B.count[i]) : 0u;
-    }
-#pragma unroll
-    for (uint32_t j = 0; j < kPer; j++) B.count[threadIdx.x + j * kPlanThreads] = base[j];
-    __syncthreads();
-}
 // Pair `pair`'s slot and rank (entry kNone32: no key).
-__device__ inline void group_block_place(const GroupPlan& G, const GroupBlock& B, uint64_t pair,
+template <typename B_>
+__device__ inline void group_block_place(const GroupPlan& G, const B_& B, uint64_t pair,
                                          uint32_t entry, uint32_t lrank) {
     if (entry == kNone32) {
         G.loc[pair] = kNone32;
@@ -204,6 +150,70 @@ __device__ inline void group_block_place(const GroupPlan& G, const GroupBlock& B
         G.loc[pair] = B.slot[entry];
         G.rank[pair] = B.count[entry] + lrank;
     }
+}
+
+// plan_keys' counting by KEY within the workgroup: every lane counts its keys in an LDS table of
+// the workgroup's distinct keys first; then each distinct key takes its global slot (group_slots:
+// the home words read, the empty ones claimed) and its range in the slot (one add) -- one global
+// probe and one add per distinct key of the workgroup instead of a probe (and, for a key first
+// seen, a CAS) per pair: a hot account's thousands of pairs in a call all found its home word
+// empty at once and all tried to claim it (config 3: TA_ADDR_STALLED_BY_TC 8.3M cycles a launch,
+// profiles/r05_commit/pmc_config3.json).
+template <uint32_t THREADS, uint32_t SLOTS>
+struct GroupKeyBlockT {
+    static constexpr uint32_t kThreads = THREADS, kSlots = SLOTS;
+    unsigned long long key[SLOTS];  // key + 1 (0: empty)
+    uint32_t count[SLOTS];          // the key's pairs here, then the base of their range
+    uint32_t slot[SLOTS];           // the key's global slot
+};
+template <typename B_>
+__device__ inline void group_key_init(B_& B) {
+    for (uint32_t i = threadIdx.x; i < B_::kSlots; i += B_::kThreads) {
+        B.key[i] = 0;
+        B.count[i] = 0;
+    }
+    __syncthreads();
+}
+// Counts `key` in the workgroup: returns its LDS entry (*lrank: its rank among the workgroup's).
+template <typename B_>
+__device__ inline uint32_t group_key_count(B_& B, uint64_t key, uint32_t* lrank) {
+    const unsigned long long tag = key + 1;
+    uint32_t h = uint32_t(group_hash(key)) & (B_::kSlots - 1);
+    while (true) {
+        const unsigned long long o = atomicCAS(&B.key[h], 0ull, tag);
+        if (o == 0 || o == tag) break;
+        h = (h + 1) & (B_::kSlots - 1);
+    }
+    *lrank = atomicAdd(&B.count[h], 1u);
+    return h;
+}
+// Each distinct key: its global slot and the base of its range (the lane's kPer entries' probes
+// and adds issued together).
+template <typename B_>
+__device__ inline void group_key_publish(const GroupPlan& G, B_& B) {
+    __syncthreads();
+    constexpr uint32_t kPer = B_::kSlots / B_::kThreads;
+    uint64_t k[kPer];
+    uint32_t gs[kPer];
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; j++) {
+        const unsigned long long t = B.key[threadIdx.x + j * B_::kThreads];
+        k[j] = t ? t - 1 : kFlowNoKey;
+    }
+    group_slots(G, k, kFlowNoKey, gs);
+    uint32_t base[kPer];
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; j++) {
+        const uint32_t i = threadIdx.x + j * B_::kThreads;
+        base[j] = k[j] != kFlowNoKey ? atomicAdd(&G.hcnt[gs[j]], B.count[i]) : 0u;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; j++) {
+        const uint32_t i = threadIdx.x + j * B_::kThreads;
+        B.slot[i] = gs[j];
+        B.count[i] = base[j];
+    }
+    __syncthreads();
 }
 
 // ---- Doomed debits ------------------------------------------------------------------------------
@@ -307,11 +317,11 @@ __device__ inline bool doomed_debit(const Tables& T, const FlowPlan& P, const tb
 
 // Everything per replayed event s (flow_keys' and lanes_check's rules); its keys' grouping slots
 // and ranks. Launched with kPlanThreads per workgroup.
-__global__ void __launch_bounds__(kPlanThreads) plan_keys(Tables T, Call<tb_transfer_t> c,
-                                                          FlowPlan P, GroupPlan G,
-                                                          LanePlan L, unsigned int call_flags) {
-    __shared__ GroupBlock B;
-    group_block_init(B);
+__global__ void __launch_bounds__(kPlanKeysThreads) plan_keys(Tables T, Call<tb_transfer_t> c,
+                                                              FlowPlan P, GroupPlan G,
+                                                              LanePlan L, unsigned int call_flags) {
+    __shared__ GroupKeyBlockT<kPlanKeysThreads, kPlanKeysSlots> B;
+    group_key_init(B);
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     uint64_t key[kFlowKeys] = {kFlowNoKey, kFlowNoKey, kFlowNoKey, kFlowNoKey};
     uint32_t local[kFlowKeys] = {kNone32, kNone32, kNone32, kNone32};
@@ -433,18 +443,17 @@ __global__ void __launch_bounds__(kPlanThreads) plan_keys(Tables T, Call<tb_tran
                 L.recs[s] = r;
             }
         }
-        // Grouping: the global slots, then this workgroup's count of each slot in LDS.
-        uint32_t gs[kFlowKeys];
-        group_slots(G, key, kFlowNoKey, gs);
+        // Grouping: this workgroup's count of each key in LDS (the global slots follow, once per
+        // distinct key: group_key_publish).
 #pragma unroll
         for (uint32_t j = 0; j < kFlowKeys; j++)
-            if (key[j] != kFlowNoKey) local[j] = group_block_count(B, gs[j], &lrank[j]);
+            if (key[j] != kFlowNoKey) local[j] = group_key_count(B, key[j], &lrank[j]);
     }
     if (G.lanes) {
         const uint64_t bad = __ballot(ineligible);
         if ((threadIdx.x & 63) == 0 && bad) atomicAdd(&L.counts[1], uint32_t(__popcll(bad)));
     }
-    group_block_publish(G, B);
+    group_key_publish(G, B);
     if (s >= P.m) return;
 #pragma unroll
     for (uint32_t j = 0; j < kFlowKeys; j++)
@@ -548,15 +557,89 @@ struct SegmentLds {
 // kGroupWindowBits values in LDS over the values' range -- set bits, prefix popcounts, enumerate --
 // or, for a sparse segment, an LDS bitonic sort of the values themselves.
 __device__ inline void segment_sort(const uint32_t* in, uint32_t* out, uint32_t off, uint32_t c,
-                                    SegmentLds& L, bool values = false) {
+                                    SegmentLds& L, bool values = false, uint32_t bound = 0) {
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint32_t* buf = L.buf;
+    // The segment's values, 16 loads a lane in flight at a time (a loop of one load per iteration
+    // waits out every load in turn: ~50 round trips for a hot account's segment).
+    constexpr uint32_t kB = 16;
+    auto for_values = [&](auto&& fn) {
+        for (uint32_t i0 = tid; i0 < c; i0 += kB * kGroupBigThreads) {
+            uint32_t v[kB];
+#pragma unroll
+            for (uint32_t j = 0; j < kB; j++) {
+                const uint32_t i = i0 + j * kGroupBigThreads;
+                v[j] = i < c ? in[off + i] : 0u;
+            }
+#pragma unroll
+            for (uint32_t j = 0; j < kB; j++)
+                if (i0 + j * kGroupBigThreads < c) fn(i0 + j * kGroupBigThreads, v[j]);
+        }
+    };
+    // Bitmap windows of kGroupWindowBits over [lo, hi]: set bits, prefix popcounts, enumerate.
+    auto bitmap_window = [&](uint32_t lo, uint32_t hi) {
+        uint32_t placed = 0;
+        for (uint64_t wb = lo; wb <= hi; wb += kGroupWindowBits) {
+            // the window's words, rounded up to whole lanes' shares
+            const uint64_t span = hi - wb + 1 < kGroupWindowBits ? hi - wb + 1 : kGroupWindowBits;
+            const uint32_t per = uint32_t((span + 32 * kGroupBigThreads - 1) / (32 * kGroupBigThreads));
+            const uint32_t words = per * kGroupBigThreads;
+            for (uint32_t i = tid; i < words; i += kGroupBigThreads) buf[i] = 0;
+            __syncthreads();
+            for_values([&](uint32_t, uint32_t v) {
+                if (v >= wb && v - wb < kGroupWindowBits) {
+                    const uint32_t d = uint32_t(v - wb);
+                    atomicOr(&buf[d >> 5], 1u << (d & 31));
+                }
+            });
+            __syncthreads();
+            // Each wave enumerates a contiguous range of the window's words, 64 consecutive
+            // words (one a lane, conflict-free LDS reads) at a time; the wave totals' prefix
+            // places the waves. (A lane owning `per` consecutive words read them 32-way
+            // bank-conflicted: ~13 us a window.)
+            constexpr uint32_t kWaves = kGroupBigThreads / 64;
+            const uint32_t ww = words / kWaves, wbase = wave * ww;
+            uint32_t cnt = 0;
+            for (uint32_t r = 0; r < ww; r += 64) cnt += __popc(buf[wbase + r + lane]);
+            cnt = wave_sum_u32(cnt);
+            if (lane == 0) L.scratch[wave] = cnt;
+            __syncthreads();
+            uint32_t run = placed, total = 0;
+            for (uint32_t v = 0; v < kWaves; v++) {
+                const uint32_t cv = L.scratch[v];
+                run += v < wave ? cv : 0u;
+                total += cv;
+            }
+            for (uint32_t r = 0; r < ww; r += 64) {
+                uint32_t bits = buf[wbase + r + lane];
+                const uint32_t pc = __popc(bits);
+                const uint32_t incl = wave_inclusive_u32(pc, lane);
+                uint32_t pos = run + incl - pc;
+                const uint64_t word_bit = wb + uint64_t(wbase + r + lane) * 32;
+                while (bits) {
+                    const uint32_t bit = __builtin_ctz(bits);
+                    bits &= bits - 1;
+                    out[off + pos++] = uint32_t(word_bit + bit);
+                }
+                run += __shfl(incl, 63, 64);
+            }
+            placed += total;
+            __syncthreads();
+        }
+        __threadfence();
+        __syncthreads();
+    };
     uint32_t lo = kNone32, hi = 0;
-    for (uint32_t i = tid; i < c; i += kGroupBigThreads) {
-        const uint32_t v = in[off + i];
+    if (bound && bound <= kGroupWindowBits && !values) {
+        // every value is below `bound` (a call's pair indices): one bitmap window over
+        // [0, bound), no pass over the values for their range
+        bitmap_window(0, bound - 1);
+        return;
+    }
+    for_values([&](uint32_t, uint32_t v) {
         lo = min(lo, v);
         hi = max(hi, v);
-    }
+    });
     for (int d = 32; d >= 1; d >>= 1) {
         lo = min(lo, uint32_t(__shfl_xor(lo, d, 64)));
         hi = max(hi, uint32_t(__shfl_xor(hi, d, 64)));
@@ -582,7 +665,8 @@ __device__ inline void segment_sort(const uint32_t* in, uint32_t* out, uint32_t 
     // values ~40 -- config 3's hot accounts.)
     const uint64_t range = uint64_t(hi - lo) + 1;
     if (pw <= kGroupLdsWords && (values || (range > kGroupWindowBits && range > 64ull * pw))) {
-        for (uint32_t i = tid; i < pw; i += kGroupBigThreads) buf[i] = i < c ? in[off + i] : kNone32;
+        for (uint32_t i = c + tid; i < pw; i += kGroupBigThreads) buf[i] = kNone32;
+        for_values([&](uint32_t i, uint32_t v) { buf[i] = v; });
         __syncthreads();
         for (uint32_t size = 2; size <= pw; size <<= 1) {
             for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
@@ -602,39 +686,7 @@ __device__ inline void segment_sort(const uint32_t* in, uint32_t* out, uint32_t 
         __syncthreads();
         return;
     }
-    uint32_t placed = 0;
-    for (uint64_t wb = lo; wb <= hi; wb += kGroupWindowBits) {
-        // the window's words, rounded up to whole lanes' shares
-        const uint64_t span = hi - wb + 1 < kGroupWindowBits ? hi - wb + 1 : kGroupWindowBits;
-        const uint32_t per = uint32_t((span + 32 * kGroupBigThreads - 1) / (32 * kGroupBigThreads));
-        const uint32_t words = per * kGroupBigThreads;
-        for (uint32_t i = tid; i < words; i += kGroupBigThreads) buf[i] = 0;
-        __syncthreads();
-        for (uint32_t i = tid; i < c; i += kGroupBigThreads) {
-            const uint32_t v = in[off + i];
-            if (v >= wb && v - wb < kGroupWindowBits) {
-                const uint32_t d = uint32_t(v - wb);
-                atomicOr(&buf[d >> 5], 1u << (d & 31));
-            }
-        }
-        __syncthreads();
-        uint32_t mine = 0;
-        for (uint32_t w = 0; w < per; w++) mine += __popc(buf[tid * per + w]);
-        uint32_t total = 0;
-        uint32_t r = placed + group_block_exclusive(mine, &total, L.scratch);
-        for (uint32_t w = 0; w < per; w++) {
-            uint32_t bits = buf[tid * per + w];
-            while (bits) {
-                const uint32_t bit = __builtin_ctz(bits);
-                bits &= bits - 1;
-                out[off + r++] = uint32_t(wb + uint64_t(tid * per + w) * 32 + bit);
-            }
-        }
-        placed += total;
-        __syncthreads();
-    }
-    __threadfence();
-    __syncthreads();
+    bitmap_window(lo, hi);
 }
 
 // A segment of kGroupSmall < c <= kGroupMid values sorted by one wave: lane l holds values
@@ -800,7 +852,7 @@ __global__ void __launch_bounds__(kGroupBigThreads) group_sort(GroupPlan G) {
     const uint32_t nbig = G.counts[1];
     for (uint32_t b = blockIdx.x; b < nbig; b += gridDim.x) {
         const uint4 e = G.big[b];
-        segment_sort(G.vals, G.vals_sorted, e.x, e.y, L);
+        segment_sort(G.vals, G.vals_sorted, e.x, e.y, L, false, G.pairs);
     }
 }
 

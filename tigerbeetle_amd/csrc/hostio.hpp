@@ -72,13 +72,16 @@ struct StageOut {
     unsigned int* host_seq;
     unsigned int seq;
     // When *finished == finished_epoch (tr_ingest ended the call: Call::finish_done) the kernel
-    // returns at once. Null: never.
+    // copies nothing and publishes nothing. Null: never.
     const unsigned int* finished;
     unsigned int finished_epoch;
+    // A small call's AccountEvents snapshot (ae_snapshot's work, kAeAsyncMax events), taken after
+    // the workgroup has been counted: the host's wait does not include it, and it costs no launch
+    // of its own. `has_snap` false: none.
+    bool has_snap;
+    AeSnapJob snap;
 };
 
-// (A small call's AccountEvents staging follows in its own kernel, ae_snapshot: the host's wait
-// ends here.)
 // The end of a stream's work for a spinning host (tbg_pulse): `seq` into the pinned word, a
 // system-scope release after every earlier kernel of the stream.
 __global__ void host_signal(unsigned int* host_seq, unsigned int seq) {
@@ -88,19 +91,17 @@ __global__ void host_signal(unsigned int* host_seq, unsigned int seq) {
     }
 }
 
-__global__ void __launch_bounds__(kStageThreads) stage_out(StageOut s) {
-    const uint32_t tid = blockIdx.x * kStageThreads + threadIdx.x;
-    if (s.finished && *s.finished == s.finished_epoch) return;
+// stage_out's copies and the sequence word (every thread of the grid calls it).
+__device__ inline void stage_out_copy(const StageOut& s, uint32_t tid, uint32_t threads) {
     if (s.fix_slots) {
         const uint64_t nfix = s.scalars->fixed;
-        for (uint64_t i = tid; i < nfix; i += uint64_t(gridDim.x) * kStageThreads)
-            s.id_slots[s.fix_slots[i]] = kTomb;
+        for (uint64_t i = tid; i < nfix; i += threads) s.id_slots[s.fix_slots[i]] = kTomb;
     }
     if (s.scalars_src && blockIdx.x == 0)
-        for (uint32_t w = threadIdx.x; w < s.scalar_words; w += kStageThreads)
+        for (uint32_t w = threadIdx.x; w < s.scalar_words; w += blockDim.x)
             s.scalars_dst[w] = s.scalars_src[w];
     if (s.src)
-        for (uint32_t i = tid; i < s.n; i += gridDim.x * kStageThreads) s.dst[i] = s.src[i];
+        for (uint32_t i = tid; i < s.n; i += threads) s.dst[i] = s.src[i];
     if (s.host_seq) {
         // Every thread releases its own stores at system scope before the barrier (a fence orders
         // only the issuing wave's stores; a workgroup barrier waits at workgroup scope only): the
@@ -114,6 +115,17 @@ __global__ void __launch_bounds__(kStageThreads) stage_out(StageOut s) {
                 __hip_atomic_store(s.host_seq, s.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             }
         }
+    }
+}
+
+__global__ void __launch_bounds__(kStageThreads) stage_out(StageOut s) {
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t threads = gridDim.x * blockDim.x;
+    if (!(s.finished && *s.finished == s.finished_epoch)) stage_out_copy(s, tid, threads);
+    if (s.has_snap && tid < kAeAsyncMax) {
+        const AeSnapJob& J = s.snap;
+        if (J.speculative && J.T.scalars->stats[0] != 0) J.st.created[tid] = 0;
+        else ae_snapshot_one(J, tid);
     }
 }
 

@@ -841,9 +841,9 @@ __global__ void tr_chunk_info(Call<tb_transfer_t> c, uint4* out, DevScalars* sca
 
 // The end of a small call by tr_ingest's last workgroup (Call::finish_done), when no event raised a
 // commit flag: what tr_commit's clean branch, stage_out and tr_reset_scalars would do, two launches
-// earlier. A workgroup is counted after its stores are released: with results for the host every
-// thread releases at system scope (mapped host memory, as in stage_out); else every wave waits for
-// its stores and lane 0 releases at agent scope (MI355X_MICROARCH.md, inter-workgroup visibility).
+// earlier (calls whose results stay in HBM: tbg_create_transfers_device). A workgroup is counted
+// after every wave has waited for its stores and lane 0 has released them at agent scope
+// (MI355X_MICROARCH.md, inter-workgroup visibility).
 // The last workgroup acquires, sums the call's counters, copies the scalars block to its mapped
 // copy, clears the call's scalar words for the next call, marks the call finished for the queued
 // tr_commit and stage_out (finish_done[1] = epoch: they return at once), and then publishes the
@@ -851,23 +851,11 @@ __global__ void tr_chunk_info(Call<tb_transfer_t> c, uint4* out, DevScalars* sca
 __device__ inline void ingest_finish(const Tables& T, const Call<tb_transfer_t>& c) {
     __shared__ unsigned int last;  // 0: not the last workgroup; else the call's flags | 1 << 31
     DevScalars* S = T.scalars;
-    if (c.finish_results) {
-        // The wave's results to the host (the lane re-reads what it wrote; final if the call
-        // finishes here, else stage_out writes them all again).
-        const uint32_t waves = blockDim.x / 64, nw = gridDim.x * waves;
-        for (uint32_t k = (blockIdx.x * waves + (threadIdx.x >> 6)) * 64 + (threadIdx.x & 63);
-             k < c.n; k += nw * 64)
-            c.finish_results[k] = c.results[k];
-        __threadfence_system();
-    } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-        if (!c.finish_results) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         last = 0;
         if (atomicAdd(c.finish_done, 1u) == gridDim.x - 1) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -933,6 +921,11 @@ __global__ void __launch_bounds__(kBlock, TBG_INGEST_WG_PER_CU) tr_ingest(Tables
     }
     uint8_t* my = lds_ev[wv];
     const uint32_t nw = gridDim.x * kIngestWaves;
+    if (c.ends_out && blockIdx.x == 0)  // (the batch bounds read from the host: the later kernels' copy)
+        for (uint32_t b = threadIdx.x; b < c.n_batches; b += blockDim.x) {
+            c.ends_out[b] = c.batch_ends[b];
+            c.ts_out[b] = c.batch_ts[b];
+        }
     unsigned int flags = 0;
     uint64_t n_fast = 0, ts_max = 0;
     uint4 q[8];

@@ -164,6 +164,10 @@ struct Call {
     // tr_ingest of a small host-buffer call reads the body straight from mapped host memory
     // (`events`) and leaves a copy here for the call's later kernels (null: no copy).
     tb_transfer_t* events_out;
+    // ... and, with no stage_in launch, its batch bounds too (`batch_ends` / `batch_ts` then the
+    // mapped pinned staging; workgroup 0 copies them here; null: no copy).
+    uint32_t* ends_out;
+    uint64_t* ts_out;
     // tr_commit's fixed failures (later_claim_status): the id slots they release, tombstoned by
     // the next kernel (stage_out) -- tr_commit's threads read other events' slots.
     uint32_t* fix_slots;
@@ -172,14 +176,13 @@ struct Call {
     // words of other epochs are free): the earliest post/void of a pending transfer in the call.
     unsigned long long* pv_slots;
     uint64_t pv_mask;
-    // Small calls without balance items: the last tr_ingest workgroup to finish ends a call that
-    // raised no commit flag (every event FAST, its effects all written) -- the call's counters,
-    // the scalars block to its mapped copy, the sequence word for a spinning host -- and sets
-    // kFlagFinished, on which tr_commit and stage_out return at once. Its FAST results also go
-    // to the mapped host destination as they are made. finish_done = null: no such ending.
-    unsigned int* finish_done;       // ingest's finished workgroups (zero between calls)
+    // Small device-buffer calls without balance items: the last tr_ingest workgroup to finish
+    // ends a call that raised no commit flag (every event FAST, its effects all written) -- the
+    // call's counters, the scalars block to its mapped copy, the call's scalar words cleared, the
+    // sequence word for a spinning host -- and finish_done[1] = epoch tells the queued tr_commit
+    // and stage_out to return at once. finish_done = null: no such ending.
+    unsigned int* finish_done;       // ingest's finished workgroups (zero between calls), epoch
     unsigned long long* finish_scalars;  // mapped pinned copy of the scalars block
-    tb_create_result_t* finish_results;  // mapped host destination of the results, or null
     unsigned int* finish_seq;        // the pinned sequence word, or null (the host synchronises)
     unsigned int seq;
 };
