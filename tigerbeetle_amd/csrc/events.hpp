@@ -267,6 +267,36 @@ __device__ inline void ae_group_touches(const AeScratch& S, AeGroupBlock& B, uin
     group_block_place(S.G, B, 2 * uint64_t(i) + 1, e1, r1);
 }
 
+// A created transfer's account rows as ingest left them, for an event that is not a post/void: its
+// record (ev_dr / ev_cr) or, for a lean FAST event, its packed balance item (pair or key items;
+// ~0 once tr_commit cleared it). kNone32: look the ids up (account_find: two hash probes an event
+// -- config 2's AccountEvents under wide amounts spent ~3 ms a 10M-event call there).
+__device__ inline void ae_known_rows(const Call<tb_transfer_t>& c, uint32_t k, uint8_t info,
+                                     uint32_t* dr, uint32_t* cr) {
+    *dr = *cr = kNone32;
+    if (!(info & kInfoLean)) {
+        if (c.ev_dr && c.ev_cr) {
+            *dr = c.ev_dr[k];
+            *cr = c.ev_cr[k];
+        }
+        return;
+    }
+    if (!c.bal_items) return;
+    if (c.pair_shift) {
+        const uint64_t x = c.bal_items[k];
+        if (x == ~0ull) return;
+        const uint64_t m = (1ull << c.pair_shift) - 1;
+        *dr = uint32_t(x & m);
+        *cr = uint32_t((x >> c.pair_shift) & m);
+    } else {
+        const uint64_t i0 = c.bal_items[2 * uint64_t(k)], i1 = c.bal_items[2 * uint64_t(k) + 1];
+        if (i0 == ~0ull || i1 == ~0ull) return;
+        const uint64_t km = (1ull << c.key_bits) - 1;
+        *dr = uint32_t((i0 & km) >> 2);
+        *cr = uint32_t((i1 & km) >> 2);
+    }
+}
+
 // Both sides' deltas of created transfer t (p: its pending transfer, for a post/void); returns the
 // event's TransferPendingStatus.
 __device__ inline uint8_t ae_transfer_sides(const AeScratch& S, uint32_t i, const tb_transfer_t& t,
@@ -309,9 +339,8 @@ __device__ inline void ae_collect_transfer(Tables T, const Call<tb_transfer_t>& 
     // ingest found (c.ev_dr / ev_cr, unless it packed them into balance items: kInfoLean); a
     // post/void's are the pending transfer's.
     const bool pv = (f & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) != 0;
-    const bool refs_ok = !pv && c.ev_dr && c.ev_cr && !(c.ev_info[k] & kInfoLean);
-    const uint32_t edr = refs_ok ? c.ev_dr[k] : kNone32;
-    const uint32_t ecr = refs_ok ? c.ev_cr[k] : kNone32;
+    uint32_t edr = kNone32, ecr = kNone32;
+    if (!pv) ae_known_rows(c, k, c.ev_info[k], &edr, &ecr);
     const uint64_t dr = edr != kNone32 ? uint64_t(edr) : account_find(T, t.debit_account_id);
     const uint64_t cr = ecr != kNone32 ? uint64_t(ecr) : account_find(T, t.credit_account_id);
     const tb_transfer_t* p =
@@ -1498,9 +1527,8 @@ __global__ void ae_dense_stage(AeDense A) {
         const tb_transfer_t& t = T.tr_rows[row];
         const uint16_t f = t.flags;
         const bool pv = (f & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) != 0;
-        const bool refs_ok = !pv && c.ev_dr && c.ev_cr && !(c.ev_info[k] & kInfoLean);
-        const uint32_t edr = refs_ok ? c.ev_dr[k] : kNone32;
-        const uint32_t ecr = refs_ok ? c.ev_cr[k] : kNone32;
+        uint32_t edr = kNone32, ecr = kNone32;
+        if (!pv) ae_known_rows(c, k, c.ev_info[k], &edr, &ecr);
         const uint64_t dr = edr != kNone32 ? uint64_t(edr) : account_find(T, t.debit_account_id);
         const uint64_t cr = ecr != kNone32 ? uint64_t(ecr) : account_find(T, t.credit_account_id);
         const tb_transfer_t* p = pv ? &T.tr_rows[ae_transfer_row(T, t.pending_id)] : nullptr;
