@@ -673,8 +673,11 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
     P.exp_base = &F.words[1];
     P.lane_counts = F.lane_counts;
     // Additive accounts get no key (Replay::additive); TBG_NO_ADDITIVE keys every account.
+    // (kFlagNoLanes: a replayed event the lanes would refuse -- the plan then keeps doomed debits
+    // off their accounts' keys; config 4's first call, no post/void yet: 825 -> ~360 us)
     const bool lanes_possible =
-        !(call_flags & (kFlagDuplicate | kFlagPostVoid | kFlagClosable | kFlagImported)) &&
+        !(call_flags & (kFlagDuplicate | kFlagPostVoid | kFlagClosable | kFlagImported |
+                        kFlagNoLanes)) &&
         !c.force_replay && !getenv("TBG_NO_LANES");
     P.add_epoch = getenv("TBG_NO_ADDITIVE") ? 0 : c.epoch;
     // Doomed debits (group.hpp): not with the account lanes (which decide limit events themselves).

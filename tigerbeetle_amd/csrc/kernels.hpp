@@ -540,6 +540,7 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
     const EvNarrow tn = ev_narrow(t);
     bool imported = false, post_void = false, dup = false, closable = false, hot = false;
     bool need_commit = false, chain_fast = false, ae_slow = false, wide_item = false;
+    bool no_lanes = false;
     if (c.pnt_force) c.pnt_call[k] = 0;  // (sharded calls record every update: none yet)
     const uint16_t f = tn.flags();
     imported = (f & TB_TRANSFER_IMPORTED) != 0;
@@ -781,6 +782,10 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
     }
     if (cls != kClassFast) {
         need_commit = true;
+        // (lanes_check's static rules, plan_keys)
+        no_lanes = cls == kClassSlow && (f != 0 || tn.timeout() != 0 || tn.amount_hi() != 0 ||
+                                         tn.timestamp() != 0 || batch_imported ||
+                                         !u128_is_zero(t.pending_id));
         if (c.bal_items && c.pair_shift)
             c.bal_items[k] = ~0ull;
         else if (c.bal_items)
@@ -789,7 +794,8 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
     return (imported ? kFlagImported : 0u) | (post_void ? kFlagPostVoid : 0u) |
            (dup ? kFlagDuplicate : 0u) | (closable ? kFlagClosable : 0u) | (hot ? kFlagHot : 0u) |
            (need_commit ? kFlagNeedCommit : 0u) | (chain_fast ? kFlagChain : 0u) |
-           (ae_slow ? kFlagAeSlow : 0u) | (wide_item ? kFlagWideItems : 0u);
+           (ae_slow ? kFlagAeSlow : 0u) | (wide_item ? kFlagWideItems : 0u) |
+           (no_lanes ? kFlagNoLanes : 0u);
 }
 
 // Per 64-event chunk of a create_transfers call (one lane each): the batch b0 of its first event,

@@ -54,6 +54,9 @@ enum : unsigned int {
     kFlagWideSums = 1u << 11,  // a window key's sum reached 2^32
     kFlagWideItems = 1u << 12, // a pair item too wide to pack (the balance window's wide layout)
     kFlagFinished = 1u << 13,  // tr_ingest ended the call (Call::finish_done)
+    // A replayed (SLOW) event the account lanes cannot take (lanes.hpp: not a plain unlinked
+    // transfer): the flow replay runs, so the plan may drop doomed debits' keys (group.hpp).
+    kFlagNoLanes = 1u << 14,
 };
 // Call flags under which tr_commit re-validates (and may demote) ingest's FAST events.
 constexpr unsigned int kCommitFlags = kFlagImported | kFlagPostVoid | kFlagDuplicate | kFlagHot |
