@@ -26,38 +26,10 @@
 #include "replay.hpp"
 #include "prims.hpp"
 
-// tr_ingest build knobs (same-box A/B builds: csrc/Makefile `variant`).
-#ifndef TBG_INGEST_EARLY_PREFETCH
-#define TBG_INGEST_EARLY_PREFETCH 0
-#endif
-#ifndef TBG_INGEST_NT
-#define TBG_INGEST_NT 1       // rows: non-temporal stores (written once, never re-read here)
-#endif
-#ifndef TBG_INGEST_NT_RESULTS
-#define TBG_INGEST_NT_RESULTS 1  // results: non-temporal (the host reads them after the call)
-#endif
-#ifndef TBG_INGEST_NT_LOADS
-#define TBG_INGEST_NT_LOADS 1    // events: non-temporal loads (read once)
-#endif
-#ifndef TBG_INGEST_WG_PER_CU
-#define TBG_INGEST_WG_PER_CU 4
-#endif
-#ifndef TBG_INGEST_JOINT_PROBE
-#define TBG_INGEST_JOINT_PROBE 1
-#endif
-#ifndef TBG_INGEST_PREV_SHFL
-#define TBG_INGEST_PREV_SHFL 1  // the previous event's flags by a lane shuffle (tr_ingest)
-#endif
-#ifndef TBG_INGEST_NARROW_B128
-#define TBG_INGEST_NARROW_B128 1  // the event's narrow fields by 16-byte LDS reads (EvNarrow)
-#endif
-#ifndef TBG_INGEST_H1_FIRST
-#define TBG_INGEST_H1_FIRST 1  // account index: the first candidate only, the second on a miss
-#endif
-
 namespace tbg {
 
 constexpr int kBlock = 256;
+constexpr uint32_t kIngestWgPerCu = 4;  // tr_ingest's occupancy (workgroups per CU, launch bounds)
 
 // Bucketed balance path: keys (account row * 4 + field) fall into buckets of 8192 consecutive
 // keys (2048 accounts); a call uses it when 4 * accounts <= kBucketsMax * 8192.
@@ -366,7 +338,6 @@ __device__ inline uint8_t classify_post_void(const Tables& T, const Call<tb_tran
 // (SQ_LDS_BANK_CONFLICT, profiles/r03_final_pmc); the 16-byte reads are conflict-free.
 struct EvNarrow {
     const uint4* w;  // the event's LDS image (16-byte words)
-#if TBG_INGEST_NARROW_B128
     __device__ uint16_t flags() const { return uint16_t(w[7].y >> 16); }
     __device__ uint16_t code() const { return uint16_t(w[7].y); }
     __device__ uint32_t ledger() const { return w[7].x; }
@@ -374,16 +345,6 @@ struct EvNarrow {
     __device__ uint64_t timestamp() const { const uint4 q = w[7]; return (uint64_t(q.w) << 32) | q.z; }
     __device__ uint64_t amount_lo() const { const uint4 q = w[3]; return (uint64_t(q.y) << 32) | q.x; }
     __device__ uint64_t amount_hi() const { const uint4 q = w[3]; return (uint64_t(q.w) << 32) | q.z; }
-#else  // (the fields one by one: same-box A/B builds)
-    __device__ const tb_transfer_t& t() const { return *reinterpret_cast<const tb_transfer_t*>(w); }
-    __device__ uint16_t flags() const { return t().flags; }
-    __device__ uint16_t code() const { return t().code; }
-    __device__ uint32_t ledger() const { return t().ledger; }
-    __device__ uint32_t timeout() const { return t().timeout; }
-    __device__ uint64_t timestamp() const { return t().timestamp; }
-    __device__ uint64_t amount_lo() const { return t().amount.lo; }
-    __device__ uint64_t amount_hi() const { return t().amount.hi; }
-#endif
 };
 __device__ inline EvNarrow ev_narrow(const tb_transfer_t& t) {
     return EvNarrow{reinterpret_cast<const uint4*>(&t)};
@@ -492,13 +453,9 @@ __device__ inline bool item_packable(const Call<tb_transfer_t>& c, uint64_t amou
 }
 
 __device__ inline void ingest_store_result(tb_create_result_t* p, const tb_create_result_t& r) {
-#if TBG_INGEST_NT_RESULTS
     typedef unsigned int v4u __attribute__((ext_vector_type(4)));
     const v4u v = {uint32_t(r.timestamp), uint32_t(r.timestamp >> 32), r.status, r.reserved};
     __builtin_nontemporal_store(v, reinterpret_cast<v4u*>(p));
-#else
-    *p = r;
-#endif
 }
 
 // Balance-delta item: key = account_row * 4 + field (0 dp, 1 dpo, 2 cp, 3 cpo).
@@ -597,7 +554,6 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
         if (valid_id)
             w_seen = atomicCAS(&T.tr.slots[s_id], (unsigned long long)kEmpty,
                                (unsigned long long)tref);
-#if TBG_INGEST_H1_FIRST
         {
             // Most entries sit at their first candidate (load <= 0.25): one 16-byte load per
             // account; the second candidate only for the lanes whose first one missed.
@@ -616,15 +572,6 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
             dr = acc_probe_snap(T, pd, dr_id, vd, true);
             cr = acc_probe_snap(T, pc, cr_id, vc, false);
         }
-#elif TBG_INGEST_JOINT_PROBE
-        const AccProbe pd = acc_probe_issue(T.acc_index, dr_id, vd);
-        const AccProbe pc = acc_probe_issue(T.acc_index, cr_id, vc);
-        dr = acc_probe_snap(T, pd, dr_id, vd, true);
-        cr = acc_probe_snap(T, pc, cr_id, vc, false);
-#else
-        dr = acc_lookup_snap(T, dr_id, vd, true);
-        cr = acc_lookup_snap(T, cr_id, vc, false);
-#endif
         if (valid_id) {
             if (w_seen == kEmpty) {
                 slot = s_id;  // claimed
@@ -915,7 +862,7 @@ __device__ inline void wave_lds_sync() {
 // event's fields, and go back out as the transfer rows (timestamp patched) with 8 coalesced
 // stores. The next chunk's loads are issued before the current chunk's table work, so the event
 // stream overlaps the claim / index round trip.
-__global__ void __launch_bounds__(kBlock, TBG_INGEST_WG_PER_CU) tr_ingest(Tables T,
+__global__ void __launch_bounds__(kBlock, kIngestWgPerCu) tr_ingest(Tables T,
                                                                          Call<tb_transfer_t> c) {
     __shared__ __attribute__((aligned(16))) uint8_t lds_ev[kIngestWaves][64 * kLdsEventStride];
     __shared__ uint64_t lds_ts[kIngestWaves][64];
@@ -944,7 +891,6 @@ __global__ void __launch_bounds__(kBlock, TBG_INGEST_WG_PER_CU) tr_ingest(Tables
             // fewer requests in flight, tools/pciebench.hip; 77 -> 73 us a commit, r05_h A/B).
             if (i == 4 && c.events_out) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             const uint32_t idx = i * 64 + lane;
-#if TBG_INGEST_NT_LOADS
             typedef unsigned int v4u __attribute__((ext_vector_type(4)));
             if (idx < parts) {
                 const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(&src[idx]));
@@ -952,9 +898,6 @@ __global__ void __launch_bounds__(kBlock, TBG_INGEST_WG_PER_CU) tr_ingest(Tables
             } else {
                 q[i] = make_uint4(0, 0, 0, 0);
             }
-#else
-            q[i] = idx < parts ? src[idx] : make_uint4(0, 0, 0, 0);
-#endif
         }
     };
     uint32_t base = (blockIdx.x * kIngestWaves + wv) * 64;
@@ -1037,39 +980,23 @@ __global__ void __launch_bounds__(kBlock, TBG_INGEST_WG_PER_CU) tr_ingest(Tables
                 q[i].w = uint32_t(ts >> 32);
             }
             if (full || i * 64 + lane < cnt * 8) {
-#if TBG_INGEST_NT
                 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
                 const v4u v = {q[i].x, q[i].y, q[i].z, q[i].w};
                 __builtin_nontemporal_store(v, reinterpret_cast<v4u*>(&dst[i * 64 + lane]));
-#else
-                dst[i * 64 + lane] = q[i];
-#endif
             }
         }
         const uint32_t next = base + nw * 64;
-#if TBG_INGEST_EARLY_PREFETCH
-        // The next chunk's loads overlap this chunk's claim and index round trips. (Issued
-        // unconditionally -- past the end the current chunk is reloaded and dropped -- so the
-        // compiler's wait counts stay exact and the claim does not wait for the prefetch.)
-        load_chunk(next < c.n ? next : ubase);
-#endif
         // (The lane's fields are read from the LDS image where they are used: 16-byte fields with
         // conflict-free ds_read_b128; the 2-8 byte ones put 2-4 lanes of a 32-lane group on a
         // bank. A register copy of the event would avoid that but spills at this kernel's
         // 128-VGPR budget.)
         // (the previous event's flags from its lane: a 2-byte LDS read of its image at the
         // 144-byte stride put 4 lanes on a bank)
-#if TBG_INGEST_PREV_SHFL
         const uint32_t own_flags =
             ev_narrow(*reinterpret_cast<const tb_transfer_t*>(my + lane * kLdsEventStride)).flags();
         const uint32_t up_flags = __shfl_up(own_flags, 1, 64);
-#endif
         if (active) {
             const tb_transfer_t& t = *reinterpret_cast<const tb_transfer_t*>(my + lane * kLdsEventStride);
-#if !TBG_INGEST_PREV_SHFL
-            const uint32_t up_flags =
-                lane > 0 ? reinterpret_cast<const tb_transfer_t*>(my + (lane - 1) * kLdsEventStride)->flags : 0u;
-#endif
             const bool prev_linked =
                 lane > 0 ? !first_of_batch && (up_flags & TB_TRANSFER_LINKED) != 0
                          : (w0 & kChunkPrevLinked) != 0;
@@ -1079,9 +1006,7 @@ __global__ void __launch_bounds__(kBlock, TBG_INGEST_WG_PER_CU) tr_ingest(Tables
             n_fast += fts != 0;
             ts_max = fts > ts_max ? fts : ts_max;
         }
-#if !TBG_INGEST_EARLY_PREFETCH
         if (next < c.n) load_chunk(next);
-#endif
         wave_lds_sync();  // the LDS image is rewritten by the next chunk
     }
     flags = block_reduce(flags, OpOr());  // (its barriers also order the histogram adds)
