@@ -553,7 +553,9 @@ struct SegmentLds {
 };
 
 // Sorts the c distinct values in[off, off + c) ascending into out[off, off + c) (one workgroup of
-// kGroupBigThreads; visible to the whole workgroup on return): bitmap windows of up to
+// kGroupBigThreads; visible to the whole workgroup on return -- a workgroup barrier: the callers'
+// other readers are later kernels. An agent-scope fence here wrote back the XCD's L2 once per
+// segment.): bitmap windows of up to
 // kGroupWindowBits values in LDS over the values' range -- set bits, prefix popcounts, enumerate --
 // or, for a sparse segment, an LDS bitonic sort of the values themselves.
 __device__ inline void segment_sort(const uint32_t* in, uint32_t* out, uint32_t off, uint32_t c,
@@ -626,8 +628,6 @@ __device__ inline void segment_sort(const uint32_t* in, uint32_t* out, uint32_t 
             placed += total;
             __syncthreads();
         }
-        __threadfence();
-        __syncthreads();
     };
     uint32_t lo = kNone32, hi = 0;
     if (bound && bound <= kGroupWindowBits && !values) {
@@ -682,7 +682,6 @@ __device__ inline void segment_sort(const uint32_t* in, uint32_t* out, uint32_t 
             }
         }
         for (uint32_t i = tid; i < c; i += kGroupBigThreads) out[off + i] = buf[i];
-        __threadfence();
         __syncthreads();
         return;
     }
