@@ -404,6 +404,9 @@ struct AeSnapJob {
     // read `created` from the speculation -- so the staging holds no created event (the side
     // stream's appends, already queued, find none) and the executor stages again after the replay.
     bool speculative;
+    // Mapped pinned word: the call's epoch when an event needs the general appends (the host reads
+    // it once the snapshot has completed and queues only the appends the staging needs), or null.
+    unsigned long long* host_general;
 };
 __device__ inline void ae_snapshot_one(const AeSnapJob& J, uint32_t k) {
     const Tables& T = J.T;
@@ -440,8 +443,12 @@ __device__ inline void ae_snapshot_one(const AeSnapJob& J, uint32_t k) {
     AeScratch D{};
     D.deltas = J.st.delta;
     const uint8_t status = ae_transfer_sides(D, k, t, p);
-    if (status != TB_PENDING_NONE || t.amount.hi != 0 || t.amount.lo >= kAeSmallAmountMax)
+    if (status != TB_PENDING_NONE || t.amount.hi != 0 || t.amount.lo >= kAeSmallAmountMax) {
         J.st.words[0] = c.epoch;  // (ae_small_emit leaves this call to the general appends)
+        if (J.host_general)
+            __hip_atomic_store(J.host_general, (unsigned long long)c.epoch, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     tb_account_event_t* rec = J.st.rec;
     ae_write_record(&rec[k], ae_final_of(T.acc_rows[dr]), ae_final_of(T.acc_rows[cr]), t.timestamp,
                     f, status, p, c.events[k].amount, t.amount, t.ledger);

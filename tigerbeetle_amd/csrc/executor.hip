@@ -244,6 +244,9 @@ struct tbg_ctx {
     bool ae_graph_deferred = false;
     uint32_t ae_def_parity = 0, ae_def_epoch = 0;
     bool ae_def_pending = false;
+    // The deferred appends are a small call's (not a pulse's): the pinned word h_pulse[4] says
+    // which appends its staging needs once its snapshot (stage_out) has completed.
+    bool ae_def_call = false;
     Call<tb_transfer_t> ae_call{};
     AeScratch ae{};
     uint64_t ae_touch_cap = 0;
@@ -1310,6 +1313,7 @@ int ae_defer_graph(tbg_ctx* ctx, uint32_t n, uint32_t epoch, bool pending) {
     ctx->ae_def_parity = p;
     ctx->ae_def_epoch = epoch;
     ctx->ae_def_pending = pending;
+    ctx->ae_def_call = false;
     ctx->ae_parity = p ^ 1;
     return 0;
 }
@@ -1318,9 +1322,15 @@ int ae_flush_graph(tbg_ctx* ctx) {
     ctx->ae_graph_deferred = false;
     const uint32_t p = ctx->ae_def_parity;
     HIP_TRY(ctx, hipStreamWaitEvent(ctx->ae_stream, ctx->ae_snap_ready[p], 0));
-    // (the pulse synchronised after its snapshot: the pinned word says which appends it needs)
+    // (the pulse synchronised after its snapshot: the pinned word says which appends it needs; a
+    // small call's snapshot has usually completed by the next call -- else every path is queued
+    // and the ones the staging does not need skip on device)
     const bool small_ok = ctx->ae_window_on && ctx->T.acc_rows_used <= kAeWinRowsMax;
-    const int which = !small_ok ? 0 : ctx->h_pulse[3] == ctx->ae_def_epoch ? 2 : 1;
+    int which = !small_ok ? 0 : ctx->h_pulse[3] == ctx->ae_def_epoch ? 2 : 1;
+    if (ctx->ae_def_call) {
+        const bool known = small_ok && hipEventQuery(ctx->ae_snap_ready[p]) == hipSuccess;
+        which = !known ? 0 : __atomic_load_n(&ctx->h_pulse[4], __ATOMIC_ACQUIRE) == ctx->ae_def_epoch ? 2 : 1;
+    }
     if (int rc = ae_launch_appends(ctx, p, ctx->ae_def_epoch, ctx->ae_def_pending, which)) return rc;
     HIP_TRY(ctx, hipEventRecord(ctx->ae_done[p], ctx->ae_stream));
     ctx->ae_done_recorded[p] = true;
@@ -2219,15 +2229,23 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
         // counted (the host's wait ends at the sequence word): final unless a replay follows, then
         // it stages nothing. Its appends are queued on the side stream now, so that the host's
         // launch calls overlap the call's kernels.
+        // (the appends themselves are queued at the next call's start, ae_flush_all, when the
+        // snapshot has told the host which of them the staging needs: one launch instead of the
+        // general path's seven that skip)
         AeSnapJob J;
         if (snap) {
             rc = ae_snap_job(ctx, c, &J);
             J.speculative = true;
+            ctx->h_pulse[4] = 0;
+            J.host_general = ctx->dh_pulse + 4;
         }
         if (!rc)
             rc = stage_call_outputs(ctx, d_results, dst, dst ? n : 0, true, snap ? &J : nullptr,
                                     true, seq, finish ? c.epoch : 0u);
-        if (!rc && snap) rc = ae_launch_graph(ctx, n, c.epoch);
+        if (!rc && snap) {
+            rc = ae_defer_graph(ctx, n, c.epoch, false);
+            ctx->ae_def_call = true;
+        }
         ctx->ae_snap_early = snap && !rc;
         if (!rc) rc = spin ? spin_wait(ctx, seq)
                            : (hip_ok(ctx, hipStreamSynchronize(ctx->stream), "sync") ? 0 : TBG_EHIP);
