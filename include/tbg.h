@@ -252,8 +252,9 @@ typedef struct tbg_stats {
     uint64_t replayed;     /* executed by the ordered replay */
     uint64_t static_fail;  /* failed on checks that depend on no in-call state */
     uint64_t ae_window;    /* the call's AccountEvents in one pass: 1 balance-window emit, 2 dense
-                            * emit (general calls, dense key spaces); 0 the general appends or the
-                            * side stream (small calls) */
+                            * emit (general calls, dense key spaces), 3 balance-window emit with
+                            * u128 sums (wide amounts); 0 the general appends or the side stream
+                            * (small calls) */
     uint64_t ingest_finished;  /* 1: the call ended in tr_ingest's last workgroup (a small call
                                 * whose events were all FAST: no tr_commit or stage_out work) */
 } tbg_stats;

@@ -388,6 +388,59 @@ def test_account_events_window(case, monkeypatch):
         p.close()
 
 
+@pytest.mark.parametrize("case", ["wide", "wide-skew", "carry"])
+def test_account_events_window_wide(case):
+    """AccountEvents of balance-window calls with wide amounts in one pass (events.hpp ae_wide_*:
+    u128 sums, the emit's rounds from the last one back): `wide`: amounts log-uniform below 2^63
+    and 1 % of them within 2^20 of 2^64 (slice sums past 2^64 in the partials' third limb);
+    `wide-skew`: the same amounts with 90 % of the touches on 8 accounts (long round lists, later
+    sums near 2^80); `carry`: packed amounts of ~2^30 on 8 hot accounts (no wide item, a window
+    key's sum past 2^32: kFlagWideSums). Statically failed events between the created ones, small
+    calls and a pulse between the window calls; the log compared with the oracle's byte for byte."""
+    rng = np.random.default_rng(78)
+    n_acc = 10_000
+    p = Pair(account_capacity=1 << 14, transfer_capacity=1 << 20, batch_events_max=1 << 17,
+             pulse_batch_max=64, pulse_next_timestamp_init=TIMESTAMP_MAX)
+    try:
+        acc = workload.accounts(n_acc, seed=4)
+        p.create_accounts(acc, _split(n_acc, rng, 8189))
+        off = 0
+        paths = []
+        for call in range(3):
+            n = 70_000 + 13_333 * call  # (slices of 16,384 events: the last one partial)
+            t = workload.transfers_uniform(n, n_acc, seed=300 + call, id_offset=off,
+                                           amounts="exp" if case == "carry" else "wide")
+            off += n
+            if case in ("wide-skew", "carry"):
+                hot = rng.random(n) < 0.9
+                t["debit_account_id"][hot, 0] = rng.integers(1, 5, size=int(hot.sum()))
+                hot = rng.random(n) < 0.9
+                t["credit_account_id"][hot, 0] = rng.integers(5, 9, size=int(hot.sum()))
+            if case == "carry":
+                t["amount"][:, 0] = rng.integers(1 << 29, 1 << 30, size=n, dtype=np.uint64)
+            else:
+                top = rng.random(n) < 0.01
+                t["amount"][top, 0] = np.uint64(2**64 - 1) - rng.integers(0, 1 << 20, size=int(top.sum()), dtype=np.uint64)
+            fail = rng.random(n)
+            t["id"][fail < 0.01] = 0                                    # id_must_not_be_zero
+            same = (fail >= 0.01) & (fail < 0.02)
+            t["credit_account_id"][same] = t["debit_account_id"][same]  # accounts_must_be_different
+            r = p.create_transfers(t, _split(n, rng, 8189))
+            assert (r["status"] == 0xFFFFFFFF).mean() > 0.95
+            paths.append(p.last_stats["ae_window"])
+            s = workload.transfers_uniform(3_000, n_acc, seed=400 + call, id_offset=off)
+            off += 3_000
+            s["flags"][rng.random(3_000) < 0.2] |= 2
+            s["timeout"][s["flags"] & 2 != 0] = 1
+            p.create_transfers(s, _split(3_000, rng, 1000))
+            p.tick(2 * NS_PER_S)
+        assert paths == [3] * 3  # (3: the wide window emit)
+        p.compare_state()
+        assert len(p.change_events()) > 0
+    finally:
+        p.close()
+
+
 @pytest.mark.parametrize("case", ["dense", "closing", "wide", "no-window"])
 def test_account_events_dense(case, monkeypatch):
     """AccountEvents of general calls in one pass (events.hpp ae_dense_*): calls of > 8,192 events

@@ -1062,6 +1062,51 @@ __device__ inline uint4 ae_sub_u32(uint4 balance, uint32_t d) {
 // 1024 lanes at most 128 registers each, spills with a batch: it keeps one group at a time.)
 constexpr uint32_t kAeRecBatch = 4;
 
+// The end of a one-pass emit's workgroup (slice w; every thread calls it): the slice's first and
+// last created timestamps (ts_lds: LDS words set to ~0 / 0 before a barrier); the last workgroup to
+// finish closes the block -- the log's length, its last timestamp and whether the block broke the
+// log's timestamp order.
+__device__ inline void ae_slices_close(uint64_t ts_min, uint64_t ts_max, unsigned long long* ts_lds,
+                                       unsigned long long* slice_ts, const unsigned int* slice_count,
+                                       unsigned int* done, unsigned long long* state, uint64_t used,
+                                       uint32_t w) {
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t a = __shfl_xor(ts_min, off), b = __shfl_xor(ts_max, off);
+        ts_min = a < ts_min ? a : ts_min;
+        ts_max = b > ts_max ? b : ts_max;
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMin(&ts_lds[0], ts_min);
+        atomicMax(&ts_lds[1], ts_max);
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    slice_ts[2 * w] = ts_lds[0];
+    slice_ts[2 * w + 1] = ts_lds[1];
+    __threadfence();
+    if (atomicAdd(done, 1u) != gridDim.x - 1) return;
+    __threadfence();
+    uint64_t total = 0, first = 0, last = 0;
+    bool any = false;
+    const volatile unsigned int* counts = slice_count;  // (other workgroups' words: no cached copy)
+    const volatile unsigned long long* sts = slice_ts;
+    for (uint32_t j = 0; j < gridDim.x; j++) {
+        const uint32_t cj = counts[j];
+        if (!cj) continue;
+        const uint64_t f = sts[2 * j], l = sts[2 * j + 1];
+        if (!any) first = f;
+        any = true;
+        last = l;
+        total += cj;
+    }
+    if (total) {
+        if (used && first <= state[1]) state[2] = 1;
+        if (last > state[1]) state[1] = last;
+        state[0] = used + total;
+    }
+    *done = 0;
+}
+
 __global__ void __launch_bounds__(kAeWinThreads) ae_window_emit(AeWindow W) {
     __shared__ uint32_t Rd[kAeWinRowsMax];    // debits_posted deltas of the events from the round on
     __shared__ uint32_t Rc[kAeWinRowsMax];    // credits_posted
@@ -1203,42 +1248,306 @@ __global__ void __launch_bounds__(kAeWinThreads) ae_window_emit(AeWindow W) {
         pos += round_total;
         __syncthreads();  // (the lists are empty and R is current for the next round)
     }
-    // The slice's first and last created timestamps; the last workgroup closes the block.
-    for (int off = 32; off > 0; off >>= 1) {
-        const uint64_t a = __shfl_xor(ts_min, off), b = __shfl_xor(ts_max, off);
-        ts_min = a < ts_min ? a : ts_min;
-        ts_max = b > ts_max ? b : ts_max;
+    ae_slices_close(ts_min, ts_max, ts_lds, W.slice_ts, W.slice_count, W.done, W.state, used, w);
+}
+
+// ---- AccountEvents of window calls with wide amounts -----------------------------------------
+//
+// A balance-window call whose created events are all plain single-phase FAST events (as for
+// ae_window_emit) but whose amounts do not fit its u32 later-sums: a wide item (an amount too wide
+// to pack, kFlagWideItems) or a window key's sum of 2^32 or more (kFlagWideSums). A call's later
+// deltas of one account reach 2^70 and more, so the per-account state is u128 and lives in HBM, not
+// LDS:
+//   ae_wide_partials  per slice of kAeWideSlice events and posted field (a workgroup each), the
+//                     field's sum per account in three u32 LDS limbs (2^96: 2^14 events of < 2^64)
+//   ae_wide_suffix    per account and field, the exclusive suffix over the slices: sums[w] = the
+//                     deltas of slices w + 1, w + 2, ... (u128)
+//   ae_wide_emit      per slice, its rounds of 1024 events from the LAST one back: R = sums[w] (the
+//                     slice's own region, updated in place) holds the deltas after the round; the
+//                     round's touch lists (LDS, as in ae_window_emit) give the deltas of the round's
+//                     events after e, and the list's head owner adds the round's deltas to R before
+//                     the round before it. A record's posted balances are the final ones less
+//                     R + those (u128); records are written once, in call order (positions from a
+//                     count of the slice's created events per round and wave).
+// account_event :4384-4465 (the balances after the event), as ae_window_emit.
+constexpr uint32_t kAeWideThreads = 1024;
+constexpr uint32_t kAeWideRounds = 16;
+constexpr uint32_t kAeWideSlice = kAeWideThreads * kAeWideRounds;
+constexpr uint32_t kAeWideWaves = kAeWideThreads / 64;
+
+struct AeWide {
+    const uint64_t* items;               // the call's pair items (~0: none)
+    const uint64_t* amounts;             // ev_amount: a wide item's amount
+    const tb_create_result_t* results;
+    const tb_account_t* acc_rows;
+    uint32_t n, ps, rows, slices;
+    uint64_t row_base;
+    u128* sums;                          // [slice][field][row]: partials, suffix sums, then R
+    unsigned int* slice_count;           // per slice: its created events
+    unsigned long long* slice_ts;        // per slice: its first and last created timestamp
+    unsigned int* done;                  // finished emit workgroups (the last one closes the block)
+    tb_account_event_t* log;
+    AeRef* refs;
+    unsigned long long* state;           // the log on device (AeScratch::state)
+    uint64_t cap;
+};
+
+__device__ inline void ae_wide_item(const AeWide& A, uint32_t e, uint64_t x, uint32_t* dr,
+                                    uint32_t* cr, uint64_t* amount) {
+    const uint64_t rmask = (1ull << A.ps) - 1;
+    *dr = uint32_t(x & rmask);
+    *cr = uint32_t((x >> A.ps) & rmask);
+    const uint64_t a = x >> (2 * A.ps + 1);
+    *amount = a == pair_amount_mask(A.ps) ? A.amounts[e] : a;
+}
+
+// Workgroup 2 w + f: slice w's sums of field f (0 debits_posted, 1 credits_posted) per account.
+__global__ void __launch_bounds__(kAeWideThreads) ae_wide_partials(AeWide A) {
+    __shared__ uint32_t lo[kAeWinRowsMax], hi[kAeWinRowsMax], top[kAeWinRowsMax];
+    __shared__ uint32_t wave_cnt[kAeWideWaves];
+    const uint32_t tid = threadIdx.x, w = blockIdx.x >> 1, f = blockIdx.x & 1;
+    for (uint32_t r = tid; r < A.rows; r += kAeWideThreads) {
+        lo[r] = 0;
+        hi[r] = 0;
+        top[r] = 0;
     }
-    if (lane == 0) {
-        atomicMin(&ts_lds[0], ts_min);
-        atomicMax(&ts_lds[1], ts_max);
+    const uint32_t b0 = w * kAeWideSlice;
+    const uint32_t b1 = b0 + kAeWideSlice < A.n ? b0 + kAeWideSlice : A.n;
+    uint64_t x[kAeWideRounds];
+#pragma unroll
+    for (uint32_t r = 0; r < kAeWideRounds; r++) {
+        const uint32_t e = b0 + r * kAeWideThreads + tid;
+        x[r] = e < b1 ? A.items[e] : ~0ull;
     }
     __syncthreads();
-    if (tid != 0) return;
-    W.slice_ts[2 * w] = ts_lds[0];
-    W.slice_ts[2 * w + 1] = ts_lds[1];
-    __threadfence();
-    if (atomicAdd(W.done, 1u) != gridDim.x - 1) return;
-    __threadfence();
-    uint64_t total = 0, first = 0, last = 0;
-    bool any = false;
-    const volatile unsigned int* counts = W.slice_count;  // (other workgroups' words: no cached copy)
-    const volatile unsigned long long* sts = W.slice_ts;
-    for (uint32_t j = 0; j < gridDim.x; j++) {
-        const uint32_t cj = counts[j];
-        if (!cj) continue;
-        const uint64_t f = sts[2 * j], l = sts[2 * j + 1];
-        if (!any) first = f;
-        any = true;
-        last = l;
-        total += cj;
+    uint32_t cnt = 0;
+#pragma unroll
+    for (uint32_t r = 0; r < kAeWideRounds; r++) {
+        if (x[r] == ~0ull) continue;
+        cnt++;
+        uint32_t dr, cr;
+        uint64_t a;
+        ae_wide_item(A, b0 + r * kAeWideThreads + tid, x[r], &dr, &cr, &a);
+        const uint32_t row = f ? cr : dr;
+        const uint32_t alo = uint32_t(a);
+        const uint32_t old = atomicAdd(&lo[row], alo);
+        const uint64_t h = (a >> 32) + (uint32_t(old + alo) < old ? 1u : 0u);
+        if (h) {
+            const uint32_t oh = atomicAdd(&hi[row], uint32_t(h));
+            const uint32_t t = uint32_t(h >> 32) + (uint32_t(oh + uint32_t(h)) < oh ? 1u : 0u);
+            if (t) atomicAdd(&top[row], t);
+        }
     }
-    if (total) {
-        if (used && first <= W.state[1]) W.state[2] = 1;
-        if (last > W.state[1]) W.state[1] = last;
-        W.state[0] = used + total;
+    for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
+    if ((tid & 63) == 0) wave_cnt[tid >> 6] = cnt;
+    __syncthreads();
+    if (f == 0 && tid == 0) {
+        uint32_t t = 0;
+        for (uint32_t j = 0; j < kAeWideWaves; j++) t += wave_cnt[j];
+        A.slice_count[w] = t;
     }
-    *W.done = 0;
+    u128* out = A.sums + uint64_t(blockIdx.x) * A.rows;
+    for (uint32_t r = tid; r < A.rows; r += kAeWideThreads)
+        out[r] = (u128(top[r]) << 64) | (uint64_t(hi[r]) << 32) | lo[r];
+}
+
+// One lane per (field, account) key: sums[w][key] = the key's sums over the slices after w.
+__global__ void ae_wide_suffix(AeWide A) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= 2 * A.rows) return;
+    const uint64_t stride = 2 * uint64_t(A.rows);
+    u128* p = A.sums + k;
+    u128 s = 0;
+    int64_t w = int64_t(A.slices) - 1;
+    for (; w >= 7; w -= 8) {  // (eight loads in flight)
+        u128 v[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) v[j] = p[uint64_t(w - j) * stride];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            p[uint64_t(w - j) * stride] = s;
+            s += v[j];
+        }
+    }
+    for (; w >= 0; w--) {
+        const u128 v = p[uint64_t(w) * stride];
+        p[uint64_t(w) * stride] = s;
+        s += v;
+    }
+}
+
+__global__ void __launch_bounds__(kAeWideThreads) ae_wide_emit(AeWide A) {
+    __shared__ uint32_t head[kAeWinRowsMax];          // the round's touch lists (node 2e + side)
+    __shared__ uint16_t next[2 * kAeWideThreads];
+    __shared__ uint64_t amt[kAeWideThreads];
+    __shared__ uint4 later[kAeWideThreads][4];        // dr debits / credits, cr debits / credits
+    __shared__ uint32_t offs[kAeWideRounds * kAeWideWaves];  // a round's wave's first record
+    __shared__ uint32_t red[2][kAeWideWaves];
+    __shared__ unsigned long long ts_lds[2];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, w = blockIdx.x;
+    const uint32_t b0 = w * kAeWideSlice;
+    const uint32_t b1 = b0 + kAeWideSlice < A.n ? b0 + kAeWideSlice : A.n;
+    const uint32_t rounds = (b1 - b0 + kAeWideThreads - 1) / kAeWideThreads;
+    // created events of the earlier slices; of all (the room in the log: else nothing is written)
+    uint32_t before = 0, all = 0;
+    for (uint32_t j = tid; j < A.slices; j += kAeWideThreads) {
+        before += j < w ? A.slice_count[j] : 0;
+        all += A.slice_count[j];
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        before += __shfl_xor(before, off);
+        all += __shfl_xor(all, off);
+    }
+    if (lane == 0) {
+        red[0][wv] = before;
+        red[1][wv] = all;
+    }
+    // the slice's created events per round and wave
+    for (uint32_t r = 0; r < kAeWideRounds; r++) {
+        const uint32_t e = b0 + r * kAeWideThreads + tid;
+        const bool valid = r < rounds && e < b1 && A.items[e] != ~0ull;
+        const uint64_t bal = __ballot(valid);
+        if (lane == 0) offs[r * kAeWideWaves + wv] = uint32_t(__popcll(bal));
+    }
+    for (uint32_t a = tid; a < A.rows; a += kAeWideThreads) head[a] = kAeWinNil;
+    if (tid == 0) {
+        ts_lds[0] = ~0ull;
+        ts_lds[1] = 0;
+    }
+    const uint64_t used = A.state[0];
+    __syncthreads();
+    uint64_t total = 0, pos = used;
+    for (uint32_t j = 0; j < kAeWideWaves; j++) {
+        pos += red[0][j];
+        total += red[1][j];
+    }
+    if (!ae_room(A.state, A.cap, total)) {
+        if (tid == 0) A.state[3] = 1;
+        return;
+    }
+    // exclusive scan of the (round, wave) counts: 256 entries, one per lane of waves 0-3
+    static_assert(kAeWideRounds * kAeWideWaves == 256, "one scan entry per lane of four waves");
+    uint32_t v = tid < 256 ? offs[tid] : 0, inc = v;
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t t = __shfl_up(inc, off, 64);
+        if (lane >= uint32_t(off)) inc += t;
+    }
+    __syncthreads();  // (every count read; red reused)
+    if (tid < 256 && lane == 63) red[0][wv] = inc;
+    __syncthreads();
+    if (tid < 256) {
+        uint32_t base = 0;
+        for (uint32_t j = 0; j < wv; j++) base += red[0][j];
+        offs[tid] = base + inc - v;
+    }
+    __syncthreads();
+    u128* R = A.sums + uint64_t(w) * 2 * A.rows;  // [0, rows) debits_posted, [rows, 2 rows) credits
+    uint64_t ts_min = ~0ull, ts_max = 0;
+    for (int32_t r = int32_t(rounds) - 1; r >= 0; r--) {
+        const uint32_t e = b0 + uint32_t(r) * kAeWideThreads + tid;
+        const uint64_t x = e < b1 ? A.items[e] : ~0ull;
+        const bool valid = x != ~0ull;
+        uint32_t dr = 0, cr = 0;
+        uint64_t a = 0, ts = 0;
+        if (valid) {
+            ae_wide_item(A, e, x, &dr, &cr, &a);
+            ts = A.results[e].timestamp;
+            next[2 * tid] = uint16_t(atomicExch(&head[dr], 2 * tid));
+            next[2 * tid + 1] = uint16_t(atomicExch(&head[cr], 2 * tid + 1));
+            amt[tid] = a;
+        }
+        const uint64_t bal = __ballot(valid);
+        __syncthreads();
+        // Per side: the account's R (deltas after the round), the round's deltas after e, and --
+        // for the list's head owner -- the round's total, which it adds to R after every read.
+        u128 Rd[2] = {0, 0}, Rc[2] = {0, 0}, td[2] = {0, 0}, tc[2] = {0, 0};
+        bool own[2] = {false, false};
+        if (valid) {
+#pragma unroll
+            for (int side = 0; side < 2; side++) {
+                const uint32_t acc = side ? cr : dr;
+                Rd[side] = R[acc];
+                Rc[side] = R[A.rows + acc];
+            }
+#pragma unroll
+            for (int side = 0; side < 2; side++) {
+                const uint32_t acc = side ? cr : dr;
+                const uint32_t h = head[acc];
+                own[side] = h == 2 * tid + side;
+                u128 ad = 0, ac = 0;
+                for (uint32_t nd = h; nd != kAeWinNil;) {
+                    const u128 val = amt[nd >> 1];
+                    const bool after = (nd >> 1) > tid;
+                    if (nd & 1) {
+                        tc[side] += val;
+                        ac += after ? val : u128(0);
+                    } else {
+                        td[side] += val;
+                        ad += after ? val : u128(0);
+                    }
+                    const uint32_t nx = next[nd];
+                    nd = nx == 0xFFFFu ? kAeWinNil : nx;
+                }
+                later[tid][2 * side] = ae_q(Rd[side] + ad);
+                later[tid][2 * side + 1] = ae_q(Rc[side] + ac);
+            }
+        }
+        __syncthreads();  // (every R read and list walked before the round's updates)
+        if (valid) {
+#pragma unroll
+            for (int side = 0; side < 2; side++) {
+                if (!own[side]) continue;
+                const uint32_t acc = side ? cr : dr;
+                R[acc] = Rd[side] + td[side];
+                R[A.rows + acc] = Rc[side] + tc[side];
+                head[acc] = kAeWinNil;
+            }
+            ts_min = ts < ts_min ? ts : ts_min;
+            ts_max = ts > ts_max ? ts : ts_max;
+        }
+        const uint64_t wave_pos = pos + offs[uint32_t(r) * kAeWideWaves + wv];
+        if (valid) {
+            const uint32_t rank = lane ? __popcll(bal & (~0ull >> (64 - lane))) : 0;
+            ae_nt_store(reinterpret_cast<uint4*>(&A.refs[wave_pos + rank]),
+                        make_uint4(uint32_t(A.row_base + e), dr, cr, 0));
+        }
+        // The wave's records, four at a time, as in ae_window_emit (lane L writes word L % 16 of
+        // the record of event lane 4 j + L / 16); the later sums come from LDS.
+        const uint32_t wd = lane & 15, sub = lane >> 4;
+        const bool credit_half = (wd >= 5 && wd < 10) || wd == 11;
+        const uint32_t k = wd < 5 ? wd : wd < 10 ? wd - 5 : 7;
+        for (uint32_t j = 0; j < 16; j++) {
+            if (((bal >> (4 * j)) & 0xF) == 0) continue;  // (wave-uniform)
+            const uint32_t src = 4 * j + sub;
+            const uint32_t s_dr = __shfl(dr, src), s_cr = __shfl(cr, src);
+            const uint32_t a_lo = __shfl(uint32_t(a), src), a_hi = __shfl(uint32_t(a >> 32), src);
+            const uint32_t ts_lo = __shfl(uint32_t(ts), src), ts_hi = __shfl(uint32_t(ts >> 32), src);
+            const bool vv = (bal >> src) & 1;
+            uint4 q = make_uint4(0, 0, 0, 0);
+            if (vv) q = reinterpret_cast<const uint4*>(&A.acc_rows[credit_half ? s_cr : s_dr])[k];
+            const uint32_t dflags = __shfl(q.y, lane > 0 ? lane - 1 : 0);
+            if (!vv) continue;
+            uint4 o = q;
+            if (k == 2 || k == 4) {
+                const uint4 l = later[wv * 64 + src][(credit_half ? 2 : 0) + (k == 4 ? 1 : 0)];
+                o = ae_q(ae_u(q) - ae_u(l));
+            } else if (wd == 10) {
+                o = make_uint4(ts_lo, ts_hi, q.z, q.w);
+            } else if (wd == 11) {
+                o = make_uint4(q.z, q.w, (dflags >> 16) | (q.y & 0xFFFF0000u), 0u);
+            } else if (wd == 12) {
+                o = make_uint4(0, 0, 0, 0);
+            } else if (wd == 13 || wd == 14) {
+                o = make_uint4(a_lo, a_hi, 0, 0);
+            } else if (wd == 15) {
+                o = make_uint4(q.x, uint32_t(TB_PENDING_NONE), 0, 0);
+            }
+            const uint64_t at = wave_pos + uint64_t(__popcll(bal & ((1ull << src) - 1)));
+            ae_nt_store(reinterpret_cast<uint4*>(&A.log[at]) + wd, o);
+        }
+        __syncthreads();  // (R current and the lists empty for the round before)
+    }
+    ae_slices_close(ts_min, ts_max, ts_lds, A.slice_ts, A.slice_count, A.done, A.state, used, w);
 }
 
 // ---- AccountEvents of small calls in one pass ----------------------------------------------------

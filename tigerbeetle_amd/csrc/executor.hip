@@ -284,6 +284,12 @@ struct tbg_ctx {
     uint32_t* ae_dense_pos = nullptr;
     unsigned int* ae_dense_fail = nullptr;
     unsigned long long* ae_small_ts = nullptr;
+    // ae_wide_* scratch (grown to the largest wide window call): per slice, field and account
+    u128* ae_wide_sums = nullptr;
+    uint64_t ae_wide_sums_cap = 0;
+    unsigned int* ae_wide_counts = nullptr;      // per slice; [ae_wide_slices_cap]: done
+    unsigned long long* ae_wide_ts = nullptr;
+    uint32_t ae_wide_slices_cap = 0;
     unsigned long long* flow_debug = nullptr;
 
     // Per-kernel timing (tbg_profile): HIP events recorded on the call's stream between launches.
@@ -1359,10 +1365,10 @@ int ae_transfers_async(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
 // AccountEvents of a balance-window call in one pass (events.hpp, ae_window_emit), when the call
 // qualifies: its window partials are still current (nothing ran since), no replay ran, and no
 // flag says an event or a sum is outside what the window emit tracks. Returns 1 when not taken.
+int ae_window_wide(tbg_ctx* ctx, const Call<tb_transfer_t>& c);
 int ae_window(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
     const DevScalars& h = *ctx->h_scalars;
-    constexpr unsigned int kNot = kFlagChain | kFlagPostVoid | kFlagImported | kFlagAeSlow |
-                                  kFlagWideSums;
+    constexpr unsigned int kNot = kFlagChain | kFlagPostVoid | kFlagImported | kFlagAeSlow;
     if (ctx->win.epoch != c.epoch || ctx->epoch != c.epoch || (h.flags & kNot) || h.stats[0] ||
         ctx->T.acc_rows_used > kAeWinRowsMax || !ctx->ae_window_on)
         return 1;
@@ -1371,6 +1377,7 @@ int ae_window(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
         if (int rc = ae_settle(ctx)) return rc;
         if (ctx->ae_used + c.n > ctx->ae_cap) return 1;  // (the general path counts exactly)
     }
+    if (h.flags & (kFlagWideItems | kFlagWideSums)) return ae_window_wide(ctx, c);
     AeWindow W{};
     W.items = ctx->bal_items;
     W.results = c.results;
@@ -1397,6 +1404,63 @@ int ae_window(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
     HIP_TRY(ctx, hipGetLastError());
     ctx->win.epoch = 0;  // (the partials are suffix sums now)
     ctx->stats.ae_window = 1;
+    ctx->ae_bound += c.n;
+    ctx->ae_pending = true;
+    return 0;
+}
+
+// AccountEvents of a balance-window call whose amounts or sums are too wide for ae_window_emit's
+// u32 later-sums (events.hpp, ae_wide_*): per-slice sums, their suffix over the slices, and the
+// emit's rounds from the last one back with the account state in HBM. ae_window checked the rest.
+int ae_window_wide(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
+    const uint32_t rows = uint32_t(ctx->T.acc_rows_used);
+    const uint32_t slices = (c.n + kAeWideSlice - 1) / kAeWideSlice;
+    const uint64_t words = 2 * uint64_t(slices) * std::max<uint32_t>(rows, 1);
+    if (words > ctx->ae_wide_sums_cap) {
+        if (ctx->ae_wide_sums) HIP_TRY(ctx, hipFree(ctx->ae_wide_sums));
+        ctx->ae_wide_sums = nullptr;
+        ctx->ae_wide_sums_cap = 0;
+        if (!dev_alloc(ctx, &ctx->ae_wide_sums, words, false)) return TBG_ENOMEM;
+        ctx->ae_wide_sums_cap = words;
+    }
+    if (slices > ctx->ae_wide_slices_cap) {
+        for (void* q : {(void*)ctx->ae_wide_counts, (void*)ctx->ae_wide_ts})
+            if (q) HIP_TRY(ctx, hipFree(q));
+        ctx->ae_wide_counts = nullptr;
+        ctx->ae_wide_ts = nullptr;
+        ctx->ae_wide_slices_cap = 0;
+        if (!(dev_alloc(ctx, &ctx->ae_wide_counts, slices + 1, true) &&
+              dev_alloc(ctx, &ctx->ae_wide_ts, 2 * uint64_t(slices), false)))
+            return TBG_ENOMEM;
+        ctx->ae_wide_slices_cap = slices;
+    }
+    AeWide A{};
+    A.items = ctx->bal_items;
+    A.amounts = c.ev_amount;
+    A.results = c.results;
+    A.acc_rows = ctx->T.acc_rows;
+    A.n = c.n;
+    A.ps = ctx->win.ps;
+    A.rows = rows;
+    A.slices = slices;
+    A.row_base = c.row_base;
+    A.sums = ctx->ae_wide_sums;
+    A.slice_count = ctx->ae_wide_counts;
+    A.slice_ts = ctx->ae_wide_ts;
+    A.done = ctx->ae_wide_counts + ctx->ae_wide_slices_cap;
+    A.log = ctx->ae_log;
+    A.refs = ctx->ae_ref;
+    A.state = ctx->ae_words + 4;
+    A.cap = ctx->ae_cap;
+    tmark(ctx, "-account_events");
+    hipLaunchKernelGGL(ae_wide_partials, dim3(2 * slices), dim3(kAeWideThreads), 0, ctx->stream, A);
+    hipLaunchKernelGGL(ae_wide_suffix, dim3((2 * rows + kBlock - 1) / kBlock), dim3(kBlock), 0,
+                       ctx->stream, A);
+    hipLaunchKernelGGL(ae_wide_emit, dim3(slices), dim3(kAeWideThreads), 0, ctx->stream, A);
+    tmark(ctx, "account_events");
+    HIP_TRY(ctx, hipGetLastError());
+    ctx->win.epoch = 0;
+    ctx->stats.ae_window = 3;
     ctx->ae_bound += c.n;
     ctx->ae_pending = true;
     return 0;
@@ -1995,7 +2059,8 @@ void tbg_close(tbg_ctx* ctx) {
     for (void* q : {(void*)ctx->ae_small_counts, (void*)ctx->ae_small_ts, (void*)ctx->ae_dense_touch,
                     (void*)ctx->ae_dense_ev, (void*)ctx->ae_dense_partials,
                     (void*)ctx->ae_dense_counts, (void*)ctx->ae_dense_ts, (void*)ctx->ae_dense_fail,
-                    (void*)ctx->ae_dense_later, (void*)ctx->ae_dense_pos})
+                    (void*)ctx->ae_dense_later, (void*)ctx->ae_dense_pos, (void*)ctx->ae_wide_sums,
+                    (void*)ctx->ae_wide_counts, (void*)ctx->ae_wide_ts})
         if (q) (void)hipFree(q);
     free_ae_scratch(ctx->ae_g);
     if (ctx->ae_stream) (void)hipStreamDestroy(ctx->ae_stream);

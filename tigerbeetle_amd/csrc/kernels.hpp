@@ -678,9 +678,8 @@ __device__ inline unsigned int ingest_event(const Tables& T, const Call<tb_trans
             const uint32_t ps = c.pair_shift;
             ae_slow = pending;  // (the AccountEvents window tracks posted balances only)
             // (too wide to pack: a wide item, its amount in ev_amount -- the event is not lean --
-            // which the AccountEvents window does not take)
+            // which the AccountEvents window takes with u128 sums, ae_wide_*)
             const bool packed = item_packable(c, amount);
-            ae_slow |= !packed;
             wide_item = !packed;
             c.bal_items[k] = ((packed ? amount : pair_amount_mask(ps)) << (2 * ps + 1)) |
                              (uint64_t(pending) << (2 * ps)) | (uint64_t(cr.row) << ps) | dr.row;
@@ -1816,11 +1815,14 @@ __global__ void __launch_bounds__(kWindowThreads) bal_window_accumulate(
     auto add_wide = [&](uint32_t row, uint64_t amount) {  // field wf, row < kWindowHalf
         const uint32_t lo = uint32_t(amount);
         const uint32_t old = atomicAdd(&lo_acc[row], lo);
-        const uint32_t hi = uint32_t(amount >> 32) + (uint32_t(old + lo) < old ? 1u : 0u);
+        // (u64: an amount's high word 2^32 - 1 plus the low word's carry is 2^32)
+        const uint64_t hi = (amount >> 32) + (uint32_t(old + lo) < old ? 1u : 0u);
         if (hi) {
-            const uint32_t old_hi = atomicAdd(&hi_acc[row], hi);
-            if (uint32_t(old_hi + hi) < old_hi)  // (2^64)
-                atomicAdd(&carry[(wf << ps) | row], 1ull << 32);
+            const uint32_t h = uint32_t(hi);
+            const uint32_t old_hi = h ? atomicAdd(&hi_acc[row], h) : 0u;
+            const uint32_t wraps = uint32_t(hi >> 32) + (uint32_t(old_hi + h) < old_hi ? 1u : 0u);
+            if (wraps)  // (2^64 each)
+                atomicAdd(&carry[(wf << ps) | row], (unsigned long long)wraps << 32);
         }
     };
     auto item = [&](uint64_t x, uint32_t e) {
