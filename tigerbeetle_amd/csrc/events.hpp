@@ -1056,10 +1056,11 @@ __device__ inline uint4 ae_sub_u32(uint4 balance, uint32_t d) {
     return ae_q(ae_u(balance) - u128(d));
 }
 
-// Record groups whose loads issue together in ae_small_emit and ae_dense_emit: every row / staged
-// word load of a batch goes out before its stores (the compiler cannot tell the log from the rows
-// it reads, so one group at a time paid a full load latency per four records). (ae_window_emit,
-// 1024 lanes at most 128 registers each, spills with a batch: it keeps one group at a time.)
+// Record groups whose loads issue together in the emits: every row / staged word load of a batch
+// goes out before its stores (the compiler cannot tell the log from the rows it reads, so one group
+// at a time paid a full load latency per four records). (ae_window_emit / ae_wide_emit, 1024 lanes
+// at most 128 registers each, keep their loop over the batches rolled: ae_window_emit 722 -> 683 us
+// per 10M events.)
 constexpr uint32_t kAeRecBatch = 4;
 
 // The end of a one-pass emit's workgroup (slice w; every thread calls it): the slice's first and
@@ -1219,31 +1220,43 @@ __global__ void __launch_bounds__(kAeWinThreads) ae_window_emit(AeWindow W) {
         const uint32_t wd = lane & 15, sub = lane >> 4;
         const bool credit_half = (wd >= 5 && wd < 10) || wd == 11;
         const uint32_t k = wd < 5 ? wd : wd < 10 ? wd - 5 : 7;
-        for (uint32_t j = 0; j < 16; j++) {
-            if (((bal >> (4 * j)) & 0xF) == 0) continue;  // (wave-uniform)
-            const uint32_t src = 4 * j + sub;
-            const uint32_t s_dr = __shfl(dr, src), s_cr = __shfl(cr, src), s_a = __shfl(a, src);
-            // (a shuffle reads the source lane's value of the expression: select after it)
-            const uint32_t l0 = __shfl(later[0], src), l1 = __shfl(later[1], src);
-            const uint32_t l2 = __shfl(later[2], src), l3 = __shfl(later[3], src);
-            const uint32_t l_dpo = credit_half ? l2 : l0, l_cpo = credit_half ? l3 : l1;
-            const uint32_t ts_lo = __shfl(uint32_t(ts), src), ts_hi = __shfl(uint32_t(ts >> 32), src);
-            const bool v = (bal >> src) & 1;
-            uint4 q = make_uint4(0, 0, 0, 0);
-            if (v) q = reinterpret_cast<const uint4*>(&W.acc_rows[credit_half ? s_cr : s_dr])[k];
-            // word 11 takes the debit account's flags from word 10's lane (its row word 7)
-            const uint32_t dflags = __shfl(q.y, lane > 0 ? lane - 1 : 0);
-            if (!v) continue;
-            uint4 o = q;
-            if (k == 2) o = ae_sub_u32(q, l_dpo);
-            else if (k == 4) o = ae_sub_u32(q, l_cpo);
-            else if (wd == 10) o = make_uint4(ts_lo, ts_hi, q.z, q.w);
-            else if (wd == 11) o = make_uint4(q.z, q.w, (dflags >> 16) | (q.y & 0xFFFF0000u), 0u);
-            else if (wd == 12) o = make_uint4(0, 0, 0, 0);
-            else if (wd == 13 || wd == 14) o = make_uint4(s_a, 0, 0, 0);
-            else if (wd == 15) o = make_uint4(q.x, uint32_t(TB_PENDING_NONE), 0, 0);
-            const uint64_t at = wave_pos + uint64_t(__popcll(bal & ((1ull << src) - 1)));
-            ae_nt_store(reinterpret_cast<uint4*>(&W.log[at]) + wd, o);
+        // (kAeRecBatch groups' row loads issued together; the loop over the batches not
+        // unrolled -- unrolled, the loads of all 16 groups are hoisted and spill)
+#pragma unroll 1
+        for (uint32_t j0 = 0; j0 < 16; j0 += kAeRecBatch) {
+            if (((bal >> (4 * j0)) & 0xFFFFull) == 0) continue;
+            uint4 qb[kAeRecBatch];
+#pragma unroll
+            for (uint32_t b = 0; b < kAeRecBatch; b++) {
+                const uint32_t src = 4 * (j0 + b) + sub;
+                const uint32_t s_dr = __shfl(dr, src), s_cr = __shfl(cr, src);
+                qb[b] = make_uint4(0, 0, 0, 0);
+                if ((bal >> src) & 1) qb[b] = reinterpret_cast<const uint4*>(&W.acc_rows[credit_half ? s_cr : s_dr])[k];
+            }
+#pragma unroll
+            for (uint32_t b = 0; b < kAeRecBatch; b++) {
+                const uint32_t j = j0 + b;
+                const uint32_t src = 4 * j + sub;
+                const uint32_t s_a = __shfl(a, src);
+                const uint32_t l0 = __shfl(later[0], src), l1 = __shfl(later[1], src);
+                const uint32_t l2 = __shfl(later[2], src), l3 = __shfl(later[3], src);
+                const uint32_t l_dpo = credit_half ? l2 : l0, l_cpo = credit_half ? l3 : l1;
+                const uint32_t ts_lo = __shfl(uint32_t(ts), src), ts_hi = __shfl(uint32_t(ts >> 32), src);
+                const bool v = (bal >> src) & 1;
+                const uint4 q = qb[b];
+                const uint32_t dflags = __shfl(q.y, lane > 0 ? lane - 1 : 0);
+                if (!v) continue;
+                uint4 o = q;
+                if (k == 2) o = ae_sub_u32(q, l_dpo);
+                else if (k == 4) o = ae_sub_u32(q, l_cpo);
+                else if (wd == 10) o = make_uint4(ts_lo, ts_hi, q.z, q.w);
+                else if (wd == 11) o = make_uint4(q.z, q.w, (dflags >> 16) | (q.y & 0xFFFF0000u), 0u);
+                else if (wd == 12) o = make_uint4(0, 0, 0, 0);
+                else if (wd == 13 || wd == 14) o = make_uint4(s_a, 0, 0, 0);
+                else if (wd == 15) o = make_uint4(q.x, uint32_t(TB_PENDING_NONE), 0, 0);
+                const uint64_t at = wave_pos + uint64_t(__popcll(bal & ((1ull << src) - 1)));
+                ae_nt_store(reinterpret_cast<uint4*>(&W.log[at]) + wd, o);
+            }
         }
         pos += round_total;
         __syncthreads();  // (the lists are empty and R is current for the next round)
@@ -1258,7 +1271,7 @@ __global__ void __launch_bounds__(kAeWinThreads) ae_window_emit(AeWindow W) {
 // to pack, kFlagWideItems) or a window key's sum of 2^32 or more (kFlagWideSums). A call's later
 // deltas of one account reach 2^70 and more, so the per-account state is u128 and lives in HBM, not
 // LDS:
-//   ae_wide_partials  per slice of kAeWideSlice events and posted field (a workgroup each), the
+//   ae_wide_partials  per slice (ae_wide_per events) and posted field (a workgroup each), the
 //                     field's sum per account in three u32 LDS limbs (2^96: 2^14 events of < 2^64)
 //   ae_wide_suffix    per account and field, the exclusive suffix over the slices: sums[w] = the
 //                     deltas of slices w + 1, w + 2, ... (u128)
@@ -1271,16 +1284,23 @@ __global__ void __launch_bounds__(kAeWinThreads) ae_window_emit(AeWindow W) {
 //                     count of the slice's created events per round and wave).
 // account_event :4384-4465 (the balances after the event), as ae_window_emit.
 constexpr uint32_t kAeWideThreads = 1024;
-constexpr uint32_t kAeWideRounds = 16;
-constexpr uint32_t kAeWideSlice = kAeWideThreads * kAeWideRounds;
 constexpr uint32_t kAeWideWaves = kAeWideThreads / 64;
+// A slice is `per` events, a multiple of 1024: at least 16 rounds, and as many as it takes for the
+// emit's workgroups (one per CU: 128 KB of LDS) to run in one generation, up to 64 rounds.
+constexpr uint32_t kAeWideRoundsMin = 16, kAeWideRoundsMax = 64;
+constexpr uint32_t kAeWideGrid = 256;
+__host__ __device__ inline uint32_t ae_wide_per(uint32_t n) {
+    uint32_t rounds = (n + kAeWideGrid * kAeWideThreads - 1) / (kAeWideGrid * kAeWideThreads);
+    rounds = rounds < kAeWideRoundsMin ? kAeWideRoundsMin : rounds > kAeWideRoundsMax ? kAeWideRoundsMax : rounds;
+    return rounds * kAeWideThreads;
+}
 
 struct AeWide {
     const uint64_t* items;               // the call's pair items (~0: none)
     const uint64_t* amounts;             // ev_amount: a wide item's amount
     const tb_create_result_t* results;
     const tb_account_t* acc_rows;
-    uint32_t n, ps, rows, slices;
+    uint32_t n, ps, rows, slices, per;
     uint64_t row_base;
     u128* sums;                          // [slice][field][row]: partials, suffix sums, then R
     unsigned int* slice_count;           // per slice: its created events
@@ -1292,13 +1312,13 @@ struct AeWide {
     uint64_t cap;
 };
 
-__device__ inline void ae_wide_item(const AeWide& A, uint32_t e, uint64_t x, uint32_t* dr,
-                                    uint32_t* cr, uint64_t* amount) {
+__device__ inline void ae_wide_item(const AeWide& A, uint64_t x, uint64_t wide_amount,
+                                    uint32_t* dr, uint32_t* cr, uint64_t* amount) {
     const uint64_t rmask = (1ull << A.ps) - 1;
     *dr = uint32_t(x & rmask);
     *cr = uint32_t((x >> A.ps) & rmask);
     const uint64_t a = x >> (2 * A.ps + 1);
-    *amount = a == pair_amount_mask(A.ps) ? A.amounts[e] : a;
+    *amount = a == pair_amount_mask(A.ps) ? wide_amount : a;
 }
 
 // Workgroup 2 w + f: slice w's sums of field f (0 debits_posted, 1 credits_posted) per account.
@@ -1311,31 +1331,36 @@ __global__ void __launch_bounds__(kAeWideThreads) ae_wide_partials(AeWide A) {
         hi[r] = 0;
         top[r] = 0;
     }
-    const uint32_t b0 = w * kAeWideSlice;
-    const uint32_t b1 = b0 + kAeWideSlice < A.n ? b0 + kAeWideSlice : A.n;
-    uint64_t x[kAeWideRounds];
-#pragma unroll
-    for (uint32_t r = 0; r < kAeWideRounds; r++) {
-        const uint32_t e = b0 + r * kAeWideThreads + tid;
-        x[r] = e < b1 ? A.items[e] : ~0ull;
-    }
+    const uint32_t b0 = w * A.per;
+    const uint32_t b1 = b0 + A.per < A.n ? b0 + A.per : A.n;
     __syncthreads();
     uint32_t cnt = 0;
+    constexpr uint32_t kLoads = 16;  // (items in flight per lane)
+    for (uint32_t e0 = b0 + tid; e0 < b1; e0 += kLoads * kAeWideThreads) {
+        uint64_t x[kLoads];
 #pragma unroll
-    for (uint32_t r = 0; r < kAeWideRounds; r++) {
-        if (x[r] == ~0ull) continue;
-        cnt++;
-        uint32_t dr, cr;
-        uint64_t a;
-        ae_wide_item(A, b0 + r * kAeWideThreads + tid, x[r], &dr, &cr, &a);
-        const uint32_t row = f ? cr : dr;
-        const uint32_t alo = uint32_t(a);
-        const uint32_t old = atomicAdd(&lo[row], alo);
-        const uint64_t h = (a >> 32) + (uint32_t(old + alo) < old ? 1u : 0u);
-        if (h) {
-            const uint32_t oh = atomicAdd(&hi[row], uint32_t(h));
-            const uint32_t t = uint32_t(h >> 32) + (uint32_t(oh + uint32_t(h)) < oh ? 1u : 0u);
-            if (t) atomicAdd(&top[row], t);
+        for (uint32_t j = 0; j < kLoads; j++) {
+            const uint32_t e = e0 + j * kAeWideThreads;
+            x[j] = e < b1 ? A.items[e] : ~0ull;
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < kLoads; j++) {
+            if (x[j] == ~0ull) continue;
+            cnt++;
+            const uint32_t e = e0 + j * kAeWideThreads;
+            const uint64_t mask = pair_amount_mask(A.ps);
+            uint32_t dr, cr;
+            uint64_t a;
+            ae_wide_item(A, x[j], (x[j] >> (2 * A.ps + 1)) == mask ? A.amounts[e] : 0, &dr, &cr, &a);
+            const uint32_t row = f ? cr : dr;
+            const uint32_t alo = uint32_t(a);
+            const uint32_t old = atomicAdd(&lo[row], alo);
+            const uint64_t h = (a >> 32) + (uint32_t(old + alo) < old ? 1u : 0u);
+            if (h) {
+                const uint32_t oh = atomicAdd(&hi[row], uint32_t(h));
+                const uint32_t t = uint32_t(h >> 32) + (uint32_t(oh + uint32_t(h)) < oh ? 1u : 0u);
+                if (t) atomicAdd(&top[row], t);
+            }
         }
     }
     for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off);
@@ -1346,9 +1371,10 @@ __global__ void __launch_bounds__(kAeWideThreads) ae_wide_partials(AeWide A) {
         for (uint32_t j = 0; j < kAeWideWaves; j++) t += wave_cnt[j];
         A.slice_count[w] = t;
     }
-    u128* out = A.sums + uint64_t(blockIdx.x) * A.rows;
+    // (an account's two fields side by side: the emit reads both with one 32-byte access)
+    u128* out = A.sums + uint64_t(w) * 2 * A.rows + f;
     for (uint32_t r = tid; r < A.rows; r += kAeWideThreads)
-        out[r] = (u128(top[r]) << 64) | (uint64_t(hi[r]) << 32) | lo[r];
+        out[2 * r] = (u128(top[r]) << 64) | (uint64_t(hi[r]) << 32) | lo[r];
 }
 
 // One lane per (field, account) key: sums[w][key] = the key's sums over the slices after w.
@@ -1380,13 +1406,13 @@ __global__ void __launch_bounds__(kAeWideThreads) ae_wide_emit(AeWide A) {
     __shared__ uint32_t head[kAeWinRowsMax];          // the round's touch lists (node 2e + side)
     __shared__ uint16_t next[2 * kAeWideThreads];
     __shared__ uint64_t amt[kAeWideThreads];
-    __shared__ uint4 later[kAeWideThreads][4];        // dr debits / credits, cr debits / credits
-    __shared__ uint32_t offs[kAeWideRounds * kAeWideWaves];  // a round's wave's first record
+    __shared__ uint4 later[4][kAeWideThreads];        // dr debits / credits, cr debits / credits
+    __shared__ uint32_t offs[kAeWideRoundsMax * kAeWideWaves];  // a round's wave's first record
     __shared__ uint32_t red[2][kAeWideWaves];
     __shared__ unsigned long long ts_lds[2];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, w = blockIdx.x;
-    const uint32_t b0 = w * kAeWideSlice;
-    const uint32_t b1 = b0 + kAeWideSlice < A.n ? b0 + kAeWideSlice : A.n;
+    const uint32_t b0 = w * A.per;
+    const uint32_t b1 = b0 + A.per < A.n ? b0 + A.per : A.n;
     const uint32_t rounds = (b1 - b0 + kAeWideThreads - 1) / kAeWideThreads;
     // created events of the earlier slices; of all (the room in the log: else nothing is written)
     uint32_t before = 0, all = 0;
@@ -1403,7 +1429,8 @@ __global__ void __launch_bounds__(kAeWideThreads) ae_wide_emit(AeWide A) {
         red[1][wv] = all;
     }
     // the slice's created events per round and wave
-    for (uint32_t r = 0; r < kAeWideRounds; r++) {
+#pragma unroll 8
+    for (uint32_t r = 0; r < kAeWideRoundsMax; r++) {
         const uint32_t e = b0 + r * kAeWideThreads + tid;
         const bool valid = r < rounds && e < b1 && A.items[e] != ~0ull;
         const uint64_t bal = __ballot(valid);
@@ -1425,33 +1452,60 @@ __global__ void __launch_bounds__(kAeWideThreads) ae_wide_emit(AeWide A) {
         if (tid == 0) A.state[3] = 1;
         return;
     }
-    // exclusive scan of the (round, wave) counts: 256 entries, one per lane of waves 0-3
-    static_assert(kAeWideRounds * kAeWideWaves == 256, "one scan entry per lane of four waves");
-    uint32_t v = tid < 256 ? offs[tid] : 0, inc = v;
+    // exclusive scan of the (round, wave) counts, one entry per thread
+    static_assert(kAeWideRoundsMax * kAeWideWaves == kAeWideThreads, "one scan entry per thread");
+    const uint32_t v = offs[tid];
+    uint32_t inc = v;
     for (int off = 1; off < 64; off <<= 1) {
         const uint32_t t = __shfl_up(inc, off, 64);
         if (lane >= uint32_t(off)) inc += t;
     }
     __syncthreads();  // (every count read; red reused)
-    if (tid < 256 && lane == 63) red[0][wv] = inc;
+    if (lane == 63) red[0][wv] = inc;
     __syncthreads();
-    if (tid < 256) {
+    {
         uint32_t base = 0;
         for (uint32_t j = 0; j < wv; j++) base += red[0][j];
         offs[tid] = base + inc - v;
     }
     __syncthreads();
-    u128* R = A.sums + uint64_t(w) * 2 * A.rows;  // [0, rows) debits_posted, [rows, 2 rows) credits
+    u128* R = A.sums + uint64_t(w) * 2 * A.rows;  // [2 row] debits_posted, [2 row + 1] credits
     uint64_t ts_min = ~0ull, ts_max = 0;
+    // (the next round's item, timestamp and amount are loaded during the current round)
+    uint64_t x_n = ~0ull, ts_n = 0, am_n = 0;
+    auto prefetch = [&](int32_t r) {
+        const uint32_t e = b0 + uint32_t(r) * kAeWideThreads + tid;
+        x_n = ~0ull;
+        if (r >= 0 && e < b1) {
+            x_n = A.items[e];
+            ts_n = A.results[e].timestamp;
+            am_n = A.amounts[e];
+        }
+    };
+    // (and the round's R words: loaded during the round after it, once its owners stored theirs)
+    u128 Rd[2] = {0, 0}, Rc[2] = {0, 0};
+    auto load_r = [&]() {
+        if (x_n == ~0ull) return;
+        uint32_t ndr, ncr;
+        uint64_t na;
+        ae_wide_item(A, x_n, am_n, &ndr, &ncr, &na);
+#pragma unroll
+        for (int side = 0; side < 2; side++) {
+            const uint32_t acc = side ? ncr : ndr;
+            Rd[side] = R[2 * acc];
+            Rc[side] = R[2 * acc + 1];
+        }
+    };
+    prefetch(int32_t(rounds) - 1);
+    load_r();
     for (int32_t r = int32_t(rounds) - 1; r >= 0; r--) {
         const uint32_t e = b0 + uint32_t(r) * kAeWideThreads + tid;
-        const uint64_t x = e < b1 ? A.items[e] : ~0ull;
+        const uint64_t x = x_n, ts = ts_n, wide_amount = am_n;
         const bool valid = x != ~0ull;
         uint32_t dr = 0, cr = 0;
-        uint64_t a = 0, ts = 0;
+        uint64_t a = 0;
         if (valid) {
-            ae_wide_item(A, e, x, &dr, &cr, &a);
-            ts = A.results[e].timestamp;
+            ae_wide_item(A, x, wide_amount, &dr, &cr, &a);
             next[2 * tid] = uint16_t(atomicExch(&head[dr], 2 * tid));
             next[2 * tid + 1] = uint16_t(atomicExch(&head[cr], 2 * tid + 1));
             amt[tid] = a;
@@ -1460,36 +1514,34 @@ __global__ void __launch_bounds__(kAeWideThreads) ae_wide_emit(AeWide A) {
         __syncthreads();
         // Per side: the account's R (deltas after the round), the round's deltas after e, and --
         // for the list's head owner -- the round's total, which it adds to R after every read.
-        u128 Rd[2] = {0, 0}, Rc[2] = {0, 0}, td[2] = {0, 0}, tc[2] = {0, 0};
+        // (the owner keeps R plus the round's total for after the barrier: nd_ / nc_)
+        u128 nd_[2] = {0, 0}, nc_[2] = {0, 0};
         bool own[2] = {false, false};
+        prefetch(r - 1);
         if (valid) {
-#pragma unroll
-            for (int side = 0; side < 2; side++) {
-                const uint32_t acc = side ? cr : dr;
-                Rd[side] = R[acc];
-                Rc[side] = R[A.rows + acc];
-            }
 #pragma unroll
             for (int side = 0; side < 2; side++) {
                 const uint32_t acc = side ? cr : dr;
                 const uint32_t h = head[acc];
                 own[side] = h == 2 * tid + side;
-                u128 ad = 0, ac = 0;
+                u128 ad = 0, ac = 0, td = 0, tc = 0;
                 for (uint32_t nd = h; nd != kAeWinNil;) {
                     const u128 val = amt[nd >> 1];
                     const bool after = (nd >> 1) > tid;
                     if (nd & 1) {
-                        tc[side] += val;
+                        tc += val;
                         ac += after ? val : u128(0);
                     } else {
-                        td[side] += val;
+                        td += val;
                         ad += after ? val : u128(0);
                     }
                     const uint32_t nx = next[nd];
                     nd = nx == 0xFFFFu ? kAeWinNil : nx;
                 }
-                later[tid][2 * side] = ae_q(Rd[side] + ad);
-                later[tid][2 * side + 1] = ae_q(Rc[side] + ac);
+                later[2 * side][tid] = ae_q(Rd[side] + ad);
+                later[2 * side + 1][tid] = ae_q(Rc[side] + ac);
+                nd_[side] = own[side] ? Rd[side] + td : u128(0);
+                nc_[side] = own[side] ? Rc[side] + tc : u128(0);
             }
         }
         __syncthreads();  // (every R read and list walked before the round's updates)
@@ -1498,13 +1550,15 @@ __global__ void __launch_bounds__(kAeWideThreads) ae_wide_emit(AeWide A) {
             for (int side = 0; side < 2; side++) {
                 if (!own[side]) continue;
                 const uint32_t acc = side ? cr : dr;
-                R[acc] = Rd[side] + td[side];
-                R[A.rows + acc] = Rc[side] + tc[side];
+                R[2 * acc] = nd_[side];
+                R[2 * acc + 1] = nc_[side];
                 head[acc] = kAeWinNil;
             }
             ts_min = ts < ts_min ? ts : ts_min;
             ts_max = ts > ts_max ? ts : ts_max;
         }
+        __syncthreads();  // (the round's R stores before the next round's loads)
+        load_r();
         const uint64_t wave_pos = pos + offs[uint32_t(r) * kAeWideWaves + wv];
         if (valid) {
             const uint32_t rank = lane ? __popcll(bal & (~0ull >> (64 - lane))) : 0;
@@ -1512,38 +1566,49 @@ __global__ void __launch_bounds__(kAeWideThreads) ae_wide_emit(AeWide A) {
                         make_uint4(uint32_t(A.row_base + e), dr, cr, 0));
         }
         // The wave's records, four at a time, as in ae_window_emit (lane L writes word L % 16 of
-        // the record of event lane 4 j + L / 16); the later sums come from LDS.
+        // the record of event lane 4 j + L / 16; the later sums from LDS), kWideRecBatch groups'
+        // row loads issued together.
+        constexpr uint32_t kWideRecBatch = 4;
         const uint32_t wd = lane & 15, sub = lane >> 4;
         const bool credit_half = (wd >= 5 && wd < 10) || wd == 11;
         const uint32_t k = wd < 5 ? wd : wd < 10 ? wd - 5 : 7;
-        for (uint32_t j = 0; j < 16; j++) {
-            if (((bal >> (4 * j)) & 0xF) == 0) continue;  // (wave-uniform)
-            const uint32_t src = 4 * j + sub;
-            const uint32_t s_dr = __shfl(dr, src), s_cr = __shfl(cr, src);
-            const uint32_t a_lo = __shfl(uint32_t(a), src), a_hi = __shfl(uint32_t(a >> 32), src);
-            const uint32_t ts_lo = __shfl(uint32_t(ts), src), ts_hi = __shfl(uint32_t(ts >> 32), src);
-            const bool vv = (bal >> src) & 1;
-            uint4 q = make_uint4(0, 0, 0, 0);
-            if (vv) q = reinterpret_cast<const uint4*>(&A.acc_rows[credit_half ? s_cr : s_dr])[k];
-            const uint32_t dflags = __shfl(q.y, lane > 0 ? lane - 1 : 0);
-            if (!vv) continue;
-            uint4 o = q;
-            if (k == 2 || k == 4) {
-                const uint4 l = later[wv * 64 + src][(credit_half ? 2 : 0) + (k == 4 ? 1 : 0)];
-                o = ae_q(ae_u(q) - ae_u(l));
-            } else if (wd == 10) {
-                o = make_uint4(ts_lo, ts_hi, q.z, q.w);
-            } else if (wd == 11) {
-                o = make_uint4(q.z, q.w, (dflags >> 16) | (q.y & 0xFFFF0000u), 0u);
-            } else if (wd == 12) {
-                o = make_uint4(0, 0, 0, 0);
-            } else if (wd == 13 || wd == 14) {
-                o = make_uint4(a_lo, a_hi, 0, 0);
-            } else if (wd == 15) {
-                o = make_uint4(q.x, uint32_t(TB_PENDING_NONE), 0, 0);
+#pragma unroll 1
+        for (uint32_t j0 = 0; j0 < 16; j0 += kWideRecBatch) {
+            if (((bal >> (4 * j0)) & ((1ull << (4 * kWideRecBatch)) - 1)) == 0) continue;
+            uint4 q[kWideRecBatch];
+#pragma unroll
+            for (uint32_t b = 0; b < kWideRecBatch; b++) {
+                const uint32_t src = 4 * (j0 + b) + sub;
+                const uint32_t s_dr = __shfl(dr, src), s_cr = __shfl(cr, src);
+                q[b] = make_uint4(0, 0, 0, 0);
+                if ((bal >> src) & 1)
+                    q[b] = reinterpret_cast<const uint4*>(&A.acc_rows[credit_half ? s_cr : s_dr])[k];
             }
-            const uint64_t at = wave_pos + uint64_t(__popcll(bal & ((1ull << src) - 1)));
-            ae_nt_store(reinterpret_cast<uint4*>(&A.log[at]) + wd, o);
+#pragma unroll
+            for (uint32_t b = 0; b < kWideRecBatch; b++) {
+                const uint32_t src = 4 * (j0 + b) + sub;
+                const uint32_t a_lo = __shfl(uint32_t(a), src), a_hi = __shfl(uint32_t(a >> 32), src);
+                const uint32_t ts_lo = __shfl(uint32_t(ts), src), ts_hi = __shfl(uint32_t(ts >> 32), src);
+                const uint32_t dflags = __shfl(q[b].y, lane > 0 ? lane - 1 : 0);
+                if (!((bal >> src) & 1)) continue;
+                uint4 o = q[b];
+                if (k == 2 || k == 4) {
+                    const uint4 l = later[(credit_half ? 2 : 0) + (k == 4 ? 1 : 0)][wv * 64 + src];
+                    o = ae_q(ae_u(q[b]) - ae_u(l));
+                } else if (wd == 10) {
+                    o = make_uint4(ts_lo, ts_hi, q[b].z, q[b].w);
+                } else if (wd == 11) {
+                    o = make_uint4(q[b].z, q[b].w, (dflags >> 16) | (q[b].y & 0xFFFF0000u), 0u);
+                } else if (wd == 12) {
+                    o = make_uint4(0, 0, 0, 0);
+                } else if (wd == 13 || wd == 14) {
+                    o = make_uint4(a_lo, a_hi, 0, 0);
+                } else if (wd == 15) {
+                    o = make_uint4(q[b].x, uint32_t(TB_PENDING_NONE), 0, 0);
+                }
+                const uint64_t at = wave_pos + uint64_t(__popcll(bal & ((1ull << src) - 1)));
+                ae_nt_store(reinterpret_cast<uint4*>(&A.log[at]) + wd, o);
+            }
         }
         __syncthreads();  // (R current and the lists empty for the round before)
     }

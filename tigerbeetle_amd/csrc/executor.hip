@@ -1414,7 +1414,8 @@ int ae_window(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
 // emit's rounds from the last one back with the account state in HBM. ae_window checked the rest.
 int ae_window_wide(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
     const uint32_t rows = uint32_t(ctx->T.acc_rows_used);
-    const uint32_t slices = (c.n + kAeWideSlice - 1) / kAeWideSlice;
+    const uint32_t per = ae_wide_per(c.n);
+    const uint32_t slices = (c.n + per - 1) / per;
     const uint64_t words = 2 * uint64_t(slices) * std::max<uint32_t>(rows, 1);
     if (words > ctx->ae_wide_sums_cap) {
         if (ctx->ae_wide_sums) HIP_TRY(ctx, hipFree(ctx->ae_wide_sums));
@@ -1443,6 +1444,7 @@ int ae_window_wide(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
     A.ps = ctx->win.ps;
     A.rows = rows;
     A.slices = slices;
+    A.per = per;
     A.row_base = c.row_base;
     A.sums = ctx->ae_wide_sums;
     A.slice_count = ctx->ae_wide_counts;
