@@ -392,7 +392,8 @@ int select_flagged(tbg_ctx* ctx, const uint8_t* flags, uint64_t n, uint32_t* out
 
 int stage_call_outputs(tbg_ctx* ctx, const tb_create_result_t* d_results, tb_create_result_t* dst,
                        uint32_t n, bool scalars, const AeSnapJob* snap = nullptr,
-                       bool fixes = false, unsigned int seq = 0, uint32_t skip_epoch = 0);
+                       bool fixes = false, unsigned int seq = 0, uint32_t skip_epoch = 0,
+                       bool clear = false);
 // The scalars block to the host (a kernel writes the mapped pinned copy: no DMA hand-off).
 int sync_scalars(tbg_ctx* ctx) {
     int rc = stage_call_outputs(ctx, nullptr, nullptr, 0, true);
@@ -1811,13 +1812,13 @@ int spin_wait(tbg_ctx* ctx, unsigned int seq) {
 
 int stage_call_outputs(tbg_ctx* ctx, const tb_create_result_t* d_results, tb_create_result_t* dst,
                        uint32_t n, bool scalars, const AeSnapJob* snap, bool fixes,
-                       unsigned int seq, uint32_t skip_epoch) {
+                       unsigned int seq, uint32_t skip_epoch, bool clear) {
     StageOut s{reinterpret_cast<const uint4*>(d_results), reinterpret_cast<uint4*>(dst), n,
                scalars ? reinterpret_cast<const unsigned long long*>(ctx->d_scalars) : nullptr,
                reinterpret_cast<unsigned long long*>(ctx->dh_scalars),
                uint32_t(sizeof(DevScalars) / 8), fixes ? ctx->fix_slots : nullptr,
                ctx->T.tr.slots, ctx->d_scalars, seq ? ctx->d_stage_done : nullptr,
-               seq ? ctx->dh_seq : nullptr, seq,
+               seq ? ctx->dh_seq : nullptr, seq, clear && seq && scalars,
                skip_epoch ? ctx->d_stage_done + 2 : nullptr, skip_epoch, snap != nullptr, {}};
     if (snap) s.snap = *snap;
     if (!dst || !n) s.src = nullptr;
@@ -2308,7 +2309,7 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
         }
         if (!rc)
             rc = stage_call_outputs(ctx, d_results, dst, dst ? n : 0, true, snap ? &J : nullptr,
-                                    true, seq, finish ? c.epoch : 0u);
+                                    true, seq, finish ? c.epoch : 0u, !c.pnt_force);
         if (!rc && snap) {
             rc = ae_defer_graph(ctx, n, c.epoch, false);
             ctx->ae_def_call = true;
@@ -2347,8 +2348,8 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
         rc = ae_transfers(ctx, c);
         hprof(ctx, "host:account_events", now_ms() - ta);
     }
-    if (!rc && (ctx->h_scalars->flags & kFlagFinished)) {
-        ctx->scalars_clean = true;  // (tr_ingest's last workgroup cleared them)
+    if (!rc && (ctx->h_scalars->flags & (kFlagFinished | kFlagStageCleared))) {
+        ctx->scalars_clean = true;  // (tr_ingest's or stage_out's last workgroup cleared them)
     } else if (!rc) {
         hipLaunchKernelGGL(tr_reset_scalars, dim3(1), dim3(64), 0, ctx->stream, ctx->d_scalars);
         ctx->scalars_clean = hip_ok(ctx, hipGetLastError(), "reset");

@@ -71,6 +71,10 @@ struct StageOut {
     unsigned int* done;
     unsigned int* host_seq;
     unsigned int seq;
+    // The last workgroup (host_seq set) also clears the call's scalar words when nothing after the
+    // host's wait reads them -- no replay (stats[0]) and no post/void (pnt_resolve) -- and marks its
+    // host copy kFlagStageCleared: tr_reset_scalars' work without its launch.
+    bool clear;
     // When *finished == finished_epoch (tr_ingest ended the call: Call::finish_done) the kernel
     // copies nothing and publishes nothing. Null: never.
     const unsigned int* finished;
@@ -111,6 +115,15 @@ __device__ inline void stage_out_copy(const StageOut& s, uint32_t tid, uint32_t 
         if (threadIdx.x == 0) {
             if (atomicAdd(s.done, 1u) == gridDim.x - 1) {
                 atomicExch(s.done, 0u);
+                // (every workgroup has counted: their reads of the scalar words are done; the
+                // snapshot's later reads of stats[0] find 0 either way)
+                DevScalars* S = const_cast<DevScalars*>(s.scalars);
+                if (s.clear && s.scalars_src && S->stats[0] == 0 && !(S->flags & kFlagPostVoid)) {
+                    constexpr uint32_t fw = offsetof(DevScalars, flags) / 8;
+                    static_assert(offsetof(DevScalars, flags) % 8 == 0, "flags: a word's low half");
+                    s.scalars_dst[fw] = s.scalars_src[fw] | kFlagStageCleared;
+                    reset_call_scalars(S);
+                }
                 __threadfence_system();
                 __hip_atomic_store(s.host_seq, s.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
             }

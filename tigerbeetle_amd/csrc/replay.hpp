@@ -57,6 +57,9 @@ enum : unsigned int {
     // A replayed (SLOW) event the account lanes cannot take (lanes.hpp: not a plain unlinked
     // transfer): the flow replay runs, so the plan may drop doomed debits' keys (group.hpp).
     kFlagNoLanes = 1u << 14,
+    // stage_out's last workgroup cleared the call's scalar words (StageOut::clear): the host
+    // launches no tr_reset_scalars. Set in the host's copy only.
+    kFlagStageCleared = 1u << 15,
 };
 // Call flags under which tr_commit re-validates (and may demote) ingest's FAST events.
 constexpr unsigned int kCommitFlags = kFlagImported | kFlagPostVoid | kFlagDuplicate | kFlagHot |
