@@ -1398,7 +1398,7 @@ int ae_window(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
     W.state = ctx->ae_words + 4;
     W.cap = ctx->ae_cap;
     tmark(ctx, "-account_events");
-    hipLaunchKernelGGL(ae_window_suffix, dim3((2 * W.rows + kBlock - 1) / kBlock), dim3(kBlock), 0,
+    hipLaunchKernelGGL(ae_window_suffix, dim3(std::max<uint32_t>(1, (2 * W.rows + kBlock - 1) / kBlock)), dim3(kBlock), 0,
                        ctx->stream, W);
     hipLaunchKernelGGL(ae_window_emit, dim3(W.nwg), dim3(kAeWinThreads), 0, ctx->stream, W);
     tmark(ctx, "account_events");
@@ -1457,8 +1457,8 @@ int ae_window_wide(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
     A.cap = ctx->ae_cap;
     tmark(ctx, "-account_events");
     hipLaunchKernelGGL(ae_wide_partials, dim3(2 * slices), dim3(kAeWideThreads), 0, ctx->stream, A);
-    hipLaunchKernelGGL(ae_wide_suffix, dim3((2 * rows + kBlock - 1) / kBlock), dim3(kBlock), 0,
-                       ctx->stream, A);
+    hipLaunchKernelGGL(ae_wide_suffix, dim3(std::max<uint32_t>(1, (2 * rows + kBlock - 1) / kBlock)),
+                       dim3(kBlock), 0, ctx->stream, A);
     hipLaunchKernelGGL(ae_wide_emit, dim3(slices), dim3(kAeWideThreads), 0, ctx->stream, A);
     tmark(ctx, "account_events");
     HIP_TRY(ctx, hipGetLastError());
