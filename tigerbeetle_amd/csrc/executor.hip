@@ -123,6 +123,13 @@ struct tbg_ctx {
     unsigned int seq = 0;
     bool spin_sync = false;
     double call_timeout_ms = 60000;  // spin_wait's bound (TBG_CALL_TIMEOUT_MS)
+    // The environment knobs (README), read once at tbg_open: a call reads these, not the
+    // environment (a getenv scans every variable; a replayed call consulted ~18 of them).
+    struct Knobs {
+        bool no_pv_fast, no_lanes, no_additive, no_doom, no_free_owners, flow_debug, walk_seq,
+            lanes_one_lane, no_window, no_lean_lookup, no_ingest_finish;
+        uint32_t flow_lpw, flow_waves, flow_blocks, flow_xcd, flow_backoff;
+    } knobs{};
     // The expires_at index's length as of the last create_transfers call or pulse (the pulse's
     // first kernels need no synchronisation for it); cleared by anything else that changes it.
     bool expiry_known = false;
@@ -525,7 +532,7 @@ Call<Event> make_call(tbg_ctx* ctx, const Event* d_events, uint32_t n, const uin
     c.fix_slots = ctx->fix_slots;
     c.chain_planes = nullptr;
     // (TBG_NO_PV_FAST: every post/void replays)
-    c.pv_slots = getenv("TBG_NO_PV_FAST") ? nullptr : ctx->pv_slots;
+    c.pv_slots = ctx->knobs.no_pv_fast ? nullptr : ctx->pv_slots;
     c.pv_mask = ctx->pv_mask;
     c.pnt_force = ctx->pnt_sharded ? 1 : 0;
     c.finish_done = nullptr;
@@ -688,10 +695,10 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
     const bool lanes_possible =
         !(call_flags & (kFlagDuplicate | kFlagPostVoid | kFlagClosable | kFlagImported |
                         kFlagNoLanes)) &&
-        !c.force_replay && !getenv("TBG_NO_LANES");
-    P.add_epoch = getenv("TBG_NO_ADDITIVE") ? 0 : c.epoch;
+        !c.force_replay && !ctx->knobs.no_lanes;
+    P.add_epoch = ctx->knobs.no_additive ? 0 : c.epoch;
     // Doomed debits (group.hpp): not with the account lanes (which decide limit events themselves).
-    const bool doom = !lanes_possible && !getenv("TBG_NO_DOOM");
+    const bool doom = !lanes_possible && !ctx->knobs.no_doom;
     P.acc_pot = doom ? F.acc_pot : nullptr;
     P.doom_off = F.doom_off;
 
@@ -717,8 +724,8 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
     G.succ = F.succ;
     G.indeg = F.indeg;
     G.lanes = lanes_possible;
-    G.free_owners = getenv("TBG_NO_FREE_OWNERS") == nullptr;
-    G.stats = getenv("TBG_FLOW_DEBUG") != nullptr;
+    G.free_owners = !ctx->knobs.no_free_owners;
+    G.stats = ctx->knobs.flow_debug;
     G.pairs = uint32_t(std::min<uint64_t>(uint64_t(kFlowKeys) * m, 0xFFFFFFFFull));
     G.epoch = c.epoch;
     G.owner_starts = F.owner_starts;
@@ -740,7 +747,7 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
     L.counts = F.lane_counts;
     L.epoch = c.epoch;
     L.acc_free = F.acc_free;
-    L.walk_seq = getenv("TBG_WALK_SEQ") != nullptr;
+    L.walk_seq = ctx->knobs.walk_seq;
 
     const dim3 block(kBlock);
     const uint64_t pairs = kFlowKeys * uint64_t(m);
@@ -776,7 +783,7 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
     if (lanes_possible) {
         // One-lane walk (lanes_replay): LDS mailbox indexes. Wave walk (lanes_walk, the
         // default): a zeroed word per position (plan_keys).
-        const bool one_lane = getenv("TBG_LANES_ONE_LANE") != nullptr;
+        const bool one_lane = ctx->knobs.lanes_one_lane;
         if (one_lane) {
             rc = launch_scan(ctx, m, ExclusiveSumU32{F.mailbox, F.mb_index, nullptr});
             if (rc) return rc;
@@ -784,12 +791,12 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
         }
         tmark(ctx, "flow_plan");
         // Free owners (their verdicts: the grouping): their events' owner bits.
-        if (!getenv("TBG_NO_FREE_OWNERS"))
+        if (!ctx->knobs.no_free_owners)
             hipLaunchKernelGGL(lanes_free, dim3(grid_for(m)), block, 0, ctx->stream, ctx->T, L);
         if (one_lane)
             hipLaunchKernelGGL(lanes_replay, dim3(1), dim3(kLanesMax), 0, ctx->stream, ctx->T, c, L);
         else {
-            const bool dbg = getenv("TBG_FLOW_DEBUG") != nullptr;
+            const bool dbg = ctx->knobs.flow_debug;
             if (dbg) {
                 if (!ctx->flow_debug) HIP_TRY(ctx, hipMalloc(&ctx->flow_debug, kFlowDebugBytes));
                 HIP_TRY(ctx, hipMemsetAsync(ctx->flow_debug, 0, kFlowDebugBytes, ctx->stream));
@@ -820,36 +827,30 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
             }
         }
         hipLaunchKernelGGL(lanes_finish, dim3(grid_for(m)), block, 0, ctx->stream, ctx->T, c, L);
-        if (!getenv("TBG_NO_FREE_OWNERS"))
+        if (!ctx->knobs.no_free_owners)
             hipLaunchKernelGGL(lanes_free_sums, dim3(grid_for(pairs)), block, 0, ctx->stream,
                                ctx->T, L, pairs);
         tmark(ctx, "tr_lanes");
         P.skip = &F.lane_counts[2];
     }
     tmark(ctx, "flow_plan");
-    const bool debug = getenv("TBG_FLOW_DEBUG") != nullptr;
+    const bool debug = ctx->knobs.flow_debug;
     if (debug) {
         if (!ctx->flow_debug) HIP_TRY(ctx, hipMalloc(&ctx->flow_debug, kFlowDebugBytes));
         HIP_TRY(ctx, hipMemsetAsync(ctx->flow_debug, 0, 128, ctx->stream));
         P.debug = ctx->flow_debug;
     }
-    // Engine shape (flow.hpp): lanes per wave x waves per workgroup x workgroups; TBG_FLOW_XCD=8
-    // packs the running workgroups onto one XCD. Default (config 4 sweeps, profiles/r02_shapes):
-    // 1 lane per wave, 4 waves x 256 workgroups (1024 lanes) over the whole chip -- with the
-    // replay's per-event latency down to ~2.8 us, lanes sharing a wave (divergent branches take
-    // turns) cost more than the extra lanes gain: 8192 lanes (8 per wave) 5.9 ms per 1M events,
-    // 4096 (1 or 4 per wave) 5.3, 1024 (1 per wave) 4.8-5.2, 512 5.2-5.6.
-    auto env_u = [](const char* name, uint32_t def, uint32_t lo, uint32_t hi) {
-        const char* e = getenv(name);
-        const uint32_t v = e ? uint32_t(atoi(e)) : def;
-        return std::max(lo, std::min(hi, v));
-    };
-    P.lanes_per_wave = env_u("TBG_FLOW_LPW", kFlowLanesPerWave, 1, 64);
-    const uint32_t waves = env_u("TBG_FLOW_WAVES", kFlowWaves, 1, kFlowThreads / 64);
-    const uint32_t blocks = env_u("TBG_FLOW_BLOCKS", kFlowBlocks, 1,
-                                  kFlowLanesMax / (waves * P.lanes_per_wave));
-    P.xcd_stride = env_u("TBG_FLOW_XCD", 1, 1, 8);
-    P.backoff = env_u("TBG_FLOW_BACKOFF", 1, 0, 1);
+    // Engine shape (flow.hpp; tbg_ctx::Knobs): lanes per wave x waves per workgroup x workgroups.
+    // Default (config 4 sweeps, profiles/r02_shapes): 1 lane per wave, 4 waves x 256 workgroups
+    // (1024 lanes) over the whole chip -- with the replay's per-event latency down to ~2.8 us,
+    // lanes sharing a wave (divergent branches take turns) cost more than the extra lanes gain:
+    // 8192 lanes (8 per wave) 5.9 ms per 1M events, 4096 (1 or 4 per wave) 5.3, 1024 (1 per wave)
+    // 4.8-5.2, 512 5.2-5.6.
+    P.lanes_per_wave = ctx->knobs.flow_lpw;
+    const uint32_t waves = ctx->knobs.flow_waves;
+    const uint32_t blocks = ctx->knobs.flow_blocks;
+    P.xcd_stride = ctx->knobs.flow_xcd;
+    P.backoff = ctx->knobs.flow_backoff;
     const uint32_t lanes = blocks * waves * P.lanes_per_wave;
     hipLaunchKernelGGL(flow_replay, dim3(blocks * P.xcd_stride), dim3(waves * 64), 0, ctx->stream,
                        ctx->T, c, P);
@@ -1985,6 +1986,33 @@ tbg_ctx* tbg_open(const tbg_options* options) {
          dev_alloc(ctx, &ctx->d_stage_done, 4, true);
     if (ok) *ctx->h_seq = 0;
     ctx->spin_sync = getenv("TBG_NO_SPIN_SYNC") == nullptr;
+    {
+        tbg_ctx::Knobs& k = ctx->knobs;
+        auto on = [](const char* name) { return getenv(name) != nullptr; };
+        k.no_pv_fast = on("TBG_NO_PV_FAST");
+        k.no_lanes = on("TBG_NO_LANES");
+        k.no_additive = on("TBG_NO_ADDITIVE");
+        k.no_doom = on("TBG_NO_DOOM");
+        k.no_free_owners = on("TBG_NO_FREE_OWNERS");
+        k.flow_debug = on("TBG_FLOW_DEBUG");
+        k.walk_seq = on("TBG_WALK_SEQ");
+        k.lanes_one_lane = on("TBG_LANES_ONE_LANE");
+        k.no_window = on("TBG_NO_WINDOW");
+        k.no_lean_lookup = on("TBG_NO_LEAN_LOOKUP");
+        k.no_ingest_finish = on("TBG_NO_INGEST_FINISH");
+        // Engine shape (flow.hpp): lanes per wave x waves per workgroup x workgroups; TBG_FLOW_XCD=8
+        // packs the running workgroups onto one XCD.
+        auto env_u = [](const char* name, uint32_t def, uint32_t lo, uint32_t hi) {
+            const char* e = getenv(name);
+            const uint32_t v = e ? uint32_t(atoi(e)) : def;
+            return std::max(lo, std::min(hi, v));
+        };
+        k.flow_lpw = env_u("TBG_FLOW_LPW", kFlowLanesPerWave, 1, 64);
+        k.flow_waves = env_u("TBG_FLOW_WAVES", kFlowWaves, 1, kFlowThreads / 64);
+        k.flow_blocks = env_u("TBG_FLOW_BLOCKS", kFlowBlocks, 1, kFlowLanesMax / (k.flow_waves * k.flow_lpw));
+        k.flow_xcd = env_u("TBG_FLOW_XCD", 1, 1, 8);
+        k.flow_backoff = env_u("TBG_FLOW_BACKOFF", 1, 0, 1);
+    }
     if (const char* e = getenv("TBG_CALL_TIMEOUT_MS")) ctx->call_timeout_ms = std::max(1.0, atof(e));
     ok = ok && hip_ok(ctx, hipEventCreateWithFlags(&ctx->results_ready, hipEventDisableTiming),
                       "hipEventCreate");
@@ -2145,7 +2173,7 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
     uint32_t pair_shift = 1;
     while ((1ull << pair_shift) < ctx->T.acc_rows_used) pair_shift++;
     const bool use_window = use_sort && ctx->window_partials && pair_shift <= kWindowShiftMax &&
-                            !getenv("TBG_NO_WINDOW");
+                            !ctx->knobs.no_window;
     const bool use_buckets = use_sort && !use_window && key_end <= kBucketsMax * kBucketKeys;
     // Sparse key spaces (many more account fields than balance items, e.g. 125M accounts under
     // 1M-event calls): u128 atomics per item instead of the sort; collisions are rare.
@@ -2157,7 +2185,7 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
     const bool ingest_atomics = use_atomic;
     if (use_buckets && key_bits < 16) key_bits = 16;
     BucketPlan plan{};
-    c.lean_lookup = ingest_atomics && !getenv("TBG_NO_LEAN_LOOKUP");
+    c.lean_lookup = ingest_atomics && !ctx->knobs.no_lean_lookup;
     if (use_sort && !ingest_atomics) {
         c.bal_items = ctx->bal_items;
         c.key_bits = key_bits;
@@ -2194,7 +2222,7 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
     // (device per-commit 27.7 -> 24.5 us, r05_g / r05_i). Host-buffer calls keep stage_out: with
     // the results' PCIe writes in tr_ingest's workgroups a commit took 71-77 us against 64-68
     // (r05_i A/B).
-    const bool finish = inline_chunks && !use_sort && !dst && !getenv("TBG_NO_INGEST_FINISH");
+    const bool finish = inline_chunks && !use_sort && !dst && !ctx->knobs.no_ingest_finish;
     if (!rc && inline_chunks) {
         c.chunk_info = nullptr;
         if (finish) {
