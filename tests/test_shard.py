@@ -775,12 +775,13 @@ def test_local_shards_gpu_cross_shard(seed):
         ref.close()
 
 
-def window_scenario(seed, n=150_000, n_acc=2_000):
+def window_scenario(seed, n=150_000, n_acc=2_000, wide=False):
     """Large sharded calls (each shard's part >= 65,536 events over <= 2^14 accounts: the balance
     window path, pnt_resolve on every sharded call): plain transfers (the one-pass AccountEvents
     window), then a call with timed pending transfers (their pulse_next_timestamp minimums resolved
     across shards; AccountEvents from the general path), then plain transfers again, with ticks so
-    that pulses expire some of the pending ones."""
+    that pulses expire some of the pending ones. `wide`: the plain calls' amounts log-uniform below
+    2^63 (the window's wide layout and the wide one-pass AccountEvents, events.hpp ae_wide_*)."""
     rng = np.random.default_rng(seed)
     acc = workload.accounts(n_acc, seed=seed)
     ids = np.arange(1, n_acc + 1)
@@ -801,6 +802,8 @@ def window_scenario(seed, n=150_000, n_acc=2_000):
         t["id"][:, 0] = next_id + np.arange(n)
         next_id += n
         t["amount"][:, 0] = rng.integers(1, 1_000, size=n)
+        if wide and not pending:
+            t["amount"][:, 0] = workload._amounts(rng, n, amounts="wide")
         t["ledger"] = ledger
         t["code"] = 1
         if pending:
@@ -813,17 +816,18 @@ def window_scenario(seed, n=150_000, n_acc=2_000):
 
 
 @pytest.mark.gpu
-def test_local_shards_gpu_window_calls():
+@pytest.mark.parametrize("amounts", ["exp", "wide"])
+def test_local_shards_gpu_window_calls(amounts):
     """window_scenario through two HBM executors: every shard's part of a call takes the balance
     window and pnt_resolve (sharded calls record every pulse_next_timestamp update); results,
     tables and AccountEvents against the unsharded oracle (pnt_resolve's scratch must
-    not be the balance items the AccountEvents window reads)."""
+    not be the balance items the AccountEvents window reads). `wide`: amounts below 2^63."""
     shards = [shard.GpuShard(1 << 12, 1 << 19, batch_events_max=1 << 18,
                              account_events_capacity=1 << 20) for _ in range(2)]
     ref = OracleShard()
     try:
         cluster = shard.LocalShards(shard.LedgerRouter(2, ledgers=LEDGERS), shards, PBM)
-        drive(cluster, ref, window_scenario(3))
+        drive(cluster, ref, window_scenario(3, wide=amounts == "wide"))
         assert_same_state([s.dump() for s in shards], ref,
                           [s.dump_account_events() for s in shards])
     finally:
