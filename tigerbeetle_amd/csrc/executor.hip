@@ -630,7 +630,12 @@ int ensure_flow(tbg_ctx* ctx, uint64_t m) {
     }
     if (m <= F.cap) return 0;
     free_flow(F);
-    const uint64_t cap = std::max<uint64_t>(next_pow2(m), 1u << 14);
+    // Sized once for the context's calls (up to 2^21 replayed events): a reallocation -- ~30
+    // allocations, their clears and the frees' synchronisation -- costs ~50-100 us of host time
+    // with the GPU idle, so growing with each call's replay list cost config 4's first calls that
+    // much each.
+    const uint64_t cap = std::max<uint64_t>(
+        {next_pow2(m), 1u << 14, std::min<uint64_t>(next_pow2(ctx->opt.batch_events_max), 1u << 21)});
     const uint64_t kc = kFlowKeys * cap;
     const uint64_t slots = 2 * kc;  // grouping table load <= 0.5
     ok = dev_alloc(ctx, &F.head8, cap, false) && dev_alloc(ctx, &F.barrier8, cap, false) &&
@@ -1418,13 +1423,19 @@ int ae_window_wide(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
     const uint32_t rows = uint32_t(ctx->T.acc_rows_used);
     const uint32_t per = ae_wide_per(c.n);
     const uint32_t slices = (c.n + per - 1) / per;
+    // (sized once for the context's largest call and the window's row limit: no reallocation)
+    const uint64_t bmax = std::max<uint64_t>(ctx->opt.batch_events_max, c.n);
+    const uint32_t slices_max = std::max<uint32_t>(
+        slices, uint32_t((bmax + ae_wide_per(uint32_t(bmax)) - 1) / ae_wide_per(uint32_t(bmax))));
+    const uint32_t slices_alloc = std::max<uint32_t>(slices_max, kAeWideGrid);
     const uint64_t words = 2 * uint64_t(slices) * std::max<uint32_t>(rows, 1);
     if (words > ctx->ae_wide_sums_cap) {
+        const uint64_t alloc_words = std::max<uint64_t>(words, 2 * uint64_t(slices_alloc) * kAeWinRowsMax);
         if (ctx->ae_wide_sums) HIP_TRY(ctx, hipFree(ctx->ae_wide_sums));
         ctx->ae_wide_sums = nullptr;
         ctx->ae_wide_sums_cap = 0;
-        if (!dev_alloc(ctx, &ctx->ae_wide_sums, words, false)) return TBG_ENOMEM;
-        ctx->ae_wide_sums_cap = words;
+        if (!dev_alloc(ctx, &ctx->ae_wide_sums, alloc_words, false)) return TBG_ENOMEM;
+        ctx->ae_wide_sums_cap = alloc_words;
     }
     if (slices > ctx->ae_wide_slices_cap) {
         for (void* q : {(void*)ctx->ae_wide_counts, (void*)ctx->ae_wide_ts})
@@ -1432,10 +1443,10 @@ int ae_window_wide(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
         ctx->ae_wide_counts = nullptr;
         ctx->ae_wide_ts = nullptr;
         ctx->ae_wide_slices_cap = 0;
-        if (!(dev_alloc(ctx, &ctx->ae_wide_counts, slices + 1, true) &&
-              dev_alloc(ctx, &ctx->ae_wide_ts, 2 * uint64_t(slices), false)))
+        if (!(dev_alloc(ctx, &ctx->ae_wide_counts, slices_alloc + 1, true) &&
+              dev_alloc(ctx, &ctx->ae_wide_ts, 2 * uint64_t(slices_alloc), false)))
             return TBG_ENOMEM;
-        ctx->ae_wide_slices_cap = slices;
+        ctx->ae_wide_slices_cap = slices_alloc;
     }
     AeWide A{};
     A.items = ctx->bal_items;

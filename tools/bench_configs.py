@@ -80,7 +80,8 @@ def run(config, n, batches, profile=True, amounts="exp"):
         p.seconds = {"gpu": 0.0, "oracle": 0.0}
         p.stats = {k: 0 for k in p.stats}
         p.pulses = []
-        p.lib.tbg_profile(p.g, 1 if profile else 0)
+        # (tbg_profile mode 1: the kernels' HIP-event marks; TBG_BENCH_PROFILE_MODE=2: host phases)
+        p.lib.tbg_profile(p.g, int(os.environ.get("TBG_BENCH_PROFILE_MODE", "1")) if profile else 0)
 
     try:
         drive = configs34.config3 if config == "config3" else configs34.config4
