@@ -84,6 +84,8 @@ struct StageOut {
     // of its own. `has_snap` false: none.
     bool has_snap;
     AeSnapJob snap;
+    // Workgroups [0, copy_wgs) copy and count for the sequence word; the rest only snapshot (0: all).
+    uint32_t copy_wgs;
 };
 
 // The end of a stream's work for a spinning host (tbg_pulse): `seq` into the pinned word, a
@@ -113,7 +115,8 @@ __device__ inline void stage_out_copy(const StageOut& s, uint32_t tid, uint32_t 
         __threadfence_system();
         __syncthreads();
         if (threadIdx.x == 0) {
-            if (atomicAdd(s.done, 1u) == gridDim.x - 1) {
+            const uint32_t counted = s.copy_wgs ? s.copy_wgs : gridDim.x;
+            if (atomicAdd(s.done, 1u) == counted - 1) {
                 atomicExch(s.done, 0u);
                 // (every workgroup has counted: their reads of the scalar words are done; the
                 // snapshot's later reads of stats[0] find 0 either way)
@@ -133,8 +136,9 @@ __device__ inline void stage_out_copy(const StageOut& s, uint32_t tid, uint32_t 
 
 __global__ void __launch_bounds__(kStageThreads) stage_out(StageOut s) {
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t threads = gridDim.x * blockDim.x;
-    if (!(s.finished && *s.finished == s.finished_epoch)) stage_out_copy(s, tid, threads);
+    const uint32_t copiers = s.copy_wgs ? s.copy_wgs : gridDim.x;
+    if (blockIdx.x < copiers && !(s.finished && *s.finished == s.finished_epoch))
+        stage_out_copy(s, tid, copiers * blockDim.x);
     if (s.has_snap && tid < kAeAsyncMax) {
         const AeSnapJob& J = s.snap;
         if (J.speculative && J.T.scalars->stats[0] != 0) J.st.created[tid] = 0;
