@@ -943,8 +943,11 @@ int pnt_resolve(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
 
 // The replay list (order-preserving), the replay, and the id slots of the replayed events.
 template <typename Event>
-int run_replay(tbg_ctx* ctx, Call<Event>& c, bool is_transfers, bool finalize_everything) {
-    int rc = select_flagged(ctx, ctx->ev_slow, c.n, ctx->slow_list, &ctx->d_scalars->slow_count);
+int run_replay(tbg_ctx* ctx, Call<Event>& c, bool is_transfers, bool finalize_everything,
+               bool selected = false) {
+    // (selected: the list was selected before the host's synchronisation)
+    int rc = selected ? 0 : select_flagged(ctx, ctx->ev_slow, c.n, ctx->slow_list,
+                                          &ctx->d_scalars->slow_count);
     if (rc) return rc;
     tmark(ctx, "select_replay_list");
     const unsigned int call_flags = ctx->h_scalars->flags;
@@ -2329,6 +2332,12 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
         tmark(ctx, "bal_hash");
         rc = hip_ok(ctx, hipGetLastError(), "launch") ? 0 : TBG_EHIP;
     }
+    // A large call that follows a replayed one selects its replay list before the host's
+    // synchronisation (a call without replayed events ignores the list): after it the host goes
+    // straight to the plan.
+    const bool pre_selected = !rc && n > kInlineChunkMax && ctx->replay_hint;
+    if (pre_selected)
+        rc = select_flagged(ctx, ctx->ev_slow, c.n, ctx->slow_list, &ctx->d_scalars->slow_count);
     // A host-buffer call's results are queued for download here, so that one host
     // synchronisation covers them when the call needs no replay (else they are downloaded again).
     // One host synchronisation: does the call need the ordered replay (and, with imported events,
@@ -2370,7 +2379,7 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
     if (replay) ctx->ae_snap_early = false;
     ctx->early_done = !rc && ctx->early_dst && !replay;  // (only the replay rewrites results)
     if (replay && (ctx->h_scalars->flags & kFlagImported)) rc = check_imported_indexes(ctx, true);
-    if (replay && !rc) rc = run_replay(ctx, c, true, false);
+    if (replay && !rc) rc = run_replay(ctx, c, true, false, pre_selected);
     if (!rc && ((ctx->h_scalars->flags & kFlagPostVoid) || c.pnt_force)) rc = pnt_resolve(ctx, c);
     if (!rc) {
         ctx->pnt_last = c;
