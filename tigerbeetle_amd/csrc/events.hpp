@@ -1889,7 +1889,8 @@ struct AeDense {
     unsigned long long* slice_ts;  // [0] / [1]: the first / last created timestamp (~0 / 0 between calls)
     uint4* later;               // per event, two words (ae_dense_later)
     uint32_t* pos;              // per event: its position among the call's created events
-    unsigned int* fail;       // == epoch: the call takes the general appends
+    unsigned int* fail;       // == epoch: the call takes the general appends (the low half of a
+                              // mapped pinned word the host reads after its synchronisation)
     uint32_t epoch;
     tb_account_event_t* log;
     AeRef* refs;
@@ -1944,7 +1945,10 @@ __global__ void ae_dense_stage(AeDense A) {
                           uint32_t(f) | (pf << 16), t.ledger);
         e[4] = make_uint4(status, 0, 0, 0);
     }
-    if (__any(bad) && (threadIdx.x & 63) == 0) *A.fail = A.epoch;
+    if (__any(bad) && (threadIdx.x & 63) == 0) {
+        *A.fail = A.epoch;
+        __threadfence_system();
+    }
     if (k < c.n) A.touch[k] = o;
 }
 
@@ -2043,7 +2047,10 @@ __global__ __launch_bounds__(kAeSufThreads) void ae_dense_suffix(AeDense A) {
             }
         }
     }
-    if (wide) *A.fail = A.epoch;
+    if (wide) {
+        *A.fail = A.epoch;
+        __threadfence_system();
+    }
 }
 
 __global__ void ae_dense_ts_init(unsigned long long* ts) {
@@ -2054,13 +2061,6 @@ __global__ void ae_dense_ts_init(unsigned long long* ts) {
 }
 
 // The refusal word for the host (mapped pinned memory).
-__global__ void ae_dense_report(const unsigned int* fail, unsigned long long* out) {
-    if (threadIdx.x == 0 && blockIdx.x == 0) {
-        *out = *fail;
-        __threadfence_system();
-    }
-}
-
 __device__ inline uint4 ae_sub_i32(uint4 balance, uint32_t d) {
     return ae_q(ae_u(balance) - u128(int64_t(int32_t(d))));  // (sign-extended: u128 wraps)
 }

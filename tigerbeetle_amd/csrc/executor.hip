@@ -289,7 +289,6 @@ struct tbg_ctx {
     AeDense ae_dense_job{};           // (ae_dense_prefix -> ae_dense)
     uint32_t ae_dense_prefixed = 0;   // the epoch whose prefix is queued
     uint32_t* ae_dense_pos = nullptr;
-    unsigned int* ae_dense_fail = nullptr;
     unsigned long long* ae_small_ts = nullptr;
     // ae_wide_* scratch (grown to the largest wide window call): per slice, field and account
     u128* ae_wide_sums = nullptr;
@@ -1504,8 +1503,7 @@ int ae_dense_prefix(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
               dev_alloc(ctx, &ctx->ae_dense_counts, slices + 1, true) &&
               dev_alloc(ctx, &ctx->ae_dense_ts, 2, false) &&
               dev_alloc(ctx, &ctx->ae_dense_later, 2 * cap, false) &&
-              dev_alloc(ctx, &ctx->ae_dense_pos, cap, false) &&
-              dev_alloc(ctx, &ctx->ae_dense_fail, 1, true)))
+              dev_alloc(ctx, &ctx->ae_dense_pos, cap, false)))
             return TBG_ENOMEM;
         // (ae_dense_records' min / max words; a kernel on the stream: a synchronous copy waited for
         // every stream, ~10 ms inside config 4's first dense call)
@@ -1531,7 +1529,9 @@ int ae_dense_prefix(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
     A.slice_ts = ctx->ae_dense_ts;
     A.later = ctx->ae_dense_later;
     A.pos = ctx->ae_dense_pos;
-    A.fail = ctx->ae_dense_fail;
+    // (the refusal word is written straight to pinned memory: no report kernel)
+    A.fail = reinterpret_cast<unsigned int*>(ctx->dh_pulse + 2);
+    static_assert(__BYTE_ORDER__ == __ORDER_LITTLE_ENDIAN__, "the word's low half");
     A.epoch = c.epoch;
     A.log = ctx->ae_log;
     A.refs = ctx->ae_ref;
@@ -1540,10 +1540,8 @@ int ae_dense_prefix(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
     tmark(ctx, "-account_events");
     hipLaunchKernelGGL(ae_dense_stage, dim3(grid_for(c.n)), dim3(kBlock), 0, ctx->stream, A);
     hipLaunchKernelGGL(ae_dense_partials, dim3(2 * A.slices), dim3(kAeWinThreads), 0, ctx->stream, A);
-    hipLaunchKernelGGL(ae_dense_suffix, dim3((4 * A.rows + 63) / 64), dim3(kAeSufThreads), 0,
-                       ctx->stream, A);
-    hipLaunchKernelGGL(ae_dense_report, dim3(1), dim3(64), 0, ctx->stream, ctx->ae_dense_fail,
-                       ctx->dh_pulse + 2);
+    hipLaunchKernelGGL(ae_dense_suffix, dim3(std::max<uint32_t>(1, (4 * A.rows + 63) / 64)),
+                       dim3(kAeSufThreads), 0, ctx->stream, A);
     tmark(ctx, "account_events");
     HIP_TRY(ctx, hipGetLastError());
     ctx->ae_dense_prefixed = c.epoch;
@@ -1557,7 +1555,7 @@ int ae_dense(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     }
     ctx->ae_dense_prefixed = 0;
-    if (ctx->h_pulse[2] == c.epoch) return 1;
+    if (uint32_t(ctx->h_pulse[2]) == c.epoch) return 1;  // (ae_dense_stage / _suffix wrote it)
     const AeDense& A = ctx->ae_dense_job;
     tmark(ctx, "-account_events");
     hipLaunchKernelGGL(ae_dense_later, dim3(A.slices), dim3(kAeDenseEmitThreads), 0, ctx->stream, A);
@@ -1997,6 +1995,7 @@ tbg_ctx* tbg_open(const tbg_options* options) {
     ok = ok && hip_ok(ctx, hipHostMalloc(reinterpret_cast<void**>(&ctx->h_pulse), 64, kCoherentHost), "hipHostMalloc") &&
          hip_ok(ctx, hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->dh_pulse), ctx->h_pulse, 0),
                 "hipHostGetDevicePointer");
+    if (ok) std::memset(ctx->h_pulse, 0, 64);
     ok = ok && hip_ok(ctx, hipHostMalloc(reinterpret_cast<void**>(&ctx->h_seq), 64, kCoherentHost), "hipHostMalloc") &&
          hip_ok(ctx, hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->dh_seq), ctx->h_seq, 0),
                 "hipHostGetDevicePointer") &&
@@ -2107,7 +2106,7 @@ void tbg_close(tbg_ctx* ctx) {
     if (ctx->ae_g_words) (void)hipFree(ctx->ae_g_words);
     for (void* q : {(void*)ctx->ae_small_counts, (void*)ctx->ae_small_ts, (void*)ctx->ae_dense_touch,
                     (void*)ctx->ae_dense_ev, (void*)ctx->ae_dense_partials,
-                    (void*)ctx->ae_dense_counts, (void*)ctx->ae_dense_ts, (void*)ctx->ae_dense_fail,
+                    (void*)ctx->ae_dense_counts, (void*)ctx->ae_dense_ts,
                     (void*)ctx->ae_dense_later, (void*)ctx->ae_dense_pos, (void*)ctx->ae_wide_sums,
                     (void*)ctx->ae_wide_counts, (void*)ctx->ae_wide_ts})
         if (q) (void)hipFree(q);
