@@ -1891,12 +1891,24 @@ struct AeDense {
     uint32_t* pos;              // per event: its position among the call's created events
     unsigned int* fail;       // == epoch: the call takes the general appends (the low half of a
                               // mapped pinned word the host reads after its synchronisation)
+    unsigned int* claim;      // device words: [0] == epoch: ae_dense_stage refused the call (the
+                              // later kernels return at once; ae_dense_suffix's block 0 forwards it
+                              // to `fail`); [1] == epoch: a suffix wave has written `fail`
     uint32_t epoch;
     tb_account_event_t* log;
     AeRef* refs;
     unsigned long long* state;
     uint64_t cap;
 };
+
+// The host's refusal word, one system-scope release per call (with wide amounts nearly every wave
+// of ae_dense_stage refuses: those only store claim[0]).
+__device__ inline void ae_dense_refuse(const AeDense& A) {
+    *A.fail = A.epoch;
+    __threadfence_system();
+}
+
+__device__ inline bool ae_dense_refused(const AeDense& A) { return A.claim[0] == A.epoch; }
 
 __global__ void ae_dense_stage(AeDense A) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1945,10 +1957,7 @@ __global__ void ae_dense_stage(AeDense A) {
                           uint32_t(f) | (pf << 16), t.ledger);
         e[4] = make_uint4(status, 0, 0, 0);
     }
-    if (__any(bad) && (threadIdx.x & 63) == 0) {
-        *A.fail = A.epoch;
-        __threadfence_system();
-    }
+    if (__any(bad) && (threadIdx.x & 63) == 0) A.claim[0] = A.epoch;
     if (k < c.n) A.touch[k] = o;
 }
 
@@ -1958,6 +1967,7 @@ __global__ void __launch_bounds__(kAeWinThreads) ae_dense_partials(AeDense A) {
     __shared__ uint32_t Rc[kAeWinRowsMax];
     __shared__ uint32_t wave_cnt[kAeWinThreads / 64];
     const uint32_t tid = threadIdx.x, s = blockIdx.x >> 1, q = blockIdx.x & 1;
+    if (ae_dense_refused(A)) return;  // (written before this launch: uniform over the block)
     for (uint32_t a = tid; a < A.rows; a += kAeWinThreads) {
         Rd[a] = 0;
         Rc[a] = 0;
@@ -2005,6 +2015,10 @@ constexpr int kAeSufThreads = 64 * kAeSufGroups;
 __global__ __launch_bounds__(kAeSufThreads) void ae_dense_suffix(AeDense A) {
     __shared__ long long total[kAeSufGroups][64];
     const uint32_t lane = threadIdx.x & 63, g = threadIdx.x >> 6;
+    if (ae_dense_refused(A)) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) ae_dense_refuse(A);
+        return;
+    }
     const uint32_t keys = 2 * A.rows;
     const uint32_t t = blockIdx.x * 64 + lane;
     const bool live = t < 2 * keys;
@@ -2047,10 +2061,7 @@ __global__ __launch_bounds__(kAeSufThreads) void ae_dense_suffix(AeDense A) {
             }
         }
     }
-    if (wide) {
-        *A.fail = A.epoch;
-        __threadfence_system();
-    }
+    if (__any(wide) && lane == 0 && atomicExch(A.claim + 1, A.epoch) != A.epoch) ae_dense_refuse(A);
 }
 
 __global__ void ae_dense_ts_init(unsigned long long* ts) {

@@ -289,6 +289,7 @@ struct tbg_ctx {
     AeDense ae_dense_job{};           // (ae_dense_prefix -> ae_dense)
     uint32_t ae_dense_prefixed = 0;   // the epoch whose prefix is queued
     uint32_t* ae_dense_pos = nullptr;
+    unsigned int* ae_dense_claim = nullptr;
     unsigned long long* ae_small_ts = nullptr;
     // ae_wide_* scratch (grown to the largest wide window call): per slice, field and account
     u128* ae_wide_sums = nullptr;
@@ -1503,7 +1504,8 @@ int ae_dense_prefix(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
               dev_alloc(ctx, &ctx->ae_dense_counts, slices + 1, true) &&
               dev_alloc(ctx, &ctx->ae_dense_ts, 2, false) &&
               dev_alloc(ctx, &ctx->ae_dense_later, 2 * cap, false) &&
-              dev_alloc(ctx, &ctx->ae_dense_pos, cap, false)))
+              dev_alloc(ctx, &ctx->ae_dense_pos, cap, false) &&
+              dev_alloc(ctx, &ctx->ae_dense_claim, 2, true)))
             return TBG_ENOMEM;
         // (ae_dense_records' min / max words; a kernel on the stream: a synchronous copy waited for
         // every stream, ~10 ms inside config 4's first dense call)
@@ -1531,6 +1533,7 @@ int ae_dense_prefix(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
     A.pos = ctx->ae_dense_pos;
     // (the refusal word is written straight to pinned memory: no report kernel)
     A.fail = reinterpret_cast<unsigned int*>(ctx->dh_pulse + 2);
+    A.claim = ctx->ae_dense_claim;
     static_assert(__BYTE_ORDER__ == __ORDER_LITTLE_ENDIAN__, "the word's low half");
     A.epoch = c.epoch;
     A.log = ctx->ae_log;
@@ -2107,7 +2110,7 @@ void tbg_close(tbg_ctx* ctx) {
     for (void* q : {(void*)ctx->ae_small_counts, (void*)ctx->ae_small_ts, (void*)ctx->ae_dense_touch,
                     (void*)ctx->ae_dense_ev, (void*)ctx->ae_dense_partials,
                     (void*)ctx->ae_dense_counts, (void*)ctx->ae_dense_ts,
-                    (void*)ctx->ae_dense_later, (void*)ctx->ae_dense_pos, (void*)ctx->ae_wide_sums,
+                    (void*)ctx->ae_dense_claim, (void*)ctx->ae_dense_later, (void*)ctx->ae_dense_pos, (void*)ctx->ae_wide_sums,
                     (void*)ctx->ae_wide_counts, (void*)ctx->ae_wide_ts})
         if (q) (void)hipFree(q);
     free_ae_scratch(ctx->ae_g);
