@@ -9,17 +9,21 @@ its own commit timestamp, TestContext rule prepare_ts += 1 + n). Inputs are resi
 the timed region starts; every step uses fresh transfer ids, so every step does the full work.
 
 Multi-GPU (weak scaling, SURVEY.md §8e, north_star "the account table and event stream shard
-naturally by ledger ... RCCL over xGMI is used only to scatter batches and gather results"): one
-process per GPU, each owning one ledger shard (10k accounts on ledger 2 + rank). The step is ONE
-client stream of N x 1,222 batches (every client batch is on one ledger); batch g belongs to the
-shard of ledger 2 + (g mod N), so shard r executes global batches r, r + N, ... with their global
-commit timestamps (TestContext rule applied over the whole stream), resident in its HBM: the
-scatter is the ledger partition itself and `value` has no data-path collective (`scaling`:
-"weak"). The mixed-ledger routed path is timed in the same run as `routed` (a per-event mixed
-stream entering at rank 0: device router, RCCL scatter, execution, RCCL gather, settle -- all in
-its own timed region; tigerbeetle_amd/routed.py); `--routed-only` makes it the line. Both timed
-regions are bracketed by a barrier + device synchronise on every rank; the reported time is the
-max over ranks.
+naturally by ledger"): the line at N > 1 is the executor group (include/tbg_group.h): ONE process
+-- rank 0 of the launch -- owns every GPU's shard, as the reference's one replica owns its one
+StateMachine; the other ranks wait at the barriers. Each step is ONE mixed-ledger client call of
+--group-transfers x N transfers (ledger uniform per event over N ledgers, 10k accounts each)
+resident in HBM on GPU 0: the device router places every event, the slices are peer-copied over
+xGMI to their shards' GPUs, every shard executes on its own host thread, the results come back
+and settle in call order -- all inside the timed region (`group`). The pre-partitioned figure
+(one process per GPU, each executing its ledger's batches of one client stream from its own HBM,
+no data-path collective) is reported beside it (`partitioned`; `--partitioned-line` makes it the
+line). Timed regions are bracketed by a barrier + device synchronise on every rank; the reported
+time is the max over ranks. At N = 1 `hazard_call` times 1M-event calls with 0.1 % injected
+failures across ledgers (unknown / cross-ledger accounts, id 0, reserved flags, posts of pending
+transfers found nowhere, exact repeats) through a group of 2 shards on the one GPU: the device
+path keeps them, validated in closed form. `--group S` makes a group of S shards on one GPU the
+line (a rehearsal).
 
 Validation (after the timed region; the workload is order-independent, so the serial reference
 outcome is known in closed form): every result of every step is `created` with its exact event
@@ -96,12 +100,18 @@ def parse_args():
                     help="record AccountEvents (the account_events groove, 256 B per created "
                          "transfer) inside the timed steps; SURVEY.md §8d excludes them from the "
                          "headline's algorithmic bytes")
-    ap.add_argument("--routed-only", action="store_true",
-                    help="N > 1: the line is the routed mixed-ledger stream (rank 0 ingress)")
-    ap.add_argument("--no-routed", action="store_true",
-                    help="N > 1: skip the `routed` sub-measurement")
-    ap.add_argument("--routed-transfers", type=int, default=2_000_000,
-                    help="routed sub-measurement: transfers per GPU per step")
+    ap.add_argument("--group-transfers", type=int, default=2_000_000,
+                    help="group line: transfers per shard per step (one call of this x shards)")
+    ap.add_argument("--partitioned-line", action="store_true",
+                    help="N > 1: the line is the pre-partitioned figure (N independent executors, "
+                         "each with its ledger's batches resident in its HBM) instead of the group")
+    ap.add_argument("--group", type=int, default=0,
+                    help="single process: the line is the group of this many shards on GPU "
+                         "--group-device (a rehearsal of the N-GPU group on one GPU)")
+    ap.add_argument("--group-device", type=int, default=0)
+    ap.add_argument("--hazard-rate", type=float, default=0.001,
+                    help="`hazard_call`: injected failures per event (N=1 line, 2 shards, 1 GPU)")
+    ap.add_argument("--no-hazard-call", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-validate", action="store_true")
     return ap.parse_args()
@@ -716,162 +726,121 @@ def account_events_line(args, lib, dev, wl, steps, d_ends, lens, N, A):
         lib.tbg_close(g2)
 
 
-def routed_call(n_per_shard, world, accounts, seed, step):
-    """The routed workload's client call for one step: world x n_per_shard transfers over `world`
-    ledgers (2 .. world + 1, `accounts` accounts each, ids (ledger - 2) * accounts + 1 ..), the
-    ledger uniform per event and debit / credit uniform within it (benchmark_load.zig
-    distributions), fresh ids per step."""
-    n = n_per_shard * world
-    t = workload.transfers_uniform(n, accounts, seed=seed, id_offset=step * n)
-    lg = np.random.default_rng(seed + 1).integers(0, world, size=n).astype(np.uint64)
-    t["debit_account_id"][:, 0] += lg * np.uint64(accounts)
-    t["credit_account_id"][:, 0] += lg * np.uint64(accounts)
-    t["ledger"] = (2 + lg).astype(np.uint32)
-    return t, lg
-
-
-def routed_measure(args, world, rank, local, dist, N1, K, W):
-    """N > 1: one mixed-ledger client stream (the ledger uniform per event) over N ledgers enters
-    at rank 0, in HBM; every step is routed by the device router (tbr), scattered to the ledger
-    shards over RCCL, executed there and the results gathered back to call order -- all inside
-    the timed region (tigerbeetle_amd/routed.py). Weak scaling: N1 transfers per
-    GPU per step. Returns rank 0's report (None elsewhere)."""
-    import torch
-    from tigerbeetle_amd.routed import RoutedShards
-    A = args.accounts or 10_000
-    N = N1 * world
+def group_measure(args, shards, devices, N1, K, W, hazard_rate=0.0):
+    """The sharded group (include/tbg_group.h): ONE mixed-ledger client call per step -- N1 x shards
+    transfers, the ledger uniform per event over `shards` ledgers (10k accounts each), sequential
+    fresh ids -- enters in HBM on the router's GPU (devices[0]); tbg_group_create_transfers_device
+    routes it (device router), copies each shard's slice to its GPU (peer copies over xGMI),
+    executes every shard on its own host thread, copies the results back and settles them in call
+    order -- all inside the timed region, K steps after W warmup steps. `hazard_rate` > 0 injects
+    failures whose statuses follow from the events alone (workload.hazard_transfers: unknown and
+    cross-ledger accounts, id 0, reserved flags, posts of pending transfers found nowhere, exact
+    repeats), which the device path places. Validation: every result equals the closed form
+    (workload.hazard_expected: created or the injected status, at the event's timestamp or the
+    repeated object's) and every account row holds exactly the sums of its created transfers.
+    Runs in this process only (the group owns every shard's GPU)."""
+    from tigerbeetle_amd import shard
+    P = args.accounts or 10_000
+    L = shards
+    N = N1 * shards
     lib = native.load()
-    cap = int(N1 * (K + W) * 1.1) + 4096
-    opt = native.TbgOptions()
-    opt.account_capacity = A
-    opt.transfer_capacity = cap
-    opt.batch_events_max = int(N1 * 1.1) + 4096
-    opt.batch_count_max = 1
-    opt.pulse_batch_max = 8190
-    opt.device = local
-    opt.pulse_next_timestamp_init = 1
-    rs = RoutedShards(opt, events_max=N, router_transfer_capacity=N * (K + W) + 4096,
-                      router_account_capacity=A * world + 4096, ledgers=world + 1,
-                      device_index=local)
-    # Each shard creates its own ledger's accounts; rank 0's directory records all of them.
-    acc = workload.accounts(A, seed=args.seed + rank, id_offset=rank * A, ledger=2 + rank)
-    res = np.zeros(A, dtype=RESULT_DTYPE)
-    rc = lib.tbg_create_accounts(rs.g, acc.ctypes.data_as(ctypes.c_void_p), A,
-                                 np.asarray([A], dtype=np.uint32).ctypes.data_as(native.c_u32p),
-                                 np.asarray([A + 1], dtype=np.uint64).ctypes.data_as(native.c_u64p),
-                                 1, res.ctypes.data_as(ctypes.c_void_p))
-    assert rc == 0 and (res["status"] == CREATED).all(), "create_accounts"
-    if rank == 0:
-        ids = np.zeros((A * world, 2), dtype=np.uint64)
-        ids[:, 0] = np.arange(1, A * world + 1, dtype=np.uint64)
-        rs.record_accounts(ids, np.arange(A * world) // A)
-    dev = torch.device("cuda", local)
+    dev = Device()
+    dev.set_device(devices[0])
     lens = batch_plan(N)
-    prepare_ts = A + 1
-    steps, host_steps = [], []
-    if rank == 0:
-        d_ends = torch.from_numpy(np.cumsum(lens).astype(np.int32)).to(dev)
+    per_shard = int(N1 * 1.1) + 8192
+    opts = [native.options(P, per_shard * (K + W), per_shard, batch_count_max=len(lens),
+                           device=d, pulse_next_timestamp_init=1) for d in devices]
+    g = shard.Group.open_gpu(opts, ledgers=L + 1, events_max=N, batch_count_max=len(lens),
+                             router_device=devices[0], router_account_capacity=P * L + 4096,
+                             router_transfer_capacity=N * (K + W) + 4096)
+    try:
+        acc = workload.group_accounts(L, P, seed=args.seed)
+        prepare_ts = len(acc) + 1
+        res = g.create_accounts(acc, [len(acc)], [prepare_ts])
+        assert (res["status"] == CREATED).all(), "group create_accounts"
+        d_ends = dev.upload(np.cumsum(lens).astype(np.uint32))
+        steps = []
         for s in range(W + K):
-            t, lg = routed_call(N1, world, A, args.seed, s)
+            if hazard_rate > 0:
+                t, kinds, src = workload.hazard_transfers(N, L, P, hazard_rate, seed=args.seed + s,
+                                                          id_offset=s * N)
+            else:
+                t, _ = workload.mixed_ledger_transfers(N, L, P, seed=args.seed + s,
+                                                       id_offset=s * N)
+                kinds = src = None
             ts, prepare_ts = step_timestamps(prepare_ts, lens)
-            steps.append((torch.from_numpy(t.view(np.uint8).reshape(-1)).to(dev),
-                          torch.from_numpy(ts.view(np.int64).copy()).to(dev),
-                          torch.zeros(N * 16, dtype=torch.uint8, device=dev)))
-            host_steps.append((ts, lg))
+            steps.append((dev.upload(t), dev.upload(ts), dev.alloc(N * 16), ts, kinds, src))
             del t
-    torch.cuda.synchronize(dev)
+        dev.sync()
 
-    def run_step(s):
-        if rank == 0:
-            d_ev, d_ts, d_res = steps[s]
-            mode = rs.create_transfers(d_ev.data_ptr(), N, d_ends.data_ptr(), d_ts.data_ptr(),
-                                       len(lens), d_res.data_ptr())
-            assert mode == 0, "the routed workload takes the device path"
-        else:
-            rs.create_transfers()
+        def run_step(s):
+            d_ev, d_ts, d_res = steps[s][:3]
+            g.create_transfers_device(d_ev.value, N, d_ends.value, d_ts.value, len(lens),
+                                      d_res.value)
 
-    for s in range(W):
-        run_step(s)
-    torch.cuda.synchronize(dev)
-    dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for s in range(W, W + K):
-        run_step(s)
-    torch.cuda.synchronize(dev)
-    dist.barrier()
-    t_max = max_over_ranks(dist, time.perf_counter() - t0)
+        for s in range(W):
+            run_step(s)
+        dev.sync()
+        t0 = time.perf_counter()
+        for s in range(W, W + K):
+            run_step(s)
+        dev.sync()
+        t_wall = time.perf_counter() - t0
+        st = g.stats()
 
-    # Validation: every result created at its exact timestamp (rank 0); every shard's accounts
-    # hold exactly the sums of its ledger's amounts over all steps.
-    ok = True
-    sums = torch.zeros(2 * A * world, dtype=torch.int64)
-    if rank == 0:
-        exp_d = np.zeros(A * world, dtype=np.uint64)
-        exp_c = np.zeros(A * world, dtype=np.uint64)
+        ok = st["device_calls"] == W + K and st["engine_calls"] == 1  # (the accounts call)
+        exp_d = np.zeros(L * P, dtype=np.uint64)
+        exp_c = np.zeros(L * P, dtype=np.uint64)
+        r = np.zeros(N, dtype=RESULT_DTYPE)
+        failed = 0
         for s in range(W + K):
-            r = steps[s][2].cpu().numpy().view(RESULT_DTYPE)
-            ts, _ = host_steps[s]
-            ok &= bool((r["status"] == CREATED).all() and
-                       (r["timestamp"] == event_timestamps(lens, ts)).all())
-            t, _ = routed_call(N1, world, A, args.seed, s)
+            _, _, d_res, ts, kinds, src = steps[s]
+            dev.download(d_res, r)
+            if hazard_rate > 0:
+                t, kinds, src = workload.hazard_transfers(N, L, P, hazard_rate, seed=args.seed + s,
+                                                          id_offset=s * N)
+            else:
+                t, _ = workload.mixed_ledger_transfers(N, L, P, seed=args.seed + s,
+                                                       id_offset=s * N)
+                kinds = np.full(N, -1, dtype=np.int64)
+                src = kinds
+            stamps = event_timestamps(lens, ts)
+            want_st, want_ts, created = workload.hazard_expected(t, kinds, src, stamps, L)
+            ok &= bool((r["status"] == want_st).all() and (r["timestamp"] == want_ts).all() and
+                       (r["reserved"] == 0).all())
+            failed += int((~created).sum())
             amt = t["amount"][:, 0]
-            np.add.at(exp_d, t["debit_account_id"][:, 0].astype(np.int64) - 1, amt)
-            np.add.at(exp_c, t["credit_account_id"][:, 0].astype(np.int64) - 1, amt)
-        sums = torch.from_numpy(np.concatenate([exp_d, exp_c]).view(np.int64).copy())
-    dist.broadcast(sums, 0) if not rs.nccl else None
-    if rs.nccl:
-        sd = sums.to(dev)
-        dist.broadcast(sd, 0)
-        sums = sd.cpu()
-    sums = sums.numpy().view(np.uint64)
-    dump = np.zeros(A, dtype=ACCOUNT_DTYPE)
-    lib.tbg_dump_accounts(rs.g, dump.ctypes.data_as(ctypes.c_void_p))
-    mine = slice(rank * A, (rank + 1) * A)
-    ok &= bool((dump["debits_posted"][:, 0] == sums[:A * world][mine]).all() and
-               (dump["credits_posted"][:, 0] == sums[A * world:][mine]).all())
-    flag = torch.tensor([0 if ok else 1], dtype=torch.int64, device=dev if rs.nccl else "cpu")
-    dist.all_reduce(flag, op=dist.ReduceOp.MAX)
-    validated = int(flag.item()) == 0
-    value = N * K / t_max
-    rs.close()
-    if rank != 0:
-        return None
-    return {
-        "value": round(value, 1), "unit": "transfers/s", "n_gpus": world, "steps": K,
-        "warmup": W, "ms_per_step": round(t_max / K * 1e3, 3), "validated": validated,
-        "workload": f"one mixed-ledger client stream of {N1} transfers per GPU over {world} "
-                    f"ledgers (10k accounts each, ledger uniform per event) entering at rank 0 in "
-                    f"HBM; device router + RCCL scatter/gather + settle in the timed region",
-        "transfers_per_step": N, "batches_per_step": int(len(lens)),
-        "calls": {"device_router": rs.fast_calls, "host_router": rs.host_calls},
-        "bound": "rank 0's xGMI fan-out: (N-1)/N of every event (128 B + 8 B timestamp) leaves "
-                 "rank 0 and 16 B of result returns",
-    }
+            np.add.at(exp_d, t["debit_account_id"][created, 0].astype(np.int64) - 1, amt[created])
+            np.add.at(exp_c, t["credit_account_id"][created, 0].astype(np.int64) - 1, amt[created])
+        rows = g.lookup_accounts(np.arange(1, L * P + 1))
+        ok &= len(rows) == L * P
+        if ok:
+            ok &= bool((rows["debits_posted"][:, 0] == exp_d).all() and
+                       (rows["credits_posted"][:, 0] == exp_c).all() and
+                       (rows["debits_posted"][:, 1] == 0).all() and
+                       (rows["debits_pending"] == 0).all() and (rows["credits_pending"] == 0).all())
+        return {
+            "value": round(N * K / t_wall, 1), "unit": "transfers/s", "steps": K, "warmup": W,
+            "ms_per_step": round(t_wall / K * 1e3, 3), "validated": bool(ok),
+            "shards": shards, "devices": list(devices), "transfers_per_step": N,
+            "batches_per_step": int(len(lens)), "accounts_per_shard": P,
+            "hazard_rate": hazard_rate, "injected_failures": failed,
+            "group_stats": st,
+            "workload": f"one mixed-ledger client call of {N1} transfers per shard per step over "
+                        f"{shards} ledgers ({P} accounts each, ledger uniform per event)" +
+                        (f", {hazard_rate:.2%} injected failures across ledgers"
+                         if hazard_rate > 0 else "") +
+                        f", entering in HBM on GPU {devices[0]}: device router + per-shard slices "
+                        f"(peer copies) + execution on every shard + settle, all timed",
+        }
+    finally:
+        g.close()
+        dev.free_all()
 
 
-def main():
-    args = parse_args()
-    world, rank, local, dist = dist_init(args)
-    if world > 1 and args.routed_only:
-        r = routed_measure(args, world, rank, local, dist, args.transfers or 10_000_000,
-                           args.steps, args.warmup)
-        if rank == 0:
-            line = {"metric": METRIC, "value": r["value"], "unit": "transfers/s", "n_gpus": world,
-                    "steps": r["steps"], "warmup": r["warmup"], "ms_per_step": r["ms_per_step"],
-                    "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-                    "dtype": "u128",
-                    "data": "synthetic (seeded; benchmark_load.zig distributions, sequential ids)",
-                    "config": {"workload": "config2 routed: " + r["workload"],
-                               "transfers_per_step": r["transfers_per_step"],
-                               "accounts_per_gpu": args.accounts or 10_000,
-                               "batches_per_step": r["batches_per_step"],
-                               "parallelism": f"ledger-shard x{world}, routed from rank 0"},
-                    "validated": r["validated"], "routed": r, "roofline": None,
-                    "cpu_baseline": None}
-            print(json.dumps(line))
-        dist.destroy_process_group()
-        return
+def single_line(args, world, rank, local, dist):
+    """The executor line: each rank's executor over its shard's batches of one client stream
+    (module doc), config 2 or 5. Returns rank 0's line (None elsewhere)."""
     wl = (Config5 if args.workload == "config5" else Config2)(args, rank, world)
     N, A, K, W = wl.N, wl.A, args.steps, args.warmup
     R = args.commit_reps if rank == 0 and world == 1 and not args.no_validate else 0
@@ -1077,9 +1046,6 @@ def main():
 
     if dist is not None and validated is not None:  # every shard validated its own partition
         validated = max_over_ranks(dist, 0.0 if validated else 1.0) == 0.0
-    routed = None
-    if world > 1 and not args.no_routed and wl.name == "config2":
-        routed = routed_measure(args, world, rank, local, dist, args.routed_transfers, 3, 1)
 
     value = N * K * world / t_max
     if rank == 0:
@@ -1101,11 +1067,63 @@ def main():
             "per_commit": commits,
             "with_account_events": with_ae,
         }
-        if world > 1:
-            line["routed"] = routed
-        print(json.dumps(line))
     lib.tbg_close(g)
     dev.free_all()
+    return line if rank == 0 else None
+
+
+def group_line(args, grp, world, extra):
+    """The JSON line whose `value` is the group's (group_measure)."""
+    return {
+        "metric": METRIC, "value": grp["value"], "unit": "transfers/s", "n_gpus": world,
+        "steps": grp["steps"], "warmup": grp["warmup"], "ms_per_step": grp["ms_per_step"],
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u128",
+        "data": "synthetic (seeded; benchmark_load.zig distributions, sequential ids)",
+        "config": {"workload": "config2 over ledger shards: " + grp["workload"],
+                   "transfers_per_step": grp["transfers_per_step"],
+                   "accounts_per_shard": grp["accounts_per_shard"],
+                   "batches_per_step": grp["batches_per_step"],
+                   "parallelism": f"ledger-shard x{grp['shards']} (one process, devices "
+                                  f"{grp['devices']}; tbg_group_create_transfers_device)"},
+        "validated": grp["validated"], "group": grp, **extra}
+
+
+def main():
+    args = parse_args()
+    world, rank, local, dist = dist_init(args)
+    K, W = args.steps, args.warmup
+    if args.group:
+        grp = group_measure(args, args.group, [args.group_device] * args.group,
+                            args.group_transfers, K, W)
+        print(json.dumps(group_line(args, grp, 1, {"roofline": None, "cpu_baseline": None})))
+        return
+    line = single_line(args, world, rank, local, dist)
+    if world == 1 and not args.no_hazard_call and not args.no_validate and \
+            args.workload == "config2":
+        # 1M-event calls with injected failures across ledgers over 2 shards on this GPU: the
+        # device path keeps them (tbg_group.h), validated in closed form
+        line["hazard_call"] = group_measure(args, 2, [local, local], 500_000, 5, 1,
+                                            hazard_rate=args.hazard_rate)
+    if world > 1 and not args.partitioned_line:
+        # The N-GPU line: rank 0 owns every shard's GPU through the group; the other ranks wait.
+        import torch
+        barrier(dist)
+        grp = None
+        if rank == 0:
+            n_dev = torch.cuda.device_count()
+            grp = group_measure(args, world, [s % n_dev for s in range(world)],
+                                args.group_transfers, K, W)
+        barrier(dist)
+        if rank == 0:
+            part = {k: line[k] for k in ("value", "ms_per_step", "validated", "config")}
+            part["note"] = ("N independent executors, each with its ledger's batches of one "
+                            "client stream resident in its HBM (no data-path collective)")
+            line = group_line(args, grp, world, {"roofline": line["roofline"],
+                                                 "roofline_source": "the partitioned run's "
+                                                                    "executor kernels",
+                                                 "cpu_baseline": None, "partitioned": part})
+    if rank == 0:
+        print(json.dumps(line))
     if dist is not None:
         dist.destroy_process_group()
 

@@ -5,20 +5,28 @@
  * assigns every event to the ledger shard (GPU) that holds its accounts, and scatters the call
  * into per-shard slices that keep every event's global commit timestamp (executed there with
  * tbg_create_transfers_stamped_device). Its directories -- account id -> shard, transfer id ->
- * shard (created and orphaned ids, `timed` when a pending transfer has a timeout) -- are HBM
- * open-addressing tables probed like the executor's id tables.
+ * shard (created and orphaned ids) -- are HBM open-addressing tables probed like the executor's
+ * id tables. The group (tbg_group.h) drives it.
  *
- * The device fast path (tbr_route_device) takes calls in which no event can observe another
- * shard's state: events whose id is new to every shard and unique in the call and whose two
- * accounts are known and on one shard; events whose id already exists (decided by the
- * id's holder, create_transfer_exists :3988-4051, before any account lookup); post/voids, on the
- * shard of their pending transfer (in the directory or created earlier in the call); and linked
- * chains whose events all go to one shard and end within their batch; imported events when every
- * event of the call is imported, their timestamps increase through the call, lie below their own
- * commit timestamps and above the imported floor (tbr_set_imported_floor). Any other event is a
- * *hazard*: the call is left to the exact engine (tigerbeetle_amd/shard.py, Engine), which reads
- * the same directories through tbr_account_shards / tbr_transfer_shards and records its outcome
- * with tbr_record_*.
+ * The device path (tbr_route_device) places:
+ *  * an event whose id already exists: on its holder (create_transfer_exists / id_already_failed,
+ *    :3733-3738, come before any account lookup);
+ *  * an event whose status follows from itself alone (nonzero padding, id 0 / maxInt, a nonzero
+ *    timestamp; an unknown debit and credit account; a post/void whose pending transfer exists
+ *    nowhere): on any shard (k mod shards, or its chain's);
+ *  * a transfer: on its accounts' shard, the known one's if the other is unknown; accounts on two
+ *    shards: a surrogate (credit := debit, accounts_must_be_different) whose status settle patches
+ *    to the reference's (:3756-3798);
+ *  * a post/void: on its pending transfer's shard (in the directory or created earlier in the
+ *    call);
+ *  * an id repeated in the call: on its first occurrence's shard, when its own placement allows;
+ *  * a linked chain: whole on one shard, closed within its batch;
+ *  * imported events: when every event of the call is imported, their timestamps increase
+ *    through the call, lie below their own commit timestamps and above the imported floor
+ *    (tbr_set_imported_floor).
+ * Any other event is a *hazard*: the call is left to the exact engine (tbg_group.h, engine.cpp),
+ * which reads the same directories through tbr_account_shards / tbr_transfer_shards and records its
+ * outcome with tbr_record_*.
  *
  * Reference: the shard boundary follows `accounts_must_have_the_same_ledger` /
  * `transfer_must_have_the_same_ledger_as_accounts` (src/state_machine.zig:3795-3798); transfer
@@ -35,13 +43,11 @@ extern "C" {
 
 typedef struct tbr_ctx tbr_ctx;
 
-#define TBR_TIMED 0x80u /* transfer directory: a pending transfer with a timeout */
-
 tbr_ctx* tbr_open(uint32_t shards, uint64_t account_capacity, uint64_t transfer_capacity,
                   uint32_t events_max, uint32_t device);
 void tbr_close(tbr_ctx* ctx);
 
-/* Directory access (host buffers). Lookups write the shard (| TBR_TIMED for transfers) or -1. */
+/* Directory access (host buffers). Lookups write the shard or -1. */
 int tbr_record_accounts(tbr_ctx* ctx, const tb_uint128_t* ids, const uint8_t* shards, uint32_t n);
 int tbr_record_transfers(tbr_ctx* ctx, const tb_uint128_t* ids, const uint8_t* shards, uint32_t n);
 int64_t tbr_account_shards(tbr_ctx* ctx, const tb_uint128_t* ids, uint32_t n, int32_t* out);
@@ -77,6 +83,9 @@ int64_t tbr_route_device(tbr_ctx* ctx, const tb_transfer_t* d_events, uint32_t n
 int tbr_settle_device(tbr_ctx* ctx, const tb_create_result_t* d_shard_results,
                       const uint32_t* d_positions, uint32_t n, tb_create_result_t* d_results,
                       uint64_t* created_timestamp_max);
+/* The last tbr_route_device call's counts: out[0] events placed anywhere, out[1] surrogates,
+ * out[2] repeats of an id of the call. */
+int tbr_route_stats(tbr_ctx* ctx, uint64_t* out);
 
 #ifdef __cplusplus
 }

@@ -1468,3 +1468,99 @@ void tbo_executor_fill(tbo_ctx* c, tb_executor* ex) {
     ex->query_accounts = ex_query_accounts;
     ex->query_transfers = ex_query_transfers;
 }
+
+/* ---- the shard executor interface (include/tbg_group.h tbg_shard_ops) ------------------------
+ * Test instrumentation: binds this oracle as one shard of a tbg_group_open_shards group, so the
+ * group's exact engine (tigerbeetle_amd/csrc/engine.cpp) runs over oracle shards in the CPU tests
+ * exactly as it runs over HIP executors. */
+static int sh_create_accounts(void* self, const tb_account_t* ev, uint32_t n, const uint32_t* lens,
+                              const uint64_t* bts, uint32_t nb, tb_create_result_t* out) {
+    (void)n;
+    tbo_create_accounts_batches((tbo_ctx*)self, ev, lens, bts, nb, out);
+    return 0;
+}
+static int sh_create_transfers(void* self, const tb_transfer_t* ev, uint32_t n,
+                               const uint32_t* lens, const uint64_t* bts, uint32_t nb,
+                               tb_create_result_t* out) {
+    (void)n;
+    tbo_create_transfers_batches((tbo_ctx*)self, ev, lens, bts, nb, out);
+    return 0;
+}
+static int sh_create_accounts_stamped(void* self, const tb_account_t* ev, uint32_t n,
+                                      const uint64_t* st, uint64_t bts, uint32_t opt,
+                                      tb_create_result_t* out) {
+    tbo_create_accounts_stamped((tbo_ctx*)self, ev, n, st, bts, opt, out);
+    return 0;
+}
+static int sh_create_transfers_stamped(void* self, const tb_transfer_t* ev, uint32_t n,
+                                       const uint64_t* st, uint64_t bts, uint32_t opt,
+                                       tb_create_result_t* out) {
+    tbo_create_transfers_stamped((tbo_ctx*)self, ev, n, st, bts, opt, out);
+    return 0;
+}
+static int64_t sh_forget_orphans(void* self, const tb_uint128_t* ids, uint32_t n) {
+    return (int64_t)tbo_forget_orphans((tbo_ctx*)self, ids, n);
+}
+static int64_t sh_timestamps_exist(void* self, int transfers, const uint64_t* ts, uint32_t n,
+                                   uint8_t* out) {
+    return (int64_t)tbo_timestamps_exist((const tbo_ctx*)self, transfers, ts, n, out);
+}
+static int sh_key_max(void* self, uint64_t* a, uint64_t* t) {
+    tbo_key_max((const tbo_ctx*)self, a, t);
+    return 0;
+}
+static int sh_raise_key_max(void* self, uint64_t a, uint64_t t) {
+    tbo_raise_key_max((tbo_ctx*)self, a, t);
+    return 0;
+}
+static int sh_set_pnt_sharded(void* self, int on) {
+    tbo_pnt_sharded((tbo_ctx*)self, on);
+    return 0;
+}
+/* tbg_pnt_ops' contract: the count (nothing copied) with ts == NULL; else up to `max` copied. */
+static int64_t sh_pnt_ops(void* self, uint64_t* ts, uint64_t* ops, uint64_t max, uint64_t* start) {
+    tbo_ctx* c = (tbo_ctx*)self;
+    if (!ts || !ops) return (int64_t)tbo_pnt_ops(c, NULL, NULL, start);
+    if (c->n_pnt > max) return -22;
+    return (int64_t)tbo_pnt_ops(c, ts, ops, start);
+}
+static uint64_t sh_pulse_next(void* self) { return tbo_pulse_next_timestamp((tbo_ctx*)self); }
+static int sh_set_pulse_next(void* self, uint64_t v) {
+    tbo_set_pulse_next_timestamp((tbo_ctx*)self, v);
+    return 0;
+}
+static int64_t sh_pulse_candidates(void* self, uint64_t ts, uint64_t* e, uint64_t* t,
+                                   uint32_t max) {
+    return (int64_t)tbo_pulse_candidates((tbo_ctx*)self, ts, e, t, max);
+}
+static int64_t sh_pulse_cut(void* self, uint64_t ts, uint64_t ce, uint64_t ct, uint64_t pnt,
+                            const uint64_t* stamps) {
+    return (int64_t)tbo_pulse_cut((tbo_ctx*)self, ts, ce, ct, pnt, stamps);
+}
+static int64_t sh_lookup_accounts(void* self, const tb_uint128_t* ids, uint32_t n,
+                                  tb_account_t* out) {
+    return (int64_t)tbo_lookup_accounts((const tbo_ctx*)self, ids, n, out);
+}
+static int64_t sh_lookup_transfers(void* self, const tb_uint128_t* ids, uint32_t n,
+                                   tb_transfer_t* out) {
+    return (int64_t)tbo_lookup_transfers((const tbo_ctx*)self, ids, n, out);
+}
+
+void tbo_shard_ops_fill(tbg_shard_ops* ops) {
+    ops->create_accounts = sh_create_accounts;
+    ops->create_transfers = sh_create_transfers;
+    ops->create_accounts_stamped = sh_create_accounts_stamped;
+    ops->create_transfers_stamped = sh_create_transfers_stamped;
+    ops->forget_orphans = sh_forget_orphans;
+    ops->timestamps_exist = sh_timestamps_exist;
+    ops->key_max = sh_key_max;
+    ops->raise_key_max = sh_raise_key_max;
+    ops->set_pnt_sharded = sh_set_pnt_sharded;
+    ops->pnt_ops = sh_pnt_ops;
+    ops->pulse_next_timestamp = sh_pulse_next;
+    ops->set_pulse_next_timestamp = sh_set_pulse_next;
+    ops->pulse_candidates = sh_pulse_candidates;
+    ops->pulse_cut = sh_pulse_cut;
+    ops->lookup_accounts = sh_lookup_accounts;
+    ops->lookup_transfers = sh_lookup_transfers;
+}

@@ -14,6 +14,7 @@
 
 #include "../include/tb_types.h"
 #include "../include/tb_state_machine.h"
+#include "../include/tbg_group.h"
 
 #ifdef __cplusplus
 extern "C" {
@@ -126,6 +127,8 @@ void tbo_set_pulse_next_timestamp(tbo_ctx* ctx, uint64_t value);
 
 /* Binds this oracle as a tb_executor (tb_state_machine.h) for the StateMachine mirror. */
 void tbo_executor_fill(tbo_ctx* ctx, tb_executor* ex);
+/* The shard executor interface (tbg_group.h) over tbo_ctx shards: tbg_group_open_shards. */
+void tbo_shard_ops_fill(tbg_shard_ops* ops);
 
 #ifdef __cplusplus
 }

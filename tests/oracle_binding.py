@@ -49,6 +49,7 @@ _SIGS = [
     ("tbo_query_accounts", ctypes.c_int64, [vp, vp, ctypes.c_uint32, vp]),
     ("tbo_query_transfers", ctypes.c_int64, [vp, vp, ctypes.c_uint32, vp]),
     ("tbo_executor_fill", None, [vp, ctypes.POINTER(native.Executor)]),
+    ("tbo_shard_ops_fill", None, [vp]),
 ]
 
 _lib = None

@@ -1,23 +1,21 @@
-"""The routed data path (tigerbeetle_amd/routed.py): the device router, per-shard stamped
+"""The routed data path of the group (include/tbg_group.h): the device router, per-shard stamped
 execution, results gathered to call order -- against one unsharded oracle, call by call, and the
-union of the shards' final tables against the oracle's.
+union of the shards' final tables and AccountEvents against the oracle's.
 
-Two ranks on the box's one GPU, over gloo (host staging; RCCL needs one GPU per rank): rank 0
-holds the client calls in HBM and the device router; each rank owns two of four ledgers. The
-calls take the device path -- interleaved ledgers and fresh ids; a linked chain on one shard,
-resubmitted ids (on their holders), posts / voids of pending transfers (on their pending
-transfer's shard), with and without a timeout: a post/void of the earliest-expiring one resets
-pulse_next_timestamp, resolved across the shards after the call -- except the one the device
-router must hand to the exact host router (a transfer between two shards' accounts); pending
-transfers expire in sharded pulses. Every shard
-records AccountEvents, and the union of the shards' logs must be the oracle's (the ADVICE item:
-the appends a device call leaves on the executor's stream read the call's buffers).
+One process owns two executors on the box's one GPU (the group's shards; on a node, one per GPU):
+the client calls are in HBM on the router's GPU (tbg_group_create_transfers_device), some come as
+host buffers (tbg_group_create_transfers). Each call is expected on a path -- the device path
+(interleaved ledgers and fresh ids; a linked chain on one shard; resubmitted ids on their holders;
+posts / voids of pending transfers on their pending transfer's shard, with and without a timeout:
+a post/void of the earliest-expiring one resets pulse_next_timestamp, resolved across the shards
+after the call; a transfer between the two shards' accounts as a surrogate; events whose status
+follows from themselves alone; ids repeated within the call on one shard) or the exact engine (a
+linked chain across the two shards failing transiently on its second shard, an imported call
+regressing across shards, an id repeated on the other shard's accounts); pending transfers expire
+in sharded pulses.
 """
-import multiprocessing as mp
 import os
-import socket
 import sys
-import traceback
 
 import numpy as np
 import pytest
@@ -26,20 +24,14 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
 sys.path.insert(0, HERE)
 
-pytestmark = pytest.mark.gpu
 
 LEDGERS = 4
 PER_LEDGER = 200
 
 
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
 def _calls(seed):
-    """(kind, events, lens) ops; kind "fast" calls are expected on the device path."""
+    """(kind, events, lens) ops; kind "device" / "engine": the path the call is expected on
+    ("-host": passed as host buffers, "-imported": imported timestamps in a gap before the call)."""
     from tigerbeetle_amd import workload
     from tigerbeetle_amd.types import TRANSFER_DTYPE
     rng = np.random.default_rng(seed)
@@ -69,11 +61,20 @@ def _calls(seed):
         return t
 
     fast1 = uniform(30_000, pending_frac=0.1)
-    ops.append(("fast", fast1, [8189, 8189, 8189, 30_000 - 3 * 8189]))
+    ops.append(("device", fast1, [8189, 8189, 8189, 30_000 - 3 * 8189]))
     cross = uniform(2_000)
     # (ledgers 1, 2 on shard 0 and 3, 4 on shard 1: the credit account two ledgers over)
-    cross["credit_account_id"][5, 0] = ((int(cross["ledger"][5]) + 1) % LEDGERS) * PER_LEDGER + 8
-    ops.append(("host", cross, [2_000]))  # a transfer between two shards' accounts
+    for j in (5, 77, 78, 901):
+        cross["credit_account_id"][j, 0] = ((int(cross["ledger"][j]) + 1) % LEDGERS) * \
+            PER_LEDGER + 8
+    cross["ledger"][77] = 0        # ledger_must_not_be_zero (patched in)
+    cross["timeout"][78] = 5       # timeout_reserved_for_pending_transfer (patched in)
+    cross["flags"][900:902] = 1, 0  # ... in a linked chain (failing it)
+    cross["debit_account_id"][900] = cross["debit_account_id"][901]
+    cross["credit_account_id"][900, 0] = int(cross["debit_account_id"][901, 0]) % PER_LEDGER + 1 + \
+        (int(cross["debit_account_id"][901, 0]) - 1) // PER_LEDGER * PER_LEDGER
+    cross["ledger"][900] = cross["ledger"][901]
+    ops.append(("device-host", cross, [2_000]))  # transfers between two shards' accounts
     haz = uniform(3_000)
     haz["flags"][10:13] |= 1  # a chain (same ledger: set its accounts)
     for j in range(10, 14):
@@ -92,7 +93,7 @@ def _calls(seed):
         haz["ledger"][e] = 0
         haz["code"][e] = 0
         haz["timeout"][e] = 0
-    ops.append(("fast", haz, [3_000]))
+    ops.append(("device", haz, [3_000]))
     # posts / voids of pending transfers with a timeout, the earliest-expiring one first (its
     # expiry is pulse_next_timestamp: the reset fires), among new pending transfers and transfers
     timed_ids = fast1["id"][(fast1["flags"] == 2) & (fast1["timeout"] == 1), 0][:40]
@@ -107,9 +108,46 @@ def _calls(seed):
         tpv["ledger"][e] = 0
         tpv["code"][e] = 0
         tpv["timeout"][e] = 0
-    ops.append(("fast", tpv, [4_000]))
+    ops.append(("device", tpv, [4_000]))
     ops.append(("tick", 2_000_000_000))
-    ops.append(("fast", uniform(20_000), [8189, 20_000 - 8189]))
+    ops.append(("device", uniform(20_000), [8189, 20_000 - 8189]))
+    # events whose status follows from themselves alone, unknown accounts, posts / voids of
+    # pending transfers found nowhere, ids repeated within the call on one shard: the device path
+    bad = uniform(6_000)
+    bad["flags"][10] |= 1 << 12                       # reserved_flag
+    bad["id"][11] = 0                                 # id_must_not_be_zero
+    bad["id"][12] = [2**64 - 1, 2**64 - 1]            # id_must_not_be_int_max
+    bad["timestamp"][13] = 99                         # timestamp_must_be_zero
+    bad["debit_account_id"][14, 0] = 555_555          # debit_account_not_found (transient)
+    bad["credit_account_id"][15, 0] = 555_556         # credit_account_not_found
+    bad["debit_account_id"][16, 0] = 555_557          # both unknown
+    bad["credit_account_id"][16, 0] = 555_558
+    bad["flags"][17] = 4                              # post of a pending transfer found nowhere
+    bad["pending_id"][17, 0] = 424_242
+    bad["id"][300] = bad["id"][20]                    # repeats of created ids (exists*)
+    bad["debit_account_id"][300] = bad["debit_account_id"][20]
+    bad["credit_account_id"][300] = bad["credit_account_id"][20]
+    bad["ledger"][300] = bad["ledger"][20]
+    bad["amount"][300, 0] = 1                         # exists_with_different_amount
+    bad["id"][301] = bad["id"][14]                    # repeat of an orphaned id: id_already_failed
+    bad["debit_account_id"][301] = bad["debit_account_id"][14]
+    bad["credit_account_id"][301] = bad["credit_account_id"][14]
+    bad["ledger"][301] = bad["ledger"][14]
+    bad["id"][302] = bad["id"][11]                    # id 0 again
+    bad["flags"][400:403] = 1, 1, 0                   # a chain with an unknown account (fails)
+    for j in (400, 401, 402):
+        bad["ledger"][j] = 2
+        bad["debit_account_id"][j, 0] = PER_LEDGER + 3 + j % 5
+        bad["credit_account_id"][j, 0] = PER_LEDGER + 10 + j % 3
+    bad["credit_account_id"][401, 0] = 777_777
+    ops.append(("device", bad, [3_000, 3_000]))
+    rep = uniform(2_000)
+    rep["id"][900] = rep["id"][100]                   # an id repeated on the other shard's accounts
+    rep["ledger"][900] = 1 + (int(rep["ledger"][100]) + 1) % LEDGERS
+    rep["debit_account_id"][900, 0] = (int(rep["ledger"][900]) - 1) * PER_LEDGER + 1
+    rep["credit_account_id"][900, 0] = (int(rep["ledger"][900]) - 1) * PER_LEDGER + 2
+    rep["debit_account_id"][100, 0] = 888_888        # (the first occurrence fails: not found)
+    ops.append(("engine", rep, [2_000]))
     # a linked chain across the two shards, failing transiently on its second shard: the host
     # engine's chain protocol (probe, the first failure across shards, the orphan kept)
     xc = uniform(1_000)
@@ -119,45 +157,35 @@ def _calls(seed):
         xc["debit_account_id"][j, 0] = (lg - 1) * PER_LEDGER + 1 + j % 7
         xc["credit_account_id"][j, 0] = (lg - 1) * PER_LEDGER + 20 + j % 5
     xc["debit_account_id"][302, 0] = 999_999  # debit_account_not_found
-    ops.append(("host", xc, [1_000]))
+    ops.append(("engine", xc, [1_000]))
     # imported calls (timestamps in a gap before the call, increasing): on the device path above
     # the floor; then with a regress across shards on the host engine
     imp = uniform(3_000)
     imp["flags"] |= 256
-    ops.append(("fast-imported", imp, [1_500, 1_500]))
+    ops.append(("device-imported", imp, [1_500, 1_500]))
     imp2 = uniform(500)
     imp2["flags"] |= 256
-    ops.append(("host-imported", imp2, [500]))
-    ops.append(("fast", uniform(5_000), [5_000]))
+    ops.append(("engine-imported", imp2, [500]))
+    ops.append(("device-host", uniform(5_000), [5_000]))
     return ops
 
 
-def _rank(rank, world, port, seed, q):
+@pytest.mark.gpu
+def test_group_routed_device_path():
+    from hipmem import Hip
+    from test_shard import OracleShard, assert_same_state
+    from tigerbeetle_amd import native, shard
+    from tigerbeetle_amd.types import RESULT_DTYPE, TIMESTAMP_MAX
+    opts = [native.options(4096, 1 << 18, 1 << 16, pulse_next_timestamp_init=TIMESTAMP_MAX,
+                           account_events_capacity=1 << 18) for _ in range(2)]
+    g = shard.Group.open_gpu(opts, ledgers=LEDGERS, events_max=1 << 16,
+                             router_transfer_capacity=1 << 19, router_account_capacity=4096)
+    views = [shard.GpuShard.wrap(g.lib, g.shard(s)) for s in range(2)]
+    ref = OracleShard()
+    hip = Hip(0)
+    ts, pulses = 0, 0
     try:
-        os.environ["MASTER_ADDR"] = "127.0.0.1"
-        os.environ["MASTER_PORT"] = str(port)
-        import torch
-        import torch.distributed as dist
-        torch.cuda.set_device(0)
-        dist.init_process_group("gloo", rank=rank, world_size=world)
-        from test_shard import OracleShard, assert_same_state
-        from tigerbeetle_amd import native
-        from tigerbeetle_amd.routed import RoutedShards
-        from tigerbeetle_amd.types import RESULT_DTYPE, TIMESTAMP_MAX
-        o = native.TbgOptions()
-        o.account_capacity = 4096
-        o.transfer_capacity = 1 << 18
-        o.batch_events_max = 1 << 16
-        o.batch_count_max = 4096
-        o.pulse_batch_max = 8190
-        o.device = 0
-        o.pulse_next_timestamp_init = TIMESTAMP_MAX
-        o.account_events_capacity = 1 << 18
-        rs = RoutedShards(o, events_max=1 << 16, router_transfer_capacity=1 << 19,
-                          router_account_capacity=4096, ledgers=LEDGERS)
-        ref = OracleShard() if rank == 0 else None
-        ts, pulses = 0, 0
-        for op in _calls(seed):
+        for i, op in enumerate(_calls(3)):
             if op[0] == "tick":
                 ts += op[1]
             else:
@@ -166,86 +194,137 @@ def _rank(rank, world, port, seed, q):
                 if kind.endswith("-imported"):  # timestamps in a gap before the call
                     ev = ev.copy()
                     ev["timestamp"] = ts + 1 + np.arange(n, dtype=np.uint64)
-                    if kind.startswith("host"):
+                    if kind.startswith("engine"):
                         ev["timestamp"][[10, 11]] = ev["timestamp"][[11, 10]]  # a regress
                     ts += n
-                    kind = kind.split("-")[0]
                 ts += 1 + n
                 batch_ts = (ts - n + np.cumsum(lens)).astype(np.uint64)
                 if kind == "accounts":
-                    got = rs.create_accounts(ev, lens, batch_ts) if rank == 0 \
-                        else rs.create_accounts()
-                    if rank == 0:
-                        want = ref.create_accounts(ev, lens, batch_ts)
-                        assert got.tobytes() == want.tobytes(), "accounts"
+                    got = g.create_accounts(ev, lens, batch_ts)
+                    want = ref.create_accounts(ev, lens, batch_ts)
+                    assert got.tobytes() == want.tobytes(), "accounts"
+                    continue
+                before = g.stats()
+                if kind.endswith("-host"):
+                    got = g.create_transfers(ev, lens, batch_ts)
                 else:
-                    if rank == 0:
-                        dev = torch.device("cuda", 0)
-                        d_ev = torch.from_numpy(ev.view(np.uint8).copy()).to(dev)
-                        d_ends = torch.from_numpy(np.cumsum(lens).astype(np.int32)).to(dev)
-                        d_ts = torch.from_numpy(batch_ts.view(np.int64).copy()).to(dev)
-                        d_res = torch.zeros(n * 16, dtype=torch.uint8, device=dev)
-                        torch.cuda.synchronize()
-                        mode = rs.create_transfers(d_ev.data_ptr(), n, d_ends.data_ptr(),
-                                                   d_ts.data_ptr(), len(lens), d_res.data_ptr(),
-                                                   host_call=(ev, lens, batch_ts))
-                        assert mode == (0 if kind == "fast" else 1), (kind, mode)
-                        got = d_res.cpu().numpy().view(RESULT_DTYPE)
-                        want = ref.create_transfers(ev, lens, batch_ts)
-                        if got.tobytes() != want.tobytes():
-                            bad = np.nonzero(got != want)[0]
-                            raise AssertionError(f"{kind} call: {len(bad)} results differ, first "
-                                                 f"{bad[:5].tolist()}: {got[bad[:3]]} vs "
-                                                 f"{want[bad[:3]]}")
-                    else:
-                        rs.create_transfers()
-            nxt = rs.pulse_next_timestamp()
-            if rank == 0:
-                assert nxt == ref.pulse_next_timestamp()
+                    got = _group_call(g, hip, ev, lens, batch_ts)
+                after = g.stats()
+                path = "device" if after["device_calls"] > before["device_calls"] else "engine"
+                assert path == kind.split("-")[0], (i, kind, path)
+                want = ref.create_transfers(ev, lens, batch_ts)
+                if got.tobytes() != want.tobytes():
+                    bad = np.nonzero(got != want)[0]
+                    raise AssertionError(f"{kind} call: {len(bad)} results differ, first "
+                                         f"{bad[:5].tolist()}: {got[bad[:3]]} vs "
+                                         f"{want[bad[:3]]}")
+            nxt = g.pulse_next_timestamp()
+            assert nxt == ref.pulse_next_timestamp()
             if nxt <= ts:
                 ts += 1 + 8190
-                expired = rs.pulse(ts)
-                if rank == 0:
-                    assert expired == ref.pulse(ts)
+                assert g.pulse(ts) == ref.pulse(ts)
                 pulses += 1
-        dumps = [None] * world
-        dist.all_gather_object(dumps, rs.shard.dump())
-        events = [None] * world
-        dist.all_gather_object(events, rs.shard.dump_account_events())
-        if rank == 0:
-            assert all(len(d[1]) for d in dumps), "every shard holds transfers"
-            assert_same_state(dumps, ref)
-            got = np.concatenate(events)
-            got = got[np.argsort(got["timestamp"], kind="stable")]
-            want = ref.dump_account_events()
-            assert len(got) > 50_000 and got.tobytes() == want.tobytes(), \
-                f"account events differ ({len(got)} vs {len(want)})"
-            assert rs.fast_calls == 6 and rs.host_calls == 3, (rs.fast_calls, rs.host_calls)
-            assert pulses > 0
-        rs.close()
-        dist.barrier()
-        dist.destroy_process_group()
-        q.put((rank, None))
-    except BaseException:  # noqa: BLE001 -- reported to the parent
-        q.put((rank, traceback.format_exc()))
-
-
-def test_routed_shards_world2():
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_rank, args=(r, 2, port, 3, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    out = {}
-    try:
-        for _ in range(2):
-            rank, err = q.get(timeout=240)
-            out[rank] = err
+        dumps = [v.dump() for v in views]
+        assert all(len(d[1]) for d in dumps), "every shard holds transfers"
+        events = [v.dump_account_events() for v in views]
+        assert sum(len(e) for e in events) > 50_000
+        assert_same_state(dumps, ref, events)
+        st = g.stats()
+        assert st["surrogates"] >= 4 and st["anywhere"] >= 8 and st["repeats"] >= 2, st
+        assert pulses > 0
     finally:
-        for p in procs:
-            p.join(timeout=30)
-            if p.is_alive():
-                p.kill()
-    for rank, err in sorted(out.items()):
-        assert err is None, f"rank {rank}:\n{err}"
+        g.close()
+        ref.close()
+        hip.free_all()
+
+
+def _group_call(g, hip, t, lens, batch_ts):
+    """One tbg_group_create_transfers_device call (the call's buffers on the router's GPU)."""
+    from tigerbeetle_amd.types import RESULT_DTYPE
+    n = len(t)
+    d_ev = hip.upload(t)
+    d_ends = hip.upload(np.cumsum(lens).astype(np.uint32))
+    d_ts = hip.upload(np.ascontiguousarray(batch_ts, dtype=np.uint64))
+    d_res = hip.zeros(n * 16)
+    g.create_transfers_device(d_ev, n, d_ends, d_ts, len(lens), d_res)
+    out = hip.download(d_res, np.zeros(n, dtype=RESULT_DTYPE))
+    hip.free_all()
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shards", [2, 3])
+def test_group_hazard_calls_on_device(shards):
+    """Calls of mixed-ledger transfers with injected failures across ledgers (bench.py's
+    `hazard_call`: unknown accounts, cross-ledger accounts, id 0, reserved flags, posts of pending
+    transfers found nowhere, exact repeats) stay on the device path: exact against the oracle and
+    against the closed form the bench validates with; the balances match."""
+    from hipmem import Hip
+    from test_shard import OracleShard
+    from tigerbeetle_amd import native, shard, workload
+    from tigerbeetle_amd.types import TIMESTAMP_MAX
+    L, P, n = shards, 5_000, 200_000
+    opts = [native.options(L * P, 1 << 20, n, pulse_next_timestamp_init=TIMESTAMP_MAX)
+            for _ in range(shards)]
+    g = shard.Group.open_gpu(opts, ledgers=L + 1, events_max=n, router_transfer_capacity=1 << 21,
+                             router_account_capacity=L * P + 16)
+    ref = OracleShard()
+    hip = Hip(0)
+    try:
+        acc = workload.group_accounts(L, P, seed=5)
+        lens = [len(acc)]
+        assert (g.create_accounts(acc, lens, [len(acc) + 1])["status"] == 0xFFFFFFFF).all()
+        ref.create_accounts(acc, lens, [len(acc) + 1])
+        ts = len(acc) + 1
+        for step in range(3):
+            t, kinds, src = workload.hazard_transfers(n, L, P, rate=0.002, seed=10 + step,
+                                                      id_offset=step * n)
+            lens = [8189] * (n // 8189) + [n % 8189]
+            batch_ts = (ts + np.cumsum(np.asarray(lens) + 1)).astype(np.uint64)
+            ts = int(batch_ts[-1])
+            before = g.stats()
+            got = _group_call(g, hip, t, lens, batch_ts)
+            after = g.stats()
+            assert after["device_calls"] == before["device_calls"] + 1, "device path"
+            want = ref.create_transfers(t, lens, batch_ts)
+            assert got.tobytes() == want.tobytes(), np.nonzero(got != want)[0][:8]
+            stamps = (np.repeat(batch_ts - np.asarray(lens, np.uint64), lens) +
+                      np.arange(n, dtype=np.uint64) -
+                      np.repeat(np.cumsum(lens) - lens, lens).astype(np.uint64) + np.uint64(1))
+            st, tts, _ = workload.hazard_expected(t, kinds, src, stamps, L)
+            assert (got["status"] == st).all() and (got["timestamp"] == tts).all()
+        ids = np.arange(1, L * P + 1)
+        got = g.lookup_accounts(ids)
+        want = ref.lookup_accounts(ids)
+        assert len(got) == L * P
+        assert all(got[i].tobytes() == want[int(got[i]["id"][0])].tobytes()
+                   for i in range(0, L * P, 97))
+    finally:
+        g.close()
+        ref.close()
+        hip.free_all()
+
+
+def test_hazard_expected_closed_form():
+    """The closed form bench.py validates its hazard calls with equals the oracle's serial
+    results (CPU, unsharded)."""
+    from test_shard import OracleShard
+    from tigerbeetle_amd import workload
+    from tigerbeetle_amd.types import TIMESTAMP_MAX  # noqa: F401
+    ref = OracleShard()
+    try:
+        L, P, n = 3, 500, 20_000
+        acc = workload.group_accounts(L, P, seed=2)
+        ref.create_accounts(acc, [len(acc)], [len(acc) + 1])
+        t, kinds, src = workload.hazard_transfers(n, L, P, rate=0.01, seed=4)
+        lens = [8189, 8189, n - 2 * 8189]
+        batch_ts = (len(acc) + 1 + np.cumsum(np.asarray(lens) + 1)).astype(np.uint64)
+        want = ref.create_transfers(t, lens, batch_ts)
+        stamps = (np.repeat(batch_ts - np.asarray(lens, np.uint64), lens) +
+                  np.arange(n, dtype=np.uint64) -
+                  np.repeat(np.cumsum(lens) - lens, lens).astype(np.uint64) + np.uint64(1))
+        st, tts, created = workload.hazard_expected(t, kinds, src, stamps, L)
+        assert (want["status"] == st).all() and (want["timestamp"] == tts).all()
+        assert (kinds >= 0).sum() == n // 100 and created.sum() == n - n // 100
+    finally:
+        ref.close()

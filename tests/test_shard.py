@@ -1,18 +1,15 @@
-"""Ledger sharding (tigerbeetle_amd/shard.py) against one unsharded executor.
+"""Ledger sharding (include/tbg_group.h: the C++ group and its exact engine, csrc/engine.cpp)
+against one unsharded executor.
 
-The CPU oracle stands in for every shard here (test infrastructure). The router and both drivers
--- LocalShards (all shards in one process) and ShardGroup (one shard per rank over
-torch.distributed gloo, world_size 2, 127.0.0.1) -- must give the unsharded oracle's results call
+The CPU oracle stands in for every shard here (test infrastructure, bound through the shard
+executor interface, tbo_shard_ops_fill). The group must give the unsharded oracle's results call
 by call, the same pulse_next_timestamp and pulse counts, and shard tables whose union in
-timestamp order is the unsharded tables byte for byte. The GPU test runs LocalShards over two HBM
-executors on cuda:0.
+timestamp order is the unsharded tables byte for byte. The GPU tests run the group over two or
+three HBM executors on cuda:0.
 """
 import ctypes
-import multiprocessing as mp
 import os
-import socket
 import sys
-import traceback
 
 import numpy as np
 import pytest
@@ -408,7 +405,7 @@ def scenario(seed, calls=8, n_acc=48, timed_post_void=True):
     return ops
 
 
-def drive(cluster, ref, ops, rank0=True, pbm=PBM, cuts=None):
+def drive(cluster, ref, ops, pbm=PBM, cuts=None):
     """Runs `ops` through `cluster` (and `ref`, compared call by call); returns the pulses run.
     Timestamps follow the TestContext rule (prepare_ts += 1 + events, pulses when due). `cuts`
     (a list) collects the pulses that expired exactly pbm transfers (a cut across shards)."""
@@ -421,9 +418,8 @@ def drive(cluster, ref, ops, rank0=True, pbm=PBM, cuts=None):
                 _, kind, ev, lens, fix = op
                 lo = ts + 1
                 ts += len(ev)
-                if rank0:
-                    ev = ev.copy()
-                    fix(ev, lo, ref)
+                ev = ev.copy()
+                fix(ev, lo, ref)
             else:
                 kind, ev, lens = op
             if kind == "imported":  # timestamps after every object so far, before the batch's
@@ -434,7 +430,7 @@ def drive(cluster, ref, ops, rank0=True, pbm=PBM, cuts=None):
             ts += 1 + n
             batch_ts = (ts - n + np.cumsum(lens)).astype(np.uint64)
             fn = getattr(cluster, "create_" + kind)
-            got = fn(ev, lens, batch_ts) if rank0 else fn()
+            got = fn(ev, lens, batch_ts)
             if ref is not None:
                 want = getattr(ref, "create_" + kind)(ev, lens, batch_ts)
                 if got.tobytes() != want.tobytes():
@@ -502,90 +498,107 @@ def _created(n, ts):
     return r
 
 
-def _plan(router, kind, events, lens, batch_ts, known=None, collisions=None):
-    """Segments the planner cuts a call into, as (start, end, chain, shard_of) -- planned against
-    fixed directories (no segment executes in between)."""
-    c = shard._Call(kind, np.ascontiguousarray(events, dtype=kind.dtype), lens, batch_ts)
-    kn = known or shard._Known()
-    p = shard.Planner(router, c, kn, collisions or {})
-    out, pos = [], 0
-    while pos < c.n:
-        seg = p.plan(pos)
-        out.append((seg.start, seg.end, seg.chain, [seg.shard_of[k] for k in range(seg.start,
-                                                                                     seg.end)]))
-        pos = seg.end
-    return out, c
+def oracle_group(shards, pbm=PBM, **kw):
+    """The C++ group over oracle shards (tbg_group_open_shards)."""
+    ops = shard.ShardOps()
+    oracle_binding.load().tbo_shard_ops_fill(ctypes.byref(ops))
+    return shard.Group.open_shards(ops, [s.o for s in shards], ledgers=LEDGERS,
+                                   pulse_batch_max=pbm, **kw)
+
+
+def gpu_group(n, pbm=PBM, account_capacity=1 << 12, transfer_capacity=1 << 16,
+              batch_events_max=4096, account_events_capacity=1 << 16, **kw):
+    """The C++ group over `n` HBM executors on cuda:0, and GpuShard views of them (dumps)."""
+    from tigerbeetle_amd import native
+    opts = [native.options(account_capacity, transfer_capacity, batch_events_max,
+                           pulse_batch_max=pbm, account_events_capacity=account_events_capacity)
+            for _ in range(n)]
+    kw.setdefault("events_max", batch_events_max)
+    kw.setdefault("router_transfer_capacity", 1 << 20)
+    g = shard.Group.open_gpu(opts, ledgers=LEDGERS, pulse_batch_max=pbm, **kw)
+    views = [shard.GpuShard.wrap(g.lib, g.shard(s)) for s in range(n)]
+    return g, views
 
 
 def test_planner_places_and_segments():
-    r = shard.LedgerRouter(2, ledgers=4)  # ledgers 1, 2 -> shard 0; 3, 4 -> shard 1
-    kn = shard._Known(accounts={1: 0, 2: 0, 3: 1, 4: 1})
-    T = shard.TRANSFERS
-    ok = _transfers([dict(id=10, debit_account_id=1, credit_account_id=2, amount=1, ledger=1, code=1),
-                     dict(id=11, debit_account_id=3, credit_account_id=4, amount=1, ledger=3, code=1),
-                     dict(id=12, debit_account_id=99, credit_account_id=4, amount=1, ledger=3,
-                          code=1)])  # missing debit account: the credit account's shard
-    segs, _ = _plan(r, T, ok, [3], [20], kn)
-    assert segs == [(0, 3, False, [0, 1, 1])]
-    # an existing id goes to its holder, whatever accounts it names
-    kn.transfers[11] = (1, False)
-    again = _transfers([dict(id=11, debit_account_id=1, credit_account_id=2, amount=1, ledger=1,
-                             code=1)])
-    assert _plan(r, T, again, [1], [30], kn)[0] == [(0, 1, False, [1])]
-    # accounts on two shards: a surrogate with the reference's status
-    cross = _transfers([dict(id=13, debit_account_id=1, credit_account_id=3, amount=1, ledger=1,
-                             code=1),
-                        dict(id=14, debit_account_id=1, credit_account_id=3, amount=1, ledger=0,
-                             code=1)])
-    c = shard._Call(T, cross, [2], [40])
-    seg = shard.Planner(r, c, kn, {}).plan(0)
-    assert seg.cross == {0: 23, 1: 19}  # accounts_must_have_the_same_ledger, ledger_must_not_be_zero
-    # a linked chain across shards: a segment of its own, between the segments around it
-    chain = _transfers([
-        dict(id=20, debit_account_id=1, credit_account_id=2, amount=1, ledger=1, code=1),
-        dict(id=21, debit_account_id=1, credit_account_id=2, amount=1, ledger=1, code=1, flags=1),
-        dict(id=22, debit_account_id=3, credit_account_id=4, amount=1, ledger=3, code=1),
-        dict(id=23, debit_account_id=3, credit_account_id=4, amount=1, ledger=3, code=1)])
-    assert _plan(r, T, chain, [4], [50], kn)[0] == [(0, 1, False, [0]), (1, 3, True, [0, 1]),
-                                                    (3, 4, False, [1])]
-    # the same events with a batch end between them: two chains (the first one left open)
-    assert _plan(r, T, chain, [2, 2], [49, 50], kn)[0] == [(0, 4, False, [0, 0, 1, 1])]
-    # an id repeated on another shard's accounts: the repeat waits for the first one's outcome
-    rep = _transfers([dict(id=30, debit_account_id=1, credit_account_id=2, amount=1, ledger=1, code=1),
-                      dict(id=30, debit_account_id=3, credit_account_id=4, amount=1, ledger=3,
-                           code=1)])
-    assert _plan(r, T, rep, [2], [60], kn)[0] == [(0, 1, False, [0]), (1, 2, False, [1])]
-    # ... but within one chain it runs where the first one did (the chain reaches it only if the
-    # first occurrence created the id: create_transfer_exists decides it there)
-    rep["flags"][0] = 1
-    assert _plan(r, T, rep, [2], [60], kn)[0] == [(0, 2, False, [0, 0])]
-    # imported events that may regress past another shard's: a new segment
-    imp = _transfers([dict(id=40, debit_account_id=1, credit_account_id=2, amount=1, ledger=1,
-                           code=1, flags=256, timestamp=55),
-                      dict(id=41, debit_account_id=3, credit_account_id=4, amount=1, ledger=3,
-                           code=1, flags=256, timestamp=56)])
-    assert len(_plan(r, T, imp, [2], [70], kn)[0]) == 1
-    imp["timestamp"] = [56, 55]
-    assert len(_plan(r, T, imp, [2], [70], kn)[0]) == 2
-    # an imported timestamp of an account on another shard: a timestamp surrogate
-    imp["timestamp"] = [55, 56]
-    c = shard._Call(T, imp, [2], [70])
-    seg = shard.Planner(r, c, kn, {56: {0}}).plan(0)
-    assert seg.tprime == {1: 1}
-    # a mismatched imported flag: the router's status (execute_create :3052-3064)
-    imp["flags"][1] = 0
-    c = shard._Call(T, imp, [2], [70])
-    assert c.pre == {1: int(shard._CT.imported_event_expected)}
+    shards = [OracleShard() for _ in range(2)]
+    try:
+        g = oracle_group(shards)  # ledgers 1, 2 -> shard 0; 3, 4 -> shard 1
+        g.record_accounts([1, 2, 3, 4], [0, 0, 1, 1])
+        ok = _transfers([dict(id=10, debit_account_id=1, credit_account_id=2, amount=1, ledger=1,
+                              code=1),
+                         dict(id=11, debit_account_id=3, credit_account_id=4, amount=1, ledger=3,
+                              code=1),
+                         dict(id=12, debit_account_id=99, credit_account_id=4, amount=1,
+                              ledger=3, code=1)])  # missing debit account: the credit's shard
+        assert g.plan(True, ok, [3], [20]) == [(0, 3, False, [0, 1, 1])]
+        # an existing id goes to its holder, whatever accounts it names
+        g.record_transfers([11], [1])
+        again = _transfers([dict(id=11, debit_account_id=1, credit_account_id=2, amount=1,
+                                 ledger=1, code=1)])
+        assert g.plan(True, again, [1], [30]) == [(0, 1, False, [1])]
+        # a linked chain across shards: a segment of its own, between the segments around it
+        chain = _transfers([
+            dict(id=20, debit_account_id=1, credit_account_id=2, amount=1, ledger=1, code=1),
+            dict(id=21, debit_account_id=1, credit_account_id=2, amount=1, ledger=1, code=1,
+                 flags=1),
+            dict(id=22, debit_account_id=3, credit_account_id=4, amount=1, ledger=3, code=1),
+            dict(id=23, debit_account_id=3, credit_account_id=4, amount=1, ledger=3, code=1)])
+        assert g.plan(True, chain, [4], [50]) == [(0, 1, False, [0]), (1, 3, True, [0, 1]),
+                                                  (3, 4, False, [1])]
+        # the same events with a batch end between them: two chains (the first one left open)
+        assert g.plan(True, chain, [2, 2], [49, 50]) == [(0, 4, False, [0, 0, 1, 1])]
+        # an id repeated on another shard's accounts: the repeat waits for the first one's outcome
+        rep = _transfers([dict(id=30, debit_account_id=1, credit_account_id=2, amount=1, ledger=1,
+                               code=1),
+                          dict(id=30, debit_account_id=3, credit_account_id=4, amount=1, ledger=3,
+                               code=1)])
+        assert g.plan(True, rep, [2], [60]) == [(0, 1, False, [0]), (1, 2, False, [1])]
+        # ... but within one chain it runs where the first one did (the chain reaches it only if
+        # the first occurrence created the id: create_transfer_exists decides it there)
+        rep["flags"][0] = 1
+        assert g.plan(True, rep, [2], [60]) == [(0, 2, False, [0, 0])]
+        # imported events that may regress past another shard's: a new segment
+        imp = _transfers([dict(id=40, debit_account_id=1, credit_account_id=2, amount=1, ledger=1,
+                               code=1, flags=256, timestamp=55),
+                          dict(id=41, debit_account_id=3, credit_account_id=4, amount=1, ledger=3,
+                               code=1, flags=256, timestamp=56)])
+        assert len(g.plan(True, imp, [2], [70])) == 1
+        imp["timestamp"] = [56, 55]
+        assert len(g.plan(True, imp, [2], [70])) == 2
+        g.close()
+    finally:
+        for s in shards:
+            s.close()
 
 
-def test_pnt_resets_fire():
-    """The reset-if-equal of a post/void (:4227-4229) fires against the value over all shards in
-    call order: a `min` recorded by another shard before it can prevent it."""
-    R = shard.PNT_RESET
-    assert shard.pnt_resets_fire([100, 50], [[], [(10, 50 | R)]])
-    assert not shard.pnt_resets_fire([100, 60], [[(5, 40)], [(10, 60 | R)]])
-    assert not shard.pnt_resets_fire([100, 60], [[(15, 40)], [(10, 50 | R)]])
-    assert shard.pnt_resets_fire([100, 100], [[(5, 40)], [(10, 40 | R)]])
+def test_surrogates_and_batch_statuses():
+    """Transfers between two shards' accounts get the reference's status (the surrogate's
+    accounts_must_be_different patched), and an imported-flag mismatch the batch's status
+    (execute_create :3052-3064) -- against the unsharded oracle."""
+    shards = [OracleShard() for _ in range(2)]
+    ref = OracleShard()
+    try:
+        g = oracle_group(shards)
+        acc = _accounts([1, 2, 3, 4], [1, 1, 3, 3])
+        for c in (g, ref):
+            c.create_accounts(acc, [4], [10])
+        cross = _transfers([dict(id=13, debit_account_id=1, credit_account_id=3, amount=1,
+                                 ledger=1, code=1),
+                            dict(id=14, debit_account_id=1, credit_account_id=3, amount=1,
+                                 ledger=0, code=1),
+                            dict(id=15, debit_account_id=1, credit_account_id=3, amount=1,
+                                 ledger=1, code=1, flags=256, timestamp=5),
+                            dict(id=16, debit_account_id=1, credit_account_id=2, amount=1,
+                                 ledger=1, code=1)])
+        got = g.create_transfers(cross, [4], [40])
+        want = ref.create_transfers(cross, [4], [40])
+        assert got.tobytes() == want.tobytes()
+        assert got["status"].tolist() == [23, 19, 57, CREATED]
+        g.close()
+    finally:
+        for s in shards + [ref]:
+            s.close()
 
 
 @pytest.mark.parametrize("seed", [0, 1, 2])
@@ -593,35 +606,31 @@ def test_local_shards_match_unsharded(seed):
     shards = [OracleShard() for _ in range(3)]
     ref = OracleShard()
     try:
-        cluster = shard.LocalShards(shard.LedgerRouter(3, ledgers=LEDGERS), shards, PBM)
-        assert drive(cluster, ref, scenario(seed)) > 0
+        g = oracle_group(shards)
+        assert drive(g, ref, scenario(seed)) > 0
         dumps = [s.dump() for s in shards]
         assert all(len(d[1]) for d in dumps), "every shard holds transfers"
         assert_same_state(dumps, ref, [s.dump_account_events() for s in shards])
+        g.close()
     finally:
         for s in shards + [ref]:
             s.close()
 
 
-def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
-@pytest.mark.parametrize("seed", list(range(6)))
+@pytest.mark.parametrize("seed", list(range(8)))
 def test_local_shards_cross_shard_calls(seed):
-    """cross_scenario through three shards: every call the router once refused, executed
+    """cross_scenario through three shards: every call no shard could execute alone, executed
     exactly -- results call by call, pulse_next_timestamp, pulses and the final tables and
     AccountEvents against the unsharded oracle."""
     shards = [OracleShard() for _ in range(3)]
     ref = OracleShard()
     try:
-        cluster = shard.LocalShards(shard.LedgerRouter(3, ledgers=LEDGERS), shards, PBM)
-        drive(cluster, ref, cross_scenario(seed))
-        assert cluster.engine.chain_segments > 0
+        g = oracle_group(shards)
+        drive(g, ref, cross_scenario(seed))
+        assert g.stats()["chain_segments"] > 0
         assert_same_state([s.dump() for s in shards], ref,
                           [s.dump_account_events() for s in shards])
+        g.close()
     finally:
         for s in shards + [ref]:
             s.close()
@@ -636,100 +645,57 @@ def test_local_shards_pulse_cut(seed):
     shards = [OracleShard(pbm) for _ in range(3)]
     ref = OracleShard(pbm)
     try:
-        cluster = shard.LocalShards(shard.LedgerRouter(3, ledgers=LEDGERS), shards, pbm)
+        g = oracle_group(shards, pbm)
         cuts = []
-        assert drive(cluster, ref, scenario(seed, calls=10), pbm=pbm, cuts=cuts) > 0
+        assert drive(g, ref, scenario(seed, calls=10), pbm=pbm, cuts=cuts) > 0
         assert cuts, "the scenario should expire more than pulse_batch_max at once"
         assert_same_state([s.dump() for s in shards], ref,
                           [s.dump_account_events() for s in shards])
+        g.close()
     finally:
         for s in shards + [ref]:
             s.close()
 
 
-def _gloo_rank(rank, world, port, seed, q, pbm=PBM, cross=False):
+def test_group_lookups_and_errors():
+    """Lookups across shards in request order (found objects only); an invalid call fails without
+    touching the shards, and the group stays usable."""
+    shards = [OracleShard() for _ in range(2)]
+    ref = OracleShard()
     try:
-        os.environ["MASTER_ADDR"] = "127.0.0.1"
-        os.environ["MASTER_PORT"] = str(port)
-        import torch.distributed as dist
-        dist.init_process_group("gloo", rank=rank, world_size=world)
-        ex = OracleShard(pbm)
-        router = shard.LedgerRouter(world, ledgers=LEDGERS) if rank == 0 else None
-        group = shard.ShardGroup(ex, router, device="cpu", pulse_batch_max=pbm)
-        ref = OracleShard(pbm) if rank == 0 else None
-        cuts = []
-        ops = cross_scenario(seed, calls=8) if cross else \
-            scenario(seed, calls=10 if pbm < PBM else 8)
-        pulses = drive(group, ref, ops, rank0=rank == 0, pbm=pbm, cuts=cuts)
-        if rank == 0 and pbm < PBM:
-            assert cuts, "the scenario should expire more than pulse_batch_max at once"
-        if rank == 0 and cross:
-            assert group.engine.chain_segments > 0
-        dumps = [None] * world
-        dist.all_gather_object(dumps, ex.dump())
-        events = [None] * world
-        dist.all_gather_object(events, ex.dump_account_events())
-        if rank == 0:
-            assert all(len(d[1]) for d in dumps), "every shard holds transfers"
-            assert_same_state(dumps, ref, events)
-        # A call that fails on rank 0 (an invalid batch layout) fails on every rank and leaves
-        # the group usable.
-        try:
-            if rank == 0:
-                group.create_transfers(np.zeros(2, dtype=TRANSFER_DTYPE), [3],
-                                       np.array([10**15], dtype=np.uint64))
-            else:
-                group.create_transfers()
-            raise AssertionError("the invalid call did not fail")
-        except (ValueError, RuntimeError):
-            pass
-        assert group.pulse_next_timestamp() > 0
-        dist.barrier()
-        dist.destroy_process_group()
-        q.put((rank, None, pulses))
-    except BaseException:  # noqa: BLE001 -- reported to the parent
-        q.put((rank, traceback.format_exc(), 0))
-
-
-@pytest.mark.parametrize("pbm,cross", [(PBM, False), (6, False), (PBM, True)],
-                         ids=["pbm8190", "pbm6-cuts", "cross-shard"])
-def test_shard_group_gloo_world2(pbm, cross):
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_gloo_rank, args=(r, 2, port, 5, q, pbm, cross))
-             for r in range(2)]
-    for p in procs:
-        p.start()
-    out = {}
-    try:
-        for _ in range(2):
-            rank, err, pulses = q.get(timeout=240)
-            out[rank] = (err, pulses)
+        g = oracle_group(shards)
+        drive(g, ref, scenario(9, calls=2))
+        ids = [5, 9999, 1, 3, 1]
+        got = g.lookup_accounts(ids)
+        want = ref.lookup_accounts(ids)
+        assert [int(r["id"][0]) for r in got] == [5, 1, 3, 1]
+        assert all(got[i].tobytes() == want[int(got[i]["id"][0])].tobytes()
+                   for i in range(len(got)))
+        tids = [1001, 1002, 77, 1003]
+        got = g.lookup_transfers(tids)
+        want = ref.lookup_transfers(tids)
+        assert [int(r["id"][0]) for r in got] == sorted(want, key=tids.index)
+        with pytest.raises(ValueError):
+            g.create_transfers(np.zeros(2, dtype=TRANSFER_DTYPE), [3], [10**15])
+        assert g.pulse_next_timestamp() == ref.pulse_next_timestamp()
+        g.close()
     finally:
-        for p in procs:
-            p.join(timeout=30)
-            if p.is_alive():
-                p.kill()
-    for rank, (err, _) in sorted(out.items()):
-        assert err is None, f"rank {rank}:\n{err}"
-    assert out[0][1] > 0 or cross
+        for s in shards + [ref]:
+            s.close()
 
 
 @pytest.mark.gpu
 def test_local_shards_gpu():
-    """Two HBM executors on cuda:0 behind the router, against the unsharded oracle."""
-    shards = [shard.GpuShard(1 << 10, 1 << 14, batch_events_max=4096,
-                             account_events_capacity=1 << 15) for _ in range(2)]
+    """Two HBM executors on cuda:0 behind the group, against the unsharded oracle."""
+    g, views = gpu_group(2, account_capacity=1 << 10, transfer_capacity=1 << 14)
     ref = OracleShard()
     try:
-        cluster = shard.LocalShards(shard.LedgerRouter(2, ledgers=LEDGERS), shards, PBM)
-        assert drive(cluster, ref, scenario(11)) > 0
-        assert_same_state([s.dump() for s in shards], ref,
-                          [s.dump_account_events() for s in shards])
+        assert drive(g, ref, scenario(11)) > 0
+        assert_same_state([v.dump() for v in views], ref,
+                          [v.dump_account_events() for v in views])
+        assert g.stats()["device_calls"] > 0
     finally:
-        for s in shards:
-            s.close()
+        g.close()
         ref.close()
 
 
@@ -738,40 +704,35 @@ def test_local_shards_gpu_pulse_cut():
     """Two HBM executors with pulse_batch_max 6: the global pulse cut through tbg_pulse_candidates
     / tbg_pulse_cut, against the unsharded oracle."""
     pbm = 6
-    shards = [shard.GpuShard(1 << 10, 1 << 14, batch_events_max=4096, pulse_batch_max=pbm,
-                             account_events_capacity=1 << 15) for _ in range(2)]
+    g, views = gpu_group(2, pbm=pbm, account_capacity=1 << 10, transfer_capacity=1 << 14)
     ref = OracleShard(pbm)
     try:
-        cluster = shard.LocalShards(shard.LedgerRouter(2, ledgers=LEDGERS), shards, pbm)
         cuts = []
-        assert drive(cluster, ref, scenario(12, calls=10), pbm=pbm, cuts=cuts) > 0
+        assert drive(g, ref, scenario(12, calls=10), pbm=pbm, cuts=cuts) > 0
         assert cuts
-        assert_same_state([s.dump() for s in shards], ref,
-                          [s.dump_account_events() for s in shards])
+        assert_same_state([v.dump() for v in views], ref,
+                          [v.dump_account_events() for v in views])
     finally:
-        for s in shards:
-            s.close()
+        g.close()
         ref.close()
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed", [0, 1, 2])
 def test_local_shards_gpu_cross_shard(seed):
-    """cross_scenario through three HBM executors on cuda:0 (stamped calls, TBG_ONE_CHAIN probes
-    and commits, tbg_forget_orphans, tbg_timestamps_exist, tbg_key_max), against the unsharded
-    oracle."""
-    shards = [shard.GpuShard(1 << 12, 1 << 16, batch_events_max=4096,
-                             account_events_capacity=1 << 16) for _ in range(3)]
+    """cross_scenario through three HBM executors on cuda:0 (the device path where it places a
+    call, else the exact engine: stamped calls, TBG_ONE_CHAIN probes and commits,
+    tbg_forget_orphans, tbg_timestamps_exist, tbg_key_max), against the unsharded oracle."""
+    g, views = gpu_group(3)
     ref = OracleShard()
     try:
-        cluster = shard.LocalShards(shard.LedgerRouter(3, ledgers=LEDGERS), shards, PBM)
-        drive(cluster, ref, cross_scenario(seed))
-        assert cluster.engine.chain_segments > 0
-        assert_same_state([s.dump() for s in shards], ref,
-                          [s.dump_account_events() for s in shards])
+        drive(g, ref, cross_scenario(seed))
+        st = g.stats()
+        assert st["chain_segments"] > 0, st
+        assert_same_state([v.dump() for v in views], ref,
+                          [v.dump_account_events() for v in views])
     finally:
-        for s in shards:
-            s.close()
+        g.close()
         ref.close()
 
 
@@ -822,33 +783,30 @@ def test_local_shards_gpu_window_calls(amounts):
     window and pnt_resolve (sharded calls record every pulse_next_timestamp update); results,
     tables and AccountEvents against the unsharded oracle (pnt_resolve's scratch must
     not be the balance items the AccountEvents window reads). `wide`: amounts below 2^63."""
-    shards = [shard.GpuShard(1 << 12, 1 << 19, batch_events_max=1 << 18,
-                             account_events_capacity=1 << 20) for _ in range(2)]
+    g, views = gpu_group(2, transfer_capacity=1 << 19, batch_events_max=1 << 18,
+                         account_events_capacity=1 << 20)
     ref = OracleShard()
     try:
-        cluster = shard.LocalShards(shard.LedgerRouter(2, ledgers=LEDGERS), shards, PBM)
-        drive(cluster, ref, window_scenario(3, wide=amounts == "wide"))
-        assert_same_state([s.dump() for s in shards], ref,
-                          [s.dump_account_events() for s in shards])
+        drive(g, ref, window_scenario(3, wide=amounts == "wide"))
+        assert_same_state([v.dump() for v in views], ref,
+                          [v.dump_account_events() for v in views])
     finally:
-        for s in shards:
-            s.close()
+        g.close()
         ref.close()
 
 
 def test_local_shards_batch_cap():
     """A shard's runs of a call whose ledgers interleave event by event become many short batches:
-    the engine splits them over sub-calls of at most max_batches batches (the executors'
-    batch_count_max), results and state unchanged."""
+    the engine splits them over sub-calls of at most batch_count_max batches, results and state
+    unchanged."""
     shards = [OracleShard() for _ in range(2)]
     ref = OracleShard()
     try:
-        cluster = shard.LocalShards(shard.LedgerRouter(2, ledgers=LEDGERS), shards, PBM)
-        cluster.engine.max_batches = 64
-        drive(cluster, ref, window_scenario(4, n=20_000, n_acc=200))
+        g = oracle_group(shards, batch_count_max=64, events_max=1 << 16)
+        drive(g, ref, window_scenario(4, n=20_000, n_acc=200))
         assert_same_state([s.dump() for s in shards], ref,
                           [s.dump_account_events() for s in shards])
+        g.close()
     finally:
-        for s in shards:
+        for s in shards + [ref]:
             s.close()
-        ref.close()

@@ -101,6 +101,24 @@ struct FlowScratch {
 
 }  // namespace
 
+// Makes a ctx's device current for the length of an entry point (a process may drive executors on
+// several GPUs from one thread, tbg_group.h) and restores the caller's.
+struct DeviceScope {
+    int prev = -1;
+    explicit DeviceScope(int device) {
+        if (device < 0 || hipGetDevice(&prev) != hipSuccess) {
+            prev = -1;
+            return;
+        }
+        if (prev != device) (void)hipSetDevice(device);
+        else prev = -1;
+    }
+    ~DeviceScope() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+#define TBG_DEVICE_SCOPE(ctx) DeviceScope tbg_device_scope_((ctx) ? int((ctx)->opt.device) : -1)
+
 struct tbg_ctx {
     tbg_options opt{};
     hipStream_t stream = nullptr;
@@ -2094,6 +2112,7 @@ tbg_ctx* tbg_open(const tbg_options* options) {
 }
 
 void tbg_close(tbg_ctx* ctx) {
+    TBG_DEVICE_SCOPE(ctx);
     if (!ctx) return;
     if (ctx->ae_stream) (void)hipStreamSynchronize(ctx->ae_stream);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
@@ -2151,7 +2170,8 @@ void tbg_close(tbg_ctx* ctx) {
     delete ctx;
 }
 
-const char* tbg_last_error(const tbg_ctx* ctx) { return ctx ? ctx->error.c_str() : "null ctx"; }
+const char* tbg_last_error(const tbg_ctx* ctx) {
+    TBG_DEVICE_SCOPE(ctx); return ctx ? ctx->error.c_str() : "null ctx"; }
 
 }  // extern "C"
 
@@ -2446,6 +2466,7 @@ extern "C" {
 int tbg_create_transfers_device(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t n,
                                 const uint32_t* d_batch_ends, const uint64_t* d_batch_ts,
                                 uint32_t n_batches, tb_create_result_t* d_results, void* stream) {
+    TBG_DEVICE_SCOPE(ctx);
     return create_transfers_impl(ctx, d_events, n, d_batch_ends, d_batch_ts, n_batches, d_results,
                                  stream, nullptr);
 }
@@ -2453,6 +2474,7 @@ int tbg_create_transfers_device(tbg_ctx* ctx, const tb_transfer_t* d_events, uin
 int tbg_create_transfers_stamped_device(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t n,
                                         const uint64_t* d_event_timestamps,
                                         tb_create_result_t* d_results, void* stream) {
+    TBG_DEVICE_SCOPE(ctx);
     if (!ctx || n > ctx->opt.batch_events_max || !d_event_timestamps) return TBG_EINVAL;
     if (n == 0) return 0;
     // One batch: its end, and its timestamp = the last event's (imported events' must_not_advance
@@ -2551,6 +2573,7 @@ extern "C" {
 int tbg_create_accounts_device(tbg_ctx* ctx, const tb_account_t* d_events, uint32_t n,
                                const uint32_t* d_batch_ends, const uint64_t* d_batch_ts,
                                uint32_t n_batches, tb_create_result_t* d_results, void* stream) {
+    TBG_DEVICE_SCOPE(ctx);
     return create_accounts_impl(ctx, d_events, n, d_batch_ends, d_batch_ts, n_batches, d_results,
                                 stream, nullptr);
 }
@@ -2558,6 +2581,7 @@ int tbg_create_accounts_device(tbg_ctx* ctx, const tb_account_t* d_events, uint3
 int tbg_create_transfers_stamped(tbg_ctx* ctx, const tb_transfer_t* events, uint32_t n,
                                  const uint64_t* event_timestamps, uint64_t batch_timestamp,
                                  uint32_t options, tb_create_result_t* results) {
+    TBG_DEVICE_SCOPE(ctx);
     if (!ctx || n > ctx->opt.batch_events_max || (options & ~TBG_ONE_CHAIN)) return TBG_EINVAL;
     if (n == 0) return 0;
     FAILED_GUARD(ctx);
@@ -2577,6 +2601,7 @@ int tbg_create_transfers_stamped(tbg_ctx* ctx, const tb_transfer_t* events, uint
 int tbg_create_accounts_stamped(tbg_ctx* ctx, const tb_account_t* events, uint32_t n,
                                 const uint64_t* event_timestamps, uint64_t batch_timestamp,
                                 uint32_t options, tb_create_result_t* results) {
+    TBG_DEVICE_SCOPE(ctx);
     if (!ctx || n > ctx->opt.batch_events_max || (options & ~TBG_ONE_CHAIN)) return TBG_EINVAL;
     if (n == 0) return 0;
     FAILED_GUARD(ctx);
@@ -2596,6 +2621,7 @@ int tbg_create_accounts_stamped(tbg_ctx* ctx, const tb_account_t* events, uint32
 int tbg_create_transfers(tbg_ctx* ctx, const tb_transfer_t* events, uint32_t n,
                          const uint32_t* batch_lens, const uint64_t* batch_ts, uint32_t nb,
                          tb_create_result_t* results) {
+    TBG_DEVICE_SCOPE(ctx);
     if (!ctx || n > ctx->opt.batch_events_max) return TBG_EINVAL;
     if (n == 0) return 0;
     const double t0 = ctx->timing_host ? now_ms() : 0;
@@ -2640,6 +2666,7 @@ int tbg_create_transfers(tbg_ctx* ctx, const tb_transfer_t* events, uint32_t n,
 int tbg_create_accounts(tbg_ctx* ctx, const tb_account_t* events, uint32_t n,
                         const uint32_t* batch_lens, const uint64_t* batch_ts, uint32_t nb,
                         tb_create_result_t* results) {
+    TBG_DEVICE_SCOPE(ctx);
     if (!ctx || n > ctx->opt.batch_events_max) return TBG_EINVAL;
     if (n == 0) return 0;
     int rc = body_buffer(ctx);
@@ -2789,6 +2816,7 @@ extern "C" {
 
 
 int tbg_register_host(tbg_ctx* ctx, void* ptr, uint64_t size) {
+    TBG_DEVICE_SCOPE(ctx);
     if (!ctx || !ptr || size == 0) return TBG_EINVAL;
     if (is_registered(ctx, ptr, size)) return 0;
     // Several ctxs of one process (shards, state machines) may register the same message pool:
@@ -2800,6 +2828,7 @@ int tbg_register_host(tbg_ctx* ctx, void* ptr, uint64_t size) {
 }
 
 int tbg_unregister_host(tbg_ctx* ctx, void* ptr) {
+    TBG_DEVICE_SCOPE(ctx);
     if (!ctx) return TBG_EINVAL;
     for (size_t i = 0; i < ctx->registered.size(); i++) {
         if (ctx->registered[i].host != reinterpret_cast<uintptr_t>(ptr)) continue;
@@ -2813,6 +2842,7 @@ int tbg_unregister_host(tbg_ctx* ctx, void* ptr) {
 }
 
 int tbg_synchronize(tbg_ctx* ctx) {
+    TBG_DEVICE_SCOPE(ctx);
     if (!ctx) return TBG_EINVAL;
     // (the side stream's AccountEvents appends too: the call's stream waits for them first)
     if (int rc = ae_join(ctx)) return rc;
@@ -2821,6 +2851,7 @@ int tbg_synchronize(tbg_ctx* ctx) {
 }
 
 int64_t tbg_pulse(tbg_ctx* ctx, uint64_t timestamp) {
+    TBG_DEVICE_SCOPE(ctx);
     if (!ctx) return TBG_EINVAL;
     FAILED_GUARD(ctx);
     const uint32_t k = uint32_t(ctx->opt.pulse_batch_max);
@@ -2913,6 +2944,7 @@ int64_t tbg_pulse(tbg_ctx* ctx, uint64_t timestamp) {
 
 int64_t tbg_pulse_candidates(tbg_ctx* ctx, uint64_t timestamp, uint64_t* expires_at,
                              uint64_t* timestamps, uint32_t max) {
+    TBG_DEVICE_SCOPE(ctx);
     if (!ctx) return TBG_EINVAL;
     PulseGather G;
     int rc = pulse_select(ctx, timestamp, std::min<uint32_t>(max, kPulseRun), &G);
@@ -2930,6 +2962,7 @@ int64_t tbg_pulse_candidates(tbg_ctx* ctx, uint64_t timestamp, uint64_t* expires
 int64_t tbg_pulse_cut(tbg_ctx* ctx, uint64_t timestamp, uint64_t cut_expires_at,
                       uint64_t cut_timestamp, uint64_t pulse_next_timestamp,
                       const uint64_t* event_timestamps) {
+    TBG_DEVICE_SCOPE(ctx);
     if (!ctx) return TBG_EINVAL;
     PulseGather G;
     int rc = pulse_select(ctx, timestamp, uint32_t(ctx->opt.pulse_batch_max), &G);
@@ -2962,6 +2995,7 @@ int64_t tbg_pulse_cut(tbg_ctx* ctx, uint64_t timestamp, uint64_t cut_expires_at,
 }
 
 int tbg_raise_key_max(tbg_ctx* ctx, uint64_t accounts_key_max, uint64_t transfers_key_max) {
+    TBG_DEVICE_SCOPE(ctx);
     if (!ctx) return TBG_EINVAL;
     int rc = sync_scalars(ctx);
     if (rc) return rc;
@@ -2978,6 +3012,7 @@ int tbg_raise_key_max(tbg_ctx* ctx, uint64_t accounts_key_max, uint64_t transfer
 }
 
 int64_t tbg_forget_orphans(tbg_ctx* ctx, const tb_uint128_t* ids, uint32_t n) {
+    TBG_DEVICE_SCOPE(ctx);
     if (!ctx || n > ctx->opt.batch_events_max || (n && !ids)) return TBG_EINVAL;
     FAILED_GUARD(ctx);
     if (n == 0) return 0;
@@ -2996,6 +3031,7 @@ int64_t tbg_forget_orphans(tbg_ctx* ctx, const tb_uint128_t* ids, uint32_t n) {
 
 int64_t tbg_timestamps_exist(tbg_ctx* ctx, int transfers, const uint64_t* timestamps, uint32_t n,
                              uint8_t* out) {
+    TBG_DEVICE_SCOPE(ctx);
     if (!ctx || n > ctx->opt.batch_events_max || (n && (!timestamps || !out))) return TBG_EINVAL;
     FAILED_GUARD(ctx);
     if (n == 0) return 0;
@@ -3019,6 +3055,7 @@ int64_t tbg_timestamps_exist(tbg_ctx* ctx, int transfers, const uint64_t* timest
 }
 
 int tbg_key_max(tbg_ctx* ctx, uint64_t* accounts_key_max, uint64_t* transfers_key_max) {
+    TBG_DEVICE_SCOPE(ctx);
     if (!ctx) return TBG_EINVAL;
     FAILED_GUARD(ctx);
     int rc = sync_scalars(ctx);
@@ -3029,11 +3066,13 @@ int tbg_key_max(tbg_ctx* ctx, uint64_t* accounts_key_max, uint64_t* transfers_ke
 }
 
 uint64_t tbg_pulse_next_timestamp(tbg_ctx* ctx) {
+    TBG_DEVICE_SCOPE(ctx);
     if (!ctx || sync_scalars(ctx)) return 0;
     return ctx->h_scalars->pulse_next_timestamp;
 }
 
 int tbg_set_pnt_sharded(tbg_ctx* ctx, int on) {
+    TBG_DEVICE_SCOPE(ctx);
     if (!ctx) return TBG_EINVAL;
     ctx->pnt_sharded = on != 0;
     ctx->pnt_last_valid = false;
@@ -3042,6 +3081,7 @@ int tbg_set_pnt_sharded(tbg_ctx* ctx, int on) {
 
 int64_t tbg_pnt_ops(tbg_ctx* ctx, uint64_t* timestamps, uint64_t* ops, uint64_t max,
                     uint64_t* start) {
+    TBG_DEVICE_SCOPE(ctx);
     if (!ctx) return TBG_EINVAL;
     FAILED_GUARD(ctx);
     if (!ctx->pnt_last_valid) {  // (no sharded call since: nothing recorded)
@@ -3075,6 +3115,7 @@ int64_t tbg_pnt_ops(tbg_ctx* ctx, uint64_t* timestamps, uint64_t* ops, uint64_t 
 }
 
 int tbg_set_pulse_next_timestamp(tbg_ctx* ctx, uint64_t value) {
+    TBG_DEVICE_SCOPE(ctx);
     if (!ctx) return TBG_EINVAL;
     FAILED_GUARD(ctx);
     const unsigned long long v = value;
@@ -3085,20 +3126,24 @@ int tbg_set_pulse_next_timestamp(tbg_ctx* ctx, uint64_t value) {
 }
 
 int64_t tbg_lookup_accounts(tbg_ctx* ctx, const tb_uint128_t* ids, uint32_t n, tb_account_t* out) {
+    TBG_DEVICE_SCOPE(ctx);
     return lookup_impl(ctx, ids, n, out, true);
 }
 
 int64_t tbg_lookup_transfers(tbg_ctx* ctx, const tb_uint128_t* ids, uint32_t n,
                              tb_transfer_t* out) {
+    TBG_DEVICE_SCOPE(ctx);
     return lookup_impl(ctx, ids, n, out, false);
 }
 
 int64_t tbg_dump_accounts(tbg_ctx* ctx, tb_account_t* out) {
+    TBG_DEVICE_SCOPE(ctx);
     if (!ctx) return TBG_EINVAL;
     return dump_impl(ctx, ctx->T.acc_rows, ctx->T.acc_live, ctx->T.acc_rows_used, out, nullptr);
 }
 
 int64_t tbg_dump_transfers(tbg_ctx* ctx, tb_transfer_t* out, uint8_t* pending_status) {
+    TBG_DEVICE_SCOPE(ctx);
     if (!ctx) return TBG_EINVAL;
     return dump_impl(ctx, ctx->T.tr_rows, ctx->T.tr_live, ctx->T.tr_rows_used, out,
                      pending_status);
@@ -3107,6 +3152,7 @@ int64_t tbg_dump_transfers(tbg_ctx* ctx, tb_transfer_t* out, uint8_t* pending_st
 int tbg_debug_set_account_balances(tbg_ctx* ctx, tb_uint128_t id, tb_uint128_t debits_pending,
                                    tb_uint128_t debits_posted, tb_uint128_t credits_pending,
                                    tb_uint128_t credits_posted) {
+    TBG_DEVICE_SCOPE(ctx);
     if (!ctx) return TBG_EINVAL;
     if (int rc = ae_flush_all(ctx)) return rc;  // (a deferred snapshot reads the rows)
     int* d_rc = reinterpret_cast<int*>(&ctx->d_scalars->slow_count);
@@ -3120,6 +3166,7 @@ int tbg_debug_set_account_balances(tbg_ctx* ctx, tb_uint128_t id, tb_uint128_t d
 }
 
 int64_t tbg_dump_account_events(tbg_ctx* ctx, tb_account_event_t* out) {
+    TBG_DEVICE_SCOPE(ctx);
     if (!ctx) return TBG_EINVAL;
     if (int rc = ae_settle(ctx)) return rc;
     if (!out || ctx->ae_used == 0) return int64_t(ctx->ae_used);
@@ -3133,6 +3180,7 @@ int64_t tbg_dump_account_events(tbg_ctx* ctx, tb_account_event_t* out) {
 
 int64_t tbg_get_change_events(tbg_ctx* ctx, const tb_change_events_filter_t* filter,
                               uint32_t limit_max, tb_change_event_t* out) {
+    TBG_DEVICE_SCOPE(ctx);
     if (!ctx || !filter) return TBG_EINVAL;
     // get_scan_from_change_events_filter (:2396-2434): an invalid filter yields no results.
     bool reserved_zero = true;
@@ -3169,6 +3217,7 @@ int64_t tbg_get_change_events(tbg_ctx* ctx, const tb_change_events_filter_t* fil
 }
 
 int tbg_last_stats(tbg_ctx* ctx, tbg_stats* out) {
+    TBG_DEVICE_SCOPE(ctx);
     if (!ctx || !out) return TBG_EINVAL;
     *out = ctx->stats;
     return 0;
@@ -3196,6 +3245,7 @@ extern "C" {
 
 int tbg_sum_overflows(tbg_ctx* ctx, uint32_t bits, const tb_uint128_t* a, const tb_uint128_t* b,
                       uint32_t n, uint8_t* out) {
+    TBG_DEVICE_SCOPE(ctx);
     if ((bits != 64 && bits != 128) || (n && (!a || !b || !out))) return TBG_EINVAL;
     if (!ctx) {
         for (uint32_t i = 0; i < n; i++) out[i] = sum_overflows_bits(bits, a[i], b[i]);
@@ -3225,24 +3275,28 @@ int tbg_sum_overflows(tbg_ctx* ctx, uint32_t bits, const tb_uint128_t* a, const 
 }
 
 int tbg_debug_force_replay(tbg_ctx* ctx, int enable) {
+    TBG_DEVICE_SCOPE(ctx);
     if (!ctx) return TBG_EINVAL;
     ctx->force_replay = enable != 0;
     return 0;
 }
 
 int tbg_debug_serial_replay(tbg_ctx* ctx, int enable) {
+    TBG_DEVICE_SCOPE(ctx);
     if (!ctx) return TBG_EINVAL;
     ctx->serial_replay = enable != 0;
     return 0;
 }
 
 int tbg_debug_ae_sync(tbg_ctx* ctx, int enable) {
+    TBG_DEVICE_SCOPE(ctx);
     if (!ctx) return TBG_EINVAL;
     ctx->ae_async = enable == 0;
     return 0;
 }
 
 int tbg_profile(tbg_ctx* ctx, int enable) {
+    TBG_DEVICE_SCOPE(ctx);
     if (!ctx) return TBG_EINVAL;
     ctx->timing = enable == 1;
     ctx->timing_host = enable != 0;
@@ -3254,6 +3308,7 @@ int tbg_profile(tbg_ctx* ctx, int enable) {
 
 int tbg_profile_read(tbg_ctx* ctx, uint32_t index, char* name, uint32_t name_len,
                      double* total_ms, uint64_t* launches) {
+    TBG_DEVICE_SCOPE(ctx);
     if (!ctx) return 0;
     if (index == 0 && ctx->timing && ctx->n_marks > 1) {  // marks still pending (AccountEvents)
         (void)hipStreamSynchronize(ctx->stream);
@@ -3414,6 +3469,7 @@ std::vector<std::pair<void*, uint64_t>> ckpt_sections(tbg_ctx* ctx, uint64_t acc
 extern "C" {
 
 int64_t tbg_compact(tbg_ctx* ctx) {
+    TBG_DEVICE_SCOPE(ctx);
     if (ctx) ctx->expiry_known = false;  // (compaction renumbers and drops index entries)
     if (!ctx) return TBG_EINVAL;
     FAILED_GUARD(ctx);
@@ -3543,6 +3599,7 @@ int64_t tbg_compact(tbg_ctx* ctx) {
 }
 
 int tbg_checkpoint(tbg_ctx* ctx, const char* path) {
+    TBG_DEVICE_SCOPE(ctx);
     if (!ctx || !path) return TBG_EINVAL;
     FAILED_GUARD(ctx);  // (never persist undefined tables)
     if (int rc = ae_join(ctx)) return rc;
@@ -3759,6 +3816,7 @@ extern "C" {
 
 int64_t tbg_get_account_transfers(tbg_ctx* ctx, const tb_account_filter_t* filter,
                                   uint32_t limit_max, tb_transfer_t* out) {
+    TBG_DEVICE_SCOPE(ctx);
     if (!ctx || !filter) return TBG_EINVAL;
     if (!account_filter_valid(filter)) return 0;
     const int64_t count = scan_account_transfers(ctx, filter);
@@ -3770,6 +3828,7 @@ int64_t tbg_get_account_transfers(tbg_ctx* ctx, const tb_account_filter_t* filte
 
 int64_t tbg_get_account_balances(tbg_ctx* ctx, const tb_account_filter_t* filter,
                                  uint32_t limit_max, tb_account_balance_t* out) {
+    TBG_DEVICE_SCOPE(ctx);
     if (!ctx || !filter) return TBG_EINVAL;
     if (!ctx->ae_log) {
         ctx->error = "get_account_balances needs account_events_capacity > 0";
@@ -3814,6 +3873,7 @@ int64_t tbg_get_account_balances(tbg_ctx* ctx, const tb_account_filter_t* filter
 
 int64_t tbg_query_accounts(tbg_ctx* ctx, const tb_query_filter_t* filter, uint32_t limit_max,
                            tb_account_t* out) {
+    TBG_DEVICE_SCOPE(ctx);
     if (!ctx || !filter) return TBG_EINVAL;
     if (!query_filter_valid(filter)) return 0;
     ScanFilter f = scan_filter_common(filter);
@@ -3831,6 +3891,7 @@ int64_t tbg_query_accounts(tbg_ctx* ctx, const tb_query_filter_t* filter, uint32
 
 int64_t tbg_query_transfers(tbg_ctx* ctx, const tb_query_filter_t* filter, uint32_t limit_max,
                             tb_transfer_t* out) {
+    TBG_DEVICE_SCOPE(ctx);
     if (!ctx || !filter) return TBG_EINVAL;
     if (!query_filter_valid(filter)) return 0;
     ScanFilter f = scan_filter_common(filter);

@@ -1,16 +1,20 @@
-// The device-side ledger router (include/tbr.h): directories and the fast path of a routed call.
+// The device-side ledger router (include/tbr.h): directories and the device path of a routed call.
 //
 // Directories are the executor's id tables (device_common.hpp: tagged slots, group-16 homes) over
-// append-only stores: accounts (id, shard) in insertion order; transfers (id, shard | TBR_TIMED)
-// per routed event position -- every event of a routed call takes a store row, like the executor's
-// transfer rows, and its slot claim is released at settle unless the id now exists on its shard.
+// append-only stores: accounts (id, shard) in insertion order; transfers (id, shard) per routed
+// event position -- every event of a routed call takes a store row, like the executor's transfer
+// rows, and its slot claim is released at settle unless the id now exists on its shard.
 //
-// Fast path, per call of n events (one workgroup per 256 consecutive events, so the scatter is
-// stable): tbr_pass1 -- the hazard checks, the id claim, the shard pinned by the id's holder or
-// both accounts; tbr_pass_pv -- a post/void's shard from its pending transfer; tbr_pass_chains --
-// linked chains whole on one shard, per-block counts per shard; the host turns the counts into
-// per-block offsets (shard-major exclusive sums); tbr_pass2 -- each event copied to its slice with
-// its global commit timestamp and its position.
+// Device path, per call of n events (one workgroup per 256 consecutive events, so the scatter is
+// stable): tbr_pass1 -- the id claim and the shard the event's own fields pin (its id's holder,
+// its accounts', or any shard for an event whose status follows from itself alone; surrogates for
+// accounts on two shards); tbr_pass_pv -- a post/void's shard from its pending transfer;
+// tbr_pass_dup -- an id repeated in the call on its first occurrence's shard; tbr_pass_chains --
+// linked chains whole on one shard, events that may run anywhere placed; tbr_pass_count --
+// per-block counts per shard; the host turns them into per-block offsets (shard-major exclusive
+// sums); tbr_pass2 -- each event copied to its slice with its global commit timestamp and its
+// position; after the shards ran: tbr_settle / tbr_settle_release -- results to call order,
+// surrogate statuses patched, directory slots kept or released.
 
 #include <hip/hip_runtime.h>
 
@@ -47,9 +51,12 @@ struct RouteArgs {
     uint32_t nblocks;
     uint8_t* ev_shard;      // per event: its shard, 0xFF for a hazard
     uint32_t* ev_slot;      // per event: its claimed slot (kNone32: none)
+    uint8_t* ev_patch;      // per event: a surrogate's status (0: none)
+    uint8_t* ev_keep;       // per first occurrence: its id exists after the call
     uint32_t* block_counts; // [shard][block]
     unsigned int* flags;    // [0] hazard, [1] table full, [2] the call posts or voids,
-                            // [3] bit 0: an imported event, bit 1: a non-imported one
+                            // [3] bit 0: an imported event, bit 1: a non-imported one,
+                            // [4] events that may run anywhere, [5] surrogates, [6] repeats
     uint64_t imported_floor;  // imported timestamps at or below it are hazards (tbr.h)
 };
 
@@ -77,50 +84,76 @@ __global__ void tbr_lookup(Dir d, const tb_uint128_t* q, uint32_t n, int32_t* ou
     out[i] = r == kNone ? -1 : int32_t(d.shard[r]);
 }
 
-// ev_shard codes besides a shard: the event is a hazard (the call goes to the host router), or a
-// post/void whose shard follows its pending transfer (resolved by tbr_pass_pv).
+// ev_shard codes besides a shard: the event is a hazard (the call goes to the exact engine), a
+// post/void whose shard follows its pending transfer (resolved by tbr_pass_pv), or an event whose
+// status follows from itself alone and runs on any shard (resolved by tbr_pass_chains).
 constexpr uint8_t kShardHazard = 0xFF;
 constexpr uint8_t kShardPending = 0xFE;
+constexpr uint8_t kShardAny = 0xFD;
 
 __device__ inline void raise_hazard(const RouteArgs& a, bool hazard) {
     if (__any(hazard) && (threadIdx.x & 63) == 0) atomicOr(&a.flags[0], 1u);
 }
+__device__ inline void count_wave(unsigned int* counter, bool x) {
+    const uint64_t m = __ballot(x);
+    if (m && (threadIdx.x & 63) == 0) atomicAdd(counter, unsigned(__popcll(m)));
+}
 
-// Pass 1, per event: the static hazards, the id claim, and the shard the event's own fields pin:
-// the holder's for an id that already exists (create_transfer_exists runs before any account
-// lookup, :3733-3760, so the holder decides it), the accounts' for a single-phase or pending
-// event (both known, on one shard), none yet for a post/void (its pending transfer's, pass 2).
+// create_transfer's status for a transfer whose two accounts exist on two shards (so on two
+// ledgers): the first failing check after accounts_must_be_different (:3756-3798) -- none of them
+// reads state, the last is accounts_must_have_the_same_ledger. (engine.hpp cross_status.)
+__device__ inline uint8_t cross_status(const tb_transfer_t& t) {
+    if (!u128_is_zero(t.pending_id)) return TB_CT_PENDING_ID_MUST_BE_ZERO;
+    if (!(t.flags & TB_TRANSFER_PENDING)) {
+        if (t.timeout != 0) return TB_CT_TIMEOUT_RESERVED_FOR_PENDING_TRANSFER;
+        if (t.flags & (TB_TRANSFER_CLOSING_DEBIT | TB_TRANSFER_CLOSING_CREDIT))
+            return TB_CT_CLOSING_TRANSFER_MUST_BE_PENDING;
+    }
+    if (t.ledger == 0) return TB_CT_LEDGER_MUST_NOT_BE_ZERO;
+    if (t.code == 0) return TB_CT_CODE_MUST_NOT_BE_ZERO;
+    return TB_CT_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;
+}
+
+// Pass 1, per event: the shard its own fields pin.
+//  * A status that follows from the event alone (a nonzero padding, an id 0 / maxInt, a nonzero
+//    timestamp on a non-imported event: execute_create :3080, create_transfer :3729-3732) reads
+//    no state: any shard, no id claim.
+//  * Otherwise the id is claimed: an id that already exists goes to its holder
+//    (create_transfer_exists / id_already_failed run before any account lookup, :3733-3738); a
+//    post/void waits for its pending transfer (tbr_pass_pv); a transfer goes to its accounts'
+//    shard -- the known one's when the other is unknown (debit_account_not_found /
+//    credit_account_not_found there, :3774-3791), any shard when neither is known; accounts on
+//    two shards: any shard as a surrogate (credit := debit fails accounts_must_be_different, one
+//    check earlier and non-transient like the reference's status, which settle patches in).
+//  * Imported events (execute_create :3066-3078, must_not_regress :3808-3817) are routed only
+//    when the whole call is imported (flags[3]; each shard's slice is one batch), their timestamps
+//    increase through the call and lie above every object of both grooves (the floor) and below
+//    their own commit timestamps.
 __global__ void __launch_bounds__(kRouteBlock) tbr_pass1(RouteArgs a) {
     const uint32_t k = blockIdx.x * kRouteBlock + threadIdx.x;
-    bool hazard = false, pv_any = false;
+    bool hazard = false, pv_any = false, any = false;
     unsigned int kinds = 0;
     if (k < a.n) {
         const tb_transfer_t& t = a.events[k];
         const uint16_t f = t.flags;
         const bool post_void = (f & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) != 0;
         const bool imported = (f & TB_TRANSFER_IMPORTED) != 0;
-        uint8_t shard = kShardHazard;
+        uint8_t shard = kShardHazard, patch = 0;
         uint32_t slot = kNone32;
-        hazard = (f & TB_TRANSFER_PADDING_MASK) != 0 || (!imported && t.timestamp != 0) ||
-                 u128_is_zero(t.id) || u128_is_max(t.id);
-        // Imported events (execute_create :3066-3078, must_not_regress :3808-3817): routed when
-        // the whole call is imported (flags[3]; each shard's slice is one batch), their
-        // timestamps increase through the call (no event can regress past another shard's) and
-        // lie above every object of both grooves (the floor: no key range or timestamp of another
-        // shard can decide them) and below their own commit timestamps (must_not_advance holds
-        // on every shard as in the reference).
+        const bool static_fail = (f & TB_TRANSFER_PADDING_MASK) != 0 ||
+                                 (!imported && t.timestamp != 0) || u128_is_zero(t.id) ||
+                                 u128_is_max(t.id);
         if (imported) {
             const uint32_t b = batch_of_guess(a.batch_ends, a.n_batches, a.n, k);
             const uint64_t stamp = a.batch_ts[b] - a.batch_ends[b] + k + 1;
-            hazard = hazard || t.timestamp < TB_TIMESTAMP_MIN || t.timestamp >= stamp ||
+            hazard = t.timestamp < TB_TIMESTAMP_MIN || t.timestamp >= stamp ||
                      t.timestamp <= a.imported_floor ||
                      (k > 0 && t.timestamp <= a.events[k - 1].timestamp);
         }
         kinds = imported ? 1u : 2u;
-        uint64_t sd = kNone;
-        if (!hazard) {
-            // The id: new to every shard and unique in the call (the serial order's first
-            // occurrence keeps the slot; an in-call repeat is a hazard), or held by one shard.
+        if (!hazard && static_fail) {
+            shard = kShardAny;
+        } else if (!hazard) {
             const tb_transfer_t* ev = a.events;
             const tb_uint128_t* ids = a.tr.ids;
             const uint64_t base = a.base;
@@ -136,47 +169,52 @@ __global__ void __launch_bounds__(kRouteBlock) tbr_pass1(RouteArgs a) {
                 const uint64_t owner = (a.tr.slots.slots[s] & kRefMask) - 1;
                 if (owner < base) {
                     shard = uint8_t(a.tr.shard[owner] & 0x7Fu);  // exists: decided on its holder
-                    hazard = dup;
+                } else if (post_void) {
+                    shard = kShardPending;
                 } else {
-                    hazard = dup || owner != base + k;
+                    const uint64_t rd = dir_find(a.acc, t.debit_account_id);
+                    const uint64_t rc = dir_find(a.acc, t.credit_account_id);
+                    if (rd != kNone && rc != kNone && a.acc.shard[rd] != a.acc.shard[rc]) {
+                        shard = kShardAny;
+                        patch = cross_status(t);
+                    } else if (rd != kNone) {
+                        shard = a.acc.shard[rd];
+                    } else if (rc != kNone) {
+                        shard = a.acc.shard[rc];
+                    } else {
+                        shard = kShardAny;
+                    }
                 }
             }
         }
-        if (!hazard && shard == kShardHazard) {
-            if (post_void) {
-                shard = kShardPending;
-            } else {
-                const uint64_t rd = dir_find(a.acc, t.debit_account_id);
-                const uint64_t rc = dir_find(a.acc, t.credit_account_id);
-                hazard = rd == kNone || rc == kNone || a.acc.shard[rd] != a.acc.shard[rc];
-                if (!hazard) shard = a.acc.shard[rd];
-            }
-        }
-        if (!hazard && shard != kShardPending) sd = shard;
+        any = shard == kShardAny;
         a.ev_shard[k] = hazard ? kShardHazard : shard;
         a.ev_slot[k] = slot;
+        a.ev_patch[k] = patch;
+        a.ev_keep[k] = 0;
         a.tr.ids[a.base + k] = t.id;
-        const bool timed = (f & TB_TRANSFER_PENDING) && t.timeout > 0;
-        a.tr.shard[a.base + k] = uint8_t(sd == kNone ? 0 : sd) | (timed ? TBR_TIMED : 0);
         pv_any = post_void;
     }
     if (__any(pv_any) && (threadIdx.x & 63) == 0) atomicOr(&a.flags[2], 1u);
     const uint64_t any_imported = __ballot(kinds & 1u), any_plain = __ballot(kinds & 2u);
     if ((threadIdx.x & 63) == 0 && (any_imported || any_plain))
         atomicOr(&a.flags[3], (any_imported ? 1u : 0u) | (any_plain ? 2u : 0u));
+    count_wave(&a.flags[4], any);
     raise_hazard(a, hazard);
 }
 
 // Pass 2, per post/void: the shard of its pending transfer -- the directory's holder, or the
 // in-call event that creates it (post_or_void_pending_transfer reads only the pending transfer,
-// its TransferPending status and its accounts, all on that shard, :4053-4299). A pending id
-// found nowhere (no shard is pinned) or created in the call by another post/void is a hazard.
+// its TransferPending status and its accounts, all on that shard, :4053-4299). A pending id found
+// nowhere fails pending_transfer_not_found (:4100) after checks that read no state: any shard; so
+// does one whose in-call creator fails whatever its shard (an event of any shard). A pending
+// transfer created in the call by another post/void is a hazard.
 // (A post/void of a pending transfer with a timeout resets pulse_next_timestamp on equality with
 // the value over all shards, :4227-4229: the shards record their updates and the caller
 // resolves them after the call -- tbg_pnt_ops.)
 __global__ void __launch_bounds__(kRouteBlock) tbr_pass_pv(RouteArgs a) {
     const uint32_t k = blockIdx.x * kRouteBlock + threadIdx.x;
-    bool hazard = false;
+    bool hazard = false, any = false;
     if (k < a.n && a.ev_shard[k] == kShardPending) {
         const tb_transfer_t& t = a.events[k];
         const tb_transfer_t* ev = a.events;
@@ -185,7 +223,7 @@ __global__ void __launch_bounds__(kRouteBlock) tbr_pass_pv(RouteArgs a) {
         const uint64_t s = probe_find(a.tr.slots, t.pending_id, [=](uint64_t r) {
             return r >= base ? ev[r - base].id : ids[r];
         });
-        uint8_t shard = kShardHazard;
+        uint8_t shard = kShardAny;
         if (s != kNone) {
             const uint64_t r = (a.tr.slots.slots[s] & kRefMask) - 1;
             if (r < base) {
@@ -194,47 +232,95 @@ __global__ void __launch_bounds__(kRouteBlock) tbr_pass_pv(RouteArgs a) {
                 const tb_transfer_t& p = ev[r - base];
                 const bool p_pv = (p.flags & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) != 0;
                 const uint8_t ps = a.ev_shard[r - base];
-                if (!p_pv && ps < kShardPending) shard = ps;
+                shard = p_pv || ps == kShardHazard ? kShardHazard : ps;
             }
         }
         hazard = shard == kShardHazard;
+        any = shard == kShardAny;
         a.ev_shard[k] = shard;
-        if (!hazard) a.tr.shard[a.base + k] = shard;
+    }
+    count_wave(&a.flags[4], any);
+    raise_hazard(a, hazard);
+}
+
+// Pass 3, per event whose id repeats an earlier event's of the call (the slot's final owner, the
+// serial order's first occurrence): it runs on the first occurrence's shard -- created or orphaned
+// there, the repeat is decided by create_transfer_exists / id_already_failed on that shard;
+// failed otherwise, the repeat executes afresh, which it may do there when its own placement is
+// any shard or the same. Else, or when the first occurrence runs anywhere, or the repeat is a
+// surrogate (whose exists comparison would see its substituted account), a hazard.
+__global__ void __launch_bounds__(kRouteBlock) tbr_pass_dup(RouteArgs a) {
+    const uint32_t k = blockIdx.x * kRouteBlock + threadIdx.x;
+    bool hazard = false, repeat = false;
+    if (k < a.n && a.ev_slot[k] != kNone32 && a.ev_shard[k] != kShardHazard) {
+        const uint64_t r = (a.tr.slots.slots[a.ev_slot[k]] & kRefMask) - 1;
+        if (r >= a.base && r != a.base + k) {
+            repeat = true;
+            const uint8_t own = a.ev_shard[k];
+            const uint8_t first = a.ev_shard[r - a.base];
+            const bool ok = a.ev_patch[k] == 0 && first < kShardAny &&
+                            (own == kShardAny || own == first);
+            a.ev_shard[k] = ok ? first : kShardHazard;
+            hazard = !ok;
+        }
+    }
+    count_wave(&a.flags[6], repeat);
+    raise_hazard(a, hazard);
+}
+
+// Pass 4, per chain head: linked chains (:3002-3213) are atomic, so a chain goes to a shard whole
+// -- every event pinned to the same shard, the chain's events that may run anywhere with them --
+// and a chain left open at its batch's end (the slice is one batch on its shard) is a hazard.
+// A single event that may run anywhere goes to shard k mod shards.
+__global__ void __launch_bounds__(kRouteBlock) tbr_pass_chains(RouteArgs a) {
+    const uint32_t k = blockIdx.x * kRouteBlock + threadIdx.x;
+    bool hazard = false;
+    if (k < a.n) {
+        const uint32_t b = batch_of_guess(a.batch_ends, a.n_batches, a.n, k);
+        const uint32_t bstart = b ? a.batch_ends[b - 1] : 0, bend = a.batch_ends[b];
+        const bool head = k == bstart || !(a.events[k - 1].flags & TB_TRANSFER_LINKED);
+        const bool linked = (a.events[k].flags & TB_TRANSFER_LINKED) != 0;
+        if (head && !linked) {
+            if (a.ev_shard[k] == kShardAny) a.ev_shard[k] = uint8_t(k % a.shards);
+        } else if (head) {
+            uint32_t sh = kShardAny, j = k;
+            bool closed = false;
+            for (; j < bend; j++) {
+                const uint8_t c = a.ev_shard[j];
+                if (c >= kShardPending || (c < kShardAny && sh != kShardAny && c != sh)) {
+                    hazard = true;
+                    break;
+                }
+                if (c < kShardAny) sh = c;
+                if (!(a.events[j].flags & TB_TRANSFER_LINKED)) {
+                    closed = true;
+                    break;
+                }
+            }
+            hazard = hazard || !closed;
+            if (!hazard) {
+                if (sh == kShardAny) sh = uint8_t(k % a.shards);
+                for (uint32_t x = k; x <= j; x++) a.ev_shard[x] = uint8_t(sh);
+            }
+        }
     }
     raise_hazard(a, hazard);
 }
 
-// Pass 3, per event: linked chains (:3002-3213) are atomic, so a chain goes to a shard whole --
-// every event pinned to the same shard -- and a chain left open at its batch's end (the slice
-// is one batch on its shard) is a hazard. The chain's first event checks it. Then the per-block
-// counts per shard of the scatter.
-__global__ void __launch_bounds__(kRouteBlock) tbr_pass_chains(RouteArgs a) {
+// Per-block counts per shard of the scatter (every event placed by now, else a hazard).
+__global__ void __launch_bounds__(kRouteBlock) tbr_pass_count(RouteArgs a) {
     __shared__ unsigned int cnt[kShardsMax];
     for (uint32_t s = threadIdx.x; s < a.shards; s += kRouteBlock) cnt[s] = 0;
     __syncthreads();
     const uint32_t k = blockIdx.x * kRouteBlock + threadIdx.x;
-    bool hazard = false;
+    bool hazard = false, patched = false;
     if (k < a.n) {
         const uint8_t sh = a.ev_shard[k];
-        hazard = sh >= kShardPending;
-        const bool linked = (a.events[k].flags & TB_TRANSFER_LINKED) != 0;
-        if (linked && !hazard) {
-            const uint32_t b = batch_of_guess(a.batch_ends, a.n_batches, a.n, k);
-            const uint32_t bstart = b ? a.batch_ends[b - 1] : 0, bend = a.batch_ends[b];
-            const bool head = k == bstart || !(a.events[k - 1].flags & TB_TRANSFER_LINKED);
-            if (head) {
-                uint32_t j = k + 1;
-                for (; j < bend; j++) {
-                    if (a.ev_shard[j] != sh) break;
-                    if (!(a.events[j].flags & TB_TRANSFER_LINKED)) break;
-                }
-                // ended by a non-linked event of the same shard; else another shard's event or
-                // the batch's end (chain open)
-                hazard = j >= bend || a.ev_shard[j] != sh;
-            }
-        }
+        hazard = sh >= a.shards;
+        patched = a.ev_patch[k] != 0;
         if (!hazard) atomicAdd(&cnt[sh], 1u);
     }
+    count_wave(&a.flags[5], patched);
     raise_hazard(a, hazard);
     __syncthreads();
     for (uint32_t s = threadIdx.x; s < a.shards; s += kRouteBlock)
@@ -251,6 +337,8 @@ __global__ void tbr_release(RouteArgs a) {
     if ((*w & kRefMask) == a.base + k + 1) *w = kTomb;
 }
 
+// Each event copied to its shard's slice with its global commit timestamp and its position (a
+// surrogate with its credit account replaced by its debit account); its shard into the store.
 __global__ void __launch_bounds__(kRouteBlock) tbr_pass2(RouteArgs a, const uint32_t* offsets,
                                                          tb_transfer_t* out_events,
                                                          uint64_t* out_ts, uint32_t* out_pos) {
@@ -273,36 +361,47 @@ __global__ void __launch_bounds__(kRouteBlock) tbr_pass2(RouteArgs a, const uint
     const uint32_t pos = offsets[uint64_t(s) * a.nblocks + blockIdx.x] + rank;
     const uint4* src = reinterpret_cast<const uint4*>(&a.events[k]);
     uint4* dst = reinterpret_cast<uint4*>(&out_events[pos]);
+    uint4 q[8];
 #pragma unroll
-    for (int i = 0; i < 8; i++) dst[i] = src[i];
+    for (int i = 0; i < 8; i++) q[i] = src[i];
+    if (a.ev_patch[k]) q[2] = q[1];  // credit_account_id (bytes 32..47) := debit_account_id
+#pragma unroll
+    for (int i = 0; i < 8; i++) dst[i] = q[i];
     const uint32_t b = batch_of_guess(a.batch_ends, a.n_batches, a.n, k);
     out_ts[pos] = a.batch_ts[b] - a.batch_ends[b] + k + 1;
     out_pos[pos] = k;
+    a.tr.shard[a.base + k] = uint8_t(s);
 }
 
-// Results back to call order; ids that exist now (created, or orphaned by a transient failure)
-// stay in the directory, the others are released.
+// Results back to call order, a surrogate's status patched to the reference's; an id that now
+// exists on its shard (created, or orphaned by a transient failure) by any of its occurrences
+// keeps its slot (ev_keep of the first occurrence, whose store row holds the id and the shard).
 // The largest timestamp of a created transfer goes to key_max (the transfers objects tree's
-// key_range.key_max, which imported events on the host path read).
+// key_range.key_max, which the imported floor follows).
 __global__ void tbr_settle(RouteArgs a, const tb_create_result_t* shard_res, const uint32_t* pos,
                            tb_create_result_t* results, unsigned long long* key_max) {
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= a.n) return;
     const uint32_t k = pos[j];
-    const tb_create_result_t r = shard_res[j];
+    tb_create_result_t r = shard_res[j];
+    if (a.ev_patch[k] && r.status == TB_CT_ACCOUNTS_MUST_BE_DIFFERENT) r.status = a.ev_patch[k];
     results[k] = r;
-    const uint64_t row = a.base + k;
-    if (r.status == TB_STATUS_CREATED) {
-        atomicMax(key_max, (unsigned long long)r.timestamp);
-        return;
-    }
-    if (tb_transfer_status_transient(r.status)) {
-        a.tr.shard[row] &= uint8_t(~TBR_TIMED);  // an orphan is no pending transfer
-        return;
-    }
+    const bool created = r.status == TB_STATUS_CREATED;
+    if (created) atomicMax(key_max, (unsigned long long)r.timestamp);
     const uint32_t s = a.ev_slot[k];
+    if (!(created || tb_transfer_status_transient(r.status)) || s == kNone32) return;
+    const uint64_t owner = (a.tr.slots.slots[s] & kRefMask) - 1;
+    if (owner >= a.base) a.ev_keep[owner - a.base] = 1;
+}
+
+// ... then the slots of first occurrences whose id exists nowhere are released.
+__global__ void tbr_settle_release(RouteArgs a) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= a.n) return;
+    const uint32_t s = a.ev_slot[k];
+    if (s == kNone32 || a.ev_keep[k]) return;
     unsigned long long* w = &a.tr.slots.slots[s];
-    if ((*w & kRefMask) == row + 1) *w = kTomb;
+    if ((*w & kRefMask) == a.base + k + 1) *w = kTomb;
 }
 
 uint64_t next_pow2(uint64_t x) {
@@ -320,6 +419,9 @@ struct tbr_ctx {
     uint64_t acc_used = 0, acc_cap = 0, tr_used = 0, tr_cap = 0;
     uint8_t* ev_shard = nullptr;
     uint32_t* ev_slot = nullptr;
+    uint8_t* ev_patch = nullptr;
+    uint8_t* ev_keep = nullptr;
+    uint64_t route_stats[3] = {0, 0, 0};  // the last routed call's (anywhere, surrogates, repeats)
     uint32_t* block_counts = nullptr;
     uint32_t* offsets = nullptr;
     unsigned int* flags = nullptr;
@@ -358,6 +460,8 @@ RouteArgs route_args(tbr_ctx* r, const tb_transfer_t* ev, uint32_t n, const uint
     a.nblocks = (n + kRouteBlock - 1) / kRouteBlock;
     a.ev_shard = r->ev_shard;
     a.ev_slot = r->ev_slot;
+    a.ev_patch = r->ev_patch;
+    a.ev_keep = r->ev_keep;
     a.block_counts = r->block_counts;
     a.flags = r->flags;
     a.imported_floor = r->imported_floor;
@@ -423,9 +527,11 @@ tbr_ctx* tbr_open(uint32_t shards, uint64_t account_capacity, uint64_t transfer_
          alloc(&r->tr.shard, transfer_capacity, false, r->stream) &&
          alloc(&r->ev_shard, events_max, false, r->stream) &&
          alloc(&r->ev_slot, events_max, false, r->stream) &&
+         alloc(&r->ev_patch, events_max, false, r->stream) &&
+         alloc(&r->ev_keep, events_max, false, r->stream) &&
          alloc(&r->block_counts, uint64_t(shards) * nblocks, false, r->stream) &&
          alloc(&r->offsets, uint64_t(shards) * nblocks, false, r->stream) &&
-         alloc(&r->flags, 4, true, r->stream) && alloc(&r->key_max, 1, true, r->stream) &&
+         alloc(&r->flags, 8, true, r->stream) && alloc(&r->key_max, 1, true, r->stream) &&
          alloc(&r->q_ids, events_max, false, r->stream) &&
          alloc(&r->q_out, events_max, false, r->stream);
     ok = ok && hipStreamSynchronize(r->stream) == hipSuccess;
@@ -443,7 +549,7 @@ void tbr_close(tbr_ctx* r) {
     if (!r) return;
     if (r->stream) (void)hipStreamSynchronize(r->stream);
     void* ptrs[] = {r->acc.slots.slots, r->acc.ids, r->acc.shard, r->tr.slots.slots, r->tr.ids,
-                    r->tr.shard, r->ev_shard, r->ev_slot, r->block_counts, r->offsets, r->flags,
+                    r->tr.shard, r->ev_shard, r->ev_slot, r->ev_patch, r->ev_keep, r->block_counts, r->offsets, r->flags,
                     r->key_max, r->q_ids, r->q_out};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
@@ -479,18 +585,23 @@ int64_t tbr_route_device(tbr_ctx* r, const tb_transfer_t* d_events, uint32_t n,
     if (r->tr_used + n > r->tr_cap) return -28;
     RouteArgs a = route_args(r, d_events, n, d_batch_ends, d_batch_ts, n_batches);
     const dim3 grid(a.nblocks), block(kRouteBlock);
-    if (hipMemsetAsync(r->flags, 0, 16, r->stream)) return -5;
+    if (hipMemsetAsync(r->flags, 0, 32, r->stream)) return -5;
     hipLaunchKernelGGL(tbr_pass1, grid, block, 0, r->stream, a);
     hipLaunchKernelGGL(tbr_pass_pv, grid, block, 0, r->stream, a);
+    hipLaunchKernelGGL(tbr_pass_dup, grid, block, 0, r->stream, a);
     hipLaunchKernelGGL(tbr_pass_chains, grid, block, 0, r->stream, a);
+    hipLaunchKernelGGL(tbr_pass_count, grid, block, 0, r->stream, a);
     std::vector<uint32_t> counts(uint64_t(r->shards) * a.nblocks);
-    unsigned int f[4] = {0, 0, 0, 0};
-    if (hipMemcpyAsync(f, r->flags, 16, hipMemcpyDeviceToHost, r->stream) ||
+    unsigned int f[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyAsync(f, r->flags, 32, hipMemcpyDeviceToHost, r->stream) ||
         hipMemcpyAsync(counts.data(), r->block_counts, counts.size() * 4, hipMemcpyDeviceToHost,
                        r->stream) ||
         hipStreamSynchronize(r->stream))
         return -5;
     if (f[3] == 3u) f[0] = 1;  // imported and non-imported events in one call
+    r->route_stats[0] = f[4];
+    r->route_stats[1] = f[5];
+    r->route_stats[2] = f[6];
     if (f[0] || f[1]) {
         hipLaunchKernelGGL(tbr_release, grid, block, 0, r->stream, a);
         if (hipStreamSynchronize(r->stream)) return -5;
@@ -519,6 +630,12 @@ int64_t tbr_route_device(tbr_ctx* r, const tb_transfer_t* d_events, uint32_t n,
     return f[2] ? 2 : 0;
 }
 
+int tbr_route_stats(tbr_ctx* r, uint64_t* out) {
+    if (!r || !out) return -22;
+    for (int i = 0; i < 3; i++) out[i] = r->route_stats[i];
+    return 0;
+}
+
 int tbr_set_imported_floor(tbr_ctx* r, uint64_t floor) {
     if (!r) return -22;
     r->imported_floor = floor;
@@ -535,6 +652,7 @@ int tbr_settle_device(tbr_ctx* r, const tb_create_result_t* d_shard_results,
     if (hipMemsetAsync(r->key_max, 0, 8, r->stream)) return -5;
     hipLaunchKernelGGL(tbr_settle, dim3((n + 255) / 256), dim3(256), 0, r->stream, a,
                        d_shard_results, d_positions, d_results, r->key_max);
+    hipLaunchKernelGGL(tbr_settle_release, dim3((n + 255) / 256), dim3(256), 0, r->stream, a);
     if (hipGetLastError() || hipMemcpyAsync(&km, r->key_max, 8, hipMemcpyDeviceToHost, r->stream) ||
         hipStreamSynchronize(r->stream))
         return -5;

@@ -38,6 +38,21 @@ class TbgOptions(ctypes.Structure):
     ]
 
 
+def options(account_capacity, transfer_capacity, batch_events_max=1 << 16, batch_count_max=4096,
+            pulse_batch_max=8190, device=0, pulse_next_timestamp_init=(1 << 63) - 1,
+            account_events_capacity=0) -> TbgOptions:
+    o = TbgOptions()
+    o.account_capacity = account_capacity
+    o.transfer_capacity = transfer_capacity
+    o.batch_events_max = batch_events_max
+    o.batch_count_max = batch_count_max
+    o.pulse_batch_max = pulse_batch_max
+    o.device = device
+    o.pulse_next_timestamp_init = pulse_next_timestamp_init
+    o.account_events_capacity = account_events_capacity
+    return o
+
+
 class TbgStats(ctypes.Structure):
     _fields_ = [
         ("events", ctypes.c_uint64),
@@ -144,6 +159,28 @@ SIGNATURES = [
                                           vp, vp]),
     ("tbr_settle_device", ctypes.c_int, [vp, vp, vp, ctypes.c_uint32, vp, c_u64p]),
     ("tbr_set_imported_floor", ctypes.c_int, [vp, ctypes.c_uint64]),
+    ("tbr_route_stats", ctypes.c_int, [vp, c_u64p]),
+    ("tbg_group_open", vp, [vp, vp]),
+    ("tbg_group_open_shards", vp, [vp, vp, vp]),
+    ("tbg_group_close", None, [vp]),
+    ("tbg_group_last_error", ctypes.c_char_p, [vp]),
+    ("tbg_group_shard", vp, [vp, ctypes.c_uint32]),
+    ("tbg_group_create_accounts", ctypes.c_int, [vp, vp, ctypes.c_uint32, vp, vp,
+                                                ctypes.c_uint32, vp]),
+    ("tbg_group_create_transfers", ctypes.c_int, [vp, vp, ctypes.c_uint32, vp, vp,
+                                                 ctypes.c_uint32, vp]),
+    ("tbg_group_create_transfers_device", ctypes.c_int, [vp, vp, ctypes.c_uint32, vp, vp,
+                                                        ctypes.c_uint32, vp]),
+    ("tbg_group_pulse", ctypes.c_int64, [vp, ctypes.c_uint64]),
+    ("tbg_group_pulse_next_timestamp", ctypes.c_uint64, [vp]),
+    ("tbg_group_lookup_accounts", ctypes.c_int64, [vp, vp, ctypes.c_uint32, vp]),
+    ("tbg_group_lookup_transfers", ctypes.c_int64, [vp, vp, ctypes.c_uint32, vp]),
+    ("tbg_group_executor", None, [vp, ctypes.POINTER(Executor)]),
+    ("tbg_group_stats_read", ctypes.c_int, [vp, vp]),
+    ("tbg_group_plan", ctypes.c_int64, [vp, ctypes.c_int, vp, ctypes.c_uint32, vp, vp,
+                                        ctypes.c_uint32, vp, vp, vp, ctypes.c_uint32]),
+    ("tbg_group_record_accounts", ctypes.c_int, [vp, vp, vp, ctypes.c_uint32]),
+    ("tbg_group_record_transfers", ctypes.c_int, [vp, vp, vp, ctypes.c_uint32]),
     ("tb_sm_open", vp, [ctypes.POINTER(SmOptions), ctypes.POINTER(Executor)]),
     ("tb_sm_open_gpu", vp, [ctypes.POINTER(SmOptions), ctypes.POINTER(TbgOptions)]),
     ("tb_sm_open_gpu_checkpoint", vp, [ctypes.POINTER(SmOptions), ctypes.POINTER(TbgOptions),

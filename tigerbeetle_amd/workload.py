@@ -366,3 +366,100 @@ def transfers_config5(n: int, accounts_per_shard: int, rank: int, world: int, se
     t["code"] = _codes(rng, n)
     _u128_col(t, "amount", _amounts(rng, n))
     return t, dr_local, cr_local
+
+
+# ---- the sharded group's workloads (bench.py group lines, tests/test_routed.py) -----------------
+
+HAZARD_KINDS = ("debit_not_found", "cross_ledger", "id_zero", "reserved_flag", "repeat_exists",
+                "pending_not_found", "credit_not_found")
+
+
+def group_accounts(ledgers: int, per_ledger: int, seed: int = 42) -> np.ndarray:
+    """`per_ledger` accounts on each of ledgers 2 .. ledgers + 1 (ids (ledger - 2) * per_ledger + 1
+    ..): the group's shards by ledger (ledger range option `ledgers + 1`)."""
+    return np.concatenate([accounts(per_ledger, seed=seed + i, id_offset=i * per_ledger,
+                                    ledger=2 + i) for i in range(ledgers)])
+
+
+def mixed_ledger_transfers(n: int, ledgers: int, per_ledger: int, seed: int = 42,
+                           id_offset: int = 0):
+    """One client call of `n` transfers whose ledger is uniform per event over ledgers 2 ..
+    ledgers + 1, debit / credit uniform within it (benchmark_load.zig's distributions), ids
+    id_offset + 1 ..; returns (transfers, ledger index per event)."""
+    t = transfers_uniform(n, per_ledger, seed=seed, id_offset=id_offset)
+    lg = np.random.default_rng(seed + 1).integers(0, ledgers, size=n).astype(U64)
+    t["debit_account_id"][:, 0] += lg * U64(per_ledger)
+    t["credit_account_id"][:, 0] += lg * U64(per_ledger)
+    t["ledger"] = (2 + lg).astype(np.uint32)
+    return t, lg
+
+
+def hazard_transfers(n: int, ledgers: int, per_ledger: int, rate: float, seed: int = 42,
+                     id_offset: int = 0):
+    """mixed_ledger_transfers with a fraction `rate` of injected failures whose statuses follow
+    from the events alone (config 4's failure kinds across ledgers; src/state_machine.zig
+    :3729-3798, :4053-4100): an unknown debit / credit account, a credit account on another
+    ledger (another shard), id 0, a reserved flag, a post of a pending transfer found nowhere, and
+    an exact repeat of an earlier transfer of the call (`exists`). Returns (transfers, kinds: -1 or
+    the HAZARD_KINDS index per event, the repeated event's index per event or -1)."""
+    if ledgers < 2:
+        raise ValueError("hazard_transfers needs two ledgers at least (cross-ledger transfers)")
+    t, lg = mixed_ledger_transfers(n, ledgers, per_ledger, seed=seed, id_offset=id_offset)
+    rng = np.random.default_rng(seed + 2)
+    m = max(1, int(n * rate))
+    pos = np.sort(rng.choice(np.arange(n // 2, n), size=m, replace=False))
+    kinds = np.full(n, -1, dtype=np.int64)
+    src = np.full(n, -1, dtype=np.int64)
+    unknown = U64(1 << 40)
+    for j, k in enumerate(pos.tolist()):
+        kind = j % len(HAZARD_KINDS)
+        kinds[k] = kind
+        name = HAZARD_KINDS[kind]
+        if name == "debit_not_found":
+            t["debit_account_id"][k, 0] = unknown + U64(k)
+        elif name == "credit_not_found":
+            t["credit_account_id"][k, 0] = unknown + U64(k)
+        elif name == "cross_ledger":
+            other = (int(lg[k]) + 1) % ledgers
+            t["credit_account_id"][k, 0] = U64(other * per_ledger + 1 + k % per_ledger)
+        elif name == "id_zero":
+            t["id"][k] = 0
+        elif name == "reserved_flag":
+            t["flags"][k] = 1 << 12
+        elif name == "pending_not_found":
+            t["flags"][k] = 4  # post_pending_transfer
+            t["pending_id"][k, 0] = unknown + U64(k)
+        elif name == "repeat_exists":
+            s = int(rng.integers(0, n // 2))  # (the first half holds no injected event)
+            t[k] = t[s]
+            src[k] = s
+    return t, kinds, src
+
+
+def hazard_expected(t: np.ndarray, kinds: np.ndarray, src: np.ndarray, stamps: np.ndarray,
+                    ledgers: int):
+    """The reference's results for hazard_transfers (closed form; every other event is created,
+    and no event's outcome depends on order) -- (status, timestamp) per event -- and the created
+    events' mask."""
+    from .types import CreateTransferStatus as S
+    status = np.full(len(t), STATUS_CREATED_U32, dtype=np.uint32)
+    ts = stamps.astype(U64).copy()
+    want = {
+        "debit_not_found": S.debit_account_not_found,
+        "credit_not_found": S.credit_account_not_found,
+        "cross_ledger": S.accounts_must_have_the_same_ledger,
+        "id_zero": S.id_must_not_be_zero,
+        "reserved_flag": S.reserved_flag,
+        "pending_not_found": S.pending_transfer_not_found,
+    }
+    for kind, name in enumerate(HAZARD_KINDS):
+        sel = kinds == kind
+        if name == "repeat_exists":
+            status[sel] = int(S.exists)
+            ts[sel] = stamps[src[sel]]
+        else:
+            status[sel] = int(want[name])
+    return status, ts, status == STATUS_CREATED_U32
+
+
+STATUS_CREATED_U32 = 0xFFFFFFFF
