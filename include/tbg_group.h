@@ -154,6 +154,10 @@ typedef struct tbg_group_stats {
     uint64_t surrogates;       /* device-path events with a patched status (cross-shard accounts) */
     uint64_t anywhere;         /* device-path events whose status followed from themselves */
     uint64_t repeats;          /* device-path events repeating an id of the call */
+    uint64_t route_ns;         /* device path, host wall time: routing (tbr_route_device) */
+    uint64_t execute_ns;       /* ... the shards' slices (copies in, execution, copies out) */
+    uint64_t settle_ns;        /* ... settle and the pulse_next_timestamp resolution */
+    uint64_t engine_ns;        /* the exact engine's calls */
 } tbg_group_stats;
 int tbg_group_stats_read(tbg_group* g, tbg_group_stats* out);
 

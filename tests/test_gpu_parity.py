@@ -441,13 +441,16 @@ def test_account_events_window_wide(case):
         p.close()
 
 
-@pytest.mark.parametrize("case", ["dense", "closing", "wide", "no-window"])
+@pytest.mark.parametrize("case", ["dense", "closing", "wide", "suffix", "no-window"])
 def test_account_events_dense(case, monkeypatch):
     """AccountEvents of general calls in one pass (events.hpp ae_dense_*): calls of > 8,192 events
     with pending transfers, posts and voids of them (replayed and FAST), linked chains with
     injected failures and limited accounts, against the oracle's log byte for byte. `closing`:
     pending transfers that close accounts (a `closed` flip) and `wide`: amounts of 2^19 and more
-    make the call take the general appends; `no-window`: TBG_NO_AE_WINDOW."""
+    make the call take the general appends; `suffix`: 3,000 created transfers of 2^19 - 1 on one
+    debit account -- every amount passes ae_dense_stage, but the account's later-delta suffix
+    crosses 2^30 and ae_dense_suffix must refuse the call; `no-window`:
+    TBG_NO_AE_WINDOW."""
     if case == "no-window":
         monkeypatch.setenv("TBG_NO_AE_WINDOW", "1")
     rng = np.random.default_rng(91)
@@ -473,7 +476,15 @@ def test_account_events_dense(case, monkeypatch):
             if case == "wide" and step == 3:
                 single = np.nonzero(t["flags"] == 0)[0][:20]
                 t["amount"][single, 0] = 1 << 20
+            if case == "suffix" and step == 3:
+                single = np.nonzero((t["flags"] == 0) & (t["debit_account_id"][:, 0] > 8) &
+                                    (t["credit_account_id"][:, 0] != 100))[0][:3_000]
+                assert len(single) == 3_000 and single[-1] - single[0] > 2 * 2_048
+                t["debit_account_id"][single, 0] = 100
+                t["amount"][single, 0] = (1 << 19) - 1
             r = p.create_transfers(t, _split(n, rng, 8189))
+            if case == "suffix" and step == 3:
+                assert (r["status"][single] == 0xFFFFFFFF).all()
             paths.append(p.last_stats["ae_window"])
             made = r["status"] == 0xFFFFFFFF
             ids = t["id"][:, 0]

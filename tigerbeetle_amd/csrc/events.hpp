@@ -2071,7 +2071,7 @@ __global__ void ae_dense_ts_init(unsigned long long* ts) {
     }
 }
 
-// The refusal word for the host (mapped pinned memory).
+// A balance less a sign-extended i32 later delta.
 __device__ inline uint4 ae_sub_i32(uint4 balance, uint32_t d) {
     return ae_q(ae_u(balance) - u128(int64_t(int32_t(d))));  // (sign-extended: u128 wraps)
 }

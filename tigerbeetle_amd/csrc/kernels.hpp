@@ -839,11 +839,19 @@ __device__ inline void ingest_finish(const Tables& T, const Call<tb_transfer_t>&
     static_assert(sizeof(DevScalars) / 8 <= 64, "one word a lane");
     const unsigned long long* src = reinterpret_cast<const unsigned long long*>(S);
     if (threadIdx.x < words) c.finish_scalars[threadIdx.x] = load(src + threadIdx.x);
-    // (the copy's stores wait for its loads: the wave's reset below comes after every read)
+    // Every lane's copy (its load and its store) happens before lane 0's reset: a wavefront-scope
+    // release / acquire around the barrier orders them in the HIP memory model, not only through
+    // the wave's in-order issue.
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (threadIdx.x == 0) reset_call_scalars(S);
-    // The sequence word's system-scope release covers the wave's copy and reset (a release is
-    // the issuing wave's cache write-back and wait); without a sequence word, a fence.
+    // The sequence word's system-scope release covers the wave's copy and reset. ISA-level
+    // assumption (gfx950): a release is a wave instruction sequence -- the L2 write-back and the
+    // s_waitcnt on the wave's outstanding stores -- so lane 0's release publishes the stores of all
+    // 64 lanes of its wave; the other lanes' stores were ordered before it by the wavefront fence
+    // above. test_gpu_parity's device-call and per-commit parity tests read finish_scalars through
+    // this publication on every small call. Without a sequence word, a fence.
     if (threadIdx.x == 0) {
         if (c.finish_seq)
             __hip_atomic_store(c.finish_seq, c.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);

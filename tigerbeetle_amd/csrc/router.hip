@@ -53,6 +53,8 @@ struct RouteArgs {
     uint32_t* ev_slot;      // per event: its claimed slot (kNone32: none)
     uint8_t* ev_patch;      // per event: a surrogate's status (0: none)
     uint8_t* ev_keep;       // per first occurrence: its id exists after the call
+    uint8_t* ev_link;       // per event: its linked flag (tbr_pass_chains reads no event again)
+    uint32_t* ev_owner;     // per repeat: its first occurrence's position (else kNone32)
     uint32_t* block_counts; // [shard][block]
     unsigned int* flags;    // [0] hazard, [1] table full, [2] the call posts or voids,
                             // [3] bit 0: an imported event, bit 1: a non-imported one,
@@ -91,8 +93,15 @@ constexpr uint8_t kShardHazard = 0xFF;
 constexpr uint8_t kShardPending = 0xFE;
 constexpr uint8_t kShardAny = 0xFD;
 
+// Sets bits of a call-wide flag word from one lane of the wave: tested first, so that only the
+// waves that find a bit clear issue the atomic (one atomic a wave to one word serialises every
+// wave of the grid in one L2 channel: ~11 ns each, 720 us over a 4M-event call).
+__device__ inline void set_flag(unsigned int* word, unsigned int bits) {
+    if ((__hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bits) != bits)
+        atomicOr(word, bits);
+}
 __device__ inline void raise_hazard(const RouteArgs& a, bool hazard) {
-    if (__any(hazard) && (threadIdx.x & 63) == 0) atomicOr(&a.flags[0], 1u);
+    if (__any(hazard) && (threadIdx.x & 63) == 0) set_flag(&a.flags[0], 1u);
 }
 __device__ inline void count_wave(unsigned int* counter, bool x) {
     const uint64_t m = __ballot(x);
@@ -114,6 +123,32 @@ __device__ inline uint8_t cross_status(const tb_transfer_t& t) {
     return TB_CT_ACCOUNTS_MUST_HAVE_THE_SAME_LEDGER;
 }
 
+// The wave's 64 consecutive events staged in LDS with fully coalesced 16-byte loads (each lane
+// then reads its own event's fields from LDS): 8 load instructions a wave instead of one per
+// field, each touching 64 lines. 144 bytes per event: an 8-lane group writes one event's 128
+// contiguous bytes, no two lanes on a bank (kernels.hpp tr_ingest).
+constexpr uint32_t kStageStride = 144;
+__device__ inline const tb_transfer_t* stage_wave_events(const tb_transfer_t* events, uint32_t n,
+                                                         uint8_t* my) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t k0 = blockIdx.x * kRouteBlock + (threadIdx.x & ~63u);
+    const uint32_t cnt = n > k0 ? (n - k0 < 64 ? n - k0 : 64) : 0;
+    const uint4* src = reinterpret_cast<const uint4*>(events + k0);
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const uint32_t idx = i * 64 + lane;
+        v4u v = {0, 0, 0, 0};
+        if (idx < cnt * 8) v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(&src[idx]));
+        const uint32_t e = i * 8 + (lane >> 3), part = lane & 7;
+        *reinterpret_cast<v4u*>(__builtin_assume_aligned(my + e * kStageStride + part * 16, 16)) = v;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    return reinterpret_cast<const tb_transfer_t*>(my + lane * kStageStride);
+}
+
 // Pass 1, per event: the shard its own fields pin.
 //  * A status that follows from the event alone (a nonzero padding, an id 0 / maxInt, a nonzero
 //    timestamp on a non-imported event: execute_create :3080, create_transfer :3729-3732) reads
@@ -130,11 +165,13 @@ __device__ inline uint8_t cross_status(const tb_transfer_t& t) {
 //    increase through the call and lie above every object of both grooves (the floor) and below
 //    their own commit timestamps.
 __global__ void __launch_bounds__(kRouteBlock) tbr_pass1(RouteArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds_ev[kRouteBlock / 64][64 * kStageStride];
     const uint32_t k = blockIdx.x * kRouteBlock + threadIdx.x;
+    const tb_transfer_t* mine = stage_wave_events(a.events, a.n, lds_ev[threadIdx.x >> 6]);
     bool hazard = false, pv_any = false, any = false;
     unsigned int kinds = 0;
     if (k < a.n) {
-        const tb_transfer_t& t = a.events[k];
+        const tb_transfer_t& t = *mine;
         const uint16_t f = t.flags;
         const bool post_void = (f & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) != 0;
         const bool imported = (f & TB_TRANSFER_IMPORTED) != 0;
@@ -192,13 +229,14 @@ __global__ void __launch_bounds__(kRouteBlock) tbr_pass1(RouteArgs a) {
         a.ev_slot[k] = slot;
         a.ev_patch[k] = patch;
         a.ev_keep[k] = 0;
+        a.ev_link[k] = uint8_t(f & TB_TRANSFER_LINKED);
         a.tr.ids[a.base + k] = t.id;
         pv_any = post_void;
     }
-    if (__any(pv_any) && (threadIdx.x & 63) == 0) atomicOr(&a.flags[2], 1u);
+    if (__any(pv_any) && (threadIdx.x & 63) == 0) set_flag(&a.flags[2], 1u);
     const uint64_t any_imported = __ballot(kinds & 1u), any_plain = __ballot(kinds & 2u);
     if ((threadIdx.x & 63) == 0 && (any_imported || any_plain))
-        atomicOr(&a.flags[3], (any_imported ? 1u : 0u) | (any_plain ? 2u : 0u));
+        set_flag(&a.flags[3], (any_imported ? 1u : 0u) | (any_plain ? 2u : 0u));
     count_wave(&a.flags[4], any);
     raise_hazard(a, hazard);
 }
@@ -252,10 +290,12 @@ __global__ void __launch_bounds__(kRouteBlock) tbr_pass_pv(RouteArgs a) {
 __global__ void __launch_bounds__(kRouteBlock) tbr_pass_dup(RouteArgs a) {
     const uint32_t k = blockIdx.x * kRouteBlock + threadIdx.x;
     bool hazard = false, repeat = false;
+    uint32_t owner = kNone32;
     if (k < a.n && a.ev_slot[k] != kNone32 && a.ev_shard[k] != kShardHazard) {
         const uint64_t r = (a.tr.slots.slots[a.ev_slot[k]] & kRefMask) - 1;
         if (r >= a.base && r != a.base + k) {
             repeat = true;
+            owner = uint32_t(r - a.base);
             const uint8_t own = a.ev_shard[k];
             const uint8_t first = a.ev_shard[r - a.base];
             const bool ok = a.ev_patch[k] == 0 && first < kShardAny &&
@@ -264,6 +304,7 @@ __global__ void __launch_bounds__(kRouteBlock) tbr_pass_dup(RouteArgs a) {
             hazard = !ok;
         }
     }
+    if (k < a.n) a.ev_owner[k] = owner;
     count_wave(&a.flags[6], repeat);
     raise_hazard(a, hazard);
 }
@@ -278,8 +319,8 @@ __global__ void __launch_bounds__(kRouteBlock) tbr_pass_chains(RouteArgs a) {
     if (k < a.n) {
         const uint32_t b = batch_of_guess(a.batch_ends, a.n_batches, a.n, k);
         const uint32_t bstart = b ? a.batch_ends[b - 1] : 0, bend = a.batch_ends[b];
-        const bool head = k == bstart || !(a.events[k - 1].flags & TB_TRANSFER_LINKED);
-        const bool linked = (a.events[k].flags & TB_TRANSFER_LINKED) != 0;
+        const bool head = k == bstart || !a.ev_link[k - 1];
+        const bool linked = a.ev_link[k] != 0;
         if (head && !linked) {
             if (a.ev_shard[k] == kShardAny) a.ev_shard[k] = uint8_t(k % a.shards);
         } else if (head) {
@@ -292,7 +333,7 @@ __global__ void __launch_bounds__(kRouteBlock) tbr_pass_chains(RouteArgs a) {
                     break;
                 }
                 if (c < kShardAny) sh = c;
-                if (!(a.events[j].flags & TB_TRANSFER_LINKED)) {
+                if (!a.ev_link[j]) {
                     closed = true;
                     break;
                 }
@@ -377,29 +418,65 @@ __global__ void __launch_bounds__(kRouteBlock) tbr_pass2(RouteArgs a, const uint
 // exists on its shard (created, or orphaned by a transient failure) by any of its occurrences
 // keeps its slot (ev_keep of the first occurrence, whose store row holds the id and the shard).
 // The largest timestamp of a created transfer goes to key_max (the transfers objects tree's
-// key_range.key_max, which the imported floor follows).
-__global__ void tbr_settle(RouteArgs a, const tb_create_result_t* shard_res, const uint32_t* pos,
-                           tb_create_result_t* results, unsigned long long* key_max) {
+// key_range.key_max, which the imported floor follows): a maximum per workgroup in block_max,
+// reduced by tbr_settle_release's first workgroup.
+__global__ void __launch_bounds__(kRouteBlock) tbr_settle(RouteArgs a,
+                                                          const tb_create_result_t* shard_res,
+                                                          const uint32_t* pos,
+                                                          tb_create_result_t* results,
+                                                          unsigned long long* block_max) {
+    __shared__ uint64_t wave_max[kRouteBlock / 64];
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= a.n) return;
-    const uint32_t k = pos[j];
-    tb_create_result_t r = shard_res[j];
-    if (a.ev_patch[k] && r.status == TB_CT_ACCOUNTS_MUST_BE_DIFFERENT) r.status = a.ev_patch[k];
-    results[k] = r;
-    const bool created = r.status == TB_STATUS_CREATED;
-    if (created) atomicMax(key_max, (unsigned long long)r.timestamp);
-    const uint32_t s = a.ev_slot[k];
-    if (!(created || tb_transfer_status_transient(r.status)) || s == kNone32) return;
-    const uint64_t owner = (a.tr.slots.slots[s] & kRefMask) - 1;
-    if (owner >= a.base) a.ev_keep[owner - a.base] = 1;
+    uint64_t ts_max = 0;
+    if (j < a.n) {
+        const uint32_t k = pos[j];
+        tb_create_result_t r = shard_res[j];
+        if (a.ev_patch[k] && r.status == TB_CT_ACCOUNTS_MUST_BE_DIFFERENT) r.status = a.ev_patch[k];
+        results[k] = r;
+        const bool created = r.status == TB_STATUS_CREATED;
+        if (created) ts_max = r.timestamp;
+        if ((created || tb_transfer_status_transient(r.status)) && a.ev_slot[k] != kNone32) {
+            const uint32_t o = a.ev_owner[k];
+            a.ev_keep[o == kNone32 ? k : o] = 1;
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const uint64_t other = __shfl_xor(ts_max, off);
+        ts_max = other > ts_max ? other : ts_max;
+    }
+    if ((threadIdx.x & 63) == 0) wave_max[threadIdx.x >> 6] = ts_max;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t m = 0;
+        for (uint32_t w = 0; w < kRouteBlock / 64; w++) m = wave_max[w] > m ? wave_max[w] : m;
+        block_max[blockIdx.x] = m;
+    }
 }
 
-// ... then the slots of first occurrences whose id exists nowhere are released.
-__global__ void tbr_settle_release(RouteArgs a) {
+// ... then the slots of first occurrences whose id exists nowhere are released; the first
+// workgroup reduces the per-workgroup maxima to key_max.
+__global__ void __launch_bounds__(kRouteBlock) tbr_settle_release(
+    RouteArgs a, const unsigned long long* block_max, uint32_t nblocks,
+    unsigned long long* key_max) {
+    if (blockIdx.x == 0) {
+        __shared__ uint64_t part[kRouteBlock];
+        uint64_t m = 0;
+        for (uint32_t b = threadIdx.x; b < nblocks; b += kRouteBlock)
+            m = block_max[b] > m ? block_max[b] : m;
+        part[threadIdx.x] = m;
+        __syncthreads();
+        for (uint32_t w = kRouteBlock / 2; w > 0; w >>= 1) {
+            if (threadIdx.x < w && part[threadIdx.x + w] > part[threadIdx.x])
+                part[threadIdx.x] = part[threadIdx.x + w];
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) *key_max = part[0];
+    }
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= a.n) return;
     const uint32_t s = a.ev_slot[k];
-    if (s == kNone32 || a.ev_keep[k]) return;
+    if (s == kNone32 || a.ev_keep[k] || a.ev_owner[k] != kNone32) return;
+    // (a first occurrence's own claim -- not the slot of an id that already existed)
     unsigned long long* w = &a.tr.slots.slots[s];
     if ((*w & kRefMask) == a.base + k + 1) *w = kTomb;
 }
@@ -421,11 +498,14 @@ struct tbr_ctx {
     uint32_t* ev_slot = nullptr;
     uint8_t* ev_patch = nullptr;
     uint8_t* ev_keep = nullptr;
+    uint8_t* ev_link = nullptr;
+    uint32_t* ev_owner = nullptr;
     uint64_t route_stats[3] = {0, 0, 0};  // the last routed call's (anywhere, surrogates, repeats)
     uint32_t* block_counts = nullptr;
     uint32_t* offsets = nullptr;
     unsigned int* flags = nullptr;
     unsigned long long* key_max = nullptr;  // settle: created timestamps' maximum
+    unsigned long long* block_max = nullptr;  // ... per settle workgroup
     uint64_t imported_floor = ~0ull;        // tbr_set_imported_floor (none yet: every import)
     tb_uint128_t* q_ids = nullptr;  // lookup / record staging (events_max)
     int32_t* q_out = nullptr;
@@ -462,6 +542,8 @@ RouteArgs route_args(tbr_ctx* r, const tb_transfer_t* ev, uint32_t n, const uint
     a.ev_slot = r->ev_slot;
     a.ev_patch = r->ev_patch;
     a.ev_keep = r->ev_keep;
+    a.ev_link = r->ev_link;
+    a.ev_owner = r->ev_owner;
     a.block_counts = r->block_counts;
     a.flags = r->flags;
     a.imported_floor = r->imported_floor;
@@ -523,15 +605,18 @@ tbr_ctx* tbr_open(uint32_t shards, uint64_t account_capacity, uint64_t transfer_
          alloc(&r->acc.ids, account_capacity, false, r->stream) &&
          alloc(&r->acc.shard, account_capacity, false, r->stream) &&
          alloc(&r->tr.slots.slots, tr_slots, true, r->stream) &&
-         alloc(&r->tr.ids, transfer_capacity, false, r->stream) &&
-         alloc(&r->tr.shard, transfer_capacity, false, r->stream) &&
+         alloc(&r->tr.ids, transfer_capacity, true, r->stream) &&
+         alloc(&r->tr.shard, transfer_capacity, true, r->stream) &&
          alloc(&r->ev_shard, events_max, false, r->stream) &&
          alloc(&r->ev_slot, events_max, false, r->stream) &&
          alloc(&r->ev_patch, events_max, false, r->stream) &&
          alloc(&r->ev_keep, events_max, false, r->stream) &&
+         alloc(&r->ev_link, events_max, false, r->stream) &&
+         alloc(&r->ev_owner, events_max, false, r->stream) &&
          alloc(&r->block_counts, uint64_t(shards) * nblocks, false, r->stream) &&
          alloc(&r->offsets, uint64_t(shards) * nblocks, false, r->stream) &&
          alloc(&r->flags, 8, true, r->stream) && alloc(&r->key_max, 1, true, r->stream) &&
+         alloc(&r->block_max, nblocks, true, r->stream) &&
          alloc(&r->q_ids, events_max, false, r->stream) &&
          alloc(&r->q_out, events_max, false, r->stream);
     ok = ok && hipStreamSynchronize(r->stream) == hipSuccess;
@@ -549,8 +634,8 @@ void tbr_close(tbr_ctx* r) {
     if (!r) return;
     if (r->stream) (void)hipStreamSynchronize(r->stream);
     void* ptrs[] = {r->acc.slots.slots, r->acc.ids, r->acc.shard, r->tr.slots.slots, r->tr.ids,
-                    r->tr.shard, r->ev_shard, r->ev_slot, r->ev_patch, r->ev_keep, r->block_counts, r->offsets, r->flags,
-                    r->key_max, r->q_ids, r->q_out};
+                    r->tr.shard, r->ev_shard, r->ev_slot, r->ev_patch, r->ev_keep, r->ev_link, r->ev_owner, r->block_counts, r->offsets, r->flags,
+                    r->key_max, r->block_max, r->q_ids, r->q_out};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (r->stream) (void)hipStreamDestroy(r->stream);
@@ -649,10 +734,11 @@ int tbr_settle_device(tbr_ctx* r, const tb_create_result_t* d_shard_results,
     RouteArgs a = route_args(r, nullptr, n, nullptr, nullptr, 1);
     a.base = r->call_base;
     unsigned long long km = 0;
-    if (hipMemsetAsync(r->key_max, 0, 8, r->stream)) return -5;
-    hipLaunchKernelGGL(tbr_settle, dim3((n + 255) / 256), dim3(256), 0, r->stream, a,
-                       d_shard_results, d_positions, d_results, r->key_max);
-    hipLaunchKernelGGL(tbr_settle_release, dim3((n + 255) / 256), dim3(256), 0, r->stream, a);
+    const uint32_t nb = (n + kRouteBlock - 1) / kRouteBlock;
+    hipLaunchKernelGGL(tbr_settle, dim3(nb), dim3(kRouteBlock), 0, r->stream, a, d_shard_results,
+                       d_positions, d_results, r->block_max);
+    hipLaunchKernelGGL(tbr_settle_release, dim3(nb), dim3(kRouteBlock), 0, r->stream, a,
+                       r->block_max, nb, r->key_max);
     if (hipGetLastError() || hipMemcpyAsync(&km, r->key_max, 8, hipMemcpyDeviceToHost, r->stream) ||
         hipStreamSynchronize(r->stream))
         return -5;

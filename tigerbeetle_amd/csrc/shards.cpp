@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <condition_variable>
 #include <cstdio>
 #include <memory>
@@ -223,6 +224,12 @@ struct tbg_group {
 
 namespace {
 
+uint64_t now_ns() {
+    return uint64_t(std::chrono::duration_cast<std::chrono::nanoseconds>(
+                        std::chrono::steady_clock::now().time_since_epoch())
+                        .count());
+}
+
 int fail(tbg_group* g, int rc, const std::string& what) {
     g->error = what;
     return rc < 0 ? rc : TBG_EHIP;
@@ -241,6 +248,7 @@ void refresh_floor(tbg_group* g) {
 int engine_call(tbg_group* g, tbs::Kind kind, const void* events, uint32_t n,
                 const uint32_t* lens, const uint64_t* bts, uint32_t nb,
                 tb_create_result_t* results) {
+    const uint64_t t0 = now_ns();
     try {
         const tbs::EngineStats before = g->eng->stats;
         g->eng->run(kind, static_cast<const uint8_t*>(events), n, lens, bts, nb, results);
@@ -251,6 +259,7 @@ int engine_call(tbg_group* g, tbs::Kind kind, const void* events, uint32_t n,
     } catch (const tbs::EngineError& e) {
         return fail(g, e.code, e.what());
     }
+    g->st.engine_ns += now_ns() - t0;
     return 0;
 }
 
@@ -260,6 +269,7 @@ int route_device(tbg_group* g, const tb_transfer_t* d_ev, uint32_t n, const uint
                  const uint64_t* d_ts, uint32_t nb, tb_create_result_t* d_res) {
     const uint32_t W = g->o.shards;
     std::vector<uint32_t> counts(W, 0);
+    const uint64_t t0 = now_ns();
     const int64_t mode = tbr_route_device(g->tbr, d_ev, n, d_ends, d_ts, nb, g->d_slices,
                                           g->d_slice_ts, g->d_pos, counts.data());
     if (mode < 0) return fail(g, int(mode), "tbr_route_device");
@@ -271,6 +281,8 @@ int route_device(tbg_group* g, const tb_transfer_t* d_ev, uint32_t n, const uint
         if (counts[s]) run.push_back(int(s));
     const int rdev = int(g->o.router_device);
     std::vector<int> rcs;
+    const uint64_t t1 = now_ns();
+    g->st.route_ns += t1 - t0;
     g->runner->run(run, [&](int s) -> int {
         const ShardLink& L = g->link[s];
         const uint64_t a = off[s], c = counts[s];
@@ -302,6 +314,8 @@ int route_device(tbg_group* g, const tb_transfer_t* d_ev, uint32_t n, const uint
             return fail(g, rcs[i], "shard " + std::to_string(run[i]) + ": " +
                                        tbg_last_error(static_cast<tbg_ctx*>(g->shards[run[i]])) +
                                        " (the shards' state is undefined)");
+    const uint64_t t2 = now_ns();
+    g->st.execute_ns += t2 - t1;
     uint64_t km = 0;
     const int rc = tbr_settle_device(g->tbr, g->d_slice_res, g->d_pos, n, d_res, &km);
     if (rc != 0) return fail(g, rc, "tbr_settle_device");
@@ -337,6 +351,7 @@ int route_device(tbg_group* g, const tb_transfer_t* d_ev, uint32_t n, const uint
             for (uint32_t s = 0; s < W; s++)
                 tbg_set_pulse_next_timestamp(static_cast<tbg_ctx*>(g->shards[s]), TB_TIMESTAMP_MIN);
     }
+    g->st.settle_ns += now_ns() - t2;
     return 0;
 }
 

@@ -53,7 +53,7 @@ class GroupOptions(ctypes.Structure):
 class GroupStats(ctypes.Structure):
     _fields_ = [(name, ctypes.c_uint64) for name in (
         "calls", "device_calls", "engine_calls", "segments", "chain_segments", "surrogates",
-        "anywhere", "repeats")]
+        "anywhere", "repeats", "route_ns", "execute_ns", "settle_ns", "engine_ns")]
 
 
 class ShardOps(ctypes.Structure):

@@ -13,6 +13,7 @@ from collections import defaultdict
 
 
 def short(name):
+    name = name.replace("(anonymous namespace)::", "")
     n = name.split("(")[0]
     for key in ("tr_ingest", "tr_commit", "bal_hash_apply", "bal_bucket_scatter",
                 "bal_bucket_accumulate", "bal_bucket_apply", "onesweep_iteration",
