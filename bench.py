@@ -762,17 +762,21 @@ def group_measure(args, shards, devices, N1, K, W, hazard_rate=0.0):
         res = g.create_accounts(acc, [len(acc)], [prepare_ts])
         assert (res["status"] == CREATED).all(), "group create_accounts"
         d_ends = dev.upload(np.cumsum(lens).astype(np.uint32))
+        # One generated call; step s is it with every nonzero id moved by s * N (fresh ids every
+        # step; the injected repeats keep repeating, ids 0 stay 0)
+        if hazard_rate > 0:
+            base, kinds, src = workload.hazard_transfers(N, L, P, hazard_rate, seed=args.seed)
+        else:
+            base, _ = workload.mixed_ledger_transfers(N, L, P, seed=args.seed)
+            kinds = np.full(N, -1, dtype=np.int64)
+            src = kinds
+        nonzero = (base["id"][:, 0] != 0) | (base["id"][:, 1] != 0)
         steps = []
         for s in range(W + K):
-            if hazard_rate > 0:
-                t, kinds, src = workload.hazard_transfers(N, L, P, hazard_rate, seed=args.seed + s,
-                                                          id_offset=s * N)
-            else:
-                t, _ = workload.mixed_ledger_transfers(N, L, P, seed=args.seed + s,
-                                                       id_offset=s * N)
-                kinds = src = None
+            t = base.copy()
+            t["id"][nonzero, 0] += np.uint64(s * N)
             ts, prepare_ts = step_timestamps(prepare_ts, lens)
-            steps.append((dev.upload(t), dev.upload(ts), dev.alloc(N * 16), ts, kinds, src))
+            steps.append((dev.upload(t), dev.upload(ts), dev.alloc(N * 16), ts))
             del t
         dev.sync()
 
@@ -792,34 +796,27 @@ def group_measure(args, shards, devices, N1, K, W, hazard_rate=0.0):
         st = g.stats()
 
         ok = st["device_calls"] == W + K and st["engine_calls"] == 1  # (the accounts call)
-        exp_d = np.zeros(L * P, dtype=np.uint64)
-        exp_c = np.zeros(L * P, dtype=np.uint64)
         r = np.zeros(N, dtype=RESULT_DTYPE)
-        failed = 0
+        created = None
         for s in range(W + K):
-            _, _, d_res, ts, kinds, src = steps[s]
+            _, _, d_res, ts = steps[s]
             dev.download(d_res, r)
-            if hazard_rate > 0:
-                t, kinds, src = workload.hazard_transfers(N, L, P, hazard_rate, seed=args.seed + s,
-                                                          id_offset=s * N)
-            else:
-                t, _ = workload.mixed_ledger_transfers(N, L, P, seed=args.seed + s,
-                                                       id_offset=s * N)
-                kinds = np.full(N, -1, dtype=np.int64)
-                src = kinds
-            stamps = event_timestamps(lens, ts)
-            want_st, want_ts, created = workload.hazard_expected(t, kinds, src, stamps, L)
+            want_st, want_ts, created = workload.hazard_expected(
+                base, kinds, src, event_timestamps(lens, ts), L)
             ok &= bool((r["status"] == want_st).all() and (r["timestamp"] == want_ts).all() and
                        (r["reserved"] == 0).all())
-            failed += int((~created).sum())
-            amt = t["amount"][:, 0]
-            np.add.at(exp_d, t["debit_account_id"][created, 0].astype(np.int64) - 1, amt[created])
-            np.add.at(exp_c, t["credit_account_id"][created, 0].astype(np.int64) - 1, amt[created])
+        failed = int((~created).sum()) * (W + K)
+        amt = base["amount"][created, 0]
+        exp_d = np.zeros(L * P, dtype=np.uint64)
+        exp_c = np.zeros(L * P, dtype=np.uint64)
+        np.add.at(exp_d, base["debit_account_id"][created, 0].astype(np.int64) - 1, amt)
+        np.add.at(exp_c, base["credit_account_id"][created, 0].astype(np.int64) - 1, amt)
         rows = g.lookup_accounts(np.arange(1, L * P + 1))
         ok &= len(rows) == L * P
         if ok:
-            ok &= bool((rows["debits_posted"][:, 0] == exp_d).all() and
-                       (rows["credits_posted"][:, 0] == exp_c).all() and
+            reps = np.uint64(W + K)
+            ok &= bool((rows["debits_posted"][:, 0] == exp_d * reps).all() and
+                       (rows["credits_posted"][:, 0] == exp_c * reps).all() and
                        (rows["debits_posted"][:, 1] == 0).all() and
                        (rows["debits_pending"] == 0).all() and (rows["credits_pending"] == 0).all())
         return {

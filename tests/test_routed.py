@@ -171,7 +171,12 @@ def _calls(seed):
 
 
 @pytest.mark.gpu
-def test_group_routed_device_path():
+@pytest.mark.parametrize("transport", ["in-place", "copies"])
+def test_group_routed_device_path(transport, monkeypatch):
+    """`copies`: every shard's slice goes through its own buffers and hipMemcpyPeerAsync
+    (TBG_GROUP_COPY_SLICES), the transport of shards on other GPUs, here on one."""
+    if transport == "copies":
+        monkeypatch.setenv("TBG_GROUP_COPY_SLICES", "1")
     from hipmem import Hip
     from test_shard import OracleShard, assert_same_state
     from tigerbeetle_amd import native, shard
@@ -253,8 +258,8 @@ def _group_call(g, hip, t, lens, batch_ts):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("shards", [2, 3])
-def test_group_hazard_calls_on_device(shards):
+@pytest.mark.parametrize("shards,transport", [(2, "in-place"), (3, "in-place"), (3, "copies")])
+def test_group_hazard_calls_on_device(shards, transport, monkeypatch):
     """Calls of mixed-ledger transfers with injected failures across ledgers (bench.py's
     `hazard_call`: unknown accounts, cross-ledger accounts, id 0, reserved flags, posts of pending
     transfers found nowhere, exact repeats) stay on the device path: exact against the oracle and
@@ -263,6 +268,8 @@ def test_group_hazard_calls_on_device(shards):
     from test_shard import OracleShard
     from tigerbeetle_amd import native, shard, workload
     from tigerbeetle_amd.types import TIMESTAMP_MAX
+    if transport == "copies":
+        monkeypatch.setenv("TBG_GROUP_COPY_SLICES", "1")
     L, P, n = shards, 5_000, 200_000
     opts = [native.options(L * P, 1 << 20, n, pulse_next_timestamp_init=TIMESTAMP_MAX)
             for _ in range(shards)]

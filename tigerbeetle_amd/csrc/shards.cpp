@@ -15,6 +15,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -523,7 +524,9 @@ tbg_group* tbg_group_open(const tbg_group_options* options, const tbg_options* s
         g->shards[s] = tbg_open(&shard_options[s]);
         ok = g->shards[s] != nullptr;
         g->link[s].device = shard_options[s].device;
-        g->link[s].local = int(shard_options[s].device) == rdev;
+        // (TBG_GROUP_COPY_SLICES: every slice through its shard's own buffers and the peer copies,
+        // on one GPU too -- the transport the tests run on a one-GPU box)
+        g->link[s].local = int(shard_options[s].device) == rdev && !getenv("TBG_GROUP_COPY_SLICES");
     }
     if (ok && W > 1) {
         const uint64_t E = options->events_max;
