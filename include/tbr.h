@@ -75,6 +75,22 @@ int64_t tbr_route_device(tbr_ctx* ctx, const tb_transfer_t* d_events, uint32_t n
                          uint32_t n_batches, tb_transfer_t* d_out_events,
                          uint64_t* d_out_timestamps, uint32_t* d_out_positions,
                          uint32_t* shard_counts);
+/* A shard's slice of a routed call (device pointers, possibly in another GPU's HBM: the scatter
+ * stores and settle reads across xGMI, no staging copy): where its events and their global
+ * commit timestamps go, and where its executor writes their results. */
+typedef struct tbr_slice {
+    tb_transfer_t* events;
+    uint64_t* timestamps;
+    const tb_create_result_t* results;
+    uint64_t capacity; /* events the slice holds: a call that routes more to it returns -22 */
+} tbr_slice;
+/* tbr_route_device with every shard's slice at its own `slices[s]` (host array of `shards`
+ * entries); d_out_positions = each slice event's position in the call, in shard order. Settle with
+ * d_shard_results NULL (the results are read from the slices). */
+int64_t tbr_route_device_slices(tbr_ctx* ctx, const tb_transfer_t* d_events, uint32_t n,
+                                const uint32_t* d_batch_ends, const uint64_t* d_batch_timestamps,
+                                uint32_t n_batches, const tbr_slice* slices,
+                                uint32_t* d_out_positions, uint32_t* shard_counts);
 /* The routed call's results (in shard order) back to call order; records the ids that now exist
  * on their shard (created, or orphaned by a transient failure) and releases the others.
  * *created_timestamp_max (if not NULL) receives the largest timestamp of a created transfer (0 if

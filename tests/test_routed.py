@@ -171,12 +171,10 @@ def _calls(seed):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("transport", ["in-place", "copies"])
-def test_group_routed_device_path(transport, monkeypatch):
-    """`copies`: every shard's slice goes through its own buffers and hipMemcpyPeerAsync
-    (TBG_GROUP_COPY_SLICES), the transport of shards on other GPUs, here on one."""
-    if transport == "copies":
-        monkeypatch.setenv("TBG_GROUP_COPY_SLICES", "1")
+def test_group_routed_device_path():
+    """Every routed call's scatter stores each shard's slice into that shard's own buffers and
+    settle reads the results from there (tbr_route_device_slices) -- the transport shards on other
+    GPUs take (stores and loads across xGMI), here on one GPU."""
     from hipmem import Hip
     from test_shard import OracleShard, assert_same_state
     from tigerbeetle_amd import native, shard
@@ -258,8 +256,8 @@ def _group_call(g, hip, t, lens, batch_ts):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("shards,transport", [(2, "in-place"), (3, "in-place"), (3, "copies")])
-def test_group_hazard_calls_on_device(shards, transport, monkeypatch):
+@pytest.mark.parametrize("shards", [2, 3])
+def test_group_hazard_calls_on_device(shards):
     """Calls of mixed-ledger transfers with injected failures across ledgers (bench.py's
     `hazard_call`: unknown accounts, cross-ledger accounts, id 0, reserved flags, posts of pending
     transfers found nowhere, exact repeats) stay on the device path: exact against the oracle and
@@ -268,8 +266,6 @@ def test_group_hazard_calls_on_device(shards, transport, monkeypatch):
     from test_shard import OracleShard
     from tigerbeetle_amd import native, shard, workload
     from tigerbeetle_amd.types import TIMESTAMP_MAX
-    if transport == "copies":
-        monkeypatch.setenv("TBG_GROUP_COPY_SLICES", "1")
     L, P, n = shards, 5_000, 200_000
     opts = [native.options(L * P, 1 << 20, n, pulse_next_timestamp_init=TIMESTAMP_MAX)
             for _ in range(shards)]
@@ -335,3 +331,42 @@ def test_hazard_expected_closed_form():
         assert (kinds >= 0).sum() == n // 100 and created.sum() == n - n // 100
     finally:
         ref.close()
+
+
+@pytest.mark.gpu
+def test_group_slice_capacity():
+    """A call whose part for one shard exceeds that shard's batch_events_max fails with EINVAL
+    before anything is scattered (its id claims released); the group stays usable and exact."""
+    from hipmem import Hip
+    from test_shard import OracleShard
+    from tigerbeetle_amd import native, shard, workload
+    from tigerbeetle_amd.types import TIMESTAMP_MAX
+    opts = [native.options(4096, 1 << 16, 1000, pulse_next_timestamp_init=TIMESTAMP_MAX)
+            for _ in range(2)]
+    g = shard.Group.open_gpu(opts, ledgers=3, events_max=4000, router_transfer_capacity=1 << 16,
+                             router_account_capacity=4096)
+    ref = OracleShard()
+    hip = Hip(0)
+    try:
+        acc = workload.group_accounts(2, 500, seed=1)
+        for c in (g, ref):
+            c.create_accounts(acc, [len(acc)], [len(acc) + 1])
+        t, _ = workload.mixed_ledger_transfers(3000, 2, 500, seed=2, id_offset=10_000)
+        t["ledger"] = 2  # every event on ledger 2's shard: 3,000 > its 1,000
+        t["debit_account_id"][:, 0] = t["debit_account_id"][:, 0] % 500 + 1
+        t["credit_account_id"][:, 0] = (t["debit_account_id"][:, 0]) % 500 + 1
+        with pytest.raises(RuntimeError, match="-22"):
+            _group_call(g, hip, t, [3000], np.asarray([5000], np.uint64))
+        ok, _ = workload.mixed_ledger_transfers(1500, 2, 500, seed=3, id_offset=20_000)
+        got = _group_call(g, hip, ok, [1500], np.asarray([7000], np.uint64))
+        want = ref.create_transfers(ok, [1500], [7000])
+        assert got.tobytes() == want.tobytes()
+        # the refused call's ids were released: the same ids, resubmitted within limits, create
+        t2 = t[:900].copy()
+        got = _group_call(g, hip, t2, [900], np.asarray([9000], np.uint64))
+        want = ref.create_transfers(t2, [900], [9000])
+        assert got.tobytes() == want.tobytes() and (got["status"] == 0xFFFFFFFF).all()
+    finally:
+        g.close()
+        ref.close()
+        hip.free_all()

@@ -62,6 +62,15 @@ struct RouteArgs {
     uint64_t imported_floor;  // imported timestamps at or below it are hazards (tbr.h)
 };
 
+// A shard's slice: where the scatter writes its events and timestamps, where its executor writes
+// the results, and its first position in the call's shard-major order.
+struct SliceDst {
+    tb_transfer_t* events;
+    uint64_t* timestamps;
+    const tb_create_result_t* results;
+    uint64_t base;
+};
+
 __device__ inline uint64_t dir_find(const Dir& d, const tb_uint128_t& id) {
     const tb_uint128_t* ids = d.ids;
     const uint64_t s = probe_find(d.slots, id, [=](uint64_t r) { return ids[r]; });
@@ -164,6 +173,61 @@ __device__ inline const tb_transfer_t* stage_wave_events(const tb_transfer_t* ev
 //    when the whole call is imported (flags[3]; each shard's slice is one batch), their timestamps
 //    increase through the call and lie above every object of both grooves (the floor) and below
 //    their own commit timestamps.
+// The account directory's shard of two ids at once: both home slots load together, then both
+// candidates' ids (the common case resolves at home: load <= 0.25); a miss continues the probe.
+__device__ inline void dir_find2(const Dir& d, const tb_uint128_t& x, const tb_uint128_t& y,
+                                 uint64_t* rx, uint64_t* ry) {
+    const uint64_t sx = hash_id(x) & d.slots.mask, sy = hash_id(y) & d.slots.mask;
+    const uint64_t wx = d.slots.slots[sx], wy = d.slots.slots[sy];
+    const bool cx = slot_tag_is(wx, id_tag(x)), cy = slot_tag_is(wy, id_tag(y));
+    const uint64_t qx = (wx & kRefMask) - 1, qy = (wy & kRefMask) - 1;
+    tb_uint128_t ix{0, 0}, iy{0, 0};
+    if (cx) ix = d.ids[qx];
+    if (cy) iy = d.ids[qy];
+    const tb_uint128_t* ids = d.ids;
+    auto row_id = [=](uint64_t r) { return ids[r]; };
+    // (probe_find_from returns a slot: its row is the slot word's ref)
+    auto row_at = [&](uint64_t s) { return s == kNone ? kNone : (d.slots.slots[s] & kRefMask) - 1; };
+    if (cx && u128_eq(ix, x)) *rx = qx;
+    else if (wx == kEmpty) *rx = kNone;
+    else *rx = row_at(probe_find_from(d.slots, x, probe_next(sx, d.slots.mask), row_id));
+    if (cy && u128_eq(iy, y)) *ry = qy;
+    else if (wy == kEmpty) *ry = kNone;
+    else *ry = row_at(probe_find_from(d.slots, y, probe_next(sy, d.slots.mask), row_id));
+}
+
+// The id claim (device_common.hpp probe_claim) returning the slot and the ref it found there: the
+// call's own (base + k + 1) when the claim took an empty slot, else the holder's -- no reload of
+// the slot after the claim.
+template <typename RowId>
+__device__ inline uint64_t claim_ref(const IdTable& t, const tb_uint128_t& id, uint64_t ref,
+                                     uint64_t row_base, RowId row_id, uint64_t* found) {
+    const uint64_t tag = id_tag(id);
+    const uint64_t tref = ref | tag;
+    uint64_t s = hash_id(id) & t.mask;
+    uint64_t w = t.slots[s];
+    for (uint64_t n = 0; n < probe_limit(t.mask); n++) {
+        if (w == kEmpty) {
+            w = atomicCAS(&t.slots[s], (unsigned long long)kEmpty, (unsigned long long)tref);
+            if (w == kEmpty) {
+                *found = ref;
+                return s;
+            }
+        }
+        if (slot_tag_is(w, tag)) {
+            const uint64_t r = (w & kRefMask) - 1;
+            if (u128_eq(row_id(r), id)) {
+                if (r >= row_base && tref < w) atomicMin(&t.slots[s], (unsigned long long)tref);
+                *found = (w & kRefMask);
+                return s;
+            }
+        }
+        s = probe_next(s, t.mask);
+        w = t.slots[s];
+    }
+    return kNone;
+}
+
 __global__ void __launch_bounds__(kRouteBlock) tbr_pass1(RouteArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t lds_ev[kRouteBlock / 64][64 * kStageStride];
     const uint32_t k = blockIdx.x * kRouteBlock + threadIdx.x;
@@ -194,23 +258,24 @@ __global__ void __launch_bounds__(kRouteBlock) tbr_pass1(RouteArgs a) {
             const tb_transfer_t* ev = a.events;
             const tb_uint128_t* ids = a.tr.ids;
             const uint64_t base = a.base;
-            bool dup = false;
-            const uint64_t s = probe_claim(a.tr.slots, t.id, base + k + 1, base, [=](uint64_t r) {
+            // (the accounts' lookups are issued with the claim: neither waits on the other)
+            uint64_t rd = kNone, rc = kNone;
+            if (!post_void) dir_find2(a.acc, t.debit_account_id, t.credit_account_id, &rd, &rc);
+            uint64_t found = 0;
+            const uint64_t s = claim_ref(a.tr.slots, t.id, base + k + 1, base, [=](uint64_t r) {
                 return r >= base ? ev[r - base].id : ids[r];
-            }, &dup);
+            }, &found);
             if (s == kNone) {
-                atomicOr(&a.flags[1], 1u);
+                set_flag(&a.flags[1], 1u);
                 hazard = true;
             } else {
                 slot = uint32_t(s);
-                const uint64_t owner = (a.tr.slots.slots[s] & kRefMask) - 1;
+                const uint64_t owner = found - 1;
                 if (owner < base) {
                     shard = uint8_t(a.tr.shard[owner] & 0x7Fu);  // exists: decided on its holder
                 } else if (post_void) {
                     shard = kShardPending;
                 } else {
-                    const uint64_t rd = dir_find(a.acc, t.debit_account_id);
-                    const uint64_t rc = dir_find(a.acc, t.credit_account_id);
                     if (rd != kNone && rc != kNone && a.acc.shard[rd] != a.acc.shard[rc]) {
                         shard = kShardAny;
                         patch = cross_status(t);
@@ -368,6 +433,42 @@ __global__ void __launch_bounds__(kRouteBlock) tbr_pass_count(RouteArgs a) {
         a.block_counts[uint64_t(s) * a.nblocks + blockIdx.x] = cnt[s];
 }
 
+// Shard-major offsets of the scatter: workgroup s scans row s of the per-block counts (exclusive,
+// row-local; wave shuffles, one barrier pair per 1,024 counts) and writes the row's total -- the
+// host reads W totals, not W x blocks counts.
+constexpr uint32_t kScanThreads = 1024;
+__global__ void __launch_bounds__(kScanThreads) tbr_scan_counts(const uint32_t* counts,
+                                                                uint32_t nblocks,
+                                                                uint32_t* offsets,
+                                                                uint32_t* totals) {
+    __shared__ uint32_t wave_sum[kScanThreads / 64];
+    const uint32_t s = blockIdx.x, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t* row = counts + uint64_t(s) * nblocks;
+    uint32_t* out = offsets + uint64_t(s) * nblocks;
+    uint32_t carry = 0;
+    for (uint32_t b0 = 0; b0 < nblocks; b0 += kScanThreads) {
+        const uint32_t b = b0 + threadIdx.x;
+        const uint32_t v = b < nblocks ? row[b] : 0;
+        uint32_t x = v;  // inclusive scan within the wave
+        for (uint32_t off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(x, off, 64);
+            if (lane >= off) x += y;
+        }
+        if (lane == 63) wave_sum[wv] = x;
+        __syncthreads();
+        uint32_t before = carry, total = 0;
+        for (uint32_t w = 0; w < kScanThreads / 64; w++) {
+            const uint32_t t = wave_sum[w];
+            if (w < wv) before += t;
+            total += t;
+        }
+        if (b < nblocks) out[b] = before + x - v;
+        carry += total;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) totals[s] = carry;
+}
+
 // A call with a hazard takes nothing: its claims are released.
 __global__ void tbr_release(RouteArgs a) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
@@ -381,8 +482,8 @@ __global__ void tbr_release(RouteArgs a) {
 // Each event copied to its shard's slice with its global commit timestamp and its position (a
 // surrogate with its credit account replaced by its debit account); its shard into the store.
 __global__ void __launch_bounds__(kRouteBlock) tbr_pass2(RouteArgs a, const uint32_t* offsets,
-                                                         tb_transfer_t* out_events,
-                                                         uint64_t* out_ts, uint32_t* out_pos) {
+                                                         const SliceDst* dst_tab,
+                                                         uint32_t* out_pos) {
     __shared__ unsigned int wave_cnt[kRouteBlock / 64][kShardsMax];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t k = blockIdx.x * kRouteBlock + threadIdx.x;
@@ -399,9 +500,11 @@ __global__ void __launch_bounds__(kRouteBlock) tbr_pass2(RouteArgs a, const uint
     if (!active) return;
     uint32_t rank = my_rank;
     for (uint32_t w = 0; w < wv; w++) rank += wave_cnt[w][s];
+    // (the slice may live in another GPU's HBM: these stores cross xGMI, no staging copy)
+    const SliceDst d = dst_tab[s];
     const uint32_t pos = offsets[uint64_t(s) * a.nblocks + blockIdx.x] + rank;
     const uint4* src = reinterpret_cast<const uint4*>(&a.events[k]);
-    uint4* dst = reinterpret_cast<uint4*>(&out_events[pos]);
+    uint4* dst = reinterpret_cast<uint4*>(&d.events[pos]);
     uint4 q[8];
 #pragma unroll
     for (int i = 0; i < 8; i++) q[i] = src[i];
@@ -409,8 +512,8 @@ __global__ void __launch_bounds__(kRouteBlock) tbr_pass2(RouteArgs a, const uint
 #pragma unroll
     for (int i = 0; i < 8; i++) dst[i] = q[i];
     const uint32_t b = batch_of_guess(a.batch_ends, a.n_batches, a.n, k);
-    out_ts[pos] = a.batch_ts[b] - a.batch_ends[b] + k + 1;
-    out_pos[pos] = k;
+    d.timestamps[pos] = a.batch_ts[b] - a.batch_ends[b] + k + 1;
+    out_pos[d.base + pos] = k;
     a.tr.shard[a.base + k] = uint8_t(s);
 }
 
@@ -420,17 +523,23 @@ __global__ void __launch_bounds__(kRouteBlock) tbr_pass2(RouteArgs a, const uint
 // The largest timestamp of a created transfer goes to key_max (the transfers objects tree's
 // key_range.key_max, which the imported floor follows): a maximum per workgroup in block_max,
 // reduced by tbr_settle_release's first workgroup.
-__global__ void __launch_bounds__(kRouteBlock) tbr_settle(RouteArgs a,
-                                                          const tb_create_result_t* shard_res,
+__global__ void __launch_bounds__(kRouteBlock) tbr_settle(RouteArgs a, const SliceDst* dst_tab,
                                                           const uint32_t* pos,
                                                           tb_create_result_t* results,
                                                           unsigned long long* block_max) {
     __shared__ uint64_t wave_max[kRouteBlock / 64];
+    __shared__ uint32_t bases[kShardsMax + 1];
+    for (uint32_t s = threadIdx.x; s < a.shards; s += kRouteBlock) bases[s] = dst_tab[s].base;
+    if (threadIdx.x == 0) bases[a.shards] = a.n;
+    __syncthreads();
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     uint64_t ts_max = 0;
     if (j < a.n) {
+        uint32_t s = 0;  // (the shard whose slice holds position j: bases ascend)
+        while (bases[s + 1] <= j) s++;
         const uint32_t k = pos[j];
-        tb_create_result_t r = shard_res[j];
+        // (the results may live in the shard's GPU: read across xGMI)
+        tb_create_result_t r = dst_tab[s].results[j - bases[s]];
         if (a.ev_patch[k] && r.status == TB_CT_ACCOUNTS_MUST_BE_DIFFERENT) r.status = a.ev_patch[k];
         results[k] = r;
         const bool created = r.status == TB_STATUS_CREATED;
@@ -506,6 +615,9 @@ struct tbr_ctx {
     unsigned int* flags = nullptr;
     unsigned long long* key_max = nullptr;  // settle: created timestamps' maximum
     unsigned long long* block_max = nullptr;  // ... per settle workgroup
+    uint32_t* totals = nullptr;               // per shard: the routed call's events
+    SliceDst* d_tab = nullptr;                // the routed call's slices (device copy of tab)
+    std::vector<SliceDst> tab;
     uint64_t imported_floor = ~0ull;        // tbr_set_imported_floor (none yet: every import)
     tb_uint128_t* q_ids = nullptr;  // lookup / record staging (events_max)
     int32_t* q_out = nullptr;
@@ -584,6 +696,76 @@ int64_t lookup(tbr_ctx* r, const Dir& d, const tb_uint128_t* ids, uint32_t n, in
 
 }  // namespace
 
+namespace {
+
+// The device path of one call (tbr_route_device / _slices): the placement passes, the offsets
+// scanned on the device (the host reads the W totals with the flags: one synchronisation), the
+// slice table (a shard's events / timestamps at `slices`, or contiguous in shard order at c_ev /
+// c_ts) uploaded, the scatter.
+int64_t route_impl(tbr_ctx* r, const tb_transfer_t* d_events, uint32_t n,
+                   const uint32_t* d_batch_ends, const uint64_t* d_batch_ts, uint32_t n_batches,
+                   const tbr_slice* slices, tb_transfer_t* c_ev, uint64_t* c_ts,
+                   uint32_t* d_out_pos, uint32_t* shard_counts) {
+    if (!r || r->pending || n > r->events_max || n_batches == 0) return -22;
+    if (r->tr_used + n > r->tr_cap) return -28;
+    RouteArgs a = route_args(r, d_events, n, d_batch_ends, d_batch_ts, n_batches);
+    const dim3 grid(a.nblocks), block(kRouteBlock);
+    const uint32_t W = r->shards;
+    if (hipMemsetAsync(r->flags, 0, 32, r->stream)) return -5;
+    hipLaunchKernelGGL(tbr_pass1, grid, block, 0, r->stream, a);
+    hipLaunchKernelGGL(tbr_pass_pv, grid, block, 0, r->stream, a);
+    hipLaunchKernelGGL(tbr_pass_dup, grid, block, 0, r->stream, a);
+    hipLaunchKernelGGL(tbr_pass_chains, grid, block, 0, r->stream, a);
+    hipLaunchKernelGGL(tbr_pass_count, grid, block, 0, r->stream, a);
+    hipLaunchKernelGGL(tbr_scan_counts, dim3(W), dim3(kScanThreads), 0, r->stream,
+                       r->block_counts, a.nblocks, r->offsets, r->totals);
+    unsigned int f[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    std::vector<uint32_t> totals(W);
+    if (hipMemcpyAsync(f, r->flags, 32, hipMemcpyDeviceToHost, r->stream) ||
+        hipMemcpyAsync(totals.data(), r->totals, size_t(W) * 4, hipMemcpyDeviceToHost,
+                       r->stream) ||
+        hipStreamSynchronize(r->stream))
+        return -5;
+    if (f[3] == 3u) f[0] = 1;  // imported and non-imported events in one call
+    r->route_stats[0] = f[4];
+    r->route_stats[1] = f[5];
+    r->route_stats[2] = f[6];
+    bool over = false;  // (a slice too small for its part: nothing is scattered)
+    for (uint32_t s = 0; s < W && slices; s++) over |= totals[s] > slices[s].capacity;
+    if (f[0] || f[1] || over) {
+        hipLaunchKernelGGL(tbr_release, grid, block, 0, r->stream, a);
+        if (hipStreamSynchronize(r->stream)) return -5;
+        return f[1] ? -28 : (over && !f[0]) ? -22 : 1;
+    }
+    uint64_t base = 0;
+    for (uint32_t s = 0; s < W; s++) {
+        SliceDst& d = r->tab[s];
+        d.base = base;
+        if (slices) {
+            d.events = slices[s].events;
+            d.timestamps = slices[s].timestamps;
+            d.results = slices[s].results;
+        } else {
+            d.events = c_ev + base;
+            d.timestamps = c_ts + base;
+            d.results = nullptr;  // (tbr_settle_device's d_shard_results)
+        }
+        shard_counts[s] = totals[s];
+        base += totals[s];
+    }
+    if (hipMemcpyAsync(r->d_tab, r->tab.data(), sizeof(SliceDst) * W, hipMemcpyHostToDevice,
+                       r->stream))
+        return -5;
+    hipLaunchKernelGGL(tbr_pass2, grid, block, 0, r->stream, a, r->offsets, r->d_tab, d_out_pos);
+    if (hipGetLastError() || hipStreamSynchronize(r->stream)) return -5;
+    r->pending = true;
+    r->call_base = a.base;
+    r->call_n = n;
+    return f[2] ? 2 : 0;
+}
+
+}  // namespace
+
 extern "C" {
 
 tbr_ctx* tbr_open(uint32_t shards, uint64_t account_capacity, uint64_t transfer_capacity,
@@ -595,6 +777,7 @@ tbr_ctx* tbr_open(uint32_t shards, uint64_t account_capacity, uint64_t transfer_
     tbr_ctx* r = new tbr_ctx();
     r->shards = shards;
     r->events_max = events_max;
+    r->tab.assign(shards, SliceDst{nullptr, nullptr, nullptr, 0});
     r->acc_cap = account_capacity;
     r->tr_cap = transfer_capacity;
     const uint64_t acc_slots = std::max<uint64_t>(next_pow2(account_capacity * 4), 64);
@@ -617,6 +800,7 @@ tbr_ctx* tbr_open(uint32_t shards, uint64_t account_capacity, uint64_t transfer_
          alloc(&r->offsets, uint64_t(shards) * nblocks, false, r->stream) &&
          alloc(&r->flags, 8, true, r->stream) && alloc(&r->key_max, 1, true, r->stream) &&
          alloc(&r->block_max, nblocks, true, r->stream) &&
+         alloc(&r->totals, shards, true, r->stream) && alloc(&r->d_tab, shards, true, r->stream) &&
          alloc(&r->q_ids, events_max, false, r->stream) &&
          alloc(&r->q_out, events_max, false, r->stream);
     ok = ok && hipStreamSynchronize(r->stream) == hipSuccess;
@@ -635,7 +819,7 @@ void tbr_close(tbr_ctx* r) {
     if (r->stream) (void)hipStreamSynchronize(r->stream);
     void* ptrs[] = {r->acc.slots.slots, r->acc.ids, r->acc.shard, r->tr.slots.slots, r->tr.ids,
                     r->tr.shard, r->ev_shard, r->ev_slot, r->ev_patch, r->ev_keep, r->ev_link, r->ev_owner, r->block_counts, r->offsets, r->flags,
-                    r->key_max, r->block_max, r->q_ids, r->q_out};
+                    r->key_max, r->block_max, r->totals, r->d_tab, r->q_ids, r->q_out};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (r->stream) (void)hipStreamDestroy(r->stream);
@@ -666,53 +850,17 @@ int64_t tbr_route_device(tbr_ctx* r, const tb_transfer_t* d_events, uint32_t n,
                          const uint32_t* d_batch_ends, const uint64_t* d_batch_ts,
                          uint32_t n_batches, tb_transfer_t* d_out_events, uint64_t* d_out_ts,
                          uint32_t* d_out_pos, uint32_t* shard_counts) {
-    if (!r || r->pending || n > r->events_max || n_batches == 0) return -22;
-    if (r->tr_used + n > r->tr_cap) return -28;
-    RouteArgs a = route_args(r, d_events, n, d_batch_ends, d_batch_ts, n_batches);
-    const dim3 grid(a.nblocks), block(kRouteBlock);
-    if (hipMemsetAsync(r->flags, 0, 32, r->stream)) return -5;
-    hipLaunchKernelGGL(tbr_pass1, grid, block, 0, r->stream, a);
-    hipLaunchKernelGGL(tbr_pass_pv, grid, block, 0, r->stream, a);
-    hipLaunchKernelGGL(tbr_pass_dup, grid, block, 0, r->stream, a);
-    hipLaunchKernelGGL(tbr_pass_chains, grid, block, 0, r->stream, a);
-    hipLaunchKernelGGL(tbr_pass_count, grid, block, 0, r->stream, a);
-    std::vector<uint32_t> counts(uint64_t(r->shards) * a.nblocks);
-    unsigned int f[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (hipMemcpyAsync(f, r->flags, 32, hipMemcpyDeviceToHost, r->stream) ||
-        hipMemcpyAsync(counts.data(), r->block_counts, counts.size() * 4, hipMemcpyDeviceToHost,
-                       r->stream) ||
-        hipStreamSynchronize(r->stream))
-        return -5;
-    if (f[3] == 3u) f[0] = 1;  // imported and non-imported events in one call
-    r->route_stats[0] = f[4];
-    r->route_stats[1] = f[5];
-    r->route_stats[2] = f[6];
-    if (f[0] || f[1]) {
-        hipLaunchKernelGGL(tbr_release, grid, block, 0, r->stream, a);
-        if (hipStreamSynchronize(r->stream)) return -5;
-        return f[1] ? -28 : 1;
-    }
-    // per-block offsets: shard-major exclusive sums
-    uint32_t run = 0;
-    for (uint32_t s = 0; s < r->shards; s++) {
-        const uint32_t start = run;
-        for (uint32_t b = 0; b < a.nblocks; b++) {
-            const uint32_t c = counts[uint64_t(s) * a.nblocks + b];
-            counts[uint64_t(s) * a.nblocks + b] = run;
-            run += c;
-        }
-        shard_counts[s] = run - start;
-    }
-    if (hipMemcpyAsync(r->offsets, counts.data(), counts.size() * 4, hipMemcpyHostToDevice,
-                       r->stream))
-        return -5;
-    hipLaunchKernelGGL(tbr_pass2, grid, block, 0, r->stream, a, r->offsets, d_out_events,
-                       d_out_ts, d_out_pos);
-    if (hipGetLastError() || hipStreamSynchronize(r->stream)) return -5;
-    r->pending = true;
-    r->call_base = a.base;
-    r->call_n = n;
-    return f[2] ? 2 : 0;
+    return route_impl(r, d_events, n, d_batch_ends, d_batch_ts, n_batches, nullptr, d_out_events,
+                      d_out_ts, d_out_pos, shard_counts);
+}
+
+int64_t tbr_route_device_slices(tbr_ctx* r, const tb_transfer_t* d_events, uint32_t n,
+                                const uint32_t* d_batch_ends, const uint64_t* d_batch_ts,
+                                uint32_t n_batches, const tbr_slice* slices,
+                                uint32_t* d_out_pos, uint32_t* shard_counts) {
+    if (!slices) return -22;
+    return route_impl(r, d_events, n, d_batch_ends, d_batch_ts, n_batches, slices, nullptr,
+                      nullptr, d_out_pos, shard_counts);
 }
 
 int tbr_route_stats(tbr_ctx* r, uint64_t* out) {
@@ -735,7 +883,16 @@ int tbr_settle_device(tbr_ctx* r, const tb_create_result_t* d_shard_results,
     a.base = r->call_base;
     unsigned long long km = 0;
     const uint32_t nb = (n + kRouteBlock - 1) / kRouteBlock;
-    hipLaunchKernelGGL(tbr_settle, dim3(nb), dim3(kRouteBlock), 0, r->stream, a, d_shard_results,
+    if (d_shard_results) {  // (contiguous results in shard order, else the routed slices')
+        for (uint32_t s = 0; s < r->shards; s++) r->tab[s].results = d_shard_results + r->tab[s].base;
+        if (hipMemcpyAsync(r->d_tab, r->tab.data(), sizeof(SliceDst) * r->shards,
+                           hipMemcpyHostToDevice, r->stream))
+            return -5;
+    }
+    for (uint32_t s = 0; s < r->shards; s++)
+        if (!r->tab[s].results && r->tab[s].base < (s + 1 < r->shards ? r->tab[s + 1].base : n))
+            return -22;
+    hipLaunchKernelGGL(tbr_settle, dim3(nb), dim3(kRouteBlock), 0, r->stream, a, r->d_tab,
                        d_positions, d_results, r->block_max);
     hipLaunchKernelGGL(tbr_settle_release, dim3(nb), dim3(kRouteBlock), 0, r->stream, a,
                        r->block_max, nb, r->key_max);

@@ -6,9 +6,9 @@
 // out), the exact engine's sub-calls of a segment. Everything else runs on the caller's thread
 // (every tbg_* entry point makes its executor's device current).
 //
-// Transport: slices are scattered on the router's GPU (tbr_pass2) and copied to each shard's GPU
-// with hipMemcpyPeerAsync (xGMI; peer access enabled at open); a shard on the router's GPU reads
-// its slice in place. Results come back the same way and settle in call order on the router's GPU.
+// Transport: the router's scatter (tbr_pass2) stores each shard's slice straight into that shard's
+// buffers in its own GPU's HBM (stores across xGMI; peer access enabled at open), and settle reads
+// the results the shard's executor wrote there: no staging copy and no DMA-engine hand-off.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -167,11 +167,10 @@ tbg_shard_ops tbg_ops() {
     return o;
 }
 
-// A shard's transport buffers on its own GPU (none when it shares the router's).
+// A shard's slice buffers, in its own GPU's HBM.
 struct ShardLink {
     uint32_t device = 0;
-    bool local = true;
-    hipStream_t stream = nullptr;
+    uint64_t cap = 0;  // events its slice holds (its executor's batch_events_max)
     tb_transfer_t* ev = nullptr;
     uint64_t* ts = nullptr;
     tb_create_result_t* res = nullptr;
@@ -215,10 +214,7 @@ struct tbg_group {
     uint32_t* d_in_ends = nullptr;
     uint64_t* d_in_ts = nullptr;
     tb_create_result_t* d_in_res = nullptr;
-    tb_transfer_t* d_slices = nullptr;  // the scatter (router GPU)
-    uint64_t* d_slice_ts = nullptr;
-    uint32_t* d_pos = nullptr;
-    tb_create_result_t* d_slice_res = nullptr;
+    uint32_t* d_pos = nullptr;  // the scatter's positions (router GPU)
     uint64_t floor = ~0ull;  // the imported floor (unknown until an engine call)
     bool floor_known = false;
 };
@@ -270,45 +266,29 @@ int route_device(tbg_group* g, const tb_transfer_t* d_ev, uint32_t n, const uint
                  const uint64_t* d_ts, uint32_t nb, tb_create_result_t* d_res) {
     const uint32_t W = g->o.shards;
     std::vector<uint32_t> counts(W, 0);
+    std::vector<tbr_slice> slices(W);
+    for (uint32_t s = 0; s < W; s++)
+        slices[s] = tbr_slice{g->link[s].ev, g->link[s].ts, g->link[s].res, g->link[s].cap};
     const uint64_t t0 = now_ns();
-    const int64_t mode = tbr_route_device(g->tbr, d_ev, n, d_ends, d_ts, nb, g->d_slices,
-                                          g->d_slice_ts, g->d_pos, counts.data());
+    const int64_t mode = tbr_route_device_slices(g->tbr, d_ev, n, d_ends, d_ts, nb, slices.data(),
+                                                 g->d_pos, counts.data());
+    if (mode == TBG_EINVAL)
+        return fail(g, TBG_EINVAL, "a shard's part of the call exceeds its batch_events_max");
     if (mode < 0) return fail(g, int(mode), "tbr_route_device");
     if (mode == 1) return 1;
-    std::vector<uint64_t> off(W + 1, 0);
-    for (uint32_t s = 0; s < W; s++) off[s + 1] = off[s] + counts[s];
     std::vector<int> run;
     for (uint32_t s = 0; s < W; s++)
         if (counts[s]) run.push_back(int(s));
-    const int rdev = int(g->o.router_device);
     std::vector<int> rcs;
     const uint64_t t1 = now_ns();
     g->st.route_ns += t1 - t0;
     g->runner->run(run, [&](int s) -> int {
         const ShardLink& L = g->link[s];
-        const uint64_t a = off[s], c = counts[s];
-        const tb_transfer_t* ev = g->d_slices + a;
-        const uint64_t* ts = g->d_slice_ts + a;
-        tb_create_result_t* res = g->d_slice_res + a;
-        if (!L.local) {
-            if (hipMemcpyPeerAsync(L.ev, int(L.device), ev, rdev, c * 128, L.stream) ||
-                hipMemcpyPeerAsync(L.ts, int(L.device), ts, rdev, c * 8, L.stream) ||
-                hipStreamSynchronize(L.stream))
-                return TBG_EHIP;
-            ev = L.ev;
-            ts = L.ts;
-            res = L.res;
-        }
-        int rc = tbg_create_transfers_stamped_device(static_cast<tbg_ctx*>(g->shards[s]), ev,
-                                                     uint32_t(c), ts, res, nullptr);
+        int rc = tbg_create_transfers_stamped_device(static_cast<tbg_ctx*>(g->shards[s]), L.ev,
+                                                     counts[s], L.ts, L.res, nullptr);
         // (the executor may leave AccountEvents appends reading the slice behind the call)
         if (rc == 0) rc = tbg_synchronize(static_cast<tbg_ctx*>(g->shards[s]));
-        if (rc != 0) return rc;
-        if (!L.local &&
-            (hipMemcpyPeerAsync(g->d_slice_res + a, rdev, L.res, int(L.device), c * 16, L.stream) ||
-             hipStreamSynchronize(L.stream)))
-            return TBG_EHIP;
-        return 0;
+        return rc;
     }, rcs);
     for (size_t i = 0; i < rcs.size(); i++)
         if (rcs[i] != 0)
@@ -318,7 +298,7 @@ int route_device(tbg_group* g, const tb_transfer_t* d_ev, uint32_t n, const uint
     const uint64_t t2 = now_ns();
     g->st.execute_ns += t2 - t1;
     uint64_t km = 0;
-    const int rc = tbr_settle_device(g->tbr, g->d_slice_res, g->d_pos, n, d_res, &km);
+    const int rc = tbr_settle_device(g->tbr, nullptr, g->d_pos, n, d_res, &km);
     if (rc != 0) return fail(g, rc, "tbr_settle_device");
     if (g->floor_known) {
         g->floor = std::max(g->floor, km);
@@ -369,13 +349,11 @@ void destroy(tbg_group* g) {
         DeviceScope ds(int(g->o.router_device));
         for (ShardLink& L : g->link) {
             DeviceScope d2(int(L.device));
-            if (L.stream) (void)hipStreamDestroy(L.stream);
             void* ptrs[] = {L.ev, L.ts, L.res};
             for (void* p : ptrs)
                 if (p) (void)hipFree(p);
         }
-        void* ptrs[] = {g->d_in_ev, g->d_in_ends, g->d_in_ts, g->d_in_res, g->d_slices,
-                        g->d_slice_ts, g->d_pos, g->d_slice_res};
+        void* ptrs[] = {g->d_in_ev, g->d_in_ends, g->d_in_ts, g->d_in_res, g->d_pos};
         {
             DeviceScope d3(int(g->o.router_device));
             for (void* p : ptrs)
@@ -524,9 +502,6 @@ tbg_group* tbg_group_open(const tbg_group_options* options, const tbg_options* s
         g->shards[s] = tbg_open(&shard_options[s]);
         ok = g->shards[s] != nullptr;
         g->link[s].device = shard_options[s].device;
-        // (TBG_GROUP_COPY_SLICES: every slice through its shard's own buffers and the peer copies,
-        // on one GPU too -- the transport the tests run on a one-GPU box)
-        g->link[s].local = int(shard_options[s].device) == rdev && !getenv("TBG_GROUP_COPY_SLICES");
     }
     if (ok && W > 1) {
         const uint64_t E = options->events_max;
@@ -534,20 +509,23 @@ tbg_group* tbg_group_open(const tbg_group_options* options, const tbg_options* s
         g->tbr = tbr_open(W, options->router_account_capacity, options->router_transfer_capacity,
                           options->events_max, uint32_t(rdev));
         ok = g->tbr && dalloc(&g->d_in_ev, E) && dalloc(&g->d_in_ends, E) &&
-             dalloc(&g->d_in_ts, E) && dalloc(&g->d_in_res, E) && dalloc(&g->d_slices, E) &&
-             dalloc(&g->d_slice_ts, E) && dalloc(&g->d_pos, E) && dalloc(&g->d_slice_res, E);
+             dalloc(&g->d_in_ts, E) && dalloc(&g->d_in_res, E) && dalloc(&g->d_pos, E);
         for (uint32_t s = 0; s < W && ok; s++) {
             ShardLink& L = g->link[s];
-            if (L.local) continue;
-            {
-                DeviceScope d2(rdev);
-                (void)hipDeviceEnablePeerAccess(int(L.device), 0);  // (already enabled: fine)
+            // a shard's slice can hold the whole call (every event may go to one shard)
+            const uint64_t cap = std::min<uint64_t>(E, shard_options[s].batch_events_max);
+            L.cap = cap;
+            if (int(L.device) != rdev) {
+                {
+                    DeviceScope d2(rdev);  // (the router's kernels store and load there)
+                    (void)hipDeviceEnablePeerAccess(int(L.device), 0);  // (already enabled: fine)
+                }
+                DeviceScope d3(int(L.device));
+                (void)hipDeviceEnablePeerAccess(rdev, 0);
+                (void)hipGetLastError();
             }
-            DeviceScope d3(int(L.device));
-            (void)hipDeviceEnablePeerAccess(rdev, 0);
-            (void)hipGetLastError();
-            ok = hipStreamCreateWithFlags(&L.stream, hipStreamNonBlocking) == hipSuccess &&
-                 dalloc(&L.ev, E) && dalloc(&L.ts, E) && dalloc(&L.res, E);
+            DeviceScope d4(int(L.device));
+            ok = dalloc(&L.ev, cap) && dalloc(&L.ts, cap) && dalloc(&L.res, cap);
         }
         (void)hipGetLastError();
     }

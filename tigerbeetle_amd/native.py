@@ -160,6 +160,8 @@ SIGNATURES = [
     ("tbr_settle_device", ctypes.c_int, [vp, vp, vp, ctypes.c_uint32, vp, c_u64p]),
     ("tbr_set_imported_floor", ctypes.c_int, [vp, ctypes.c_uint64]),
     ("tbr_route_stats", ctypes.c_int, [vp, c_u64p]),
+    ("tbr_route_device_slices", ctypes.c_int64, [vp, vp, ctypes.c_uint32, vp, vp, ctypes.c_uint32,
+                                                 vp, vp, vp]),
     ("tbg_group_open", vp, [vp, vp]),
     ("tbg_group_open_shards", vp, [vp, vp, vp]),
     ("tbg_group_close", None, [vp]),
