@@ -1061,7 +1061,10 @@ __device__ inline uint4 ae_sub_u32(uint4 balance, uint32_t d) {
 // at a time paid a full load latency per four records). (ae_window_emit / ae_wide_emit, 1024 lanes
 // at most 128 registers each, keep their loop over the batches rolled: ae_window_emit 722 -> 683 us
 // per 10M events.)
-constexpr uint32_t kAeRecBatch = 4;
+#ifndef TBG_AE_REC_BATCH
+#define TBG_AE_REC_BATCH 4
+#endif
+constexpr uint32_t kAeRecBatch = TBG_AE_REC_BATCH;
 
 // The end of a one-pass emit's workgroup (slice w; every thread calls it): the slice's first and
 // last created timestamps (ts_lds: LDS words set to ~0 / 0 before a barrier); the last workgroup to

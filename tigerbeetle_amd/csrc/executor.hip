@@ -828,12 +828,13 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
                                ctx->stream, ctx->T, c, L, F.mb_index,
                                dbg ? ctx->flow_debug : nullptr);
             if (dbg) {
-                unsigned long long d[8] = {};
-                (void)hipMemcpyAsync(d, ctx->flow_debug, 64, hipMemcpyDeviceToHost, ctx->stream);
+                unsigned long long d[16] = {};
+                (void)hipMemcpyAsync(d, ctx->flow_debug, 128, hipMemcpyDeviceToHost, ctx->stream);
                 (void)hipStreamSynchronize(ctx->stream);
                 fprintf(stderr, "walk: m=%u walks=%llu windows=%llu events=%llu polls=%llu "
-                        "poll_us=%.1f snapshot_hits=%llu longest_walk_us=%.1f\n", m, d[6], d[0],
-                        d[1], d[2], d[3] / 100.0, d[5], d[4] / 100.0);
+                        "poll_us=%.1f snapshot_hits=%llu longest_walk_us=%.1f refreshes=%llu "
+                        "refresh_us=%.1f window_head_us=%.1f\n", m, d[6], d[0], d[1], d[2],
+                        d[3] / 100.0, d[5], d[4] / 100.0, d[7], d[8] / 100.0, d[9] / 100.0);
                 std::vector<unsigned long long> o(8 * 1000);
                 (void)hipMemcpy(o.data(), ctx->flow_debug + 16, o.size() * 8, hipMemcpyDeviceToHost);
                 std::vector<uint32_t> idx;
@@ -843,9 +844,14 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
                           [&](uint32_t a, uint32_t b) { return o[8 * a] > o[8 * b]; });
                 for (size_t i = 0; i < idx.size() && i < 3; i++) {
                     const unsigned long long* w = &o[8 * idx[i]];
+                    const unsigned long long lo24 = (1ull << 24) - 1;
                     fprintf(stderr, "  owner %u: events=%llu windows=%llu all_pass=%llu iters=%llu "
-                            "polls=%llu poll_us=%.1f walk_us=%.1f\n", idx[i], w[0], w[4], w[6],
-                            w[5], w[1], w[2] / 100.0, w[3] / 100.0);
+                            "polls=%llu poll_us=%.1f walk_us=%.1f refreshes=%llu refresh_us=%.1f "
+                            "head_us=%.1f window_us=%.1f stepB_us=%.1f tail_us=%.1f\n",
+                            idx[i], w[0], w[4] & lo24, w[6] & lo24, w[5] & lo24, w[1] & lo24,
+                            w[2] / 100.0, w[3] / 100.0, w[7] >> 32, (w[7] & 0xFFFFFFFFull) / 100.0,
+                            (w[4] >> 24) / 100.0, (w[1] >> 24) / 100.0, (w[5] >> 24) / 100.0,
+                            (w[6] >> 24) / 100.0);
                 }
             }
         }
@@ -967,7 +973,7 @@ int run_replay(tbg_ctx* ctx, Call<Event>& c, bool is_transfers, bool finalize_ev
     int rc = selected ? 0 : select_flagged(ctx, ctx->ev_slow, c.n, ctx->slow_list,
                                           &ctx->d_scalars->slow_count);
     if (rc) return rc;
-    tmark(ctx, "select_replay_list");
+    if (!selected) tmark(ctx, "select_replay_list");
     const unsigned int call_flags = ctx->h_scalars->flags;
     const uint64_t m = ctx->h_scalars->stats[0];
     if constexpr (__is_same(Event, tb_transfer_t)) {
@@ -2255,7 +2261,10 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
         dst = mapped(ctx, ctx->early_dst, uint64_t(n) * 16);
         if (!dst) dst = ctx->dh_results;
     }
-    const bool spin = ctx->spin_sync && !ctx->timing;
+    // (timed calls wait as untimed ones do: a stream synchronisation's slower wake-up, ~70 us, was
+    // counted into the next mark's span -- the flow plan's -- with the GPU idle; end_call still
+    // synchronises the stream before the marks are read)
+    const bool spin = ctx->spin_sync;
     const unsigned int seq = spin ? (++ctx->seq ? ctx->seq : ++ctx->seq) : 0u;
     // A small device-buffer call without balance items may end in its last tr_ingest workgroup
     // (Call::finish_done); tr_commit and stage_out are queued all the same and return at once then
@@ -2389,9 +2398,11 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
             ctx->ae_def_call = true;
         }
         ctx->ae_snap_early = snap && !rc;
+        // (the mark before the wait: recorded after it, on an idle GPU, its host cost delayed the
+        // replay's first launch and was counted into the flow plan's span)
+        tmark(ctx, "host_sync");
         if (!rc) rc = spin ? spin_wait(ctx, seq)
                            : (hip_ok(ctx, hipStreamSynchronize(ctx->stream), "sync") ? 0 : TBG_EHIP);
-        tmark(ctx, "host_sync");
     }
     const bool replay = !rc && ctx->h_scalars->stats[0] > 0;
     if (!rc && n > kInlineChunkMax) {
@@ -2920,7 +2931,7 @@ int64_t tbg_pulse(tbg_ctx* ctx, uint64_t timestamp) {
     if (ae_async) ae_defer_graph(ctx, upper, ae_epoch, true);
     // (the host spins on a pinned word, as a call's end does: a stream synchronisation's wake-up
     // is the slower path)
-    if (ctx->spin_sync && !ctx->timing) {
+    if (ctx->spin_sync) {
         const unsigned int seq = ++ctx->seq ? ctx->seq : ++ctx->seq;
         hipLaunchKernelGGL(host_signal, dim3(1), dim3(64), 0, ctx->stream, ctx->dh_seq, seq);
         HIP_TRY(ctx, hipGetLastError());
@@ -2936,6 +2947,7 @@ int64_t tbg_pulse(tbg_ctx* ctx, uint64_t timestamp) {
                 (ht[4] - ht[3]) * 1e3);
     }
     tmark(ctx, "pulse:report");
+    if (ctx->timing) (void)hipStreamSynchronize(ctx->stream);  // (the marks complete)
     tcollect(ctx);
     ctx->expiry_host = ctx->h_pulse[1];
     ctx->expiry_known = true;

@@ -345,18 +345,37 @@ __device__ inline u128 walk_uniform128(const tb_uint128_t& x) {
     return (u128(walk_uniform64(x.hi)) << 64) | walk_uniform64(x.lo);
 }
 // The window sums of lanes_walk in u64 (narrow owners and amounts) or u128 (wide ones).
-__device__ inline uint64_t walk_uniform_v(uint64_t v) { return walk_uniform64(v); }
-__device__ inline u128 walk_uniform_v(u128 v) {
-    return (u128(walk_uniform64(uint64_t(v >> 64))) << 64) | walk_uniform64(uint64_t(v));
+// Wave sums on DPP (with every lane active): an inclusive scan within each row of 16 lanes (row
+// shifts 1, 2, 4, 8), then the row broadcasts 15 and 31 carry the rows' totals up, and lane 63 holds
+// the sum -- six dependent VALU steps. (A __shfl_xor butterfly is an LDS permute round trip per
+// step: the walk's per-window sums took ~0.4 us each on it.)
+template <int kCtrl, int kRowMask>
+__device__ inline uint32_t walk_dpp(uint32_t v) {
+    return uint32_t(__builtin_amdgcn_update_dpp(0, int(v), kCtrl, kRowMask, 0xF, true));
 }
-__device__ inline uint64_t walk_shfl_xor(uint64_t v, int off) { return __shfl_xor(v, off); }
-__device__ inline u128 walk_shfl_xor(u128 v, int off) {
-    return (u128(__shfl_xor(uint64_t(v >> 64), off)) << 64) | __shfl_xor(uint64_t(v), off);
+template <int kCtrl, int kRowMask>
+__device__ inline void walk_dpp_add(uint64_t& v) {
+    const uint32_t lo = walk_dpp<kCtrl, kRowMask>(uint32_t(v));
+    const uint32_t hi = walk_dpp<kCtrl, kRowMask>(uint32_t(v >> 32));
+    v += walk_u64(lo, hi);
 }
-template <typename V>
-__device__ inline V walk_wave_sum(V v) {
-    for (int off = 32; off > 0; off >>= 1) v += walk_shfl_xor(v, off);
-    return walk_uniform_v(v);
+__device__ inline uint64_t walk_dpp_sum64(uint64_t v) {
+    walk_dpp_add<0x111, 0xF>(v);  // row_shr:1
+    walk_dpp_add<0x112, 0xF>(v);  // row_shr:2
+    walk_dpp_add<0x114, 0xF>(v);  // row_shr:4
+    walk_dpp_add<0x118, 0xF>(v);  // row_shr:8
+    walk_dpp_add<0x142, 0xA>(v);  // row_bcast:15 into rows 1 and 3
+    walk_dpp_add<0x143, 0xC>(v);  // row_bcast:31 into rows 2 and 3
+    return walk_u64(uint32_t(__builtin_amdgcn_readlane(int(uint32_t(v)), 63)),
+                    uint32_t(__builtin_amdgcn_readlane(int(uint32_t(v >> 32)), 63)));
+}
+__device__ inline uint64_t walk_wave_sum(uint64_t v) { return walk_dpp_sum64(v); }
+// u128: each 32-bit limb summed in u64 (64 lanes: < 2^38), then recombined with the carries.
+__device__ inline u128 walk_wave_sum(u128 v) {
+    const uint64_t lo = uint64_t(v), hi = uint64_t(v >> 64);
+    const uint64_t s0 = walk_dpp_sum64(lo & 0xFFFFFFFFull), s1 = walk_dpp_sum64(lo >> 32);
+    const uint64_t s2 = walk_dpp_sum64(hi & 0xFFFFFFFFull), s3 = walk_dpp_sum64(hi >> 32);
+    return u128(s0) + (u128(s1) << 32) + (u128(s2) << 64) + (u128(s3) << 96);
 }
 
 __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_transfer_t> c,
@@ -366,6 +385,7 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
     // [4] max walk cycles, [5] verdicts found in snapshots, [6] walks (100 MHz wall clock)
     const uint64_t t_walk0 = wall_clock64();
     uint64_t n_win = 0, n_ev = 0, n_poll = 0, t_poll = 0, n_snap = 0, n_iter = 0, n_alla = 0;
+    uint64_t n_refresh = 0, t_refresh = 0, t_fetch = 0, t_b = 0, t_tail = 0, t_a = 0;
     const uint32_t owners = L.counts[0];
     const bool run = L.counts[1] == 0 && owners != 0 && owners <= kLanesMax;
     if (blockIdx.x == 0 && threadIdx.x == 0 && run) {
@@ -473,6 +493,7 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
             fetch_pairs(base + 704, &q3);
         }
       for (uint32_t sub = 0; sub < 4; sub++) {
+        const uint64_t tf0 = dbg ? wall_clock64() : 0;
         // (field by field: a select of whole structs goes through scratch)
         WalkRaw x;
         x.s = sub == 0 ? b0.s : sub == 1 ? b1.s : sub == 2 ? b2.s : b3.s;
@@ -497,6 +518,7 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
         const uint64_t snap_set =
             __ballot((cur.mb & (my_debit ? kMbCrSet : kMbDrSet)) != 0);
         const uint64_t snap_ok = __ballot((cur.mb & (my_debit ? kMbCrOk : kMbDrOk)) != 0);
+        if (dbg) t_fetch += wall_clock64() - tf0;
         const bool more = (vmask >> 63) & 1;  // the segment continues past this window
         const uint32_t cnt = uint32_t(__popcll(vmask));
         uint64_t created_m = 0, drfail_m = 0, myok_m = 0, published = 0;
@@ -582,8 +604,12 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
                 const bool cr_fail = debit ? !other_ok : !my_ok;
                 if (!dr_fail && !cr_fail) {
                     created_m |= bit;
-                    if (debit) dpo_v += amt;
-                    else cpo_v += amt;
+                    // (value selects: an if / else here becomes a store through a selected
+                    // pointer, and the balances then live in scratch -- whose loads wait, in order,
+                    // for every memory operation issued before them, the prefetched windows
+                    // included)
+                    dpo_v += debit ? amt : V(0);
+                    cpo_v += debit ? V(0) : amt;
                 } else if (dr_fail) {
                     drfail_m |= bit;
                 }
@@ -612,6 +638,8 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
             // The words of the window events in `want` read again, all at once (the snapshot is
             // two windows old): one round trip instead of a poll per event.
             auto refresh = [&](uint64_t want) {
+                const uint64_t tr0 = dbg ? wall_clock64() : 0;
+                n_refresh++;
                 publish();
                 const bool w = (want >> lane) & 1;
                 const uint32_t mb2 = w ? __hip_atomic_load(&mbox[cur.s], __ATOMIC_RELAXED,
@@ -621,6 +649,7 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
                 const uint64_t ok = __ballot(w && (mb2 & (my_debit ? kMbCrOk : kMbDrOk)));
                 known |= set;
                 known_ok |= ok & set;
+                if (dbg) t_refresh += wall_clock64() - tr0;
             };
             const V mine_sum = walk_wave_sum(l_mine ? amt : V(0));
             if (used + mine_sum <= cap) {
@@ -639,6 +668,7 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
                 used += walk_wave_sum(((created_m & mine_m) >> lane) & 1 ? amt : V(0));
                 cap += walk_wave_sum(((created_m & ~mine_m) >> lane) & 1 ? amt : V(0));
             } else {
+                const uint64_t tb0 = dbg ? wall_clock64() : 0;
                 uint64_t rem = vmask;
                 while (rem != 0 && !stalled) {
                     n_iter++;
@@ -691,15 +721,13 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
                     rem &= ~bit;
                     publish();
                 }
+                if (dbg) t_b += wall_clock64() - tb0;
             }
-            if (owner_dm) {
-                dpo += u128(used - used0);
-                cpo += u128(cap - cap0);
-            } else {
-                cpo += u128(used - used0);
-                dpo += u128(cap - cap0);
-            }
+            const u128 d_used = u128(used - used0), d_cap = u128(cap - cap0);
+            dpo += owner_dm ? d_used : d_cap;
+            cpo += owner_dm ? d_cap : d_used;
         };
+        const uint64_t ta0 = dbg ? wall_clock64() : 0;
         if (one_limit && narrow) {
             one_limit_window(uint64_t(0));
         } else if (one_limit) {
@@ -712,6 +740,8 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
         } else {
             walk_events(dpe, dpo, cpe, cpo);
         }
+        const uint64_t tt0 = dbg ? wall_clock64() : 0;
+        if (dbg) t_a += tt0 - ta0;
         publish();
         if (stalled) {
             if (lane == 0) atomicOr(&T.scalars->flags, kFlagFlowStalled);
@@ -724,6 +754,7 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
             L.outcome[cur.s] = out;
         }
         if (lane == 0) atomicAdd(progress, 1u);
+        if (dbg) t_tail += wall_clock64() - tt0;
         n_win++;
         n_ev += cnt;
         if (!more) {
@@ -756,6 +787,9 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
             atomicMax(&dbg[4], wall_clock64() - t_walk0);
             atomicAdd(&dbg[5], n_snap);
             atomicAdd(&dbg[6], 1ull);
+            atomicAdd(&dbg[7], n_refresh);
+            atomicAdd(&dbg[8], t_refresh);
+            atomicAdd(&dbg[9], t_fetch);
             if (o < 1000) {  // per owner: events, polls, poll time, walk time, windows, step
                              // B iterations, all-pass windows
                 unsigned long long* w = &dbg[16 + 8 * o];
@@ -763,9 +797,11 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
                 w[1] = n_poll;
                 w[2] = t_poll;
                 w[3] = wall_clock64() - t_walk0;
-                w[4] = n_win;
-                w[5] = n_iter;
-                w[6] = n_alla;
+                w[4] = n_win | (t_fetch << 24);
+                w[5] = n_iter | (t_b << 24);
+                w[6] = n_alla | (t_tail << 24);
+                w[1] = n_poll | (t_a << 24);
+                w[7] = (n_refresh << 32) | (t_refresh & 0xFFFFFFFFull);
             }
         }
     }
