@@ -824,9 +824,14 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
                 if (!ctx->flow_debug) HIP_TRY(ctx, hipMalloc(&ctx->flow_debug, kFlowDebugBytes));
                 HIP_TRY(ctx, hipMemsetAsync(ctx->flow_debug, 0, kFlowDebugBytes, ctx->stream));
             }
-            hipLaunchKernelGGL(lanes_walk, dim3(kLanesMax / kWalkWaves), dim3(kWalkWaves * 64), 0,
-                               ctx->stream, ctx->T, c, L, F.mb_index,
-                               dbg ? ctx->flow_debug : nullptr);
+            if (dbg)
+                hipLaunchKernelGGL(lanes_walk<true>, dim3(kLanesMax / kWalkWaves),
+                                   dim3(kWalkWaves * 64), 0, ctx->stream, ctx->T, c, L, F.mb_index,
+                                   ctx->flow_debug);
+            else
+                hipLaunchKernelGGL(lanes_walk<false>, dim3(kLanesMax / kWalkWaves),
+                                   dim3(kWalkWaves * 64), 0, ctx->stream, ctx->T, c, L, F.mb_index,
+                                   nullptr);
             if (dbg) {
                 unsigned long long d[16] = {};
                 (void)hipMemcpyAsync(d, ctx->flow_debug, 128, hipMemcpyDeviceToHost, ctx->stream);
@@ -881,8 +886,12 @@ int run_flow_replay(tbg_ctx* ctx, Call<tb_transfer_t>& c, uint32_t m, unsigned i
     P.xcd_stride = ctx->knobs.flow_xcd;
     P.backoff = ctx->knobs.flow_backoff;
     const uint32_t lanes = blocks * waves * P.lanes_per_wave;
-    hipLaunchKernelGGL(flow_replay, dim3(blocks * P.xcd_stride), dim3(waves * 64), 0, ctx->stream,
-                       ctx->T, c, P);
+    if (debug)
+        hipLaunchKernelGGL(flow_replay<true>, dim3(blocks * P.xcd_stride), dim3(waves * 64), 0,
+                           ctx->stream, ctx->T, c, P);
+    else
+        hipLaunchKernelGGL(flow_replay<false>, dim3(blocks * P.xcd_stride), dim3(waves * 64), 0,
+                           ctx->stream, ctx->T, c, P);
     tmark(ctx, "tr_flow");
     if (debug) {
         unsigned int cnt[2] = {0, 0};

@@ -184,6 +184,8 @@ struct SelectHeads {
 // relaxed decrements of its successors' indeg; a lane that takes a unit -- from its own decrement
 // or from a relaxed poll of the queue -- runs one acquire fence (L1 invalidate) before it reads
 // anything another unit wrote. The queue counters live in global memory (P.engine).
+// (kDbg: TBG_FLOW_DEBUG's counters; the production instance holds none of them)
+template <bool kDbg>
 __global__ void __launch_bounds__(kFlowThreads) flow_replay(Tables T, Call<tb_transfer_t> c,
                                                            FlowPlan P) {
     if (P.skip && *P.skip) return;
@@ -195,7 +197,7 @@ __global__ void __launch_bounds__(kFlowThreads) flow_replay(Tables T, Call<tb_tr
     const uint32_t units = P.counts[0];
     unsigned int* q_head = P.engine;
     unsigned int* q_tail = P.engine + 32;
-    const uint64_t t_start = wall_clock64();
+    const uint64_t t_start = kDbg ? wall_clock64() : 0;
     uint64_t it_count = 0, ev_count = 0, exec_cycles = 0, conts = 0;
     bool chain_open = false, chain_broken = false;
     uint32_t chain_start = 0;
@@ -234,7 +236,7 @@ __global__ void __launch_bounds__(kFlowThreads) flow_replay(Tables T, Call<tb_tr
         const uint32_t end = u + 1 < units ? P.heads[u + 1] : P.m;
         R.undo_len = 0;
         R.key_max = 0;
-        const uint64_t t0 = P.debug ? wall_clock64() : 0;
+        const uint64_t t0 = kDbg ? wall_clock64() : 0;
         // Step records and events are addressed by position and never written during the
         // replay: a chain's next pair loads while the current event runs.
         Step st = P.steps[begin];
@@ -263,7 +265,7 @@ __global__ void __launch_bounds__(kFlowThreads) flow_replay(Tables T, Call<tb_tr
                 ev = ev_next;
             }
         }
-        if (P.debug) {
+        if (kDbg) {
             exec_cycles += wall_clock64() - t0;
             ev_count += end - begin;
         }
@@ -379,7 +381,7 @@ __global__ void __launch_bounds__(kFlowThreads) flow_replay(Tables T, Call<tb_tr
                         // Watchdog: a replay that stops progressing is a bug; leave with a flag
                         // (the call fails) instead of holding the GPU.
                         atomicOr(&T.scalars->flags, kFlagFlowStalled);
-                        if (P.debug) {
+                        if (kDbg) {
                             P.debug[8] = *q_head;
                             P.debug[9] = *q_tail;
                             P.debug[10] = seen;
@@ -404,7 +406,7 @@ __global__ void __launch_bounds__(kFlowThreads) flow_replay(Tables T, Call<tb_tr
     }
     if (lane_key_max)
         atomicMax(&T.scalars->transfers_key_max, (unsigned long long)lane_key_max);
-    if (P.debug) {
+    if (kDbg) {
         atomicAdd(&P.debug[0], (unsigned long long)it_count);
         atomicAdd(&P.debug[1], (unsigned long long)ev_count);
         atomicAdd(&P.debug[2], (unsigned long long)exec_cycles);
@@ -413,7 +415,7 @@ __global__ void __launch_bounds__(kFlowThreads) flow_replay(Tables T, Call<tb_tr
     __syncthreads();
     if (block == 0 && tid == 0) {
         T.scalars->stats[2] = P.m;
-        if (P.debug) P.debug[3] = wall_clock64() - t_start;
+        if (kDbg) P.debug[3] = wall_clock64() - t_start;
     }
 }
 

@@ -378,12 +378,15 @@ __device__ inline u128 walk_wave_sum(u128 v) {
     return u128(s0) + (u128(s1) << 32) + (u128(s2) << 64) + (u128(s3) << 96);
 }
 
+// (kDbg: TBG_FLOW_DEBUG's counters and timers; the production instance holds none of them:
+// thirteen 64-bit counters live across the walk were ~26 SGPRs of a kernel that spills SGPRs)
+template <bool kDbg>
 __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_transfer_t> c,
                                                                LanePlan L, uint32_t* mbox,
                                                                unsigned long long* dbg) {
     // dbg (TBG_FLOW_DEBUG): [0] windows, [1] events, [2] live polls, [3] poll cycles,
     // [4] max walk cycles, [5] verdicts found in snapshots, [6] walks (100 MHz wall clock)
-    const uint64_t t_walk0 = wall_clock64();
+    const uint64_t t_walk0 = kDbg ? wall_clock64() : 0;
     uint64_t n_win = 0, n_ev = 0, n_poll = 0, t_poll = 0, n_snap = 0, n_iter = 0, n_alla = 0;
     uint64_t n_refresh = 0, t_refresh = 0, t_fetch = 0, t_b = 0, t_tail = 0, t_a = 0;
     const uint32_t owners = L.counts[0];
@@ -493,7 +496,7 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
             fetch_pairs(base + 704, &q3);
         }
       for (uint32_t sub = 0; sub < 4; sub++) {
-        const uint64_t tf0 = dbg ? wall_clock64() : 0;
+        const uint64_t tf0 = kDbg ? wall_clock64() : 0;
         // (field by field: a select of whole structs goes through scratch)
         WalkRaw x;
         x.s = sub == 0 ? b0.s : sub == 1 ? b1.s : sub == 2 ? b2.s : b3.s;
@@ -518,7 +521,7 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
         const uint64_t snap_set =
             __ballot((cur.mb & (my_debit ? kMbCrSet : kMbDrSet)) != 0);
         const uint64_t snap_ok = __ballot((cur.mb & (my_debit ? kMbCrOk : kMbDrOk)) != 0);
-        if (dbg) t_fetch += wall_clock64() - tf0;
+        if (kDbg) t_fetch += wall_clock64() - tf0;
         const bool more = (vmask >> 63) & 1;  // the segment continues past this window
         const uint32_t cnt = uint32_t(__popcll(vmask));
         uint64_t created_m = 0, drfail_m = 0, myok_m = 0, published = 0;
@@ -545,7 +548,7 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
                             (cpo >> 62) == 0;
         // The other side's verdict of window event j (not in the snapshot): poll its word.
         auto wait_verdict = [&](uint32_t j, bool debit) -> bool {
-            const uint64_t tp0 = dbg ? wall_clock64() : 0;
+            const uint64_t tp0 = kDbg ? wall_clock64() : 0;
             n_poll++;
             publish();  // (an owner this one waits on may wait on these)
             const uint32_t sj = __builtin_amdgcn_readlane(cur.s, j);
@@ -567,7 +570,7 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
                     }
                 }
             }
-            if (dbg) t_poll += wall_clock64() - tp0;
+            if (kDbg) t_poll += wall_clock64() - tp0;
             return (mb & (debit ? kMbCrOk : kMbDrOk)) != 0;
         };
         auto walk_events = [&](auto dpe_v, auto& dpo_v, auto cpe_v, auto& cpo_v) {
@@ -638,7 +641,7 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
             // The words of the window events in `want` read again, all at once (the snapshot is
             // two windows old): one round trip instead of a poll per event.
             auto refresh = [&](uint64_t want) {
-                const uint64_t tr0 = dbg ? wall_clock64() : 0;
+                const uint64_t tr0 = kDbg ? wall_clock64() : 0;
                 n_refresh++;
                 publish();
                 const bool w = (want >> lane) & 1;
@@ -649,7 +652,7 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
                 const uint64_t ok = __ballot(w && (mb2 & (my_debit ? kMbCrOk : kMbDrOk)));
                 known |= set;
                 known_ok |= ok & set;
-                if (dbg) t_refresh += wall_clock64() - tr0;
+                if (kDbg) t_refresh += wall_clock64() - tr0;
             };
             const V mine_sum = walk_wave_sum(l_mine ? amt : V(0));
             if (used + mine_sum <= cap) {
@@ -668,7 +671,7 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
                 used += walk_wave_sum(((created_m & mine_m) >> lane) & 1 ? amt : V(0));
                 cap += walk_wave_sum(((created_m & ~mine_m) >> lane) & 1 ? amt : V(0));
             } else {
-                const uint64_t tb0 = dbg ? wall_clock64() : 0;
+                const uint64_t tb0 = kDbg ? wall_clock64() : 0;
                 uint64_t rem = vmask;
                 while (rem != 0 && !stalled) {
                     n_iter++;
@@ -721,13 +724,13 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
                     rem &= ~bit;
                     publish();
                 }
-                if (dbg) t_b += wall_clock64() - tb0;
+                if (kDbg) t_b += wall_clock64() - tb0;
             }
             const u128 d_used = u128(used - used0), d_cap = u128(cap - cap0);
             dpo += owner_dm ? d_used : d_cap;
             cpo += owner_dm ? d_cap : d_used;
         };
-        const uint64_t ta0 = dbg ? wall_clock64() : 0;
+        const uint64_t ta0 = kDbg ? wall_clock64() : 0;
         if (one_limit && narrow) {
             one_limit_window(uint64_t(0));
         } else if (one_limit) {
@@ -740,8 +743,8 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
         } else {
             walk_events(dpe, dpo, cpe, cpo);
         }
-        const uint64_t tt0 = dbg ? wall_clock64() : 0;
-        if (dbg) t_a += tt0 - ta0;
+        const uint64_t tt0 = kDbg ? wall_clock64() : 0;
+        if (kDbg) t_a += tt0 - ta0;
         publish();
         if (stalled) {
             if (lane == 0) atomicOr(&T.scalars->flags, kFlagFlowStalled);
@@ -754,7 +757,7 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
             L.outcome[cur.s] = out;
         }
         if (lane == 0) atomicAdd(progress, 1u);
-        if (dbg) t_tail += wall_clock64() - tt0;
+        if (kDbg) t_tail += wall_clock64() - tt0;
         n_win++;
         n_ev += cnt;
         if (!more) {
@@ -779,7 +782,7 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
         acc.credits_posted = W(cpo);
         const uint16_t h = acc_hazard_of(acc);
         if (h) acc_hazard_set(T.acc_index, T.acc_entry_of, row, h);
-        if (dbg) {
+        if (kDbg) {
             atomicAdd(&dbg[0], n_win);
             atomicAdd(&dbg[1], n_ev);
             atomicAdd(&dbg[2], n_poll);
