@@ -481,6 +481,12 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
     bool stalled = false;
     bool done = false;
     while (!done) {
+        // This super window's records and the next one's pairs arrived during the previous super
+        // window: one wait for them here, before the next loads issue. (Without it the compiler's
+        // wait at the window loop's head -- its pending-load state merged over the loop -- was a
+        // vmcnt(0) that also waited for the loads issued just below: the prefetch never overlapped.
+        // A builtin, not inline asm, so that the compiler's wait pass sees it.)
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) (gfx9 encoding; expcnt, lgkmcnt not waited)
         const bool more_super = (__ballot(b3.valid) >> 63) & 1;
         WalkRaw n0, n1, n2, n3;
         n0.valid = n1.valid = n2.valid = n3.valid = false;
