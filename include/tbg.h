@@ -187,6 +187,11 @@ int64_t tbg_lookup_transfers(tbg_ctx* ctx, const tb_uint128_t* ids, uint32_t n,
 /* Parity dumps: live objects in creation order; `out` may be NULL to query the count. */
 int64_t tbg_dump_accounts(tbg_ctx* ctx, tb_account_t* out);
 int64_t tbg_dump_transfers(tbg_ctx* ctx, tb_transfer_t* out, uint8_t* pending_status);
+/* Every transfer id the transfers' id table holds -- created transfers and orphaned ids
+ * (transient failures, :3215-3252), not tombstones -- in row order; out NULL: the count. A group
+ * reopened from its shards' checkpoints rebuilds its router's directory from these
+ * (tbg_group_open_checkpoint). */
+int64_t tbg_dump_transfer_ids(tbg_ctx* ctx, tb_uint128_t* out);
 
 /* The account_events groove (AccountEvent, state_machine.zig:104-220; written by account_event
  * :4384-4465 for every created transfer, post/void and expiry), in timestamp order; `out` may be

@@ -112,6 +112,15 @@ tbg_group* tbg_group_open(const tbg_group_options* options, const tbg_options* s
  * thread. */
 tbg_group* tbg_group_open_shards(const tbg_group_options* options, const tbg_shard_ops* ops,
                                  void* const* shards);
+/* Durability (StateMachine.checkpoint :2937-2958 / open :964-978, for a group): every shard
+ * writes its image to paths[s] (tbg_checkpoint: tables, AccountEvents, pulse_next_timestamp, key
+ * ranges), between calls; tbg_group_open_checkpoint opens each shard from paths[s]
+ * (tbg_open_checkpoint) and rebuilds the router's directories from the shards' accounts and
+ * transfer ids, orphaned ids included (tbg_dump_transfer_ids). Groups of HIP executors only
+ * (tbg_group_open). */
+int tbg_group_checkpoint(tbg_group* g, const char* const* paths);
+tbg_group* tbg_group_open_checkpoint(const tbg_group_options* options,
+                                     const tbg_options* shard_options, const char* const* paths);
 void tbg_group_close(tbg_group* g);
 const char* tbg_group_last_error(const tbg_group* g);
 /* Shard s's executor (a tbg_ctx* for tbg_group_open, the caller's pointer otherwise): dumps,

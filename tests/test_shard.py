@@ -405,11 +405,12 @@ def scenario(seed, calls=8, n_acc=48, timed_post_void=True):
     return ops
 
 
-def drive(cluster, ref, ops, pbm=PBM, cuts=None):
+def drive(cluster, ref, ops, pbm=PBM, cuts=None, clock=None):
     """Runs `ops` through `cluster` (and `ref`, compared call by call); returns the pulses run.
     Timestamps follow the TestContext rule (prepare_ts += 1 + events, pulses when due). `cuts`
-    (a list) collects the pulses that expired exactly pbm transfers (a cut across shards)."""
-    ts, pulses = 0, 0
+    (a list) collects the pulses that expired exactly pbm transfers (a cut across shards).
+    `clock` (a one-element list): the timestamp to start from, and where the last one is left."""
+    ts, pulses = (clock[0] if clock else 0), 0
     for op in ops:
         if op[0] == "tick":
             ts += op[1]
@@ -449,6 +450,8 @@ def drive(cluster, ref, ops, pbm=PBM, cuts=None):
             if cuts is not None and expired == pbm:
                 cuts.append(ts)
             pulses += 1
+    if clock is not None:
+        clock[0] = ts
     return pulses
 
 
@@ -810,3 +813,36 @@ def test_local_shards_batch_cap():
     finally:
         for s in shards + [ref]:
             s.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [1, 6])
+def test_group_checkpoint_gpu(seed, tmp_path):
+    """tbg_group_checkpoint / tbg_group_open_checkpoint: half of a cross-shard scenario, every
+    shard's image written, the group closed and reopened from the images (the router's
+    directories rebuilt from the shards' accounts and transfer ids, orphaned ids included), the
+    other half -- results, pulses, tables and AccountEvents against the unsharded oracle, which
+    runs straight through."""
+    from tigerbeetle_amd import native
+    n = 2
+    opts = [native.options(1 << 12, 1 << 16, 4096, pulse_batch_max=PBM,
+                           account_events_capacity=1 << 16) for _ in range(n)]
+    kw = dict(ledgers=LEDGERS, pulse_batch_max=PBM, events_max=4096,
+              router_transfer_capacity=1 << 20)
+    ops = cross_scenario(seed, calls=12)
+    half = len(ops) // 2
+    ref = OracleShard()
+    g = shard.Group.open_gpu(opts, **kw)
+    try:
+        clock = [0]
+        drive(g, ref, ops[:half], clock=clock)
+        paths = [str(tmp_path / f"shard{s}.img") for s in range(n)]
+        g.checkpoint(paths)
+        g.close()
+        g = shard.Group.open_gpu_checkpoint(opts, paths, **kw)
+        drive(g, ref, ops[half:], clock=clock)
+        views = [shard.GpuShard.wrap(g.lib, g.shard(s)) for s in range(n)]
+        assert_same_state([v.dump() for v in views], ref, [v.dump_account_events() for v in views])
+    finally:
+        g.close()
+        ref.close()

@@ -3170,6 +3170,59 @@ int64_t tbg_dump_transfers(tbg_ctx* ctx, tb_transfer_t* out, uint8_t* pending_st
                      pending_status);
 }
 
+// Rows an occupied id slot references: created transfers and orphaned ids (tombstones and empty
+// slots reference none).
+__global__ void mark_slot_rows(const unsigned long long* slots, uint64_t n_slots, uint8_t* flags,
+                               uint64_t used) {
+    const uint64_t s = blockIdx.x * uint64_t(blockDim.x) + threadIdx.x;
+    if (s >= n_slots) return;
+    const uint64_t w = slots[s];
+    if (w == kEmpty || w == kTomb) return;
+    const uint64_t r = (w & kRefMask) - 1;
+    if (r < used) flags[r] = 1;
+}
+__global__ void gather_transfer_ids(const tb_transfer_t* rows, const uint32_t* sel, uint32_t n,
+                                    tb_uint128_t* out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = rows[sel[i]].id;
+}
+
+int64_t tbg_dump_transfer_ids(tbg_ctx* ctx, tb_uint128_t* out) {
+    TBG_DEVICE_SCOPE(ctx);
+    if (!ctx) return TBG_EINVAL;
+    const uint64_t used = ctx->T.tr_rows_used;
+    if (used == 0) return 0;
+    uint8_t* flags = nullptr;
+    if (!dev_alloc(ctx, &flags, used, true)) return TBG_ENOMEM;
+    const uint64_t n_slots = ctx->T.tr.mask + 1;
+    hipLaunchKernelGGL(mark_slot_rows, dim3(grid_for(n_slots)), dim3(kBlock), 0, ctx->stream,
+                       ctx->T.tr.slots, n_slots, flags, used);
+    unsigned int* d_count = &ctx->d_scalars->slow_count;
+    int64_t result = select_flagged(ctx, flags, used, ctx->sel_buf, d_count);
+    if (result == 0 && !hip_ok(ctx, hipMemcpyAsync(&ctx->h_scalars->slow_count, d_count, 4,
+                                                   hipMemcpyDeviceToHost, ctx->stream), "count"))
+        result = TBG_EHIP;
+    if (result == 0 && !hip_ok(ctx, hipStreamSynchronize(ctx->stream), "sync")) result = TBG_EHIP;
+    const uint64_t count = result == 0 ? ctx->h_scalars->slow_count : 0;
+    if (result == 0 && out && count) {
+        tb_uint128_t* d_out = nullptr;
+        if (!dev_alloc(ctx, &d_out, count, false)) {
+            result = TBG_ENOMEM;
+        } else {
+            hipLaunchKernelGGL(gather_transfer_ids, dim3(grid_for(count)), dim3(kBlock), 0,
+                               ctx->stream, ctx->T.tr_rows, ctx->sel_buf, uint32_t(count), d_out);
+            if (!hip_ok(ctx, hipMemcpyAsync(out, d_out, count * sizeof(tb_uint128_t),
+                                            hipMemcpyDeviceToHost, ctx->stream), "ids copy"))
+                result = TBG_EHIP;
+            (void)hipStreamSynchronize(ctx->stream);
+            (void)hipFree(d_out);
+        }
+    }
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipFree(flags);
+    return result < 0 ? result : int64_t(count);
+}
+
 int tbg_debug_set_account_balances(tbg_ctx* ctx, tb_uint128_t id, tb_uint128_t debits_pending,
                                    tb_uint128_t debits_posted, tb_uint128_t credits_pending,
                                    tb_uint128_t credits_posted) {

@@ -481,7 +481,45 @@ tbg_group* tbg_group_open_shards(const tbg_group_options* options, const tbg_sha
     return g;
 }
 
-tbg_group* tbg_group_open(const tbg_group_options* options, const tbg_options* shard_options) {
+}  // extern "C"
+
+namespace {
+
+// A group reopened from its shards' checkpoints: the router's directories hold every account id
+// and every transfer id (created or orphaned) at its shard again, and the imported floor is the
+// largest timestamp over the shards (the shards' own state -- tables, AccountEvents,
+// pulse_next_timestamp, key ranges -- comes with their images).
+int rebuild_directories(tbg_group* g) {
+    DeviceScope ds(int(g->o.router_device));
+    for (uint32_t s = 0; s < g->o.shards; s++) {
+        tbg_ctx* ctx = static_cast<tbg_ctx*>(g->shards[s]);
+        const int64_t na = tbg_dump_accounts(ctx, nullptr);
+        if (na < 0) return int(na);
+        std::vector<tb_account_t> a(static_cast<size_t>(na));
+        if (na && tbg_dump_accounts(ctx, a.data()) != na) return TBG_EHIP;
+        std::vector<tb_uint128_t> ids(a.size());
+        for (size_t i = 0; i < a.size(); i++) ids[i] = a[i].id;
+        std::vector<uint8_t> sh(ids.size(), uint8_t(s));
+        int rc = tbr_record_accounts(g->tbr, ids.data(), sh.data(), uint32_t(ids.size()));
+        if (rc) return rc;
+        const int64_t nt = tbg_dump_transfer_ids(ctx, nullptr);
+        if (nt < 0) return int(nt);
+        ids.assign(size_t(nt), tb_uint128_t{});
+        if (nt && tbg_dump_transfer_ids(ctx, ids.data()) != nt) return TBG_EHIP;
+        sh.assign(ids.size(), uint8_t(s));
+        rc = tbr_record_transfers(g->tbr, ids.data(), sh.data(), uint32_t(ids.size()));
+        if (rc) return rc;
+    }
+    try {
+        refresh_floor(g);
+    } catch (const tbs::EngineError& e) {
+        return e.code < 0 ? e.code : TBG_EHIP;
+    }
+    return 0;
+}
+
+tbg_group* open_gpu_group(const tbg_group_options* options, const tbg_options* shard_options,
+                          const char* const* paths) {
     if (!valid_options(options) || !shard_options) return nullptr;
     if (options->router_transfer_capacity >= (1ull << 31) ||
         options->router_account_capacity >= (1ull << 31))
@@ -499,7 +537,8 @@ tbg_group* tbg_group_open(const tbg_group_options* options, const tbg_options* s
     const int rdev = int(options->router_device);
     bool ok = true;
     for (uint32_t s = 0; s < W && ok; s++) {
-        g->shards[s] = tbg_open(&shard_options[s]);
+        g->shards[s] = paths ? tbg_open_checkpoint(&shard_options[s], paths[s])
+                             : tbg_open(&shard_options[s]);
         ok = g->shards[s] != nullptr;
         g->link[s].device = shard_options[s].device;
     }
@@ -546,7 +585,39 @@ tbg_group* tbg_group_open(const tbg_group_options* options, const tbg_options* s
     }
     g->eng.reset(new tbs::Engine(W, options->ledgers, options->batch_count_max, &g->ops,
                                  g->shards, g->dir.get(), g->runner.get()));
+    if (paths && W > 1) {
+        const int rc = rebuild_directories(g);
+        if (rc) {
+            fprintf(stderr, "tbg_group_open_checkpoint: rebuilding the directories failed (%d)\n",
+                    rc);
+            destroy(g);
+            return nullptr;
+        }
+    }
     return g;
+}
+
+}  // namespace
+
+extern "C" {
+
+tbg_group* tbg_group_open(const tbg_group_options* options, const tbg_options* shard_options) {
+    return open_gpu_group(options, shard_options, nullptr);
+}
+
+tbg_group* tbg_group_open_checkpoint(const tbg_group_options* options,
+                                     const tbg_options* shard_options, const char* const* paths) {
+    return paths ? open_gpu_group(options, shard_options, paths) : nullptr;
+}
+
+int tbg_group_checkpoint(tbg_group* g, const char* const* paths) {
+    if (!g || !g->gpu || !paths) return TBG_EINVAL;
+    for (uint32_t s = 0; s < g->o.shards; s++) {
+        tbg_ctx* ctx = static_cast<tbg_ctx*>(g->shards[s]);
+        const int rc = tbg_checkpoint(ctx, paths[s]);
+        if (rc) return fail(g, rc, "shard " + std::to_string(s) + " checkpoint: " + tbg_last_error(ctx));
+    }
+    return 0;
 }
 
 void tbg_group_close(tbg_group* g) { destroy(g); }

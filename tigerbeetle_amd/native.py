@@ -130,6 +130,7 @@ SIGNATURES = [
     ("tbg_lookup_transfers", ctypes.c_int64, [vp, vp, ctypes.c_uint32, vp]),
     ("tbg_dump_accounts", ctypes.c_int64, [vp, vp]),
     ("tbg_dump_transfers", ctypes.c_int64, [vp, vp, vp]),
+    ("tbg_dump_transfer_ids", ctypes.c_int64, [vp, vp]),
     ("tbg_dump_account_events", ctypes.c_int64, [vp, vp]),
     ("tbg_get_change_events", ctypes.c_int64, [vp, vp, ctypes.c_uint32, vp]),
     ("tbg_compact", ctypes.c_int64, [vp]),
@@ -165,6 +166,8 @@ SIGNATURES = [
     ("tbg_group_open", vp, [vp, vp]),
     ("tbg_group_open_shards", vp, [vp, vp, vp]),
     ("tbg_group_close", None, [vp]),
+    ("tbg_group_checkpoint", ctypes.c_int, [vp, vp]),
+    ("tbg_group_open_checkpoint", vp, [vp, vp, vp]),
     ("tbg_group_last_error", ctypes.c_char_p, [vp]),
     ("tbg_group_shard", vp, [vp, ctypes.c_uint32]),
     ("tbg_group_create_accounts", ctypes.c_int, [vp, vp, ctypes.c_uint32, vp, vp,

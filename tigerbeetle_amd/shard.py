@@ -15,6 +15,7 @@ marshals numpy arrays:
 * `GpuShard` -- one HIP executor (tbg.h) with the same numpy interface, for tests and the bench.
 """
 import ctypes
+import os
 
 import numpy as np
 
@@ -102,6 +103,21 @@ class Group:
         o = group_options(len(shard_options), **kw)
         arr = (native.TbgOptions * len(shard_options))(*shard_options)
         return cls(lib, lib.tbg_group_open(ctypes.byref(o), arr), o)
+
+    @classmethod
+    def open_gpu_checkpoint(cls, shard_options, paths, **kw):
+        """open_gpu from the shards' checkpoint images (tbg_group_open_checkpoint: the router's
+        directories rebuilt from the shards' tables)."""
+        lib = native.load()
+        o = group_options(len(shard_options), **kw)
+        arr = (native.TbgOptions * len(shard_options))(*shard_options)
+        cp = (ctypes.c_char_p * len(paths))(*[os.fsencode(p) for p in paths])
+        return cls(lib, lib.tbg_group_open_checkpoint(ctypes.byref(o), arr, cp), o)
+
+    def checkpoint(self, paths):
+        """Every shard's image to paths[s] (tbg_group_checkpoint)."""
+        cp = (ctypes.c_char_p * len(paths))(*[os.fsencode(p) for p in paths])
+        return self._check(self.lib.tbg_group_checkpoint(self.g, cp), "checkpoint")
 
     @classmethod
     def open_shards(cls, ops: ShardOps, selves, **kw):
