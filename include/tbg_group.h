@@ -107,6 +107,9 @@ typedef struct tbg_group_options {
  * the device router on options->router_device, and peer access between the router's GPU and
  * every shard's. A group of one shard passes every call straight to its executor. */
 tbg_group* tbg_group_open(const tbg_group_options* options, const tbg_options* shard_options);
+/* The shard operations of HIP executors (tbg_ctx*), for a group over executors the caller owns --
+ * e.g. executors in other processes reached through the caller's transport (remote.py). */
+void tbg_group_hip_shard_ops(tbg_shard_ops* out);
 /* A group over executors the caller owns (`ops` applied to shards[s]): host directories and the
  * exact engine only (no device path); shard calls are made one at a time from the caller's
  * thread. */

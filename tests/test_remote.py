@@ -24,7 +24,7 @@ def _port():
         return s.getsockname()[1]
 
 
-def _rank(rank, world, port, case, seed):
+def _rank(rank, world, port, case, seed, gpu=False):
     import ctypes
 
     import torch.distributed as dist
@@ -39,10 +39,21 @@ def _rank(rank, world, port, case, seed):
                             timeout=datetime.timedelta(seconds=120))
     try:
         pbm = 6 if case == "pulse_cut" else ts.PBM
-        mine = ts.OracleShard(pbm)
         ops = shard.ShardOps()
-        oracle_binding.load().tbo_shard_ops_fill(ctypes.byref(ops))
-        rs = remote.RemoteShards(ops, mine.o, ledgers=ts.LEDGERS, pulse_batch_max=pbm)
+        if gpu:  # this rank's executor: a HIP executor on cuda:0 (every rank shares the one GPU)
+            from tigerbeetle_amd import native
+            lib = native.load()
+            ctx = lib.tbg_open(ctypes.byref(native.options(
+                1 << 12, 1 << 16, 4096, pulse_batch_max=pbm, account_events_capacity=1 << 16)))
+            assert ctx, "tbg_open"
+            mine = shard.GpuShard.wrap(lib, ctx)
+            lib.tbg_group_hip_shard_ops(ctypes.byref(ops))
+            self_ptr = ctx
+        else:
+            mine = ts.OracleShard(pbm)
+            oracle_binding.load().tbo_shard_ops_fill(ctypes.byref(ops))
+            self_ptr = mine.o
+        rs = remote.RemoteShards(ops, self_ptr, ledgers=ts.LEDGERS, pulse_batch_max=pbm)
         if rank == 0:
             ref = ts.OracleShard(pbm)
             g = rs.group
@@ -65,7 +76,10 @@ def _rank(rank, world, port, case, seed):
             assert all(len(d[1]) for d in dumps), "every rank's shard holds transfers"
             ts.assert_same_state(dumps, ref, events)
             ref.close()
-        mine.close()
+        if gpu:
+            lib.tbg_close(ctx)
+        else:
+            mine.close()
     finally:
         dist.destroy_process_group()
 
@@ -74,3 +88,12 @@ def _rank(rank, world, port, case, seed):
 def test_remote_shards_gloo_world2(case, seed):
     import torch.multiprocessing as mp
     mp.spawn(_rank, args=(2, _port(), case, seed), nprocs=2, join=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [2])
+def test_remote_hip_shards_gloo_world2(seed):
+    """The same transport over HIP executors (tbg_group_hip_shard_ops): each rank opens its own
+    executor on cuda:0, rank 0's group reaches rank 1's over gloo."""
+    import torch.multiprocessing as mp
+    mp.spawn(_rank, args=(2, _port(), "cross", seed, True), nprocs=2, join=True)

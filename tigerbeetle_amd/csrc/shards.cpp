@@ -605,6 +605,10 @@ tbg_group* tbg_group_open(const tbg_group_options* options, const tbg_options* s
     return open_gpu_group(options, shard_options, nullptr);
 }
 
+void tbg_group_hip_shard_ops(tbg_shard_ops* out) {
+    if (out) *out = tbg_ops();
+}
+
 tbg_group* tbg_group_open_checkpoint(const tbg_group_options* options,
                                      const tbg_options* shard_options, const char* const* paths) {
     return paths ? open_gpu_group(options, shard_options, paths) : nullptr;

@@ -166,6 +166,7 @@ SIGNATURES = [
     ("tbg_group_open", vp, [vp, vp]),
     ("tbg_group_open_shards", vp, [vp, vp, vp]),
     ("tbg_group_close", None, [vp]),
+    ("tbg_group_hip_shard_ops", None, [vp]),
     ("tbg_group_checkpoint", ctypes.c_int, [vp, vp]),
     ("tbg_group_open_checkpoint", vp, [vp, vp, vp]),
     ("tbg_group_last_error", ctypes.c_char_p, [vp]),
