@@ -854,8 +854,8 @@ def single_line(args, world, rank, local, dist):
 
     opt = native.TbgOptions()
     opt.account_capacity = A
-    # + one host-buffer step (pcie_inclusive) + the per-commit bodies
-    opt.transfer_capacity = N * (K + W + 1) + R * BATCH
+    # + two host-buffer steps (pcie_inclusive: pageable, registered) + the per-commit bodies
+    opt.transfer_capacity = N * (K + W + 2) + R * BATCH
     opt.batch_events_max = max(N, wl.chunk)
     opt.batch_count_max = len(lens)
     opt.pulse_batch_max = 8190
@@ -966,24 +966,42 @@ def single_line(args, world, rank, local, dist):
 
     # The same step through the host-buffer ABI (tbg_create_transfers: events copied in, results
     # copied out over PCIe) -- the rate a caller holding host buffers sees; never `value`.
+    # Registered: the caller pins and maps its buffers once (tbg_register_host), as a replica
+    # registers its message pool; pageable: plain host memory, staged by the runtime.
     pcie = None
     if not args.no_validate:
-        ev = base.copy()
-        ev["id"][:, 0] += np.uint64((W + K) * N * world)
-        ts, prepare_ts = global_step_timestamps(prepare_ts, lens, world, rank)
         h_lens = lens.astype(np.uint32)
-        h_res = np.zeros(N, dtype=RESULT_DTYPE)
-        t0 = time.perf_counter()
-        rc = lib.tbg_create_transfers(g, ev.ctypes.data_as(ctypes.c_void_p), N,
-                                      h_lens.ctypes.data_as(native.c_u32p),
-                                      ts.ctypes.data_as(native.c_u64p), len(lens),
-                                      h_res.ctypes.data_as(ctypes.c_void_p))
-        t_host = time.perf_counter() - t0
-        ok = rc == 0 and bool((h_res["status"] == CREATED).all())
-        validated = bool(validated) and ok
+        rates = {}
+        for j, mode in enumerate(("pageable", "registered")):
+            ev = base.copy()
+            ev["id"][:, 0] += np.uint64((W + K + j) * N * world)
+            ts, prepare_ts = global_step_timestamps(prepare_ts, lens, world, rank)
+            h_res = np.zeros(N, dtype=RESULT_DTYPE)
+            if mode == "registered":
+                assert lib.tbg_register_host(g, ev.ctypes.data, ev.nbytes) == 0
+                assert lib.tbg_register_host(g, h_res.ctypes.data, h_res.nbytes) == 0
+            t0 = time.perf_counter()
+            rc = lib.tbg_create_transfers(g, ev.ctypes.data_as(ctypes.c_void_p), N,
+                                          h_lens.ctypes.data_as(native.c_u32p),
+                                          ts.ctypes.data_as(native.c_u64p), len(lens),
+                                          h_res.ctypes.data_as(ctypes.c_void_p))
+            t_host = time.perf_counter() - t0
+            if mode == "registered":
+                lib.tbg_unregister_host(g, ev.ctypes.data)
+                lib.tbg_unregister_host(g, h_res.ctypes.data)
+            ok = rc == 0 and bool((h_res["status"] == CREATED).all())
+            validated = bool(validated) and ok
+            rates[mode] = (t_host, ok)
+            del ev, h_res
+        t_host = rates["registered"][0]
+        t_page = rates["pageable"][0]
         pcie = {"value": round(N / t_host, 1), "unit": "transfers/s", "ms": round(t_host * 1e3, 3),
+                "pcie_gb_per_s": round(N * 144 / t_host / 1e9, 1),
+                "pageable": {"value": round(N / t_page, 1), "ms": round(t_page * 1e3, 3),
+                             "pcie_gb_per_s": round(N * 144 / t_page / 1e9, 1)},
                 "note": "one step through tbg_create_transfers with host buffers (events in, "
-                        "results out over PCIe)"}
+                        "results out over PCIe), registered once (tbg_register_host, as a "
+                        "replica's message pool); `pageable`: unregistered host memory"}
 
     # The integrated drop-in records an AccountEvent for every created transfer
     # (state_machine.zig:4417, "For CDC we always insert the history"): the same steps on a second
@@ -997,7 +1015,7 @@ def single_line(args, world, rank, local, dist):
     commits = None
     if R > 0:
         commits, prepare_ts = per_commit(args, lib, dev, g, wl, prepare_ts,
-                                         (W + K + 1) * N * world)
+                                         (W + K + 2) * N * world)
 
     # Algorithmic bytes of the path: 288 B per event + 256 B per distinct account.
     distinct = len(np.union1d(wl.dr, wl.cr))
