@@ -8,7 +8,8 @@ The group's ops table on rank 0 is a table of Python callbacks: an operation on 
 calls its C op with the engine's pointers as they are; an operation on shard s is sent to rank s
 (a header word vector, then the input buffers) and rank s replies (a return code, then the output
 buffers). Ranks > 0 serve until rank 0 ends the session. The transport is torch.distributed's
-point-to-point send / recv: gloo here (host buffers), nccl (device buffers over RCCL) on GPUs.
+point-to-point send / recv of host tensors, so the process group must carry CPU tensors (gloo; an
+RCCL group would need the buffers staged in device memory, which this module does not do).
 
 The in-process group over a node's GPUs (tbg_group_open: device router, peer stores, per-shard
 threads) is the production path; this transport is for executors the caller cannot put in one
