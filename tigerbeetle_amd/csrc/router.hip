@@ -481,9 +481,16 @@ __global__ void tbr_release(RouteArgs a) {
 
 // Each event copied to its shard's slice with its global commit timestamp and its position (a
 // surrogate with its credit account replaced by its debit account); its shard into the store.
+// The wave's events are staged in LDS with coalesced loads (stage_wave_events), and each 8-lane
+// group then stores one event's 128 contiguous bytes to its slot in its shard's slice: a wave's
+// events bound for one shard land in consecutive slots, so the stores (across xGMI for another
+// GPU's slice) are as coalesced as the loads. (A lane copying its own event issued 8 loads and 8
+// stores that each touched 64 lines.)
 __global__ void __launch_bounds__(kRouteBlock) tbr_pass2(RouteArgs a, const uint32_t* offsets,
                                                          const SliceDst* dst_tab,
                                                          uint32_t* out_pos) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds_ev[kRouteBlock / 64][64 * kStageStride];
+    __shared__ unsigned long long lds_dst[kRouteBlock / 64][64];
     __shared__ unsigned int wave_cnt[kRouteBlock / 64][kShardsMax];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t k = blockIdx.x * kRouteBlock + threadIdx.x;
@@ -496,25 +503,39 @@ __global__ void __launch_bounds__(kRouteBlock) tbr_pass2(RouteArgs a, const uint
         if (lane == 0) wave_cnt[wv][sv] = __popcll(m);
         if (s == sv) my_rank = __popcll(m & lt);
     }
+    const uint8_t* my = lds_ev[wv];
+    stage_wave_events(a.events, a.n, lds_ev[wv]);
     __syncthreads();
-    if (!active) return;
-    uint32_t rank = my_rank;
-    for (uint32_t w = 0; w < wv; w++) rank += wave_cnt[w][s];
-    // (the slice may live in another GPU's HBM: these stores cross xGMI, no staging copy)
-    const SliceDst d = dst_tab[s];
-    const uint32_t pos = offsets[uint64_t(s) * a.nblocks + blockIdx.x] + rank;
-    const uint4* src = reinterpret_cast<const uint4*>(&a.events[k]);
-    uint4* dst = reinterpret_cast<uint4*>(&d.events[pos]);
-    uint4 q[8];
+    // this lane's event: its slot (bit 0: a surrogate -- credit_account_id := debit_account_id)
+    unsigned long long dst = 0;
+    if (active) {
+        uint32_t rank = my_rank;
+        for (uint32_t w = 0; w < wv; w++) rank += wave_cnt[w][s];
+        const SliceDst d = dst_tab[s];
+        const uint32_t pos = offsets[uint64_t(s) * a.nblocks + blockIdx.x] + rank;
+        dst = reinterpret_cast<unsigned long long>(&d.events[pos]) | (a.ev_patch[k] ? 1ull : 0ull);
+        const uint32_t b = batch_of_guess(a.batch_ends, a.n_batches, a.n, k);
+        d.timestamps[pos] = a.batch_ts[b] - a.batch_ends[b] + k + 1;
+        out_pos[d.base + pos] = k;
+        a.tr.shard[a.base + k] = uint8_t(s);
+    }
+    lds_dst[wv][lane] = dst;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+    const uint32_t part = lane & 7;
 #pragma unroll
-    for (int i = 0; i < 8; i++) q[i] = src[i];
-    if (a.ev_patch[k]) q[2] = q[1];  // credit_account_id (bytes 32..47) := debit_account_id
-#pragma unroll
-    for (int i = 0; i < 8; i++) dst[i] = q[i];
-    const uint32_t b = batch_of_guess(a.batch_ends, a.n_batches, a.n, k);
-    d.timestamps[pos] = a.batch_ts[b] - a.batch_ends[b] + k + 1;
-    out_pos[d.base + pos] = k;
-    a.tr.shard[a.base + k] = uint8_t(s);
+    for (int i = 0; i < 8; i++) {
+        const uint32_t e = i * 8 + (lane >> 3);
+        const unsigned long long de = lds_dst[wv][e];
+        if (de == 0) continue;
+        // (a surrogate's part 2, bytes 32..47, is its part 1: credit := debit)
+        const uint32_t src_part = (part == 2 && (de & 1ull)) ? 1u : part;
+        const v4u v = *reinterpret_cast<const v4u*>(
+            __builtin_assume_aligned(my + e * kStageStride + src_part * 16, 16));
+        *reinterpret_cast<v4u*>((de & ~1ull) + part * 16) = v;
+    }
 }
 
 // Results back to call order, a surrogate's status patched to the reference's; an id that now
