@@ -1611,13 +1611,20 @@ __global__ void tr_commit(Tables T, Call<tb_transfer_t> c) {
         return;
     }
     uint64_t n_applied = 0, n_done = 0, n_slow = 0, ts_max = 0;
-    // (wave-uniform loop: chain_pre_wave combines the wave's lanes)
     const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
-    for (uint64_t kb = uint64_t(blockIdx.x) * blockDim.x + (threadIdx.x & ~63u); kb < c.n;
-         kb += stride) {
+    // A block-uniform loop: the workgroup's expires_at entries take one reservation (one returning
+    // add on expiry_count a workgroup, not a wave: same-address atomics serialise at ~11 ns on
+    // MI355X, and config 4's every wave appends). chain_pre_wave combines the wave's lanes; a wave
+    // wholly past the call skips it (its bit planes end with the call).
+    __shared__ unsigned int exp_cnt[kBlock / 64];
+    __shared__ unsigned long long exp_base;
+    const uint32_t wv = threadIdx.x >> 6;
+    for (uint64_t kb0 = uint64_t(blockIdx.x) * blockDim.x; kb0 < c.n; kb0 += stride) {
+        const uint64_t kb = kb0 + (threadIdx.x & ~63u);
         const uint32_t k = uint32_t(kb) + (threadIdx.x & 63);
         const bool active = k < c.n;
-        const ChainPre pre = chain_pre_wave(T, c, k, active, call_flags);
+        ChainPre pre{false, false, 0, -1, false, FastRec{}};
+        if (kb < c.n) pre = chain_pre_wave(T, c, k, active, call_flags);
         uint64_t exp_row = kNone;
         if (active) {
             bool applied, done, slow;
@@ -1628,22 +1635,23 @@ __global__ void tr_commit(Tables T, Call<tb_transfer_t> c) {
             n_slow += slow;
             ts_max = ts > ts_max ? ts : ts_max;
         }
-        // The wave's expires_at entries with one counter add (a returning add per entry on one
-        // word serialises: config 4 appends ~30k per 131k-event call).
+        const uint32_t lane = threadIdx.x & 63;
         const uint64_t want = __ballot(exp_row != kNone);
-        if (want) {
-            const uint32_t lane = threadIdx.x & 63;
-            const int leader = __ffsll((unsigned long long)want) - 1;
-            unsigned long long base = 0;
-            if (lane == uint32_t(leader))
-                base = atomicAdd(&T.scalars->expiry_count, (unsigned long long)__popcll(want));
-            base = __shfl(base, leader);
-            if (exp_row != kNone) {
-                const uint64_t i = base + __popcll(want & ((1ull << lane) - 1));
-                if (i < T.expiry_capacity) T.expiry[i] = exp_row;
-                else atomicOr(&T.scalars->flags, kFlagTableFull);
-            }
+        if (lane == 0) exp_cnt[wv] = uint32_t(__popcll(want));
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned int total = 0;
+            for (uint32_t w = 0; w < kBlock / 64; w++) total += exp_cnt[w];
+            exp_base = total ? atomicAdd(&T.scalars->expiry_count, (unsigned long long)total) : 0;
         }
+        __syncthreads();
+        if (exp_row != kNone) {
+            uint64_t i = exp_base + __popcll(want & ((1ull << lane) - 1));
+            for (uint32_t w = 0; w < wv; w++) i += exp_cnt[w];
+            if (i < T.expiry_capacity) T.expiry[i] = exp_row;
+            else atomicOr(&T.scalars->flags, kFlagTableFull);
+        }
+        __syncthreads();  // (exp_cnt and exp_base are the next iteration's)
     }
     // transfers objects tree key_range (groove.zig:1780): the largest committed timestamp.
     n_applied = block_reduce(n_applied, OpAdd());
