@@ -557,6 +557,10 @@ Call<Event> make_call(tbg_ctx* ctx, const Event* d_events, uint32_t n, const uin
     c.finish_scalars = nullptr;
     c.finish_seq = nullptr;
     c.seq = 0;
+    c.commit_done = nullptr;
+    c.commit_scalars = nullptr;
+    c.commit_seq = nullptr;
+    c.commit_seq_val = 0;
     return c;
 }
 
@@ -1837,12 +1841,17 @@ int stage_call_inputs(tbg_ctx* ctx, const void* events, uint64_t bytes, uint32_t
 // ends the call with TBG_EHIP and leaves the ctx failed (its tables are undefined).
 int spin_wait(tbg_ctx* ctx, unsigned int seq) {
     const double deadline = now_ms() + ctx->call_timeout_ms;
+    // (seq or any later number: the stream writes them in order, and a call's early signal may
+    // already be overwritten by its stage_out's)
+    auto reached = [&] {
+        return int32_t(__atomic_load_n(ctx->h_seq, __ATOMIC_ACQUIRE) - seq) >= 0;
+    };
     for (uint64_t spins = 1;; spins++) {
-        if (__atomic_load_n(ctx->h_seq, __ATOMIC_ACQUIRE) == seq) return 0;
+        if (reached()) return 0;
         if ((spins & 4095) == 0) {
             const hipError_t q = hipStreamQuery(ctx->stream);
             if (q == hipSuccess) {
-                if (__atomic_load_n(ctx->h_seq, __ATOMIC_ACQUIRE) == seq) return 0;
+                if (reached()) return 0;
                 return hip_ok(ctx, hipStreamSynchronize(ctx->stream), "sync") ? 0 : TBG_EHIP;
             }
             if (q != hipErrorNotReady) return hip_ok(ctx, q, "sync") ? 0 : TBG_EHIP;
@@ -2274,7 +2283,21 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
     // counted into the next mark's span -- the flow plan's -- with the GPU idle; end_call still
     // synchronises the stream before the marks are read)
     const bool spin = ctx->spin_sync;
+    // A large call after a replayed one is expected to replay too: tr_commit's last workgroup
+    // publishes the scalars block (the replay count is final there) under a sequence word of its
+    // own, and the host launches the plan while the balance kernels and stage_out run -- the
+    // launch latency that idled the GPU before the plan's first kernel. (The earlier number: the
+    // host's wait accepts any later one.)
+    const unsigned int early_seq =
+        spin && !inline_chunks && n > kInlineChunkMax && ctx->replay_hint && !ae_async_ok(ctx, n)
+            ? (++ctx->seq ? ctx->seq : ++ctx->seq) : 0u;
     const unsigned int seq = spin ? (++ctx->seq ? ctx->seq : ++ctx->seq) : 0u;
+    if (early_seq) {
+        c.commit_done = ctx->d_stage_done + 3;
+        c.commit_scalars = reinterpret_cast<unsigned long long*>(ctx->dh_scalars);
+        c.commit_seq = ctx->dh_seq;
+        c.commit_seq_val = early_seq;
+    }
     // A small device-buffer call without balance items may end in its last tr_ingest workgroup
     // (Call::finish_done); tr_commit and stage_out are queued all the same and return at once then
     // (device per-commit 27.7 -> 24.5 us, r05_g / r05_i). Host-buffer calls keep stage_out: with
@@ -2410,8 +2433,10 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
         // (the mark before the wait: recorded after it, on an idle GPU, its host cost delayed the
         // replay's first launch and was counted into the flow plan's span)
         tmark(ctx, "host_sync");
-        if (!rc) rc = spin ? spin_wait(ctx, seq)
+        if (!rc) rc = spin ? spin_wait(ctx, early_seq ? early_seq : seq)
                            : (hip_ok(ctx, hipStreamSynchronize(ctx->stream), "sync") ? 0 : TBG_EHIP);
+        // (no replay after all: the call's end is stage_out's sequence word)
+        if (!rc && early_seq && ctx->h_scalars->stats[0] == 0) rc = spin_wait(ctx, seq);
     }
     const bool replay = !rc && ctx->h_scalars->stats[0] > 0;
     if (!rc && n > kInlineChunkMax) {

@@ -1596,17 +1596,57 @@ __global__ void tr_chain_planes(Tables T, Call<tb_transfer_t> c) {
     }
 }
 
+// tr_commit's early signal (Call::commit_done). What the host reads there are scalar words that
+// tr_commit changes only with agent-scope atomics, each workgroup's by its lane 0 at the end
+// (tr_ingest's flags were final at the kernel boundary), so a workgroup is counted once lane 0's
+// atomics have completed (its vector memory counter drained) -- no L2 write-back per workgroup,
+// which an agent-scope release is (+3.5 us on config 3's tr_commit). The last one acquires, reads
+// the words with agent-scope atomic loads, copies them to the mapped copy, and publishes the
+// sequence word at system scope. (A table-full flag another lane may raise is read again at the call's end.)
+// The call's scalar words are not cleared: the kernels queued behind tr_commit still run.
+__device__ inline void commit_signal(const Tables& T, const Call<tb_transfer_t>& c) {
+    __shared__ bool last;
+    if (threadIdx.x == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        last = atomicAdd(c.commit_done, 1u) == gridDim.x - 1;
+        if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            atomicExch(c.commit_done, 0u);
+        }
+    }
+    __syncthreads();
+    if (!last || threadIdx.x >= 64) return;
+    constexpr uint32_t words = uint32_t(sizeof(DevScalars) / 8);
+    static_assert(words <= 64, "one word a lane");
+    const unsigned long long* src = reinterpret_cast<const unsigned long long*>(T.scalars);
+    if (threadIdx.x < words)
+        c.commit_scalars[threadIdx.x] =
+            __hip_atomic_load(src + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // (the wave's copies before lane 0's release, as in ingest_finish)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (threadIdx.x == 0)
+        __hip_atomic_store(c.commit_seq, c.commit_seq_val, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // tr_commit: when ingest raised no commit flag, every event is a confirmed FAST event whose
 // effects ingest already wrote; only the call's counters remain (from ingest's speculative
 // ones). Otherwise every event is re-validated.
+__device__ inline void tr_commit_body(const Tables& T, const Call<tb_transfer_t>& c);
 __global__ void tr_commit(Tables T, Call<tb_transfer_t> c) {
     if (c.finish_done && c.finish_done[1] == c.epoch) return;  // (tr_ingest ended the call)
+    tr_commit_body(T, c);
+    if (c.commit_done) commit_signal(T, c);
+}
+
+__device__ inline void tr_commit_body(const Tables& T, const Call<tb_transfer_t>& c) {
     const unsigned int call_flags = T.scalars->flags;
     if (!(call_flags & kCommitFlags)) {
-        if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) {  // (atomics: commit_signal reads them)
             const unsigned long long ts = T.scalars->spec_ts_max;
-            if (ts > T.scalars->transfers_key_max) T.scalars->transfers_key_max = ts;
-            T.scalars->stats[1] += T.scalars->spec_fast;
+            if (ts > T.scalars->transfers_key_max) atomicMax(&T.scalars->transfers_key_max, ts);
+            atomicAdd(&T.scalars->stats[1], T.scalars->spec_fast);
         }
         return;
     }

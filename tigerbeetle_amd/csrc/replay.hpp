@@ -191,6 +191,14 @@ struct Call {
     unsigned long long* finish_scalars;  // mapped pinned copy of the scalars block
     unsigned int* finish_seq;        // the pinned sequence word, or null (the host synchronises)
     unsigned int seq;
+    // Large calls the host expects to replay (tbg_ctx::replay_hint): tr_commit's last workgroup
+    // copies the scalars block (the replay count is final there) to its mapped copy and publishes
+    // commit_seq_val, so that the host launches the replay while the balance kernels and stage_out
+    // still run. commit_done = null: no such signal.
+    unsigned int* commit_done;           // tr_commit's finished workgroups (zero between calls)
+    unsigned long long* commit_scalars;  // mapped pinned copy of the scalars block
+    unsigned int* commit_seq;            // the pinned sequence word
+    unsigned int commit_seq_val;
 };
 
 constexpr uint32_t kNone32 = 0xFFFFFFFFu;
