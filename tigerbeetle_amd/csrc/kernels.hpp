@@ -1370,21 +1370,25 @@ __device__ inline void commit_post_void(const Tables& T, const Call<tb_transfer_
     const bool post = (t.flags & TB_TRANSFER_POST_PENDING) != 0;
     const u128 p_amount = U(p.amount);
     const u128 amount = post ? (U(t.amount) == kU128Max ? p_amount : U(t.amount)) : p_amount;
-    tb_transfer_t o;
-    o.id = t.id;
-    o.debit_account_id = p.debit_account_id;
-    o.credit_account_id = p.credit_account_id;
-    o.amount = W(amount);
-    o.pending_id = t.pending_id;
-    o.user_data_128 = W(U(t.user_data_128) > 0 ? U(t.user_data_128) : U(p.user_data_128));  // (scalar select: a struct select keeps both rows in scratch)
-    o.user_data_64 = t.user_data_64 > 0 ? t.user_data_64 : p.user_data_64;
-    o.user_data_32 = t.user_data_32 > 0 ? t.user_data_32 : p.user_data_32;
-    o.timeout = 0;
-    o.ledger = p.ledger;
-    o.code = p.code;
-    o.flags = t.flags;
-    o.timestamp = ts;
-    T.tr_rows[row] = o;
+    // The row as eight 16-byte words stored straight from registers (a tb_transfer_t local copied
+    // by assignment stayed in scratch: 72 bytes a lane, and each scratch load waited for every
+    // memory operation issued before it). Scalar selects: a struct select keeps both rows in scratch.
+    auto q = [](uint64_t lo, uint64_t hi) {
+        return make_uint4(uint32_t(lo), uint32_t(lo >> 32), uint32_t(hi), uint32_t(hi >> 32));
+    };
+    const u128 ud128 = U(t.user_data_128) > 0 ? U(t.user_data_128) : U(p.user_data_128);
+    const uint64_t ud64 = t.user_data_64 > 0 ? t.user_data_64 : p.user_data_64;
+    const uint32_t ud32 = t.user_data_32 > 0 ? t.user_data_32 : p.user_data_32;
+    uint4* o = reinterpret_cast<uint4*>(&T.tr_rows[row]);
+    o[0] = q(t.id.lo, t.id.hi);
+    o[1] = q(p.debit_account_id.lo, p.debit_account_id.hi);
+    o[2] = q(p.credit_account_id.lo, p.credit_account_id.hi);
+    o[3] = q(uint64_t(amount), uint64_t(amount >> 64));
+    o[4] = q(t.pending_id.lo, t.pending_id.hi);
+    o[5] = q(uint64_t(ud128), uint64_t(ud128 >> 64));
+    o[6] = make_uint4(uint32_t(ud64), uint32_t(ud64 >> 32), ud32, 0u);  // (timeout 0)
+    o[7] = make_uint4(p.ledger, uint32_t(p.code) | (uint32_t(t.flags) << 16), uint32_t(ts),
+                      uint32_t(ts >> 32));
     T.tr_status[pr] = post ? TB_PENDING_POSTED : TB_PENDING_VOIDED;
     // The balance words as atomic_sub_u128 / atomic_add_u128 would update them, the four low-word
     // adds in flight together and their carries after (FAST: both amounts are < 2^64,
