@@ -359,16 +359,24 @@ __device__ inline void walk_dpp_add(uint64_t& v) {
     const uint32_t hi = walk_dpp<kCtrl, kRowMask>(uint32_t(v >> 32));
     v += walk_u64(lo, hi);
 }
-__device__ inline uint64_t walk_dpp_sum64(uint64_t v) {
+// (the inclusive scan: lane i holds the sum over lanes 0..i)
+__device__ inline uint64_t walk_dpp_scan64(uint64_t v) {
     walk_dpp_add<0x111, 0xF>(v);  // row_shr:1
     walk_dpp_add<0x112, 0xF>(v);  // row_shr:2
     walk_dpp_add<0x114, 0xF>(v);  // row_shr:4
     walk_dpp_add<0x118, 0xF>(v);  // row_shr:8
     walk_dpp_add<0x142, 0xA>(v);  // row_bcast:15 into rows 1 and 3
     walk_dpp_add<0x143, 0xC>(v);  // row_bcast:31 into rows 2 and 3
-    return walk_u64(uint32_t(__builtin_amdgcn_readlane(int(uint32_t(v)), 63)),
-                    uint32_t(__builtin_amdgcn_readlane(int(uint32_t(v >> 32)), 63)));
+    return v;
 }
+__device__ inline uint64_t walk_lane(uint64_t v, uint32_t j) {
+    return walk_u64(uint32_t(__builtin_amdgcn_readlane(int(uint32_t(v)), j)),
+                    uint32_t(__builtin_amdgcn_readlane(int(uint32_t(v >> 32)), j)));
+}
+__device__ inline u128 walk_lane(u128 v, uint32_t j) {
+    return (u128(walk_lane(uint64_t(v >> 64), j)) << 64) | walk_lane(uint64_t(v), j);
+}
+__device__ inline uint64_t walk_dpp_sum64(uint64_t v) { return walk_lane(walk_dpp_scan64(v), 63); }
 __device__ inline uint64_t walk_wave_sum(uint64_t v) { return walk_dpp_sum64(v); }
 // u128: each 32-bit limb summed in u64 (64 lanes: < 2^38), then recombined with the carries.
 __device__ inline u128 walk_wave_sum(u128 v) {
@@ -376,6 +384,14 @@ __device__ inline u128 walk_wave_sum(u128 v) {
     const uint64_t s0 = walk_dpp_sum64(lo & 0xFFFFFFFFull), s1 = walk_dpp_sum64(lo >> 32);
     const uint64_t s2 = walk_dpp_sum64(hi & 0xFFFFFFFFull), s3 = walk_dpp_sum64(hi >> 32);
     return u128(s0) + (u128(s1) << 32) + (u128(s2) << 64) + (u128(s3) << 96);
+}
+// Exclusive wave scans (lane i: the sum over lanes 0..i-1), u64 or u128 as above.
+__device__ inline uint64_t walk_wave_scan_excl(uint64_t v) { return walk_dpp_scan64(v) - v; }
+__device__ inline u128 walk_wave_scan_excl(u128 v) {
+    const uint64_t lo = uint64_t(v), hi = uint64_t(v >> 64);
+    const uint64_t s0 = walk_dpp_scan64(lo & 0xFFFFFFFFull), s1 = walk_dpp_scan64(lo >> 32);
+    const uint64_t s2 = walk_dpp_scan64(hi & 0xFFFFFFFFull), s3 = walk_dpp_scan64(hi >> 32);
+    return u128(s0) + (u128(s1) << 32) + (u128(s2) << 64) + (u128(s3) << 96) - v;
 }
 
 // (kDbg: TBG_FLOW_DEBUG's counters and timers; the production instance holds none of them:
@@ -633,10 +649,8 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
             // not_exceed_debits: used = cpe + cpo, cap = dpo -- a created mine event adds to
             // `used`, a created other event to `cap`. The window resolves in wave-wide steps:
             // (A) if used + (every mine amount) <= cap, every mine check passes whatever the
-            // other events do; (B) else, with the state fixed, every event up to the first one
-            // that would be created (or whose other verdict is unknown) is not created -- a
-            // ballot finds it, it is applied, and the scan resumes after it. Steps are created
-            // events + polls, not events: config 3's exhausted owners fail most of theirs.
+            // other events do; (B) else the window resolves in speculative steps (below): steps
+            // are disagreements + polls, not events.
             V used = owner_dm ? V(dpe) + V(dpo) : V(cpe) + V(cpo);
             V cap = owner_dm ? V(cpo) : V(dpo);
             const V used0 = used, cap0 = cap;
@@ -679,36 +693,50 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
             } else {
                 const uint64_t tb0 = kDbg ? wall_clock64() : 0;
                 uint64_t rem = vmask;
+                // Each step decides every remaining event on the state at the step's start (the
+                // single-event rule below), then checks each again against that state plus the
+                // amounts of the events so created before it (exclusive wave scans): up to the
+                // first event the two disagree on, or that waits on an unknown verdict with its
+                // own check passing, the speculation is the serial outcome, and the step applies
+                // all of it. Steps are disagreements + polls, not created events (wide amounts:
+                // most events pass, a few huge ones fail -- a step per created event was ~11 a
+                // window).
                 while (rem != 0 && !stalled) {
                     n_iter++;
                     const bool in = (rem >> lane) & 1;
-                    const bool ok_mine = !l_mine || used + amt <= cap;
+                    const bool kok = ((known_ok >> lane) & 1) != 0;
+                    const bool l_debit = ((debit_m >> lane) & 1) != 0;
                     const bool unknown = l_other && !((known >> lane) & 1);
-                    const bool creates = ok_mine && (!l_other || ((known_ok >> lane) & 1));
-                    // (an unknown verdict matters only when the own check passes: else the event
-                    // is not created, and a credit event's other side is a walked owner -- the
-                    // writer of its outcome)
-                    const uint64_t brk = __ballot(in && ((unknown && ok_mine) || creates));
-                    const uint64_t okm = __ballot(in && l_mine && ok_mine);
-                    // (not created: a debit event's debit side fails when it is the owner's check,
-                    // a credit event's when the other owner said so)
-                    const uint64_t drf = __ballot(in && ((l_mine && !ok_mine && ((debit_m >> lane) & 1)) ||
-                                                         (l_other && !((debit_m >> lane) & 1) &&
-                                                          !((known_ok >> lane) & 1))));
-                    const uint64_t before = brk ? ((brk & (0 - brk)) - 1) & rem : rem;
+                    const bool ok0 = !l_mine || used + amt <= cap;
+                    const bool cr0 = in && ok0 && (!l_other || kok);
+                    const V am = cr0 && l_mine ? amt : V(0), ao = cr0 && !l_mine ? amt : V(0);
+                    const V pm = walk_wave_scan_excl(am), po = walk_wave_scan_excl(ao);
+                    const bool ok1 = !l_mine || used + pm + amt <= cap + po;
+                    const bool cr1 = ok1 && (!l_other || kok);
+                    const uint64_t stop = __ballot(in && (cr1 != cr0 || (unknown && ok1)));
+                    const uint64_t before = stop ? ((stop & (0 - stop)) - 1) & rem : rem;
+                    const uint64_t crm = __ballot(in && cr1);
+                    const uint64_t okm = __ballot(in && l_mine && ok1);
+                    // (not created: as in the single-event rule)
+                    const uint64_t drf = __ballot(in && ((l_mine && !ok1 && l_debit) ||
+                                                         (l_other && !l_debit && !kok)));
+                    created_m |= before & crm;
                     decided |= before & mine_m;
                     myok_m |= before & okm;
                     drfail_m |= before & drf;
                     rem &= ~before;
-                    if (brk == 0) break;
-                    const uint32_t j = uint32_t(__builtin_ctzll(brk));
+                    // the state after `before`: the sums up to the stop (or over the window)
+                    const uint32_t j = stop ? uint32_t(__builtin_ctzll(stop)) : 63u;
+                    used += walk_lane(stop ? pm : pm + am, j);
+                    cap += walk_lane(stop ? po : po + ao, j);
+                    if (stop == 0) break;
                     const uint64_t bit = 1ull << j;
-                    if ((other_m & bit) && !(known & bit)) {
+                    if ((other_m & bit) && !(known & bit) && ((okm >> j) & 1 || !(mine_m & bit))) {
                         // Its own check first (the state is final up to j): the other owner may
                         // be waiting on this very verdict.
                         if (mine_m & bit) {
                             decided |= bit;
-                            if ((okm >> j) & 1) myok_m |= bit;
+                            myok_m |= bit;
                         }
                         refresh(other_m & ~known & rem);
                         if (!(known & bit)) {
@@ -717,18 +745,7 @@ __global__ void __launch_bounds__(kWalkWaves * 64) lanes_walk(Tables T, Call<tb_
                         }
                         continue;
                     }
-                    const V a = V(walk_u64(__builtin_amdgcn_readlane(cur.amt_lo, j),
-                                           __builtin_amdgcn_readlane(cur.amt_hi, j)));
-                    created_m |= bit;
-                    if (mine_m & bit) {
-                        decided |= bit;
-                        myok_m |= bit;
-                        used += a;
-                    } else {
-                        cap += a;
-                    }
-                    rem &= ~bit;
-                    publish();
+                    publish();  // (j disagreed: the next step starts at it, on the new state)
                 }
                 if (kDbg) t_b += wall_clock64() - tb0;
             }

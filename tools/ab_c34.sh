@@ -8,7 +8,7 @@ for rep in 1 2; do
   for v in "$@"; do
     lib=""
     [ "$v" = default ] || lib=$PWD/tigerbeetle_amd/lib/variants/libtbg_$v.so
-    TBG_LIB=$lib timeout -k 10 300 python3 tools/bench_configs.py > $out/c34_${v}_$rep.json 2> $out/c34_${v}_$rep.err || { tail -5 $out/c34_${v}_$rep.err; exit 1; }
+    TBG_LIB=$lib timeout -k 10 300 python3 tools/bench_configs.py $AB_ARGS > $out/c34_${v}_$rep.json 2> $out/c34_${v}_$rep.err || { tail -5 $out/c34_${v}_$rep.err; exit 1; }
     python3 - $out/c34_${v}_$rep.json $v <<'PY'
 import json, sys
 for line in open(sys.argv[1]):
