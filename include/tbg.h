@@ -284,7 +284,9 @@ int tbg_debug_serial_replay(tbg_ctx* ctx, int enable);
 int tbg_debug_ae_sync(tbg_ctx* ctx, int enable);
 
 /* Per-kernel timing with HIP events on the call's stream (off by default; resets the totals);
- * enable == 2 records only the host-wall phases of host-buffer calls (host:*), no HIP events.
+ * enable == 2 records only the host-wall phases of host-buffer calls (host:*), no HIP events;
+ * enable == 3 records only the marks that bound a call's device spans (no per-kernel entries: each
+ * mark recorded between two launches idles the GPU a few microseconds).
  * tbg_profile_read returns 1 and fills name / accumulated milliseconds / launches for entry
  * `index`, or 0 past the last entry. */
 int tbg_profile(tbg_ctx* ctx, int enable);

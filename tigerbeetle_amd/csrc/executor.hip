@@ -320,6 +320,10 @@ struct tbg_ctx {
     // Per-kernel timing (tbg_profile): HIP events recorded on the call's stream between launches.
     bool timing = false;
     bool timing_host = false;  // host phases only (tbg_profile(ctx, 2): no HIP events)
+    // Span marks only (tbg_profile(ctx, 3)): each HIP event recorded between two launches idles
+    // the GPU ~6 us (profiles/r06_lean/), so the per-kernel marks inflate a call's device time by
+    // ~10 % on configs 3 / 4; these keep only the marks that bound the call's device spans.
+    bool timing_lean = false;
     static constexpr int kMaxMarks = 32;
     hipEvent_t marks[kMaxMarks] = {};
     const char* mark_names[kMaxMarks] = {};
@@ -427,8 +431,16 @@ int sync_scalars(tbg_ctx* ctx) {
     return 0;
 }
 
+// The marks tbg_profile(ctx, 3) records: the call's start, the host's waits, the end of a
+// replayed call's work ("call"), the skipped spans ('-'), the AccountEvents and pulse spans, and
+// the accounts' (their calls keep every mark).
+bool lean_mark(const char* n) {
+    return n[0] == '-' || !strcmp(n, "begin") || !strcmp(n, "host_sync") || !strcmp(n, "call") ||
+           !strcmp(n, "account_events") || !strncmp(n, "pulse:", 6) || !strncmp(n, "acc_", 4);
+}
 void tmark(tbg_ctx* ctx, const char* name) {
     if (!ctx->timing || ctx->n_marks >= tbg_ctx::kMaxMarks) return;
+    if (ctx->timing_lean && !lean_mark(name)) return;
     if (!ctx->marks[ctx->n_marks]) (void)hipEventCreate(&ctx->marks[ctx->n_marks]);
     (void)hipEventRecord(ctx->marks[ctx->n_marks], ctx->stream);
     ctx->mark_names[ctx->n_marks++] = name;
@@ -2447,7 +2459,10 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
     ctx->early_done = !rc && ctx->early_dst && !replay;  // (only the replay rewrites results)
     if (replay && (ctx->h_scalars->flags & kFlagImported)) rc = check_imported_indexes(ctx, true);
     if (replay && !rc) rc = run_replay(ctx, c, true, false, pre_selected);
-    if (!rc && ((ctx->h_scalars->flags & kFlagPostVoid) || c.pnt_force)) rc = pnt_resolve(ctx, c);
+    const bool pnt = !rc && ((ctx->h_scalars->flags & kFlagPostVoid) || c.pnt_force);
+    if (pnt) rc = pnt_resolve(ctx, c);
+    // (lean marks: the end of the work queued after the host's wait)
+    if (!rc && ctx->timing_lean && (replay || pnt)) tmark(ctx, "call");
     if (!rc) {
         ctx->pnt_last = c;
         ctx->pnt_last_valid = c.pnt_force != 0;
@@ -3397,7 +3412,8 @@ int tbg_debug_ae_sync(tbg_ctx* ctx, int enable) {
 int tbg_profile(tbg_ctx* ctx, int enable) {
     TBG_DEVICE_SCOPE(ctx);
     if (!ctx) return TBG_EINVAL;
-    ctx->timing = enable == 1;
+    ctx->timing = enable == 1 || enable == 3;
+    ctx->timing_lean = enable == 3;
     ctx->timing_host = enable != 0;
     ctx->prof_names.clear();
     ctx->prof_ms.clear();

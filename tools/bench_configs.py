@@ -6,7 +6,9 @@ through the host-buffer C ABI (tbg_create_transfers: PCIe copies included) and t
 oracle on the same batches; every call's results and, at the end, every Account / Transfer row,
 TransferPending status and AccountEvent must be byte-identical (tests/parity.py). Prints one JSON
 line per config with the GPU and oracle rates over the create_transfers calls, and the device
-time of the calls' kernels (HIP events on the executor's stream).
+time of the calls' kernels (HIP events on the executor's stream: `device_ms` from the marks that
+bound each call's device spans, `kernels_ms` the per-kernel split of a second run with a mark
+between every two kernels, whose sum is `device_ms_per_kernel_marks`).
 
 Usage: python tools/bench_configs.py [--transfers N] [--batches B] [--configs 3,4]
   --batches 1 runs every call as one replica commit of one 8189-event batch.
@@ -72,6 +74,25 @@ def line(name, p, n, t_wall, extra):
 
 
 def run(config, n, batches, profile=True, amounts="exp"):
+    """One validated run per profile mode: the device time from the span marks (tbg_profile mode
+    3: each HIP event recorded between two launches idles the GPU a few microseconds, so the
+    per-kernel marks inflate it), the per-kernel split from the per-kernel marks (mode 1)."""
+    if not profile or os.environ.get("TBG_BENCH_PROFILE_MODE"):
+        return run_mode(config, n, batches, profile, amounts)
+    os.environ["TBG_BENCH_PROFILE_MODE"] = "3"
+    try:
+        lean = run_mode(config, n, batches, True, amounts)
+    finally:
+        del os.environ["TBG_BENCH_PROFILE_MODE"]
+    full = run_mode(config, n, batches, True, amounts)
+    full["device_ms_per_kernel_marks"] = full["device_ms"]
+    full["device_ms"] = lean["device_ms"]
+    full["device_transfers_per_s"] = lean["device_transfers_per_s"]
+    full["spans_ms"] = lean["kernels_ms"]
+    return full
+
+
+def run_mode(config, n, batches, profile=True, amounts="exp"):
     t0 = time.perf_counter()
     p = Pair(account_capacity=1 << 14, transfer_capacity=n + (1 << 12),
              batch_events_max=max(BATCH * batches, 1 << 14), batch_count_max=batches)
