@@ -441,6 +441,11 @@ bool lean_mark(const char* n) {
 void tmark(tbg_ctx* ctx, const char* name) {
     if (!ctx->timing || ctx->n_marks >= tbg_ctx::kMaxMarks) return;
     if (ctx->timing_lean && !lean_mark(name)) return;
+    // (a skipped span right after "call" is empty: the next span starts at "call" instead of a
+    // second event recorded back to back)
+    if (ctx->timing_lean && name[0] == '-' && ctx->n_marks > 0 &&
+        !strcmp(ctx->mark_names[ctx->n_marks - 1], "call"))
+        return;
     if (!ctx->marks[ctx->n_marks]) (void)hipEventCreate(&ctx->marks[ctx->n_marks]);
     (void)hipEventRecord(ctx->marks[ctx->n_marks], ctx->stream);
     ctx->mark_names[ctx->n_marks++] = name;
