@@ -1896,7 +1896,9 @@ struct AeDense {
                               // mapped pinned word the host reads after its synchronisation)
     unsigned int* claim;      // device words: [0] == epoch: ae_dense_stage refused the call (the
                               // later kernels return at once; ae_dense_suffix's block 0 forwards it
-                              // to `fail`); [1] == epoch: a suffix wave has written `fail`
+                              // to `fail`); [1] == epoch: a suffix wave has written `fail`;
+                              // [2] == epoch: a created event moves a pending balance (else the
+                              // pending pair's partials are neither written nor read: all zero)
     uint32_t epoch;
     tb_account_event_t* log;
     AeRef* refs;
@@ -1961,6 +1963,7 @@ __global__ void ae_dense_stage(AeDense A) {
         e[4] = make_uint4(status, 0, 0, 0);
     }
     if (__any(bad) && (threadIdx.x & 63) == 0) A.claim[0] = A.epoch;
+    if (__any(o.dpe != 0) && (threadIdx.x & 63) == 0) A.claim[2] = A.epoch;
     if (k < c.n) A.touch[k] = o;
 }
 
@@ -1971,6 +1974,7 @@ __global__ void __launch_bounds__(kAeWinThreads) ae_dense_partials(AeDense A) {
     __shared__ uint32_t wave_cnt[kAeWinThreads / 64];
     const uint32_t tid = threadIdx.x, s = blockIdx.x >> 1, q = blockIdx.x & 1;
     if (ae_dense_refused(A)) return;  // (written before this launch: uniform over the block)
+    if (q == 0 && A.claim[2] != A.epoch) return;  // (no pending deltas in the call)
     for (uint32_t a = tid; a < A.rows; a += kAeWinThreads) {
         Rd[a] = 0;
         Rc[a] = 0;
@@ -1997,7 +2001,7 @@ __global__ void __launch_bounds__(kAeWinThreads) ae_dense_partials(AeDense A) {
         out[a] = Rd[a];
         out[A.rows + a] = Rc[a];
     }
-    if (q == 0 && tid == 0) {
+    if (q == 1 && tid == 0) {  // (the posted pair's workgroups always run)
         uint32_t total = 0;
         for (uint32_t w = 0; w < kAeWinThreads / 64; w++) total += wave_cnt[w];
         A.slice_count[s] = total;
@@ -2024,8 +2028,8 @@ __global__ __launch_bounds__(kAeSufThreads) void ae_dense_suffix(AeDense A) {
     }
     const uint32_t keys = 2 * A.rows;
     const uint32_t t = blockIdx.x * 64 + lane;
-    const bool live = t < 2 * keys;
-    const uint32_t q = live ? t / keys : 0, key = live ? t % keys : 0;
+    const uint32_t q = t < 2 * keys ? t / keys : 0, key = t < 2 * keys ? t % keys : 0;
+    const bool live = t < 2 * keys && (q == 1 || A.claim[2] == A.epoch);  // (pending: all zero)
     uint32_t* p = A.partials + uint64_t(q) * A.slices * keys + key;
     const uint32_t per = (A.slices + kAeSufGroups - 1) / kAeSufGroups;
     const uint32_t lo = min(g * per, A.slices), hi = min(lo + per, A.slices);
@@ -2181,13 +2185,15 @@ __global__ void __launch_bounds__(kAeDenseEmitThreads) ae_dense_later(AeDense A)
     // Every touch's later deltas: the suffix from this slice less its account's sums so far.
     const uint32_t* suf_pe = A.partials + (uint64_t(0) * A.slices + s) * 2 * A.rows;
     const uint32_t* suf_po = A.partials + (uint64_t(1) * A.slices + s) * 2 * A.rows;
+    const bool pend = A.claim[2] == A.epoch;  // (else the pending partials were not written)
 #pragma unroll
     for (uint32_t m = 0; m < N; m++) {
         run = f[m] ? v[m] : ae_add4(run, v[m]);
         const uint32_t key = k[m];
         if (key == ~0u) continue;
         const uint32_t acc = key >> kAeDenseTixBits;
-        L.later[key & kTixMask] = make_uint4(suf_pe[acc] - run.x, suf_pe[A.rows + acc] - run.y,
+        const uint32_t pe_d = pend ? suf_pe[acc] : 0u, pe_c = pend ? suf_pe[A.rows + acc] : 0u;
+        L.later[key & kTixMask] = make_uint4(pe_d - run.x, pe_c - run.y,
                                              suf_po[acc] - run.z, suf_po[A.rows + acc] - run.w);
     }
     uint64_t bals[kAeDenseEv];

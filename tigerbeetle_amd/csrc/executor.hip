@@ -1559,7 +1559,7 @@ int ae_dense_prefix(tbg_ctx* ctx, const Call<tb_transfer_t>& c) {
               dev_alloc(ctx, &ctx->ae_dense_ts, 2, false) &&
               dev_alloc(ctx, &ctx->ae_dense_later, 2 * cap, false) &&
               dev_alloc(ctx, &ctx->ae_dense_pos, cap, false) &&
-              dev_alloc(ctx, &ctx->ae_dense_claim, 2, true)))
+              dev_alloc(ctx, &ctx->ae_dense_claim, 4, true)))
             return TBG_ENOMEM;
         // (ae_dense_records' min / max words; a kernel on the stream: a synchronous copy waited for
         // every stream, ~10 ms inside config 4's first dense call)

@@ -122,7 +122,7 @@ __global__ void flow_heads(Tables T, Call<tb_transfer_t> c, FlowPlan P) {
     bool head = true;
     if (s > 0 && P.slow_list[s - 1] == k - 1 && (c.events[k - 1].flags & TB_TRANSFER_LINKED)) {
         // k continues k - 1's chain unless k opens a new batch (a chain cannot cross one).
-        const uint32_t b = batch_of(c.batch_ends, c.n_batches, k);
+        const uint32_t b = batch_of_guess(c.batch_ends, c.n_batches, c.n, k);
         head = batch_start_of(c, b) == k;
     }
     P.head8[s] = head;

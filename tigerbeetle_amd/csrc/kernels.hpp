@@ -2223,7 +2223,7 @@ __device__ inline void replay_chain_step_at(Replay& R, const Call<Event>& c, uin
 // The event's batch facts, from the batch bounds (serial replay) or precomputed (flow plan).
 template <typename Event>
 __device__ inline StepInfo step_info(const Call<Event>& c, uint32_t k, uint16_t imported_flag) {
-    const uint32_t b = batch_of(c.batch_ends, c.n_batches, k);
+    const uint32_t b = batch_of_guess(c.batch_ends, c.n_batches, c.n, k);
     StepInfo si;
     si.ts_event = ts_event_of(c, b, k);
     si.batch = b;
