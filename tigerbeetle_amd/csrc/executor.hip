@@ -2087,7 +2087,7 @@ tbg_ctx* tbg_open(const tbg_options* options) {
             return std::max(lo, std::min(hi, v));
         };
         k.flow_lpw = env_u("TBG_FLOW_LPW", kFlowLanesPerWave, 1, 64);
-        k.flow_waves = env_u("TBG_FLOW_WAVES", kFlowWaves, 1, kFlowThreads / 64);
+        k.flow_waves = env_u("TBG_FLOW_WAVES", kFlowWaves, 1, kFlowReplayThreads / 64);
         k.flow_blocks = env_u("TBG_FLOW_BLOCKS", kFlowBlocks, 1, kFlowLanesMax / (k.flow_waves * k.flow_lpw));
         k.flow_xcd = env_u("TBG_FLOW_XCD", 1, 1, 8);
         k.flow_backoff = env_u("TBG_FLOW_BACKOFF", 1, 0, 1);

@@ -39,7 +39,10 @@
 
 namespace tbg {
 
-constexpr uint32_t kFlowThreads = 512;      // threads of an engine workgroup
+constexpr uint32_t kFlowThreads = 512;      // threads of a lanes workgroup (kLanesMax)
+// flow_replay's workgroup bound: 4 waves (the default shape) leave a lane 512 VGPRs; at 512
+// threads the replay's registers spilled to scratch
+constexpr uint32_t kFlowReplayThreads = 256;
 constexpr uint32_t kFlowLanesMax = 8192;    // lanes running units, over all engine workgroups
 constexpr uint32_t kFlowLanesPerWave = 1;   // default engine shape (TBG_FLOW_LPW / _WAVES / _BLOCKS)
 constexpr uint32_t kFlowWaves = 4;
@@ -186,7 +189,7 @@ struct SelectHeads {
 // anything another unit wrote. The queue counters live in global memory (P.engine).
 // (kDbg: TBG_FLOW_DEBUG's counters; the production instance holds none of them)
 template <bool kDbg>
-__global__ void __launch_bounds__(kFlowThreads) flow_replay(Tables T, Call<tb_transfer_t> c,
+__global__ void __launch_bounds__(kFlowReplayThreads) flow_replay(Tables T, Call<tb_transfer_t> c,
                                                            FlowPlan P) {
     if (P.skip && *P.skip) return;
     if (blockIdx.x % P.xcd_stride) return;
@@ -265,6 +268,7 @@ __global__ void __launch_bounds__(kFlowThreads) flow_replay(Tables T, Call<tb_tr
                 ev = ev_next;
             }
         }
+        R.flush_adds();  // (the unit's last carries, before its release)
         if (kDbg) {
             exec_cycles += wall_clock64() - t0;
             ev_count += end - begin;

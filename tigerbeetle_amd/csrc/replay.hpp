@@ -386,14 +386,16 @@ struct Replay {
         undo_len = scope.undo_len;
         scope.open = false;
     }
-    __device__ void log_status(uint64_t row) {
+    // (`old`: the status as the event read it -- a load here, behind the event's stores, waited
+    // for all of them in issue order)
+    __device__ void log_status(uint64_t row, uint8_t old) {
         if (!scope.open) return;
         if (undo_len >= undo_cap) {
             overflow = true;
             return;
         }
         undo[undo_len].kind_index = kUndoStatus | row;
-        undo[undo_len].row.timestamp = T.tr_status[row];
+        undo[undo_len].row.timestamp = old;
         undo_len++;
     }
     // (`old`: the row as this event read it, logged from registers). Only the balances and flags
@@ -429,35 +431,60 @@ struct Replay {
     // credits_posted of row a (da) and of row b (db); kNone32 skips a row. Every low-word atomic
     // goes out before any returns (one round trip to the point of coherence, not one per field),
     // then the carries.
-    __device__ void add_balances2(uint32_t a, const u128 (&da)[4], uint32_t b, const u128 (&db)[4]) {
-        uint64_t old[8];
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const uint32_t row = j < 4 ? a : b;
-            const u128 d = j < 4 ? da[j] : db[j - 4];
-            old[j] = 0;
-            if (row != kNone32 && uint64_t(d) != 0) {
-                tb_uint128_t* f = &T.acc_rows[row].debits_pending + (j & 3);
-                old[j] = atomicAdd((unsigned long long*)&f->lo, (unsigned long long)uint64_t(d));
-            }
+    // Adds pending delta P and posted delta Q to row a's debits and row b's credits (modular;
+    // kNone32 skips a row): every call's deltas have this shape. The low-word atomics go out
+    // together. Flow mode defers their returns: the carries into the high words (and the hazard
+    // marks) are applied by flush_adds -- called after the next event's loads are issued, and at
+    // the unit's end -- so that the atomics' round trip overlaps the next event's loads instead
+    // of adding one to every event (a returned value is waited for in issue order, behind every
+    // store the event made before it). No replayed event reads these balances, and the adds
+    // commute (a chain's rollback subtracts whole deltas).
+    // (scalar members, no array: an array member kept the whole Replay in scratch)
+    uint64_t add_o0 = 0, add_o1 = 0, add_o2 = 0, add_o3 = 0;  // a.dpe, a.dpo, b.cpe, b.cpo
+    uint64_t add_p_lo = 0, add_p_hi = 0, add_q_lo = 0, add_q_hi = 0;  // (no u128 members either)
+    uint32_t add_a = kNone32, add_b = kNone32;
+    bool add_pending = false;
+    // The carry of one field's deferred add into its high word: returns the new high word (0: none).
+    __device__ __attribute__((always_inline)) uint64_t add_carry(tb_uint128_t* f, uint64_t lo, uint64_t dhi, uint64_t old) {
+        const uint64_t hi = dhi + ((lo != 0 && old + lo < old) ? 1 : 0);
+        return hi ? atomicAdd((unsigned long long*)&f->hi, (unsigned long long)hi) + hi : 0;
+    }
+    __device__ __attribute__((always_inline)) void flush_adds() {
+        if (!add_pending) return;
+        add_pending = false;
+        if (add_a != kNone32) {
+            tb_account_t& r = T.acc_rows[add_a];
+            const uint64_t h = add_carry(&r.debits_pending, add_p_lo, add_p_hi, add_o0) |
+                               add_carry(&r.debits_posted, add_q_lo, add_q_hi, add_o1);
+            if (h >= kHazardHiLimit) acc_hazard_set(T.acc_index, T.acc_entry_of, add_a, kHazardHigh);
         }
-        uint64_t hi_a = 0, hi_b = 0;
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const uint32_t row = j < 4 ? a : b;
-            const u128 d = j < 4 ? da[j] : db[j - 4];
-            if (row == kNone32) continue;
-            const uint64_t lo = uint64_t(d);
-            const uint64_t hi = uint64_t(d >> 64) + ((lo != 0 && old[j] + lo < old[j]) ? 1 : 0);
-            if (hi) {
-                tb_uint128_t* f = &T.acc_rows[row].debits_pending + (j & 3);
-                const uint64_t h = atomicAdd((unsigned long long*)&f->hi, (unsigned long long)hi) + hi;
-                if (j < 4) hi_a |= h;
-                else hi_b |= h;
-            }
+        if (add_b != kNone32) {
+            tb_account_t& r = T.acc_rows[add_b];
+            const uint64_t h = add_carry(&r.credits_pending, add_p_lo, add_p_hi, add_o2) |
+                               add_carry(&r.credits_posted, add_q_lo, add_q_hi, add_o3);
+            if (h >= kHazardHiLimit) acc_hazard_set(T.acc_index, T.acc_entry_of, add_b, kHazardHigh);
         }
-        if (a != kNone32 && hi_a >= kHazardHiLimit) acc_hazard_set(T.acc_index, T.acc_entry_of, a, kHazardHigh);
-        if (b != kNone32 && hi_b >= kHazardHiLimit) acc_hazard_set(T.acc_index, T.acc_entry_of, b, kHazardHigh);
+    }
+    __device__ __attribute__((always_inline)) void add_pq(uint32_t a, uint32_t b, u128 P, u128 Q) {
+        flush_adds();
+        auto add_lo = [&](uint32_t row, tb_uint128_t* f, u128 d) -> uint64_t {
+            return row != kNone32 && uint64_t(d) != 0
+                       ? atomicAdd((unsigned long long*)&f->lo, (unsigned long long)uint64_t(d))
+                       : 0ull;
+        };
+        tb_account_t* A = T.acc_rows;
+        add_o0 = add_lo(a, &A[a].debits_pending, P);
+        add_o1 = add_lo(a, &A[a].debits_posted, Q);
+        add_o2 = add_lo(b, &A[b].credits_pending, P);
+        add_o3 = add_lo(b, &A[b].credits_posted, Q);
+        add_a = a;
+        add_b = b;
+        add_p_lo = uint64_t(P);
+        add_p_hi = uint64_t(P >> 64);
+        add_q_lo = uint64_t(Q);
+        add_q_hi = uint64_t(Q >> 64);
+        add_pending = true;
+        if (!concurrent) flush_adds();
         if (!scope.open) return;
         if (undo_len + (a != kNone32) + (b != kNone32) > undo_cap) {
             overflow = true;
@@ -467,17 +494,16 @@ struct Replay {
         for (int r = 0; r < 2; r++) {
             const uint32_t row = r == 0 ? a : b;
             if (row == kNone32) continue;
-            const u128* d = r == 0 ? da : db;
             UndoEntry& u = undo[undo_len++];
             u.kind_index = kUndoDelta | row;
-            u.row.debits_pending = W(d[0]);
-            u.row.debits_posted = W(d[1]);
-            u.row.credits_pending = W(d[2]);
-            u.row.credits_posted = W(d[3]);
+            u.row.debits_pending = W(r == 0 ? P : u128(0));
+            u.row.debits_posted = W(r == 0 ? Q : u128(0));
+            u.row.credits_pending = W(r == 0 ? u128(0) : P);
+            u.row.credits_posted = W(r == 0 ? u128(0) : Q);
         }
     }
-    __device__ void update_status(uint64_t row, uint8_t status) {
-        log_status(row);
+    __device__ void update_status(uint64_t row, uint8_t status, uint8_t old) {
+        log_status(row, old);
         T.tr_status[row] = status;
     }
     // The transfers objects tree key_range.key_max (groove.zig:1780) after an insert at `ts`.
@@ -684,7 +710,8 @@ __device__ uint32_t replay_post_or_void(Replay& R, const C& c, uint32_t k, uint6
     if ((f & TB_TRANSFER_VOID_PENDING) && amount < p_amount)
         return TB_CT_PENDING_TRANSFER_HAS_DIFFERENT_AMOUNT;
 
-    switch (T.tr_status[p_row]) {
+    const uint8_t p_status = T.tr_status[p_row];
+    switch (p_status) {
         case TB_PENDING_PENDING: break;
         case TB_PENDING_POSTED: return TB_CT_PENDING_TRANSFER_ALREADY_POSTED;
         case TB_PENDING_VOIDED: return TB_CT_PENDING_TRANSFER_ALREADY_VOIDED;
@@ -730,7 +757,8 @@ __device__ uint32_t replay_post_or_void(Replay& R, const C& c, uint32_t k, uint6
     R.note_transfer_ts(ts_actual);
 
     if (has_expiry) R.pulse_reset(expires_at);
-    R.update_status(p_row, (f & TB_TRANSFER_POST_PENDING) ? TB_PENDING_POSTED : TB_PENDING_VOIDED);
+    R.update_status(p_row, (f & TB_TRANSFER_POST_PENDING) ? TB_PENDING_POSTED : TB_PENDING_VOIDED,
+                    p_status);
 
     tb_account_t dr_new = dr, cr_new = cr;
     dr_new.debits_pending = W(U(dr.debits_pending) - p_amount);
@@ -747,11 +775,9 @@ __device__ uint32_t replay_post_or_void(Replay& R, const C& c, uint32_t k, uint6
     const EvRefs xa{x.slot, x.dr, x.cr, x.pslot, hinted ? x.add : 0u};
     // (additive rows: flags unchanged -- a void of a closing transfer marks closable)
     const bool add_dr = R.additive(dr_row, xa, kAddDr), add_cr = R.additive(cr_row, xa, kAddCr);
-    if (add_dr || add_cr) {
-        const u128 da[4] = {u128(0) - p_amount, posted, 0, 0};
-        const u128 db[4] = {0, 0, u128(0) - p_amount, posted};
-        R.add_balances2(add_dr ? uint32_t(dr_row) : kNone32, da, add_cr ? uint32_t(cr_row) : kNone32, db);
-    }
+    if (add_dr || add_cr)
+        R.add_pq(add_dr ? uint32_t(dr_row) : kNone32, add_cr ? uint32_t(cr_row) : kNone32,
+                 u128(0) - p_amount, posted);
     if (!add_dr && (amount > 0 || p_amount > 0 || dr_new.flags != dr.flags))
         R.update_account(dr_row, dr, dr_new);
     if (!add_cr && (amount > 0 || p_amount > 0 || cr_new.flags != cr.flags))
@@ -776,6 +802,7 @@ __device__ uint32_t replay_create_transfer(Replay& R, const C& c, uint32_t k, ui
         dr = T.acc_rows[x.dr];
         cr = T.acc_rows[x.cr];
     }
+    R.flush_adds();  // (the previous event's carries, behind this event's loads)
     if (f & TB_TRANSFER_PADDING_MASK) return TB_CT_RESERVED_FLAG;
     if (u128_is_zero(t.id)) return TB_CT_ID_MUST_NOT_BE_ZERO;
     if (u128_is_max(t.id)) return TB_CT_ID_MUST_NOT_BE_INT_MAX;
@@ -893,11 +920,9 @@ __device__ uint32_t replay_create_transfer(Replay& R, const C& c, uint32_t k, ui
     const bool pend = (f & TB_TRANSFER_PENDING) != 0;
     // (additive rows are never closing: a closing transfer marks closable)
     const bool add_dr = R.additive(dr_row, x, kAddDr), add_cr = R.additive(cr_row, x, kAddCr);
-    if (add_dr || add_cr) {
-        const u128 da[4] = {pend ? amount : 0, pend ? 0 : amount, 0, 0};
-        const u128 db[4] = {0, 0, pend ? amount : 0, pend ? 0 : amount};
-        R.add_balances2(add_dr ? dr_row : kNone32, da, add_cr ? cr_row : kNone32, db);
-    }
+    if (add_dr || add_cr)
+        R.add_pq(add_dr ? dr_row : kNone32, add_cr ? cr_row : kNone32, pend ? amount : u128(0),
+                 pend ? u128(0) : amount);
     if (!add_dr && (amount > 0 || (dr_new.flags & TB_ACCOUNT_CLOSED)))
         R.update_account(dr_row, dr, dr_new);
     if (!add_cr && (amount > 0 || (cr_new.flags & TB_ACCOUNT_CLOSED)))
