@@ -7,9 +7,10 @@ tag=${1:-final}
 bash tools/gpu_check.sh $tag || exit 1
 out=gpurun_out/$tag
 timeout -k 10 400 python -u tools/bench_configs.py --configs 3,4 > $out/configs34.json 2>&1 || { tail -20 $out/configs34.json; exit 1; }
+timeout -k 10 400 python -u tools/bench_configs.py --configs 3,4 --amounts wide > $out/configs34_wide.json 2>&1 || { tail -20 $out/configs34_wide.json; exit 1; }
 python3 -c "
 import json
-for l in open('$out/configs34.json'):
+for l in list(open('$out/configs34.json')) + list(open('$out/configs34_wide.json')):
     if l.startswith('{'):
-        d=json.loads(l); print(d['config'], d['validated'], d['device_transfers_per_s'], d['gpu_transfers_per_s'], d['replayed'])
+        d=json.loads(l); print(d['config'], d['amounts'], d['validated'], d['device_transfers_per_s'], d['gpu_transfers_per_s'], d['replayed'])
 "
