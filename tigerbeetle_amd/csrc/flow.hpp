@@ -11,7 +11,8 @@
 //   * id keys: a 32-bit hash of the event's id and, for post/void, of its pending_id. They cover
 //     the id slot and its in-call holder's result (groove.get visibility, replay.hpp header), the
 //     transfer row behind it, and the pending transfer's TransferPending status. (A collision
-//     only adds an ordering the serial order already has.)
+//     only adds an ordering the serial order already has.) A call without duplicate ids or
+//     post/void takes none: each id's slot and row are then its own event's alone.
 //   * account keys: the row of every account the event may read or write -- its debit and credit
 //     accounts, or the pending transfer's for post/void, resolved before the replay: the committed
 //     pending row's, or the in-call creator's event's. When that creator is not certain (the

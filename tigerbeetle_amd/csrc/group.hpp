@@ -339,7 +339,12 @@ __global__ void __launch_bounds__(kPlanKeysThreads) plan_keys(Tables T, Call<tb_
         auto keyless = [&](uint64_t row) { return acc_additive(T, row, P.add_epoch); };
         uint32_t pslot = kPvNoHint, pdr = kNone32, pcr = kNone32;  // a post/void's pending
         uint32_t add = kAddKnown;  // the replay's additive verdicts (EvRefs::add)
-        if (!u128_is_zero(t.id) && !u128_is_max(t.id)) key[0] = flow_id_key(t.id);
+        // (an id key orders the events of one id, and a post/void after its pending transfer's
+        // creator: a call without duplicate ids or post/void needs none -- every id slot is then
+        // its own event's)
+        if ((call_flags & (kFlagDuplicate | kFlagPostVoid)) && !u128_is_zero(t.id) &&
+            !u128_is_max(t.id))
+            key[0] = flow_id_key(t.id);
         if (t.flags & (TB_TRANSFER_POST_PENDING | TB_TRANSFER_VOID_PENDING)) {
             if (!u128_is_zero(t.pending_id) && !u128_is_max(t.pending_id)) {
                 key[1] = flow_id_key(t.pending_id);
