@@ -7,6 +7,8 @@ results byte for byte, then every Account / Transfer row, TransferPending status
 (parity.Pair). Config 3 also runs with the one-lane account walk (TBG_LANES_ONE_LANE), config 4
 with every post/void replayed (TBG_NO_PV_FAST) on its one-batch form.
 """
+import ctypes
+
 import pytest
 
 import configs34
@@ -105,3 +107,35 @@ def test_configs34_wide_amounts(config):
         p.compare_state()
     finally:
         p.close()
+
+
+def _profile(p):
+    out, i = {}, 0
+    name = ctypes.create_string_buffer(64)
+    ms, cnt = ctypes.c_double(), ctypes.c_uint64()
+    while p.lib.tbg_profile_read(p.g, i, name, 64, ctypes.byref(ms), ctypes.byref(cnt)):
+        out[name.value.decode()] = ms.value
+        i += 1
+    return out
+
+
+@pytest.mark.parametrize("config", ["config3", "config4"])
+def test_profile_span_marks(config):
+    """tbg_profile(ctx, 3), the span marks tools/bench_configs.py reports `device_ms` from: only the
+    call's device spans are recorded (no per-kernel entries), and the calls stay exact against the
+    oracle; with every mark (mode 1) the per-kernel entries appear."""
+    n = 4 * 16 * BATCH
+    seen = {}
+    for mode in (3, 1):
+        p = _pair(n, 16)
+        try:
+            drive = configs34.config3 if config == "config3" else configs34.config4
+            drive(p, n, batches_per_commit=16, before_calls=lambda: p.lib.tbg_profile(p.g, mode))
+            seen[mode] = _profile(p)
+            p.compare_state()
+        finally:
+            p.close()
+    spans = {k for k in seen[3] if not k.startswith(("host:", "pulse:"))}
+    assert spans and spans <= {"host_sync", "call", "account_events"}, seen[3]
+    assert {"host_sync", "call"} <= spans
+    assert "tr_ingest" in seen[1] and ("tr_lanes" in seen[1] or "tr_flow" in seen[1])
