@@ -574,6 +574,7 @@ Call<Event> make_call(tbg_ctx* ctx, const Event* d_events, uint32_t n, const uin
     c.finish_scalars = nullptr;
     c.finish_seq = nullptr;
     c.seq = 0;
+    c.finish_always = 0;
     c.commit_done = nullptr;
     c.commit_scalars = nullptr;
     c.commit_seq = nullptr;
@@ -2321,6 +2322,11 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
     // the results' PCIe writes in tr_ingest's workgroups a commit took 71-77 us against 64-68
     // (r05_i A/B).
     const bool finish = inline_chunks && !use_sort && !dst && !ctx->knobs.no_ingest_finish;
+    // A spinning host launches tr_commit and stage_out only when the ingest did not end the call:
+    // queued behind it and returning at once, the two launches were ~9.5 of the ~25 us a small
+    // device call took on the GPU (profiles/r06_pc/). (A call whose stage_out carries an
+    // AccountEvents snapshot keeps them queued.)
+    const bool finish_first = finish && spin && !ae_async_ok(ctx, n);
     if (!rc && inline_chunks) {
         c.chunk_info = nullptr;
         if (finish) {
@@ -2328,6 +2334,7 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
             c.finish_scalars = reinterpret_cast<unsigned long long*>(ctx->dh_scalars);
             c.finish_seq = seq ? ctx->dh_seq : nullptr;
             c.seq = seq;
+            c.finish_always = finish_first ? 1u : 0u;
         }
         Call<tb_transfer_t> ci = c;
         if (ctx->events_host) {
@@ -2342,8 +2349,10 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
         }
         hipLaunchKernelGGL(tr_ingest, dim3(ig), block, 0, ctx->stream, ctx->T, ci);
         tmark(ctx, "tr_ingest");
-        hipLaunchKernelGGL(tr_commit, grid, block, 0, ctx->stream, ctx->T, c);
-        tmark(ctx, "tr_commit");
+        if (!finish_first) {
+            hipLaunchKernelGGL(tr_commit, grid, block, 0, ctx->stream, ctx->T, c);
+            tmark(ctx, "tr_commit");
+        }
         rc = hip_ok(ctx, hipGetLastError(), "launch") ? 0 : TBG_EHIP;
         if (!rc) rc = ae_flush_all(ctx);  // (deferred appends, while this call runs)
     } else if (!rc) {
@@ -2423,7 +2432,22 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
     // One host synchronisation: does the call need the ordered replay (and, with imported events,
     // the accounts' timestamp index)? One kernel writes the scalars and, for a host-buffer call,
     // its results to mapped host memory (the registered destination, or the pinned staging).
-    if (!rc) {
+    if (!rc && finish_first) {
+        ctx->ae_snap_early = false;
+        tmark(ctx, "host_sync");
+        rc = spin_wait(ctx, seq);
+        if (!rc && !(ctx->h_scalars->flags & kFlagFinished)) {
+            // (the ingest raised a commit flag: the call's tr_commit and stage_out, now)
+            const unsigned int seq2 = ++ctx->seq ? ctx->seq : ++ctx->seq;
+            hipLaunchKernelGGL(tr_commit, grid, block, 0, ctx->stream, ctx->T, c);
+            tmark(ctx, "tr_commit");
+            rc = hip_ok(ctx, hipGetLastError(), "launch") ? 0 : TBG_EHIP;
+            if (!rc) rc = stage_call_outputs(ctx, d_results, nullptr, 0, true, nullptr, true, seq2,
+                                             0u, !c.pnt_force);
+            tmark(ctx, "host_sync");
+            if (!rc) rc = spin_wait(ctx, seq2);
+        }
+    } else if (!rc) {
         const bool snap = ae_async_ok(ctx, n);
         // A small call's AccountEvents snapshot is taken by stage_out's workgroups once they are
         // counted (the host's wait ends at the sequence word): final unless a replay follows, then

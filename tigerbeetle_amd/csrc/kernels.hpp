@@ -821,10 +821,25 @@ __device__ inline void ingest_finish(const Tables& T, const Call<tb_transfer_t>&
     // (tr_commit and stage_out end a call with a commit flag; the rest is the first wave's alone:
     // one system-scope release, the sequence word's, instead of a fence per wave -- 3.4 -> 2.5 us
     // from the last workgroup's acquire to the sequence word)
-    if (!(flags >> 31) || (flags & kCommitFlags) || threadIdx.x >= 64) return;
+    if (!(flags >> 31) || threadIdx.x >= 64) return;
     auto load = [](const unsigned long long* p) {
         return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
+    constexpr uint32_t words = uint32_t(sizeof(DevScalars) / 8);
+    static_assert(sizeof(DevScalars) / 8 <= 64, "one word a lane");
+    const unsigned long long* src = reinterpret_cast<const unsigned long long*>(S);
+    if (flags & kCommitFlags) {
+        // Not ended here: with finish_always the host learns it now (the flags without
+        // kFlagFinished) and launches tr_commit and stage_out; the scalar words stay.
+        if (!c.finish_always || !c.finish_seq) return;
+        if (threadIdx.x < words) c.finish_scalars[threadIdx.x] = load(src + threadIdx.x);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (threadIdx.x == 0)
+            __hip_atomic_store(c.finish_seq, c.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+    }
     if (threadIdx.x == 0) {
         // tr_commit's clean branch: transfers key_range and the FAST count
         const unsigned long long ts = load(&S->spec_ts_max);
@@ -835,9 +850,6 @@ __device__ inline void ingest_finish(const Tables& T, const Call<tb_transfer_t>&
         __threadfence();
     }
     __builtin_amdgcn_wave_barrier();
-    const uint32_t words = uint32_t(sizeof(DevScalars) / 8);
-    static_assert(sizeof(DevScalars) / 8 <= 64, "one word a lane");
-    const unsigned long long* src = reinterpret_cast<const unsigned long long*>(S);
     if (threadIdx.x < words) c.finish_scalars[threadIdx.x] = load(src + threadIdx.x);
     // Every lane's copy (its load and its store) happens before lane 0's reset: a wavefront-scope
     // release / acquire around the barrier orders them in the HIP memory model, not only through

@@ -191,6 +191,10 @@ struct Call {
     unsigned long long* finish_scalars;  // mapped pinned copy of the scalars block
     unsigned int* finish_seq;        // the pinned sequence word, or null (the host synchronises)
     unsigned int seq;
+    // The host launches tr_commit and stage_out only when the call needs them: the last ingest
+    // workgroup publishes the sequence word either way, with the scalars block (kFlagFinished
+    // set when it ended the call). 0: they are queued behind tr_ingest and it publishes only an end.
+    uint32_t finish_always;
     // Large calls the host expects to replay (tbg_ctx::replay_hint): tr_commit's last workgroup
     // copies the scalars block (the replay count is final there) to its mapped copy and publishes
     // commit_seq_val, so that the host launches the replay while the balance kernels and stage_out
