@@ -2219,6 +2219,9 @@ const char* tbg_last_error(const tbg_ctx* ctx) {
 
 namespace {
 
+#ifndef TBG_SMALL_INGEST_THREADS
+#define TBG_SMALL_INGEST_THREADS 128
+#endif
 int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t n,
                           const uint32_t* d_batch_ends, const uint64_t* d_batch_ts,
                           uint32_t n_batches, tb_create_result_t* d_results, void* stream,
@@ -2347,7 +2350,12 @@ int create_transfers_impl(tbg_ctx* ctx, const tb_transfer_t* d_events, uint32_t 
             ci.ends_out = const_cast<uint32_t*>(c.batch_ends);
             ci.ts_out = const_cast<uint64_t*>(c.batch_ts);
         }
-        hipLaunchKernelGGL(tr_ingest, dim3(ig), block, 0, ctx->stream, ctx->T, ci);
+        // (small calls: one 64-event chunk a wave, two waves a workgroup -- the chunks' dependent
+        // round trips on twice as many CUs: per-commit p50 24.6-26.0 -> 23.3-25.1 us with 128 lanes,
+        // 23.6-24.7 with 64, profiles/r06_si/)
+        const uint32_t sthreads = TBG_SMALL_INGEST_THREADS;
+        hipLaunchKernelGGL(tr_ingest, dim3((n + sthreads - 1) / sthreads), dim3(sthreads), 0,
+                           ctx->stream, ctx->T, ci);
         tmark(ctx, "tr_ingest");
         if (!finish_first) {
             hipLaunchKernelGGL(tr_commit, grid, block, 0, ctx->stream, ctx->T, c);

@@ -73,8 +73,7 @@ __device__ inline V block_reduce(V v, Op op) {
     if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = v;
     __syncthreads();
     V r = lds[0];
-#pragma unroll
-    for (int i = 1; i < kBlock / 64; i++) r = op(r, lds[i]);
+    for (int i = 1; i < int(blockDim.x >> 6); i++) r = op(r, lds[i]);  // (kBlock or fewer lanes)
     __syncthreads();
     return r;
 }
@@ -896,11 +895,12 @@ __global__ void __launch_bounds__(kBlock, kIngestWgPerCu) tr_ingest(Tables T,
     __shared__ unsigned int bucket_hist[kBucketsMax];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     if (c.bucket_counts) {
-        for (uint32_t i = threadIdx.x; i < c.n_buckets; i += kBlock) bucket_hist[i] = 0;
+        for (uint32_t i = threadIdx.x; i < c.n_buckets; i += blockDim.x) bucket_hist[i] = 0;
         __syncthreads();
     }
     uint8_t* my = lds_ev[wv];
-    const uint32_t nw = gridDim.x * kIngestWaves;
+    const uint32_t waves = blockDim.x >> 6;  // (kIngestWaves, or fewer for small calls)
+    const uint32_t nw = gridDim.x * waves;
     if (c.ends_out && blockIdx.x == 0)  // (the batch bounds read from the host: the later kernels' copy)
         for (uint32_t b = threadIdx.x; b < c.n_batches; b += blockDim.x) {
             c.ends_out[b] = c.batch_ends[b];
@@ -927,7 +927,7 @@ __global__ void __launch_bounds__(kBlock, kIngestWgPerCu) tr_ingest(Tables T,
             }
         }
     };
-    uint32_t base = (blockIdx.x * kIngestWaves + wv) * 64;
+    uint32_t base = (blockIdx.x * waves + wv) * 64;
     if (base < c.n) load_chunk(base);
     for (; base < c.n; base += nw * 64) {
         const uint32_t ubase = __builtin_amdgcn_readfirstlane(base);
@@ -1040,7 +1040,7 @@ __global__ void __launch_bounds__(kBlock, kIngestWgPerCu) tr_ingest(Tables T,
     n_fast = block_reduce(n_fast, OpAdd());
     ts_max = block_reduce(ts_max, OpMax());
     if (c.bucket_counts)
-        for (uint32_t i = threadIdx.x; i < c.n_buckets; i += kBlock)
+        for (uint32_t i = threadIdx.x; i < c.n_buckets; i += blockDim.x)
             if (bucket_hist[i]) atomicAdd(&c.bucket_counts[i], bucket_hist[i]);
     if (threadIdx.x == 0) {
         if (flags) atomicOr(&T.scalars->flags, flags);
