@@ -563,8 +563,27 @@ struct SegmentLds {
 // segment.): bitmap windows of up to
 // kGroupWindowBits values in LDS over the values' range -- set bits, prefix popcounts, enumerate --
 // or, for a sparse segment, an LDS bitonic sort of the values themselves.
+// Wave scans on DPP for the bitmap windows (every lane active): lanes_walk's sequence (a
+// __shfl_up scan is six dependent LDS permutes).
+__device__ inline uint32_t seg_wave_inclusive(uint32_t v) {
+    v += walk_dpp<0x111, 0xF>(v);  // row_shr:1
+    v += walk_dpp<0x112, 0xF>(v);  // row_shr:2
+    v += walk_dpp<0x114, 0xF>(v);  // row_shr:4
+    v += walk_dpp<0x118, 0xF>(v);  // row_shr:8
+    v += walk_dpp<0x142, 0xA>(v);  // row_bcast:15
+    v += walk_dpp<0x143, 0xC>(v);  // row_bcast:31
+    return v;
+}
+__device__ inline uint32_t seg_wave_last(uint32_t v) {
+    return uint32_t(__builtin_amdgcn_readlane(int(v), 63));
+}
+
+// `compress` (the grouping's pair indices, group_sort): a segment's pair indices 4 s + j all have
+// the same j >> 1 (id keys j 0 / 1, account keys 2 / 3), so 2 s + (j & 1) is one-to-one and keeps
+// their order: the bitmap covers half the range, and `jhi` (j & 2) restores the indices.
 __device__ inline void segment_sort(const uint32_t* in, uint32_t* out, uint32_t off, uint32_t c,
-                                    SegmentLds& L, bool values = false, uint32_t bound = 0) {
+                                    SegmentLds& L, bool values = false, uint32_t bound = 0,
+                                    bool compress = false, uint32_t jhi = 0) {
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint32_t* buf = L.buf;
     // The segment's values, 16 loads a lane in flight at a time (a loop of one load per iteration
@@ -594,8 +613,9 @@ __device__ inline void segment_sort(const uint32_t* in, uint32_t* out, uint32_t 
             for (uint32_t i = tid; i < words; i += kGroupBigThreads) buf[i] = 0;
             __syncthreads();
             for_values([&](uint32_t, uint32_t v) {
-                if (v >= wb && v - wb < kGroupWindowBits) {
-                    const uint32_t d = uint32_t(v - wb);
+                const uint32_t cv = compress ? ((v >> 2) << 1) | (v & 1) : v;
+                if (cv >= wb && cv - wb < kGroupWindowBits) {
+                    const uint32_t d = uint32_t(cv - wb);
                     atomicOr(&buf[d >> 5], 1u << (d & 31));
                 }
             });
@@ -608,7 +628,7 @@ __device__ inline void segment_sort(const uint32_t* in, uint32_t* out, uint32_t 
             const uint32_t ww = words / kWaves, wbase = wave * ww;
             uint32_t cnt = 0;
             for (uint32_t r = 0; r < ww; r += 64) cnt += __popc(buf[wbase + r + lane]);
-            cnt = wave_sum_u32(cnt);
+            cnt = seg_wave_last(seg_wave_inclusive(cnt));
             if (lane == 0) L.scratch[wave] = cnt;
             __syncthreads();
             uint32_t run = placed, total = 0;
@@ -620,15 +640,16 @@ __device__ inline void segment_sort(const uint32_t* in, uint32_t* out, uint32_t 
             for (uint32_t r = 0; r < ww; r += 64) {
                 uint32_t bits = buf[wbase + r + lane];
                 const uint32_t pc = __popc(bits);
-                const uint32_t incl = wave_inclusive_u32(pc, lane);
+                const uint32_t incl = seg_wave_inclusive(pc);
                 uint32_t pos = run + incl - pc;
                 const uint64_t word_bit = wb + uint64_t(wbase + r + lane) * 32;
                 while (bits) {
                     const uint32_t bit = __builtin_ctz(bits);
                     bits &= bits - 1;
-                    out[off + pos++] = uint32_t(word_bit + bit);
+                    const uint32_t idx = uint32_t(word_bit + bit);
+                    out[off + pos++] = compress ? ((idx >> 1) << 2) | jhi | (idx & 1) : idx;
                 }
-                run += __shfl(incl, 63, 64);
+                run += seg_wave_last(incl);
             }
             placed += total;
             __syncthreads();
@@ -642,8 +663,9 @@ __device__ inline void segment_sort(const uint32_t* in, uint32_t* out, uint32_t 
         return;
     }
     for_values([&](uint32_t, uint32_t v) {
-        lo = min(lo, v);
-        hi = max(hi, v);
+        const uint32_t cv = compress ? ((v >> 2) << 1) | (v & 1) : v;  // (the bitmap's index)
+        lo = min(lo, cv);
+        hi = max(hi, cv);
     });
     for (int d = 32; d >= 1; d >>= 1) {
         lo = min(lo, uint32_t(__shfl_xor(lo, d, 64)));
@@ -856,7 +878,9 @@ __global__ void __launch_bounds__(kGroupBigThreads) group_sort(GroupPlan G) {
     const uint32_t nbig = G.counts[1];
     for (uint32_t b = blockIdx.x; b < nbig; b += gridDim.x) {
         const uint4 e = G.big[b];
-        segment_sort(G.vals, G.vals_sorted, e.x, e.y, L, false, G.pairs);
+        // (the key's type, e.w's top bit: account keys' pairs have j >> 1 == 1)
+        segment_sort(G.vals, G.vals_sorted, e.x, e.y, L, false, G.pairs / 2, true,
+                     (e.w >> 31) ? 2u : 0u);
     }
 }
 
